@@ -1,0 +1,235 @@
+/*
+ * orb_mi355x.h — C ABI of the MI355X-native ORB front-end and Hamming matcher.
+ *
+ * Drop-in boundary for the hot path of vdoom/ORB_SLAM3_VIO_FIXES
+ * (paths are relative to the reference tree):
+ *   ORBextractor  include/ORBextractor.h:43-109, src/ORBextractor.cc:409-1195
+ *   ORBmatcher    include/ORBmatcher.h:36-103,  src/ORBmatcher.cc:43-763,1676-2074
+ *   Frame grid    src/Frame.cc:385-416,657-735
+ *   DBoW2         Thirdparty/DBoW2/DBoW2/TemplatedVocabulary.h:1126-1259
+ *
+ * Plain pointers and sizes only.  Nothing throws across this boundary; every
+ * entry point returns an integer status (ORB_OK = 0, negatives below) unless
+ * documented otherwise.  All functions without "_device" take and return
+ * HOST memory; "_device" entry points take device pointers already resident
+ * in HBM and an optional hipStream_t (passed as void*, NULL = default stream).
+ */
+#ifndef ORB_MI355X_H
+#define ORB_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes (mirrors ORBextractor::operator() -1 on empty input,
+ *      src/ORBextractor.cc:1090-1091) ---- */
+#define ORB_OK              0
+#define ORB_ERR_EMPTY      (-1)  /* empty image                          */
+#define ORB_ERR_CAPACITY   (-2)  /* output capacity too small; *n_out = required */
+#define ORB_ERR_PARAM      (-3)  /* bad type / size / parameter           */
+#define ORB_ERR_DEVICE     (-4)  /* HIP runtime error or no device        */
+#define ORB_ERR_UNSUPPORTED (-5) /* configuration outside the restated semantics */
+
+/* cv::KeyPoint layout, 28 bytes (OpenCV core/types.hpp; used as
+ * std::vector<cv::KeyPoint> throughout Frame.h). */
+typedef struct orb_keypoint {
+    float x, y;        /* pt */
+    float size;
+    float angle;
+    float response;
+    int32_t octave;
+    int32_t class_id;
+} orb_keypoint;
+
+/* ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST,
+ * int minThFAST)  (include/ORBextractor.h:49-50).  The two knobs select the
+ * platform-dependent semantics of the reference build. */
+typedef struct orbx_params {
+    int32_t nfeatures;
+    float   scale_factor;
+    int32_t nlevels;
+    int32_t ini_th_fast;
+    int32_t min_th_fast;
+    int32_t blur_variant;   /* 0 = OpenCV>=4.5 error-diffused kernel [18,34,48,56,..] (default),
+                               1 = legacy rounded kernel [18,34,49,55,..] */
+    int32_t fma_sampling;   /* 1 = fused sampling (reference -O3 -march=native on an FMA host,
+                               default), 0 = unfused */
+    int32_t reserved;
+} orbx_params;
+
+typedef struct orbx_handle orbx_handle;
+
+/* ---------------- extractor ---------------- */
+
+/* ORBextractor::ORBextractor (src/ORBextractor.cc:409-469).  device = HIP
+ * ordinal.  Returns NULL on bad params / no device. */
+orbx_handle* orbx_create(const orbx_params* params, int device);
+void         orbx_destroy(orbx_handle* h);
+
+/* Getters of include/ORBextractor.h:61-81 (GetLevels, GetScaleFactors,
+ * GetInverseScaleFactors, GetScaleSigmaSquares, GetInverseScaleSigmaSquares)
+ * plus the per-level feature budget and the IC_Angle umax table.  Each array
+ * argument may be NULL; sized nlevels (umax: 16). */
+int orbx_get_tables(const orbx_handle* h, float* scale, float* inv_scale,
+                    float* sigma2, float* inv_sigma2, int32_t* features_per_level,
+                    int32_t* umax);
+
+/* Upper bound on keypoints one image of w x h can produce (capacity hint). */
+int orbx_max_keypoints(orbx_handle* h, int w, int h_);
+
+/* ORBextractor::operator() (src/ORBextractor.cc:1086-1168) on one 8UC1 host
+ * image.  lap0/lap1 = vLappingArea.  Writes *n_out keypoints and *n_out x 32
+ * descriptor bytes; *mono_index_out = the return value of the reference
+ * (monoIndex).  Returns ORB_OK, ORB_ERR_EMPTY, ORB_ERR_CAPACITY (then *n_out
+ * = required), ORB_ERR_PARAM or ORB_ERR_DEVICE. */
+int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int h_, size_t step,
+                 int lap0, int lap1, orb_keypoint* kps, uint8_t* desc, int cap,
+                 int* n_out, int* mono_index_out);
+
+/* mvImagePyramid[level] (include/ORBextractor.h:83) of the LAST image
+ * extracted by orbx_extract (host copy).  dst may be NULL to query w/h. */
+int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step,
+                   int* w, int* h_);
+
+/* Batched, HBM-resident path: nframes images of w x h, frame f at
+ * d_frames + f*frame_stride, rows row_step apart.  Outputs per frame f:
+ * d_kps[f*cap ...], d_desc[(f*cap ...)*32], d_n[f], d_mono[f].
+ * cap must be >= orbx_max_keypoints(h, w, h_).  Asynchronous on `stream`. */
+int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_frames,
+                              size_t frame_stride, size_t row_step, int w, int h_,
+                              int lap0, int lap1, orb_keypoint* d_kps, uint8_t* d_desc,
+                              int cap, int32_t* d_n, int32_t* d_mono, void* stream);
+
+/* Per-stage debug/parity hooks for the last orbx_extract call (host copies).
+ * stage 0: per-level FAST candidates (vToDistributeKeys, ORBextractor.cc:794-872)
+ * stage 1: per-level DistributeOctTree output (ORBextractor.cc:877-890, before
+ *          orientation).  Keypoints are written level after level; counts[l]
+ *          receives the per-level count. */
+int orbx_debug_stage(orbx_handle* h, int stage, orb_keypoint* kps, int cap,
+                     int32_t* counts);
+
+/* ---------------- matcher ---------------- */
+
+/* ORBmatcher::DescriptorDistance / DBoW2::FORB::distance
+ * (src/ORBmatcher.cc:2058-2074, FORB.cpp:81-100). */
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b);
+
+/* A Frame as the matchers see it (Frame.h): N keypoints (mvKeysUn), N x 32
+ * descriptors, image bounds and grid factors (Frame.h:250-251,287-290).
+ * The library builds the 64 x 48 cell grid itself (Frame.cc:385-416). */
+typedef struct orbm_frame {
+    int32_t n;
+    const orb_keypoint* kps;
+    const uint8_t* desc;
+    float min_x, max_x, min_y, max_y;
+    float grid_inv_w, grid_inv_h;
+    const float* u_right;        /* mvuRight (N) or NULL (mono: all -1) */
+    const float* scale_factors;  /* mvScaleFactors (nlevels) or NULL */
+    int32_t nlevels;
+} orbm_frame;
+
+/* ORBmatcher(nnratio, checkOri).SearchForInitialization(F1, F2, vbPrevMatched,
+ * vnMatches12, windowSize)  (src/ORBmatcher.cc:648-763).  prev_xy: N1 x 2
+ * in/out.  matches12: N1 out.  Returns nmatches (>= 0) or a negative status. */
+int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2,
+                                   float* prev_xy, int window, float nnratio,
+                                   int check_ori, int32_t* matches12);
+
+/* Batched device form used by the throughput bench: pairs (F[t], F[t+1]) of
+ * consecutive frames of an orbx_extract_batch_device output, prev = F[t]'s own
+ * keypoint positions (Tracking.cc:2459-2461).  d_matches: npairs x cap,
+ * d_nmatches: npairs.  Grid factors as in orbm_frame. */
+int orbm_search_for_initialization_batch_device(
+    int nframes, const orb_keypoint* d_kps, const uint8_t* d_desc, const int32_t* d_n,
+    int cap, float min_x, float max_x, float min_y, float max_y, float grid_inv_w,
+    float grid_inv_h, int window, float nnratio, int check_ori, int32_t* d_matches,
+    int32_t* d_nmatches, void* stream);
+
+/* FeatureVector (DBoW2 FeatureVector.h:24-25) as CSR: nnodes node ids in
+ * ascending order, offsets[nnodes+1] into idx[] (feature indices ascending). */
+typedef struct orbm_featvec {
+    int32_t nnodes;
+    const uint32_t* node_ids;
+    const int32_t* offsets;
+    const uint32_t* idx;
+} orbm_featvec;
+
+/* ORBmatcher(nnratio, checkOri).SearchByBoW(KeyFrame*, Frame&, matches)
+ * (src/ORBmatcher.cc:223-425), monocular/rectified case (F.Nleft == -1,
+ * !pKF->mpCamera2).  kf_mp_valid[i] = (pMP != NULL && !pMP->isBad()) for KF
+ * feature i.  match_f[F.N] out = KF feature index matched to each F feature
+ * or -1.  Returns nmatches. */
+int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kf_fv,
+                       const uint8_t* kf_mp_valid, const orbm_frame* f,
+                       const orbm_featvec* f_fv, float nnratio, int check_ori,
+                       int32_t* match_f);
+
+/* Map points projected into F (the fields ORBmatcher reads from MapPoint,
+ * MapPoint.h mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos, mbTrackInView,
+ * isBad(), GetDescriptor(), Observations()). */
+typedef struct orbm_mappoints {
+    int32_t n;
+    const float* proj_x;
+    const float* proj_y;
+    const float* proj_xr;
+    const int32_t* level;
+    const float* view_cos;
+    const float* track_depth;
+    const uint8_t* in_view;     /* mbTrackInView && !isBad() */
+    const uint8_t* has_obs;     /* Observations() > 0 */
+    const uint8_t* desc;        /* n x 32 */
+} orbm_mappoints;
+
+/* SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFarPoints)
+ * (src/ORBmatcher.cc:43-213) for F.Nleft == -1.  owner[F.N] in/out: -1 = no
+ * MapPoint, <= -2 = a pre-existing MapPoint (opaque), >= 0 = index into mps
+ * set by this call.  blocked[F.N] in: the pre-existing MapPoint has
+ * Observations() > 0.  Returns nmatches. */
+int orbm_search_by_projection_mps(const orbm_frame* f, const orbm_mappoints* mps,
+                                  float th, int far_points, float th_far,
+                                  float nnratio, int32_t* owner, const uint8_t* blocked);
+
+/* SearchByProjection(Frame& Current, const Frame& Last, th, bMono)
+ * (src/ORBmatcher.cc:1676-1887) for CurrentFrame.Nleft == -1.  The pose math
+ * is done by the caller: for each last-frame point i, valid[i] (pMP && !outlier
+ * && invzc >= 0 && inside bounds), u,v (projection), ur (u - mbf*invzc),
+ * last_octave[i], has_obs[i] and descriptor.  mode: 0 = neither, 1 = bForward,
+ * 2 = bBackward.  owner/blocked as above (indices into the last frame).
+ * Returns nmatches. */
+int orbm_search_by_projection_last(const orbm_frame* cur, int nlast,
+                                   const uint8_t* valid, const float* u, const float* v,
+                                   const float* ur, const int32_t* last_octave,
+                                   const float* last_angle, const uint8_t* has_obs,
+                                   const uint8_t* last_desc, float th, int mode,
+                                   int check_ori,
+                                   int32_t* owner, const uint8_t* blocked);
+
+/* ---------------- vocabulary (DBoW2 TemplatedVocabulary<FORB>) ---------------- */
+
+/* A k-ary vocabulary tree laid out breadth first: node 0 = root; children of
+ * node i are first_child[i] .. first_child[i]+nchild[i]-1 (nchild 0 = leaf).
+ * node_desc: nnodes x 32, word_id/weight per node (leaves). */
+typedef struct orbv_vocab {
+    int32_t nnodes;
+    int32_t depth_levels;       /* m_L */
+    const int32_t* first_child;
+    const int32_t* nchild;
+    const uint8_t* node_desc;
+    const int32_t* word_id;
+    const double* weight;
+} orbv_vocab;
+
+/* TemplatedVocabulary::transform(feature, word_id, weight, &nid, levelsup)
+ * (TemplatedVocabulary.h:1217-1259) for n descriptors: out word ids, weights
+ * and the node id at level m_L - levelsup.  GPU when device >= 0. */
+int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levelsup,
+                   int32_t* word_id, double* weight, int32_t* node_id, int device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ORB_MI355X_H */
