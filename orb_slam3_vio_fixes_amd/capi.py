@@ -1,0 +1,64 @@
+"""ctypes bindings of liborb_mi355x.so (the product C ABI, include/orb_mi355x.h).
+
+There is no CPU fallback: if the library is missing or no device is visible,
+every entry point raises.  The shared object is built in-tree by build.py.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from pathlib import Path
+
+from . import abi
+
+LIB_PATH = Path(__file__).resolve().parent / "liborb_mi355x.so"
+
+EXPORTS = [
+    "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_max_keypoints", "orbx_extract", "orbx_get_level",
+    "orbx_extract_batch_device", "orbx_debug_stage", "orbm_descriptor_distance", "orbm_search_for_initialization",
+    "orbm_search_for_initialization_batch_device", "orbm_search_by_bow", "orbm_search_by_projection_mps",
+    "orbm_search_by_projection_last", "orbv_transform",
+]
+
+_lib = None
+
+
+def load(path: Path | str = LIB_PATH):
+    """dlopen + prototypes, no device call (usable without a GPU)."""
+    L = C.CDLL(str(path))
+    vp, i32, f32, sz = C.c_void_p, C.c_int, C.c_float, C.c_size_t
+    L.orbx_create.restype = vp
+    L.orbx_create.argtypes = [vp, i32]
+    L.orbx_destroy.argtypes = [vp]
+    L.orbx_get_tables.argtypes = [vp] * 7
+    L.orbx_max_keypoints.argtypes = [vp, i32, i32]
+    L.orbx_extract.argtypes = [vp, vp, i32, i32, sz, i32, i32, vp, vp, i32, vp, vp]
+    L.orbx_get_level.argtypes = [vp, i32, vp, sz, vp, vp]
+    L.orbx_extract_batch_device.argtypes = [vp, i32, vp, sz, sz, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp]
+    L.orbx_debug_stage.argtypes = [vp, i32, vp, i32, vp]
+    L.orbm_descriptor_distance.argtypes = [vp, vp]
+    L.orbm_search_for_initialization.argtypes = [vp, vp, vp, i32, f32, i32, vp]
+    L.orbm_search_for_initialization_batch_device.argtypes = [i32, vp, vp, vp, i32, f32, f32, f32, f32, f32, f32,
+                                                              i32, f32, i32, vp, vp, vp]
+    L.orbm_search_by_bow.argtypes = [vp, vp, vp, vp, vp, f32, i32, vp]
+    L.orbm_search_by_projection_mps.argtypes = [vp, vp, f32, i32, f32, f32, vp, vp]
+    L.orbm_search_by_projection_last.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, vp]
+    L.orbv_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp, i32]
+    return L
+
+
+def lib():
+    """The loaded product library; raises if it is absent (no fallback)."""
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        _lib = load()
+    return _lib
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        names = {abi.ORB_ERR_EMPTY: "empty image", abi.ORB_ERR_CAPACITY: "capacity", abi.ORB_ERR_PARAM: "bad parameter",
+                 abi.ORB_ERR_DEVICE: "HIP device error", abi.ORB_ERR_UNSUPPORTED: "unsupported configuration"}
+        raise RuntimeError(f"{what} failed: {names.get(rc, rc)}")
+    return rc

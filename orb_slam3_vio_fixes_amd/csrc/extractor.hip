@@ -1,0 +1,1216 @@
+// extractor.hip — MI355X-native ORBextractor (gfx950).
+//
+// Replaces ORB_SLAM3::ORBextractor (reference include/ORBextractor.h:43-109,
+// src/ORBextractor.cc:409-1195) behind the C ABI of include/orb_mi355x.h.
+//
+// Per batch of same-size frames the path is seven kinds of launches, all
+// batched over frames (gridDim.y = frame):
+//   k_resize       level l from level l-1, OpenCV INTER_LINEAR 8U fixed point
+//   k_blur         7x7 sigma-2 fixed-point Gaussian of every level (REFLECT_101)
+//   k_fast_cells   one wave per FAST cell: LDS-staged ROI, FAST-9 score map,
+//                  cell-local 3x3 NMS at iniThFAST / minThFAST, ballot compaction
+//   k_quadtree     one workgroup per (frame, level): DistributeOctTree as
+//                  data-parallel passes over the node list + exact std::sort
+//   k_describe     one wave per keypoint: IC_Angle moments (wave reduction),
+//                  glibc-exact sincosf, 256 rBRIEF tests -> ballot bytes
+//   k_assemble     per frame: scaling, lapping partition (monoIndex), output
+// Everything is integer/bitwise; no MFMA.
+#include "../../include/orb_mi355x.h"
+#include "common.h"
+#include "orb_math.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+namespace orbmi {
+
+constexpr int kMaxLevels = 32;
+constexpr int kHalfPatch = 15;
+constexpr int kEdge = 19;
+
+__constant__ int8_t c_pattern[1024];
+static const int8_t h_pattern[1024] = {
+#include "brief_pattern.inc"
+};
+
+// ---------------------------------------------------------------------------
+// Plan: everything that depends only on (params, w, h), computed once on the
+// host with the reference's own float/double expressions.
+// ---------------------------------------------------------------------------
+struct LevelDev {
+    int w, h, pitch;
+    long long off;      // byte offset of the level inside one frame's pyramid slab (l >= 1)
+    long long boff;     // byte offset inside one frame's blurred slab
+    int bpitch;
+    float scale;
+    int patch;          // int(PATCH_SIZE * scale)  (ORBextractor.cc:880)
+    // quadtree (DistributeOctTree arguments, ORBextractor.cc:877-878)
+    int qW, qH, N, nIni;
+    float hX;
+    int cell_base, ncells, slot_base, slot_total;   // cells / key slots of this level
+    int out_base, out_cap;                          // quadtree output slots
+};
+
+struct CellDev {
+    int level;
+    int x0, y0, cols, rows;   // ROI in level coordinates (ORBextractor.cc:807-826)
+    int slot_off, cap;        // key slots (u32) relative to the frame's slot slab
+};
+
+struct Plan {
+    int w = 0, h = 0, L = 0, maxB = 0;
+    std::vector<LevelDev> lv;
+    std::vector<CellDev> cells;
+    long long pyr_bytes = 0, blur_bytes = 0;
+    int ncells = 0, slot_total = 0, out_total = 0;
+    int roi_max = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
+    std::vector<int> xmax;           // per level
+    std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
+    // device
+    uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_in = nullptr;
+    int2* d_tab = nullptr;
+    LevelDev* d_lv = nullptr;
+    CellDev* d_cells = nullptr;
+    int* d_cell_count = nullptr;
+    uint32_t *d_cell_keys = nullptr, *d_key_scr = nullptr;
+    int* d_knode = nullptr;
+    uint8_t* d_kq = nullptr;
+    uint32_t* d_qt_key = nullptr;
+    int* d_qt_n = nullptr;
+    float* d_angle = nullptr;
+    uint8_t* d_sdesc = nullptr;
+    // single-image host path outputs
+    orb_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int32_t *d_n = nullptr, *d_mono = nullptr;
+    int host_cap = 0;
+    size_t in_pitch = 0;
+
+    void release() {
+        void* ps[] = {d_pyr, d_blur, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
+                      d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+        *this = Plan();
+    }
+};
+
+}  // namespace orbmi
+
+struct orbx_handle {
+    orbx_params prm{};
+    int device = 0;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> nfeat, umax;
+    orbmi::Plan plan;
+    bool have_last = false;
+    int last_w = 0, last_h = 0;
+};
+
+namespace orbmi {
+
+static int cv_round_d(double v) { return (int)std::nearbyint(v); }
+static int cv_floor_f(float v) { int i = (int)v; return i - (i > v); }
+static int cv_ceil_f(float v) { int i = (int)v; return i + (i < v); }
+static short sat_short(float v) {
+    const int i = (int)std::nearbyintf(v);
+    return (short)std::min(32767, std::max(-32768, i));
+}
+
+// ORBextractor::ORBextractor tables (ORBextractor.cc:414-468).
+static void init_tables(orbx_handle* h) {
+    const int L = h->prm.nlevels;
+    const double sf = (double)h->prm.scale_factor;
+    h->scale.assign(L, 1.f); h->sigma2.assign(L, 1.f);
+    h->inv_scale.assign(L, 1.f); h->inv_sigma2.assign(L, 1.f);
+    for (int i = 1; i < L; ++i) {
+        h->scale[i] = (float)(h->scale[i - 1] * sf);
+        h->sigma2[i] = h->scale[i] * h->scale[i];
+    }
+    for (int i = 0; i < L; ++i) { h->inv_scale[i] = 1.f / h->scale[i]; h->inv_sigma2[i] = 1.f / h->sigma2[i]; }
+    h->nfeat.assign(L, 0);
+    const float factor = (float)(1.0f / sf);
+    float per = h->prm.nfeatures * (1 - factor) / (1 - (float)std::pow((double)factor, (double)L));
+    int sum = 0;
+    for (int l = 0; l < L - 1; ++l) {
+        h->nfeat[l] = cv_round(per);
+        sum += h->nfeat[l];
+        per *= factor;
+    }
+    h->nfeat[L - 1] = std::max(h->prm.nfeatures - sum, 0);
+    h->umax.assign(kHalfPatch + 1, 0);
+    const int vmax = cv_floor_f(kHalfPatch * std::sqrt(2.f) / 2 + 1);
+    const int vmin = cv_ceil_f(kHalfPatch * std::sqrt(2.f) / 2);
+    const double hp2 = kHalfPatch * kHalfPatch;
+    for (int v = 0; v <= vmax; ++v) h->umax[v] = cv_round_d(std::sqrt(hp2 - v * v));
+    for (int v = kHalfPatch, v0 = 0; v >= vmin; --v) {
+        while (h->umax[v0] == h->umax[v0 + 1]) ++v0;
+        h->umax[v] = v0;
+        ++v0;
+    }
+}
+
+static int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// Builds the size-dependent plan; returns ORB_OK or an error.
+static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
+    Plan& P = hd->plan;
+    if (P.w == w && P.h == h && P.maxB >= maxB && P.L == hd->prm.nlevels) return ORB_OK;
+    P.release();
+    if (w > 4096 + 16 || h > 4096 + 16) return ORB_ERR_UNSUPPORTED;   // 12-bit key coordinates
+    const int L = hd->prm.nlevels;
+    P.w = w; P.h = h; P.L = L; P.maxB = maxB;
+    P.lv.assign(L, LevelDev{});
+    std::vector<int2> tab;
+    P.xmax.assign(L, 0);
+    P.tab_off.assign(L, 0);
+    long long poff = 0, boff = 0;
+    int cellsum = 0, slotsum = 0, outsum = 0;
+    for (int l = 0; l < L; ++l) {
+        LevelDev& d = P.lv[l];
+        // ComputePyramid sizes (ORBextractor.cc:1174-1175)
+        d.w = cv_round((float)w * hd->inv_scale[l]);
+        d.h = cv_round((float)h * hd->inv_scale[l]);
+        if (d.w < 2 * kEdge + 8 || d.h < 2 * kEdge + 8) return ORB_ERR_UNSUPPORTED;
+        d.pitch = round_up(d.w, 64);
+        d.bpitch = d.pitch;
+        d.off = l == 0 ? 0 : poff;
+        if (l > 0) poff += (long long)d.pitch * d.h;
+        d.boff = boff;
+        boff += (long long)d.bpitch * d.h;
+        d.scale = hd->scale[l];
+        d.patch = (int)(31 * hd->scale[l]);
+        if (l > 0) {
+            // cv::resize coefficient tables (imgproc resize.cpp)
+            const LevelDev& s = P.lv[l - 1];
+            const double sx_inv = (double)d.w / s.w, sy_inv = (double)d.h / s.h;
+            const double scx = 1. / sx_inv, scy = 1. / sy_inv;
+            const int isx = (int)std::nearbyint(scx), isy = (int)std::nearbyint(scy);
+            if (std::fabs(scx - isx) < 2.220446049250313e-16 && std::fabs(scy - isy) < 2.220446049250313e-16 &&
+                isx == 2 && isy == 2)
+                return ORB_ERR_UNSUPPORTED;   // OpenCV would take its INTER_AREA path
+            P.tab_off[l] = (long long)tab.size();
+            int xmax = d.w;
+            for (int dx = 0; dx < d.w; ++dx) {
+                float fx = (float)((dx + 0.5) * scx - 0.5);
+                int sx = cv_floor_f(fx);
+                fx -= sx;
+                if (sx < 0) { fx = 0.f; sx = 0; }
+                if (sx + 1 >= s.w) {
+                    xmax = std::min(xmax, dx);
+                    if (sx >= s.w - 1) { fx = 0.f; sx = s.w - 1; }
+                }
+                const int a0 = sat_short((1.f - fx) * 2048.f), a1 = sat_short(fx * 2048.f);
+                tab.push_back(make_int2(sx, (a0 & 0xffff) | (a1 << 16)));
+            }
+            for (int dy = 0; dy < d.h; ++dy) {
+                float fy = (float)((dy + 0.5) * scy - 0.5);
+                int sy = cv_floor_f(fy);
+                fy -= sy;
+                const int b0 = sat_short((1.f - fy) * 2048.f), b1 = sat_short(fy * 2048.f);
+                tab.push_back(make_int2(sy, (b0 & 0xffff) | (b1 << 16)));
+            }
+            P.xmax[l] = xmax;
+        }
+        // ComputeKeyPointsOctTree cell grid (ORBextractor.cc:785-822)
+        const int minBX = kEdge - 3, minBY = minBX;
+        const int maxBX = d.w - kEdge + 3, maxBY = d.h - kEdge + 3;
+        const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
+        const int nCols = (int)(width / 35.f), nRows = (int)(height / 35.f);
+        if (nCols < 1 || nRows < 1) return ORB_ERR_UNSUPPORTED;
+        const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        const int cap = ((wCell + 1) / 2) * ((hCell + 1) / 2);
+        d.cell_base = cellsum;
+        d.slot_base = slotsum;
+        int nc = 0;
+        for (int i = 0; i < nRows; ++i) {
+            const float iniY = (float)(minBY + i * hCell);
+            float maxY = iniY + hCell + 6;
+            if (iniY >= maxBY - 3) continue;
+            if (maxY > maxBY) maxY = (float)maxBY;
+            for (int j = 0; j < nCols; ++j) {
+                const float iniX = (float)(minBX + j * wCell);
+                float maxX = iniX + wCell + 6;
+                if (iniX >= maxBX - 6) continue;
+                if (maxX > maxBX) maxX = (float)maxBX;
+                CellDev c;
+                c.level = l;
+                c.x0 = (int)iniX; c.y0 = (int)iniY;
+                c.cols = (int)maxX - c.x0; c.rows = (int)maxY - c.y0;
+                c.slot_off = slotsum;
+                c.cap = cap;
+                slotsum += cap;
+                P.cells.push_back(c);
+                P.roi_max = std::max(P.roi_max, c.cols * c.rows);
+                P.win_max = std::max(P.win_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
+                ++nc;
+            }
+        }
+        d.ncells = nc;
+        cellsum += nc;
+        d.slot_total = slotsum - d.slot_base;
+        P.max_level_cells = std::max(P.max_level_cells, nc);
+        // DistributeOctTree sizing (ORBextractor.cc:559-561)
+        d.qW = maxBX - minBX;
+        d.qH = maxBY - minBY;
+        d.N = hd->nfeat[l];
+        d.nIni = (int)std::round((float)(maxBX - minBX) / (maxBY - minBY));
+        if (d.nIni < 1) return ORB_ERR_UNSUPPORTED;
+        d.hX = (float)(maxBX - minBX) / d.nIni;
+        d.out_base = outsum;
+        d.out_cap = std::max(d.N + 3, 4 * d.nIni);
+        outsum += d.out_cap;
+        P.max_out_cap = std::max(P.max_out_cap, d.out_cap);
+    }
+    P.pyr_bytes = poff;
+    P.blur_bytes = boff;
+    P.ncells = cellsum;
+    P.slot_total = slotsum;
+    P.out_total = outsum;
+    P.in_pitch = (size_t)round_up(w, 64);
+
+    const size_t B = (size_t)maxB;
+    ORB_CHECK(hipMalloc(&P.d_pyr, std::max<size_t>(1, B * P.pyr_bytes)));
+    ORB_CHECK(hipMalloc(&P.d_blur, B * P.blur_bytes));
+    ORB_CHECK(hipMalloc(&P.d_in, P.in_pitch * h));
+    ORB_CHECK(hipMalloc(&P.d_tab, std::max<size_t>(1, tab.size()) * sizeof(int2)));
+    ORB_CHECK(hipMalloc(&P.d_lv, L * sizeof(LevelDev)));
+    ORB_CHECK(hipMalloc(&P.d_cells, P.cells.size() * sizeof(CellDev)));
+    ORB_CHECK(hipMalloc(&P.d_cell_count, B * P.ncells * sizeof(int)));
+    ORB_CHECK(hipMalloc(&P.d_cell_keys, B * P.slot_total * sizeof(uint32_t)));
+    ORB_CHECK(hipMalloc(&P.d_key_scr, B * P.slot_total * sizeof(uint32_t)));
+    ORB_CHECK(hipMalloc(&P.d_knode, B * P.slot_total * sizeof(int)));
+    ORB_CHECK(hipMalloc(&P.d_kq, B * P.slot_total));
+    ORB_CHECK(hipMalloc(&P.d_qt_key, B * P.out_total * sizeof(uint32_t)));
+    ORB_CHECK(hipMalloc(&P.d_qt_n, B * L * sizeof(int)));
+    ORB_CHECK(hipMalloc(&P.d_angle, B * P.out_total * sizeof(float)));
+    ORB_CHECK(hipMalloc(&P.d_sdesc, B * P.out_total * 32));
+    P.host_cap = P.out_total;
+    ORB_CHECK(hipMalloc(&P.d_kps, P.host_cap * sizeof(orb_keypoint)));
+    ORB_CHECK(hipMalloc(&P.d_desc, (size_t)P.host_cap * 32));
+    ORB_CHECK(hipMalloc(&P.d_n, sizeof(int32_t)));
+    ORB_CHECK(hipMalloc(&P.d_mono, sizeof(int32_t)));
+    if (!tab.empty()) ORB_CHECK(hipMemcpy(P.d_tab, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
+    ORB_CHECK(hipMemcpy(P.d_lv, P.lv.data(), L * sizeof(LevelDev), hipMemcpyHostToDevice));
+    ORB_CHECK(hipMemcpy(P.d_cells, P.cells.data(), P.cells.size() * sizeof(CellDev), hipMemcpyHostToDevice));
+    return ORB_OK;
+}
+
+// ---------------------------------------------------------------------------
+// k_resize: cv::resize INTER_LINEAR 8UC1.  One output row per
+// wave; four rows per block.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src, long long s_fstride, int s_pitch,
+                                                int sh, uint8_t* __restrict__ dst, long long d_fstride, int d_pitch,
+                                                int dw, int dh, const int2* __restrict__ xt,
+                                                const int2* __restrict__ yt, int xmax) {
+    const int dy = blockIdx.x * 4 + wave_id();
+    if (dy >= dh) return;
+    const int f = blockIdx.y;
+    const uint8_t* S = src + f * s_fstride;
+    uint8_t* D = dst + f * d_fstride + (long long)dy * d_pitch;
+    const int2 ty = yt[dy];
+    const int r0 = min(max(ty.x, 0), sh - 1), r1 = min(max(ty.x + 1, 0), sh - 1);
+    const int b0 = (short)(ty.y & 0xffff), b1 = ty.y >> 16;
+    const uint8_t* S0 = S + (long long)r0 * s_pitch;
+    const uint8_t* S1 = S + (long long)r1 * s_pitch;
+    for (int dx = lane_id(); dx < dw; dx += kWave) {
+        const int2 tx = xt[dx];
+        const int sx = tx.x, a0 = (short)(tx.y & 0xffff), a1 = tx.y >> 16;
+        int h0, h1;
+        if (dx < xmax) {
+            h0 = S0[sx] * a0 + S0[sx + 1] * a1;
+            h1 = S1[sx] * a0 + S1[sx + 1] * a1;
+        } else {
+            h0 = S0[sx] * 2048;
+            h1 = S1[sx] * 2048;
+        }
+        D[dx] = (uint8_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_blur: GaussianBlur(7x7, sigma 2, REFLECT_101), fixed point:
+// h = sum k*p (u16), out = (sum k*h + 2^15) >> 16.  64x16 output tiles.
+// ---------------------------------------------------------------------------
+struct BlurKernel { int k[7]; };
+
+__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ src, long long s_fstride, int s_pitch,
+                                              uint8_t* __restrict__ dst, long long d_fstride, int d_pitch, int w,
+                                              int h, BlurKernel K) {
+    __shared__ uint8_t tin[22][72];
+    __shared__ uint32_t th[22][65];
+    const int f = blockIdx.z;
+    const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 16;
+    const uint8_t* S = src + f * s_fstride;
+    auto refl = [](int p, int n) {
+        if (n == 1) return 0;
+        while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
+        return p;
+    };
+    for (int i = threadIdx.x; i < 22 * 70; i += 256) {
+        const int r = i / 70, c = i - r * 70;
+        const int yy = refl(y0 + r - 3, h), xx = refl(x0 + c - 3, w);
+        tin[r][c] = S[(long long)yy * s_pitch + xx];
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 22 * 64; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) acc += K.k[t] * tin[r][c + t];
+        th[r][c] = acc;
+    }
+    __syncthreads();
+    uint8_t* D = dst + f * d_fstride;
+    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
+        const int r = i >> 6, c = i & 63;
+        const int yy = y0 + r, xx = x0 + c;
+        if (yy >= h || xx >= w) continue;
+        uint32_t acc = 0;
+#pragma unroll
+        for (int t = 0; t < 7; ++t) acc += K.k[t] * th[r + t][c];
+        D[(long long)yy * d_pitch + xx] = (uint8_t)((acc + 32768u) >> 16);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_fast_cells: FAST-9/16 with 3x3 NMS per cell ROI, exact reformulation of
+// cv::FAST on the ROI: score s(p) = max over the 16 arcs of
+// 9 contiguous ring pixels of the arc's min |difference| - 1; corner at t iff
+// s(p) >= t; NMS keeps p iff s(p) > s_t(q) for its 8 neighbours inside the
+// cell's detection window.  One wave per cell, 4 cells per block.
+// ---------------------------------------------------------------------------
+struct FastArgs {
+    const uint8_t* in;      // level 0 of every frame
+    long long in_fstride;
+    int in_pitch;
+    const uint8_t* pyr;     // levels >= 1
+    long long pyr_fstride;
+    const LevelDev* lv;
+    const CellDev* cells;
+    int ncells;
+    int* cell_count;        // [B][ncells]
+    uint32_t* cell_keys;    // [B][slot_total]
+    int slot_total;
+    int ini_th, min_th;
+    int roi_max, win_max;   // LDS per wave
+};
+
+__device__ __forceinline__ int fast_score(const uint8_t* roi, int stride, int r, int c) {
+    const uint8_t* p = roi + r * stride + c;
+    const int v = p[0];
+    int d[16];
+    d[0] = v - p[3 * stride];
+    d[1] = v - p[3 * stride + 1];
+    d[2] = v - p[2 * stride + 2];
+    d[3] = v - p[stride + 3];
+    d[4] = v - p[3];
+    d[5] = v - p[-stride + 3];
+    d[6] = v - p[-2 * stride + 2];
+    d[7] = v - p[-3 * stride + 1];
+    d[8] = v - p[-3 * stride];
+    d[9] = v - p[-3 * stride - 1];
+    d[10] = v - p[-2 * stride - 2];
+    d[11] = v - p[-stride - 3];
+    d[12] = v - p[-3];
+    d[13] = v - p[stride - 3];
+    d[14] = v - p[2 * stride - 2];
+    d[15] = v - p[3 * stride - 1];
+    int mn3[16], mx3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mn3[k] = min(d[k], min(d[(k + 1) & 15], d[(k + 2) & 15]));
+        mx3[k] = max(d[k], max(d[(k + 1) & 15], d[(k + 2) & 15]));
+    }
+    int a = -1000, b = 1000;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        a = max(a, min(mn3[k], min(mn3[(k + 3) & 15], mn3[(k + 6) & 15])));
+        b = min(b, max(mx3[k], max(mx3[(k + 3) & 15], mx3[(k + 6) & 15])));
+    }
+    const int s = max(a, -b) - 1;
+    return s < 0 ? 0 : s;
+}
+
+__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int ww, int wh, int r, int c, int t) {
+    const int s = sc[r * ww + c];
+    if (s < max(t, 1)) return false;
+#pragma unroll
+    for (int dr = -1; dr <= 1; ++dr)
+#pragma unroll
+        for (int dc = -1; dc <= 1; ++dc) {
+            if (!dr && !dc) continue;
+            const int rr = r + dr, cc = c + dc;
+            if (rr < 0 || rr >= wh || cc < 0 || cc >= ww) continue;
+            const int q = sc[rr * ww + cc];
+            const int bv = q >= t ? q : 0;
+            if (!(s > bv)) return false;
+        }
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = lane_id(), wv = wave_id();
+    const int ci = blockIdx.x * 4 + wv;
+    const int f = blockIdx.y;
+    const bool active = ci < a.ncells;
+    CellDev c{};
+    if (active) c = a.cells[ci];
+    uint8_t* roi = smem + wv * (a.roi_max + a.win_max);
+    uint8_t* sc = roi + a.roi_max;
+    const uint8_t* img = nullptr;
+    int pitch = 0;
+    if (active) {
+        if (c.level == 0) { img = a.in + f * a.in_fstride; pitch = a.in_pitch; }
+        else { img = a.pyr + f * a.pyr_fstride + a.lv[c.level].off; pitch = a.lv[c.level].pitch; }
+        const int n = c.rows * c.cols;
+        for (int i = lane; i < n; i += kWave) {
+            const int r = i / c.cols, cc = i - r * c.cols;
+            roi[i] = img[(long long)(c.y0 + r) * pitch + c.x0 + cc];
+        }
+    }
+    __syncthreads();
+    const int ww = active ? max(0, c.cols - 6) : 0, wh = active ? max(0, c.rows - 6) : 0;
+    const int nwin = ww * wh;
+    for (int i = lane; i < nwin; i += kWave) {
+        const int r = i / ww, cc = i - r * ww;
+        sc[i] = (uint8_t)fast_score(roi, c.cols, r + 3, cc + 3);
+    }
+    __syncthreads();
+    int cnt = 0;
+    for (int base = 0; base < nwin; base += kWave) {
+        const int i = base + lane;
+        bool keep = false;
+        if (i < nwin) { const int r = i / ww; keep = nms_keep(sc, ww, wh, r, i - r * ww, a.ini_th); }
+        cnt += __popcll(__ballot(keep));
+    }
+    const int t = cnt > 0 ? a.ini_th : a.min_th;
+    uint32_t* out = a.cell_keys + (long long)f * a.slot_total + c.slot_off;
+    int written = 0;
+    for (int base = 0; base < nwin; base += kWave) {
+        const int i = base + lane;
+        bool keep = false;
+        int r = 0, cc = 0;
+        if (i < nwin) { r = i / ww; cc = i - r * ww; keep = nms_keep(sc, ww, wh, r, cc, t); }
+        const uint64_t m = __ballot(keep);
+        if (keep) {
+            const int pos = written + mask_rank(m);
+            if (pos < c.cap) {
+                // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
+                const uint32_t x = (uint32_t)(c.x0 + cc + 3 - (kEdge - 3));
+                const uint32_t y = (uint32_t)(c.y0 + r + 3 - (kEdge - 3));
+                out[pos] = x | (y << 12) | ((uint32_t)sc[i] << 24);
+            }
+        }
+        written += __popcll(m);
+    }
+    if (active && lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, c.cap);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_quadtree: ORBextractor::DistributeOctTree (ORBextractor.cc:555-779) for
+// one (frame, level) per workgroup.
+//
+// The std::list becomes an array in list order rebuilt by scans.  One step
+// divides a set of nodes given in processing order; the rebuilt list is the
+// children blocks (n4,n3,n2,n1, non-empty only) in REVERSE processing order
+// followed by the undivided nodes in their old order -- exactly what the
+// reference's push_front + erase produce (:633-679, :703-744).  Children with
+// >1 key are queued (n1..n4, processing order) like vSizeAndPointerToNode.
+// Outer passes divide every node that still holds >1 key; the last rounds
+// (:689-754) sort the queue with the libstdc++ std::sort port and divide from
+// the largest down until the list holds N nodes.  Keys never move: each key
+// carries the list index of its node, remapped after every step.  A node keeps
+// its max-response key, the first in vToDistributeKeys order on ties
+// (:757-776).
+// ---------------------------------------------------------------------------
+struct QtArgs {
+    const LevelDev* lv;
+    const int* cell_count;
+    const uint32_t* cell_keys;
+    uint32_t* key_scr;
+    int* knode;
+    uint8_t* kq;
+    int ncells_total, slot_total;
+    uint32_t* qt_key;   // [B][out_total]
+    int* qt_n;          // [B][L]
+    int out_total, L, ncap;
+};
+
+struct QtLds {
+    int* off;
+    short4* rect[2];
+    int* cnt[2];
+    uint8_t* nomore[2];
+    int* ccnt;      // 4 per node
+    int* newpos;    // 4 per node
+    int* keep;      // new index of an undivided node
+    int* div;       // node divides in this step
+    int* ord;       // processing order (node indices)
+    int* rne;       // per rank: #non-empty children (scanned)
+    int* rgt;       // per rank: #children with >1 key (scanned)
+    int* nd;        // per node: undivided (scanned)
+    int* expand;    // queue of list indices (processing order)
+    SortRec* srt;
+    int* tmp;       // scan scratch
+    int* misc;
+};
+
+__device__ __forceinline__ int quadrant(uint32_t key, short4 r) {
+    const int x = key & 0xfff, y = (key >> 12) & 0xfff;
+    const int hx = (int)ceilf((float)(r.z - r.x) / 2), hy = (int)ceilf((float)(r.w - r.y) / 2);
+    const bool left = x < r.x + hx, top = y < r.y + hy;
+    return left ? (top ? 0 : 2) : (top ? 1 : 3);
+}
+
+// ExtractorNode::DivideNode child boundaries (ORBextractor.cc:480-508).
+__device__ __forceinline__ short4 child_rect(short4 r, int q) {
+    const int hx = (int)ceilf((float)(r.z - r.x) / 2), hy = (int)ceilf((float)(r.w - r.y) / 2);
+    const short mx = (short)(r.x + hx), my = (short)(r.y + hy);
+    switch (q) {
+        case 0: return make_short4(r.x, r.y, mx, my);
+        case 1: return make_short4(mx, r.y, r.z, my);
+        case 2: return make_short4(r.x, my, mx, r.w);
+        default: return make_short4(mx, my, r.z, r.w);
+    }
+}
+
+// Divide s.ord[0..m) (ccnt/kq already computed for them, s.div set for every
+// node); rebuild the list into buffer cur^1; remap the keys.  Returns the new
+// size; *nexp receives the queue length.
+__device__ int qt_divide(QtLds& s, int& cur, int size, int m, const int K, int* knode, const uint8_t* kq,
+                         int* nexp) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    for (int r = tid; r < m; r += T) {
+        const int i = s.ord[r];
+        int ne = 0, gt = 0;
+        for (int q = 0; q < 4; ++q) { ne += s.ccnt[4 * i + q] > 0; gt += s.ccnt[4 * i + q] > 1; }
+        s.rne[r] = ne;
+        s.rgt[r] = gt;
+    }
+    for (int i = tid; i < size; i += T) s.nd[i] = s.div[i] ? 0 : 1;
+    __syncthreads();
+    const int totNE = block_excl_scan(s.rne, m, s.tmp);
+    const int totGT = block_excl_scan(s.rgt, m, s.tmp);
+    block_excl_scan(s.nd, size, s.tmp);
+    const int nx = cur ^ 1;
+    const short4* R = s.rect[cur];
+    const int* C = s.cnt[cur];
+    for (int r = tid; r < m; r += T) {
+        const int i = s.ord[r];
+        int ne = 0;
+        for (int q = 0; q < 4; ++q) ne += s.ccnt[4 * i + q] > 0;
+        const int start = totNE - s.rne[r] - ne;   // reverse processing order
+        int w = 0;
+        for (int q = 3; q >= 0; --q) {
+            const int c = s.ccnt[4 * i + q];
+            if (c > 0) {
+                const int np = start + w++;
+                s.newpos[4 * i + q] = np;
+                s.rect[nx][np] = child_rect(R[i], q);
+                s.cnt[nx][np] = c;
+                s.nomore[nx][np] = c == 1;
+            }
+        }
+        int e = s.rgt[r];
+        for (int q = 0; q < 4; ++q)
+            if (s.ccnt[4 * i + q] > 1) s.expand[e++] = s.newpos[4 * i + q];
+    }
+    for (int i = tid; i < size; i += T) {
+        if (s.div[i]) continue;
+        const int np = totNE + s.nd[i];
+        s.keep[i] = np;
+        s.rect[nx][np] = R[i];
+        s.cnt[nx][np] = C[i];
+        s.nomore[nx][np] = s.nomore[cur][i];
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += T) {
+        const int n = knode[k];
+        knode[k] = s.div[n] ? s.newpos[4 * n + kq[k]] : s.keep[n];
+    }
+    __syncthreads();
+    cur = nx;
+    *nexp = totGT;
+    return totNE + (size - m);
+}
+
+// Count keys per child quadrant for every node with s.div set.
+__device__ void qt_count(QtLds& s, int cur, int size, const int K, const uint32_t* keys, const int* knode,
+                         uint8_t* kq) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    for (int i = tid; i < 4 * size; i += T) s.ccnt[i] = 0;
+    __syncthreads();
+    const short4* R = s.rect[cur];
+    for (int k = tid; k < K; k += T) {
+        const int n = knode[k];
+        if (s.div[n]) {
+            const int q = quadrant(keys[k], R[n]);
+            kq[k] = (uint8_t)q;
+            atomicAdd(&s.ccnt[4 * n + q], 1);
+        }
+    }
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+    const LevelDev lv = a.lv[l];
+    const int NC = a.ncap;
+    QtLds s;
+    {
+        uint8_t* p = smem;
+        auto take = [&](size_t bytes) { uint8_t* q = p; p += (bytes + 15) & ~size_t(15); return q; };
+        s.off = (int*)take((lv.ncells + 1) * sizeof(int));
+        s.rect[0] = (short4*)take(NC * sizeof(short4));
+        s.rect[1] = (short4*)take(NC * sizeof(short4));
+        s.cnt[0] = (int*)take(NC * sizeof(int));
+        s.cnt[1] = (int*)take(NC * sizeof(int));
+        s.nomore[0] = take(NC);
+        s.nomore[1] = take(NC);
+        s.ccnt = (int*)take(4 * NC * sizeof(int));
+        s.newpos = (int*)take(4 * NC * sizeof(int));
+        s.keep = (int*)take(NC * sizeof(int));
+        s.div = (int*)take(NC * sizeof(int));
+        s.ord = (int*)take(NC * sizeof(int));
+        s.rne = (int*)take(NC * sizeof(int));
+        s.rgt = (int*)take(NC * sizeof(int));
+        s.nd = (int*)take(NC * sizeof(int));
+        s.expand = (int*)take(NC * sizeof(int));
+        s.srt = (SortRec*)take(NC * sizeof(SortRec));
+        s.tmp = (int*)take(16 * sizeof(int));
+        s.misc = (int*)take(16 * sizeof(int));
+    }
+    const int* ccount = a.cell_count + (long long)f * a.ncells_total + lv.cell_base;
+    const uint32_t* cslots = a.cell_keys + (long long)f * a.slot_total + lv.slot_base;
+    const long long kb = (long long)f * a.slot_total + lv.slot_base;
+    uint32_t* keys = a.key_scr + kb;
+    int* knode = a.knode + kb;
+    uint8_t* kq = a.kq + kb;
+    uint32_t* out = a.qt_key + (long long)f * a.out_total + lv.out_base;
+
+    // 1. vToDistributeKeys: cells in (row, col) order, row-major inside a cell (:805-872)
+    for (int i = tid; i < lv.ncells; i += T) s.off[i] = ccount[i];
+    __syncthreads();
+    const int K = block_excl_scan(s.off, lv.ncells, s.tmp);
+    const int cap = lv.ncells ? lv.slot_total / lv.ncells : 0;
+    for (int c = wave_id(); c < lv.ncells; c += T / kWave) {
+        const int base = s.off[c];
+        const int n = (c + 1 < lv.ncells ? s.off[c + 1] : K) - base;
+        for (int j = lane_id(); j < n; j += kWave) keys[base + j] = cslots[c * cap + j];
+    }
+    __syncthreads();
+    if (K == 0) {
+        if (tid == 0) a.qt_n[f * a.L + l] = 0;
+        return;
+    }
+    // 2. initial nodes (:559-601)
+    const int nIni = lv.nIni;
+    int* bcnt = s.rne;
+    int* bpos = s.rgt;
+    for (int i = tid; i < nIni; i += T) bcnt[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < K; k += T) {
+        const int b = (int)((float)(keys[k] & 0xfff) / lv.hX);
+        knode[k] = b;
+        atomicAdd(&bcnt[b], 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int n = 0;
+        for (int i = 0; i < nIni; ++i) {
+            bpos[i] = -1;
+            if (bcnt[i] == 0) continue;
+            bpos[i] = n;
+            s.rect[0][n] = make_short4((short)(int)(lv.hX * (float)i), 0, (short)(int)(lv.hX * (float)(i + 1)),
+                                       (short)lv.qH);
+            s.cnt[0][n] = bcnt[i];
+            s.nomore[0][n] = bcnt[i] == 1;
+            ++n;
+        }
+        s.misc[0] = n;
+    }
+    __syncthreads();
+    for (int k = tid; k < K; k += T) knode[k] = bpos[knode[k]];
+    int size = s.misc[0];
+    int cur = 0;
+    const int N = lv.N;
+    __syncthreads();
+
+    // 3. outer passes (:610-689)
+    int nexp = 0;
+    bool last = false;
+    while (true) {
+        const int prev = size;
+        for (int i = tid; i < size; i += T) s.nd[i] = s.nomore[cur][i] ? 0 : 1;
+        __syncthreads();
+        for (int i = tid; i < size; i += T) s.div[i] = s.nd[i];
+        __syncthreads();
+        const int m = block_excl_scan(s.nd, size, s.tmp);
+        for (int i = tid; i < size; i += T)
+            if (s.div[i]) s.ord[s.nd[i]] = i;
+        __syncthreads();
+        qt_count(s, cur, size, K, keys, knode, kq);
+        size = qt_divide(s, cur, size, m, K, knode, kq, &nexp);
+        if (size >= N || size == prev) break;
+        if (size + nexp * 3 > N) { last = true; break; }
+    }
+    // 4. last rounds (:692-753)
+    while (last) {
+        const int prev = size;
+        const int m = nexp;
+        for (int j = tid; j < m; j += T) {
+            const int i = s.expand[j];
+            s.srt[j] = SortRec{s.cnt[cur][i], (int)s.rect[cur][i].x, i};
+        }
+        for (int i = tid; i < size; i += T) s.div[i] = 0;
+        __syncthreads();
+        if (tid == 0) std_sort(s.srt, m);
+        __syncthreads();
+        for (int j = tid; j < m; j += T) s.div[s.srt[j].pos] = 1;
+        __syncthreads();
+        qt_count(s, cur, size, K, keys, knode, kq);
+        // processing rank r = m-1-j; stop after the first rank at which the list reaches N
+        for (int r = tid; r < m; r += T) {
+            const int i = s.srt[m - 1 - r].pos;
+            int ne = 0;
+            for (int q = 0; q < 4; ++q) ne += s.ccnt[4 * i + q] > 0;
+            s.rne[r] = ne - 1;
+        }
+        if (tid == 0) s.misc[1] = m;
+        __syncthreads();
+        block_excl_scan(s.rne, m, s.tmp);
+        for (int r = tid; r < m; r += T) {
+            const int i = s.srt[m - 1 - r].pos;
+            int ne = 0;
+            for (int q = 0; q < 4; ++q) ne += s.ccnt[4 * i + q] > 0;
+            if (size + s.rne[r] + ne - 1 >= N) atomicMin(&s.misc[1], r + 1);
+        }
+        __syncthreads();
+        const int mp = s.misc[1];
+        for (int r = tid; r < m; r += T) {
+            const int i = s.srt[m - 1 - r].pos;
+            if (r < mp) s.ord[r] = i;
+            else s.div[i] = 0;
+        }
+        __syncthreads();
+        size = qt_divide(s, cur, size, mp, K, knode, kq, &nexp);
+        if (size >= N || size == prev) break;
+    }
+    // 5. retain the best key per node (:757-776)
+    int* best = s.ccnt;
+    for (int i = tid; i < size; i += T) best[i] = 0;
+    __syncthreads();
+    for (int k = tid; k < K; k += T)
+        atomicMax(&best[knode[k]], (int)(((keys[k] >> 24) << 23) | (0x7FFFFF - k)));
+    __syncthreads();
+    const int nout = min(size, lv.out_cap);
+    for (int i = tid; i < nout; i += T) out[i] = keys[0x7FFFFF - (best[i] & 0x7FFFFF)];
+    if (tid == 0) a.qt_n[f * a.L + l] = nout;
+}
+
+// ---------------------------------------------------------------------------
+// k_describe: computeOrientation/IC_Angle (ORBextractor.cc:76-103,471-478) on
+// the unblurred level and computeOrbDescriptor (:107-146) on the blurred
+// level.  One wave per keypoint; lane l evaluates rBRIEF tests 4l..4l+3.
+// ---------------------------------------------------------------------------
+struct DescArgs {
+    const uint8_t* in;
+    long long in_fstride;
+    int in_pitch;
+    const uint8_t* pyr;
+    long long pyr_fstride;
+    const uint8_t* blur;
+    long long blur_fstride;
+    const LevelDev* lv;
+    const uint32_t* qt_key;
+    const int* qt_n;
+    float* angle;
+    uint8_t* sdesc;
+    int out_total, L;
+    int fma;
+    int umax[16];
+};
+
+__global__ __launch_bounds__(256) void k_describe(DescArgs a) {
+    __shared__ int8_t pat[1024];
+    for (int i = threadIdx.x; i < 1024; i += 256) pat[i] = c_pattern[i];
+    __syncthreads();
+    const int l = blockIdx.x, f = blockIdx.y, lane = lane_id();
+    const LevelDev lv = a.lv[l];
+    const int n = a.qt_n[f * a.L + l];
+    const uint8_t* img;
+    int pitch;
+    if (l == 0) { img = a.in + f * a.in_fstride; pitch = a.in_pitch; }
+    else { img = a.pyr + f * a.pyr_fstride + lv.off; pitch = lv.pitch; }
+    const uint8_t* bimg = a.blur + f * a.blur_fstride + lv.boff;
+    const int bp = lv.bpitch;
+    const uint32_t* keys = a.qt_key + (long long)f * a.out_total + lv.out_base;
+    const int u = lane - kHalfPatch;
+    for (int p = blockIdx.z * 4 + wave_id(); p < n; p += gridDim.z * 4) {
+        const uint32_t key = keys[p];
+        const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
+        const uint8_t* c = img + (long long)cy * pitch + cx;
+        int m10 = 0, m01 = 0;
+        if (lane < 2 * kHalfPatch + 1) {
+            m10 = u * c[u];
+            for (int v = 1; v <= kHalfPatch; ++v) {
+                if (u < -a.umax[v] || u > a.umax[v]) continue;
+                const int up = c[u + v * pitch], dn = c[u - v * pitch];
+                m10 += u * (up + dn);
+                m01 += v * (up - dn);
+            }
+        }
+        m10 = wave_sum(m10);
+        m01 = wave_sum(m01);
+        const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
+        const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
+        float sb, ca;
+        glibc_sincosf(ang, &sb, &ca);
+        const uint8_t* bc = bimg + (long long)cy * bp + cx;
+        int nib = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int t = 4 * lane + k;
+            int val[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float x = (float)pat[4 * t + 2 * e], y = (float)pat[4 * t + 2 * e + 1];
+                int r, q;
+                if (a.fma) {
+                    r = cv_round(__builtin_fmaf(x, sb, y * ca));
+                    q = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
+                } else {
+                    r = cv_round(x * sb + y * ca);
+                    q = cv_round(x * ca - y * sb);
+                }
+                val[e] = bc[r * bp + q];
+            }
+            nib |= (val[0] < val[1]) << k;
+        }
+        const int hi = __shfl_down(nib, 1, kWave);
+        uint8_t* d = a.sdesc + ((long long)f * a.out_total + lv.out_base + p) * 32;
+        if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
+        if (lane == 0) a.angle[(long long)f * a.out_total + lv.out_base + p] = ang_deg;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_assemble: ORBextractor::operator() output loop (ORBextractor.cc:1105-1167):
+// levels in order, keypoints in quadtree list order; pt *= scale for level>0;
+// x in [lap0, lap1] goes to the tail in reverse, others to the head; returns
+// monoIndex.  One workgroup per frame.
+// ---------------------------------------------------------------------------
+struct AsmArgs {
+    const LevelDev* lv;
+    const uint32_t* qt_key;
+    const int* qt_n;
+    const float* angle;
+    const uint8_t* sdesc;
+    int out_total, L;
+    float lap0, lap1;
+    orb_keypoint* kps;
+    uint8_t* desc;
+    int cap;
+    int32_t* n_out;
+    int32_t* mono_out;
+};
+
+__global__ __launch_bounds__(256) void k_assemble(AsmArgs a) {
+    __shared__ int lvl_start[kMaxLevels + 1];
+    __shared__ int tmp[16];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    int* inlap = (int*)smem;                    // per keypoint, scanned
+    const int f = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
+    if (tid == 0) {
+        int acc = 0;
+        for (int l = 0; l < a.L; ++l) { lvl_start[l] = acc; acc += a.qt_n[f * a.L + l]; }
+        lvl_start[a.L] = acc;
+    }
+    __syncthreads();
+    const int total = lvl_start[a.L];
+    auto locate = [&](int g, int& l, int& p) {
+        l = 0;
+        while (g >= lvl_start[l + 1]) ++l;
+        p = g - lvl_start[l];
+    };
+    for (int g = tid; g < total; g += T) {
+        int l, p;
+        locate(g, l, p);
+        const uint32_t key = a.qt_key[(long long)f * a.out_total + a.lv[l].out_base + p];
+        float x = (float)((int)(key & 0xfff) + (kEdge - 3));
+        if (l != 0) x *= a.lv[l].scale;
+        inlap[g] = (x >= a.lap0 && x <= a.lap1) ? 1 : 0;
+    }
+    __syncthreads();
+    // keep the flags: recompute them after the scan from the scanned values
+    const int nlap = block_excl_scan(inlap, total, tmp);
+    for (int g = tid; g < total; g += T) {
+        int l, p;
+        locate(g, l, p);
+        const LevelDev lv = a.lv[l];
+        const long long src = (long long)f * a.out_total + lv.out_base + p;
+        const uint32_t key = a.qt_key[src];
+        float x = (float)((int)(key & 0xfff) + (kEdge - 3));
+        float y = (float)((int)((key >> 12) & 0xfff) + (kEdge - 3));
+        if (l != 0) { x *= lv.scale; y *= lv.scale; }
+        const bool in = x >= a.lap0 && x <= a.lap1;
+        const int before_lap = inlap[g];
+        const int dst = in ? total - 1 - before_lap : g - before_lap;
+        orb_keypoint kp;
+        kp.x = x; kp.y = y;
+        kp.size = (float)lv.patch;
+        kp.angle = a.angle[src];
+        kp.response = (float)(key >> 24);
+        kp.octave = l;
+        kp.class_id = -1;
+        if (dst < a.cap) {
+            a.kps[(long long)f * a.cap + dst] = kp;
+            const uint4* s4 = (const uint4*)(a.sdesc + src * 32);
+            uint4* d4 = (uint4*)(a.desc + ((long long)f * a.cap + dst) * 32);
+            d4[0] = s4[0];
+            d4[1] = s4[1];
+        }
+    }
+    if (tid == 0) {
+        a.n_out[f] = total;
+        a.mono_out[f] = total - nlap;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host orchestration
+// ---------------------------------------------------------------------------
+static size_t qt_lds_bytes(const Plan& P) {
+    const size_t NC = (size_t)P.max_out_cap + 8;
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    size_t b = al((P.max_level_cells + 1) * 4);
+    b += 2 * al(NC * 8) + 2 * al(NC * 4) + 2 * al(NC) + 2 * al(NC * 16);
+    b += 7 * al(NC * 4) + al(NC * sizeof(SortRec)) + 2 * al(64);
+    return b;
+}
+
+static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long long fstride, int pitch0, float lap0,
+                        float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono,
+                        hipStream_t st) {
+    Plan& P = hd->plan;
+    const int L = P.L;
+    // pyramid
+    for (int l = 1; l < L; ++l) {
+        const LevelDev& d = P.lv[l];
+        const LevelDev& s = P.lv[l - 1];
+        const uint8_t* src = l == 1 ? d_frames : P.d_pyr + s.off;
+        const long long sfs = l == 1 ? fstride : P.pyr_bytes;
+        const int sp = l == 1 ? pitch0 : s.pitch;
+        const int2* xt = P.d_tab + P.tab_off[l];
+        hipLaunchKernelGGL(k_resize, dim3((d.h + 3) / 4, B), dim3(256), 0, st, src, sfs, sp, s.h, P.d_pyr + d.off,
+                           P.pyr_bytes, d.pitch, d.w, d.h, xt, xt + d.w, P.xmax[l]);
+    }
+    // blurred levels
+    BlurKernel K;
+    static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
+    for (int t = 0; t < 7; ++t) K.k[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
+    for (int l = 0; l < L; ++l) {
+        const LevelDev& d = P.lv[l];
+        const uint8_t* src = l == 0 ? d_frames : P.d_pyr + d.off;
+        const long long sfs = l == 0 ? fstride : P.pyr_bytes;
+        const int sp = l == 0 ? pitch0 : d.pitch;
+        hipLaunchKernelGGL(k_blur, dim3((d.w + 63) / 64, (d.h + 15) / 16, B), dim3(256), 0, st, src, sfs, sp,
+                           P.d_blur + d.boff, P.blur_bytes, d.bpitch, d.w, d.h, K);
+    }
+    // FAST cells
+    FastArgs fa;
+    fa.in = d_frames; fa.in_fstride = fstride; fa.in_pitch = pitch0;
+    fa.pyr = P.d_pyr; fa.pyr_fstride = P.pyr_bytes;
+    fa.lv = P.d_lv; fa.cells = P.d_cells; fa.ncells = P.ncells;
+    fa.cell_count = P.d_cell_count; fa.cell_keys = P.d_cell_keys; fa.slot_total = P.slot_total;
+    fa.ini_th = std::min(std::max(hd->prm.ini_th_fast, 0), 255);
+    fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
+    fa.roi_max = (P.roi_max + 15) & ~15;
+    fa.win_max = (P.win_max + 15) & ~15;
+    const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max);
+    hipLaunchKernelGGL(k_fast_cells, dim3((P.ncells + 3) / 4, B), dim3(256), flds, st, fa);
+    // quadtree
+    QtArgs qa;
+    qa.lv = P.d_lv; qa.cell_count = P.d_cell_count; qa.cell_keys = P.d_cell_keys;
+    qa.key_scr = P.d_key_scr; qa.knode = P.d_knode; qa.kq = P.d_kq;
+    qa.ncells_total = P.ncells; qa.slot_total = P.slot_total;
+    qa.qt_key = P.d_qt_key; qa.qt_n = P.d_qt_n; qa.out_total = P.out_total; qa.L = L;
+    qa.ncap = P.max_out_cap + 8;
+    hipLaunchKernelGGL(k_quadtree, dim3(L, B), dim3(256), qt_lds_bytes(P), st, qa);
+    // describe
+    DescArgs da;
+    da.in = d_frames; da.in_fstride = fstride; da.in_pitch = pitch0;
+    da.pyr = P.d_pyr; da.pyr_fstride = P.pyr_bytes;
+    da.blur = P.d_blur; da.blur_fstride = P.blur_bytes;
+    da.lv = P.d_lv; da.qt_key = P.d_qt_key; da.qt_n = P.d_qt_n;
+    da.angle = P.d_angle; da.sdesc = P.d_sdesc; da.out_total = P.out_total; da.L = L;
+    da.fma = hd->prm.fma_sampling != 0;
+    for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
+    hipLaunchKernelGGL(k_describe, dim3(L, B, 8), dim3(256), 0, st, da);
+    // assemble
+    AsmArgs aa;
+    aa.lv = P.d_lv; aa.qt_key = P.d_qt_key; aa.qt_n = P.d_qt_n; aa.angle = P.d_angle; aa.sdesc = P.d_sdesc;
+    aa.out_total = P.out_total; aa.L = L; aa.lap0 = lap0; aa.lap1 = lap1;
+    aa.kps = d_kps; aa.desc = d_desc; aa.cap = cap; aa.n_out = d_n; aa.mono_out = d_mono;
+    hipLaunchKernelGGL(k_assemble, dim3(B), dim3(256), (size_t)P.out_total * 4 + 64, st, aa);
+    ORB_CHECK(hipGetLastError());
+    return ORB_OK;
+}
+
+}  // namespace orbmi
+
+using namespace orbmi;
+
+extern "C" {
+
+orbx_handle* orbx_create(const orbx_params* p, int device) {
+    if (!p || p->nlevels < 1 || p->nlevels > kMaxLevels || !(p->scale_factor > 1.f) || p->nfeatures < 0)
+        return nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    static bool pattern_loaded[64] = {false};
+    if (!pattern_loaded[device]) {
+        if (hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), h_pattern, sizeof(h_pattern)) != hipSuccess) return nullptr;
+        pattern_loaded[device] = true;
+    }
+    orbx_handle* h = new orbx_handle();
+    h->prm = *p;
+    h->device = device;
+    init_tables(h);
+    return h;
+}
+
+void orbx_destroy(orbx_handle* h) {
+    if (!h) return;
+    (void)hipSetDevice(h->device);
+    h->plan.release();
+    delete h;
+}
+
+int orbx_get_tables(const orbx_handle* h, float* scale, float* inv_scale, float* sigma2, float* inv_sigma2,
+                    int32_t* fpl, int32_t* umax) {
+    if (!h) return ORB_ERR_PARAM;
+    for (int l = 0; l < h->prm.nlevels; ++l) {
+        if (scale) scale[l] = h->scale[l];
+        if (inv_scale) inv_scale[l] = h->inv_scale[l];
+        if (sigma2) sigma2[l] = h->sigma2[l];
+        if (inv_sigma2) inv_sigma2[l] = h->inv_sigma2[l];
+        if (fpl) fpl[l] = h->nfeat[l];
+    }
+    if (umax) for (int v = 0; v <= kHalfPatch; ++v) umax[v] = h->umax[v];
+    return ORB_OK;
+}
+
+int orbx_max_keypoints(orbx_handle* h, int w, int hh) {
+    if (!h) return ORB_ERR_PARAM;
+    (void)hipSetDevice(h->device);
+    const int maxB = std::max(1, h->plan.maxB);
+    int rc = build_plan(h, w, hh, maxB);
+    if (rc) return rc;
+    return h->plan.out_total;
+}
+
+int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_frames, size_t frame_stride,
+                              size_t row_step, int w, int hh, int lap0, int lap1, orb_keypoint* d_kps,
+                              uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono, void* stream) {
+    if (!h || nframes <= 0 || !d_frames) return ORB_ERR_PARAM;
+    if (w <= 0 || hh <= 0) return ORB_ERR_EMPTY;
+    if (hipSetDevice(h->device) != hipSuccess) return ORB_ERR_DEVICE;
+    int rc = build_plan(h, w, hh, std::max(nframes, h->plan.maxB));
+    if (rc) return rc;
+    if (cap < h->plan.out_total) return ORB_ERR_CAPACITY;
+    return run_pipeline(h, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
+                        d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
+}
+
+int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step, int lap0, int lap1,
+                 orb_keypoint* kps, uint8_t* desc, int cap, int* n_out, int* mono_out) {
+    if (!h) return ORB_ERR_PARAM;
+    if (!img || w <= 0 || hh <= 0) return ORB_ERR_EMPTY;      // ORBextractor.cc:1090-1091
+    if (hipSetDevice(h->device) != hipSuccess) return ORB_ERR_DEVICE;
+    int rc = build_plan(h, w, hh, std::max(1, h->plan.maxB));
+    if (rc) return rc;
+    Plan& P = h->plan;
+    ORB_CHECK(hipMemcpy2D(P.d_in, P.in_pitch, img, step, w, hh, hipMemcpyHostToDevice));
+    rc = run_pipeline(h, 1, P.d_in, (long long)P.in_pitch * hh, (int)P.in_pitch, (float)lap0, (float)lap1, P.d_kps,
+                      P.d_desc, P.host_cap, P.d_n, P.d_mono, 0);
+    if (rc) return rc;
+    int32_t n = 0, mono = 0;
+    ORB_CHECK(hipMemcpy(&n, P.d_n, 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(&mono, P.d_mono, 4, hipMemcpyDeviceToHost));
+    if (n_out) *n_out = n;
+    if (mono_out) *mono_out = mono;
+    h->have_last = true;
+    h->last_w = w; h->last_h = hh;
+    if (n > cap) return ORB_ERR_CAPACITY;
+    if (n > 0) {
+        ORB_CHECK(hipMemcpy(kps, P.d_kps, n * sizeof(orb_keypoint), hipMemcpyDeviceToHost));
+        ORB_CHECK(hipMemcpy(desc, P.d_desc, (size_t)n * 32, hipMemcpyDeviceToHost));
+    }
+    return ORB_OK;
+}
+
+int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step, int* w, int* hh) {
+    if (!h || !h->have_last || level < 0 || level >= h->plan.L) return ORB_ERR_PARAM;
+    const Plan& P = h->plan;
+    const LevelDev& d = P.lv[level];
+    if (w) *w = d.w;
+    if (hh) *hh = d.h;
+    if (!dst) return ORB_OK;
+    (void)hipSetDevice(h->device);
+    const uint8_t* src = level == 0 ? P.d_in : P.d_pyr + d.off;
+    const size_t sp = level == 0 ? P.in_pitch : (size_t)d.pitch;
+    ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_debug_stage(orbx_handle* h, int stage, orb_keypoint* kps, int cap, int32_t* counts) {
+    if (!h || !h->have_last) return ORB_ERR_PARAM;
+    (void)hipSetDevice(h->device);
+    const Plan& P = h->plan;
+    int off = 0;
+    if (stage == 0) {
+        std::vector<int> cc(P.ncells);
+        std::vector<uint32_t> keys(P.slot_total);
+        ORB_CHECK(hipMemcpy(cc.data(), P.d_cell_count, cc.size() * 4, hipMemcpyDeviceToHost));
+        ORB_CHECK(hipMemcpy(keys.data(), P.d_cell_keys, keys.size() * 4, hipMemcpyDeviceToHost));
+        for (int l = 0; l < P.L; ++l) {
+            const LevelDev& d = P.lv[l];
+            int nl = 0;
+            for (int c = d.cell_base; c < d.cell_base + d.ncells; ++c)
+                for (int j = 0; j < cc[c]; ++j, ++nl, ++off) {
+                    const uint32_t k = keys[P.cells[c].slot_off + j];
+                    if (off < cap) kps[off] = orb_keypoint{(float)(k & 0xfff), (float)((k >> 12) & 0xfff), 7.f,
+                                                           -1.f, (float)(k >> 24), 0, -1};
+                }
+            if (counts) counts[l] = nl;
+        }
+    } else {
+        std::vector<int> qn(P.L);
+        std::vector<uint32_t> keys(P.out_total);
+        ORB_CHECK(hipMemcpy(qn.data(), P.d_qt_n, qn.size() * 4, hipMemcpyDeviceToHost));
+        ORB_CHECK(hipMemcpy(keys.data(), P.d_qt_key, keys.size() * 4, hipMemcpyDeviceToHost));
+        for (int l = 0; l < P.L; ++l) {
+            const LevelDev& d = P.lv[l];
+            if (counts) counts[l] = qn[l];
+            for (int p = 0; p < qn[l]; ++p, ++off) {
+                const uint32_t k = keys[d.out_base + p];
+                if (off < cap)
+                    kps[off] = orb_keypoint{(float)((k & 0xfff) + kEdge - 3), (float)(((k >> 12) & 0xfff) + kEdge - 3),
+                                            (float)d.patch, -1.f, (float)(k >> 24), l, -1};
+            }
+        }
+    }
+    return off <= cap ? off : ORB_ERR_CAPACITY;
+}
+
+}  // extern "C"

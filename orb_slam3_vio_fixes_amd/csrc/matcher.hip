@@ -1,0 +1,831 @@
+// matcher.hip — MI355X-native ORBmatcher searches, Frame grid and DBoW2 descent.
+//
+// Replaces ORB_SLAM3::ORBmatcher (reference src/ORBmatcher.cc:43-763,
+// 1676-2074), Frame::AssignFeaturesToGrid / GetFeaturesInArea (Frame.cc:385-416,
+// 657-735) and TemplatedVocabulary::transform (TemplatedVocabulary.h:1217-1259).
+//
+// Every search has a serial dependency in the reference (a query skips frame
+// features that an EARLIER query already took), so each search runs as one
+// wavefront per (query set, frame): queries are visited in reference order by
+// the whole wave, the candidates of one query are spread over the 64 lanes,
+// Hamming distances use v_xor + v_bcnt on 8 dwords, and the best / second-best
+// selection is a lexicographic (distance, candidate order) wave reduction that
+// reproduces the reference's sequential `if (d < best) ... else if (d < best2)`.
+// Candidate order is GetFeaturesInArea's: grid cells column-major (ix outer,
+// iy inner), feature index ascending inside a cell.  The grid is a per-frame
+// array of feature indices sorted by (ix*48+iy, index) built by a bitonic sort
+// in LDS; scanning that array in order and testing the cell range and the
+// |dx| < r, |dy| < r window yields exactly the reference's candidate list.
+#include "../../include/orb_mi355x.h"
+#include "common.h"
+#include "orb_math.h"
+
+#include <algorithm>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+namespace orbmi {
+
+constexpr int kGridCols = 64, kGridRows = 48;        // Frame.h:44-45
+constexpr int kThHigh = 100, kThLow = 50, kHisto = 30;   // ORBmatcher.cc:35-37
+constexpr int kGridInvalid = 0x7fff;
+
+struct GridParams { float min_x, min_y, inv_w, inv_h; };
+
+// Frame::PosInGrid (Frame.cc:725-735)
+__device__ __forceinline__ int grid_cell(const orb_keypoint& k, const GridParams& g) {
+    const int gx = (int)roundf((k.x - g.min_x) * g.inv_w);
+    const int gy = (int)roundf((k.y - g.min_y) * g.inv_h);
+    if (gx < 0 || gx >= kGridCols || gy < 0 || gy >= kGridRows) return -1;
+    return gx * kGridRows + gy;
+}
+
+__device__ __forceinline__ int hamming32(const uint4 a0, const uint4 a1, const uint8_t* b) {
+    const uint4 b0 = *(const uint4*)b, b1 = *(const uint4*)(b + 16);
+    return __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+           __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+}
+
+// ---------------------------------------------------------------------------
+// k_grid: AssignFeaturesToGrid for a batch of frames.  Output per frame: the
+// feature indices sorted by (cell, index), packed (cell << 16 | index), and
+// their count (features outside the grid are dropped, as PosInGrid does).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_grid(const orb_keypoint* __restrict__ kps, const int* __restrict__ n,
+                                              int cap, GridParams g, uint32_t* __restrict__ sorted,
+                                              int* __restrict__ count, int sort_cap) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
+    const int f = blockIdx.x, tid = threadIdx.x;
+    const int nf = min(n[f], cap);
+    for (int i = tid; i < sort_cap; i += blockDim.x) {
+        uint32_t v = 0xffffffffu;
+        if (i < nf) {
+            const int c = grid_cell(kps[(long long)f * cap + i], g);
+            if (c >= 0) v = ((uint32_t)c << 16) | (uint32_t)i;
+        }
+        keys[i] = v;
+    }
+    __syncthreads();
+    for (int k = 2; k <= sort_cap; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < sort_cap; i += blockDim.x) {
+                const int ixj = i ^ j;
+                if (ixj > i) {
+                    const uint32_t a = keys[i], b = keys[ixj];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { keys[i] = b; keys[ixj] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    int valid = 0;
+    for (int i = tid; i < sort_cap; i += blockDim.x) {
+        const uint32_t v = keys[i];
+        if (v != 0xffffffffu) { sorted[(long long)f * cap + i] = v; ++valid; }
+    }
+    valid = wave_sum(valid);
+    __shared__ int wsum[4];
+    if (lane_id() == 0) wsum[wave_id()] = valid;
+    __syncthreads();
+    if (tid == 0) count[f] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+
+// GetFeaturesInArea cell range (Frame.cc:661-689); false = empty.
+struct CellRange { int x0, x1, y0, y1; };
+__device__ __forceinline__ bool cell_range(float x, float y, float r, const GridParams& g, CellRange& cr) {
+    cr.x0 = max(0, (int)floorf((x - g.min_x - r) * g.inv_w));
+    if (cr.x0 >= kGridCols) return false;
+    cr.x1 = min(kGridCols - 1, (int)ceilf((x - g.min_x + r) * g.inv_w));
+    if (cr.x1 < 0) return false;
+    cr.y0 = max(0, (int)floorf((y - g.min_y - r) * g.inv_h));
+    if (cr.y0 >= kGridRows) return false;
+    cr.y1 = min(kGridRows - 1, (int)ceilf((y - g.min_y + r) * g.inv_h));
+    if (cr.y1 < 0) return false;
+    return true;
+}
+
+// Running best / second-best over a candidate stream in reference order.
+struct Best2 {
+    int best, best2, idx, lvl, lvl2;
+};
+
+// Merge one wave chunk (candidate of this lane: dist d (INT_MAX = none), feature
+// index fi, level lv; lanes in stream order) into the running state with the
+// exact semantics of the sequential loop
+//   if (d < best) {best2 = best; lvl2 = lvl; best = d; lvl = lv; idx = fi;}
+//   else if (d < best2) {best2 = d; lvl2 = lv;}
+__device__ __forceinline__ void merge_chunk(Best2& st, int d, int fi, int lv) {
+    // chunk minimum and its first lane
+    int m = d;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, kWave));
+    if (m == INT_MAX) return;
+    const uint64_t at = __ballot(d == m);
+    const int first = __ffsll((long long)at) - 1;
+    const int fi_m = __shfl(fi, first, kWave), lv_m = __shfl(lv, first, kWave);
+    // chunk second: min over lanes other than `first`, with its first lane
+    int d2 = lane_id() == first ? INT_MAX : d;
+    int m2 = d2;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m2 = min(m2, __shfl_xor(m2, o, kWave));
+    int lv_m2 = -1;
+    if (m2 != INT_MAX) {
+        const uint64_t at2 = __ballot(d2 == m2);
+        lv_m2 = __shfl(lv, __ffsll((long long)at2) - 1, kWave);
+    }
+    // sequential merge: the chunk's elements come after the running ones.
+    // New best: strictly smaller chunk min replaces; the old best becomes a
+    // second candidate.  The second-smallest of the union with the level of
+    // the element the sequential loop would have recorded.
+    if (m < st.best) {
+        // old best is pushed to second unless the chunk's own second is smaller
+        int nb2 = st.best, nl2 = st.lvl;
+        if (m2 < nb2) { nb2 = m2; nl2 = lv_m2; }
+        st.best2 = nb2; st.lvl2 = nl2;
+        st.best = m; st.lvl = lv_m; st.idx = fi_m;
+    } else {
+        // chunk min m >= best: it competes for second (first lane of m first)
+        if (m < st.best2) { st.best2 = m; st.lvl2 = lv_m; }
+    }
+}
+
+__device__ __forceinline__ int rot_bin(float a1, float a2) {
+    float rot = a1 - a2;
+    if (rot < 0.0f) rot += 360.0f;
+    int bin = (int)roundf(rot * (1.0f / kHisto));
+    if (bin == kHisto) bin = 0;
+    return bin;
+}
+
+// ComputeThreeMaxima (ORBmatcher.cc:2012-2053)
+__device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
+    int m1 = 0, m2 = 0, m3 = 0;
+    i1 = i2 = i3 = -1;
+    for (int i = 0; i < kHisto; ++i) {
+        const int s = h[i];
+        if (s > m1) { m3 = m2; m2 = m1; m1 = s; i3 = i2; i2 = i1; i1 = i; }
+        else if (s > m2) { m3 = m2; m2 = s; i3 = i2; i2 = i; }
+        else if (s > m3) { m3 = s; i3 = i; }
+    }
+    if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+    else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+}
+
+// ---------------------------------------------------------------------------
+// k_sfi: ORBmatcher::SearchForInitialization (ORBmatcher.cc:648-763), one wave
+// per frame pair.  LDS: F2's level-0 features in grid order, vMatchedDistance,
+// vnMatches21, the rotation bin of every accepted F1 feature.
+// ---------------------------------------------------------------------------
+struct SfiArgs {
+    const orb_keypoint* kps;
+    const uint8_t* desc;
+    const int* n;
+    int cap;
+    const uint32_t* gsorted;
+    const int* gcount;
+    const int* pair_f1;      // per pair: frame index of F1 (F2 = pair_f2)
+    const int* pair_f2;
+    const float* prev_in;    // [pair][cap][2] or null (= F1 keypoint positions)
+    float* prev_out;         // [pair][cap][2] or null
+    GridParams g;
+    float window, ratio;
+    int check_ori;
+    int32_t* matches;        // [pair][cap]
+    int32_t* nmatches;       // [pair]
+};
+
+__global__ __launch_bounds__(64) void k_sfi(SfiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int pr = blockIdx.x, lane = lane_id();
+    const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
+    const int n1 = min(a.n[f1], a.cap), n2 = min(a.n[f2], a.cap);
+    const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
+    const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
+    const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
+    const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
+    int* list = lds;                          // cap: (cell<<16 | idx) of level-0 F2 features
+    int* mdist = list + a.cap;                // cap
+    int* m21 = mdist + a.cap;                 // cap
+    int* hist = m21 + a.cap;                  // 32
+    int8_t* bin1 = (int8_t*)(hist + 32);      // cap: rotation bin of F1 feature or -1
+    int32_t* m12 = a.matches + (long long)pr * a.cap;
+    // level-0 filter of the grid order (GetFeaturesInArea(..., level1, level1) with level1 = 0)
+    const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
+    const int gn = a.gcount[f2];
+    int nl = 0;
+    for (int base = 0; base < gn; base += kWave) {
+        const int i = base + lane;
+        uint32_t v = 0;
+        bool keep = false;
+        if (i < gn) { v = gs[i]; keep = K2[v & 0xffff].octave == 0; }
+        const uint64_t m = __ballot(keep);
+        if (keep) list[nl + mask_rank(m)] = (int)v;
+        nl += __popcll(m);
+    }
+    for (int i = lane; i < n2; i += kWave) { mdist[i] = INT_MAX; m21[i] = -1; }
+    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
+    for (int i = lane; i < n1; i += kWave) { m12[i] = -1; bin1[i] = -1; }
+    __syncthreads();
+    int nm = 0;
+    const float r = a.window;
+    for (int i1 = 0; i1 < n1; ++i1) {
+        const orb_keypoint k1 = K1[i1];
+        if (k1.octave > 0) continue;
+        float px = k1.x, py = k1.y;
+        if (a.prev_in) { px = a.prev_in[((long long)pr * a.cap + i1) * 2]; py = a.prev_in[((long long)pr * a.cap + i1) * 2 + 1]; }
+        CellRange cr;
+        if (!cell_range(px, py, r, a.g, cr)) continue;
+        const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32), q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+        Best2 st{INT_MAX, INT_MAX, -1, 0, 0};
+        for (int base = 0; base < nl; base += kWave) {
+            const int j = base + lane;
+            int d = INT_MAX, fi = -1;
+            if (j < nl) {
+                const int v = list[j];
+                const int cell = v >> 16, gx = cell / kGridRows, gy = cell - gx * kGridRows;
+                fi = v & 0xffff;
+                if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1) {
+                    const orb_keypoint k2 = K2[fi];
+                    if (fabsf(k2.x - px) < r && fabsf(k2.y - py) < r) {
+                        const int dist = hamming32(q0, q1, D2 + (long long)fi * 32);
+                        if (!(mdist[fi] <= dist)) d = dist;
+                    }
+                }
+            }
+            merge_chunk(st, d, fi, 0);
+        }
+        if (st.best <= kThLow && (float)st.best < (float)st.best2 * a.ratio) {
+            const int b2 = st.idx;
+            if (m21[b2] >= 0) {
+                if (lane == 0) m12[m21[b2]] = -1;
+                --nm;
+            }
+            if (lane == 0) {
+                m12[i1] = b2;
+                m21[b2] = i1;
+                mdist[b2] = st.best;
+            }
+            ++nm;
+            if (a.check_ori) {
+                const int bn = rot_bin(k1.angle, K2[b2].angle);
+                if (lane == 0) { hist[bn]++; bin1[i1] = (int8_t)bn; }
+            }
+        }
+        __syncthreads();
+    }
+    if (a.check_ori) {
+        int i1x, i2x, i3x;
+        three_maxima(hist, i1x, i2x, i3x);
+        int drop = 0;
+        for (int i = lane; i < n1; i += kWave) {
+            const int b = bin1[i];
+            if (b < 0 || b == i1x || b == i2x || b == i3x) continue;
+            if (m12[i] >= 0) { m12[i] = -1; ++drop; }
+        }
+        nm -= wave_sum(drop);
+    }
+    if (a.prev_out) {
+        for (int i = lane; i < n1; i += kWave) {
+            float px = K1[i].x, py = K1[i].y;
+            if (a.prev_in) { px = a.prev_in[((long long)pr * a.cap + i) * 2]; py = a.prev_in[((long long)pr * a.cap + i) * 2 + 1]; }
+            const int m = m12[i];
+            if (m >= 0) { px = K2[m].x; py = K2[m].y; }
+            a.prev_out[((long long)pr * a.cap + i) * 2] = px;
+            a.prev_out[((long long)pr * a.cap + i) * 2 + 1] = py;
+        }
+    }
+    if (lane == 0) a.nmatches[pr] = nm;
+}
+
+// ---------------------------------------------------------------------------
+// k_bow: ORBmatcher::SearchByBoW(KeyFrame*, Frame&) (ORBmatcher.cc:223-425),
+// mono branch, one wave per (keyframe, frame) pair: merge-join of the two
+// FeatureVectors by node id; per KF feature with a valid MapPoint, best/second
+// over the frame features of the node that are not yet matched.
+// ---------------------------------------------------------------------------
+struct BowArgs {
+    // keyframes (npairs): features, FeatureVector CSR, MapPoint validity
+    const orb_keypoint* kf_kps;  const long long* kf_kp_off;
+    const uint8_t* kf_desc;      // same offsets * 32
+    const uint8_t* kf_valid;     // same offsets
+    const uint32_t* kf_node;     const int* kf_off;   const uint32_t* kf_idx;
+    const long long* kf_fv_node_off;   // per pair: offset into kf_node / (kf_off - 1 more)
+    const int* kf_fv_nnodes;
+    const long long* kf_fv_off_off;    // per pair: offset into kf_off
+    const long long* kf_fv_idx_off;    // per pair: offset into kf_idx
+    // frame (shared by all pairs)
+    const orb_keypoint* f_kps;  const uint8_t* f_desc;  int f_n;
+    const uint32_t* f_node;  const int* f_off;  const uint32_t* f_idx;  int f_nnodes;
+    float ratio;
+    int check_ori;
+    int32_t* match;      // [pair][f_n]
+    int32_t* nmatches;   // [pair]
+};
+
+__global__ __launch_bounds__(64) void k_bow(BowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int pr = blockIdx.x, lane = lane_id();
+    int* hist = lds;                  // 32
+    int8_t* fbin = (int8_t*)(lds + 32);   // f_n: bin of the match recorded at F feature, or -1
+    int32_t* match = a.match + (long long)pr * a.f_n;
+    for (int i = lane; i < a.f_n; i += kWave) { match[i] = -1; fbin[i] = -1; }
+    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
+    __syncthreads();
+    const long long kpo = a.kf_kp_off[pr];
+    const orb_keypoint* KK = a.kf_kps + kpo;
+    const uint8_t* KD = a.kf_desc + kpo * 32;
+    const uint8_t* KV = a.kf_valid + kpo;
+    const uint32_t* kn = a.kf_node + a.kf_fv_node_off[pr];
+    const int* ko = a.kf_off + a.kf_fv_off_off[pr];
+    const uint32_t* ki = a.kf_idx + a.kf_fv_idx_off[pr];
+    const int knn = a.kf_fv_nnodes[pr];
+    int nm = 0;
+    int ia = 0, ib = 0;
+    while (ia < knn && ib < a.f_nnodes) {
+        const uint32_t na = kn[ia], nb = a.f_node[ib];
+        if (na == nb) {
+            const int fb = a.f_off[ib], fe = a.f_off[ib + 1];
+            for (int p = ko[ia]; p < ko[ia + 1]; ++p) {
+                const int ikf = (int)ki[p];
+                if (!KV[ikf]) continue;
+                const uint4 q0 = *(const uint4*)(KD + (long long)ikf * 32);
+                const uint4 q1 = *(const uint4*)(KD + (long long)ikf * 32 + 16);
+                Best2 st{256, 256, -1, 0, 0};
+                for (int base = fb; base < fe; base += kWave) {
+                    const int q = base + lane;
+                    int d = INT_MAX, fi = -1;
+                    if (q < fe) {
+                        fi = (int)a.f_idx[q];
+                        if (match[fi] < 0) d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
+                    }
+                    merge_chunk(st, d, fi, 0);
+                }
+                if (st.best <= kThLow && (float)st.best < a.ratio * (float)st.best2) {
+                    if (lane == 0) match[st.idx] = ikf;
+                    if (a.check_ori) {
+                        const int bn = rot_bin(KK[ikf].angle, a.f_kps[st.idx].angle);
+                        if (lane == 0) { hist[bn]++; fbin[st.idx] = (int8_t)bn; }
+                    }
+                    ++nm;
+                }
+                __syncthreads();
+            }
+            ++ia; ++ib;
+        } else if (na < nb) {
+            while (ia < knn && kn[ia] < nb) ++ia;      // lower_bound
+        } else {
+            while (ib < a.f_nnodes && a.f_node[ib] < na) ++ib;
+        }
+    }
+    if (a.check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        int drop = 0;
+        for (int i = lane; i < a.f_n; i += kWave) {
+            const int b = fbin[i];
+            if (b < 0 || b == i1 || b == i2 || b == i3) continue;
+            match[i] = -1;
+            ++drop;
+        }
+        nm -= wave_sum(drop);
+    }
+    if (lane == 0) a.nmatches[pr] = nm;
+}
+
+// ---------------------------------------------------------------------------
+// k_proj: SearchByProjection(Frame&, vector<MapPoint*>) (ORBmatcher.cc:43-213)
+// and SearchByProjection(Frame&, const Frame&) (ORBmatcher.cc:1676-1887), the
+// Nleft == -1 branches, one wave per frame.
+// ---------------------------------------------------------------------------
+struct ProjArgs {
+    int mode;                 // 0 = map points, 1 = last frame
+    const orb_keypoint* kps; const uint8_t* desc; int n; const float* u_right; const float* scale;
+    const uint32_t* gsorted; const int* gcount;
+    GridParams g;
+    int nq;
+    const float* qx; const float* qy; const float* qxr;
+    const int32_t* qlevel; const float* qviewcos; const float* qdepth;
+    const uint8_t* qvalid; const uint8_t* qhas_obs; const uint8_t* qdesc; const float* qangle;
+    float th, th_far, ratio;
+    int far_points, last_mode, check_ori;
+    int32_t* owner; const uint8_t* blocked;
+    int32_t* nmatches;
+};
+
+__global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int lane = lane_id();
+    int* hist = lds;
+    int* slot_bin_cnt = hist + 32;            // unused padding
+    (void)slot_bin_cnt;
+    int8_t* sbin = (int8_t*)(lds + 64);      // per F slot: list of bins is needed -> histogram entries
+    // rotation histogram entries in push order: (bin, slot)
+    int* hent = lds + 64 + (a.n + 3) / 4;
+    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
+    (void)sbin;
+    __syncthreads();
+    const int gn = a.gcount[0];
+    int nm = 0, nh = 0;
+    for (int i = 0; i < a.nq; ++i) {
+        if (!a.qvalid[i]) continue;
+        float r, x = a.qx[i], y = a.qy[i];
+        int minL, maxL;
+        if (a.mode == 0) {
+            if (a.far_points && a.qdepth[i] > a.th_far) continue;
+            const int lvl = a.qlevel[i];
+            r = a.qviewcos[i] > 0.998f ? 2.5f : 4.0f;      // RadiusByViewingCos
+            if (a.th != 1.0f) r *= a.th;
+            r = r * a.scale[lvl];
+            minL = lvl - 1; maxL = lvl;
+        } else {
+            const int oct = a.qlevel[i];
+            r = a.th * a.scale[oct];
+            if (a.last_mode == 1) { minL = oct; maxL = -1; }
+            else if (a.last_mode == 2) { minL = 0; maxL = oct; }
+            else { minL = oct - 1; maxL = oct + 1; }
+        }
+        CellRange cr;
+        if (!cell_range(x, y, r, a.g, cr)) continue;
+        const bool checkL = (minL > 0) || (maxL >= 0);
+        const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
+        const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+        Best2 st{256, 256, -1, -1, -1};
+        bool any = false;
+        for (int base = 0; base < gn; base += kWave) {
+            const int j = base + lane;
+            int d = INT_MAX, fi = -1, lv = -1;
+            if (j < gn) {
+                const uint32_t v = a.gsorted[j];
+                const int cell = (int)(v >> 16), gx = cell / kGridRows, gy = cell - gx * kGridRows;
+                fi = (int)(v & 0xffff);
+                if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1) {
+                    const orb_keypoint k = a.kps[fi];
+                    bool ok = true;
+                    if (checkL) {
+                        if (k.octave < minL) ok = false;
+                        if (maxL >= 0 && k.octave > maxL) ok = false;
+                    }
+                    if (ok && fabsf(k.x - x) < r && fabsf(k.y - y) < r) {
+                        const int o = a.owner[fi];
+                        const bool blk = o == -1 ? false : (o <= -2 ? a.blocked[fi] != 0 : a.qhas_obs[o] != 0);
+                        bool pass = !blk;
+                        if (pass && a.u_right && a.u_right[fi] > 0) {
+                            const float er = fabsf(a.qxr[i] - a.u_right[fi]);
+                            if (er > r) pass = false;
+                        }
+                        if (pass) { d = hamming32(q0, q1, a.desc + (long long)fi * 32); lv = k.octave; }
+                        any = true;
+                    }
+                }
+            }
+            merge_chunk(st, d, fi, lv);
+        }
+        (void)any;
+        if (a.mode == 0) {
+            if (st.best <= kThHigh) {
+                if (st.lvl == st.lvl2 && (float)st.best > a.ratio * (float)st.best2) continue;
+                if (st.lvl != st.lvl2 || (float)st.best <= a.ratio * (float)st.best2) {
+                    if (lane == 0) a.owner[st.idx] = i;
+                    ++nm;
+                }
+            }
+        } else {
+            if (st.best <= kThHigh) {
+                if (lane == 0) a.owner[st.idx] = i;
+                ++nm;
+                if (a.check_ori) {
+                    const int bn = rot_bin(a.qangle[i], a.kps[st.idx].angle);
+                    if (lane == 0) { hist[bn]++; hent[nh] = (bn << 16) | st.idx; }
+                    ++nh;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    if (a.mode == 1 && a.check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        __syncthreads();
+        // entries in push order: every entry in a rejected bin clears its slot and decrements
+        int drop = 0;
+        for (int e = lane; e < nh; e += kWave) {
+            const int bn = hent[e] >> 16;
+            if (bn == i1 || bn == i2 || bn == i3) continue;
+            a.owner[hent[e] & 0xffff] = -1;
+            ++drop;
+        }
+        nm -= wave_sum(drop);
+    }
+    if (lane == 0) a.nmatches[0] = nm;
+}
+
+// ---------------------------------------------------------------------------
+// k_transform: TemplatedVocabulary::transform per descriptor
+// (TemplatedVocabulary.h:1217-1259): greedy descent, first child wins ties;
+// one thread per descriptor (the tree lives in L2 / Infinity Cache).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_transform(const int* __restrict__ first_child, const int* __restrict__ nchild,
+                                                   const uint8_t* __restrict__ node_desc,
+                                                   const int* __restrict__ word_id, const double* __restrict__ weight,
+                                                   int n, const uint8_t* __restrict__ desc, int nid_level,
+                                                   int32_t* __restrict__ wid_out, double* __restrict__ w_out,
+                                                   int32_t* __restrict__ nid_out) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint4 q0 = *(const uint4*)(desc + (long long)i * 32), q1 = *(const uint4*)(desc + (long long)i * 32 + 16);
+    int fin = 0, level = 0, nid = 0;
+    do {
+        ++level;
+        const int c0 = first_child[fin], nc = nchild[fin];
+        int best = hamming32(q0, q1, node_desc + (long long)c0 * 32), bid = c0;
+        for (int c = c0 + 1; c < c0 + nc; ++c) {
+            const int d = hamming32(q0, q1, node_desc + (long long)c * 32);
+            if (d < best) { best = d; bid = c; }
+        }
+        fin = bid;
+        if (level == nid_level) nid = fin;
+    } while (nchild[fin] != 0);
+    wid_out[i] = word_id[fin];
+    w_out[i] = weight[fin];
+    nid_out[i] = nid;
+}
+
+// ---------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------
+template <typename T>
+struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t cnt) {
+        if (cnt <= n) return ORB_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        n = 0;
+        if (hipMalloc(&p, std::max<size_t>(1, cnt) * sizeof(T)) != hipSuccess) return ORB_ERR_DEVICE;
+        n = cnt;
+        return ORB_OK;
+    }
+    int put(const T* src, size_t cnt, hipStream_t st = 0) {
+        int rc = alloc(cnt);
+        if (rc) return rc;
+        if (cnt && hipMemcpyAsync(p, src, cnt * sizeof(T), hipMemcpyHostToDevice, st) != hipSuccess) return ORB_ERR_DEVICE;
+        return ORB_OK;
+    }
+    ~DBuf() { if (p) (void)hipFree(p); }
+};
+
+static int pow2_at_least(int n) { int p = 64; while (p < n) p <<= 1; return p; }
+
+static GridParams grid_params(const orbm_frame* f) {
+    return GridParams{f->min_x, f->min_y, f->grid_inv_w, f->grid_inv_h};
+}
+
+// Upload one frame and build its grid order on the device.
+struct DevFrame {
+    DBuf<orb_keypoint> kps;
+    DBuf<uint8_t> desc;
+    DBuf<int> n;
+    DBuf<uint32_t> sorted;
+    DBuf<int> count;
+    DBuf<float> ur, scale;
+    int upload(const orbm_frame* f, bool grid, hipStream_t st) {
+        int rc;
+        const int nn = std::max(1, f->n);
+        if ((rc = kps.alloc(nn)) || (rc = desc.alloc((size_t)nn * 32)) || (rc = n.put(&f->n, 1, st))) return rc;
+        if (f->n) {
+            if (hipMemcpyAsync(kps.p, f->kps, f->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, st) != hipSuccess ||
+                hipMemcpyAsync(desc.p, f->desc, (size_t)f->n * 32, hipMemcpyHostToDevice, st) != hipSuccess)
+                return ORB_ERR_DEVICE;
+        }
+        if (f->u_right && (rc = ur.put(f->u_right, f->n, st))) return rc;
+        if (f->scale_factors && (rc = scale.put(f->scale_factors, f->nlevels, st))) return rc;
+        if (grid) {
+            if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1))) return rc;
+            const int sc = pow2_at_least(nn);
+            hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
+                               grid_params(f), sorted.p, count.p, sc);
+        }
+        return ORB_OK;
+    }
+};
+
+static int device_ok() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return ORB_ERR_DEVICE;
+    return ORB_OK;
+}
+
+}  // namespace orbmi
+
+using namespace orbmi;
+
+extern "C" {
+
+int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b) {
+    // host inline utility (Frame.cc:886, MapPoint.cc:377 call it on single pairs)
+    int d = 0;
+    for (int i = 0; i < 32; ++i) d += __builtin_popcount((unsigned)(a[i] ^ b[i]));
+    return d;
+}
+
+int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, float* prev_xy, int window,
+                                   float nnratio, int check_ori, int32_t* matches12) {
+    if (!f1 || !f2 || !prev_xy || !matches12) return ORB_ERR_PARAM;
+    if (device_ok()) return ORB_ERR_DEVICE;
+    if (f1->n > 0xffff || f2->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    // both frames share one [2][cap] layout
+    const int cap = std::max(1, std::max(f1->n, f2->n));
+    DBuf<orb_keypoint> kps; DBuf<uint8_t> desc; DBuf<int> n; DBuf<uint32_t> sorted; DBuf<int> count;
+    DBuf<int> pf; DBuf<float> prev_in, prev_out; DBuf<int32_t> m; DBuf<int32_t> nm;
+    int rc;
+    if ((rc = kps.alloc(2 * cap)) || (rc = desc.alloc((size_t)2 * cap * 32)) || (rc = sorted.alloc(2 * cap)) ||
+        (rc = count.alloc(2)) || (rc = m.alloc(cap)) || (rc = nm.alloc(1)) || (rc = prev_out.alloc((size_t)2 * cap)))
+        return rc;
+    const int ns[2] = {f1->n, f2->n};
+    const int pfs[2] = {0, 1};
+    if ((rc = n.put(ns, 2)) || (rc = pf.put(pfs, 2))) return rc;
+    std::vector<float> pv((size_t)2 * cap, 0.f);
+    std::memcpy(pv.data(), prev_xy, sizeof(float) * 2 * f1->n);
+    if ((rc = prev_in.put(pv.data(), pv.size()))) return rc;
+    if (f1->n) {
+        ORB_CHECK(hipMemcpy(kps.p, f1->kps, f1->n * sizeof(orb_keypoint), hipMemcpyHostToDevice));
+        ORB_CHECK(hipMemcpy(desc.p, f1->desc, (size_t)f1->n * 32, hipMemcpyHostToDevice));
+    }
+    if (f2->n) {
+        ORB_CHECK(hipMemcpy(kps.p + cap, f2->kps, f2->n * sizeof(orb_keypoint), hipMemcpyHostToDevice));
+        ORB_CHECK(hipMemcpy(desc.p + (size_t)cap * 32, f2->desc, (size_t)f2->n * 32, hipMemcpyHostToDevice));
+    }
+    const GridParams g = grid_params(f2);
+    const int sc = pow2_at_least(cap);
+    hipLaunchKernelGGL(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p, count.p, sc);
+    SfiArgs a;
+    a.kps = kps.p; a.desc = desc.p; a.n = n.p; a.cap = cap; a.gsorted = sorted.p; a.gcount = count.p;
+    a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = prev_in.p; a.prev_out = prev_out.p;
+    a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
+    a.matches = m.p; a.nmatches = nm.p;
+    const size_t lds = (size_t)cap * 12 + 128 + cap + 16;
+    hipLaunchKernelGGL(k_sfi, dim3(1), dim3(64), lds, 0, a);
+    ORB_CHECK(hipGetLastError());
+    int32_t res = 0;
+    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
+    if (f1->n) {
+        ORB_CHECK(hipMemcpy(matches12, m.p, f1->n * 4, hipMemcpyDeviceToHost));
+        ORB_CHECK(hipMemcpy(prev_xy, prev_out.p, f1->n * 8, hipMemcpyDeviceToHost));
+    }
+    return res;
+}
+
+int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint* d_kps, const uint8_t* d_desc,
+                                                const int32_t* d_n, int cap, float min_x, float max_x, float min_y,
+                                                float max_y, float grid_inv_w, float grid_inv_h, int window,
+                                                float nnratio, int check_ori, int32_t* d_matches, int32_t* d_nmatches,
+                                                void* stream) {
+    (void)max_x; (void)max_y;
+    if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
+    hipStream_t st = (hipStream_t)stream;
+    static thread_local DBuf<uint32_t> sorted;
+    static thread_local DBuf<int> count, pf;
+    static thread_local int pf_frames = 0;
+    int rc;
+    if ((rc = sorted.alloc((size_t)nframes * cap)) || (rc = count.alloc(nframes))) return rc;
+    if (pf_frames < nframes) {
+        std::vector<int> idx(nframes);
+        for (int i = 0; i < nframes; ++i) idx[i] = i;
+        if ((rc = pf.put(idx.data(), nframes))) return rc;
+        ORB_CHECK(hipDeviceSynchronize());
+        pf_frames = nframes;
+    }
+    const GridParams g{min_x, min_y, grid_inv_w, grid_inv_h};
+    const int sc = pow2_at_least(cap);
+    hipLaunchKernelGGL(k_grid, dim3(nframes), dim3(256), sc * sizeof(uint32_t), st, d_kps, d_n, cap, g, sorted.p,
+                       count.p, sc);
+    SfiArgs a;
+    a.kps = d_kps; a.desc = d_desc; a.n = d_n; a.cap = cap; a.gsorted = sorted.p; a.gcount = count.p;
+    a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = nullptr; a.prev_out = nullptr;
+    a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
+    a.matches = d_matches; a.nmatches = d_nmatches;
+    const size_t lds = (size_t)cap * 12 + 128 + cap + 16;
+    hipLaunchKernelGGL(k_sfi, dim3(nframes - 1), dim3(64), lds, st, a);
+    ORB_CHECK(hipGetLastError());
+    return ORB_OK;
+}
+
+int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid, const orbm_frame* f,
+                       const orbm_featvec* ffv, float nnratio, int check_ori, int32_t* match_f) {
+    if (!kf || !kfv || !kf_valid || !f || !ffv || !match_f) return ORB_ERR_PARAM;
+    if (device_ok()) return ORB_ERR_DEVICE;
+    int rc;
+    DBuf<orb_keypoint> kk, fk; DBuf<uint8_t> kd, fd, kvv; DBuf<uint32_t> kn, ki, fn, fi; DBuf<int> ko, fo;
+    DBuf<long long> z; DBuf<int> knn; DBuf<int32_t> m, nm;
+    const long long zeros[4] = {0, 0, 0, 0};
+    if ((rc = kk.put(kf->kps, kf->n)) || (rc = kd.put(kf->desc, (size_t)kf->n * 32)) || (rc = kvv.put(kf_valid, kf->n)) ||
+        (rc = kn.put(kfv->node_ids, kfv->nnodes)) || (rc = ko.put(kfv->offsets, kfv->nnodes + 1)) ||
+        (rc = ki.put(kfv->idx, kfv->offsets[kfv->nnodes])) || (rc = fk.put(f->kps, f->n)) ||
+        (rc = fd.put(f->desc, (size_t)f->n * 32)) || (rc = fn.put(ffv->node_ids, ffv->nnodes)) ||
+        (rc = fo.put(ffv->offsets, ffv->nnodes + 1)) || (rc = fi.put(ffv->idx, ffv->offsets[ffv->nnodes])) ||
+        (rc = z.put(zeros, 4)) || (rc = knn.put(&kfv->nnodes, 1)) || (rc = m.alloc(std::max(1, f->n))) ||
+        (rc = nm.alloc(1)))
+        return rc;
+    BowArgs a;
+    a.kf_kps = kk.p; a.kf_kp_off = z.p; a.kf_desc = kd.p; a.kf_valid = kvv.p;
+    a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p;
+    a.kf_fv_node_off = z.p; a.kf_fv_nnodes = knn.p; a.kf_fv_off_off = z.p; a.kf_fv_idx_off = z.p;
+    a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
+    a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
+    hipLaunchKernelGGL(k_bow, dim3(1), dim3(64), 128 + f->n + 16, 0, a);
+    ORB_CHECK(hipGetLastError());
+    int32_t res = 0;
+    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
+    if (f->n) ORB_CHECK(hipMemcpy(match_f, m.p, f->n * 4, hipMemcpyDeviceToHost));
+    return res;
+}
+
+static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* owner, const uint8_t* blocked) {
+    int rc;
+    DBuf<int32_t> own, nm; DBuf<uint8_t> blk;
+    if ((rc = own.put(owner, std::max(1, f->n))) || (rc = blk.put(blocked, std::max(1, f->n))) || (rc = nm.alloc(1)))
+        return rc;
+    a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
+    a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.g = grid_params(f);
+    a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
+    const size_t lds = 64 * 4 + (f->n + 3) / 4 * 4 + (size_t)(a.nq + 1) * 4 + 64;
+    hipLaunchKernelGGL(k_proj, dim3(1), dim3(64), lds, 0, a);
+    ORB_CHECK(hipGetLastError());
+    int32_t res = 0;
+    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
+    if (f->n) ORB_CHECK(hipMemcpy(owner, own.p, f->n * 4, hipMemcpyDeviceToHost));
+    return res;
+}
+
+int orbm_search_by_projection_mps(const orbm_frame* f, const orbm_mappoints* mps, float th, int far_points,
+                                  float th_far, float nnratio, int32_t* owner, const uint8_t* blocked) {
+    if (!f || !mps || !owner || !blocked || !f->scale_factors) return ORB_ERR_PARAM;
+    if (device_ok()) return ORB_ERR_DEVICE;
+    if (f->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    DevFrame df;
+    int rc = df.upload(f, true, 0);
+    if (rc) return rc;
+    const int nq = mps->n;
+    DBuf<float> qx, qy, qxr, vc, dp; DBuf<int32_t> lv; DBuf<uint8_t> iv, ho, qd;
+    if ((rc = qx.put(mps->proj_x, nq)) || (rc = qy.put(mps->proj_y, nq)) || (rc = qxr.put(mps->proj_xr, nq)) ||
+        (rc = lv.put(mps->level, nq)) || (rc = vc.put(mps->view_cos, nq)) || (rc = dp.put(mps->track_depth, nq)) ||
+        (rc = iv.put(mps->in_view, nq)) || (rc = ho.put(mps->has_obs, nq)) || (rc = qd.put(mps->desc, (size_t)nq * 32)))
+        return rc;
+    ProjArgs a{};
+    a.mode = 0; a.nq = nq; a.qx = qx.p; a.qy = qy.p; a.qxr = qxr.p; a.qlevel = lv.p; a.qviewcos = vc.p;
+    a.qdepth = dp.p; a.qvalid = iv.p; a.qhas_obs = ho.p; a.qdesc = qd.p; a.qangle = nullptr;
+    a.th = th; a.th_far = th_far; a.ratio = nnratio; a.far_points = far_points; a.last_mode = 0; a.check_ori = 0;
+    return run_proj(a, f, df, owner, blocked);
+}
+
+int orbm_search_by_projection_last(const orbm_frame* cur, int nlast, const uint8_t* valid, const float* u,
+                                   const float* v, const float* ur, const int32_t* last_octave,
+                                   const float* last_angle, const uint8_t* has_obs, const uint8_t* last_desc,
+                                   float th, int mode, int check_ori, int32_t* owner, const uint8_t* blocked) {
+    if (!cur || !valid || !u || !v || !ur || !last_octave || !last_angle || !has_obs || !last_desc || !owner ||
+        !blocked || !cur->scale_factors)
+        return ORB_ERR_PARAM;
+    if (device_ok()) return ORB_ERR_DEVICE;
+    if (cur->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    DevFrame df;
+    int rc = df.upload(cur, true, 0);
+    if (rc) return rc;
+    DBuf<float> qx, qy, qxr, qa; DBuf<int32_t> lv; DBuf<uint8_t> iv, ho, qd;
+    if ((rc = qx.put(u, nlast)) || (rc = qy.put(v, nlast)) || (rc = qxr.put(ur, nlast)) ||
+        (rc = lv.put(last_octave, nlast)) || (rc = qa.put(last_angle, nlast)) || (rc = iv.put(valid, nlast)) ||
+        (rc = ho.put(has_obs, nlast)) || (rc = qd.put(last_desc, (size_t)nlast * 32)))
+        return rc;
+    ProjArgs a{};
+    a.mode = 1; a.nq = nlast; a.qx = qx.p; a.qy = qy.p; a.qxr = qxr.p; a.qlevel = lv.p; a.qviewcos = nullptr;
+    a.qdepth = nullptr; a.qvalid = iv.p; a.qhas_obs = ho.p; a.qdesc = qd.p; a.qangle = qa.p;
+    a.th = th; a.th_far = 0; a.ratio = 0; a.far_points = 0; a.last_mode = mode; a.check_ori = check_ori;
+    return run_proj(a, cur, df, owner, blocked);
+}
+
+int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levelsup, int32_t* word_id,
+                   double* weight, int32_t* node_id, int device) {
+    if (!voc || n < 0 || !desc || !word_id || !weight || !node_id) return ORB_ERR_PARAM;
+    if (device < 0) return ORB_ERR_PARAM;     // the product path runs on the GPU only
+    if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    if (n == 0) return ORB_OK;
+    int rc;
+    DBuf<int> fc, nc, wid; DBuf<uint8_t> nd, dd; DBuf<double> wt, wo; DBuf<int32_t> wio, nio;
+    if ((rc = fc.put(voc->first_child, voc->nnodes)) || (rc = nc.put(voc->nchild, voc->nnodes)) ||
+        (rc = nd.put(voc->node_desc, (size_t)voc->nnodes * 32)) || (rc = wid.put(voc->word_id, voc->nnodes)) ||
+        (rc = wt.put(voc->weight, voc->nnodes)) || (rc = dd.put(desc, (size_t)n * 32)) || (rc = wo.alloc(n)) ||
+        (rc = wio.alloc(n)) || (rc = nio.alloc(n)))
+        return rc;
+    const int nid_level = voc->depth_levels - levelsup;
+    hipLaunchKernelGGL(k_transform, dim3((n + 255) / 256), dim3(256), 0, 0, fc.p, nc.p, nd.p, wid.p, wt.p, n, dd.p,
+                       nid_level, wio.p, wo.p, nio.p);
+    ORB_CHECK(hipGetLastError());
+    ORB_CHECK(hipMemcpy(word_id, wio.p, n * 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(weight, wo.p, n * 8, hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(node_id, nio.p, n * 4, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+// orb_math.h — bit-exact scalar semantics shared by host and device code.
+//
+// Everything here reproduces a platform detail the reference binary depends
+// on.  Compiled with -ffp-contract=off; every fused
+// multiply-add below is an explicit fma()/fmaf().
+#pragma once
+#include <stdint.h>
+#include <math.h>
+#include <string.h>
+
+#if defined(__HIPCC__)
+#define ORB_HD __host__ __device__ __forceinline__
+#else
+#define ORB_HD inline
+#endif
+
+namespace orbmi {
+
+// cvRound(float): ties to even under the default rounding mode.
+ORB_HD int cv_round(float v) { return (int)rintf(v); }
+
+ORB_HD uint32_t f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
+
+// ---------------------------------------------------------------------------
+// glibc 2.35 sincosf, FMA variant (x86_64 multiarch __sincosf_fma, selected by
+// the ifunc on every FMA/AVX2 host).  The reference calls sincosf@PLT from
+// computeOrbDescriptor (ORBextractor.cc:111-112).  Restated from the
+// disassembly of the system libm (table at .rodata: sign[4], hpi_inv*2^24,
+// hpi, c0, c1, s1, c2, s2, c3, s3, c4) and checked exhaustively against it in
+// tests/test_math_host.py for every float in [0, 2*pi].  Valid for |y| < 120
+// (descriptor angles are in [0, 2*pi)); larger inputs return NaN.
+// ---------------------------------------------------------------------------
+struct SinCosTab { double sgn[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4; };
+
+ORB_HD void sincosf_poly(double x, double x2, const SinCosTab& p, int n, float* sinp, float* cosp) {
+    const double x3 = x2 * x;
+    const double x4 = x2 * x2;
+    const double s1p = fma(x2, p.s3, p.s2);
+    const double c2p = fma(x2, p.c4, p.c3);
+    const double c1p = fma(x2, p.c1, p.c0);
+    const double x5 = x2 * x3;
+    const double x6 = x2 * x4;
+    const double s = fma(x3, p.s1, x);
+    const double c = fma(x4, p.c2, c1p);
+    const float so = (float)fma(s1p, x5, s);
+    const float co = (float)fma(c2p, x6, c);
+    if (n & 1) { *sinp = co; *cosp = so; }
+    else { *sinp = so; *cosp = co; }
+}
+
+ORB_HD void glibc_sincosf(float y, float* sinp, float* cosp) {
+    const SinCosTab t0 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+                          0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
+                          0x1.1107605230bc4p-7, -0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
+                          0x1.99343027bf8c3p-16};
+    const SinCosTab t1 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
+                          -0x1p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
+                          0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
+                          -0x1.99343027bf8c3p-16};
+    const double x = (double)y;
+    const uint32_t top = (f32_bits(y) >> 20) & 0x7ff;
+    if (top < 0x3f4) {                       // |y| < pi/4
+        if (top < 0x398) { *sinp = y; *cosp = 1.0f; return; }   // |y| < 2^-12
+        sincosf_poly(x, x * x, t0, 0, sinp, cosp);
+    } else if (top < 0x42f) {                // |y| < 120
+        const double r = x * t0.hpi_inv;
+        const int n = ((int32_t)r + 0x800000) >> 24;
+        const double xr = fma(-(double)n, t0.hpi, x);
+        const double s = t0.sgn[n & 3];
+        sincosf_poly(xr * s, xr * xr, (n & 2) ? t1 : t0, n, sinp, cosp);
+    } else {
+        *sinp = *cosp = NAN;
+    }
+}
+
+// cv::fastAtan2 (OpenCV 4.x atan_f32), degrees; no contraction (A.4).
+ORB_HD float fast_atan2_deg(float y, float x) {
+    const float k = (float)(180 / 3.14159265358979323846);
+    const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
+    const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
+    const float ax = fabsf(x), ay = fabsf(y);
+    float a;
+    if (ax >= ay) {
+        const float c = ay / (ax + (float)2.220446049250313e-16);
+        const float c2 = c * c;
+        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    } else {
+        const float c = ax / (ay + (float)2.220446049250313e-16);
+        const float c2 = c * c;
+        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    }
+    if (x < 0) a = 180.f - a;
+    if (y < 0) a = 360.f - a;
+    return a;
+}
+
+// ---------------------------------------------------------------------------
+// libstdc++ std::sort (introsort, _S_threshold = 16, median-of-3 to first,
+// unguarded partition, heap-sort fallback at depth 2*lg(n), final insertion
+// sort), restated for a POD array so the device reproduces the exact
+// permutation std::sort gives for DistributeOctTree's unstable sort of
+// (count, node) pairs under compareNodes (ORBextractor.cc:538-553, :700).
+// Checked against std::sort with heavy ties in tests/test_math_host.py.
+// ---------------------------------------------------------------------------
+struct SortRec { int cnt; int x0; int pos; };
+
+ORB_HD bool node_less(const SortRec& a, const SortRec& b) {
+    if (a.cnt < b.cnt) return true;
+    if (a.cnt > b.cnt) return false;
+    return a.x0 < b.x0;
+}
+ORB_HD void rec_swap(SortRec* a, SortRec* b) { SortRec t = *a; *a = *b; *b = t; }
+ORB_HD int ilg(int n) { int l = 0; while (n >>= 1) ++l; return l; }
+
+ORB_HD void push_heap_(SortRec* f, int hole, int top, SortRec v) {
+    int parent = (hole - 1) / 2;
+    while (hole > top && node_less(f[parent], v)) {
+        f[hole] = f[parent];
+        hole = parent;
+        parent = (hole - 1) / 2;
+    }
+    f[hole] = v;
+}
+ORB_HD void adjust_heap_(SortRec* f, int hole, int len, SortRec v) {
+    const int top = hole;
+    int child = hole;
+    while (child < (len - 1) / 2) {
+        child = 2 * (child + 1);
+        if (node_less(f[child], f[child - 1])) child--;
+        f[hole] = f[child];
+        hole = child;
+    }
+    if ((len & 1) == 0 && child == (len - 2) / 2) {
+        child = 2 * (child + 1);
+        f[hole] = f[child - 1];
+        hole = child - 1;
+    }
+    push_heap_(f, hole, top, v);
+}
+ORB_HD void heap_sort_(SortRec* f, int len) {
+    if (len >= 2) {                                   // __make_heap
+        for (int parent = (len - 2) / 2;; --parent) {
+            adjust_heap_(f, parent, len, f[parent]);
+            if (parent == 0) break;
+        }
+    }
+    for (int last = len; last > 1;) {                 // __sort_heap
+        --last;
+        SortRec v = f[last];
+        f[last] = f[0];
+        adjust_heap_(f, 0, last, v);
+    }
+}
+ORB_HD void median_to_first_(SortRec* r, SortRec* a, SortRec* b, SortRec* c) {
+    if (node_less(*a, *b)) {
+        if (node_less(*b, *c)) rec_swap(r, b);
+        else if (node_less(*a, *c)) rec_swap(r, c);
+        else rec_swap(r, a);
+    } else if (node_less(*a, *c)) rec_swap(r, a);
+    else if (node_less(*b, *c)) rec_swap(r, c);
+    else rec_swap(r, b);
+}
+ORB_HD SortRec* unguarded_partition_(SortRec* first, SortRec* last, SortRec* pivot) {
+    while (true) {
+        while (node_less(*first, *pivot)) ++first;
+        --last;
+        while (node_less(*pivot, *last)) --last;
+        if (!(first < last)) return first;
+        rec_swap(first, last);
+        ++first;
+    }
+}
+ORB_HD void unguarded_linear_insert_(SortRec* last) {
+    SortRec v = *last;
+    SortRec* next = last - 1;
+    while (node_less(v, *next)) { *last = *next; last = next; --next; }
+    *last = v;
+}
+ORB_HD void insertion_sort_(SortRec* first, SortRec* last) {
+    if (first == last) return;
+    for (SortRec* i = first + 1; i != last; ++i) {
+        if (node_less(*i, *first)) {
+            SortRec v = *i;
+            for (SortRec* p = i; p != first; --p) *p = *(p - 1);
+            *first = v;
+        } else {
+            unguarded_linear_insert_(i);
+        }
+    }
+}
+// Iterative form of __introsort_loop: the recursion (right part first, then
+// loop on the left part) is replayed with an explicit stack in the same order.
+ORB_HD void std_sort(SortRec* first, int n) {
+    if (n <= 1) return;
+    struct Frame { SortRec* f; SortRec* l; int depth; };
+    Frame stk[64];
+    int sp = 0;
+    stk[sp++] = {first, first + n, ilg(n) * 2};
+    while (sp) {
+        Frame fr = stk[--sp];
+        SortRec* f = fr.f;
+        SortRec* l = fr.l;
+        int depth = fr.depth;
+        while (l - f > 16) {
+            if (depth == 0) { heap_sort_(f, (int)(l - f)); break; }
+            --depth;
+            SortRec* mid = f + (l - f) / 2;
+            median_to_first_(f, f + 1, mid, l - 1);
+            SortRec* cut = unguarded_partition_(f + 1, l, f);
+            // recursion on [cut, l) happens before the loop continues on [f, cut);
+            // an explicit stack must finish [cut, l) first: push [f,cut) then [cut,l).
+            stk[sp++] = {f, cut, depth};
+            stk[sp++] = {cut, l, depth};
+            l = f;   // consumed: both halves are on the stack
+            break;
+        }
+    }
+    // __final_insertion_sort
+    if (n > 16) {
+        insertion_sort_(first, first + 16);
+        for (SortRec* i = first + 16; i != first + n; ++i) unguarded_linear_insert_(i);
+    } else {
+        insertion_sort_(first, first + n);
+    }
+}
+
+}  // namespace orbmi

@@ -1,0 +1,190 @@
+"""Host-side mirror of the reference interface for the ORB hot path.
+
+``ORBextractor`` follows ORB_SLAM3::ORBextractor (reference
+include/ORBextractor.h:43-109): same constructor arguments, ``__call__`` ==
+``operator()(image, mask, keypoints, descriptors, vLappingArea)`` returning
+(keypoints, descriptors, monoIndex), the scale-table getters and
+``mvImagePyramid``.  ``ORBmatcher`` follows include/ORBmatcher.h:36-103
+(nnratio, checkOri, the Search* entry points, DescriptorDistance).  Every
+call goes through the C ABI of liborb_mi355x.so onto the GPU; there is no
+CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi, capi
+
+
+class ORBextractor:
+    HARRIS_SCORE, FAST_SCORE = 0, 1
+
+    def __init__(self, nfeatures: int, scaleFactor: float, nlevels: int, iniThFAST: int, minThFAST: int,
+                 device: int = 0, blur_variant: int = 0, fma_sampling: int = 1):
+        self._p = abi.params(nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, blur_variant, fma_sampling)
+        self.nlevels = nlevels
+        self.scaleFactor = float(np.float32(scaleFactor))
+        self._h = capi.lib().orbx_create(C.byref(self._p), device)
+        if not self._h:
+            raise RuntimeError("orbx_create failed (bad parameters or no HIP device)")
+        L = nlevels
+        self._tab = [np.zeros(L, np.float32) for _ in range(4)] + [np.zeros(L, np.int32), np.zeros(16, np.int32)]
+        capi.check(capi.lib().orbx_get_tables(self._h, *[abi.ptr(a) for a in self._tab]), "orbx_get_tables")
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            capi.lib().orbx_destroy(h)
+            self._h = None
+
+    # getters (ORBextractor.h:61-81)
+    def GetLevels(self): return self.nlevels
+    def GetScaleFactor(self): return self.scaleFactor
+    def GetScaleFactors(self): return self._tab[0].copy()
+    def GetInverseScaleFactors(self): return self._tab[1].copy()
+    def GetScaleSigmaSquares(self): return self._tab[2].copy()
+    def GetInverseScaleSigmaSquares(self): return self._tab[3].copy()
+    def FeaturesPerLevel(self): return self._tab[4].copy()
+    def UMax(self): return self._tab[5].copy()
+
+    def max_keypoints(self, w: int, h: int) -> int:
+        return capi.check(capi.lib().orbx_max_keypoints(self._h, w, h), "orbx_max_keypoints")
+
+    def __call__(self, image: np.ndarray, mask=None, vLappingArea=(0, 0)):
+        """operator() (ORBextractor.cc:1086-1168): returns (keypoints, descriptors, monoIndex);
+        -1 for an empty image like the reference."""
+        if image is None or image.size == 0:
+            return np.zeros(0, abi.KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8), -1
+        img = np.ascontiguousarray(image, np.uint8)
+        if img.ndim != 2:
+            raise ValueError("ORBextractor expects an 8UC1 image")
+        h, w = img.shape
+        cap = self.max_keypoints(w, h)
+        kps = np.zeros(cap, abi.KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n, mono = C.c_int(0), C.c_int(0)
+        rc = capi.lib().orbx_extract(self._h, abi.ptr(img), w, h, w, int(vLappingArea[0]), int(vLappingArea[1]),
+                                     abi.ptr(kps), abi.ptr(desc), cap, C.byref(n), C.byref(mono))
+        capi.check(rc, "orbx_extract")
+        return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
+
+    @property
+    def mvImagePyramid(self):
+        out = []
+        for l in range(self.nlevels):
+            w, h = C.c_int(0), C.c_int(0)
+            capi.check(capi.lib().orbx_get_level(self._h, l, None, 0, C.byref(w), C.byref(h)), "orbx_get_level")
+            a = np.zeros((h.value, w.value), np.uint8)
+            capi.check(capi.lib().orbx_get_level(self._h, l, abi.ptr(a), w.value, C.byref(w), C.byref(h)),
+                       "orbx_get_level")
+            out.append(a)
+        return out
+
+    def debug_stage(self, stage: int, cap: int = 400000):
+        kps = np.zeros(cap, abi.KEYPOINT_DTYPE)
+        counts = np.zeros(self.nlevels, np.int32)
+        n = capi.check(capi.lib().orbx_debug_stage(self._h, stage, abi.ptr(kps), cap, abi.ptr(counts)),
+                       "orbx_debug_stage")
+        out, off = [], 0
+        for c in counts[:self.nlevels]:
+            out.append(kps[off:off + c].copy())
+            off += c
+        assert off == n
+        return out
+
+    def extract_batch_device(self, frames, lapping=(0, 1000), out=None, stream=None):
+        """HBM-resident batch path: ``frames`` is a (B, H, W) uint8 CUDA tensor.
+        Returns (kps (B, cap) as a raw int32 tensor view, desc (B, cap, 32),
+        n (B,), mono (B,))."""
+        import torch
+        assert frames.is_cuda and frames.dtype == torch.uint8 and frames.dim() == 3
+        frames = frames.contiguous()
+        B, H, W = frames.shape
+        cap = self.max_keypoints(W, H)
+        if out is None:
+            dev = frames.device
+            out = (torch.empty((B, cap, 7), dtype=torch.int32, device=dev),
+                   torch.empty((B, cap, 32), dtype=torch.uint8, device=dev),
+                   torch.empty(B, dtype=torch.int32, device=dev), torch.empty(B, dtype=torch.int32, device=dev))
+        kps, desc, n, mono = out
+        st = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        rc = capi.lib().orbx_extract_batch_device(self._h, B, frames.data_ptr(), H * W, W, W, H, int(lapping[0]),
+                                                  int(lapping[1]), kps.data_ptr(), desc.data_ptr(), cap,
+                                                  n.data_ptr(), mono.data_ptr(), C.c_void_p(st))
+        capi.check(rc, "orbx_extract_batch_device")
+        return kps, desc, n, mono, cap
+
+
+def keypoints_from_device(kps_i32) -> np.ndarray:
+    """(cap, 7) int32 tensor/array -> structured KEYPOINT_DTYPE array."""
+    a = np.ascontiguousarray(kps_i32.cpu().numpy() if hasattr(kps_i32, "cpu") else kps_i32, dtype=np.int32)
+    return a.view(abi.KEYPOINT_DTYPE).reshape(a.shape[:-1])
+
+
+class ORBmatcher:
+    TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
+
+    def __init__(self, nnratio: float = 0.6, checkOri: bool = True):
+        self.mfNNratio = float(nnratio)
+        self.mbCheckOrientation = bool(checkOri)
+
+    @staticmethod
+    def DescriptorDistance(a: np.ndarray, b: np.ndarray) -> int:
+        a = np.ascontiguousarray(a, np.uint8)
+        b = np.ascontiguousarray(b, np.uint8)
+        return capi.lib().orbm_descriptor_distance(abi.ptr(a), abi.ptr(b))
+
+    def SearchForInitialization(self, F1: abi.Keep, F2: abi.Keep, vbPrevMatched: np.ndarray, windowSize: int = 10):
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32).copy()
+        m12 = np.zeros(F1.struct.n, np.int32)
+        nm = capi.lib().orbm_search_for_initialization(F1.ref(), F2.ref(), abi.ptr(prev), windowSize,
+                                                       self.mfNNratio, int(self.mbCheckOrientation), abi.ptr(m12))
+        capi.check(nm, "SearchForInitialization")
+        return nm, m12, prev
+
+    def SearchByBoW(self, KF: abi.Keep, KFfv: abi.Keep, kf_valid: np.ndarray, F: abi.Keep, Ffv: abi.Keep):
+        kf_valid = np.ascontiguousarray(kf_valid, np.uint8)
+        match = np.zeros(F.struct.n, np.int32)
+        nm = capi.lib().orbm_search_by_bow(KF.ref(), KFfv.ref(), abi.ptr(kf_valid), F.ref(), Ffv.ref(),
+                                           self.mfNNratio, int(self.mbCheckOrientation), abi.ptr(match))
+        capi.check(nm, "SearchByBoW")
+        return nm, match
+
+    def SearchByProjection(self, F: abi.Keep, mps: abi.Keep, th: float = 3.0, bFarPoints: bool = False,
+                           thFarPoints: float = 50.0, owner=None, blocked=None):
+        n = F.struct.n
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        blocked = np.zeros(n, np.uint8) if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nm = capi.lib().orbm_search_by_projection_mps(F.ref(), mps.ref(), th, int(bFarPoints), thFarPoints,
+                                                      self.mfNNratio, abi.ptr(owner), abi.ptr(blocked))
+        capi.check(nm, "SearchByProjection(F, MPs)")
+        return nm, owner
+
+    def SearchByProjectionLast(self, cur: abi.Keep, valid, u, v, ur, octave, angle, has_obs, desc, th: float,
+                               mode: int = 0, owner=None, blocked=None):
+        n = cur.struct.n
+        arrs = [np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),
+                np.ascontiguousarray(v, np.float32), np.ascontiguousarray(ur, np.float32),
+                np.ascontiguousarray(octave, np.int32), np.ascontiguousarray(angle, np.float32),
+                np.ascontiguousarray(has_obs, np.uint8), np.ascontiguousarray(desc, np.uint8)]
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        blocked = np.zeros(n, np.uint8) if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nm = capi.lib().orbm_search_by_projection_last(cur.ref(), len(arrs[0]), *[abi.ptr(a) for a in arrs], th,
+                                                       mode, int(self.mbCheckOrientation), abi.ptr(owner),
+                                                       abi.ptr(blocked))
+        capi.check(nm, "SearchByProjection(F, LastFrame)")
+        return nm, owner
+
+
+def transform(voc: abi.Keep, desc: np.ndarray, levelsup: int = 4, device: int = 0):
+    """TemplatedVocabulary::transform per descriptor on the GPU: (word_id, weight, node_id)."""
+    desc = np.ascontiguousarray(desc, np.uint8)
+    n = len(desc)
+    wid = np.zeros(n, np.int32)
+    w = np.zeros(n, np.float64)
+    nid = np.zeros(n, np.int32)
+    capi.check(capi.lib().orbv_transform(voc.ref(), n, abi.ptr(desc), levelsup, abi.ptr(wid), abi.ptr(w),
+                                         abi.ptr(nid), device), "orbv_transform")
+    return wid, w, nid

@@ -1,0 +1,80 @@
+// Host-side checks of orb_slam3_vio_fixes_amd/csrc/orb_math.h (product code,
+// compiled for the CPU): the glibc sincosf port against the system libm, and
+// the introsort port against std::sort.  Built and driven by
+// tests/test_math_host.py.
+#include "../../orb_slam3_vio_fixes_amd/csrc/orb_math.h"
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <random>
+#include <thread>
+#include <utility>
+#include <vector>
+
+extern "C" {
+
+// Number of floats in [lo_bits, hi_bits) (bit patterns of non-negative floats)
+// where the port's (sin, cos) bits differ from libm sincosf.
+long long sincos_mismatches(uint32_t lo_bits, uint32_t hi_bits, int nthreads, uint32_t* first_bad) {
+    std::atomic<long long> bad{0};
+    std::atomic<uint32_t> first{0xffffffffu};
+    std::vector<std::thread> th;
+    const uint64_t span = (uint64_t)hi_bits - lo_bits;
+    for (int t = 0; t < nthreads; ++t) {
+        th.emplace_back([&, t] {
+            const uint32_t b0 = lo_bits + (uint32_t)(span * t / nthreads);
+            const uint32_t b1 = lo_bits + (uint32_t)(span * (t + 1) / nthreads);
+            long long local = 0;
+            for (uint32_t b = b0; b < b1; ++b) {
+                float y;
+                memcpy(&y, &b, 4);
+                float s0, c0, s1, c1;
+                sincosf(y, &s0, &c0);
+                orbmi::glibc_sincosf(y, &s1, &c1);
+                if (orbmi::f32_bits(s0) != orbmi::f32_bits(s1) || orbmi::f32_bits(c0) != orbmi::f32_bits(c1)) {
+                    ++local;
+                    uint32_t cur = first.load();
+                    while (b < cur && !first.compare_exchange_weak(cur, b)) {}
+                }
+            }
+            bad += local;
+        });
+    }
+    for (auto& x : th) x.join();
+    *first_bad = first.load();
+    return bad.load();
+}
+
+// Sort `trials` random arrays (heavy ties) with std::sort on pair<int,Node*>
+// under compareNodes semantics and with the port; return #arrays that differ.
+int sort_mismatches(int trials, int maxn, unsigned seed) {
+    std::mt19937 rng(seed);
+    int bad = 0;
+    struct Node { int x0; };
+    for (int t = 0; t < trials; ++t) {
+        const int n = 1 + (int)(rng() % (unsigned)maxn);
+        const int cmax = 1 + (int)(rng() % 6), xmax = 1 + (int)(rng() % 8);
+        std::vector<Node> nodes(n);
+        std::vector<std::pair<int, Node*>> ref(n);
+        std::vector<orbmi::SortRec> port(n);
+        for (int i = 0; i < n; ++i) {
+            nodes[i].x0 = (int)(rng() % (unsigned)xmax);
+            const int c = 2 + (int)(rng() % (unsigned)cmax);
+            ref[i] = {c, &nodes[i]};
+            port[i] = {c, nodes[i].x0, i};
+        }
+        std::sort(ref.begin(), ref.end(), [](const std::pair<int, Node*>& a, const std::pair<int, Node*>& b) {
+            if (a.first < b.first) return true;
+            if (a.first > b.first) return false;
+            return a.second->x0 < b.second->x0;
+        });
+        orbmi::std_sort(port.data(), n);
+        for (int i = 0; i < n; ++i)
+            if (ref[i].second != &nodes[port[i].pos]) { ++bad; break; }
+    }
+    return bad;
+}
+
+float port_fast_atan2(float y, float x) { return orbmi::fast_atan2_deg(y, x); }
+}
