@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Throughput bench of the ORB extract + match hot path on MI355X.
+
+Metric (BASELINE.json): frames/s ORB extract+match (752x480, 1000 feat),
+keypoints/descriptors bit-exact.  One step = one batch of B distinct
+synthetic 752x480 frames, resident in HBM before the timed region:
+ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
+on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
+F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
+(Tracking.cc:2459-2492).  Multi-GPU: one process per GPU, frames sharded
+(weak scaling, no data-path collective); timing = max over ranks.
+
+Extra objects on the JSON line:
+  roofline     dominant kernel (k_fast_cells, the FAST pass) measured with HIP
+               events on the extraction stream over the timed steps;
+               algorithmic bytes = every pyramid pixel read once
+               (sum_l w_l*h_l per frame) x frames per launch.
+  cpu_baseline the CPU oracle (oracle/, "port") on the host, rank 0, N=1,
+               on a bounded sample of the same frames, threads stated; its
+               outputs double as a parity check of the sampled frames.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+
+W, H, NFEAT, LAP = 752, 480, 1000, (0, 1000)
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "frames/s ORB extract+match (752×480, 1000 feat) @1/2/4/8 GPU; bit-exact kp/desc"
+STAGES = ["pyramid", "blur", "fast_cells", "quadtree", "describe", "assemble"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
+    ap.add_argument("--cpu-sample", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-profile", action="store_true")
+    return ap.parse_args()
+
+
+def level_pixels(ex):
+    inv = ex.GetInverseScaleFactors()
+    tot = 0
+    for s in inv:
+        tot += int(np.rint(np.float32(W) * np.float32(s))) * int(np.rint(np.float32(H) * np.float32(s)))
+    return tot
+
+
+def cpu_baseline(frames_np, threads):
+    """The CPU oracle on the host: extraction + SearchForInitialization on the
+    same consecutive pairs; frames spread over a thread pool (ctypes releases
+    the GIL).  Returns (frames/s, outputs)."""
+    from oracle import oracle as O
+    from orb_slam3_vio_fixes_amd import abi
+    n = len(frames_np)
+    exs = [O.OracleExtractor(NFEAT, 1.2, 8, 20, 7) for _ in range(threads)]
+    outs = [None] * n
+
+    def work(t):
+        for i in range(t, n, threads):
+            outs[i] = exs[t](frames_np[i], LAP)
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as pool:
+        list(pool.map(work, range(threads)))
+
+    def match(t):
+        res = []
+        for i in range(t, n - 1, threads):
+            k1, d1, _ = outs[i]
+            k2, d2, _ = outs[i + 1]
+            prev = np.stack([k1["x"], k1["y"]], 1)
+            res.append((i, O.search_for_initialization(abi.frame_struct(k1, d1, W, H), abi.frame_struct(k2, d2, W, H),
+                                                       prev, 100, 0.9, True)[0]))
+        return res
+    with ThreadPoolExecutor(threads) as pool:
+        nms = dict(x for r in pool.map(match, range(threads)) for x in r)
+    dt = time.perf_counter() - t0
+    return n / dt, outs, nms
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from orb_slam3_vio_fixes_amd import capi, orb, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    B = args.batch
+
+    # distinct frames per rank (weak scaling), generated once, uploaded before timing
+    frames_np = synth.batch(W, H, B, config=2, start=rank * B)
+    frames = torch.from_numpy(frames_np).to(dev)
+    ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local)
+    L = capi.lib()
+    stream = torch.cuda.current_stream(dev)
+    kps, desc, n, mono, cap = ex.extract_batch_device(frames, LAP)
+    matches = torch.empty((B - 1, cap), dtype=torch.int32, device=dev)
+    nmatch = torch.empty(B - 1, dtype=torch.int32, device=dev)
+    inv_w = float(np.float32(64) / np.float32(W))
+    inv_h = float(np.float32(48) / np.float32(H))
+
+    def step():
+        ex.extract_batch_device(frames, LAP, out=(kps, desc, n, mono))
+        rc = L.orbm_search_for_initialization_batch_device(
+            B, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
+            100, 0.9, 1, matches.data_ptr(), nmatch.data_ptr(), stream.cuda_stream)
+        capi.check(rc, "SearchForInitialization batch")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    prof = not args.no_profile
+    if prof:
+        L.orbx_set_profiling(ex._h, 1)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    stage_ms = np.zeros(len(STAGES), np.float32)
+    if prof:
+        calls = L.orbx_get_profile(ex._h, stage_ms.ctypes.data, len(STAGES))
+        L.orbx_set_profiling(ex._h, 0)
+        stage_ms /= max(1, calls)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+
+    if rank == 0:
+        total_frames = B * args.steps * world
+        value = total_frames / elapsed
+        px = level_pixels(ex)                          # algorithmic bytes per frame of the FAST pass
+        fast_ms = float(stage_ms[2])
+        achieved = (px * B / (fast_ms * 1e-3)) / 1e9 if fast_ms > 0 else None
+        roof = {"kernel": "k_fast_cells", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                "bytes_per_launch": px * B, "ms_per_launch": fast_ms}
+        out = {"metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
+               "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
+               "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
+               "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
+                                      "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
+                          "frames_per_step_per_gpu": B, "parallelism": f"frames sharded over {world} GPU(s)"},
+               "stage_ms": {k: float(v) for k, v in zip(STAGES, stage_ms)},
+               "roofline": roof}
+        if world == 1 and args.cpu_sample > 0:
+            ns = min(args.cpu_sample, B)
+            fps, outs, nms = cpu_baseline(frames_np[:ns], args.cpu_threads)
+            # parity of the sampled frames (the CPU leg doubles as a checker)
+            kh = kps[:ns].cpu().numpy()
+            dh = desc[:ns].cpu().numpy()
+            nh = n[:ns].cpu().numpy()
+            mh = nmatch[:ns - 1].cpu().numpy()
+            bad = 0
+            for i in range(ns):
+                rk, rd, _ = outs[i]
+                if nh[i] != len(rk) or not np.array_equal(orb.keypoints_from_device(kh[i][:nh[i]]).view(np.uint8),
+                                                          rk.view(np.uint8)) or not np.array_equal(dh[i][:nh[i]], rd):
+                    bad += 1
+            bad_m = sum(int(mh[i] != nms[i]) for i in range(ns - 1))
+            out["cpu_baseline"] = {"value": fps, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
+                                   "sample": f"first {ns} frames of the step batch, extract + SearchForInitialization "
+                                             f"on {ns - 1} pairs, oracle/liborb_oracle.so on {args.cpu_threads} threads"}
+            out["parity"] = {"frames_checked": ns, "frames_mismatched": bad, "pairs_checked": ns - 1,
+                             "pairs_mismatched": bad_m}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -111,6 +111,14 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
 int orbx_debug_stage(orbx_handle* h, int stage, orb_keypoint* kps, int cap,
                      int32_t* counts);
 
+/* Per-stage HIP-event timing of subsequent orbx_extract* calls (on the stream
+ * they run on).  orbx_get_profile sums, over the recorded calls, the stage
+ * times in ms: [0] pyramid (k_resize x L-1), [1] blur, [2] FAST cells,
+ * [3] quadtree, [4] describe, [5] assemble; returns the number of calls and
+ * clears the record.  Not part of the reference interface. */
+int orbx_set_profiling(orbx_handle* h, int enable);
+int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);
+
 /* ---------------- matcher ---------------- */
 
 /* ORBmatcher::DescriptorDistance / DBoW2::FORB::distance

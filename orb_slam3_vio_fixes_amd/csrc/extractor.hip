@@ -108,6 +108,11 @@ struct orbx_handle {
     orbmi::Plan plan;
     bool have_last = false;
     int last_w = 0, last_h = 0;
+    // optional per-stage HIP-event timing (orbx_set_profiling)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::vector<hipEvent_t>> ev_calls;
+    size_t ev_next = 0;
 };
 
 namespace orbmi {
@@ -1002,6 +1007,19 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
                         hipStream_t st) {
     Plan& P = hd->plan;
     const int L = P.L;
+    std::vector<hipEvent_t> marks;
+    auto mark = [&]() {
+        if (!hd->profiling) return;
+        if (hd->ev_next >= hd->ev_pool.size()) {
+            hipEvent_t e;
+            if (hipEventCreate(&e) != hipSuccess) return;
+            hd->ev_pool.push_back(e);
+        }
+        hipEvent_t e = hd->ev_pool[hd->ev_next++];
+        (void)hipEventRecord(e, st);
+        marks.push_back(e);
+    };
+    mark();
     // pyramid
     for (int l = 1; l < L; ++l) {
         const LevelDev& d = P.lv[l];
@@ -1013,6 +1031,7 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
         hipLaunchKernelGGL(k_resize, dim3((d.h + 3) / 4, B), dim3(256), 0, st, src, sfs, sp, s.h, P.d_pyr + d.off,
                            P.pyr_bytes, d.pitch, d.w, d.h, xt, xt + d.w, P.xmax[l]);
     }
+    mark();
     // blurred levels
     BlurKernel K;
     static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
@@ -1025,6 +1044,7 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
         hipLaunchKernelGGL(k_blur, dim3((d.w + 63) / 64, (d.h + 15) / 16, B), dim3(256), 0, st, src, sfs, sp,
                            P.d_blur + d.boff, P.blur_bytes, d.bpitch, d.w, d.h, K);
     }
+    mark();
     // FAST cells
     FastArgs fa;
     fa.in = d_frames; fa.in_fstride = fstride; fa.in_pitch = pitch0;
@@ -1037,6 +1057,7 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     fa.win_max = (P.win_max + 15) & ~15;
     const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max);
     hipLaunchKernelGGL(k_fast_cells, dim3((P.ncells + 3) / 4, B), dim3(256), flds, st, fa);
+    mark();
     // quadtree
     QtArgs qa;
     qa.lv = P.d_lv; qa.cell_count = P.d_cell_count; qa.cell_keys = P.d_cell_keys;
@@ -1045,6 +1066,7 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     qa.qt_key = P.d_qt_key; qa.qt_n = P.d_qt_n; qa.out_total = P.out_total; qa.L = L;
     qa.ncap = P.max_out_cap + 8;
     hipLaunchKernelGGL(k_quadtree, dim3(L, B), dim3(256), qt_lds_bytes(P), st, qa);
+    mark();
     // describe
     DescArgs da;
     da.in = d_frames; da.in_fstride = fstride; da.in_pitch = pitch0;
@@ -1055,12 +1077,15 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     da.fma = hd->prm.fma_sampling != 0;
     for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
     hipLaunchKernelGGL(k_describe, dim3(L, B, 8), dim3(256), 0, st, da);
+    mark();
     // assemble
     AsmArgs aa;
     aa.lv = P.d_lv; aa.qt_key = P.d_qt_key; aa.qt_n = P.d_qt_n; aa.angle = P.d_angle; aa.sdesc = P.d_sdesc;
     aa.out_total = P.out_total; aa.L = L; aa.lap0 = lap0; aa.lap1 = lap1;
     aa.kps = d_kps; aa.desc = d_desc; aa.cap = cap; aa.n_out = d_n; aa.mono_out = d_mono;
     hipLaunchKernelGGL(k_assemble, dim3(B), dim3(256), (size_t)P.out_total * 4 + 64, st, aa);
+    mark();
+    if (hd->profiling) hd->ev_calls.push_back(marks);
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }
@@ -1093,6 +1118,7 @@ void orbx_destroy(orbx_handle* h) {
     if (!h) return;
     (void)hipSetDevice(h->device);
     h->plan.release();
+    for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
     delete h;
 }
 
@@ -1157,6 +1183,33 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
         ORB_CHECK(hipMemcpy(desc, P.d_desc, (size_t)n * 32, hipMemcpyDeviceToHost));
     }
     return ORB_OK;
+}
+
+int orbx_set_profiling(orbx_handle* h, int enable) {
+    if (!h) return ORB_ERR_PARAM;
+    h->profiling = enable != 0;
+    h->ev_calls.clear();
+    h->ev_next = 0;
+    return ORB_OK;
+}
+
+int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages) {
+    if (!h || !stage_ms) return ORB_ERR_PARAM;
+    for (int i = 0; i < nstages; ++i) stage_ms[i] = 0.f;
+    int calls = 0;
+    for (auto& m : h->ev_calls) {
+        if (m.size() < 2) continue;
+        ORB_CHECK(hipEventSynchronize(m.back()));
+        for (size_t i = 0; i + 1 < m.size() && (int)i < nstages; ++i) {
+            float ms = 0.f;
+            ORB_CHECK(hipEventElapsedTime(&ms, m[i], m[i + 1]));
+            stage_ms[i] += ms;
+        }
+        ++calls;
+    }
+    h->ev_calls.clear();
+    h->ev_next = 0;
+    return calls;
 }
 
 int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step, int* w, int* hh) {

@@ -17,30 +17,44 @@ def frame_seed(config: int, index: int) -> int:
 
 
 def image(w: int, h: int, seed: int, n_shapes: int | None = None) -> np.ndarray:
-    """One u8 image (h, w), deterministic in ``seed``."""
+    """One u8 image (h, w), deterministic in ``seed``.  Shapes are rendered in
+    their bounding windows only, so a 752x480 frame takes a few ms."""
     rng = np.random.default_rng(seed)
-    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
     ang = rng.uniform(0, 2 * np.pi)
-    ramp = 60.0 * (np.cos(ang) * xx / w + np.sin(ang) * yy / h)
-    img = 100.0 + ramp
+    xs = np.arange(w, dtype=np.float32)
+    ys = np.arange(h, dtype=np.float32)
+    img = (100.0 + 60.0 * (np.cos(ang) * xs[None, :] / w + np.sin(ang) * ys[:, None] / h)).astype(np.float32)
     n = n_shapes if n_shapes is not None else int(w * h / 900)
-    for _ in range(n):
-        kind = rng.integers(0, 3)
-        val = rng.uniform(0, 255)
-        cx, cy = rng.uniform(0, w), rng.uniform(0, h)
+    kinds = rng.integers(0, 3, n)
+    vals = rng.uniform(0, 255, n)
+    cxs = rng.uniform(0, w, n)
+    cys = rng.uniform(0, h, n)
+    sizes = rng.uniform(0, 1, (n, 2))
+    for kind, val, cx, cy, (s0, s1) in zip(kinds, vals, cxs, cys, sizes):
         if kind == 0:
-            rw, rh = rng.uniform(3, 40, size=2)
-            m = (np.abs(xx - cx) < rw) & (np.abs(yy - cy) < rh)
-            img[m] = val
+            rw, rh = 3 + 37 * s0, 3 + 37 * s1
         elif kind == 1:
-            r = rng.uniform(2, 25)
-            m = (xx - cx) ** 2 + (yy - cy) ** 2 < r * r
-            img[m] = val
+            rw = rh = 2 + 23 * s0
         else:
-            r = rng.uniform(4, 30)
-            g = np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * r * r))
-            img = img * (1 - g) + val * g
-    img += rng.normal(0, 3.0, size=img.shape)
+            rw = rh = 3 * (4 + 26 * s0)
+        x0, x1 = max(0, int(cx - rw) - 1), min(w, int(cx + rw) + 2)
+        y0, y1 = max(0, int(cy - rh) - 1), min(h, int(cy + rh) + 2)
+        if x0 >= x1 or y0 >= y1:
+            continue
+        xx = xs[None, x0:x1] - cx
+        yy = ys[y0:y1, None] - cy
+        win = img[y0:y1, x0:x1]
+        if kind == 0:
+            m = (np.abs(xx) < rw) & (np.abs(yy) < rh)
+            win[m] = val
+        elif kind == 1:
+            m = xx ** 2 + yy ** 2 < rw * rw
+            win[m] = val
+        else:
+            r = rw / 3
+            g = np.exp(-(xx ** 2 + yy ** 2) / (2 * r * r))
+            win[:] = win * (1 - g) + val * g
+    img += rng.normal(0, 3.0, size=img.shape).astype(np.float32)
     # ~10 % flat patches (no texture, no noise): exercises the minThFAST fallback
     for _ in range(max(1, int(0.10 * w * h / (48 * 48)))):
         x0, y0 = int(rng.integers(0, max(1, w - 48))), int(rng.integers(0, max(1, h - 48)))
