@@ -3,7 +3,8 @@
 
 Metric (BASELINE.json): frames/s ORB extract+match (752x480, 1000 feat),
 keypoints/descriptors bit-exact.  One step = one batch of B distinct
-synthetic 752x480 frames, resident in HBM before the timed region:
+synthetic 752x480 frames of a panning camera (synth.sequence), resident in
+HBM before the timed region:
 ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
 on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
 F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
@@ -111,7 +112,7 @@ def main():
     B = args.batch
 
     # distinct frames per rank (weak scaling), generated once, uploaded before timing
-    frames_np = synth.batch(W, H, B, config=2, start=rank * B)
+    frames_np = synth.sequence(W, H, B, config=2, start=rank * B)
     frames = torch.from_numpy(frames_np).to(dev)
     ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local)
     L = capi.lib()

@@ -3,7 +3,7 @@
 No EuRoC / TUM-VI images and no ORBvoc.txt exist in the image, so every
 workload is synthetic and seeded: u8 frames with full-range texture (random
 rectangles and blobs of random intensity over a smooth illumination ramp,
-additive noise sigma ~3, ~10 % flat patches so the minThFAST fallback and the
+additive integer noise sigma ~3, ~10 % flat patches so the minThFAST fallback and the
 reflect-border paths are exercised), stereo right images shifted by a per-row
 disparity field, a synthetic k-ary vocabulary and keyframe descriptor sets.
 """
@@ -19,11 +19,13 @@ def frame_seed(config: int, index: int) -> int:
 def image(w: int, h: int, seed: int, n_shapes: int | None = None) -> np.ndarray:
     """One u8 image (h, w), deterministic in ``seed``.  Shapes are rendered in
     their bounding windows only, so a 752x480 frame takes a few ms."""
+    # only IEEE basic arithmetic (no exp/sin/cos): bit-identical on every host CPU
     rng = np.random.default_rng(seed)
-    ang = rng.uniform(0, 2 * np.pi)
+    gx, gy = rng.uniform(-1, 1, 2)
     xs = np.arange(w, dtype=np.float32)
     ys = np.arange(h, dtype=np.float32)
-    img = (100.0 + 60.0 * (np.cos(ang) * xs[None, :] / w + np.sin(ang) * ys[:, None] / h)).astype(np.float32)
+    img = (np.float32(100.0) + np.float32(60.0 * gx / w) * xs[None, :]
+           + np.float32(60.0 * gy / h) * ys[:, None]).astype(np.float32)
     n = n_shapes if n_shapes is not None else int(w * h / 900)
     kinds = rng.integers(0, 3, n)
     vals = rng.uniform(0, 255, n)
@@ -51,10 +53,10 @@ def image(w: int, h: int, seed: int, n_shapes: int | None = None) -> np.ndarray:
             m = xx ** 2 + yy ** 2 < rw * rw
             win[m] = val
         else:
-            r = rw / 3
-            g = np.exp(-(xx ** 2 + yy ** 2) / (2 * r * r))
-            win[:] = win * (1 - g) + val * g
-    img += rng.normal(0, 3.0, size=img.shape).astype(np.float32)
+            t = np.maximum(np.float32(0), np.float32(1) - (xx * xx + yy * yy) / np.float32(rw * rw))
+            g = t * t * t
+            win[:] = win * (1 - g) + np.float32(val) * g
+    img += rng.integers(-5, 6, size=img.shape).astype(np.float32)   # ~sigma 3, exact on any host
     # ~10 % flat patches (no texture, no noise): exercises the minThFAST fallback
     for _ in range(max(1, int(0.10 * w * h / (48 * 48)))):
         x0, y0 = int(rng.integers(0, max(1, w - 48))), int(rng.integers(0, max(1, h - 48)))
@@ -66,19 +68,40 @@ def stereo_pair(w: int, h: int, seed: int) -> tuple[np.ndarray, np.ndarray]:
     """Left image and a right image shifted by a 0-48 px per-row disparity."""
     left = image(w, h, seed)
     rng = np.random.default_rng(seed + 7_000_000)
-    disp = np.clip(24 + 24 * np.sin(np.linspace(0, rng.uniform(1, 6), h)), 0, 48).astype(np.int64)
+    knots = rng.integers(0, 49, 9)
+    disp = np.rint(np.interp(np.arange(h), np.linspace(0, h - 1, 9), knots)).astype(np.int64)
     right = np.empty_like(left)
     cols = np.arange(w)
     for y in range(h):
         right[y] = left[y, np.clip(cols + disp[y], 0, w - 1)]
-    noise = rng.normal(0, 2.0, size=left.shape)
-    right = np.clip(np.rint(right.astype(np.float64) + noise), 0, 255).astype(np.uint8)
+    noise = rng.integers(-2, 3, size=left.shape)
+    right = np.clip(right.astype(np.int64) + noise, 0, 255).astype(np.uint8)
     return left, right
 
 
 def batch(w: int, h: int, nframes: int, config: int = 2, start: int = 0) -> np.ndarray:
     """(nframes, h, w) u8 stack of distinct seeded frames."""
     return np.stack([image(w, h, frame_seed(config, start + i)) for i in range(nframes)])
+
+
+def sequence(w: int, h: int, nframes: int, config: int = 2, start: int = 0, step: float = 3.0) -> np.ndarray:
+    """(nframes, h, w) u8 frames of a camera panning over one static scene:
+    crops of a large seeded canvas along a smooth integer trajectory (a few px
+    per frame), each with fresh integer sensor noise.  Consecutive frames share
+    most of their content, so SearchForInitialization finds real matches."""
+    seed = frame_seed(config, start)
+    rng = np.random.default_rng(seed + 11_000_000)
+    span = int(step * nframes) + 8
+    canvas = image(w + span, h + span, seed).astype(np.int16)
+    vx, vy = rng.uniform(0.3, 1.0, 2)
+    norm = max(vx, vy)
+    out = np.empty((nframes, h, w), np.uint8)
+    for i in range(nframes):
+        ox = int(round(i * step * vx / norm)) % (span - 4)
+        oy = int(round(i * step * vy / norm)) % (span - 4)
+        noise = rng.integers(-2, 3, size=(h, w), dtype=np.int16)
+        out[i] = np.clip(canvas[oy:oy + h, ox:ox + w] + noise, 0, 255).astype(np.uint8)
+    return out
 
 
 def vocabulary(k: int = 10, levels: int = 6, seed: int = 5, max_nodes: int | None = None):

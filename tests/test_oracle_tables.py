@@ -1,0 +1,48 @@
+"""Known-answer tests of the constructor tables and size plan (reference
+src/ORBextractor.cc:409-469, :1174-1175, :785-803) against the values the
+survey evaluated from the reference code."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+FEATURES = {
+    1000: [217, 181, 151, 126, 105, 87, 73, 60],
+    1200: [261, 217, 181, 151, 126, 105, 87, 72],
+    1500: [326, 271, 226, 189, 157, 131, 109, 91],
+    5000: [1086, 905, 754, 628, 524, 436, 364, 303],
+}
+SCALES = [1, 1.2000000477, 1.4400000572, 1.7280001640, 2.0736002922, 2.4883203506, 2.9859845638, 3.5831816196]
+UMAX = [15, 15, 15, 15, 14, 14, 14, 13, 13, 12, 11, 10, 9, 8, 6, 3]
+LEVELS = {
+    (752, 480): [(752, 480), (627, 400), (522, 333), (435, 278), (363, 231), (302, 193), (252, 161), (210, 134)],
+    (512, 512): [(512, 512), (427, 427), (356, 356), (296, 296), (247, 247), (206, 206), (171, 171), (143, 143)],
+    (1920, 1080): [(1920, 1080), (1600, 900), (1333, 750), (1111, 625), (926, 521), (772, 434), (643, 362),
+                   (536, 301)],
+}
+SUMP = {(752, 480): 1117367, (512, 512): 811960, (1920, 1080): 6419321}
+
+
+@pytest.mark.parametrize("nf", sorted(FEATURES))
+def test_features_per_level(nf):
+    t = O.OracleExtractor(nf, 1.2, 8, 20, 7).tables()
+    assert t["features"].tolist() == FEATURES[nf]
+
+
+def test_scale_tables_and_umax():
+    t = O.OracleExtractor(1000, 1.2, 8, 20, 7).tables()
+    np.testing.assert_allclose(t["scale"], SCALES, rtol=0, atol=5e-10)
+    assert t["scale"][1] == np.float32(np.float64(np.float32(1.2)))
+    np.testing.assert_array_equal(t["sigma2"], t["scale"] * t["scale"])
+    np.testing.assert_array_equal(t["inv_scale"], np.float32(1) / t["scale"])
+    assert t["umax"].tolist() == UMAX
+
+
+@pytest.mark.parametrize("size", sorted(LEVELS))
+def test_pyramid_sizes(size):
+    w, h = size
+    ex = O.OracleExtractor(1000, 1.2, 8, 20, 7)
+    ex(np.full((h, w), 128, np.uint8), (0, 0))
+    got = [ex.level(l).shape[::-1] for l in range(8)]
+    assert got == LEVELS[size]
+    assert sum(a * b for a, b in got) == SUMP[size]

@@ -1,0 +1,85 @@
+"""world_size-2 gloo tests of the multi-GPU path on CPU: shard coverage,
+vocabulary / query broadcast, and sharded map-wide SearchByBoW equal to the
+unsharded result (compute done by the CPU oracle as the checker)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from orb_slam3_vio_fixes_amd import sharding
+
+
+def test_shard_covers():
+    for n in (0, 1, 7, 64, 10000):
+        for world in (1, 2, 3, 8):
+            got = [list(sharding.shard(n, r, world)) for r in range(world)]
+            assert sum(got, []) == list(range(n))
+            assert max(map(len, got)) - min(map(len, got)) <= 1
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+    from oracle import oracle as O
+    from orb_slam3_vio_fixes_amd import abi, synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        voc = synth.vocabulary(k=4, levels=4, seed=1) if rank == 0 else None
+        v = sharding.broadcast_vocabulary(voc)
+        ref = synth.vocabulary(k=4, levels=4, seed=1)
+        same = all(np.array_equal(v[k], ref[k]) for k in ("first_child", "nchild", "node_desc", "word_id", "weight"))
+        # query frame from rank 0; keyframes = perturbed copies, sharded by id
+        rng = np.random.default_rng(5)
+        fk = np.zeros(300, abi.KEYPOINT_DTYPE)
+        fk["angle"] = rng.uniform(0, 360, 300)
+        fd = rng.integers(0, 256, (300, 32), dtype=np.uint8)
+        k, d = sharding.broadcast_frame(fk if rank == 0 else None, fd if rank == 0 else None)
+        same &= np.array_equal(k.view(np.uint8), fk.view(np.uint8)) and np.array_equal(d, fd)
+        vk = abi.vocab_struct(v)
+        _, _, fnode = O.transform(vk, d, 2)
+        res = {}
+        for kf in sharding.shard(6, rank, world):
+            r2 = np.random.default_rng(100 + kf)
+            kd = d.copy()
+            flips = r2.random((300, 256)) < 0.05
+            kd = np.packbits(np.unpackbits(kd, axis=1) ^ flips, axis=1)
+            kk = k.copy()
+            kk["angle"] = (kk["angle"] + r2.uniform(-5, 5, 300)) % 360
+            _, _, knode = O.transform(vk, kd, 2)
+            nm, match = O.search_by_bow(abi.frame_struct(kk, kd, 752, 480), abi.featvec_struct(knode),
+                                        np.ones(300, np.uint8), abi.frame_struct(k, d, 752, 480),
+                                        abi.featvec_struct(fnode), 0.7, True)
+            res[kf] = (nm, match.tolist())
+        q.put((rank, same, res))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_broadcast_and_sharded_bow():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = [q.get(timeout=240) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(o[1] for o in out)
+    merged = {}
+    for _, _, res in out:
+        merged.update(res)
+    assert sorted(merged) == list(range(6))
+    assert all(merged[k][0] > 0 for k in merged)
