@@ -38,7 +38,7 @@ sys.path.insert(0, str(ROOT))
 W, H, NFEAT, LAP = 752, 480, 1000, (0, 1000)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 METRIC = "frames/s ORB extract+match (752×480, 1000 feat) @1/2/4/8 GPU; bit-exact kp/desc"
-STAGES = ["pyramid", "blur", "fast_cells", "quadtree", "describe", "assemble"]
+STAGES = ["pyramid", "fast_cells", "quadtree", "describe", "assemble"]
 
 
 def parse():
@@ -161,7 +161,7 @@ def main():
         total_frames = B * args.steps * world
         value = total_frames / elapsed
         px = level_pixels(ex)                          # algorithmic bytes per frame of the FAST pass
-        fast_ms = float(stage_ms[2])
+        fast_ms = float(stage_ms[1])
         achieved = (px * B / (fast_ms * 1e-3)) / 1e9 if fast_ms > 0 else None
         roof = {"kernel": "k_fast_cells", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,

@@ -113,8 +113,8 @@ int orbx_debug_stage(orbx_handle* h, int stage, orb_keypoint* kps, int cap,
 
 /* Per-stage HIP-event timing of subsequent orbx_extract* calls (on the stream
  * they run on).  orbx_get_profile sums, over the recorded calls, the stage
- * times in ms: [0] pyramid (k_resize x L-1), [1] blur, [2] FAST cells,
- * [3] quadtree, [4] describe, [5] assemble; returns the number of calls and
+ * times in ms: [0] pyramid (k_resize x L-1), [1] FAST cells, [2] quadtree,
+ * [3] describe (orientation + blur + rBRIEF), [4] assemble; returns the number of calls and
  * clears the record.  Not part of the reference interface. */
 int orbx_set_profiling(orbx_handle* h, int enable);
 int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);

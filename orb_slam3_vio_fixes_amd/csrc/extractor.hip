@@ -6,13 +6,13 @@
 // Per batch of same-size frames the path is seven kinds of launches, all
 // batched over frames (gridDim.y = frame):
 //   k_resize       level l from level l-1, OpenCV INTER_LINEAR 8U fixed point
-//   k_blur         7x7 sigma-2 fixed-point Gaussian of every level (REFLECT_101)
 //   k_fast_cells   one wave per FAST cell: LDS-staged ROI, FAST-9 score map,
 //                  cell-local 3x3 NMS at iniThFAST / minThFAST, ballot compaction
 //   k_quadtree     one workgroup per (frame, level): DistributeOctTree as
 //                  data-parallel passes over the node list + exact std::sort
-//   k_describe     one wave per keypoint: IC_Angle moments (wave reduction),
-//                  glibc-exact sincosf, 256 rBRIEF tests -> ballot bytes
+//   k_describe     one wave per keypoint: LDS raw patch, IC_Angle moments,
+//                  7x7 fixed-point blur of the 37x37 patch only, glibc-exact
+//                  sincosf, 256 rBRIEF tests
 //   k_assemble     per frame: scaling, lapping partition (monoIndex), output
 // Everything is integer/bitwise; no MFMA.
 #include "../../include/orb_mi355x.h"
@@ -43,8 +43,6 @@ static const int8_t h_pattern[1024] = {
 struct LevelDev {
     int w, h, pitch;
     long long off;      // byte offset of the level inside one frame's pyramid slab (l >= 1)
-    long long boff;     // byte offset inside one frame's blurred slab
-    int bpitch;
     float scale;
     int patch;          // int(PATCH_SIZE * scale)  (ORBextractor.cc:880)
     // quadtree (DistributeOctTree arguments, ORBextractor.cc:877-878)
@@ -64,13 +62,13 @@ struct Plan {
     int w = 0, h = 0, L = 0, maxB = 0;
     std::vector<LevelDev> lv;
     std::vector<CellDev> cells;
-    long long pyr_bytes = 0, blur_bytes = 0;
+    long long pyr_bytes = 0;
     int ncells = 0, slot_total = 0, out_total = 0;
     int roi_max = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     std::vector<int> xmax;           // per level
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     // device
-    uint8_t *d_pyr = nullptr, *d_blur = nullptr, *d_in = nullptr;
+    uint8_t *d_pyr = nullptr, *d_in = nullptr;
     int2* d_tab = nullptr;
     LevelDev* d_lv = nullptr;
     CellDev* d_cells = nullptr;
@@ -90,7 +88,7 @@ struct Plan {
     size_t in_pitch = 0;
 
     void release() {
-        void* ps[] = {d_pyr, d_blur, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
+        void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono};
         for (void* p : ps)
             if (p) (void)hipFree(p);
@@ -172,7 +170,7 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     std::vector<int2> tab;
     P.xmax.assign(L, 0);
     P.tab_off.assign(L, 0);
-    long long poff = 0, boff = 0;
+    long long poff = 0;
     int cellsum = 0, slotsum = 0, outsum = 0;
     for (int l = 0; l < L; ++l) {
         LevelDev& d = P.lv[l];
@@ -181,11 +179,8 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
         d.h = cv_round((float)h * hd->inv_scale[l]);
         if (d.w < 2 * kEdge + 8 || d.h < 2 * kEdge + 8) return ORB_ERR_UNSUPPORTED;
         d.pitch = round_up(d.w, 64);
-        d.bpitch = d.pitch;
         d.off = l == 0 ? 0 : poff;
         if (l > 0) poff += (long long)d.pitch * d.h;
-        d.boff = boff;
-        boff += (long long)d.bpitch * d.h;
         d.scale = hd->scale[l];
         d.patch = (int)(31 * hd->scale[l]);
         if (l > 0) {
@@ -249,7 +244,7 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
                 c.cap = cap;
                 slotsum += cap;
                 P.cells.push_back(c);
-                P.roi_max = std::max(P.roi_max, c.cols * c.rows);
+                P.roi_max = std::max(P.roi_max, c.rows * ((c.cols + 6) & ~3) + 16);
                 P.win_max = std::max(P.win_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
                 ++nc;
             }
@@ -271,7 +266,6 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
         P.max_out_cap = std::max(P.max_out_cap, d.out_cap);
     }
     P.pyr_bytes = poff;
-    P.blur_bytes = boff;
     P.ncells = cellsum;
     P.slot_total = slotsum;
     P.out_total = outsum;
@@ -279,7 +273,6 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
 
     const size_t B = (size_t)maxB;
     ORB_CHECK(hipMalloc(&P.d_pyr, std::max<size_t>(1, B * P.pyr_bytes)));
-    ORB_CHECK(hipMalloc(&P.d_blur, B * P.blur_bytes));
     ORB_CHECK(hipMalloc(&P.d_in, P.in_pitch * h));
     ORB_CHECK(hipMalloc(&P.d_tab, std::max<size_t>(1, tab.size()) * sizeof(int2)));
     ORB_CHECK(hipMalloc(&P.d_lv, L * sizeof(LevelDev)));
@@ -334,51 +327,6 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src,
             h1 = S1[sx] * 2048;
         }
         D[dx] = (uint8_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_blur: GaussianBlur(7x7, sigma 2, REFLECT_101), fixed point:
-// h = sum k*p (u16), out = (sum k*h + 2^15) >> 16.  64x16 output tiles.
-// ---------------------------------------------------------------------------
-struct BlurKernel { int k[7]; };
-
-__global__ __launch_bounds__(256) void k_blur(const uint8_t* __restrict__ src, long long s_fstride, int s_pitch,
-                                              uint8_t* __restrict__ dst, long long d_fstride, int d_pitch, int w,
-                                              int h, BlurKernel K) {
-    __shared__ uint8_t tin[22][72];
-    __shared__ uint32_t th[22][65];
-    const int f = blockIdx.z;
-    const int x0 = blockIdx.x * 64, y0 = blockIdx.y * 16;
-    const uint8_t* S = src + f * s_fstride;
-    auto refl = [](int p, int n) {
-        if (n == 1) return 0;
-        while (p < 0 || p >= n) p = p < 0 ? -p : 2 * n - 2 - p;
-        return p;
-    };
-    for (int i = threadIdx.x; i < 22 * 70; i += 256) {
-        const int r = i / 70, c = i - r * 70;
-        const int yy = refl(y0 + r - 3, h), xx = refl(x0 + c - 3, w);
-        tin[r][c] = S[(long long)yy * s_pitch + xx];
-    }
-    __syncthreads();
-    for (int i = threadIdx.x; i < 22 * 64; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) acc += K.k[t] * tin[r][c + t];
-        th[r][c] = acc;
-    }
-    __syncthreads();
-    uint8_t* D = dst + f * d_fstride;
-    for (int i = threadIdx.x; i < 16 * 64; i += 256) {
-        const int r = i >> 6, c = i & 63;
-        const int yy = y0 + r, xx = x0 + c;
-        if (yy >= h || xx >= w) continue;
-        uint32_t acc = 0;
-#pragma unroll
-        for (int t = 0; t < 7; ++t) acc += K.k[t] * th[r + t][c];
-        D[(long long)yy * d_pitch + xx] = (uint8_t)((acc + 32768u) >> 16);
     }
 }
 
@@ -458,6 +406,23 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int ww, int wh, int 
     return true;
 }
 
+// Compass pre-test: a 9-pixel arc of the 16-ring always covers >= 2 of the 4
+// compass pixels, so a corner at threshold t has >= 2 compass pixels brighter
+// than v+t or >= 2 darker than v-t.  Pixels failing it at min(iniTh, minTh)
+// are corners at no threshold used; their score is stored as 0, which the NMS
+// treats exactly like a non-corner (s_t(q) = 0).
+__device__ __forceinline__ bool fast_pretest(const uint8_t* roi, int stride, int r, int c, int t) {
+    const uint8_t* p = roi + r * stride + c;
+    const int v = p[0];
+    const int n0 = p[3 * stride], n4 = p[3], n8 = p[-3 * stride], n12 = p[-3];
+    const int nb = (n0 - v > t) + (n4 - v > t) + (n8 - v > t) + (n12 - v > t);
+    const int nd = (v - n0 > t) + (v - n4 > t) + (v - n8 > t) + (v - n12 > t);
+    return nb >= 2 || nd >= 2;
+}
+
+// row/column of linear window index i (ww <= 4096): exact via a float reciprocal
+__device__ __forceinline__ int div_row(int i, float inv_ww) { return (int)(((float)i + 0.5f) * inv_ww); }
+
 __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
@@ -466,42 +431,90 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     const bool active = ci < a.ncells;
     CellDev c{};
     if (active) c = a.cells[ci];
-    uint8_t* roi = smem + wv * (a.roi_max + a.win_max);
+    uint8_t* roi = smem + wv * (a.roi_max + 3 * a.win_max);   // roi_max, win_max are multiples of 16
     uint8_t* sc = roi + a.roi_max;
+    uint16_t* cand = (uint16_t*)(sc + a.win_max);       // candidate queue (window indices)
     const uint8_t* img = nullptr;
-    int pitch = 0;
+    int pitch = 0, rstride = 4, shift = 0;
     if (active) {
         if (c.level == 0) { img = a.in + f * a.in_fstride; pitch = a.in_pitch; }
         else { img = a.pyr + f * a.pyr_fstride + a.lv[c.level].off; pitch = a.lv[c.level].pitch; }
-        const int n = c.rows * c.cols;
-        for (int i = lane; i < n; i += kWave) {
-            const int r = i / c.cols, cc = i - r * c.cols;
-            roi[i] = img[(long long)(c.y0 + r) * pitch + c.x0 + cc];
+        // ROI rows as aligned dwords (the ROI lies >= 16 px inside the level, so
+        // the <= 3 bytes read past its right edge stay inside the image row)
+        const int base = c.x0 & ~3;
+        shift = c.x0 - base;
+        const int nd = (shift + c.cols + 3) >> 2;
+        rstride = nd * 4;
+        const int n = c.rows * nd;
+        const float inv_nd = 1.0f / (float)nd;
+        for (int b0 = 0; b0 < n; b0 += 8 * kWave) {
+            uint32_t v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = b0 + lane + j * kWave;
+                if (i < n) {
+                    const int r = div_row(i, inv_nd), d = i - r * nd;
+                    v[j] = *(const uint32_t*)(img + (long long)(c.y0 + r) * pitch + base + 4 * d);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int i = b0 + lane + j * kWave;
+                if (i < n) ((uint32_t*)roi)[i] = v[j];
+            }
         }
     }
+    const uint8_t* R = roi + shift;
     __syncthreads();
     const int ww = active ? max(0, c.cols - 6) : 0, wh = active ? max(0, c.rows - 6) : 0;
     const int nwin = ww * wh;
-    for (int i = lane; i < nwin; i += kWave) {
-        const int r = i / ww, cc = i - r * ww;
-        sc[i] = (uint8_t)fast_score(roi, c.cols, r + 3, cc + 3);
-    }
-    __syncthreads();
-    int cnt = 0;
+    const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
+    const int tmin = min(a.ini_th, a.min_th);
+    int ncand = 0;
     for (int base = 0; base < nwin; base += kWave) {
         const int i = base + lane;
+        bool pass = false;
+        if (i < nwin) {
+            const int r = div_row(i, inv_ww);
+            sc[i] = 0;
+            pass = fast_pretest(R, rstride, r + 3, i - r * ww + 3, tmin);
+        }
+        const uint64_t m = __ballot(pass);
+        if (pass) cand[ncand + mask_rank(m)] = (uint16_t)i;
+        ncand += __popcll(m);
+    }
+    __syncthreads();
+    for (int q = lane; q < ncand; q += kWave) {
+        const int i = cand[q];
+        const int r = div_row(i, inv_ww);
+        sc[i] = (uint8_t)fast_score(R, rstride, r + 3, i - r * ww + 3);
+    }
+    __syncthreads();
+    // NMS at iniThFAST; a cell without survivors re-runs at minThFAST (ORBextractor.cc:826-846).
+    // Only candidates can survive, so both passes walk the candidate queue (row-major order).
+    int cnt = 0;
+    for (int base = 0; base < ncand; base += kWave) {
+        const int q = base + lane;
         bool keep = false;
-        if (i < nwin) { const int r = i / ww; keep = nms_keep(sc, ww, wh, r, i - r * ww, a.ini_th); }
+        if (q < ncand) {
+            const int i = cand[q], r = div_row(i, inv_ww);
+            keep = nms_keep(sc, ww, wh, r, i - r * ww, a.ini_th);
+        }
         cnt += __popcll(__ballot(keep));
     }
     const int t = cnt > 0 ? a.ini_th : a.min_th;
     uint32_t* out = a.cell_keys + (long long)f * a.slot_total + c.slot_off;
     int written = 0;
-    for (int base = 0; base < nwin; base += kWave) {
-        const int i = base + lane;
+    for (int base = 0; base < ncand; base += kWave) {
+        const int q = base + lane;
         bool keep = false;
-        int r = 0, cc = 0;
-        if (i < nwin) { r = i / ww; cc = i - r * ww; keep = nms_keep(sc, ww, wh, r, cc, t); }
+        int i = 0, r = 0, cc = 0;
+        if (q < ncand) {
+            i = cand[q];
+            r = div_row(i, inv_ww);
+            cc = i - r * ww;
+            keep = nms_keep(sc, ww, wh, r, cc, t);
+        }
         const uint64_t m = __ballot(keep);
         if (keep) {
             const int pos = written + mask_rank(m);
@@ -516,7 +529,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     }
     if (active && lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, c.cap);
 }
-
 
 // ---------------------------------------------------------------------------
 // k_quadtree: ORBextractor::DistributeOctTree (ORBextractor.cc:555-779) for
@@ -822,18 +834,25 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// k_describe: computeOrientation/IC_Angle (ORBextractor.cc:76-103,471-478) on
-// the unblurred level and computeOrbDescriptor (:107-146) on the blurred
-// level.  One wave per keypoint; lane l evaluates rBRIEF tests 4l..4l+3.
+// k_describe: computeOrientation/IC_Angle (ORBextractor.cc:76-103,471-478) and
+// computeOrbDescriptor (:107-146) with the level blur folded in.
+//
+// The reference blurs every full level (GaussianBlur 7x7, sigma 2,
+// REFLECT_101 on a clone(), :1132-1133) and samples it.  Here one wave per
+// keypoint stages the 43x43 raw patch around the keypoint in LDS (reflected
+// at the level border exactly like the full-level blur would see it), reads
+// the IC_Angle disc (radius 15) from it, blurs the 37x37 centre with the same
+// fixed-point separable kernel and evaluates the 256 tests on
+// it: the blurred level never goes to HBM.  Lane l evaluates tests 4l..4l+3.
 // ---------------------------------------------------------------------------
+constexpr int kRaw = 43, kRawP = 48, kBl = 37;
+
 struct DescArgs {
     const uint8_t* in;
     long long in_fstride;
     int in_pitch;
     const uint8_t* pyr;
     long long pyr_fstride;
-    const uint8_t* blur;
-    long long blur_fstride;
     const LevelDev* lv;
     const uint32_t* qt_key;
     const int* qt_n;
@@ -841,69 +860,150 @@ struct DescArgs {
     uint8_t* sdesc;
     int out_total, L;
     int fma;
+    int kern[7];
     int umax[16];
 };
 
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int refl101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
+
+// Stage the 43 x 43 raw patch whose top-left level pixel is (x0, y0) into
+// `raw` (row pitch 48); returns the byte shift of column 0 inside a row.
+// Interior patches move as 12 aligned dwords per row, all loads in flight at
+// once; patches touching the level border fall back to reflected byte loads.
+__device__ __forceinline__ int stage_patch(const uint8_t* img, int pitch, int w, int h, int x0, int y0,
+                                           uint8_t* raw) {
+    const int lane = lane_id();
+    const int base = x0 & ~3;
+    if (y0 >= 0 && y0 + kRaw <= h && x0 >= 0 && base + kRawP <= w) {
+        constexpr int kDw = kRawP / 4, kN = kRaw * kDw;   // 516 dwords
+        uint32_t v[(kN + kWave - 1) / kWave];
+#pragma unroll
+        for (int j = 0; j < (kN + kWave - 1) / kWave; ++j) {
+            const int i = lane + j * kWave;
+            if (i < kN) {
+                const int r = i / kDw, d = i - r * kDw;
+                v[j] = *(const uint32_t*)(img + (long long)(y0 + r) * pitch + base + 4 * d);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < (kN + kWave - 1) / kWave; ++j) {
+            const int i = lane + j * kWave;
+            if (i < kN) ((uint32_t*)raw)[i] = v[j];
+        }
+        return x0 - base;
+    }
+    for (int i = lane; i < kRaw * kRaw; i += kWave) {
+        const int r = i / kRaw, c = i - r * kRaw;
+        raw[r * kRawP + c] = img[(long long)refl101(y0 + r, h) * pitch + refl101(x0 + c, w)];
+    }
+    return 0;
+}
+
 __global__ __launch_bounds__(256) void k_describe(DescArgs a) {
     __shared__ int8_t pat[1024];
+    __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
+    __shared__ uint16_t hb_s[4][kRaw * kBl];
+    __shared__ uint8_t bl_s[4][kBl * kBl];
     for (int i = threadIdx.x; i < 1024; i += 256) pat[i] = c_pattern[i];
     __syncthreads();
-    const int l = blockIdx.x, f = blockIdx.y, lane = lane_id();
+    const int l = blockIdx.x, f = blockIdx.y, lane = lane_id(), wv = wave_id();
+    uint8_t* raw = raw_s[wv];
+    uint16_t* hb = hb_s[wv];
+    uint8_t* bl = bl_s[wv];
     const LevelDev lv = a.lv[l];
     const int n = a.qt_n[f * a.L + l];
     const uint8_t* img;
     int pitch;
     if (l == 0) { img = a.in + f * a.in_fstride; pitch = a.in_pitch; }
     else { img = a.pyr + f * a.pyr_fstride + lv.off; pitch = lv.pitch; }
-    const uint8_t* bimg = a.blur + f * a.blur_fstride + lv.boff;
-    const int bp = lv.bpitch;
     const uint32_t* keys = a.qt_key + (long long)f * a.out_total + lv.out_base;
-    const int u = lane - kHalfPatch;
-    for (int p = blockIdx.z * 4 + wave_id(); p < n; p += gridDim.z * 4) {
+    // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
+    const uint32_t k0 = a.kern[0], k1 = a.kern[1], k2 = a.kern[2], k3 = a.kern[3];
+    for (int p = blockIdx.z * 4 + wv; p < n; p += gridDim.z * 4) {
         const uint32_t key = keys[p];
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
-        const uint8_t* c = img + (long long)cy * pitch + cx;
+        // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
+        const int sh = stage_patch(img, pitch, lv.w, lv.h, cx - 21, cy - 21, raw);
+        const uint8_t* R = raw + sh;
+        wave_sync();
+        // 2. IC_Angle on the unblurred disc (centre = R[21][21])
         int m10 = 0, m01 = 0;
         if (lane < 2 * kHalfPatch + 1) {
+            const int u = lane - kHalfPatch;
+            const uint8_t* c = R + 21 * kRawP + 21;
             m10 = u * c[u];
+#pragma unroll
             for (int v = 1; v <= kHalfPatch; ++v) {
-                if (u < -a.umax[v] || u > a.umax[v]) continue;
-                const int up = c[u + v * pitch], dn = c[u - v * pitch];
-                m10 += u * (up + dn);
-                m01 += v * (up - dn);
+                if (u >= -a.umax[v] && u <= a.umax[v]) {
+                    const int up = c[u + v * kRawP], dn = c[u - v * kRawP];
+                    m10 += u * (up + dn);
+                    m01 += v * (up - dn);
+                }
+            }
+        }
+        // 3. horizontal pass (ufixedpoint16): lane r slides along row r, 37 outputs
+        if (lane < kRaw) {
+            const uint8_t* s = R + lane * kRawP;
+            uint32_t w0 = s[0], w1 = s[1], w2 = s[2], w3 = s[3], w4 = s[4], w5 = s[5], w6 = s[6];
+            uint16_t* o = hb + lane * kBl;
+#pragma unroll
+            for (int c = 0; c < kBl; ++c) {
+                o[c] = (uint16_t)(k0 * (w0 + w6) + k1 * (w1 + w5) + k2 * (w2 + w4) + k3 * w3);
+                if (c + 1 < kBl) { w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6; w6 = s[c + 7]; }
             }
         }
         m10 = wave_sum(m10);
         m01 = wave_sum(m01);
+        wave_sync();
+        // 4. vertical pass (ufixedpoint32) + rounding: lane c slides down column c
+        if (lane < kBl) {
+            const uint16_t* s = hb + lane;
+            uint32_t w0 = s[0], w1 = s[kBl], w2 = s[2 * kBl], w3 = s[3 * kBl], w4 = s[4 * kBl], w5 = s[5 * kBl],
+                     w6 = s[6 * kBl];
+#pragma unroll
+            for (int r = 0; r < kBl; ++r) {
+                bl[r * kBl + lane] = (uint8_t)((k0 * (w0 + w6) + k1 * (w1 + w5) + k2 * (w2 + w4) + k3 * w3 + 32768u) >> 16);
+                if (r + 1 < kBl) { w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6; w6 = s[(r + 7) * kBl]; }
+            }
+        }
         const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
         const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
         float sb, ca;
         glibc_sincosf(ang, &sb, &ca);
-        const uint8_t* bc = bimg + (long long)cy * bp + cx;
+        wave_sync();
+        // 5. rBRIEF tests on the blurred patch (centre = bl[18][18])
+        const uint8_t* bc = bl + 18 * kBl + 18;
         int nib = 0;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int t = 4 * lane + k;
+        for (int q = 0; q < 4; ++q) {
+            const int t = 4 * lane + q;
             int val[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
                 const float x = (float)pat[4 * t + 2 * e], y = (float)pat[4 * t + 2 * e + 1];
-                int r, q;
+                int r, c;
                 if (a.fma) {
                     r = cv_round(__builtin_fmaf(x, sb, y * ca));
-                    q = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
+                    c = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
                 } else {
                     r = cv_round(x * sb + y * ca);
-                    q = cv_round(x * ca - y * sb);
+                    c = cv_round(x * ca - y * sb);
                 }
-                val[e] = bc[r * bp + q];
+                val[e] = bc[r * kBl + c];
             }
-            nib |= (val[0] < val[1]) << k;
+            nib |= (val[0] < val[1]) << q;
         }
         const int hi = __shfl_down(nib, 1, kWave);
         uint8_t* d = a.sdesc + ((long long)f * a.out_total + lv.out_base + p) * 32;
         if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
         if (lane == 0) a.angle[(long long)f * a.out_total + lv.out_base + p] = ang_deg;
+        wave_sync();
     }
 }
 
@@ -1032,19 +1132,6 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
                            P.pyr_bytes, d.pitch, d.w, d.h, xt, xt + d.w, P.xmax[l]);
     }
     mark();
-    // blurred levels
-    BlurKernel K;
-    static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
-    for (int t = 0; t < 7; ++t) K.k[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
-    for (int l = 0; l < L; ++l) {
-        const LevelDev& d = P.lv[l];
-        const uint8_t* src = l == 0 ? d_frames : P.d_pyr + d.off;
-        const long long sfs = l == 0 ? fstride : P.pyr_bytes;
-        const int sp = l == 0 ? pitch0 : d.pitch;
-        hipLaunchKernelGGL(k_blur, dim3((d.w + 63) / 64, (d.h + 15) / 16, B), dim3(256), 0, st, src, sfs, sp,
-                           P.d_blur + d.boff, P.blur_bytes, d.bpitch, d.w, d.h, K);
-    }
-    mark();
     // FAST cells
     FastArgs fa;
     fa.in = d_frames; fa.in_fstride = fstride; fa.in_pitch = pitch0;
@@ -1055,7 +1142,7 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
     fa.roi_max = (P.roi_max + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
-    const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max);
+    const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max);
     hipLaunchKernelGGL(k_fast_cells, dim3((P.ncells + 3) / 4, B), dim3(256), flds, st, fa);
     mark();
     // quadtree
@@ -1071,7 +1158,10 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     DescArgs da;
     da.in = d_frames; da.in_fstride = fstride; da.in_pitch = pitch0;
     da.pyr = P.d_pyr; da.pyr_fstride = P.pyr_bytes;
-    da.blur = P.d_blur; da.blur_fstride = P.blur_bytes;
+    {
+        static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
+        for (int t = 0; t < 7; ++t) da.kern[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
+    }
     da.lv = P.d_lv; da.qt_key = P.d_qt_key; da.qt_n = P.d_qt_n;
     da.angle = P.d_angle; da.sdesc = P.d_sdesc; da.out_total = P.out_total; da.L = L;
     da.fma = hd->prm.fma_sampling != 0;
