@@ -1,0 +1,132 @@
+// orb_slam3_mi355x.hpp — C++ host interface over the C ABI (orb_mi355x.h),
+// mirroring ORB_SLAM3::ORBextractor (reference include/ORBextractor.h:43-109)
+// and ORB_SLAM3::ORBmatcher (include/ORBmatcher.h:36-103) with the same names,
+// argument meaning and error behaviour, but without OpenCV types: keypoints
+// are orb_keypoint (layout-identical to cv::KeyPoint), descriptors a
+// row-major N x 32 byte buffer (cv::Mat CV_8U N x 32), images 8UC1 pointers.
+// INTEGRATION.md shows the cv::Mat glue a maintainer adds.
+#pragma once
+#include <cstdint>
+#include <stdexcept>
+#include <vector>
+
+#include "orb_mi355x.h"
+
+namespace ORB_SLAM3_MI355X {
+
+typedef orb_keypoint KeyPoint;
+
+struct Descriptors {                       // cv::Mat(N, 32, CV_8U), continuous
+    int rows = 0;
+    std::vector<uint8_t> data;
+    const uint8_t* row(int i) const { return data.data() + 32 * (size_t)i; }
+};
+
+class ORBextractor {
+public:
+    enum { HARRIS_SCORE = 0, FAST_SCORE = 1 };
+
+    // ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST)
+    ORBextractor(int nfeatures, float scaleFactor, int nlevels, int iniThFAST, int minThFAST, int device = 0)
+        : nlevels_(nlevels), scaleFactor_(scaleFactor) {
+        orbx_params p{nfeatures, scaleFactor, nlevels, iniThFAST, minThFAST, 0, 1, 0};
+        h_ = orbx_create(&p, device);
+        if (!h_) throw std::runtime_error("orbx_create: bad parameters or no HIP device");
+        scale_.resize(nlevels); inv_scale_.resize(nlevels); sigma2_.resize(nlevels); inv_sigma2_.resize(nlevels);
+        orbx_get_tables(h_, scale_.data(), inv_scale_.data(), sigma2_.data(), inv_sigma2_.data(), nullptr, nullptr);
+    }
+    ~ORBextractor() { orbx_destroy(h_); }
+    ORBextractor(const ORBextractor&) = delete;
+    ORBextractor& operator=(const ORBextractor&) = delete;
+
+    // int operator()(InputArray image, InputArray mask, vector<KeyPoint>& keypoints,
+    //                OutputArray descriptors, vector<int>& vLappingArea)
+    // Returns monoIndex, or -1 for an empty image (ORBextractor.cc:1090-1091).
+    int operator()(const uint8_t* image, int cols, int rows, size_t step, const void* /*mask: ignored*/,
+                   std::vector<KeyPoint>& keypoints, Descriptors& descriptors, const std::vector<int>& vLappingArea) {
+        if (!image || cols <= 0 || rows <= 0) return -1;
+        const int cap = orbx_max_keypoints(h_, cols, rows);
+        if (cap < 0) throw std::runtime_error("orbx_max_keypoints failed");
+        keypoints.resize(cap);
+        descriptors.data.resize((size_t)cap * 32);
+        int n = 0, mono = 0;
+        const int rc = orbx_extract(h_, image, cols, rows, step, vLappingArea.at(0), vLappingArea.at(1),
+                                    keypoints.data(), descriptors.data.data(), cap, &n, &mono);
+        if (rc != ORB_OK) throw std::runtime_error("orbx_extract failed");
+        keypoints.resize(n);
+        descriptors.rows = n;
+        descriptors.data.resize((size_t)n * 32);
+        return mono;
+    }
+
+    int GetLevels() const { return nlevels_; }
+    float GetScaleFactor() const { return scaleFactor_; }
+    std::vector<float> GetScaleFactors() const { return scale_; }
+    std::vector<float> GetInverseScaleFactors() const { return inv_scale_; }
+    std::vector<float> GetScaleSigmaSquares() const { return sigma2_; }
+    std::vector<float> GetInverseScaleSigmaSquares() const { return inv_sigma2_; }
+
+    // mvImagePyramid[level] of the last image (host copy)
+    std::vector<uint8_t> ImagePyramid(int level, int* cols, int* rows) const {
+        int w = 0, h = 0;
+        if (orbx_get_level(h_, level, nullptr, 0, &w, &h) != ORB_OK) throw std::runtime_error("orbx_get_level");
+        std::vector<uint8_t> out((size_t)w * h);
+        orbx_get_level(h_, level, out.data(), w, &w, &h);
+        if (cols) *cols = w;
+        if (rows) *rows = h;
+        return out;
+    }
+
+    orbx_handle* handle() const { return h_; }
+
+private:
+    orbx_handle* h_ = nullptr;
+    int nlevels_;
+    float scaleFactor_;
+    std::vector<float> scale_, inv_scale_, sigma2_, inv_sigma2_;
+};
+
+class ORBmatcher {
+public:
+    static const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;
+
+    explicit ORBmatcher(float nnratio = 0.6f, bool checkOri = true) : mfNNratio(nnratio), mbCheckOrientation(checkOri) {}
+
+    static int DescriptorDistance(const uint8_t* a, const uint8_t* b) { return orbm_descriptor_distance(a, b); }
+
+    // int SearchForInitialization(Frame &F1, Frame &F2, vector<cv::Point2f> &vbPrevMatched,
+    //                             vector<int> &vnMatches12, int windowSize=10)
+    int SearchForInitialization(const orbm_frame& F1, const orbm_frame& F2, std::vector<float>& vbPrevMatchedXY,
+                                std::vector<int>& vnMatches12, int windowSize = 10) const {
+        vnMatches12.assign(F1.n, -1);
+        const int nm = orbm_search_for_initialization(&F1, &F2, vbPrevMatchedXY.data(), windowSize, mfNNratio,
+                                                      mbCheckOrientation, vnMatches12.data());
+        if (nm < 0) throw std::runtime_error("SearchForInitialization failed");
+        return nm;
+    }
+
+    // int SearchByBoW(KeyFrame *pKF, Frame &F, vector<MapPoint*> &vpMapPointMatches)
+    int SearchByBoW(const orbm_frame& KF, const orbm_featvec& KFfv, const std::vector<uint8_t>& kfMapPointValid,
+                    const orbm_frame& F, const orbm_featvec& Ffv, std::vector<int>& vMatchesKFIdx) const {
+        vMatchesKFIdx.assign(F.n, -1);
+        const int nm = orbm_search_by_bow(&KF, &KFfv, kfMapPointValid.data(), &F, &Ffv, mfNNratio,
+                                          mbCheckOrientation, vMatchesKFIdx.data());
+        if (nm < 0) throw std::runtime_error("SearchByBoW failed");
+        return nm;
+    }
+
+    // int SearchByProjection(Frame &F, const vector<MapPoint*> &vpMapPoints, const float th=3, ...)
+    int SearchByProjection(const orbm_frame& F, const orbm_mappoints& mps, std::vector<int>& owner,
+                           const std::vector<uint8_t>& blocked, float th = 3, bool bFarPoints = false,
+                           float thFarPoints = 50.0f) const {
+        const int nm = orbm_search_by_projection_mps(&F, &mps, th, bFarPoints, thFarPoints, mfNNratio, owner.data(),
+                                                     blocked.data());
+        if (nm < 0) throw std::runtime_error("SearchByProjection failed");
+        return nm;
+    }
+
+    float mfNNratio;
+    bool mbCheckOrientation;
+};
+
+}  // namespace ORB_SLAM3_MI355X
