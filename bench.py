@@ -123,12 +123,20 @@ def main():
     inv_w = float(np.float32(64) / np.float32(W))
     inv_h = float(np.float32(48) / np.float32(H))
 
-    def step():
+    match_events = []
+
+    def step(timed=False):
         ex.extract_batch_device(frames, LAP, out=(kps, desc, n, mono))
+        if timed:
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
         rc = L.orbm_search_for_initialization_batch_device(
             B, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
             100, 0.9, 1, matches.data_ptr(), nmatch.data_ptr(), stream.cuda_stream)
         capi.check(rc, "SearchForInitialization batch")
+        if timed:
+            e1.record(stream)
+            match_events.append((e0, e1))
 
     for _ in range(args.warmup):
         step()
@@ -141,7 +149,7 @@ def main():
         L.orbx_set_profiling(ex._h, 1)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=prof)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -172,7 +180,9 @@ def main():
                "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
                           "frames_per_step_per_gpu": B, "parallelism": f"frames sharded over {world} GPU(s)"},
-               "stage_ms": {k: float(v) for k, v in zip(STAGES, stage_ms)},
+               "stage_ms": {**{k: float(v) for k, v in zip(STAGES, stage_ms)},
+                            "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
+                                                          if match_events else None)},
                "roofline": roof}
         if world == 1 and args.cpu_sample > 0:
             ns = min(args.cpu_sample, B)

@@ -64,7 +64,7 @@ struct Plan {
     std::vector<CellDev> cells;
     long long pyr_bytes = 0;
     int ncells = 0, slot_total = 0, out_total = 0;
-    int roi_max = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
+    int roi_max = 0, roi_dwords = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     std::vector<int> xmax;           // per level
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     // device
@@ -245,7 +245,8 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
                 slotsum += cap;
                 P.cells.push_back(c);
                 P.roi_max = std::max(P.roi_max, c.rows * ((c.cols + 6) & ~3) + 16);
-                P.win_max = std::max(P.win_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
+                P.roi_dwords = std::max(P.roi_dwords, c.rows * (((c.x0 & 3) + c.cols + 3) >> 2));
+                P.win_max = std::max(P.win_max, (std::max(0, c.cols - 6) + 2) * (std::max(0, c.rows - 6) + 2));
                 ++nc;
             }
         }
@@ -389,21 +390,18 @@ __device__ __forceinline__ int fast_score(const uint8_t* roi, int stride, int r,
     return s < 0 ? 0 : s;
 }
 
-__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int ww, int wh, int r, int c, int t) {
-    const int s = sc[r * ww + c];
+// NMS on the zero-padded score map (pitch ww+2): p survives at threshold t iff
+// s(p) >= max(t, 1) and s(p) > s_t(q) for its 8 neighbours, s_t(q) = s(q) if
+// s(q) >= t else 0; the zero border stands for pixels outside the window.
+__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c, int t) {
+    const uint8_t* p = sc + (r + 1) * sp + (c + 1);
+    const int s = p[0];
     if (s < max(t, 1)) return false;
+    const int q[8] = {p[-sp - 1], p[-sp], p[-sp + 1], p[-1], p[1], p[sp - 1], p[sp], p[sp + 1]};
+    bool keep = true;
 #pragma unroll
-    for (int dr = -1; dr <= 1; ++dr)
-#pragma unroll
-        for (int dc = -1; dc <= 1; ++dc) {
-            if (!dr && !dc) continue;
-            const int rr = r + dr, cc = c + dc;
-            if (rr < 0 || rr >= wh || cc < 0 || cc >= ww) continue;
-            const int q = sc[rr * ww + cc];
-            const int bv = q >= t ? q : 0;
-            if (!(s > bv)) return false;
-        }
-    return true;
+    for (int k = 0; k < 8; ++k) keep &= s > (q[k] >= t ? q[k] : 0);
+    return keep;
 }
 
 // Compass pre-test: a 9-pixel arc of the 16-ring always covers >= 2 of the 4
@@ -420,114 +418,153 @@ __device__ __forceinline__ bool fast_pretest(const uint8_t* roi, int stride, int
     return nb >= 2 || nd >= 2;
 }
 
+// each wave of k_fast_cells owns its cells and its LDS region: wave-level sync only
+__device__ __forceinline__ void fast_wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // row/column of linear window index i (ww <= 4096): exact via a float reciprocal
 __device__ __forceinline__ int div_row(int i, float inv_ww) { return (int)(((float)i + 0.5f) * inv_ww); }
 
+constexpr int kCellsPerWave = 4;
+
+struct RoiFetch {
+    const uint8_t* src;
+    int pitch, base, nd, n;
+    float inv_nd;
+};
+
+template <int NV>
+__device__ __forceinline__ void roi_issue(const RoiFetch& rf, int y0, uint32_t (&v)[NV]) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int i = lane + j * kWave;
+        if (i < rf.n) {
+            const int r = div_row(i, rf.inv_nd), d = i - r * rf.nd;
+            v[j] = *(const uint32_t*)(rf.src + (long long)(y0 + r) * rf.pitch + rf.base + 4 * d);
+        }
+    }
+}
+
+template <int NV>
 __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
-    const int ci = blockIdx.x * 4 + wv;
     const int f = blockIdx.y;
-    const bool active = ci < a.ncells;
+    uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 4);   // multiples of 16
+    uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max*2 bytes
+    uint16_t* cand = (uint16_t*)(sc + 2 * a.win_max);         // <= win_max entries
+    uint64_t* kmask = (uint64_t*)(roi);                       // reused after scoring (ROI no longer needed)
+    const int c_begin = (blockIdx.x * 4 + wv) * kCellsPerWave;
+    const int c_end = min(c_begin + kCellsPerWave, a.ncells);
+    auto fetch_of = [&](const CellDev& c) {
+        RoiFetch rf;
+        if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
+        else { rf.src = a.pyr + f * a.pyr_fstride + a.lv[c.level].off; rf.pitch = a.lv[c.level].pitch; }
+        rf.base = c.x0 & ~3;
+        rf.nd = ((c.x0 - rf.base) + c.cols + 3) >> 2;
+        rf.n = c.rows * rf.nd;
+        rf.inv_nd = 1.0f / (float)rf.nd;
+        return rf;
+    };
+    uint32_t v[NV];
     CellDev c{};
-    if (active) c = a.cells[ci];
-    uint8_t* roi = smem + wv * (a.roi_max + 3 * a.win_max);   // roi_max, win_max are multiples of 16
-    uint8_t* sc = roi + a.roi_max;
-    uint16_t* cand = (uint16_t*)(sc + a.win_max);       // candidate queue (window indices)
-    const uint8_t* img = nullptr;
-    int pitch = 0, rstride = 4, shift = 0;
-    if (active) {
-        if (c.level == 0) { img = a.in + f * a.in_fstride; pitch = a.in_pitch; }
-        else { img = a.pyr + f * a.pyr_fstride + a.lv[c.level].off; pitch = a.lv[c.level].pitch; }
-        // ROI rows as aligned dwords (the ROI lies >= 16 px inside the level, so
-        // the <= 3 bytes read past its right edge stay inside the image row)
-        const int base = c.x0 & ~3;
-        shift = c.x0 - base;
-        const int nd = (shift + c.cols + 3) >> 2;
-        rstride = nd * 4;
-        const int n = c.rows * nd;
-        const float inv_nd = 1.0f / (float)nd;
-        for (int b0 = 0; b0 < n; b0 += 8 * kWave) {
-            uint32_t v[8];
+    RoiFetch rf{};
+    if (c_begin < c_end) {
+        c = a.cells[c_begin];
+        rf = fetch_of(c);
+        roi_issue<NV>(rf, c.y0, v);
+    }
+    const int tmin = min(a.ini_th, a.min_th);
+    for (int ci = c_begin; ci < c_end; ++ci) {
+        // land the prefetched ROI in LDS, then prefetch the next cell's ROI
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int i = b0 + lane + j * kWave;
-                if (i < n) {
-                    const int r = div_row(i, inv_nd), d = i - r * nd;
-                    v[j] = *(const uint32_t*)(img + (long long)(c.y0 + r) * pitch + base + 4 * d);
+        for (int j = 0; j < NV; ++j) {
+            const int i = lane + j * kWave;
+            if (i < rf.n) ((uint32_t*)roi)[i] = v[j];
+        }
+        const int shift = c.x0 - rf.base, rstride = rf.nd * 4;
+        const uint8_t* R = roi + shift;
+        const int ww = max(0, c.cols - 6), wh = max(0, c.rows - 6);
+        const int sp = ww + 2, npad = sp * (wh + 2);
+        for (int i = lane; i < (npad + 3) / 4; i += kWave) ((uint32_t*)sc)[i] = 0u;
+        const CellDev cur = c;
+        if (ci + 1 < c_end) {
+            c = a.cells[ci + 1];
+            rf = fetch_of(c);
+            roi_issue<NV>(rf, c.y0, v);
+        }
+        fast_wave_sync();
+        const int nwin = ww * wh;
+        const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
+        // 1. compass pre-test, ballot-compacted candidate queue (row-major)
+        int ncand = 0;
+        for (int base = 0; base < nwin; base += kWave) {
+            const int i = base + lane;
+            bool pass = false;
+            if (i < nwin) {
+                const int r = div_row(i, inv_ww);
+                pass = fast_pretest(R, rstride, r + 3, i - r * ww + 3, tmin);
+            }
+            const uint64_t m = __ballot(pass);
+            if (pass) cand[ncand + mask_rank(m)] = (uint16_t)i;
+            ncand += __popcll(m);
+        }
+        fast_wave_sync();
+        // 2. FAST score of the candidates
+        for (int q = lane; q < ncand; q += kWave) {
+            const int i = cand[q];
+            const int r = div_row(i, inv_ww), cc = i - r * ww;
+            sc[(r + 1) * sp + cc + 1] = (uint8_t)fast_score(R, rstride, r + 3, cc + 3);
+        }
+        fast_wave_sync();
+        // 3. NMS at iniThFAST once; keep its ballots (ORBextractor.cc:826-827)
+        int cnt = 0;
+        const int nchunk = (ncand + kWave - 1) / kWave;
+        for (int k = 0; k < nchunk; ++k) {
+            const int q = k * kWave + lane;
+            bool keep = false;
+            if (q < ncand) {
+                const int i = cand[q], r = div_row(i, inv_ww);
+                keep = nms_keep(sc, sp, r, i - r * ww, a.ini_th);
+            }
+            const uint64_t m = __ballot(keep);
+            if (lane == 0) kmask[k] = m;
+            cnt += __popcll(m);
+        }
+        fast_wave_sync();
+        // 4. survivors (cells without any re-run at minThFAST, :843-846), row-major
+        const bool rerun = cnt == 0;
+        uint32_t* out = a.cell_keys + (long long)f * a.slot_total + cur.slot_off;
+        int written = 0;
+        for (int k = 0; k < nchunk; ++k) {
+            const int q = k * kWave + lane;
+            int i = 0, r = 0, cc = 0;
+            bool keep = false;
+            if (q < ncand) {
+                i = cand[q];
+                r = div_row(i, inv_ww);
+                cc = i - r * ww;
+                keep = rerun ? nms_keep(sc, sp, r, cc, a.min_th) : ((kmask[k] >> lane) & 1);
+            }
+            const uint64_t m = __ballot(keep);
+            if (keep) {
+                const int pos = written + mask_rank(m);
+                if (pos < cur.cap) {
+                    // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
+                    const uint32_t x = (uint32_t)(cur.x0 + cc + 3 - (kEdge - 3));
+                    const uint32_t y = (uint32_t)(cur.y0 + r + 3 - (kEdge - 3));
+                    out[pos] = x | (y << 12) | ((uint32_t)sc[(r + 1) * sp + cc + 1] << 24);
                 }
             }
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const int i = b0 + lane + j * kWave;
-                if (i < n) ((uint32_t*)roi)[i] = v[j];
-            }
+            written += __popcll(m);
         }
+        if (lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, cur.cap);
+        fast_wave_sync();
     }
-    const uint8_t* R = roi + shift;
-    __syncthreads();
-    const int ww = active ? max(0, c.cols - 6) : 0, wh = active ? max(0, c.rows - 6) : 0;
-    const int nwin = ww * wh;
-    const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
-    const int tmin = min(a.ini_th, a.min_th);
-    int ncand = 0;
-    for (int base = 0; base < nwin; base += kWave) {
-        const int i = base + lane;
-        bool pass = false;
-        if (i < nwin) {
-            const int r = div_row(i, inv_ww);
-            sc[i] = 0;
-            pass = fast_pretest(R, rstride, r + 3, i - r * ww + 3, tmin);
-        }
-        const uint64_t m = __ballot(pass);
-        if (pass) cand[ncand + mask_rank(m)] = (uint16_t)i;
-        ncand += __popcll(m);
-    }
-    __syncthreads();
-    for (int q = lane; q < ncand; q += kWave) {
-        const int i = cand[q];
-        const int r = div_row(i, inv_ww);
-        sc[i] = (uint8_t)fast_score(R, rstride, r + 3, i - r * ww + 3);
-    }
-    __syncthreads();
-    // NMS at iniThFAST; a cell without survivors re-runs at minThFAST (ORBextractor.cc:826-846).
-    // Only candidates can survive, so both passes walk the candidate queue (row-major order).
-    int cnt = 0;
-    for (int base = 0; base < ncand; base += kWave) {
-        const int q = base + lane;
-        bool keep = false;
-        if (q < ncand) {
-            const int i = cand[q], r = div_row(i, inv_ww);
-            keep = nms_keep(sc, ww, wh, r, i - r * ww, a.ini_th);
-        }
-        cnt += __popcll(__ballot(keep));
-    }
-    const int t = cnt > 0 ? a.ini_th : a.min_th;
-    uint32_t* out = a.cell_keys + (long long)f * a.slot_total + c.slot_off;
-    int written = 0;
-    for (int base = 0; base < ncand; base += kWave) {
-        const int q = base + lane;
-        bool keep = false;
-        int i = 0, r = 0, cc = 0;
-        if (q < ncand) {
-            i = cand[q];
-            r = div_row(i, inv_ww);
-            cc = i - r * ww;
-            keep = nms_keep(sc, ww, wh, r, cc, t);
-        }
-        const uint64_t m = __ballot(keep);
-        if (keep) {
-            const int pos = written + mask_rank(m);
-            if (pos < c.cap) {
-                // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
-                const uint32_t x = (uint32_t)(c.x0 + cc + 3 - (kEdge - 3));
-                const uint32_t y = (uint32_t)(c.y0 + r + 3 - (kEdge - 3));
-                out[pos] = x | (y << 12) | ((uint32_t)sc[i] << 24);
-            }
-        }
-        written += __popcll(m);
-    }
-    if (active && lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, c.cap);
 }
 
 // ---------------------------------------------------------------------------
@@ -575,6 +612,7 @@ struct QtLds {
     int* nd;        // per node: undivided (scanned)
     int* expand;    // queue of list indices (processing order)
     SortRec* srt;
+    SortFrame* stk; // introsort stack
     int* tmp;       // scan scratch
     int* misc;
 };
@@ -702,6 +740,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         s.nd = (int*)take(NC * sizeof(int));
         s.expand = (int*)take(NC * sizeof(int));
         s.srt = (SortRec*)take(NC * sizeof(SortRec));
+        s.stk = (SortFrame*)take(80 * sizeof(SortFrame));
         s.tmp = (int*)take(16 * sizeof(int));
         s.misc = (int*)take(16 * sizeof(int));
     }
@@ -789,7 +828,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         }
         for (int i = tid; i < size; i += T) s.div[i] = 0;
         __syncthreads();
-        if (tid == 0) std_sort(s.srt, m);
+        if (tid == 0) std_sort(s.srt, m, s.stk);
         __syncthreads();
         for (int j = tid; j < m; j += T) s.div[s.srt[j].pos] = 1;
         __syncthreads();
@@ -845,7 +884,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 // fixed-point separable kernel and evaluates the 256 tests on
 // it: the blurred level never goes to HBM.  Lane l evaluates tests 4l..4l+3.
 // ---------------------------------------------------------------------------
-constexpr int kRaw = 43, kRawP = 48, kBl = 37;
+constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 44;   // hbT pitch: 88 B rows, 8-B aligned
 
 struct DescArgs {
     const uint8_t* in;
@@ -905,10 +944,10 @@ __device__ __forceinline__ int stage_patch(const uint8_t* img, int pitch, int w,
     return 0;
 }
 
-__global__ __launch_bounds__(256) void k_describe(DescArgs a) {
+__global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
     __shared__ int8_t pat[1024];
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
-    __shared__ uint16_t hb_s[4][kRaw * kBl];
+    __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][kBl * kHbP];
     __shared__ uint8_t bl_s[4][kBl * kBl];
     for (int i = threadIdx.x; i < 1024; i += 256) pat[i] = c_pattern[i];
     __syncthreads();
@@ -947,30 +986,43 @@ __global__ __launch_bounds__(256) void k_describe(DescArgs a) {
                 }
             }
         }
-        // 3. horizontal pass (ufixedpoint16): lane r slides along row r, 37 outputs
+        // 3. horizontal pass (ufixedpoint16): lane r holds row r in registers
+        //    (3 x ds_read_b128 + v_alignbyte for the column shift) and writes
+        //    its 37 outputs transposed, hbT[c][r], so step 4 reads columns
+        //    as contiguous runs
         if (lane < kRaw) {
-            const uint8_t* s = R + lane * kRawP;
-            uint32_t w0 = s[0], w1 = s[1], w2 = s[2], w3 = s[3], w4 = s[4], w5 = s[5], w6 = s[6];
-            uint16_t* o = hb + lane * kBl;
+            const uint4* rowp = (const uint4*)(raw + lane * kRawP);
+            const uint4 q0 = rowp[0], q1 = rowp[1], q2 = rowp[2];
+            const uint32_t wd[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
+            uint32_t al[11];
 #pragma unroll
-            for (int c = 0; c < kBl; ++c) {
-                o[c] = (uint16_t)(k0 * (w0 + w6) + k1 * (w1 + w5) + k2 * (w2 + w4) + k3 * w3);
-                if (c + 1 < kBl) { w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6; w6 = s[c + 7]; }
-            }
+            for (int j = 0; j < 11; ++j) al[j] = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], (uint32_t)sh);
+            uint32_t px[kRaw];
+#pragma unroll
+            for (int j = 0; j < kRaw; ++j) px[j] = (al[j >> 2] >> (8 * (j & 3))) & 0xffu;
+#pragma unroll
+            for (int c = 0; c < kBl; ++c)
+                hb[c * kHbP + lane] = (uint16_t)(k0 * (px[c] + px[c + 6]) + k1 * (px[c + 1] + px[c + 5]) +
+                                                 k2 * (px[c + 2] + px[c + 4]) + k3 * px[c + 3]);
         }
         m10 = wave_sum(m10);
         m01 = wave_sum(m01);
         wave_sync();
-        // 4. vertical pass (ufixedpoint32) + rounding: lane c slides down column c
+        // 4. vertical pass (ufixedpoint32) + rounding: lane c holds column c
+        //    (11 x ds_read_b64 of hbT[c][0..43])
         if (lane < kBl) {
-            const uint16_t* s = hb + lane;
-            uint32_t w0 = s[0], w1 = s[kBl], w2 = s[2 * kBl], w3 = s[3 * kBl], w4 = s[4 * kBl], w5 = s[5 * kBl],
-                     w6 = s[6 * kBl];
+            const uint2* colp = (const uint2*)(hb + lane * kHbP);
+            uint32_t hv[44];
 #pragma unroll
-            for (int r = 0; r < kBl; ++r) {
-                bl[r * kBl + lane] = (uint8_t)((k0 * (w0 + w6) + k1 * (w1 + w5) + k2 * (w2 + w4) + k3 * w3 + 32768u) >> 16);
-                if (r + 1 < kBl) { w0 = w1; w1 = w2; w2 = w3; w3 = w4; w4 = w5; w5 = w6; w6 = s[(r + 7) * kBl]; }
+            for (int j = 0; j < 11; ++j) {
+                const uint2 v = colp[j];
+                hv[4 * j] = v.x & 0xffffu; hv[4 * j + 1] = v.x >> 16;
+                hv[4 * j + 2] = v.y & 0xffffu; hv[4 * j + 3] = v.y >> 16;
             }
+#pragma unroll
+            for (int r = 0; r < kBl; ++r)
+                bl[r * kBl + lane] = (uint8_t)((k0 * (hv[r] + hv[r + 6]) + k1 * (hv[r + 1] + hv[r + 5]) +
+                                                k2 * (hv[r + 2] + hv[r + 4]) + k3 * hv[r + 3] + 32768u) >> 16);
         }
         const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
         const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
@@ -1098,7 +1150,7 @@ static size_t qt_lds_bytes(const Plan& P) {
     auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
     size_t b = al((P.max_level_cells + 1) * 4);
     b += 2 * al(NC * 8) + 2 * al(NC * 4) + 2 * al(NC) + 2 * al(NC * 16);
-    b += 7 * al(NC * 4) + al(NC * sizeof(SortRec)) + 2 * al(64);
+    b += 7 * al(NC * 4) + al(NC * sizeof(SortRec)) + al(80 * sizeof(SortFrame)) + 2 * al(64);
     return b;
 }
 
@@ -1142,8 +1194,12 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
     fa.roi_max = (P.roi_max + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
-    const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max);
-    hipLaunchKernelGGL(k_fast_cells, dim3((P.ncells + 3) / 4, B), dim3(256), flds, st, fa);
+    const size_t flds = 4 * (size_t)(fa.roi_max + 4 * fa.win_max);
+    const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
+    const int nv = (P.roi_dwords + kWave - 1) / kWave;
+    if (nv <= 12) hipLaunchKernelGGL(k_fast_cells<12>, fgrid, dim3(256), flds, st, fa);
+    else if (nv <= 24) hipLaunchKernelGGL(k_fast_cells<24>, fgrid, dim3(256), flds, st, fa);
+    else hipLaunchKernelGGL(k_fast_cells<48>, fgrid, dim3(256), flds, st, fa);
     mark();
     // quadtree
     QtArgs qa;

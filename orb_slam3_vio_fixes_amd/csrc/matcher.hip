@@ -48,6 +48,12 @@ __device__ __forceinline__ int hamming32(const uint4 a0, const uint4 a1, const u
            __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
 }
 
+__device__ __forceinline__ void wave_sync_m() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // ---------------------------------------------------------------------------
 // k_grid: AssignFeaturesToGrid for a batch of frames.  Output per frame: the
 // feature indices sorted by (cell, index), packed (cell << 16 | index), and
@@ -174,10 +180,21 @@ __device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int
 }
 
 // ---------------------------------------------------------------------------
-// k_sfi: ORBmatcher::SearchForInitialization (ORBmatcher.cc:648-763), one wave
-// per frame pair.  LDS: F2's level-0 features in grid order, vMatchedDistance,
-// vnMatches21, the rotation bin of every accepted F1 feature.
+// SearchForInitialization (ORBmatcher.cc:648-763) in two kernels.
+//
+// The only order dependence is the skip rule `if (vMatchedDistance[i2] <=
+// dist) continue;` (:687-688): the best and second-best of F1 feature i1 are
+// the first two elements, in (distance, candidate order), of its candidates
+// that survive that rule under the state left by i1-1.  k_sfi_topk computes,
+// for every level-0 F1 feature in parallel, its candidate count and its
+// kTopK smallest (distance, order) pairs.  k_sfi_resolve then walks F1 in
+// order with one wave per frame pair; each step filters <= kTopK entries
+// against vMatchedDistance.  When fewer than two entries survive and the list
+// was truncated, the wave re-scans the full candidate list (exact fallback).
 // ---------------------------------------------------------------------------
+constexpr int kTopK = 8;
+constexpr uint32_t kNoKey = 0xffffffffu;
+
 struct SfiArgs {
     const orb_keypoint* kps;
     const uint8_t* desc;
@@ -185,18 +202,122 @@ struct SfiArgs {
     int cap;
     const uint32_t* gsorted;
     const int* gcount;
-    const int* pair_f1;      // per pair: frame index of F1 (F2 = pair_f2)
+    const int* pair_f1;      // per pair: frame index of F1 / F2
     const int* pair_f2;
     const float* prev_in;    // [pair][cap][2] or null (= F1 keypoint positions)
     float* prev_out;         // [pair][cap][2] or null
     GridParams g;
     float window, ratio;
     int check_ori;
+    uint32_t* topk;          // [pair][cap][kTopK]  (dist << 16 | order in the level-0 list)
+    int* ncand;              // [pair][cap]  (-1: not a query)
     int32_t* matches;        // [pair][cap]
     int32_t* nmatches;       // [pair]
 };
 
-__global__ __launch_bounds__(64) void k_sfi(SfiArgs a) {
+// F2's level-0 features in grid order (GetFeaturesInArea(.., level1, level1)
+// with level1 = 0 keeps octave 0 only, :668) -> LDS, returns the count.
+__device__ int level0_list(const SfiArgs& a, int f2, int* list) {
+    const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
+    const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
+    const int gn = a.gcount[f2];
+    int nl = 0;
+    for (int base = 0; base < gn; base += kWave) {
+        const int i = base + lane_id();
+        uint32_t v = 0;
+        bool keep = false;
+        if (i < gn) { v = gs[i]; keep = K2[v & 0xffff].octave == 0; }
+        const uint64_t m = __ballot(keep);
+        if (keep) list[nl + mask_rank(m)] = (int)v;
+        nl += __popcll(m);
+    }
+    return nl;
+}
+
+__device__ __forceinline__ void query_pos(const SfiArgs& a, int pr, int i1, const orb_keypoint& k1, float& px,
+                                          float& py) {
+    px = k1.x; py = k1.y;
+    if (a.prev_in) {
+        px = a.prev_in[((long long)pr * a.cap + i1) * 2];
+        py = a.prev_in[((long long)pr * a.cap + i1) * 2 + 1];
+    }
+}
+
+// distance of list entry j to query i1 if it is a candidate, else INT_MAX
+__device__ __forceinline__ int cand_dist(const int* list, int j, const CellRange& cr, float px, float py, float r,
+                                         const orb_keypoint* K2, const uint8_t* D2, uint4 q0, uint4 q1) {
+    const int v = list[j];
+    const int cell = v >> 16, gx = cell / kGridRows, gy = cell - gx * kGridRows;
+    if (gx < cr.x0 || gx > cr.x1 || gy < cr.y0 || gy > cr.y1) return INT_MAX;
+    const int fi = v & 0xffff;
+    const orb_keypoint k2 = K2[fi];
+    if (!(fabsf(k2.x - px) < r && fabsf(k2.y - py) < r)) return INT_MAX;
+    return hamming32(q0, q1, D2 + (long long)fi * 32);
+}
+
+// grid (npairs, ceil(cap / 16)), 256 threads: 4 waves x 4 queries each
+__global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    int* list = lds;                              // cap entries (block-shared)
+    uint32_t* pool = (uint32_t*)(lds + a.cap);    // per wave: cap keys
+    const int pr = blockIdx.x, lane = lane_id(), wv = wave_id();
+    const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
+    const int n1 = min(a.n[f1], a.cap);
+    __shared__ int s_nl;
+    if (wv == 0) {
+        const int nl = level0_list(a, f2, list);
+        if (lane == 0) s_nl = nl;
+    }
+    __syncthreads();
+    const int nl = s_nl;
+    uint32_t* mypool = pool + wv * a.cap;
+    const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
+    const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
+    const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
+    const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
+    const float r = a.window;
+    for (int t = 0; t < 4; ++t) {
+        const int i1 = blockIdx.y * 16 + wv * 4 + t;
+        if (i1 >= n1) break;
+        uint32_t* tk = a.topk + ((long long)pr * a.cap + i1) * kTopK;
+        int* nc = a.ncand + (long long)pr * a.cap + i1;
+        const orb_keypoint k1 = K1[i1];
+        float px, py;
+        query_pos(a, pr, i1, k1, px, py);
+        CellRange cr;
+        if (k1.octave > 0 || !cell_range(px, py, r, a.g, cr)) {
+            if (lane == 0) *nc = -1;
+            continue;
+        }
+        const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32), q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+        int cnt = 0;
+        for (int base = 0; base < nl; base += kWave) {
+            const int j = base + lane;
+            const int d = j < nl ? cand_dist(list, j, cr, px, py, r, K2, D2, q0, q1) : INT_MAX;
+            const uint64_t m = __ballot(d != INT_MAX);
+            if (d != INT_MAX) mypool[cnt + mask_rank(m)] = ((uint32_t)d << 16) | (uint32_t)j;
+            cnt += __popcll(m);
+        }
+        wave_sync_m();
+        // kTopK rounds of wave minimum over the pool
+        for (int k = 0; k < kTopK; ++k) {
+            uint32_t mn = kNoKey;
+            for (int q = lane; q < cnt; q += kWave) mn = min(mn, mypool[q]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, kWave));
+            if (lane == 0) tk[k] = mn;
+            if (mn == kNoKey) { for (int kk = k + 1 + lane; kk < kTopK; kk += kWave) tk[kk] = kNoKey; break; }
+            for (int q = lane; q < cnt; q += kWave)
+                if (mypool[q] == mn) mypool[q] = kNoKey;
+            wave_sync_m();
+        }
+        if (lane == 0) *nc = cnt;
+        wave_sync_m();
+    }
+}
+
+// one wave per pair: the serial pass
+__global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id();
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
@@ -205,76 +326,92 @@ __global__ __launch_bounds__(64) void k_sfi(SfiArgs a) {
     const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
     const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
     const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
-    int* list = lds;                          // cap: (cell<<16 | idx) of level-0 F2 features
+    int* list = lds;                          // cap
     int* mdist = list + a.cap;                // cap
     int* m21 = mdist + a.cap;                 // cap
     int* hist = m21 + a.cap;                  // 32
-    int8_t* bin1 = (int8_t*)(hist + 32);      // cap: rotation bin of F1 feature or -1
+    int8_t* bin1 = (int8_t*)(hist + 32);      // cap
     int32_t* m12 = a.matches + (long long)pr * a.cap;
-    // level-0 filter of the grid order (GetFeaturesInArea(..., level1, level1) with level1 = 0)
-    const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
-    const int gn = a.gcount[f2];
-    int nl = 0;
-    for (int base = 0; base < gn; base += kWave) {
-        const int i = base + lane;
-        uint32_t v = 0;
-        bool keep = false;
-        if (i < gn) { v = gs[i]; keep = K2[v & 0xffff].octave == 0; }
-        const uint64_t m = __ballot(keep);
-        if (keep) list[nl + mask_rank(m)] = (int)v;
-        nl += __popcll(m);
-    }
+    const int nl = level0_list(a, f2, list);
     for (int i = lane; i < n2; i += kWave) { mdist[i] = INT_MAX; m21[i] = -1; }
     for (int i = lane; i < 32; i += kWave) hist[i] = 0;
     for (int i = lane; i < n1; i += kWave) { m12[i] = -1; bin1[i] = -1; }
     __syncthreads();
+    const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
+    const int* ncand = a.ncand + (long long)pr * a.cap;
     int nm = 0;
     const float r = a.window;
+    // prefetch the first query's list
+    uint32_t key = lane < kTopK ? topk[lane] : kNoKey;
+    int cnt = ncand[0];
     for (int i1 = 0; i1 < n1; ++i1) {
-        const orb_keypoint k1 = K1[i1];
-        if (k1.octave > 0) continue;
-        float px = k1.x, py = k1.y;
-        if (a.prev_in) { px = a.prev_in[((long long)pr * a.cap + i1) * 2]; py = a.prev_in[((long long)pr * a.cap + i1) * 2 + 1]; }
-        CellRange cr;
-        if (!cell_range(px, py, r, a.g, cr)) continue;
-        const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32), q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
-        Best2 st{INT_MAX, INT_MAX, -1, 0, 0};
-        for (int base = 0; base < nl; base += kWave) {
-            const int j = base + lane;
-            int d = INT_MAX, fi = -1;
-            if (j < nl) {
-                const int v = list[j];
-                const int cell = v >> 16, gx = cell / kGridRows, gy = cell - gx * kGridRows;
-                fi = v & 0xffff;
-                if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1) {
-                    const orb_keypoint k2 = K2[fi];
-                    if (fabsf(k2.x - px) < r && fabsf(k2.y - py) < r) {
-                        const int dist = hamming32(q0, q1, D2 + (long long)fi * 32);
-                        if (!(mdist[fi] <= dist)) d = dist;
-                    }
+        const uint32_t cur_key = key;
+        const int cur_cnt = cnt;
+        if (i1 + 1 < n1) {
+            key = lane < kTopK ? topk[(long long)(i1 + 1) * kTopK + lane] : kNoKey;
+            cnt = ncand[i1 + 1];
+        }
+        if (cur_cnt <= 0) continue;          // not a query, or no candidate
+        int best = INT_MAX, best2 = INT_MAX, bi = -1;
+        bool ok = false;
+        {
+            const bool have = lane < kTopK && cur_key != kNoKey;
+            const int d = (int)(cur_key >> 16);
+            const int fi = have ? (list[cur_key & 0xffff] & 0xffff) : 0;
+            const bool live = have && !(mdist[fi] <= d);
+            uint64_t m = __ballot(live);
+            const int nlive = __popcll(m);
+            if (nlive >= 2 || cur_cnt <= kTopK) {
+                ok = true;
+                if (nlive >= 1) {
+                    const int l0 = __ffsll((long long)m) - 1;
+                    best = __shfl(d, l0, kWave);
+                    bi = __shfl(fi, l0, kWave);
+                    m &= m - 1;
+                    if (m) best2 = __shfl(d, __ffsll((long long)m) - 1, kWave);
                 }
             }
-            merge_chunk(st, d, fi, 0);
         }
-        if (st.best <= kThLow && (float)st.best < (float)st.best2 * a.ratio) {
-            const int b2 = st.idx;
-            if (m21[b2] >= 0) {
-                if (lane == 0) m12[m21[b2]] = -1;
+        if (!ok) {   // exact fallback: full candidate scan under the current state
+            const orb_keypoint k1 = K1[i1];
+            float px, py;
+            query_pos(a, pr, i1, k1, px, py);
+            CellRange cr;
+            cell_range(px, py, r, a.g, cr);
+            const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32);
+            const uint4 q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+            Best2 st{INT_MAX, INT_MAX, -1, 0, 0};
+            for (int base = 0; base < nl; base += kWave) {
+                const int j = base + lane;
+                int d = INT_MAX, fi = -1;
+                if (j < nl) {
+                    d = cand_dist(list, j, cr, px, py, r, K2, D2, q0, q1);
+                    fi = list[j] & 0xffff;
+                    if (d != INT_MAX && mdist[fi] <= d) d = INT_MAX;
+                }
+                merge_chunk(st, d, fi, 0);
+            }
+            best = st.best; best2 = st.best2; bi = st.idx;
+        }
+        if (best <= kThLow && (float)best < (float)best2 * a.ratio) {
+            if (m21[bi] >= 0) {
+                if (lane == 0) m12[m21[bi]] = -1;
                 --nm;
             }
             if (lane == 0) {
-                m12[i1] = b2;
-                m21[b2] = i1;
-                mdist[b2] = st.best;
+                m12[i1] = bi;
+                m21[bi] = i1;
+                mdist[bi] = best;
             }
             ++nm;
             if (a.check_ori) {
-                const int bn = rot_bin(k1.angle, K2[b2].angle);
+                const int bn = rot_bin(K1[i1].angle, K2[bi].angle);
                 if (lane == 0) { hist[bn]++; bin1[i1] = (int8_t)bn; }
             }
+            wave_sync_m();
         }
-        __syncthreads();
     }
+    __syncthreads();
     if (a.check_ori) {
         int i1x, i2x, i3x;
         three_maxima(hist, i1x, i2x, i3x);
@@ -286,10 +423,11 @@ __global__ __launch_bounds__(64) void k_sfi(SfiArgs a) {
         }
         nm -= wave_sum(drop);
     }
+    __syncthreads();
     if (a.prev_out) {
         for (int i = lane; i < n1; i += kWave) {
-            float px = K1[i].x, py = K1[i].y;
-            if (a.prev_in) { px = a.prev_in[((long long)pr * a.cap + i) * 2]; py = a.prev_in[((long long)pr * a.cap + i) * 2 + 1]; }
+            float px, py;
+            query_pos(a, pr, i, K1[i], px, py);
             const int m = m12[i];
             if (m >= 0) { px = K2[m].x; py = K2[m].y; }
             a.prev_out[((long long)pr * a.cap + i) * 2] = px;
@@ -297,6 +435,13 @@ __global__ __launch_bounds__(64) void k_sfi(SfiArgs a) {
         }
     }
     if (lane == 0) a.nmatches[pr] = nm;
+}
+
+static void launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
+    const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
+    hipLaunchKernelGGL(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
+    const size_t lds_res = (size_t)a.cap * 12 + 128 + a.cap + 16;
+    hipLaunchKernelGGL(k_sfi_resolve, dim3(npairs), dim3(64), lds_res, st, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -640,9 +785,11 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     const int cap = std::max(1, std::max(f1->n, f2->n));
     DBuf<orb_keypoint> kps; DBuf<uint8_t> desc; DBuf<int> n; DBuf<uint32_t> sorted; DBuf<int> count;
     DBuf<int> pf; DBuf<float> prev_in, prev_out; DBuf<int32_t> m; DBuf<int32_t> nm;
+    DBuf<uint32_t> topk; DBuf<int> ncand;
     int rc;
     if ((rc = kps.alloc(2 * cap)) || (rc = desc.alloc((size_t)2 * cap * 32)) || (rc = sorted.alloc(2 * cap)) ||
-        (rc = count.alloc(2)) || (rc = m.alloc(cap)) || (rc = nm.alloc(1)) || (rc = prev_out.alloc((size_t)2 * cap)))
+        (rc = count.alloc(2)) || (rc = m.alloc(cap)) || (rc = nm.alloc(1)) || (rc = prev_out.alloc((size_t)2 * cap)) ||
+        (rc = topk.alloc((size_t)cap * kTopK)) || (rc = ncand.alloc(cap)))
         return rc;
     const int ns[2] = {f1->n, f2->n};
     const int pfs[2] = {0, 1};
@@ -665,9 +812,8 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     a.kps = kps.p; a.desc = desc.p; a.n = n.p; a.cap = cap; a.gsorted = sorted.p; a.gcount = count.p;
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = prev_in.p; a.prev_out = prev_out.p;
     a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
-    a.matches = m.p; a.nmatches = nm.p;
-    const size_t lds = (size_t)cap * 12 + 128 + cap + 16;
-    hipLaunchKernelGGL(k_sfi, dim3(1), dim3(64), lds, 0, a);
+    a.matches = m.p; a.nmatches = nm.p; a.topk = topk.p; a.ncand = ncand.p;
+    launch_sfi(a, 1, 0);
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
     ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
@@ -686,11 +832,13 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     (void)max_x; (void)max_y;
     if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
     hipStream_t st = (hipStream_t)stream;
-    static thread_local DBuf<uint32_t> sorted;
-    static thread_local DBuf<int> count, pf;
+    static thread_local DBuf<uint32_t> sorted, topk;
+    static thread_local DBuf<int> count, pf, ncand;
     static thread_local int pf_frames = 0;
     int rc;
-    if ((rc = sorted.alloc((size_t)nframes * cap)) || (rc = count.alloc(nframes))) return rc;
+    if ((rc = sorted.alloc((size_t)nframes * cap)) || (rc = count.alloc(nframes)) ||
+        (rc = topk.alloc((size_t)nframes * cap * kTopK)) || (rc = ncand.alloc((size_t)nframes * cap)))
+        return rc;
     if (pf_frames < nframes) {
         std::vector<int> idx(nframes);
         for (int i = 0; i < nframes; ++i) idx[i] = i;
@@ -706,9 +854,8 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     a.kps = d_kps; a.desc = d_desc; a.n = d_n; a.cap = cap; a.gsorted = sorted.p; a.gcount = count.p;
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = nullptr; a.prev_out = nullptr;
     a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
-    a.matches = d_matches; a.nmatches = d_nmatches;
-    const size_t lds = (size_t)cap * 12 + 128 + cap + 16;
-    hipLaunchKernelGGL(k_sfi, dim3(nframes - 1), dim3(64), lds, st, a);
+    a.matches = d_matches; a.nmatches = d_nmatches; a.topk = topk.p; a.ncand = ncand.p;
+    launch_sfi(a, nframes - 1, st);
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }

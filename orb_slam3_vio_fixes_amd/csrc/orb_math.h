@@ -188,32 +188,30 @@ ORB_HD void insertion_sort_(SortRec* first, SortRec* last) {
         }
     }
 }
-// Iterative form of __introsort_loop: the recursion (right part first, then
-// loop on the left part) is replayed with an explicit stack in the same order.
-ORB_HD void std_sort(SortRec* first, int n) {
+// Iterative form of __introsort_loop.  The recursion (right part, then loop
+// on the left part) only ever touches disjoint ranges, so any processing order
+// of the pending ranges yields the same permutation; each range keeps the
+// depth budget the recursion would give it.  `stk` holds >= 2*lg(n)+4 frames
+// (the device passes an LDS buffer so nothing spills to scratch).
+struct SortFrame { int f, l, depth; };
+
+ORB_HD void std_sort(SortRec* first, int n, SortFrame* stk) {
     if (n <= 1) return;
-    struct Frame { SortRec* f; SortRec* l; int depth; };
-    Frame stk[64];
     int sp = 0;
-    stk[sp++] = {first, first + n, ilg(n) * 2};
+    stk[sp++] = {0, n, ilg(n) * 2};
     while (sp) {
-        Frame fr = stk[--sp];
-        SortRec* f = fr.f;
-        SortRec* l = fr.l;
+        const SortFrame fr = stk[--sp];
+        SortRec* f = first + fr.f;
+        SortRec* l = first + fr.l;
         int depth = fr.depth;
-        while (l - f > 16) {
-            if (depth == 0) { heap_sort_(f, (int)(l - f)); break; }
-            --depth;
-            SortRec* mid = f + (l - f) / 2;
-            median_to_first_(f, f + 1, mid, l - 1);
-            SortRec* cut = unguarded_partition_(f + 1, l, f);
-            // recursion on [cut, l) happens before the loop continues on [f, cut);
-            // an explicit stack must finish [cut, l) first: push [f,cut) then [cut,l).
-            stk[sp++] = {f, cut, depth};
-            stk[sp++] = {cut, l, depth};
-            l = f;   // consumed: both halves are on the stack
-            break;
-        }
+        if (l - f <= 16) continue;
+        if (depth == 0) { heap_sort_(f, (int)(l - f)); continue; }
+        --depth;
+        SortRec* mid = f + (l - f) / 2;
+        median_to_first_(f, f + 1, mid, l - 1);
+        SortRec* cut = unguarded_partition_(f + 1, l, f);
+        stk[sp++] = {fr.f, (int)(cut - first), depth};
+        stk[sp++] = {(int)(cut - first), fr.l, depth};
     }
     // __final_insertion_sort
     if (n > 16) {

@@ -69,7 +69,8 @@ int sort_mismatches(int trials, int maxn, unsigned seed) {
             if (a.first > b.first) return false;
             return a.second->x0 < b.second->x0;
         });
-        orbmi::std_sort(port.data(), n);
+        orbmi::SortFrame stk[80];
+        orbmi::std_sort(port.data(), n, stk);
         for (int i = 0; i < n; ++i)
             if (ref[i].second != &nodes[port[i].pos]) { ++bad; break; }
     }

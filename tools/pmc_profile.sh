@@ -1,0 +1,18 @@
+#!/bin/bash
+# Collect rocprofv3 PMC passes on a short bench run (one counter group per pass,
+# kernel-trace only, never combined with sys/runtime traces).
+# usage: tools/pmc_profile.sh <outdir> [bench args...]
+set -o pipefail
+OUT=${1:-gpurun_out/pmc}; shift
+ARGS=${@:---steps 3 --warmup 1 --cpu-sample 0 --no-profile}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
+i=0
+for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $grp --kernel-trace --output-format csv -d "$OUT/p$i" -o run -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1 || { echo "pass $i failed rc=$?"; tail -5 "$OUT/p$i.log"; exit 1; }
+done
+echo done
