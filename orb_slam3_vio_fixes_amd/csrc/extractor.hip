@@ -66,6 +66,7 @@ struct Plan {
     int ncells = 0, slot_total = 0, out_total = 0;
     int roi_max = 0, roi_dwords = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     std::vector<int> xmax;           // per level
+    std::vector<std::vector<int>> ytab_host;   // per level: source row of each output row
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     // device
     uint8_t *d_pyr = nullptr, *d_in = nullptr;
@@ -170,6 +171,7 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     std::vector<int2> tab;
     P.xmax.assign(L, 0);
     P.tab_off.assign(L, 0);
+    P.ytab_host.assign(L, {});
     long long poff = 0;
     int cellsum = 0, slotsum = 0, outsum = 0;
     for (int l = 0; l < L; ++l) {
@@ -212,6 +214,7 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
                 fy -= sy;
                 const int b0 = sat_short((1.f - fy) * 2048.f), b1 = sat_short(fy * 2048.f);
                 tab.push_back(make_int2(sy, (b0 & 0xffff) | (b1 << 16)));
+                P.ytab_host[l].push_back(sy);
             }
             P.xmax[l] = xmax;
         }

@@ -61,7 +61,8 @@ __device__ __forceinline__ void wave_sync_m() {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_grid(const orb_keypoint* __restrict__ kps, const int* __restrict__ n,
                                               int cap, GridParams g, uint32_t* __restrict__ sorted,
-                                              int* __restrict__ count, int sort_cap) {
+                                              int* __restrict__ count, int sort_cap,
+                                              uint32_t* __restrict__ l0sorted, int* __restrict__ l0count) {
     extern __shared__ __attribute__((aligned(16))) uint32_t keys[];
     const int f = blockIdx.x, tid = threadIdx.x;
     const int nf = min(n[f], cap);
@@ -96,6 +97,21 @@ __global__ __launch_bounds__(256) void k_grid(const orb_keypoint* __restrict__ k
     if (lane_id() == 0) wsum[wave_id()] = valid;
     __syncthreads();
     if (tid == 0) count[f] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    // the octave-0 subsequence (SearchForInitialization queries level 0 only, ORBmatcher.cc:664-668)
+    if (l0sorted && wave_id() == 0) {
+        const int tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        int nl = 0;
+        for (int base = 0; base < tot; base += kWave) {
+            const int i = base + lane_id();
+            bool keep = false;
+            uint32_t v = 0;
+            if (i < tot) { v = keys[i]; keep = kps[(long long)f * cap + (v & 0xffff)].octave == 0; }
+            const uint64_t m = __ballot(keep);
+            if (keep) l0sorted[(long long)f * cap + nl + mask_rank(m)] = v;
+            nl += __popcll(m);
+        }
+        if (lane_id() == 0) l0count[f] = nl;
+    }
 }
 
 // GetFeaturesInArea cell range (Frame.cc:661-689); false = empty.
@@ -200,7 +216,7 @@ struct SfiArgs {
     const uint8_t* desc;
     const int* n;
     int cap;
-    const uint32_t* gsorted;
+    const uint32_t* gsorted;   // per frame: level-0 features in grid order (k_grid l0 list)
     const int* gcount;
     const int* pair_f1;      // per pair: frame index of F1 / F2
     const int* pair_f2;
@@ -216,21 +232,11 @@ struct SfiArgs {
 };
 
 // F2's level-0 features in grid order (GetFeaturesInArea(.., level1, level1)
-// with level1 = 0 keeps octave 0 only, :668) -> LDS, returns the count.
-__device__ int level0_list(const SfiArgs& a, int f2, int* list) {
-    const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
+// with level1 = 0 keeps octave 0 only, :668), prepared by k_grid -> LDS.
+__device__ int level0_list(const SfiArgs& a, int f2, int* list, int tid, int nthreads) {
     const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
-    const int gn = a.gcount[f2];
-    int nl = 0;
-    for (int base = 0; base < gn; base += kWave) {
-        const int i = base + lane_id();
-        uint32_t v = 0;
-        bool keep = false;
-        if (i < gn) { v = gs[i]; keep = K2[v & 0xffff].octave == 0; }
-        const uint64_t m = __ballot(keep);
-        if (keep) list[nl + mask_rank(m)] = (int)v;
-        nl += __popcll(m);
-    }
+    const int nl = a.gcount[f2];
+    for (int i = tid; i < nl; i += nthreads) list[i] = (int)gs[i];
     return nl;
 }
 
@@ -263,13 +269,23 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
     const int pr = blockIdx.x, lane = lane_id(), wv = wave_id();
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
     const int n1 = min(a.n[f1], a.cap);
-    __shared__ int s_nl;
-    if (wv == 0) {
-        const int nl = level0_list(a, f2, list);
-        if (lane == 0) s_nl = nl;
+    __shared__ int s_any;
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    {   // does this block hold any level-0 query?
+        const int i1 = blockIdx.y * 16 + (int)threadIdx.x;
+        if (threadIdx.x < 16 && i1 < n1 && a.kps[(long long)f1 * a.cap + i1].octave == 0) s_any = 1;
     }
     __syncthreads();
-    const int nl = s_nl;
+    if (!s_any) {
+        for (int t = threadIdx.x; t < 16; t += blockDim.x) {
+            const int i1 = blockIdx.y * 16 + t;
+            if (i1 < n1) a.ncand[(long long)pr * a.cap + i1] = -1;
+        }
+        return;
+    }
+    const int nl = level0_list(a, f2, list, threadIdx.x, blockDim.x);
+    __syncthreads();
     uint32_t* mypool = pool + wv * a.cap;
     const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
     const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
@@ -330,28 +346,35 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
     int* mdist = list + a.cap;                // cap
     int* m21 = mdist + a.cap;                 // cap
     int* hist = m21 + a.cap;                  // 32
-    int8_t* bin1 = (int8_t*)(hist + 32);      // cap
+    int* qlist = hist + 32;                   // cap: query indices i1 (level 0, >= 1 candidate)
+    int* qcnt = qlist + a.cap;                // cap: candidate counts
+    uint32_t* qtop = (uint32_t*)(qcnt + a.cap);   // cap * kTopK
+    int8_t* bin1 = (int8_t*)(qtop + (size_t)a.cap * kTopK);   // cap
     int32_t* m12 = a.matches + (long long)pr * a.cap;
-    const int nl = level0_list(a, f2, list);
+    const int nl = level0_list(a, f2, list, lane, kWave);
     for (int i = lane; i < n2; i += kWave) { mdist[i] = INT_MAX; m21[i] = -1; }
     for (int i = lane; i < 32; i += kWave) hist[i] = 0;
     for (int i = lane; i < n1; i += kWave) { m12[i] = -1; bin1[i] = -1; }
-    __syncthreads();
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
     const int* ncand = a.ncand + (long long)pr * a.cap;
+    // compact the queries in F1 order and stage their top-K lists in LDS
+    int nq = 0;
+    for (int base = 0; base < n1; base += kWave) {
+        const int i = base + lane;
+        const int c = i < n1 ? ncand[i] : -1;
+        const uint64_t m = __ballot(c > 0);
+        if (c > 0) { qlist[nq + mask_rank(m)] = i; qcnt[nq + mask_rank(m)] = c; }
+        nq += __popcll(m);
+    }
+    __syncthreads();
+    for (int e = lane; e < nq * kTopK; e += kWave) qtop[e] = topk[(long long)qlist[e / kTopK] * kTopK + e % kTopK];
+    __syncthreads();
     int nm = 0;
     const float r = a.window;
-    // prefetch the first query's list
-    uint32_t key = lane < kTopK ? topk[lane] : kNoKey;
-    int cnt = ncand[0];
-    for (int i1 = 0; i1 < n1; ++i1) {
-        const uint32_t cur_key = key;
-        const int cur_cnt = cnt;
-        if (i1 + 1 < n1) {
-            key = lane < kTopK ? topk[(long long)(i1 + 1) * kTopK + lane] : kNoKey;
-            cnt = ncand[i1 + 1];
-        }
-        if (cur_cnt <= 0) continue;          // not a query, or no candidate
+    for (int j = 0; j < nq; ++j) {
+        const int i1 = qlist[j];
+        const int cur_cnt = qcnt[j];
+        const uint32_t cur_key = lane < kTopK ? qtop[j * kTopK + lane] : kNoKey;
         int best = INT_MAX, best2 = INT_MAX, bi = -1;
         bool ok = false;
         {
@@ -382,11 +405,11 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
             const uint4 q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
             Best2 st{INT_MAX, INT_MAX, -1, 0, 0};
             for (int base = 0; base < nl; base += kWave) {
-                const int j = base + lane;
+                const int jj = base + lane;
                 int d = INT_MAX, fi = -1;
-                if (j < nl) {
-                    d = cand_dist(list, j, cr, px, py, r, K2, D2, q0, q1);
-                    fi = list[j] & 0xffff;
+                if (jj < nl) {
+                    d = cand_dist(list, jj, cr, px, py, r, K2, D2, q0, q1);
+                    fi = list[jj] & 0xffff;
                     if (d != INT_MAX && mdist[fi] <= d) d = INT_MAX;
                 }
                 merge_chunk(st, d, fi, 0);
@@ -440,7 +463,7 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
 static void launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
     hipLaunchKernelGGL(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
-    const size_t lds_res = (size_t)a.cap * 12 + 128 + a.cap + 16;
+    const size_t lds_res = (size_t)a.cap * (20 + 4 * kTopK + 1) + 128 + 16;
     hipLaunchKernelGGL(k_sfi_resolve, dim3(npairs), dim3(64), lds_res, st, a);
 }
 
@@ -751,7 +774,7 @@ struct DevFrame {
             if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1))) return rc;
             const int sc = pow2_at_least(nn);
             hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
-                               grid_params(f), sorted.p, count.p, sc);
+                               grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
         }
         return ORB_OK;
     }
@@ -807,9 +830,12 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     }
     const GridParams g = grid_params(f2);
     const int sc = pow2_at_least(cap);
-    hipLaunchKernelGGL(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p, count.p, sc);
+    DBuf<uint32_t> l0s; DBuf<int> l0c;
+    if ((rc = l0s.alloc((size_t)2 * cap)) || (rc = l0c.alloc(2))) return rc;
+    hipLaunchKernelGGL(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p, count.p, sc,
+                       l0s.p, l0c.p);
     SfiArgs a;
-    a.kps = kps.p; a.desc = desc.p; a.n = n.p; a.cap = cap; a.gsorted = sorted.p; a.gcount = count.p;
+    a.kps = kps.p; a.desc = desc.p; a.n = n.p; a.cap = cap; a.gsorted = l0s.p; a.gcount = l0c.p;
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = prev_in.p; a.prev_out = prev_out.p;
     a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
     a.matches = m.p; a.nmatches = nm.p; a.topk = topk.p; a.ncand = ncand.p;
@@ -832,12 +858,13 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     (void)max_x; (void)max_y;
     if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
     hipStream_t st = (hipStream_t)stream;
-    static thread_local DBuf<uint32_t> sorted, topk;
-    static thread_local DBuf<int> count, pf, ncand;
+    static thread_local DBuf<uint32_t> sorted, topk, l0s;
+    static thread_local DBuf<int> count, pf, ncand, l0c;
     static thread_local int pf_frames = 0;
     int rc;
     if ((rc = sorted.alloc((size_t)nframes * cap)) || (rc = count.alloc(nframes)) ||
-        (rc = topk.alloc((size_t)nframes * cap * kTopK)) || (rc = ncand.alloc((size_t)nframes * cap)))
+        (rc = topk.alloc((size_t)nframes * cap * kTopK)) || (rc = ncand.alloc((size_t)nframes * cap)) ||
+        (rc = l0s.alloc((size_t)nframes * cap)) || (rc = l0c.alloc(nframes)))
         return rc;
     if (pf_frames < nframes) {
         std::vector<int> idx(nframes);
@@ -849,9 +876,9 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     const GridParams g{min_x, min_y, grid_inv_w, grid_inv_h};
     const int sc = pow2_at_least(cap);
     hipLaunchKernelGGL(k_grid, dim3(nframes), dim3(256), sc * sizeof(uint32_t), st, d_kps, d_n, cap, g, sorted.p,
-                       count.p, sc);
+                       count.p, sc, l0s.p, l0c.p);
     SfiArgs a;
-    a.kps = d_kps; a.desc = d_desc; a.n = d_n; a.cap = cap; a.gsorted = sorted.p; a.gcount = count.p;
+    a.kps = d_kps; a.desc = d_desc; a.n = d_n; a.cap = cap; a.gsorted = l0s.p; a.gcount = l0c.p;
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = nullptr; a.prev_out = nullptr;
     a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
     a.matches = d_matches; a.nmatches = d_nmatches; a.topk = topk.p; a.ncand = ncand.p;
