@@ -175,6 +175,33 @@ int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kf_fv,
                        const orbm_featvec* f_fv, float nnratio, int check_ori,
                        int32_t* match_f);
 
+/* A keyframe map resident in HBM for map-wide SearchByBoW (relocalization:
+ * Tracking.cc:3641-3648 runs one SearchByBoW(KF_i, F) per candidate).  All
+ * pointers are DEVICE pointers.  Keyframe i owns features
+ * [kp_off[i], kp_off[i+1]) of kps/desc/valid and FeatureVector nodes
+ * [fv_node_off[i], fv_node_off[i+1]) of fv_node; its CSR offsets are the
+ * (nnodes_i + 1) entries of fv_off starting at fv_node_off[i] + i, relative to
+ * fv_idx + fv_idx_off[i]. */
+typedef struct orbm_kf_map_device {
+    int32_t nkf;
+    const orb_keypoint* kps;
+    const uint8_t* desc;
+    const uint8_t* valid;        /* MapPoint != NULL && !isBad() */
+    const int64_t* kp_off;       /* nkf + 1 */
+    const uint32_t* fv_node;
+    const int32_t* fv_off;
+    const uint32_t* fv_idx;
+    const int64_t* fv_node_off;  /* nkf + 1 */
+    const int64_t* fv_idx_off;   /* nkf */
+} orbm_kf_map_device;
+
+/* SearchByBoW(KF_i, F) for every keyframe of the map against one frame; f and
+ * ffv hold DEVICE pointers.  d_match: nkf x f->n (KF feature index or -1),
+ * d_nmatches: nkf.  Asynchronous on `stream`. */
+int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f,
+                                    const orbm_featvec* ffv, float nnratio, int check_ori,
+                                    int32_t* d_match, int32_t* d_nmatches, void* stream);
+
 /* Map points projected into F (the fields ORBmatcher reads from MapPoint,
  * MapPoint.h mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos, mbTrackInView,
  * isBad(), GetDescriptor(), Observations()). */

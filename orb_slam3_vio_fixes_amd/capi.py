@@ -16,7 +16,7 @@ EXPORTS = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_max_keypoints", "orbx_extract", "orbx_get_level",
     "orbx_extract_batch_device", "orbx_debug_stage", "orbm_descriptor_distance", "orbm_search_for_initialization",
     "orbm_search_for_initialization_batch_device", "orbm_search_by_bow", "orbm_search_by_projection_mps",
-    "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile",
+    "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device",
 ]
 
 _lib = None
@@ -45,6 +45,7 @@ def load(path: Path | str = LIB_PATH):
     L.orbv_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp, i32]
     L.orbx_set_profiling.argtypes = [vp, i32]
     L.orbx_get_profile.argtypes = [vp, vp, i32]
+    L.orbm_search_by_bow_batch_device.argtypes = [vp, vp, vp, f32, i32, vp, vp, vp]
     return L
 
 

@@ -474,15 +474,19 @@ static void launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
 // over the frame features of the node that are not yet matched.
 // ---------------------------------------------------------------------------
 struct BowArgs {
-    // keyframes (npairs): features, FeatureVector CSR, MapPoint validity
-    const orb_keypoint* kf_kps;  const long long* kf_kp_off;
-    const uint8_t* kf_desc;      // same offsets * 32
-    const uint8_t* kf_valid;     // same offsets
-    const uint32_t* kf_node;     const int* kf_off;   const uint32_t* kf_idx;
-    const long long* kf_fv_node_off;   // per pair: offset into kf_node / (kf_off - 1 more)
-    const int* kf_fv_nnodes;
-    const long long* kf_fv_off_off;    // per pair: offset into kf_off
-    const long long* kf_fv_idx_off;    // per pair: offset into kf_idx
+    // keyframes (one per pair), concatenated: kf i owns features
+    // [kp_off[i], kp_off[i+1]) and FeatureVector nodes [node_off[i], node_off[i+1]);
+    // its CSR offsets start at fv_off[node_off[i] + i] (nnodes_i + 1 entries, relative
+    // to idx_off[i]).
+    const orb_keypoint* kf_kps;
+    const uint8_t* kf_desc;
+    const uint8_t* kf_valid;
+    const long long* kp_off;
+    const uint32_t* kf_node;
+    const int* kf_off;
+    const uint32_t* kf_idx;
+    const long long* node_off;
+    const long long* idx_off;
     // frame (shared by all pairs)
     const orb_keypoint* f_kps;  const uint8_t* f_desc;  int f_n;
     const uint32_t* f_node;  const int* f_off;  const uint32_t* f_idx;  int f_nnodes;
@@ -495,20 +499,21 @@ struct BowArgs {
 __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id();
-    int* hist = lds;                  // 32
-    int8_t* fbin = (int8_t*)(lds + 32);   // f_n: bin of the match recorded at F feature, or -1
-    int32_t* match = a.match + (long long)pr * a.f_n;
+    int* hist = lds;                          // 32
+    int* match = lds + 32;                    // f_n: KF feature matched to each F feature (vpMapPointMatches)
+    int8_t* fbin = (int8_t*)(match + a.f_n);  // f_n: rotation bin recorded for F feature, or -1
     for (int i = lane; i < a.f_n; i += kWave) { match[i] = -1; fbin[i] = -1; }
     for (int i = lane; i < 32; i += kWave) hist[i] = 0;
     __syncthreads();
-    const long long kpo = a.kf_kp_off[pr];
+    const long long kpo = a.kp_off[pr];
     const orb_keypoint* KK = a.kf_kps + kpo;
     const uint8_t* KD = a.kf_desc + kpo * 32;
     const uint8_t* KV = a.kf_valid + kpo;
-    const uint32_t* kn = a.kf_node + a.kf_fv_node_off[pr];
-    const int* ko = a.kf_off + a.kf_fv_off_off[pr];
-    const uint32_t* ki = a.kf_idx + a.kf_fv_idx_off[pr];
-    const int knn = a.kf_fv_nnodes[pr];
+    const long long no = a.node_off[pr];
+    const uint32_t* kn = a.kf_node + no;
+    const int* ko = a.kf_off + no + pr;
+    const uint32_t* ki = a.kf_idx + a.idx_off[pr];
+    const int knn = (int)(a.node_off[pr + 1] - no);
     int nm = 0;
     int ia = 0, ib = 0;
     while (ia < knn && ib < a.f_nnodes) {
@@ -537,8 +542,8 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
                         if (lane == 0) { hist[bn]++; fbin[st.idx] = (int8_t)bn; }
                     }
                     ++nm;
+                    wave_sync_m();
                 }
-                __syncthreads();
             }
             ++ia; ++ib;
         } else if (na < nb) {
@@ -547,6 +552,7 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
             while (ib < a.f_nnodes && a.f_node[ib] < na) ++ib;
         }
     }
+    __syncthreads();
     if (a.check_ori) {
         int i1, i2, i3;
         three_maxima(hist, i1, i2, i3);
@@ -559,7 +565,17 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
         }
         nm -= wave_sum(drop);
     }
+    __syncthreads();
+    int32_t* out = a.match + (long long)pr * a.f_n;
+    for (int i = lane; i < a.f_n; i += kWave) out[i] = match[i];
     if (lane == 0) a.nmatches[pr] = nm;
+}
+
+static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
+    const size_t lds = 128 + (size_t)a.f_n * 5 + 16;
+    if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_bow, dim3(npairs), dim3(64), lds, st, a);
+    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
 // ---------------------------------------------------------------------------
@@ -893,28 +909,40 @@ int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint
     if (device_ok()) return ORB_ERR_DEVICE;
     int rc;
     DBuf<orb_keypoint> kk, fk; DBuf<uint8_t> kd, fd, kvv; DBuf<uint32_t> kn, ki, fn, fi; DBuf<int> ko, fo;
-    DBuf<long long> z; DBuf<int> knn; DBuf<int32_t> m, nm;
-    const long long zeros[4] = {0, 0, 0, 0};
+    DBuf<long long> kpo, nodo, idxo; DBuf<int32_t> m, nm;
+    const long long kp_off[2] = {0, kf->n}, node_off[2] = {0, kfv->nnodes}, idx_off[1] = {0};
     if ((rc = kk.put(kf->kps, kf->n)) || (rc = kd.put(kf->desc, (size_t)kf->n * 32)) || (rc = kvv.put(kf_valid, kf->n)) ||
         (rc = kn.put(kfv->node_ids, kfv->nnodes)) || (rc = ko.put(kfv->offsets, kfv->nnodes + 1)) ||
         (rc = ki.put(kfv->idx, kfv->offsets[kfv->nnodes])) || (rc = fk.put(f->kps, f->n)) ||
         (rc = fd.put(f->desc, (size_t)f->n * 32)) || (rc = fn.put(ffv->node_ids, ffv->nnodes)) ||
         (rc = fo.put(ffv->offsets, ffv->nnodes + 1)) || (rc = fi.put(ffv->idx, ffv->offsets[ffv->nnodes])) ||
-        (rc = z.put(zeros, 4)) || (rc = knn.put(&kfv->nnodes, 1)) || (rc = m.alloc(std::max(1, f->n))) ||
-        (rc = nm.alloc(1)))
+        (rc = kpo.put(kp_off, 2)) || (rc = nodo.put(node_off, 2)) || (rc = idxo.put(idx_off, 1)) ||
+        (rc = m.alloc(std::max(1, f->n))) || (rc = nm.alloc(1)))
         return rc;
     BowArgs a;
-    a.kf_kps = kk.p; a.kf_kp_off = z.p; a.kf_desc = kd.p; a.kf_valid = kvv.p;
-    a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p;
-    a.kf_fv_node_off = z.p; a.kf_fv_nnodes = knn.p; a.kf_fv_off_off = z.p; a.kf_fv_idx_off = z.p;
+    a.kf_kps = kk.p; a.kf_desc = kd.p; a.kf_valid = kvv.p; a.kp_off = kpo.p;
+    a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
-    hipLaunchKernelGGL(k_bow, dim3(1), dim3(64), 128 + f->n + 16, 0, a);
-    ORB_CHECK(hipGetLastError());
+    if ((rc = launch_bow(a, 1, 0))) return rc;
     int32_t res = 0;
     ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
     if (f->n) ORB_CHECK(hipMemcpy(match_f, m.p, f->n * 4, hipMemcpyDeviceToHost));
     return res;
+}
+
+int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f, const orbm_featvec* ffv,
+                                    float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
+    if (!map || !f || !ffv || !d_match || !d_nmatches || map->nkf < 0) return ORB_ERR_PARAM;
+    if (map->nkf == 0) return ORB_OK;
+    BowArgs a;
+    a.kf_kps = map->kps; a.kf_desc = map->desc; a.kf_valid = map->valid; a.kp_off = (const long long*)map->kp_off;
+    a.kf_node = map->fv_node; a.kf_off = map->fv_off; a.kf_idx = map->fv_idx;
+    a.node_off = (const long long*)map->fv_node_off; a.idx_off = (const long long*)map->fv_idx_off;
+    a.f_kps = f->kps; a.f_desc = f->desc; a.f_n = f->n; a.f_node = ffv->node_ids; a.f_off = ffv->offsets;
+    a.f_idx = ffv->idx; a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
+    a.match = d_match; a.nmatches = d_nmatches;
+    return launch_bow(a, map->nkf, (hipStream_t)stream);
 }
 
 static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* owner, const uint8_t* blocked) {

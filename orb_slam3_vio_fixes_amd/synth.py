@@ -104,37 +104,36 @@ def sequence(w: int, h: int, nframes: int, config: int = 2, start: int = 0, step
     return out
 
 
-def vocabulary(k: int = 10, levels: int = 6, seed: int = 5, max_nodes: int | None = None):
-    """Synthetic complete k-ary vocabulary of depth ``levels`` laid out breadth
-    first (orbv_vocab): node 0 = root, TF-IDF-like random leaf weights.
-    Children descriptors are perturbations of their parent so descents are
-    stable.  Returns a dict of numpy arrays."""
+def vocabulary(k: int = 10, levels: int = 6, seed: int = 5):
+    """Synthetic complete k-ary vocabulary of depth ``levels`` (the ORBvoc.txt
+    shape is k=10, L=6: 1,111,111 nodes) laid out breadth first (orbv_vocab):
+    node 0 = root, children of a node contiguous.  Each child descriptor is
+    its parent's with every bit flipped with probability 2^-min(4, level+1)
+    (AND of random bytes), so descents are stable; leaf weights are random
+    TF-IDF-like values.  Vectorised per level; returns a dict of arrays."""
     rng = np.random.default_rng(seed)
     counts = [k ** l for l in range(levels + 1)]
     nnodes = sum(counts)
-    if max_nodes is not None and nnodes > max_nodes:
-        raise ValueError("vocabulary too large")
-    desc = np.zeros((nnodes, 32), np.uint8)
+    desc = np.empty((nnodes, 32), np.uint8)
     first_child = np.zeros(nnodes, np.int32)
     nchild = np.zeros(nnodes, np.int32)
     word_id = np.full(nnodes, -1, np.int32)
     weight = np.zeros(nnodes, np.float64)
     desc[0] = rng.integers(0, 256, 32, dtype=np.uint8)
     start = 0
-    nxt = 1
     for l in range(levels):
-        for i in range(start, start + counts[l]):
-            first_child[i] = nxt
-            nchild[i] = k
-            flip_p = 0.35 / (l + 1)
-            for c in range(k):
-                bits = np.unpackbits(desc[i])
-                flips = rng.random(256) < flip_p
-                desc[nxt + c] = np.packbits(bits ^ flips.astype(np.uint8))
-            nxt += k
-        start += counts[l]
-    leaves = np.arange(start, nnodes)
-    word_id[leaves] = np.arange(len(leaves), dtype=np.int32)
-    weight[leaves] = rng.uniform(0.1, 5.0, len(leaves))
+        n = counts[l]
+        cstart = start + n
+        first_child[start:start + n] = cstart + np.arange(n, dtype=np.int32) * k
+        nchild[start:start + n] = k
+        par = np.repeat(desc[start:start + n], k, axis=0)
+        flips = rng.integers(0, 256, par.shape, dtype=np.uint8)
+        for _ in range(min(4, l + 1) - 1):
+            flips &= rng.integers(0, 256, par.shape, dtype=np.uint8)
+        desc[cstart:cstart + n * k] = par ^ flips
+        start = cstart
+    nleaf = counts[levels]
+    word_id[start:] = np.arange(nleaf, dtype=np.int32)
+    weight[start:] = rng.uniform(0.1, 5.0, nleaf)
     return dict(nnodes=nnodes, depth_levels=levels, first_child=first_child, nchild=nchild,
                 node_desc=desc, word_id=word_id, weight=weight)
