@@ -211,7 +211,8 @@ const int kBlurLegacy[7] = {18, 34, 49, 55, 49, 34, 18};
 
 // GaussianBlur(workingMat, workingMat, Size(7,7), 2, 2, BORDER_REFLECT_101) on a
 // clone() of the level (ORBextractor.cc:1132-1133): GaussianBlurFixedPoint,
-// horizontal ufixedpoint16 pass, vertical ufixedpoint32 pass, round to u8.
+// horizontal ufixedpoint16 pass, vertical ufixedpoint32 pass, round and
+// saturate to u8 (the legacy kernel sums to 257, so 255-regions overflow).
 void blur7(const Img& s, Img& d, const int* k) {
     d.alloc(s.w, s.h);
     std::vector<uint32_t> hbuf((size_t)s.w * s.h);
@@ -225,7 +226,7 @@ void blur7(const Img& s, Img& d, const int* k) {
         for (int x = 0; x < s.w; ++x) {
             uint32_t acc = 0;
             for (int t = 0; t < 7; ++t) acc += k[t] * hbuf[(size_t)refl101(y + t - 3, s.h) * s.w + x];
-            d.row(y)[x] = (uint8_t)((acc + 32768u) >> 16);
+            d.row(y)[x] = (uint8_t)std::min(255u, (acc + 32768u) >> 16);   // saturate_cast<uchar>
         }
 }
 

@@ -457,9 +457,9 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
     const int f = blockIdx.y;
-    uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 4);   // multiples of 16
-    uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max*2 bytes
-    uint16_t* cand = (uint16_t*)(sc + 2 * a.win_max);         // <= win_max entries
+    uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 3);   // multiples of 16
+    uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
+    uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_max entries
     uint64_t* kmask = (uint64_t*)(roi);                       // reused after scoring (ROI no longer needed)
     const int c_begin = (blockIdx.x * 4 + wv) * kCellsPerWave;
     const int c_end = min(c_begin + kCellsPerWave, a.ncells);
@@ -887,7 +887,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 // fixed-point separable kernel and evaluates the 256 tests on
 // it: the blurred level never goes to HBM.  Lane l evaluates tests 4l..4l+3.
 // ---------------------------------------------------------------------------
-constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 44;   // hbT pitch: 88 B rows, 8-B aligned
+constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 40;   // hb pitch: 80 B rows (38 used), 16-B aligned
 
 struct DescArgs {
     const uint8_t* in;
@@ -914,50 +914,55 @@ __device__ __forceinline__ void wave_sync() {
 
 __device__ __forceinline__ int refl101(int p, int n) { return p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p); }
 
-// Stage the 43 x 43 raw patch whose top-left level pixel is (x0, y0) into
-// `raw` (row pitch 48); returns the byte shift of column 0 inside a row.
-// Interior patches move as 12 aligned dwords per row, all loads in flight at
-// once; patches touching the level border fall back to reflected byte loads.
-__device__ __forceinline__ int stage_patch(const uint8_t* img, int pitch, int w, int h, int x0, int y0,
-                                           uint8_t* raw) {
-    const int lane = lane_id();
-    const int base = x0 & ~3;
-    if (y0 >= 0 && y0 + kRaw <= h && x0 >= 0 && base + kRawP <= w) {
-        constexpr int kDw = kRawP / 4, kN = kRaw * kDw;   // 516 dwords
-        uint32_t v[(kN + kWave - 1) / kWave];
+// The 43 x 43 raw patch whose top-left level pixel is (x0, y0), row pitch 48 in
+// LDS.  Interior patches move as 12 aligned dwords per row: patch_issue puts
+// all 516 dword loads of one patch in flight into registers (the caller does
+// this one keypoint ahead), patch_land writes them to LDS.  Patches touching
+// the level border take reflected byte loads (patch_border).
+constexpr int kPDw = kRawP / 4, kPN = kRaw * kPDw, kPV = (kPN + kWave - 1) / kWave;   // 12, 516, 9
+
+__device__ __forceinline__ bool patch_interior(int w, int h, int x0, int y0) {
+    return y0 >= 0 && y0 + kRaw <= h && x0 >= 0 && (x0 & ~3) + kRawP <= w;
+}
+
+__device__ __forceinline__ void patch_issue(const uint8_t* img, int pitch, int x0, int y0, uint32_t (&v)[kPV]) {
+    const int lane = lane_id(), base = x0 & ~3;
 #pragma unroll
-        for (int j = 0; j < (kN + kWave - 1) / kWave; ++j) {
-            const int i = lane + j * kWave;
-            if (i < kN) {
-                const int r = i / kDw, d = i - r * kDw;
-                v[j] = *(const uint32_t*)(img + (long long)(y0 + r) * pitch + base + 4 * d);
-            }
+    for (int j = 0; j < kPV; ++j) {
+        const int i = lane + j * kWave;
+        if (i < kPN) {
+            const int r = i / kPDw, d = i - r * kPDw;
+            v[j] = *(const uint32_t*)(img + (long long)(y0 + r) * pitch + base + 4 * d);
         }
-#pragma unroll
-        for (int j = 0; j < (kN + kWave - 1) / kWave; ++j) {
-            const int i = lane + j * kWave;
-            if (i < kN) ((uint32_t*)raw)[i] = v[j];
-        }
-        return x0 - base;
     }
-    for (int i = lane; i < kRaw * kRaw; i += kWave) {
+}
+
+__device__ __forceinline__ void patch_land(const uint32_t (&v)[kPV], uint8_t* raw) {
+    const int lane = lane_id();
+#pragma unroll
+    for (int j = 0; j < kPV; ++j) {
+        const int i = lane + j * kWave;
+        if (i < kPN) ((uint32_t*)raw)[i] = v[j];
+    }
+}
+
+__device__ __forceinline__ void patch_border(const uint8_t* img, int pitch, int w, int h, int x0, int y0,
+                                             uint8_t* raw) {
+    for (int i = lane_id(); i < kRaw * kRaw; i += kWave) {
         const int r = i / kRaw, c = i - r * kRaw;
         raw[r * kRawP + c] = img[(long long)refl101(y0 + r, h) * pitch + refl101(x0 + c, w)];
     }
-    return 0;
 }
 
-__global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
+__global__ __launch_bounds__(256) void k_describe(DescArgs a) {
     __shared__ int8_t pat[1024];
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
-    __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][kBl * kHbP];
-    __shared__ uint8_t bl_s[4][kBl * kBl];
+    __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][kRaw * kHbP];
     for (int i = threadIdx.x; i < 1024; i += 256) pat[i] = c_pattern[i];
     __syncthreads();
     const int l = blockIdx.x, f = blockIdx.y, lane = lane_id(), wv = wave_id();
     uint8_t* raw = raw_s[wv];
     uint16_t* hb = hb_s[wv];
-    uint8_t* bl = bl_s[wv];
     const LevelDev lv = a.lv[l];
     const int n = a.qt_n[f * a.L + l];
     const uint8_t* img;
@@ -967,11 +972,32 @@ __global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
     const uint32_t* keys = a.qt_key + (long long)f * a.out_total + lv.out_base;
     // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
     const uint32_t k0 = a.kern[0], k1 = a.kern[1], k2 = a.kern[2], k3 = a.kern[3];
-    for (int p = blockIdx.z * 4 + wv; p < n; p += gridDim.z * 4) {
-        const uint32_t key = keys[p];
+    const int pstep = gridDim.z * 4;
+    int p = blockIdx.z * 4 + wv;
+    uint32_t pv[kPV];
+    uint32_t key = p < n ? keys[p] : 0u;
+    if (p < n) {
+        const int x0 = (int)(key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((key >> 12) & 0xfff) + (kEdge - 3) - 21;
+        if (patch_interior(lv.w, lv.h, x0, y0)) patch_issue(img, pitch, x0, y0, pv);
+    }
+    for (; p < n; p += pstep) {
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
         // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
-        const int sh = stage_patch(img, pitch, lv.w, lv.h, cx - 21, cy - 21, raw);
+        int sh = 0;
+        if (patch_interior(lv.w, lv.h, cx - 21, cy - 21)) {
+            patch_land(pv, raw);
+            sh = (cx - 21) & 3;
+        } else {
+            patch_border(img, pitch, lv.w, lv.h, cx - 21, cy - 21, raw);
+        }
+        // prefetch the next keypoint's patch (in flight during this keypoint)
+        const int pn = p + pstep;
+        uint32_t knext = 0u;
+        if (pn < n) {
+            knext = keys[pn];
+            const int x0 = (int)(knext & 0xfff) + (kEdge - 3) - 21, y0 = (int)((knext >> 12) & 0xfff) + (kEdge - 3) - 21;
+            if (patch_interior(lv.w, lv.h, x0, y0)) patch_issue(img, pitch, x0, y0, pv);
+        }
         const uint8_t* R = raw + sh;
         wave_sync();
         // 2. IC_Angle on the unblurred disc (centre = R[21][21])
@@ -989,10 +1015,9 @@ __global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
                 }
             }
         }
-        // 3. horizontal pass (ufixedpoint16): lane r holds row r in registers
-        //    (3 x ds_read_b128 + v_alignbyte for the column shift) and writes
-        //    its 37 outputs transposed, hbT[c][r], so step 4 reads columns
-        //    as contiguous runs
+        // 3. horizontal pass (ufixedpoint16): lane r holds raw row r in registers
+        //    (3 x ds_read_b128 + v_alignbyte for the column shift) and writes its
+        //    37 outputs row-major as packed dwords
         if (lane < kRaw) {
             const uint4* rowp = (const uint4*)(raw + lane * kRawP);
             const uint4 q0 = rowp[0], q1 = rowp[1], q2 = rowp[2];
@@ -1000,40 +1025,35 @@ __global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
             uint32_t al[11];
 #pragma unroll
             for (int j = 0; j < 11; ++j) al[j] = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], (uint32_t)sh);
-            uint32_t px[kRaw];
+            uint32_t* orow = (uint32_t*)(hb + lane * kHbP);
+            // 4 outputs per step from the 10 bytes al[g] .. al[g+2] (short live ranges)
 #pragma unroll
-            for (int j = 0; j < kRaw; ++j) px[j] = (al[j >> 2] >> (8 * (j & 3))) & 0xffu;
+            for (int g = 0; g < (kBl + 3) / 4; ++g) {
+                uint32_t px[10];
 #pragma unroll
-            for (int c = 0; c < kBl; ++c)
-                hb[c * kHbP + lane] = (uint16_t)(k0 * (px[c] + px[c + 6]) + k1 * (px[c + 1] + px[c + 5]) +
-                                                 k2 * (px[c + 2] + px[c + 4]) + k3 * px[c + 3]);
+                for (int j = 0; j < 10; ++j) {
+                    const int b = 4 * g + j;
+                    px[j] = b < kRaw ? (al[b >> 2] >> (8 * (b & 3))) & 0xffu : 0u;
+                }
+                uint32_t h[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    h[k] = k0 * (px[k] + px[k + 6]) + k1 * (px[k + 1] + px[k + 5]) + k2 * (px[k + 2] + px[k + 4]) +
+                           k3 * px[k + 3];
+                orow[2 * g] = (h[0] & 0xffffu) | (h[1] << 16);
+                if (2 * g + 1 < (kBl + 1) / 2) orow[2 * g + 1] = (h[2] & 0xffffu) | (h[3] << 16);
+            }
         }
         m10 = wave_sum(m10);
         m01 = wave_sum(m01);
-        wave_sync();
-        // 4. vertical pass (ufixedpoint32) + rounding: lane c holds column c
-        //    (11 x ds_read_b64 of hbT[c][0..43])
-        if (lane < kBl) {
-            const uint2* colp = (const uint2*)(hb + lane * kHbP);
-            uint32_t hv[44];
-#pragma unroll
-            for (int j = 0; j < 11; ++j) {
-                const uint2 v = colp[j];
-                hv[4 * j] = v.x & 0xffffu; hv[4 * j + 1] = v.x >> 16;
-                hv[4 * j + 2] = v.y & 0xffffu; hv[4 * j + 3] = v.y >> 16;
-            }
-#pragma unroll
-            for (int r = 0; r < kBl; ++r)
-                bl[r * kBl + lane] = (uint8_t)((k0 * (hv[r] + hv[r + 6]) + k1 * (hv[r + 1] + hv[r + 5]) +
-                                                k2 * (hv[r + 2] + hv[r + 4]) + k3 * hv[r + 3] + 32768u) >> 16);
-        }
         const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
         const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
         float sb, ca;
         glibc_sincosf(ang, &sb, &ca);
         wave_sync();
-        // 5. rBRIEF tests on the blurred patch (centre = bl[18][18])
-        const uint8_t* bc = bl + 18 * kBl + 18;
+        // 4. rBRIEF tests: the vertical pass (ufixedpoint32 + rounding) evaluated
+        //    only at the 512 sample points, hb rows R..R+6 at blurred column C,
+        //    blurred centre (18, 18)
         int nib = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1050,7 +1070,10 @@ __global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
                     r = cv_round(x * sb + y * ca);
                     c = cv_round(x * ca - y * sb);
                 }
-                val[e] = bc[r * kBl + c];
+                const uint16_t* col = hb + (18 + r) * kHbP + 18 + c;
+                const uint32_t acc = k0 * ((uint32_t)col[0] + col[6 * kHbP]) + k1 * ((uint32_t)col[kHbP] + col[5 * kHbP]) +
+                                     k2 * ((uint32_t)col[2 * kHbP] + col[4 * kHbP]) + k3 * (uint32_t)col[3 * kHbP];
+                val[e] = (int)min(255u, (acc + 32768u) >> 16);   // saturate_cast<uchar>
             }
             nib |= (val[0] < val[1]) << q;
         }
@@ -1058,6 +1081,7 @@ __global__ __launch_bounds__(256, 4) void k_describe(DescArgs a) {
         uint8_t* d = a.sdesc + ((long long)f * a.out_total + lv.out_base + p) * 32;
         if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
         if (lane == 0) a.angle[(long long)f * a.out_total + lv.out_base + p] = ang_deg;
+        key = knext;
         wave_sync();
     }
 }
@@ -1197,7 +1221,7 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
     fa.roi_max = (P.roi_max + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
-    const size_t flds = 4 * (size_t)(fa.roi_max + 4 * fa.win_max);
+    const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max);
     const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
     const int nv = (P.roi_dwords + kWave - 1) / kWave;
     if (nv <= 12) hipLaunchKernelGGL(k_fast_cells<12>, fgrid, dim3(256), flds, st, fa);

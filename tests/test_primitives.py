@@ -95,12 +95,14 @@ def test_blur_matches_formula(variant, kern):
     pad = np.pad(img.astype(np.int64), 3, mode="reflect")      # numpy 'reflect' == REFLECT_101
     hpass = sum(k[t] * pad[:, t:t + img.shape[1]] for t in range(7))
     v = sum(k[t] * hpass[t:t + img.shape[0], :] for t in range(7))
-    ref = ((v + 32768) >> 16).astype(np.uint8)
+    ref = np.minimum((v + 32768) >> 16, 255).astype(np.uint8)     # saturate_cast<uchar>
     np.testing.assert_array_equal(O.blur(img, variant), ref)
-    # flat images are fixed points of both kernels' normalisation only for ED (sum 256)
+    # ED taps sum to 256: flat images are fixed points; the legacy taps sum
+    # to 257 and saturate on white
     flat = np.full((20, 20), 200, np.uint8)
     if variant == 0:
         assert (O.blur(flat, 0) == 200).all()
+    assert (O.blur(np.full((9, 9), 255, np.uint8), variant) == 255).all()
 
 
 def test_gaussian_ed_kernel_derivation():
