@@ -4,7 +4,7 @@
 // src/ORBextractor.cc:409-1195) behind the C ABI of include/orb_mi355x.h.
 //
 // Per batch of same-size frames the path is seven kinds of launches, all
-// batched over frames (gridDim.y = frame):
+// batched over frames (one grid dimension indexes the frame):
 //   k_resize       level l from level l-1, OpenCV INTER_LINEAR 8U fixed point
 //   k_fast_cells   one wave per FAST cell: LDS-staged ROI, FAST-9 score map,
 //                  cell-local 3x3 NMS at iniThFAST / minThFAST, ballot compaction
@@ -30,8 +30,9 @@ namespace orbmi {
 constexpr int kMaxLevels = 32;
 constexpr int kHalfPatch = 15;
 constexpr int kEdge = 19;
+constexpr int kMinSubFrames = 16;   // smallest frame range worth its own stream
 
-__constant__ int8_t c_pattern[1024];
+__constant__ __attribute__((aligned(16))) int8_t c_pattern[1024];
 static const int8_t h_pattern[1024] = {
 #include "brief_pattern.inc"
 };
@@ -112,6 +113,11 @@ struct orbx_handle {
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::vector<hipEvent_t>> ev_calls;
     size_t ev_next = 0;
+    // sub-batch streams (orbx_set_streams)
+    int nsub = 2;
+    std::vector<hipStream_t> sub_streams;
+    std::vector<hipEvent_t> sub_done;
+    hipEvent_t fork_ev = nullptr;
 };
 
 namespace orbmi {
@@ -303,15 +309,18 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
 
 // ---------------------------------------------------------------------------
 // k_resize: cv::resize INTER_LINEAR 8UC1.  One output row per
-// wave; four rows per block.
+// wave, lanes over consecutive columns (coalesced byte taps and stores); four
+// rows per block.  The column taps and weights are recomputed in registers
+// with the host table's exact double/float steps (build_plan): a table load per
+// pixel cost a third of the kernel's time.  Row taps come from the table.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src, long long s_fstride, int s_pitch,
-                                                int sh, uint8_t* __restrict__ dst, long long d_fstride, int d_pitch,
-                                                int dw, int dh, const int2* __restrict__ xt,
+                                                int sw, int sh, uint8_t* __restrict__ dst, long long d_fstride,
+                                                int d_pitch, int dw, int dh, double scx,
                                                 const int2* __restrict__ yt, int xmax) {
     const int dy = blockIdx.x * 4 + wave_id();
     if (dy >= dh) return;
-    const int f = blockIdx.y;
+    const long long f = blockIdx.y;
     const uint8_t* S = src + f * s_fstride;
     uint8_t* D = dst + f * d_fstride + (long long)dy * d_pitch;
     const int2 ty = yt[dy];
@@ -320,8 +329,12 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src,
     const uint8_t* S0 = S + (long long)r0 * s_pitch;
     const uint8_t* S1 = S + (long long)r1 * s_pitch;
     for (int dx = lane_id(); dx < dw; dx += kWave) {
-        const int2 tx = xt[dx];
-        const int sx = tx.x, a0 = (short)(tx.y & 0xffff), a1 = tx.y >> 16;
+        float fx = (float)((dx + 0.5) * scx - 0.5);
+        int sx = (int)floorf(fx);
+        fx -= (float)sx;
+        if (sx < 0) { fx = 0.f; sx = 0; }
+        if (sx >= sw - 1) { fx = 0.f; sx = sw - 1; }
+        const int a0 = (int)rintf((1.f - fx) * 2048.f), a1 = (int)rintf(fx * 2048.f);
         int h0, h1;
         if (dx < xmax) {
             h0 = S0[sx] * a0 + S0[sx + 1] * a1;
@@ -357,40 +370,52 @@ struct FastArgs {
     int roi_max, win_max;   // LDS per wave
 };
 
-__device__ __forceinline__ int fast_score(const uint8_t* roi, int stride, int r, int c) {
+// Arc strength of one direction on the raw ring values: max over the 16 arcs
+// of 9 contiguous ring pixels of min(x ^ m), m = 0 (brighter ring: the arc's
+// min x) or 0xff (darker ring: 255 - the arc's max x).  With d = v - x,
+// cv::FAST's score is max(A, B) - 1 for B = strength(0) - v and
+// A = strength(0xff) - (255 - v).
+__device__ __forceinline__ int arc_strength(const int (&x)[16], int m) {
+    int w[16], w3[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w[k] = x[k] ^ m;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) w3[k] = min(w[k], min(w[(k + 1) & 15], w[(k + 2) & 15]));
+    int a = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) a = max(a, min(w3[k], min(w3[(k + 3) & 15], w3[(k + 6) & 15])));
+    return a;
+}
+
+__device__ __forceinline__ void fast_ring(const uint8_t* roi, int stride, int r, int c, int& v, int (&x)[16]) {
     const uint8_t* p = roi + r * stride + c;
-    const int v = p[0];
-    int d[16];
-    d[0] = v - p[3 * stride];
-    d[1] = v - p[3 * stride + 1];
-    d[2] = v - p[2 * stride + 2];
-    d[3] = v - p[stride + 3];
-    d[4] = v - p[3];
-    d[5] = v - p[-stride + 3];
-    d[6] = v - p[-2 * stride + 2];
-    d[7] = v - p[-3 * stride + 1];
-    d[8] = v - p[-3 * stride];
-    d[9] = v - p[-3 * stride - 1];
-    d[10] = v - p[-2 * stride - 2];
-    d[11] = v - p[-stride - 3];
-    d[12] = v - p[-3];
-    d[13] = v - p[stride - 3];
-    d[14] = v - p[2 * stride - 2];
-    d[15] = v - p[3 * stride - 1];
-    int mn3[16], mx3[16];
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        mn3[k] = min(d[k], min(d[(k + 1) & 15], d[(k + 2) & 15]));
-        mx3[k] = max(d[k], max(d[(k + 1) & 15], d[(k + 2) & 15]));
-    }
-    int a = -1000, b = 1000;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-        a = max(a, min(mn3[k], min(mn3[(k + 3) & 15], mn3[(k + 6) & 15])));
-        b = min(b, max(mx3[k], max(mx3[(k + 3) & 15], mx3[(k + 6) & 15])));
-    }
-    const int s = max(a, -b) - 1;
-    return s < 0 ? 0 : s;
+    v = p[0];
+    x[0] = p[3 * stride];
+    x[1] = p[3 * stride + 1];
+    x[2] = p[2 * stride + 2];
+    x[3] = p[stride + 3];
+    x[4] = p[3];
+    x[5] = p[-stride + 3];
+    x[6] = p[-2 * stride + 2];
+    x[7] = p[-3 * stride + 1];
+    x[8] = p[-3 * stride];
+    x[9] = p[-3 * stride - 1];
+    x[10] = p[-2 * stride - 2];
+    x[11] = p[-stride - 3];
+    x[12] = p[-3];
+    x[13] = p[stride - 3];
+    x[14] = p[2 * stride - 2];
+    x[15] = p[3 * stride - 1];
+}
+
+// Score of one direction (dark = 0: brighter ring, 1: darker ring) minus one.
+// A pixel whose compass pre-test at tmin fails in a direction has that
+// direction's strength - 1 < tmin, so dropping it changes no score >= tmin,
+// and scores < t act as 0 in the NMS: the candidate's score is the max over
+// its passing directions only (exact for every threshold >= tmin).
+__device__ __forceinline__ int fast_dir_score(const int (&x)[16], int v, int dark) {
+    const int m = dark ? 0xff : 0;
+    return arc_strength(x, m) - (v ^ m) - 1;
 }
 
 // NMS on the zero-padded score map (pitch ww+2): p survives at threshold t iff
@@ -407,19 +432,42 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c
     return keep;
 }
 
-// Compass pre-test: a 9-pixel arc of the 16-ring always covers >= 2 of the 4
-// compass pixels, so a corner at threshold t has >= 2 compass pixels brighter
-// than v+t or >= 2 darker than v-t.  Pixels failing it at min(iniTh, minTh)
-// are corners at no threshold used; their score is stored as 0, which the NMS
-// treats exactly like a non-corner (s_t(q) = 0).
-__device__ __forceinline__ bool fast_pretest(const uint8_t* roi, int stride, int r, int c, int t) {
-    const uint8_t* p = roi + r * stride + c;
-    const int v = p[0];
-    const int n0 = p[3 * stride], n4 = p[3], n8 = p[-3 * stride], n12 = p[-3];
-    const int nb = (n0 - v > t) + (n4 - v > t) + (n8 - v > t) + (n12 - v > t);
-    const int nd = (v - n0 > t) + (v - n4 > t) + (v - n8 > t) + (v - n12 > t);
-    return nb >= 2 || nd >= 2;
+// Compass pre-test, 4 pixels per lane: a 9-pixel arc of the 16-ring always
+// covers >= 2 of the 4 compass pixels, so a brighter corner at threshold t has
+// the second largest compass pixel > v + t and a darker one the second smallest
+// < v - t.  Pixels failing both at min(iniTh, minTh) are corners at no
+// threshold used; their score stays 0, which the NMS treats exactly like a
+// non-corner (s_t(q) = 0).  Bytes are split into u16 pairs (pixels 0/2 and
+// 1/3) and tested with packed u16 min/max and saturating subtracts.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+
+// bit 0 / bit 16 set where the pixel of that half passes (bright, dark)
+__device__ __forceinline__ void compass_pair(uint32_t c, uint32_t u, uint32_t d, uint32_t l, uint32_t r,
+                                             u16x2 tt, uint32_t& bright, uint32_t& dark) {
+    const u16x2 C = as_u16x2(c), U = as_u16x2(u), D = as_u16x2(d), L = as_u16x2(l), R = as_u16x2(r);
+    const u16x2 m1 = __builtin_elementwise_min(U, D), M1 = __builtin_elementwise_max(U, D);
+    const u16x2 m2 = __builtin_elementwise_min(L, R), M2 = __builtin_elementwise_max(L, R);
+    const u16x2 X = __builtin_elementwise_min(M1, M2), Y = __builtin_elementwise_max(m1, m2);
+    const u16x2 L2 = __builtin_elementwise_max(X, Y), S2 = __builtin_elementwise_min(X, Y);
+    const u16x2 one = {1, 1};
+    const u16x2 br = __builtin_elementwise_sub_sat(L2, C + tt);
+    const u16x2 dk = __builtin_elementwise_sub_sat(__builtin_elementwise_sub_sat(C, tt), S2);
+    bright = as_u32(__builtin_elementwise_min(br, one));
+    dark = as_u32(__builtin_elementwise_min(dk, one));
 }
+
+__device__ __forceinline__ uint32_t lo_bytes(uint32_t x) { return x & 0x00ff00ffu; }
+__device__ __forceinline__ uint32_t hi_bytes(uint32_t x) { return (x >> 8) & 0x00ff00ffu; }
+// bits {0, 16} of lo and hi masks -> 4-bit pixel mask (bit b = byte b)
+__device__ __forceinline__ uint32_t pix4(uint32_t lo, uint32_t hi) {
+    const uint32_t m = lo | (hi << 1);
+    return (m | (m >> 14)) & 0xfu;
+}
+
+constexpr int kCandIdx = 0x3fff, kCandBright = 0x4000, kCandDark = 0x8000;
 
 // each wave of k_fast_cells owns its cells and its LDS region: wave-level sync only
 __device__ __forceinline__ void fast_wave_sync() {
@@ -503,25 +551,86 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         fast_wave_sync();
         const int nwin = ww * wh;
         const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
-        // 1. compass pre-test, ballot-compacted candidate queue (row-major)
-        int ncand = 0;
-        for (int base = 0; base < nwin; base += kWave) {
-            const int i = base + lane;
-            bool pass = false;
-            if (i < nwin) {
-                const int r = div_row(i, inv_ww);
-                pass = fast_pretest(R, rstride, r + 3, i - r * ww + 3, tmin);
+        // 1. compass pre-test on (row, aligned dword) items: candidates in
+        //    row-major order tagged with their passing directions; pixels that
+        //    pass both also enter a second list growing down from the top of
+        //    `cand` (dropped, with a two-direction fallback, if it would collide)
+        const int X0 = shift + 3, j0 = X0 >> 2;
+        const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
+        const int nitems = wh * ndw;
+        const float inv_ndw = ndw ? 1.0f / (float)ndw : 0.f;
+        const uint32_t* roi32 = (const uint32_t*)roi;
+        const int rs4 = rstride >> 2;
+        const u16x2 tt = {(unsigned short)tmin, (unsigned short)tmin};
+        const int cap = a.win_max;
+        int ncand = 0, nsec = 0;
+        bool sec_ok = true;
+        for (int base = 0; base < nitems; base += kWave) {
+            const int it = base + lane;
+            uint32_t bm = 0, dm = 0;
+            int idx0 = 0;
+            if (it < nitems) {
+                const int r = div_row(it, inv_ndw);
+                const int j = j0 + (it - (int)__umul24(r, ndw));
+                const uint32_t* row = roi32 + __umul24(r + 3, rs4) + j;
+                const uint32_t c = row[0], u = row[-3 * rs4], d = row[3 * rs4];
+                const uint32_t lf = __builtin_amdgcn_alignbyte(c, row[-1], 1);
+                const uint32_t rt = __builtin_amdgcn_alignbyte(row[1], c, 3);
+                uint32_t b0, d0, b1, d1;
+                compass_pair(lo_bytes(c), lo_bytes(u), lo_bytes(d), lo_bytes(lf), lo_bytes(rt), tt, b0, d0);
+                compass_pair(hi_bytes(c), hi_bytes(u), hi_bytes(d), hi_bytes(lf), hi_bytes(rt), tt, b1, d1);
+                const int cx = 4 * j - X0;                       // window column of byte 0
+                const int s0 = min(max(-cx, 0), 4), e0 = min(max(ww - cx, 0), 4);
+                const uint32_t valid = (0xfu << s0) & ((1u << e0) - 1u);
+                bm = pix4(b0, b1) & valid;
+                dm = pix4(d0, d1) & valid;
+                idx0 = (int)__umul24(r, ww) + cx;
             }
-            const uint64_t m = __ballot(pass);
-            if (pass) cand[ncand + mask_rank(m)] = (uint16_t)i;
-            ncand += __popcll(m);
+            const uint32_t pm = bm | dm, both = bm & dm;
+            const int cnt = __popc(pm), cb = __popc(both);
+            // lane-exclusive prefixes of the per-lane counts (<= 4) by bit ballots
+            const uint64_t c0 = __ballot(cnt & 1), c1 = __ballot(cnt & 2), c2 = __ballot(cnt & 4);
+            const uint64_t q0 = __ballot(cb & 1), q1 = __ballot(cb & 2), q2 = __ballot(cb & 4);
+            const int tot = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
+            const int stot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
+            if (ncand + tot + nsec + stot > cap) sec_ok = false;
+            if (pm) {
+                int pos = ncand + mask_rank(c0) + 2 * mask_rank(c1) + 4 * mask_rank(c2);
+                int spos = nsec + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2);
+#pragma unroll
+                for (int bb = 0; bb < 4; ++bb) {
+                    if ((pm >> bb) & 1) {
+                        const int fl = (((bm >> bb) & 1) ? kCandBright : 0) | (((dm >> bb) & 1) ? kCandDark : 0);
+                        cand[pos++] = (uint16_t)((idx0 + bb) | fl);
+                        if (sec_ok && ((both >> bb) & 1)) cand[cap - 1 - spos++] = (uint16_t)(idx0 + bb);
+                    }
+                }
+            }
+            ncand += tot;
+            nsec += stot;
         }
         fast_wave_sync();
-        // 2. FAST score of the candidates
+        // 2. FAST score of the candidates (first passing direction; the second
+        //    direction of two-direction pixels from the second list)
         for (int q = lane; q < ncand; q += kWave) {
-            const int i = cand[q];
-            const int r = div_row(i, inv_ww), cc = i - r * ww;
-            sc[(r + 1) * sp + cc + 1] = (uint8_t)fast_score(R, rstride, r + 3, cc + 3);
+            const int e = cand[q], i = e & kCandIdx;
+            const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+            int v, x[16];
+            fast_ring(R, rstride, r + 3, cc + 3, v, x);
+            int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
+            if (!sec_ok && (e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
+            sc[(r + 1) * sp + cc + 1] = (uint8_t)max(sv, 0);
+        }
+        if (sec_ok && nsec > 0) {
+            fast_wave_sync();
+            for (int q = lane; q < nsec; q += kWave) {
+                const int i = cand[cap - 1 - q];
+                const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                int v, x[16];
+                fast_ring(R, rstride, r + 3, cc + 3, v, x);
+                uint8_t* sq = sc + (r + 1) * sp + cc + 1;
+                *sq = (uint8_t)max((int)*sq, max(fast_dir_score(x, v, 1), 0));
+            }
         }
         fast_wave_sync();
         // 3. NMS at iniThFAST once; keep its ballots (ORBextractor.cc:826-827)
@@ -531,7 +640,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
             const int q = k * kWave + lane;
             bool keep = false;
             if (q < ncand) {
-                const int i = cand[q], r = div_row(i, inv_ww);
+                const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
                 keep = nms_keep(sc, sp, r, i - r * ww, a.ini_th);
             }
             const uint64_t m = __ballot(keep);
@@ -548,7 +657,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
             int i = 0, r = 0, cc = 0;
             bool keep = false;
             if (q < ncand) {
-                i = cand[q];
+                i = cand[q] & kCandIdx;
                 r = div_row(i, inv_ww);
                 cc = i - r * ww;
                 keep = rerun ? nms_keep(sc, sp, r, cc, a.min_th) : ((kmask[k] >> lane) & 1);
@@ -887,7 +996,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 // fixed-point separable kernel and evaluates the 256 tests on
 // it: the blurred level never goes to HBM.  Lane l evaluates tests 4l..4l+3.
 // ---------------------------------------------------------------------------
-constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 40;   // hb pitch: 80 B rows (38 used), 16-B aligned
+constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 42;   // hb pitch: 21 dwords (odd: conflict-free row stores)
 
 struct DescArgs {
     const uint8_t* in;
@@ -954,13 +1063,19 @@ __device__ __forceinline__ void patch_border(const uint8_t* img, int pitch, int 
     }
 }
 
-__global__ __launch_bounds__(256) void k_describe(DescArgs a) {
-    __shared__ int8_t pat[1024];
+#ifndef ORB_DESC_WAVES
+#define ORB_DESC_WAVES 4
+#endif
+#ifndef ORB_Q_UNROLL
+#define ORB_Q_UNROLL 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WAVES))) void k_describe(DescArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
     __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][kRaw * kHbP];
-    for (int i = threadIdx.x; i < 1024; i += 256) pat[i] = c_pattern[i];
-    __syncthreads();
     const int l = blockIdx.x, f = blockIdx.y, lane = lane_id(), wv = wave_id();
+    // lane's 4 tests = 16 consecutive pattern bytes, kept packed in registers
+    const uint4 patv = ((const uint4*)c_pattern)[lane];
+    const uint32_t patw[4] = {patv.x, patv.y, patv.z, patv.w};
     uint8_t* raw = raw_s[wv];
     uint16_t* hb = hb_s[wv];
     const LevelDev lv = a.lv[l];
@@ -1055,13 +1170,13 @@ __global__ __launch_bounds__(256) void k_describe(DescArgs a) {
         //    only at the 512 sample points, hb rows R..R+6 at blurred column C,
         //    blurred centre (18, 18)
         int nib = 0;
-#pragma unroll
+#pragma unroll ORB_Q_UNROLL
         for (int q = 0; q < 4; ++q) {
-            const int t = 4 * lane + q;
             int val[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
-                const float x = (float)pat[4 * t + 2 * e], y = (float)pat[4 * t + 2 * e + 1];
+                const float x = (float)(int)(int8_t)(patw[q] >> (16 * e));
+                const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
                 int r, c;
                 if (a.fma) {
                     r = cv_round(__builtin_fmaf(x, sb, y * ca));
@@ -1181,11 +1296,36 @@ static size_t qt_lds_bytes(const Plan& P) {
     return b;
 }
 
-static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long long fstride, int pitch0, float lap0,
-                        float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono,
-                        hipStream_t st) {
-    Plan& P = hd->plan;
-    const int L = P.L;
+// Frames [f0, f0+B) of the batch: every per-frame work buffer is addressed
+// through pointers offset by f0, so disjoint frame ranges can run on separate
+// streams without sharing scratch.
+static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames, long long fstride, int pitch0,
+                        float lap0, float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n,
+                        int32_t* d_mono, hipStream_t st) {
+    const Plan& P0 = hd->plan;
+    const int L = P0.L;
+    Plan P;                         // shallow view: host tables + offset device pointers (never released)
+    P.lv = P0.lv; P.cells = P0.cells; P.pyr_bytes = P0.pyr_bytes; P.ncells = P0.ncells;
+    P.slot_total = P0.slot_total; P.out_total = P0.out_total; P.roi_max = P0.roi_max;
+    P.roi_dwords = P0.roi_dwords; P.win_max = P0.win_max; P.max_level_cells = P0.max_level_cells;
+    P.max_out_cap = P0.max_out_cap; P.xmax = P0.xmax; P.tab_off = P0.tab_off; P.L = L;
+    P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells;
+    const long long F = f0;
+    P.d_pyr = P0.d_pyr + F * P0.pyr_bytes;
+    P.d_cell_count = P0.d_cell_count + F * P0.ncells;
+    P.d_cell_keys = P0.d_cell_keys + F * P0.slot_total;
+    P.d_key_scr = P0.d_key_scr + F * P0.slot_total;
+    P.d_knode = P0.d_knode + F * P0.slot_total;
+    P.d_kq = P0.d_kq + F * P0.slot_total;
+    P.d_qt_key = P0.d_qt_key + F * P0.out_total;
+    P.d_qt_n = P0.d_qt_n + F * L;
+    P.d_angle = P0.d_angle + F * P0.out_total;
+    P.d_sdesc = P0.d_sdesc + F * P0.out_total * 32;
+    d_frames += F * fstride;
+    d_kps += F * cap;
+    d_desc += F * cap * 32;
+    d_n += F;
+    d_mono += F;
     std::vector<hipEvent_t> marks;
     auto mark = [&]() {
         if (!hd->profiling) return;
@@ -1207,8 +1347,9 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
         const long long sfs = l == 1 ? fstride : P.pyr_bytes;
         const int sp = l == 1 ? pitch0 : s.pitch;
         const int2* xt = P.d_tab + P.tab_off[l];
-        hipLaunchKernelGGL(k_resize, dim3((d.h + 3) / 4, B), dim3(256), 0, st, src, sfs, sp, s.h, P.d_pyr + d.off,
-                           P.pyr_bytes, d.pitch, d.w, d.h, xt, xt + d.w, P.xmax[l]);
+        const double scx = 1. / ((double)d.w / s.w);          // as build_plan / cv::resize
+        hipLaunchKernelGGL(k_resize, dim3((d.h + 3) / 4, B), dim3(256), 0, st, src, sfs, sp, s.w, s.h,
+                           P.d_pyr + d.off, P.pyr_bytes, d.pitch, d.w, d.h, scx, xt + d.w, P.xmax[l]);
     }
     mark();
     // FAST cells
@@ -1263,6 +1404,41 @@ static int run_pipeline(orbx_handle* hd, int B, const uint8_t* d_frames, long lo
     return ORB_OK;
 }
 
+// Splits a batch into hd->nsub frame ranges on private non-blocking streams
+// that fork from and join back into the caller's stream.  The quadtree,
+// pyramid and assemble kernels are latency bound (one block per frame-level,
+// barrier heavy); running them beside the VALU-bound FAST/describe kernels
+// of the other range fills the CUs they leave idle.
+static int run_batched(orbx_handle* hd, int B, const uint8_t* d_frames, long long fstride, int pitch0, float lap0,
+                       float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono,
+                       hipStream_t st) {
+    const int S = std::min(hd->nsub, std::max(1, B / kMinSubFrames));
+    if (S <= 1)
+        return run_pipeline(hd, 0, B, d_frames, fstride, pitch0, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, st);
+    while ((int)hd->sub_streams.size() < S) {
+        hipStream_t s;
+        hipEvent_t e;
+        ORB_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        ORB_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        hd->sub_streams.push_back(s);
+        hd->sub_done.push_back(e);
+    }
+    if (!hd->fork_ev) ORB_CHECK(hipEventCreateWithFlags(&hd->fork_ev, hipEventDisableTiming));
+    ORB_CHECK(hipEventRecord(hd->fork_ev, st));
+    int f0 = 0;
+    for (int i = 0; i < S; ++i) {
+        const int nb = B / S + (i < B % S ? 1 : 0);
+        ORB_CHECK(hipStreamWaitEvent(hd->sub_streams[i], hd->fork_ev, 0));
+        const int rc = run_pipeline(hd, f0, nb, d_frames, fstride, pitch0, lap0, lap1, d_kps, d_desc, cap, d_n,
+                                    d_mono, hd->sub_streams[i]);
+        if (rc) return rc;
+        ORB_CHECK(hipEventRecord(hd->sub_done[i], hd->sub_streams[i]));
+        f0 += nb;
+    }
+    for (int i = 0; i < S; ++i) ORB_CHECK(hipStreamWaitEvent(st, hd->sub_done[i], 0));
+    return ORB_OK;
+}
+
 }  // namespace orbmi
 
 using namespace orbmi;
@@ -1292,6 +1468,9 @@ void orbx_destroy(orbx_handle* h) {
     (void)hipSetDevice(h->device);
     h->plan.release();
     for (hipEvent_t e : h->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : h->sub_done) (void)hipEventDestroy(e);
+    for (hipStream_t s : h->sub_streams) (void)hipStreamDestroy(s);
+    if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
     delete h;
 }
 
@@ -1327,8 +1506,8 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     int rc = build_plan(h, w, hh, std::max(nframes, h->plan.maxB));
     if (rc) return rc;
     if (cap < h->plan.out_total) return ORB_ERR_CAPACITY;
-    return run_pipeline(h, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
-                        d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
+    return run_batched(h, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
+                       d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
 }
 
 int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step, int lap0, int lap1,
@@ -1340,7 +1519,7 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
     if (rc) return rc;
     Plan& P = h->plan;
     ORB_CHECK(hipMemcpy2D(P.d_in, P.in_pitch, img, step, w, hh, hipMemcpyHostToDevice));
-    rc = run_pipeline(h, 1, P.d_in, (long long)P.in_pitch * hh, (int)P.in_pitch, (float)lap0, (float)lap1, P.d_kps,
+    rc = run_pipeline(h, 0, 1, P.d_in, (long long)P.in_pitch * hh, (int)P.in_pitch, (float)lap0, (float)lap1, P.d_kps,
                       P.d_desc, P.host_cap, P.d_n, P.d_mono, 0);
     if (rc) return rc;
     int32_t n = 0, mono = 0;
@@ -1363,6 +1542,12 @@ int orbx_set_profiling(orbx_handle* h, int enable) {
     h->profiling = enable != 0;
     h->ev_calls.clear();
     h->ev_next = 0;
+    return ORB_OK;
+}
+
+int orbx_set_streams(orbx_handle* h, int nsub) {
+    if (!h || nsub < 1 || nsub > 16) return ORB_ERR_PARAM;
+    h->nsub = nsub;
     return ORB_OK;
 }
 
