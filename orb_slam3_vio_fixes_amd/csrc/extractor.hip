@@ -23,6 +23,7 @@
 #include <cmath>
 #include <cstring>
 #include <memory>
+#include <type_traits>
 #include <vector>
 
 namespace orbmi {
@@ -82,6 +83,7 @@ struct Plan {
     int* d_qt_n = nullptr;
     float* d_angle = nullptr;
     uint8_t* d_sdesc = nullptr;
+    uint8_t* d_slot_level = nullptr;
     // single-image host path outputs
     orb_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
@@ -91,7 +93,8 @@ struct Plan {
 
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
-                      d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono};
+                      d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
+                      d_slot_level};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();
@@ -304,6 +307,13 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     if (!tab.empty()) ORB_CHECK(hipMemcpy(P.d_tab, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
     ORB_CHECK(hipMemcpy(P.d_lv, P.lv.data(), L * sizeof(LevelDev), hipMemcpyHostToDevice));
     ORB_CHECK(hipMemcpy(P.d_cells, P.cells.data(), P.cells.size() * sizeof(CellDev), hipMemcpyHostToDevice));
+    {
+        std::vector<uint8_t> sl(P.out_total);
+        for (int l = 0; l < L; ++l)
+            for (int o = 0; o < P.lv[l].out_cap; ++o) sl[P.lv[l].out_base + o] = (uint8_t)l;
+        ORB_CHECK(hipMalloc(&P.d_slot_level, std::max<size_t>(1, sl.size())));
+        ORB_CHECK(hipMemcpy(P.d_slot_level, sl.data(), sl.size(), hipMemcpyHostToDevice));
+    }
     return ORB_OK;
 }
 
@@ -368,6 +378,7 @@ struct FastArgs {
     int slot_total;
     int ini_th, min_th;
     int roi_max, win_max;   // LDS per wave
+    int kmask_bytes;
 };
 
 // Arc strength of one direction on the raw ring values: max over the 16 arcs
@@ -409,10 +420,10 @@ __device__ __forceinline__ void fast_ring(const uint8_t* roi, int stride, int r,
 }
 
 // Score of one direction (dark = 0: brighter ring, 1: darker ring) minus one.
-// A pixel whose compass pre-test at tmin fails in a direction has that
-// direction's strength - 1 < tmin, so dropping it changes no score >= tmin,
-// and scores < t act as 0 in the NMS: the candidate's score is the max over
-// its passing directions only (exact for every threshold >= tmin).
+// A pixel whose compass pre-test at the pass threshold t fails in a direction
+// has that direction's strength - 1 < t, so dropping it changes no score >= t,
+// and scores < t act as 0 in the NMS at t: the candidate's score is the max
+// over its passing directions only (exact for the NMS at t).
 __device__ __forceinline__ int fast_dir_score(const int (&x)[16], int v, int dark) {
     const int m = dark ? 0xff : 0;
     return arc_strength(x, m) - (v ^ m) - 1;
@@ -505,10 +516,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
     const int f = blockIdx.y;
-    uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 3);   // multiples of 16
+    uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 3 + a.kmask_bytes);   // multiples of 16
     uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
     uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_max entries
-    uint64_t* kmask = (uint64_t*)(roi);                       // reused after scoring (ROI no longer needed)
+    uint64_t* kmask = (uint64_t*)(sc + 3 * a.win_max);        // NMS ballots, one per 64 candidates
     const int c_begin = (blockIdx.x * 4 + wv) * kCellsPerWave;
     const int c_end = min(c_begin + kCellsPerWave, a.ncells);
     auto fetch_of = [&](const CellDev& c) {
@@ -529,7 +540,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         rf = fetch_of(c);
         roi_issue<NV>(rf, c.y0, v);
     }
-    const int tmin = min(a.ini_th, a.min_th);
     for (int ci = c_begin; ci < c_end; ++ci) {
         // land the prefetched ROI in LDS, then prefetch the next cell's ROI
 #pragma unroll
@@ -549,130 +559,135 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
             roi_issue<NV>(rf, c.y0, v);
         }
         fast_wave_sync();
-        const int nwin = ww * wh;
         const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
-        // 1. compass pre-test on (row, aligned dword) items: candidates in
-        //    row-major order tagged with their passing directions; pixels that
-        //    pass both also enter a second list growing down from the top of
-        //    `cand` (dropped, with a two-direction fallback, if it would collide)
         const int X0 = shift + 3, j0 = X0 >> 2;
         const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
         const int nitems = wh * ndw;
         const float inv_ndw = ndw ? 1.0f / (float)ndw : 0.f;
         const uint32_t* roi32 = (const uint32_t*)roi;
         const int rs4 = rstride >> 2;
-        const u16x2 tt = {(unsigned short)tmin, (unsigned short)tmin};
         const int cap = a.win_max;
-        int ncand = 0, nsec = 0;
-        bool sec_ok = true;
-        for (int base = 0; base < nitems; base += kWave) {
-            const int it = base + lane;
-            uint32_t bm = 0, dm = 0;
-            int idx0 = 0;
-            if (it < nitems) {
-                const int r = div_row(it, inv_ndw);
-                const int j = j0 + (it - (int)__umul24(r, ndw));
-                const uint32_t* row = roi32 + __umul24(r + 3, rs4) + j;
-                const uint32_t c = row[0], u = row[-3 * rs4], d = row[3 * rs4];
-                const uint32_t lf = __builtin_amdgcn_alignbyte(c, row[-1], 1);
-                const uint32_t rt = __builtin_amdgcn_alignbyte(row[1], c, 3);
-                uint32_t b0, d0, b1, d1;
-                compass_pair(lo_bytes(c), lo_bytes(u), lo_bytes(d), lo_bytes(lf), lo_bytes(rt), tt, b0, d0);
-                compass_pair(hi_bytes(c), hi_bytes(u), hi_bytes(d), hi_bytes(lf), hi_bytes(rt), tt, b1, d1);
-                const int cx = 4 * j - X0;                       // window column of byte 0
-                const int s0 = min(max(-cx, 0), 4), e0 = min(max(ww - cx, 0), 4);
-                const uint32_t valid = (0xfu << s0) & ((1u << e0) - 1u);
-                bm = pix4(b0, b1) & valid;
-                dm = pix4(d0, d1) & valid;
-                idx0 = (int)__umul24(r, ww) + cx;
-            }
-            const uint32_t pm = bm | dm, both = bm & dm;
-            const int cnt = __popc(pm), cb = __popc(both);
-            // lane-exclusive prefixes of the per-lane counts (<= 4) by bit ballots
-            const uint64_t c0 = __ballot(cnt & 1), c1 = __ballot(cnt & 2), c2 = __ballot(cnt & 4);
-            const uint64_t q0 = __ballot(cb & 1), q1 = __ballot(cb & 2), q2 = __ballot(cb & 4);
-            const int tot = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
-            const int stot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
-            if (ncand + tot + nsec + stot > cap) sec_ok = false;
-            if (pm) {
-                int pos = ncand + mask_rank(c0) + 2 * mask_rank(c1) + 4 * mask_rank(c2);
-                int spos = nsec + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2);
+        // FAST(ROI, iniThFAST) and, only if that leaves no corner, FAST(ROI,
+        // minThFAST) (ORBextractor.cc:826-846).  Each pass pre-tests at its own
+        // threshold, so the iniTh pass scores far fewer pixels; scores stored by
+        // the first pass stay exact for the second (its candidates are a superset).
+        int ncand = 0, cnt = 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            const int t = pass == 0 ? a.ini_th : a.min_th;
+            // 1. compass pre-test on (row, aligned dword) items: candidates in
+            //    row-major order tagged with their passing directions; pixels that
+            //    pass both also enter a second list growing down from the top of
+            //    `cand` (dropped, with a two-direction fallback, if it would collide)
+            const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+            int nsec = 0;
+            bool sec_ok = true;
+            ncand = 0;
+            for (int base = 0; base < nitems; base += kWave) {
+                const int it = base + lane;
+                uint32_t bm = 0, dm = 0;
+                int idx0 = 0;
+                if (it < nitems) {
+                    const int r = div_row(it, inv_ndw);
+                    const int j = j0 + (it - (int)__umul24(r, ndw));
+                    const uint32_t* row = roi32 + __umul24(r + 3, rs4) + j;
+                    const uint32_t c = row[0], u = row[-3 * rs4], d = row[3 * rs4];
+                    const uint32_t lf = __builtin_amdgcn_alignbyte(c, row[-1], 1);
+                    const uint32_t rt = __builtin_amdgcn_alignbyte(row[1], c, 3);
+                    uint32_t b0, d0, b1, d1;
+                    compass_pair(lo_bytes(c), lo_bytes(u), lo_bytes(d), lo_bytes(lf), lo_bytes(rt), tt, b0, d0);
+                    compass_pair(hi_bytes(c), hi_bytes(u), hi_bytes(d), hi_bytes(lf), hi_bytes(rt), tt, b1, d1);
+                    const int cx = 4 * j - X0;                       // window column of byte 0
+                    const int s0 = min(max(-cx, 0), 4), e0 = min(max(ww - cx, 0), 4);
+                    const uint32_t valid = (0xfu << s0) & ((1u << e0) - 1u);
+                    bm = pix4(b0, b1) & valid;
+                    dm = pix4(d0, d1) & valid;
+                    idx0 = (int)__umul24(r, ww) + cx;
+                }
+                const uint32_t pm = bm | dm, both = bm & dm;
+                const int pc = __popc(pm), cb = __popc(both);
+                // lane-exclusive prefixes of the per-lane counts (<= 4) by bit ballots
+                const uint64_t c0 = __ballot(pc & 1), c1 = __ballot(pc & 2), c2 = __ballot(pc & 4);
+                const uint64_t q0 = __ballot(cb & 1), q1 = __ballot(cb & 2), q2 = __ballot(cb & 4);
+                const int tot = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
+                const int stot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
+                if (ncand + tot + nsec + stot > cap) sec_ok = false;
+                if (pm) {
+                    int pos = ncand + mask_rank(c0) + 2 * mask_rank(c1) + 4 * mask_rank(c2);
+                    int spos = nsec + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2);
 #pragma unroll
-                for (int bb = 0; bb < 4; ++bb) {
-                    if ((pm >> bb) & 1) {
-                        const int fl = (((bm >> bb) & 1) ? kCandBright : 0) | (((dm >> bb) & 1) ? kCandDark : 0);
-                        cand[pos++] = (uint16_t)((idx0 + bb) | fl);
-                        if (sec_ok && ((both >> bb) & 1)) cand[cap - 1 - spos++] = (uint16_t)(idx0 + bb);
+                    for (int bb = 0; bb < 4; ++bb) {
+                        if ((pm >> bb) & 1) {
+                            const int fl = (((bm >> bb) & 1) ? kCandBright : 0) | (((dm >> bb) & 1) ? kCandDark : 0);
+                            cand[pos++] = (uint16_t)((idx0 + bb) | fl);
+                            if (sec_ok && ((both >> bb) & 1)) cand[cap - 1 - spos++] = (uint16_t)(idx0 + bb);
+                        }
                     }
                 }
+                ncand += tot;
+                nsec += stot;
             }
-            ncand += tot;
-            nsec += stot;
-        }
-        fast_wave_sync();
-        // 2. FAST score of the candidates (first passing direction; the second
-        //    direction of two-direction pixels from the second list)
-        for (int q = lane; q < ncand; q += kWave) {
-            const int e = cand[q], i = e & kCandIdx;
-            const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
-            int v, x[16];
-            fast_ring(R, rstride, r + 3, cc + 3, v, x);
-            int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
-            if (!sec_ok && (e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
-            sc[(r + 1) * sp + cc + 1] = (uint8_t)max(sv, 0);
-        }
-        if (sec_ok && nsec > 0) {
             fast_wave_sync();
-            for (int q = lane; q < nsec; q += kWave) {
-                const int i = cand[cap - 1 - q];
+            // 2. FAST score of the candidates (first passing direction; the second
+            //    direction of two-direction pixels from the second list)
+            for (int q = lane; q < ncand; q += kWave) {
+                const int e = cand[q], i = e & kCandIdx;
                 const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
                 int v, x[16];
                 fast_ring(R, rstride, r + 3, cc + 3, v, x);
-                uint8_t* sq = sc + (r + 1) * sp + cc + 1;
-                *sq = (uint8_t)max((int)*sq, max(fast_dir_score(x, v, 1), 0));
+                int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
+                if (!sec_ok && (e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
+                sc[(r + 1) * sp + cc + 1] = (uint8_t)max(sv, 0);
             }
-        }
-        fast_wave_sync();
-        // 3. NMS at iniThFAST once; keep its ballots (ORBextractor.cc:826-827)
-        int cnt = 0;
-        const int nchunk = (ncand + kWave - 1) / kWave;
-        for (int k = 0; k < nchunk; ++k) {
-            const int q = k * kWave + lane;
-            bool keep = false;
-            if (q < ncand) {
-                const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
-                keep = nms_keep(sc, sp, r, i - r * ww, a.ini_th);
-            }
-            const uint64_t m = __ballot(keep);
-            if (lane == 0) kmask[k] = m;
-            cnt += __popcll(m);
-        }
-        fast_wave_sync();
-        // 4. survivors (cells without any re-run at minThFAST, :843-846), row-major
-        const bool rerun = cnt == 0;
-        uint32_t* out = a.cell_keys + (long long)f * a.slot_total + cur.slot_off;
-        int written = 0;
-        for (int k = 0; k < nchunk; ++k) {
-            const int q = k * kWave + lane;
-            int i = 0, r = 0, cc = 0;
-            bool keep = false;
-            if (q < ncand) {
-                i = cand[q] & kCandIdx;
-                r = div_row(i, inv_ww);
-                cc = i - r * ww;
-                keep = rerun ? nms_keep(sc, sp, r, cc, a.min_th) : ((kmask[k] >> lane) & 1);
-            }
-            const uint64_t m = __ballot(keep);
-            if (keep) {
-                const int pos = written + mask_rank(m);
-                if (pos < cur.cap) {
-                    // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
-                    const uint32_t x = (uint32_t)(cur.x0 + cc + 3 - (kEdge - 3));
-                    const uint32_t y = (uint32_t)(cur.y0 + r + 3 - (kEdge - 3));
-                    out[pos] = x | (y << 12) | ((uint32_t)sc[(r + 1) * sp + cc + 1] << 24);
+            if (sec_ok && nsec > 0) {
+                fast_wave_sync();
+                for (int q = lane; q < nsec; q += kWave) {
+                    const int i = cand[cap - 1 - q];
+                    const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                    int v, x[16];
+                    fast_ring(R, rstride, r + 3, cc + 3, v, x);
+                    uint8_t* sq = sc + (r + 1) * sp + cc + 1;
+                    *sq = (uint8_t)max((int)*sq, max(fast_dir_score(x, v, 1), 0));
                 }
             }
-            written += __popcll(m);
+            fast_wave_sync();
+            // 3. NMS at this pass's threshold; keep its ballots
+            cnt = 0;
+            const int nchunk = (ncand + kWave - 1) / kWave;
+            for (int k = 0; k < nchunk; ++k) {
+                const int q = k * kWave + lane;
+                bool keep = false;
+                if (q < ncand) {
+                    const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
+                    keep = nms_keep(sc, sp, r, i - (int)__umul24(r, ww), t);
+                }
+                const uint64_t m = __ballot(keep);
+                if (lane == 0) kmask[k] = m;
+                cnt += __popcll(m);
+            }
+            fast_wave_sync();
+            if (cnt > 0) break;
+        }
+        // 4. survivors of the deciding pass, row-major
+        uint32_t* out = a.cell_keys + (long long)f * a.slot_total + cur.slot_off;
+        int written = 0;
+        if (cnt > 0) {
+            const int nchunk = (ncand + kWave - 1) / kWave;
+            for (int k = 0; k < nchunk; ++k) {
+                const bool keep = (kmask[k] >> lane) & 1;
+                const uint64_t m = __ballot(keep);
+                if (keep) {
+                    const int pos = written + mask_rank(m);
+                    if (pos < cur.cap) {
+                        const int i = cand[k * kWave + lane] & kCandIdx;
+                        const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                        // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
+                        const uint32_t x = (uint32_t)(cur.x0 + cc + 3 - (kEdge - 3));
+                        const uint32_t y = (uint32_t)(cur.y0 + r + 3 - (kEdge - 3));
+                        out[pos] = x | (y << 12) | ((uint32_t)sc[(r + 1) * sp + cc + 1] << 24);
+                    }
+                }
+                written += __popcll(m);
+            }
         }
         if (lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, cur.cap);
         fast_wave_sync();
@@ -996,7 +1011,11 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 // fixed-point separable kernel and evaluates the 256 tests on
 // it: the blurred level never goes to HBM.  Lane l evaluates tests 4l..4l+3.
 // ---------------------------------------------------------------------------
-constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 42;   // hb pitch: 21 dwords (odd: conflict-free row stores)
+constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 42;
+#ifndef ORB_DESC_SLOTS
+#define ORB_DESC_SLOTS 16
+#endif
+constexpr int kDescSlots = ORB_DESC_SLOTS;   // keypoint slots per wave   // hb pitch: 21 dwords (odd: conflict-free row stores)
 
 struct DescArgs {
     const uint8_t* in;
@@ -1010,10 +1029,38 @@ struct DescArgs {
     float* angle;
     uint8_t* sdesc;
     int out_total, L;
+    const uint8_t* slot_level;      // level of each of the out_total per-frame slots
+    long long nslots;               // frames * out_total
     int fma;
     int kern[7];
     int umax[16];
 };
+
+// One keypoint slot of the flat (frame, quadtree output) space: qt_key, angle
+// and sdesc are all indexed by the slot.
+struct DescKp {
+    const uint8_t* img;
+    int pitch, w, h;
+    uint32_t key;
+};
+
+__device__ __forceinline__ bool desc_slot(const DescArgs& a, long long s, DescKp& k) {
+    const int f = (int)(s / a.out_total);
+    const int o = (int)(s - (long long)f * a.out_total);
+    const int l = a.slot_level[o];
+    const LevelDev& lv = a.lv[l];
+    if (o - lv.out_base >= a.qt_n[f * a.L + l]) return false;
+    const uint8_t* img = l == 0 ? a.in + f * a.in_fstride : a.pyr + f * a.pyr_fstride + lv.off;
+    // wave-uniform: pin to SGPRs
+    const uint64_t ip = (uint64_t)img;
+    k.img = (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ip >> 32)) << 32) |
+                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ip));
+    k.pitch = __builtin_amdgcn_readfirstlane(l == 0 ? a.in_pitch : lv.pitch);
+    k.w = __builtin_amdgcn_readfirstlane(lv.w);
+    k.h = __builtin_amdgcn_readfirstlane(lv.h);
+    k.key = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.qt_key[s]);
+    return true;
+}
 
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1067,72 +1114,76 @@ __device__ __forceinline__ void patch_border(const uint8_t* img, int pitch, int 
 #define ORB_DESC_WAVES 4
 #endif
 #ifndef ORB_Q_UNROLL
-#define ORB_Q_UNROLL 2
+#define ORB_Q_UNROLL 1
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WAVES))) void k_describe(DescArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
     __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][kRaw * kHbP];
-    const int l = blockIdx.x, f = blockIdx.y, lane = lane_id(), wv = wave_id();
+    const int lane = lane_id(), wv = wave_id();
     // lane's 4 tests = 16 consecutive pattern bytes, kept packed in registers
     const uint4 patv = ((const uint4*)c_pattern)[lane];
     const uint32_t patw[4] = {patv.x, patv.y, patv.z, patv.w};
     uint8_t* raw = raw_s[wv];
     uint16_t* hb = hb_s[wv];
-    const LevelDev lv = a.lv[l];
-    const int n = a.qt_n[f * a.L + l];
-    const uint8_t* img;
-    int pitch;
-    if (l == 0) { img = a.in + f * a.in_fstride; pitch = a.in_pitch; }
-    else { img = a.pyr + f * a.pyr_fstride + lv.off; pitch = lv.pitch; }
-    const uint32_t* keys = a.qt_key + (long long)f * a.out_total + lv.out_base;
     // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
     const uint32_t k0 = a.kern[0], k1 = a.kern[1], k2 = a.kern[2], k3 = a.kern[3];
-    const int pstep = gridDim.z * 4;
-    int p = blockIdx.z * 4 + wv;
+    // this wave's run of kDescSlots slots; the next valid slot's patch is
+    // always in flight while the current one is described
+    const long long s_begin = ((long long)blockIdx.x * 4 + wv) * kDescSlots;
+    const long long s_end = min(s_begin + kDescSlots, a.nslots);
     uint32_t pv[kPV];
-    uint32_t key = p < n ? keys[p] : 0u;
-    if (p < n) {
-        const int x0 = (int)(key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((key >> 12) & 0xfff) + (kEdge - 3) - 21;
-        if (patch_interior(lv.w, lv.h, x0, y0)) patch_issue(img, pitch, x0, y0, pv);
+    DescKp cur{}, nxt{};
+    long long s = s_begin;
+    while (s < s_end && !desc_slot(a, s, cur)) ++s;
+    if (s < s_end) {
+        const int x0 = (int)(cur.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((cur.key >> 12) & 0xfff) + (kEdge - 3) - 21;
+        if (patch_interior(cur.w, cur.h, x0, y0)) patch_issue(cur.img, cur.pitch, x0, y0, pv);
     }
-    for (; p < n; p += pstep) {
+    while (s < s_end) {
+        const uint32_t key = cur.key;
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
         // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
         int sh = 0;
-        if (patch_interior(lv.w, lv.h, cx - 21, cy - 21)) {
+        if (patch_interior(cur.w, cur.h, cx - 21, cy - 21)) {
             patch_land(pv, raw);
             sh = (cx - 21) & 3;
         } else {
-            patch_border(img, pitch, lv.w, lv.h, cx - 21, cy - 21, raw);
+            patch_border(cur.img, cur.pitch, cur.w, cur.h, cx - 21, cy - 21, raw);
         }
         // prefetch the next keypoint's patch (in flight during this keypoint)
-        const int pn = p + pstep;
-        uint32_t knext = 0u;
-        if (pn < n) {
-            knext = keys[pn];
-            const int x0 = (int)(knext & 0xfff) + (kEdge - 3) - 21, y0 = (int)((knext >> 12) & 0xfff) + (kEdge - 3) - 21;
-            if (patch_interior(lv.w, lv.h, x0, y0)) patch_issue(img, pitch, x0, y0, pv);
+        long long sn = s + 1;
+        while (sn < s_end && !desc_slot(a, sn, nxt)) ++sn;
+        if (sn < s_end) {
+            const int x0 = (int)(nxt.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((nxt.key >> 12) & 0xfff) + (kEdge - 3) - 21;
+            if (patch_interior(nxt.w, nxt.h, x0, y0)) patch_issue(nxt.img, nxt.pitch, x0, y0, pv);
         }
         const uint8_t* R = raw + sh;
         wave_sync();
-        // 2. IC_Angle on the unblurred disc (centre = R[21][21])
+        // 2. IC_Angle on the unblurred disc (centre = R[21][21]): lanes 0-30 sum
+        //    rows v = 0..8, lanes 32-62 rows v = 9..15 of column u
         int m10 = 0, m01 = 0;
-        if (lane < 2 * kHalfPatch + 1) {
-            const int u = lane - kHalfPatch;
+        {
+            const int u = (lane & 31) - kHalfPatch;
             const uint8_t* c = R + 21 * kRawP + 21;
-            m10 = u * c[u];
+            if ((lane & 31) < 2 * kHalfPatch + 1) {
+                if (lane < 32) m10 = u * c[u];
+                const int v0 = lane < 32 ? 1 : 9;
 #pragma unroll
-            for (int v = 1; v <= kHalfPatch; ++v) {
-                if (u >= -a.umax[v] && u <= a.umax[v]) {
-                    const int up = c[u + v * kRawP], dn = c[u - v * kRawP];
-                    m10 += u * (up + dn);
-                    m01 += v * (up - dn);
+                for (int k = 0; k < 8; ++k) {
+                    const int v = v0 + k;
+                    if (v <= kHalfPatch && u >= -a.umax[v] && u <= a.umax[v]) {
+                        const int up = c[u + v * kRawP], dn = c[u - v * kRawP];
+                        m10 += u * (up + dn);
+                        m01 += v * (up - dn);
+                    }
                 }
             }
         }
         // 3. horizontal pass (ufixedpoint16): lane r holds raw row r in registers
-        //    (3 x ds_read_b128 + v_alignbyte for the column shift) and writes its
-        //    37 outputs row-major as packed dwords
+        //    (3 x ds_read_b128 + v_alignbyte for the column shift), splits it
+        //    into u16 pixel pairs starting at even (E) and odd (O) columns and
+        //    makes two outputs per packed-u16 op (every partial sum fits 16 bits:
+        //    the kernel sums to <= 257); outputs 2m, 2m+1 go out as one dword
         if (lane < kRaw) {
             const uint4* rowp = (const uint4*)(raw + lane * kRawP);
             const uint4 q0 = rowp[0], q1 = rowp[1], q2 = rowp[2];
@@ -1140,24 +1191,35 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             uint32_t al[11];
 #pragma unroll
             for (int j = 0; j < 11; ++j) al[j] = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], (uint32_t)sh);
+            const u16x2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
+            const u16x2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
             uint32_t* orow = (uint32_t*)(hb + lane * kHbP);
-            // 4 outputs per step from the 10 bytes al[g] .. al[g+2] (short live ranges)
+            // E(k) = (p[2k], p[2k+1]), O(k) = (p[2k+1], p[2k+2]); two halves of
+            // the row keep at most ~26 pairs live
+            auto Ep = [&](int k) {
+                return as_u16x2(__builtin_amdgcn_perm(0u, al[k >> 1], (k & 1) ? 0x0c030c02u : 0x0c010c00u));
+            };
+            auto Op = [&](int k) {
+                return (k & 1) ? as_u16x2(__builtin_amdgcn_perm(al[(k >> 1) + 1], al[k >> 1], 0x0c040c03u))
+                               : as_u16x2(__builtin_amdgcn_perm(0u, al[k >> 1], 0x0c020c01u));
+            };
+            auto half = [&](auto mlo_c, auto mhi_c) {
+                constexpr int mlo = decltype(mlo_c)::value, mhi = decltype(mhi_c)::value;
+                u16x2 E[mhi - mlo + 3], O[mhi - mlo + 2];
 #pragma unroll
-            for (int g = 0; g < (kBl + 3) / 4; ++g) {
-                uint32_t px[10];
+                for (int k = 0; k < mhi - mlo + 3; ++k) E[k] = Ep(mlo + k);
 #pragma unroll
-                for (int j = 0; j < 10; ++j) {
-                    const int b = 4 * g + j;
-                    px[j] = b < kRaw ? (al[b >> 2] >> (8 * (b & 3))) & 0xffu : 0u;
+                for (int k = 0; k < mhi - mlo + 2; ++k) O[k] = Op(mlo + k);
+#pragma unroll
+                for (int m = 0; m < mhi - mlo; ++m) {
+                    const u16x2 h = K0 * (E[m] + E[m + 3]) + K1 * (O[m] + O[m + 2]) + K2 * (E[m + 1] + E[m + 2]) +
+                                    K3 * O[m + 1];
+                    orow[mlo + m] = as_u32(h);
                 }
-                uint32_t h[4];
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-                    h[k] = k0 * (px[k] + px[k + 6]) + k1 * (px[k + 1] + px[k + 5]) + k2 * (px[k + 2] + px[k + 4]) +
-                           k3 * px[k + 3];
-                orow[2 * g] = (h[0] & 0xffffu) | (h[1] << 16);
-                if (2 * g + 1 < (kBl + 1) / 2) orow[2 * g + 1] = (h[2] & 0xffffu) | (h[3] << 16);
-            }
+            };
+            half(std::integral_constant<int, 0>{}, std::integral_constant<int, 10>{});
+            __builtin_amdgcn_sched_barrier(0);
+            half(std::integral_constant<int, 10>{}, std::integral_constant<int, (kBl + 1) / 2>{});
         }
         m10 = wave_sum(m10);
         m01 = wave_sum(m01);
@@ -1193,10 +1255,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             nib |= (val[0] < val[1]) << q;
         }
         const int hi = __shfl_down(nib, 1, kWave);
-        uint8_t* d = a.sdesc + ((long long)f * a.out_total + lv.out_base + p) * 32;
+        uint8_t* d = a.sdesc + s * 32;
         if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
-        if (lane == 0) a.angle[(long long)f * a.out_total + lv.out_base + p] = ang_deg;
-        key = knext;
+        if (lane == 0) a.angle[s] = ang_deg;
+        s = sn;
+        cur = nxt;
         wave_sync();
     }
 }
@@ -1309,7 +1372,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     P.slot_total = P0.slot_total; P.out_total = P0.out_total; P.roi_max = P0.roi_max;
     P.roi_dwords = P0.roi_dwords; P.win_max = P0.win_max; P.max_level_cells = P0.max_level_cells;
     P.max_out_cap = P0.max_out_cap; P.xmax = P0.xmax; P.tab_off = P0.tab_off; P.L = L;
-    P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells;
+    P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells; P.d_slot_level = P0.d_slot_level;
     const long long F = f0;
     P.d_pyr = P0.d_pyr + F * P0.pyr_bytes;
     P.d_cell_count = P0.d_cell_count + F * P0.ncells;
@@ -1362,7 +1425,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
     fa.roi_max = (P.roi_max + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
-    const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max);
+    fa.kmask_bytes = ((fa.win_max + kWave - 1) / kWave * 8 + 15) & ~15;
+    const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max + fa.kmask_bytes);
     const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
     const int nv = (P.roi_dwords + kWave - 1) / kWave;
     if (nv <= 12) hipLaunchKernelGGL(k_fast_cells<12>, fgrid, dim3(256), flds, st, fa);
@@ -1390,7 +1454,10 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     da.angle = P.d_angle; da.sdesc = P.d_sdesc; da.out_total = P.out_total; da.L = L;
     da.fma = hd->prm.fma_sampling != 0;
     for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
-    hipLaunchKernelGGL(k_describe, dim3(L, B, 8), dim3(256), 0, st, da);
+    da.slot_level = P.d_slot_level;
+    da.nslots = (long long)B * P.out_total;
+    hipLaunchKernelGGL(k_describe, dim3((unsigned)((da.nslots + 4 * kDescSlots - 1) / (4 * kDescSlots))), dim3(256), 0,
+                       st, da);
     mark();
     // assemble
     AsmArgs aa;

@@ -58,6 +58,23 @@ def summarize(outdir):
                     r[n] = avg[c] / wc
         if avg.get("SQ_LDS_IDX_ACTIVE"):
             r["lds_conflict"] = avg.get("SQ_LDS_BANK_CONFLICT", 0.0) / avg["SQ_LDS_IDX_ACTIVE"]
+        if waves:
+            for c, n in (("SQ_INSTS_VMEM_RD", "vmem_rd_per_wave"), ("SQ_INSTS_VMEM_WR", "vmem_wr_per_wave"),
+                         ("SQ_INSTS_SMEM", "smem_per_wave")):
+                if c in avg:
+                    r[n] = avg[c] / waves
+        if wc:
+            for c, n in (("SQ_WAIT_INST_LDS", "lds_wait"), ("SQ_ACTIVE_INST_LDS", "lds_active"),
+                         ("SQ_ACTIVE_INST_VMEM", "vmem_active")):
+                if c in avg:
+                    r[n] = avg[c] / wc
+        if avg.get("SQ_LDS_IDX_ACTIVE") and "SQ_LDS_ADDR_CONFLICT" in avg:
+            r["lds_addr_conflict"] = avg["SQ_LDS_ADDR_CONFLICT"] / avg["SQ_LDS_IDX_ACTIVE"]
+        if gui_ta := avg.get("GRBM_GUI_ACTIVE"):
+            if "TA_TA_BUSY" in avg:
+                r["ta_busy"] = avg["TA_TA_BUSY"] / (gui_ta / 8 * CUS)
+            if "TA_ADDR_STALLED_BY_TC_CYCLES" in avg:
+                r["ta_addr_stall_tc"] = avg["TA_ADDR_STALLED_BY_TC_CYCLES"] / (gui_ta / 8 * CUS)
         if "FETCH_SIZE" in avg:
             r["fetch_MB_x2"] = 2 * avg["FETCH_SIZE"] / 1024          # FETCH_SIZE is in KB
         if "WRITE_SIZE" in avg:
@@ -78,7 +95,9 @@ def main():
     outdir = sys.argv[1]
     rows = summarize(outdir)
     keys = ["kernel", "dispatches", "us", "waves", "valu_per_wave", "lds_per_wave", "salu_per_wave", "wait",
-            "issue_stall", "active", "lds_conflict", "fetch_MB_x2", "write_MB", "clock_GHz", "valu_issue_frac"]
+            "issue_stall", "active", "lds_conflict", "fetch_MB_x2", "write_MB", "clock_GHz", "valu_issue_frac",
+            "vmem_rd_per_wave", "vmem_wr_per_wave", "smem_per_wave", "lds_wait", "lds_active", "vmem_active",
+            "lds_addr_conflict", "ta_busy", "ta_addr_stall_tc"]
     if "--csv" in sys.argv:
         with open(sys.argv[sys.argv.index("--csv") + 1], "w", newline="") as fh:
             w = csv.DictWriter(fh, fieldnames=keys, extrasaction="ignore")
