@@ -16,6 +16,11 @@ Extra objects on the JSON line:
                events on the extraction stream over the timed steps;
                algorithmic bytes = every pyramid pixel read once
                (sum_l w_l*h_l per frame) x frames per launch.
+               traffic = HBM bytes per launch of the same kernel from the committed
+               rocprofv3 PMC summary (FETCH_SIZE x2 per the gfx950 note +
+               WRITE_SIZE; tools/pmc_profile.sh, same command/config), and
+               valu_issue_frac = its VALU wave-instructions / (2 per CU per
+               cycle) from the same summary: the FAST pass is VALU-bound.
   cpu_baseline the CPU oracle (oracle/, "port") on the host, rank 0, N=1,
                on a bounded sample of the same frames, threads stated; its
                outputs double as a parity check of the sampled frames.
@@ -37,6 +42,7 @@ sys.path.insert(0, str(ROOT))
 
 W, H, NFEAT, LAP = 752, 480, 1000, (0, 1000)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PMC_SUMMARY = ROOT / "profiles" / "pmc_summary_latest.csv"
 METRIC = "frames/s ORB extract+match (752×480, 1000 feat) @1/2/4/8 GPU; bit-exact kp/desc"
 STAGES = ["pyramid", "fast_cells", "quadtree", "describe", "assemble"]
 
@@ -50,8 +56,22 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true")
-    ap.add_argument("--streams", type=int, default=2, help="sub-batch streams per extractor (orbx_set_streams)")
+    ap.add_argument("--pmc-summary", default=str(PMC_SUMMARY), help="rocprofv3 PMC summary (tools/pmc_summary.py)")
+    ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
     return ap.parse_args()
+
+
+def pmc_row(path, kernel):
+    """Row of a tools/pmc_summary.py CSV for `kernel`, or None."""
+    import csv
+    try:
+        with open(path) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["kernel"]:
+                    return row
+    except OSError:
+        pass
+    return None
 
 
 def level_pixels(ex):
@@ -182,10 +202,18 @@ def main():
         px = level_pixels(ex)                          # algorithmic bytes per frame of the FAST pass
         fast_ms = float(stage_ms[1])
         achieved = (px * frames_per_launch / (fast_ms * 1e-3)) / 1e9 if fast_ms > 0 else None
+        pmc = pmc_row(args.pmc_summary, "k_fast_cells")
+        traffic = valu = None
+        if pmc and pmc.get("fetch_MB_x2") and pmc.get("write_MB"):
+            traffic = (float(pmc["fetch_MB_x2"]) + float(pmc["write_MB"])) * 1024 * 1024
+        if pmc and pmc.get("valu_issue_frac"):
+            valu = float(pmc["valu_issue_frac"])
         roof = {"kernel": "k_fast_cells", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": None,
+                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "bytes_per_launch": px * frames_per_launch, "ms_per_launch": fast_ms,
-                "frames_per_launch": frames_per_launch}
+                "frames_per_launch": frames_per_launch,
+                "traffic_source": (os.path.relpath(args.pmc_summary, ROOT) if traffic else None),
+                "valu_issue_frac": valu}
         out = {"metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
