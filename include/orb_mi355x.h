@@ -126,6 +126,31 @@ int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);
  * interface. */
 int orbx_set_streams(orbx_handle* h, int nsub);
 
+/* ---------------- stereo ---------------- */
+
+/* Frame::ComputeStereoMatches (src/Frame.cc:811-981) for one rectified pair:
+ * `left` / `right` are the extractors whose last orbx_extract inputs were the
+ * left / right images (their mvImagePyramid, read on the device); kl/dl and
+ * kr/dr their keypoints (mvKeys, mvKeysRight) and descriptors; mb = baseline
+ * (m), mbf = baseline * fx.  uright / depth (nl floats each) receive
+ * mvuRight / mvDepth, -1 where no match.  The reference reads vDistIdx[0] of an
+ * empty list when nothing matches; here that case leaves every entry at -1. */
+int orbs_compute_stereo_matches(orbx_handle* left, orbx_handle* right,
+                                const orb_keypoint* kl, int nl, const uint8_t* dl,
+                                const orb_keypoint* kr, int nr, const uint8_t* dr,
+                                float mb, float mbf, float* uright, float* depth);
+
+/* Batched, HBM-resident form: pairs i = 0..npairs-1 are frames left0+i and
+ * right0+i of the last orbx_extract_batch_device call on h (whose frame buffer
+ * must still hold them); d_kps/d_desc/d_n/cap are that call's outputs.
+ * d_uright/d_depth/d_sad are [npairs][cap] (d_sad: the correlation distance of
+ * kept matches before the median cut, -1 otherwise). */
+int orbs_compute_stereo_matches_batch_device(orbx_handle* h, int npairs, int left0, int right0,
+                                             const orb_keypoint* d_kps, const uint8_t* d_desc,
+                                             const int32_t* d_n, int cap, float mb, float mbf,
+                                             float* d_uright, float* d_depth, int32_t* d_sad,
+                                             void* stream);
+
 /* ---------------- matcher ---------------- */
 
 /* ORBmatcher::DescriptorDistance / DBoW2::FORB::distance

@@ -86,6 +86,22 @@ private:
     std::vector<float> scale_, inv_scale_, sigma2_, inv_sigma2_;
 };
 
+// Frame::ComputeStereoMatches (src/Frame.cc:811-981) for a rectified pair whose
+// images were the last inputs of `left` / `right`: fills mvuRight / mvDepth
+// (-1 where unmatched).  mb = baseline, mbf = baseline * fx.
+inline void ComputeStereoMatches(const ORBextractor& left, const ORBextractor& right,
+                                 const std::vector<KeyPoint>& mvKeys, const Descriptors& mDescriptors,
+                                 const std::vector<KeyPoint>& mvKeysRight, const Descriptors& mDescriptorsRight,
+                                 float mb, float mbf, std::vector<float>& mvuRight, std::vector<float>& mvDepth) {
+    mvuRight.assign(mvKeys.size(), -1.0f);
+    mvDepth.assign(mvKeys.size(), -1.0f);
+    const int rc = orbs_compute_stereo_matches(left.handle(), right.handle(), mvKeys.data(), (int)mvKeys.size(),
+                                               mDescriptors.data.data(), mvKeysRight.data(), (int)mvKeysRight.size(),
+                                               mDescriptorsRight.data.data(), mb, mbf, mvuRight.data(),
+                                               mvDepth.data());
+    if (rc != ORB_OK) throw std::runtime_error("ComputeStereoMatches failed");
+}
+
 class ORBmatcher {
 public:
     static const int TH_HIGH = 100, TH_LOW = 50, HISTO_LENGTH = 30;

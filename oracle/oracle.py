@@ -53,6 +53,7 @@ def lib():
         L.orbo_search_by_projection_mps.argtypes = [vp, vp, f32, i32, f32, f32, vp, vp]
         L.orbo_search_by_projection_last.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, vp]
         L.orbo_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp]
+        L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
         _lib = L
     return _lib
 
@@ -192,3 +193,20 @@ def transform(voc: abi.Keep, desc: np.ndarray, levelsup: int = 4):
     nid = np.zeros(n, np.int32)
     lib().orbo_transform(voc.ref(), n, abi.ptr(desc), levelsup, abi.ptr(wid), abi.ptr(w), abi.ptr(nid))
     return wid, w, nid
+
+
+def compute_stereo_matches(ex_left: "OracleExtractor", ex_right: "OracleExtractor", kl, dl, kr, dr,
+                           mb: float, mbf: float):
+    """Frame::ComputeStereoMatches on the last images of the two extractors:
+    (mvuRight, mvDepth) as float32 arrays."""
+    t = ex_left.tables()
+    kl = np.ascontiguousarray(kl, abi.KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(kr, abi.KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(dl, np.uint8)
+    dr = np.ascontiguousarray(dr, np.uint8)
+    ur = np.zeros(len(kl), np.float32)
+    dep = np.zeros(len(kl), np.float32)
+    lib().orbo_compute_stereo_matches(ex_left.h, ex_right.h, abi.ptr(kl), len(kl), abi.ptr(dl), abi.ptr(kr), len(kr),
+                                      abi.ptr(dr), abi.ptr(t["scale"]), abi.ptr(t["inv_scale"]), mb, mbf,
+                                      abi.ptr(ur), abi.ptr(dep))
+    return ur, dep

@@ -963,4 +963,98 @@ int orbo_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
     return 0;
 }
 
+// Frame::ComputeStereoMatches (src/Frame.cc:811-981) for a rectified pair whose
+// left/right images were the last inputs of the extractors hl/hr (their
+// mvImagePyramid).  kl/kr are the extractors' keypoints (mvKeys, mvKeysRight),
+// scale/inv_scale the level tables.  uright/depth receive mvuRight/mvDepth.
+int orbo_compute_stereo_matches(void* hl, void* hr, const orb_keypoint* kl, int nl, const uint8_t* dl,
+                                const orb_keypoint* kr, int nr, const uint8_t* dr, const float* scale,
+                                const float* inv_scale, float mb, float mbf, float* uright, float* depth) {
+    const Extractor* el = static_cast<const Extractor*>(hl);
+    const Extractor* er = static_cast<const Extractor*>(hr);
+    for (int i = 0; i < nl; ++i) uright[i] = depth[i] = -1.0f;                       // :813-814
+    const int thOrbDist = (kThHigh + kThLow) / 2;                                    // :816
+    const int nRows = el->pyr[0].h;                                                  // :818
+    std::vector<std::vector<int>> rows(nRows);                                       // :821
+    for (int iR = 0; iR < nr; ++iR) {                                                // :828-838
+        const float kpY = kr[iR].y;
+        const float r = 2.0f * scale[kr[iR].octave];
+        const int maxr = (int)std::ceil(kpY + r);
+        const int minr = (int)std::floor(kpY - r);
+        for (int yi = minr; yi <= maxr; ++yi)
+            if (yi >= 0 && yi < nRows) rows[yi].push_back(iR);
+    }
+    const float minZ = mb, minD = 0, maxD = mbf / minZ;                              // :841-843
+    std::vector<std::pair<int, int>> dist_idx;                                        // :846
+    for (int iL = 0; iL < nl; ++iL) {
+        const orb_keypoint& kpL = kl[iL];
+        const int levelL = kpL.octave;
+        const float vL = kpL.y, uL = kpL.x;
+        const std::vector<int>& cand = rows[(size_t)vL];                             // :856
+        if (cand.empty()) continue;
+        const float minU = uL - maxD, maxU = uL - minD;                              // :861-862
+        if (maxU < 0) continue;
+        int bestDist = kThHigh;                                                      // :867-868
+        int bestIdxR = 0;
+        for (int iR : cand) {                                                        // :873-893
+            const orb_keypoint& kpR = kr[iR];
+            if (kpR.octave < levelL - 1 || kpR.octave > levelL + 1) continue;
+            const float uR = kpR.x;
+            if (uR >= minU && uR <= maxU) {
+                const int dist = hamming(dl + (size_t)iL * 32, dr + (size_t)iR * 32);
+                if (dist < bestDist) { bestDist = dist; bestIdxR = iR; }
+            }
+        }
+        if (bestDist >= thOrbDist) continue;                                         // :896
+        // sub-pixel match by 11-position L1 correlation at the keypoint's level (:898-933)
+        const float uR0 = kr[bestIdxR].x;
+        const float sf = inv_scale[kpL.octave];
+        const float scaleduL = std::round(kpL.x * sf), scaledvL = std::round(kpL.y * sf);
+        const float scaleduR0 = std::round(uR0 * sf);
+        const int w = 5, L = 5;
+        const Img& IL = el->pyr[kpL.octave];
+        const Img& IR = er->pyr[kpL.octave];
+        const float iniu = scaleduR0 + L - w, endu = scaleduR0 + L + w + 1;
+        if (iniu < 0 || endu >= IR.w) continue;
+        int bestSad = INT32_MAX, bestincR = 0;
+        float dists[2 * L + 1];
+        const int yl0 = (int)scaledvL - w, xl0 = (int)scaleduL - w;
+        for (int incR = -L; incR <= L; ++incR) {
+            const int xr0 = (int)scaleduR0 + incR - w;
+            int sad = 0;
+            for (int y = 0; y < 2 * w + 1; ++y)
+                for (int x = 0; x < 2 * w + 1; ++x)
+                    sad += std::abs((int)IL.row(yl0 + y)[xl0 + x] - (int)IR.row(yl0 + y)[xr0 + x]);
+            const float dist = (float)(double)sad;                                   // cv::norm(NORM_L1) -> double
+            if (dist < bestSad) { bestSad = (int)dist; bestincR = incR; }
+            dists[L + incR] = dist;
+        }
+        if (bestincR == -L || bestincR == L) continue;                               // :935-936
+        const float d1 = dists[L + bestincR - 1], d2 = dists[L + bestincR], d3 = dists[L + bestincR + 1];
+        const float deltaR = (d1 - d3) / (2.0f * (d1 + d3 - 2.0f * d2));             // :943
+        if (deltaR < -1 || deltaR > 1) continue;
+        float bestuR = scale[kpL.octave] * ((float)scaleduR0 + (float)bestincR + deltaR);   // :949
+        float disparity = uL - bestuR;
+        if (disparity >= minD && disparity < maxD) {                                 // :953-964
+            if (disparity <= 0) {
+                disparity = 0.01;
+                bestuR = uL - 0.01;
+            }
+            depth[iL] = mbf / disparity;
+            uright[iL] = bestuR;
+            dist_idx.push_back(std::make_pair(bestSad, iL));
+        }
+    }
+    if (dist_idx.empty()) return 0;      // the reference reads vDistIdx[0] here (undefined)
+    std::sort(dist_idx.begin(), dist_idx.end());                                     // :968-971
+    const float median = dist_idx[dist_idx.size() / 2].first;
+    const float thDist = 1.5f * 1.4f * median;
+    for (int i = (int)dist_idx.size() - 1; i >= 0; --i) {                           // :973-980
+        if (dist_idx[i].first < thDist) break;
+        uright[dist_idx[i].second] = -1;
+        depth[dist_idx[i].second] = -1;
+    }
+    return 0;
+}
+
 }  // extern "C"

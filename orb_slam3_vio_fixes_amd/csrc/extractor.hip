@@ -28,7 +28,6 @@
 
 namespace orbmi {
 
-constexpr int kMaxLevels = 32;
 constexpr int kHalfPatch = 15;
 constexpr int kEdge = 19;
 constexpr int kMinSubFrames = 16;   // smallest frame range worth its own stream
@@ -38,90 +37,9 @@ static const int8_t h_pattern[1024] = {
 #include "brief_pattern.inc"
 };
 
-// ---------------------------------------------------------------------------
-// Plan: everything that depends only on (params, w, h), computed once on the
-// host with the reference's own float/double expressions.
-// ---------------------------------------------------------------------------
-struct LevelDev {
-    int w, h, pitch;
-    long long off;      // byte offset of the level inside one frame's pyramid slab (l >= 1)
-    float scale;
-    int patch;          // int(PATCH_SIZE * scale)  (ORBextractor.cc:880)
-    // quadtree (DistributeOctTree arguments, ORBextractor.cc:877-878)
-    int qW, qH, N, nIni;
-    float hX;
-    int cell_base, ncells, slot_base, slot_total;   // cells / key slots of this level
-    int out_base, out_cap;                          // quadtree output slots
-};
-
-struct CellDev {
-    int level;
-    int x0, y0, cols, rows;   // ROI in level coordinates (ORBextractor.cc:807-826)
-    int slot_off, cap;        // key slots (u32) relative to the frame's slot slab
-};
-
-struct Plan {
-    int w = 0, h = 0, L = 0, maxB = 0;
-    std::vector<LevelDev> lv;
-    std::vector<CellDev> cells;
-    long long pyr_bytes = 0;
-    int ncells = 0, slot_total = 0, out_total = 0;
-    int roi_max = 0, roi_dwords = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
-    std::vector<int> xmax;           // per level
-    std::vector<std::vector<int>> ytab_host;   // per level: source row of each output row
-    std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
-    // device
-    uint8_t *d_pyr = nullptr, *d_in = nullptr;
-    int2* d_tab = nullptr;
-    LevelDev* d_lv = nullptr;
-    CellDev* d_cells = nullptr;
-    int* d_cell_count = nullptr;
-    uint32_t *d_cell_keys = nullptr, *d_key_scr = nullptr;
-    int* d_knode = nullptr;
-    uint8_t* d_kq = nullptr;
-    uint32_t* d_qt_key = nullptr;
-    int* d_qt_n = nullptr;
-    float* d_angle = nullptr;
-    uint8_t* d_sdesc = nullptr;
-    uint8_t* d_slot_level = nullptr;
-    // single-image host path outputs
-    orb_keypoint* d_kps = nullptr;
-    uint8_t* d_desc = nullptr;
-    int32_t *d_n = nullptr, *d_mono = nullptr;
-    int host_cap = 0;
-    size_t in_pitch = 0;
-
-    void release() {
-        void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
-                      d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level};
-        for (void* p : ps)
-            if (p) (void)hipFree(p);
-        *this = Plan();
-    }
-};
-
 }  // namespace orbmi
 
-struct orbx_handle {
-    orbx_params prm{};
-    int device = 0;
-    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
-    std::vector<int> nfeat, umax;
-    orbmi::Plan plan;
-    bool have_last = false;
-    int last_w = 0, last_h = 0;
-    // optional per-stage HIP-event timing (orbx_set_profiling)
-    bool profiling = false;
-    std::vector<hipEvent_t> ev_pool;
-    std::vector<std::vector<hipEvent_t>> ev_calls;
-    size_t ev_next = 0;
-    // sub-batch streams (orbx_set_streams)
-    int nsub = 2;
-    std::vector<hipStream_t> sub_streams;
-    std::vector<hipEvent_t> sub_done;
-    hipEvent_t fork_ev = nullptr;
-};
+#include "plan.h"
 
 namespace orbmi {
 
@@ -180,7 +98,6 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     std::vector<int2> tab;
     P.xmax.assign(L, 0);
     P.tab_off.assign(L, 0);
-    P.ytab_host.assign(L, {});
     long long poff = 0;
     int cellsum = 0, slotsum = 0, outsum = 0;
     for (int l = 0; l < L; ++l) {
@@ -223,7 +140,6 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
                 fy -= sy;
                 const int b0 = sat_short((1.f - fy) * 2048.f), b1 = sat_short(fy * 2048.f);
                 tab.push_back(make_int2(sy, (b0 & 0xffff) | (b1 << 16)));
-                P.ytab_host[l].push_back(sy);
             }
             P.xmax[l] = xmax;
         }
@@ -1538,6 +1454,7 @@ void orbx_destroy(orbx_handle* h) {
     for (hipEvent_t e : h->sub_done) (void)hipEventDestroy(e);
     for (hipStream_t s : h->sub_streams) (void)hipStreamDestroy(s);
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+    if (h->st_scratch) (void)hipFree(h->st_scratch);
     delete h;
 }
 
@@ -1573,6 +1490,10 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     int rc = build_plan(h, w, hh, std::max(nframes, h->plan.maxB));
     if (rc) return rc;
     if (cap < h->plan.out_total) return ORB_ERR_CAPACITY;
+    h->last_frames = d_frames;
+    h->last_fstride = (long long)frame_stride;
+    h->last_pitch0 = (int)row_step;
+    h->last_B = nframes;
     return run_batched(h, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
                        d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
 }

@@ -1,0 +1,102 @@
+// plan.h — extractor plan and handle (shared by extractor.hip and stereo.hip).
+#pragma once
+#include "../../include/orb_mi355x.h"
+#include "common.h"
+
+#include <vector>
+
+namespace orbmi {
+
+constexpr int kMaxLevels = 32;
+
+// ---------------------------------------------------------------------------
+// Plan: everything that depends only on (params, w, h), computed once on the
+// host with the reference's own float/double expressions.
+// ---------------------------------------------------------------------------
+struct LevelDev {
+    int w, h, pitch;
+    long long off;      // byte offset of the level inside one frame's pyramid slab (l >= 1)
+    float scale;
+    int patch;          // int(PATCH_SIZE * scale)  (ORBextractor.cc:880)
+    // quadtree (DistributeOctTree arguments, ORBextractor.cc:877-878)
+    int qW, qH, N, nIni;
+    float hX;
+    int cell_base, ncells, slot_base, slot_total;   // cells / key slots of this level
+    int out_base, out_cap;                          // quadtree output slots
+};
+
+struct CellDev {
+    int level;
+    int x0, y0, cols, rows;   // ROI in level coordinates (ORBextractor.cc:807-826)
+    int slot_off, cap;        // key slots (u32) relative to the frame's slot slab
+};
+
+struct Plan {
+    int w = 0, h = 0, L = 0, maxB = 0;
+    std::vector<LevelDev> lv;
+    std::vector<CellDev> cells;
+    long long pyr_bytes = 0;
+    int ncells = 0, slot_total = 0, out_total = 0;
+    int roi_max = 0, roi_dwords = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
+    std::vector<int> xmax;           // per level
+    std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
+    // device
+    uint8_t *d_pyr = nullptr, *d_in = nullptr;
+    int2* d_tab = nullptr;
+    LevelDev* d_lv = nullptr;
+    CellDev* d_cells = nullptr;
+    int* d_cell_count = nullptr;
+    uint32_t *d_cell_keys = nullptr, *d_key_scr = nullptr;
+    int* d_knode = nullptr;
+    uint8_t* d_kq = nullptr;
+    uint32_t* d_qt_key = nullptr;
+    int* d_qt_n = nullptr;
+    float* d_angle = nullptr;
+    uint8_t* d_sdesc = nullptr;
+    uint8_t* d_slot_level = nullptr;
+    // single-image host path outputs
+    orb_keypoint* d_kps = nullptr;
+    uint8_t* d_desc = nullptr;
+    int32_t *d_n = nullptr, *d_mono = nullptr;
+    int host_cap = 0;
+    size_t in_pitch = 0;
+
+    void release() {
+        void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
+                      d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
+                      d_slot_level};
+        for (void* p : ps)
+            if (p) (void)hipFree(p);
+        *this = Plan();
+    }
+};
+
+}  // namespace orbmi
+
+struct orbx_handle {
+    orbx_params prm{};
+    int device = 0;
+    std::vector<float> scale, inv_scale, sigma2, inv_sigma2;
+    std::vector<int> nfeat, umax;
+    orbmi::Plan plan;
+    bool have_last = false;
+    int last_w = 0, last_h = 0;
+    // optional per-stage HIP-event timing (orbx_set_profiling)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::vector<hipEvent_t>> ev_calls;
+    size_t ev_next = 0;
+    // sub-batch streams (orbx_set_streams)
+    int nsub = 1;
+    std::vector<hipStream_t> sub_streams;
+    std::vector<hipEvent_t> sub_done;
+    hipEvent_t fork_ev = nullptr;
+    // frames of the last orbx_extract_batch_device call (level 0 of its
+    // pyramid; levels >= 1 stay in plan.d_pyr until the next call)
+    const uint8_t* last_frames = nullptr;
+    long long last_fstride = 0;
+    int last_pitch0 = 0, last_B = 0;
+    // device scratch of the stereo matcher (stereo.hip), grown on demand
+    void* st_scratch = nullptr;
+    size_t st_scratch_bytes = 0;
+};

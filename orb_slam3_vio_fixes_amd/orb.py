@@ -117,6 +117,41 @@ class ORBextractor:
         return kps, desc, n, mono, cap
 
 
+def ComputeStereoMatches(ex_left: ORBextractor, ex_right: ORBextractor, mvKeys, mDescriptors, mvKeysRight,
+                         mDescriptorsRight, mb: float, mbf: float):
+    """Frame::ComputeStereoMatches (Frame.cc:811-981) on the GPU pyramids of the
+    last images given to the two extractors: returns (mvuRight, mvDepth)."""
+    kl = np.ascontiguousarray(mvKeys, abi.KEYPOINT_DTYPE)
+    kr = np.ascontiguousarray(mvKeysRight, abi.KEYPOINT_DTYPE)
+    dl = np.ascontiguousarray(mDescriptors, np.uint8).reshape(-1, 32)
+    dr = np.ascontiguousarray(mDescriptorsRight, np.uint8).reshape(-1, 32)
+    ur = np.full(len(kl), -1.0, np.float32)
+    dep = np.full(len(kl), -1.0, np.float32)
+    capi.check(capi.lib().orbs_compute_stereo_matches(ex_left._h, ex_right._h, abi.ptr(kl), len(kl), abi.ptr(dl),
+                                                      abi.ptr(kr), len(kr), abi.ptr(dr), mb, mbf, abi.ptr(ur),
+                                                      abi.ptr(dep)), "orbs_compute_stereo_matches")
+    return ur, dep
+
+
+def compute_stereo_matches_batch_device(ex: ORBextractor, npairs: int, left0: int, right0: int, kps, desc, n,
+                                        cap: int, mb: float, mbf: float, stream=None):
+    """Batched stereo matching on the outputs of ``ex.extract_batch_device``
+    (pairs = frames left0+i / right0+i of that batch).  Returns CUDA tensors
+    (uright, depth, sad), each (npairs, cap)."""
+    import torch
+    dev = kps.device
+    ur = torch.empty((npairs, cap), dtype=torch.float32, device=dev)
+    dep = torch.empty((npairs, cap), dtype=torch.float32, device=dev)
+    sad = torch.empty((npairs, cap), dtype=torch.int32, device=dev)
+    st = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    rc = capi.lib().orbs_compute_stereo_matches_batch_device(ex._h, npairs, left0, right0, kps.data_ptr(),
+                                                             desc.data_ptr(), n.data_ptr(), cap, mb, mbf,
+                                                             ur.data_ptr(), dep.data_ptr(), sad.data_ptr(),
+                                                             C.c_void_p(st))
+    capi.check(rc, "orbs_compute_stereo_matches_batch_device")
+    return ur, dep, sad
+
+
 def keypoints_from_device(kps_i32) -> np.ndarray:
     """(cap, 7) int32 tensor/array -> structured KEYPOINT_DTYPE array."""
     a = np.ascontiguousarray(kps_i32.cpu().numpy() if hasattr(kps_i32, "cpu") else kps_i32, dtype=np.int32)

@@ -64,18 +64,30 @@ def image(w: int, h: int, seed: int, n_shapes: int | None = None) -> np.ndarray:
     return np.clip(np.rint(img), 0, 255).astype(np.uint8)
 
 
-def stereo_pair(w: int, h: int, seed: int) -> tuple[np.ndarray, np.ndarray]:
-    """Left image and a right image shifted by a 0-48 px per-row disparity."""
-    left = image(w, h, seed)
+def right_view(left: np.ndarray, seed: int) -> np.ndarray:
+    """Right image of a rectified pair: ``left`` shifted by a smooth 0-48 px
+    per-row disparity (integer), plus independent sensor noise."""
+    h, w = left.shape
     rng = np.random.default_rng(seed + 7_000_000)
     knots = rng.integers(0, 49, 9)
     disp = np.rint(np.interp(np.arange(h), np.linspace(0, h - 1, 9), knots)).astype(np.int64)
-    right = np.empty_like(left)
     cols = np.arange(w)
-    for y in range(h):
-        right[y] = left[y, np.clip(cols + disp[y], 0, w - 1)]
+    right = left[np.arange(h)[:, None], np.clip(cols[None, :] + disp[:, None], 0, w - 1)]
     noise = rng.integers(-2, 3, size=left.shape)
-    right = np.clip(right.astype(np.int64) + noise, 0, 255).astype(np.uint8)
+    return np.clip(right.astype(np.int64) + noise, 0, 255).astype(np.uint8)
+
+
+def stereo_pair(w: int, h: int, seed: int) -> tuple[np.ndarray, np.ndarray]:
+    """Left image and a right image shifted by a 0-48 px per-row disparity."""
+    left = image(w, h, seed)
+    return left, right_view(left, seed)
+
+
+def stereo_sequence(w: int, h: int, npairs: int, config: int = 3, start: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """(npairs, h, w) left frames of a panning camera (``sequence``) and their
+    right views (``right_view``, seeded per frame)."""
+    left = sequence(w, h, npairs, config=config, start=start)
+    right = np.stack([right_view(left[i], frame_seed(config, start + i)) for i in range(npairs)])
     return left, right
 
 

@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Measurement of the SURVEY.md §8(f) row-1 workload (config C3): rectified
+752x480 stereo pairs, ORBextractor(1200, 1.2, 8, 20, 7) with lapping {0, 0}
+on left and right, Frame::ComputeStereoMatches (Frame.cc:811-981) on every
+pair, SearchForInitialization(window 100, 0.9, checkOri) on consecutive left
+frames (Tracking.cc:2459-2492).  One step = one batch of B pairs resident in
+HBM (left and right frames extracted in one launch chain).  Prints one JSON
+line with pairs/s, per-stage times (HIP events), a CPU-oracle baseline on a
+bounded sample and the parity of that sample.
+
+usage: python tools/bench_stereo.py [--pairs 128] [--steps 10] [--warmup 2]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import sys
+import time
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+W, H, NFEAT, LAP = 752, 480, 1200, (0, 0)
+FX, BASE = 435.2, 0.11            # EuRoC-like rectified rig
+MBF = float(np.float32(BASE) * np.float32(FX))
+
+
+def cpu_baseline(left, right, threads):
+    from oracle import oracle as O
+    O.lib()                      # load (and build if stale) once, before the worker threads
+    n = len(left)
+    outs = [None] * n
+
+    def work(t):
+        el, er = O.OracleExtractor(NFEAT, 1.2, 8, 20, 7), O.OracleExtractor(NFEAT, 1.2, 8, 20, 7)
+        for i in range(t, n, threads):
+            kl, dl, _ = el(left[i], LAP)
+            kr, dr, _ = er(right[i], LAP)
+            outs[i] = (kl, O.compute_stereo_matches(el, er, kl, dl, kr, dr, BASE, MBF))
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as pool:
+        list(pool.map(work, range(threads)))
+    return n / (time.perf_counter() - t0), outs
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=128)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--cpu-sample", type=int, default=64)
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    args = ap.parse_args()
+    import torch
+    from orb_slam3_vio_fixes_amd import capi, orb, synth
+    dev = torch.device("cuda", 0)
+    P = args.pairs
+    left, right = synth.stereo_sequence(W, H, P, config=3)
+    frames = torch.from_numpy(np.concatenate([left, right])).to(dev)
+    ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7)
+    L = capi.lib()
+    stream = torch.cuda.current_stream(dev)
+    kps, desc, n, mono, cap = ex.extract_batch_device(frames, LAP)
+    ur = torch.empty((P, cap), dtype=torch.float32, device=dev)
+    dep = torch.empty_like(ur)
+    sad = torch.empty((P, cap), dtype=torch.int32, device=dev)
+    matches = torch.empty((P - 1, cap), dtype=torch.int32, device=dev)
+    nmatch = torch.empty(P - 1, dtype=torch.int32, device=dev)
+    inv_w = float(np.float32(64) / np.float32(W))
+    inv_h = float(np.float32(48) / np.float32(H))
+    ev = []
+
+    def step(timed=False):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        if timed:
+            e[0].record(stream)
+        ex.extract_batch_device(frames, LAP, out=(kps, desc, n, mono))
+        if timed:
+            e[1].record(stream)
+        capi.check(L.orbs_compute_stereo_matches_batch_device(ex._h, P, 0, P, kps.data_ptr(), desc.data_ptr(),
+                                                              n.data_ptr(), cap, BASE, MBF, ur.data_ptr(),
+                                                              dep.data_ptr(), sad.data_ptr(), stream.cuda_stream),
+                   "stereo")
+        if timed:
+            e[2].record(stream)
+        capi.check(L.orbm_search_for_initialization_batch_device(
+            P, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
+            100, 0.9, 1, matches.data_ptr(), nmatch.data_ptr(), stream.cuda_stream), "sfi")
+        if timed:
+            e[3].record(stream)
+            ev.append(e)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(timed=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stage = {k: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in ev]))
+             for i, k in enumerate(["extract_2B_images", "compute_stereo_matches", "search_for_initialization"])}
+    out = {"metric": "stereo pairs/s (752x480 L+R ORB extract, ComputeStereoMatches, SearchForInitialization)",
+           "value": P * args.steps / dt, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": "C3: 752x480 rectified stereo, ORBextractor(1200,1.2,8,20,7), lapping {0,0}, "
+                                  "mb 0.11 m, fx 435.2", "pairs_per_step": P},
+           "stage_ms": stage}
+    if args.cpu_sample > 0:
+        ns = min(args.cpu_sample, P)
+        fps, outs = cpu_baseline(left[:ns], right[:ns], args.cpu_threads)
+        urh, deph, nh = ur.cpu().numpy(), dep.cpu().numpy(), n.cpu().numpy()
+        bad = 0
+        for i in range(ns):
+            rk, (rur, rdep) = outs[i]
+            if nh[i] != len(rk) or not np.array_equal(urh[i, :nh[i]].view(np.uint32), rur.view(np.uint32)) or \
+                    not np.array_equal(deph[i, :nh[i]].view(np.uint32), rdep.view(np.uint32)):
+                bad += 1
+        out["cpu_baseline"] = {"value": fps, "unit": "pairs/s", "cores": args.cpu_threads, "kind": "port",
+                               "sample": f"first {ns} pairs: oracle extraction of L and R + ComputeStereoMatches"}
+        out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad,
+                         "matched_fraction": float(np.mean([(o[1][0] >= 0).mean() for o in outs]))}
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
