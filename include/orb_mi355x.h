@@ -151,6 +151,25 @@ int orbs_compute_stereo_matches_batch_device(orbx_handle* h, int npairs, int lef
                                              float* d_uright, float* d_depth, int32_t* d_sad,
                                              void* stream);
 
+/* cv::BFMatcher(NORM_HAMMING).knnMatch(query, train, matches, 2) as used by
+ * Frame::ComputeStereoFishEyeMatches (src/Frame.cc:1144): idx/dist are
+ * [nq][2] (host), the two nearest train rows per query in (distance, index)
+ * order, -1 where fewer than two train rows exist. */
+int orbs_knn_match2(const uint8_t* query, int nq, const uint8_t* train, int nt,
+                    int32_t* idx, int32_t* dist, int device);
+
+/* Batched, HBM-resident fisheye stereo candidates (Frame.cc:1126-1156): for
+ * pair p, the lapping-area rows [mono, n) of frame left0+p (queries) against
+ * those of frame right0+p (train) from the outputs of one
+ * orbx_extract_batch_device call; d_idx/d_dist [npairs][cap][2] and
+ * d_l2r [npairs][cap] (absolute right row passing Lowe's ratio, -1 otherwise)
+ * are indexed by absolute left row.  The triangulation check of each candidate
+ * (KannalaBrandt8::TriangulateMatches, :1155) stays with the caller. */
+int orbs_fisheye_stereo_candidates_batch_device(int npairs, int left0, int right0, const uint8_t* d_desc,
+                                                const int32_t* d_n, const int32_t* d_mono, int cap,
+                                                double ratio, int32_t* d_idx, int32_t* d_dist,
+                                                int32_t* d_l2r, void* stream);
+
 /* ---------------- matcher ---------------- */
 
 /* ORBmatcher::DescriptorDistance / DBoW2::FORB::distance

@@ -53,6 +53,7 @@ def lib():
         L.orbo_search_by_projection_mps.argtypes = [vp, vp, f32, i32, f32, f32, vp, vp]
         L.orbo_search_by_projection_last.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, vp]
         L.orbo_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp]
+        L.orbo_knn_match2.argtypes = [vp, i32, vp, i32, vp, vp]
         L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
         _lib = L
     return _lib
@@ -210,3 +211,13 @@ def compute_stereo_matches(ex_left: "OracleExtractor", ex_right: "OracleExtracto
                                       abi.ptr(dr), abi.ptr(t["scale"]), abi.ptr(t["inv_scale"]), mb, mbf,
                                       abi.ptr(ur), abi.ptr(dep))
     return ur, dep
+
+
+def knn_match2(query: np.ndarray, train: np.ndarray):
+    """BFMatcher(NORM_HAMMING).knnMatch(query, train, 2): (idx, dist), each (nq, 2), -1 if missing."""
+    q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.int32)
+    lib().orbo_knn_match2(abi.ptr(q), len(q), abi.ptr(t), len(t), abi.ptr(idx), abi.ptr(dist))
+    return idx, dist

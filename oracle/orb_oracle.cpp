@@ -1057,4 +1057,30 @@ int orbo_compute_stereo_matches(void* hl, void* hr, const orb_keypoint* kl, int 
     return 0;
 }
 
+// cv::BFMatcher(NORM_HAMMING).knnMatch(query, train, matches, 2) as called by
+// Frame::ComputeStereoFishEyeMatches (src/Frame.cc:1144; BFmatcher :43):
+// per query the two nearest train rows, OpenCV batchDistance's insertion
+// (strict '<' against the current 2nd best, equal distances keep index
+// order).  idx/dist are [nq][2], -1 where fewer than two train rows exist.
+int orbo_knn_match2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t* idx, int32_t* dist) {
+    for (int i = 0; i < nq; ++i) {
+        int bi[2] = {-1, -1};
+        int bd[2] = {INT32_MAX, INT32_MAX};
+        for (int j = 0; j < nt; ++j) {
+            const int d = hamming(q + (size_t)i * 32, t + (size_t)j * 32);
+            if (d < bd[1]) {
+                int k = 0;
+                for (k = 0; k >= 0 && bd[k] > d; --k) { bi[k + 1] = bi[k]; bd[k + 1] = bd[k]; }
+                bi[k + 1] = j;
+                bd[k + 1] = d;
+            }
+        }
+        for (int k = 0; k < 2; ++k) {
+            idx[2 * i + k] = bi[k];
+            dist[2 * i + k] = bi[k] >= 0 ? bd[k] : -1;
+        }
+    }
+    return 0;
+}
+
 }  // extern "C"

@@ -18,6 +18,7 @@ EXPORTS = [
     "orbm_search_for_initialization_batch_device", "orbm_search_by_bow", "orbm_search_by_projection_mps",
     "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device",
     "orbx_set_streams", "orbs_compute_stereo_matches", "orbs_compute_stereo_matches_batch_device",
+    "orbs_knn_match2", "orbs_fisheye_stereo_candidates_batch_device",
 ]
 
 _lib = None
@@ -48,6 +49,9 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_get_profile.argtypes = [vp, vp, i32]
     L.orbm_search_by_bow_batch_device.argtypes = [vp, vp, vp, f32, i32, vp, vp, vp]
     L.orbx_set_streams.argtypes = [vp, i32]
+    L.orbs_knn_match2.argtypes = [vp, i32, vp, i32, vp, vp, i32]
+    L.orbs_fisheye_stereo_candidates_batch_device.argtypes = [i32, i32, i32, vp, vp, vp, i32, C.c_double, vp, vp,
+                                                              vp, vp]
     L.orbs_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, f32, f32, vp, vp]
     L.orbs_compute_stereo_matches_batch_device.argtypes = [vp, i32, i32, i32, vp, vp, vp, i32, f32, f32, vp, vp, vp,
                                                            vp]

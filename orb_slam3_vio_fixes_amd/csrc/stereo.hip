@@ -275,6 +275,85 @@ __global__ __launch_bounds__(256) void k_stereo_prune(StereoArgs a, int np2) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Frame::ComputeStereoFishEyeMatches (Frame.cc:1126-1166): brute-force
+// BFMatcher(NORM_HAMMING).knnMatch(k = 2) of the left lapping-area
+// descriptors against the right ones and Lowe's 0.7 ratio.  One query per
+// thread (its 32 B in registers), train descriptors streamed through LDS in
+// tiles of 256 (broadcast reads); the per-thread top-2 insertion is OpenCV's
+// batchDistance rule (strict '<' against the 2nd best, equal distances keep
+// index order).  The Kannala-Brandt triangulation of the candidates stays on
+// the host.
+// ---------------------------------------------------------------------------
+struct KnnArgs {
+    const uint8_t* q;           // pair p: q + p * stride * 32, rows [q0[p], qn[p])
+    const uint8_t* t;
+    const int32_t* q0;
+    const int32_t* qn;
+    const int32_t* t0;
+    const int32_t* tn;
+    long long stride;           // rows per pair (cap)
+    double ratio;
+    int32_t* idx;               // [pair][stride][2], absolute train rows, -1 if none
+    int32_t* dist;              // [pair][stride][2]
+    int32_t* l2r;               // [pair][stride]: ratio-passing candidate or -1
+};
+
+__global__ __launch_bounds__(256) void k_knn2(KnnArgs a) {
+    __shared__ uint4 tile[256][2];
+    const int p = blockIdx.y, tid = threadIdx.x;
+    const int q0 = a.q0[p], qn = a.qn[p], t0 = a.t0[p], tn = a.tn[p];
+    const int nt = max(0, tn - t0);
+    const int q = q0 + blockIdx.x * 256 + tid;
+    int32_t* idx = a.idx + p * a.stride * 2;
+    int32_t* dst = a.dist + p * a.stride * 2;
+    int32_t* l2r = a.l2r + p * a.stride;
+    if (blockIdx.x == 0)                       // rows outside the lapping area
+        for (int i = tid; i < q0; i += 256) {
+            idx[2 * i] = idx[2 * i + 1] = -1;
+            dst[2 * i] = dst[2 * i + 1] = -1;
+            l2r[i] = -1;
+        }
+    if (q0 + (int)blockIdx.x * 256 >= qn) return;          // block-uniform
+    const bool act = q < qn;
+    uint4 a0 = make_uint4(0, 0, 0, 0), a1 = a0;
+    if (act) {
+        const uint4* qp = (const uint4*)(a.q + (p * a.stride + q) * 32);
+        a0 = qp[0];
+        a1 = qp[1];
+    }
+    int d1 = INT_MAX, d2 = INT_MAX, i1 = -1, i2 = -1;
+    const uint4* tp = (const uint4*)(a.t + (p * a.stride + t0) * 32);
+    for (int base = 0; base < nt; base += 256) {
+        __syncthreads();
+        if (base + tid < nt) {
+            tile[tid][0] = tp[2 * (base + tid)];
+            tile[tid][1] = tp[2 * (base + tid) + 1];
+        }
+        __syncthreads();
+        const int m = min(256, nt - base);
+        if (act)
+            for (int j = 0; j < m; ++j) {
+                const uint4 b0 = tile[j][0], b1 = tile[j][1];
+                const int d = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) +
+                              __popc(a0.w ^ b0.w) + __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) +
+                              __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+                if (d < d2) {
+                    if (d1 > d) { d2 = d1; i2 = i1; d1 = d; i1 = base + j; }
+                    else { d2 = d; i2 = base + j; }
+                }
+            }
+    }
+    if (act) {
+        idx[2 * q] = i1 >= 0 ? i1 + t0 : -1;
+        idx[2 * q + 1] = i2 >= 0 ? i2 + t0 : -1;
+        dst[2 * q] = i1 >= 0 ? d1 : -1;
+        dst[2 * q + 1] = i2 >= 0 ? d2 : -1;
+        // (*it).size() >= 2 && (*it)[0].distance < (*it)[1].distance * 0.7 (:1151), in double
+        l2r[q] = (i2 >= 0 && (double)d1 < (double)d2 * a.ratio) ? i1 + t0 : -1;
+    }
+}
+
 static PyrView pyr_view(const orbx_handle* h, const uint8_t* l0, long long l0_fstride, int l0_pitch, int first) {
     PyrView v;
     v.l0 = l0 + first * l0_fstride;
@@ -415,6 +494,55 @@ int orbs_compute_stereo_matches(orbx_handle* left, orbx_handle* right, const orb
     if (rc) return rc;
     ORB_CHECK(hipMemcpy(uright, bur.p, nl * sizeof(float), hipMemcpyDeviceToHost));
     ORB_CHECK(hipMemcpy(depth, bdp.p, nl * sizeof(float), hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbs_knn_match2(const uint8_t* query, int nq, const uint8_t* train, int nt, int32_t* idx, int32_t* dist,
+                    int device) {
+    if (nq < 0 || nt < 0 || (nq && (!query || !idx || !dist)) || (nt && !train)) return ORB_ERR_PARAM;
+    if (nq == 0) return ORB_OK;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return ORB_ERR_DEVICE;
+    if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    const long long stride = std::max(nq, nt);
+    SBuf<uint8_t> bq, bt;
+    SBuf<int32_t> bi, bd, bl, bn;
+    if (bq.alloc(stride * 32) || bt.alloc(stride * 32) || bi.alloc(stride * 2) || bd.alloc(stride * 2) ||
+        bl.alloc(stride) || bn.alloc(4))
+        return ORB_ERR_DEVICE;
+    const int32_t ns[4] = {0, nq, 0, nt};
+    ORB_CHECK(hipMemcpy(bq.p, query, (size_t)nq * 32, hipMemcpyHostToDevice));
+    if (nt) ORB_CHECK(hipMemcpy(bt.p, train, (size_t)nt * 32, hipMemcpyHostToDevice));
+    ORB_CHECK(hipMemcpy(bn.p, ns, sizeof(ns), hipMemcpyHostToDevice));
+    KnnArgs a{bq.p, bt.p, bn.p, bn.p + 1, bn.p + 2, bn.p + 3, stride, 0.7, bi.p, bd.p, bl.p};
+    hipLaunchKernelGGL(k_knn2, dim3((nq + 255) / 256, 1), dim3(256), 0, 0, a);
+    ORB_CHECK(hipGetLastError());
+    ORB_CHECK(hipMemcpy(idx, bi.p, (size_t)nq * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(dist, bd.p, (size_t)nq * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbs_fisheye_stereo_candidates_batch_device(int npairs, int left0, int right0, const uint8_t* d_desc,
+                                                const int32_t* d_n, const int32_t* d_mono, int cap, double ratio,
+                                                int32_t* d_idx, int32_t* d_dist, int32_t* d_l2r, void* stream) {
+    if (npairs <= 0 || left0 < 0 || right0 < 0 || !d_desc || !d_n || !d_mono || cap <= 0 || !d_idx || !d_dist ||
+        !d_l2r)
+        return ORB_ERR_PARAM;
+    // left pair p: rows [mono[left0+p], n[left0+p]) of frame left0+p; right likewise
+    KnnArgs a;
+    a.q = d_desc + (long long)left0 * cap * 32;
+    a.t = d_desc + (long long)right0 * cap * 32;
+    a.q0 = d_mono + left0;
+    a.qn = d_n + left0;
+    a.t0 = d_mono + right0;
+    a.tn = d_n + right0;
+    a.stride = cap;
+    a.ratio = ratio;
+    a.idx = d_idx;
+    a.dist = d_dist;
+    a.l2r = d_l2r;
+    hipLaunchKernelGGL(k_knn2, dim3((cap + 255) / 256, npairs), dim3(256), 0, (hipStream_t)stream, a);
+    ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }
 

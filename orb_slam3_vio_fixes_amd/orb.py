@@ -152,6 +152,33 @@ def compute_stereo_matches_batch_device(ex: ORBextractor, npairs: int, left0: in
     return ur, dep, sad
 
 
+def knn_match2(query: np.ndarray, train: np.ndarray, device: int = 0):
+    """BFMatcher(NORM_HAMMING).knnMatch(query, train, 2) on the GPU: (idx, dist), each (nq, 2)."""
+    q = np.ascontiguousarray(query, np.uint8).reshape(-1, 32)
+    t = np.ascontiguousarray(train, np.uint8).reshape(-1, 32)
+    idx = np.zeros((len(q), 2), np.int32)
+    dist = np.zeros((len(q), 2), np.int32)
+    capi.check(capi.lib().orbs_knn_match2(abi.ptr(q), len(q), abi.ptr(t), len(t), abi.ptr(idx), abi.ptr(dist),
+                                          device), "orbs_knn_match2")
+    return idx, dist
+
+
+def fisheye_stereo_candidates_batch_device(npairs: int, left0: int, right0: int, desc, n, mono, cap: int,
+                                           ratio: float = 0.7, stream=None):
+    """ComputeStereoFishEyeMatches' knnMatch + ratio on device batch outputs:
+    (idx (P, cap, 2), dist (P, cap, 2), l2r (P, cap)) CUDA tensors."""
+    import torch
+    dev = desc.device
+    idx = torch.empty((npairs, cap, 2), dtype=torch.int32, device=dev)
+    dist = torch.empty((npairs, cap, 2), dtype=torch.int32, device=dev)
+    l2r = torch.empty((npairs, cap), dtype=torch.int32, device=dev)
+    st = stream.cuda_stream if stream is not None else torch.cuda.current_stream().cuda_stream
+    capi.check(capi.lib().orbs_fisheye_stereo_candidates_batch_device(
+        npairs, left0, right0, desc.data_ptr(), n.data_ptr(), mono.data_ptr(), cap, ratio, idx.data_ptr(),
+        dist.data_ptr(), l2r.data_ptr(), C.c_void_p(st)), "orbs_fisheye_stereo_candidates_batch_device")
+    return idx, dist, l2r
+
+
 def keypoints_from_device(kps_i32) -> np.ndarray:
     """(cap, 7) int32 tensor/array -> structured KEYPOINT_DTYPE array."""
     a = np.ascontiguousarray(kps_i32.cpu().numpy() if hasattr(kps_i32, "cpu") else kps_i32, dtype=np.int32)

@@ -62,3 +62,44 @@ def test_stereo_empty_right(gpu_lib):
     xr(right, None, (0, 0))
     ur, dep = orb.ComputeStereoMatches(xl, xr, kl, dl, kl[:0], dl[:0], BASE, MBF)
     assert (ur == -1).all() and (dep == -1).all()
+
+
+@pytest.mark.parametrize("nq,nt,seed", [(300, 280, 1), (1500, 1500, 5), (50, 1, 2), (40, 0, 3), (700, 300, 6)])
+def test_knn2_host_api(gpu_lib, nq, nt, seed):
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, 256, (nt, 32), dtype=np.uint8)
+    if nt > 3:
+        t[1] = t[0]
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    if nt:
+        q[: nq // 2] = t[rng.integers(0, nt, nq // 2)]
+    i, d = orb.knn_match2(q, t)
+    ri, rd = O.knn_match2(q, t)
+    np.testing.assert_array_equal(i, ri)
+    np.testing.assert_array_equal(d, rd)
+
+
+def test_fisheye_candidates_batch_device(gpu_lib):
+    """C4 shape: 512x512 fisheye pairs, 1500 features, lapping {0, 511}."""
+    import torch
+    P = 4
+    pairs = [synth.stereo_pair(512, 512, 4000 + i) for i in range(P)]
+    frames = torch.from_numpy(np.stack([p[0] for p in pairs] + [p[1] for p in pairs])).cuda()
+    ex = orb.ORBextractor(1500, 1.2, 8, 20, 7)
+    kps, desc, n, mono, cap = ex.extract_batch_device(frames, (0, 511))
+    idx, dist, l2r = orb.fisheye_stereo_candidates_batch_device(P, 0, P, desc, n, mono, cap)
+    torch.cuda.synchronize()
+    idx, dist, l2r = idx.cpu().numpy(), dist.cpu().numpy(), l2r.cpu().numpy()
+    desc_h, n_h, mono_h = desc.cpu().numpy(), n.cpu().numpy(), mono.cpu().numpy()
+    good = 0
+    for p in range(P):
+        nl, ml, nr, mr = n_h[p], mono_h[p], n_h[P + p], mono_h[P + p]
+        ri, rd = O.knn_match2(desc_h[p, ml:nl], desc_h[P + p, mr:nr])
+        ri = np.where(ri >= 0, ri + mr, -1)
+        np.testing.assert_array_equal(idx[p, ml:nl], ri)
+        np.testing.assert_array_equal(dist[p, ml:nl], rd)
+        ok = (ri[:, 1] >= 0) & (rd[:, 0].astype(np.float64) < rd[:, 1].astype(np.float64) * 0.7)
+        np.testing.assert_array_equal(l2r[p, ml:nl], np.where(ok, ri[:, 0], -1))
+        assert (l2r[p, :ml] == -1).all()
+        good += ok.sum()
+    assert good > P * 200

@@ -38,3 +38,33 @@ def test_oracle_stereo_no_right_keypoints():
     er(right, (0, 0))
     ur, dep = O.compute_stereo_matches(el, er, kl, dl, kl[:0], dl[:0], BASE, MBF)
     assert (ur == -1).all() and (dep == -1).all()
+
+
+def knn2_numpy(q, t):
+    """BFMatcher knnMatch(k=2) restated with a stable lexicographic sort."""
+    if len(t) == 0:
+        return np.full((len(q), 2), -1, np.int32), np.full((len(q), 2), -1, np.int32)
+    d = np.unpackbits(np.bitwise_xor(q[:, None, :], t[None, :, :]), axis=-1).sum(-1)
+    order = np.argsort(d, axis=1, kind="stable")[:, :2]
+    idx = np.full((len(q), 2), -1, np.int32)
+    dist = np.full((len(q), 2), -1, np.int32)
+    k = min(2, len(t))
+    idx[:, :k] = order[:, :k]
+    dist[:, :k] = np.take_along_axis(d, order[:, :k], 1)
+    return idx, dist
+
+
+@pytest.mark.parametrize("nq,nt,seed", [(300, 280, 1), (50, 1, 2), (40, 0, 3), (200, 200, 4)])
+def test_oracle_knn2_vs_numpy(nq, nt, seed):
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, (max(nt, 1), 32), dtype=np.uint8)
+    t = base[:nt].copy()
+    if nt > 3:
+        t[1] = t[0]                                    # duplicate rows: equal distances, index order
+    q = rng.integers(0, 256, (nq, 32), dtype=np.uint8)
+    if nt:
+        q[: nq // 2] = t[rng.integers(0, nt, nq // 2)] ^ (rng.random((nq // 2, 32)) < 0.03).astype(np.uint8)
+    i, d = O.knn_match2(q, t)
+    ri, rd = knn2_numpy(q, t)
+    np.testing.assert_array_equal(i, ri)
+    np.testing.assert_array_equal(d, rd)

@@ -8,7 +8,12 @@ HBM (left and right frames extracted in one launch chain).  Prints one JSON
 line with pairs/s, per-stage times (HIP events), a CPU-oracle baseline on a
 bounded sample and the parity of that sample.
 
-usage: python tools/bench_stereo.py [--pairs 128] [--steps 10] [--warmup 2]
+With --workload c4: 512x512 fisheye stereo pairs,
+ORBextractor(1500) with lapping {0, 511}, the ComputeStereoFishEyeMatches
+candidates (knnMatch k=2 + Lowe 0.7 over the lapping areas, Frame.cc:1126-1156);
+the Kannala-Brandt triangulation of the candidates stays on the host.
+
+usage: python tools/bench_stereo.py [--workload c3|c4] [--pairs 128] [--steps 10] [--warmup 2]
 """
 from __future__ import annotations
 
@@ -49,12 +54,15 @@ def cpu_baseline(left, right, threads):
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", choices=["c3", "c4"], default="c3")
     ap.add_argument("--pairs", type=int, default=128)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
+    if args.workload == "c4":
+        return main_c4(args)
     import torch
     from orb_slam3_vio_fixes_amd import capi, orb, synth
     dev = torch.device("cuda", 0)
@@ -124,6 +132,70 @@ def main():
                                "sample": f"first {ns} pairs: oracle extraction of L and R + ComputeStereoMatches"}
         out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad,
                          "matched_fraction": float(np.mean([(o[1][0] >= 0).mean() for o in outs]))}
+    print(json.dumps(out), flush=True)
+
+
+def main_c4(args):
+    import torch
+    from oracle import oracle as O
+    from orb_slam3_vio_fixes_amd import orb, synth
+    w = h = 512
+    nf, lap = 1500, (0, 511)
+    dev = torch.device("cuda", 0)
+    P = args.pairs
+    left = synth.sequence(w, h, P, config=4)
+    right = np.stack([synth.right_view(left[i], synth.frame_seed(4, i)) for i in range(P)])
+    frames = torch.from_numpy(np.concatenate([left, right])).to(dev)
+    ex = orb.ORBextractor(nf, 1.2, 8, 20, 7)
+    stream = torch.cuda.current_stream(dev)
+    kps, desc, n, mono, cap = ex.extract_batch_device(frames, lap)
+    ev = []
+
+    def step(timed=False):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)] if timed else None
+        if timed:
+            e[0].record(stream)
+        ex.extract_batch_device(frames, lap, out=(kps, desc, n, mono))
+        if timed:
+            e[1].record(stream)
+        res = orb.fisheye_stereo_candidates_batch_device(P, 0, P, desc, n, mono, cap)
+        if timed:
+            e[2].record(stream)
+            ev.append(e)
+        return res
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        idx, dist, l2r = step(timed=True)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    stage = {k: float(np.mean([e[i].elapsed_time(e[i + 1]) for e in ev]))
+             for i, k in enumerate(["extract_2B_images", "fisheye_knn2_ratio"])}
+    out = {"metric": "fisheye stereo pairs/s (512x512 L+R ORB extract, knnMatch(2) + ratio over the lapping areas)",
+           "value": P * args.steps / dt, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+           "config": {"workload": "C4: 512x512 fisheye stereo, ORBextractor(1500,1.2,8,20,7), lapping {0,511}",
+                      "pairs_per_step": P}, "stage_ms": stage}
+    if args.cpu_sample > 0:
+        ns = min(args.cpu_sample, P)
+        O.lib()
+        dh, nh, mh, ih = desc.cpu().numpy(), n.cpu().numpy(), mono.cpu().numpy(), idx.cpu().numpy()
+        t0 = time.perf_counter()
+        bad = 0
+        for p in range(ns):
+            el, er = O.OracleExtractor(nf, 1.2, 8, 20, 7), O.OracleExtractor(nf, 1.2, 8, 20, 7)
+            kl, dl, ml = el(left[p], lap)
+            kr, dr, mr = er(right[p], lap)
+            ri, _ = O.knn_match2(dl[ml:], dr[mr:])
+            if nh[p] != len(kl) or not np.array_equal(ih[p, ml:nh[p]], np.where(ri >= 0, ri + mr, -1)):
+                bad += 1
+        fps = ns / (time.perf_counter() - t0)
+        out["cpu_baseline"] = {"value": fps, "unit": "pairs/s", "cores": 1, "kind": "port",
+                               "sample": f"first {ns} pairs: oracle extraction of L and R + knnMatch(2), one thread"}
+        out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad}
     print(json.dumps(out), flush=True)
 
 
