@@ -306,6 +306,11 @@ typedef struct orbv_vocab {
     const uint8_t* node_desc;
     const int32_t* word_id;
     const double* weight;
+    /* NULL: the children of node i are first_child[i] .. first_child[i]+nchild[i]-1;
+     * otherwise they are child_idx[first_child[i] + j], j < nchild[i], in the
+     * order of Node::children (a loaded text vocabulary, whose ids are line
+     * numbers). */
+    const int32_t* child_idx;
 } orbv_vocab;
 
 /* TemplatedVocabulary::transform(feature, word_id, weight, &nid, levelsup)
@@ -313,6 +318,61 @@ typedef struct orbv_vocab {
  * and the node id at level m_L - levelsup.  GPU when device >= 0. */
 int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levelsup,
                    int32_t* word_id, double* weight, int32_t* node_id, int device);
+
+/* ---------------- vocabulary side ---------------- */
+
+/* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424): the
+ * DBoW2 text format ("k L scoring weighting" header, then one node per line:
+ * parent, is-leaf, 32 descriptor bytes, weight).  Node ids are line numbers,
+ * word ids follow the order of the leaf lines, and -- as in the reference --
+ * the empty read after a final newline appends one non-leaf child of the root
+ * with weight 0 (its descriptor is undefined in the reference, 0 here).
+ * Returns NULL on failure (*err: ORB_ERR_EMPTY unreadable, ORB_ERR_PARAM bad
+ * header or a parent index out of range). */
+typedef struct orbv_text_vocab orbv_text_vocab;
+orbv_text_vocab* orbv_load_text(const char* path, int32_t* err);
+/* Pointers into the loaded vocabulary (valid until orbv_free_text); fills
+ * child_idx.  k, scoring (0 L1 .. 5 dot product), weighting (0 TF-IDF, 1 TF,
+ * 2 IDF, 3 binary) and the word count as in the header / file. */
+int orbv_text_vocab_view(const orbv_text_vocab* v, orbv_vocab* view, int32_t* k, int32_t* scoring,
+                         int32_t* weighting, int32_t* nwords);
+void orbv_free_text(orbv_text_vocab* v);
+
+/* TemplatedVocabulary::transform(features, BowVector, FeatureVector, levelsup)
+ * (TemplatedVocabulary.h:1126-1194) assembled from the per-descriptor word,
+ * weight and node id of orbv_transform: BowVector as (word, value) pairs in
+ * word order, normalised as `scoring` requires; FeatureVector as CSR (nodes
+ * ascending, feature indices ascending).  Capacities: n entries each, fv_off
+ * n + 1. */
+int orbv_bow_assemble(int scoring, int weighting, int n, const int32_t* word_id, const double* weight,
+                      const int32_t* node_id, int32_t* bow_words, double* bow_values, int32_t* nbow,
+                      int32_t* fv_nodes, int32_t* fv_off, int32_t* fv_idx, int32_t* nfv);
+/* GeneralScoring::score for two BowVectors (ScoringObject.cpp): scoring 0 L1,
+ * 1 L2, 2 chi-square, 3 KL, 4 Bhattacharyya, 5 dot product. */
+double orbv_score(int scoring, const int32_t* w1, const double* v1, int n1, const int32_t* w2, const double* v2,
+                  int n2);
+
+/* ---------------- keyframe database ---------------- */
+
+/* Device-resident snapshot of KeyFrameDatabase (src/KeyFrameDatabase.cc) for
+ * relocalisation.  Keyframes are 0..nkf-1: per-keyframe BowVectors as CSR
+ * (bow_off[nkf+1]; words ascending, L1-normalised values), the inverted file
+ * mvInvertedFile as CSR by word (inv_off[nwords+1], keyframes in list order),
+ * per-keyframe GetBestCovisibilityKeyFrames(10) as CSR and map ids. */
+typedef struct orbk_db orbk_db;
+orbk_db* orbk_db_create(int device);
+void orbk_db_destroy(orbk_db* db);
+int orbk_db_upload(orbk_db* db, int nkf, const int32_t* bow_off, const int32_t* bow_words, const double* bow_vals,
+                   int nwords, const int32_t* inv_off, const int32_t* inv_kf, const int32_t* cov_off,
+                   const int32_t* cov_kf, const int32_t* kf_map);
+/* KeyFrameDatabase::DetectRelocalizationCandidates(F, pMap) (:733-845) for the
+ * query BowVector (words ascending).  reloc_score[nkf] is every keyframe's
+ * mRelocScore: the scored ones are overwritten, and -- as in the reference --
+ * neighbours that share words without being scored contribute their current
+ * (previous-query) value.  Writes up to cap keyframe indices in the
+ * reference's order; returns their count or an error < 0. */
+int orbk_detect_relocalization_candidates(orbk_db* db, const int32_t* q_words, const double* q_vals, int nq,
+                                          int32_t map_id, float* reloc_score, int32_t* cand, int cap);
 
 #ifdef __cplusplus
 }

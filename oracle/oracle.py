@@ -54,6 +54,8 @@ def lib():
         L.orbo_search_by_projection_last.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, vp]
         L.orbo_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp]
         L.orbo_knn_match2.argtypes = [vp, i32, vp, i32, vp, vp]
+        L.orbo_detect_relocalization_candidates.argtypes = [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp,
+                                                             i32, vp, vp, i32]
         L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
         _lib = L
     return _lib
@@ -221,3 +223,20 @@ def knn_match2(query: np.ndarray, train: np.ndarray):
     dist = np.zeros((len(q), 2), np.int32)
     lib().orbo_knn_match2(abi.ptr(q), len(q), abi.ptr(t), len(t), abi.ptr(idx), abi.ptr(dist))
     return idx, dist
+
+
+def detect_relocalization_candidates(db: dict, q_words, q_vals, map_id: int, reloc_score: np.ndarray):
+    """KeyFrameDatabase::DetectRelocalizationCandidates on a database snapshot
+    (dict of CSR arrays, see tests/kfdb_ref.py); updates reloc_score in place."""
+    qw = np.ascontiguousarray(q_words, np.int32)
+    qv = np.ascontiguousarray(q_vals, np.float64)
+    cap = db["nkf"]
+    cand = np.zeros(max(cap, 1), np.int32)
+    n = lib().orbo_detect_relocalization_candidates(
+        abi.ptr(qw), abi.ptr(qv), len(qw), db["nkf"], abi.ptr(db["bow_off"]), abi.ptr(db["bow_words"]),
+        abi.ptr(db["bow_vals"]), db["nwords"], abi.ptr(db["inv_off"]), abi.ptr(db["inv_kf"]),
+        abi.ptr(db["cov_off"]), abi.ptr(db["cov_kf"]), abi.ptr(db["kf_map"]), map_id, abi.ptr(reloc_score),
+        abi.ptr(cand), cap)
+    if n < 0:
+        raise RuntimeError(f"oracle reloc failed {n}")
+    return cand[:n].copy()

@@ -946,10 +946,13 @@ int orbo_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
         int fin = 0, level = 0;
         do {
             ++level;
+            // nodes = m_nodes[final_id].children; first child wins ties (:1236-1249)
             const int c0 = voc->first_child[fin], nc = voc->nchild[fin];
-            int best_id = c0;
-            double best = hamming(d, voc->node_desc + (size_t)c0 * 32);
-            for (int c = c0 + 1; c < c0 + nc; ++c) {
+            auto child = [&](int j) { return voc->child_idx ? voc->child_idx[c0 + j] : c0 + j; };
+            int best_id = child(0);
+            double best = hamming(d, voc->node_desc + (size_t)best_id * 32);
+            for (int j = 1; j < nc; ++j) {
+                const int c = child(j);
                 const double dd = hamming(d, voc->node_desc + (size_t)c * 32);
                 if (dd < best) { best = dd; best_id = c; }
             }
@@ -1081,6 +1084,98 @@ int orbo_knn_match2(const uint8_t* q, int nq, const uint8_t* t, int nt, int32_t*
         }
     }
     return 0;
+}
+
+// KeyFrameDatabase::DetectRelocalizationCandidates (src/KeyFrameDatabase.cc:733-845)
+// over a snapshot of the database: per-KF BowVectors (CSR, words ascending),
+// the inverted file (CSR by word, list order), per-KF
+// GetBestCovisibilityKeyFrames(10) (CSR), per-KF map id.  reloc_score is the
+// mRelocScore member of every KF: read for neighbours that share words but
+// were not scored in this query (the reference reads their stale value) and
+// overwritten for the scored ones.  Returns the number of candidates.
+int orbo_detect_relocalization_candidates(const int32_t* q_words, const double* q_vals, int nq, int nkf,
+                                          const int32_t* bow_off, const int32_t* bow_words, const double* bow_vals,
+                                          int nwords, const int32_t* inv_off, const int32_t* inv_kf,
+                                          const int32_t* cov_off, const int32_t* cov_kf, const int32_t* kf_map,
+                                          int32_t map_id, float* reloc_score, int32_t* cand, int cap) {
+    std::vector<int> reloc_query(nkf, 0), reloc_words(nkf, 0);
+    const int qid = 1;
+    std::list<int> sharing;                                                          // :735-757
+    for (int r = 0; r < nq; ++r) {
+        const int w = q_words[r];
+        if (w < 0 || w >= nwords) return ORB_ERR_PARAM;
+        for (int e = inv_off[w]; e < inv_off[w + 1]; ++e) {
+            const int kf = inv_kf[e];
+            if (reloc_query[kf] != qid) {
+                reloc_words[kf] = 0;
+                reloc_query[kf] = qid;
+                sharing.push_back(kf);
+            }
+            reloc_words[kf]++;
+        }
+    }
+    if (sharing.empty()) return 0;
+    int maxCommonWords = 0;                                                          // :762-767
+    for (int kf : sharing) maxCommonWords = std::max(maxCommonWords, reloc_words[kf]);
+    const int minCommonWords = maxCommonWords * 0.8f;
+    std::list<std::pair<float, int>> score_match;                                   // :771-787
+    for (int kf : sharing) {
+        if (reloc_words[kf] > minCommonWords) {
+            // L1Scoring::score (ScoringObject.cpp): common words in order
+            double sc = 0;
+            int i = 0, j = bow_off[kf];
+            const int j1 = bow_off[kf + 1];
+            while (i < nq && j < j1) {
+                if (q_words[i] == bow_words[j]) {
+                    const double vi = q_vals[i], wi = bow_vals[j];
+                    sc += std::fabs(vi - wi) - std::fabs(vi) - std::fabs(wi);
+                    ++i;
+                    ++j;
+                } else if (q_words[i] < bow_words[j]) {
+                    ++i;
+                } else {
+                    ++j;
+                }
+            }
+            const float si = (float)(-sc / 2.0);
+            reloc_score[kf] = si;
+            score_match.push_back(std::make_pair(si, kf));
+        }
+    }
+    if (score_match.empty()) return 0;
+    std::list<std::pair<float, int>> acc_match;                                     // :792-819
+    float bestAccScore = 0;
+    for (auto& it : score_match) {
+        const int kfi = it.second;
+        float bestScore = it.first, accScore = bestScore;
+        int best_kf = kfi;
+        for (int e = cov_off[kfi]; e < cov_off[kfi + 1]; ++e) {
+            const int kf2 = cov_kf[e];
+            if (reloc_query[kf2] != qid) continue;
+            accScore += reloc_score[kf2];
+            if (reloc_score[kf2] > bestScore) {
+                best_kf = kf2;
+                bestScore = reloc_score[kf2];
+            }
+        }
+        acc_match.push_back(std::make_pair(accScore, best_kf));
+        if (accScore > bestAccScore) bestAccScore = accScore;
+    }
+    const float minScoreToRetain = 0.75f * bestAccScore;                            // :822-842
+    std::vector<char> added(nkf, 0);
+    int n = 0;
+    for (auto& it : acc_match) {
+        if (it.first > minScoreToRetain) {
+            const int kf = it.second;
+            if (kf_map[kf] != map_id) continue;
+            if (!added[kf]) {
+                if (n < cap) cand[n] = kf;
+                ++n;
+                added[kf] = 1;
+            }
+        }
+    }
+    return n;
 }
 
 }  // extern "C"

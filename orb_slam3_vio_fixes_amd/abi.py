@@ -56,7 +56,7 @@ class OrbmMapPoints(C.Structure):
 class OrbvVocab(C.Structure):
     _fields_ = [("nnodes", C.c_int32), ("depth_levels", C.c_int32), ("first_child", C.c_void_p),
                 ("nchild", C.c_void_p), ("node_desc", C.c_void_p), ("word_id", C.c_void_p),
-                ("weight", C.c_void_p)]
+                ("weight", C.c_void_p), ("child_idx", C.c_void_p)]
 
 
 def ptr(a: np.ndarray | None) -> int | None:
@@ -115,9 +115,12 @@ def featvec_struct(node_of_feature: np.ndarray) -> Keep:
 
 
 def vocab_struct(v: dict) -> Keep:
-    arrs = {k: np.ascontiguousarray(v[k]) for k in ("first_child", "nchild", "node_desc", "word_id", "weight")}
+    keys = ("first_child", "nchild", "node_desc", "word_id", "weight")
+    arrs = {k: np.ascontiguousarray(v[k]) for k in keys}
+    if v.get("child_idx") is not None:
+        arrs["child_idx"] = np.ascontiguousarray(v["child_idx"], np.int32)
     s = OrbvVocab(int(v["nnodes"]), int(v["depth_levels"]), ptr(arrs["first_child"]), ptr(arrs["nchild"]),
-                  ptr(arrs["node_desc"]), ptr(arrs["word_id"]), ptr(arrs["weight"]))
+                  ptr(arrs["node_desc"]), ptr(arrs["word_id"]), ptr(arrs["weight"]), ptr(arrs.get("child_idx")))
     return Keep(s, list(arrs.values()))
 
 

@@ -19,6 +19,8 @@ EXPORTS = [
     "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device",
     "orbx_set_streams", "orbs_compute_stereo_matches", "orbs_compute_stereo_matches_batch_device",
     "orbs_knn_match2", "orbs_fisheye_stereo_candidates_batch_device",
+    "orbv_load_text", "orbv_text_vocab_view", "orbv_free_text", "orbv_bow_assemble", "orbv_score",
+    "orbk_db_create", "orbk_db_destroy", "orbk_db_upload", "orbk_detect_relocalization_candidates",
 ]
 
 _lib = None
@@ -49,6 +51,18 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_get_profile.argtypes = [vp, vp, i32]
     L.orbm_search_by_bow_batch_device.argtypes = [vp, vp, vp, f32, i32, vp, vp, vp]
     L.orbx_set_streams.argtypes = [vp, i32]
+    L.orbk_db_create.restype = vp
+    L.orbk_db_create.argtypes = [i32]
+    L.orbk_db_destroy.argtypes = [vp]
+    L.orbk_db_upload.argtypes = [vp, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp]
+    L.orbk_detect_relocalization_candidates.argtypes = [vp, vp, vp, i32, i32, vp, vp, i32]
+    L.orbv_load_text.restype = vp
+    L.orbv_load_text.argtypes = [C.c_char_p, vp]
+    L.orbv_text_vocab_view.argtypes = [vp, vp, vp, vp, vp, vp]
+    L.orbv_free_text.argtypes = [vp]
+    L.orbv_bow_assemble.argtypes = [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    L.orbv_score.restype = C.c_double
+    L.orbv_score.argtypes = [i32, vp, vp, i32, vp, vp, i32]
     L.orbs_knn_match2.argtypes = [vp, i32, vp, i32, vp, vp, i32]
     L.orbs_fisheye_stereo_candidates_batch_device.argtypes = [i32, i32, i32, vp, vp, vp, i32, C.c_double, vp, vp,
                                                               vp, vp]

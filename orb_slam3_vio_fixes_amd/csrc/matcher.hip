@@ -711,6 +711,7 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
 // one thread per descriptor (the tree lives in L2 / Infinity Cache).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_transform(const int* __restrict__ first_child, const int* __restrict__ nchild,
+                                                   const int* __restrict__ child_idx,
                                                    const uint8_t* __restrict__ node_desc,
                                                    const int* __restrict__ word_id, const double* __restrict__ weight,
                                                    int n, const uint8_t* __restrict__ desc, int nid_level,
@@ -723,8 +724,10 @@ __global__ __launch_bounds__(256) void k_transform(const int* __restrict__ first
     do {
         ++level;
         const int c0 = first_child[fin], nc = nchild[fin];
-        int best = hamming32(q0, q1, node_desc + (long long)c0 * 32), bid = c0;
-        for (int c = c0 + 1; c < c0 + nc; ++c) {
+        const int b0 = child_idx ? child_idx[c0] : c0;
+        int best = hamming32(q0, q1, node_desc + (long long)b0 * 32), bid = b0;
+        for (int j = 1; j < nc; ++j) {
+            const int c = child_idx ? child_idx[c0 + j] : c0 + j;
             const int d = hamming32(q0, q1, node_desc + (long long)c * 32);
             if (d < best) { best = d; bid = c; }
         }
@@ -1011,17 +1014,24 @@ int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
                    double* weight, int32_t* node_id, int device) {
     if (!voc || n < 0 || !desc || !word_id || !weight || !node_id) return ORB_ERR_PARAM;
     if (device < 0) return ORB_ERR_PARAM;     // the product path runs on the GPU only
+    if (voc->nnodes < 2 || voc->nchild[0] == 0) return ORB_ERR_EMPTY;   // no words (TemplatedVocabulary::empty)
     if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
     if (n == 0) return ORB_OK;
     int rc;
-    DBuf<int> fc, nc, wid; DBuf<uint8_t> nd, dd; DBuf<double> wt, wo; DBuf<int32_t> wio, nio;
+    DBuf<int> fc, nc, wid, ci; DBuf<uint8_t> nd, dd; DBuf<double> wt, wo; DBuf<int32_t> wio, nio;
+    if (voc->child_idx) {
+        int nchild_total = 0;
+        for (int i = 0; i < voc->nnodes; ++i) nchild_total = std::max(nchild_total, voc->first_child[i] + voc->nchild[i]);
+        if ((rc = ci.put(voc->child_idx, nchild_total))) return rc;
+    }
     if ((rc = fc.put(voc->first_child, voc->nnodes)) || (rc = nc.put(voc->nchild, voc->nnodes)) ||
         (rc = nd.put(voc->node_desc, (size_t)voc->nnodes * 32)) || (rc = wid.put(voc->word_id, voc->nnodes)) ||
         (rc = wt.put(voc->weight, voc->nnodes)) || (rc = dd.put(desc, (size_t)n * 32)) || (rc = wo.alloc(n)) ||
         (rc = wio.alloc(n)) || (rc = nio.alloc(n)))
         return rc;
     const int nid_level = voc->depth_levels - levelsup;
-    hipLaunchKernelGGL(k_transform, dim3((n + 255) / 256), dim3(256), 0, 0, fc.p, nc.p, nd.p, wid.p, wt.p, n, dd.p,
+    hipLaunchKernelGGL(k_transform, dim3((n + 255) / 256), dim3(256), 0, 0, fc.p, nc.p, voc->child_idx ? ci.p : nullptr,
+                       nd.p, wid.p, wt.p, n, dd.p,
                        nid_level, wio.p, wo.p, nio.p);
     ORB_CHECK(hipGetLastError());
     ORB_CHECK(hipMemcpy(word_id, wio.p, n * 4, hipMemcpyDeviceToHost));

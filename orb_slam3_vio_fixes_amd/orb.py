@@ -179,6 +179,107 @@ def fisheye_stereo_candidates_batch_device(npairs: int, left0: int, right0: int,
     return idx, dist, l2r
 
 
+class TextVocabulary:
+    """TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424)
+    through the library's loader.  ``.struct`` is the orbv_vocab view (valid
+    while this object lives); ``.arrays()`` copies it into the dict layout of
+    ``synth.vocabulary`` (with ``child_idx``)."""
+
+    def __init__(self, path):
+        err = C.c_int32(0)
+        self._h = capi.lib().orbv_load_text(str(path).encode(), C.byref(err))
+        if not self._h:
+            raise ValueError(f"vocabulary loading failure ({err.value}): {path}")
+        self.struct = abi.OrbvVocab()
+        k, sc, wt, nw = C.c_int32(), C.c_int32(), C.c_int32(), C.c_int32()
+        capi.check(capi.lib().orbv_text_vocab_view(self._h, C.byref(self.struct), C.byref(k), C.byref(sc),
+                                                   C.byref(wt), C.byref(nw)), "orbv_text_vocab_view")
+        self.k, self.L, self.scoring, self.weighting, self.nwords = k.value, self.struct.depth_levels, sc.value, \
+            wt.value, nw.value
+        self.nnodes = self.struct.nnodes
+
+    def ref(self):
+        return C.byref(self.struct)
+
+    def arrays(self) -> dict:
+        n = self.nnodes
+
+        def arr(p, ctype, count, dtype):
+            if not p or count == 0:
+                return np.zeros(count, dtype)
+            return np.ctypeslib.as_array(C.cast(p, C.POINTER(ctype)), (count,)).astype(dtype).copy()
+        nchild = arr(self.struct.nchild, C.c_int32, n, np.int32)
+        first = arr(self.struct.first_child, C.c_int32, n, np.int32)
+        total = int((first + nchild).max()) if n else 0
+        return dict(nnodes=n, depth_levels=self.L, first_child=first, nchild=nchild,
+                    node_desc=arr(self.struct.node_desc, C.c_uint8, n * 32, np.uint8).reshape(n, 32),
+                    word_id=arr(self.struct.word_id, C.c_int32, n, np.int32),
+                    weight=arr(self.struct.weight, C.c_double, n, np.float64),
+                    child_idx=arr(self.struct.child_idx, C.c_int32, total, np.int32))
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            capi.lib().orbv_free_text(self._h)
+            self._h = None
+
+
+def transform_bow(voc, desc: np.ndarray, scoring: int = 0, weighting: int = 0, levelsup: int = 4,
+                  device: int = 0):
+    """transform(features, BowVector, FeatureVector, levelsup): the descent on
+    the GPU, then the library's BowVector/FeatureVector assembly.  Returns
+    (bow_words, bow_values, fv_nodes, fv_off, fv_idx)."""
+    wid, w, nid = transform(voc, desc, levelsup, device)
+    n = len(wid)
+    bw, bv = np.zeros(n, np.int32), np.zeros(n, np.float64)
+    fn, fo, fi = np.zeros(n, np.int32), np.zeros(n + 1, np.int32), np.zeros(n, np.int32)
+    nb, nf = C.c_int32(), C.c_int32()
+    capi.check(capi.lib().orbv_bow_assemble(scoring, weighting, n, abi.ptr(wid), abi.ptr(w), abi.ptr(nid),
+                                            abi.ptr(bw), abi.ptr(bv), C.byref(nb), abi.ptr(fn), abi.ptr(fo),
+                                            abi.ptr(fi), C.byref(nf)), "orbv_bow_assemble")
+    return bw[:nb.value], bv[:nb.value], fn[:nf.value], fo[:nf.value + 1], fi[:fo[nf.value]]
+
+
+def score(scoring: int, w1, v1, w2, v2) -> float:
+    """GeneralScoring::score of two BowVectors (ScoringObject.cpp)."""
+    w1, v1 = np.ascontiguousarray(w1, np.int32), np.ascontiguousarray(v1, np.float64)
+    w2, v2 = np.ascontiguousarray(w2, np.int32), np.ascontiguousarray(v2, np.float64)
+    return capi.lib().orbv_score(scoring, abi.ptr(w1), abi.ptr(v1), len(w1), abi.ptr(w2), abi.ptr(v2), len(w2))
+
+
+class KeyFrameDatabase:
+    """Device snapshot of KeyFrameDatabase for DetectRelocalizationCandidates
+    (KeyFrameDatabase.cc:733-845).  ``db`` is a dict of CSR arrays: bow_off,
+    bow_words, bow_vals, inv_off, inv_kf, cov_off, cov_kf, kf_map, nkf, nwords."""
+
+    def __init__(self, db: dict, device: int = 0):
+        self._h = capi.lib().orbk_db_create(device)
+        if not self._h:
+            raise RuntimeError("orbk_db_create failed (no HIP device)")
+        self.nkf = int(db["nkf"])
+        self._keep = [np.ascontiguousarray(db[k], dt) for k, dt in
+                      (("bow_off", np.int32), ("bow_words", np.int32), ("bow_vals", np.float64), ("inv_off", np.int32),
+                       ("inv_kf", np.int32), ("cov_off", np.int32), ("cov_kf", np.int32), ("kf_map", np.int32))]
+        bo, bw, bv, io, ik, co, ck, km = self._keep
+        capi.check(capi.lib().orbk_db_upload(self._h, self.nkf, abi.ptr(bo), abi.ptr(bw), abi.ptr(bv),
+                                             int(db["nwords"]), abi.ptr(io), abi.ptr(ik), abi.ptr(co), abi.ptr(ck),
+                                             abi.ptr(km)), "orbk_db_upload")
+
+    def DetectRelocalizationCandidates(self, q_words, q_vals, map_id: int, reloc_score: np.ndarray):
+        qw = np.ascontiguousarray(q_words, np.int32)
+        qv = np.ascontiguousarray(q_vals, np.float64)
+        assert reloc_score.dtype == np.float32 and reloc_score.flags["C_CONTIGUOUS"] and len(reloc_score) >= self.nkf
+        cand = np.zeros(max(1, self.nkf), np.int32)
+        n = capi.lib().orbk_detect_relocalization_candidates(self._h, abi.ptr(qw), abi.ptr(qv), len(qw), map_id,
+                                                              abi.ptr(reloc_score), abi.ptr(cand), self.nkf)
+        capi.check(min(n, 0), "orbk_detect_relocalization_candidates")
+        return cand[:n].copy()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            capi.lib().orbk_db_destroy(self._h)
+            self._h = None
+
+
 def keypoints_from_device(kps_i32) -> np.ndarray:
     """(cap, 7) int32 tensor/array -> structured KEYPOINT_DTYPE array."""
     a = np.ascontiguousarray(kps_i32.cpu().numpy() if hasattr(kps_i32, "cpu") else kps_i32, dtype=np.int32)
@@ -240,7 +341,7 @@ class ORBmatcher:
         return nm, owner
 
 
-def transform(voc: abi.Keep, desc: np.ndarray, levelsup: int = 4, device: int = 0):
+def transform(voc, desc: np.ndarray, levelsup: int = 4, device: int = 0):
     """TemplatedVocabulary::transform per descriptor on the GPU: (word_id, weight, node_id)."""
     desc = np.ascontiguousarray(desc, np.uint8)
     n = len(desc)

@@ -48,6 +48,10 @@ def broadcast_vocabulary(voc: dict | None, src: int = 0, device="cpu") -> dict:
     out = {}
     for key in ("first_child", "nchild", "node_desc", "word_id", "weight"):
         out[key] = _bcast_array(voc[key] if rank == src else None, src, device, rank)
+    has_ci = _bcast_array(np.array([int(voc.get("child_idx") is not None)], np.int32) if rank == src else None,
+                          src, device, rank)
+    out["child_idx"] = _bcast_array(voc["child_idx"] if rank == src else None, src, device, rank) if has_ci[0] \
+        else None
     out["nnodes"] = len(out["nchild"])
     dims = _bcast_array(np.array([voc["depth_levels"]], np.int32) if rank == src else None, src, device, rank)
     out["depth_levels"] = int(dims[0])
