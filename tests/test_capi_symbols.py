@@ -11,7 +11,7 @@ HEADER = ROOT / "include" / "orb_mi355x.h"
 
 def declared():
     txt = re.sub(r"/\*.*?\*/", " ", HEADER.read_text(), flags=re.S)
-    return sorted(set(re.findall(r"\b(orb[xmvs]_[a-z0-9_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(orb[xmvsk]_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_declares_entry_points():
