@@ -319,6 +319,46 @@ typedef struct orbv_vocab {
 int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levelsup,
                    int32_t* word_id, double* weight, int32_t* node_id, int device);
 
+/* ---------------- mapping matchers ---------------- */
+
+/* ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight = false) (src/ORBmatcher.cc:1148-1331)
+ * for a pinhole keyframe (NLeft == -1): the matching of every map point.  The
+ * caller does the per-point geometry of :1183-1240 on the host (Tcw * P,
+ * depth > 0, IsInImage, ur = u - bf / z, distance invariance, viewing angle,
+ * PredictScale) and passes valid[i] = false for NULL, bad or already-in-KF
+ * points.  kf: mvKeysUn, descriptors, grid bounds, mvuRight (or NULL),
+ * mvScaleFactors; inv_level_sigma2: mvInvLevelSigma2.  best_idx[i] receives
+ * the keyframe keypoint the point fuses with (bestDist <= TH_LOW) or -1,
+ * best_dist[i] its distance.  The replace / add decisions (:1311-1328) depend
+ * on the map state and stay with the caller, in index order.  fma = 1
+ * reproduces the reference build's contraction of the chi-square sums.
+ * Returns the number of points with a keypoint. */
+int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, const uint8_t* valid, const float* u,
+              const float* v, const float* ur, const int32_t* level, const uint8_t* desc, float th, int fma,
+              int32_t* best_idx, int32_t* best_dist);
+
+/* ORBmatcher::SearchForTriangulation(pKF1, pKF2, vMatchedPairs, bOnlyStereo,
+ * bCoarse) (src/ORBmatcher.cc:907-1146) for pinhole keyframes.  F12 is the
+ * 3x3 fundamental matrix row-major exactly as Pinhole::epipolarConstrain
+ * computes it (K1^-T [t12]x R12 K2^-1, Pinhole.cpp:109-112), ep the epipole of
+ * KF1's centre in KF2 (pKF2->mpCamera->project(T2w * Cw)); both are host
+ * geometry.  has_mp: GetMapPoint(i) != NULL.  matches12[N1] out (the pairs of
+ * vMatchedPairs are (i, matches12[i]) for matches12[i] >= 0).  Returns the
+ * number of matches. */
+int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                  const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                  const float* F12, float ep_x, float ep_y, const float* level_sigma2_2,
+                                  int only_stereo, int coarse, int check_ori, int fma, int32_t* matches12);
+
+/* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:329-405) for
+ * npoints points at once: point p's observed descriptors (the order of its
+ * observation map, gathered by the caller) are rows off[p] .. off[p+1]-1 of
+ * desc; best[p] receives the index (within the point's rows) of the
+ * descriptor with the least median Hamming distance to the others (first on
+ * ties), -1 for a point without descriptors.  GPU device `device`. */
+int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best,
+                                         int device);
+
 /* ---------------- vocabulary side ---------------- */
 
 /* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424): the

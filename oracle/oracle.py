@@ -54,6 +54,9 @@ def lib():
         L.orbo_search_by_projection_last.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, vp]
         L.orbo_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp]
         L.orbo_knn_match2.argtypes = [vp, i32, vp, i32, vp, vp]
+        L.orbo_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp]
+        L.orbo_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
+        L.orbo_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
         L.orbo_detect_relocalization_candidates.argtypes = [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp,
                                                              i32, vp, vp, i32]
         L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
@@ -240,3 +243,36 @@ def detect_relocalization_candidates(db: dict, q_words, q_vals, map_id: int, rel
     if n < 0:
         raise RuntimeError(f"oracle reloc failed {n}")
     return cand[:n].copy()
+
+
+def fuse(kf, inv_sigma2, valid, u, v, ur, level, desc, th=3.0, fma=1):
+    n = len(valid)
+    arrs = [np.ascontiguousarray(inv_sigma2, np.float32), np.ascontiguousarray(valid, np.uint8),
+            np.ascontiguousarray(u, np.float32), np.ascontiguousarray(v, np.float32),
+            np.ascontiguousarray(ur, np.float32), np.ascontiguousarray(level, np.int32),
+            np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)]
+    bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    nf = lib().orbo_fuse(kf.ref(), abi.ptr(arrs[0]), n, *[abi.ptr(a) for a in arrs[1:]], th, fma, abi.ptr(bi),
+                         abi.ptr(bd))
+    return nf, bi, bd
+
+
+def search_for_triangulation(kf1, fv1, has_mp1, kf2, fv2, has_mp2, F12, ep, sigma2_2, only_stereo=False,
+                             coarse=False, check_ori=True, fma=1):
+    m1 = np.ascontiguousarray(has_mp1, np.uint8)
+    m2 = np.ascontiguousarray(has_mp2, np.uint8)
+    F = np.ascontiguousarray(F12, np.float32).reshape(9)
+    s2 = np.ascontiguousarray(sigma2_2, np.float32)
+    out = np.zeros(len(m1), np.int32)
+    nm = lib().orbo_search_for_triangulation(kf1.ref(), fv1.ref(), abi.ptr(m1), kf2.ref(), fv2.ref(), abi.ptr(m2),
+                                             abi.ptr(F), float(ep[0]), float(ep[1]), abi.ptr(s2), int(only_stereo),
+                                             int(coarse), int(check_ori), fma, abi.ptr(out))
+    return nm, out
+
+
+def compute_distinctive_descriptors(off, desc):
+    off = np.ascontiguousarray(off, np.int32)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    best = np.zeros(max(len(off) - 1, 0), np.int32)
+    lib().orbo_compute_distinctive_descriptors(len(best), abi.ptr(off), abi.ptr(desc), abi.ptr(best))
+    return best

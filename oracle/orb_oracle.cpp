@@ -1178,4 +1178,147 @@ int orbo_detect_relocalization_candidates(const int32_t* q_words, const double* 
     return n;
 }
 
+// ORBmatcher::Fuse(pKF, vpMapPoints, th) (src/ORBmatcher.cc:1148-1331), the
+// matching of each point (pinhole keyframe); geometry from the caller, fma =
+// the reference build's contraction (e2 = fma(er, er, fma(ex, ex, ey*ey))).
+int orbo_fuse(const orbm_frame* kf, const float* inv_sigma2, int nmp, const uint8_t* valid, const float* u,
+              const float* v, const float* ur, const int32_t* level, const uint8_t* desc, float th, int fma,
+              int32_t* best_idx, int32_t* best_dist) {
+    Grid grid(kf);
+    int nf = 0;
+    for (int i = 0; i < nmp; ++i) {
+        best_idx[i] = -1;
+        best_dist[i] = -1;
+        if (!valid[i]) continue;
+        const int pl = level[i];
+        const float radius = th * kf->scale_factors[pl];                             // :1242
+        const std::vector<int> cand = grid.area(u[i], v[i], radius, -1, -1);
+        if (cand.empty()) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (int idx : cand) {                                                       // :1255-1308
+            const orb_keypoint& kp = kf->kps[idx];
+            const int kl = kp.octave;
+            if (kl < pl - 1 || kl > pl) continue;
+            const float ex = u[i] - kp.x, ey = v[i] - kp.y;
+            if (kf->u_right && kf->u_right[idx] >= 0) {
+                const float er = ur[i] - kf->u_right[idx];
+                const float e2 = fma ? std::fmaf(er, er, std::fmaf(ex, ex, ey * ey)) : ex * ex + ey * ey + er * er;
+                if (e2 * inv_sigma2[kl] > 7.8) continue;
+            } else {
+                const float e2 = fma ? std::fmaf(ex, ex, ey * ey) : ex * ex + ey * ey;
+                if (e2 * inv_sigma2[kl] > 5.99) continue;
+            }
+            const int dist = hamming(desc + (size_t)i * 32, kf->desc + (size_t)idx * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+        }
+        if (bestDist <= kThLow) {
+            best_idx[i] = bestIdx;
+            best_dist[i] = bestDist;
+            ++nf;
+        }
+    }
+    return nf;
+}
+
+// ORBmatcher::SearchForTriangulation (src/ORBmatcher.cc:907-1146), pinhole
+// keyframes: F12 row-major, ep = epipole of KF1's centre in KF2.
+int orbo_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                  const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                  const float* F, float ep_x, float ep_y, const float* sigma2_2, int only_stereo,
+                                  int coarse, int check_ori, int fma, int32_t* matches12) {
+    auto lin = [&](float x, float a, float y, float b, float c) {
+        return fma ? std::fmaf(x, a, y * b) + c : x * a + y * b + c;
+    };
+    auto sq = [&](float a, float b) { return fma ? std::fmaf(a, a, b * b) : a * a + b * b; };
+    int nmatches = 0;
+    std::vector<char> matched2(kf2->n, 0);                 // vbMatched2: never set in the reference
+    for (int i = 0; i < kf1->n; ++i) matches12[i] = -1;
+    std::vector<int> hist[kHisto];
+    int a = 0, b = 0;
+    while (a < fv1->nnodes && b < fv2->nnodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            for (int p = fv1->offsets[a]; p < fv1->offsets[a + 1]; ++p) {
+                const int idx1 = (int)fv1->idx[p];
+                if (has_mp1[idx1]) continue;
+                const bool st1 = kf1->u_right && kf1->u_right[idx1] >= 0;
+                if (only_stereo && !st1) continue;
+                const orb_keypoint& kp1 = kf1->kps[idx1];
+                int bestDist = kThLow, bestIdx2 = -1;
+                for (int q = fv2->offsets[b]; q < fv2->offsets[b + 1]; ++q) {
+                    const int idx2 = (int)fv2->idx[q];
+                    if (matched2[idx2] || has_mp2[idx2]) continue;
+                    const bool st2 = kf2->u_right && kf2->u_right[idx2] >= 0;
+                    if (only_stereo && !st2) continue;
+                    const int dist = hamming(kf1->desc + (size_t)idx1 * 32, kf2->desc + (size_t)idx2 * 32);
+                    if (dist > kThLow || dist > bestDist) continue;
+                    const orb_keypoint& kp2 = kf2->kps[idx2];
+                    if (!st1 && !st2) {
+                        const float distex = ep_x - kp2.x, distey = ep_y - kp2.y;
+                        if (sq(distex, distey) < 100 * kf2->scale_factors[kp2.octave]) continue;
+                    }
+                    bool ok = coarse != 0;
+                    if (!ok) {                                                       // Pinhole.cpp:115-128
+                        const float la = lin(kp1.x, F[0], kp1.y, F[3], F[6]);
+                        const float lb = lin(kp1.x, F[1], kp1.y, F[4], F[7]);
+                        const float lc = lin(kp1.x, F[2], kp1.y, F[5], F[8]);
+                        const float num = lin(la, kp2.x, lb, kp2.y, lc);
+                        const float den = sq(la, lb);
+                        if (den != 0) ok = num * num / den < 3.84 * sigma2_2[kp2.octave];
+                    }
+                    if (ok) { bestIdx2 = idx2; bestDist = dist; }
+                }
+                if (bestIdx2 >= 0) {
+                    matches12[idx1] = bestIdx2;
+                    ++nmatches;
+                    if (check_ori) hist[rot_bin(kp1.angle, kf2->kps[bestIdx2].angle)].push_back(idx1);
+                }
+            }
+            ++a;
+            ++b;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) {
+            a = (int)(std::lower_bound(fv1->node_ids + a, fv1->node_ids + fv1->nnodes, fv2->node_ids[b]) - fv1->node_ids);
+        } else {
+            b = (int)(std::lower_bound(fv2->node_ids + b, fv2->node_ids + fv2->nnodes, fv1->node_ids[a]) - fv2->node_ids);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < kHisto; ++i) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int idx1 : hist[i]) { matches12[idx1] = -1; --nmatches; }
+        }
+    }
+    return nmatches;
+}
+
+// MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:368-397) per point
+// of a CSR batch: the N x N distance matrix, each row sorted, the median at
+// 0.5 * (N - 1), the first row with the least median.
+int orbo_compute_distinctive_descriptors(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best) {
+    for (int p = 0; p < npoints; ++p) {
+        const int b = off[p];
+        const size_t N = (size_t)(off[p + 1] - b);
+        if (N == 0) { best[p] = -1; continue; }
+        std::vector<float> dist(N * N);
+        for (size_t i = 0; i < N; ++i) {
+            dist[i * N + i] = 0;
+            for (size_t j = i + 1; j < N; ++j) {
+                const int d = hamming(desc + (size_t)(b + i) * 32, desc + (size_t)(b + j) * 32);
+                dist[i * N + j] = d;
+                dist[j * N + i] = d;
+            }
+        }
+        int bestMedian = INT32_MAX, bestIdx = 0;
+        for (size_t i = 0; i < N; ++i) {
+            std::vector<int> v(dist.begin() + i * N, dist.begin() + (i + 1) * N);
+            std::sort(v.begin(), v.end());
+            const int median = v[(size_t)(0.5 * (N - 1))];
+            if (median < bestMedian) { bestMedian = median; bestIdx = (int)i; }
+        }
+        best[p] = bestIdx;
+    }
+    return 0;
+}
+
 }  // extern "C"

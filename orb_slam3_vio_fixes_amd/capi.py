@@ -21,6 +21,7 @@ EXPORTS = [
     "orbs_knn_match2", "orbs_fisheye_stereo_candidates_batch_device",
     "orbv_load_text", "orbv_text_vocab_view", "orbv_free_text", "orbv_bow_assemble", "orbv_score",
     "orbk_db_create", "orbk_db_destroy", "orbk_db_upload", "orbk_detect_relocalization_candidates",
+    "orbm_fuse", "orbm_search_for_triangulation", "orbm_compute_distinctive_descriptors",
 ]
 
 _lib = None
@@ -51,6 +52,9 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_get_profile.argtypes = [vp, vp, i32]
     L.orbm_search_by_bow_batch_device.argtypes = [vp, vp, vp, f32, i32, vp, vp, vp]
     L.orbx_set_streams.argtypes = [vp, i32]
+    L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]
+    L.orbm_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
+    L.orbm_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
     L.orbk_db_create.restype = vp
     L.orbk_db_create.argtypes = [i32]
     L.orbk_db_destroy.argtypes = [vp]

@@ -739,6 +739,251 @@ __global__ __launch_bounds__(256) void k_transform(const int* __restrict__ first
     nid_out[i] = nid;
 }
 
+
+// ---------------------------------------------------------------------------
+// Mapping-thread matchers, pinhole keyframes
+// (NLeft == -1, no mpCamera2).  The float expressions follow the reference
+// build's contraction (GCC -O3 -march=native, probed in this container):
+// a*b + c*d + e*f -> fma(e, f, fma(a, b, c*d)); x*f0 + y*f1 + f2 ->
+// fma(x, f0, y*f1) + f2.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sq2(float a, float b, int fma) { return fma ? __builtin_fmaf(a, a, b * b) : a * a + b * b; }
+__device__ __forceinline__ float lin2(float x, float a, float y, float b, float c, int fma) {
+    return fma ? __builtin_fmaf(x, a, y * b) + c : x * a + y * b + c;
+}
+
+// k_fuse: Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:1148-1331) -- the keypoint
+// each map point would fuse with; one wave per map point (the matching of a
+// point reads none of the others' results).
+struct FuseArgs {
+    const orb_keypoint* kps;
+    const uint8_t* desc;
+    const float* u_right;       // mvuRight or NULL
+    const float* scale;         // mvScaleFactors
+    const float* inv_sigma2;    // mvInvLevelSigma2
+    GridParams g;
+    const uint32_t* gsorted;
+    const int* gcount;
+    int nmp;
+    const uint8_t* valid;
+    const float *u, *v, *ur;
+    const int32_t* level;       // PredictScale
+    const uint8_t* mdesc;       // GetDescriptor()
+    float th;
+    int fma;
+    int32_t* best_idx;
+    int32_t* best_dist;
+};
+
+__global__ __launch_bounds__(256) void k_fuse(FuseArgs a) {
+    const int i = blockIdx.x * 4 + wave_id(), lane = lane_id();
+    if (i >= a.nmp) return;
+    int out_idx = -1, out_dist = 256;
+    if (a.valid[i]) {
+        const int pl = a.level[i];
+        const float r = a.th * a.scale[pl];                        // :1242
+        const float x = a.u[i], y = a.v[i];
+        CellRange cr;
+        if (cell_range(x, y, r, a.g, cr)) {
+            const uint4 q0 = *(const uint4*)(a.mdesc + (long long)i * 32);
+            const uint4 q1 = *(const uint4*)(a.mdesc + (long long)i * 32 + 16);
+            const int gn = a.gcount[0];
+            uint32_t best = 0xffffffffu;            // (dist << 20) | position in GetFeaturesInArea order
+            for (int j = lane; j < gn; j += kWave) {
+                const uint32_t gv = a.gsorted[j];
+                const int cell = (int)(gv >> 16), gx = cell / kGridRows, gy = cell - gx * kGridRows;
+                if (gx < cr.x0 || gx > cr.x1 || gy < cr.y0 || gy > cr.y1) continue;
+                const int fi = (int)(gv & 0xffff);
+                const orb_keypoint k = a.kps[fi];
+                if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;          // KeyFrame.cc:741
+                const int kl = k.octave;
+                if (kl < pl - 1 || kl > pl) continue;                               // :1262-1265
+                const float ex = x - k.x, ey = y - k.y;
+                if (a.u_right && a.u_right[fi] >= 0) {                              // :1267-1280
+                    const float er = a.ur[i] - a.u_right[fi];
+                    const float e2 = a.fma ? __builtin_fmaf(er, er, __builtin_fmaf(ex, ex, ey * ey))
+                                           : ex * ex + ey * ey + er * er;
+                    if ((double)(e2 * a.inv_sigma2[kl]) > 7.8) continue;
+                } else {
+                    const float e2 = sq2(ex, ey, a.fma);
+                    if ((double)(e2 * a.inv_sigma2[kl]) > 5.99) continue;
+                }
+                const int d = hamming32(q0, q1, a.desc + (long long)fi * 32);
+                if (d < 256) best = min(best, ((uint32_t)d << 20) | (uint32_t)j);
+            }
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+            if (best != 0xffffffffu && (int)(best >> 20) <= kThLow) {               // :1311
+                out_dist = (int)(best >> 20);
+                out_idx = (int)(a.gsorted[best & 0xfffff] & 0xffff);
+            }
+        }
+    }
+    if (lane == 0) {
+        a.best_idx[i] = out_idx;
+        a.best_dist[i] = out_idx >= 0 ? out_dist : -1;
+    }
+}
+
+// k_tri: SearchForTriangulation(pKF1, pKF2, ...) (ORBmatcher.cc:907-1146).
+// vbMatched2 is never set in the reference, so every KF1 feature is matched
+// independently: one wave per (KF1 feature, shared vocabulary node) item.
+// Inside a node the reference keeps the LAST candidate at the minimum
+// distance among those passing the checks (`dist > bestDist` skips, equal
+// distances overwrite), i.e. the lexicographic (min distance, max position).
+struct TriArgs {
+    const orb_keypoint *k1, *k2;
+    const uint8_t *d1, *d2;
+    const float *ur1, *ur2;     // mvuRight or NULL
+    const uint8_t *mp1, *mp2;   // GetMapPoint(idx) != NULL
+    const float* scale2;        // pKF2->mvScaleFactors
+    const float* sigma2_2;      // pKF2->mvLevelSigma2
+    const int32_t* item_i1;     // items: KF1 feature, range of its node's KF2 features
+    const int32_t* item_b;
+    const int32_t* item_e;
+    const uint32_t* fv2_idx;
+    int nitems;
+    float F[9];                 // F12 row-major (Eigen F12(r, c) = F[3 r + c])
+    float ep_x, ep_y;
+    int only_stereo, coarse, fma, check_ori;
+    int32_t* item_match;        // KF2 feature or -1
+    int32_t* item_bin;
+};
+
+__global__ __launch_bounds__(256) void k_tri(TriArgs a) {
+    const int t = blockIdx.x * 4 + wave_id(), lane = lane_id();
+    if (t >= a.nitems) return;
+    const int i1 = a.item_i1[t];
+    int res = -1;
+    const bool st1 = a.ur1 && a.ur1[i1] >= 0;
+    if (!a.mp1[i1] && (!a.only_stereo || st1)) {
+        const orb_keypoint kp1 = a.k1[i1];
+        const uint4 q0 = *(const uint4*)(a.d1 + (long long)i1 * 32), q1 = *(const uint4*)(a.d1 + (long long)i1 * 32 + 16);
+        // epipolar line of kp1 in image 2 (Pinhole::epipolarConstrain, Pinhole.cpp:115-117)
+        const float la = lin2(kp1.x, a.F[0], kp1.y, a.F[3], a.F[6], a.fma);
+        const float lb = lin2(kp1.x, a.F[1], kp1.y, a.F[4], a.F[7], a.fma);
+        const float lc = lin2(kp1.x, a.F[2], kp1.y, a.F[5], a.F[8], a.fma);
+        uint32_t best = 0xffffffffu;                // (dist << 16) | (0xffff - position)
+        for (int j = a.item_b[t] + lane; j < a.item_e[t]; j += kWave) {
+            const int i2 = (int)a.fv2_idx[j];
+            if (a.mp2[i2]) continue;
+            const bool st2 = a.ur2 && a.ur2[i2] >= 0;
+            if (a.only_stereo && !st2) continue;
+            const int dist = hamming32(q0, q1, a.d2 + (long long)i2 * 32);
+            if (dist > kThLow) continue;
+            const orb_keypoint kp2 = a.k2[i2];
+            if (!st1 && !st2) {                                                   // :1014-1021
+                const float ex = a.ep_x - kp2.x, ey = a.ep_y - kp2.y;
+                if (sq2(ex, ey, a.fma) < 100 * a.scale2[kp2.octave]) continue;
+            }
+            bool ok = a.coarse != 0;
+            if (!ok) {                                                            // Pinhole.cpp:119-128
+                const float num = lin2(la, kp2.x, lb, kp2.y, lc, a.fma);
+                const float den = sq2(la, lb, a.fma);
+                if (den != 0) ok = (double)(num * num / den) < 3.84 * (double)a.sigma2_2[kp2.octave];
+            }
+            if (ok) best = min(best, ((uint32_t)dist << 16) | (uint32_t)(0xffff - (j - a.item_b[t])));
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+        if (best != 0xffffffffu) res = (int)a.fv2_idx[a.item_b[t] + (0xffff - (int)(best & 0xffff))];
+        if (lane == 0 && res >= 0) a.item_bin[t] = rot_bin(kp1.angle, a.k2[res].angle);
+    }
+    if (lane == 0) a.item_match[t] = res;
+}
+
+// rotation-consistency filter and vMatches12 (:1106-1144), one workgroup
+__global__ __launch_bounds__(256) void k_tri_final(TriArgs a, int n1, int32_t* matches12, int32_t* nmatches) {
+    __shared__ int hist[kHisto];
+    __shared__ int keep[3];
+    __shared__ int cnt;
+    const int tid = threadIdx.x;
+    if (tid < kHisto) hist[tid] = 0;
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    for (int i = tid; i < n1; i += 256) matches12[i] = -1;
+    if (a.check_ori)
+        for (int t = tid; t < a.nitems; t += 256)
+            if (a.item_match[t] >= 0) atomicAdd(&hist[a.item_bin[t]], 1);
+    __syncthreads();
+    if (tid == 0) {
+        int i1 = -1, i2 = -1, i3 = -1;
+        if (a.check_ori) three_maxima(hist, i1, i2, i3);
+        keep[0] = i1; keep[1] = i2; keep[2] = i3;
+    }
+    __syncthreads();
+    for (int t = tid; t < a.nitems; t += 256) {
+        const int m = a.item_match[t];
+        if (m < 0) continue;
+        if (a.check_ori) {
+            const int b = a.item_bin[t];
+            if (b != keep[0] && b != keep[1] && b != keep[2]) continue;
+        }
+        matches12[a.item_i1[t]] = m;
+        atomicAdd(&cnt, 1);
+    }
+    __syncthreads();
+    if (tid == 0) nmatches[0] = cnt;
+}
+
+
+// k_distinctive: MapPoint::ComputeDistinctiveDescriptors (MapPoint.cc:329-405)
+// for many points; one wave per point.  Row i's median (vDists[0.5 (N-1)]
+// after sorting) is the smallest m with #{j : d_ij <= m} > (N-1)/2, found by
+// bisection over [0, 256] with the distances recomputed from the LDS copy of
+// the point's descriptors; the first row with the least median wins.
+constexpr int kDistinctiveLds = 256;   // descriptors per point held in LDS
+
+__global__ __launch_bounds__(64) void k_distinctive(int npoints, const int32_t* off, const uint8_t* desc,
+                                                    int32_t* best_out) {
+    __shared__ uint4 sd[kDistinctiveLds][2];
+    const int p = blockIdx.x, lane = lane_id();
+    if (p >= npoints) return;
+    const int b = off[p], n = off[p + 1] - b;
+    if (n <= 0) {
+        if (lane == 0) best_out[p] = -1;
+        return;
+    }
+    const uint8_t* D = desc + (long long)b * 32;
+    const bool lds = n <= kDistinctiveLds;
+    if (lds)
+        for (int i = lane; i < n; i += kWave) {
+            sd[i][0] = *(const uint4*)(D + (long long)i * 32);
+            sd[i][1] = *(const uint4*)(D + (long long)i * 32 + 16);
+        }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    auto row = [&](int i, uint4& a0, uint4& a1) {
+        if (lds) { a0 = sd[i][0]; a1 = sd[i][1]; }
+        else { a0 = *(const uint4*)(D + (long long)i * 32); a1 = *(const uint4*)(D + (long long)i * 32 + 16); }
+    };
+    const int k = (int)(0.5 * (n - 1));                       // vDists[0.5*(N-1)]
+    uint32_t best = 0xffffffffu;                               // (median << 16) | row
+    for (int i = lane; i < n; i += kWave) {
+        uint4 a0, a1;
+        row(i, a0, a1);
+        int lo = 0, hi = 256;                                  // smallest m with count(d <= m) >= k + 1
+        while (lo < hi) {
+            const int m = (lo + hi) >> 1;
+            int c = 0;
+            for (int j = 0; j < n; ++j) {
+                uint4 b0, b1;
+                row(j, b0, b1);
+                const int d = __popc(a0.x ^ b0.x) + __popc(a0.y ^ b0.y) + __popc(a0.z ^ b0.z) + __popc(a0.w ^ b0.w) +
+                              __popc(a1.x ^ b1.x) + __popc(a1.y ^ b1.y) + __popc(a1.z ^ b1.z) + __popc(a1.w ^ b1.w);
+                c += d <= m;
+            }
+            if (c >= k + 1) hi = m;
+            else lo = m + 1;
+        }
+        best = min(best, ((uint32_t)lo << 16) | (uint32_t)i);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+    if (lane == 0) best_out[p] = (int)(best & 0xffff);
+}
+
 // ---------------------------------------------------------------------------
 // host helpers
 // ---------------------------------------------------------------------------
@@ -1037,6 +1282,111 @@ int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
     ORB_CHECK(hipMemcpy(word_id, wio.p, n * 4, hipMemcpyDeviceToHost));
     ORB_CHECK(hipMemcpy(weight, wo.p, n * 8, hipMemcpyDeviceToHost));
     ORB_CHECK(hipMemcpy(node_id, nio.p, n * 4, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, const uint8_t* valid, const float* u,
+              const float* v, const float* ur, const int32_t* level, const uint8_t* desc, float th, int fma,
+              int32_t* best_idx, int32_t* best_dist) {
+    if (!kf || !inv_level_sigma2 || !kf->scale_factors || nmp < 0 || !best_idx || !best_dist) return ORB_ERR_PARAM;
+    if (nmp && (!valid || !u || !v || !ur || !level || !desc)) return ORB_ERR_PARAM;
+    if (nmp == 0) return 0;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    for (int i = 0; i < nmp; ++i)
+        if (valid[i] && (level[i] < 0 || level[i] >= kf->nlevels)) return ORB_ERR_PARAM;
+    DevFrame df;
+    if ((rc = df.upload(kf, true, 0))) return rc;
+    DBuf<float> is2, bu, bv, bur; DBuf<uint8_t> bval, bd; DBuf<int32_t> blv, bi, bdist;
+    if ((rc = is2.put(inv_level_sigma2, kf->nlevels)) || (rc = bu.put(u, nmp)) || (rc = bv.put(v, nmp)) ||
+        (rc = bur.put(ur, nmp)) || (rc = bval.put(valid, nmp)) || (rc = bd.put(desc, (size_t)nmp * 32)) ||
+        (rc = blv.put(level, nmp)) || (rc = bi.alloc(nmp)) || (rc = bdist.alloc(nmp)))
+        return rc;
+    FuseArgs a;
+    a.kps = df.kps.p; a.desc = df.desc.p; a.u_right = kf->u_right ? df.ur.p : nullptr; a.scale = df.scale.p;
+    a.inv_sigma2 = is2.p; a.g = grid_params(kf); a.gsorted = df.sorted.p; a.gcount = df.count.p; a.nmp = nmp;
+    a.valid = bval.p; a.u = bu.p; a.v = bv.p; a.ur = bur.p; a.level = blv.p; a.mdesc = bd.p; a.th = th; a.fma = fma;
+    a.best_idx = bi.p; a.best_dist = bdist.p;
+    hipLaunchKernelGGL(k_fuse, dim3((nmp + 3) / 4), dim3(256), 0, 0, a);
+    ORB_CHECK(hipGetLastError());
+    ORB_CHECK(hipMemcpy(best_idx, bi.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(best_dist, bdist.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int i = 0; i < nmp; ++i) n += best_idx[i] >= 0;
+    return n;
+}
+
+int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                  const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                  const float* F12, float ep_x, float ep_y, const float* level_sigma2_2,
+                                  int only_stereo, int coarse, int check_ori, int fma, int32_t* matches12) {
+    if (!kf1 || !kf2 || !fv1 || !fv2 || !has_mp1 || !has_mp2 || !F12 || !level_sigma2_2 || !matches12 ||
+        !kf2->scale_factors)
+        return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    // items: every KF1 feature of a node both FeatureVectors hold (the merge of :962-1100)
+    std::vector<int32_t> it_i1, it_b, it_e;
+    int a = 0, b = 0;
+    while (a < fv1->nnodes && b < fv2->nnodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            for (int j = fv1->offsets[a]; j < fv1->offsets[a + 1]; ++j) {
+                it_i1.push_back((int32_t)fv1->idx[j]);
+                it_b.push_back(fv2->offsets[b]);
+                it_e.push_back(fv2->offsets[b + 1]);
+            }
+            ++a;
+            ++b;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) {
+            ++a;
+        } else {
+            ++b;
+        }
+    }
+    const int nitems = (int)it_i1.size();
+    DevFrame f1, f2;
+    if ((rc = f1.upload(kf1, false, 0)) || (rc = f2.upload(kf2, false, 0))) return rc;
+    DBuf<uint8_t> m1, m2; DBuf<float> s2; DBuf<int32_t> bi1, bb, be, bm, bbin, out, nm; DBuf<uint32_t> fidx;
+    const int n2idx = fv2->nnodes ? fv2->offsets[fv2->nnodes] : 0;
+    if ((rc = m1.put(has_mp1, std::max(1, kf1->n))) || (rc = m2.put(has_mp2, std::max(1, kf2->n))) ||
+        (rc = s2.put(level_sigma2_2, kf2->nlevels)) || (rc = bi1.put(it_i1.data(), nitems)) ||
+        (rc = bb.put(it_b.data(), nitems)) || (rc = be.put(it_e.data(), nitems)) ||
+        (rc = fidx.put(fv2->idx, n2idx)) || (rc = bm.alloc(std::max(1, nitems))) ||
+        (rc = bbin.alloc(std::max(1, nitems))) || (rc = out.alloc(std::max(1, kf1->n))) || (rc = nm.alloc(1)))
+        return rc;
+    TriArgs ta;
+    ta.k1 = f1.kps.p; ta.k2 = f2.kps.p; ta.d1 = f1.desc.p; ta.d2 = f2.desc.p;
+    ta.ur1 = kf1->u_right ? f1.ur.p : nullptr; ta.ur2 = kf2->u_right ? f2.ur.p : nullptr;
+    ta.mp1 = m1.p; ta.mp2 = m2.p; ta.scale2 = f2.scale.p; ta.sigma2_2 = s2.p;
+    ta.item_i1 = bi1.p; ta.item_b = bb.p; ta.item_e = be.p; ta.fv2_idx = fidx.p; ta.nitems = nitems;
+    for (int k = 0; k < 9; ++k) ta.F[k] = F12[k];
+    ta.ep_x = ep_x; ta.ep_y = ep_y; ta.only_stereo = only_stereo; ta.coarse = coarse; ta.fma = fma;
+    ta.check_ori = check_ori; ta.item_match = bm.p; ta.item_bin = bbin.p;
+    if (nitems) hipLaunchKernelGGL(k_tri, dim3((nitems + 3) / 4), dim3(256), 0, 0, ta);
+    hipLaunchKernelGGL(k_tri_final, dim3(1), dim3(256), 0, 0, ta, kf1->n, out.p, nm.p);
+    ORB_CHECK(hipGetLastError());
+    int32_t n = 0;
+    if (kf1->n) ORB_CHECK(hipMemcpy(matches12, out.p, kf1->n * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(&n, nm.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    return n;
+}
+
+int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best,
+                                         int device) {
+    if (npoints < 0 || (npoints && (!off || !best))) return ORB_ERR_PARAM;
+    if (npoints == 0) return ORB_OK;
+    const int total = off[npoints];
+    if (off[0] != 0 || total < 0 || (total && !desc)) return ORB_ERR_PARAM;
+    for (int p = 0; p < npoints; ++p)
+        if (off[p + 1] < off[p] || off[p + 1] - off[p] > 65535) return ORB_ERR_PARAM;
+    if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    int rc;
+    DBuf<int32_t> bo, bb; DBuf<uint8_t> bd;
+    if ((rc = bo.put(off, (size_t)npoints + 1)) || (rc = bd.put(desc, (size_t)total * 32)) || (rc = bb.alloc(npoints)))
+        return rc;
+    hipLaunchKernelGGL(k_distinctive, dim3(npoints), dim3(64), 0, 0, npoints, bo.p, bd.p, bb.p);
+    ORB_CHECK(hipGetLastError());
+    ORB_CHECK(hipMemcpy(best, bb.p, npoints * sizeof(int32_t), hipMemcpyDeviceToHost));
     return ORB_OK;
 }
 

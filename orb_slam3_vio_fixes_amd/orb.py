@@ -340,6 +340,47 @@ class ORBmatcher:
         capi.check(nm, "SearchByProjection(F, LastFrame)")
         return nm, owner
 
+    @staticmethod
+    def Fuse(KF: abi.Keep, inv_level_sigma2, valid, u, v, ur, level, desc, th: float = 3.0, fma: int = 1):
+        """Fuse(pKF, vpMapPoints, th) matching (ORBmatcher.cc:1148-1331): (nfused, best_idx, best_dist)."""
+        n = len(valid)
+        arrs = [np.ascontiguousarray(inv_level_sigma2, np.float32), np.ascontiguousarray(valid, np.uint8),
+                np.ascontiguousarray(u, np.float32), np.ascontiguousarray(v, np.float32),
+                np.ascontiguousarray(ur, np.float32), np.ascontiguousarray(level, np.int32),
+                np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)]
+        bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        nf = capi.lib().orbm_fuse(KF.ref(), *[abi.ptr(a) for a in arrs[:1]], n, *[abi.ptr(a) for a in arrs[1:]],
+                                  th, fma, abi.ptr(bi), abi.ptr(bd))
+        capi.check(min(nf, 0), "Fuse")
+        return nf, bi, bd
+
+    def SearchForTriangulation(self, KF1: abi.Keep, fv1: abi.Keep, has_mp1, KF2: abi.Keep, fv2: abi.Keep, has_mp2,
+                               F12, ep, level_sigma2_2, bOnlyStereo: bool = False, bCoarse: bool = False,
+                               fma: int = 1):
+        """SearchForTriangulation (ORBmatcher.cc:907-1146): (nmatches, matches12)."""
+        m1 = np.ascontiguousarray(has_mp1, np.uint8)
+        m2 = np.ascontiguousarray(has_mp2, np.uint8)
+        F = np.ascontiguousarray(F12, np.float32).reshape(9)
+        s2 = np.ascontiguousarray(level_sigma2_2, np.float32)
+        out = np.full(len(m1), -1, np.int32)
+        nm = capi.lib().orbm_search_for_triangulation(KF1.ref(), fv1.ref(), abi.ptr(m1), KF2.ref(), fv2.ref(),
+                                                      abi.ptr(m2), abi.ptr(F), float(ep[0]), float(ep[1]),
+                                                      abi.ptr(s2), int(bOnlyStereo), int(bCoarse),
+                                                      int(self.mbCheckOrientation), fma, abi.ptr(out))
+        capi.check(min(nm, 0), "SearchForTriangulation")
+        return nm, out
+
+
+def compute_distinctive_descriptors(off, desc, device: int = 0) -> np.ndarray:
+    """MapPoint::ComputeDistinctiveDescriptors for every point of a CSR batch:
+    per point the index of its most distinctive descriptor (-1 if none)."""
+    off = np.ascontiguousarray(off, np.int32)
+    desc = np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)
+    best = np.zeros(max(len(off) - 1, 0), np.int32)
+    capi.check(capi.lib().orbm_compute_distinctive_descriptors(len(best), abi.ptr(off), abi.ptr(desc), abi.ptr(best),
+                                                               device), "orbm_compute_distinctive_descriptors")
+    return best
+
 
 def transform(voc, desc: np.ndarray, levelsup: int = 4, device: int = 0):
     """TemplatedVocabulary::transform per descriptor on the GPU: (word_id, weight, node_id)."""
