@@ -679,6 +679,101 @@ __device__ __forceinline__ short4 child_rect(short4 r, int q) {
     }
 }
 
+// One __introsort_loop step on [f, l) by a whole wave: partition_ranks
+// (orb_math.h) with the L / R lists built by ballots.
+__device__ int wave_partition(SortRec* a, int f, int l, int* Lp, int* Rp) {
+    const int lane = lane_id();
+    if (lane == 0) median_to_first_(a + f, a + f + 1, a + f + (l - f) / 2, a + l - 1);
+    fast_wave_sync();
+    const SortRec pv = a[f];
+    int cl = 0, cr = 0;
+    for (int base = f + 1; base < l; base += kWave) {
+        const int p = base + lane;
+        bool ge = false, le = false;
+        if (p < l) {
+            const SortRec x = a[p];
+            ge = !node_less(x, pv);
+            le = !node_less(pv, x);
+        }
+        const uint64_t mg = __ballot(ge), ml = __ballot(le);
+        if (ge) Lp[f + cl + mask_rank(mg)] = p;
+        if (le) Rp[f + cr + mask_rank(ml)] = p;
+        cl += __popcll(mg);
+        cr += __popcll(ml);
+    }
+    fast_wave_sync();
+    const int kmax = min(cl, cr + 1);
+    int ks = 0;
+    for (int base = 0; base < kmax; base += kWave) {
+        const int k = base + lane;
+        bool pr = false;
+        if (k < kmax) pr = Lp[f + k] < (k < cr ? Rp[f + cr - 1 - k] : f);
+        ks += __popcll(__ballot(pr));            // the predicate holds on a prefix
+    }
+    const int lk = ks < cl ? Lp[f + ks] : 0x7fffffff;
+    const int rk = ks == 0 ? l : (ks - 1 < cr ? Rp[f + cr - ks] : f);
+    const int cut = min(lk, rk);
+    for (int k = lane; k < ks; k += kWave) {
+        const int i = Lp[f + k], j = Rp[f + cr - 1 - k];
+        const SortRec x = a[i], y = a[j];
+        a[i] = y;
+        a[j] = x;
+    }
+    fast_wave_sync();
+    return cut;
+}
+
+// std::sort(a, a + m) under compareNodes by the whole workgroup: levels of
+// disjoint ranges partitioned by one wave each, then a stable insertion sort
+// per leaf by one thread each (std_sort_levels, orb_math.h, checked against
+// std::sort on the host).  Where the reference would heap-sort (depth limit),
+// the original array is restored and sorted by the sequential port.
+__device__ void block_std_sort(SortRec* a, int m, SortRec* backup, int* Lp, int* Rp, SortFrame* qa, SortFrame* qb,
+                               int* leaves, int* ctl, SortFrame* stk) {
+    const int tid = threadIdx.x, T = blockDim.x, lane = lane_id(), wv = wave_id(), nw = T / kWave;
+    if (m <= 1) return;
+    for (int i = tid; i < m; i += T) backup[i] = a[i];
+    if (tid == 0) {
+        ctl[0] = 0; ctl[1] = 0; ctl[2] = 0; ctl[3] = 0;
+        if (m > 16) { qa[0] = SortFrame{0, m, ilg(m) * 2}; ctl[0] = 1; }
+        else { leaves[0] = m; ctl[3] = 1; }                // leaf = (f << 16) | l
+    }
+    __syncthreads();
+    while (true) {
+        const int na = ctl[0];
+        if (na == 0 || ctl[2]) break;
+        for (int r = wv; r < na; r += nw) {
+            const SortFrame fr = qa[r];
+            if (fr.depth == 0) {
+                if (lane == 0) ctl[2] = 1;
+                continue;
+            }
+            const int cut = wave_partition(a, fr.f, fr.l, Lp, Rp);
+            if (lane == 0) {
+                const SortFrame kids[2] = {SortFrame{fr.f, cut, fr.depth - 1}, SortFrame{cut, fr.l, fr.depth - 1}};
+                for (int c = 0; c < 2; ++c) {
+                    if (kids[c].l - kids[c].f > 16) qb[atomicAdd(&ctl[1], 1)] = kids[c];
+                    else leaves[atomicAdd(&ctl[3], 1)] = (kids[c].f << 16) | kids[c].l;
+                }
+            }
+        }
+        __syncthreads();
+        if (tid == 0) { ctl[0] = ctl[1]; ctl[1] = 0; }
+        SortFrame* t = qa; qa = qb; qb = t;
+        __syncthreads();
+    }
+    if (ctl[2]) {
+        for (int i = tid; i < m; i += T) a[i] = backup[i];
+        __syncthreads();
+        if (tid == 0) std_sort(a, m, stk);
+        __syncthreads();
+        return;
+    }
+    const int nleaf = ctl[3];
+    for (int i = tid; i < nleaf; i += T) insertion_sort_(a + (leaves[i] >> 16), a + (leaves[i] & 0xffff));
+    __syncthreads();
+}
+
 // Divide s.ord[0..m) (ccnt/kq already computed for them, s.div set for every
 // node); rebuild the list into buffer cur^1; remap the keys.  Returns the new
 // size; *nexp receives the queue length.
@@ -871,8 +966,9 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         }
         for (int i = tid; i < size; i += T) s.div[i] = 0;
         __syncthreads();
-        if (tid == 0) std_sort(s.srt, m, s.stk);
-        __syncthreads();
+        // ccnt / newpos / ord are free until qt_count below
+        block_std_sort(s.srt, m, (SortRec*)s.ccnt, s.newpos, s.newpos + NC, (SortFrame*)(s.newpos + 2 * NC),
+                       (SortFrame*)(s.newpos + 3 * NC), s.ord, s.misc + 4, s.stk);
         for (int j = tid; j < m; j += T) s.div[s.srt[j].pos] = 1;
         __syncthreads();
         qt_count(s, cur, size, K, keys, knode, kq);

@@ -222,4 +222,65 @@ ORB_HD void std_sort(SortRec* first, int n, SortFrame* stk) {
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// The same permutation from data-parallel steps (k_quadtree).  One step of
+// __introsort_loop on [f, l): median of three to first, then
+// __unguarded_partition restated by ranks.  With L = ascending positions in
+// [f+1, l) holding x >= pivot (!(x < pivot)) and R = descending positions in
+// [f, l) holding x <= pivot, the scanners' k-th stops are L[k] and R[k] as
+// long as L[k] < R[k] (each scanner only passes unexamined originals), the
+// first k* with L[k*] >= R[k*] ends the loop at min(L[k*], R[k*-1]) (R[-1] = l:
+// the left scanner runs into the value the last swap left at R[k*-1]), and the
+// swaps are the pairs (L[k], R[k]), k < k*, all disjoint.  Every leaf range
+// (<= 16 elements) ends up holding exactly its own elements, so the final
+// insertion pass is a stable insertion sort per leaf.
+// partition_ranks is the sequential statement (host check); the kernel
+// computes L, R and k* with ballots.
+// ---------------------------------------------------------------------------
+ORB_HD int partition_ranks(SortRec* a, int f, int l, int* Lp, int* Rp) {
+    median_to_first_(a + f, a + f + 1, a + f + (l - f) / 2, a + l - 1);
+    const SortRec pv = a[f];
+    int cl = 0, cr = 0;
+    for (int p = f + 1; p < l; ++p) {
+        if (!node_less(a[p], pv)) Lp[f + cl++] = p;
+        if (!node_less(pv, a[p])) Rp[f + cr++] = p;          // ascending; R[k] = Rp[f + cr - 1 - k]
+    }
+    auto R = [&](int k) { return k < cr ? Rp[f + cr - 1 - k] : f; };
+    int ks = 0;
+    while (ks < cl && ks <= cr && Lp[f + ks] < R(ks)) ++ks;
+    const int lk = ks < cl ? Lp[f + ks] : 0x7fffffff;
+    const int rk = ks == 0 ? l : R(ks - 1);
+    const int cut = lk < rk ? lk : rk;
+    for (int k = 0; k < ks; ++k) rec_swap(a + Lp[f + k], a + R(k));
+    return cut;
+}
+
+// Sequential statement of k_quadtree's level-synchronous driver: returns
+// false where the reference would heap-sort a range (depth limit reached),
+// in which case the caller falls back to std_sort on the original array.
+ORB_HD bool std_sort_levels(SortRec* a, int n, int* Lp, int* Rp, SortFrame* qa, SortFrame* qb, SortFrame* leaves) {
+    if (n <= 1) return true;
+    int na = 0, nleaf = 0;
+    if (n > 16) qa[na++] = {0, n, ilg(n) * 2};
+    else leaves[nleaf++] = {0, n, 0};
+    while (na) {
+        int nb = 0;
+        for (int r = 0; r < na; ++r) {
+            const SortFrame fr = qa[r];
+            if (fr.depth == 0) return false;
+            const int cut = partition_ranks(a, fr.f, fr.l, Lp, Rp);
+            const SortFrame kids[2] = {{fr.f, cut, fr.depth - 1}, {cut, fr.l, fr.depth - 1}};
+            for (const SortFrame& k : kids) {
+                if (k.l - k.f > 16) qb[nb++] = k;
+                else leaves[nleaf++] = k;
+            }
+        }
+        for (int r = 0; r < nb; ++r) qa[r] = qb[r];
+        na = nb;
+    }
+    for (int i = 0; i < nleaf; ++i) insertion_sort_(a + leaves[i].f, a + leaves[i].l);
+    return true;
+}
+
 }  // namespace orbmi

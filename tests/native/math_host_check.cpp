@@ -48,6 +48,9 @@ long long sincos_mismatches(uint32_t lo_bits, uint32_t hi_bits, int nthreads, ui
 
 // Sort `trials` random arrays (heavy ties) with std::sort on pair<int,Node*>
 // under compareNodes semantics and with the port; return #arrays that differ.
+static int g_level_fallbacks = 0;
+int level_fallbacks() { return g_level_fallbacks; }
+
 int sort_mismatches(int trials, int maxn, unsigned seed) {
     std::mt19937 rng(seed);
     int bad = 0;
@@ -70,9 +73,22 @@ int sort_mismatches(int trials, int maxn, unsigned seed) {
             return a.second->x0 < b.second->x0;
         });
         orbmi::SortFrame stk[80];
+        std::vector<orbmi::SortRec> lev(port);
         orbmi::std_sort(port.data(), n, stk);
         for (int i = 0; i < n; ++i)
             if (ref[i].second != &nodes[port[i].pos]) { ++bad; break; }
+        // the data-parallel restatement (k_quadtree): same permutation, or a
+        // reported depth-limit case that falls back to std_sort
+        std::vector<int> Lp(n), Rp(n);
+        std::vector<orbmi::SortFrame> qa(n + 1), qb(n + 1), lv(n + 1);
+        std::vector<orbmi::SortRec> orig(lev);
+        if (!orbmi::std_sort_levels(lev.data(), n, Lp.data(), Rp.data(), qa.data(), qb.data(), lv.data())) {
+            lev = orig;
+            orbmi::std_sort(lev.data(), n, stk);
+            ++g_level_fallbacks;
+        }
+        for (int i = 0; i < n; ++i)
+            if (ref[i].second != &nodes[lev[i].pos]) { ++bad; break; }
     }
     return bad;
 }

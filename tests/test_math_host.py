@@ -23,6 +23,7 @@ def lib(tmp_path_factory):
     L.sincos_mismatches.restype = C.c_longlong
     L.sincos_mismatches.argtypes = [C.c_uint32, C.c_uint32, C.c_int, C.POINTER(C.c_uint32)]
     L.sort_mismatches.argtypes = [C.c_int, C.c_int, C.c_uint]
+    L.level_fallbacks.argtypes = []
     L.port_fast_atan2.restype = C.c_float
     L.port_fast_atan2.argtypes = [C.c_float, C.c_float]
     return L
@@ -35,8 +36,12 @@ def test_sincosf_exhaustive_0_2pi(lib):
 
 
 def test_introsort_port_matches_std_sort(lib):
+    """The iterative port and the data-parallel restatement (partition by
+    ranks, stable per-leaf insertion) both give std::sort's permutation."""
     assert lib.sort_mismatches(5000, 600, 7) == 0
     assert lib.sort_mismatches(2000, 40, 11) == 0
+    assert lib.sort_mismatches(3000, 1200, 13) == 0
+    assert lib.level_fallbacks() < 50
 
 
 def test_fast_atan2_port_matches_oracle(lib):
