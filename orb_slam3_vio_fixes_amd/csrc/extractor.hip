@@ -1056,22 +1056,40 @@ struct DescKp {
     uint32_t key;
 };
 
-__device__ __forceinline__ bool desc_slot(const DescArgs& a, long long s, DescKp& k) {
+// The wave's run of slots is resolved once, lane j holding slot s_begin + j
+// (validity, key, level geometry), so the keypoint loop reads everything from
+// registers (readlane) and no dependent load chain stands between a keypoint
+// and the prefetch of the next one's patch.
+struct DescLane {
+    uint64_t img;
+    int pitch, w, h;
+    uint32_t key;
+};
+
+__device__ __forceinline__ bool desc_lane(const DescArgs& a, long long s, DescLane& k) {
     const int f = (int)(s / a.out_total);
     const int o = (int)(s - (long long)f * a.out_total);
     const int l = a.slot_level[o];
     const LevelDev& lv = a.lv[l];
     if (o - lv.out_base >= a.qt_n[f * a.L + l]) return false;
-    const uint8_t* img = l == 0 ? a.in + f * a.in_fstride : a.pyr + f * a.pyr_fstride + lv.off;
-    // wave-uniform: pin to SGPRs
-    const uint64_t ip = (uint64_t)img;
-    k.img = (const uint8_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ip >> 32)) << 32) |
-                             (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ip));
-    k.pitch = __builtin_amdgcn_readfirstlane(l == 0 ? a.in_pitch : lv.pitch);
-    k.w = __builtin_amdgcn_readfirstlane(lv.w);
-    k.h = __builtin_amdgcn_readfirstlane(lv.h);
-    k.key = (uint32_t)__builtin_amdgcn_readfirstlane((int)a.qt_key[s]);
+    k.img = (uint64_t)(l == 0 ? a.in + f * a.in_fstride : a.pyr + f * a.pyr_fstride + lv.off);
+    k.pitch = l == 0 ? a.in_pitch : lv.pitch;
+    k.w = lv.w;
+    k.h = lv.h;
+    k.key = a.qt_key[s];
     return true;
+}
+
+__device__ __forceinline__ DescKp desc_pick(const DescLane& k, int j) {
+    DescKp d;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)k.img, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(k.img >> 32), j);
+    d.img = (const uint8_t*)(((uint64_t)hi << 32) | lo);
+    d.pitch = __builtin_amdgcn_readlane(k.pitch, j);
+    d.w = __builtin_amdgcn_readlane(k.w, j);
+    d.h = __builtin_amdgcn_readlane(k.h, j);
+    d.key = (uint32_t)__builtin_amdgcn_readlane((int)k.key, j);
+    return d;
 }
 
 __device__ __forceinline__ void wave_sync() {
@@ -1142,16 +1160,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     // this wave's run of kDescSlots slots; the next valid slot's patch is
     // always in flight while the current one is described
     const long long s_begin = ((long long)blockIdx.x * 4 + wv) * kDescSlots;
-    const long long s_end = min(s_begin + kDescSlots, a.nslots);
+    const int nrun = (int)min((long long)kDescSlots, a.nslots - s_begin);
+    DescLane mine{};
+    const bool valid = lane < nrun && desc_lane(a, s_begin + lane, mine);
+    uint64_t todo = __ballot(valid);
     uint32_t pv[kPV];
-    DescKp cur{}, nxt{};
-    long long s = s_begin;
-    while (s < s_end && !desc_slot(a, s, cur)) ++s;
-    if (s < s_end) {
+    DescKp cur{};
+    int jc = -1;
+    if (todo) {
+        jc = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        cur = desc_pick(mine, jc);
         const int x0 = (int)(cur.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((cur.key >> 12) & 0xfff) + (kEdge - 3) - 21;
         if (patch_interior(cur.w, cur.h, x0, y0)) patch_issue(cur.img, cur.pitch, x0, y0, pv);
     }
-    while (s < s_end) {
+    while (jc >= 0) {
+        const long long s = s_begin + jc;
         const uint32_t key = cur.key;
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
         // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
@@ -1163,9 +1187,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             patch_border(cur.img, cur.pitch, cur.w, cur.h, cx - 21, cy - 21, raw);
         }
         // prefetch the next keypoint's patch (in flight during this keypoint)
-        long long sn = s + 1;
-        while (sn < s_end && !desc_slot(a, sn, nxt)) ++sn;
-        if (sn < s_end) {
+        int jn = -1;
+        DescKp nxt{};
+        if (todo) {
+            jn = __builtin_ctzll(todo);
+            todo &= todo - 1;
+            nxt = desc_pick(mine, jn);
             const int x0 = (int)(nxt.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((nxt.key >> 12) & 0xfff) + (kEdge - 3) - 21;
             if (patch_interior(nxt.w, nxt.h, x0, y0)) patch_issue(nxt.img, nxt.pitch, x0, y0, pv);
         }
@@ -1270,7 +1297,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         uint8_t* d = a.sdesc + s * 32;
         if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
         if (lane == 0) a.angle[s] = ang_deg;
-        s = sn;
+        jc = jn;
         cur = nxt;
         wave_sync();
     }
