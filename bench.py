@@ -8,7 +8,10 @@ HBM before the timed region:
 ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
 on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
 F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
-(Tracking.cc:2459-2492).  Multi-GPU: one process per GPU, frames sharded
+(Tracking.cc:2459-2492).  Steps are pipelined: the matching of step k runs
+on a second HIP stream while step k+1 extracts into a second output set
+(--no-pipeline serialises them); all K steps' work is inside the timed
+region.  Multi-GPU: one process per GPU, frames sharded
 (weak scaling, no data-path collective); timing = max over ranks.
 
 Extra objects on the JSON line:
@@ -57,6 +60,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--pmc-summary", default=str(PMC_SUMMARY), help="rocprofv3 PMC summary (tools/pmc_summary.py)")
+    ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
+                    help="run SearchForInitialization on the extraction stream (no step overlap)")
     ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
     return ap.parse_args()
 
@@ -146,25 +151,42 @@ def main():
     capi.check(L.orbx_set_streams(ex._h, args.streams), "orbx_set_streams")
     stream = torch.cuda.current_stream(dev)
     kps, desc, n, mono, cap = ex.extract_batch_device(frames, LAP)
+    # two output sets: SearchForInitialization of step k runs on its own
+    # stream while step k+1 extracts into the other set (--no-pipeline: both
+    # on the extraction stream)
+    outs = [(kps, desc, n, mono), tuple(torch.empty_like(x) for x in (kps, desc, n, mono))]
+    mstream = torch.cuda.Stream(dev) if args.pipeline else stream
+    done = [None, None]                  # match of set i finished (recorded on mstream)
     matches = torch.empty((B - 1, cap), dtype=torch.int32, device=dev)
     nmatch = torch.empty(B - 1, dtype=torch.int32, device=dev)
     inv_w = float(np.float32(64) / np.float32(W))
     inv_h = float(np.float32(48) / np.float32(H))
 
     match_events = []
+    counter = [0]
 
     def step(timed=False):
-        ex.extract_batch_device(frames, LAP, out=(kps, desc, n, mono))
+        i = counter[0] % 2
+        counter[0] += 1
+        k_, d_, n_, m_ = outs[i]
+        if done[i] is not None:
+            stream.wait_event(done[i])   # the match that read this set has finished
+        ex.extract_batch_device(frames, LAP, out=(k_, d_, n_, m_))
+        extracted = torch.cuda.Event()
+        extracted.record(stream)
+        mstream.wait_event(extracted)
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
+            e0.record(mstream)
         rc = L.orbm_search_for_initialization_batch_device(
-            B, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
-            100, 0.9, 1, matches.data_ptr(), nmatch.data_ptr(), stream.cuda_stream)
+            B, k_.data_ptr(), d_.data_ptr(), n_.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
+            100, 0.9, 1, matches.data_ptr(), nmatch.data_ptr(), mstream.cuda_stream)
         capi.check(rc, "SearchForInitialization batch")
         if timed:
-            e1.record(stream)
+            e1.record(mstream)
             match_events.append((e0, e1))
+        done[i] = torch.cuda.Event()
+        done[i].record(mstream)
 
     for _ in range(args.warmup):
         step()
@@ -219,7 +241,7 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
-                          "frames_per_step_per_gpu": B, "streams": args.streams, "parallelism": f"frames sharded over {world} GPU(s)"},
+                          "frames_per_step_per_gpu": B, "streams": args.streams, "pipeline": args.pipeline, "parallelism": f"frames sharded over {world} GPU(s)"},
                "stage_ms": {**{k: float(v) for k, v in zip(STAGES, stage_ms)},
                             "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
                                                           if match_events else None)},
