@@ -14,7 +14,9 @@ namespace orbmi {
 constexpr int kWave = 64;
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
-__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+// wave index within the block, made wave-uniform (SGPR) so per-wave indexing
+// of global tables compiles to scalar loads
+__device__ __forceinline__ int wave_id() { return __builtin_amdgcn_readfirstlane(threadIdx.x >> 6); }
 
 __device__ __forceinline__ int wave_sum(int v) {
 #pragma unroll

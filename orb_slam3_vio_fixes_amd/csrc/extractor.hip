@@ -396,6 +396,29 @@ __device__ __forceinline__ uint32_t pix4(uint32_t lo, uint32_t hi) {
 
 constexpr int kCandIdx = 0x3fff, kCandBright = 0x4000, kCandDark = 0x8000;
 
+#ifdef ORB_FAST_TIMING
+// phase profile of k_fast_cells (tools/fast_phases.py): shader cycles per phase
+__device__ unsigned long long g_fast_t[1024][16];   // spread: no contended atomics
+#define FAST_T(k)                                                            \
+    do {                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+        const unsigned long long d_ = t_ - tlast;                            \
+        tlast = t_;                                                          \
+        switch (k) {                                                         \
+            case 0: t0 += d_; break;                                         \
+            case 1: t1 += d_; break;                                         \
+            case 2: t2 += d_; break;                                         \
+            case 3: t3 += d_; break;                                         \
+            case 5: t5 += d_; break;                                         \
+            case 6: t6 += d_; break;                                         \
+            case 7: t7 += d_; break;                                         \
+            default: t9 += d_; break;                                        \
+        }                                                                    \
+    } while (0)
+#else
+#define FAST_T(k) do { } while (0)
+#endif
+
 // each wave of k_fast_cells owns its cells and its LDS region: wave-level sync only
 __device__ __forceinline__ void fast_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -406,7 +429,10 @@ __device__ __forceinline__ void fast_wave_sync() {
 // row/column of linear window index i (ww <= 4096): exact via a float reciprocal
 __device__ __forceinline__ int div_row(int i, float inv_ww) { return (int)(((float)i + 0.5f) * inv_ww); }
 
-constexpr int kCellsPerWave = 4;
+#ifndef ORB_FAST_CELLS_PER_WAVE
+#define ORB_FAST_CELLS_PER_WAVE 4
+#endif
+constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 
 struct RoiFetch {
     const uint8_t* src;
@@ -419,16 +445,21 @@ __device__ __forceinline__ void roi_issue(const RoiFetch& rf, int y0, uint32_t (
     const int lane = lane_id();
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const int i = lane + j * kWave;
-        if (i < rf.n) {
-            const int r = div_row(i, rf.inv_nd), d = i - r * rf.nd;
-            v[j] = *(const uint32_t*)(rf.src + (long long)(y0 + r) * rf.pitch + rf.base + 4 * d);
-        }
+        // branch-free: lanes past the ROI re-read its last dword (rf.n >= 1), so
+        // the loads issue back to back with no per-load vmcnt waits at joins
+        const int i = min(lane + j * kWave, rf.n - 1);
+        const int r = div_row(i, rf.inv_nd), d = i - r * rf.nd;
+        v[j] = *(const uint32_t*)(rf.src + (long long)(y0 + r) * rf.pitch + rf.base + 4 * d);
     }
 }
 
+#ifdef ORB_FAST_WPE
+#define FAST_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ORB_FAST_WPE)))
+#else
+#define FAST_WPE_ATTR
+#endif
 template <int NV>
-__global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
+__global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
     const int f = blockIdx.y;
@@ -436,33 +467,50 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
     uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
     uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_max entries
     uint64_t* kmask = (uint64_t*)(sc + 3 * a.win_max);        // NMS ballots, one per 64 candidates
+#ifdef ORB_FAST_TIMING
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+#endif
     const int c_begin = (blockIdx.x * 4 + wv) * kCellsPerWave;
     const int c_end = min(c_begin + kCellsPerWave, a.ncells);
+    // the plan tables are read-only here: constant address space -> scalar loads
+    typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
+    typedef __attribute__((address_space(4))) const CellDev* ConstCells;
+    const ConstLevels lvc = (ConstLevels)a.lv;
+    const ConstCells cells = (ConstCells)a.cells;
+    auto cell_at = [&](int i) {
+        CellDev r;
+        r.level = cells[i].level; r.x0 = cells[i].x0; r.y0 = cells[i].y0; r.cols = cells[i].cols;
+        r.rows = cells[i].rows; r.slot_off = cells[i].slot_off; r.cap = cells[i].cap;
+        return r;
+    };
     auto fetch_of = [&](const CellDev& c) {
         RoiFetch rf;
         if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
-        else { rf.src = a.pyr + f * a.pyr_fstride + a.lv[c.level].off; rf.pitch = a.lv[c.level].pitch; }
+        else { rf.src = a.pyr + f * a.pyr_fstride + lvc[c.level].off; rf.pitch = lvc[c.level].pitch; }
         rf.base = c.x0 & ~3;
         rf.nd = ((c.x0 - rf.base) + c.cols + 3) >> 2;
-        rf.n = c.rows * rf.nd;
+        rf.n = max(1, c.rows * rf.nd);   // >= 1: the branch-free issue clamps to rf.n - 1
         rf.inv_nd = 1.0f / (float)rf.nd;
         return rf;
     };
+    // cell descriptors (scalar loads) run two cells ahead, ROI loads one cell ahead
     uint32_t v[NV];
-    CellDev c{};
+    CellDev c{}, cn{};
     RoiFetch rf{};
     if (c_begin < c_end) {
-        c = a.cells[c_begin];
+        c = cell_at(c_begin);
         rf = fetch_of(c);
         roi_issue<NV>(rf, c.y0, v);
     }
+    if (c_begin + 1 < c_end) cn = cell_at(c_begin + 1);
+#ifdef ORB_FAST_TIMING
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t5 = 0, t6 = 0, t7 = 0, t9 = 0;
+    unsigned long long tlast = t_start;
+#endif
     for (int ci = c_begin; ci < c_end; ++ci) {
         // land the prefetched ROI in LDS, then prefetch the next cell's ROI
 #pragma unroll
-        for (int j = 0; j < NV; ++j) {
-            const int i = lane + j * kWave;
-            if (i < rf.n) ((uint32_t*)roi)[i] = v[j];
-        }
+        for (int j = 0; j < NV; ++j) ((uint32_t*)roi)[min(lane + j * kWave, rf.n - 1)] = v[j];
         const int shift = c.x0 - rf.base, rstride = rf.nd * 4;
         const uint8_t* R = roi + shift;
         const int ww = max(0, c.cols - 6), wh = max(0, c.rows - 6);
@@ -470,11 +518,13 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         for (int i = lane; i < (npad + 3) / 4; i += kWave) ((uint32_t*)sc)[i] = 0u;
         const CellDev cur = c;
         if (ci + 1 < c_end) {
-            c = a.cells[ci + 1];
+            c = cn;
             rf = fetch_of(c);
             roi_issue<NV>(rf, c.y0, v);
         }
+        if (ci + 2 < c_end) cn = cell_at(ci + 2);
         fast_wave_sync();
+        FAST_T(0);
         const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
         const int X0 = shift + 3, j0 = X0 >> 2;
         const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
@@ -482,7 +532,6 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         const float inv_ndw = ndw ? 1.0f / (float)ndw : 0.f;
         const uint32_t* roi32 = (const uint32_t*)roi;
         const int rs4 = rstride >> 2;
-        const int cap = a.win_max;
         // FAST(ROI, iniThFAST) and, only if that leaves no corner, FAST(ROI,
         // minThFAST) (ORBextractor.cc:826-846).  Each pass pre-tests at its own
         // threshold, so the iniTh pass scores far fewer pixels; scores stored by
@@ -491,12 +540,10 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         for (int pass = 0; pass < 2; ++pass) {
             const int t = pass == 0 ? a.ini_th : a.min_th;
             // 1. compass pre-test on (row, aligned dword) items: candidates in
-            //    row-major order tagged with their passing directions; pixels that
-            //    pass both also enter a second list growing down from the top of
-            //    `cand` (dropped, with a two-direction fallback, if it would collide)
+            //    row-major order tagged with their passing directions (~4% of
+            //    pixels pass, ~8% of items hold one, so the compaction writes
+            //    loop over the set bits instead of visiting all four bytes)
             const u16x2 tt = {(unsigned short)t, (unsigned short)t};
-            int nsec = 0;
-            bool sec_ok = true;
             ncand = 0;
             for (int base = 0; base < nitems; base += kWave) {
                 const int it = base + lane;
@@ -519,53 +566,35 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
                     dm = pix4(d0, d1) & valid;
                     idx0 = (int)__umul24(r, ww) + cx;
                 }
-                const uint32_t pm = bm | dm, both = bm & dm;
-                const int pc = __popc(pm), cb = __popc(both);
+                uint32_t pm = bm | dm;
+                const int pc = __popc(pm);
                 // lane-exclusive prefixes of the per-lane counts (<= 4) by bit ballots
                 const uint64_t c0 = __ballot(pc & 1), c1 = __ballot(pc & 2), c2 = __ballot(pc & 4);
-                const uint64_t q0 = __ballot(cb & 1), q1 = __ballot(cb & 2), q2 = __ballot(cb & 4);
                 const int tot = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
-                const int stot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2);
-                if (ncand + tot + nsec + stot > cap) sec_ok = false;
-                if (pm) {
-                    int pos = ncand + mask_rank(c0) + 2 * mask_rank(c1) + 4 * mask_rank(c2);
-                    int spos = nsec + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2);
-#pragma unroll
-                    for (int bb = 0; bb < 4; ++bb) {
-                        if ((pm >> bb) & 1) {
-                            const int fl = (((bm >> bb) & 1) ? kCandBright : 0) | (((dm >> bb) & 1) ? kCandDark : 0);
-                            cand[pos++] = (uint16_t)((idx0 + bb) | fl);
-                            if (sec_ok && ((both >> bb) & 1)) cand[cap - 1 - spos++] = (uint16_t)(idx0 + bb);
-                        }
-                    }
+                int pos = ncand + mask_rank(c0) + 2 * mask_rank(c1) + 4 * mask_rank(c2);
+                while (pm) {
+                    const int bb = __builtin_ctz(pm);
+                    pm &= pm - 1;
+                    const uint32_t fl = (((bm >> bb) & 1u) << 14) | (((dm >> bb) & 1u) << 15);
+                    cand[pos++] = (uint16_t)((uint32_t)(idx0 + bb) | fl);
                 }
                 ncand += tot;
-                nsec += stot;
             }
             fast_wave_sync();
-            // 2. FAST score of the candidates (first passing direction; the second
-            //    direction of two-direction pixels from the second list)
+            if (pass == 0) FAST_T(1); else FAST_T(5);
+            // 2. FAST score of the candidates (the dark direction too for the rare
+            //    pixels passing both pre-tests)
             for (int q = lane; q < ncand; q += kWave) {
                 const int e = cand[q], i = e & kCandIdx;
                 const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
                 int v, x[16];
                 fast_ring(R, rstride, r + 3, cc + 3, v, x);
                 int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
-                if (!sec_ok && (e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
+                if ((e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
                 sc[(r + 1) * sp + cc + 1] = (uint8_t)max(sv, 0);
             }
-            if (sec_ok && nsec > 0) {
-                fast_wave_sync();
-                for (int q = lane; q < nsec; q += kWave) {
-                    const int i = cand[cap - 1 - q];
-                    const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
-                    int v, x[16];
-                    fast_ring(R, rstride, r + 3, cc + 3, v, x);
-                    uint8_t* sq = sc + (r + 1) * sp + cc + 1;
-                    *sq = (uint8_t)max((int)*sq, max(fast_dir_score(x, v, 1), 0));
-                }
-            }
             fast_wave_sync();
+            if (pass == 0) FAST_T(2); else FAST_T(6);
             // 3. NMS at this pass's threshold; keep its ballots
             cnt = 0;
             const int nchunk = (ncand + kWave - 1) / kWave;
@@ -581,6 +610,7 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
                 cnt += __popcll(m);
             }
             fast_wave_sync();
+            if (pass == 0) FAST_T(3); else FAST_T(7);
             if (cnt > 0) break;
         }
         // 4. survivors of the deciding pass, row-major
@@ -607,8 +637,34 @@ __global__ __launch_bounds__(256) void k_fast_cells(FastArgs a) {
         }
         if (lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, cur.cap);
         fast_wave_sync();
+        FAST_T(9);
     }
+#ifdef ORB_FAST_TIMING
+    if (lane == 0) {
+        const unsigned long long tv[10] = {t0, t1, t2, t3, __builtin_amdgcn_s_memtime() - t_start, t5, t6, t7,
+                                           1ull, t9};
+#pragma unroll
+        for (int k = 0; k < 10; ++k)
+            atomicAdd(&g_fast_t[(blockIdx.x * 4 + wv + blockIdx.y * 61) & 1023][k], tv[k]);
+    }
+#endif
 }
+
+#ifdef ORB_FAST_TIMING
+extern "C" int orbx_debug_fast_timing(unsigned long long* out, int reset) {
+    static unsigned long long h[1024][16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_fast_t), sizeof(h)) != hipSuccess) return -4;
+    for (int k = 0; k < 16; ++k) {
+        out[k] = 0;
+        for (int i = 0; i < 1024; ++i) out[k] += h[i][k];
+    }
+    if (reset) {
+        static unsigned long long z[1024][16];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_fast_t), z, sizeof(z)) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // k_quadtree: ORBextractor::DistributeOctTree (ORBextractor.cc:555-779) for

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""Phase profile of k_fast_cells from a library built with -DORB_FAST_TIMING
+(variants/lib_fastt.so copied over the product library): shader cycles per
+phase summed over all waves for one 256-frame batch."""
+import ctypes as C
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+
+
+def main():
+    import torch
+    from orb_slam3_vio_fixes_amd import capi, orb, synth
+    frames = torch.from_numpy(synth.sequence(752, 480, 256, config=2)).cuda()
+    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    L = capi.lib()
+    timing = hasattr(L, "orbx_debug_fast_timing")
+    if timing:
+        L.orbx_debug_fast_timing.argtypes = [C.c_void_p, C.c_int]
+    else:
+        L.orbx_debug_fast_timing = lambda *a: 0
+    out = np.zeros(16, np.uint64)
+    for _ in range(3):
+        ex.extract_batch_device(frames, (0, 1000))
+    torch.cuda.synchronize()
+    L.orbx_debug_fast_timing(out.ctypes.data, 1)
+    ex.extract_batch_device(frames, (0, 1000))
+    torch.cuda.synchronize()
+    L.orbx_debug_fast_timing(out.ctypes.data, 1)
+    names = {0: "land+zero+prefetch", 1: "pretest(ini)", 2: "score(ini)", 3: "nms(ini)", 5: "pretest(min)",
+             6: "score(min)", 7: "nms(min)", 9: "output"}
+    tot = max(1, sum(int(out[k]) for k in names))
+    for k, nme in names.items():
+        print(f"{nme:22s} {int(out[k]) / 1e9:8.3f} Gcyc  {100 * int(out[k]) / tot:5.1f} %")
+    nw = int(out[8])
+    print(f"waves {nw}  lifetime/wave {int(out[4]) / max(nw, 1):.0f} cyc  (phases sum {tot / max(nw, 1):.0f})")
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record()
+    for _ in range(10):
+        ex.extract_batch_device(frames, (0, 1000))
+    ev1.record()
+    torch.cuda.synchronize()
+    print(f"extract batch {ev0.elapsed_time(ev1) / 10:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

@@ -331,6 +331,82 @@ __global__ __launch_bounds__(256) void v7(P a, double scale_x, int sw) {
     }
 }
 
+// V8: v4 (LDS-staged source rows, coalesced lanes) with computed x taps
+template <int TR>
+__global__ __launch_bounds__(256) void v8(P a, double scale_x, int sw) {
+    __shared__ __attribute__((aligned(16))) uint8_t rows[(2 * TR + 4) * 1024];
+    const int y0 = blockIdx.x * TR;
+    const int f = blockIdx.y;
+    const uint8_t* S = a.src + (long long)f * a.sfs;
+    const int ylast = min(y0 + TR, a.dh) - 1;
+    const int sr0 = min(max(a.yt[y0].x, 0), a.sh - 1);
+    const int sr1 = min(max(a.yt[ylast].x + 1, 0), a.sh - 1);
+    const int nr = sr1 - sr0 + 1;
+    const int rw16 = (a.sp + 15) >> 4;
+    const int rp = rw16 * 16;
+    for (int i = threadIdx.x; i < nr * rw16; i += 256) {
+        const int r = i / rw16, c = i - r * rw16;
+        ((uint4*)(rows + r * rp))[c] = ((const uint4*)(S + (long long)(sr0 + r) * a.sp))[c];
+    }
+    __syncthreads();
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int ry = w; ry < TR; ry += 4) {
+        const int dy = y0 + ry;
+        if (dy >= a.dh) break;
+        const int2 ty = a.yt[dy];
+        const int r0 = min(max(ty.x, 0), a.sh - 1) - sr0, r1 = min(max(ty.x + 1, 0), a.sh - 1) - sr0;
+        const int b0 = (short)(ty.y & 0xffff), b1 = ty.y >> 16;
+        const uint8_t* S0 = rows + r0 * rp;
+        const uint8_t* S1 = rows + r1 * rp;
+        uint8_t* D = a.dst + (long long)f * a.dfs + (long long)dy * a.dp;
+        for (int dx = lane; dx < a.dw; dx += 64) {
+            float fx = (float)((dx + 0.5) * scale_x - 0.5);
+            int sx = (int)floorf(fx); fx -= sx;
+            int a0 = (int)rintf((1.f - fx) * 2048), a1 = (int)rintf(fx * 2048);
+            if (sx < 0) { sx = 0; a0 = 2048; a1 = 0; }
+            int h0, h1;
+            if (dx < a.xmax) { h0 = S0[sx] * a0 + S0[sx + 1] * a1; h1 = S1[sx] * a0 + S1[sx + 1] * a1; }
+            else { h0 = S0[sx] * 2048; h1 = S1[sx] * 2048; }
+            D[dx] = (uint8_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+        }
+    }
+}
+
+// V9: v5 with two consecutive output rows per wave sharing the middle source row
+__global__ __launch_bounds__(256) void v9(P a, double scale_x, int sw) {
+    const int dy = (blockIdx.x * 4 + (threadIdx.x >> 6)) * 2;
+    if (dy >= a.dh) return;
+    const int f = blockIdx.y;
+    const uint8_t* S = a.src + f * a.sfs;
+    const bool two = dy + 1 < a.dh;
+    const int2 ta = a.yt[dy], tb = a.yt[two ? dy + 1 : dy];
+    const int ra0 = min(max(ta.x, 0), a.sh - 1), ra1 = min(max(ta.x + 1, 0), a.sh - 1);
+    const int rb0 = min(max(tb.x, 0), a.sh - 1), rb1 = min(max(tb.x + 1, 0), a.sh - 1);
+    const int ab0 = (short)(ta.y & 0xffff), ab1 = ta.y >> 16, bb0 = (short)(tb.y & 0xffff), bb1 = tb.y >> 16;
+    const uint8_t *A0 = S + (long long)ra0 * a.sp, *A1 = S + (long long)ra1 * a.sp;
+    const uint8_t *B0 = S + (long long)rb0 * a.sp, *B1 = S + (long long)rb1 * a.sp;
+    const bool share = rb0 == ra1;
+    uint8_t* DA = a.dst + f * a.dfs + (long long)dy * a.dp;
+    uint8_t* DB = DA + a.dp;
+    for (int dx = threadIdx.x & 63; dx < a.dw; dx += 64) {
+        float fx = (float)((dx + 0.5) * scale_x - 0.5);
+        int sx = (int)floorf(fx); fx -= sx;
+        int a0 = (int)rintf((1.f - fx) * 2048), a1 = (int)rintf(fx * 2048);
+        if (sx < 0) { sx = 0; a0 = 2048; a1 = 0; }
+        const bool in = dx < a.xmax;
+        const int sx1 = in ? sx + 1 : sx;
+        const int c0 = in ? a0 : 2048, c1 = in ? a1 : 0;
+        const int hA0 = A0[sx] * c0 + A0[sx1] * c1;
+        const int hA1 = A1[sx] * c0 + A1[sx1] * c1;
+        DA[dx] = (uint8_t)((((ab0 * (hA0 >> 4)) >> 16) + ((ab1 * (hA1 >> 4)) >> 16) + 2) >> 2);
+        if (two) {
+            const int hB0 = share ? hA1 : B0[sx] * c0 + B0[sx1] * c1;
+            const int hB1 = B1[sx] * c0 + B1[sx1] * c1;
+            DB[dx] = (uint8_t)((((bb0 * (hB0 >> 4)) >> 16) + ((bb1 * (hB1 >> 4)) >> 16) + 2) >> 2);
+        }
+    }
+}
+
 int main() {
     const int B = 256, sw = 752, sh = 480, dw = 627, dh = 400;
     const int sp = 768, dp = 640;
@@ -390,6 +466,9 @@ int main() {
     run("v4_tr8", [&] { hipLaunchKernelGGL(v4<8>, dim3((dh + 7) / 8, B), dim3(256), 0, 0, a); });
     run("v4_tr16", [&] { hipLaunchKernelGGL(v4<16>, dim3((dh + 15) / 16, B), dim3(256), 0, 0, a); });
     run("v5_xcalc", [&] { hipLaunchKernelGGL(v5, dim3((dh + 3) / 4, B), dim3(256), 0, 0, a, sx_, sw); });
+    run("v8_lds_calc4", [&] { hipLaunchKernelGGL(v8<4>, dim3((dh + 3) / 4, B), dim3(256), 0, 0, a, sx_, sw); });
+    run("v8_lds_calc8", [&] { hipLaunchKernelGGL(v8<8>, dim3((dh + 7) / 8, B), dim3(256), 0, 0, a, sx_, sw); });
+    run("v9_2rows", [&] { hipLaunchKernelGGL(v9, dim3((dh + 7) / 8, B), dim3(256), 0, 0, a, sx_, sw); });
     run("v6_u16", [&] { hipLaunchKernelGGL(v6, dim3((dh + 3) / 4, B), dim3(256), 0, 0, a, sx_, sw); });
     run("v7_dwstore", [&] { hipLaunchKernelGGL(v7, dim3((dh + 3) / 4, B), dim3(256), 0, 0, a, sx_, sw); });
     run("v3_tr4", [&] { hipLaunchKernelGGL(v3<4>, dim3((dh + 3) / 4, B), dim3(256), 0, 0, a); });
