@@ -289,6 +289,7 @@ struct FastArgs {
     const LevelDev* lv;
     const CellDev* cells;
     int ncells;
+    int nframes;
     int* cell_count;        // [B][ncells]
     uint32_t* cell_keys;    // [B][slot_total]
     int slot_total;
@@ -412,6 +413,7 @@ __device__ unsigned long long g_fast_t[1024][16];   // spread: no contended atom
             case 5: t5 += d_; break;                                         \
             case 6: t6 += d_; break;                                         \
             case 7: t7 += d_; break;                                         \
+            case 10: t10 += d_; break;                                       \
             default: t9 += d_; break;                                        \
         }                                                                    \
     } while (0)
@@ -462,7 +464,6 @@ template <int NV>
 __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
-    const int f = blockIdx.y;
     uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 3 + a.kmask_bytes);   // multiples of 16
     uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
     uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_max entries
@@ -470,20 +471,24 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #ifdef ORB_FAST_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
+    // work items it = frame * ncells + cell
     const int c_begin = (blockIdx.x * 4 + wv) * kCellsPerWave;
-    const int c_end = min(c_begin + kCellsPerWave, a.ncells);
+    const int it0 = blockIdx.y * a.ncells + c_begin, step = 1;
+    const int it_end = blockIdx.y * a.ncells + min(c_begin + kCellsPerWave, a.ncells);
     // the plan tables are read-only here: constant address space -> scalar loads
     typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
     typedef __attribute__((address_space(4))) const CellDev* ConstCells;
     const ConstLevels lvc = (ConstLevels)a.lv;
     const ConstCells cells = (ConstCells)a.cells;
-    auto cell_at = [&](int i) {
+    auto cell_at = [&](int it) {
+        const int i = it % a.ncells;
         CellDev r;
         r.level = cells[i].level; r.x0 = cells[i].x0; r.y0 = cells[i].y0; r.cols = cells[i].cols;
         r.rows = cells[i].rows; r.slot_off = cells[i].slot_off; r.cap = cells[i].cap;
         return r;
     };
-    auto fetch_of = [&](const CellDev& c) {
+    auto fetch_of = [&](const CellDev& c, int it) {
+        const int f = it / a.ncells;
         RoiFetch rf;
         if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
         else { rf.src = a.pyr + f * a.pyr_fstride + lvc[c.level].off; rf.pitch = lvc[c.level].pitch; }
@@ -497,39 +502,36 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     uint32_t v[NV];
     CellDev c{}, cn{};
     RoiFetch rf{};
-    if (c_begin < c_end) {
-        c = cell_at(c_begin);
-        rf = fetch_of(c);
+    if (it0 < it_end) {
+        c = cell_at(it0);
+        rf = fetch_of(c, it0);
         roi_issue<NV>(rf, c.y0, v);
     }
-    if (c_begin + 1 < c_end) cn = cell_at(c_begin + 1);
+    if (it0 + step < it_end) cn = cell_at(it0 + step);
 #ifdef ORB_FAST_TIMING
-    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t5 = 0, t6 = 0, t7 = 0, t9 = 0;
+    unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t5 = 0, t6 = 0, t7 = 0, t9 = 0, t10 = 0;
     unsigned long long tlast = t_start;
 #endif
-    for (int ci = c_begin; ci < c_end; ++ci) {
-        // land the prefetched ROI in LDS, then prefetch the next cell's ROI
+    auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) {
 #pragma unroll
-        for (int j = 0; j < NV; ++j) ((uint32_t*)roi)[min(lane + j * kWave, rf.n - 1)] = v[j];
-        const int shift = c.x0 - rf.base, rstride = rf.nd * 4;
+        for (int j = 0; j < NV; ++j) ((uint32_t*)roi)[min(lane + j * kWave, r.n - 1)] = vv[j];
+    };
+    // one cell from its landed ROI
+    auto process = [&](const CellDev& cur, const RoiFetch& rfc, int it) {
+        const int f = it / a.ncells;
+        const int shift = cur.x0 - rfc.base, rstride = rfc.nd * 4;
         const uint8_t* R = roi + shift;
-        const int ww = max(0, c.cols - 6), wh = max(0, c.rows - 6);
+        const int ww = max(0, cur.cols - 6), wh = max(0, cur.rows - 6);
         const int sp = ww + 2, npad = sp * (wh + 2);
         for (int i = lane; i < (npad + 3) / 4; i += kWave) ((uint32_t*)sc)[i] = 0u;
-        const CellDev cur = c;
-        if (ci + 1 < c_end) {
-            c = cn;
-            rf = fetch_of(c);
-            roi_issue<NV>(rf, c.y0, v);
-        }
-        if (ci + 2 < c_end) cn = cell_at(ci + 2);
         fast_wave_sync();
-        FAST_T(0);
+        if (it == it0) FAST_T(10); else FAST_T(0);
         const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
         const int X0 = shift + 3, j0 = X0 >> 2;
         const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
-        const int nitems = wh * ndw;
-        const float inv_ndw = ndw ? 1.0f / (float)ndw : 0.f;
+        const int ndp = (ndw + 1) >> 1;                   // items: pairs of aligned dwords
+        const int nitems = wh * ndp;
+        const float inv_ndp = ndp ? 1.0f / (float)ndp : 0.f;
         const uint32_t* roi32 = (const uint32_t*)roi;
         const int rs4 = rstride >> 2;
         // FAST(ROI, iniThFAST) and, only if that leaves no corner, FAST(ROI,
@@ -550,28 +552,33 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 uint32_t bm = 0, dm = 0;
                 int idx0 = 0;
                 if (it < nitems) {
-                    const int r = div_row(it, inv_ndw);
-                    const int j = j0 + (it - (int)__umul24(r, ndw));
+                    const int r = div_row(it, inv_ndp);
+                    const int j = j0 + 2 * (it - (int)__umul24(r, ndp));
                     const uint32_t* row = roi32 + __umul24(r + 3, rs4) + j;
-                    const uint32_t c = row[0], u = row[-3 * rs4], d = row[3 * rs4];
-                    const uint32_t lf = __builtin_amdgcn_alignbyte(c, row[-1], 1);
-                    const uint32_t rt = __builtin_amdgcn_alignbyte(row[1], c, 3);
-                    uint32_t b0, d0, b1, d1;
-                    compass_pair(lo_bytes(c), lo_bytes(u), lo_bytes(d), lo_bytes(lf), lo_bytes(rt), tt, b0, d0);
-                    compass_pair(hi_bytes(c), hi_bytes(u), hi_bytes(d), hi_bytes(lf), hi_bytes(rt), tt, b1, d1);
+                    const uint32_t cm = row[-1], c0 = row[0], c1 = row[1], c2 = row[2];
+                    const uint32_t u0 = row[-3 * rs4], u1 = row[1 - 3 * rs4];
+                    const uint32_t d0 = row[3 * rs4], d1 = row[1 + 3 * rs4];
+                    const uint32_t lf0 = __builtin_amdgcn_alignbyte(c0, cm, 1), rt0 = __builtin_amdgcn_alignbyte(c1, c0, 3);
+                    const uint32_t lf1 = __builtin_amdgcn_alignbyte(c1, c0, 1), rt1 = __builtin_amdgcn_alignbyte(c2, c1, 3);
+                    uint32_t b0, k0, b1, k1, b2, k2, b3, k3;
+                    compass_pair(lo_bytes(c0), lo_bytes(u0), lo_bytes(d0), lo_bytes(lf0), lo_bytes(rt0), tt, b0, k0);
+                    compass_pair(hi_bytes(c0), hi_bytes(u0), hi_bytes(d0), hi_bytes(lf0), hi_bytes(rt0), tt, b1, k1);
+                    compass_pair(lo_bytes(c1), lo_bytes(u1), lo_bytes(d1), lo_bytes(lf1), lo_bytes(rt1), tt, b2, k2);
+                    compass_pair(hi_bytes(c1), hi_bytes(u1), hi_bytes(d1), hi_bytes(lf1), hi_bytes(rt1), tt, b3, k3);
                     const int cx = 4 * j - X0;                       // window column of byte 0
-                    const int s0 = min(max(-cx, 0), 4), e0 = min(max(ww - cx, 0), 4);
-                    const uint32_t valid = (0xfu << s0) & ((1u << e0) - 1u);
-                    bm = pix4(b0, b1) & valid;
-                    dm = pix4(d0, d1) & valid;
+                    const int s0 = min(max(-cx, 0), 8), e0 = min(max(ww - cx, 0), 8);
+                    const uint32_t valid = (0xffu << s0) & ((1u << e0) - 1u);
+                    bm = (pix4(b0, b1) | (pix4(b2, b3) << 4)) & valid;
+                    dm = (pix4(k0, k1) | (pix4(k2, k3) << 4)) & valid;
                     idx0 = (int)__umul24(r, ww) + cx;
                 }
                 uint32_t pm = bm | dm;
                 const int pc = __popc(pm);
-                // lane-exclusive prefixes of the per-lane counts (<= 4) by bit ballots
-                const uint64_t c0 = __ballot(pc & 1), c1 = __ballot(pc & 2), c2 = __ballot(pc & 4);
-                const int tot = __popcll(c0) + 2 * __popcll(c1) + 4 * __popcll(c2);
-                int pos = ncand + mask_rank(c0) + 2 * mask_rank(c1) + 4 * mask_rank(c2);
+                // lane-exclusive prefixes of the per-lane counts (<= 8) by bit ballots
+                const uint64_t q0 = __ballot(pc & 1), q1 = __ballot(pc & 2), q2 = __ballot(pc & 4),
+                               q3 = __ballot(pc & 8);
+                const int tot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2) + 8 * __popcll(q3);
+                int pos = ncand + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2) + 8 * mask_rank(q3);
                 while (pm) {
                     const int bb = __builtin_ctz(pm);
                     pm &= pm - 1;
@@ -635,16 +642,29 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 written += __popcll(m);
             }
         }
-        if (lane == 0) a.cell_count[(long long)f * a.ncells + ci] = min(written, cur.cap);
+        if (lane == 0) a.cell_count[it] = min(written, cur.cap);
         fast_wave_sync();
         FAST_T(9);
+    };
+    for (int it = it0; it < it_end; it += step) {
+        // land the prefetched ROI in LDS, then prefetch the next cell's ROI
+        land(v, rf);
+        const CellDev cur = c;
+        const RoiFetch rcur = rf;
+        if (it + step < it_end) {
+            c = cn;
+            rf = fetch_of(c, it + step);
+            roi_issue<NV>(rf, c.y0, v);
+        }
+        if (it + 2 * step < it_end) cn = cell_at(it + 2 * step);
+        process(cur, rcur, it);
     }
 #ifdef ORB_FAST_TIMING
     if (lane == 0) {
-        const unsigned long long tv[10] = {t0, t1, t2, t3, __builtin_amdgcn_s_memtime() - t_start, t5, t6, t7,
-                                           1ull, t9};
+        const unsigned long long tv[11] = {t0, t1, t2, t3, __builtin_amdgcn_s_memtime() - t_start, t5, t6, t7,
+                                           1ull, t9, t10};
 #pragma unroll
-        for (int k = 0; k < 10; ++k)
+        for (int k = 0; k < 11; ++k)
             atomicAdd(&g_fast_t[(blockIdx.x * 4 + wv + blockIdx.y * 61) & 1023][k], tv[k]);
     }
 #endif
@@ -1167,14 +1187,21 @@ __device__ __forceinline__ bool patch_interior(int w, int h, int x0, int y0) {
     return y0 >= 0 && y0 + kRaw <= h && x0 >= 0 && (x0 & ~3) + kRawP <= w;
 }
 
+// the image pointers reach the describe loop through readlanes, which loses
+// their address space: without the global cast these become flat loads, which
+// also count in lgkmcnt, so the next LDS wait would drain the prefetch
+typedef __attribute__((address_space(1))) const uint8_t* GlobalBytes;
+typedef __attribute__((address_space(1))) const uint32_t* GlobalWords;
+
 __device__ __forceinline__ void patch_issue(const uint8_t* img, int pitch, int x0, int y0, uint32_t (&v)[kPV]) {
     const int lane = lane_id(), base = x0 & ~3;
+    const GlobalBytes g = (GlobalBytes)img;
 #pragma unroll
     for (int j = 0; j < kPV; ++j) {
         const int i = lane + j * kWave;
         if (i < kPN) {
             const int r = i / kPDw, d = i - r * kPDw;
-            v[j] = *(const uint32_t*)(img + (long long)(y0 + r) * pitch + base + 4 * d);
+            v[j] = *(GlobalWords)(g + (long long)(y0 + r) * pitch + base + 4 * d);
         }
     }
 }
@@ -1192,7 +1219,7 @@ __device__ __forceinline__ void patch_border(const uint8_t* img, int pitch, int 
                                              uint8_t* raw) {
     for (int i = lane_id(); i < kRaw * kRaw; i += kWave) {
         const int r = i / kRaw, c = i - r * kRaw;
-        raw[r * kRawP + c] = img[(long long)refl101(y0 + r, h) * pitch + refl101(x0 + c, w)];
+        raw[r * kRawP + c] = ((GlobalBytes)img)[(long long)refl101(y0 + r, h) * pitch + refl101(x0 + c, w)];
     }
 }
 
@@ -1208,11 +1235,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     const int lane = lane_id(), wv = wave_id();
     // lane's 4 tests = 16 consecutive pattern bytes, kept packed in registers
     const uint4 patv = ((const uint4*)c_pattern)[lane];
+    // wait for the pattern here: a use inside the keypoint loop would get a
+    // conservative vmcnt(0) that also drains the patch prefetch
+    asm volatile("" ::"v"(patv.x), "v"(patv.y), "v"(patv.z), "v"(patv.w));
     const uint32_t patw[4] = {patv.x, patv.y, patv.z, patv.w};
     uint8_t* raw = raw_s[wv];
     uint16_t* hb = hb_s[wv];
     // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
     const uint32_t k0 = a.kern[0], k1 = a.kern[1], k2 = a.kern[2], k3 = a.kern[3];
+    // umax in SGPRs: a lane-indexed a.umax[v] compiles to a vector load from
+    // the kernarg segment whose vmcnt wait would also drain the patch prefetch
+    int um_s[kHalfPatch + 1];
+#pragma unroll
+    for (int v = 0; v <= kHalfPatch; ++v) um_s[v] = __builtin_amdgcn_readfirstlane(a.umax[v]);
     // this wave's run of kDescSlots slots; the next valid slot's patch is
     // always in flight while the current one is described
     const long long s_begin = ((long long)blockIdx.x * 4 + wv) * kDescSlots;
@@ -1266,7 +1301,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
                     const int v = v0 + k;
-                    if (v <= kHalfPatch && u >= -a.umax[v] && u <= a.umax[v]) {
+                    const int um = lane < 32 ? um_s[1 + k] : um_s[min(9 + k, kHalfPatch)];
+                    if (v <= kHalfPatch && u >= -um && u <= um) {
                         const int up = c[u + v * kRawP], dn = c[u - v * kRawP];
                         m10 += u * (up + dn);
                         m01 += v * (up - dn);
@@ -1522,8 +1558,9 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.win_max = (P.win_max + 15) & ~15;
     fa.kmask_bytes = ((fa.win_max + kWave - 1) / kWave * 8 + 15) & ~15;
     const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max + fa.kmask_bytes);
-    const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
+    fa.nframes = B;
     const int nv = (P.roi_dwords + kWave - 1) / kWave;
+    const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
     if (nv <= 12) hipLaunchKernelGGL(k_fast_cells<12>, fgrid, dim3(256), flds, st, fa);
     else if (nv <= 24) hipLaunchKernelGGL(k_fast_cells<24>, fgrid, dim3(256), flds, st, fa);
     else hipLaunchKernelGGL(k_fast_cells<48>, fgrid, dim3(256), flds, st, fa);

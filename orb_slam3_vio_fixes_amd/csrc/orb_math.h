@@ -66,7 +66,9 @@ ORB_HD void glibc_sincosf(float y, float* sinp, float* cosp) {
         const double r = x * t0.hpi_inv;
         const int n = ((int32_t)r + 0x800000) >> 24;
         const double xr = fma(-(double)n, t0.hpi, x);
-        const double s = t0.sgn[n & 3];
+        // t0.sgn[n & 3] = {1, -1, -1, 1}[n & 3], as a select: an indexed table
+        // read becomes a device memory load (and a vmcnt wait) in the kernels
+        const double s = ((n + 1) & 2) ? -1.0 : 1.0;
         sincosf_poly(xr * s, xr * xr, (n & 2) ? t1 : t0, n, sinp, cosp);
     } else {
         *sinp = *cosp = NAN;

@@ -31,7 +31,7 @@ def main():
     ex.extract_batch_device(frames, (0, 1000))
     torch.cuda.synchronize()
     L.orbx_debug_fast_timing(out.ctypes.data, 1)
-    names = {0: "land+zero+prefetch", 1: "pretest(ini)", 2: "score(ini)", 3: "nms(ini)", 5: "pretest(min)",
+    names = {10: "first land", 0: "land+zero+prefetch", 1: "pretest(ini)", 2: "score(ini)", 3: "nms(ini)", 5: "pretest(min)",
              6: "score(min)", 7: "nms(min)", 9: "output"}
     tot = max(1, sum(int(out[k]) for k in names))
     for k, nme in names.items():
