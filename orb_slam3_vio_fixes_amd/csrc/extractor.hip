@@ -716,6 +716,11 @@ struct QtArgs {
     int out_total, L, ncap;
 };
 
+// double-buffered arrays are picked by a select, never by a dynamic index:
+// an indexed pointer array would live in scratch and every access through it
+// would become a flat memory op
+template <class T> __device__ __forceinline__ T* qsel(T* const (&arr)[2], int i) { return i ? arr[1] : arr[0]; }
+
 struct QtLds {
     int* off;
     short4* rect[2];
@@ -869,8 +874,8 @@ __device__ int qt_divide(QtLds& s, int& cur, int size, int m, const int K, int* 
     const int totGT = block_excl_scan(s.rgt, m, s.tmp);
     block_excl_scan(s.nd, size, s.tmp);
     const int nx = cur ^ 1;
-    const short4* R = s.rect[cur];
-    const int* C = s.cnt[cur];
+    const short4* R = qsel(s.rect, cur);
+    const int* C = qsel(s.cnt, cur);
     for (int r = tid; r < m; r += T) {
         const int i = s.ord[r];
         int ne = 0;
@@ -882,9 +887,9 @@ __device__ int qt_divide(QtLds& s, int& cur, int size, int m, const int K, int* 
             if (c > 0) {
                 const int np = start + w++;
                 s.newpos[4 * i + q] = np;
-                s.rect[nx][np] = child_rect(R[i], q);
-                s.cnt[nx][np] = c;
-                s.nomore[nx][np] = c == 1;
+                qsel(s.rect, nx)[np] = child_rect(R[i], q);
+                qsel(s.cnt, nx)[np] = c;
+                qsel(s.nomore, nx)[np] = c == 1;
             }
         }
         int e = s.rgt[r];
@@ -895,9 +900,9 @@ __device__ int qt_divide(QtLds& s, int& cur, int size, int m, const int K, int* 
         if (s.div[i]) continue;
         const int np = totNE + s.nd[i];
         s.keep[i] = np;
-        s.rect[nx][np] = R[i];
-        s.cnt[nx][np] = C[i];
-        s.nomore[nx][np] = s.nomore[cur][i];
+        qsel(s.rect, nx)[np] = R[i];
+        qsel(s.cnt, nx)[np] = C[i];
+        qsel(s.nomore, nx)[np] = qsel(s.nomore, cur)[i];
     }
     __syncthreads();
     for (int k = tid; k < K; k += T) {
@@ -916,7 +921,7 @@ __device__ void qt_count(QtLds& s, int cur, int size, const int K, const uint32_
     const int tid = threadIdx.x, T = blockDim.x;
     for (int i = tid; i < 4 * size; i += T) s.ccnt[i] = 0;
     __syncthreads();
-    const short4* R = s.rect[cur];
+    const short4* R = qsel(s.rect, cur);
     for (int k = tid; k < K; k += T) {
         const int n = knode[k];
         if (s.div[n]) {
@@ -1019,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     bool last = false;
     while (true) {
         const int prev = size;
-        for (int i = tid; i < size; i += T) s.nd[i] = s.nomore[cur][i] ? 0 : 1;
+        for (int i = tid; i < size; i += T) s.nd[i] = qsel(s.nomore, cur)[i] ? 0 : 1;
         __syncthreads();
         for (int i = tid; i < size; i += T) s.div[i] = s.nd[i];
         __syncthreads();
@@ -1038,7 +1043,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         const int m = nexp;
         for (int j = tid; j < m; j += T) {
             const int i = s.expand[j];
-            s.srt[j] = SortRec{s.cnt[cur][i], (int)s.rect[cur][i].x, i};
+            s.srt[j] = SortRec{qsel(s.cnt, cur)[i], (int)qsel(s.rect, cur)[i].x, i};
         }
         for (int i = tid; i < size; i += T) s.div[i] = 0;
         __syncthreads();
