@@ -1228,6 +1228,32 @@ __device__ __forceinline__ void patch_border(const uint8_t* img, int pitch, int 
     }
 }
 
+#ifdef ORB_DESC_TIMING
+// phase profile of k_describe (tools/fast_phases.py --describe): shader cycles per phase
+__device__ unsigned long long g_desc_t[1024][8];
+#define DESC_T(var)                                                          \
+    do {                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+        var += t_ - tlast;                                                   \
+        tlast = t_;                                                          \
+    } while (0)
+extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
+    static unsigned long long h[1024][8];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_desc_t), sizeof(h)) != hipSuccess) return -4;
+    for (int k = 0; k < 8; ++k) {
+        out[k] = 0;
+        for (int i = 0; i < 1024; ++i) out[k] += h[i][k];
+    }
+    if (reset) {
+        static unsigned long long z[1024][8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_desc_t), z, sizeof(z)) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#else
+#define DESC_T(var) do { } while (0)
+#endif
+
 #ifndef ORB_DESC_WAVES
 #define ORB_DESC_WAVES 4
 #endif
@@ -1253,6 +1279,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     int um_s[kHalfPatch + 1];
 #pragma unroll
     for (int v = 0; v <= kHalfPatch; ++v) um_s[v] = __builtin_amdgcn_readfirstlane(a.umax[v]);
+    // IC_Angle disc masks for the h-pass lanes: lane r holds patch row r
+    // (v = r - 21); byte b of its aligned word j is column 4j + b (u = 4j + b - 21)
+    uint32_t icm[9];
+    {
+        const int av = lane >= 21 ? lane - 21 : 21 - lane;
+        int um = -1;
+#pragma unroll
+        for (int k = 0; k <= kHalfPatch; ++k)
+            if (av == k) um = um_s[k];
+        if (lane >= kRaw) um = -1;
+#pragma unroll
+        for (int j = 1; j <= 9; ++j) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * j + b - 21;
+                if (u >= -um && u <= um) m |= 0xffu << (8 * b);
+            }
+            icm[j - 1] = m;
+        }
+    }
     // this wave's run of kDescSlots slots; the next valid slot's patch is
     // always in flight while the current one is described
     const long long s_begin = ((long long)blockIdx.x * 4 + wv) * kDescSlots;
@@ -1263,6 +1310,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     uint32_t pv[kPV];
     DescKp cur{};
     int jc = -1;
+#ifdef ORB_DESC_TIMING
+    const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+    unsigned long long tlast = t_start, d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0, dk = 0;
+#endif
     if (todo) {
         jc = __builtin_ctzll(todo);
         todo &= todo - 1;
@@ -1294,27 +1345,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         }
         const uint8_t* R = raw + sh;
         wave_sync();
-        // 2. IC_Angle on the unblurred disc (centre = R[21][21]): lanes 0-30 sum
-        //    rows v = 0..8, lanes 32-62 rows v = 9..15 of column u
+        DESC_T(d0);
+#ifdef ORB_DESC_TIMING
+        ++dk;
+#endif
         int m10 = 0, m01 = 0;
-        {
-            const int u = (lane & 31) - kHalfPatch;
-            const uint8_t* c = R + 21 * kRawP + 21;
-            if ((lane & 31) < 2 * kHalfPatch + 1) {
-                if (lane < 32) m10 = u * c[u];
-                const int v0 = lane < 32 ? 1 : 9;
-#pragma unroll
-                for (int k = 0; k < 8; ++k) {
-                    const int v = v0 + k;
-                    const int um = lane < 32 ? um_s[1 + k] : um_s[min(9 + k, kHalfPatch)];
-                    if (v <= kHalfPatch && u >= -um && u <= um) {
-                        const int up = c[u + v * kRawP], dn = c[u - v * kRawP];
-                        m10 += u * (up + dn);
-                        m01 += v * (up - dn);
-                    }
-                }
-            }
-        }
+        DESC_T(d1);
         // 3. horizontal pass (ufixedpoint16): lane r holds raw row r in registers
         //    (3 x ds_read_b128 + v_alignbyte for the column shift), splits it
         //    into u16 pixel pairs starting at even (E) and odd (O) columns and
@@ -1327,6 +1363,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             uint32_t al[11];
 #pragma unroll
             for (int j = 0; j < 11; ++j) al[j] = __builtin_amdgcn_alignbyte(wd[j + 1], wd[j], (uint32_t)sh);
+            // 2. IC_Angle (ORBextractor.cc:76-103) on this row of the unblurred
+            //    disc: sum I and sum (u + 15) I by byte dot products, then
+            //    m10 = sum u I, m01 = v sum I (integer, order-free)
+            {
+                uint32_t s1 = 0, sw = 0;
+#pragma unroll
+                for (int j = 1; j <= 9; ++j) {
+                    uint32_t wgt = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int u = 4 * j + b - 21;
+                        if (u >= -kHalfPatch && u <= kHalfPatch) wgt |= (uint32_t)(u + kHalfPatch) << (8 * b);
+                    }
+                    const uint32_t px = al[j] & icm[j - 1];
+                    s1 = __builtin_amdgcn_udot4(px, 0x01010101u, s1, false);
+                    sw = __builtin_amdgcn_udot4(px, wgt, sw, false);
+                }
+                m10 = (int)sw - kHalfPatch * (int)s1;
+                m01 = (lane - 21) * (int)s1;
+            }
             const u16x2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
             const u16x2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
             uint32_t* orow = (uint32_t*)(hb + lane * kHbP);
@@ -1357,6 +1413,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             __builtin_amdgcn_sched_barrier(0);
             half(std::integral_constant<int, 10>{}, std::integral_constant<int, (kBl + 1) / 2>{});
         }
+        DESC_T(d2);
         m10 = wave_sum(m10);
         m01 = wave_sum(m01);
         const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
@@ -1364,6 +1421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         float sb, ca;
         glibc_sincosf(ang, &sb, &ca);
         wave_sync();
+        DESC_T(d3);
         // 4. rBRIEF tests: the vertical pass (ufixedpoint32 + rounding) evaluated
         //    only at the 512 sample points, hb rows R..R+6 at blurred column C,
         //    blurred centre (18, 18)
@@ -1390,6 +1448,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             }
             nib |= (val[0] < val[1]) << q;
         }
+        DESC_T(d4);
         const int hi = __shfl_down(nib, 1, kWave);
         uint8_t* d = a.sdesc + s * 32;
         if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
@@ -1397,7 +1456,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         jc = jn;
         cur = nxt;
         wave_sync();
+        DESC_T(d5);
     }
+#ifdef ORB_DESC_TIMING
+    if (lane == 0) {
+        const unsigned long long tv[8] = {d0, d1, d2, d3, d4, d5, dk, __builtin_amdgcn_s_memtime() - t_start};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_desc_t[(blockIdx.x * 4 + wv) & 1023][k], tv[k]);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------

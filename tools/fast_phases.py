@@ -18,6 +18,8 @@ def main():
     frames = torch.from_numpy(synth.sequence(752, 480, 256, config=2)).cuda()
     ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
     L = capi.lib()
+    if hasattr(L, "orbx_debug_desc_timing"):
+        return describe_phases(L, ex, frames)
     timing = hasattr(L, "orbx_debug_fast_timing")
     if timing:
         L.orbx_debug_fast_timing.argtypes = [C.c_void_p, C.c_int]
@@ -45,6 +47,25 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     print(f"extract batch {ev0.elapsed_time(ev1) / 10:.3f} ms")
+
+
+def describe_phases(L, ex, frames):
+    """k_describe phases from a -DORB_DESC_TIMING library."""
+    import torch
+    L.orbx_debug_desc_timing.argtypes = [C.c_void_p, C.c_int]
+    out = np.zeros(8, np.uint64)
+    for _ in range(3):
+        ex.extract_batch_device(frames, (0, 1000))
+    torch.cuda.synchronize()
+    L.orbx_debug_desc_timing(out.ctypes.data, 1)
+    ex.extract_batch_device(frames, (0, 1000))
+    torch.cuda.synchronize()
+    L.orbx_debug_desc_timing(out.ctypes.data, 1)
+    names = ["land patch", "IC moments", "h-pass", "angle+sincos", "rBRIEF tests", "output"]
+    tot = max(1, sum(int(out[k]) for k in range(6)))
+    for k, nme in enumerate(names):
+        print(f"{nme:16s} {int(out[k]) / 1e9:8.3f} Gcyc  {100 * int(out[k]) / tot:5.1f} %")
+    print(f"keypoints {int(out[6])}  cycles/keypoint {tot / max(1, int(out[6])):.0f}  wave lifetimes {int(out[7]) / 1e9:.3f} Gcyc")
 
 
 if __name__ == "__main__":
