@@ -1350,14 +1350,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         ++dk;
 #endif
         int m10 = 0, m01 = 0;
+        float ang_deg, sb, ca;
         DESC_T(d1);
         // 3. horizontal pass (ufixedpoint16): lane r holds raw row r in registers
         //    (3 x ds_read_b128 + v_alignbyte for the column shift), splits it
         //    into u16 pixel pairs starting at even (E) and odd (O) columns and
         //    makes two outputs per packed-u16 op (every partial sum fits 16 bits:
         //    the kernel sums to <= 257); outputs 2m, 2m+1 go out as one dword
-        if (lane < kRaw) {
-            const uint4* rowp = (const uint4*)(raw + lane * kRawP);
+        // all 64 lanes run it (lanes past the patch repeat row 42 and rewrite
+        // identical values), so the angle chain below shares its basic block
+        // and is scheduled among the h-pass ops
+        {
+            const int rr = min(lane, kRaw - 1);
+            const uint4* rowp = (const uint4*)(raw + rr * kRawP);
             const uint4 q0 = rowp[0], q1 = rowp[1], q2 = rowp[2];
             const uint32_t wd[12] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w};
             uint32_t al[11];
@@ -1383,9 +1388,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                 m10 = (int)sw - kHalfPatch * (int)s1;
                 m01 = (lane - 21) * (int)s1;
             }
+            m10 = wave_sum(m10);
+            m01 = wave_sum(m01);
+            ang_deg = fast_atan2_deg((float)m01, (float)m10);
+            const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
+            glibc_sincosf(ang, &sb, &ca);
             const u16x2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
             const u16x2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
-            uint32_t* orow = (uint32_t*)(hb + lane * kHbP);
+            uint32_t* orow = (uint32_t*)(hb + rr * kHbP);
             // E(k) = (p[2k], p[2k+1]), O(k) = (p[2k+1], p[2k+2]); two halves of
             // the row keep at most ~26 pairs live
             auto Ep = [&](int k) {
@@ -1414,12 +1424,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             half(std::integral_constant<int, 10>{}, std::integral_constant<int, (kBl + 1) / 2>{});
         }
         DESC_T(d2);
-        m10 = wave_sum(m10);
-        m01 = wave_sum(m01);
-        const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
-        const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
-        float sb, ca;
-        glibc_sincosf(ang, &sb, &ca);
         wave_sync();
         DESC_T(d3);
         // 4. rBRIEF tests: the vertical pass (ufixedpoint32 + rounding) evaluated

@@ -32,22 +32,6 @@ ORB_HD uint32_t f32_bits(float f) { uint32_t u; memcpy(&u, &f, 4); return u; }
 // ---------------------------------------------------------------------------
 struct SinCosTab { double sgn[4], hpi_inv, hpi, c0, c1, s1, c2, s2, c3, s3, c4; };
 
-ORB_HD void sincosf_poly(double x, double x2, const SinCosTab& p, int n, float* sinp, float* cosp) {
-    const double x3 = x2 * x;
-    const double x4 = x2 * x2;
-    const double s1p = fma(x2, p.s3, p.s2);
-    const double c2p = fma(x2, p.c4, p.c3);
-    const double c1p = fma(x2, p.c1, p.c0);
-    const double x5 = x2 * x3;
-    const double x6 = x2 * x4;
-    const double s = fma(x3, p.s1, x);
-    const double c = fma(x4, p.c2, c1p);
-    const float so = (float)fma(s1p, x5, s);
-    const float co = (float)fma(c2p, x6, c);
-    if (n & 1) { *sinp = co; *cosp = so; }
-    else { *sinp = so; *cosp = co; }
-}
-
 ORB_HD void glibc_sincosf(float y, float* sinp, float* cosp) {
     const SinCosTab t0 = {{1.0, -1.0, -1.0, 1.0}, 0x1.45f306dc9c883p+23, 0x1.921fb54442d18p+0,
                           0x1p+0, -0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, 0x1.55553e1068f19p-5,
@@ -57,22 +41,35 @@ ORB_HD void glibc_sincosf(float y, float* sinp, float* cosp) {
                           -0x1p+0, 0x1.ffffffd0c621cp-2, -0x1.555545995a603p-3, -0x1.55553e1068f19p-5,
                           0x1.1107605230bc4p-7, 0x1.6c087e89a359dp-10, -0x1.994eb3774cf24p-13,
                           -0x1.99343027bf8c3p-16};
+    // Branch-free restatement (the device schedules it among independent
+    // work): for |y| < pi/4 the reduction below gives n = 0 and xr = y exactly,
+    // i.e. glibc's first branch; the tiny and out-of-range cases are selects.
     const double x = (double)y;
     const uint32_t top = (f32_bits(y) >> 20) & 0x7ff;
-    if (top < 0x3f4) {                       // |y| < pi/4
-        if (top < 0x398) { *sinp = y; *cosp = 1.0f; return; }   // |y| < 2^-12
-        sincosf_poly(x, x * x, t0, 0, sinp, cosp);
-    } else if (top < 0x42f) {                // |y| < 120
-        const double r = x * t0.hpi_inv;
-        const int n = ((int32_t)r + 0x800000) >> 24;
-        const double xr = fma(-(double)n, t0.hpi, x);
-        // t0.sgn[n & 3] = {1, -1, -1, 1}[n & 3], as a select: an indexed table
-        // read becomes a device memory load (and a vmcnt wait) in the kernels
-        const double s = ((n + 1) & 2) ? -1.0 : 1.0;
-        sincosf_poly(xr * s, xr * xr, (n & 2) ? t1 : t0, n, sinp, cosp);
-    } else {
-        *sinp = *cosp = NAN;
-    }
+    const double r = x * t0.hpi_inv;
+    const int n = top < 0x42f ? ((int32_t)r + 0x800000) >> 24 : 0;
+    const double xr = fma(-(double)n, t0.hpi, x);
+    // t0.sgn[n & 3] = {1, -1, -1, 1}[n & 3], as a select: an indexed table
+    // read becomes a device memory load (and a vmcnt wait) in the kernels
+    const double sg = ((n + 1) & 2) ? -1.0 : 1.0;
+    const SinCosTab& p = (n & 2) ? t1 : t0;
+    const double xs = xr * sg, x2 = xr * xr;
+    const double x3 = x2 * xs;
+    const double x4 = x2 * x2;
+    const double s1p = fma(x2, p.s3, p.s2);
+    const double c2p = fma(x2, p.c4, p.c3);
+    const double c1p = fma(x2, p.c1, p.c0);
+    const double x5 = x2 * x3;
+    const double x6 = x2 * x4;
+    const double sv = fma(x3, p.s1, xs);
+    const double cv = fma(x4, p.c2, c1p);
+    const float so = (float)fma(s1p, x5, sv);
+    const float co = (float)fma(c2p, x6, cv);
+    float sn = (n & 1) ? co : so, cs = (n & 1) ? so : co;
+    if (top < 0x398) { sn = y; cs = 1.0f; }                 // |y| < 2^-12
+    if (top >= 0x42f) { sn = NAN; cs = NAN; }               // |y| >= 120 (not reached)
+    *sinp = sn;
+    *cosp = cs;
 }
 
 // cv::fastAtan2 (OpenCV 4.x atan_f32), degrees; no contraction (A.4).
@@ -81,18 +78,14 @@ ORB_HD float fast_atan2_deg(float y, float x) {
     const float p1 = 0.9997878412794807f * k, p3 = -0.3258083974640975f * k;
     const float p5 = 0.1555786518463281f * k, p7 = -0.04432655554792128f * k;
     const float ax = fabsf(x), ay = fabsf(y);
-    float a;
-    if (ax >= ay) {
-        const float c = ay / (ax + (float)2.220446049250313e-16);
-        const float c2 = c * c;
-        a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    } else {
-        const float c = ax / (ay + (float)2.220446049250313e-16);
-        const float c2 = c * c;
-        a = 90.f - (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
-    }
-    if (x < 0) a = 180.f - a;
-    if (y < 0) a = 360.f - a;
+    // both octant cases as selects (same operations, no branch)
+    const bool xbig = ax >= ay;
+    const float c = (xbig ? ay : ax) / ((xbig ? ax : ay) + (float)2.220446049250313e-16);
+    const float c2 = c * c;
+    float a = (((p7 * c2 + p5) * c2 + p3) * c2 + p1) * c;
+    a = xbig ? a : 90.f - a;
+    a = x < 0 ? 180.f - a : a;
+    a = y < 0 ? 360.f - a : a;
     return a;
 }
 
