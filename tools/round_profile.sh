@@ -7,7 +7,7 @@ tag=${1:-prof}
 out=gpurun_out/$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
-timeout -k 10 900 python -m pytest tests -m gpu -q > "$out/gpu_tests.log" 2>&1 || { echo "gpu tests failed"; tail -20 "$out/gpu_tests.log"; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { echo "gpu tests failed"; tail -20 "$out/gpu_tests.log"; exit 1; }
 tail -2 "$out/gpu_tests.log"
 timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err" || { echo "bench failed"; tail -20 "$out/bench.err"; exit 1; }
 cat "$out/bench.json"
