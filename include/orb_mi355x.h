@@ -359,6 +359,67 @@ int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
 int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best,
                                          int device);
 
+/* ---------------- relocalisation / loop-closing matchers ---------------- */
+
+/* ORBmatcher(nnratio, checkOri).SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2,
+ * vpMatches12) (src/ORBmatcher.cc:765-905) for keyframes with NLeft == -1.
+ * valid1 / valid2[i] = (GetMapPointMatches()[i] != NULL && !isBad()).
+ * matches12[kf1->n] out: the KF2 feature whose MapPoint becomes
+ * vpMatches12[i1], or -1 (NULL).  Returns nmatches. */
+int orbm_search_by_bow_kf(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* valid1,
+                          const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* valid2,
+                          float nnratio, int check_ori, int32_t* matches12);
+
+/* SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound, th,
+ * ORBdist) (src/ORBmatcher.cc:1889-2010) for CurrentFrame.Nleft == -1.  The
+ * caller does the per-point geometry of :1906-1934 (Tcw * X, the
+ * [mnMinX, mnMaxX] x [mnMinY, mnMaxY] bounds, the distance invariance,
+ * PredictScale) for the keyframe's map points i < nq: valid[i] = (pMP && !bad
+ * && !sAlreadyFound.count(pMP) && all checks pass), u, v, level, the point's
+ * descriptor and kf_angle[i] = pKF->mvKeysUn[i].angle.  owner[f->n] in/out:
+ * -1 = CurrentFrame.mvpMapPoints[i2] is NULL, any other value = occupied;
+ * slots matched here receive the keyframe index i (cleared again by the
+ * rotation filter).  Returns nmatches. */
+int orbm_search_by_projection_kf(const orbm_frame* f, int nq, const uint8_t* valid, const float* u,
+                                 const float* v, const int32_t* level, const float* kf_angle, const uint8_t* desc,
+                                 float th, int orb_dist, int check_ori, int32_t* owner);
+
+/* SearchByProjection(KeyFrame* pKF, Sim3 Scw, vpPoints, vpMatched, th,
+ * ratioHamming) (src/ORBmatcher.cc:427-532) and the vpPointsKFs variant
+ * (:534-646) for a pinhole keyframe.  Caller geometry (:446-486): valid[i] =
+ * (!isBad && !spAlreadyFound.count && depth >= 0 && IsInImage && distance
+ * invariance && viewing angle), u, v, level = PredictScale(dist, pKF), the
+ * point's descriptor.  matched[kf->n] in/out: -1 = vpMatched[idx] NULL, any
+ * other value = occupied; slots matched here receive the point index (the
+ * variant sets vpMatchedKF[idx] = vpPointsKFs[matched[idx]]).  Returns
+ * nmatches. */
+int orbm_search_by_projection_sim3(const orbm_frame* kf, int nq, const uint8_t* valid, const float* u,
+                                   const float* v, const int32_t* level, const uint8_t* desc, float th,
+                                   float ratio_hamming, int32_t* matched);
+
+/* SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (src/ORBmatcher.cc:1457-1674)
+ * for pinhole keyframes.  Caller geometry: for KF1's map points (kf1->n
+ * entries) valid1 (pMP && !already matched && !bad && depth >= 0 && inside
+ * KF2 && distance invariance), u1/v1 = projection into KF2 by S21 * T1w,
+ * level1 = PredictScale(dist3D, pKF2), mdesc1 = GetDescriptor(); for KF2's
+ * map points the same into KF1 (S12 * T2w).  matches12[kf1->n] out: the KF2
+ * feature of every NEW mutual match (i1 -> idx2 -> i1, :1658-1671), else -1
+ * (vpMatches12[i1] keeps its value).  Returns nFound. */
+int orbm_search_by_sim3(const orbm_frame* kf1, const orbm_frame* kf2, const uint8_t* valid1, const float* u1,
+                        const float* v1, const int32_t* level1, const uint8_t* mdesc1, const uint8_t* valid2,
+                        const float* u2, const float* v2, const int32_t* level2, const uint8_t* mdesc2, float th,
+                        int32_t* matches12);
+
+/* Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (src/ORBmatcher.cc:1340-1455)
+ * for a pinhole keyframe: the matching of every point.  Caller geometry as
+ * for orbm_search_by_projection_sim3 (with spAlreadyFound = pKF->GetMapPoints()).
+ * best_idx[i] = the keyframe keypoint (bestDist <= TH_LOW) or -1, best_dist[i]
+ * its distance; the replace / add decisions (:1439-1449) read the map and
+ * stay with the caller, in index order.  Returns the number of points with a
+ * keypoint (nFused). */
+int orbm_fuse_sim3(const orbm_frame* kf, int nmp, const uint8_t* valid, const float* u, const float* v,
+                   const int32_t* level, const uint8_t* desc, float th, int32_t* best_idx, int32_t* best_dist);
+
 /* ---------------- vocabulary side ---------------- */
 
 /* TemplatedVocabulary::loadFromTextFile (TemplatedVocabulary.h:1338-1424): the

@@ -59,6 +59,11 @@ def lib():
         L.orbo_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
         L.orbo_detect_relocalization_candidates.argtypes = [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp,
                                                              i32, vp, vp, i32]
+        L.orbo_search_by_bow_kf.argtypes = [vp, vp, vp, vp, vp, vp, f32, i32, vp]
+        L.orbo_search_by_projection_kf.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp]
+        L.orbo_search_by_projection_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, f32, vp]
+        L.orbo_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp]
+        L.orbo_fuse_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, vp, vp]
         L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
         _lib = L
     return _lib
@@ -276,3 +281,53 @@ def compute_distinctive_descriptors(off, desc):
     best = np.zeros(max(len(off) - 1, 0), np.int32)
     lib().orbo_compute_distinctive_descriptors(len(best), abi.ptr(off), abi.ptr(desc), abi.ptr(best))
     return best
+
+
+def _q(valid, u, v, level, desc):
+    return (np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),
+            np.ascontiguousarray(v, np.float32), np.ascontiguousarray(level, np.int32),
+            np.ascontiguousarray(desc, np.uint8).reshape(-1, 32))
+
+
+def search_by_bow_kf(kf1, fv1, valid1, kf2, fv2, valid2, nnratio=0.75, check_ori=True):
+    v1 = np.ascontiguousarray(valid1, np.uint8)
+    v2 = np.ascontiguousarray(valid2, np.uint8)
+    m12 = np.zeros(kf1.struct.n, np.int32)
+    nm = lib().orbo_search_by_bow_kf(kf1.ref(), fv1.ref(), abi.ptr(v1), kf2.ref(), fv2.ref(), abi.ptr(v2), nnratio,
+                                     int(check_ori), abi.ptr(m12))
+    return nm, m12
+
+
+def search_by_projection_kf(f, valid, u, v, level, kf_angle, desc, th, orb_dist, check_ori=True, owner=None):
+    q = _q(valid, u, v, level, desc)
+    ang = np.ascontiguousarray(kf_angle, np.float32)
+    own = np.full(f.struct.n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+    nm = lib().orbo_search_by_projection_kf(f.ref(), len(q[0]), abi.ptr(q[0]), abi.ptr(q[1]), abi.ptr(q[2]),
+                                            abi.ptr(q[3]), abi.ptr(ang), abi.ptr(q[4]), th, orb_dist,
+                                            int(check_ori), abi.ptr(own))
+    return nm, own
+
+
+def search_by_projection_sim3(kf, valid, u, v, level, desc, th, ratio_hamming=1.0, matched=None):
+    q = _q(valid, u, v, level, desc)
+    m = np.full(kf.struct.n, -1, np.int32) if matched is None else np.ascontiguousarray(matched, np.int32).copy()
+    nm = lib().orbo_search_by_projection_sim3(kf.ref(), len(q[0]), *[abi.ptr(a) for a in q], th, ratio_hamming,
+                                              abi.ptr(m))
+    return nm, m
+
+
+def search_by_sim3(kf1, kf2, q1, q2, th):
+    """q1 / q2 = (valid, u, v, level, desc) of KF1's points in KF2 and KF2's points in KF1."""
+    a1, a2 = _q(*q1), _q(*q2)
+    m12 = np.zeros(kf1.struct.n, np.int32)
+    nf = lib().orbo_search_by_sim3(kf1.ref(), kf2.ref(), *[abi.ptr(a) for a in a1], *[abi.ptr(a) for a in a2], th,
+                                   abi.ptr(m12))
+    return nf, m12
+
+
+def fuse_sim3(kf, valid, u, v, level, desc, th):
+    q = _q(valid, u, v, level, desc)
+    n = len(q[0])
+    bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
+    nf = lib().orbo_fuse_sim3(kf.ref(), n, *[abi.ptr(a) for a in q], th, abi.ptr(bi), abi.ptr(bd))
+    return nf, bi, bd

@@ -24,6 +24,7 @@
 #include "../include/orb_mi355x.h"
 
 #include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -1319,6 +1320,192 @@ int orbo_compute_distinctive_descriptors(int npoints, const int32_t* off, const 
         best[p] = bestIdx;
     }
     return 0;
+}
+
+
+// ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vpMatches12)
+// (src/ORBmatcher.cc:765-905), NLeft == -1.  valid = MapPoint != NULL && !isBad.
+int orbo_search_by_bow_kf(const orbm_frame* k1, const orbm_featvec* fv1, const uint8_t* valid1,
+                          const orbm_frame* k2, const orbm_featvec* fv2, const uint8_t* valid2, float ratio,
+                          int check_ori, int32_t* m12) {
+    for (int i = 0; i < k1->n; ++i) m12[i] = -1;
+    std::vector<char> matched2(k2->n, 0);
+    std::vector<int> hist[kHisto];
+    int nm = 0;
+    int a = 0, b = 0;
+    while (a < fv1->nnodes && b < fv2->nnodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            for (int p = fv1->offsets[a]; p < fv1->offsets[a + 1]; ++p) {
+                const int idx1 = (int)fv1->idx[p];
+                if (!valid1[idx1]) continue;                                        // :804-808
+                const uint8_t* d1 = k1->desc + (size_t)idx1 * 32;
+                int best1 = 256, bestIdx2 = -1, best2 = 256;
+                for (int q = fv2->offsets[b]; q < fv2->offsets[b + 1]; ++q) {
+                    const int idx2 = (int)fv2->idx[q];
+                    if (matched2[idx2] || !valid2[idx2]) continue;                  // :826-830
+                    const int dist = hamming(d1, k2->desc + (size_t)idx2 * 32);
+                    if (dist < best1) { best2 = best1; best1 = dist; bestIdx2 = idx2; }
+                    else if (dist < best2) best2 = dist;
+                }
+                if (best1 < kThLow) {                                               // :848
+                    if ((float)best1 < ratio * (float)best2) {
+                        m12[idx1] = bestIdx2;
+                        matched2[bestIdx2] = 1;
+                        if (check_ori) hist[rot_bin(k1->kps[idx1].angle, k2->kps[bestIdx2].angle)].push_back(idx1);
+                        ++nm;
+                    }
+                }
+            }
+            ++a;
+            ++b;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) {
+            a = (int)(std::lower_bound(fv1->node_ids + a, fv1->node_ids + fv1->nnodes, fv2->node_ids[b]) - fv1->node_ids);
+        } else {
+            b = (int)(std::lower_bound(fv2->node_ids + b, fv2->node_ids + fv2->nnodes, fv1->node_ids[a]) - fv2->node_ids);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < kHisto; ++i) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int idx1 : hist[i]) { m12[idx1] = -1; --nm; }
+        }
+    }
+    return nm;
+}
+
+// ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, sAlreadyFound,
+// th, ORBdist) (src/ORBmatcher.cc:1889-2010), Nleft == -1; geometry from the
+// caller.  owner: -1 = mvpMapPoints[i2] NULL, else occupied.
+int orbo_search_by_projection_kf(const orbm_frame* f, int nq, const uint8_t* valid, const float* u, const float* v,
+                                 const int32_t* level, const float* kf_angle, const uint8_t* desc, float th,
+                                 int orb_dist, int check_ori, int32_t* owner) {
+    Grid g(f);
+    int nm = 0;
+    std::vector<int> hist[kHisto];
+    for (int i = 0; i < nq; ++i) {
+        if (!valid[i]) continue;
+        const int pl = level[i];
+        const float radius = th * f->scale_factors[pl];                             // :1937
+        const std::vector<int> cand = g.area(u[i], v[i], radius, pl - 1, pl + 1);   // :1939
+        if (cand.empty()) continue;
+        int bestDist = 256, bestIdx2 = -1;
+        for (int i2 : cand) {
+            if (owner[i2] != -1) continue;                                          // :1952
+            const int dist = hamming(desc + (size_t)i * 32, f->desc + (size_t)i2 * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx2 = i2; }
+        }
+        if (bestDist <= orb_dist && bestIdx2 >= 0) {                                // :1966
+            owner[bestIdx2] = i;
+            ++nm;
+            if (check_ori) hist[rot_bin(kf_angle[i], f->kps[bestIdx2].angle)].push_back(bestIdx2);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int k = 0; k < kHisto; ++k) {
+            if (k == i1 || k == i2 || k == i3) continue;
+            for (int j : hist[k]) { owner[j] = -1; --nm; }
+        }
+    }
+    return nm;
+}
+
+// ORBmatcher::SearchByProjection(KeyFrame* pKF, Sim3 Scw, vpPoints, vpMatched, th,
+// ratioHamming) (src/ORBmatcher.cc:427-532; the vpPointsKFs twin :534-646 matches
+// identically); geometry from the caller.  matched: -1 = NULL, else occupied.
+int orbo_search_by_projection_sim3(const orbm_frame* kf, int nq, const uint8_t* valid, const float* u,
+                                   const float* v, const int32_t* level, const uint8_t* desc, float th,
+                                   float ratio_hamming, int32_t* matched) {
+    Grid g(kf);
+    int nm = 0;
+    for (int i = 0; i < nq; ++i) {
+        if (!valid[i]) continue;
+        const int pl = level[i];
+        const float radius = th * kf->scale_factors[pl];                            // :489
+        const std::vector<int> cand = g.area(u[i], v[i], radius, -1, -1);          // :491
+        if (cand.empty()) continue;
+        int bestDist = 256, bestIdx = -1;
+        for (int idx : cand) {
+            if (matched[idx] != -1) continue;                                       // :504
+            const int kl = kf->kps[idx].octave;
+            if (kl < pl - 1 || kl > pl) continue;                                   // :509
+            const int dist = hamming(desc + (size_t)i * 32, kf->desc + (size_t)idx * 32);
+            if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+        }
+        if ((float)bestDist <= (float)kThLow * ratio_hamming && bestIdx >= 0) {     // :523
+            matched[bestIdx] = i;
+            ++nm;
+        }
+    }
+    return nm;
+}
+
+namespace {
+// one direction of SearchBySim3 / the matching of Fuse(Sim3): first least
+// distance over the levels pl-1 .. pl of KeyFrame::GetFeaturesInArea.
+int best_in_area(const Grid& g, const orbm_frame* kf, float x, float y, int pl, const uint8_t* d, float th,
+                 int& bestDist) {
+    const float radius = th * kf->scale_factors[pl];
+    const std::vector<int> cand = g.area(x, y, radius, -1, -1);
+    bestDist = INT_MAX;
+    int bestIdx = -1;
+    for (int idx : cand) {
+        const int kl = kf->kps[idx].octave;
+        if (kl < pl - 1 || kl > pl) continue;
+        const int dist = hamming(d, kf->desc + (size_t)idx * 32);
+        if (dist < bestDist) { bestDist = dist; bestIdx = idx; }
+    }
+    return bestIdx;
+}
+}  // namespace
+
+// ORBmatcher::SearchBySim3 (src/ORBmatcher.cc:1457-1674), pinhole keyframes,
+// projections and predicted levels from the caller.  m12: new mutual matches.
+int orbo_search_by_sim3(const orbm_frame* kf1, const orbm_frame* kf2, const uint8_t* valid1, const float* u1,
+                        const float* v1, const int32_t* level1, const uint8_t* mdesc1, const uint8_t* valid2,
+                        const float* u2, const float* v2, const int32_t* level2, const uint8_t* mdesc2, float th,
+                        int32_t* m12) {
+    Grid g1(kf1), g2(kf2);
+    std::vector<int> vnMatch1(kf1->n, -1), vnMatch2(kf2->n, -1);
+    for (int i1 = 0; i1 < kf1->n; ++i1) {                                           // :1496-1573
+        if (!valid1[i1]) continue;
+        int bd;
+        const int bi = best_in_area(g2, kf2, u1[i1], v1[i1], level1[i1], mdesc1 + (size_t)i1 * 32, th, bd);
+        if (bd <= kThHigh) vnMatch1[i1] = bi;
+    }
+    for (int i2 = 0; i2 < kf2->n; ++i2) {                                           // :1576-1653
+        if (!valid2[i2]) continue;
+        int bd;
+        const int bi = best_in_area(g1, kf1, u2[i2], v2[i2], level2[i2], mdesc2 + (size_t)i2 * 32, th, bd);
+        if (bd <= kThHigh) vnMatch2[i2] = bi;
+    }
+    int nFound = 0;
+    for (int i1 = 0; i1 < kf1->n; ++i1) {                                           // :1658-1671
+        m12[i1] = -1;
+        const int idx2 = vnMatch1[i1];
+        if (idx2 >= 0 && vnMatch2[idx2] == i1) { m12[i1] = idx2; ++nFound; }
+    }
+    return nFound;
+}
+
+// ORBmatcher::Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (src/ORBmatcher.cc:1340-1455),
+// the matching of each point; geometry from the caller.
+int orbo_fuse_sim3(const orbm_frame* kf, int nmp, const uint8_t* valid, const float* u, const float* v,
+                   const int32_t* level, const uint8_t* desc, float th, int32_t* best_idx, int32_t* best_dist) {
+    Grid g(kf);
+    int nf = 0;
+    for (int i = 0; i < nmp; ++i) {
+        best_idx[i] = -1;
+        best_dist[i] = -1;
+        if (!valid[i]) continue;
+        int bd;
+        const int bi = best_in_area(g, kf, u[i], v[i], level[i], desc + (size_t)i * 32, th, bd);
+        if (bd <= kThLow) { best_idx[i] = bi; best_dist[i] = bd; ++nf; }            // :1437
+    }
+    return nf;
 }
 
 }  // extern "C"

@@ -22,6 +22,8 @@ EXPORTS = [
     "orbv_load_text", "orbv_text_vocab_view", "orbv_free_text", "orbv_bow_assemble", "orbv_score",
     "orbk_db_create", "orbk_db_destroy", "orbk_db_upload", "orbk_detect_relocalization_candidates",
     "orbm_fuse", "orbm_search_for_triangulation", "orbm_compute_distinctive_descriptors",
+    "orbm_search_by_bow_kf", "orbm_search_by_projection_kf", "orbm_search_by_projection_sim3",
+    "orbm_search_by_sim3", "orbm_fuse_sim3",
 ]
 
 _lib = None
@@ -55,6 +57,11 @@ def load(path: Path | str = LIB_PATH):
     L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]
     L.orbm_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
     L.orbm_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
+    L.orbm_search_by_bow_kf.argtypes = [vp, vp, vp, vp, vp, vp, f32, i32, vp]
+    L.orbm_search_by_projection_kf.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp]
+    L.orbm_search_by_projection_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, f32, vp]
+    L.orbm_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp]
+    L.orbm_fuse_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, vp, vp]
     L.orbk_db_create.restype = vp
     L.orbk_db_create.argtypes = [i32]
     L.orbk_db_destroy.argtypes = [vp]

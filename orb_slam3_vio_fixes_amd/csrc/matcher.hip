@@ -128,6 +128,68 @@ __device__ __forceinline__ bool cell_range(float x, float y, float r, const Grid
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Cell-start table of a grid order: cs[c] = first position of `gsorted` whose
+// cell is >= c, c in [0, 3072].  The candidates of GetFeaturesInArea
+// (ix outer, iy inner, index order inside a cell) are then, per grid column
+// gx in [x0, x1], the contiguous run [cs[gx*48 + y0], cs[gx*48 + y1 + 1]) of
+// the grid order, and the runs concatenated in column order ARE the
+// reference's candidate list -- no scan over the whole frame per query.
+// ---------------------------------------------------------------------------
+constexpr int kCells = kGridCols * kGridRows;
+
+__global__ __launch_bounds__(256) void k_cell_start(const uint32_t* __restrict__ gsorted,
+                                                    const int* __restrict__ gcount, int cap, int* __restrict__ cs) {
+    const int f = blockIdx.x;
+    const uint32_t* gs = gsorted + (long long)f * cap;
+    const int gn = gcount[f];
+    int* out = cs + (long long)f * (kCells + 1);
+    for (int c = threadIdx.x; c <= kCells; c += blockDim.x) {
+        const uint32_t key = (uint32_t)c << 16;
+        int lo = 0, hi = gn;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (gs[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        out[c] = lo;
+    }
+}
+
+// Lane l holds the run of grid column x0 + l (the grid has 64 columns, so one
+// wave covers every column range): its start `lo` in the grid order and its
+// offset `off` in the concatenated candidate list; `total` = list length.
+struct AreaRuns { int lo, off, total; };
+
+__device__ __forceinline__ AreaRuns area_runs(const int* cs, const CellRange& cr) {
+    const int lane = lane_id();
+    int lo = 0, len = 0;
+    if (lane <= cr.x1 - cr.x0) {
+        const int c = (cr.x0 + lane) * kGridRows;
+        lo = cs[c + cr.y0];
+        len = cs[c + cr.y1 + 1] - lo;
+    }
+    int inc = len;
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const int t = __shfl_up(inc, o, kWave);
+        if (lane >= o) inc += t;
+    }
+    return AreaRuns{lo, inc - len, __shfl(inc, kWave - 1, kWave)};
+}
+
+// Grid-order position of candidate t (0 <= t < total): the run s is the last
+// lane with off_s <= t (offsets are non-decreasing).  Every lane takes part.
+__device__ __forceinline__ int area_pos(const AreaRuns& r, int t) {
+    int s = 0;
+#pragma unroll
+    for (int step = kWave / 2; step > 0; step >>= 1) {
+        const int o = __shfl(r.off, s + step, kWave);
+        if (o <= t) s += step;
+    }
+    return __shfl(r.lo, s, kWave) + (t - __shfl(r.off, s, kWave));
+}
+
 // Running best / second-best over a candidate stream in reference order.
 struct Best2 {
     int best, best2, idx, lvl, lvl2;
@@ -472,6 +534,12 @@ static void launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
 // mono branch, one wave per (keyframe, frame) pair: merge-join of the two
 // FeatureVectors by node id; per KF feature with a valid MapPoint, best/second
 // over the frame features of the node that are not yet matched.
+// With f_valid set it is SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2)
+// (:765-905): the second keyframe plays the frame, its features need a valid
+// MapPoint (:824-830), the acceptance is strict (`bestDist1 < TH_LOW`, :848)
+// and out12 receives vpMatches12 by KF1 feature.  The two forms record the
+// rotation bin of a match on opposite sides (:352 bestIdxF, :864 idx1); every
+// match is a one-to-one pair, so filtering by either side is the same.
 // ---------------------------------------------------------------------------
 struct BowArgs {
     // keyframes (one per pair), concatenated: kf i owns features
@@ -494,6 +562,8 @@ struct BowArgs {
     int check_ori;
     int32_t* match;      // [pair][f_n]
     int32_t* nmatches;   // [pair]
+    const uint8_t* f_valid;   // KF-KF form: pKF2 MapPoint != NULL && !isBad(), else NULL
+    int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
 };
 
 __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
@@ -531,11 +601,13 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
                     int d = INT_MAX, fi = -1;
                     if (q < fe) {
                         fi = (int)a.f_idx[q];
-                        if (match[fi] < 0) d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
+                        if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
+                            d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
                     }
                     merge_chunk(st, d, fi, 0);
                 }
-                if (st.best <= kThLow && (float)st.best < a.ratio * (float)st.best2) {
+                const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;
+                if (low && (float)st.best < a.ratio * (float)st.best2) {
                     if (lane == 0) match[st.idx] = ikf;
                     if (a.check_ori) {
                         const int bn = rot_bin(KK[ikf].angle, a.f_kps[st.idx].angle);
@@ -568,6 +640,14 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
     __syncthreads();
     int32_t* out = a.match + (long long)pr * a.f_n;
     for (int i = lane; i < a.f_n; i += kWave) out[i] = match[i];
+    if (a.out12) {
+        const int kn1 = (int)(a.kp_off[pr + 1] - kpo);
+        int32_t* o12 = a.out12 + kpo;
+        for (int i = lane; i < kn1; i += kWave) o12[i] = -1;
+        __syncthreads();
+        for (int i = lane; i < a.f_n; i += kWave)
+            if (match[i] >= 0) o12[match[i]] = i;
+    }
     if (lane == 0) a.nmatches[pr] = nm;
 }
 
@@ -579,14 +659,27 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
-// k_proj: SearchByProjection(Frame&, vector<MapPoint*>) (ORBmatcher.cc:43-213)
-// and SearchByProjection(Frame&, const Frame&) (ORBmatcher.cc:1676-1887), the
-// Nleft == -1 branches, one wave per frame.
+// k_proj: the projection searches with a serial claim on the target's slots,
+// one wave per target, queries in reference order, the candidates of a query
+// spread over the lanes (cell-start runs, in GetFeaturesInArea order).
+//   mode 0  SearchByProjection(Frame&, vector<MapPoint*>) (ORBmatcher.cc:43-213),
+//           best + second best with their levels, F.Nleft == -1.
+//   mode 1  "best only" searches (strict `dist < bestDist` from 256, accept
+//           bestDist <= accept):
+//     SearchByProjection(Frame&, const Frame&) (:1676-1887): win 0/1/2,
+//       skip a slot whose MapPoint has observations, mvuRight gate, TH_HIGH,
+//       rotation filter;
+//     SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist)
+//       (:1889-2010): win 0 (levels pl-1 .. pl+1), skip any occupied slot,
+//       ORBdist, rotation filter;
+//     SearchByProjection(KeyFrame*, Sim3, vpPoints, vpMatched, th,
+//       ratioHamming) and its vpPointsKFs twin (:427-646): win 3 (levels
+//       pl-1 .. pl, :509), skip any matched slot, TH_LOW * ratioHamming.
 // ---------------------------------------------------------------------------
 struct ProjArgs {
-    int mode;                 // 0 = map points, 1 = last frame
+    int mode;                 // 0 = map points, 1 = best-only searches
     const orb_keypoint* kps; const uint8_t* desc; int n; const float* u_right; const float* scale;
-    const uint32_t* gsorted; const int* gcount;
+    const uint32_t* gsorted; const int* gcount; const int* cellstart;
     GridParams g;
     int nq;
     const float* qx; const float* qy; const float* qxr;
@@ -594,6 +687,8 @@ struct ProjArgs {
     const uint8_t* qvalid; const uint8_t* qhas_obs; const uint8_t* qdesc; const float* qangle;
     float th, th_far, ratio;
     int far_points, last_mode, check_ori;
+    int skip_any;             // any occupied slot is skipped (vpMatched[idx] / mvpMapPoints[i2] != NULL)
+    float accept;             // mode 1: bestDist <= accept
     int32_t* owner; const uint8_t* blocked;
     int32_t* nmatches;
 };
@@ -601,16 +696,12 @@ struct ProjArgs {
 __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int lane = lane_id();
-    int* hist = lds;
-    int* slot_bin_cnt = hist + 32;            // unused padding
-    (void)slot_bin_cnt;
-    int8_t* sbin = (int8_t*)(lds + 64);      // per F slot: list of bins is needed -> histogram entries
-    // rotation histogram entries in push order: (bin, slot)
-    int* hent = lds + 64 + (a.n + 3) / 4;
+    int* hist = lds;                          // 32
+    int* cs = lds + 32;                       // kCells + 1: cell-start table
+    int* hent = cs + kCells + 1;              // rotation histogram entries in push order: (bin << 16) | slot
     for (int i = lane; i < 32; i += kWave) hist[i] = 0;
-    (void)sbin;
+    for (int i = lane; i <= kCells; i += kWave) cs[i] = a.cellstart[i];
     __syncthreads();
-    const int gn = a.gcount[0];
     int nm = 0, nh = 0;
     for (int i = 0; i < a.nq; ++i) {
         if (!a.qvalid[i]) continue;
@@ -628,6 +719,7 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
             r = a.th * a.scale[oct];
             if (a.last_mode == 1) { minL = oct; maxL = -1; }
             else if (a.last_mode == 2) { minL = 0; maxL = oct; }
+            else if (a.last_mode == 3) { minL = oct - 1; maxL = oct; }
             else { minL = oct - 1; maxL = oct + 1; }
         }
         CellRange cr;
@@ -635,38 +727,34 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
         const bool checkL = (minL > 0) || (maxL >= 0);
         const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
         const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+        const AreaRuns ar = area_runs(cs, cr);
         Best2 st{256, 256, -1, -1, -1};
-        bool any = false;
-        for (int base = 0; base < gn; base += kWave) {
-            const int j = base + lane;
+        for (int base = 0; base < ar.total; base += kWave) {
+            const int t = base + lane;
+            const int j = area_pos(ar, min(t, ar.total - 1));
             int d = INT_MAX, fi = -1, lv = -1;
-            if (j < gn) {
-                const uint32_t v = a.gsorted[j];
-                const int cell = (int)(v >> 16), gx = cell / kGridRows, gy = cell - gx * kGridRows;
-                fi = (int)(v & 0xffff);
-                if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1) {
-                    const orb_keypoint k = a.kps[fi];
-                    bool ok = true;
-                    if (checkL) {
-                        if (k.octave < minL) ok = false;
-                        if (maxL >= 0 && k.octave > maxL) ok = false;
+            if (t < ar.total) {
+                fi = (int)(a.gsorted[j] & 0xffff);
+                const orb_keypoint k = a.kps[fi];
+                bool ok = true;
+                if (checkL) {
+                    if (k.octave < minL) ok = false;
+                    if (maxL >= 0 && k.octave > maxL) ok = false;
+                }
+                if (ok && fabsf(k.x - x) < r && fabsf(k.y - y) < r) {
+                    const int o = a.owner[fi];
+                    const bool blk = o == -1 ? false
+                                   : (a.skip_any ? true : (o <= -2 ? a.blocked[fi] != 0 : a.qhas_obs[o] != 0));
+                    bool pass = !blk;
+                    if (pass && a.u_right && a.u_right[fi] > 0) {
+                        const float er = fabsf(a.qxr[i] - a.u_right[fi]);
+                        if (er > r) pass = false;
                     }
-                    if (ok && fabsf(k.x - x) < r && fabsf(k.y - y) < r) {
-                        const int o = a.owner[fi];
-                        const bool blk = o == -1 ? false : (o <= -2 ? a.blocked[fi] != 0 : a.qhas_obs[o] != 0);
-                        bool pass = !blk;
-                        if (pass && a.u_right && a.u_right[fi] > 0) {
-                            const float er = fabsf(a.qxr[i] - a.u_right[fi]);
-                            if (er > r) pass = false;
-                        }
-                        if (pass) { d = hamming32(q0, q1, a.desc + (long long)fi * 32); lv = k.octave; }
-                        any = true;
-                    }
+                    if (pass) { d = hamming32(q0, q1, a.desc + (long long)fi * 32); lv = k.octave; }
                 }
             }
             merge_chunk(st, d, fi, lv);
         }
-        (void)any;
         if (a.mode == 0) {
             if (st.best <= kThHigh) {
                 if (st.lvl == st.lvl2 && (float)st.best > a.ratio * (float)st.best2) continue;
@@ -676,7 +764,7 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
                 }
             }
         } else {
-            if (st.best <= kThHigh) {
+            if (st.idx >= 0 && (float)st.best <= a.accept) {
                 if (lane == 0) a.owner[st.idx] = i;
                 ++nm;
                 if (a.check_ori) {
@@ -704,6 +792,8 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
     }
     if (lane == 0) a.nmatches[0] = nm;
 }
+
+static size_t proj_lds(int nq) { return (size_t)(32 + kCells + 1 + nq + 1) * 4 + 64; }
 
 // ---------------------------------------------------------------------------
 // k_transform: TemplatedVocabulary::transform per descriptor
@@ -754,7 +844,11 @@ __device__ __forceinline__ float lin2(float x, float a, float y, float b, float 
 
 // k_fuse: Fuse(pKF, vpMapPoints, th) (ORBmatcher.cc:1148-1331) -- the keypoint
 // each map point would fuse with; one wave per map point (the matching of a
-// point reads none of the others' results).
+// point reads none of the others' results).  chi2 = 0, accept = TH_LOW is the
+// matching of Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) (:1340-1455);
+// chi2 = 0, accept = TH_HIGH one direction of SearchBySim3 (:1496-1573,
+// :1576-1653).  All take the first candidate at the least distance
+// (`dist < bestDist`) among the levels pl-1 .. pl.
 struct FuseArgs {
     const orb_keypoint* kps;
     const uint8_t* desc;
@@ -764,6 +858,7 @@ struct FuseArgs {
     GridParams g;
     const uint32_t* gsorted;
     const int* gcount;
+    const int* cellstart;
     int nmp;
     const uint8_t* valid;
     const float *u, *v, *ur;
@@ -771,6 +866,8 @@ struct FuseArgs {
     const uint8_t* mdesc;       // GetDescriptor()
     float th;
     int fma;
+    int chi2;                   // 1: the reprojection-error gate of :1267-1280
+    int accept;                 // bestDist <= accept
     int32_t* best_idx;
     int32_t* best_dist;
 };
@@ -787,35 +884,37 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs a) {
         if (cell_range(x, y, r, a.g, cr)) {
             const uint4 q0 = *(const uint4*)(a.mdesc + (long long)i * 32);
             const uint4 q1 = *(const uint4*)(a.mdesc + (long long)i * 32 + 16);
-            const int gn = a.gcount[0];
+            const AreaRuns ar = area_runs(a.cellstart, cr);
             uint32_t best = 0xffffffffu;            // (dist << 20) | position in GetFeaturesInArea order
-            for (int j = lane; j < gn; j += kWave) {
-                const uint32_t gv = a.gsorted[j];
-                const int cell = (int)(gv >> 16), gx = cell / kGridRows, gy = cell - gx * kGridRows;
-                if (gx < cr.x0 || gx > cr.x1 || gy < cr.y0 || gy > cr.y1) continue;
-                const int fi = (int)(gv & 0xffff);
+            for (int base = 0; base < ar.total; base += kWave) {
+                const int t = base + lane;
+                const int j = area_pos(ar, min(t, ar.total - 1));
+                if (t >= ar.total) continue;
+                const int fi = (int)(a.gsorted[j] & 0xffff);
                 const orb_keypoint k = a.kps[fi];
                 if (!(fabsf(k.x - x) < r && fabsf(k.y - y) < r)) continue;          // KeyFrame.cc:741
                 const int kl = k.octave;
                 if (kl < pl - 1 || kl > pl) continue;                               // :1262-1265
-                const float ex = x - k.x, ey = y - k.y;
-                if (a.u_right && a.u_right[fi] >= 0) {                              // :1267-1280
-                    const float er = a.ur[i] - a.u_right[fi];
-                    const float e2 = a.fma ? __builtin_fmaf(er, er, __builtin_fmaf(ex, ex, ey * ey))
-                                           : ex * ex + ey * ey + er * er;
-                    if ((double)(e2 * a.inv_sigma2[kl]) > 7.8) continue;
-                } else {
-                    const float e2 = sq2(ex, ey, a.fma);
-                    if ((double)(e2 * a.inv_sigma2[kl]) > 5.99) continue;
+                if (a.chi2) {
+                    const float ex = x - k.x, ey = y - k.y;
+                    if (a.u_right && a.u_right[fi] >= 0) {                          // :1267-1280
+                        const float er = a.ur[i] - a.u_right[fi];
+                        const float e2 = a.fma ? __builtin_fmaf(er, er, __builtin_fmaf(ex, ex, ey * ey))
+                                               : ex * ex + ey * ey + er * er;
+                        if ((double)(e2 * a.inv_sigma2[kl]) > 7.8) continue;
+                    } else {
+                        const float e2 = sq2(ex, ey, a.fma);
+                        if ((double)(e2 * a.inv_sigma2[kl]) > 5.99) continue;
+                    }
                 }
                 const int d = hamming32(q0, q1, a.desc + (long long)fi * 32);
-                if (d < 256) best = min(best, ((uint32_t)d << 20) | (uint32_t)j);
+                best = min(best, ((uint32_t)d << 20) | (uint32_t)t);
             }
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
-            if (best != 0xffffffffu && (int)(best >> 20) <= kThLow) {               // :1311
+            if (best != 0xffffffffu && (int)(best >> 20) <= a.accept) {
                 out_dist = (int)(best >> 20);
-                out_idx = (int)(a.gsorted[best & 0xfffff] & 0xffff);
+                out_idx = (int)(a.gsorted[area_pos(ar, (int)(best & 0xfffff))] & 0xffff);
             }
         }
     }
@@ -823,6 +922,25 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs a) {
         a.best_idx[i] = out_idx;
         a.best_dist[i] = out_idx >= 0 ? out_dist : -1;
     }
+}
+
+// SearchBySim3's agreement check (ORBmatcher.cc:1655-1671): i1 -> idx2 -> i1.
+__global__ __launch_bounds__(256) void k_sim3_agree(const int32_t* __restrict__ m1, int n1,
+                                                    const int32_t* __restrict__ m2, int32_t* __restrict__ m12,
+                                                    int32_t* __restrict__ nfound) {
+    __shared__ int cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    int c = 0;
+    for (int i = threadIdx.x; i < n1; i += blockDim.x) {
+        const int idx2 = m1[i];
+        const bool ok = idx2 >= 0 && m2[idx2] == i;
+        m12[i] = ok ? idx2 : -1;
+        c += ok;
+    }
+    atomicAdd(&cnt, c);
+    __syncthreads();
+    if (threadIdx.x == 0) nfound[0] = cnt;
 }
 
 // k_tri: SearchForTriangulation(pKF1, pKF2, ...) (ORBmatcher.cc:907-1146).
@@ -1022,6 +1140,7 @@ struct DevFrame {
     DBuf<int> n;
     DBuf<uint32_t> sorted;
     DBuf<int> count;
+    DBuf<int> cs;               // cell-start table (k_cell_start)
     DBuf<float> ur, scale;
     int upload(const orbm_frame* f, bool grid, hipStream_t st) {
         int rc;
@@ -1039,6 +1158,8 @@ struct DevFrame {
             const int sc = pow2_at_least(nn);
             hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
                                grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
+            if ((rc = cs.alloc(kCells + 1))) return rc;
+            hipLaunchKernelGGL(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
         }
         return ORB_OK;
     }
@@ -1167,7 +1288,7 @@ int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint
         (rc = kpo.put(kp_off, 2)) || (rc = nodo.put(node_off, 2)) || (rc = idxo.put(idx_off, 1)) ||
         (rc = m.alloc(std::max(1, f->n))) || (rc = nm.alloc(1)))
         return rc;
-    BowArgs a;
+    BowArgs a{};
     a.kf_kps = kk.p; a.kf_desc = kd.p; a.kf_valid = kvv.p; a.kp_off = kpo.p;
     a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
@@ -1183,7 +1304,7 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
                                     float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
     if (!map || !f || !ffv || !d_match || !d_nmatches || map->nkf < 0) return ORB_ERR_PARAM;
     if (map->nkf == 0) return ORB_OK;
-    BowArgs a;
+    BowArgs a{};
     a.kf_kps = map->kps; a.kf_desc = map->desc; a.kf_valid = map->valid; a.kp_off = (const long long*)map->kp_off;
     a.kf_node = map->fv_node; a.kf_off = map->fv_off; a.kf_idx = map->fv_idx;
     a.node_off = (const long long*)map->fv_node_off; a.idx_off = (const long long*)map->fv_idx_off;
@@ -1199,9 +1320,10 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     if ((rc = own.put(owner, std::max(1, f->n))) || (rc = blk.put(blocked, std::max(1, f->n))) || (rc = nm.alloc(1)))
         return rc;
     a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
-    a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.g = grid_params(f);
-    a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
-    const size_t lds = 64 * 4 + (f->n + 3) / 4 * 4 + (size_t)(a.nq + 1) * 4 + 64;
+    a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p;
+    a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
+    const size_t lds = proj_lds(a.nq);
+    if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
     hipLaunchKernelGGL(k_proj, dim3(1), dim3(64), lds, 0, a);
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
@@ -1252,6 +1374,7 @@ int orbm_search_by_projection_last(const orbm_frame* cur, int nlast, const uint8
     a.mode = 1; a.nq = nlast; a.qx = qx.p; a.qy = qy.p; a.qxr = qxr.p; a.qlevel = lv.p; a.qviewcos = nullptr;
     a.qdepth = nullptr; a.qvalid = iv.p; a.qhas_obs = ho.p; a.qdesc = qd.p; a.qangle = qa.p;
     a.th = th; a.th_far = 0; a.ratio = 0; a.far_points = 0; a.last_mode = mode; a.check_ori = check_ori;
+    a.skip_any = 0; a.accept = (float)kThHigh;                                   // :1770
     return run_proj(a, cur, df, owner, blocked);
 }
 
@@ -1302,10 +1425,12 @@ int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, cons
         (rc = bur.put(ur, nmp)) || (rc = bval.put(valid, nmp)) || (rc = bd.put(desc, (size_t)nmp * 32)) ||
         (rc = blv.put(level, nmp)) || (rc = bi.alloc(nmp)) || (rc = bdist.alloc(nmp)))
         return rc;
-    FuseArgs a;
+    FuseArgs a{};
     a.kps = df.kps.p; a.desc = df.desc.p; a.u_right = kf->u_right ? df.ur.p : nullptr; a.scale = df.scale.p;
-    a.inv_sigma2 = is2.p; a.g = grid_params(kf); a.gsorted = df.sorted.p; a.gcount = df.count.p; a.nmp = nmp;
+    a.inv_sigma2 = is2.p; a.g = grid_params(kf); a.gsorted = df.sorted.p; a.gcount = df.count.p;
+    a.cellstart = df.cs.p; a.nmp = nmp;
     a.valid = bval.p; a.u = bu.p; a.v = bv.p; a.ur = bur.p; a.level = blv.p; a.mdesc = bd.p; a.th = th; a.fma = fma;
+    a.chi2 = 1; a.accept = kThLow;                                               // :1311
     a.best_idx = bi.p; a.best_dist = bdist.p;
     hipLaunchKernelGGL(k_fuse, dim3((nmp + 3) / 4), dim3(256), 0, 0, a);
     ORB_CHECK(hipGetLastError());
@@ -1388,6 +1513,175 @@ int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const 
     ORB_CHECK(hipGetLastError());
     ORB_CHECK(hipMemcpy(best, bb.p, npoints * sizeof(int32_t), hipMemcpyDeviceToHost));
     return ORB_OK;
+}
+
+
+// ---------------- loop-closing / relocalisation matchers ----------------
+
+int orbm_search_by_bow_kf(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* valid1,
+                          const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* valid2, float nnratio,
+                          int check_ori, int32_t* matches12) {
+    if (!kf1 || !fv1 || !valid1 || !kf2 || !fv2 || !valid2 || !matches12) return ORB_ERR_PARAM;
+    if (kf1->n < 0 || kf2->n < 0) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    DBuf<orb_keypoint> kk, fk; DBuf<uint8_t> kd, fd, kvv, fvv; DBuf<uint32_t> kn, ki, fn, fi; DBuf<int> ko, fo;
+    DBuf<long long> kpo, nodo, idxo; DBuf<int32_t> m, nm, o12;
+    const long long kp_off[2] = {0, kf1->n}, node_off[2] = {0, fv1->nnodes}, idx_off[1] = {0};
+    const int n1idx = fv1->nnodes ? fv1->offsets[fv1->nnodes] : 0;
+    const int n2idx = fv2->nnodes ? fv2->offsets[fv2->nnodes] : 0;
+    static const int zero = 0;
+    if ((rc = kk.put(kf1->kps, kf1->n)) || (rc = kd.put(kf1->desc, (size_t)kf1->n * 32)) ||
+        (rc = kvv.put(valid1, kf1->n)) || (rc = kn.put(fv1->node_ids, fv1->nnodes)) ||
+        (rc = ko.put(fv1->nnodes ? fv1->offsets : &zero, fv1->nnodes + 1)) || (rc = ki.put(fv1->idx, n1idx)) ||
+        (rc = fk.put(kf2->kps, kf2->n)) || (rc = fd.put(kf2->desc, (size_t)kf2->n * 32)) ||
+        (rc = fvv.put(valid2, kf2->n)) || (rc = fn.put(fv2->node_ids, fv2->nnodes)) ||
+        (rc = fo.put(fv2->nnodes ? fv2->offsets : &zero, fv2->nnodes + 1)) || (rc = fi.put(fv2->idx, n2idx)) ||
+        (rc = kpo.put(kp_off, 2)) || (rc = nodo.put(node_off, 2)) || (rc = idxo.put(idx_off, 1)) ||
+        (rc = m.alloc(std::max(1, kf2->n))) || (rc = nm.alloc(1)) || (rc = o12.alloc(std::max(1, kf1->n))))
+        return rc;
+    BowArgs a{};
+    a.kf_kps = kk.p; a.kf_desc = kd.p; a.kf_valid = kvv.p; a.kp_off = kpo.p;
+    a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
+    a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = kf2->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
+    a.f_nnodes = fv2->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
+    a.f_valid = fvv.p; a.out12 = o12.p;
+    if ((rc = launch_bow(a, 1, 0))) return rc;
+    int32_t res = 0;
+    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
+    if (kf1->n) ORB_CHECK(hipMemcpy(matches12, o12.p, kf1->n * 4, hipMemcpyDeviceToHost));
+    return res;
+}
+
+// Shared by the two "best only" projection searches with a claim on any
+// occupied slot (mode 1 of k_proj).
+static int proj_best_only(const orbm_frame* f, int nq, const uint8_t* valid, const float* u, const float* v,
+                          const int32_t* level, const float* angle, const uint8_t* desc, float th, int win,
+                          float accept, int check_ori, int32_t* owner) {
+    if (!f || nq < 0 || !owner || !f->scale_factors) return ORB_ERR_PARAM;
+    if (nq && (!valid || !u || !v || !level || !desc || (check_ori && !angle))) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    if (f->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    for (int i = 0; i < nq; ++i)
+        if (valid[i] && (level[i] < 0 || level[i] >= f->nlevels)) return ORB_ERR_PARAM;
+    if (nq == 0) return 0;
+    orbm_frame fn = *f;
+    fn.u_right = nullptr;                       // no stereo gate in these searches
+    DevFrame df;
+    if ((rc = df.upload(&fn, true, 0))) return rc;
+    DBuf<float> qx, qy, qa; DBuf<int32_t> lv; DBuf<uint8_t> iv, qd;
+    if ((rc = qx.put(u, nq)) || (rc = qy.put(v, nq)) || (rc = lv.put(level, nq)) || (rc = iv.put(valid, nq)) ||
+        (rc = qd.put(desc, (size_t)nq * 32)))
+        return rc;
+    if (check_ori && (rc = qa.put(angle, nq))) return rc;
+    std::vector<uint8_t> blocked(std::max(1, f->n), 1);
+    ProjArgs a{};
+    a.mode = 1; a.nq = nq; a.qx = qx.p; a.qy = qy.p; a.qxr = nullptr; a.qlevel = lv.p; a.qvalid = iv.p;
+    a.qhas_obs = nullptr; a.qdesc = qd.p; a.qangle = check_ori ? qa.p : nullptr;
+    a.th = th; a.last_mode = win; a.check_ori = check_ori; a.skip_any = 1; a.accept = accept;
+    return run_proj(a, &fn, df, owner, blocked.data());
+}
+
+int orbm_search_by_projection_kf(const orbm_frame* f, int nq, const uint8_t* valid, const float* u,
+                                 const float* v, const int32_t* level, const float* kf_angle, const uint8_t* desc,
+                                 float th, int orb_dist, int check_ori, int32_t* owner) {
+    // GetFeaturesInArea(.., nPredictedLevel-1, nPredictedLevel+1) (:1939), bestDist <= ORBdist (:1966)
+    return proj_best_only(f, nq, valid, u, v, level, kf_angle, desc, th, 0, (float)orb_dist, check_ori, owner);
+}
+
+int orbm_search_by_projection_sim3(const orbm_frame* kf, int nq, const uint8_t* valid, const float* u,
+                                   const float* v, const int32_t* level, const uint8_t* desc, float th,
+                                   float ratio_hamming, int32_t* matched) {
+    // levels pl-1 .. pl (:509), bestDist <= TH_LOW * ratioHamming (:523), no rotation filter
+    return proj_best_only(kf, nq, valid, u, v, level, nullptr, desc, th, 3, (float)kThLow * ratio_hamming, 0,
+                          matched);
+}
+
+// One "independent best" pass (k_fuse without the chi-square gate) of nq
+// points against the keyframe kf, into device buffers bi / bd.
+static int best_in_area(const orbm_frame* kf, DevFrame& df, int nq, const uint8_t* valid, const float* u,
+                        const float* v, const int32_t* level, const uint8_t* desc, float th, int accept,
+                        DBuf<int32_t>& bi, DBuf<int32_t>& bd, DBuf<uint8_t>& bval, DBuf<float>& bu,
+                        DBuf<float>& bv, DBuf<int32_t>& blv, DBuf<uint8_t>& bdesc) {
+    int rc;
+    if ((rc = bu.put(u, nq)) || (rc = bv.put(v, nq)) || (rc = bval.put(valid, nq)) ||
+        (rc = bdesc.put(desc, (size_t)nq * 32)) || (rc = blv.put(level, nq)) || (rc = bi.alloc(nq)) ||
+        (rc = bd.alloc(nq)))
+        return rc;
+    FuseArgs a{};
+    a.kps = df.kps.p; a.desc = df.desc.p; a.u_right = nullptr; a.scale = df.scale.p; a.inv_sigma2 = nullptr;
+    a.g = grid_params(kf); a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p; a.nmp = nq;
+    a.valid = bval.p; a.u = bu.p; a.v = bv.p; a.ur = nullptr; a.level = blv.p; a.mdesc = bdesc.p; a.th = th;
+    a.fma = 0; a.chi2 = 0; a.accept = accept; a.best_idx = bi.p; a.best_dist = bd.p;
+    hipLaunchKernelGGL(k_fuse, dim3((nq + 3) / 4), dim3(256), 0, 0, a);
+    ORB_CHECK(hipGetLastError());
+    return ORB_OK;
+}
+
+static int check_levels(int nq, const uint8_t* valid, const int32_t* level, int nlevels) {
+    for (int i = 0; i < nq; ++i)
+        if (valid[i] && (level[i] < 0 || level[i] >= nlevels)) return ORB_ERR_PARAM;
+    return ORB_OK;
+}
+
+int orbm_fuse_sim3(const orbm_frame* kf, int nmp, const uint8_t* valid, const float* u, const float* v,
+                   const int32_t* level, const uint8_t* desc, float th, int32_t* best_idx, int32_t* best_dist) {
+    if (!kf || !kf->scale_factors || nmp < 0 || !best_idx || !best_dist) return ORB_ERR_PARAM;
+    if (nmp && (!valid || !u || !v || !level || !desc)) return ORB_ERR_PARAM;
+    if (nmp == 0) return 0;
+    int rc;
+    if ((rc = device_ok()) || (rc = check_levels(nmp, valid, level, kf->nlevels))) return rc;
+    if (kf->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    DevFrame df;
+    if ((rc = df.upload(kf, true, 0))) return rc;
+    DBuf<int32_t> bi, bd, blv; DBuf<uint8_t> bval, bdesc; DBuf<float> bu, bv;
+    if ((rc = best_in_area(kf, df, nmp, valid, u, v, level, desc, th, kThLow, bi, bd, bval, bu, bv, blv, bdesc)))
+        return rc;                                                               // :1437
+    ORB_CHECK(hipMemcpy(best_idx, bi.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(best_dist, bd.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int i = 0; i < nmp; ++i) n += best_idx[i] >= 0;
+    return n;
+}
+
+int orbm_search_by_sim3(const orbm_frame* kf1, const orbm_frame* kf2, const uint8_t* valid1, const float* u1,
+                        const float* v1, const int32_t* level1, const uint8_t* mdesc1, const uint8_t* valid2,
+                        const float* u2, const float* v2, const int32_t* level2, const uint8_t* mdesc2, float th,
+                        int32_t* matches12) {
+    if (!kf1 || !kf2 || !kf1->scale_factors || !kf2->scale_factors || !matches12 || kf1->n < 0 || kf2->n < 0)
+        return ORB_ERR_PARAM;
+    const int n1 = kf1->n, n2 = kf2->n;
+    if (n1 && (!valid1 || !u1 || !v1 || !level1 || !mdesc1)) return ORB_ERR_PARAM;
+    if (n2 && (!valid2 || !u2 || !v2 || !level2 || !mdesc2)) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    if (n1 > 0xffff || n2 > 0xffff) return ORB_ERR_UNSUPPORTED;
+    // KF1's points are predicted in KF2's pyramid and vice versa (:1534, :1614)
+    if ((rc = check_levels(n1, valid1, level1, kf2->nlevels)) || (rc = check_levels(n2, valid2, level2, kf1->nlevels)))
+        return rc;
+    if (n1 == 0) return 0;
+    DevFrame f1, f2;
+    if ((rc = f1.upload(kf1, true, 0)) || (rc = f2.upload(kf2, true, 0))) return rc;
+    DBuf<int32_t> b1, d1, l1, b2, d2, l2, out, nf; DBuf<uint8_t> va1, de1, va2, de2; DBuf<float> x1, y1, x2, y2;
+    // KF1 -> KF2 (:1496-1573) and KF2 -> KF1 (:1576-1653), bestDist <= TH_HIGH
+    if ((rc = best_in_area(kf2, f2, n1, valid1, u1, v1, level1, mdesc1, th, kThHigh, b1, d1, va1, x1, y1, l1, de1)))
+        return rc;
+    if ((rc = b2.alloc(std::max(1, n2)))) return rc;
+    if (n2) {
+        if ((rc = best_in_area(kf1, f1, n2, valid2, u2, v2, level2, mdesc2, th, kThHigh, b2, d2, va2, x2, y2, l2,
+                               de2)))
+            return rc;
+    } else {
+        ORB_CHECK(hipMemset(b2.p, 0xff, sizeof(int32_t)));
+    }
+    if ((rc = out.alloc(n1)) || (rc = nf.alloc(1))) return rc;
+    hipLaunchKernelGGL(k_sim3_agree, dim3(1), dim3(256), 0, 0, b1.p, n1, b2.p, out.p, nf.p);
+    ORB_CHECK(hipGetLastError());
+    int32_t res = 0;
+    ORB_CHECK(hipMemcpy(matches12, out.p, n1 * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(hipMemcpy(&res, nf.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    return res;
 }
 
 }  // extern "C"

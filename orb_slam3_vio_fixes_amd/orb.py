@@ -370,6 +370,74 @@ class ORBmatcher:
         capi.check(min(nm, 0), "SearchForTriangulation")
         return nm, out
 
+    # ---- relocalisation / loop closing (ORBmatcher.h:55-63,71-84) ----
+
+    def SearchByBoWKF(self, KF1: abi.Keep, fv1: abi.Keep, valid1, KF2: abi.Keep, fv2: abi.Keep, valid2):
+        """SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vpMatches12) (ORBmatcher.cc:765-905):
+        (nmatches, matches12) with matches12[i1] = KF2 feature or -1."""
+        v1 = np.ascontiguousarray(valid1, np.uint8)
+        v2 = np.ascontiguousarray(valid2, np.uint8)
+        m12 = np.full(KF1.struct.n, -1, np.int32)
+        nm = capi.lib().orbm_search_by_bow_kf(KF1.ref(), fv1.ref(), abi.ptr(v1), KF2.ref(), fv2.ref(), abi.ptr(v2),
+                                              self.mfNNratio, int(self.mbCheckOrientation), abi.ptr(m12))
+        capi.check(nm, "SearchByBoW(KF1, KF2)")
+        return nm, m12
+
+    def SearchByProjectionKF(self, F: abi.Keep, valid, u, v, level, kf_angle, desc, th: float, ORBdist: int,
+                             owner=None):
+        """SearchByProjection(Frame&, KeyFrame*, sAlreadyFound, th, ORBdist) (ORBmatcher.cc:1889-2010):
+        (nmatches, owner) -- owner[i2] = keyframe point index for the new matches."""
+        q = _queries(valid, u, v, level, desc)
+        ang = np.ascontiguousarray(kf_angle, np.float32)
+        own = np.full(F.struct.n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        nm = capi.lib().orbm_search_by_projection_kf(F.ref(), len(q[0]), abi.ptr(q[0]), abi.ptr(q[1]),
+                                                     abi.ptr(q[2]), abi.ptr(q[3]), abi.ptr(ang), abi.ptr(q[4]),
+                                                     float(th), int(ORBdist), int(self.mbCheckOrientation),
+                                                     abi.ptr(own))
+        capi.check(nm, "SearchByProjection(F, KF)")
+        return nm, own
+
+    @staticmethod
+    def SearchByProjectionSim3(KF: abi.Keep, valid, u, v, level, desc, th: float, ratioHamming: float = 1.0,
+                               matched=None):
+        """SearchByProjection(KeyFrame*, Sim3, vpPoints, vpMatched, th, ratioHamming)
+        (ORBmatcher.cc:427-646): (nmatches, matched) -- matched[idx] = point index for the new matches."""
+        q = _queries(valid, u, v, level, desc)
+        m = np.full(KF.struct.n, -1, np.int32) if matched is None else np.ascontiguousarray(matched, np.int32).copy()
+        nm = capi.lib().orbm_search_by_projection_sim3(KF.ref(), len(q[0]), *[abi.ptr(a) for a in q], float(th),
+                                                       float(ratioHamming), abi.ptr(m))
+        capi.check(nm, "SearchByProjection(KF, Sim3)")
+        return nm, m
+
+    @staticmethod
+    def SearchBySim3(KF1: abi.Keep, KF2: abi.Keep, q1, q2, th: float):
+        """SearchBySim3(pKF1, pKF2, vpMatches12, S12, th) (ORBmatcher.cc:1457-1674); q1 / q2 =
+        (valid, u, v, level, desc) of KF1's points projected into KF2 and KF2's into KF1:
+        (nFound, matches12) with the new mutual matches."""
+        a1, a2 = _queries(*q1), _queries(*q2)
+        m12 = np.full(KF1.struct.n, -1, np.int32)
+        nf = capi.lib().orbm_search_by_sim3(KF1.ref(), KF2.ref(), *[abi.ptr(a) for a in a1],
+                                            *[abi.ptr(a) for a in a2], float(th), abi.ptr(m12))
+        capi.check(nf, "SearchBySim3")
+        return nf, m12
+
+    @staticmethod
+    def FuseSim3(KF: abi.Keep, valid, u, v, level, desc, th: float):
+        """Fuse(pKF, Scw, vpPoints, th, vpReplacePoint) matching (ORBmatcher.cc:1340-1455):
+        (nfused, best_idx, best_dist)."""
+        q = _queries(valid, u, v, level, desc)
+        n = len(q[0])
+        bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
+        nf = capi.lib().orbm_fuse_sim3(KF.ref(), n, *[abi.ptr(a) for a in q], float(th), abi.ptr(bi), abi.ptr(bd))
+        capi.check(nf, "Fuse(KF, Sim3)")
+        return nf, bi, bd
+
+
+def _queries(valid, u, v, level, desc):
+    return (np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),
+            np.ascontiguousarray(v, np.float32), np.ascontiguousarray(level, np.int32),
+            np.ascontiguousarray(desc, np.uint8).reshape(-1, 32))
+
 
 def compute_distinctive_descriptors(off, desc, device: int = 0) -> np.ndarray:
     """MapPoint::ComputeDistinctiveDescriptors for every point of a CSR batch:
