@@ -8,6 +8,7 @@
 #pragma once
 #include <cstdint>
 #include <stdexcept>
+#include <utility>
 #include <vector>
 
 #include "orb_mi355x.h"
@@ -139,6 +140,119 @@ public:
                                                      blocked.data());
         if (nm < 0) throw std::runtime_error("SearchByProjection failed");
         return nm;
+    }
+
+    // int SearchByProjection(Frame &CurrentFrame, const Frame &LastFrame, const float th, const bool bMono)
+    // The caller projects the last frame's points (Tcw * X); bForwardMode: 0 none, 1 forward, 2 backward.
+    int SearchByProjection(const orbm_frame& CurrentFrame, const std::vector<uint8_t>& valid,
+                           const std::vector<float>& u, const std::vector<float>& v, const std::vector<float>& ur,
+                           const std::vector<int32_t>& lastOctave, const std::vector<float>& lastAngle,
+                           const std::vector<uint8_t>& hasObs, const uint8_t* lastDescriptors, float th,
+                           int motionMode, std::vector<int>& owner, const std::vector<uint8_t>& blocked) const {
+        const int nm = orbm_search_by_projection_last(&CurrentFrame, (int)valid.size(), valid.data(), u.data(),
+                                                      v.data(), ur.data(), lastOctave.data(), lastAngle.data(),
+                                                      hasObs.data(), lastDescriptors, th, motionMode,
+                                                      mbCheckOrientation, owner.data(), blocked.data());
+        if (nm < 0) throw std::runtime_error("SearchByProjection(F, LastFrame) failed");
+        return nm;
+    }
+
+    // int SearchByProjection(Frame &CurrentFrame, KeyFrame* pKF, const set<MapPoint*> &sAlreadyFound,
+    //                        const float th, const int ORBdist)
+    int SearchByProjection(const orbm_frame& CurrentFrame, const std::vector<uint8_t>& valid,
+                           const std::vector<float>& u, const std::vector<float>& v,
+                           const std::vector<int32_t>& predictedLevel, const std::vector<float>& kfAngle,
+                           const uint8_t* mapPointDescriptors, float th, int ORBdist, std::vector<int>& owner) const {
+        const int nm = orbm_search_by_projection_kf(&CurrentFrame, (int)valid.size(), valid.data(), u.data(), v.data(),
+                                                    predictedLevel.data(), kfAngle.data(), mapPointDescriptors, th,
+                                                    ORBdist, mbCheckOrientation, owner.data());
+        if (nm < 0) throw std::runtime_error("SearchByProjection(F, KF) failed");
+        return nm;
+    }
+
+    // int SearchByProjection(KeyFrame* pKF, Sophus::Sim3<float> &Scw, const vector<MapPoint*> &vpPoints,
+    //                        vector<MapPoint*> &vpMatched, int th, float ratioHamming=1.0)
+    // (and the vpPointsKFs variant: vpMatchedKF[idx] = vpPointsKFs[vMatched[idx]] for new matches)
+    int SearchByProjection(const orbm_frame& KF, const std::vector<uint8_t>& valid, const std::vector<float>& u,
+                           const std::vector<float>& v, const std::vector<int32_t>& predictedLevel,
+                           const uint8_t* mapPointDescriptors, std::vector<int>& vMatched, int th,
+                           float ratioHamming = 1.0f) const {
+        const int nm = orbm_search_by_projection_sim3(&KF, (int)valid.size(), valid.data(), u.data(), v.data(),
+                                                      predictedLevel.data(), mapPointDescriptors, (float)th,
+                                                      ratioHamming, vMatched.data());
+        if (nm < 0) throw std::runtime_error("SearchByProjection(KF, Sim3) failed");
+        return nm;
+    }
+
+    // int SearchByBoW(KeyFrame *pKF1, KeyFrame* pKF2, vector<MapPoint*> &vpMatches12)
+    int SearchByBoW(const orbm_frame& KF1, const orbm_featvec& fv1, const std::vector<uint8_t>& valid1,
+                    const orbm_frame& KF2, const orbm_featvec& fv2, const std::vector<uint8_t>& valid2,
+                    std::vector<int>& vMatches12) const {
+        vMatches12.assign(KF1.n, -1);
+        const int nm = orbm_search_by_bow_kf(&KF1, &fv1, valid1.data(), &KF2, &fv2, valid2.data(), mfNNratio,
+                                             mbCheckOrientation, vMatches12.data());
+        if (nm < 0) throw std::runtime_error("SearchByBoW(KF1, KF2) failed");
+        return nm;
+    }
+
+    // int SearchForTriangulation(KeyFrame *pKF1, KeyFrame* pKF2, vector<pair<size_t, size_t> > &vMatchedPairs,
+    //                            const bool bOnlyStereo, const bool bCoarse = false)
+    int SearchForTriangulation(const orbm_frame& KF1, const orbm_featvec& fv1, const std::vector<uint8_t>& hasMP1,
+                               const orbm_frame& KF2, const orbm_featvec& fv2, const std::vector<uint8_t>& hasMP2,
+                               const float F12[9], float epx, float epy, const std::vector<float>& levelSigma2_2,
+                               std::vector<std::pair<size_t, size_t>>& vMatchedPairs, bool bOnlyStereo,
+                               bool bCoarse = false) const {
+        std::vector<int32_t> m12(KF1.n, -1);
+        const int nm = orbm_search_for_triangulation(&KF1, &fv1, hasMP1.data(), &KF2, &fv2, hasMP2.data(), F12, epx,
+                                                     epy, levelSigma2_2.data(), bOnlyStereo, bCoarse,
+                                                     mbCheckOrientation, 1, m12.data());
+        if (nm < 0) throw std::runtime_error("SearchForTriangulation failed");
+        vMatchedPairs.clear();
+        for (int i = 0; i < KF1.n; ++i)
+            if (m12[i] >= 0) vMatchedPairs.emplace_back((size_t)i, (size_t)m12[i]);
+        return nm;
+    }
+
+    // int SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*> &vpMatches12, const Sophus::Sim3f &S12,
+    //                  const float th) -- new mutual matches only (vNewMatches12[i1] = KF2 feature or -1)
+    int SearchBySim3(const orbm_frame& KF1, const orbm_frame& KF2, const std::vector<uint8_t>& valid1,
+                     const std::vector<float>& u1, const std::vector<float>& v1, const std::vector<int32_t>& level1,
+                     const uint8_t* desc1, const std::vector<uint8_t>& valid2, const std::vector<float>& u2,
+                     const std::vector<float>& v2, const std::vector<int32_t>& level2, const uint8_t* desc2,
+                     float th, std::vector<int>& vNewMatches12) const {
+        vNewMatches12.assign(KF1.n, -1);
+        const int nf = orbm_search_by_sim3(&KF1, &KF2, valid1.data(), u1.data(), v1.data(), level1.data(), desc1,
+                                           valid2.data(), u2.data(), v2.data(), level2.data(), desc2, th,
+                                           vNewMatches12.data());
+        if (nf < 0) throw std::runtime_error("SearchBySim3 failed");
+        return nf;
+    }
+
+    // int Fuse(KeyFrame* pKF, const vector<MapPoint *> &vpMapPoints, const float th=3.0, const bool bRight=false)
+    // -- the matching; the caller replaces / adds in index order from vBestIdx.
+    static int Fuse(const orbm_frame& KF, const std::vector<float>& invLevelSigma2, const std::vector<uint8_t>& valid,
+                    const std::vector<float>& u, const std::vector<float>& v, const std::vector<float>& ur,
+                    const std::vector<int32_t>& level, const uint8_t* desc, std::vector<int>& vBestIdx,
+                    std::vector<int>& vBestDist, float th = 3.0f) {
+        vBestIdx.resize(valid.size());
+        vBestDist.resize(valid.size());
+        const int nf = orbm_fuse(&KF, invLevelSigma2.data(), (int)valid.size(), valid.data(), u.data(), v.data(),
+                                 ur.data(), level.data(), desc, th, 1, vBestIdx.data(), vBestDist.data());
+        if (nf < 0) throw std::runtime_error("Fuse failed");
+        return nf;
+    }
+
+    // int Fuse(KeyFrame* pKF, Sophus::Sim3f &Scw, const vector<MapPoint*> &vpPoints, float th,
+    //          vector<MapPoint *> &vpReplacePoint) -- the matching, as above
+    static int Fuse(const orbm_frame& KF, const std::vector<uint8_t>& valid, const std::vector<float>& u,
+                    const std::vector<float>& v, const std::vector<int32_t>& level, const uint8_t* desc, float th,
+                    std::vector<int>& vBestIdx, std::vector<int>& vBestDist) {
+        vBestIdx.resize(valid.size());
+        vBestDist.resize(valid.size());
+        const int nf = orbm_fuse_sim3(&KF, (int)valid.size(), valid.data(), u.data(), v.data(), level.data(), desc,
+                                      th, vBestIdx.data(), vBestDist.data());
+        if (nf < 0) throw std::runtime_error("Fuse(KF, Sim3) failed");
+        return nf;
     }
 
     float mfNNratio;

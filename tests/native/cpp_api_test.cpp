@@ -41,9 +41,29 @@ int main(int argc, char** argv) {
     std::vector<int> m12;
     ORB_SLAM3_MI355X::ORBmatcher matcher(0.9f, true);
     const int nm = matcher.SearchForInitialization(f[0], f[1], prev, m12, 100);
-    std::printf("%zu %d %016llx %016llx %zu %d %d %016llx\n", k[0].size(), mono[0],
+    // SearchByBoW(KF1, KF2) with FeatureVectors node(i) = i % 16 on both sides, every MapPoint valid
+    std::vector<uint32_t> nodes[2], idx[2];
+    std::vector<int32_t> offs[2];
+    std::vector<uint8_t> valid[2];
+    orbm_featvec fv[2];
+    for (int i = 0; i < 2; ++i) {
+        const int n = (int)k[i].size();
+        for (int nd = 0; nd < 16; ++nd) {
+            const int before = (int)idx[i].size();
+            for (int j = nd; j < n; j += 16) idx[i].push_back((uint32_t)j);
+            if ((int)idx[i].size() > before) { nodes[i].push_back(nd); offs[i].push_back(before); }
+        }
+        offs[i].push_back((int)idx[i].size());
+        valid[i].assign(n, 1);
+        fv[i] = orbm_featvec{(int32_t)nodes[i].size(), nodes[i].data(), offs[i].data(), idx[i].data()};
+    }
+    std::vector<int> b12;
+    ORB_SLAM3_MI355X::ORBmatcher loop_matcher(0.75f, true);
+    const int nb = loop_matcher.SearchByBoW(f[0], fv[0], valid[0], f[1], fv[1], valid[1], b12);
+    std::printf("%zu %d %016llx %016llx %zu %d %d %016llx %d %016llx\n", k[0].size(), mono[0],
                 (unsigned long long)fnv(k[0].data(), k[0].size() * sizeof(orb_keypoint)),
                 (unsigned long long)fnv(d[0].data.data(), d[0].data.size()), k[1].size(), mono[1], nm,
-                (unsigned long long)fnv(m12.data(), m12.size() * sizeof(int)));
+                (unsigned long long)fnv(m12.data(), m12.size() * sizeof(int)), nb,
+                (unsigned long long)fnv(b12.data(), b12.size() * sizeof(int)));
     return 0;
 }

@@ -38,5 +38,10 @@ def test_cpp_interface(gpu_lib, tmp_path):
     prev = np.stack([k0["x"], k0["y"]], 1)
     nm, m12, _ = O.search_for_initialization(abi.frame_struct(k0, d0, 752, 480), abi.frame_struct(k1, d1, 752, 480),
                                              prev, 100, 0.9, True)
+    f0, f1 = abi.frame_struct(k0, d0, 752, 480), abi.frame_struct(k1, d1, 752, 480)
+    fv0, fv1 = abi.featvec_struct(np.arange(len(k0)) % 16), abi.featvec_struct(np.arange(len(k1)) % 16)
+    nb, b12 = O.search_by_bow_kf(f0, fv0, np.ones(len(k0), np.uint8), f1, fv1, np.ones(len(k1), np.uint8), 0.75,
+                                 True)
+    assert nb > 0
     assert out == [str(len(k0)), str(m0), fnv(k0.tobytes()), fnv(d0.tobytes()), str(len(k1)), str(m1), str(nm),
-                   fnv(m12.astype(np.int32).tobytes())]
+                   fnv(m12.astype(np.int32).tobytes()), str(nb), fnv(b12.astype(np.int32).tobytes())]
