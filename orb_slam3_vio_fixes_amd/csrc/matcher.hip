@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -560,74 +561,140 @@ struct BowArgs {
     const uint32_t* f_node;  const int* f_off;  const uint32_t* f_idx;  int f_nnodes;
     float ratio;
     int check_ori;
-    int32_t* match;      // [pair][f_n]
-    int32_t* nmatches;   // [pair]
+    int npairs;
+    int32_t* match;      // [pair][f_n]  (-1 before k_bow_nodes)
+    int32_t* nmatches;   // [pair]       (0 before k_bow_nodes)
+    int8_t* fbin;        // [pair][f_n]  rotation bin of the match of F feature, -1 = none
+    int* hist;           // [pair][32]   (0 before k_bow_nodes)
     const uint8_t* f_valid;   // KF-KF form: pKF2 MapPoint != NULL && !isBad(), else NULL
     int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
 };
 
-__global__ __launch_bounds__(64) void k_bow(BowArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];
-    const int pr = blockIdx.x, lane = lane_id();
-    int* hist = lds;                          // 32
-    int* match = lds + 32;                    // f_n: KF feature matched to each F feature (vpMapPointMatches)
-    int8_t* fbin = (int8_t*)(match + a.f_n);  // f_n: rotation bin recorded for F feature, or -1
-    for (int i = lane; i < a.f_n; i += kWave) { match[i] = -1; fbin[i] = -1; }
-    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
-    __syncthreads();
-    const long long kpo = a.kp_off[pr];
-    const orb_keypoint* KK = a.kf_kps + kpo;
-    const uint8_t* KD = a.kf_desc + kpo * 32;
-    const uint8_t* KV = a.kf_valid + kpo;
-    const long long no = a.node_off[pr];
-    const uint32_t* kn = a.kf_node + no;
-    const int* ko = a.kf_off + no + pr;
-    const uint32_t* ki = a.kf_idx + a.idx_off[pr];
-    const int knn = (int)(a.node_off[pr + 1] - no);
-    int nm = 0;
-    int ia = 0, ib = 0;
-    while (ia < knn && ib < a.f_nnodes) {
-        const uint32_t na = kn[ia], nb = a.f_node[ib];
-        if (na == nb) {
-            const int fb = a.f_off[ib], fe = a.f_off[ib + 1];
-            for (int p = ko[ia]; p < ko[ia + 1]; ++p) {
-                const int ikf = (int)ki[p];
-                if (!KV[ikf]) continue;
-                const uint4 q0 = *(const uint4*)(KD + (long long)ikf * 32);
-                const uint4 q1 = *(const uint4*)(KD + (long long)ikf * 32 + 16);
-                Best2 st{256, 256, -1, 0, 0};
-                for (int base = fb; base < fe; base += kWave) {
-                    const int q = base + lane;
-                    int d = INT_MAX, fi = -1;
+// One wave per KF FeatureVector node (all pairs flattened, grid-stride): the
+// reference's merge-join (:239-402) visits each node both FeatureVectors hold
+// exactly once, and a node's matching reads and writes only that node's
+// features, so nodes are independent.  Inside the node the KF features run in
+// order; the F features sit on the lanes (chunk c, lane l) with their
+// "already matched" flags in a per-lane bit mask (chunks >= 64 of a node with
+// more than 4096 frame features read the flag from `match` itself: only this
+// wave touches the node's features).
+constexpr int kBowMaskChunks = 64;
+
+__global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
+    const int lane = lane_id();
+    const long long total = a.node_off[a.npairs];
+    for (long long g = (long long)blockIdx.x * 4 + wave_id(); g < total; g += (long long)gridDim.x * 4) {
+        int lo = 0, hi = a.npairs;                       // pair: last pr with node_off[pr] <= g
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (a.node_off[mid] <= g) lo = mid;
+            else hi = mid;
+        }
+        const int pr = lo;
+        const int ia = (int)(g - a.node_off[pr]);
+        const uint32_t na = a.kf_node[g];
+        int fl = 0, fh = a.f_nnodes;                     // lower_bound of na in F's node ids
+        while (fl < fh) {
+            const int mid = (fl + fh) >> 1;
+            if (a.f_node[mid] < na) fl = mid + 1;
+            else fh = mid;
+        }
+        if (fl >= a.f_nnodes || a.f_node[fl] != na) continue;
+        const long long kpo = a.kp_off[pr];
+        const orb_keypoint* KK = a.kf_kps + kpo;
+        const uint8_t* KD = a.kf_desc + kpo * 32;
+        const uint8_t* KV = a.kf_valid + kpo;
+        const int* ko = a.kf_off + a.node_off[pr] + pr;
+        const uint32_t* ki = a.kf_idx + a.idx_off[pr];
+        const int fb = a.f_off[fl], fe = a.f_off[fl + 1];
+        const int nch = (fe - fb + kWave - 1) / kWave;
+        int32_t* match = a.match + (long long)pr * a.f_n;
+        // chunk 0 of the node's F features stays in registers across the KF features
+        uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
+        int fi0 = -1;
+        uint64_t taken = 0;                              // bit c: (chunk c, this lane) is matched / invalid
+        for (int c = 0; c < nch; ++c) {
+            const int q = fb + c * kWave + lane;
+            if (c >= kBowMaskChunks) break;
+            if (q < fe) {
+                const int fi = (int)a.f_idx[q];
+                if (a.f_valid && !a.f_valid[fi]) taken |= 1ull << c;
+                if (c == 0) {
+                    fi0 = fi;
+                    f0 = *(const uint4*)(a.f_desc + (long long)fi * 32);
+                    f1 = *(const uint4*)(a.f_desc + (long long)fi * 32 + 16);
+                }
+            } else {
+                taken |= 1ull << c;
+            }
+        }
+        int nm = 0;
+        for (int p = ko[ia]; p < ko[ia + 1]; ++p) {
+            const int ikf = (int)ki[p];
+            if (!KV[ikf]) continue;
+            const uint4 q0 = *(const uint4*)(KD + (long long)ikf * 32);
+            const uint4 q1 = *(const uint4*)(KD + (long long)ikf * 32 + 16);
+            Best2 st{256, 256, -1, 0, 0};
+            for (int c = 0; c < nch; ++c) {
+                int d = INT_MAX;
+                if (c < kBowMaskChunks) {
+                    if (!((taken >> c) & 1)) {
+                        if (c == 0) {
+                            d = __popc(q0.x ^ f0.x) + __popc(q0.y ^ f0.y) + __popc(q0.z ^ f0.z) +
+                                __popc(q0.w ^ f0.w) + __popc(q1.x ^ f1.x) + __popc(q1.y ^ f1.y) +
+                                __popc(q1.z ^ f1.z) + __popc(q1.w ^ f1.w);
+                        } else {
+                            const int fi = (int)a.f_idx[fb + c * kWave + lane];
+                            d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
+                        }
+                    }
+                } else {
+                    const int q = fb + c * kWave + lane;
                     if (q < fe) {
-                        fi = (int)a.f_idx[q];
+                        const int fi = (int)a.f_idx[q];
                         if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
                             d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
                     }
-                    merge_chunk(st, d, fi, 0);
                 }
-                const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;
-                if (low && (float)st.best < a.ratio * (float)st.best2) {
-                    if (lane == 0) match[st.idx] = ikf;
+                merge_chunk(st, d, c * kWave + lane, 0);
+            }
+            const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;     // :848 / :327
+            if (low && (float)st.best < a.ratio * (float)st.best2) {
+                const int pos = st.idx;                  // position in the node's F list
+                if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
+                const int fi = (pos < kWave) ? __shfl(fi0, pos, kWave) : (int)a.f_idx[fb + pos];
+                if (lane == 0) {
+                    match[fi] = ikf;
                     if (a.check_ori) {
-                        const int bn = rot_bin(KK[ikf].angle, a.f_kps[st.idx].angle);
-                        if (lane == 0) { hist[bn]++; fbin[st.idx] = (int8_t)bn; }
+                        const int bn = rot_bin(KK[ikf].angle, a.f_kps[fi].angle);
+                        atomicAdd(&a.hist[pr * 32 + bn], 1);
+                        a.fbin[(long long)pr * a.f_n + fi] = (int8_t)bn;
                     }
-                    ++nm;
-                    wave_sync_m();
+                }
+                ++nm;
+                if (nch > kBowMaskChunks) {              // the flag lives in `match` (global memory)
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
             }
-            ++ia; ++ib;
-        } else if (na < nb) {
-            while (ia < knn && kn[ia] < nb) ++ia;      // lower_bound
-        } else {
-            while (ib < a.f_nnodes && a.f_node[ib] < na) ++ib;
         }
+        if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
     }
-    __syncthreads();
+}
+
+// Rotation-consistency filter (:404-422 / :884-902) and the KF-KF output, one
+// wave per pair.
+__global__ __launch_bounds__(64) void k_bow_final(BowArgs a) {
+    const int pr = blockIdx.x, lane = lane_id();
+    int32_t* match = a.match + (long long)pr * a.f_n;
     if (a.check_ori) {
+        __shared__ int hist[32];
+        if (lane < 32) hist[lane] = a.hist[pr * 32 + lane];
+        __syncthreads();
         int i1, i2, i3;
         three_maxima(hist, i1, i2, i3);
+        const int8_t* fbin = a.fbin + (long long)pr * a.f_n;
         int drop = 0;
         for (int i = lane; i < a.f_n; i += kWave) {
             const int b = fbin[i];
@@ -635,12 +702,12 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
             match[i] = -1;
             ++drop;
         }
-        nm -= wave_sum(drop);
+        drop = wave_sum(drop);
+        if (lane == 0) a.nmatches[pr] -= drop;
     }
-    __syncthreads();
-    int32_t* out = a.match + (long long)pr * a.f_n;
-    for (int i = lane; i < a.f_n; i += kWave) out[i] = match[i];
     if (a.out12) {
+        __syncthreads();
+        const long long kpo = a.kp_off[pr];
         const int kn1 = (int)(a.kp_off[pr + 1] - kpo);
         int32_t* o12 = a.out12 + kpo;
         for (int i = lane; i < kn1; i += kWave) o12[i] = -1;
@@ -648,13 +715,38 @@ __global__ __launch_bounds__(64) void k_bow(BowArgs a) {
         for (int i = lane; i < a.f_n; i += kWave)
             if (match[i] >= 0) o12[match[i]] = i;
     }
-    if (lane == 0) a.nmatches[pr] = nm;
 }
 
+// Scratch for the BoW kernels (grows, per host thread).
+struct BowScratch {
+    int8_t* fbin = nullptr; size_t fbin_n = 0;
+    int* hist = nullptr; size_t hist_n = 0;
+    ~BowScratch() { if (fbin) (void)hipFree(fbin); if (hist) (void)hipFree(hist); }
+};
+
 static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
-    const size_t lds = 128 + (size_t)a.f_n * 5 + 16;
-    if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(k_bow, dim3(npairs), dim3(64), lds, st, a);
+    static thread_local BowScratch sc;
+    const size_t nf = (size_t)npairs * std::max(1, a.f_n), nh = (size_t)npairs * 32;
+    if (sc.fbin_n < nf) {
+        if (sc.fbin) (void)hipFree(sc.fbin);
+        sc.fbin = nullptr; sc.fbin_n = 0;
+        if (hipMalloc(&sc.fbin, nf) != hipSuccess) return ORB_ERR_DEVICE;
+        sc.fbin_n = nf;
+    }
+    if (sc.hist_n < nh) {
+        if (sc.hist) (void)hipFree(sc.hist);
+        sc.hist = nullptr; sc.hist_n = 0;
+        if (hipMalloc(&sc.hist, nh * sizeof(int)) != hipSuccess) return ORB_ERR_DEVICE;
+        sc.hist_n = nh;
+    }
+    a.npairs = npairs; a.fbin = sc.fbin; a.hist = sc.hist;
+    ORB_CHECK(hipMemsetAsync(a.match, 0xff, (size_t)npairs * a.f_n * sizeof(int32_t), st));
+    ORB_CHECK(hipMemsetAsync(a.fbin, 0xff, (size_t)npairs * a.f_n, st));
+    ORB_CHECK(hipMemsetAsync(a.hist, 0, nh * sizeof(int), st));
+    ORB_CHECK(hipMemsetAsync(a.nmatches, 0, (size_t)npairs * sizeof(int32_t), st));
+    const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, (long long)npairs * 32));
+    hipLaunchKernelGGL(k_bow_nodes, dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
@@ -693,6 +785,108 @@ struct ProjArgs {
     int32_t* nmatches;
 };
 
+// The query's search window: radius, level range and cell range; false = no
+// candidate list (invalid, far point, or an empty cell range).
+struct ProjQuery { float x, y, r; int minL, maxL; CellRange cr; };
+
+__device__ __forceinline__ bool proj_query(const ProjArgs& a, int i, ProjQuery& q) {
+    if (!a.qvalid[i]) return false;
+    q.x = a.qx[i]; q.y = a.qy[i];
+    if (a.mode == 0) {
+        if (a.far_points && a.qdepth[i] > a.th_far) return false;
+        const int lvl = a.qlevel[i];
+        float r = a.qviewcos[i] > 0.998f ? 2.5f : 4.0f;      // RadiusByViewingCos
+        if (a.th != 1.0f) r *= a.th;
+        q.r = r * a.scale[lvl];
+        q.minL = lvl - 1; q.maxL = lvl;
+    } else {
+        const int oct = a.qlevel[i];
+        q.r = a.th * a.scale[oct];
+        if (a.last_mode == 1) { q.minL = oct; q.maxL = -1; }
+        else if (a.last_mode == 2) { q.minL = 0; q.maxL = oct; }
+        else if (a.last_mode == 3) { q.minL = oct - 1; q.maxL = oct; }
+        else { q.minL = oct - 1; q.maxL = oct + 1; }
+    }
+    return cell_range(q.x, q.y, q.r, a.g, q.cr);
+}
+
+// Static candidate test (window, level range, stereo gate) of feature fi.
+__device__ __forceinline__ bool proj_static(const ProjArgs& a, int i, const ProjQuery& q, int fi, int& lv) {
+    const orb_keypoint k = a.kps[fi];
+    lv = k.octave;
+    if ((q.minL > 0) || (q.maxL >= 0)) {
+        if (k.octave < q.minL) return false;
+        if (q.maxL >= 0 && k.octave > q.maxL) return false;
+    }
+    if (!(fabsf(k.x - q.x) < q.r && fabsf(k.y - q.y) < q.r)) return false;
+    if (a.u_right && a.u_right[fi] > 0 && fabsf(a.qxr[i] - a.u_right[fi]) > q.r) return false;
+    return true;
+}
+
+// The slot holds a MapPoint the search must skip (:88-90, :1747-1749, :504, :1952).
+__device__ __forceinline__ bool proj_blocked(const ProjArgs& a, const int* owner, int fi) {
+    const int o = owner[fi];
+    if (o == -1) return false;
+    if (a.skip_any) return true;
+    return o <= -2 ? a.blocked[fi] != 0 : a.qhas_obs[o] != 0;
+}
+
+// Exact scan of query i's whole candidate list under the current slot state.
+__device__ Best2 proj_scan(const ProjArgs& a, int i, const ProjQuery& q, const int* cs, const int* owner) {
+    const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
+    const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+    const AreaRuns ar = area_runs(cs, q.cr);
+    Best2 st{256, 256, -1, -1, -1};
+    for (int base = 0; base < ar.total; base += kWave) {
+        const int t = base + lane_id();
+        const int j = area_pos(ar, min(t, ar.total - 1));
+        int d = INT_MAX, fi = -1, lv = -1;
+        if (t < ar.total) {
+            fi = (int)(a.gsorted[j] & 0xffff);
+            if (proj_static(a, i, q, fi, lv) && !proj_blocked(a, owner, fi))
+                d = hamming32(q0, q1, a.desc + (long long)fi * 32);
+        }
+        merge_chunk(st, d, fi, lv);
+    }
+    return st;
+}
+
+// Acceptance (mode 0: :123-139; mode 1: :1770, :1966, :523).
+__device__ __forceinline__ bool proj_accept(const ProjArgs& a, const Best2& st) {
+    if (a.mode == 0) return st.best <= kThHigh && !(st.lvl == st.lvl2 && (float)st.best > a.ratio * (float)st.best2);
+    return st.idx >= 0 && (float)st.best <= a.accept;
+}
+
+__device__ __forceinline__ void proj_claim(const ProjArgs& a, const Best2& st, int i, int* owner, int* hist, int* hent,
+                                           int& nm, int& nh) {
+    if (lane_id() == 0) owner[st.idx] = i;
+    ++nm;
+    if (a.mode == 1 && a.check_ori) {
+        const int bn = rot_bin(a.qangle[i], a.kps[st.idx].angle);
+        if (lane_id() == 0) { hist[bn]++; hent[nh] = (bn << 16) | st.idx; }
+        ++nh;
+    }
+}
+
+// Rotation filter of the mode-1 searches: entries in push order; every entry
+// in a rejected bin clears its slot and decrements (:1864-1884, :1988-2007).
+__device__ __forceinline__ void proj_rot_filter(const ProjArgs& a, const int* hist, const int* hent, int nh,
+                                                int* owner, int& nm) {
+    int i1, i2, i3;
+    three_maxima(hist, i1, i2, i3);
+    __syncthreads();
+    int drop = 0;
+    for (int e = lane_id(); e < nh; e += kWave) {
+        const int bn = hent[e] >> 16;
+        if (bn == i1 || bn == i2 || bn == i3) continue;
+        owner[hent[e] & 0xffff] = -1;
+        ++drop;
+    }
+    nm -= wave_sum(drop);
+}
+
+// Single-wave form (slot state in global memory): the fallback when the slot
+// table or the query list does not fit in LDS.
 __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int lane = lane_id();
@@ -704,96 +898,156 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
     __syncthreads();
     int nm = 0, nh = 0;
     for (int i = 0; i < a.nq; ++i) {
-        if (!a.qvalid[i]) continue;
-        float r, x = a.qx[i], y = a.qy[i];
-        int minL, maxL;
-        if (a.mode == 0) {
-            if (a.far_points && a.qdepth[i] > a.th_far) continue;
-            const int lvl = a.qlevel[i];
-            r = a.qviewcos[i] > 0.998f ? 2.5f : 4.0f;      // RadiusByViewingCos
-            if (a.th != 1.0f) r *= a.th;
-            r = r * a.scale[lvl];
-            minL = lvl - 1; maxL = lvl;
-        } else {
-            const int oct = a.qlevel[i];
-            r = a.th * a.scale[oct];
-            if (a.last_mode == 1) { minL = oct; maxL = -1; }
-            else if (a.last_mode == 2) { minL = 0; maxL = oct; }
-            else if (a.last_mode == 3) { minL = oct - 1; maxL = oct; }
-            else { minL = oct - 1; maxL = oct + 1; }
-        }
-        CellRange cr;
-        if (!cell_range(x, y, r, a.g, cr)) continue;
-        const bool checkL = (minL > 0) || (maxL >= 0);
-        const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
-        const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
-        const AreaRuns ar = area_runs(cs, cr);
-        Best2 st{256, 256, -1, -1, -1};
-        for (int base = 0; base < ar.total; base += kWave) {
-            const int t = base + lane;
-            const int j = area_pos(ar, min(t, ar.total - 1));
-            int d = INT_MAX, fi = -1, lv = -1;
-            if (t < ar.total) {
-                fi = (int)(a.gsorted[j] & 0xffff);
-                const orb_keypoint k = a.kps[fi];
-                bool ok = true;
-                if (checkL) {
-                    if (k.octave < minL) ok = false;
-                    if (maxL >= 0 && k.octave > maxL) ok = false;
-                }
-                if (ok && fabsf(k.x - x) < r && fabsf(k.y - y) < r) {
-                    const int o = a.owner[fi];
-                    const bool blk = o == -1 ? false
-                                   : (a.skip_any ? true : (o <= -2 ? a.blocked[fi] != 0 : a.qhas_obs[o] != 0));
-                    bool pass = !blk;
-                    if (pass && a.u_right && a.u_right[fi] > 0) {
-                        const float er = fabsf(a.qxr[i] - a.u_right[fi]);
-                        if (er > r) pass = false;
-                    }
-                    if (pass) { d = hamming32(q0, q1, a.desc + (long long)fi * 32); lv = k.octave; }
-                }
-            }
-            merge_chunk(st, d, fi, lv);
-        }
-        if (a.mode == 0) {
-            if (st.best <= kThHigh) {
-                if (st.lvl == st.lvl2 && (float)st.best > a.ratio * (float)st.best2) continue;
-                if (st.lvl != st.lvl2 || (float)st.best <= a.ratio * (float)st.best2) {
-                    if (lane == 0) a.owner[st.idx] = i;
-                    ++nm;
-                }
-            }
-        } else {
-            if (st.idx >= 0 && (float)st.best <= a.accept) {
-                if (lane == 0) a.owner[st.idx] = i;
-                ++nm;
-                if (a.check_ori) {
-                    const int bn = rot_bin(a.qangle[i], a.kps[st.idx].angle);
-                    if (lane == 0) { hist[bn]++; hent[nh] = (bn << 16) | st.idx; }
-                    ++nh;
-                }
-            }
-        }
+        ProjQuery q;
+        if (!proj_query(a, i, q)) continue;
+        const Best2 st = proj_scan(a, i, q, cs, a.owner);
+        if (proj_accept(a, st)) proj_claim(a, st, i, a.owner, hist, hent, nm, nh);
         __syncthreads();
     }
-    if (a.mode == 1 && a.check_ori) {
-        int i1, i2, i3;
-        three_maxima(hist, i1, i2, i3);
-        __syncthreads();
-        // entries in push order: every entry in a rejected bin clears its slot and decrements
-        int drop = 0;
-        for (int e = lane; e < nh; e += kWave) {
-            const int bn = hent[e] >> 16;
-            if (bn == i1 || bn == i2 || bn == i3) continue;
-            a.owner[hent[e] & 0xffff] = -1;
-            ++drop;
-        }
-        nm -= wave_sum(drop);
-    }
+    if (a.mode == 1 && a.check_ori) proj_rot_filter(a, hist, hent, nh, a.owner, nm);
     if (lane == 0) a.nmatches[0] = nm;
 }
 
 static size_t proj_lds(int nq) { return (size_t)(32 + kCells + 1 + nq + 1) * 4 + 64; }
+
+// ---- two-phase form ------------------------------------------------------
+// Phase 1 (k_proj_topk, every query in parallel, one wave each): the static
+// candidates whose distance can still decide the outcome (d <= bound: mode 1
+// bestDist <= accept; mode 0 the best <= TH_HIGH, and a second best only
+// while ratio * d < TH_HIGH can fail the ratio test), and the kProjK smallest
+// of them in (distance, candidate order), packed d << 24 | level << 16 | slot;
+// cnt = how many there are (-1: no list).  Phase 2 (k_proj_resolve, one
+// wave): queries in reference order against the slot state in LDS; the first
+// (and second) unblocked entries of the list ARE the reference's best (and
+// second best) because every unlisted candidate sorts after them; when a
+// truncated list runs dry the wave rescans the query exactly.
+constexpr int kProjK = 8;
+
+__global__ __launch_bounds__(256) void k_proj_topk(ProjArgs a, int bound, uint32_t* __restrict__ topk,
+                                                   int* __restrict__ cnt) {
+    const int i = blockIdx.x * 4 + wave_id(), lane = lane_id();
+    if (i >= a.nq) return;
+    ProjQuery q;
+    if (!proj_query(a, i, q)) {
+        if (lane == 0) cnt[i] = -1;
+        return;
+    }
+    const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
+    const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+    const AreaRuns ar = area_runs(a.cellstart, q.cr);
+    int run = INT_MAX;                        // lanes < kProjK: running list, sort key (d << 16 | order)
+    uint32_t run_e = 0xffffffffu;             //                 and its packed entry
+    int total = 0;
+    for (int base = 0; base < ar.total; base += kWave) {
+        const int t = base + lane;
+        const int j = area_pos(ar, min(t, ar.total - 1));
+        int key = INT_MAX;
+        uint32_t ent = 0xffffffffu;
+        if (t < ar.total) {
+            const int fi = (int)(a.gsorted[j] & 0xffff);
+            int lv;
+            if (proj_static(a, i, q, fi, lv)) {
+                const int d = hamming32(q0, q1, a.desc + (long long)fi * 32);
+                if (d <= bound) {
+                    key = (d << 16) | t;
+                    ent = ((uint32_t)d << 24) | ((uint32_t)(lv & 0xff) << 16) | (uint32_t)fi;
+                }
+            }
+        }
+        total += __popcll(__ballot(key != INT_MAX));
+        // kProjK smallest of (running list) U (this chunk); keys are distinct
+        int prev = -1, nrun = INT_MAX;
+        uint32_t nrun_e = 0xffffffffu;
+        for (int r = 0; r < kProjK; ++r) {
+            const int xa = key > prev ? key : INT_MAX;
+            const int xb = (lane < kProjK && run > prev) ? run : INT_MAX;
+            const int x = min(xa, xb);
+            const uint32_t xe = xa <= xb ? ent : run_e;
+            int m = x;
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, kWave));
+            if (m == INT_MAX) break;
+            const int src = __ffsll((long long)__ballot(x == m)) - 1;
+            const uint32_t me = (uint32_t)__shfl((int)xe, src, kWave);
+            if (lane == r) { nrun = m; nrun_e = me; }
+            prev = m;
+        }
+        run = nrun; run_e = nrun_e;
+    }
+    if (lane < kProjK) topk[(long long)i * kProjK + lane] = run_e;
+    if (lane == 0) cnt[i] = total;
+}
+
+__global__ __launch_bounds__(64) void k_proj_resolve(ProjArgs a, const uint32_t* __restrict__ topk,
+                                                     const int* __restrict__ cnt) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int lane = lane_id();
+    int* hist = lds;                          // 32
+    int* cs = lds + 32;                       // kCells + 1
+    int* own = cs + kCells + 1;               // n: slot state
+    int* hent = own + a.n;                    // nq
+    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
+    for (int i = lane; i <= kCells; i += kWave) cs[i] = a.cellstart[i];
+    for (int i = lane; i < a.n; i += kWave) own[i] = a.owner[i];
+    __syncthreads();
+    int nm = 0, nh = 0;
+    constexpr int kQ = kWave / kProjK;        // queries per load
+    for (int base = 0; base < a.nq; base += kQ) {
+        const int qi = base + lane / kProjK, k = lane % kProjK;
+        int c = -1;
+        uint32_t e = 0xffffffffu;
+        if (qi < a.nq) {
+            c = cnt[qi];
+            if (k < min(c, kProjK)) e = topk[(long long)qi * kProjK + k];
+        }
+        const int nj = min(kQ, a.nq - base);
+        for (int jq = 0; jq < nj; ++jq) {
+            const int i = base + jq;
+            const int ci = __shfl(c, jq * kProjK, kWave);
+            if (ci <= 0) continue;
+            const uint32_t ej = (uint32_t)__shfl((int)e, jq * kProjK + (lane % kProjK), kWave);
+            const bool fr = lane < min(ci, kProjK) && !proj_blocked(a, own, (int)(ej & 0xffff));
+            const uint64_t fm = __ballot(fr);
+            Best2 st{256, 256, -1, -1, -1};
+            bool exact = true;
+            if (fm) {
+                const uint32_t e1 = (uint32_t)__shfl((int)ej, __ffsll((long long)fm) - 1, kWave);
+                st.best = (int)(e1 >> 24); st.lvl = (int)((e1 >> 16) & 0xff); st.idx = (int)(e1 & 0xffff);
+                const uint64_t fm2 = fm & (fm - 1);
+                if (fm2) {
+                    const uint32_t e2 = (uint32_t)__shfl((int)ej, __ffsll((long long)fm2) - 1, kWave);
+                    st.best2 = (int)(e2 >> 24); st.lvl2 = (int)((e2 >> 16) & 0xff);
+                } else if (a.mode == 0 && ci > kProjK) {
+                    exact = false;
+                }
+            } else if (ci > kProjK) {
+                exact = false;
+            }
+            if (!exact) {
+                ProjQuery q;
+                proj_query(a, i, q);
+                st = proj_scan(a, i, q, cs, own);
+            }
+            if (proj_accept(a, st)) proj_claim(a, st, i, own, hist, hent, nm, nh);
+            wave_sync_m();
+        }
+    }
+    if (a.mode == 1 && a.check_ori) proj_rot_filter(a, hist, hent, nh, own, nm);
+    __syncthreads();
+    for (int i = lane; i < a.n; i += kWave) a.owner[i] = own[i];
+    if (lane == 0) a.nmatches[0] = nm;
+}
+
+static size_t proj_resolve_lds(int n, int nq) { return (size_t)(32 + kCells + 1 + n + nq + 1) * 4 + 64; }
+
+// Largest distance that can still decide a query (see k_proj_topk).
+static int proj_bound(const ProjArgs& a) {
+    if (a.mode == 1) return a.accept < 0 ? -1 : (int)std::min(255.0f, std::floor(a.accept));
+    int b = kThHigh;
+    for (int d = kThHigh + 1; d <= 255; ++d)
+        if (a.ratio <= 0.0f || a.ratio * (float)d < (float)kThHigh) b = d;
+    return b;
+}
 
 // ---------------------------------------------------------------------------
 // k_transform: TemplatedVocabulary::transform per descriptor
@@ -1322,9 +1576,20 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
     a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p;
     a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
-    const size_t lds = proj_lds(a.nq);
-    if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(k_proj, dim3(1), dim3(64), lds, 0, a);
+    // two-phase form unless its LDS slot table does not fit (or the single-wave
+    // form is forced for testing: ORBM_PROJ_SINGLE_WAVE=1)
+    const char* force = std::getenv("ORBM_PROJ_SINGLE_WAVE");
+    const size_t lds2 = proj_resolve_lds(a.n, a.nq);
+    if (lds2 <= 160 * 1024 && !(force && force[0] == '1')) {
+        DBuf<uint32_t> topk; DBuf<int> cnt;
+        if ((rc = topk.alloc((size_t)std::max(1, a.nq) * kProjK)) || (rc = cnt.alloc(std::max(1, a.nq)))) return rc;
+        if (a.nq) hipLaunchKernelGGL(k_proj_topk, dim3((a.nq + 3) / 4), dim3(256), 0, 0, a, proj_bound(a), topk.p, cnt.p);
+        hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);
+    } else {
+        const size_t lds = proj_lds(a.nq);
+        if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
+        hipLaunchKernelGGL(k_proj, dim3(1), dim3(64), lds, 0, a);
+    }
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
     ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));

@@ -90,8 +90,10 @@ def projection_queries(frames, seed, n=600):
     return rng, src, cur, k, qx.astype(np.float32), qy.astype(np.float32)
 
 
+@pytest.mark.parametrize("single", [False, True])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
-def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far):
+def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, monkeypatch):
+    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single else "0")
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
@@ -112,8 +114,10 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far):
     np.testing.assert_array_equal(own, rown)
 
 
+@pytest.mark.parametrize("single", [False, True])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
-def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori):
+def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, monkeypatch):
+    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single else "0")
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     valid = (rng.random(n) < 0.9).astype(np.uint8)
