@@ -115,6 +115,75 @@ __global__ __launch_bounds__(256) void k_grid(const orb_keypoint* __restrict__ k
     }
 }
 
+// k_grid_cs: the same grid order by a counting sort, one frame per block:
+// per-cell counts (LDS atomics), their exclusive scan (= the cell-start table
+// of k_cell_start below), atomic placement, then an insertion sort of each
+// cell's few entries restores index order inside the cell.  cellstart may be
+// NULL; l0sorted / l0count as in k_grid.
+constexpr int kGridCells = 64 * 48;
+
+static size_t grid_cs_lds(int cap) { return (size_t)(2 * kGridCells + 1) * 4 + (size_t)cap * 6 + 64; }
+
+__global__ __launch_bounds__(256) void k_grid_cs(const orb_keypoint* __restrict__ kps, const int* __restrict__ n,
+                                                 int cap, GridParams g, uint32_t* __restrict__ sorted,
+                                                 int* __restrict__ count, int* __restrict__ cellstart,
+                                                 uint32_t* __restrict__ l0sorted, int* __restrict__ l0count) {
+    extern __shared__ __attribute__((aligned(16))) int glds[];
+    __shared__ int tmp[8];
+    int* start = glds;                                   // kGridCells + 1
+    int* cursor = start + kGridCells + 1;                // kGridCells
+    uint32_t* out = (uint32_t*)(cursor + kGridCells);    // cap
+    short* cellof = (short*)(out + cap);                 // cap
+    const int f = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
+    const int nf = min(n[f], cap);
+    const orb_keypoint* K = kps + (long long)f * cap;
+    for (int c = tid; c < kGridCells; c += T) start[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < nf; i += T) {
+        const int c = grid_cell(K[i], g);
+        cellof[i] = (short)c;
+        if (c >= 0) atomicAdd(&start[c], 1);
+    }
+    __syncthreads();
+    const int total = block_excl_scan(start, kGridCells, tmp);
+    if (tid == 0) start[kGridCells] = total;
+    for (int c = tid; c < kGridCells; c += T) cursor[c] = start[c];
+    __syncthreads();
+    for (int i = tid; i < nf; i += T) {
+        const int c = cellof[i];
+        if (c >= 0) out[atomicAdd(&cursor[c], 1)] = ((uint32_t)c << 16) | (uint32_t)i;
+    }
+    __syncthreads();
+    for (int c = tid; c < kGridCells; c += T) {          // index order inside each cell
+        const int b = start[c], e = start[c + 1];
+        for (int x = b + 1; x < e; ++x) {
+            const uint32_t v = out[x];
+            int y = x - 1;
+            while (y >= b && out[y] > v) { out[y + 1] = out[y]; --y; }
+            out[y + 1] = v;
+        }
+    }
+    __syncthreads();
+    for (int j = tid; j < total; j += T) sorted[(long long)f * cap + j] = out[j];
+    if (tid == 0) count[f] = total;
+    if (cellstart)
+        for (int c = tid; c <= kGridCells; c += T) cellstart[(long long)f * (kGridCells + 1) + c] = start[c];
+    // the octave-0 subsequence (SearchForInitialization queries level 0 only, ORBmatcher.cc:664-668)
+    if (l0sorted && wave_id() == 0) {
+        int nl = 0;
+        for (int base = 0; base < total; base += kWave) {
+            const int i = base + lane_id();
+            bool keep = false;
+            uint32_t v = 0;
+            if (i < total) { v = out[i]; keep = K[v & 0xffff].octave == 0; }
+            const uint64_t m = __ballot(keep);
+            if (keep) l0sorted[(long long)f * cap + nl + mask_rank(m)] = v;
+            nl += __popcll(m);
+        }
+        if (lane_id() == 0) l0count[f] = nl;
+    }
+}
+
 // GetFeaturesInArea cell range (Frame.cc:661-689); false = empty.
 struct CellRange { int x0, x1, y0, y1; };
 __device__ __forceinline__ bool cell_range(float x, float y, float r, const GridParams& g, CellRange& cr) {
@@ -915,7 +984,8 @@ static size_t proj_lds(int nq) { return (size_t)(32 + kCells + 1 + nq + 1) * 4 +
 // candidates whose distance can still decide the outcome (d <= bound: mode 1
 // bestDist <= accept; mode 0 the best <= TH_HIGH, and a second best only
 // while ratio * d < TH_HIGH can fail the ratio test), and the kProjK smallest
-// of them in (distance, candidate order), packed d << 24 | level << 16 | slot;
+// of them in (distance, candidate order), packed
+//   x = d << 24 | level << 16 | slot,  y = rotation bin of (query, slot);
 // cnt = how many there are (-1: no list).  Phase 2 (k_proj_resolve, one
 // wave): queries in reference order against the slot state in LDS; the first
 // (and second) unblocked entries of the list ARE the reference's best (and
@@ -923,7 +993,7 @@ static size_t proj_lds(int nq) { return (size_t)(32 + kCells + 1 + nq + 1) * 4 +
 // truncated list runs dry the wave rescans the query exactly.
 constexpr int kProjK = 8;
 
-__global__ __launch_bounds__(256) void k_proj_topk(ProjArgs a, int bound, uint32_t* __restrict__ topk,
+__global__ __launch_bounds__(256) void k_proj_topk(ProjArgs a, int bound, uint2* __restrict__ topk,
                                                    int* __restrict__ cnt) {
     const int i = blockIdx.x * 4 + wave_id(), lane = lane_id();
     if (i >= a.nq) return;
@@ -934,6 +1004,7 @@ __global__ __launch_bounds__(256) void k_proj_topk(ProjArgs a, int bound, uint32
     }
     const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
     const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+    const float qang = (a.mode == 1 && a.check_ori) ? a.qangle[i] : 0.0f;
     const AreaRuns ar = area_runs(a.cellstart, q.cr);
     int run = INT_MAX;                        // lanes < kProjK: running list, sort key (d << 16 | order)
     uint32_t run_e = 0xffffffffu;             //                 and its packed entry
@@ -974,71 +1045,155 @@ __global__ __launch_bounds__(256) void k_proj_topk(ProjArgs a, int bound, uint32
         }
         run = nrun; run_e = nrun_e;
     }
-    if (lane < kProjK) topk[(long long)i * kProjK + lane] = run_e;
+    if (lane < kProjK) {
+        uint32_t bin = 0;
+        if (run_e != 0xffffffffu && a.mode == 1 && a.check_ori) bin = (uint32_t)rot_bin(qang, a.kps[run_e & 0xffff].angle);
+        topk[(long long)i * kProjK + lane] = make_uint2(run_e, bin);
+    }
     if (lane == 0) cnt[i] = total;
 }
 
-__global__ __launch_bounds__(64) void k_proj_resolve(ProjArgs a, const uint32_t* __restrict__ topk,
+// LDS layout of k_proj_resolve: hist[32] | own[n] | hent[nq] | bl[n] bytes
+// (slot blocked now) | has_obs[nq] bytes.
+static size_t proj_resolve_lds(int n, int nq) { return (size_t)(32 + n + nq + 1) * 4 + (size_t)n + nq + 64; }
+
+// Compiler-only ordering between one wave's LDS accesses: DS instructions of a
+// wave execute in order, so a later ds_read sees an earlier ds_write.
+__device__ __forceinline__ void lds_order() { __asm__ __volatile__("" ::: "memory"); }
+
+constexpr int kResQ = kWave / kProjK;             // queries per lane group load (8)
+constexpr int kResBlk = kResQ * 8;                // queries per prefetched block (64)
+
+// The lists of block `blk` (64 queries): lane (grp, k) holds entry k of query
+// blk*64 + u*8 + grp in slot u.  Loads are unconditional (in bounds) so the
+// whole block is in flight at once.
+__device__ __forceinline__ void res_load(const ProjArgs& a, const uint2* topk, const int* cnt, int blk,
+                                         uint2 (&E)[8], int (&C)[8], int (&HO)[8]) {
+    const int grp = lane_id() / kProjK, k = lane_id() % kProjK;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int qi = min(blk * kResBlk + u * kResQ + grp, a.nq - 1);
+        C[u] = cnt[qi];
+        E[u] = topk[(long long)qi * kProjK + k];
+        HO[u] = a.skip_any ? 1 : a.qhas_obs[qi];
+    }
+}
+
+__global__ __launch_bounds__(64) void k_proj_resolve(ProjArgs a, const uint2* __restrict__ topk,
                                                      const int* __restrict__ cnt) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int lane = lane_id();
-    int* hist = lds;                          // 32
-    int* cs = lds + 32;                       // kCells + 1
-    int* own = cs + kCells + 1;               // n: slot state
+    int* hist = lds;                          // 32 (final filter only; counted in registers)
+    int* own = lds + 32;                      // n: slot owner (-1 free, <= -2 pre-existing, >= 0 query)
     int* hent = own + a.n;                    // nq
-    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
-    for (int i = lane; i <= kCells; i += kWave) cs[i] = a.cellstart[i];
+    uint8_t* bl = (uint8_t*)(hent + a.nq + 1);    // n: slot is skipped by the search now
+    uint8_t* hob = bl + a.n;                      // nq
+    uint2 EA[8], EB[8];
+    int CA[8], CB[8], HA[8], HB[8];
+    const int nblk = (a.nq + kResBlk - 1) / kResBlk;
+    if (nblk) res_load(a, topk, cnt, 0, EA, CA, HA);     // in flight during the init
+#pragma unroll 8
     for (int i = lane; i < a.n; i += kWave) own[i] = a.owner[i];
-    __syncthreads();
-    int nm = 0, nh = 0;
-    constexpr int kQ = kWave / kProjK;        // queries per load
-    for (int base = 0; base < a.nq; base += kQ) {
-        const int qi = base + lane / kProjK, k = lane % kProjK;
-        int c = -1;
-        uint32_t e = 0xffffffffu;
-        if (qi < a.nq) {
-            c = cnt[qi];
-            if (k < min(c, kProjK)) e = topk[(long long)qi * kProjK + k];
-        }
-        const int nj = min(kQ, a.nq - base);
-        for (int jq = 0; jq < nj; ++jq) {
-            const int i = base + jq;
-            const int ci = __shfl(c, jq * kProjK, kWave);
-            if (ci <= 0) continue;
-            const uint32_t ej = (uint32_t)__shfl((int)e, jq * kProjK + (lane % kProjK), kWave);
-            const bool fr = lane < min(ci, kProjK) && !proj_blocked(a, own, (int)(ej & 0xffff));
-            const uint64_t fm = __ballot(fr);
-            Best2 st{256, 256, -1, -1, -1};
-            bool exact = true;
-            if (fm) {
-                const uint32_t e1 = (uint32_t)__shfl((int)ej, __ffsll((long long)fm) - 1, kWave);
-                st.best = (int)(e1 >> 24); st.lvl = (int)((e1 >> 16) & 0xff); st.idx = (int)(e1 & 0xffff);
-                const uint64_t fm2 = fm & (fm - 1);
-                if (fm2) {
-                    const uint32_t e2 = (uint32_t)__shfl((int)ej, __ffsll((long long)fm2) - 1, kWave);
-                    st.best2 = (int)(e2 >> 24); st.lvl2 = (int)((e2 >> 16) & 0xff);
-                } else if (a.mode == 0 && ci > kProjK) {
-                    exact = false;
-                }
-            } else if (ci > kProjK) {
-                exact = false;
-            }
-            if (!exact) {
-                ProjQuery q;
-                proj_query(a, i, q);
-                st = proj_scan(a, i, q, cs, own);
-            }
-            if (proj_accept(a, st)) proj_claim(a, st, i, own, hist, hent, nm, nh);
-            wave_sync_m();
+    if (a.skip_any) {
+#pragma unroll 8
+        for (int i = lane; i < a.n; i += kWave) bl[i] = own[i] != -1;
+    } else {
+#pragma unroll 8
+        for (int i = lane; i < a.nq; i += kWave) hob[i] = a.qhas_obs[i];
+#pragma unroll 8
+        for (int i = lane; i < a.n; i += kWave) {
+            const int o = own[i];
+            bl[i] = o == -1 ? 0 : (o <= -2 ? a.blocked[i] : a.qhas_obs[o]);
         }
     }
-    if (a.mode == 1 && a.check_ori) proj_rot_filter(a, hist, hent, nh, own, nm);
+    __syncthreads();
+    int nm = 0, nh = 0, hcount = 0;           // lane b < 30 counts rotation bin b
+    const int grp = lane / kProjK, k = lane % kProjK;
+    // the per-query decisions read these scalars only (SGPRs, no argument reloads)
+    const int mode = a.mode, skip_any = a.skip_any, ori = a.mode == 1 && a.check_ori, nq = a.nq;
+    const float ratio = a.ratio, accept = a.accept;
+    auto accept_st = [&](const Best2& st) {
+        if (mode == 0) return st.best <= kThHigh && !(st.lvl == st.lvl2 && (float)st.best > ratio * (float)st.best2);
+        return st.idx >= 0 && (float)st.best <= accept;
+    };
+    // Per group of 8 queries (always register slot 0; the slots shift after
+    // each group so ONE rolled copy of the body runs: a serial wave must not
+    // stream through unrolled code): one LDS read of every listed slot's
+    // blocked flag (lane (grp, k) = entry k of query grp), then the queries in
+    // order with the group's own claims tracked in registers -- a claim by
+    // query i blocks its slot for later queries iff skip_any or has_obs[i].
+    for (int blk = 0; blk < nblk; ++blk) {
+        if (blk + 1 < nblk) res_load(a, topk, cnt, blk + 1, EB, CB, HB);
+#pragma unroll 1
+        for (int u = 0; u < 8; ++u) {
+            const int base = blk * kResBlk + u * kResQ;
+            const int nj = min(kResQ, nq - base);
+            const uint2 e0 = EA[0];
+            const int c0 = CA[0], h0 = HA[0];
+#pragma unroll
+            for (int v = 0; v < 7; ++v) { EA[v] = EA[v + 1]; CA[v] = CA[v + 1]; HA[v] = HA[v + 1]; }
+            if (nj <= 0) continue;
+            const int slot = (int)(e0.x & 0xffff);
+            bool avail = k < min(c0, kProjK) && bl[slot] == 0;
+            for (int jq = 0; jq < nj; ++jq) {
+                const int i = base + jq;
+                const int ci = __builtin_amdgcn_readlane(c0, jq * kProjK);
+                if (ci <= 0) continue;
+                const uint64_t fm = __ballot(grp == jq && avail);
+                Best2 st{256, 256, -1, -1, -1};
+                int bin = 0;
+                bool exact = true;
+                if (fm) {
+                    const int l1 = __ffsll((long long)fm) - 1;
+                    const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)e0.x, l1);
+                    bin = __builtin_amdgcn_readlane((int)e0.y, l1);
+                    st.best = (int)(e1 >> 24); st.lvl = (int)((e1 >> 16) & 0xff); st.idx = (int)(e1 & 0xffff);
+                    const uint64_t fm2 = fm & (fm - 1);
+                    if (fm2) {
+                        const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)e0.x, __ffsll((long long)fm2) - 1);
+                        st.best2 = (int)(e2 >> 24); st.lvl2 = (int)((e2 >> 16) & 0xff);
+                    } else if (mode == 0 && ci > kProjK) {
+                        exact = false;
+                    }
+                } else if (ci > kProjK) {
+                    exact = false;
+                }
+                if (!exact) {                  // a truncated list ran dry: exact rescan
+                    ProjQuery q;
+                    proj_query(a, i, q);
+                    wave_sync_m();
+                    st = proj_scan(a, i, q, a.cellstart, own);
+                    if (st.idx >= 0 && ori) bin = rot_bin(a.qangle[i], a.kps[st.idx].angle);
+                }
+                if (accept_st(st)) {
+                    const int blocks = skip_any ? 1 : __builtin_amdgcn_readlane(h0, jq * kProjK);
+                    if (lane == 0) {
+                        own[st.idx] = i;
+                        bl[st.idx] = (uint8_t)blocks;
+                    }
+                    if (blocks) avail = avail && slot != st.idx;
+                    ++nm;
+                    if (ori) {
+                        if (lane == 0) hent[nh] = (bin << 16) | st.idx;
+                        hcount += lane == bin;
+                        ++nh;
+                    }
+                    lds_order();
+                }
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < 8; ++v) { EA[v] = EB[v]; CA[v] = CB[v]; HA[v] = HB[v]; }
+    }
+    if (a.mode == 1 && a.check_ori) {
+        if (lane < 32) hist[lane] = hcount;
+        __syncthreads();
+        proj_rot_filter(a, hist, hent, nh, own, nm);
+    }
     __syncthreads();
     for (int i = lane; i < a.n; i += kWave) a.owner[i] = own[i];
     if (lane == 0) a.nmatches[0] = nm;
 }
-
-static size_t proj_resolve_lds(int n, int nq) { return (size_t)(32 + kCells + 1 + n + nq + 1) * 4 + 64; }
 
 // Largest distance that can still decide a query (see k_proj_topk).
 static int proj_bound(const ProjArgs& a) {
@@ -1359,8 +1514,96 @@ __global__ __launch_bounds__(64) void k_distinctive(int npoints, const int32_t* 
 // ---------------------------------------------------------------------------
 // host helpers
 // ---------------------------------------------------------------------------
+// Per-host-thread bump arenas for the synchronous host APIs: device memory
+// and pinned staging, reset at the start of every call (the previous call has
+// completed: each ends with a synchronous download).  A call that outgrows
+// the arena takes an extra chunk; the next reset coalesces the chunks into
+// one, so steady-state calls never allocate.  Arenas live until process exit
+// (no destructors: the HIP runtime may already be gone at thread teardown).
+struct Arena {
+    bool pinned = false;
+    std::vector<std::pair<char*, size_t>> chunks;
+    size_t cur = 0, off = 0;
+    size_t capacity() const { size_t c = 0; for (auto& ch : chunks) c += ch.second; return c; }
+    bool grow(size_t bytes) {
+        char* q = nullptr;
+        const size_t sz = std::max(bytes, std::max<size_t>(size_t(4) << 20, capacity()));
+        if (pinned ? hipHostMalloc((void**)&q, sz, hipHostMallocDefault) != hipSuccess
+                   : hipMalloc((void**)&q, sz) != hipSuccess)
+            return false;
+        chunks.emplace_back(q, sz);
+        cur = chunks.size() - 1;
+        off = 0;
+        return true;
+    }
+    void* get(size_t bytes) {
+        bytes = (std::max<size_t>(bytes, 1) + 255) & ~size_t(255);
+        if (chunks.empty() || off + bytes > chunks[cur].second)
+            if (!grow(bytes)) return nullptr;
+        void* r = chunks[cur].first + off;
+        off += bytes;
+        return r;
+    }
+    void reset() {
+        if (chunks.size() > 1) {
+            const size_t tot = capacity();
+            for (auto& ch : chunks) (void)(pinned ? hipHostFree(ch.first) : hipFree(ch.first));
+            chunks.clear();
+            (void)grow(tot);
+        }
+        cur = 0;
+        off = 0;
+    }
+};
+
+static Arena& dev_arena() { static thread_local Arena* a = new Arena(); return *a; }
+static Arena& host_stage() {
+    static thread_local Arena* a = [] { Arena* x = new Arena(); x->pinned = true; return x; }();
+    return *a;
+}
+static void arena_reset() { dev_arena().reset(); host_stage().reset(); }
+
+// H2D through pinned staging (asynchronous on the null stream), D2H through
+// pinned staging (synchronous).
+static hipError_t h2d(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return hipSuccess;
+    void* st = host_stage().get(bytes);
+    if (!st) return hipErrorOutOfMemory;
+    std::memcpy(st, src, bytes);
+    return hipMemcpyAsync(dst, st, bytes, hipMemcpyHostToDevice, 0);
+}
+static hipError_t d2h(void* dst, const void* src, size_t bytes) {
+    if (!bytes) return hipSuccess;
+    void* st = host_stage().get(bytes);
+    if (!st) return hipErrorOutOfMemory;
+    hipError_t e = hipMemcpyAsync(st, src, bytes, hipMemcpyDeviceToHost, 0);
+    if (e == hipSuccess) e = hipStreamSynchronize(0);
+    if (e == hipSuccess) std::memcpy(dst, st, bytes);
+    return e;
+}
+
+// A device buffer of the current host-API call (arena-backed).
 template <typename T>
 struct DBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    int alloc(size_t cnt) {
+        if (p && cnt <= n) return ORB_OK;
+        p = (T*)dev_arena().get(std::max<size_t>(1, cnt) * sizeof(T));
+        if (!p) return ORB_ERR_DEVICE;
+        n = cnt;
+        return ORB_OK;
+    }
+    int put(const T* src, size_t cnt, hipStream_t = 0) {
+        int rc = alloc(cnt);
+        if (rc) return rc;
+        return h2d(p, src, cnt * sizeof(T)) == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+    }
+};
+
+// A persistent device buffer (the asynchronous batch APIs' workspaces).
+template <typename T>
+struct PBuf {
     T* p = nullptr;
     size_t n = 0;
     int alloc(size_t cnt) {
@@ -1378,7 +1621,6 @@ struct DBuf {
         if (cnt && hipMemcpyAsync(p, src, cnt * sizeof(T), hipMemcpyHostToDevice, st) != hipSuccess) return ORB_ERR_DEVICE;
         return ORB_OK;
     }
-    ~DBuf() { if (p) (void)hipFree(p); }
 };
 
 static int pow2_at_least(int n) { int p = 64; while (p < n) p <<= 1; return p; }
@@ -1401,27 +1643,34 @@ struct DevFrame {
         const int nn = std::max(1, f->n);
         if ((rc = kps.alloc(nn)) || (rc = desc.alloc((size_t)nn * 32)) || (rc = n.put(&f->n, 1, st))) return rc;
         if (f->n) {
-            if (hipMemcpyAsync(kps.p, f->kps, f->n * sizeof(orb_keypoint), hipMemcpyHostToDevice, st) != hipSuccess ||
-                hipMemcpyAsync(desc.p, f->desc, (size_t)f->n * 32, hipMemcpyHostToDevice, st) != hipSuccess)
+            if (h2d(kps.p, f->kps, f->n * sizeof(orb_keypoint)) != hipSuccess ||
+                h2d(desc.p, f->desc, (size_t)f->n * 32) != hipSuccess)
                 return ORB_ERR_DEVICE;
         }
         if (f->u_right && (rc = ur.put(f->u_right, f->n, st))) return rc;
         if (f->scale_factors && (rc = scale.put(f->scale_factors, f->nlevels, st))) return rc;
         if (grid) {
-            if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1))) return rc;
-            const int sc = pow2_at_least(nn);
-            hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
-                               grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
-            if ((rc = cs.alloc(kCells + 1))) return rc;
-            hipLaunchKernelGGL(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
+            if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1)) || (rc = cs.alloc(kCells + 1))) return rc;
+            if (grid_cs_lds(nn) <= 160 * 1024) {
+                hipLaunchKernelGGL(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), st, kps.p, n.p, nn,
+                                   grid_params(f), sorted.p, count.p, cs.p, (uint32_t*)nullptr, (int*)nullptr);
+            } else {
+                const int sc = pow2_at_least(nn);
+                hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
+                                   grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
+                hipLaunchKernelGGL(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
+            }
         }
         return ORB_OK;
     }
 };
 
+// Start of a synchronous host-API call: a device must be present; the call's
+// arenas start empty.
 static int device_ok() {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return ORB_ERR_DEVICE;
+    arena_reset();
     return ORB_OK;
 }
 
@@ -1460,19 +1709,23 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     std::memcpy(pv.data(), prev_xy, sizeof(float) * 2 * f1->n);
     if ((rc = prev_in.put(pv.data(), pv.size()))) return rc;
     if (f1->n) {
-        ORB_CHECK(hipMemcpy(kps.p, f1->kps, f1->n * sizeof(orb_keypoint), hipMemcpyHostToDevice));
-        ORB_CHECK(hipMemcpy(desc.p, f1->desc, (size_t)f1->n * 32, hipMemcpyHostToDevice));
+        ORB_CHECK(h2d(kps.p, f1->kps, f1->n * sizeof(orb_keypoint)));
+        ORB_CHECK(h2d(desc.p, f1->desc, (size_t)f1->n * 32));
     }
     if (f2->n) {
-        ORB_CHECK(hipMemcpy(kps.p + cap, f2->kps, f2->n * sizeof(orb_keypoint), hipMemcpyHostToDevice));
-        ORB_CHECK(hipMemcpy(desc.p + (size_t)cap * 32, f2->desc, (size_t)f2->n * 32, hipMemcpyHostToDevice));
+        ORB_CHECK(h2d(kps.p + cap, f2->kps, f2->n * sizeof(orb_keypoint)));
+        ORB_CHECK(h2d(desc.p + (size_t)cap * 32, f2->desc, (size_t)f2->n * 32));
     }
     const GridParams g = grid_params(f2);
     const int sc = pow2_at_least(cap);
     DBuf<uint32_t> l0s; DBuf<int> l0c;
     if ((rc = l0s.alloc((size_t)2 * cap)) || (rc = l0c.alloc(2))) return rc;
-    hipLaunchKernelGGL(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p, count.p, sc,
-                       l0s.p, l0c.p);
+    if (grid_cs_lds(cap) <= 160 * 1024)
+        hipLaunchKernelGGL(k_grid_cs, dim3(2), dim3(256), grid_cs_lds(cap), 0, kps.p, n.p, cap, g, sorted.p, count.p,
+                           (int*)nullptr, l0s.p, l0c.p);
+    else
+        hipLaunchKernelGGL(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p,
+                           count.p, sc, l0s.p, l0c.p);
     SfiArgs a;
     a.kps = kps.p; a.desc = desc.p; a.n = n.p; a.cap = cap; a.gsorted = l0s.p; a.gcount = l0c.p;
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = prev_in.p; a.prev_out = prev_out.p;
@@ -1481,10 +1734,10 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     launch_sfi(a, 1, 0);
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
-    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(&res, nm.p, 4));
     if (f1->n) {
-        ORB_CHECK(hipMemcpy(matches12, m.p, f1->n * 4, hipMemcpyDeviceToHost));
-        ORB_CHECK(hipMemcpy(prev_xy, prev_out.p, f1->n * 8, hipMemcpyDeviceToHost));
+        ORB_CHECK(d2h(matches12, m.p, f1->n * 4));
+        ORB_CHECK(d2h(prev_xy, prev_out.p, f1->n * 8));
     }
     return res;
 }
@@ -1497,8 +1750,8 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     (void)max_x; (void)max_y;
     if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
     hipStream_t st = (hipStream_t)stream;
-    static thread_local DBuf<uint32_t> sorted, topk, l0s;
-    static thread_local DBuf<int> count, pf, ncand, l0c;
+    static thread_local PBuf<uint32_t> sorted, topk, l0s;
+    static thread_local PBuf<int> count, pf, ncand, l0c;
     static thread_local int pf_frames = 0;
     int rc;
     if ((rc = sorted.alloc((size_t)nframes * cap)) || (rc = count.alloc(nframes)) ||
@@ -1514,8 +1767,12 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     }
     const GridParams g{min_x, min_y, grid_inv_w, grid_inv_h};
     const int sc = pow2_at_least(cap);
-    hipLaunchKernelGGL(k_grid, dim3(nframes), dim3(256), sc * sizeof(uint32_t), st, d_kps, d_n, cap, g, sorted.p,
-                       count.p, sc, l0s.p, l0c.p);
+    if (grid_cs_lds(cap) <= 160 * 1024)
+        hipLaunchKernelGGL(k_grid_cs, dim3(nframes), dim3(256), grid_cs_lds(cap), st, d_kps, d_n, cap, g, sorted.p,
+                           count.p, (int*)nullptr, l0s.p, l0c.p);
+    else
+        hipLaunchKernelGGL(k_grid, dim3(nframes), dim3(256), sc * sizeof(uint32_t), st, d_kps, d_n, cap, g,
+                           sorted.p, count.p, sc, l0s.p, l0c.p);
     SfiArgs a;
     a.kps = d_kps; a.desc = d_desc; a.n = d_n; a.cap = cap; a.gsorted = l0s.p; a.gcount = l0c.p;
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = nullptr; a.prev_out = nullptr;
@@ -1549,8 +1806,8 @@ int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
     if ((rc = launch_bow(a, 1, 0))) return rc;
     int32_t res = 0;
-    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
-    if (f->n) ORB_CHECK(hipMemcpy(match_f, m.p, f->n * 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(&res, nm.p, 4));
+    if (f->n) ORB_CHECK(d2h(match_f, m.p, f->n * 4));
     return res;
 }
 
@@ -1581,7 +1838,7 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     const char* force = std::getenv("ORBM_PROJ_SINGLE_WAVE");
     const size_t lds2 = proj_resolve_lds(a.n, a.nq);
     if (lds2 <= 160 * 1024 && !(force && force[0] == '1')) {
-        DBuf<uint32_t> topk; DBuf<int> cnt;
+        DBuf<uint2> topk; DBuf<int> cnt;
         if ((rc = topk.alloc((size_t)std::max(1, a.nq) * kProjK)) || (rc = cnt.alloc(std::max(1, a.nq)))) return rc;
         if (a.nq) hipLaunchKernelGGL(k_proj_topk, dim3((a.nq + 3) / 4), dim3(256), 0, 0, a, proj_bound(a), topk.p, cnt.p);
         hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);
@@ -1592,8 +1849,8 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     }
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
-    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
-    if (f->n) ORB_CHECK(hipMemcpy(owner, own.p, f->n * 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(&res, nm.p, 4));
+    if (f->n) ORB_CHECK(d2h(owner, own.p, f->n * 4));
     return res;
 }
 
@@ -1649,6 +1906,7 @@ int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
     if (device < 0) return ORB_ERR_PARAM;     // the product path runs on the GPU only
     if (voc->nnodes < 2 || voc->nchild[0] == 0) return ORB_ERR_EMPTY;   // no words (TemplatedVocabulary::empty)
     if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    arena_reset();
     if (n == 0) return ORB_OK;
     int rc;
     DBuf<int> fc, nc, wid, ci; DBuf<uint8_t> nd, dd; DBuf<double> wt, wo; DBuf<int32_t> wio, nio;
@@ -1667,9 +1925,9 @@ int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
                        nd.p, wid.p, wt.p, n, dd.p,
                        nid_level, wio.p, wo.p, nio.p);
     ORB_CHECK(hipGetLastError());
-    ORB_CHECK(hipMemcpy(word_id, wio.p, n * 4, hipMemcpyDeviceToHost));
-    ORB_CHECK(hipMemcpy(weight, wo.p, n * 8, hipMemcpyDeviceToHost));
-    ORB_CHECK(hipMemcpy(node_id, nio.p, n * 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(word_id, wio.p, n * 4));
+    ORB_CHECK(d2h(weight, wo.p, n * 8));
+    ORB_CHECK(d2h(node_id, nio.p, n * 4));
     return ORB_OK;
 }
 
@@ -1699,8 +1957,8 @@ int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, cons
     a.best_idx = bi.p; a.best_dist = bdist.p;
     hipLaunchKernelGGL(k_fuse, dim3((nmp + 3) / 4), dim3(256), 0, 0, a);
     ORB_CHECK(hipGetLastError());
-    ORB_CHECK(hipMemcpy(best_idx, bi.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
-    ORB_CHECK(hipMemcpy(best_dist, bdist.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(best_idx, bi.p, nmp * sizeof(int32_t)));
+    ORB_CHECK(d2h(best_dist, bdist.p, nmp * sizeof(int32_t)));
     int n = 0;
     for (int i = 0; i < nmp; ++i) n += best_idx[i] >= 0;
     return n;
@@ -1756,8 +2014,8 @@ int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
     hipLaunchKernelGGL(k_tri_final, dim3(1), dim3(256), 0, 0, ta, kf1->n, out.p, nm.p);
     ORB_CHECK(hipGetLastError());
     int32_t n = 0;
-    if (kf1->n) ORB_CHECK(hipMemcpy(matches12, out.p, kf1->n * sizeof(int32_t), hipMemcpyDeviceToHost));
-    ORB_CHECK(hipMemcpy(&n, nm.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    if (kf1->n) ORB_CHECK(d2h(matches12, out.p, kf1->n * sizeof(int32_t)));
+    ORB_CHECK(d2h(&n, nm.p, sizeof(int32_t)));
     return n;
 }
 
@@ -1770,13 +2028,14 @@ int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const 
     for (int p = 0; p < npoints; ++p)
         if (off[p + 1] < off[p] || off[p + 1] - off[p] > 65535) return ORB_ERR_PARAM;
     if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    arena_reset();
     int rc;
     DBuf<int32_t> bo, bb; DBuf<uint8_t> bd;
     if ((rc = bo.put(off, (size_t)npoints + 1)) || (rc = bd.put(desc, (size_t)total * 32)) || (rc = bb.alloc(npoints)))
         return rc;
     hipLaunchKernelGGL(k_distinctive, dim3(npoints), dim3(64), 0, 0, npoints, bo.p, bd.p, bb.p);
     ORB_CHECK(hipGetLastError());
-    ORB_CHECK(hipMemcpy(best, bb.p, npoints * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(best, bb.p, npoints * sizeof(int32_t)));
     return ORB_OK;
 }
 
@@ -1813,8 +2072,8 @@ int orbm_search_by_bow_kf(const orbm_frame* kf1, const orbm_featvec* fv1, const 
     a.f_valid = fvv.p; a.out12 = o12.p;
     if ((rc = launch_bow(a, 1, 0))) return rc;
     int32_t res = 0;
-    ORB_CHECK(hipMemcpy(&res, nm.p, 4, hipMemcpyDeviceToHost));
-    if (kf1->n) ORB_CHECK(hipMemcpy(matches12, o12.p, kf1->n * 4, hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(&res, nm.p, 4));
+    if (kf1->n) ORB_CHECK(d2h(matches12, o12.p, kf1->n * 4));
     return res;
 }
 
@@ -1903,8 +2162,8 @@ int orbm_fuse_sim3(const orbm_frame* kf, int nmp, const uint8_t* valid, const fl
     DBuf<int32_t> bi, bd, blv; DBuf<uint8_t> bval, bdesc; DBuf<float> bu, bv;
     if ((rc = best_in_area(kf, df, nmp, valid, u, v, level, desc, th, kThLow, bi, bd, bval, bu, bv, blv, bdesc)))
         return rc;                                                               // :1437
-    ORB_CHECK(hipMemcpy(best_idx, bi.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
-    ORB_CHECK(hipMemcpy(best_dist, bd.p, nmp * sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(best_idx, bi.p, nmp * sizeof(int32_t)));
+    ORB_CHECK(d2h(best_dist, bd.p, nmp * sizeof(int32_t)));
     int n = 0;
     for (int i = 0; i < nmp; ++i) n += best_idx[i] >= 0;
     return n;
@@ -1944,8 +2203,8 @@ int orbm_search_by_sim3(const orbm_frame* kf1, const orbm_frame* kf2, const uint
     hipLaunchKernelGGL(k_sim3_agree, dim3(1), dim3(256), 0, 0, b1.p, n1, b2.p, out.p, nf.p);
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
-    ORB_CHECK(hipMemcpy(matches12, out.p, n1 * sizeof(int32_t), hipMemcpyDeviceToHost));
-    ORB_CHECK(hipMemcpy(&res, nf.p, sizeof(int32_t), hipMemcpyDeviceToHost));
+    ORB_CHECK(d2h(matches12, out.p, n1 * sizeof(int32_t)));
+    ORB_CHECK(d2h(&res, nf.p, sizeof(int32_t)));
     return res;
 }
 
