@@ -293,6 +293,52 @@ int orbm_search_by_projection_last(const orbm_frame* cur, int nlast,
                                    int check_ori,
                                    int32_t* owner, const uint8_t* blocked);
 
+/* ---------------- fisheye stereo frames (Frame::Nleft != -1) ----------------
+ * The frame is the combined keypoint array [mvKeys (nleft); mvKeysRight] with
+ * f->n = N descriptor rows; the library builds mGrid over the left keypoints
+ * and mGridRight over the right ones by local index (Frame.cc:385-416).  The
+ * stereo gate on mvuRight does not apply (f->u_right is ignored). */
+
+/* The right-camera fields ORBmatcher reads from MapPoint (MapPoint.h
+ * mbTrackInViewR, mTrackProjXR / YR, mnTrackScaleLevelR, mTrackViewCosR). */
+typedef struct orbm_mappoints_right {
+    const uint8_t* in_view;     /* mbTrackInViewR && !isBad() */
+    const float* proj_x;
+    const float* proj_y;
+    const int32_t* level;       /* -1: not predicted */
+    const float* view_cos;
+} orbm_mappoints_right;
+
+/* SearchByBoW(KeyFrame*, Frame&, matches) (src/ORBmatcher.cc:223-425) for
+ * F.Nleft = f_nleft >= 0: separate left / right best matches per KF feature
+ * (:296-323, :357-386).  Arguments otherwise as orbm_search_by_bow. */
+int orbm_search_by_bow_fisheye(const orbm_frame* kf, const orbm_featvec* kf_fv, const uint8_t* kf_valid,
+                               const orbm_frame* f, const orbm_featvec* f_fv, int f_nleft, float nnratio,
+                               int check_ori, int32_t* match_f);
+
+/* SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFarPoints)
+ * (src/ORBmatcher.cc:43-213) for F.Nleft = nleft >= 0: left search, then the
+ * right camera (its radius carries no th factor, :147), stereo partners set
+ * through l2r = mvLeftToRightMatch [nleft] and r2l = mvRightToLeftMatch
+ * [N - nleft]; mps->in_view is mbTrackInView && !isBad(), mps->proj_xr is not
+ * read.  owner / blocked as orbm_search_by_projection_mps. */
+int orbm_search_by_projection_mps_fisheye(const orbm_frame* f, int nleft, const int32_t* l2r, const int32_t* r2l,
+                                          const orbm_mappoints* mps, const orbm_mappoints_right* mps_r, float th,
+                                          int far_points, float th_far, float nnratio, int32_t* owner,
+                                          const uint8_t* blocked);
+
+/* SearchByProjection(Frame& Current, const Frame& Last, th, bMono)
+ * (src/ORBmatcher.cc:1676-1887) for CurrentFrame.Nleft = nleft >= 0: ur / vr
+ * are each point's projection into the right camera (GetRelativePoseTrl *
+ * Tcw * X, :1795-1796); the right search runs when the left candidate list
+ * was not empty.  last_octave / last_angle are the last frame's (combined)
+ * keypoints.  Other arguments as orbm_search_by_projection_last. */
+int orbm_search_by_projection_last_fisheye(const orbm_frame* cur, int nleft, int nlast, const uint8_t* valid,
+                                           const float* u, const float* v, const float* ur, const float* vr,
+                                           const int32_t* last_octave, const float* last_angle,
+                                           const uint8_t* has_obs, const uint8_t* last_desc, float th, int mode,
+                                           int check_ori, int32_t* owner, const uint8_t* blocked);
+
 /* ---------------- vocabulary (DBoW2 TemplatedVocabulary<FORB>) ---------------- */
 
 /* A k-ary vocabulary tree laid out breadth first: node 0 = root; children of

@@ -64,6 +64,10 @@ def lib():
         L.orbo_search_by_projection_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, f32, vp]
         L.orbo_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp]
         L.orbo_fuse_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, vp, vp]
+        L.orbo_search_by_bow_fisheye.argtypes = [vp, vp, vp, vp, vp, i32, f32, i32, vp]
+        L.orbo_search_by_projection_mps_fisheye.argtypes = [vp, i32, vp, vp, vp, vp, f32, i32, f32, f32, vp, vp]
+        L.orbo_search_by_projection_last_fisheye.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
+                                                             i32, i32, vp, vp]
         L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
         _lib = L
     return _lib
@@ -331,3 +335,37 @@ def fuse_sim3(kf, valid, u, v, level, desc, th):
     bi, bd = np.zeros(n, np.int32), np.zeros(n, np.int32)
     nf = lib().orbo_fuse_sim3(kf.ref(), n, *[abi.ptr(a) for a in q], th, abi.ptr(bi), abi.ptr(bd))
     return nf, bi, bd
+
+
+def search_by_bow_fisheye(kf, kfv, kf_valid, f, fv, nleft, nnratio=0.7, check_ori=True):
+    kv = np.ascontiguousarray(kf_valid, np.uint8)
+    match = np.zeros(f.struct.n, np.int32)
+    nm = lib().orbo_search_by_bow_fisheye(kf.ref(), kfv.ref(), abi.ptr(kv), f.ref(), fv.ref(), int(nleft), nnratio,
+                                          int(check_ori), abi.ptr(match))
+    return nm, match
+
+
+def search_by_projection_mps_fisheye(f, nleft, l2r, r2l, mps, mps_r, th, far_points, th_far, nnratio, owner,
+                                     blocked):
+    l2r = np.ascontiguousarray(l2r, np.int32)
+    r2l = np.ascontiguousarray(r2l, np.int32)
+    own = np.ascontiguousarray(owner, np.int32).copy()
+    blk = np.ascontiguousarray(blocked, np.uint8)
+    nm = lib().orbo_search_by_projection_mps_fisheye(f.ref(), int(nleft), abi.ptr(l2r), abi.ptr(r2l), mps.ref(),
+                                                     mps_r.ref(), th, int(far_points), th_far, nnratio, abi.ptr(own),
+                                                     abi.ptr(blk))
+    return nm, own
+
+
+def search_by_projection_last_fisheye(cur, nleft, valid, u, v, ur, vr, octave, angle, has_obs, desc, th, mode,
+                                      check_ori, owner, blocked):
+    arrs = [np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),
+            np.ascontiguousarray(v, np.float32), np.ascontiguousarray(ur, np.float32),
+            np.ascontiguousarray(vr, np.float32), np.ascontiguousarray(octave, np.int32),
+            np.ascontiguousarray(angle, np.float32), np.ascontiguousarray(has_obs, np.uint8),
+            np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)]
+    own = np.ascontiguousarray(owner, np.int32).copy()
+    blk = np.ascontiguousarray(blocked, np.uint8)
+    nm = lib().orbo_search_by_projection_last_fisheye(cur.ref(), int(nleft), len(arrs[0]), *[abi.ptr(x) for x in arrs],
+                                                      th, mode, int(check_ori), abi.ptr(own), abi.ptr(blk))
+    return nm, own

@@ -1508,4 +1508,218 @@ int orbo_fuse_sim3(const orbm_frame* kf, int nmp, const uint8_t* valid, const fl
     return nf;
 }
 
+
+// ---- fisheye stereo frames (Nleft != -1) ------------------------------------
+// The frame is the combined keypoint array [mvKeys (Nleft); mvKeysRight] with N
+// descriptor rows; mGrid holds the left keypoints, mGridRight the right ones by
+// local index (Frame.cc:385-416), queried with bRight (Frame.cc:657-723).
+namespace {
+orbm_frame sub_frame(const orbm_frame* f, int b, int e) {
+    orbm_frame s = *f;
+    s.n = e - b;
+    s.kps = f->kps + b;
+    s.desc = f->desc + (size_t)b * 32;
+    s.u_right = nullptr;
+    return s;
+}
+float radius_by_viewing_cos(float c) { return c > 0.998 ? 2.5f : 4.0f; }   // ORBmatcher.cc:215-221
+}  // namespace
+
+// ORBmatcher::SearchByBoW(KeyFrame*, Frame&, ...) (ORBmatcher.cc:223-425) with
+// F.Nleft = nleft (>= 0): left and right best/second over each node's frame
+// features (:296-323); the right match is taken only inside the left's
+// `bestDist1 <= TH_LOW` and ignores the ratio (`|| true`, :357-359).
+int orbo_search_by_bow_fisheye(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid,
+                               const orbm_frame* f, const orbm_featvec* ffv, int nleft, float ratio, int check_ori,
+                               int32_t* match) {
+    for (int i = 0; i < f->n; ++i) match[i] = -1;
+    std::vector<int> hist[kHisto];
+    int nm = 0, a = 0, b = 0;
+    while (a < kfv->nnodes && b < ffv->nnodes) {
+        const uint32_t na = kfv->node_ids[a], nb = ffv->node_ids[b];
+        if (na == nb) {
+            for (int p = kfv->offsets[a]; p < kfv->offsets[a + 1]; ++p) {
+                const int ikf = (int)kfv->idx[p];
+                if (!kf_valid[ikf]) continue;
+                const uint8_t* dk = kf->desc + (size_t)ikf * 32;
+                int b1 = 256, bi = -1, b2 = 256, b1r = 256, bir = -1, b2r = 256;
+                for (int q = ffv->offsets[b]; q < ffv->offsets[b + 1]; ++q) {
+                    const int jf = (int)ffv->idx[q];
+                    if (match[jf] >= 0) continue;
+                    const int dist = hamming(dk, f->desc + (size_t)jf * 32);
+                    if (jf < nleft && dist < b1) { b2 = b1; b1 = dist; bi = jf; }
+                    else if (jf < nleft && dist < b2) b2 = dist;
+                    if (jf >= nleft && dist < b1r) { b2r = b1r; b1r = dist; bir = jf; }
+                    else if (jf >= nleft && dist < b2r) b2r = dist;
+                }
+                if (b1 <= kThLow) {
+                    if ((float)b1 < ratio * (float)b2) {
+                        match[bi] = ikf;
+                        if (check_ori) hist[rot_bin(kf->kps[ikf].angle, f->kps[bi].angle)].push_back(bi);
+                        ++nm;
+                    }
+                    if (b1r <= kThLow) {
+                        match[bir] = ikf;
+                        if (check_ori) hist[rot_bin(kf->kps[ikf].angle, f->kps[bir].angle)].push_back(bir);
+                        ++nm;
+                    }
+                }
+            }
+            ++a; ++b;
+        } else if (na < nb) {
+            a = (int)(std::lower_bound(kfv->node_ids + a, kfv->node_ids + kfv->nnodes, nb) - kfv->node_ids);
+        } else {
+            b = (int)(std::lower_bound(ffv->node_ids + b, ffv->node_ids + ffv->nnodes, na) - ffv->node_ids);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < kHisto; ++i) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int j : hist[i]) { match[j] = -1; --nm; }
+        }
+    }
+    return nm;
+}
+
+// ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints,
+// thFarPoints) (ORBmatcher.cc:43-213) with F.Nleft = nleft: left search on
+// mGrid, then the right camera on mGridRight (:144-210; its radius has no th
+// factor), stereo partners via mvLeftToRightMatch / mvRightToLeftMatch; a
+// left best failing the ratio test skips the point's right search (:125-126).
+int orbo_search_by_projection_mps_fisheye(const orbm_frame* f, int nleft, const int32_t* l2r, const int32_t* r2l,
+                                          const orbm_mappoints* mp, const orbm_mappoints_right* mr, float th,
+                                          int far_points, float th_far, float ratio, int32_t* owner,
+                                          const uint8_t* blocked) {
+    const orbm_frame fl = sub_frame(f, 0, nleft), fr = sub_frame(f, nleft, f->n);
+    Grid gl(&fl), gr(&fr);
+    int nm = 0;
+    const bool factor = th != 1.0;
+    auto slot_blocked = [&](int idx) {
+        const int o = owner[idx];
+        if (o == -1) return false;
+        if (o <= -2) return blocked[idx] != 0;
+        return mp->has_obs[o] != 0;
+    };
+    for (int i = 0; i < mp->n; ++i) {
+        if (!mp->in_view[i] && !mr->in_view[i]) continue;
+        if (far_points && mp->track_depth[i] > th_far) continue;
+        const uint8_t* dm = mp->desc + (size_t)i * 32;
+        if (mp->in_view[i]) {
+            const int lvl = mp->level[i];
+            float r = radius_by_viewing_cos(mp->view_cos[i]);
+            if (factor) r *= th;
+            const std::vector<int> cand = gl.area(mp->proj_x[i], mp->proj_y[i], r * f->scale_factors[lvl], lvl - 1, lvl);
+            if (!cand.empty()) {
+                int best = 256, bl = -1, best2 = 256, bl2 = -1, bi = -1;
+                for (int idx : cand) {
+                    if (slot_blocked(idx)) continue;
+                    const int dist = hamming(dm, f->desc + (size_t)idx * 32);
+                    if (dist < best) { best2 = best; best = dist; bl2 = bl; bl = f->kps[idx].octave; bi = idx; }
+                    else if (dist < best2) { bl2 = f->kps[idx].octave; best2 = dist; }
+                }
+                if (best <= kThHigh) {
+                    if (bl == bl2 && best > ratio * best2) continue;
+                    if (bl != bl2 || best <= ratio * best2) {
+                        owner[bi] = i;
+                        if (l2r[bi] != -1) { owner[l2r[bi] + nleft] = i; ++nm; }
+                        ++nm;
+                    }
+                }
+            }
+        }
+        if (mr->in_view[i]) {
+            const int lvl = mr->level[i];
+            if (lvl != -1) {
+                const float r = radius_by_viewing_cos(mr->view_cos[i]);
+                const std::vector<int> cand = gr.area(mr->proj_x[i], mr->proj_y[i], r * f->scale_factors[lvl], lvl - 1, lvl);
+                if (cand.empty()) continue;
+                int best = 256, bl = -1, best2 = 256, bl2 = -1, bi = -1;
+                for (int idx : cand) {
+                    if (slot_blocked(idx + nleft)) continue;
+                    const int dist = hamming(dm, f->desc + (size_t)(idx + nleft) * 32);
+                    if (dist < best) { best2 = best; best = dist; bl2 = bl; bl = f->kps[idx + nleft].octave; bi = idx; }
+                    else if (dist < best2) { bl2 = f->kps[idx + nleft].octave; best2 = dist; }
+                }
+                if (best <= kThHigh) {
+                    if (bl == bl2 && best > ratio * best2) continue;
+                    if (r2l[bi] != -1) { owner[r2l[bi]] = i; ++nm; }
+                    owner[bi + nleft] = i;
+                    ++nm;
+                }
+            }
+        }
+    }
+    return nm;
+}
+
+// ORBmatcher::SearchByProjection(Frame& Current, const Frame& Last, th, bMono)
+// (ORBmatcher.cc:1676-1887) with CurrentFrame.Nleft = nleft: after the left
+// search (reached only when its candidate list is not empty) the point is
+// searched again in the right camera (projection ur/vr from the caller,
+// GetRelativePoseTrl, :1794-1859) with the same octave window.
+int orbo_search_by_projection_last_fisheye(const orbm_frame* cur, int nleft, int nlast, const uint8_t* valid,
+                                           const float* u, const float* v, const float* ur, const float* vr,
+                                           const int32_t* last_octave, const float* last_angle,
+                                           const uint8_t* has_obs, const uint8_t* last_desc, float th, int mode,
+                                           int check_ori, int32_t* owner, const uint8_t* blocked) {
+    const orbm_frame fl = sub_frame(cur, 0, nleft), fr = sub_frame(cur, nleft, cur->n);
+    Grid gl(&fl), gr(&fr);
+    int nm = 0;
+    std::vector<int> hist[kHisto];
+    auto slot_blocked = [&](int idx) {
+        const int o = owner[idx];
+        if (o == -1) return false;
+        if (o <= -2) return blocked[idx] != 0;
+        return has_obs[o] != 0;
+    };
+    auto area = [&](const Grid& g, float x, float y, float radius, int oct) {
+        if (mode == 1) return g.area(x, y, radius, oct, -1);
+        if (mode == 2) return g.area(x, y, radius, 0, oct);
+        return g.area(x, y, radius, oct - 1, oct + 1);
+    };
+    for (int i = 0; i < nlast; ++i) {
+        if (!valid[i]) continue;
+        const int oct = last_octave[i];
+        const float radius = th * cur->scale_factors[oct];
+        const uint8_t* dm = last_desc + (size_t)i * 32;
+        std::vector<int> cand = area(gl, u[i], v[i], radius, oct);
+        if (cand.empty()) continue;
+        int best = 256, bi = -1;
+        for (int i2 : cand) {
+            if (slot_blocked(i2)) continue;
+            const int dist = hamming(dm, cur->desc + (size_t)i2 * 32);
+            if (dist < best) { best = dist; bi = i2; }
+        }
+        if (best <= kThHigh) {
+            owner[bi] = i;
+            ++nm;
+            if (check_ori) hist[rot_bin(last_angle[i], cur->kps[bi].angle)].push_back(bi);
+        }
+        cand = area(gr, ur[i], vr[i], radius, oct);
+        best = 256;
+        bi = -1;
+        for (int i2 : cand) {
+            if (slot_blocked(i2 + nleft)) continue;
+            const int dist = hamming(dm, cur->desc + (size_t)(i2 + nleft) * 32);
+            if (dist < best) { best = dist; bi = i2; }
+        }
+        if (best <= kThHigh) {
+            owner[bi + nleft] = i;
+            ++nm;
+            if (check_ori) hist[rot_bin(last_angle[i], cur->kps[bi + nleft].angle)].push_back(bi + nleft);
+        }
+    }
+    if (check_ori) {
+        int a, b, c;
+        three_maxima(hist, a, b, c);
+        for (int k = 0; k < kHisto; ++k) {
+            if (k == a || k == b || k == c) continue;
+            for (int j : hist[k]) { owner[j] = -1; --nm; }
+        }
+    }
+    return nm;
+}
+
 }  // extern "C"

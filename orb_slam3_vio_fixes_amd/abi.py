@@ -59,6 +59,11 @@ class OrbvVocab(C.Structure):
                 ("weight", C.c_void_p), ("child_idx", C.c_void_p)]
 
 
+class OrbmMapPointsRight(C.Structure):
+    _fields_ = [("in_view", C.c_void_p), ("proj_x", C.c_void_p), ("proj_y", C.c_void_p), ("level", C.c_void_p),
+                ("view_cos", C.c_void_p)]
+
+
 def ptr(a: np.ndarray | None) -> int | None:
     if a is None:
         return None
@@ -132,3 +137,12 @@ def mappoints_struct(proj_x, proj_y, proj_xr, level, view_cos, track_depth, in_v
          np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)]
     s = OrbmMapPoints(len(a[0]), *[ptr(x) for x in a])
     return Keep(s, a)
+
+
+def mappoints_right_struct(in_view, proj_x, proj_y, level, view_cos) -> Keep:
+    """orbm_mappoints_right: MapPoint mbTrackInViewR (&& !isBad), mTrackProjXR/YR, mnTrackScaleLevelR,
+    mTrackViewCosR."""
+    a = [np.ascontiguousarray(in_view, np.uint8), np.ascontiguousarray(proj_x, np.float32),
+         np.ascontiguousarray(proj_y, np.float32), np.ascontiguousarray(level, np.int32),
+         np.ascontiguousarray(view_cos, np.float32)]
+    return Keep(OrbmMapPointsRight(*[ptr(x) for x in a]), a)

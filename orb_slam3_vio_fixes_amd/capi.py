@@ -23,7 +23,8 @@ EXPORTS = [
     "orbk_db_create", "orbk_db_destroy", "orbk_db_upload", "orbk_detect_relocalization_candidates",
     "orbm_fuse", "orbm_search_for_triangulation", "orbm_compute_distinctive_descriptors",
     "orbm_search_by_bow_kf", "orbm_search_by_projection_kf", "orbm_search_by_projection_sim3",
-    "orbm_search_by_sim3", "orbm_fuse_sim3",
+    "orbm_search_by_sim3", "orbm_fuse_sim3", "orbm_search_by_bow_fisheye", "orbm_search_by_projection_mps_fisheye",
+    "orbm_search_by_projection_last_fisheye",
 ]
 
 _lib = None
@@ -62,6 +63,10 @@ def load(path: Path | str = LIB_PATH):
     L.orbm_search_by_projection_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, f32, vp]
     L.orbm_search_by_sim3.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, vp]
     L.orbm_fuse_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, vp, vp]
+    L.orbm_search_by_bow_fisheye.argtypes = [vp, vp, vp, vp, vp, i32, f32, i32, vp]
+    L.orbm_search_by_projection_mps_fisheye.argtypes = [vp, i32, vp, vp, vp, vp, f32, i32, f32, f32, vp, vp]
+    L.orbm_search_by_projection_last_fisheye.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32,
+                                                         i32, vp, vp]
     L.orbk_db_create.restype = vp
     L.orbk_db_create.argtypes = [i32]
     L.orbk_db_destroy.argtypes = [vp]

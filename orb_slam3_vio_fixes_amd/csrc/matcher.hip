@@ -637,6 +637,7 @@ struct BowArgs {
     int* hist;           // [pair][32]   (0 before k_bow_nodes)
     const uint8_t* f_valid;   // KF-KF form: pKF2 MapPoint != NULL && !isBad(), else NULL
     int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
+    int f_nleft = -1;         // the frame's Nleft (-1: mono / rectified)
 };
 
 // One wave per KF FeatureVector node (all pairs flattened, grid-stride): the
@@ -678,6 +679,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
         const int fb = a.f_off[fl], fe = a.f_off[fl + 1];
         const int nch = (fe - fb + kWave - 1) / kWave;
         int32_t* match = a.match + (long long)pr * a.f_n;
+        const bool fish = a.f_nleft >= 0;
         // chunk 0 of the node's F features stays in registers across the KF features
         uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
         int fi0 = -1;
@@ -703,9 +705,13 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
             if (!KV[ikf]) continue;
             const uint4 q0 = *(const uint4*)(KD + (long long)ikf * 32);
             const uint4 q1 = *(const uint4*)(KD + (long long)ikf * 32 + 16);
-            Best2 st{256, 256, -1, 0, 0};
+            // left (or only) track st; right track sr when the frame is fisheye stereo (:296-323)
+            Best2 st{256, 256, -1, 0, 0}, sr{256, 256, -1, 0, 0};
             for (int c = 0; c < nch; ++c) {
-                int d = INT_MAX;
+                int d = INT_MAX, fi = -1;
+                const int q = fb + c * kWave + lane;
+                if (c == 0) fi = fi0;
+                else if (q < fe) fi = (int)a.f_idx[q];
                 if (c < kBowMaskChunks) {
                     if (!((taken >> c) & 1)) {
                         if (c == 0) {
@@ -713,23 +719,18 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
                                 __popc(q0.w ^ f0.w) + __popc(q1.x ^ f1.x) + __popc(q1.y ^ f1.y) +
                                 __popc(q1.z ^ f1.z) + __popc(q1.w ^ f1.w);
                         } else {
-                            const int fi = (int)a.f_idx[fb + c * kWave + lane];
                             d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
                         }
                     }
-                } else {
-                    const int q = fb + c * kWave + lane;
-                    if (q < fe) {
-                        const int fi = (int)a.f_idx[q];
-                        if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
-                            d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
-                    }
+                } else if (q < fe) {
+                    if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
+                        d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
                 }
-                merge_chunk(st, d, c * kWave + lane, 0);
+                const bool right = fish && fi >= a.f_nleft;
+                merge_chunk(st, right ? INT_MAX : d, c * kWave + lane, 0);
+                if (fish) merge_chunk(sr, right ? d : INT_MAX, c * kWave + lane, 0);
             }
-            const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;     // :848 / :327
-            if (low && (float)st.best < a.ratio * (float)st.best2) {
-                const int pos = st.idx;                  // position in the node's F list
+            auto claim = [&](int pos) {                  // pos: position in the node's F list
                 if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
                 const int fi = (pos < kWave) ? __shfl(fi0, pos, kWave) : (int)a.f_idx[fb + pos];
                 if (lane == 0) {
@@ -746,7 +747,10 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
                     __builtin_amdgcn_wave_barrier();
                     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
                 }
-            }
+            };
+            const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;     // :848 / :327
+            if (low && (float)st.best < a.ratio * (float)st.best2) claim(st.idx);
+            if (fish && low && sr.best <= kThLow) claim(sr.idx);                   // :357-386, ratio ignored
         }
         if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
     }
@@ -978,6 +982,144 @@ __global__ __launch_bounds__(64) void k_proj(ProjArgs a) {
 }
 
 static size_t proj_lds(int nq) { return (size_t)(32 + kCells + 1 + nq + 1) * 4 + 64; }
+
+// ---- fisheye stereo frames (Frame::Nleft != -1) ---------------------------
+// Slots [0, nleft) are the left keypoints (mvKeys), [nleft, n) the right ones
+// (mvKeysRight); each camera has its own grid order and cell-start table, the
+// right one by local index (Frame.cc:385-416).  One wave, queries in order, the
+// left search then the right one per query (ORBmatcher.cc:61-210 / :1695-1859).
+struct FishArgs {
+    int nleft;
+    const uint32_t *gs_l, *gs_r;
+    const int *cs_l, *cs_r;
+    const int32_t *l2r, *r2l;                      // mvLeftToRightMatch / mvRightToLeftMatch (mode 0)
+    const uint8_t* rvalid;                         // mode 0: mbTrackInViewR && !isBad()
+    const float *rqx, *rqy;                        // right-camera projections
+    const int32_t* rlevel;                         // mode 0: mnTrackScaleLevelR
+    const float* rviewcos;                         // mode 0: mTrackViewCosR
+};
+
+// Exact scan of one camera's candidate list (grid order gs / cell starts cs,
+// slot = local index + off); *nstatic = the GetFeaturesInArea list length.
+__device__ Best2 proj_scan_cam(const ProjArgs& a, int i, const ProjQuery& q, const uint32_t* gs, const int* cs,
+                               int off, int& nstatic) {
+    const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
+    const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+    const AreaRuns ar = area_runs(cs, q.cr);
+    Best2 st{256, 256, -1, -1, -1};
+    int ns = 0;
+    for (int base = 0; base < ar.total; base += kWave) {
+        const int t = base + lane_id();
+        const int j = area_pos(ar, min(t, ar.total - 1));
+        int d = INT_MAX, fi = -1, lv = -1;
+        bool stat = false;
+        if (t < ar.total) {
+            fi = (int)(gs[j] & 0xffff) + off;
+            stat = proj_static(a, i, q, fi, lv);
+            if (stat && !proj_blocked(a, a.owner, fi)) d = hamming32(q0, q1, a.desc + (long long)fi * 32);
+        }
+        ns += __popcll(__ballot(stat));
+        merge_chunk(st, d, fi, lv);
+    }
+    nstatic = ns;
+    return st;
+}
+
+__device__ __forceinline__ void proj_window(const ProjArgs& a, int oct, ProjQuery& q) {
+    if (a.last_mode == 1) { q.minL = oct; q.maxL = -1; }
+    else if (a.last_mode == 2) { q.minL = 0; q.maxL = oct; }
+    else { q.minL = oct - 1; q.maxL = oct + 1; }
+}
+
+__global__ __launch_bounds__(64) void k_proj_fisheye(ProjArgs a, FishArgs fa) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int lane = lane_id();
+    int* hist = lds;                          // 32
+    int* hent = lds + 32;                     // 2 nq: (bin << 16) | slot in push order
+    for (int k = lane; k < 32; k += kWave) hist[k] = 0;
+    __syncthreads();
+    int nm = 0, nh = 0;
+    auto ori_push = [&](int i, int slot) {
+        const int bn = rot_bin(a.qangle[i], a.kps[slot].angle);
+        if (lane == 0) { hist[bn]++; hent[nh] = (bn << 16) | slot; }
+        ++nh;
+    };
+    auto set_owner = [&](int slot, int i) { if (lane == 0) a.owner[slot] = i; };
+    for (int i = 0; i < a.nq; ++i) {
+        const bool lv = a.qvalid[i] != 0;
+        const bool rv = a.mode == 0 ? fa.rvalid[i] != 0 : lv;
+        if (!lv && !rv) continue;
+        if (a.mode == 0 && a.far_points && a.qdepth[i] > a.th_far) continue;
+        bool go_right = true;
+        if (lv) {
+            ProjQuery q;
+            q.x = a.qx[i]; q.y = a.qy[i];
+            const int lvl = a.qlevel[i];
+            if (a.mode == 0) {
+                float r = a.qviewcos[i] > 0.998f ? 2.5f : 4.0f;
+                if (a.th != 1.0f) r *= a.th;
+                q.r = r * a.scale[lvl];
+                q.minL = lvl - 1; q.maxL = lvl;
+            } else {
+                q.r = a.th * a.scale[lvl];
+                proj_window(a, lvl, q);
+            }
+            int ns = 0;
+            Best2 st{256, 256, -1, -1, -1};
+            if (cell_range(q.x, q.y, q.r, a.g, q.cr)) st = proj_scan_cam(a, i, q, fa.gs_l, fa.cs_l, 0, ns);
+            if (a.mode == 0) {
+                if (ns > 0 && st.best <= kThHigh) {                                   // :123-139
+                    if (st.lvl == st.lvl2 && (float)st.best > a.ratio * (float)st.best2) {
+                        go_right = false;                                             // `continue` (:126)
+                    } else {
+                        set_owner(st.idx, i);
+                        if (fa.l2r[st.idx] != -1) { set_owner(fa.l2r[st.idx] + fa.nleft, i); ++nm; }
+                        ++nm;
+                    }
+                }
+            } else {
+                if (ns == 0) go_right = false;                                        // :1735-1736
+                else if (st.best <= kThHigh) {                                        // :1770-1792
+                    set_owner(st.idx, i);
+                    ++nm;
+                    if (a.check_ori) ori_push(i, st.idx);
+                }
+            }
+            __syncthreads();
+        }
+        if (!go_right || !rv) continue;
+        ProjQuery q;
+        q.x = fa.rqx[i]; q.y = fa.rqy[i];
+        if (a.mode == 0) {                                                            // :144-150
+            const int lvl = fa.rlevel[i];
+            if (lvl == -1) continue;
+            q.r = (fa.rviewcos[i] > 0.998f ? 2.5f : 4.0f) * a.scale[lvl];
+            q.minL = lvl - 1; q.maxL = lvl;
+        } else {                                                                      // :1798-1811
+            const int oct = a.qlevel[i];
+            q.r = a.th * a.scale[oct];
+            proj_window(a, oct, q);
+        }
+        if (!cell_range(q.x, q.y, q.r, a.g, q.cr)) continue;
+        int ns = 0;
+        const Best2 st = proj_scan_cam(a, i, q, fa.gs_r, fa.cs_r, fa.nleft, ns);
+        if (st.best > kThHigh) continue;
+        if (a.mode == 0) {                                                            // :193-208
+            if (st.lvl == st.lvl2 && (float)st.best > a.ratio * (float)st.best2) continue;
+            const int partner = fa.r2l[st.idx - fa.nleft];
+            if (partner != -1) { set_owner(partner, i); ++nm; }
+            set_owner(st.idx, i);
+            ++nm;
+        } else {                                                                      // :1836-1857
+            set_owner(st.idx, i);
+            ++nm;
+            if (a.check_ori) ori_push(i, st.idx);
+        }
+        __syncthreads();
+    }
+    if (a.mode == 1 && a.check_ori) proj_rot_filter(a, hist, hent, nh, a.owner, nm);
+    if (lane == 0) a.nmatches[0] = nm;
+}
 
 // ---- two-phase form ------------------------------------------------------
 // Phase 1 (k_proj_topk, every query in parallel, one wave each): the static
@@ -1783,8 +1925,8 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     return ORB_OK;
 }
 
-int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid, const orbm_frame* f,
-                       const orbm_featvec* ffv, float nnratio, int check_ori, int32_t* match_f) {
+static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid, const orbm_frame* f,
+                    const orbm_featvec* ffv, int f_nleft, float nnratio, int check_ori, int32_t* match_f) {
     if (!kf || !kfv || !kf_valid || !f || !ffv || !match_f) return ORB_ERR_PARAM;
     if (device_ok()) return ORB_ERR_DEVICE;
     int rc;
@@ -1804,11 +1946,24 @@ int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint
     a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
+    a.f_nleft = f_nleft;
     if ((rc = launch_bow(a, 1, 0))) return rc;
     int32_t res = 0;
     ORB_CHECK(d2h(&res, nm.p, 4));
     if (f->n) ORB_CHECK(d2h(match_f, m.p, f->n * 4));
     return res;
+}
+
+int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid, const orbm_frame* f,
+                       const orbm_featvec* ffv, float nnratio, int check_ori, int32_t* match_f) {
+    return bow_host(kf, kfv, kf_valid, f, ffv, -1, nnratio, check_ori, match_f);
+}
+
+int orbm_search_by_bow_fisheye(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid,
+                               const orbm_frame* f, const orbm_featvec* ffv, int f_nleft, float nnratio,
+                               int check_ori, int32_t* match_f) {
+    if (!f || f_nleft < 0 || f_nleft > f->n) return ORB_ERR_PARAM;
+    return bow_host(kf, kfv, kf_valid, f, ffv, f_nleft, nnratio, check_ori, match_f);
 }
 
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f, const orbm_featvec* ffv,
@@ -2206,6 +2361,116 @@ int orbm_search_by_sim3(const orbm_frame* kf1, const orbm_frame* kf2, const uint
     ORB_CHECK(d2h(matches12, out.p, n1 * sizeof(int32_t)));
     ORB_CHECK(d2h(&res, nf.p, sizeof(int32_t)));
     return res;
+}
+
+
+// ---------------- fisheye stereo frames ----------------
+
+// One grid order + cell-start table over cnt keypoints at kps_dev (one frame).
+static int grid_one(const orb_keypoint* kps_dev, const int* n_dev, int cnt, GridParams g, DBuf<uint32_t>& sorted,
+                    DBuf<int>& count, DBuf<int>& cs) {
+    int rc;
+    const int nn = std::max(1, cnt);
+    if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1)) || (rc = cs.alloc(kCells + 1))) return rc;
+    if (grid_cs_lds(nn) <= 160 * 1024) {
+        hipLaunchKernelGGL(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), 0, kps_dev, n_dev, nn, g, sorted.p,
+                           count.p, cs.p, (uint32_t*)nullptr, (int*)nullptr);
+    } else {
+        const int sc = pow2_at_least(nn);
+        hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), 0, kps_dev, n_dev, nn, g, sorted.p,
+                           count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
+        hipLaunchKernelGGL(k_cell_start, dim3(1), dim3(256), 0, 0, sorted.p, count.p, nn, cs.p);
+    }
+    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+}
+
+// Upload the combined frame and build the left / right grids; run k_proj_fisheye.
+static int run_fisheye(ProjArgs& a, FishArgs& fa, const orbm_frame* f, int nleft, int32_t* owner,
+                       const uint8_t* blocked) {
+    int rc;
+    orbm_frame fn = *f;
+    fn.u_right = nullptr;                       // no mvuRight gate for Nleft != -1 (:92, :1751)
+    DevFrame df;
+    if ((rc = df.upload(&fn, false, 0))) return rc;
+    const int ns[2] = {nleft, f->n - nleft};
+    DBuf<int> dn; DBuf<uint32_t> gl, gr; DBuf<int> cl, cr, csl, csr;
+    if ((rc = dn.put(ns, 2))) return rc;
+    const GridParams g = grid_params(f);
+    if ((rc = grid_one(df.kps.p, dn.p, nleft, g, gl, cl, csl)) ||
+        (rc = grid_one(df.kps.p + nleft, dn.p + 1, f->n - nleft, g, gr, cr, csr)))
+        return rc;
+    DBuf<int32_t> own, nm; DBuf<uint8_t> blk;
+    if ((rc = own.put(owner, std::max(1, f->n))) || (rc = blk.put(blocked, std::max(1, f->n))) || (rc = nm.alloc(1)))
+        return rc;
+    a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = nullptr; a.scale = df.scale.p; a.g = g;
+    a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
+    fa.nleft = nleft; fa.gs_l = gl.p; fa.gs_r = gr.p; fa.cs_l = csl.p; fa.cs_r = csr.p;
+    const size_t lds = (size_t)(32 + 2 * a.nq + 1) * 4 + 64;
+    if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(k_proj_fisheye, dim3(1), dim3(64), lds, 0, a, fa);
+    ORB_CHECK(hipGetLastError());
+    int32_t res = 0;
+    ORB_CHECK(d2h(&res, nm.p, 4));
+    if (f->n) ORB_CHECK(d2h(owner, own.p, f->n * 4));
+    return res;
+}
+
+int orbm_search_by_projection_mps_fisheye(const orbm_frame* f, int nleft, const int32_t* l2r, const int32_t* r2l,
+                                          const orbm_mappoints* mps, const orbm_mappoints_right* mr, float th,
+                                          int far_points, float th_far, float nnratio, int32_t* owner,
+                                          const uint8_t* blocked) {
+    if (!f || !mps || !mr || !owner || !blocked || !f->scale_factors || !l2r || !r2l) return ORB_ERR_PARAM;
+    if (nleft < 0 || nleft > f->n || f->n > 0xffff) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    const int nq = mps->n, nr = f->n - nleft;
+    for (int i = 0; i < nq; ++i) {
+        if (mps->in_view[i] && (mps->level[i] < 0 || mps->level[i] >= f->nlevels)) return ORB_ERR_PARAM;
+        if (mr->in_view[i] && (mr->level[i] < -1 || mr->level[i] >= f->nlevels)) return ORB_ERR_PARAM;
+    }
+    DBuf<float> qx, qy, vc, dp, rx, ry, rvc; DBuf<int32_t> lv, rlv, dl2r, dr2l; DBuf<uint8_t> iv, ho, qd, riv;
+    if ((rc = qx.put(mps->proj_x, nq)) || (rc = qy.put(mps->proj_y, nq)) || (rc = lv.put(mps->level, nq)) ||
+        (rc = vc.put(mps->view_cos, nq)) || (rc = dp.put(mps->track_depth, nq)) || (rc = iv.put(mps->in_view, nq)) ||
+        (rc = ho.put(mps->has_obs, nq)) || (rc = qd.put(mps->desc, (size_t)nq * 32)) ||
+        (rc = rx.put(mr->proj_x, nq)) || (rc = ry.put(mr->proj_y, nq)) || (rc = rlv.put(mr->level, nq)) ||
+        (rc = rvc.put(mr->view_cos, nq)) || (rc = riv.put(mr->in_view, nq)) ||
+        (rc = dl2r.put(l2r, std::max(1, nleft))) || (rc = dr2l.put(r2l, std::max(1, nr))))
+        return rc;
+    ProjArgs a{};
+    a.mode = 0; a.nq = nq; a.qx = qx.p; a.qy = qy.p; a.qxr = nullptr; a.qlevel = lv.p; a.qviewcos = vc.p;
+    a.qdepth = dp.p; a.qvalid = iv.p; a.qhas_obs = ho.p; a.qdesc = qd.p; a.qangle = nullptr;
+    a.th = th; a.th_far = th_far; a.ratio = nnratio; a.far_points = far_points; a.last_mode = 0; a.check_ori = 0;
+    FishArgs fa{};
+    fa.l2r = dl2r.p; fa.r2l = dr2l.p; fa.rvalid = riv.p; fa.rqx = rx.p; fa.rqy = ry.p; fa.rlevel = rlv.p;
+    fa.rviewcos = rvc.p;
+    return run_fisheye(a, fa, f, nleft, owner, blocked);
+}
+
+int orbm_search_by_projection_last_fisheye(const orbm_frame* cur, int nleft, int nlast, const uint8_t* valid,
+                                           const float* u, const float* v, const float* ur, const float* vr,
+                                           const int32_t* last_octave, const float* last_angle,
+                                           const uint8_t* has_obs, const uint8_t* last_desc, float th, int mode,
+                                           int check_ori, int32_t* owner, const uint8_t* blocked) {
+    if (!cur || !owner || !blocked || !cur->scale_factors || nlast < 0) return ORB_ERR_PARAM;
+    if (nlast && (!valid || !u || !v || !ur || !vr || !last_octave || !last_angle || !has_obs || !last_desc))
+        return ORB_ERR_PARAM;
+    if (nleft < 0 || nleft > cur->n || cur->n > 0xffff) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    for (int i = 0; i < nlast; ++i)
+        if (valid[i] && (last_octave[i] < 0 || last_octave[i] >= cur->nlevels)) return ORB_ERR_PARAM;
+    DBuf<float> qx, qy, rx, ry, qa; DBuf<int32_t> lv; DBuf<uint8_t> iv, ho, qd;
+    if ((rc = qx.put(u, nlast)) || (rc = qy.put(v, nlast)) || (rc = rx.put(ur, nlast)) || (rc = ry.put(vr, nlast)) ||
+        (rc = lv.put(last_octave, nlast)) || (rc = qa.put(last_angle, nlast)) || (rc = iv.put(valid, nlast)) ||
+        (rc = ho.put(has_obs, nlast)) || (rc = qd.put(last_desc, (size_t)nlast * 32)))
+        return rc;
+    ProjArgs a{};
+    a.mode = 1; a.nq = nlast; a.qx = qx.p; a.qy = qy.p; a.qxr = nullptr; a.qlevel = lv.p; a.qvalid = iv.p;
+    a.qhas_obs = ho.p; a.qdesc = qd.p; a.qangle = qa.p; a.th = th; a.last_mode = mode; a.check_ori = check_ori;
+    a.skip_any = 0; a.accept = (float)kThHigh;
+    FishArgs fa{};
+    fa.rqx = rx.p; fa.rqy = ry.p;
+    return run_fisheye(a, fa, cur, nleft, owner, blocked);
 }
 
 }  // extern "C"

@@ -432,6 +432,53 @@ class ORBmatcher:
         capi.check(nf, "Fuse(KF, Sim3)")
         return nf, bi, bd
 
+    # ---- fisheye stereo frames (Frame::Nleft != -1; F = [mvKeys; mvKeysRight]) ----
+
+    def SearchByBoWFisheye(self, KF: abi.Keep, KFfv: abi.Keep, kf_valid, F: abi.Keep, Ffv: abi.Keep, Nleft: int):
+        """SearchByBoW(KeyFrame*, Frame&) with F.Nleft != -1 (ORBmatcher.cc:296-386): (nmatches, match)."""
+        kf_valid = np.ascontiguousarray(kf_valid, np.uint8)
+        match = np.zeros(F.struct.n, np.int32)
+        nm = capi.lib().orbm_search_by_bow_fisheye(KF.ref(), KFfv.ref(), abi.ptr(kf_valid), F.ref(), Ffv.ref(),
+                                                   int(Nleft), self.mfNNratio, int(self.mbCheckOrientation),
+                                                   abi.ptr(match))
+        capi.check(nm, "SearchByBoW(KF, F fisheye)")
+        return nm, match
+
+    def SearchByProjectionFisheye(self, F: abi.Keep, Nleft: int, l2r, r2l, mps: abi.Keep, mps_r: abi.Keep,
+                                  th: float = 3.0, bFarPoints: bool = False, thFarPoints: float = 50.0, owner=None,
+                                  blocked=None):
+        """SearchByProjection(Frame&, vector<MapPoint*>) with F.Nleft != -1 (ORBmatcher.cc:43-213)."""
+        n = F.struct.n
+        l2r = np.ascontiguousarray(l2r, np.int32)
+        r2l = np.ascontiguousarray(r2l, np.int32)
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        blocked = np.zeros(n, np.uint8) if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nm = capi.lib().orbm_search_by_projection_mps_fisheye(F.ref(), int(Nleft), abi.ptr(l2r), abi.ptr(r2l),
+                                                              mps.ref(), mps_r.ref(), th, int(bFarPoints),
+                                                              thFarPoints, self.mfNNratio, abi.ptr(owner),
+                                                              abi.ptr(blocked))
+        capi.check(nm, "SearchByProjection(F fisheye, MPs)")
+        return nm, owner
+
+    def SearchByProjectionLastFisheye(self, cur: abi.Keep, Nleft: int, valid, u, v, ur, vr, octave, angle, has_obs,
+                                      desc, th: float, mode: int = 0, owner=None, blocked=None):
+        """SearchByProjection(Frame& Current, const Frame& Last) with Current.Nleft != -1
+        (ORBmatcher.cc:1676-1887); ur / vr = projections into the right camera."""
+        n = cur.struct.n
+        arrs = [np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),
+                np.ascontiguousarray(v, np.float32), np.ascontiguousarray(ur, np.float32),
+                np.ascontiguousarray(vr, np.float32), np.ascontiguousarray(octave, np.int32),
+                np.ascontiguousarray(angle, np.float32), np.ascontiguousarray(has_obs, np.uint8),
+                np.ascontiguousarray(desc, np.uint8).reshape(-1, 32)]
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        blocked = np.zeros(n, np.uint8) if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nm = capi.lib().orbm_search_by_projection_last_fisheye(cur.ref(), int(Nleft), len(arrs[0]),
+                                                               *[abi.ptr(x) for x in arrs], th, mode,
+                                                               int(self.mbCheckOrientation), abi.ptr(owner),
+                                                               abi.ptr(blocked))
+        capi.check(nm, "SearchByProjection(F fisheye, LastFrame)")
+        return nm, owner
+
 
 def _queries(valid, u, v, level, desc):
     return (np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),

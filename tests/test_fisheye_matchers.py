@@ -1,0 +1,198 @@
+"""Fisheye-stereo branches (Frame::Nleft != -1) of SearchByBoW(KF, F),
+SearchByProjection(F, MapPoints) and SearchByProjection(F, LastFrame)
+(src/ORBmatcher.cc:223-425, 43-213, 1676-1887).  The frame is the combined
+keypoint array [mvKeys; mvKeysRight] of two synthetic images (C2 shape); map
+points aim at left keypoints and, through a random stereo pairing
+(mvLeftToRightMatch), at right ones.  CPU: oracle vs the independent Python
+restatements (tests/fisheye_ref.py); GPU: the HIP kernels vs the oracle."""
+import numpy as np
+import pytest
+
+import fisheye_ref as R
+from oracle import oracle as O
+from orb_slam3_vio_fixes_amd import abi, synth
+
+W, H = 752, 480
+
+
+@pytest.fixture(scope="module")
+def scene():
+    frames = synth.sequence(W, H, 3, config=11, start=5000)
+    ex = O.OracleExtractor(1000, 1.2, 8, 20, 7)
+    t = ex.tables()
+    (kl, dl), (kr, dr), (kk, kd) = [ex(f, (0, 0))[:2] for f in frames]
+    k = np.concatenate([kl, kr])
+    d = np.concatenate([dl, dr])
+    return k, d, len(kl), (kk, kd), t
+
+
+def flips(d, rng, p):
+    bits = np.unpackbits(d, axis=-1)
+    return np.packbits(bits ^ (rng.random(bits.shape) < p), axis=-1)
+
+
+def stereo_pairs(nleft, nright, rng):
+    l2r = np.full(nleft, -1, np.int32)
+    r2l = np.full(nright, -1, np.int32)
+    m = min(nleft, nright) // 2
+    a = rng.choice(nleft, m, replace=False)
+    b = rng.choice(nright, m, replace=False)
+    l2r[a] = b
+    r2l[b] = a
+    return l2r, r2l
+
+
+def mps_inputs(scene, seed, n=900):
+    k, d, nleft, _, t = scene
+    rng = np.random.default_rng(seed)
+    nright = len(k) - nleft
+    l2r, r2l = stereo_pairs(nleft, nright, rng)
+    tl = rng.integers(0, nleft, n)
+    tr = np.where(l2r[tl] >= 0, l2r[tl], rng.integers(0, nright, n))
+    q = {"in_view": (rng.random(n) < 0.85).astype(np.uint8),
+         "x": (k["x"][tl] + rng.normal(0, 2, n)).astype(np.float32),
+         "y": (k["y"][tl] + rng.normal(0, 2, n)).astype(np.float32),
+         "level": np.clip(k["octave"][tl] + rng.integers(0, 2, n), 0, 7).astype(np.int32),
+         "view_cos": rng.uniform(0.995, 1.0, n).astype(np.float32),
+         "depth": rng.uniform(0, 100, n).astype(np.float32),
+         "has_obs": (rng.random(n) < 0.7).astype(np.uint8),
+         "desc": flips(d[tl], rng, 0.06)}
+    ktr = k[nleft:][tr]
+    qr = {"in_view": (rng.random(n) < 0.7).astype(np.uint8),
+          "x": (ktr["x"] + rng.normal(0, 2, n)).astype(np.float32),
+          "y": (ktr["y"] + rng.normal(0, 2, n)).astype(np.float32),
+          "level": np.where(rng.random(n) < 0.1, -1, np.clip(ktr["octave"] + rng.integers(0, 2, n), 0, 7)).astype(np.int32),
+          "view_cos": rng.uniform(0.995, 1.0, n).astype(np.float32)}
+    N = len(k)
+    owner = np.full(N, -1, np.int32)
+    pre = rng.random(N) < 0.05
+    owner[pre] = -2
+    blocked = (pre & (rng.random(N) < 0.5)).astype(np.uint8)
+    mps = abi.mappoints_struct(q["x"], q["y"], q["x"], q["level"], q["view_cos"], q["depth"], q["in_view"],
+                               q["has_obs"], q["desc"])
+    mps_r = abi.mappoints_right_struct(qr["in_view"], qr["x"], qr["y"], qr["level"], qr["view_cos"])
+    f = abi.frame_struct(k, d, W, H, scale_factors=t["scale"])
+    return f, l2r, r2l, q, qr, mps, mps_r, owner, blocked
+
+
+CASES_MPS = [(1, 3.0, False, 0.8), (2, 1.0, False, 0.8), (3, 5.0, True, 0.6)]
+
+
+@pytest.mark.parametrize("seed,th,far,ratio", CASES_MPS)
+def test_oracle_mps_fisheye_vs_python(scene, seed, th, far, ratio):
+    k, d, nleft, _, t = scene
+    f, l2r, r2l, q, qr, mps, mps_r, owner, blocked = mps_inputs(scene, seed)
+    nm, own = O.search_by_projection_mps_fisheye(f, nleft, l2r, r2l, mps, mps_r, th, far, 50.0, ratio, owner, blocked)
+    rn, ro = R.search_by_projection_mps_fisheye(k, d, W, H, t["scale"], nleft, l2r, r2l, q, qr, th, far, 50.0, ratio,
+                                                owner, blocked)
+    np.testing.assert_array_equal(own, ro)
+    assert nm == rn and (own[nleft:] >= 0).sum() > 50 and (own[:nleft] >= 0).sum() > 50
+
+
+def last_inputs(scene, seed, n=900):
+    k, d, nleft, _, t = scene
+    rng = np.random.default_rng(seed)
+    nright = len(k) - nleft
+    tl = rng.integers(0, nleft, n)
+    tr = rng.integers(0, nright, n)
+    ktr = k[nleft:][tr]
+    valid = (rng.random(n) < 0.9).astype(np.uint8)
+    u = (k["x"][tl] + rng.normal(0, 2, n)).astype(np.float32)
+    v = (k["y"][tl] + rng.normal(0, 2, n)).astype(np.float32)
+    ur = (ktr["x"] + rng.normal(0, 2, n)).astype(np.float32)
+    vr = (ktr["y"] + rng.normal(0, 2, n)).astype(np.float32)
+    octave = k["octave"][tl].astype(np.int32)
+    angle = (k["angle"][tl] + rng.normal(0, 6, n)).astype(np.float32) % 360
+    has_obs = (rng.random(n) < 0.6).astype(np.uint8)
+    desc = flips(d[tl], rng, 0.06)
+    N = len(k)
+    owner = np.where(rng.random(N) < 0.05, -2, -1).astype(np.int32)
+    blocked = ((owner == -2) & (rng.random(N) < 0.5)).astype(np.uint8)
+    f = abi.frame_struct(k, d, W, H, scale_factors=t["scale"])
+    return f, (valid, u, v, ur, vr, octave, angle, has_obs, desc), owner, blocked
+
+
+CASES_LAST = [(4, 0, True, 7.0), (5, 1, True, 15.0), (6, 2, False, 7.0)]
+
+
+@pytest.mark.parametrize("seed,mode,ori,th", CASES_LAST)
+def test_oracle_last_fisheye_vs_python(scene, seed, mode, ori, th):
+    k, d, nleft, _, t = scene
+    f, args, owner, blocked = last_inputs(scene, seed)
+    nm, own = O.search_by_projection_last_fisheye(f, nleft, *args, th, mode, ori, owner, blocked)
+    rn, ro = R.search_by_projection_last_fisheye(k, d, W, H, t["scale"], nleft, *args, th, mode, ori, owner, blocked)
+    np.testing.assert_array_equal(own, ro)
+    assert nm == rn and nm > 50
+
+
+def featvec_dict(nid):
+    fv = {}
+    for i, n in enumerate(nid.tolist()):
+        if n >= 0:
+            fv.setdefault(n, []).append(i)
+    return fv
+
+
+def bow_inputs(scene, seed, nodes=30):
+    k, d, nleft, (kk, kd), t = scene
+    rng = np.random.default_rng(seed)
+    knode = rng.integers(0, nodes, len(kk))
+    fnode = rng.integers(0, nodes, len(k))
+    kvalid = (rng.random(len(kk)) < 0.8).astype(np.uint8)
+    d = d.copy()
+    pick = rng.choice(len(k), len(k) // 3, replace=False)     # near-duplicates on both cameras
+    src = rng.integers(0, len(kk), len(pick))
+    d[pick] = flips(kd[src], rng, 0.04)
+    fnode[pick] = knode[src]
+    return kk, kd, knode, kvalid, k, d, fnode, nleft
+
+
+@pytest.mark.parametrize("ratio,ori,seed", [(0.7, True, 7), (0.75, False, 8)])
+def test_oracle_bow_fisheye_vs_python(scene, ratio, ori, seed):
+    kk, kd, knode, kvalid, k, d, fnode, nleft = bow_inputs(scene, seed)
+    nm, m = O.search_by_bow_fisheye(abi.frame_struct(kk, kd, W, H), abi.featvec_struct(knode), kvalid,
+                                    abi.frame_struct(k, d, W, H), abi.featvec_struct(fnode), nleft, ratio, ori)
+    rn, rm = R.search_by_bow_fisheye(kk, kd, featvec_dict(knode), kvalid, k, d, featvec_dict(fnode), nleft, ratio, ori)
+    np.testing.assert_array_equal(m, rm)
+    assert nm == rn and (m[:nleft] >= 0).sum() > 20 and (m[nleft:] >= 0).sum() > 20
+
+
+# ------------------------------------------------------------------ GPU parity
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,th,far,ratio", CASES_MPS)
+def test_gpu_mps_fisheye(gpu_lib, scene, seed, th, far, ratio):
+    from orb_slam3_vio_fixes_amd import orb
+    nleft = scene[2]
+    f, l2r, r2l, q, qr, mps, mps_r, owner, blocked = mps_inputs(scene, seed)
+    rn, ro = O.search_by_projection_mps_fisheye(f, nleft, l2r, r2l, mps, mps_r, th, far, 50.0, ratio, owner, blocked)
+    gn, go = orb.ORBmatcher(ratio, True).SearchByProjectionFisheye(f, nleft, l2r, r2l, mps, mps_r, th, far, 50.0,
+                                                                   owner, blocked)
+    assert gn == rn
+    np.testing.assert_array_equal(go, ro)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,mode,ori,th", CASES_LAST)
+def test_gpu_last_fisheye(gpu_lib, scene, seed, mode, ori, th):
+    from orb_slam3_vio_fixes_amd import orb
+    nleft = scene[2]
+    f, args, owner, blocked = last_inputs(scene, seed)
+    rn, ro = O.search_by_projection_last_fisheye(f, nleft, *args, th, mode, ori, owner, blocked)
+    gn, go = orb.ORBmatcher(0.9, ori).SearchByProjectionLastFisheye(f, nleft, *args, th, mode, owner, blocked)
+    assert gn == rn
+    np.testing.assert_array_equal(go, ro)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ratio,ori,seed", [(0.7, True, 7), (0.75, False, 8)])
+def test_gpu_bow_fisheye(gpu_lib, scene, ratio, ori, seed):
+    from orb_slam3_vio_fixes_amd import orb
+    kk, kd, knode, kvalid, k, d, fnode, nleft = bow_inputs(scene, seed)
+    kf, f = abi.frame_struct(kk, kd, W, H), abi.frame_struct(k, d, W, H)
+    kfv, fv = abi.featvec_struct(knode), abi.featvec_struct(fnode)
+    rn, rm = O.search_by_bow_fisheye(kf, kfv, kvalid, f, fv, nleft, ratio, ori)
+    gn, gm = orb.ORBmatcher(ratio, ori).SearchByBoWFisheye(kf, kfv, kvalid, f, fv, nleft)
+    assert gn == rn
+    np.testing.assert_array_equal(gm, rm)
