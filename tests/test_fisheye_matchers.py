@@ -196,3 +196,35 @@ def test_gpu_bow_fisheye(gpu_lib, scene, ratio, ori, seed):
     gn, gm = orb.ORBmatcher(ratio, ori).SearchByBoWFisheye(kf, kfv, kvalid, f, fv, nleft)
     assert gn == rn
     np.testing.assert_array_equal(gm, rm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bright", [False, True])
+def test_gpu_fuse_camera_of_fisheye_keyframe(gpu_lib, scene, bright):
+    """Fuse(pKF, vpMapPoints, th, bRight) (ORBmatcher.cc:1148-1331) on a fisheye
+    keyframe is orbm_fuse on that camera's view: GetFeaturesInArea(.., bRight)
+    searches mGridRight by local index, the keypoint is mvKeysRight[idx], the
+    stereo gate reads mvuRight[idx] with the LOCAL index (as the reference
+    does), and the descriptor / returned slot are idx + NLeft (:1298)."""
+    import mapping_ref as MR
+    from orb_slam3_vio_fixes_amd import orb
+    k, d, nleft, _, t = scene
+    rng = np.random.default_rng(21 + bright)
+    b, e = (nleft, len(k)) if bright else (0, nleft)
+    kk, dd = k[b:e], d[b:e]
+    n = 800
+    tgt = rng.integers(0, len(kk), n)
+    u = (kk["x"][tgt] + rng.normal(0, 1.5, n)).astype(np.float32)
+    v = (kk["y"][tgt] + rng.normal(0, 1.5, n)).astype(np.float32)
+    ur = (u - rng.uniform(5, 30, n)).astype(np.float32)
+    level = np.minimum(kk["octave"][tgt] + rng.integers(0, 2, n), 7).astype(np.int32)
+    md = flips(dd[tgt], rng, 0.05)
+    valid = (rng.random(n) < 0.9).astype(np.uint8)
+    mvuright = np.where(rng.random(len(k)) < 0.3, k["x"] - 10, -1).astype(np.float32)   # combined, N entries
+    view = abi.frame_struct(kk, dd, W, H, u_right=mvuright[:len(kk)], scale_factors=t["scale"])
+    gn, gb, _ = orb.ORBmatcher.Fuse(view, t["inv_sigma2"], valid, u, v, ur, level, md, 3.0)
+    gslot = np.where(gb >= 0, gb + b, -1)
+    grid = MR.make_grid(kk, 0.0, W, 0.0, H)
+    ref = MR.fuse(kk, dd, mvuright[:len(kk)], t["scale"], t["inv_sigma2"], grid, valid, u, v, ur, level, md, 3.0)
+    np.testing.assert_array_equal(gslot, np.where(ref >= 0, ref + b, -1))
+    assert gn == (ref >= 0).sum() and gn > 100
