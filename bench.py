@@ -24,6 +24,9 @@ Extra objects on the JSON line:
                WRITE_SIZE; tools/pmc_profile.sh, same command/config), and
                valu_issue_frac = its VALU wave-instructions / (2 per CU per
                cycle) from the same summary: the FAST pass is VALU-bound.
+  stage_roofline  achieved GB/s of each stage on its algorithmic bytes, and the
+               north-star pass (pyramid + FAST read bytes, R = 2*sum(P) - P_7
+               per frame) against the HBM peak.
   cpu_baseline the CPU oracle (oracle/, "port") on the host, rank 0, N=1,
                on a bounded sample of the same frames, threads stated; its
                outputs double as a parity check of the sampled frames.
@@ -79,12 +82,38 @@ def pmc_row(path, kernel):
     return None
 
 
+def level_sizes(ex):
+    """Pixels of each pyramid level (ComputePyramid sizes, ORBextractor.cc:1174-1175)."""
+    return [int(np.rint(np.float32(W) * np.float32(s))) * int(np.rint(np.float32(H) * np.float32(s)))
+            for s in ex.GetInverseScaleFactors()]
+
+
 def level_pixels(ex):
-    inv = ex.GetInverseScaleFactors()
-    tot = 0
-    for s in inv:
-        tot += int(np.rint(np.float32(W) * np.float32(s))) * int(np.rint(np.float32(H) * np.float32(s)))
-    return tot
+    return sum(level_sizes(ex))
+
+
+def stage_roofline(ex, stage_ms, frames_per_launch, kps_per_frame):
+    """Achieved GB/s of each stage on its algorithmic bytes:
+    pyramid reads levels 0..L-2 and writes 1..L-1; FAST reads every level once;
+    the north-star pass (pyramid + FAST) reads R = 2*sum(P) - P_{L-1} per frame;
+    describe reads the 43x43 raw patch (1,849 B) and writes 36 B per keypoint."""
+    P = level_sizes(ex)
+    per_frame = {"pyramid": sum(P[:-1]) + sum(P[1:]), "fast_cells": sum(P),
+                 "describe": (1849 + 36) * kps_per_frame}
+    out = {}
+    for k, b in per_frame.items():
+        ms = float(stage_ms.get(k) or 0)
+        if ms > 0:
+            gbs = b * frames_per_launch / (ms * 1e-3) / 1e9
+            out[k] = {"bytes_per_launch": b * frames_per_launch, "ms": ms, "achieved_GBs": gbs,
+                      "frac": gbs / HBM_PEAK_GBS}
+    ms = float(stage_ms.get("pyramid") or 0) + float(stage_ms.get("fast_cells") or 0)
+    if ms > 0:
+        r = (2 * sum(P) - P[-1]) * frames_per_launch
+        gbs = r / (ms * 1e-3) / 1e9
+        out["north_star_pyramid_fast_read"] = {"bytes_per_launch": r, "ms": ms, "achieved_GBs": gbs,
+                                               "frac": gbs / HBM_PEAK_GBS}
+    return out
 
 
 def cpu_baseline(frames_np, threads):
@@ -245,7 +274,9 @@ def main():
                "stage_ms": {**{k: float(v) for k, v in zip(STAGES, stage_ms)},
                             "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
                                                           if match_events else None)},
-               "roofline": roof}
+               "roofline": roof,
+               "stage_roofline": stage_roofline(ex, dict(zip(STAGES, map(float, stage_ms))), frames_per_launch,
+                                                float(n.float().mean().item()))}
         if world == 1 and args.cpu_sample > 0:
             ns = min(args.cpu_sample, B)
             fps, outs, nms = cpu_baseline(frames_np[:ns], args.cpu_threads)
