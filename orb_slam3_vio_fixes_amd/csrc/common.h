@@ -24,6 +24,34 @@ __device__ __forceinline__ int wave_sum(int v) {
     return v;
 }
 
+// Wave-wide minimum in registers (DPP): quad permutes and row rotations give
+// every lane its row-of-16 minimum, row_bcast:15 / row_bcast:31 (gfx9 DPP)
+// fold the rows into lane 63, read back as a wave-uniform value.  Lanes of
+// rows a broadcast does not write keep `old` = the identity.  No LDS traffic,
+// unlike __shfl_xor (ds_bpermute).
+template <int CTRL, int ROWS>
+__device__ __forceinline__ int dpp_mov(int v, int id) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, ROWS, 0xf, false);
+}
+
+template <typename T>
+__device__ __forceinline__ T dpp_min2(T v, int x) {
+    const T o = __builtin_bit_cast(T, x);
+    return o < v ? o : v;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_min(T v, T id) {
+    const int ii = __builtin_bit_cast(int, id);
+    v = dpp_min2(v, dpp_mov<0xb1, 0xf>(__builtin_bit_cast(int, v), ii));    // quad_perm [1,0,3,2]
+    v = dpp_min2(v, dpp_mov<0x4e, 0xf>(__builtin_bit_cast(int, v), ii));    // quad_perm [2,3,0,1]
+    v = dpp_min2(v, dpp_mov<0x124, 0xf>(__builtin_bit_cast(int, v), ii));   // row_ror:4
+    v = dpp_min2(v, dpp_mov<0x128, 0xf>(__builtin_bit_cast(int, v), ii));   // row_ror:8
+    v = dpp_min2(v, dpp_mov<0x142, 0xa>(__builtin_bit_cast(int, v), ii));   // row_bcast:15 -> rows 1, 3
+    v = dpp_min2(v, dpp_mov<0x143, 0xc>(__builtin_bit_cast(int, v), ii));   // row_bcast:31 -> rows 2, 3
+    return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), kWave - 1));
+}
+
 // Position of this lane among the set bits of `mask` below it.
 __device__ __forceinline__ int mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));

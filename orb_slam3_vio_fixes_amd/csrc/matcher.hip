@@ -271,23 +271,19 @@ struct Best2 {
 //   if (d < best) {best2 = best; lvl2 = lvl; best = d; lvl = lv; idx = fi;}
 //   else if (d < best2) {best2 = d; lvl2 = lv;}
 __device__ __forceinline__ void merge_chunk(Best2& st, int d, int fi, int lv) {
-    // chunk minimum and its first lane
-    int m = d;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, kWave));
+    // chunk minimum and its first lane (DPP reduction, readlane broadcasts)
+    const int m = wave_min(d, INT_MAX);
     if (m == INT_MAX) return;
     const uint64_t at = __ballot(d == m);
     const int first = __ffsll((long long)at) - 1;
-    const int fi_m = __shfl(fi, first, kWave), lv_m = __shfl(lv, first, kWave);
+    const int fi_m = __builtin_amdgcn_readlane(fi, first), lv_m = __builtin_amdgcn_readlane(lv, first);
     // chunk second: min over lanes other than `first`, with its first lane
-    int d2 = lane_id() == first ? INT_MAX : d;
-    int m2 = d2;
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) m2 = min(m2, __shfl_xor(m2, o, kWave));
+    const int d2 = lane_id() == first ? INT_MAX : d;
+    const int m2 = wave_min(d2, INT_MAX);
     int lv_m2 = -1;
     if (m2 != INT_MAX) {
         const uint64_t at2 = __ballot(d2 == m2);
-        lv_m2 = __shfl(lv, __ffsll((long long)at2) - 1, kWave);
+        lv_m2 = __builtin_amdgcn_readlane(lv, __ffsll((long long)at2) - 1);
     }
     // sequential merge: the chunk's elements come after the running ones.
     // New best: strictly smaller chunk min replaces; the old best becomes a
@@ -451,8 +447,7 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
         for (int k = 0; k < kTopK; ++k) {
             uint32_t mn = kNoKey;
             for (int q = lane; q < cnt; q += kWave) mn = min(mn, mypool[q]);
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) mn = min(mn, (uint32_t)__shfl_xor((int)mn, o, kWave));
+            mn = wave_min(mn, 0xffffffffu);
             if (lane == 0) tk[k] = mn;
             if (mn == kNoKey) { for (int kk = k + 1 + lane; kk < kTopK; kk += kWave) tk[kk] = kNoKey; break; }
             for (int q = lane; q < cnt; q += kWave)
@@ -700,11 +695,30 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
             }
         }
         int nm = 0;
-        for (int p = ko[ia]; p < ko[ia + 1]; ++p) {
-            const int ikf = (int)ki[p];
-            if (!KV[ikf]) continue;
-            const uint4 q0 = *(const uint4*)(KD + (long long)ikf * 32);
-            const uint4 q1 = *(const uint4*)(KD + (long long)ikf * 32 + 16);
+        // the node's KF features, 64 at a time, prefetched lane-parallel (index,
+        // MapPoint validity, descriptor, angle) and visited in order by readlane
+        const int pe = ko[ia + 1];
+        for (int pbase = ko[ia]; pbase < pe; pbase += kWave) {
+          const int pl = pbase + lane;
+          int my_ikf = 0, my_ok = 0;
+          uint4 mq0 = make_uint4(0, 0, 0, 0), mq1 = mq0;
+          float my_ang = 0.f;
+          if (pl < pe) {
+              my_ikf = (int)ki[pl];
+              my_ok = KV[my_ikf];
+              mq0 = *(const uint4*)(KD + (long long)my_ikf * 32);
+              mq1 = *(const uint4*)(KD + (long long)my_ikf * 32 + 16);
+              my_ang = KK[my_ikf].angle;
+          }
+          for (uint64_t rem = __ballot(my_ok != 0); rem; rem &= rem - 1) {
+            const int src = __ffsll((long long)rem) - 1;
+            const int ikf = __builtin_amdgcn_readlane(my_ikf, src);
+            const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), src));
+            uint4 q0, q1;
+            q0.x = __builtin_amdgcn_readlane(mq0.x, src); q0.y = __builtin_amdgcn_readlane(mq0.y, src);
+            q0.z = __builtin_amdgcn_readlane(mq0.z, src); q0.w = __builtin_amdgcn_readlane(mq0.w, src);
+            q1.x = __builtin_amdgcn_readlane(mq1.x, src); q1.y = __builtin_amdgcn_readlane(mq1.y, src);
+            q1.z = __builtin_amdgcn_readlane(mq1.z, src); q1.w = __builtin_amdgcn_readlane(mq1.w, src);
             // left (or only) track st; right track sr when the frame is fisheye stereo (:296-323)
             Best2 st{256, 256, -1, 0, 0}, sr{256, 256, -1, 0, 0};
             for (int c = 0; c < nch; ++c) {
@@ -736,7 +750,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
                 if (lane == 0) {
                     match[fi] = ikf;
                     if (a.check_ori) {
-                        const int bn = rot_bin(KK[ikf].angle, a.f_kps[fi].angle);
+                        const int bn = rot_bin(kang, a.f_kps[fi].angle);
                         atomicAdd(&a.hist[pr * 32 + bn], 1);
                         a.fbin[(long long)pr * a.f_n + fi] = (int8_t)bn;
                     }
@@ -751,6 +765,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
             const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;     // :848 / :327
             if (low && (float)st.best < a.ratio * (float)st.best2) claim(st.idx);
             if (fish && low && sr.best <= kThLow) claim(sr.idx);                   // :357-386, ratio ignored
+          }
         }
         if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
     }
@@ -1177,11 +1192,10 @@ __global__ __launch_bounds__(256) void k_proj_topk(ProjArgs a, int bound, uint2*
             const int x = min(xa, xb);
             const uint32_t xe = xa <= xb ? ent : run_e;
             int m = x;
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) m = min(m, __shfl_xor(m, o, kWave));
+            m = wave_min(m, INT_MAX);
             if (m == INT_MAX) break;
             const int src = __ffsll((long long)__ballot(x == m)) - 1;
-            const uint32_t me = (uint32_t)__shfl((int)xe, src, kWave);
+            const uint32_t me = (uint32_t)__builtin_amdgcn_readlane((int)xe, src);
             if (lane == r) { nrun = m; nrun_e = me; }
             prev = m;
         }
@@ -1461,8 +1475,7 @@ __global__ __launch_bounds__(256) void k_fuse(FuseArgs a) {
                 const int d = hamming32(q0, q1, a.desc + (long long)fi * 32);
                 best = min(best, ((uint32_t)d << 20) | (uint32_t)t);
             }
-#pragma unroll
-            for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+            best = wave_min(best, 0xffffffffu);
             if (best != 0xffffffffu && (int)(best >> 20) <= a.accept) {
                 out_dist = (int)(best >> 20);
                 out_idx = (int)(a.gsorted[area_pos(ar, (int)(best & 0xfffff))] & 0xffff);
@@ -1553,8 +1566,7 @@ __global__ __launch_bounds__(256) void k_tri(TriArgs a) {
             }
             if (ok) best = min(best, ((uint32_t)dist << 16) | (uint32_t)(0xffff - (j - a.item_b[t])));
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+        best = wave_min(best, 0xffffffffu);
         if (best != 0xffffffffu) res = (int)a.fv2_idx[a.item_b[t] + (0xffff - (int)(best & 0xffff))];
         if (lane == 0 && res >= 0) a.item_bin[t] = rot_bin(kp1.angle, a.k2[res].angle);
     }
@@ -1648,8 +1660,7 @@ __global__ __launch_bounds__(64) void k_distinctive(int npoints, const int32_t* 
         }
         best = min(best, ((uint32_t)lo << 16) | (uint32_t)i);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+    best = wave_min(best, 0xffffffffu);
     if (lane == 0) best_out[p] = (int)(best & 0xffff);
 }
 

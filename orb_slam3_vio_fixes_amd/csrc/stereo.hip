@@ -150,8 +150,7 @@ __global__ __launch_bounds__(256) void k_stereo_match(StereoArgs a) {
             const int dist = hamming_st(q0, q1, DR + (long long)iR * 32);
             if (dist < kStThHigh) best = min(best, ((uint32_t)dist << 16) | (uint32_t)iR);
         }
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) best = min(best, (uint32_t)__shfl_xor((int)best, o, kWave));
+        best = wave_min(best, 0xffffffffu);
         const int bestDist = (int)(best >> 16), bestIdxR = (int)(best & 0xffff);
         if (bestDist < (kStThHigh + kStThLow) / 2) {               // :896
             // sub-pixel match by correlation (:898-933)
