@@ -645,51 +645,87 @@ struct BowArgs {
 // wave touches the node's features).
 constexpr int kBowMaskChunks = 64;
 
+constexpr int kBowRegChunks = 2;        // frame-feature chunks held in registers per node
+constexpr int kBowLdsNodes = 4096;      // frame FeatureVector nodes staged in LDS (dynamic size)
+
+static size_t bow_lds(int f_nnodes) { return f_nnodes <= kBowLdsNodes ? (size_t)(2 * f_nnodes + 1) * 4 : 0; }
+
 __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int bow_smem[];
+    uint32_t* s_fnode = (uint32_t*)bow_smem;
+    int* s_foff = bow_smem + a.f_nnodes;
     const int lane = lane_id();
+    const bool lds_f = a.f_nnodes <= kBowLdsNodes;
+    if (lds_f) {
+        for (int i = threadIdx.x; i < a.f_nnodes; i += blockDim.x) s_fnode[i] = a.f_node[i];
+        for (int i = threadIdx.x; i <= a.f_nnodes; i += blockDim.x) s_foff[i] = a.f_off[i];
+    }
+    __syncthreads();
+    const uint32_t* fnode = lds_f ? s_fnode : a.f_node;
+    const int* foff = lds_f ? s_foff : a.f_off;
+    // each wave owns a contiguous run of KF nodes: one pair search per run, the
+    // pair advanced incrementally (KF nodes of consecutive keyframes are adjacent)
     const long long total = a.node_off[a.npairs];
-    for (long long g = (long long)blockIdx.x * 4 + wave_id(); g < total; g += (long long)gridDim.x * 4) {
-        int lo = 0, hi = a.npairs;                       // pair: last pr with node_off[pr] <= g
+    const long long nw = (long long)gridDim.x * 4, w = (long long)blockIdx.x * 4 + wave_id();
+    const long long per = (total + nw - 1) / nw;
+    const long long g0 = w * per, g1 = min(total, g0 + per);
+    if (g0 >= g1) return;
+    int pr;
+    {
+        int lo = 0, hi = a.npairs;                       // last pr with node_off[pr] <= g0
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (a.node_off[mid] <= g) lo = mid;
+            if (a.node_off[mid] <= g0) lo = mid;
             else hi = mid;
         }
-        const int pr = lo;
+        pr = lo;
+    }
+    long long pr_end = a.node_off[pr + 1];
+    for (long long g = g0; g < g1; ++g) {
+        while (g >= pr_end) { ++pr; pr_end = a.node_off[pr + 1]; }
         const int ia = (int)(g - a.node_off[pr]);
         const uint32_t na = a.kf_node[g];
         int fl = 0, fh = a.f_nnodes;                     // lower_bound of na in F's node ids
         while (fl < fh) {
             const int mid = (fl + fh) >> 1;
-            if (a.f_node[mid] < na) fl = mid + 1;
+            if (fnode[mid] < na) fl = mid + 1;
             else fh = mid;
         }
-        if (fl >= a.f_nnodes || a.f_node[fl] != na) continue;
+        if (fl >= a.f_nnodes || fnode[fl] != na) continue;
         const long long kpo = a.kp_off[pr];
         const orb_keypoint* KK = a.kf_kps + kpo;
         const uint8_t* KD = a.kf_desc + kpo * 32;
         const uint8_t* KV = a.kf_valid + kpo;
         const int* ko = a.kf_off + a.node_off[pr] + pr;
         const uint32_t* ki = a.kf_idx + a.idx_off[pr];
-        const int fb = a.f_off[fl], fe = a.f_off[fl + 1];
+        const int fb = foff[fl], fe = foff[fl + 1];
         const int nch = (fe - fb + kWave - 1) / kWave;
         int32_t* match = a.match + (long long)pr * a.f_n;
         const bool fish = a.f_nleft >= 0;
-        // chunk 0 of the node's F features stays in registers across the KF features
-        uint4 f0 = make_uint4(0, 0, 0, 0), f1 = f0;
-        int fi0 = -1;
+        // the first kBowRegChunks chunks of the node's F features stay in registers
+        uint4 fr0[kBowRegChunks], fr1[kBowRegChunks];
+        int fir[kBowRegChunks];
         uint64_t taken = 0;                              // bit c: (chunk c, this lane) is matched / invalid
-        for (int c = 0; c < nch; ++c) {
+#pragma unroll
+        for (int c = 0; c < kBowRegChunks; ++c) {
+            fr0[c] = make_uint4(0, 0, 0, 0); fr1[c] = fr0[c]; fir[c] = -1;
             const int q = fb + c * kWave + lane;
-            if (c >= kBowMaskChunks) break;
-            if (q < fe) {
+            if (c < nch && q < fe) {
                 const int fi = (int)a.f_idx[q];
-                if (a.f_valid && !a.f_valid[fi]) taken |= 1ull << c;
-                if (c == 0) {
-                    fi0 = fi;
-                    f0 = *(const uint4*)(a.f_desc + (long long)fi * 32);
-                    f1 = *(const uint4*)(a.f_desc + (long long)fi * 32 + 16);
-                }
+                fir[c] = fi;
+                fr0[c] = *(const uint4*)(a.f_desc + (long long)fi * 32);
+                fr1[c] = *(const uint4*)(a.f_desc + (long long)fi * 32 + 16);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kBowRegChunks; ++c) {
+            if (fir[c] < 0) taken |= 1ull << c;                               // past the node's end
+            else if (a.f_valid && !a.f_valid[fir[c]]) taken |= 1ull << c;
+        }
+        for (int c = kBowRegChunks; c < nch && c < kBowMaskChunks; ++c) {
+            const int q = fb + c * kWave + lane;
+            if (q < fe) {
+                if (a.f_valid && !a.f_valid[(int)a.f_idx[q]]) taken |= 1ull << c;
             } else {
                 taken |= 1ull << c;
             }
@@ -721,21 +757,26 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
             q1.z = __builtin_amdgcn_readlane(mq1.z, src); q1.w = __builtin_amdgcn_readlane(mq1.w, src);
             // left (or only) track st; right track sr when the frame is fisheye stereo (:296-323)
             Best2 st{256, 256, -1, 0, 0}, sr{256, 256, -1, 0, 0};
-            for (int c = 0; c < nch; ++c) {
+            auto dist_reg = [&](const uint4& f0, const uint4& f1) {
+                return __popc(q0.x ^ f0.x) + __popc(q0.y ^ f0.y) + __popc(q0.z ^ f0.z) + __popc(q0.w ^ f0.w) +
+                       __popc(q1.x ^ f1.x) + __popc(q1.y ^ f1.y) + __popc(q1.z ^ f1.z) + __popc(q1.w ^ f1.w);
+            };
+#pragma unroll
+            for (int c = 0; c < kBowRegChunks; ++c) {            // register chunks
+                if (c >= nch) break;
+                int d = INT_MAX;
+                const int fi = fir[c];
+                if (!((taken >> c) & 1)) d = dist_reg(fr0[c], fr1[c]);
+                const bool right = fish && fi >= a.f_nleft;
+                merge_chunk(st, right ? INT_MAX : d, c * kWave + lane, 0);
+                if (fish) merge_chunk(sr, right ? d : INT_MAX, c * kWave + lane, 0);
+            }
+            for (int c = kBowRegChunks; c < nch; ++c) {
                 int d = INT_MAX, fi = -1;
                 const int q = fb + c * kWave + lane;
-                if (c == 0) fi = fi0;
-                else if (q < fe) fi = (int)a.f_idx[q];
+                if (q < fe) fi = (int)a.f_idx[q];
                 if (c < kBowMaskChunks) {
-                    if (!((taken >> c) & 1)) {
-                        if (c == 0) {
-                            d = __popc(q0.x ^ f0.x) + __popc(q0.y ^ f0.y) + __popc(q0.z ^ f0.z) +
-                                __popc(q0.w ^ f0.w) + __popc(q1.x ^ f1.x) + __popc(q1.y ^ f1.y) +
-                                __popc(q1.z ^ f1.z) + __popc(q1.w ^ f1.w);
-                        } else {
-                            d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
-                        }
-                    }
+                    if (!((taken >> c) & 1)) d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
                 } else if (q < fe) {
                     if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
                         d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
@@ -746,7 +787,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
             }
             auto claim = [&](int pos) {                  // pos: position in the node's F list
                 if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
-                const int fi = (pos < kWave) ? __shfl(fi0, pos, kWave) : (int)a.f_idx[fb + pos];
+                const int fi = (int)a.f_idx[fb + pos];
                 if (lane == 0) {
                     match[fi] = ikf;
                     if (a.check_ori) {
@@ -833,7 +874,7 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
     ORB_CHECK(hipMemsetAsync(a.hist, 0, nh * sizeof(int), st));
     ORB_CHECK(hipMemsetAsync(a.nmatches, 0, (size_t)npairs * sizeof(int32_t), st));
     const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, (long long)npairs * 32));
-    hipLaunchKernelGGL(k_bow_nodes, dim3(blocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_bow_nodes, dim3(blocks), dim3(256), bow_lds(a.f_nnodes), st, a);
     hipLaunchKernelGGL(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
