@@ -635,7 +635,7 @@ struct BowArgs {
     int f_nleft = -1;         // the frame's Nleft (-1: mono / rectified)
 };
 
-// One wave per KF FeatureVector node (all pairs flattened, grid-stride): the
+// One wave per (pair, vocabulary node) the two FeatureVectors share: the
 // reference's merge-join (:239-402) visits each node both FeatureVectors hold
 // exactly once, and a node's matching reads and writes only that node's
 // features, so nodes are independent.  Inside the node the KF features run in
@@ -643,18 +643,213 @@ struct BowArgs {
 // "already matched" flags in a per-lane bit mask (chunks >= 64 of a node with
 // more than 4096 frame features read the flag from `match` itself: only this
 // wave touches the node's features).
+// Frame nodes of at most kBowRegChunks chunks run in k_bow_nodes with their F
+// descriptors in registers; larger ones (a vocabulary's skew puts hundreds of
+// features in a few nodes) run in k_bow_big, which stages the node's F
+// descriptors in LDS once and shares them between the block's keyframes.
 constexpr int kBowMaskChunks = 64;
 
 constexpr int kBowRegChunks = 2;        // frame-feature chunks held in registers per node
+static_assert(kBowRegChunks == 2, "bow_node's claim selects between two register chunks");
 constexpr int kBowLdsNodes = 4096;      // frame FeatureVector nodes staged in LDS (dynamic size)
+constexpr int kBowBigCap = 512;         // k_bow_big: node positions staged in LDS
+constexpr int kBowBigPairs = 4;         // k_bow_big: keyframes per block (one per wave)
 
 static size_t bow_lds(int f_nnodes) { return f_nnodes <= kBowLdsNodes ? (size_t)(2 * f_nnodes + 1) * 4 : 0; }
 
+// Best / second over a BoW node's frame features for one KF feature.  A
+// candidate is the key dist << 22 | position (unique; ordered like the
+// reference's stream: the first position of the smallest distance is the best,
+// and bestDist2 is the second smallest distance of the multiset).  Each lane
+// folds its chunks into a local (smallest, second) pair; two DPP minima finish:
+// the chunk-independent work has no serial dependency between chunks.
+__device__ __forceinline__ void key_push(int& lo, int& hi, int key) {
+    hi = min(hi, max(lo, key));
+    lo = min(lo, key);
+}
+__device__ __forceinline__ Best2 key_best2(int lo, int hi) {
+    Best2 st{256, 256, -1, 0, 0};
+    const int m = wave_min(lo, INT_MAX);
+    if (m == INT_MAX) return st;
+    const int m2 = wave_min(lane_id() == (m & (kWave - 1)) ? hi : lo, INT_MAX);
+    st.best = m >> 22; st.idx = m & ((1 << 22) - 1);
+    st.best2 = m2 == INT_MAX ? 256 : m2 >> 22;
+    return st;
+}
+
+// The merge-join step of one (pair, node): KF node ia of pair pr against the
+// frame node's positions [fb, fe).  kLds: positions < kBowBigCap come from the
+// block's LDS copy (s_fd descriptor bytes 0-15 at [pos], 16-31 at
+// [kBowBigCap + pos]; s_fi frame index | invalid << 31; s_fa angle);
+// otherwise the first kBowRegChunks chunks are loaded into registers.  Anything
+// past either reads global memory.
+template <bool kLds>
+__device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
+                                         const uint4* s_fd, const int* s_fi, const float* s_fa) {
+    const int lane = lane_id();
+    const long long kpo = a.kp_off[pr];
+    const orb_keypoint* KK = a.kf_kps + kpo;
+    const uint8_t* KD = a.kf_desc + kpo * 32;
+    const uint8_t* KV = a.kf_valid + kpo;
+    const int* ko = a.kf_off + a.node_off[pr] + pr;
+    const uint32_t* ki = a.kf_idx + a.idx_off[pr];
+    const int nf = fe - fb;
+    const int nch = (nf + kWave - 1) / kWave;
+    int32_t* match = a.match + (long long)pr * a.f_n;
+    const bool fish = a.f_nleft >= 0;
+    constexpr int kReg = kLds ? 0 : kBowRegChunks;
+    const int nlds = kLds ? min(nch, kBowBigCap / kWave) : 0;   // chunks [0, nlds) in LDS
+    uint4 fr0[kBowRegChunks], fr1[kBowRegChunks];
+    int fir[kBowRegChunks];
+    float far_[kBowRegChunks];                       // the F feature's angle (rotation bin of a claim)
+    uint64_t taken = 0;                              // bit c: (chunk c, this lane) is matched / invalid
+    if constexpr (!kLds) {
+#pragma unroll
+        for (int c = 0; c < kBowRegChunks; ++c) {
+            fr0[c] = make_uint4(0, 0, 0, 0); fr1[c] = fr0[c]; fir[c] = -1; far_[c] = 0.f;
+            const int q = fb + c * kWave + lane;
+            if (c < nch && q < fe) {
+                const int fi = (int)a.f_idx[q];
+                fir[c] = fi;
+                far_[c] = a.f_kps[fi].angle;
+                fr0[c] = *(const uint4*)(a.f_desc + (long long)fi * 32);
+                fr1[c] = *(const uint4*)(a.f_desc + (long long)fi * 32 + 16);
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < kBowRegChunks; ++c) {
+            if (fir[c] < 0) taken |= 1ull << c;                               // past the node's end
+            else if (a.f_valid && !a.f_valid[fir[c]]) taken |= 1ull << c;
+        }
+    }
+    for (int c = kReg; c < nch && c < kBowMaskChunks; ++c) {
+        const int pos = c * kWave + lane;
+        if (pos >= nf) taken |= 1ull << c;
+        else if (c < nlds) { if (s_fi[pos] < 0) taken |= 1ull << c; }
+        else if (a.f_valid && !a.f_valid[(int)a.f_idx[fb + pos]]) taken |= 1ull << c;
+    }
+    int nm = 0;
+    // the node's KF features, 64 at a time, prefetched lane-parallel (index,
+    // MapPoint validity, descriptor, angle) and visited in order by readlane
+    const int pe = ko[ia + 1];
+    for (int pbase = ko[ia]; pbase < pe; pbase += kWave) {
+      const int pl = pbase + lane;
+      int my_ikf = 0, my_ok = 0;
+      uint4 mq0 = make_uint4(0, 0, 0, 0), mq1 = mq0;
+      float my_ang = 0.f;
+      if (pl < pe) {
+          my_ikf = (int)ki[pl];
+          my_ok = KV[my_ikf];
+          mq0 = *(const uint4*)(KD + (long long)my_ikf * 32);
+          mq1 = *(const uint4*)(KD + (long long)my_ikf * 32 + 16);
+          my_ang = KK[my_ikf].angle;
+      }
+      for (uint64_t rem = __ballot(my_ok != 0); rem; rem &= rem - 1) {
+        const int src = __ffsll((long long)rem) - 1;
+        const int ikf = __builtin_amdgcn_readlane(my_ikf, src);
+        const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), src));
+        uint4 q0, q1;
+        q0.x = __builtin_amdgcn_readlane(mq0.x, src); q0.y = __builtin_amdgcn_readlane(mq0.y, src);
+        q0.z = __builtin_amdgcn_readlane(mq0.z, src); q0.w = __builtin_amdgcn_readlane(mq0.w, src);
+        q1.x = __builtin_amdgcn_readlane(mq1.x, src); q1.y = __builtin_amdgcn_readlane(mq1.y, src);
+        q1.z = __builtin_amdgcn_readlane(mq1.z, src); q1.w = __builtin_amdgcn_readlane(mq1.w, src);
+        // left (or only) track; right track when the frame is fisheye stereo (:296-323)
+        int klo = INT_MAX, khi = INT_MAX, rlo = INT_MAX, rhi = INT_MAX;
+        // branch-free (INT_MAX keys are no-ops; both tracks always pushed, so no
+        // reference to a track is ever selected at run time)
+        auto push_key = [&](int key, bool right) {
+            key_push(klo, khi, right ? INT_MAX : key);
+            key_push(rlo, rhi, right ? key : INT_MAX);
+        };
+        auto push = [&](int d, int pos, bool right) { push_key(d == INT_MAX ? INT_MAX : (d << 22) | pos, right); };
+        // key of a distance, INT_MAX when the lane's chunk-c bit is taken (arithmetic, no branch)
+        auto key_of = [&](int d, int pos, int c) {
+            const int tb = (int)((taken >> c) & 1);
+            return ((d << 22) | pos) | (-tb & INT_MAX);
+        };
+        auto dist_reg = [&](const uint4& f0, const uint4& f1) {
+            return __popc(q0.x ^ f0.x) + __popc(q0.y ^ f0.y) + __popc(q0.z ^ f0.z) + __popc(q0.w ^ f0.w) +
+                   __popc(q1.x ^ f1.x) + __popc(q1.y ^ f1.y) + __popc(q1.z ^ f1.z) + __popc(q1.w ^ f1.w);
+        };
+        if constexpr (!kLds) {
+#pragma unroll
+            for (int c = 0; c < kBowRegChunks; ++c) {            // register chunks
+                if (c >= nch) break;
+                push_key(key_of(dist_reg(fr0[c], fr1[c]), c * kWave + lane, c), fish && fir[c] >= a.f_nleft);
+            }
+        } else {
+            // LDS chunks (k_bow_big): positions past the node's end are taken, so
+            // whatever the staging area holds there is never a candidate
+#pragma unroll 2
+            for (int c = 0; c < nlds; ++c) {
+                const int pos = c * kWave + lane;
+                const uint4 f0 = s_fd[pos], f1 = s_fd[kBowBigCap + pos];
+                push_key(key_of(dist_reg(f0, f1), pos, c), fish && (s_fi[pos] & 0x7fffffff) >= a.f_nleft);
+            }
+        }
+        for (int c = kLds ? nlds : kReg; c < nch; ++c) {     // global memory
+            int d = INT_MAX, fi = -1;
+            const int pos = c * kWave + lane;
+            {
+                if (pos < nf) fi = (int)a.f_idx[fb + pos];
+                if (c < kBowMaskChunks) {
+                    if (!((taken >> c) & 1)) d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
+                } else if (pos < nf) {
+                    if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
+                        d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
+                }
+            }
+            push(d, pos, fish && fi >= a.f_nleft);
+        }
+        const Best2 st = key_best2(klo, khi);
+        const Best2 sr = fish ? key_best2(rlo, rhi) : Best2{256, 256, -1, 0, 0};
+        auto claim = [&](int pos) {                  // pos: position in the node's F list
+            if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
+            // frame index and angle without a global round trip where they are staged
+            int fi;
+            float fang;
+            if (kLds && pos < kBowBigCap) {
+                fi = s_fi[pos] & 0x7fffffff;
+                fang = s_fa[pos];
+            } else if (!kLds && pos < kBowRegChunks * kWave) {
+                const int c = pos >> 6, l = pos & (kWave - 1);
+                fi = __builtin_amdgcn_readlane(c == 0 ? fir[0] : fir[kBowRegChunks - 1], l);
+                fang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
+                    __builtin_bit_cast(int, c == 0 ? far_[0] : far_[kBowRegChunks - 1]), l));
+            } else {
+                fi = (int)a.f_idx[fb + pos];
+                fang = a.check_ori ? a.f_kps[fi].angle : 0.f;
+            }
+            if (lane == 0) {
+                match[fi] = ikf;
+                if (a.check_ori) {
+                    const int bn = rot_bin(kang, fang);
+                    atomicAdd(&a.hist[pr * 32 + bn], 1);
+                    a.fbin[(long long)pr * a.f_n + fi] = (int8_t)bn;
+                }
+            }
+            ++nm;
+            if (nch > kBowMaskChunks) {              // the flag lives in `match` (global memory)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+        };
+        const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;     // :848 / :327
+        if (low && (float)st.best < a.ratio * (float)st.best2) claim(st.idx);
+        if (fish && low && sr.best <= kThLow) claim(sr.idx);                   // :357-386, ratio ignored
+      }
+    }
+    if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
+}
+
+// Small frame nodes: each wave owns a contiguous run of KF nodes (all pairs
+// flattened), one pair search per run, the pair advanced incrementally (KF
+// nodes of consecutive keyframes are adjacent).
 __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
     extern __shared__ __attribute__((aligned(16))) int bow_smem[];
     uint32_t* s_fnode = (uint32_t*)bow_smem;
     int* s_foff = bow_smem + a.f_nnodes;
-    const int lane = lane_id();
     const bool lds_f = a.f_nnodes <= kBowLdsNodes;
     if (lds_f) {
         for (int i = threadIdx.x; i < a.f_nnodes; i += blockDim.x) s_fnode[i] = a.f_node[i];
@@ -663,8 +858,6 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
     __syncthreads();
     const uint32_t* fnode = lds_f ? s_fnode : a.f_node;
     const int* foff = lds_f ? s_foff : a.f_off;
-    // each wave owns a contiguous run of KF nodes: one pair search per run, the
-    // pair advanced incrementally (KF nodes of consecutive keyframes are adjacent)
     const long long total = a.node_off[a.npairs];
     const long long nw = (long long)gridDim.x * 4, w = (long long)blockIdx.x * 4 + wave_id();
     const long long per = (total + nw - 1) / nw;
@@ -683,7 +876,6 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
     long long pr_end = a.node_off[pr + 1];
     for (long long g = g0; g < g1; ++g) {
         while (g >= pr_end) { ++pr; pr_end = a.node_off[pr + 1]; }
-        const int ia = (int)(g - a.node_off[pr]);
         const uint32_t na = a.kf_node[g];
         int fl = 0, fh = a.f_nnodes;                     // lower_bound of na in F's node ids
         while (fl < fh) {
@@ -692,123 +884,44 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
             else fh = mid;
         }
         if (fl >= a.f_nnodes || fnode[fl] != na) continue;
-        const long long kpo = a.kp_off[pr];
-        const orb_keypoint* KK = a.kf_kps + kpo;
-        const uint8_t* KD = a.kf_desc + kpo * 32;
-        const uint8_t* KV = a.kf_valid + kpo;
-        const int* ko = a.kf_off + a.node_off[pr] + pr;
-        const uint32_t* ki = a.kf_idx + a.idx_off[pr];
         const int fb = foff[fl], fe = foff[fl + 1];
-        const int nch = (fe - fb + kWave - 1) / kWave;
-        int32_t* match = a.match + (long long)pr * a.f_n;
-        const bool fish = a.f_nleft >= 0;
-        // the first kBowRegChunks chunks of the node's F features stay in registers
-        uint4 fr0[kBowRegChunks], fr1[kBowRegChunks];
-        int fir[kBowRegChunks];
-        uint64_t taken = 0;                              // bit c: (chunk c, this lane) is matched / invalid
-#pragma unroll
-        for (int c = 0; c < kBowRegChunks; ++c) {
-            fr0[c] = make_uint4(0, 0, 0, 0); fr1[c] = fr0[c]; fir[c] = -1;
-            const int q = fb + c * kWave + lane;
-            if (c < nch && q < fe) {
-                const int fi = (int)a.f_idx[q];
-                fir[c] = fi;
-                fr0[c] = *(const uint4*)(a.f_desc + (long long)fi * 32);
-                fr1[c] = *(const uint4*)(a.f_desc + (long long)fi * 32 + 16);
-            }
+        if (fe - fb > kBowRegChunks * kWave) continue;  // k_bow_big's
+        bow_node<false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr);
+    }
+}
+
+// Large frame nodes: block = kBowBigPairs consecutive keyframes; for each frame
+// node of more than kBowRegChunks chunks the block stages the node's F
+// descriptors in LDS, then wave w finds the node in keyframe w's FeatureVector.
+__global__ __launch_bounds__(256) void k_bow_big(BowArgs a) {
+    __shared__ uint4 s_fd[2 * kBowBigCap];
+    __shared__ int s_fi[kBowBigCap];
+    __shared__ float s_fa[kBowBigCap];
+    const int pr = blockIdx.x * kBowBigPairs + wave_id();
+    long long k0 = 0, k1 = 0;
+    if (pr < a.npairs) { k0 = a.node_off[pr]; k1 = a.node_off[pr + 1]; }
+    for (int fl = 0; fl < a.f_nnodes; ++fl) {
+        const int fb = a.f_off[fl], fe = a.f_off[fl + 1];
+        if (fe - fb <= kBowRegChunks * kWave) continue;              // uniform over the block
+        __syncthreads();                                             // previous node's readers done
+        const int ns = min(fe - fb, kBowBigCap);
+        for (int p = threadIdx.x; p < ns; p += blockDim.x) {
+            const int fi = (int)a.f_idx[fb + p];
+            const uint4* src = (const uint4*)(a.f_desc + (long long)fi * 32);
+            s_fd[p] = src[0];
+            s_fd[kBowBigCap + p] = src[1];
+            s_fi[p] = fi | ((a.f_valid && !a.f_valid[fi]) ? (int)0x80000000u : 0);
+            s_fa[p] = a.f_kps[fi].angle;
         }
-#pragma unroll
-        for (int c = 0; c < kBowRegChunks; ++c) {
-            if (fir[c] < 0) taken |= 1ull << c;                               // past the node's end
-            else if (a.f_valid && !a.f_valid[fir[c]]) taken |= 1ull << c;
+        __syncthreads();
+        const uint32_t na = a.f_node[fl];
+        long long lo = k0, hi = k1;                                  // lower_bound in KF pr's nodes
+        while (lo < hi) {
+            const long long mid = (lo + hi) >> 1;
+            if (a.kf_node[mid] < na) lo = mid + 1;
+            else hi = mid;
         }
-        for (int c = kBowRegChunks; c < nch && c < kBowMaskChunks; ++c) {
-            const int q = fb + c * kWave + lane;
-            if (q < fe) {
-                if (a.f_valid && !a.f_valid[(int)a.f_idx[q]]) taken |= 1ull << c;
-            } else {
-                taken |= 1ull << c;
-            }
-        }
-        int nm = 0;
-        // the node's KF features, 64 at a time, prefetched lane-parallel (index,
-        // MapPoint validity, descriptor, angle) and visited in order by readlane
-        const int pe = ko[ia + 1];
-        for (int pbase = ko[ia]; pbase < pe; pbase += kWave) {
-          const int pl = pbase + lane;
-          int my_ikf = 0, my_ok = 0;
-          uint4 mq0 = make_uint4(0, 0, 0, 0), mq1 = mq0;
-          float my_ang = 0.f;
-          if (pl < pe) {
-              my_ikf = (int)ki[pl];
-              my_ok = KV[my_ikf];
-              mq0 = *(const uint4*)(KD + (long long)my_ikf * 32);
-              mq1 = *(const uint4*)(KD + (long long)my_ikf * 32 + 16);
-              my_ang = KK[my_ikf].angle;
-          }
-          for (uint64_t rem = __ballot(my_ok != 0); rem; rem &= rem - 1) {
-            const int src = __ffsll((long long)rem) - 1;
-            const int ikf = __builtin_amdgcn_readlane(my_ikf, src);
-            const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), src));
-            uint4 q0, q1;
-            q0.x = __builtin_amdgcn_readlane(mq0.x, src); q0.y = __builtin_amdgcn_readlane(mq0.y, src);
-            q0.z = __builtin_amdgcn_readlane(mq0.z, src); q0.w = __builtin_amdgcn_readlane(mq0.w, src);
-            q1.x = __builtin_amdgcn_readlane(mq1.x, src); q1.y = __builtin_amdgcn_readlane(mq1.y, src);
-            q1.z = __builtin_amdgcn_readlane(mq1.z, src); q1.w = __builtin_amdgcn_readlane(mq1.w, src);
-            // left (or only) track st; right track sr when the frame is fisheye stereo (:296-323)
-            Best2 st{256, 256, -1, 0, 0}, sr{256, 256, -1, 0, 0};
-            auto dist_reg = [&](const uint4& f0, const uint4& f1) {
-                return __popc(q0.x ^ f0.x) + __popc(q0.y ^ f0.y) + __popc(q0.z ^ f0.z) + __popc(q0.w ^ f0.w) +
-                       __popc(q1.x ^ f1.x) + __popc(q1.y ^ f1.y) + __popc(q1.z ^ f1.z) + __popc(q1.w ^ f1.w);
-            };
-#pragma unroll
-            for (int c = 0; c < kBowRegChunks; ++c) {            // register chunks
-                if (c >= nch) break;
-                int d = INT_MAX;
-                const int fi = fir[c];
-                if (!((taken >> c) & 1)) d = dist_reg(fr0[c], fr1[c]);
-                const bool right = fish && fi >= a.f_nleft;
-                merge_chunk(st, right ? INT_MAX : d, c * kWave + lane, 0);
-                if (fish) merge_chunk(sr, right ? d : INT_MAX, c * kWave + lane, 0);
-            }
-            for (int c = kBowRegChunks; c < nch; ++c) {
-                int d = INT_MAX, fi = -1;
-                const int q = fb + c * kWave + lane;
-                if (q < fe) fi = (int)a.f_idx[q];
-                if (c < kBowMaskChunks) {
-                    if (!((taken >> c) & 1)) d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
-                } else if (q < fe) {
-                    if (match[fi] < 0 && (!a.f_valid || a.f_valid[fi]))
-                        d = hamming32(q0, q1, a.f_desc + (long long)fi * 32);
-                }
-                const bool right = fish && fi >= a.f_nleft;
-                merge_chunk(st, right ? INT_MAX : d, c * kWave + lane, 0);
-                if (fish) merge_chunk(sr, right ? d : INT_MAX, c * kWave + lane, 0);
-            }
-            auto claim = [&](int pos) {                  // pos: position in the node's F list
-                if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
-                const int fi = (int)a.f_idx[fb + pos];
-                if (lane == 0) {
-                    match[fi] = ikf;
-                    if (a.check_ori) {
-                        const int bn = rot_bin(kang, a.f_kps[fi].angle);
-                        atomicAdd(&a.hist[pr * 32 + bn], 1);
-                        a.fbin[(long long)pr * a.f_n + fi] = (int8_t)bn;
-                    }
-                }
-                ++nm;
-                if (nch > kBowMaskChunks) {              // the flag lives in `match` (global memory)
-                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-                    __builtin_amdgcn_wave_barrier();
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-                }
-            };
-            const bool low = a.f_valid ? st.best < kThLow : st.best <= kThLow;     // :848 / :327
-            if (low && (float)st.best < a.ratio * (float)st.best2) claim(st.idx);
-            if (fish && low && sr.best <= kThLow) claim(sr.idx);                   // :357-386, ratio ignored
-          }
-        }
-        if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
+        if (lo < k1 && a.kf_node[lo] == na) bow_node<true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa);
     }
 }
 
@@ -873,8 +986,9 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
     ORB_CHECK(hipMemsetAsync(a.fbin, 0xff, (size_t)npairs * a.f_n, st));
     ORB_CHECK(hipMemsetAsync(a.hist, 0, nh * sizeof(int), st));
     ORB_CHECK(hipMemsetAsync(a.nmatches, 0, (size_t)npairs * sizeof(int32_t), st));
-    const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, (long long)npairs * 32));
+    const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, (long long)npairs * 8));
     hipLaunchKernelGGL(k_bow_nodes, dim3(blocks), dim3(256), bow_lds(a.f_nnodes), st, a);
+    hipLaunchKernelGGL(k_bow_big, dim3((npairs + kBowBigPairs - 1) / kBowBigPairs), dim3(256), 0, st, a);
     hipLaunchKernelGGL(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
