@@ -626,10 +626,10 @@ struct BowArgs {
     float ratio;
     int check_ori;
     int npairs;
-    int32_t* match;      // [pair][f_n]  (-1 before k_bow_nodes)
-    int32_t* nmatches;   // [pair]       (0 before k_bow_nodes)
+    int32_t* match;      // [pair][f_n]  (-1 before k_bow)
+    int32_t* nmatches;   // [pair]       (0 before k_bow)
     int8_t* fbin;        // [pair][f_n]  rotation bin of the match of F feature, -1 = none
-    int* hist;           // [pair][32]   (0 before k_bow_nodes)
+    int* hist;           // [pair][32]   (0 before k_bow)
     const uint8_t* f_valid;   // KF-KF form: pKF2 MapPoint != NULL && !isBad(), else NULL
     int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
     int f_nleft = -1;         // the frame's Nleft (-1: mono / rectified)
@@ -643,17 +643,17 @@ struct BowArgs {
 // "already matched" flags in a per-lane bit mask (chunks >= 64 of a node with
 // more than 4096 frame features read the flag from `match` itself: only this
 // wave touches the node's features).
-// Frame nodes of at most kBowRegChunks chunks run in k_bow_nodes with their F
+// Frame nodes of at most kBowRegChunks chunks run in k_bow's small-node blocks with their F
 // descriptors in registers; larger ones (a vocabulary's skew puts hundreds of
-// features in a few nodes) run in k_bow_big, which stages the node's F
-// descriptors in LDS once and shares them between the block's keyframes.
+// features in a few nodes) run in its large-node blocks, which stage the node's F
+// descriptors in LDS once and share them between the block's keyframes.
 constexpr int kBowMaskChunks = 64;
 
 constexpr int kBowRegChunks = 2;        // frame-feature chunks held in registers per node
 static_assert(kBowRegChunks == 2, "bow_node's claim selects between two register chunks");
 constexpr int kBowLdsNodes = 4096;      // frame FeatureVector nodes staged in LDS (dynamic size)
-constexpr int kBowBigCap = 512;         // k_bow_big: node positions staged in LDS
-constexpr int kBowBigPairs = 4;         // k_bow_big: keyframes per block (one per wave)
+constexpr int kBowBigCap = 512;         // large-node blocks: node positions staged in LDS
+constexpr int kBowBigPairs = 4;         // large-node blocks: keyframes per block (one per wave)
 
 static size_t bow_lds(int f_nnodes) { return f_nnodes <= kBowLdsNodes ? (size_t)(2 * f_nnodes + 1) * 4 : 0; }
 
@@ -683,7 +683,7 @@ __device__ __forceinline__ Best2 key_best2(int lo, int hi) {
 // [kBowBigCap + pos]; s_fi frame index | invalid << 31; s_fa angle);
 // otherwise the first kBowRegChunks chunks are loaded into registers.  Anything
 // past either reads global memory.
-template <bool kLds>
+template <bool kLds, bool kFish>
 __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
                                          const uint4* s_fd, const int* s_fi, const float* s_fa) {
     const int lane = lane_id();
@@ -696,7 +696,7 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
     const int nf = fe - fb;
     const int nch = (nf + kWave - 1) / kWave;
     int32_t* match = a.match + (long long)pr * a.f_n;
-    const bool fish = a.f_nleft >= 0;
+    constexpr bool fish = kFish;                     // the frame is fisheye stereo (f_nleft >= 0)
     constexpr int kReg = kLds ? 0 : kBowRegChunks;
     const int nlds = kLds ? min(nch, kBowBigCap / kWave) : 0;   // chunks [0, nlds) in LDS
     uint4 fr0[kBowRegChunks], fr1[kBowRegChunks];
@@ -758,8 +758,12 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
         // branch-free (INT_MAX keys are no-ops; both tracks always pushed, so no
         // reference to a track is ever selected at run time)
         auto push_key = [&](int key, bool right) {
-            key_push(klo, khi, right ? INT_MAX : key);
-            key_push(rlo, rhi, right ? key : INT_MAX);
+            if constexpr (kFish) {
+                key_push(klo, khi, right ? INT_MAX : key);
+                key_push(rlo, rhi, right ? key : INT_MAX);
+            } else {
+                key_push(klo, khi, key);
+            }
         };
         auto push = [&](int d, int pos, bool right) { push_key(d == INT_MAX ? INT_MAX : (d << 22) | pos, right); };
         // key of a distance, INT_MAX when the lane's chunk-c bit is taken (arithmetic, no branch)
@@ -778,7 +782,7 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
                 push_key(key_of(dist_reg(fr0[c], fr1[c]), c * kWave + lane, c), fish && fir[c] >= a.f_nleft);
             }
         } else {
-            // LDS chunks (k_bow_big): positions past the node's end are taken, so
+            // LDS chunks (large-node blocks): positions past the node's end are taken, so
             // whatever the staging area holds there is never a candidate
 #pragma unroll 2
             for (int c = 0; c < nlds; ++c) {
@@ -846,7 +850,7 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
 // Small frame nodes: each wave owns a contiguous run of KF nodes (all pairs
 // flattened), one pair search per run, the pair advanced incrementally (KF
 // nodes of consecutive keyframes are adjacent).
-__global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
+__device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nblocks) {
     extern __shared__ __attribute__((aligned(16))) int bow_smem[];
     uint32_t* s_fnode = (uint32_t*)bow_smem;
     int* s_foff = bow_smem + a.f_nnodes;
@@ -859,7 +863,7 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
     const uint32_t* fnode = lds_f ? s_fnode : a.f_node;
     const int* foff = lds_f ? s_foff : a.f_off;
     const long long total = a.node_off[a.npairs];
-    const long long nw = (long long)gridDim.x * 4, w = (long long)blockIdx.x * 4 + wave_id();
+    const long long nw = (long long)nblocks * 4, w = (long long)bid * 4 + wave_id();
     const long long per = (total + nw - 1) / nw;
     const long long g0 = w * per, g1 = min(total, g0 + per);
     if (g0 >= g1) return;
@@ -885,19 +889,17 @@ __global__ __launch_bounds__(256) void k_bow_nodes(BowArgs a) {
         }
         if (fl >= a.f_nnodes || fnode[fl] != na) continue;
         const int fb = foff[fl], fe = foff[fl + 1];
-        if (fe - fb > kBowRegChunks * kWave) continue;  // k_bow_big's
-        bow_node<false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr);
+        if (fe - fb > kBowRegChunks * kWave) continue;  // a large-node block's
+        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr);
+        else bow_node<false, false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr);
     }
 }
 
 // Large frame nodes: block = kBowBigPairs consecutive keyframes; for each frame
 // node of more than kBowRegChunks chunks the block stages the node's F
 // descriptors in LDS, then wave w finds the node in keyframe w's FeatureVector.
-__global__ __launch_bounds__(256) void k_bow_big(BowArgs a) {
-    __shared__ uint4 s_fd[2 * kBowBigCap];
-    __shared__ int s_fi[kBowBigCap];
-    __shared__ float s_fa[kBowBigCap];
-    const int pr = blockIdx.x * kBowBigPairs + wave_id();
+__device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, uint4* s_fd, int* s_fi, float* s_fa) {
+    const int pr = bid * kBowBigPairs + wave_id();
     long long k0 = 0, k1 = 0;
     if (pr < a.npairs) { k0 = a.node_off[pr]; k1 = a.node_off[pr + 1]; }
     for (int fl = 0; fl < a.f_nnodes; ++fl) {
@@ -921,8 +923,22 @@ __global__ __launch_bounds__(256) void k_bow_big(BowArgs a) {
             if (a.kf_node[mid] < na) lo = mid + 1;
             else hi = mid;
         }
-        if (lo < k1 && a.kf_node[lo] == na) bow_node<true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa);
+        if (lo < k1 && a.kf_node[lo] == na) {
+            if (a.f_nleft >= 0) bow_node<true, true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa);
+            else bow_node<true, false>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa);
+        }
     }
+}
+
+// One launch for both: blocks [0, big_blocks) take the large nodes (latency-
+// bound serial chains), the rest the small ones (VALU-bound), so the two
+// co-schedule on the CUs.
+__global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks) {
+    __shared__ uint4 s_fd[2 * kBowBigCap];
+    __shared__ int s_fi[kBowBigCap];
+    __shared__ float s_fa[kBowBigCap];
+    if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, s_fd, s_fi, s_fa);
+    else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks);
 }
 
 // Rotation-consistency filter (:404-422 / :884-902) and the KF-KF output, one
@@ -987,8 +1003,8 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
     ORB_CHECK(hipMemsetAsync(a.hist, 0, nh * sizeof(int), st));
     ORB_CHECK(hipMemsetAsync(a.nmatches, 0, (size_t)npairs * sizeof(int32_t), st));
     const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, (long long)npairs * 8));
-    hipLaunchKernelGGL(k_bow_nodes, dim3(blocks), dim3(256), bow_lds(a.f_nnodes), st, a);
-    hipLaunchKernelGGL(k_bow_big, dim3((npairs + kBowBigPairs - 1) / kBowBigPairs), dim3(256), 0, st, a);
+    const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs;
+    hipLaunchKernelGGL(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes), st, a, big_blocks);
     hipLaunchKernelGGL(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
