@@ -667,13 +667,18 @@ __device__ __forceinline__ void key_push(int& lo, int& hi, int key) {
     hi = min(hi, max(lo, key));
     lo = min(lo, key);
 }
+// kSecond: the caller reads best2 (only when best can pass TH_LOW: no claim is
+// possible otherwise, so the second reduction is skipped).
+template <bool kSecond>
 __device__ __forceinline__ Best2 key_best2(int lo, int hi) {
     Best2 st{256, 256, -1, 0, 0};
     const int m = wave_min(lo, INT_MAX);
     if (m == INT_MAX) return st;
-    const int m2 = wave_min(lane_id() == (m & (kWave - 1)) ? hi : lo, INT_MAX);
     st.best = m >> 22; st.idx = m & ((1 << 22) - 1);
-    st.best2 = m2 == INT_MAX ? 256 : m2 >> 22;
+    if (kSecond && st.best <= kThLow) {
+        const int m2 = wave_min(lane_id() == (m & (kWave - 1)) ? hi : lo, INT_MAX);
+        st.best2 = m2 == INT_MAX ? 256 : m2 >> 22;
+    }
     return st;
 }
 
@@ -685,7 +690,7 @@ __device__ __forceinline__ Best2 key_best2(int lo, int hi) {
 // past either reads global memory.
 template <bool kLds, bool kFish>
 __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
-                                         const uint4* s_fd, const int* s_fi, const float* s_fa) {
+                                         const uint4* s_fd, const int* s_fi, const float* s_fa, uint4* s_q) {
     const int lane = lane_id();
     const long long kpo = a.kp_off[pr];
     const orb_keypoint* KK = a.kf_kps + kpo;
@@ -744,15 +749,31 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
           mq1 = *(const uint4*)(KD + (long long)my_ikf * 32 + 16);
           my_ang = KK[my_ikf].angle;
       }
+      if constexpr (!kLds) {
+          // wave-private LDS copy: one KF descriptor is then two broadcast LDS
+          // reads instead of eight v_readlane (the small-node path is VALU-bound)
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // previous block's reads done
+          __builtin_amdgcn_wave_barrier();
+          s_q[lane] = mq0;
+          s_q[kWave + lane] = mq1;
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
       for (uint64_t rem = __ballot(my_ok != 0); rem; rem &= rem - 1) {
         const int src = __ffsll((long long)rem) - 1;
         const int ikf = __builtin_amdgcn_readlane(my_ikf, src);
         const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), src));
         uint4 q0, q1;
-        q0.x = __builtin_amdgcn_readlane(mq0.x, src); q0.y = __builtin_amdgcn_readlane(mq0.y, src);
-        q0.z = __builtin_amdgcn_readlane(mq0.z, src); q0.w = __builtin_amdgcn_readlane(mq0.w, src);
-        q1.x = __builtin_amdgcn_readlane(mq1.x, src); q1.y = __builtin_amdgcn_readlane(mq1.y, src);
-        q1.z = __builtin_amdgcn_readlane(mq1.z, src); q1.w = __builtin_amdgcn_readlane(mq1.w, src);
+        if constexpr (!kLds) {
+            q0 = s_q[src];
+            q1 = s_q[kWave + src];
+        } else {
+            q0.x = __builtin_amdgcn_readlane(mq0.x, src); q0.y = __builtin_amdgcn_readlane(mq0.y, src);
+            q0.z = __builtin_amdgcn_readlane(mq0.z, src); q0.w = __builtin_amdgcn_readlane(mq0.w, src);
+            q1.x = __builtin_amdgcn_readlane(mq1.x, src); q1.y = __builtin_amdgcn_readlane(mq1.y, src);
+            q1.z = __builtin_amdgcn_readlane(mq1.z, src); q1.w = __builtin_amdgcn_readlane(mq1.w, src);
+        }
         // left (or only) track; right track when the frame is fisheye stereo (:296-323)
         int klo = INT_MAX, khi = INT_MAX, rlo = INT_MAX, rhi = INT_MAX;
         // branch-free (INT_MAX keys are no-ops; both tracks always pushed, so no
@@ -805,8 +826,8 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
             }
             push(d, pos, fish && fi >= a.f_nleft);
         }
-        const Best2 st = key_best2(klo, khi);
-        const Best2 sr = fish ? key_best2(rlo, rhi) : Best2{256, 256, -1, 0, 0};
+        const Best2 st = key_best2<true>(klo, khi);
+        const Best2 sr = fish ? key_best2<false>(rlo, rhi) : Best2{256, 256, -1, 0, 0};   // ratio not applied
         auto claim = [&](int pos) {                  // pos: position in the node's F list
             if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
             // frame index and angle without a global round trip where they are staged
@@ -850,7 +871,7 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
 // Small frame nodes: each wave owns a contiguous run of KF nodes (all pairs
 // flattened), one pair search per run, the pair advanced incrementally (KF
 // nodes of consecutive keyframes are adjacent).
-__device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nblocks) {
+__device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nblocks, uint4* s_q) {
     extern __shared__ __attribute__((aligned(16))) int bow_smem[];
     uint32_t* s_fnode = (uint32_t*)bow_smem;
     int* s_foff = bow_smem + a.f_nnodes;
@@ -890,8 +911,8 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         if (fl >= a.f_nnodes || fnode[fl] != na) continue;
         const int fb = foff[fl], fe = foff[fl + 1];
         if (fe - fb > kBowRegChunks * kWave) continue;  // a large-node block's
-        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr);
-        else bow_node<false, false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr);
+        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr, s_q);
+        else bow_node<false, false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr, s_q);
     }
 }
 
@@ -924,21 +945,23 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, uint4* s
             else hi = mid;
         }
         if (lo < k1 && a.kf_node[lo] == na) {
-            if (a.f_nleft >= 0) bow_node<true, true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa);
-            else bow_node<true, false>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa);
+            if (a.f_nleft >= 0) bow_node<true, true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa, nullptr);
+            else bow_node<true, false>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa, nullptr);
         }
     }
 }
 
 // One launch for both: blocks [0, big_blocks) take the large nodes (latency-
 // bound serial chains), the rest the small ones (VALU-bound), so the two
-// co-schedule on the CUs.
+// co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private KF
+// descriptor areas (2 * 64 uint4 each).
+static_assert(2 * kBowBigCap >= 4 * 2 * kWave, "s_fd holds the small-node waves' descriptor areas");
 __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
     __shared__ float s_fa[kBowBigCap];
     if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, s_fd, s_fi, s_fa);
-    else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks);
+    else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 2 * kWave);
 }
 
 // Rotation-consistency filter (:404-422 / :884-902) and the KF-KF output, one
