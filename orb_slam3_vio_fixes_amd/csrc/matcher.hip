@@ -29,6 +29,11 @@
 
 namespace orbmi {
 
+// Host-API uploads are coalesced (h2d below): every other GPU operation of
+// this file flushes the pending copy first.
+static hipError_t flush_uploads();
+#define KLAUNCH(...) do { (void)flush_uploads(); hipLaunchKernelGGL(__VA_ARGS__); } while (0)
+
 constexpr int kGridCols = 64, kGridRows = 48;        // Frame.h:44-45
 constexpr int kThHigh = 100, kThLow = 50, kHisto = 30;   // ORBmatcher.cc:35-37
 constexpr int kGridInvalid = 0x7fff;
@@ -589,9 +594,9 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
 
 static void launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
-    hipLaunchKernelGGL(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
+    KLAUNCH(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
     const size_t lds_res = (size_t)a.cap * (20 + 4 * kTopK + 1) + 128 + 16;
-    hipLaunchKernelGGL(k_sfi_resolve, dim3(npairs), dim3(64), lds_res, st, a);
+    KLAUNCH(k_sfi_resolve, dim3(npairs), dim3(64), lds_res, st, a);
 }
 
 // ---------------------------------------------------------------------------
@@ -919,13 +924,20 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
 // Large frame nodes: block = kBowBigPairs consecutive keyframes; for each frame
 // node of more than kBowRegChunks chunks the block stages the node's F
 // descriptors in LDS, then wave w finds the node in keyframe w's FeatureVector.
-__device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, uint4* s_fd, int* s_fi, float* s_fa) {
-    const int pr = bid * kBowBigPairs + wave_id();
+// Block bid = (keyframe group, slot): the group's large nodes are dealt
+// round-robin over `slots` blocks (one slot per large node for a single pair,
+// where the host knows the frame's node sizes; one slot for a map).
+__device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slots, uint4* s_fd, int* s_fi,
+                                             float* s_fa) {
+    const int slot = bid % slots;
+    const int pr = (bid / slots) * kBowBigPairs + wave_id();
     long long k0 = 0, k1 = 0;
     if (pr < a.npairs) { k0 = a.node_off[pr]; k1 = a.node_off[pr + 1]; }
+    int nbig = 0;
     for (int fl = 0; fl < a.f_nnodes; ++fl) {
         const int fb = a.f_off[fl], fe = a.f_off[fl + 1];
         if (fe - fb <= kBowRegChunks * kWave) continue;              // uniform over the block
+        if (nbig++ % slots != slot) continue;
         __syncthreads();                                             // previous node's readers done
         const int ns = min(fe - fb, kBowBigCap);
         for (int p = threadIdx.x; p < ns; p += blockDim.x) {
@@ -956,11 +968,11 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, uint4* s
 // co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private KF
 // descriptor areas (2 * 64 uint4 each).
 static_assert(2 * kBowBigCap >= 4 * 2 * kWave, "s_fd holds the small-node waves' descriptor areas");
-__global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks) {
+__global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_slots) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
     __shared__ float s_fa[kBowBigCap];
-    if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, s_fd, s_fi, s_fa);
+    if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, big_slots, s_fd, s_fi, s_fa);
     else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 2 * kWave);
 }
 
@@ -1005,7 +1017,20 @@ struct BowScratch {
     ~BowScratch() { if (fbin) (void)hipFree(fbin); if (hist) (void)hipFree(hist); }
 };
 
-static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
+// The per-call state of k_bow in one launch (instead of four memsets).
+__global__ __launch_bounds__(256) void k_bow_init(BowArgs a) {
+    const long long nmf = (long long)a.npairs * a.f_n, stride = (long long)gridDim.x * blockDim.x;
+    const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    for (long long i = t0; i < nmf; i += stride) { a.match[i] = -1; a.fbin[i] = -1; }
+    for (long long i = t0; i < (long long)a.npairs * 32; i += stride) a.hist[i] = 0;
+    for (long long i = t0; i < a.npairs; i += stride) a.nmatches[i] = 0;
+}
+
+// big_slots: blocks per keyframe group for the large frame nodes (their count
+// when the host holds the frame's FeatureVector, else 1); kf_nodes: the KF
+// FeatureVector nodes in all when the host knows them (a single pair: one
+// wave per node, for latency), else -1.
+static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1, long long kf_nodes = -1) {
     static thread_local BowScratch sc;
     const size_t nf = (size_t)npairs * std::max(1, a.f_n), nh = (size_t)npairs * 32;
     if (sc.fbin_n < nf) {
@@ -1021,14 +1046,17 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st) {
         sc.hist_n = nh;
     }
     a.npairs = npairs; a.fbin = sc.fbin; a.hist = sc.hist;
-    ORB_CHECK(hipMemsetAsync(a.match, 0xff, (size_t)npairs * a.f_n * sizeof(int32_t), st));
-    ORB_CHECK(hipMemsetAsync(a.fbin, 0xff, (size_t)npairs * a.f_n, st));
-    ORB_CHECK(hipMemsetAsync(a.hist, 0, nh * sizeof(int), st));
-    ORB_CHECK(hipMemsetAsync(a.nmatches, 0, (size_t)npairs * sizeof(int32_t), st));
-    const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, (long long)npairs * 8));
-    const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs;
-    hipLaunchKernelGGL(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes), st, a, big_blocks);
-    hipLaunchKernelGGL(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
+    {
+        const long long nmf = (long long)npairs * a.f_n;
+        const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
+        KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
+    }
+    const long long want = kf_nodes >= 0 ? (kf_nodes + 3) / 4 : (long long)npairs * 8;
+    const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, want));
+    big_slots = std::max(1, big_slots);
+    const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs * big_slots;
+    KLAUNCH(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes), st, a, big_blocks, big_slots);
+    KLAUNCH(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
@@ -1908,19 +1936,45 @@ static Arena& host_stage() {
     static thread_local Arena* a = [] { Arena* x = new Arena(); x->pinned = true; return x; }();
     return *a;
 }
-static void arena_reset() { dev_arena().reset(); host_stage().reset(); }
 
-// H2D through pinned staging (asynchronous on the null stream), D2H through
-// pinned staging (synchronous).
+// H2D through pinned staging, asynchronous on the null stream and coalesced:
+// DBuf::put takes its device block and its staging block in lockstep from the
+// two bump arenas, so the uploads of one call are contiguous on both sides and
+// go as ONE copy (each hipMemcpyAsync costs microseconds of API time, and a
+// host API uploads a dozen arrays).  The pending run is issued before any other
+// GPU operation (KLAUNCH, memsets, downloads, direct copies, arena reset).
+struct PendingUpload { char* dst = nullptr; char* src = nullptr; size_t len = 0; };
+static PendingUpload& pending_upload() { static thread_local PendingUpload p; return p; }
+static size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
+static hipError_t flush_uploads() {
+    PendingUpload& p = pending_upload();
+    if (!p.len) return hipSuccess;
+    const hipError_t e = hipMemcpyAsync(p.dst, p.src, p.len, hipMemcpyHostToDevice, 0);
+    p = PendingUpload{};
+    return e;
+}
+// A run still pending at the next call's reset was never used by a GPU
+// operation: it is dropped (issuing it now would race the reused staging).
+static void arena_reset() { pending_upload() = PendingUpload{}; dev_arena().reset(); host_stage().reset(); }
+
 static hipError_t h2d(void* dst, const void* src, size_t bytes) {
     if (!bytes) return hipSuccess;
-    void* st = host_stage().get(bytes);
+    char* st = (char*)host_stage().get(bytes);
     if (!st) return hipErrorOutOfMemory;
     std::memcpy(st, src, bytes);
-    return hipMemcpyAsync(dst, st, bytes, hipMemcpyHostToDevice, 0);
+    PendingUpload& p = pending_upload();
+    if (p.len && (char*)dst == p.dst + round256(p.len) && st == p.src + round256(p.len)) {
+        p.len = (size_t)((char*)dst - p.dst) + bytes;          // extends the run (gaps are arena padding)
+        return hipSuccess;
+    }
+    const hipError_t e = flush_uploads();
+    p.dst = (char*)dst; p.src = st; p.len = bytes;
+    return e;
 }
+// D2H through pinned staging (synchronous).
 static hipError_t d2h(void* dst, const void* src, size_t bytes) {
     if (!bytes) return hipSuccess;
+    if (const hipError_t e = flush_uploads(); e != hipSuccess) return e;
     void* st = host_stage().get(bytes);
     if (!st) return hipErrorOutOfMemory;
     hipError_t e = hipMemcpyAsync(st, src, bytes, hipMemcpyDeviceToHost, 0);
@@ -1965,6 +2019,7 @@ struct PBuf {
     int put(const T* src, size_t cnt, hipStream_t st = 0) {
         int rc = alloc(cnt);
         if (rc) return rc;
+        if (flush_uploads() != hipSuccess) return ORB_ERR_DEVICE;
         if (cnt && hipMemcpyAsync(p, src, cnt * sizeof(T), hipMemcpyHostToDevice, st) != hipSuccess) return ORB_ERR_DEVICE;
         return ORB_OK;
     }
@@ -1999,13 +2054,13 @@ struct DevFrame {
         if (grid) {
             if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1)) || (rc = cs.alloc(kCells + 1))) return rc;
             if (grid_cs_lds(nn) <= 160 * 1024) {
-                hipLaunchKernelGGL(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), st, kps.p, n.p, nn,
+                KLAUNCH(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), st, kps.p, n.p, nn,
                                    grid_params(f), sorted.p, count.p, cs.p, (uint32_t*)nullptr, (int*)nullptr);
             } else {
                 const int sc = pow2_at_least(nn);
-                hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
+                KLAUNCH(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
                                    grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
-                hipLaunchKernelGGL(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
+                KLAUNCH(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
             }
         }
         return ORB_OK;
@@ -2068,10 +2123,10 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     DBuf<uint32_t> l0s; DBuf<int> l0c;
     if ((rc = l0s.alloc((size_t)2 * cap)) || (rc = l0c.alloc(2))) return rc;
     if (grid_cs_lds(cap) <= 160 * 1024)
-        hipLaunchKernelGGL(k_grid_cs, dim3(2), dim3(256), grid_cs_lds(cap), 0, kps.p, n.p, cap, g, sorted.p, count.p,
+        KLAUNCH(k_grid_cs, dim3(2), dim3(256), grid_cs_lds(cap), 0, kps.p, n.p, cap, g, sorted.p, count.p,
                            (int*)nullptr, l0s.p, l0c.p);
     else
-        hipLaunchKernelGGL(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p,
+        KLAUNCH(k_grid, dim3(2), dim3(256), sc * sizeof(uint32_t), 0, kps.p, n.p, cap, g, sorted.p,
                            count.p, sc, l0s.p, l0c.p);
     SfiArgs a;
     a.kps = kps.p; a.desc = desc.p; a.n = n.p; a.cap = cap; a.gsorted = l0s.p; a.gcount = l0c.p;
@@ -2109,16 +2164,17 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
         std::vector<int> idx(nframes);
         for (int i = 0; i < nframes; ++i) idx[i] = i;
         if ((rc = pf.put(idx.data(), nframes))) return rc;
+        ORB_CHECK(flush_uploads());
         ORB_CHECK(hipDeviceSynchronize());
         pf_frames = nframes;
     }
     const GridParams g{min_x, min_y, grid_inv_w, grid_inv_h};
     const int sc = pow2_at_least(cap);
     if (grid_cs_lds(cap) <= 160 * 1024)
-        hipLaunchKernelGGL(k_grid_cs, dim3(nframes), dim3(256), grid_cs_lds(cap), st, d_kps, d_n, cap, g, sorted.p,
+        KLAUNCH(k_grid_cs, dim3(nframes), dim3(256), grid_cs_lds(cap), st, d_kps, d_n, cap, g, sorted.p,
                            count.p, (int*)nullptr, l0s.p, l0c.p);
     else
-        hipLaunchKernelGGL(k_grid, dim3(nframes), dim3(256), sc * sizeof(uint32_t), st, d_kps, d_n, cap, g,
+        KLAUNCH(k_grid, dim3(nframes), dim3(256), sc * sizeof(uint32_t), st, d_kps, d_n, cap, g,
                            sorted.p, count.p, sc, l0s.p, l0c.p);
     SfiArgs a;
     a.kps = d_kps; a.desc = d_desc; a.n = d_n; a.cap = cap; a.gsorted = l0s.p; a.gcount = l0c.p;
@@ -2128,6 +2184,13 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     launch_sfi(a, nframes - 1, st);
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
+}
+
+// Frame nodes the large-node blocks take (host FeatureVector).
+static int bow_big_nodes(const orbm_featvec* fv) {
+    int n = 0;
+    for (int i = 0; i < fv->nnodes; ++i) n += fv->offsets[i + 1] - fv->offsets[i] > kBowRegChunks * kWave;
+    return n;
 }
 
 static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid, const orbm_frame* f,
@@ -2152,7 +2215,7 @@ static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
     a.f_nleft = f_nleft;
-    if ((rc = launch_bow(a, 1, 0))) return rc;
+    if ((rc = launch_bow(a, 1, 0, bow_big_nodes(ffv), kfv->nnodes))) return rc;
     int32_t res = 0;
     ORB_CHECK(d2h(&res, nm.p, 4));
     if (f->n) ORB_CHECK(d2h(match_f, m.p, f->n * 4));
@@ -2200,12 +2263,12 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     if (lds2 <= 160 * 1024 && !(force && force[0] == '1')) {
         DBuf<uint2> topk; DBuf<int> cnt;
         if ((rc = topk.alloc((size_t)std::max(1, a.nq) * kProjK)) || (rc = cnt.alloc(std::max(1, a.nq)))) return rc;
-        if (a.nq) hipLaunchKernelGGL(k_proj_topk, dim3((a.nq + 3) / 4), dim3(256), 0, 0, a, proj_bound(a), topk.p, cnt.p);
-        hipLaunchKernelGGL(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);
+        if (a.nq) KLAUNCH(k_proj_topk, dim3((a.nq + 3) / 4), dim3(256), 0, 0, a, proj_bound(a), topk.p, cnt.p);
+        KLAUNCH(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);
     } else {
         const size_t lds = proj_lds(a.nq);
         if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
-        hipLaunchKernelGGL(k_proj, dim3(1), dim3(64), lds, 0, a);
+        KLAUNCH(k_proj, dim3(1), dim3(64), lds, 0, a);
     }
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
@@ -2281,7 +2344,7 @@ int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
         (rc = wio.alloc(n)) || (rc = nio.alloc(n)))
         return rc;
     const int nid_level = voc->depth_levels - levelsup;
-    hipLaunchKernelGGL(k_transform, dim3((n + 255) / 256), dim3(256), 0, 0, fc.p, nc.p, voc->child_idx ? ci.p : nullptr,
+    KLAUNCH(k_transform, dim3((n + 255) / 256), dim3(256), 0, 0, fc.p, nc.p, voc->child_idx ? ci.p : nullptr,
                        nd.p, wid.p, wt.p, n, dd.p,
                        nid_level, wio.p, wo.p, nio.p);
     ORB_CHECK(hipGetLastError());
@@ -2315,7 +2378,7 @@ int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, cons
     a.valid = bval.p; a.u = bu.p; a.v = bv.p; a.ur = bur.p; a.level = blv.p; a.mdesc = bd.p; a.th = th; a.fma = fma;
     a.chi2 = 1; a.accept = kThLow;                                               // :1311
     a.best_idx = bi.p; a.best_dist = bdist.p;
-    hipLaunchKernelGGL(k_fuse, dim3((nmp + 3) / 4), dim3(256), 0, 0, a);
+    KLAUNCH(k_fuse, dim3((nmp + 3) / 4), dim3(256), 0, 0, a);
     ORB_CHECK(hipGetLastError());
     ORB_CHECK(d2h(best_idx, bi.p, nmp * sizeof(int32_t)));
     ORB_CHECK(d2h(best_dist, bdist.p, nmp * sizeof(int32_t)));
@@ -2370,8 +2433,8 @@ int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
     for (int k = 0; k < 9; ++k) ta.F[k] = F12[k];
     ta.ep_x = ep_x; ta.ep_y = ep_y; ta.only_stereo = only_stereo; ta.coarse = coarse; ta.fma = fma;
     ta.check_ori = check_ori; ta.item_match = bm.p; ta.item_bin = bbin.p;
-    if (nitems) hipLaunchKernelGGL(k_tri, dim3((nitems + 3) / 4), dim3(256), 0, 0, ta);
-    hipLaunchKernelGGL(k_tri_final, dim3(1), dim3(256), 0, 0, ta, kf1->n, out.p, nm.p);
+    if (nitems) KLAUNCH(k_tri, dim3((nitems + 3) / 4), dim3(256), 0, 0, ta);
+    KLAUNCH(k_tri_final, dim3(1), dim3(256), 0, 0, ta, kf1->n, out.p, nm.p);
     ORB_CHECK(hipGetLastError());
     int32_t n = 0;
     if (kf1->n) ORB_CHECK(d2h(matches12, out.p, kf1->n * sizeof(int32_t)));
@@ -2393,7 +2456,7 @@ int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const 
     DBuf<int32_t> bo, bb; DBuf<uint8_t> bd;
     if ((rc = bo.put(off, (size_t)npoints + 1)) || (rc = bd.put(desc, (size_t)total * 32)) || (rc = bb.alloc(npoints)))
         return rc;
-    hipLaunchKernelGGL(k_distinctive, dim3(npoints), dim3(64), 0, 0, npoints, bo.p, bd.p, bb.p);
+    KLAUNCH(k_distinctive, dim3(npoints), dim3(64), 0, 0, npoints, bo.p, bd.p, bb.p);
     ORB_CHECK(hipGetLastError());
     ORB_CHECK(d2h(best, bb.p, npoints * sizeof(int32_t)));
     return ORB_OK;
@@ -2430,7 +2493,7 @@ int orbm_search_by_bow_kf(const orbm_frame* kf1, const orbm_featvec* fv1, const 
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = kf2->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
     a.f_nnodes = fv2->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
     a.f_valid = fvv.p; a.out12 = o12.p;
-    if ((rc = launch_bow(a, 1, 0))) return rc;
+    if ((rc = launch_bow(a, 1, 0, bow_big_nodes(fv2), fv1->nnodes))) return rc;
     int32_t res = 0;
     ORB_CHECK(d2h(&res, nm.p, 4));
     if (kf1->n) ORB_CHECK(d2h(matches12, o12.p, kf1->n * 4));
@@ -2498,7 +2561,7 @@ static int best_in_area(const orbm_frame* kf, DevFrame& df, int nq, const uint8_
     a.g = grid_params(kf); a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p; a.nmp = nq;
     a.valid = bval.p; a.u = bu.p; a.v = bv.p; a.ur = nullptr; a.level = blv.p; a.mdesc = bdesc.p; a.th = th;
     a.fma = 0; a.chi2 = 0; a.accept = accept; a.best_idx = bi.p; a.best_dist = bd.p;
-    hipLaunchKernelGGL(k_fuse, dim3((nq + 3) / 4), dim3(256), 0, 0, a);
+    KLAUNCH(k_fuse, dim3((nq + 3) / 4), dim3(256), 0, 0, a);
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }
@@ -2557,10 +2620,11 @@ int orbm_search_by_sim3(const orbm_frame* kf1, const orbm_frame* kf2, const uint
                                de2)))
             return rc;
     } else {
+        ORB_CHECK(flush_uploads());
         ORB_CHECK(hipMemset(b2.p, 0xff, sizeof(int32_t)));
     }
     if ((rc = out.alloc(n1)) || (rc = nf.alloc(1))) return rc;
-    hipLaunchKernelGGL(k_sim3_agree, dim3(1), dim3(256), 0, 0, b1.p, n1, b2.p, out.p, nf.p);
+    KLAUNCH(k_sim3_agree, dim3(1), dim3(256), 0, 0, b1.p, n1, b2.p, out.p, nf.p);
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
     ORB_CHECK(d2h(matches12, out.p, n1 * sizeof(int32_t)));
@@ -2578,13 +2642,13 @@ static int grid_one(const orb_keypoint* kps_dev, const int* n_dev, int cnt, Grid
     const int nn = std::max(1, cnt);
     if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1)) || (rc = cs.alloc(kCells + 1))) return rc;
     if (grid_cs_lds(nn) <= 160 * 1024) {
-        hipLaunchKernelGGL(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), 0, kps_dev, n_dev, nn, g, sorted.p,
+        KLAUNCH(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), 0, kps_dev, n_dev, nn, g, sorted.p,
                            count.p, cs.p, (uint32_t*)nullptr, (int*)nullptr);
     } else {
         const int sc = pow2_at_least(nn);
-        hipLaunchKernelGGL(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), 0, kps_dev, n_dev, nn, g, sorted.p,
+        KLAUNCH(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), 0, kps_dev, n_dev, nn, g, sorted.p,
                            count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
-        hipLaunchKernelGGL(k_cell_start, dim3(1), dim3(256), 0, 0, sorted.p, count.p, nn, cs.p);
+        KLAUNCH(k_cell_start, dim3(1), dim3(256), 0, 0, sorted.p, count.p, nn, cs.p);
     }
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
@@ -2612,7 +2676,7 @@ static int run_fisheye(ProjArgs& a, FishArgs& fa, const orbm_frame* f, int nleft
     fa.nleft = nleft; fa.gs_l = gl.p; fa.gs_r = gr.p; fa.cs_l = csl.p; fa.cs_r = csr.p;
     const size_t lds = (size_t)(32 + 2 * a.nq + 1) * 4 + 64;
     if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;
-    hipLaunchKernelGGL(k_proj_fisheye, dim3(1), dim3(64), lds, 0, a, fa);
+    KLAUNCH(k_proj_fisheye, dim3(1), dim3(64), lds, 0, a, fa);
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
     ORB_CHECK(d2h(&res, nm.p, 4));
