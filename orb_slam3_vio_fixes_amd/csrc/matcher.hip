@@ -1573,6 +1573,148 @@ __global__ __launch_bounds__(64) void k_proj_resolve(ProjArgs a, const uint2* __
     if (lane == 0) a.nmatches[0] = nm;
 }
 
+// Speculative form of phase 2 (the default): one wave, lane = query of a
+// 64-query block.  Each round every unresolved lane decides against the slot
+// state at the round's start.  A lane's decision is the reference's when no
+// earlier lane of the round claims, blocking, a slot on its list (an earlier
+// non-blocking claim changes no one's candidates), so the longest prefix of
+// lanes without such an overlap commits: overlaps are found with a per-slot
+// mark (ds_min of the claiming lane); repeated claims of one slot resolve to
+// the last lane through the same table (the later query owns it, as in the
+// serial loop).
+// The first lane after the prefix starts the next round; if its truncated list
+// ran dry the wave rescans it exactly at that point.  Every round commits at
+// least its first lane.  Candidate lists of different queries rarely share a
+// slot within the decision bound, so a block usually commits in one round.
+// LDS: the k_proj_resolve layout + mark[n].
+static size_t proj_spec_lds(int n, int nq) { return proj_resolve_lds(n, nq) + (size_t)n * 4 + 16; }
+
+__global__ __launch_bounds__(64) void k_proj_resolve_spec(ProjArgs a, const uint2* __restrict__ topk,
+                                                          const int* __restrict__ cnt) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int lane = lane_id();
+    int* hist = lds;                          // 32
+    int* own = lds + 32;                      // n
+    int* hent = own + a.n;                    // nq
+    int* mark = hent + a.nq + 1;              // n: first lane of the round claiming the slot (64: none)
+    uint8_t* bl = (uint8_t*)(mark + a.n);     // n
+    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
+#pragma unroll 8
+    for (int i = lane; i < a.n; i += kWave) {
+        const int o = a.owner[i];
+        own[i] = o;
+        mark[i] = kWave;
+        bl[i] = o == -1 ? 0 : (a.skip_any ? 1 : (o <= -2 ? a.blocked[i] : a.qhas_obs[o]));
+    }
+    __syncthreads();
+    const int mode = a.mode, skip_any = a.skip_any, ori = a.mode == 1 && a.check_ori, nq = a.nq;
+    const float ratio = a.ratio, accept = a.accept;
+    const uint64_t lt = (1ull << lane) - 1;                                // lanes below this one
+    int nm = 0, nh = 0;
+    const int nblk = (nq + kWave - 1) / kWave;
+    for (int blk = 0; blk < nblk; ++blk) {
+        const int i = blk * kWave + lane;
+        const bool inq = i < nq;
+        const int ci = inq ? cnt[i] : -1;
+        uint2 E[kProjK];
+#pragma unroll
+        for (int k = 0; k < kProjK; ++k) E[k] = inq ? topk[(long long)i * kProjK + k] : make_uint2(0xffffffffu, 0);
+        const int hob = skip_any ? 1 : (inq ? a.qhas_obs[i] : 0);
+        const int nl = min(ci, kProjK);                                    // listed entries
+        bool done = ci <= 0;
+        while (__ballot(!done)) {
+            // tentative decision under the round's starting state
+            Best2 st{256, 256, -1, -1, -1};
+            int bin = 0, nav = 0;
+#pragma unroll
+            for (int k = 0; k < kProjK; ++k) {
+                if (k < nl) {
+                    const int s = (int)(E[k].x & 0xffff);
+                    if (!bl[s]) {
+                        if (nav == 0) {
+                            st.best = (int)(E[k].x >> 24); st.lvl = (int)((E[k].x >> 16) & 0xff); st.idx = s;
+                            bin = (int)E[k].y;
+                        } else if (nav == 1) {
+                            st.best2 = (int)(E[k].x >> 24); st.lvl2 = (int)((E[k].x >> 16) & 0xff);
+                        }
+                        ++nav;
+                    }
+                }
+            }
+            const bool exact = ci <= kProjK || nav >= 2 || (mode == 1 && nav == 1);
+            bool acc;
+            if (mode == 0) acc = st.best <= kThHigh && !(st.lvl == st.lvl2 && (float)st.best > ratio * (float)st.best2);
+            else acc = st.idx >= 0 && (float)st.best <= accept;
+            acc = acc && !done && exact;
+            const bool blocking = acc && hob;
+            if (blocking) atomicMin(&mark[st.idx], lane);
+            lds_order();
+            bool conflict = false;
+#pragma unroll
+            for (int k = 0; k < kProjK; ++k)
+                if (k < nl && mark[(int)(E[k].x & 0xffff)] < lane) conflict = true;
+            const uint64_t bad = __ballot(!done && (conflict || !exact));
+            const int p = bad ? __ffsll((long long)bad) - 1 : kWave;
+            lds_order();
+            if (blocking) mark[st.idx] = kWave;
+            const bool commit = !done && lane < p;
+            const bool cl = commit && acc;
+            // repeated claims of a slot in the prefix: the last lane (the later
+            // query) owns it, as in the serial loop
+            if (cl) atomicMin(&mark[st.idx], kWave - 1 - lane);
+            lds_order();
+            if (cl && mark[st.idx] == kWave - 1 - lane) { own[st.idx] = i; bl[st.idx] = (uint8_t)hob; }
+            lds_order();
+            if (cl) mark[st.idx] = kWave;
+            const uint64_t cm = __ballot(cl);
+            if (ori) {
+                if (cl) {
+                    hent[nh + __popcll(cm & lt)] = (bin << 16) | st.idx;
+                    atomicAdd(&hist[bin], 1);
+                }
+                nh += __popcll(cm);
+            }
+            nm += __popcll(cm);
+            done = done || commit;
+            lds_order();
+            if (p < kWave) {
+                // lane p's list ran dry (or overlapped): with every earlier lane
+                // committed, a dry list is rescanned exactly now
+                const bool dry = (bad >> p) & 1 && __builtin_amdgcn_readlane((int)(!exact), p);
+                if (dry) {
+                    const int qi = blk * kWave + p;
+                    ProjQuery q;
+                    proj_query(a, qi, q);
+                    wave_sync_m();
+                    const Best2 sx = proj_scan(a, qi, q, a.cellstart, own);
+                    bool ax;
+                    if (mode == 0) ax = sx.best <= kThHigh && !(sx.lvl == sx.lvl2 && (float)sx.best > ratio * (float)sx.best2);
+                    else ax = sx.idx >= 0 && (float)sx.best <= accept;
+                    if (ax) {
+                        const int hq = __builtin_amdgcn_readlane(hob, p);
+                        if (lane == 0) { own[sx.idx] = qi; bl[sx.idx] = (uint8_t)hq; }
+                        ++nm;
+                        if (ori) {
+                            const int bx = rot_bin(a.qangle[qi], a.kps[sx.idx].angle);
+                            if (lane == 0) { hent[nh] = (bx << 16) | sx.idx; hist[bx]++; }
+                            ++nh;
+                        }
+                    }
+                    if (lane == p) done = true;
+                    lds_order();
+                }
+            }
+        }
+    }
+    if (ori) {
+        __syncthreads();
+        proj_rot_filter(a, hist, hent, nh, own, nm);
+    }
+    __syncthreads();
+    for (int i = lane; i < a.n; i += kWave) a.owner[i] = own[i];
+    if (lane == 0) a.nmatches[0] = nm;
+}
+
 // Largest distance that can still decide a query (see k_proj_topk).
 static int proj_bound(const ProjArgs& a) {
     if (a.mode == 1) return a.accept < 0 ? -1 : (int)std::min(255.0f, std::floor(a.accept));
@@ -2256,15 +2398,21 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
     a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p;
     a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
-    // two-phase form unless its LDS slot table does not fit (or the single-wave
-    // form is forced for testing: ORBM_PROJ_SINGLE_WAVE=1)
+    // two-phase form unless its LDS slot table does not fit; phase 2 speculative
+    // unless its table does not fit.  For testing, ORBM_PROJ_SINGLE_WAVE=1
+    // forces the single-wave form and ORBM_PROJ_SERIAL_RESOLVE=1 the serial
+    // phase 2.
     const char* force = std::getenv("ORBM_PROJ_SINGLE_WAVE");
-    const size_t lds2 = proj_resolve_lds(a.n, a.nq);
+    const char* serial = std::getenv("ORBM_PROJ_SERIAL_RESOLVE");
+    const size_t lds2 = proj_resolve_lds(a.n, a.nq), lds3 = proj_spec_lds(a.n, a.nq);
     if (lds2 <= 160 * 1024 && !(force && force[0] == '1')) {
         DBuf<uint2> topk; DBuf<int> cnt;
         if ((rc = topk.alloc((size_t)std::max(1, a.nq) * kProjK)) || (rc = cnt.alloc(std::max(1, a.nq)))) return rc;
         if (a.nq) KLAUNCH(k_proj_topk, dim3((a.nq + 3) / 4), dim3(256), 0, 0, a, proj_bound(a), topk.p, cnt.p);
-        KLAUNCH(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);
+        if (lds3 <= 160 * 1024 && !(serial && serial[0] == '1'))
+            KLAUNCH(k_proj_resolve_spec, dim3(1), dim3(64), lds3, 0, a, topk.p, cnt.p);
+        else
+            KLAUNCH(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);
     } else {
         const size_t lds = proj_lds(a.nq);
         if (lds > 160 * 1024) return ORB_ERR_UNSUPPORTED;

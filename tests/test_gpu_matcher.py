@@ -90,10 +90,11 @@ def projection_queries(frames, seed, n=600):
     return rng, src, cur, k, qx.astype(np.float32), qy.astype(np.float32)
 
 
-@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
 def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, monkeypatch):
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single else "0")
+    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
+    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
@@ -114,10 +115,11 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, 
     np.testing.assert_array_equal(own, rown)
 
 
-@pytest.mark.parametrize("single", [False, True])
+@pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
 def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, monkeypatch):
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single else "0")
+    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
+    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     valid = (rng.random(n) < 0.9).astype(np.uint8)
@@ -130,6 +132,54 @@ def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, singl
     args = (valid, qx, qy, ur, k["octave"], k["angle"], has_obs, src[1][:n], 7.0, mode)
     nm, own = orb.ORBmatcher(0.9, ori).SearchByProjectionLast(F, *args, owner=owner, blocked=blocked)
     rnm, rown = O.search_by_projection_last(F, *args, ori, owner, blocked)
+    assert nm == rnm and nm > 0
+    np.testing.assert_array_equal(own, rown)
+
+
+@pytest.mark.parametrize("single", ["spec", "serial", "single"])
+@pytest.mark.parametrize("seed,reps", [(21, 2), (22, 3), (23, 4)])
+def test_search_by_projection_overlapping_lists(gpu_lib, frames, seed, reps, single, monkeypatch):
+    """Queries repeated `reps` times (consecutive and far apart in the query
+    order, positions jittered, a few descriptor bits flipped) so that candidate
+    lists overlap and later queries find their best slot claimed; slots start
+    free, pre-existing (-2) or owned by a query of this call (earlier or later
+    in the order) with or without observations."""
+    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
+    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
+    rng = np.random.default_rng(seed)
+    src, cur = frames[0], frames[1]
+    k0 = src[0][:300]
+    idx = np.concatenate([np.repeat(np.arange(len(k0)), reps - 1), rng.permutation(len(k0))])
+    k = k0[idx]
+    n = len(k)
+    qx = (k["x"] + 3 + rng.normal(0, 1.5, n)).astype(np.float32)
+    qy = (k["y"] + 3 + rng.normal(0, 1.5, n)).astype(np.float32)
+    d = src[1][:300][idx].copy()
+    flip = rng.random((n, 32)) < 0.02
+    d[flip] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    has_obs = (rng.random(n) < 0.6).astype(np.uint8)
+    mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
+                               rng.uniform(0.99, 1.0, n).astype(np.float32), rng.uniform(0, 100, n).astype(np.float32),
+                               (rng.random(n) < 0.95).astype(np.uint8), has_obs, d)
+    N = len(cur[0])
+    owner = np.full(N, -1, np.int32)
+    r = rng.random(N)
+    owner[r < 0.05] = -2
+    q_owned = (r >= 0.05) & (r < 0.15)
+    owner[q_owned] = rng.integers(0, n, int(q_owned.sum()))
+    blocked = ((owner == -2) & (rng.random(N) < 0.5)).astype(np.uint8)
+    F = abi.frame_struct(cur[0], cur[1], 752, 480, scale_factors=np.float32(1.2) ** np.arange(8, dtype=np.float32))
+    nm, own = orb.ORBmatcher(0.8, True).SearchByProjection(F, mps, 3.0, False, 50.0, owner, blocked)
+    rnm, rown = O.search_by_projection_mps(F, mps, 3.0, False, 50.0, 0.8, owner, blocked)
+    assert nm == rnm and nm > 0
+    np.testing.assert_array_equal(own, rown)
+    # best-only form (SearchByProjection(F, LastFrame) semantics) on the same overlap
+    valid = (rng.random(n) < 0.95).astype(np.uint8)
+    ur = (qx - rng.uniform(0, 40, n)).astype(np.float32)
+    owner2 = np.full(N, -1, np.int32)
+    args = (valid, qx, qy, ur, k["octave"], k["angle"], has_obs, d, 7.0, 0)
+    nm, own = orb.ORBmatcher(0.9, True).SearchByProjectionLast(F, *args, owner=owner2, blocked=np.zeros(N, np.uint8))
+    rnm, rown = O.search_by_projection_last(F, *args, True, owner2, np.zeros(N, np.uint8))
     assert nm == rnm and nm > 0
     np.testing.assert_array_equal(own, rown)
 
