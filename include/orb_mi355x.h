@@ -396,6 +396,26 @@ int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
                                   const float* F12, float ep_x, float ep_y, const float* level_sigma2_2,
                                   int only_stereo, int coarse, int check_ori, int fma, int32_t* matches12);
 
+/* SearchForTriangulation for keyframes whose epipolar test only the host can
+ * run: KannalaBrandt8 keyframes and two-camera (NLeft != -1) keyframes
+ * (ORBmatcher.cc:1014-1076 -> GeometricCamera::epipolarConstrain, for
+ * KannalaBrandt8 a Newton unprojection + Eigen JacobiSVD triangulation,
+ * KannalaBrandt8.cpp:306-380).  The GPU ranks, for every KF1 feature without a
+ * MapPoint (and stereo when only_stereo) in a node both FeatureVectors hold,
+ * the KF2 candidates of that node (no MapPoint, stereo filter, distance <=
+ * TH_LOW) by (distance ascending, node position descending); check(ctx, idx1,
+ * idx2) is the reference's per-candidate geometry (the epipole test of
+ * :1014-1021 when it applies, then epipolarConstrain with the camera pair and
+ * relative pose the reference selects at :1023-1062) and must be a pure
+ * function; the match of idx1 is the first candidate it accepts, which is the
+ * candidate the reference's loop keeps.  Then the rotation filter (check_ori),
+ * as in orbm_search_for_triangulation.  Returns nmatches. */
+typedef int (*orbm_tri_check_fn)(void* ctx, int idx1, int idx2);
+int orbm_search_for_triangulation_checked(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                          const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                          int only_stereo, int check_ori, orbm_tri_check_fn check, void* ctx,
+                                          int32_t* matches12);
+
 /* MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:329-405) for
  * npoints points at once: point p's observed descriptors (the order of its
  * observation map, gathered by the caller) are rows off[p] .. off[p+1]-1 of

@@ -7,6 +7,7 @@
 // INTEGRATION.md shows the cv::Mat glue a maintainer adds.
 #pragma once
 #include <cstdint>
+#include <functional>
 #include <stdexcept>
 #include <utility>
 #include <vector>
@@ -207,6 +208,29 @@ public:
                                                      epy, levelSigma2_2.data(), bOnlyStereo, bCoarse,
                                                      mbCheckOrientation, 1, m12.data());
         if (nm < 0) throw std::runtime_error("SearchForTriangulation failed");
+        vMatchedPairs.clear();
+        for (int i = 0; i < KF1.n; ++i)
+            if (m12[i] >= 0) vMatchedPairs.emplace_back((size_t)i, (size_t)m12[i]);
+        return nm;
+    }
+
+    // The same for KannalaBrandt8 / two-camera keyframes: `check(idx1, idx2)` is
+    // the reference's per-candidate geometry (epipole test + the selected camera
+    // pair's epipolarConstrain, src/ORBmatcher.cc:1014-1076), e.g. a lambda over
+    // pKF1/pKF2 calling pCamera1->epipolarConstrain(pCamera2, kp1, kp2, R12, t12, ...).
+    int SearchForTriangulation(const orbm_frame& KF1, const orbm_featvec& fv1, const std::vector<uint8_t>& hasMP1,
+                               const orbm_frame& KF2, const orbm_featvec& fv2, const std::vector<uint8_t>& hasMP2,
+                               const std::function<bool(int, int)>& check,
+                               std::vector<std::pair<size_t, size_t>>& vMatchedPairs, bool bOnlyStereo) const {
+        std::vector<int32_t> m12(KF1.n, -1);
+        auto tramp = [](void* ctx, int i1, int i2) -> int {
+            return (*static_cast<const std::function<bool(int, int)>*>(ctx))(i1, i2) ? 1 : 0;
+        };
+        const int nm = orbm_search_for_triangulation_checked(&KF1, &fv1, hasMP1.data(), &KF2, &fv2, hasMP2.data(),
+                                                             bOnlyStereo, mbCheckOrientation, tramp,
+                                                             const_cast<std::function<bool(int, int)>*>(&check),
+                                                             m12.data());
+        if (nm < 0) throw std::runtime_error("SearchForTriangulation (checked) failed");
         vMatchedPairs.clear();
         for (int i = 0; i < KF1.n; ++i)
             if (m12[i] >= 0) vMatchedPairs.emplace_back((size_t)i, (size_t)m12[i]);

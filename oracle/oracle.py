@@ -57,6 +57,7 @@ def lib():
         L.orbo_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp]
         L.orbo_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
         L.orbo_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
+        L.orbo_search_for_triangulation_checked.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, abi.TRI_CHECK, vp, vp]
         L.orbo_detect_relocalization_candidates.argtypes = [vp, vp, i32, i32, vp, vp, vp, i32, vp, vp, vp, vp, vp,
                                                              i32, vp, vp, i32]
         L.orbo_search_by_bow_kf.argtypes = [vp, vp, vp, vp, vp, vp, f32, i32, vp]
@@ -276,6 +277,19 @@ def search_for_triangulation(kf1, fv1, has_mp1, kf2, fv2, has_mp2, F12, ep, sigm
     nm = lib().orbo_search_for_triangulation(kf1.ref(), fv1.ref(), abi.ptr(m1), kf2.ref(), fv2.ref(), abi.ptr(m2),
                                              abi.ptr(F), float(ep[0]), float(ep[1]), abi.ptr(s2), int(only_stereo),
                                              int(coarse), int(check_ori), fma, abi.ptr(out))
+    return nm, out
+
+
+def search_for_triangulation_checked(kf1, fv1, has_mp1, kf2, fv2, has_mp2, check, only_stereo=False,
+                                     check_ori=True):
+    """check(idx1, idx2) -> bool: the caller's per-candidate geometry."""
+    m1 = np.ascontiguousarray(has_mp1, np.uint8)
+    m2 = np.ascontiguousarray(has_mp2, np.uint8)
+    out = np.zeros(len(m1), np.int32)
+    cb = abi.TRI_CHECK(lambda _ctx, i1, i2: int(bool(check(i1, i2))))
+    nm = lib().orbo_search_for_triangulation_checked(kf1.ref(), fv1.ref(), abi.ptr(m1), kf2.ref(), fv2.ref(),
+                                                     abi.ptr(m2), int(only_stereo), int(check_ori), cb, None,
+                                                     abi.ptr(out))
     return nm, out
 
 

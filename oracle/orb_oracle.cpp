@@ -1293,6 +1293,60 @@ int orbo_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
     return nmatches;
 }
 
+// SearchForTriangulation with the per-candidate geometry delegated to
+// check(ctx, idx1, idx2) (the epipole test + GeometricCamera::epipolarConstrain
+// of src/ORBmatcher.cc:1014-1076): the reference loop itself, the callback in
+// place of the two tests.
+int orbo_search_for_triangulation_checked(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                          const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                          int only_stereo, int check_ori, int (*check)(void*, int, int), void* ctx,
+                                          int32_t* matches12) {
+    int nmatches = 0;
+    for (int i = 0; i < kf1->n; ++i) matches12[i] = -1;
+    std::vector<int> hist[kHisto];
+    int a = 0, b = 0;
+    while (a < fv1->nnodes && b < fv2->nnodes) {
+        if (fv1->node_ids[a] == fv2->node_ids[b]) {
+            for (int p = fv1->offsets[a]; p < fv1->offsets[a + 1]; ++p) {
+                const int idx1 = (int)fv1->idx[p];
+                if (has_mp1[idx1]) continue;
+                const bool st1 = kf1->u_right && kf1->u_right[idx1] >= 0;
+                if (only_stereo && !st1) continue;
+                int bestDist = kThLow, bestIdx2 = -1;
+                for (int q = fv2->offsets[b]; q < fv2->offsets[b + 1]; ++q) {
+                    const int idx2 = (int)fv2->idx[q];
+                    if (has_mp2[idx2]) continue;                       // vbMatched2 is never set
+                    const bool st2 = kf2->u_right && kf2->u_right[idx2] >= 0;
+                    if (only_stereo && !st2) continue;
+                    const int dist = hamming(kf1->desc + (size_t)idx1 * 32, kf2->desc + (size_t)idx2 * 32);
+                    if (dist > kThLow || dist > bestDist) continue;
+                    if (check(ctx, idx1, idx2)) { bestIdx2 = idx2; bestDist = dist; }
+                }
+                if (bestIdx2 >= 0) {
+                    matches12[idx1] = bestIdx2;
+                    ++nmatches;
+                    if (check_ori) hist[rot_bin(kf1->kps[idx1].angle, kf2->kps[bestIdx2].angle)].push_back(idx1);
+                }
+            }
+            ++a;
+            ++b;
+        } else if (fv1->node_ids[a] < fv2->node_ids[b]) {
+            a = (int)(std::lower_bound(fv1->node_ids + a, fv1->node_ids + fv1->nnodes, fv2->node_ids[b]) - fv1->node_ids);
+        } else {
+            b = (int)(std::lower_bound(fv2->node_ids + b, fv2->node_ids + fv2->nnodes, fv1->node_ids[a]) - fv2->node_ids);
+        }
+    }
+    if (check_ori) {
+        int i1, i2, i3;
+        three_maxima(hist, i1, i2, i3);
+        for (int i = 0; i < kHisto; ++i) {
+            if (i == i1 || i == i2 || i == i3) continue;
+            for (int idx1 : hist[i]) { matches12[idx1] = -1; --nmatches; }
+        }
+    }
+    return nmatches;
+}
+
 // MapPoint::ComputeDistinctiveDescriptors (src/MapPoint.cc:368-397) per point
 // of a CSR batch: the N x N distance matrix, each row sorted, the median at
 // 0.5 * (N - 1), the first row with the least median.

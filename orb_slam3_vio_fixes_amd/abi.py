@@ -64,6 +64,10 @@ class OrbmMapPointsRight(C.Structure):
                 ("view_cos", C.c_void_p)]
 
 
+# orbm_tri_check_fn: int (*)(void* ctx, int idx1, int idx2)
+TRI_CHECK = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_int)
+
+
 def ptr(a: np.ndarray | None) -> int | None:
     if a is None:
         return None

@@ -21,7 +21,7 @@ EXPORTS = [
     "orbs_knn_match2", "orbs_fisheye_stereo_candidates_batch_device",
     "orbv_load_text", "orbv_text_vocab_view", "orbv_free_text", "orbv_bow_assemble", "orbv_score",
     "orbk_db_create", "orbk_db_destroy", "orbk_db_upload", "orbk_detect_relocalization_candidates",
-    "orbm_fuse", "orbm_search_for_triangulation", "orbm_compute_distinctive_descriptors",
+    "orbm_fuse", "orbm_search_for_triangulation", "orbm_search_for_triangulation_checked", "orbm_compute_distinctive_descriptors",
     "orbm_search_by_bow_kf", "orbm_search_by_projection_kf", "orbm_search_by_projection_sim3",
     "orbm_search_by_sim3", "orbm_fuse_sim3", "orbm_search_by_bow_fisheye", "orbm_search_by_projection_mps_fisheye",
     "orbm_search_by_projection_last_fisheye",
@@ -58,6 +58,7 @@ def load(path: Path | str = LIB_PATH):
     L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]
     L.orbm_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
     L.orbm_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
+    L.orbm_search_for_triangulation_checked.argtypes = [vp, vp, vp, vp, vp, vp, i32, i32, abi.TRI_CHECK, vp, vp]
     L.orbm_search_by_bow_kf.argtypes = [vp, vp, vp, vp, vp, vp, f32, i32, vp]
     L.orbm_search_by_projection_kf.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp]
     L.orbm_search_by_projection_sim3.argtypes = [vp, i32, vp, vp, vp, vp, vp, f32, f32, vp]

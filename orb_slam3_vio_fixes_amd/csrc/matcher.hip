@@ -306,7 +306,7 @@ __device__ __forceinline__ void merge_chunk(Best2& st, int d, int fi, int lv) {
     }
 }
 
-__device__ __forceinline__ int rot_bin(float a1, float a2) {
+__host__ __device__ __forceinline__ int rot_bin(float a1, float a2) {
     float rot = a1 - a2;
     if (rot < 0.0f) rot += 360.0f;
     int bin = (int)roundf(rot * (1.0f / kHisto));
@@ -315,7 +315,7 @@ __device__ __forceinline__ int rot_bin(float a1, float a2) {
 }
 
 // ComputeThreeMaxima (ORBmatcher.cc:2012-2053)
-__device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
+__host__ __device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
     int m1 = 0, m2 = 0, m3 = 0;
     i1 = i2 = i3 = -1;
     for (int i = 0; i < kHisto; ++i) {
@@ -1937,6 +1937,46 @@ __global__ __launch_bounds__(256) void k_tri(TriArgs a) {
     if (lane == 0) a.item_match[t] = res;
 }
 
+// k_tri_cands: the checked form's candidate ranking.  Per item (KF1 feature
+// without a MapPoint, its shared node), every KF2 candidate of the node with
+// no MapPoint, the stereo filter passed and dist <= TH_LOW, written to the
+// item's segment as key = dist << 16 | (0xffff - node position) and the KF2
+// index (ballot compaction, unordered; the host sorts the short lists).
+__global__ __launch_bounds__(256) void k_tri_cands(TriArgs a, const int32_t* __restrict__ seg_off,
+                                                   int32_t* __restrict__ seg_cnt, uint32_t* __restrict__ ent_key,
+                                                   int32_t* __restrict__ ent_i2) {
+    const int t = blockIdx.x * 4 + wave_id(), lane = lane_id();
+    if (t >= a.nitems) return;
+    const int i1 = a.item_i1[t];
+    const bool st1 = a.ur1 && a.ur1[i1] >= 0;
+    int n = 0;
+    if (!a.mp1[i1] && (!a.only_stereo || st1)) {
+        const uint4 q0 = *(const uint4*)(a.d1 + (long long)i1 * 32), q1 = *(const uint4*)(a.d1 + (long long)i1 * 32 + 16);
+        const int base = seg_off[t];
+        for (int j0 = a.item_b[t]; j0 < a.item_e[t]; j0 += kWave) {
+            const int j = j0 + lane;
+            bool ok = false;
+            int i2 = 0, dist = 0;
+            if (j < a.item_e[t]) {
+                i2 = (int)a.fv2_idx[j];
+                const bool st2 = a.ur2 && a.ur2[i2] >= 0;
+                if (!a.mp2[i2] && (!a.only_stereo || st2)) {
+                    dist = hamming32(q0, q1, a.d2 + (long long)i2 * 32);
+                    ok = dist <= kThLow;
+                }
+            }
+            const uint64_t m = __ballot(ok);
+            if (ok) {
+                const int o = base + n + __popcll(m & ((1ull << lane) - 1));
+                ent_key[o] = ((uint32_t)dist << 16) | (uint32_t)(0xffff - (j - a.item_b[t]));
+                ent_i2[o] = i2;
+            }
+            n += __popcll(m);
+        }
+    }
+    if (lane == 0) seg_cnt[t] = n;
+}
+
 // rotation-consistency filter and vMatches12 (:1106-1144), one workgroup
 __global__ __launch_bounds__(256) void k_tri_final(TriArgs a, int n1, int32_t* matches12, int32_t* nmatches) {
     __shared__ int hist[kHisto];
@@ -2535,17 +2575,10 @@ int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, cons
     return n;
 }
 
-int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
-                                  const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
-                                  const float* F12, float ep_x, float ep_y, const float* level_sigma2_2,
-                                  int only_stereo, int coarse, int check_ori, int fma, int32_t* matches12) {
-    if (!kf1 || !kf2 || !fv1 || !fv2 || !has_mp1 || !has_mp2 || !F12 || !level_sigma2_2 || !matches12 ||
-        !kf2->scale_factors)
-        return ORB_ERR_PARAM;
-    int rc;
-    if ((rc = device_ok())) return rc;
-    // items: every KF1 feature of a node both FeatureVectors hold (the merge of :962-1100)
-    std::vector<int32_t> it_i1, it_b, it_e;
+// Items of SearchForTriangulation: every KF1 feature of a node both
+// FeatureVectors hold (the merge of :962-1100), with that node's KF2 range.
+static void tri_items(const orbm_featvec* fv1, const orbm_featvec* fv2, std::vector<int32_t>& it_i1,
+                      std::vector<int32_t>& it_b, std::vector<int32_t>& it_e) {
     int a = 0, b = 0;
     while (a < fv1->nnodes && b < fv2->nnodes) {
         if (fv1->node_ids[a] == fv2->node_ids[b]) {
@@ -2562,6 +2595,19 @@ int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
             ++b;
         }
     }
+}
+
+int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                  const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                  const float* F12, float ep_x, float ep_y, const float* level_sigma2_2,
+                                  int only_stereo, int coarse, int check_ori, int fma, int32_t* matches12) {
+    if (!kf1 || !kf2 || !fv1 || !fv2 || !has_mp1 || !has_mp2 || !F12 || !level_sigma2_2 || !matches12 ||
+        !kf2->scale_factors)
+        return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    std::vector<int32_t> it_i1, it_b, it_e;
+    tri_items(fv1, fv2, it_i1, it_b, it_e);
     const int nitems = (int)it_i1.size();
     DevFrame f1, f2;
     if ((rc = f1.upload(kf1, false, 0)) || (rc = f2.upload(kf2, false, 0))) return rc;
@@ -2588,6 +2634,75 @@ int orbm_search_for_triangulation(const orbm_frame* kf1, const orbm_featvec* fv1
     if (kf1->n) ORB_CHECK(d2h(matches12, out.p, kf1->n * sizeof(int32_t)));
     ORB_CHECK(d2h(&n, nm.p, sizeof(int32_t)));
     return n;
+}
+
+int orbm_search_for_triangulation_checked(const orbm_frame* kf1, const orbm_featvec* fv1, const uint8_t* has_mp1,
+                                          const orbm_frame* kf2, const orbm_featvec* fv2, const uint8_t* has_mp2,
+                                          int only_stereo, int check_ori, orbm_tri_check_fn check, void* ctx,
+                                          int32_t* matches12) {
+    if (!kf1 || !kf2 || !fv1 || !fv2 || !has_mp1 || !has_mp2 || !check || !matches12) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = device_ok())) return rc;
+    std::vector<int32_t> it_i1, it_b, it_e;
+    tri_items(fv1, fv2, it_i1, it_b, it_e);
+    const int nitems = (int)it_i1.size();
+    std::vector<int32_t> seg(nitems + 1, 0);
+    for (int t = 0; t < nitems; ++t) seg[t + 1] = seg[t] + (it_e[t] - it_b[t]);
+    const int total = seg[nitems];
+    for (int i = 0; i < kf1->n; ++i) matches12[i] = -1;
+    std::vector<int32_t> res(1 + nitems + 2 * (size_t)total);       // [unused | counts | keys | KF2 indices]
+    if (nitems) {
+        DevFrame f1, f2;
+        if ((rc = f1.upload(kf1, false, 0)) || (rc = f2.upload(kf2, false, 0))) return rc;
+        DBuf<uint8_t> m1, m2; DBuf<int32_t> bi1, bb, be, bseg, out; DBuf<uint32_t> fidx;
+        const int n2idx = fv2->nnodes ? fv2->offsets[fv2->nnodes] : 0;
+        if ((rc = m1.put(has_mp1, std::max(1, kf1->n))) || (rc = m2.put(has_mp2, std::max(1, kf2->n))) ||
+            (rc = bi1.put(it_i1.data(), nitems)) || (rc = bb.put(it_b.data(), nitems)) ||
+            (rc = be.put(it_e.data(), nitems)) || (rc = bseg.put(seg.data(), nitems + 1)) ||
+            (rc = fidx.put(fv2->idx, n2idx)) || (rc = out.alloc(res.size())))
+            return rc;
+        TriArgs ta{};
+        ta.k1 = f1.kps.p; ta.k2 = f2.kps.p; ta.d1 = f1.desc.p; ta.d2 = f2.desc.p;
+        ta.ur1 = kf1->u_right ? f1.ur.p : nullptr; ta.ur2 = kf2->u_right ? f2.ur.p : nullptr;
+        ta.mp1 = m1.p; ta.mp2 = m2.p; ta.item_i1 = bi1.p; ta.item_b = bb.p; ta.item_e = be.p;
+        ta.fv2_idx = fidx.p; ta.nitems = nitems; ta.only_stereo = only_stereo;
+        KLAUNCH(k_tri_cands, dim3((nitems + 3) / 4), dim3(256), 0, 0, ta, bseg.p, out.p + 1,
+                (uint32_t*)(out.p + 1 + nitems), out.p + 1 + nitems + total);
+        ORB_CHECK(hipGetLastError());
+        ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
+    }
+    // the caller's geometric check in (distance, last position) order: the
+    // first candidate it accepts is the reference's surviving bestIdx2
+    // (accepted distances never increase and equal ones overwrite, :1010-1076)
+    const int32_t* cnt = res.data() + 1;
+    const uint32_t* key = (const uint32_t*)(res.data() + 1 + nitems);
+    const int32_t* i2s = res.data() + 1 + nitems + total;
+    int nmatches = 0, hist[kHisto] = {0};
+    std::vector<int32_t> bins(nitems, -1);
+    std::vector<std::pair<uint32_t, int32_t>> cand;
+    for (int t = 0; t < nitems; ++t) {
+        cand.clear();
+        for (int e = seg[t]; e < seg[t] + cnt[t]; ++e) cand.emplace_back(key[e], i2s[e]);
+        std::sort(cand.begin(), cand.end());
+        const int i1 = it_i1[t];
+        for (const auto& c : cand) {
+            if (!check(ctx, i1, c.second)) continue;
+            matches12[i1] = c.second;
+            ++nmatches;
+            if (check_ori) {
+                bins[t] = rot_bin(kf1->kps[i1].angle, kf2->kps[c.second].angle);
+                ++hist[bins[t]];
+            }
+            break;
+        }
+    }
+    if (check_ori) {
+        int k1, k2, k3;
+        three_maxima(hist, k1, k2, k3);
+        for (int t = 0; t < nitems; ++t)
+            if (bins[t] >= 0 && bins[t] != k1 && bins[t] != k2 && bins[t] != k3) { matches12[it_i1[t]] = -1; --nmatches; }
+    }
+    return nmatches;
 }
 
 int orbm_compute_distinctive_descriptors(int npoints, const int32_t* off, const uint8_t* desc, int32_t* best,

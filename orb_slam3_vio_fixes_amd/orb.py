@@ -370,6 +370,23 @@ class ORBmatcher:
         capi.check(min(nm, 0), "SearchForTriangulation")
         return nm, out
 
+    def SearchForTriangulationChecked(self, KF1: abi.Keep, fv1: abi.Keep, has_mp1, KF2: abi.Keep, fv2: abi.Keep,
+                                      has_mp2, check, bOnlyStereo: bool = False):
+        """SearchForTriangulation (ORBmatcher.cc:907-1146) with the per-candidate
+        geometry supplied by the caller, check(idx1, idx2) -> bool (the epipole
+        test + epipolarConstrain of a KannalaBrandt8 or two-camera keyframe
+        pair, :1014-1076): the GPU ranks the candidates, the first one the check
+        accepts is the match.  (nmatches, matches12)."""
+        m1 = np.ascontiguousarray(has_mp1, np.uint8)
+        m2 = np.ascontiguousarray(has_mp2, np.uint8)
+        out = np.full(len(m1), -1, np.int32)
+        cb = abi.TRI_CHECK(lambda _ctx, i1, i2: int(bool(check(i1, i2))))
+        nm = capi.lib().orbm_search_for_triangulation_checked(KF1.ref(), fv1.ref(), abi.ptr(m1), KF2.ref(),
+                                                              fv2.ref(), abi.ptr(m2), int(bOnlyStereo),
+                                                              int(self.mbCheckOrientation), cb, None, abi.ptr(out))
+        capi.check(min(nm, 0), "SearchForTriangulationChecked")
+        return nm, out
+
     # ---- relocalisation / loop closing (ORBmatcher.h:55-63,71-84) ----
 
     def SearchByBoWKF(self, KF1: abi.Keep, fv1: abi.Keep, valid1, KF2: abi.Keep, fv2: abi.Keep, valid2):

@@ -173,3 +173,107 @@ def test_gpu_distinctive(gpu_lib):
     got = orb.compute_distinctive_descriptors(edge, desc[:3])
     assert got[0] == -1
     np.testing.assert_array_equal(got, O.compute_distinctive_descriptors(edge, desc[:3]))
+
+
+# ---- SearchForTriangulation with the caller's geometry (KannalaBrandt8 / two-camera keyframes) ----
+
+def _tri_predicates(k1, k2):
+    """Pure per-candidate checks standing in for epipolarConstrain: accept all,
+    an arbitrary hash (ties between equal distances matter), and a row-band
+    constraint (a geometric stand-in for the panning pair)."""
+    return {
+        "all": lambda i1, i2: True,
+        "hash": lambda i1, i2: (i1 * 2654435761 + i2 * 40503) % 7 != 0,
+        "band": lambda i1, i2: abs(float(k1[i1]["y"]) - float(k2[i2]["y"])) < 6.0 + 2.0 * int(k2[i2]["octave"]),
+    }
+
+
+def ref_tri_checked(k1, d1, ur1, mp1, fv1, k2, d2, ur2, mp2, fv2, only_stereo, check):
+    """The reference loop (ORBmatcher.cc:962-1144), the callback in place of the
+    epipole test and epipolarConstrain; independent of the C++ oracle."""
+    from tests import matcher_ref as M
+    m12 = np.full(len(k1), -1, np.int32)
+    hist = [[] for _ in range(M.HISTO)]
+    nm = 0
+    for node in sorted(set(fv1) & set(fv2)):
+        for i1 in fv1[node]:
+            if mp1[i1]:
+                continue
+            st1 = ur1 is not None and ur1[i1] >= 0
+            if only_stereo and not st1:
+                continue
+            best, bi = M.TH_LOW, -1
+            for i2 in fv2[node]:
+                if mp2[i2]:
+                    continue
+                st2 = ur2 is not None and ur2[i2] >= 0
+                if only_stereo and not st2:
+                    continue
+                dist = M.hamming(d1[i1], d2[i2])
+                if dist > M.TH_LOW or dist > best:
+                    continue
+                if check(i1, i2):
+                    best, bi = dist, i2
+            if bi >= 0:
+                m12[i1] = bi
+                nm += 1
+                hist[M.rot_bin(k1[i1]["angle"], k2[bi]["angle"])].append(i1)
+    keep = M.three_maxima([len(h) for h in hist])
+    for b in range(M.HISTO):
+        if b not in keep:
+            for i1 in hist[b]:
+                m12[i1] = -1
+                nm -= 1
+    return nm, m12
+
+
+@pytest.mark.parametrize("stereo,only_stereo,pred,seed", [(False, False, "hash", 11), (True, False, "band", 12),
+                                                           (True, True, "hash", 13), (False, False, "band", 14)])
+def test_oracle_triangulation_checked_vs_python(scene, stereo, only_stereo, pred, seed):
+    k1, d1, k2, d2, mp1, mp2, ur1, ur2 = tri_inputs(scene, stereo, seed)
+    nid1, nid2 = scene[1]
+    t = scene[2]
+    f1 = abi.frame_struct(k1, d1, W, H, u_right=ur1, scale_factors=t["scale"])
+    f2 = abi.frame_struct(k2, d2, W, H, u_right=ur2, scale_factors=t["scale"])
+    check = _tri_predicates(k1, k2)[pred]
+    nm, m12 = O.search_for_triangulation_checked(f1, abi.featvec_struct(nid1), mp1, f2, abi.featvec_struct(nid2),
+                                                 mp2, check, only_stereo)
+    rn, rm = ref_tri_checked(k1, d1, ur1, mp1, featvec_dict(nid1), k2, d2, ur2, mp2, featvec_dict(nid2),
+                             only_stereo, check)
+    assert nm == rn and nm > 0
+    np.testing.assert_array_equal(m12, rm)
+
+
+@pytest.mark.parametrize("stereo", [False, True])
+def test_oracle_triangulation_checked_accept_all_is_coarse(scene, stereo):
+    """With a check that accepts everything and the epipole out of reach, the
+    checked form is the pinhole form with bCoarse."""
+    k1, d1, k2, d2, mp1, mp2, ur1, ur2 = tri_inputs(scene, stereo, 15)
+    nid1, nid2 = scene[1]
+    t = scene[2]
+    F, _ = F12_and_ep()
+    f1 = abi.frame_struct(k1, d1, W, H, u_right=ur1, scale_factors=t["scale"])
+    f2 = abi.frame_struct(k2, d2, W, H, u_right=ur2, scale_factors=t["scale"])
+    fv1, fv2 = abi.featvec_struct(nid1), abi.featvec_struct(nid2)
+    a = O.search_for_triangulation_checked(f1, fv1, mp1, f2, fv2, mp2, lambda i1, i2: True)
+    b = O.search_for_triangulation(f1, fv1, mp1, f2, fv2, mp2, F, (-1e6, -1e6), t["sigma2"], False, True, True)
+    assert a[0] == b[0] and a[0] > 0
+    np.testing.assert_array_equal(a[1], b[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stereo,only_stereo,pred,seed", [(False, False, "all", 21), (False, False, "hash", 22),
+                                                           (True, False, "band", 23), (True, True, "hash", 24)])
+def test_gpu_triangulation_checked(gpu_lib, scene, stereo, only_stereo, pred, seed):
+    from orb_slam3_vio_fixes_amd import orb
+    k1, d1, k2, d2, mp1, mp2, ur1, ur2 = tri_inputs(scene, stereo, seed)
+    nid1, nid2 = scene[1]
+    t = scene[2]
+    f1 = abi.frame_struct(k1, d1, W, H, u_right=ur1, scale_factors=t["scale"])
+    f2 = abi.frame_struct(k2, d2, W, H, u_right=ur2, scale_factors=t["scale"])
+    fv1, fv2 = abi.featvec_struct(nid1), abi.featvec_struct(nid2)
+    check = _tri_predicates(k1, k2)[pred]
+    rn, rm = O.search_for_triangulation_checked(f1, fv1, mp1, f2, fv2, mp2, check, only_stereo)
+    gn, gm = orb.ORBmatcher(0.6, True).SearchForTriangulationChecked(f1, fv1, mp1, f2, fv2, mp2, check, only_stereo)
+    assert gn == rn and gn > 0
+    np.testing.assert_array_equal(gm, rm)
