@@ -66,7 +66,7 @@ def test_search_for_initialization_batch_device(gpu_lib):
         np.testing.assert_array_equal(m[t, :len(k1)].cpu().numpy(), rm12)
 
 
-@pytest.mark.parametrize("ori,ratio,nodes", [(True, 0.7, 40), (False, 0.75, 12), (True, 0.9, 200)])
+@pytest.mark.parametrize("ori,ratio,nodes", [(True, 0.7, 40), (False, 0.75, 12), (True, 0.9, 200), (True, 0.8, 4), (False, 0.75, 2)])
 def test_search_by_bow(gpu_lib, frames, ori, ratio, nodes):
     rng = np.random.default_rng(nodes)
     kf, f = frames[0], frames[1]
