@@ -89,6 +89,20 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int h_, size_t step,
                  int lap0, int lap1, orb_keypoint* kps, uint8_t* desc, int cap,
                  int* n_out, int* mono_index_out);
 
+/* operator() on nframes host images of one size at once (the left and right
+ * images of a stereo frame, which Frame.cc:122-125,222 extract on two
+ * threads, or a window of frames): one upload, one batched pipeline, one
+ * download.  imgs[f] with row step steps[f] (steps NULL: w); lap[2f], lap[2f+1]
+ * = frame f's vLappingArea (lap NULL: {0, 1000}).  Frame f's outputs:
+ * kps[f*cap ...], desc[(f*cap ...) * 32], n_out[f], mono_out[f] (may be NULL).
+ * Returns ORB_OK, ORB_ERR_EMPTY (an empty image), ORB_ERR_CAPACITY (some
+ * n_out[f] > cap: that frame is not copied), ORB_ERR_PARAM or ORB_ERR_DEVICE.
+ * The frames stay on the device for orbs_compute_stereo_matches_batch_device
+ * like those of orbx_extract_batch_device. */
+int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, const size_t* steps, int w, int h_,
+                       const int32_t* lap, orb_keypoint* kps, uint8_t* desc, int cap, int32_t* n_out,
+                       int32_t* mono_out);
+
 /* mvImagePyramid[level] (include/ORBextractor.h:83) of the LAST image
  * extracted by orbx_extract (host copy).  dst may be NULL to query w/h. */
 int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step,

@@ -61,6 +61,34 @@ public:
         return mono;
     }
 
+    // operator() on several images of one size in one call (orbx_extract_batch),
+    // e.g. the left and right images of a stereo frame; returns the monoIndex
+    // of each image.  images[f] has row step steps[f]; laps[f] = its vLappingArea.
+    std::vector<int> ExtractBatch(const std::vector<const uint8_t*>& images, const std::vector<size_t>& steps,
+                                  int cols, int rows, const std::vector<std::pair<int, int>>& laps,
+                                  std::vector<std::vector<KeyPoint>>& keypoints,
+                                  std::vector<Descriptors>& descriptors) {
+        const int nf = (int)images.size();
+        if (nf == 0) return {};
+        const int cap = orbx_max_keypoints(h_, cols, rows);
+        if (cap < 0) throw std::runtime_error("orbx_max_keypoints failed");
+        std::vector<KeyPoint> kps((size_t)nf * cap);
+        std::vector<uint8_t> desc((size_t)nf * cap * 32);
+        std::vector<int32_t> lap(2 * (size_t)nf), n(nf), mono(nf);
+        for (int f = 0; f < nf; ++f) { lap[2 * f] = laps.at(f).first; lap[2 * f + 1] = laps.at(f).second; }
+        const int rc = orbx_extract_batch(h_, nf, images.data(), steps.data(), cols, rows, lap.data(), kps.data(),
+                                          desc.data(), cap, n.data(), mono.data());
+        if (rc != ORB_OK) throw std::runtime_error("orbx_extract_batch failed");
+        keypoints.assign(nf, {});
+        descriptors.assign(nf, {});
+        for (int f = 0; f < nf; ++f) {
+            keypoints[f].assign(kps.begin() + (size_t)f * cap, kps.begin() + (size_t)f * cap + n[f]);
+            descriptors[f].rows = n[f];
+            descriptors[f].data.assign(desc.begin() + (size_t)f * cap * 32, desc.begin() + ((size_t)f * cap + n[f]) * 32);
+        }
+        return std::vector<int>(mono.begin(), mono.end());
+    }
+
     int GetLevels() const { return nlevels_; }
     float GetScaleFactor() const { return scaleFactor_; }
     std::vector<float> GetScaleFactors() const { return scale_; }

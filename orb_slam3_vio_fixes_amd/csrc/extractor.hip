@@ -1770,6 +1770,8 @@ void orbx_destroy(orbx_handle* h) {
     for (hipStream_t s : h->sub_streams) (void)hipStreamDestroy(s);
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
     if (h->st_scratch) (void)hipFree(h->st_scratch);
+    if (h->hb_dev) (void)hipFree(h->hb_dev);
+    if (h->hb_pin) (void)hipHostFree(h->hb_pin);
     delete h;
 }
 
@@ -1811,6 +1813,78 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     h->last_B = nframes;
     return run_batched(h, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
                        d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
+}
+
+int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, const size_t* steps, int w, int hh,
+                       const int32_t* lap, orb_keypoint* kps, uint8_t* desc, int cap, int32_t* n_out,
+                       int32_t* mono_out) {
+    if (!h || nframes <= 0 || !imgs || !kps || !desc || !n_out || cap < 0) return ORB_ERR_PARAM;
+    if (w <= 0 || hh <= 0) return ORB_ERR_EMPTY;                     // ORBextractor.cc:1090-1091
+    for (int f = 0; f < nframes; ++f)
+        if (!imgs[f]) return ORB_ERR_EMPTY;
+    if (hipSetDevice(h->device) != hipSuccess) return ORB_ERR_DEVICE;
+    int rc = build_plan(h, w, hh, std::max(nframes, h->plan.maxB));
+    if (rc) return rc;
+    const int ot = h->plan.out_total;                                // device slots per frame
+    const size_t pitch = ((size_t)w + 63) & ~size_t(63), fbytes = pitch * hh;
+    const size_t in_b = (size_t)nframes * fbytes, kp_b = (size_t)nframes * ot * sizeof(orb_keypoint),
+                 de_b = (size_t)nframes * ot * 32, nm_b = (size_t)nframes * 2 * sizeof(int32_t);
+    const size_t o_kp = (in_b + 255) & ~size_t(255), o_de = o_kp + ((kp_b + 255) & ~size_t(255)),
+                 o_nm = o_de + ((de_b + 255) & ~size_t(255)), total = o_nm + nm_b;
+    if (h->hb_dev_bytes < total) {
+        if (h->hb_dev) (void)hipFree(h->hb_dev);
+        h->hb_dev = nullptr; h->hb_dev_bytes = 0;
+        if (hipMalloc(&h->hb_dev, total) != hipSuccess) return ORB_ERR_DEVICE;
+        h->hb_dev_bytes = total;
+    }
+    if (h->hb_pin_bytes < total) {
+        if (h->hb_pin) (void)hipHostFree(h->hb_pin);
+        h->hb_pin = nullptr; h->hb_pin_bytes = 0;
+        if (hipHostMalloc(&h->hb_pin, total, hipHostMallocDefault) != hipSuccess) return ORB_ERR_DEVICE;
+        h->hb_pin_bytes = total;
+    }
+    uint8_t* dev = (uint8_t*)h->hb_dev;
+    uint8_t* pin = (uint8_t*)h->hb_pin;
+    // one upload: the frames gathered into pinned memory at a common pitch
+    for (int f = 0; f < nframes; ++f) {
+        const size_t st = steps ? steps[f] : (size_t)w;
+        for (int y = 0; y < hh; ++y) std::memcpy(pin + f * fbytes + y * pitch, imgs[f] + y * st, w);
+    }
+    ORB_CHECK(hipMemcpyAsync(dev, pin, in_b, hipMemcpyHostToDevice, 0));
+    orb_keypoint* d_kps = (orb_keypoint*)(dev + o_kp);
+    uint8_t* d_desc = dev + o_de;
+    int32_t* d_nm = (int32_t*)(dev + o_nm);                          // n[nframes] | mono[nframes]
+    // consecutive frames with the same vLappingArea run as one batch
+    for (int f0 = 0; f0 < nframes;) {
+        const int l0 = lap ? lap[2 * f0] : 0, l1 = lap ? lap[2 * f0 + 1] : 1000;
+        int f1 = f0 + 1;
+        while (f1 < nframes && (!lap || (lap[2 * f1] == l0 && lap[2 * f1 + 1] == l1))) ++f1;
+        rc = run_batched(h, f1 - f0, dev + f0 * fbytes, (long long)fbytes, (int)pitch, (float)l0, (float)l1,
+                         d_kps + (size_t)f0 * ot, d_desc + (size_t)f0 * ot * 32, ot, d_nm + f0, d_nm + nframes + f0,
+                         0);
+        if (rc) return rc;
+        f0 = f1;
+    }
+    h->last_frames = dev;
+    h->last_fstride = (long long)fbytes;
+    h->last_pitch0 = (int)pitch;
+    h->last_B = nframes;
+    // one download of everything, then per-frame copies out of pinned memory
+    ORB_CHECK(hipMemcpyAsync(pin + o_kp, dev + o_kp, total - o_kp, hipMemcpyDeviceToHost, 0));
+    ORB_CHECK(hipStreamSynchronize(0));
+    const int32_t* nm = (const int32_t*)(pin + o_nm);
+    const orb_keypoint* hk = (const orb_keypoint*)(pin + o_kp);
+    const uint8_t* hd = pin + o_de;
+    bool over = false;
+    for (int f = 0; f < nframes; ++f) {
+        const int n = nm[f];
+        n_out[f] = n;
+        if (mono_out) mono_out[f] = nm[nframes + f];
+        if (n > cap) { over = true; continue; }
+        std::memcpy(kps + (size_t)f * cap, hk + (size_t)f * ot, (size_t)n * sizeof(orb_keypoint));
+        std::memcpy(desc + (size_t)f * cap * 32, hd + (size_t)f * ot * 32, (size_t)n * 32);
+    }
+    return over ? ORB_ERR_CAPACITY : ORB_OK;
 }
 
 int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step, int lap0, int lap1,

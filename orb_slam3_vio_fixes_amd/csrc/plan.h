@@ -99,4 +99,10 @@ struct orbx_handle {
     // device scratch of the stereo matcher (stereo.hip), grown on demand
     void* st_scratch = nullptr;
     size_t st_scratch_bytes = 0;
+    // orbx_extract_batch (host images): staged frames on the device, the batch
+    // outputs, and the pinned staging both ways; grown on demand
+    void* hb_dev = nullptr;
+    size_t hb_dev_bytes = 0;
+    void* hb_pin = nullptr;
+    size_t hb_pin_bytes = 0;
 };

@@ -70,6 +70,28 @@ class ORBextractor:
         capi.check(rc, "orbx_extract")
         return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
 
+    def extract_batch(self, images, laps=None):
+        """operator() on several images of one size in one call (orbx_extract_batch):
+        a list of (keypoints, descriptors, monoIndex)."""
+        imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
+        if not imgs:
+            return []
+        h, w = imgs[0].shape
+        if any(im.ndim != 2 or im.shape != (h, w) for im in imgs):
+            raise ValueError("extract_batch expects 8UC1 images of one size")
+        nf = len(imgs)
+        ptrs = (C.c_void_p * nf)(*[im.ctypes.data for im in imgs])
+        lap = None if laps is None else np.ascontiguousarray(np.asarray(laps, np.int32).reshape(nf, 2))
+        cap = self.max_keypoints(w, h)
+        kps = np.zeros((nf, cap), abi.KEYPOINT_DTYPE)
+        desc = np.zeros((nf, cap, 32), np.uint8)
+        n = np.zeros(nf, np.int32)
+        mono = np.zeros(nf, np.int32)
+        rc = capi.lib().orbx_extract_batch(self._h, nf, ptrs, None, w, h, abi.ptr(lap), abi.ptr(kps), abi.ptr(desc),
+                                           cap, abi.ptr(n), abi.ptr(mono))
+        capi.check(rc, "orbx_extract_batch")
+        return [(kps[f, :n[f]].copy(), desc[f, :n[f]].copy(), int(mono[f])) for f in range(nf)]
+
     @property
     def mvImagePyramid(self):
         out = []

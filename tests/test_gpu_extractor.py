@@ -164,3 +164,24 @@ def test_full_size_batch_properties(gpu_lib):
             x = kl["x"] / scales[l]
             assert (x >= 18.5).all() and (x <= lw - 19.5).all()
         assert (k["class_id"] == -1).all()
+
+
+def test_extract_batch_host_images(gpu_lib):
+    """orbx_extract_batch: a stereo pair plus two more frames, per-frame lapping
+    areas (grouped into runs), one of them repeated; every frame identical to
+    the oracle on the same image."""
+    l, r = synth.stereo_pair(752, 480, 3000)
+    seq = synth.sequence(752, 480, 2, config=2, start=300)
+    imgs = [l, r, seq[0], seq[1]]
+    laps = [(0, 0), (0, 0), (200, 500), (0, 1000)]
+    ex, ref = pair()
+    out = ex.extract_batch(imgs, laps)
+    for im, lap, (k, d, m) in zip(imgs, laps, out):
+        rk, rd, rm = ref(im, lap)
+        assert (len(k), m) == (len(rk), rm)
+        assert np.array_equal(k.view(np.uint8), rk.view(np.uint8)), "keypoints differ"
+        assert np.array_equal(d, rd), "descriptors differ"
+    # default lapping ({0, 1000}) and a single frame
+    (k, d, m), = ex.extract_batch([seq[1]])
+    rk, rd, rm = ref(seq[1], (0, 1000))
+    assert (len(k), m) == (len(rk), rm) and np.array_equal(d, rd)
