@@ -260,6 +260,15 @@ typedef struct orbm_kf_map_device {
     const int64_t* fv_idx_off;   /* nkf */
 } orbm_kf_map_device;
 
+/* SearchByBoW(KF_i, F) for nkf host keyframes against one frame in one launch:
+ * the relocalisation loop over candidates (src/Tracking.cc:3641-3648).
+ * kfs[i], kfvs[i], kf_valid[i] as in orbm_search_by_bow; match_f: nkf x f->n
+ * (row i = candidate i's vpMapPointMatches as KF feature indices, -1 = none),
+ * counts: nkf.  Returns ORB_OK or an error. */
+int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_featvec* const* kfvs,
+                            const uint8_t* const* kf_valid, const orbm_frame* f, const orbm_featvec* ffv, float nnratio,
+                            int check_ori, int32_t* match_f, int32_t* counts);
+
 /* SearchByBoW(KF_i, F) for every keyframe of the map against one frame; f and
  * ffv hold DEVICE pointers.  d_match: nkf x f->n (KF feature index or -1),
  * d_nmatches: nkf.  Asynchronous on `stream`. */

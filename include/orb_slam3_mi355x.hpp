@@ -161,6 +161,23 @@ public:
         return nm;
     }
 
+    // The relocalisation loop (Tracking.cc:3641-3648): SearchByBoW(KF_i, F) for
+    // every candidate in one launch; returns the per-candidate counts and fills
+    // vvMatchesKFIdx[i] like the single form.
+    std::vector<int> SearchByBoW(const std::vector<const orbm_frame*>& KFs, const std::vector<const orbm_featvec*>& KFfvs,
+                                 const std::vector<const uint8_t*>& kfMapPointValid, const orbm_frame& F,
+                                 const orbm_featvec& Ffv, std::vector<std::vector<int>>& vvMatchesKFIdx) const {
+        const int nkf = (int)KFs.size();
+        std::vector<int32_t> match((size_t)nkf * F.n), counts(nkf);
+        const int rc = orbm_search_by_bow_many(nkf, KFs.data(), KFfvs.data(), kfMapPointValid.data(), &F, &Ffv,
+                                               mfNNratio, mbCheckOrientation, match.data(), counts.data());
+        if (rc != ORB_OK) throw std::runtime_error("SearchByBoW (many) failed");
+        vvMatchesKFIdx.assign(nkf, {});
+        for (int i = 0; i < nkf; ++i)
+            vvMatchesKFIdx[i].assign(match.begin() + (size_t)i * F.n, match.begin() + (size_t)(i + 1) * F.n);
+        return std::vector<int>(counts.begin(), counts.end());
+    }
+
     // int SearchByProjection(Frame &F, const vector<MapPoint*> &vpMapPoints, const float th=3, ...)
     int SearchByProjection(const orbm_frame& F, const orbm_mappoints& mps, std::vector<int>& owner,
                            const std::vector<uint8_t>& blocked, float th = 3, bool bFarPoints = false,

@@ -2416,6 +2416,67 @@ int orbm_search_by_bow_fisheye(const orbm_frame* kf, const orbm_featvec* kfv, co
     return bow_host(kf, kfv, kf_valid, f, ffv, f_nleft, nnratio, check_ori, match_f);
 }
 
+int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_featvec* const* kfvs,
+                            const uint8_t* const* kf_valid, const orbm_frame* f, const orbm_featvec* ffv, float nnratio,
+                            int check_ori, int32_t* match_f, int32_t* counts) {
+    if (nkf < 0 || (nkf && (!kfs || !kfvs || !kf_valid)) || !f || !ffv || !match_f || !counts) return ORB_ERR_PARAM;
+    for (int i = 0; i < nkf; ++i)
+        if (!kfs[i] || !kfvs[i] || !kf_valid[i] || kfs[i]->n < 0) return ORB_ERR_PARAM;
+    if (nkf == 0) return ORB_OK;
+    if (device_ok()) return ORB_ERR_DEVICE;
+    // the candidates packed like orbm_kf_map_device: features, FeatureVector
+    // nodes and per-keyframe CSR offsets concatenated
+    std::vector<long long> kp_off(nkf + 1, 0), node_off(nkf + 1, 0), idx_off(nkf, 0);
+    long long nidx = 0;
+    for (int i = 0; i < nkf; ++i) {
+        kp_off[i + 1] = kp_off[i] + kfs[i]->n;
+        node_off[i + 1] = node_off[i] + kfvs[i]->nnodes;
+        idx_off[i] = nidx;
+        nidx += kfvs[i]->nnodes ? kfvs[i]->offsets[kfvs[i]->nnodes] : 0;
+    }
+    const long long nkp = kp_off[nkf], nnode = node_off[nkf];
+    std::vector<orb_keypoint> kk((size_t)std::max(1LL, nkp));
+    std::vector<uint8_t> kd((size_t)std::max(1LL, nkp) * 32), kv((size_t)std::max(1LL, nkp));
+    std::vector<uint32_t> kn((size_t)std::max(1LL, nnode)), ki((size_t)std::max(1LL, nidx));
+    std::vector<int> ko((size_t)(nnode + nkf));
+    for (int i = 0; i < nkf; ++i) {
+        const orbm_frame* kf = kfs[i];
+        const orbm_featvec* fv = kfvs[i];
+        std::copy(kf->kps, kf->kps + kf->n, kk.begin() + kp_off[i]);
+        std::memcpy(kd.data() + kp_off[i] * 32, kf->desc, (size_t)kf->n * 32);
+        std::memcpy(kv.data() + kp_off[i], kf_valid[i], (size_t)kf->n);
+        std::copy(fv->node_ids, fv->node_ids + fv->nnodes, kn.begin() + node_off[i]);
+        for (int j = 0; j <= fv->nnodes; ++j) ko[(size_t)(node_off[i] + i + j)] = fv->nnodes ? fv->offsets[j] : 0;
+        const int ni = fv->nnodes ? fv->offsets[fv->nnodes] : 0;
+        std::copy(fv->idx, fv->idx + ni, ki.begin() + idx_off[i]);
+    }
+    int rc;
+    DBuf<orb_keypoint> dk, fk; DBuf<uint8_t> dd, dv, fd; DBuf<uint32_t> dn, di, fn, fi; DBuf<int> dof, fo;
+    DBuf<long long> dkpo, dnodo, didxo; DBuf<int32_t> out;
+    const int fidx = ffv->nnodes ? ffv->offsets[ffv->nnodes] : 0;
+    const int zero = 0;
+    if ((rc = dk.put(kk.data(), kk.size())) || (rc = dd.put(kd.data(), kd.size())) || (rc = dv.put(kv.data(), kv.size())) ||
+        (rc = dn.put(kn.data(), kn.size())) || (rc = dof.put(ko.data(), ko.size())) || (rc = di.put(ki.data(), ki.size())) ||
+        (rc = dkpo.put(kp_off.data(), kp_off.size())) || (rc = dnodo.put(node_off.data(), node_off.size())) ||
+        (rc = didxo.put(idx_off.data(), idx_off.size())) || (rc = fk.put(f->kps, std::max(1, f->n))) ||
+        (rc = fd.put(f->desc, (size_t)std::max(1, f->n) * 32)) || (rc = fn.put(ffv->node_ids, std::max(1, ffv->nnodes))) ||
+        (rc = fo.put(ffv->nnodes ? ffv->offsets : &zero, ffv->nnodes + 1)) || (rc = fi.put(ffv->idx, std::max(1, fidx))) ||
+        (rc = out.alloc((size_t)nkf * f->n + nkf)))
+        return rc;
+    BowArgs a{};
+    a.kf_kps = dk.p; a.kf_desc = dd.p; a.kf_valid = dv.p; a.kp_off = dkpo.p;
+    a.kf_node = dn.p; a.kf_off = dof.p; a.kf_idx = di.p; a.node_off = dnodo.p; a.idx_off = didxo.p;
+    a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
+    a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
+    a.match = out.p; a.nmatches = out.p + (size_t)nkf * f->n;
+    if ((rc = launch_bow(a, nkf, 0, bow_big_nodes(ffv), nnode))) return rc;
+    std::vector<int32_t> res((size_t)nkf * f->n + nkf);
+    ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
+    std::memcpy(match_f, res.data(), (size_t)nkf * f->n * sizeof(int32_t));
+    std::memcpy(counts, res.data() + (size_t)nkf * f->n, (size_t)nkf * sizeof(int32_t));
+    return ORB_OK;
+}
+
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f, const orbm_featvec* ffv,
                                     float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
     if (!map || !f || !ffv || !d_match || !d_nmatches || map->nkf < 0) return ORB_ERR_PARAM;

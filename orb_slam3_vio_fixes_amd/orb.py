@@ -337,6 +337,22 @@ class ORBmatcher:
         capi.check(nm, "SearchByBoW")
         return nm, match
 
+    def SearchByBoWMany(self, KFs, KFfvs, kf_valids, F: abi.Keep, Ffv: abi.Keep):
+        """SearchByBoW(KF_i, F) for several candidate keyframes in one launch
+        (orbm_search_by_bow_many; the loop of Tracking.cc:3641-3648):
+        (counts[nkf], match[nkf, F.n])."""
+        nkf = len(KFs)
+        valids = [np.ascontiguousarray(v, np.uint8) for v in kf_valids]
+        ks = (C.c_void_p * max(1, nkf))(*[C.addressof(k.struct) for k in KFs])
+        fs = (C.c_void_p * max(1, nkf))(*[C.addressof(k.struct) for k in KFfvs])
+        vs = (C.c_void_p * max(1, nkf))(*[v.ctypes.data for v in valids])
+        match = np.zeros((nkf, F.struct.n), np.int32)
+        counts = np.zeros(nkf, np.int32)
+        rc = capi.lib().orbm_search_by_bow_many(nkf, ks, fs, vs, F.ref(), Ffv.ref(), self.mfNNratio,
+                                                int(self.mbCheckOrientation), abi.ptr(match), abi.ptr(counts))
+        capi.check(rc, "SearchByBoWMany")
+        return counts, match
+
     def SearchByProjection(self, F: abi.Keep, mps: abi.Keep, th: float = 3.0, bFarPoints: bool = False,
                            thFarPoints: float = 50.0, owner=None, blocked=None):
         n = F.struct.n

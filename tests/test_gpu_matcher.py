@@ -192,3 +192,29 @@ def test_vocabulary_transform(gpu_lib, frames, k, levels, levelsup):
     ref = O.transform(voc, d, levelsup)
     for a, b in zip(got, ref):
         np.testing.assert_array_equal(a, b)
+
+
+def test_search_by_bow_many(gpu_lib, frames):
+    """orbm_search_by_bow_many: candidates of different sizes and node counts
+    (one with an empty FeatureVector, one with large nodes) in one launch; each
+    row identical to the oracle's SearchByBoW(KF_i, F)."""
+    rng = np.random.default_rng(77)
+    f = frames[1]
+    fnode = rng.integers(0, 20, len(f[0]))
+    F, Ffv = fr(f), abi.featvec_struct(fnode)
+    kfs, fvs, valids = [], [], []
+    for i, (nodes, n) in enumerate([(20, None), (4, 400), (20, 0), (60, 700), (2, None)]):
+        k, d = frames[(i + 2) % len(frames)][:2]
+        if n is not None:
+            k, d = k[:n], d[:n]
+        kn = rng.integers(0, nodes, len(k)) if len(k) else np.zeros(0, np.int64)
+        kfs.append(fr((k, d)))
+        fvs.append(abi.featvec_struct(kn))
+        valids.append((rng.random(len(k)) < 0.85).astype(np.uint8))
+    m = orb.ORBmatcher(0.75, True)
+    counts, match = m.SearchByBoWMany(kfs, fvs, valids, F, Ffv)
+    for i in range(len(kfs)):
+        rn, rm = O.search_by_bow(kfs[i], fvs[i], valids[i], F, Ffv, 0.75, True)
+        assert counts[i] == rn
+        np.testing.assert_array_equal(match[i], rm)
+    assert counts.sum() > 0
