@@ -109,6 +109,24 @@ def main():
                                       "cpu_ms_per_call": tc,
                                       "mismatched": sum(int(not same(x, y)) for x, y in zip(g, r)),
                                       "mean_matches": float(np.mean([x[0] for x in g]))}
+    # relocalisation: SearchByBoW(KF_i, F) over 10 candidates (Tracking.cc:3641-3648)
+    # as one orbm_search_by_bow_many call vs the oracle looping over them
+    cand = list(range(1, 11))
+    mm = orb.ORBmatcher(0.75, True)
+    args = ([fs[j] for j in cand], [fvs[j] for j in cand], [valid[j] for j in cand], fs[0], fvs[0])
+    mm.SearchByBoWMany(*args)
+    reps = 10
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        gc, gmatch = mm.SearchByBoWMany(*args)
+    tg = (time.perf_counter() - t0) / reps * 1e3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        rr = [O.search_by_bow(fs[j], fvs[j], valid[j], fs[0], fvs[0], 0.75, True) for j in cand]
+    tc = (time.perf_counter() - t0) / reps * 1e3
+    bad = sum(int(gc[i] != rr[i][0] or not np.array_equal(gmatch[i], rr[i][1])) for i in range(len(cand)))
+    res["search_by_bow_many"] = {"calls": reps, "candidates_per_call": len(cand), "gpu_ms_per_call": tg,
+                                 "cpu_ms_per_call": tc, "mismatched": bad, "mean_matches": float(np.mean(gc))}
     print(json.dumps({"metric": "loop-closing / relocalisation matchers, host APIs", "n_gpus": 1,
                       "data": "synthetic", "cpu_baseline_kind": "port, 1 thread", "results": res}), flush=True)
 
