@@ -633,8 +633,6 @@ struct BowArgs {
     int npairs;
     int32_t* match;      // [pair][f_n]  (-1 before k_bow)
     int32_t* nmatches;   // [pair]       (0 before k_bow)
-    int8_t* fbin;        // [pair][f_n]  rotation bin of the match of F feature, -1 = none
-    int* hist;           // [pair][32]   (0 before k_bow)
     const uint8_t* f_valid;   // KF-KF form: pKF2 MapPoint != NULL && !isBad(), else NULL
     int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
     int f_nleft = -1;         // the frame's Nleft (-1: mono / rectified)
@@ -690,15 +688,14 @@ __device__ __forceinline__ Best2 key_best2(int lo, int hi) {
 // The merge-join step of one (pair, node): KF node ia of pair pr against the
 // frame node's positions [fb, fe).  kLds: positions < kBowBigCap come from the
 // block's LDS copy (s_fd descriptor bytes 0-15 at [pos], 16-31 at
-// [kBowBigCap + pos]; s_fi frame index | invalid << 31; s_fa angle);
+// [kBowBigCap + pos]; s_fi frame index | invalid << 31);
 // otherwise the first kBowRegChunks chunks are loaded into registers.  Anything
 // past either reads global memory.
 template <bool kLds, bool kFish>
 __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
-                                         const uint4* s_fd, const int* s_fi, const float* s_fa, uint4* s_q) {
+                                         const uint4* s_fd, const int* s_fi, uint4* s_q) {
     const int lane = lane_id();
     const long long kpo = a.kp_off[pr];
-    const orb_keypoint* KK = a.kf_kps + kpo;
     const uint8_t* KD = a.kf_desc + kpo * 32;
     const uint8_t* KV = a.kf_valid + kpo;
     const int* ko = a.kf_off + a.node_off[pr] + pr;
@@ -711,17 +708,15 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
     const int nlds = kLds ? min(nch, kBowBigCap / kWave) : 0;   // chunks [0, nlds) in LDS
     uint4 fr0[kBowRegChunks], fr1[kBowRegChunks];
     int fir[kBowRegChunks];
-    float far_[kBowRegChunks];                       // the F feature's angle (rotation bin of a claim)
     uint64_t taken = 0;                              // bit c: (chunk c, this lane) is matched / invalid
     if constexpr (!kLds) {
 #pragma unroll
         for (int c = 0; c < kBowRegChunks; ++c) {
-            fr0[c] = make_uint4(0, 0, 0, 0); fr1[c] = fr0[c]; fir[c] = -1; far_[c] = 0.f;
+            fr0[c] = make_uint4(0, 0, 0, 0); fr1[c] = fr0[c]; fir[c] = -1;
             const int q = fb + c * kWave + lane;
             if (c < nch && q < fe) {
                 const int fi = (int)a.f_idx[q];
                 fir[c] = fi;
-                far_[c] = a.f_kps[fi].angle;
                 fr0[c] = *(const uint4*)(a.f_desc + (long long)fi * 32);
                 fr1[c] = *(const uint4*)(a.f_desc + (long long)fi * 32 + 16);
             }
@@ -746,13 +741,11 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
       const int pl = pbase + lane;
       int my_ikf = 0, my_ok = 0;
       uint4 mq0 = make_uint4(0, 0, 0, 0), mq1 = mq0;
-      float my_ang = 0.f;
       if (pl < pe) {
           my_ikf = (int)ki[pl];
           my_ok = KV[my_ikf];
           mq0 = *(const uint4*)(KD + (long long)my_ikf * 32);
           mq1 = *(const uint4*)(KD + (long long)my_ikf * 32 + 16);
-          my_ang = KK[my_ikf].angle;
       }
       if constexpr (!kLds) {
           // wave-private LDS copy: one KF descriptor is then two broadcast LDS
@@ -768,7 +761,6 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
       for (uint64_t rem = __ballot(my_ok != 0); rem; rem &= rem - 1) {
         const int src = __ffsll((long long)rem) - 1;
         const int ikf = __builtin_amdgcn_readlane(my_ikf, src);
-        const float kang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, my_ang), src));
         uint4 q0, q1;
         if constexpr (!kLds) {
             q0 = s_q[src];
@@ -835,29 +827,18 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
         const Best2 sr = fish ? key_best2<false>(rlo, rhi) : Best2{256, 256, -1, 0, 0};   // ratio not applied
         auto claim = [&](int pos) {                  // pos: position in the node's F list
             if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
-            // frame index and angle without a global round trip where they are staged
+            // the frame index without a global round trip where it is staged; the
+            // rotation bin of the match is k_bow_final's (it needs only the angles)
             int fi;
-            float fang;
             if (kLds && pos < kBowBigCap) {
                 fi = s_fi[pos] & 0x7fffffff;
-                fang = s_fa[pos];
             } else if (!kLds && pos < kBowRegChunks * kWave) {
                 const int c = pos >> 6, l = pos & (kWave - 1);
                 fi = __builtin_amdgcn_readlane(c == 0 ? fir[0] : fir[kBowRegChunks - 1], l);
-                fang = __builtin_bit_cast(float, __builtin_amdgcn_readlane(
-                    __builtin_bit_cast(int, c == 0 ? far_[0] : far_[kBowRegChunks - 1]), l));
             } else {
                 fi = (int)a.f_idx[fb + pos];
-                fang = a.check_ori ? a.f_kps[fi].angle : 0.f;
             }
-            if (lane == 0) {
-                match[fi] = ikf;
-                if (a.check_ori) {
-                    const int bn = rot_bin(kang, fang);
-                    atomicAdd(&a.hist[pr * 32 + bn], 1);
-                    a.fbin[(long long)pr * a.f_n + fi] = (int8_t)bn;
-                }
-            }
+            if (lane == 0) match[fi] = ikf;
             ++nm;
             if (nch > kBowMaskChunks) {              // the flag lives in `match` (global memory)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -916,8 +897,8 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         if (fl >= a.f_nnodes || fnode[fl] != na) continue;
         const int fb = foff[fl], fe = foff[fl + 1];
         if (fe - fb > kBowRegChunks * kWave) continue;  // a large-node block's
-        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr, s_q);
-        else bow_node<false, false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, nullptr, s_q);
+        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, s_q);
+        else bow_node<false, false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, s_q);
     }
 }
 
@@ -927,8 +908,7 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
 // Block bid = (keyframe group, slot): the group's large nodes are dealt
 // round-robin over `slots` blocks (one slot per large node for a single pair,
 // where the host knows the frame's node sizes; one slot for a map).
-__device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slots, uint4* s_fd, int* s_fi,
-                                             float* s_fa) {
+__device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slots, uint4* s_fd, int* s_fi) {
     const int slot = bid % slots;
     const int pr = (bid / slots) * kBowBigPairs + wave_id();
     long long k0 = 0, k1 = 0;
@@ -946,7 +926,6 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
             s_fd[p] = src[0];
             s_fd[kBowBigCap + p] = src[1];
             s_fi[p] = fi | ((a.f_valid && !a.f_valid[fi]) ? (int)0x80000000u : 0);
-            s_fa[p] = a.f_kps[fi].angle;
         }
         __syncthreads();
         const uint32_t na = a.f_node[fl];
@@ -957,8 +936,8 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
             else hi = mid;
         }
         if (lo < k1 && a.kf_node[lo] == na) {
-            if (a.f_nleft >= 0) bow_node<true, true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa, nullptr);
-            else bow_node<true, false>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, s_fa, nullptr);
+            if (a.f_nleft >= 0) bow_node<true, true>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, nullptr);
+            else bow_node<true, false>(a, pr, (int)(lo - k0), fb, fe, s_fd, s_fi, nullptr);
         }
     }
 }
@@ -971,58 +950,68 @@ static_assert(2 * kBowBigCap >= 4 * 2 * kWave, "s_fd holds the small-node waves'
 __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_slots) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
-    __shared__ float s_fa[kBowBigCap];
-    if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, big_slots, s_fd, s_fi, s_fa);
+    if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, big_slots, s_fd, s_fi);
     else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 2 * kWave);
 }
 
 // Rotation-consistency filter (:404-422 / :884-902) and the KF-KF output, one
-// wave per pair.
-__global__ __launch_bounds__(64) void k_bow_final(BowArgs a) {
-    const int pr = blockIdx.x, lane = lane_id();
+// workgroup per pair.  Every match of either track enters the reference's
+// histogram with the bin of (KF angle - F angle), so the bins are computed
+// here, lane-parallel over the frame features, instead of in the serial loop.
+constexpr int kBowFinalBins = 16384;    // frame features whose bin k_bow_final keeps in LDS
+
+__global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
+    const int pr = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
     int32_t* match = a.match + (long long)pr * a.f_n;
+    __shared__ int hist[32];
+    __shared__ int drop;
+    __shared__ uint8_t sbin[kBowFinalBins];             // bin of each match (one gather of the KF angle)
     if (a.check_ori) {
-        __shared__ int hist[32];
-        if (lane < 32) hist[lane] = a.hist[pr * 32 + lane];
+        const orb_keypoint* KK = a.kf_kps + a.kp_off[pr];
+        if (tid < 32) hist[tid] = 0;
+        if (tid == 0) drop = 0;
+        __syncthreads();
+        for (int i = tid; i < a.f_n; i += nt) {
+            const int m = match[i];
+            if (m < 0) continue;
+            const int b = rot_bin(KK[m].angle, a.f_kps[i].angle);
+            atomicAdd(&hist[b], 1);
+            if (i < kBowFinalBins) sbin[i] = (uint8_t)b;
+        }
         __syncthreads();
         int i1, i2, i3;
         three_maxima(hist, i1, i2, i3);
-        const int8_t* fbin = a.fbin + (long long)pr * a.f_n;
-        int drop = 0;
-        for (int i = lane; i < a.f_n; i += kWave) {
-            const int b = fbin[i];
-            if (b < 0 || b == i1 || b == i2 || b == i3) continue;
+        int d = 0;
+        for (int i = tid; i < a.f_n; i += nt) {
+            const int m = match[i];
+            if (m < 0) continue;
+            const int b = i < kBowFinalBins ? sbin[i] : rot_bin(KK[m].angle, a.f_kps[i].angle);
+            if (b == i1 || b == i2 || b == i3) continue;
             match[i] = -1;
-            ++drop;
+            ++d;
         }
-        drop = wave_sum(drop);
-        if (lane == 0) a.nmatches[pr] -= drop;
+        d = wave_sum(d);
+        if (lane_id() == 0 && d) atomicAdd(&drop, d);
+        __syncthreads();
+        if (tid == 0) a.nmatches[pr] -= drop;
     }
     if (a.out12) {
         __syncthreads();
         const long long kpo = a.kp_off[pr];
         const int kn1 = (int)(a.kp_off[pr + 1] - kpo);
         int32_t* o12 = a.out12 + kpo;
-        for (int i = lane; i < kn1; i += kWave) o12[i] = -1;
+        for (int i = tid; i < kn1; i += nt) o12[i] = -1;
         __syncthreads();
-        for (int i = lane; i < a.f_n; i += kWave)
+        for (int i = tid; i < a.f_n; i += nt)
             if (match[i] >= 0) o12[match[i]] = i;
     }
 }
 
-// Scratch for the BoW kernels (grows, per host thread).
-struct BowScratch {
-    int8_t* fbin = nullptr; size_t fbin_n = 0;
-    int* hist = nullptr; size_t hist_n = 0;
-    ~BowScratch() { if (fbin) (void)hipFree(fbin); if (hist) (void)hipFree(hist); }
-};
-
-// The per-call state of k_bow in one launch (instead of four memsets).
+// The per-call state of k_bow in one launch (instead of memsets).
 __global__ __launch_bounds__(256) void k_bow_init(BowArgs a) {
     const long long nmf = (long long)a.npairs * a.f_n, stride = (long long)gridDim.x * blockDim.x;
     const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    for (long long i = t0; i < nmf; i += stride) { a.match[i] = -1; a.fbin[i] = -1; }
-    for (long long i = t0; i < (long long)a.npairs * 32; i += stride) a.hist[i] = 0;
+    for (long long i = t0; i < nmf; i += stride) a.match[i] = -1;
     for (long long i = t0; i < a.npairs; i += stride) a.nmatches[i] = 0;
 }
 
@@ -1031,21 +1020,7 @@ __global__ __launch_bounds__(256) void k_bow_init(BowArgs a) {
 // FeatureVector nodes in all when the host knows them (a single pair: one
 // wave per node, for latency), else -1.
 static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1, long long kf_nodes = -1) {
-    static thread_local BowScratch sc;
-    const size_t nf = (size_t)npairs * std::max(1, a.f_n), nh = (size_t)npairs * 32;
-    if (sc.fbin_n < nf) {
-        if (sc.fbin) (void)hipFree(sc.fbin);
-        sc.fbin = nullptr; sc.fbin_n = 0;
-        if (hipMalloc(&sc.fbin, nf) != hipSuccess) return ORB_ERR_DEVICE;
-        sc.fbin_n = nf;
-    }
-    if (sc.hist_n < nh) {
-        if (sc.hist) (void)hipFree(sc.hist);
-        sc.hist = nullptr; sc.hist_n = 0;
-        if (hipMalloc(&sc.hist, nh * sizeof(int)) != hipSuccess) return ORB_ERR_DEVICE;
-        sc.hist_n = nh;
-    }
-    a.npairs = npairs; a.fbin = sc.fbin; a.hist = sc.hist;
+    a.npairs = npairs;
     {
         const long long nmf = (long long)npairs * a.f_n;
         const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
@@ -1056,7 +1031,7 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
     big_slots = std::max(1, big_slots);
     const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs * big_slots;
     KLAUNCH(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes), st, a, big_blocks, big_slots);
-    KLAUNCH(k_bow_final, dim3(npairs), dim3(64), 0, st, a);
+    KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
