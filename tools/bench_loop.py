@@ -109,6 +109,51 @@ def main():
                                       "cpu_ms_per_call": tc,
                                       "mismatched": sum(int(not same(x, y)) for x, y in zip(g, r)),
                                       "mean_matches": float(np.mean([x[0] for x in g]))}
+    # tracking: SearchByProjection(F, local map points) (TrackLocalMap, th 3) and
+    # SearchByProjection(F, LastFrame) (TrackWithMotionModel, th 7 at mode 0)
+    calls, calls_last = [], []
+    for j in range(1, 11):
+        k, d = kfs[j]
+        n = 3000
+        src = rng.integers(0, len(k), n)
+        qx = (k["x"][src] + rng.normal(0, 2, n)).astype(np.float32)
+        qy = (k["y"][src] + rng.normal(0, 2, n)).astype(np.float32)
+        lvl = np.clip(k["octave"][src] + rng.integers(0, 2, n), 0, 7).astype(np.int32)
+        qd = d[src].copy()
+        qd[rng.random((n, 32)) < 0.03] ^= np.uint8(0x10)
+        mps = abi.mappoints_struct(qx, qy, qx - 20, lvl, rng.uniform(0.99, 1.0, n).astype(np.float32),
+                                   rng.uniform(0, 100, n).astype(np.float32), (rng.random(n) < 0.9).astype(np.uint8),
+                                   (rng.random(n) < 0.7).astype(np.uint8), qd)
+        owner = np.full(len(k), -1, np.int32)
+        calls.append((fs[j], mps, owner))
+        nl = 1000
+        sl = src[:nl]
+        calls_last.append((fs[j], (rng.random(nl) < 0.9).astype(np.uint8), qx[:nl], qy[:nl], (qx[:nl] - 20),
+                           k["octave"][sl].astype(np.int32), k["angle"][sl], (rng.random(nl) < 0.7).astype(np.uint8),
+                           qd[:nl], 7.0, 0))
+    mp = orb.ORBmatcher(0.8, True)
+    f_mps = lambda F, mps, owner: mp.SearchByProjection(F, mps, 3.0, False, 50.0, owner, None)
+    r_mps = lambda F, mps, owner: O.search_by_projection_mps(F, mps, 3.0, False, 50.0, 0.8, owner,
+                                                             np.zeros(F.struct.n, np.uint8))
+    f_mps(*calls[0])
+    g, tg = timed(f_mps, calls)
+    r, tc = timed(r_mps, calls)
+    res["search_by_projection_mps"] = {"calls": len(calls), "points_per_call": 3000, "gpu_ms_per_call": tg,
+                                       "cpu_ms_per_call": tc,
+                                       "mismatched": sum(int(not same(x, y)) for x, y in zip(g, r)),
+                                       "mean_matches": float(np.mean([x[0] for x in g]))}
+    ml = orb.ORBmatcher(0.9, True)
+    zero = lambda F: (np.full(F.struct.n, -1, np.int32), np.zeros(F.struct.n, np.uint8))
+    f_last = lambda F, *q: ml.SearchByProjectionLast(F, *q, owner=zero(F)[0], blocked=zero(F)[1])
+    r_last = lambda F, *q: O.search_by_projection_last(F, *q, True, *zero(F))
+    f_last(*calls_last[0])
+    g, tg = timed(f_last, calls_last)
+    r, tc = timed(r_last, calls_last)
+    res["search_by_projection_last"] = {"calls": len(calls_last), "points_per_call": 1000, "gpu_ms_per_call": tg,
+                                        "cpu_ms_per_call": tc,
+                                        "mismatched": sum(int(not same(x, y)) for x, y in zip(g, r)),
+                                        "mean_matches": float(np.mean([x[0] for x in g]))}
+
     # relocalisation: SearchByBoW(KF_i, F) over 10 candidates (Tracking.cc:3641-3648)
     # as one orbm_search_by_bow_many call vs the oracle looping over them
     cand = list(range(1, 11))
@@ -127,7 +172,7 @@ def main():
     bad = sum(int(gc[i] != rr[i][0] or not np.array_equal(gmatch[i], rr[i][1])) for i in range(len(cand)))
     res["search_by_bow_many"] = {"calls": reps, "candidates_per_call": len(cand), "gpu_ms_per_call": tg,
                                  "cpu_ms_per_call": tc, "mismatched": bad, "mean_matches": float(np.mean(gc))}
-    print(json.dumps({"metric": "loop-closing / relocalisation matchers, host APIs", "n_gpus": 1,
+    print(json.dumps({"metric": "tracking / relocalisation / loop-closing matchers, host APIs", "n_gpus": 1,
                       "data": "synthetic", "cpu_baseline_kind": "port, 1 thread", "results": res}), flush=True)
 
 
