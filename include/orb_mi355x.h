@@ -136,7 +136,7 @@ int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);
 /* orbx_extract_batch_device splits a batch into up to `nsub` frame ranges
  * (each >= 16 frames) run on private streams that fork from and join back into
  * the caller's stream; results are identical for every nsub.  With profiling
- * on, each range is one recorded call.  Default 2.  Not part of the reference
+ * on, each range is one recorded call.  Default 1.  Not part of the reference
  * interface. */
 int orbx_set_streams(orbx_handle* h, int nsub);
 
