@@ -2418,8 +2418,10 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
         const orbm_frame* kf = kfs[i];
         const orbm_featvec* fv = kfvs[i];
         std::copy(kf->kps, kf->kps + kf->n, kk.begin() + kp_off[i]);
-        std::memcpy(kd.data() + kp_off[i] * 32, kf->desc, (size_t)kf->n * 32);
-        std::memcpy(kv.data() + kp_off[i], kf_valid[i], (size_t)kf->n);
+        if (kf->n) {
+            std::memcpy(kd.data() + kp_off[i] * 32, kf->desc, (size_t)kf->n * 32);
+            std::memcpy(kv.data() + kp_off[i], kf_valid[i], (size_t)kf->n);
+        }
         std::copy(fv->node_ids, fv->node_ids + fv->nnodes, kn.begin() + node_off[i]);
         for (int j = 0; j <= fv->nnodes; ++j) ko[(size_t)(node_off[i] + i + j)] = fv->nnodes ? fv->offsets[j] : 0;
         const int ni = fv->nnodes ? fv->offsets[fv->nnodes] : 0;
@@ -2433,9 +2435,9 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
     if ((rc = dk.put(kk.data(), kk.size())) || (rc = dd.put(kd.data(), kd.size())) || (rc = dv.put(kv.data(), kv.size())) ||
         (rc = dn.put(kn.data(), kn.size())) || (rc = dof.put(ko.data(), ko.size())) || (rc = di.put(ki.data(), ki.size())) ||
         (rc = dkpo.put(kp_off.data(), kp_off.size())) || (rc = dnodo.put(node_off.data(), node_off.size())) ||
-        (rc = didxo.put(idx_off.data(), idx_off.size())) || (rc = fk.put(f->kps, std::max(1, f->n))) ||
-        (rc = fd.put(f->desc, (size_t)std::max(1, f->n) * 32)) || (rc = fn.put(ffv->node_ids, std::max(1, ffv->nnodes))) ||
-        (rc = fo.put(ffv->nnodes ? ffv->offsets : &zero, ffv->nnodes + 1)) || (rc = fi.put(ffv->idx, std::max(1, fidx))) ||
+        (rc = didxo.put(idx_off.data(), idx_off.size())) || (rc = fk.put(f->kps, f->n)) ||
+        (rc = fd.put(f->desc, (size_t)f->n * 32)) || (rc = fn.put(ffv->node_ids, ffv->nnodes)) ||
+        (rc = fo.put(ffv->nnodes ? ffv->offsets : &zero, ffv->nnodes + 1)) || (rc = fi.put(ffv->idx, fidx)) ||
         (rc = out.alloc((size_t)nkf * f->n + nkf)))
         return rc;
     BowArgs a{};

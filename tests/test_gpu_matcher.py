@@ -218,3 +218,7 @@ def test_search_by_bow_many(gpu_lib, frames):
         assert counts[i] == rn
         np.testing.assert_array_equal(match[i], rm)
     assert counts.sum() > 0
+    # an empty frame (no features, empty FeatureVector): every count 0
+    e = (np.zeros(0, abi.KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8))
+    c0, m0 = m.SearchByBoWMany(kfs, fvs, valids, fr(e), abi.featvec_struct(np.zeros(0, np.int64)))
+    assert (c0 == 0).all() and m0.shape == (len(kfs), 0)
