@@ -4,6 +4,7 @@
 // for tests/test_gpu_cpp_api.py to compare with the oracle.
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "../../include/orb_slam3_mi355x.hpp"
@@ -60,6 +61,44 @@ int main(int argc, char** argv) {
     std::vector<int> b12;
     ORB_SLAM3_MI355X::ORBmatcher loop_matcher(0.75f, true);
     const int nb = loop_matcher.SearchByBoW(f[0], fv[0], valid[0], f[1], fv[1], valid[1], b12);
+    // ExtractBatch == the single calls
+    {
+        std::vector<std::vector<ORB_SLAM3_MI355X::KeyPoint>> kb;
+        std::vector<ORB_SLAM3_MI355X::Descriptors> db;
+        const std::vector<int> mb = ex.ExtractBatch({im[0].data(), im[1].data()}, {(size_t)cols, (size_t)cols}, cols,
+                                                    rows, {{0, 1000}, {0, 1000}}, kb, db);
+        for (int i = 0; i < 2; ++i)
+            if (mb[i] != mono[i] || kb[i].size() != k[i].size() || db[i].data != d[i].data ||
+                std::memcmp(kb[i].data(), k[i].data(), k[i].size() * sizeof(orb_keypoint)) != 0)
+                return 5;
+    }
+    // SearchByBoW over candidates == the single form
+    {
+        std::vector<int> single, unused;
+        ORB_SLAM3_MI355X::ORBmatcher m(0.75f, true);
+        const int ns = m.SearchByBoW(f[0], fv[0], valid[0], f[1], fv[1], single);
+        std::vector<std::vector<int>> many;
+        const std::vector<int> cnt = m.SearchByBoW({&f[0], &f[0]}, {&fv[0], &fv[0]}, {valid[0].data(), valid[0].data()},
+                                                   f[1], fv[1], many);
+        if (cnt.size() != 2 || cnt[0] != ns || cnt[1] != ns || many[0] != single || many[1] != single) return 6;
+    }
+    // SearchForTriangulation with an accept-all check == the pinhole form with bCoarse and the epipole out of reach
+    {
+        const std::vector<uint8_t> no_mp0(k[0].size(), 0), no_mp1(k[1].size(), 0);
+        const std::vector<float> sig2(8, 1.f);
+        const float F12[9] = {0, 0, 0, 0, 0, 0, 0, 0, 1};
+        std::vector<float> sc(8, 1.f);
+        orbm_frame g1 = f[1];
+        g1.scale_factors = sc.data();
+        g1.nlevels = 8;
+        std::vector<std::pair<size_t, size_t>> pa, pb;
+        ORB_SLAM3_MI355X::ORBmatcher m(0.6f, true);
+        const int na = m.SearchForTriangulation(f[0], fv[0], no_mp0, g1, fv[1], no_mp1, F12, -1e6f, -1e6f, sig2, pa,
+                                                false, true);
+        const int nb2 = m.SearchForTriangulation(f[0], fv[0], no_mp0, g1, fv[1], no_mp1,
+                                                 [](int, int) { return true; }, pb, false);
+        if (na != nb2 || pa != pb || na <= 0) return 7;
+    }
     std::printf("%zu %d %016llx %016llx %zu %d %d %016llx %d %016llx\n", k[0].size(), mono[0],
                 (unsigned long long)fnv(k[0].data(), k[0].size() * sizeof(orb_keypoint)),
                 (unsigned long long)fnv(d[0].data.data(), d[0].data.size()), k[1].size(), mono[1], nm,
