@@ -708,6 +708,7 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
     const int nlds = kLds ? min(nch, kBowBigCap / kWave) : 0;   // chunks [0, nlds) in LDS
     uint4 fr0[kBowRegChunks], fr1[kBowRegChunks];
     int fir[kBowRegChunks];
+    int mcl[kBowRegChunks] = {-1, -1};               // register chunks: this lane's claim (KF feature)
     uint64_t taken = 0;                              // bit c: (chunk c, this lane) is matched / invalid
     if constexpr (!kLds) {
 #pragma unroll
@@ -826,19 +827,21 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
         const Best2 st = key_best2<true>(klo, khi);
         const Best2 sr = fish ? key_best2<false>(rlo, rhi) : Best2{256, 256, -1, 0, 0};   // ratio not applied
         auto claim = [&](int pos) {                  // pos: position in the node's F list
-            if ((pos >> 6) < kBowMaskChunks && lane == (pos & (kWave - 1))) taken |= 1ull << (pos >> 6);
-            // the frame index without a global round trip where it is staged; the
-            // rotation bin of the match is k_bow_final's (it needs only the angles)
-            int fi;
-            if (kLds && pos < kBowBigCap) {
-                fi = s_fi[pos] & 0x7fffffff;
-            } else if (!kLds && pos < kBowRegChunks * kWave) {
-                const int c = pos >> 6, l = pos & (kWave - 1);
-                fi = __builtin_amdgcn_readlane(c == 0 ? fir[0] : fir[kBowRegChunks - 1], l);
+            const bool mine = lane == (pos & (kWave - 1));
+            if ((pos >> 6) < kBowMaskChunks && mine) taken |= 1ull << (pos >> 6);
+            // register chunks: the owning lane keeps the claim and the node's
+            // matches go out as one coalesced store per chunk at its end; elsewhere
+            // the frame index comes from the LDS copy or global memory.  (The
+            // rotation bin of a match is k_bow_final's: it needs only the angles.)
+            if (!kLds && pos < kBowRegChunks * kWave) {
+                if (mine) {
+                    if (pos < kWave) mcl[0] = ikf;
+                    else mcl[kBowRegChunks - 1] = ikf;
+                }
             } else {
-                fi = (int)a.f_idx[fb + pos];
+                const int fi = (kLds && pos < kBowBigCap) ? (s_fi[pos] & 0x7fffffff) : (int)a.f_idx[fb + pos];
+                if (lane == 0) match[fi] = ikf;
             }
-            if (lane == 0) match[fi] = ikf;
             ++nm;
             if (nch > kBowMaskChunks) {              // the flag lives in `match` (global memory)
                 __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
@@ -850,6 +853,11 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
         if (low && (float)st.best < a.ratio * (float)st.best2) claim(st.idx);
         if (fish && low && sr.best <= kThLow) claim(sr.idx);                   // :357-386, ratio ignored
       }
+    }
+    if constexpr (!kLds) {
+#pragma unroll
+        for (int c = 0; c < kBowRegChunks; ++c)
+            if (mcl[c] >= 0) match[fir[c]] = mcl[c];
     }
     if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
 }
