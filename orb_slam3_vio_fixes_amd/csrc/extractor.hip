@@ -91,6 +91,7 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     Plan& P = hd->plan;
     if (P.w == w && P.h == h && P.maxB >= maxB && P.L == hd->prm.nlevels) return ORB_OK;
     P.release();
+    ++hd->plan_epoch;                                        // captured graphs point at the old buffers
     if (w > 4096 + 16 || h > 4096 + 16) return ORB_ERR_UNSUPPORTED;   // 12-bit key coordinates
     const int L = hd->prm.nlevels;
     P.w = w; P.h = h; P.L = L; P.maxB = maxB;
@@ -1772,6 +1773,9 @@ void orbx_destroy(orbx_handle* h) {
     if (h->st_scratch) (void)hipFree(h->st_scratch);
     if (h->hb_dev) (void)hipFree(h->hb_dev);
     if (h->hb_pin) (void)hipHostFree(h->hb_pin);
+    if (h->x_exec) (void)hipGraphExecDestroy(h->x_exec);
+    if (h->x_stream) (void)hipStreamDestroy(h->x_stream);
+    if (h->x_pin) (void)hipHostFree(h->x_pin);
     delete h;
 }
 
@@ -1887,6 +1891,64 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
     return over ? ORB_ERR_CAPACITY : ORB_OK;
 }
 
+// orbx_extract's launch-bound sequence (upload, ~12 dependent kernels, four
+// downloads) as one hipGraph, captured per (size, lapping, plan epoch, staging
+// buffer) and replayed; the host copies the image into the pinned staging
+// buffer and reads the outputs back from it after one synchronisation.
+static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step, int lap0, int lap1,
+                         orb_keypoint* kps, uint8_t* desc, int cap, int* n_out, int* mono_out) {
+    Plan& P = h->plan;
+    const size_t in_b = (size_t)P.in_pitch * hh, kp_b = (size_t)P.host_cap * sizeof(orb_keypoint),
+                 de_b = (size_t)P.host_cap * 32;
+    const size_t o_kp = (in_b + 255) & ~size_t(255), o_de = o_kp + ((kp_b + 255) & ~size_t(255)),
+                 o_nm = o_de + ((de_b + 255) & ~size_t(255)), total = o_nm + 16;
+    if (h->x_pin_bytes < total) {
+        if (h->x_pin) (void)hipHostFree(h->x_pin);
+        h->x_pin = nullptr; h->x_pin_bytes = 0;
+        if (hipHostMalloc(&h->x_pin, total, hipHostMallocDefault) != hipSuccess) return ORB_ERR_DEVICE;
+        h->x_pin_bytes = total;
+        ++h->x_pin_gen;
+    }
+    if (!h->x_stream && hipStreamCreateWithFlags(&h->x_stream, hipStreamNonBlocking) != hipSuccess)
+        return ORB_ERR_DEVICE;
+    uint8_t* pin = (uint8_t*)h->x_pin;
+    const long long key[6] = {w, hh, lap0, lap1, h->plan_epoch, h->x_pin_gen};
+    if (!h->x_exec || !std::equal(key, key + 6, h->x_key)) {
+        if (h->x_exec) (void)hipGraphExecDestroy(h->x_exec);
+        h->x_exec = nullptr;
+        hipStream_t st = h->x_stream;
+        if (hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed) != hipSuccess) return ORB_ERR_DEVICE;
+        bool ok = hipMemcpyAsync(P.d_in, pin, in_b, hipMemcpyHostToDevice, st) == hipSuccess;
+        ok = ok && run_pipeline(h, 0, 1, P.d_in, (long long)in_b, (int)P.in_pitch, (float)lap0, (float)lap1, P.d_kps,
+                                P.d_desc, P.host_cap, P.d_n, P.d_mono, st) == ORB_OK;
+        ok = ok && hipMemcpyAsync(pin + o_kp, P.d_kps, kp_b, hipMemcpyDeviceToHost, st) == hipSuccess;
+        ok = ok && hipMemcpyAsync(pin + o_de, P.d_desc, de_b, hipMemcpyDeviceToHost, st) == hipSuccess;
+        ok = ok && hipMemcpyAsync(pin + o_nm, P.d_n, 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+        ok = ok && hipMemcpyAsync(pin + o_nm + 4, P.d_mono, 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+        hipGraph_t g = nullptr;
+        const bool ended = hipStreamEndCapture(st, &g) == hipSuccess;
+        if (ok && ended && g) ok = hipGraphInstantiate(&h->x_exec, g, nullptr, nullptr, 0) == hipSuccess;
+        if (g) (void)hipGraphDestroy(g);
+        (void)hipGetLastError();
+        if (!ok || !ended || !h->x_exec) { h->x_exec = nullptr; return ORB_ERR_UNSUPPORTED; }
+        std::copy(key, key + 6, h->x_key);
+    }
+    for (int y = 0; y < hh; ++y) std::memcpy(pin + (size_t)y * P.in_pitch, img + (size_t)y * step, w);
+    ORB_CHECK(hipGraphLaunch(h->x_exec, h->x_stream));
+    ORB_CHECK(hipStreamSynchronize(h->x_stream));
+    const int32_t n = *(const int32_t*)(pin + o_nm), mono = *(const int32_t*)(pin + o_nm + 4);
+    if (n_out) *n_out = n;
+    if (mono_out) *mono_out = mono;
+    h->have_last = true;
+    h->last_w = w; h->last_h = hh;
+    if (n > cap) return ORB_ERR_CAPACITY;
+    if (n > 0) {
+        std::memcpy(kps, pin + o_kp, (size_t)n * sizeof(orb_keypoint));
+        std::memcpy(desc, pin + o_de, (size_t)n * 32);
+    }
+    return ORB_OK;
+}
+
 int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step, int lap0, int lap1,
                  orb_keypoint* kps, uint8_t* desc, int cap, int* n_out, int* mono_out) {
     if (!h) return ORB_ERR_PARAM;
@@ -1895,6 +1957,12 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
     int rc = build_plan(h, w, hh, std::max(1, h->plan.maxB));
     if (rc) return rc;
     Plan& P = h->plan;
+    // the graph path unless per-stage profiling is on (its events are recorded
+    // per call) or capture is unavailable (then the direct launches below)
+    if (!h->profiling) {
+        rc = extract_graph(h, img, w, hh, step, lap0, lap1, kps, desc, cap, n_out, mono_out);
+        if (rc != ORB_ERR_UNSUPPORTED) return rc;
+    }
     ORB_CHECK(hipMemcpy2D(P.d_in, P.in_pitch, img, step, w, hh, hipMemcpyHostToDevice));
     rc = run_pipeline(h, 0, 1, P.d_in, (long long)P.in_pitch * hh, (int)P.in_pitch, (float)lap0, (float)lap1, P.d_kps,
                       P.d_desc, P.host_cap, P.d_n, P.d_mono, 0);

@@ -105,4 +105,13 @@ struct orbx_handle {
     size_t hb_dev_bytes = 0;
     void* hb_pin = nullptr;
     size_t hb_pin_bytes = 0;
+    // orbx_extract as one captured hipGraph (upload, pipeline, downloads) per
+    // (size, lapping, plan epoch, staging buffer); build_plan bumps the epoch
+    int plan_epoch = 0;
+    hipStream_t x_stream = nullptr;
+    hipGraphExec_t x_exec = nullptr;
+    long long x_key[6] = {0, 0, 0, 0, -1, 0};
+    void* x_pin = nullptr;
+    size_t x_pin_bytes = 0;
+    int x_pin_gen = 0;
 };
