@@ -1367,7 +1367,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             const int x0 = (int)(nxt.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((nxt.key >> 12) & 0xfff) + (kEdge - 3) - 21;
             if (patch_interior(nxt.w, nxt.h, x0, y0)) patch_issue(nxt.img, nxt.pitch, x0, y0, pv);
         }
-        const uint8_t* R = raw + sh;
         wave_sync();
         DESC_T(d0);
 #ifdef ORB_DESC_TIMING

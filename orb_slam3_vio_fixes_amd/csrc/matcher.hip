@@ -36,7 +36,6 @@ static hipError_t flush_uploads();
 
 constexpr int kGridCols = 64, kGridRows = 48;        // Frame.h:44-45
 constexpr int kThHigh = 100, kThLow = 50, kHisto = 30;   // ORBmatcher.cc:35-37
-constexpr int kGridInvalid = 0x7fff;
 
 struct GridParams { float min_x, min_y, inv_w, inv_h; };
 
