@@ -24,6 +24,7 @@
 #include <cstring>
 #include <memory>
 #include <type_traits>
+#include <thread>
 #include <vector>
 
 namespace orbmi {
@@ -1848,10 +1849,22 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
     }
     uint8_t* dev = (uint8_t*)h->hb_dev;
     uint8_t* pin = (uint8_t*)h->hb_pin;
-    // one upload: the frames gathered into pinned memory at a common pitch
-    for (int f = 0; f < nframes; ++f) {
-        const size_t st = steps ? steps[f] : (size_t)w;
-        for (int y = 0; y < hh; ++y) std::memcpy(pin + f * fbytes + y * pitch, imgs[f] + y * st, w);
+    // one upload: the frames gathered into pinned memory at a common pitch (a
+    // few host threads for larger batches: the gather is the host-side cost)
+    auto gather = [&](int f0, int f1) {
+        for (int f = f0; f < f1; ++f) {
+            const size_t st = steps ? steps[f] : (size_t)w;
+            for (int y = 0; y < hh; ++y) std::memcpy(pin + f * fbytes + y * pitch, imgs[f] + y * st, w);
+        }
+    };
+    const int nth = std::min(8, nframes / 16);              // >= 16 frames per thread
+    if (nth <= 1) {
+        gather(0, nframes);
+    } else {
+        std::vector<std::thread> th;
+        for (int t = 0; t < nth; ++t)
+            th.emplace_back(gather, (int)((long long)nframes * t / nth), (int)((long long)nframes * (t + 1) / nth));
+        for (auto& x : th) x.join();
     }
     ORB_CHECK(hipMemcpyAsync(dev, pin, in_b, hipMemcpyHostToDevice, 0));
     orb_keypoint* d_kps = (orb_keypoint*)(dev + o_kp);
