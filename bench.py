@@ -60,7 +60,10 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
     ap.add_argument("--cpu-sample", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="threads of the CPU-baseline pool (0 = the cores this process may run on, at most 16)")
+    ap.add_argument("--no-host-api", dest="host_api", action="store_false",
+                    help="skip the PCIe-inclusive drop-in latency leg")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--pmc-summary", default=str(PMC_SUMMARY), help="rocprofv3 PMC summary (tools/pmc_summary.py)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
@@ -116,14 +119,14 @@ def stage_roofline(ex, stage_ms, frames_per_launch, kps_per_frame):
     return out
 
 
-def cpu_baseline(frames_np, threads):
+def cpu_baseline(frames_np, threads, lib_path):
     """The CPU oracle on the host: extraction + SearchForInitialization on the
-    same consecutive pairs; frames spread over a thread pool (ctypes releases
-    the GIL).  Returns (frames/s, outputs)."""
+    same consecutive pairs; frames spread over a pool of `threads` threads
+    (ctypes releases the GIL).  Returns (frames/s, outputs, {pair: (nm, m12)})."""
     from oracle import oracle as O
     from orb_slam3_vio_fixes_amd import abi
     n = len(frames_np)
-    exs = [O.OracleExtractor(NFEAT, 1.2, 8, 20, 7) for _ in range(threads)]
+    exs = [O.OracleExtractor(NFEAT, 1.2, 8, 20, 7, lib_path=lib_path) for _ in range(threads)]
     outs = [None] * n
 
     def work(t):
@@ -139,13 +142,65 @@ def cpu_baseline(frames_np, threads):
             k1, d1, _ = outs[i]
             k2, d2, _ = outs[i + 1]
             prev = np.stack([k1["x"], k1["y"]], 1)
-            res.append((i, O.search_for_initialization(abi.frame_struct(k1, d1, W, H), abi.frame_struct(k2, d2, W, H),
-                                                       prev, 100, 0.9, True)[0]))
+            nm, m12, _ = O.search_for_initialization(abi.frame_struct(k1, d1, W, H), abi.frame_struct(k2, d2, W, H),
+                                                     prev, 100, 0.9, True, lib_path=lib_path)
+            res.append((i, (nm, m12)))
         return res
     with ThreadPoolExecutor(threads) as pool:
         nms = dict(x for r in pool.map(match, range(threads)) for x in r)
     dt = time.perf_counter() - t0
     return n / dt, outs, nms
+
+
+def cpu_single_thread(frames_np, lib_path, seconds=4.0):
+    """The reference's own threading model for a monocular stream: the
+    Tracking thread extracts one image at a time (Frame.cc:418-425; a stereo
+    frame runs its two images on two threads, Frame.cc:122-125) and matches it
+    against the previous frame.  One thread, frames in order, for about
+    `seconds`.  Returns (frames/s, frames done)."""
+    from oracle import oracle as O
+    from orb_slam3_vio_fixes_amd import abi
+    ex = O.OracleExtractor(NFEAT, 1.2, 8, 20, 7, lib_path=lib_path)
+    prev = None
+    t0 = time.perf_counter()
+    done = 0
+    for img in frames_np:
+        cur = ex(img, LAP)
+        if prev is not None:
+            k1, d1, _ = prev
+            O.search_for_initialization(abi.frame_struct(k1, d1, W, H), abi.frame_struct(cur[0], cur[1], W, H),
+                                        np.stack([k1["x"], k1["y"]], 1), 100, 0.9, True, lib_path=lib_path)
+        prev = cur
+        done += 1
+        if time.perf_counter() - t0 > seconds:
+            break
+    return done / (time.perf_counter() - t0), done
+
+
+def host_api_rates(frames_np, reps=200):
+    """PCIe-inclusive rates of the Tracking thread's drop-in calls (host image
+    in, host keypoints out): orbx_extract one image per call (Frame.cc:418-425)
+    and orbx_extract_batch on a stereo pair per call (Frame.cc:122-125).  Not
+    the metric (that is HBM-resident); the drop-in latency."""
+    from orb_slam3_vio_fixes_amd import orb
+    ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7)
+    imgs = [np.ascontiguousarray(f) for f in frames_np[:16]]
+    for i in range(10):
+        ex(imgs[i % len(imgs)], None, LAP)
+    t0 = time.perf_counter()
+    for i in range(reps):
+        ex(imgs[i % len(imgs)], None, LAP)
+    single = (time.perf_counter() - t0) / reps
+    for i in range(5):
+        ex.extract_batch([imgs[i % 16], imgs[(i + 1) % 16]], [LAP, LAP])
+    t0 = time.perf_counter()
+    for i in range(reps // 2):
+        ex.extract_batch([imgs[i % 16], imgs[(i + 1) % 16]], [LAP, LAP])
+    pair = (time.perf_counter() - t0) / (reps // 2)
+    return {"orbx_extract_ms": single * 1e3, "orbx_extract_frames_per_s": 1.0 / single,
+            "orbx_extract_batch_stereo_pair_ms": pair * 1e3, "orbx_extract_batch_frames_per_s": 2.0 / pair,
+            "calls": reps, "image": f"{W}x{H} u8, host memory, outputs copied back to host",
+            "note": "PCIe-inclusive drop-in rate (one Tracking-thread call at a time); not the metric"}
 
 
 def main():
@@ -184,6 +239,7 @@ def main():
     # stream while step k+1 extracts into the other set (--no-pipeline: both
     # on the extraction stream)
     outs = [(kps, desc, n, mono), tuple(torch.empty_like(x) for x in (kps, desc, n, mono))]
+    outs_dev = outs
     mstream = torch.cuda.Stream(dev) if args.pipeline else stream
     done = [None, None]                  # match of set i finished (recorded on mstream)
     matches = torch.empty((B - 1, cap), dtype=torch.int32, device=dev)
@@ -278,25 +334,46 @@ def main():
                "stage_roofline": stage_roofline(ex, dict(zip(STAGES, map(float, stage_ms))), frames_per_launch,
                                                 float(n.float().mean().item()))}
         if world == 1 and args.cpu_sample > 0:
+            from oracle import oracle as O
             ns = min(args.cpu_sample, B)
-            fps, outs, nms = cpu_baseline(frames_np[:ns], args.cpu_threads)
-            # parity of the sampled frames (the CPU leg doubles as a checker)
-            kh = kps[:ns].cpu().numpy()
-            dh = desc[:ns].cpu().numpy()
-            nh = n[:ns].cpu().numpy()
+            avail = len(os.sched_getaffinity(0))
+            threads = args.cpu_threads or min(16, avail)
+            lib_path, flags = O.fast_variant()
+            fps, outs, nms = cpu_baseline(frames_np[:ns], threads, lib_path)
+            fps1, n1 = cpu_single_thread(frames_np[:ns], lib_path)
+            # parity of the sampled frames (the CPU leg doubles as a checker):
+            # every keypoint byte, descriptor, and the whole matches12 array
+            # of every sampled pair (the output set of the last step)
+            last = outs_dev[(counter[0] - 1) % 2]
+            kh = last[0][:ns].cpu().numpy()
+            dh = last[1][:ns].cpu().numpy()
+            nh = last[2][:ns].cpu().numpy()
             mh = nmatch[:ns - 1].cpu().numpy()
+            m12h = matches[:ns - 1].cpu().numpy()
             bad = 0
             for i in range(ns):
                 rk, rd, _ = outs[i]
                 if nh[i] != len(rk) or not np.array_equal(orb.keypoints_from_device(kh[i][:nh[i]]).view(np.uint8),
                                                           rk.view(np.uint8)) or not np.array_equal(dh[i][:nh[i]], rd):
                     bad += 1
-            bad_m = sum(int(mh[i] != nms[i]) for i in range(ns - 1))
-            out["cpu_baseline"] = {"value": fps, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
-                                   "sample": f"first {ns} frames of the step batch, extract + SearchForInitialization "
-                                             f"on {ns - 1} pairs, oracle/liborb_oracle.so on {args.cpu_threads} threads"}
+            bad_m = 0
+            for i in range(ns - 1):
+                rnm, rm12 = nms[i]
+                if mh[i] != rnm or not np.array_equal(m12h[i][:len(rm12)], rm12):
+                    bad_m += 1
+            out["cpu_baseline"] = {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
+                                   "cores_available": avail, "flags": flags,
+                                   "library": os.path.relpath(lib_path, ROOT),
+                                   "single_thread_fps": fps1, "single_thread_frames": n1,
+                                   "sample": f"first {ns} frames of the step batch: extraction + SearchForInitialization "
+                                             f"on {ns - 1} consecutive pairs by the oracle on a pool of {threads} "
+                                             f"threads (value); single_thread_fps: the reference's model, one "
+                                             f"Tracking thread extracting and matching frame after frame"}
             out["parity"] = {"frames_checked": ns, "frames_mismatched": bad, "pairs_checked": ns - 1,
-                             "pairs_mismatched": bad_m}
+                             "pairs_mismatched": bad_m, "compared": "all 28 keypoint bytes, 32 descriptor bytes, "
+                                                                   "monoIndex count, nmatches and the full matches12"}
+        if world == 1 and args.host_api:
+            out["host_api"] = host_api_rates(frames_np)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

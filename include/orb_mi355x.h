@@ -97,8 +97,8 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int h_, size_t step,
  * kps[f*cap ...], desc[(f*cap ...) * 32], n_out[f], mono_out[f] (may be NULL).
  * Returns ORB_OK, ORB_ERR_EMPTY (an empty image), ORB_ERR_CAPACITY (some
  * n_out[f] > cap: that frame is not copied), ORB_ERR_PARAM or ORB_ERR_DEVICE.
- * The frames stay on the device for orbs_compute_stereo_matches_batch_device
- * like those of orbx_extract_batch_device. */
+ * Every frame's pyramid stays on the device (orbx_get_batch_level) until the
+ * next extraction call on this handle. */
 int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, const size_t* steps, int w, int h_,
                        const int32_t* lap, orb_keypoint* kps, uint8_t* desc, int cap, int32_t* n_out,
                        int32_t* mono_out);
@@ -107,6 +107,18 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
  * extracted by orbx_extract (host copy).  dst may be NULL to query w/h. */
 int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step,
                    int* w, int* h_);
+
+/* mvImagePyramid[level] of frame `frame` of the LAST batch call
+ * (orbx_extract_batch or orbx_extract_batch_device) on this handle: the
+ * per-image pyramid each of the reference's extractor objects exposes
+ * (include/ORBextractor.h:83), read by Frame::ComputeStereoMatches
+ * (src/Frame.cc:818-923) for the left and right image of a stereo frame
+ * extracted in one call.  Level 0 is read from the batch's input frames (for
+ * orbx_extract_batch_device: the caller's buffer, which must still be live).
+ * ORB_ERR_PARAM when no batch is current (any orbx_extract or plan rebuild
+ * ends it).  dst may be NULL to query w/h. */
+int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step,
+                         int* w, int* h_);
 
 /* Batched, HBM-resident path: nframes images of w x h, frame f at
  * d_frames + f*frame_stride, rows row_step apart.  Outputs per frame f:
@@ -124,6 +136,18 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
  *          receives the per-level count. */
 int orbx_debug_stage(orbx_handle* h, int stage, orb_keypoint* kps, int cap,
                      int32_t* counts);
+
+/* Exhaustive check of the device compile of the descriptor's scalar math
+ * (test infrastructure; tests/test_gpu_math.py compares the hashes with the
+ * oracle's orbo_debug_math, which uses the system libm like the reference):
+ * what 0 = glibc sincosf on every float bit pattern in [begin, end) (radians),
+ * what 1 = the angle conversion, sincosf and the 512 rBRIEF sampling offsets
+ * of every float degree angle in [begin, end) (ORBextractor.cc:107-146),
+ * what 2 = fastAtan2 on integer moment pairs (ORBextractor.cc:76-103).
+ * hashes[(i - begin) >> chunk_log2] receives sum e_i (2 i + 1) mod 2^64
+ * (csrc/orb_math.h: math_mix). */
+int orbx_debug_math(int device, int what, long long begin, long long end, int chunk_log2, int fused,
+                    unsigned long long* hashes);
 
 /* Per-stage HIP-event timing of subsequent orbx_extract* calls (on the stream
  * they run on).  orbx_get_profile sums, over the recorded calls, the stage

@@ -26,15 +26,45 @@ def build(force: bool = False) -> Path:
     return LIB
 
 
-_lib = None
+_libs = {}
 
 
-def lib():
-    global _lib
-    if _lib is None:
-        build()
-        L = C.CDLL(str(LIB))
+def cpu_isa() -> str:
+    """x86-64 ISA level of this host for the -O3 -march builds: "v4" (AVX-512
+    F/BW/CD/DQ/VL), "v3" (AVX2 + FMA + BMI2) or "" (neither)."""
+    try:
+        flags = next(l for l in open("/proc/cpuinfo") if l.startswith("flags")).split()
+    except (OSError, StopIteration):
+        return ""
+    if all(f in flags for f in ("avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl")):
+        return "v4"
+    if all(f in flags for f in ("avx2", "fma", "bmi2")):
+        return "v3"
+    return ""
+
+
+def fast_variant() -> tuple[Path, str]:
+    """The -O3 -march build for this host's ISA level (the reference's own
+    -O3 -march=native, CMakeLists.txt:16,31), or the -O2 checker."""
+    isa = cpu_isa()
+    p = HERE / f"liborb_oracle_{isa}.so"
+    if isa and p.exists():
+        return p, f"-O3 -march=x86-64-{isa} -ffp-contract=off"
+    return LIB, "-O2 -ffp-contract=off"
+
+
+def fast_lib():
+    return lib(fast_variant()[0])
+
+
+def lib(path: Path | None = None):
+    path = Path(path) if path else LIB
+    if path not in _libs:
+        if path == LIB:
+            build()
+        L = C.CDLL(str(path))
         vp, i32, f32 = C.c_void_p, C.c_int, C.c_float
+        L.orbo_debug_math.argtypes = [i32, C.c_longlong, C.c_longlong, i32, i32, i32, vp]
         L.orbo_create.restype = vp
         L.orbo_create.argtypes = [vp]
         L.orbo_destroy.argtypes = [vp]
@@ -70,24 +100,25 @@ def lib():
         L.orbo_search_by_projection_last_fisheye.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32,
                                                              i32, i32, vp, vp]
         L.orbo_compute_stereo_matches.argtypes = [vp, vp, vp, i32, vp, vp, i32, vp, vp, vp, f32, f32, vp, vp]
-        _lib = L
-    return _lib
+        _libs[path] = L
+    return _libs[path]
 
 
 class OracleExtractor:
     """ORBextractor restated on the CPU (checker)."""
 
     def __init__(self, nfeatures=1000, scale_factor=1.2, nlevels=8, ini_th_fast=20, min_th_fast=7,
-                 blur_variant=0, fma_sampling=1):
+                 blur_variant=0, fma_sampling=1, lib_path=None):
         self.p = abi.params(nfeatures, scale_factor, nlevels, ini_th_fast, min_th_fast, blur_variant, fma_sampling)
         self.nlevels = nlevels
-        self.h = lib().orbo_create(C.byref(self.p))
+        self.L = lib(lib_path)
+        self.h = self.L.orbo_create(C.byref(self.p))
         if not self.h:
             raise ValueError("bad ORBextractor parameters")
 
     def __del__(self):
         if getattr(self, "h", None):
-            lib().orbo_destroy(self.h)
+            self.L.orbo_destroy(self.h)
             self.h = None
 
     def tables(self):
@@ -103,7 +134,7 @@ class OracleExtractor:
         desc = np.zeros((cap, 32), np.uint8)
         n = C.c_int(0)
         mono = C.c_int(0)
-        rc = lib().orbo_extract(self.h, abi.ptr(img), w, h, w, int(lapping[0]), int(lapping[1]),
+        rc = self.L.orbo_extract(self.h, abi.ptr(img), w, h, w, int(lapping[0]), int(lapping[1]),
                                 abi.ptr(kps), abi.ptr(desc), cap, C.byref(n), C.byref(mono))
         if rc != 0:
             raise RuntimeError(f"oracle extract failed: {rc}")
@@ -163,10 +194,10 @@ def descriptor_distance(a: np.ndarray, b: np.ndarray) -> int:
 
 
 def search_for_initialization(f1: abi.Keep, f2: abi.Keep, prev: np.ndarray, window=100, nnratio=0.9,
-                              check_ori=True):
+                              check_ori=True, lib_path=None):
     prev = np.ascontiguousarray(prev, np.float32).copy()
     m12 = np.zeros(f1.struct.n, np.int32)
-    nm = lib().orbo_search_for_initialization(f1.ref(), f2.ref(), abi.ptr(prev), window, nnratio,
+    nm = lib(lib_path).orbo_search_for_initialization(f1.ref(), f2.ref(), abi.ptr(prev), window, nnratio,
                                               int(check_ori), abi.ptr(m12))
     return nm, m12, prev
 

@@ -29,6 +29,7 @@
 #include <cstdint>
 #include <cstring>
 #include <list>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -737,6 +738,119 @@ int orbo_blur(const uint8_t* src, int w, int hh, int variant, uint8_t* dst) {
     return 0;
 }
 float orbo_fast_atan2(float y, float x) { return fast_atan2_deg(y, x); }
+
+// Host side of the exhaustive device math check (include/orb_mi355x.h:
+// orbx_debug_math; tests/test_gpu_math.py): the same chunk hashes from the
+// system libm's sincosf (what the reference binary calls), this oracle's
+// fastAtan2 and its sampling formula (orb_descriptor above).  The hash and
+// the moment-pair enumeration are restated here, not shared with the product.
+static inline uint32_t dm_lowbias32(uint32_t v) {
+    v ^= v >> 16; v *= 0x7feb352du; v ^= v >> 15; v *= 0x846ca68bu; v ^= v >> 16;
+    return v;
+}
+static inline uint32_t dm_bits(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+static inline float dm_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+
+static uint32_t dm_element(int what, uint64_t i, int fused) {
+    if (what == 0) {
+        float s, c;
+        sincosf(dm_float((uint32_t)i), &s, &c);
+        return dm_bits(s) ^ (dm_bits(c) * 0x9E3779B9u);
+    }
+    if (what == 1) {
+        // the pattern as float columns and the word weights, once: the loop
+        // below then vectorises (the -O3 -march builds, liborb_oracle_v3.so)
+        static const struct Cols {
+            float x[512], y[512];
+            uint32_t w[512];
+            Cols() {
+                for (int k = 0; k < 512; ++k) {
+                    x[k] = (float)kPattern[2 * k];
+                    y[k] = (float)kPattern[2 * k + 1];
+                    w[k] = (uint32_t)k * 0x9E3779B1u | 1u;
+                }
+            }
+        } P;
+        const float ang = dm_float((uint32_t)i) * (float)(3.14159265358979323846 / 180.f);
+        float b, a;
+        sincosf(ang, &b, &a);
+        // cvRound of |v| < 2^22 as (v + 1.5*2^23) - 1.5*2^23: the same
+        // ties-to-even result, in a form the compiler vectorises
+        const float M = 12582912.f;
+        auto rnd = [M](float v) { return (int)((v + M) - M); };
+        uint32_t e = 0;
+        if (fused) {
+            for (int k = 0; k < 512; ++k) {
+                const int r = rnd(std::fmaf(P.x[k], b, P.y[k] * a));
+                const int q = rnd(std::fmaf(P.x[k], a, -(P.y[k] * b)));
+                e += ((uint32_t)(r & 0xff) | ((uint32_t)(q & 0xff) << 8)) * P.w[k];
+            }
+        } else {
+            for (int k = 0; k < 512; ++k) {
+                const int r = rnd(P.x[k] * b + P.y[k] * a);
+                const int q = rnd(P.x[k] * a - P.y[k] * b);
+                e += ((uint32_t)(r & 0xff) | ((uint32_t)(q & 0xff) << 8)) * P.w[k];
+            }
+        }
+        return e;
+    }
+    float y, x;
+    if (i < 4097ull * 4097ull) {
+        y = (float)((int)(i / 4097) - 2048);
+        x = (float)((int)(i % 4097) - 2048);
+    } else {
+        y = (float)((int)(dm_lowbias32((uint32_t)(2 * i)) % 3000001u) - 1500000);
+        x = (float)((int)(dm_lowbias32((uint32_t)(2 * i + 1)) % 3000001u) - 1500000);
+    }
+    return dm_bits(fast_atan2_deg(y, x));
+}
+
+// Degree angles below 2^-36 (float bits < kTinyDeg): the radian angle is
+// below 2^-41, where sincosf returns (angle, 1.0f) exactly, so every product
+// x*b, y*b is below 2^-36 in magnitude: fmaf(x, b, y*1) rounds to y and
+// fmaf(x, 1, -(y*b)) to x for the nonzero integers of the pattern, and to a
+// value of magnitude < 0.5 (cvRound 0) for a zero one; the unfused forms
+// likewise.  Every such angle has the offsets (r, c) = (y, x).  The host
+// takes that word instead of evaluating ~7.6e8 angles whose products are
+// subnormal (microcode assists: ~30x slower); orbo_debug_math checks it
+// against the full evaluation at both ends of the range before using it.
+static const uint32_t kTinyDeg = 0x2d800000u;   // 2^-36
+static uint32_t dm_tiny_word() {
+    uint32_t e = 0;
+    for (int k = 0; k < 512; ++k)
+        e += ((uint32_t)(kPattern[2 * k + 1] & 0xff) | ((uint32_t)(kPattern[2 * k] & 0xff) << 8)) *
+             ((uint32_t)k * 0x9E3779B1u | 1u);
+    return e;
+}
+
+int orbo_debug_math(int what, long long begin, long long end, int chunk_log2, int fused, int nthreads,
+                    unsigned long long* hashes) {
+    if (what < 0 || what > 2 || begin < 0 || end <= begin || chunk_log2 < 8 || chunk_log2 > 30 || !hashes ||
+        nthreads < 1)
+        return -1;
+    const uint32_t tiny = dm_tiny_word();
+    // fused bit 1: evaluate the tiny range too (tests/test_oracle_math.py)
+    if (what == 1 && (dm_element(1, 1, fused & 1) != tiny || dm_element(1, kTinyDeg - 1, fused & 1) != tiny ||
+                      dm_element(1, 0, fused & 1) != tiny))
+        return -2;
+    const long long nchunks = ((end - begin) + (1ll << chunk_log2) - 1) >> chunk_log2;
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; ++t)
+        th.emplace_back([=] {
+            for (long long ck = t; ck < nchunks; ck += nthreads) {
+                const long long c0 = begin + (ck << chunk_log2), c1 = std::min(end, c0 + (1ll << chunk_log2));
+                unsigned long long acc = 0;
+                for (long long i = c0; i < c1; ++i) {
+                    const uint32_t e = (what == 1 && !(fused & 2) && i < (long long)kTinyDeg)
+                                           ? tiny : dm_element(what, (uint64_t)i, fused & 1);
+                    acc += (unsigned long long)e * (2 * (uint64_t)i + 1);
+                }
+                hashes[ck] = acc;
+            }
+        });
+    for (auto& x : th) x.join();
+    return 0;
+}
 
 int orbo_descriptor_distance(const uint8_t* a, const uint8_t* b) { return hamming(a, b); }
 

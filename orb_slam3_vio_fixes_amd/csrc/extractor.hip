@@ -87,15 +87,13 @@ static void init_tables(orbx_handle* h) {
 
 static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 
-// Builds the size-dependent plan; returns ORB_OK or an error.
-static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
-    Plan& P = hd->plan;
-    if (P.w == w && P.h == h && P.maxB >= maxB && P.L == hd->prm.nlevels) return ORB_OK;
-    P.release();
-    ++hd->plan_epoch;                                        // captured graphs point at the old buffers
+// Builds the size-dependent plan into P; returns ORB_OK or an error.  The
+// caller (build_plan) releases P on any error, so a failed size never leaves a
+// plan that a later call with the same size would take for a built one.
+static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     if (w > 4096 + 16 || h > 4096 + 16) return ORB_ERR_UNSUPPORTED;   // 12-bit key coordinates
     const int L = hd->prm.nlevels;
-    P.w = w; P.h = h; P.L = L; P.maxB = maxB;
+    P.L = L;
     P.lv.assign(L, LevelDev{});
     std::vector<int2> tab;
     P.xmax.assign(L, 0);
@@ -107,6 +105,10 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
         // ComputePyramid sizes (ORBextractor.cc:1174-1175)
         d.w = cv_round((float)w * hd->inv_scale[l]);
         d.h = cv_round((float)h * hd->inv_scale[l]);
+        // The reference needs a level of at least 2*19+35 px per side (nCols,
+        // nRows >= 1), else it divides by zero at ORBextractor.cc:800-802;
+        // levels narrower than 46 px are refused here (the 35-px cell check
+        // below refuses the rest of that range).
         if (d.w < 2 * kEdge + 8 || d.h < 2 * kEdge + 8) return ORB_ERR_UNSUPPORTED;
         d.pitch = round_up(d.w, 64);
         d.off = l == 0 ? 0 : poff;
@@ -232,7 +234,23 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
         ORB_CHECK(hipMalloc(&P.d_slot_level, std::max<size_t>(1, sl.size())));
         ORB_CHECK(hipMemcpy(P.d_slot_level, sl.data(), sl.size(), hipMemcpyHostToDevice));
     }
+    // the size keys last: only a complete plan answers the cache check
+    P.w = w; P.h = h; P.maxB = maxB;
     return ORB_OK;
+}
+
+static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
+    Plan& P = hd->plan;
+    if (P.w == w && P.h == h && P.maxB >= maxB && P.L == hd->prm.nlevels) return ORB_OK;
+    P.release();
+    ++hd->plan_epoch;                                        // captured graphs point at the old buffers
+    // the pyramids of earlier calls lived in the released buffers
+    hd->have_last = false;
+    hd->last_frames = nullptr;
+    hd->last_B = 0;
+    const int rc = build_plan_into(hd, P, w, h, maxB);
+    if (rc != ORB_OK) P.release();
+    return rc;
 }
 
 // ---------------------------------------------------------------------------
@@ -1415,8 +1433,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             m10 = wave_sum(m10);
             m01 = wave_sum(m01);
             ang_deg = fast_atan2_deg((float)m01, (float)m10);
-            const float ang = ang_deg * (float)(3.14159265358979323846 / 180.f);
-            glibc_sincosf(ang, &sb, &ca);
+            glibc_sincosf(deg_to_rad(ang_deg), &sb, &ca);
             const u16x2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
             const u16x2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
             uint32_t* orow = (uint32_t*)(hb + rr * kHbP);
@@ -1462,13 +1479,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                 const float x = (float)(int)(int8_t)(patw[q] >> (16 * e));
                 const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
                 int r, c;
-                if (a.fma) {
-                    r = cv_round(__builtin_fmaf(x, sb, y * ca));
-                    c = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
-                } else {
-                    r = cv_round(x * sb + y * ca);
-                    c = cv_round(x * ca - y * sb);
-                }
+                brief_offset(x, y, sb, ca, a.fma, r, c);
                 const uint16_t* col = hb + (18 + r) * kHbP + 18 + c;
                 const uint32_t acc = k0 * ((uint32_t)col[0] + col[6 * kHbP]) + k1 * ((uint32_t)col[kHbP] + col[5 * kHbP]) +
                                      k2 * ((uint32_t)col[2 * kHbP] + col[4 * kHbP]) + k3 * (uint32_t)col[3 * kHbP];
@@ -1493,6 +1504,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         for (int k = 0; k < 8; ++k) atomicAdd(&g_desc_t[(blockIdx.x * 4 + wv) & 1023][k], tv[k]);
     }
 #endif
+}
+
+// ---------------------------------------------------------------------------
+// k_debug_math: the device compile of k_describe's scalar math over whole
+// input domains, as chunk hashes (orbx_debug_math; host side: the oracle with
+// the system libm, tests/test_gpu_math.py).  One workgroup per chunk.
+//   what 0: glibc_sincosf on every float bit pattern i (radians)
+//   what 1: deg_to_rad + glibc_sincosf + the 512 brief_offset()s of every
+//           float degree angle i
+//   what 2: fast_atan2_deg on the integer moment pairs atan_pair(i)
+// ---------------------------------------------------------------------------
+template <int WHAT>
+__global__ __launch_bounds__(256) void k_debug_math(long long begin, long long end, int chunk_log2, int fused,
+                                                    unsigned long long* hashes) {
+    __shared__ unsigned long long part[4];
+    const long long nchunks = ((end - begin) + (1ll << chunk_log2) - 1) >> chunk_log2;
+    for (long long ck = blockIdx.x; ck < nchunks; ck += gridDim.x) {
+        const long long c0 = begin + (ck << chunk_log2), c1 = min(end, c0 + (1ll << chunk_log2));
+        unsigned long long acc = 0;
+        for (long long i = c0 + threadIdx.x; i < c1; i += blockDim.x) {
+            uint32_t e;
+            if (WHAT == 0) {
+                float s, c;
+                glibc_sincosf(__builtin_bit_cast(float, (uint32_t)i), &s, &c);
+                e = f32_bits(s) ^ (f32_bits(c) * 0x9E3779B9u);
+            } else if (WHAT == 1) {
+                float sb, ca;
+                glibc_sincosf(deg_to_rad(__builtin_bit_cast(float, (uint32_t)i)), &sb, &ca);
+                e = 0;
+                for (int k = 0; k < 512; ++k) {
+                    int r, c;
+                    brief_offset((float)c_pattern[2 * k], (float)c_pattern[2 * k + 1], sb, ca, fused != 0, r, c);
+                    e = offsets_word(e, k, r, c);
+                }
+            } else {
+                float y, x;
+                atan_pair((uint64_t)i, y, x);
+                e = f32_bits(fast_atan2_deg(y, x));
+            }
+            acc += math_mix(e, (uint64_t)i);
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, kWave);
+        if (lane_id() == 0) part[wave_id()] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) hashes[ck] = part[0] + part[1] + part[2] + part[3];
+        __syncthreads();
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1703,17 +1762,19 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     return ORB_OK;
 }
 
-// Splits a batch into hd->nsub frame ranges on private non-blocking streams
-// that fork from and join back into the caller's stream.  The quadtree,
+// Frames [fb, fb+B) of a batch whose base pointers are given (frame fb also
+// uses scratch/pyramid slot fb, so separate runs of one batch never share
+// slots).  Splits the range into hd->nsub frame ranges on private non-blocking
+// streams that fork from and join back into the caller's stream.  The quadtree,
 // pyramid and assemble kernels are latency bound (one block per frame-level,
 // barrier heavy); running them beside the VALU-bound FAST/describe kernels
 // of the other range fills the CUs they leave idle.
-static int run_batched(orbx_handle* hd, int B, const uint8_t* d_frames, long long fstride, int pitch0, float lap0,
-                       float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n, int32_t* d_mono,
-                       hipStream_t st) {
+static int run_batched(orbx_handle* hd, int fb, int B, const uint8_t* d_frames, long long fstride, int pitch0,
+                       float lap0, float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n,
+                       int32_t* d_mono, hipStream_t st) {
     const int S = std::min(hd->nsub, std::max(1, B / kMinSubFrames));
     if (S <= 1)
-        return run_pipeline(hd, 0, B, d_frames, fstride, pitch0, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, st);
+        return run_pipeline(hd, fb, B, d_frames, fstride, pitch0, lap0, lap1, d_kps, d_desc, cap, d_n, d_mono, st);
     while ((int)hd->sub_streams.size() < S) {
         hipStream_t s;
         hipEvent_t e;
@@ -1724,7 +1785,7 @@ static int run_batched(orbx_handle* hd, int B, const uint8_t* d_frames, long lon
     }
     if (!hd->fork_ev) ORB_CHECK(hipEventCreateWithFlags(&hd->fork_ev, hipEventDisableTiming));
     ORB_CHECK(hipEventRecord(hd->fork_ev, st));
-    int f0 = 0;
+    int f0 = fb;
     for (int i = 0; i < S; ++i) {
         const int nb = B / S + (i < B % S ? 1 : 0);
         ORB_CHECK(hipStreamWaitEvent(hd->sub_streams[i], hd->fork_ev, 0));
@@ -1815,7 +1876,8 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     h->last_fstride = (long long)frame_stride;
     h->last_pitch0 = (int)row_step;
     h->last_B = nframes;
-    return run_batched(h, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
+    h->have_last = false;          // pyramid slot 0 now holds this batch's frame 0
+    return run_batched(h, 0, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
                        d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
 }
 
@@ -1858,12 +1920,22 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
         }
     };
     const int nth = std::min(8, nframes / 16);              // >= 16 frames per thread
-    if (nth <= 1) {
-        gather(0, nframes);
-    } else {
+    {
+        // frames [done, nframes) are left for this thread: every worker that
+        // could not be started (std::system_error must not cross the C ABI)
         std::vector<std::thread> th;
-        for (int t = 0; t < nth; ++t)
-            th.emplace_back(gather, (int)((long long)nframes * t / nth), (int)((long long)nframes * (t + 1) / nth));
+        int done = 0;
+        if (nth > 1) {
+            try {
+                for (int t = 0; t < nth - 1; ++t) {
+                    const int a0 = (int)((long long)nframes * t / nth), a1 = (int)((long long)nframes * (t + 1) / nth);
+                    th.emplace_back(gather, a0, a1);
+                    done = a1;
+                }
+            } catch (...) {
+            }
+        }
+        gather(done, nframes);
         for (auto& x : th) x.join();
     }
     ORB_CHECK(hipMemcpyAsync(dev, pin, in_b, hipMemcpyHostToDevice, 0));
@@ -1875,13 +1947,13 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
         const int l0 = lap ? lap[2 * f0] : 0, l1 = lap ? lap[2 * f0 + 1] : 1000;
         int f1 = f0 + 1;
         while (f1 < nframes && (!lap || (lap[2 * f1] == l0 && lap[2 * f1 + 1] == l1))) ++f1;
-        rc = run_batched(h, f1 - f0, dev + f0 * fbytes, (long long)fbytes, (int)pitch, (float)l0, (float)l1,
-                         d_kps + (size_t)f0 * ot, d_desc + (size_t)f0 * ot * 32, ot, d_nm + f0, d_nm + nframes + f0,
-                         0);
+        rc = run_batched(h, f0, f1 - f0, dev, (long long)fbytes, (int)pitch, (float)l0, (float)l1, d_kps, d_desc,
+                         ot, d_nm, d_nm + nframes, 0);
         if (rc) return rc;
         f0 = f1;
     }
     h->last_frames = dev;
+    h->have_last = false;          // pyramid slot 0 now holds this batch's frame 0
     h->last_fstride = (long long)fbytes;
     h->last_pitch0 = (int)pitch;
     h->last_B = nframes;
@@ -1953,6 +2025,8 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size
     if (mono_out) *mono_out = mono;
     h->have_last = true;
     h->last_w = w; h->last_h = hh;
+    h->last_frames = nullptr;      // pyramid slot 0 now holds this image
+    h->last_B = 0;
     if (n > cap) return ORB_ERR_CAPACITY;
     if (n > 0) {
         std::memcpy(kps, pin + o_kp, (size_t)n * sizeof(orb_keypoint));
@@ -1986,6 +2060,8 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
     if (mono_out) *mono_out = mono;
     h->have_last = true;
     h->last_w = w; h->last_h = hh;
+    h->last_frames = nullptr;      // pyramid slot 0 now holds this image
+    h->last_B = 0;
     if (n > cap) return ORB_ERR_CAPACITY;
     if (n > 0) {
         ORB_CHECK(hipMemcpy(kps, P.d_kps, n * sizeof(orb_keypoint), hipMemcpyDeviceToHost));
@@ -2037,6 +2113,44 @@ int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step, int
     (void)hipSetDevice(h->device);
     const uint8_t* src = level == 0 ? P.d_in : P.d_pyr + d.off;
     const size_t sp = level == 0 ? P.in_pitch : (size_t)d.pitch;
+    ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_debug_math(int device, int what, long long begin, long long end, int chunk_log2, int fused,
+                    unsigned long long* hashes) {
+    if (what < 0 || what > 2 || begin < 0 || end <= begin || chunk_log2 < 8 || chunk_log2 > 30 || !hashes)
+        return ORB_ERR_PARAM;
+    if (what != 2 && end > (1ll << 32)) return ORB_ERR_PARAM;
+    if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    if (what == 1) {   // the pattern table lives in constant memory (orbx_create loads it per device)
+        ORB_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), h_pattern, sizeof(h_pattern)));
+    }
+    const long long nchunks = ((end - begin) + (1ll << chunk_log2) - 1) >> chunk_log2;
+    unsigned long long* d = nullptr;
+    ORB_CHECK(hipMalloc(&d, nchunks * sizeof(unsigned long long)));
+    const dim3 grid((unsigned)std::min<long long>(nchunks, 8192));
+    if (what == 0) hipLaunchKernelGGL(k_debug_math<0>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    else if (what == 1) hipLaunchKernelGGL(k_debug_math<1>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    else hipLaunchKernelGGL(k_debug_math<2>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemcpy(hashes, d, nchunks * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    return e == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+}
+
+int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int* w, int* hh) {
+    if (!h || !h->last_frames || frame < 0 || frame >= h->last_B || level < 0 || level >= h->plan.L)
+        return ORB_ERR_PARAM;
+    const Plan& P = h->plan;
+    const LevelDev& d = P.lv[level];
+    if (w) *w = d.w;
+    if (hh) *hh = d.h;
+    if (!dst) return ORB_OK;
+    (void)hipSetDevice(h->device);
+    const uint8_t* src = level == 0 ? h->last_frames + (long long)frame * h->last_fstride
+                                    : P.d_pyr + (long long)frame * P.pyr_bytes + d.off;
+    const size_t sp = level == 0 ? (size_t)h->last_pitch0 : (size_t)d.pitch;
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
     return ORB_OK;
 }

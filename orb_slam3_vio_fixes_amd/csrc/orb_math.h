@@ -89,6 +89,51 @@ ORB_HD float fast_atan2_deg(float y, float x) {
     return a;
 }
 
+// Sampling offsets of one rBRIEF point (computeOrbDescriptor's GET_VALUE,
+// ORBextractor.cc:115-118): row = x sin + y cos, column = x cos - y sin, in
+// the fused form GCC emits for the reference's -O3 -march=native build on an
+// FMA host (A.6), or unfused.  Used by k_describe and by the exhaustive device
+// check (orbx_debug_math, tests/test_gpu_math.py).
+ORB_HD void brief_offset(float x, float y, float sb, float ca, bool fused, int& r, int& c) {
+    if (fused) {
+        r = cv_round(__builtin_fmaf(x, sb, y * ca));
+        c = cv_round(__builtin_fmaf(x, ca, -(y * sb)));
+    } else {
+        r = cv_round(x * sb + y * ca);
+        c = cv_round(x * ca - y * sb);
+    }
+}
+
+// The angle conversion of computeOrbDescriptor (ORBextractor.cc:110).
+ORB_HD float deg_to_rad(float deg) { return deg * (float)(3.14159265358979323846 / 180.f); }
+
+// Hashes of the exhaustive math check (orbx_debug_math on the device, the
+// oracle's orbo_debug_math with the system libm on the host).  Element i of
+// [begin, end) goes to chunk (i - begin) >> chunk_log2; a chunk's hash is
+// sum_i e_i * (2 i + 1) mod 2^64 over its elements.
+ORB_HD uint64_t math_mix(uint32_t e, uint64_t i) { return (uint64_t)e * (2 * i + 1); }
+ORB_HD uint32_t lowbias32(uint32_t v) {
+    v ^= v >> 16; v *= 0x7feb352du; v ^= v >> 15; v *= 0x846ca68bu; v ^= v >> 16;
+    return v;
+}
+// what 2 (fastAtan2): index -> (y, x) integer moments: every pair of
+// [-2048, 2048]^2 first, then pseudo-random pairs over +-1.5e6 (|m10|, |m01|
+// of a radius-15 disc of bytes stay below 1.2e6)
+constexpr uint64_t kAtanGrid = 4097ull * 4097ull;
+ORB_HD void atan_pair(uint64_t i, float& y, float& x) {
+    if (i < kAtanGrid) {
+        y = (float)((int)(i / 4097) - 2048);
+        x = (float)((int)(i % 4097) - 2048);
+    } else {
+        y = (float)((int)(lowbias32((uint32_t)(2 * i)) % 3000001u) - 1500000);
+        x = (float)((int)(lowbias32((uint32_t)(2 * i + 1)) % 3000001u) - 1500000);
+    }
+}
+// what 1: one degree angle's 512 sampling offsets folded into one word
+ORB_HD uint32_t offsets_word(uint32_t acc, int k, int r, int c) {
+    return acc + ((uint32_t)(r & 0xff) | ((uint32_t)(c & 0xff) << 8)) * ((uint32_t)k * 0x9E3779B1u | 1u);
+}
+
 // ---------------------------------------------------------------------------
 // libstdc++ std::sort (introsort, _S_threshold = 16, median-of-3 to first,
 // unguarded partition, heap-sort fallback at depth 2*lg(n), final insertion

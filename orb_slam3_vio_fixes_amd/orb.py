@@ -73,7 +73,9 @@ class ORBextractor:
     def extract_batch(self, images, laps=None):
         """operator() on several images of one size in one call (orbx_extract_batch):
         a list of (keypoints, descriptors, monoIndex)."""
-        imgs = [np.ascontiguousarray(im, np.uint8) for im in images]
+        # row-strided 8UC1 views are passed as they are (cv::Mat::step)
+        imgs = [im if (isinstance(im, np.ndarray) and im.dtype == np.uint8 and im.ndim == 2 and im.strides[1] == 1
+                       and im.strides[0] >= im.shape[1]) else np.ascontiguousarray(im, np.uint8) for im in images]
         if not imgs:
             return []
         h, w = imgs[0].shape
@@ -81,13 +83,14 @@ class ORBextractor:
             raise ValueError("extract_batch expects 8UC1 images of one size")
         nf = len(imgs)
         ptrs = (C.c_void_p * nf)(*[im.ctypes.data for im in imgs])
+        steps = np.array([im.strides[0] for im in imgs], np.uintp)
         lap = None if laps is None else np.ascontiguousarray(np.asarray(laps, np.int32).reshape(nf, 2))
         cap = self.max_keypoints(w, h)
         kps = np.zeros((nf, cap), abi.KEYPOINT_DTYPE)
         desc = np.zeros((nf, cap, 32), np.uint8)
         n = np.zeros(nf, np.int32)
         mono = np.zeros(nf, np.int32)
-        rc = capi.lib().orbx_extract_batch(self._h, nf, ptrs, None, w, h, abi.ptr(lap), abi.ptr(kps), abi.ptr(desc),
+        rc = capi.lib().orbx_extract_batch(self._h, nf, ptrs, abi.ptr(steps), w, h, abi.ptr(lap), abi.ptr(kps), abi.ptr(desc),
                                            cap, abi.ptr(n), abi.ptr(mono))
         capi.check(rc, "orbx_extract_batch")
         return [(kps[f, :n[f]].copy(), desc[f, :n[f]].copy(), int(mono[f])) for f in range(nf)]
@@ -101,6 +104,19 @@ class ORBextractor:
             a = np.zeros((h.value, w.value), np.uint8)
             capi.check(capi.lib().orbx_get_level(self._h, l, abi.ptr(a), w.value, C.byref(w), C.byref(h)),
                        "orbx_get_level")
+            out.append(a)
+        return out
+
+    def batch_pyramid(self, frame: int):
+        """mvImagePyramid of frame `frame` of the last batch call (orbx_get_batch_level)."""
+        out = []
+        for l in range(self.nlevels):
+            w, h = C.c_int(0), C.c_int(0)
+            capi.check(capi.lib().orbx_get_batch_level(self._h, frame, l, None, 0, C.byref(w), C.byref(h)),
+                       "orbx_get_batch_level")
+            a = np.zeros((h.value, w.value), np.uint8)
+            capi.check(capi.lib().orbx_get_batch_level(self._h, frame, l, abi.ptr(a), w.value, C.byref(w),
+                                                       C.byref(h)), "orbx_get_batch_level")
             out.append(a)
         return out
 
