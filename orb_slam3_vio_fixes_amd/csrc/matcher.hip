@@ -463,7 +463,12 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
     }
 }
 
-// one wave per pair: the serial pass
+// one wave per pair: the serial pass.  STAGED: the queries' top-K lists are
+// copied into LDS first (32 B per F1 keypoint); otherwise (frames of more
+// than ~2,900 keypoints, e.g. the 5 x nFeatures initialization extractor of
+// Tracking.cc:601) each query reads its list from global memory, one query
+// ahead of its use (the lists do not depend on the serial state).
+template <bool STAGED>
 __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id();
@@ -479,8 +484,8 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
     int* hist = m21 + a.cap;                  // 32
     int* qlist = hist + 32;                   // cap: query indices i1 (level 0, >= 1 candidate)
     int* qcnt = qlist + a.cap;                // cap: candidate counts
-    uint32_t* qtop = (uint32_t*)(qcnt + a.cap);   // cap * kTopK
-    int8_t* bin1 = (int8_t*)(qtop + (size_t)a.cap * kTopK);   // cap
+    uint32_t* qtop = (uint32_t*)(qcnt + a.cap);   // STAGED: cap * kTopK
+    int8_t* bin1 = (int8_t*)(qtop + (STAGED ? (size_t)a.cap * kTopK : 0));   // cap
     int32_t* m12 = a.matches + (long long)pr * a.cap;
     const int nl = level0_list(a, f2, list, lane, kWave);
     for (int i = lane; i < n2; i += kWave) { mdist[i] = INT_MAX; m21[i] = -1; }
@@ -498,14 +503,23 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
         nq += __popcll(m);
     }
     __syncthreads();
-    for (int e = lane; e < nq * kTopK; e += kWave) qtop[e] = topk[(long long)qlist[e / kTopK] * kTopK + e % kTopK];
+    if (STAGED)
+        for (int e = lane; e < nq * kTopK; e += kWave) qtop[e] = topk[(long long)qlist[e / kTopK] * kTopK + e % kTopK];
     __syncthreads();
     int nm = 0;
     const float r = a.window;
+    uint32_t next_key = kNoKey;
+    if (!STAGED && nq > 0 && lane < kTopK) next_key = topk[(long long)qlist[0] * kTopK + lane];
     for (int j = 0; j < nq; ++j) {
         const int i1 = qlist[j];
         const int cur_cnt = qcnt[j];
-        const uint32_t cur_key = lane < kTopK ? qtop[j * kTopK + lane] : kNoKey;
+        uint32_t cur_key;
+        if (STAGED) {
+            cur_key = lane < kTopK ? qtop[j * kTopK + lane] : kNoKey;
+        } else {
+            cur_key = next_key;
+            if (j + 1 < nq && lane < kTopK) next_key = topk[(long long)qlist[j + 1] * kTopK + lane];
+        }
         int best = INT_MAX, best2 = INT_MAX, bi = -1;
         bool ok = false;
         {
@@ -591,11 +605,19 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
     if (lane == 0) a.nmatches[pr] = nm;
 }
 
-static void launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
+constexpr size_t kLdsMax = 160 * 1024;
+
+// Frames up to ~7,800 keypoints (LDS of the candidate pools); beyond that
+// ORB_ERR_UNSUPPORTED before any launch.
+static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
+    const size_t lds_staged = (size_t)a.cap * (20 + 4 * kTopK + 1) + 128 + 16;
+    const size_t lds_direct = (size_t)a.cap * (20 + 1) + 128 + 16;
+    if (lds_topk > kLdsMax || lds_direct > kLdsMax) return ORB_ERR_UNSUPPORTED;
     KLAUNCH(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
-    const size_t lds_res = (size_t)a.cap * (20 + 4 * kTopK + 1) + 128 + 16;
-    KLAUNCH(k_sfi_resolve, dim3(npairs), dim3(64), lds_res, st, a);
+    if (lds_staged <= kLdsMax) KLAUNCH(k_sfi_resolve<true>, dim3(npairs), dim3(64), lds_staged, st, a);
+    else KLAUNCH(k_sfi_resolve<false>, dim3(npairs), dim3(64), lds_direct, st, a);
+    return ORB_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -2297,7 +2319,7 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = prev_in.p; a.prev_out = prev_out.p;
     a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
     a.matches = m.p; a.nmatches = nm.p; a.topk = topk.p; a.ncand = ncand.p;
-    launch_sfi(a, 1, 0);
+    if ((rc = launch_sfi(a, 1, 0))) return rc;
     ORB_CHECK(hipGetLastError());
     int32_t res = 0;
     ORB_CHECK(d2h(&res, nm.p, 4));
@@ -2345,7 +2367,7 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     a.pair_f1 = pf.p; a.pair_f2 = pf.p + 1; a.prev_in = nullptr; a.prev_out = nullptr;
     a.g = g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
     a.matches = d_matches; a.nmatches = d_nmatches; a.topk = topk.p; a.ncand = ncand.p;
-    launch_sfi(a, nframes - 1, st);
+    if ((rc = launch_sfi(a, nframes - 1, st))) return rc;
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }
