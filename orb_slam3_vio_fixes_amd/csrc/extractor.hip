@@ -20,7 +20,10 @@
 #include "orb_math.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <type_traits>
@@ -86,6 +89,118 @@ static void init_tables(orbx_handle* h) {
 }
 
 static int round_up(int x, int m) { return (x + m - 1) / m * m; }
+
+// ---------------------------------------------------------------------------
+// k_pyramid plan: column/row tap tables in the form the kernel reads, and the
+// launch groups with their band tables.
+// ---------------------------------------------------------------------------
+constexpr int kPyrLdsBudget = 64 * 1024;   // per workgroup: 2 workgroups of 256 threads per CU
+
+static int pyr_lds_pitch(int w) { return round_up(w + 4, 16); }
+
+// Bands of one group (la, lb) with R rows of level lb per band; returns the
+// LDS bytes (A + B) and fills `band` ([nb][lb-la+1] int4 {n0, n1, p0, p1}).
+static int pyr_bands(const Plan& P, const std::vector<int2>& yt, int la, int lb, int R, std::vector<int4>& band,
+                     int& lds_a, int& lds_b) {
+    const int nl = lb - la + 1, hb = P.lv[lb].h;
+    const int nb = (hb + R - 1) / R;
+    band.assign((size_t)nb * nl, make_int4(0, 0, 0, 0));
+    auto B = [&](int b, int l) -> int4& { return band[(size_t)b * nl + (l - la)]; };
+    for (int b = 0; b < nb; ++b) B(b, lb) = make_int4(b * R, std::min(hb, (b + 1) * R), 0, 0);
+    for (int l = lb; l > la; --l) {
+        const int h = P.lv[l].h;
+        // every row of a written level is computed by some band: close the
+        // gaps between the bands' ranges and reach both edges
+        B(0, l).x = 0;
+        B(nb - 1, l).y = h;
+        for (int b = 0; b + 1 < nb; ++b) B(b, l).y = std::max(B(b, l).y, B(b + 1, l).x);
+        // rows of level l-1 those rows read (clamped row taps)
+        for (int b = 0; b < nb; ++b) {
+            const int2 t0 = yt[P.lv[l].ytab + B(b, l).x], t1 = yt[P.lv[l].ytab + B(b, l).y - 1];
+            B(b, l - 1).x = t0.x & 0xffff;
+            B(b, l - 1).y = (t1.x >> 16) + 1;
+        }
+        // owned rows: what the previous band did not compute
+        for (int b = 0; b < nb; ++b) {
+            B(b, l).z = b == 0 ? 0 : std::max(B(b, l).x, B(b - 1, l).y);
+            B(b, l).w = B(b, l).y;
+        }
+    }
+    lds_a = lds_b = 0;
+    for (int l = la; l < lb; ++l) {
+        int rows = 0;
+        for (int b = 0; b < nb; ++b) rows = std::max(rows, B(b, l).y - B(b, l).x);
+        int& dst = ((l - la) & 1) ? lds_b : lds_a;
+        dst = std::max(dst, rows * pyr_lds_pitch(P.lv[l].w));
+    }
+    return lds_a + lds_b;
+}
+
+// Tap tables and launch groups of k_pyramid.  Groups: greedily the longest
+// run of levels (at most 4) whose bands of >= 8 top-level rows fit the LDS
+// budget; ORB_PYR_GROUPS="la-lb:R,..." overrides (A/B experiments).
+static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int4>& bands, std::vector<int>& xs,
+                          std::vector<uint32_t>& xw, std::vector<int2>& yt) {
+    const int L = P.L;
+    for (int l = 1; l < L; ++l) {
+        LevelDev& d = P.lv[l];
+        const LevelDev& s = P.lv[l - 1];
+        d.xtab = (int)xs.size();
+        for (int dx = 0; dx < round_up(d.w, 4); ++dx) {
+            const int2 e = tab[P.tab_off[l] + std::min(dx, d.w - 1)];
+            xs.push_back(e.x);
+            xw.push_back((uint32_t)e.y);
+        }
+        d.ytab = (int)yt.size();
+        for (int dy = 0; dy < d.h; ++dy) {
+            const int2 e = tab[P.tab_off[l] + d.w + dy];
+            const int r0 = std::min(std::max(e.x, 0), s.h - 1), r1 = std::min(std::max(e.x + 1, 0), s.h - 1);
+            yt.push_back(make_int2(r0 | (r1 << 16), e.y));
+        }
+    }
+    P.pgroups.clear();
+    std::vector<std::array<int, 3>> req;
+    if (const char* env = std::getenv("ORB_PYR_GROUPS")) {
+        int la, lb, R, n = 0;
+        const char* q = env;
+        while (std::sscanf(q, "%d-%d:%d%n", &la, &lb, &R, &n) == 3) {
+            req.push_back({la, lb, R});
+            q += n;
+            if (*q == ',') ++q;
+        }
+    }
+    std::vector<int4> bt;
+    int la = 0;
+    size_t ri = 0;
+    while (la < L - 1) {
+        PyrGroup g{};
+        bool ok = false;
+        if (ri < req.size() && req[ri][0] == la && req[ri][1] > la && req[ri][1] < L && req[ri][2] > 0) {
+            g.la = la; g.lb = req[ri][1]; g.R = req[ri][2];
+            pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b);
+            ok = g.lds_a + g.lds_b <= 160 * 1024;
+            ++ri;
+        }
+        for (int span = 4; span >= 1 && !ok; --span) {
+            const int lb = std::min(L - 1, la + span);
+            for (int R : {32, 24, 16, 12, 8, 6, 4, 2, 1}) {
+                if (R < 8 && span > 1) break;
+                int a, b;
+                if (pyr_bands(P, yt, la, lb, R, bt, a, b) <= kPyrLdsBudget || (span == 1 && R == 1)) {
+                    g.la = la; g.lb = lb; g.R = R; g.lds_a = a; g.lds_b = b;
+                    ok = true;
+                    break;
+                }
+            }
+        }
+        pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b);
+        g.nb = (int)(bt.size() / (size_t)(g.lb - g.la + 1));
+        g.band_off = (long long)bands.size();
+        bands.insert(bands.end(), bt.begin(), bt.end());
+        P.pgroups.push_back(g);
+        la = g.lb;
+    }
+}
 
 // Builds the size-dependent plan into P; returns ORB_OK or an error.  The
 // caller (build_plan) releases P on any error, so a failed size never leaves a
@@ -198,6 +313,13 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         outsum += d.out_cap;
         P.max_out_cap = std::max(P.max_out_cap, d.out_cap);
     }
+    std::vector<int4> pband;
+    std::vector<int> pxs;
+    std::vector<uint32_t> pxw;
+    std::vector<int2> pyt;
+    build_pyramid(P, tab, pband, pxs, pxw, pyt);
+    for (const PyrGroup& g : P.pgroups)
+        if (g.lds_a + g.lds_b > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
     P.pyr_bytes = poff;
     P.ncells = cellsum;
     P.slot_total = slotsum;
@@ -225,6 +347,17 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     ORB_CHECK(hipMalloc(&P.d_n, sizeof(int32_t)));
     ORB_CHECK(hipMalloc(&P.d_mono, sizeof(int32_t)));
     if (!tab.empty()) ORB_CHECK(hipMemcpy(P.d_tab, tab.data(), tab.size() * sizeof(int2), hipMemcpyHostToDevice));
+    ORB_CHECK(hipMalloc(&P.d_pband, std::max<size_t>(1, pband.size()) * sizeof(int4)));
+    ORB_CHECK(hipMalloc(&P.d_pxs, std::max<size_t>(1, pxs.size()) * sizeof(int)));
+    ORB_CHECK(hipMalloc(&P.d_pxw, std::max<size_t>(1, pxw.size()) * sizeof(uint32_t)));
+    ORB_CHECK(hipMalloc(&P.d_pyt, std::max<size_t>(1, pyt.size()) * sizeof(int2)));
+    if (!pband.empty())
+        ORB_CHECK(hipMemcpy(P.d_pband, pband.data(), pband.size() * sizeof(int4), hipMemcpyHostToDevice));
+    if (!pxs.empty()) {
+        ORB_CHECK(hipMemcpy(P.d_pxs, pxs.data(), pxs.size() * sizeof(int), hipMemcpyHostToDevice));
+        ORB_CHECK(hipMemcpy(P.d_pxw, pxw.data(), pxw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        ORB_CHECK(hipMemcpy(P.d_pyt, pyt.data(), pyt.size() * sizeof(int2), hipMemcpyHostToDevice));
+    }
     ORB_CHECK(hipMemcpy(P.d_lv, P.lv.data(), L * sizeof(LevelDev), hipMemcpyHostToDevice));
     ORB_CHECK(hipMemcpy(P.d_cells, P.cells.data(), P.cells.size() * sizeof(CellDev), hipMemcpyHostToDevice));
     {
@@ -252,6 +385,11 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     if (rc != ORB_OK) P.release();
     return rc;
 }
+
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
+__device__ __forceinline__ int round_up_d(int x, int m) { return (x + m - 1) / m * m; }
 
 // ---------------------------------------------------------------------------
 // k_resize: cv::resize INTER_LINEAR 8UC1.  One output row per
@@ -290,6 +428,136 @@ __global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src,
             h1 = S1[sx] * 2048;
         }
         D[dx] = (uint8_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_pyramid: ComputePyramid (ORBextractor.cc:1170-1195) for levels la+1..lb
+// of every frame in one launch, cv::resize INTER_LINEAR 8UC1.
+//
+// A workgroup owns a band of rows of every level of the group.  It stages the
+// rows of level la its band needs in LDS with 16-byte coalesced loads, then
+// builds each next level from the previous one in LDS (two ping-pong
+// buffers), writing the rows it owns to HBM and keeping the rows the next
+// level reads (its own plus a few halo rows the neighbouring band also
+// computes) in LDS.  Each HBM row of a level is written once; level la is read
+// once plus the halo.  One thread makes 4 consecutive outputs of a row: the
+// frame-invariant column taps come from the plan tables (one 16-byte load
+// each for the 4 source columns and the 4 weight pairs), the horizontal pass
+// is one v_dot2_u32_u16 per row tap (pixel pair x weight pair), the vertical
+// one OpenCV's (b * (h >> 4)) >> 16 as a v_mul_hi_u32 by b << 16.
+//
+// Workgroup -> (frame, band) is XCD-aware: the bands of one frame run on one
+// XCD (workgroups are dealt round-robin over the 8 XCDs), so the halo rows
+// two bands share are L2 hits.
+// ---------------------------------------------------------------------------
+struct PyrArgs {
+    const uint8_t* src;         // level la of frame 0
+    long long src_fstride;
+    int src_pitch, load_mode;   // 16 / 4 / 1: widest aligned load of a row of level la
+    uint8_t* pyr;               // levels >= 1 of frame 0
+    long long pyr_fstride;
+    const LevelDev* lv;
+    const int4* band;           // [nb][lb-la+1] {n0, n1, p0, p1}
+    const int* xs;
+    const uint32_t* xw;
+    const int2* yt;
+    int la, lb, nb, nframes, lds_b;
+};
+
+__global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t pyr_lds[];
+    const int wg = blockIdx.x;
+    const int f = (wg / 8 / a.nb) * 8 + (wg & 7), b = (wg / 8) % a.nb;
+    if (f >= a.nframes) return;
+    const int tid = threadIdx.x, nl = a.lb - a.la + 1;
+    typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
+    const ConstLevels lv = (ConstLevels)a.lv;
+    const int4* bd = a.band + (long long)b * nl;
+    // 1. rows [n0, n1) of level la -> buffer A
+    {
+        const int4 nb0 = bd[0];
+        const int w = lv[a.la].w, P = round_up_d(w + 4, 16);
+        const uint8_t* src = a.src + f * a.src_fstride + (long long)nb0.x * a.src_pitch;
+        const int rows = nb0.y - nb0.x;
+        if (a.load_mode == 16) {
+            const int nq = (w + 15) >> 4, n = rows * nq;
+            const float inv = 1.0f / (float)nq;
+            int i = tid;
+            for (; i + 3 * 256 < n; i += 4 * 256) {   // four 16-byte loads in flight per thread
+                uint4 v[4];
+                int r[4], q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int ii = i + k * 256;
+                    r[k] = (int)(((float)ii + 0.5f) * inv);
+                    q[k] = ii - r[k] * nq;
+                    v[k] = *(const uint4*)(src + (long long)r[k] * a.src_pitch + 16 * q[k]);
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) *(uint4*)(pyr_lds + r[k] * P + 16 * q[k]) = v[k];
+            }
+            for (; i < n; i += 256) {
+                const int r = (int)(((float)i + 0.5f) * inv), q = i - r * nq;
+                *(uint4*)(pyr_lds + r * P + 16 * q) = *(const uint4*)(src + (long long)r * a.src_pitch + 16 * q);
+            }
+        } else if (a.load_mode == 4) {
+            const int nq = (w + 3) >> 2, n = rows * nq;
+            const float inv = 1.0f / (float)nq;
+            for (int i = tid; i < n; i += 256) {
+                const int r = (int)(((float)i + 0.5f) * inv), q = i - r * nq;
+                *(uint32_t*)(pyr_lds + r * P + 4 * q) = *(const uint32_t*)(src + (long long)r * a.src_pitch + 4 * q);
+            }
+        } else {
+            const int n = rows * w;
+            const float inv = 1.0f / (float)w;
+            for (int i = tid; i < n; i += 256) {
+                const int r = (int)(((float)i + 0.5f) * inv), q = i - r * w;
+                pyr_lds[r * P + q] = src[(long long)r * a.src_pitch + q];
+            }
+        }
+    }
+    __syncthreads();
+    // 2. each next level from the previous one
+    for (int l = a.la + 1; l <= a.lb; ++l) {
+        const int k = l - a.la;
+        const int4 sb = bd[k - 1], db = bd[k];
+        const uint8_t* S = pyr_lds + ((k - 1) & 1 ? a.lds_b : 0);
+        uint8_t* Dl = pyr_lds + (k & 1 ? a.lds_b : 0);
+        const int sP = round_up_d(lv[l - 1].w + 4, 16);
+        const int w = lv[l].w, dP = round_up_d(w + 4, 16), pitch = lv[l].pitch;
+        const bool keep = l < a.lb;
+        uint8_t* G = a.pyr + f * a.pyr_fstride + lv[l].off;
+        const int* xs = a.xs + lv[l].xtab;
+        const uint32_t* xw = a.xw + lv[l].xtab;
+        const int2* yt = a.yt + lv[l].ytab;
+        const int ng = (w + 3) >> 2, n = (db.y - db.x) * ng;
+        const float inv = 1.0f / (float)ng;
+        for (int i = tid; i < n; i += 256) {
+            const int r = (int)(((float)i + 0.5f) * inv), g = i - r * ng;
+            const int row = db.x + r;
+            const int2 ty = yt[row];
+            const uint32_t B0 = (ty.y & 0xffff) << 16, B1 = ((uint32_t)ty.y >> 16) << 16;
+            const uint8_t* S0 = S + ((ty.x & 0xffff) - sb.x) * sP;
+            const uint8_t* S1 = S + ((ty.x >> 16) - sb.x) * sP;
+            const int4 sx = *(const int4*)(xs + 4 * g);
+            const uint4 wt = *(const uint4*)(xw + 4 * g);
+            const int sxa[4] = {sx.x, sx.y, sx.z, sx.w};
+            const uint32_t wta[4] = {wt.x, wt.y, wt.z, wt.w};
+            uint32_t out = 0;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                const uint32_t p0 = (uint32_t)S0[sxa[c]] | ((uint32_t)S0[sxa[c] + 1] << 16);
+                const uint32_t p1 = (uint32_t)S1[sxa[c]] | ((uint32_t)S1[sxa[c] + 1] << 16);
+                const uint32_t h0 = __builtin_amdgcn_udot2(as_u16x2(p0), as_u16x2(wta[c]), 0u, false);
+                const uint32_t h1 = __builtin_amdgcn_udot2(as_u16x2(p1), as_u16x2(wta[c]), 0u, false);
+                const uint32_t v = (__umulhi(B0, h0 >> 4) + __umulhi(B1, h1 >> 4) + 2) >> 2;
+                out |= v << (8 * c);
+            }
+            if (keep) *(uint32_t*)(Dl + r * dP + 4 * g) = out;
+            if (row >= db.z && row < db.w) *(uint32_t*)(G + (long long)row * pitch + 4 * g) = out;
+        }
+        __syncthreads();
     }
 }
 
@@ -390,10 +658,6 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c
 // differences, gathered into one flag byte per pixel.  (A planar u16 ROI --
 // even and odd columns de-interleaved at landing, no splitting here -- was
 // measured slower: 0.575 vs 0.510 ms, twice the LDS reads per item.)
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
-__device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 
 // Flags as signs: (C + t) - L2 and (S2 + t) - C as packed u16 differences;
 // every value is < 2^10, so the i16 sign bit is exactly the bright / dark test.
@@ -1661,7 +1925,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     P.lv = P0.lv; P.cells = P0.cells; P.pyr_bytes = P0.pyr_bytes; P.ncells = P0.ncells;
     P.slot_total = P0.slot_total; P.out_total = P0.out_total; P.roi_max = P0.roi_max;
     P.roi_dwords = P0.roi_dwords; P.win_max = P0.win_max; P.max_level_cells = P0.max_level_cells;
-    P.max_out_cap = P0.max_out_cap; P.xmax = P0.xmax; P.tab_off = P0.tab_off; P.L = L;
+    P.max_out_cap = P0.max_out_cap; P.xmax = P0.xmax; P.tab_off = P0.tab_off; P.L = L; P.pgroups = P0.pgroups;
     P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells; P.d_slot_level = P0.d_slot_level;
     const long long F = f0;
     P.d_pyr = P0.d_pyr + F * P0.pyr_bytes;
@@ -1693,6 +1957,25 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     };
     mark();
     // pyramid
+    static const bool legacy_pyr = [] { const char* e = std::getenv("ORB_PYR_LEGACY"); return e && e[0] == '1'; }();
+    if (!legacy_pyr) {
+        for (const PyrGroup& g : P.pgroups) {
+            PyrArgs pa;
+            if (g.la == 0) {
+                pa.src = d_frames; pa.src_fstride = fstride; pa.src_pitch = pitch0;
+            } else {
+                pa.src = P.d_pyr + P.lv[g.la].off; pa.src_fstride = P.pyr_bytes; pa.src_pitch = P.lv[g.la].pitch;
+            }
+            const uintptr_t al = (uintptr_t)pa.src | (uintptr_t)pa.src_pitch | (uintptr_t)(B > 1 ? pa.src_fstride : 0);
+            pa.load_mode = (al & 15) == 0 ? 16 : ((al & 3) == 0 ? 4 : 1);
+            pa.pyr = P.d_pyr; pa.pyr_fstride = P.pyr_bytes;
+            pa.lv = P.d_lv; pa.band = P0.d_pband + g.band_off;
+            pa.xs = P0.d_pxs; pa.xw = P0.d_pxw; pa.yt = P0.d_pyt;
+            pa.la = g.la; pa.lb = g.lb; pa.nb = g.nb; pa.nframes = B; pa.lds_b = g.lds_a;
+            const unsigned nwg = (unsigned)((B + 7) / 8 * 8 * g.nb);
+            hipLaunchKernelGGL(k_pyramid, dim3(nwg), dim3(256), g.lds_a + g.lds_b, st, pa);
+        }
+    } else
     for (int l = 1; l < L; ++l) {
         const LevelDev& d = P.lv[l];
         const LevelDev& s = P.lv[l - 1];

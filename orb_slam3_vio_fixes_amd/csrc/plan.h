@@ -23,6 +23,19 @@ struct LevelDev {
     float hX;
     int cell_base, ncells, slot_base, slot_total;   // cells / key slots of this level
     int out_base, out_cap;                          // quadtree output slots
+    // k_pyramid tables (l >= 1): column taps at xtab (padded to a multiple of
+    // 4 columns), row taps at ytab
+    int xtab, ytab;
+};
+
+// One launch of k_pyramid: levels la+1..lb from level la, in nb bands of
+// rows per frame (band b owns rows of every level it writes; the rows it
+// needs below are recomputed as a halo).  band_off indexes the device band
+// table: int4 {n0, n1, p0, p1} per (band, level la..lb).
+struct PyrGroup {
+    int la, lb, nb, R;
+    long long band_off;
+    int lds_a, lds_b;
 };
 
 struct CellDev {
@@ -40,6 +53,7 @@ struct Plan {
     int roi_max = 0, roi_dwords = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     std::vector<int> xmax;           // per level
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
+    std::vector<PyrGroup> pgroups;   // k_pyramid launches
     // device
     uint8_t *d_pyr = nullptr, *d_in = nullptr;
     int2* d_tab = nullptr;
@@ -54,6 +68,10 @@ struct Plan {
     float* d_angle = nullptr;
     uint8_t* d_sdesc = nullptr;
     uint8_t* d_slot_level = nullptr;
+    int4* d_pband = nullptr;         // k_pyramid band tables
+    int* d_pxs = nullptr;            // k_pyramid column taps: source column
+    uint32_t* d_pxw = nullptr;       //   and weights a0 | a1 << 16
+    int2* d_pyt = nullptr;           // k_pyramid row taps: sy0 | sy1 << 16 (clamped), b0 | b1 << 16
     // single-image host path outputs
     orb_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
@@ -64,7 +82,7 @@ struct Plan {
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level};
+                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();

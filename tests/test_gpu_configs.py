@@ -176,3 +176,22 @@ def test_extract_batch_threaded_gather_row_steps(gpu_lib):
     ref = O.OracleExtractor(1000, 1.2, 8, 20, 7)
     for i in (0, 17, 39):
         same_frame(*out[i], *ref(seq[i], (0, 1000)))
+
+
+@pytest.mark.parametrize("w,h", [(753, 481), (756, 480), (1920, 1080), (320, 240)])
+def test_pyramid_row_load_widths(gpu_lib, w, h):
+    """k_pyramid stages level 0 with 16-byte, 4-byte or 1-byte row loads by
+    the alignment of the caller's frames (row step = width here): every level
+    of every frame equal to the oracle's ComputePyramid, keypoints too."""
+    import torch
+    seq = synth.sequence(w, h, 3, config=2, start=1200)
+    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
+    torch.cuda.synchronize()
+    for f in range(len(seq)):
+        ref = O.OracleExtractor(1000, 1.2, 8, 20, 7)
+        rk, rd, rm = ref(seq[f], (0, 1000))
+        for lev, a in enumerate(ex.batch_pyramid(f)):
+            np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"frame {f} level {lev}")
+        ni = int(n[f])
+        same_frame(orb.keypoints_from_device(kps[f, :ni]), desc[f, :ni].cpu().numpy(), int(mono[f]), rk, rd, rm)
