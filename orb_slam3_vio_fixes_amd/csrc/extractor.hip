@@ -101,7 +101,7 @@ static int pyr_lds_pitch(int w) { return round_up(w + 4, 16); }
 // Bands of one group (la, lb) with R rows of level lb per band; returns the
 // LDS bytes (A + B) and fills `band` ([nb][lb-la+1] int4 {n0, n1, p0, p1}).
 static int pyr_bands(const Plan& P, const std::vector<int2>& yt, int la, int lb, int R, std::vector<int4>& band,
-                     int& lds_a, int& lds_b) {
+                     int& lds_a, int& lds_b, int& lds_x, int& lds_y) {
     const int nl = lb - la + 1, hb = P.lv[lb].h;
     const int nb = (hb + R - 1) / R;
     band.assign((size_t)nb * nl, make_int4(0, 0, 0, 0));
@@ -126,6 +126,13 @@ static int pyr_bands(const Plan& P, const std::vector<int2>& yt, int la, int lb,
             B(b, l).w = B(b, l).y;
         }
     }
+    lds_x = lds_y = 0;
+    for (int l = la + 1; l <= lb; ++l) {
+        int rows = 0;
+        for (int b = 0; b < nb; ++b) rows = std::max(rows, B(b, l).y - B(b, l).x);
+        lds_x = std::max(lds_x, round_up(P.lv[l].w, 4) * 8);
+        lds_y = std::max(lds_y, rows * 8);
+    }
     lds_a = lds_b = 0;
     for (int l = la; l < lb; ++l) {
         int rows = 0;
@@ -133,8 +140,10 @@ static int pyr_bands(const Plan& P, const std::vector<int2>& yt, int la, int lb,
         int& dst = ((l - la) & 1) ? lds_b : lds_a;
         dst = std::max(dst, rows * pyr_lds_pitch(P.lv[l].w));
     }
-    return lds_a + lds_b;
+    return lds_a + lds_b + lds_x + lds_y;
 }
+
+static int pyr_group_lds(const PyrGroup& g) { return g.lds_a + g.lds_b + g.lds_x + g.lds_y; }
 
 // Tap tables and launch groups of k_pyramid.  Groups: greedily the longest
 // run of levels (at most 4) whose bands of >= 8 top-level rows fit the LDS
@@ -177,23 +186,22 @@ static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int
         bool ok = false;
         if (ri < req.size() && req[ri][0] == la && req[ri][1] > la && req[ri][1] < L && req[ri][2] > 0) {
             g.la = la; g.lb = req[ri][1]; g.R = req[ri][2];
-            pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b);
-            ok = g.lds_a + g.lds_b <= 160 * 1024;
+            ok = pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b, g.lds_x, g.lds_y) <= 160 * 1024;
             ++ri;
         }
         for (int span = 4; span >= 1 && !ok; --span) {
             const int lb = std::min(L - 1, la + span);
             for (int R : {32, 24, 16, 12, 8, 6, 4, 2, 1}) {
                 if (R < 8 && span > 1) break;
-                int a, b;
-                if (pyr_bands(P, yt, la, lb, R, bt, a, b) <= kPyrLdsBudget || (span == 1 && R == 1)) {
-                    g.la = la; g.lb = lb; g.R = R; g.lds_a = a; g.lds_b = b;
+                int a, b, x, y;
+                if (pyr_bands(P, yt, la, lb, R, bt, a, b, x, y) <= kPyrLdsBudget || (span == 1 && R == 1)) {
+                    g.la = la; g.lb = lb; g.R = R;
                     ok = true;
                     break;
                 }
             }
         }
-        pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b);
+        pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b, g.lds_x, g.lds_y);
         g.nb = (int)(bt.size() / (size_t)(g.lb - g.la + 1));
         g.band_off = (long long)bands.size();
         bands.insert(bands.end(), bt.begin(), bt.end());
@@ -319,7 +327,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     std::vector<int2> pyt;
     build_pyramid(P, tab, pband, pxs, pxw, pyt);
     for (const PyrGroup& g : P.pgroups)
-        if (g.lds_a + g.lds_b > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
+        if (pyr_group_lds(g) > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
     P.pyr_bytes = poff;
     P.ncells = cellsum;
     P.slot_total = slotsum;
@@ -463,6 +471,7 @@ struct PyrArgs {
     const uint32_t* xw;
     const int2* yt;
     int la, lb, nb, nframes, lds_b;
+    int lds_x, lds_y;           // offsets of the staged column / row tap tables
 };
 
 __global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
@@ -528,18 +537,32 @@ __global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
         const int w = lv[l].w, dP = round_up_d(w + 4, 16), pitch = lv[l].pitch;
         const bool keep = l < a.lb;
         uint8_t* G = a.pyr + f * a.pyr_fstride + lv[l].off;
-        const int* xs = a.xs + lv[l].xtab;
-        const uint32_t* xw = a.xw + lv[l].xtab;
-        const int2* yt = a.yt + lv[l].ytab;
-        const int ng = (w + 3) >> 2, n = (db.y - db.x) * ng;
+        const int ng = (w + 3) >> 2, nrows = db.y - db.x, n = nrows * ng;
+        // this level's tap tables -> LDS (a dependent global load per item
+        // would leave every item waiting on L2 latency)
+        int* xs = (int*)(pyr_lds + a.lds_x);
+        uint32_t* xw = (uint32_t*)(xs + 4 * ng);
+        int2* yt = (int2*)(pyr_lds + a.lds_y);
+        {
+            const uint4* gx = (const uint4*)(a.xs + lv[l].xtab);
+            const uint4* gw = (const uint4*)(a.xw + lv[l].xtab);
+            const int2* gy = a.yt + lv[l].ytab + db.x;
+            for (int i = tid; i < ng; i += 256) {
+                ((uint4*)xs)[i] = gx[i];
+                ((uint4*)xw)[i] = gw[i];
+            }
+            for (int i = tid; i < nrows; i += 256) yt[i] = gy[i];
+        }
+        __syncthreads();
         const float inv = 1.0f / (float)ng;
+#pragma unroll 2
         for (int i = tid; i < n; i += 256) {
-            const int r = (int)(((float)i + 0.5f) * inv), g = i - r * ng;
+            const int r = (int)(((float)i + 0.5f) * inv), g = i - (int)__umul24(r, ng);
             const int row = db.x + r;
-            const int2 ty = yt[row];
+            const int2 ty = yt[r];
             const uint32_t B0 = (ty.y & 0xffff) << 16, B1 = ((uint32_t)ty.y >> 16) << 16;
-            const uint8_t* S0 = S + ((ty.x & 0xffff) - sb.x) * sP;
-            const uint8_t* S1 = S + ((ty.x >> 16) - sb.x) * sP;
+            const uint8_t* S0 = S + __umul24((ty.x & 0xffff) - sb.x, sP);
+            const uint8_t* S1 = S + __umul24((ty.x >> 16) - sb.x, sP);
             const int4 sx = *(const int4*)(xs + 4 * g);
             const uint4 wt = *(const uint4*)(xw + 4 * g);
             const int sxa[4] = {sx.x, sx.y, sx.z, sx.w};
@@ -554,8 +577,9 @@ __global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
                 const uint32_t v = (__umulhi(B0, h0 >> 4) + __umulhi(B1, h1 >> 4) + 2) >> 2;
                 out |= v << (8 * c);
             }
-            if (keep) *(uint32_t*)(Dl + r * dP + 4 * g) = out;
-            if (row >= db.z && row < db.w) *(uint32_t*)(G + (long long)row * pitch + 4 * g) = out;
+            if (keep) *(uint32_t*)(Dl + __umul24(r, dP) + 4 * g) = out;
+            // a level is < 2^24 bytes (4112 x 4112 at most)
+            if (row >= db.z && row < db.w) *(uint32_t*)(G + (__umul24(row, pitch) + 4 * g)) = out;
         }
         __syncthreads();
     }
@@ -1972,8 +1996,9 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
             pa.lv = P.d_lv; pa.band = P0.d_pband + g.band_off;
             pa.xs = P0.d_pxs; pa.xw = P0.d_pxw; pa.yt = P0.d_pyt;
             pa.la = g.la; pa.lb = g.lb; pa.nb = g.nb; pa.nframes = B; pa.lds_b = g.lds_a;
+            pa.lds_x = g.lds_a + g.lds_b; pa.lds_y = pa.lds_x + g.lds_x;
             const unsigned nwg = (unsigned)((B + 7) / 8 * 8 * g.nb);
-            hipLaunchKernelGGL(k_pyramid, dim3(nwg), dim3(256), g.lds_a + g.lds_b, st, pa);
+            hipLaunchKernelGGL(k_pyramid, dim3(nwg), dim3(256), pyr_group_lds(g), st, pa);
         }
     } else
     for (int l = 1; l < L; ++l) {

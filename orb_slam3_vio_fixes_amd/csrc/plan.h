@@ -35,7 +35,7 @@ struct LevelDev {
 struct PyrGroup {
     int la, lb, nb, R;
     long long band_off;
-    int lds_a, lds_b;
+    int lds_a, lds_b, lds_x, lds_y;   // LDS: two level buffers, column taps, row taps
 };
 
 struct CellDev {
