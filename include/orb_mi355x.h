@@ -164,6 +164,18 @@ int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);
  * interface. */
 int orbx_set_streams(orbx_handle* h, int nsub);
 
+/* Pyramid kernel of subsequent extractions (results identical for every
+ * choice): 0 auto (k_pyr_stream for batches of >= 32 frames, k_pyramid row
+ * bands below that), 1 k_pyramid, 2 k_pyr_stream (one workgroup sliding down
+ * each frame) whenever the image size allows it, 3 per-level k_resize, 4
+ * k_pyr_level (one launch per level, a wave per run of rows) whenever the
+ * size and the frames' 4-byte alignment allow it.  orbx_pyramid_kernel returns
+ * the kernel (1-4) the last extraction on the handle ran, 0 before any.  The
+ * environment variable ORB_PYR_MODE sets a new handle's mode.  Not part of
+ * the reference interface. */
+int orbx_set_pyramid_mode(orbx_handle* h, int mode);
+int orbx_pyramid_kernel(orbx_handle* h);
+
 /* ---------------- stereo ---------------- */
 
 /* Frame::ComputeStereoMatches (src/Frame.cc:811-981) for one rectified pair:

@@ -210,6 +210,246 @@ static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int
     }
 }
 
+constexpr int kPyrStreamMinFrames = 32;   // below this a frame per CU leaves the chip idle: row bands
+constexpr int kPsRun = 4;                 // k_pyr_stream: output rows per run (one lane, one column group)
+
+// k_pyr_stream layout for level-0 chunks of K0 rows: runs the step schedule
+// (level l computes at step s every row whose two source rows of level l-1
+// were visible at the start of step s, i.e. written at a step < s; chunk c of
+// level 0 is written at step c) and sizes each level's ring to the rows that
+// must coexist: those written at a step and every row still to be read at
+// that step or later.  Fills PS (except the table offsets) and `steps`;
+// returns the LDS bytes of the rings.
+static long long pyr_stream_schedule(const Plan& P, const std::vector<int2>& rows_tab, int K0, int R, PyrStream& PS,
+                                     std::vector<int4>& steps) {
+    const int L = P.L, h0 = P.lv[0].h;
+    PS.K0 = K0;
+    PS.nchunks = (h0 + K0 - 1) / K0;
+    std::vector<int> next(L, 0), vis(L, 0);
+    struct Span { int rd_lo, wr_lo, wr_hi; };
+    std::vector<std::vector<Span>> hist(L);
+    steps.clear();
+    int s = 0;
+    for (;; ++s) {
+        bool done = true;
+        for (int l = 1; l < L; ++l) done &= next[l] >= P.lv[l].h;
+        if (done) break;
+        if (s > 4 * h0 + 64) return -1;                  // no progress (cannot happen for valid tables)
+        vis[0] = std::min(s * K0, h0);
+        std::vector<int4> row(L, make_int4(0, 0, 0, 0));
+        int wtotal = 0;
+        std::vector<Span> sp(L, Span{INT32_MAX, 0, 0});
+        // level 0: chunk s written at this step
+        if (s < PS.nchunks) sp[0].wr_lo = s * K0, sp[0].wr_hi = std::min(h0, (s + 1) * K0);
+        for (int l = 1; l < L; ++l) {
+            const int hl = P.lv[l].h, ng = (P.lv[l].w + 3) / 4;
+            const int lo = next[l];
+            int hi = lo;
+            while (hi < hl && (rows_tab[P.lv[l].ytab + hi].x >> 16) < vis[l - 1]) ++hi;
+            if (hi > lo) sp[l - 1].rd_lo = rows_tab[P.lv[l].ytab + lo].x & 0xffff;
+            if (l < L - 1) sp[l].wr_lo = lo, sp[l].wr_hi = hi;
+            const int runs = (hi - lo + R - 1) / R;           // runs of <= R rows per column group
+            const int wi = (runs * ng + kWave - 1) / kWave;
+            row[l] = make_int4(lo, hi - lo, wtotal, ng | (runs << 16));
+            wtotal += wi;
+            next[l] = hi;
+        }
+        row[0] = make_int4(wtotal, 0, 0, 0);
+        steps.insert(steps.end(), row.begin(), row.end());
+        for (int l = 1; l < L; ++l) vis[l] = next[l];
+        for (int m = 0; m < L - 1; ++m) hist[m].push_back(sp[m]);
+    }
+    PS.nsteps = s;
+    long long bytes = 0;
+    for (int m = 0; m < L - 1; ++m) {
+        int need = 1, fut = INT32_MAX;
+        for (int t = s - 1; t >= 0; --t) {                // minimum row read at step >= t
+            fut = std::min(fut, hist[m][t].rd_lo);
+            const Span& x = hist[m][t];
+            if (x.wr_hi > x.wr_lo) need = std::max(need, x.wr_hi - std::min(fut, x.wr_lo));
+        }
+        PS.ring_rows[m] = std::min(need, P.lv[m].h);
+        PS.ring_pitch[m] = round_up(P.lv[m].w + 12, 16);
+        bytes += (long long)PS.ring_rows[m] * PS.ring_pitch[m];
+    }
+    return bytes;
+}
+
+// Column records of level l (>= 1) for k_pyr_stream / k_pyr_level: per group
+// of 4 output columns the weights (16 a0 | 16 a1 << 16) of each output, the
+// v_perm selectors that place (S[sx] << 8, S[sx+1] << 8) in a u16 pair from
+// the 3 dwords at the group's first tap dword bd, and bd | window flags << 16
+// (outputs 0-2 take their taps from dwords 0:1, output 3 from 0:1 or 1:2).
+// Layout W[4 ng], S[4 ng], BF[ng].  False when a tap span or weight is outside
+// what that selection handles (scale factors near 2).
+static bool pyr_col_records(const Plan& P, const std::vector<int2>& tab, int l, std::vector<uint32_t>& rec) {
+    const LevelDev& d = P.lv[l];
+    const int ng = (d.w + 3) / 4, ws = P.lv[l - 1].w;
+    rec.assign((size_t)9 * ng, 0u);
+    for (int g = 0; g < ng; ++g) {
+        const int sx0 = tab[P.tab_off[l] + std::min(4 * g, d.w - 1)].x;
+        const int bd = sx0 >> 2;
+        uint32_t flags = 0;
+        for (int c = 0; c < 4; ++c) {
+            const int2 e = tab[P.tab_off[l] + std::min(4 * g + c, d.w - 1)];
+            const int a0 = (short)(e.y & 0xffff), a1 = e.y >> 16;
+            const int o = e.x - 4 * bd;
+            if (a0 < 0 || a0 > 2048 || a1 < 0 || a1 > 2048 || o < 0 || o > 10 || e.x + 1 > ws) return false;
+            if (c < 3 && o > 6) return false;
+            const int win = c == 3 && o >= 4, op = o - 4 * win;
+            rec[4 * g + c] = (uint32_t)(16 * a0) | ((uint32_t)(16 * a1) << 16);
+            rec[4 * ng + 4 * g + c] = 0x0cu | ((uint32_t)op << 8) | (0x0cu << 16) | ((uint32_t)(op + 1) << 24);
+            flags |= (uint32_t)win << c;
+        }
+        rec[8 * ng + g] = (uint32_t)bd | (flags << 16);
+    }
+    return true;
+}
+
+// k_pyr_level plan: column records of every level, and per level the run
+// length R (output rows per wave) such that a run's source rows fit kPlNS.
+static void build_pyr_level(Plan& P, const std::vector<int2>& tab, const std::vector<int2>& yt,
+                            std::vector<uint32_t>& col) {
+    PyrLevelPlan& Q = P.pl;
+    Q = PyrLevelPlan();
+    col.clear();
+    const int L = P.L;
+    for (int l = 1; l < L; ++l) {
+        const LevelDev& d = P.lv[l];
+        std::vector<uint32_t> rec;
+        if (!pyr_col_records(P, tab, l, rec)) return;
+        const int ng = (d.w + 3) / 4;
+        // dword loads of 3 dwords at bd stay inside the source row's pitch
+        // (level 0: the kernel clamps them in the buffer's last row)
+        if (l >= 2)
+            for (int g = 0; g < ng; ++g)
+                if (4 * (int)(rec[8 * ng + g] & 0xffff) + 12 > P.lv[l - 1].pitch) return;
+        Q.col_off[l] = (int)col.size();
+        col.insert(col.end(), rec.begin(), rec.end());
+        col.resize(round_up((int)col.size(), 4), 0u);
+        int R = 0;
+        for (int r = kPlRmax; r >= 1 && !R; --r) {
+            bool fits = true;
+            for (int y0 = 0; y0 < d.h && fits; y0 += r) {
+                const int y1 = std::min(d.h, y0 + r);
+                fits = (yt[d.ytab + y1 - 1].x >> 16) - (yt[d.ytab + y0].x & 0xffff) + 1 <= kPlNS;
+            }
+            if (fits) R = r;
+        }
+        if (!R) return;
+        Q.R[l] = R;
+        Q.runs[l] = (d.h + R - 1) / R;
+    }
+    Q.ok = true;
+}
+
+// The k_pyr_stream plan: table image (column records, row records) and
+// rings in one LDS image of at most 160 KiB, with the largest level-0 chunk
+// (<= 32 rows) that fits; PS.ok stays false when the size is not supported
+// (more than kPsMaxLevels levels, weights or tap spans outside what the
+// kernel's byte selection handles, or no chunk size fits).
+static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<uint32_t>& img,
+                             std::vector<int4>& steps) {
+    PyrStream PS;
+    P.ps = PS;
+    const int L = P.L;
+    if (L < 2 || L > kPsMaxLevels) return;
+    // per level l >= 1: the row table of k_pyramid form (clamped rows) for the schedule
+    std::vector<int2> rows_tab;
+    std::vector<LevelDev> lv = P.lv;
+    for (int l = 1; l < L; ++l) {
+        const LevelDev& s = P.lv[l - 1];
+        lv[l].ytab = (int)rows_tab.size();
+        for (int dy = 0; dy < P.lv[l].h; ++dy) {
+            const int2 e = tab[P.tab_off[l] + P.lv[l].w + dy];
+            const int r0 = std::min(std::max(e.x, 0), s.h - 1), r1 = std::min(std::max(e.x + 1, 0), s.h - 1);
+            const int b0 = (short)(e.y & 0xffff), b1 = e.y >> 16;
+            if (b0 < 0 || b0 > 2048 || b1 < 0 || b1 > 2048) return;
+            rows_tab.push_back(make_int2(r0 | (r1 << 16), e.y));
+        }
+    }
+    Plan Q = P;                       // the schedule reads lv[l].ytab of the row table above
+    Q.lv = lv;
+    int K0 = 0;
+    int rec_dw = 0;                   // column and row records
+    for (int l = 1; l < L; ++l) {
+        const int ng = (P.lv[l].w + 3) / 4;
+        rec_dw += round_up(9 * ng, 4) + 4 * P.lv[l].h;
+    }
+    int k0_env = 0, run_rows = kPsRun;
+    if (const char* e = std::getenv("ORB_PYR_K0")) k0_env = std::atoi(e);
+    if (const char* e = std::getenv("ORB_PYR_RUN")) run_rows = std::max(1, std::min(kPsRun, std::atoi(e)));
+    const int nq16 = (P.lv[0].w + 15) / 16;
+    int tab_dw = 0;
+    for (int k : {32, 24, 16, 12, 8, 6, 4}) {
+        if (k0_env > 0 && k != k0_env) continue;
+        if (k * nq16 > 2 * 1024) continue;                 // two 16-byte chunk loads per thread at most
+        std::vector<int4> st;
+        PyrStream T;
+        const long long rb = pyr_stream_schedule(Q, rows_tab, k, run_rows, T, st);
+        const int td = round_up(T.nsteps, 4) + 4 * L + 4 * T.nsteps * L + rec_dw;
+        if (rb < 0 || 4LL * td + rb > 160 * 1024) continue;
+        K0 = k;
+        tab_dw = td;
+        PS = T;
+        steps = st;
+        break;
+    }
+    if (K0 == 0) return;
+    // LDS image: level table, step table, records, then the rings (16-byte aligned)
+    img.assign(tab_dw, 0u);
+    // per-step wave-item counters first (zeros in the image), then the level
+    // and step tables
+    PS.cnt_dw = 0;
+    PS.lev_u4 = round_up(PS.nsteps, 4) / 4;
+    PS.steps_u4 = PS.lev_u4 + L;
+    std::memcpy(&img[4 * PS.steps_u4], steps.data(), steps.size() * sizeof(int4));
+    int dw = 4 * (PS.steps_u4 + PS.nsteps * L);
+    for (int l = 1; l < L; ++l) {
+        const int ng = (P.lv[l].w + 3) / 4;
+        PS.ng[l] = ng;
+        PS.rec_dw[l] = dw;
+        dw += round_up(9 * ng, 4);
+        PS.yt_dw[l] = dw;
+        dw += 4 * P.lv[l].h;
+        img[4 * (PS.lev_u4 + l)] = (uint32_t)PS.rec_dw[l];
+        img[4 * (PS.lev_u4 + l) + 1] = (uint32_t)PS.yt_dw[l];
+    }
+    int rdw = tab_dw;
+    for (int m = 0; m < L - 1; ++m) {
+        PS.ring_dw[m] = rdw;
+        rdw += PS.ring_rows[m] * PS.ring_pitch[m] / 4;
+    }
+    if (rdw >= 65536) return;                              // row records hold 16-bit dword offsets
+    if (4LL * rdw > 160 * 1024) return;
+    for (int l = 1; l < L; ++l) {
+        const LevelDev& d = P.lv[l];
+        const int ng = PS.ng[l];
+        std::vector<uint32_t> rec;
+        if (!pyr_col_records(P, tab, l, rec)) return;
+        for (int g = 0; g < ng; ++g)
+            if ((int)(rec[8 * ng + g] & 0xffff) + 2 >= PS.ring_pitch[l - 1] / 4) return;
+        std::copy(rec.begin(), rec.end(), img.begin() + PS.rec_dw[l]);
+        for (int dy = 0; dy < d.h; ++dy) {
+            const int2 e = rows_tab[lv[l].ytab + dy];
+            const int r0 = e.x & 0xffff, r1 = e.x >> 16, m = l - 1;
+            const uint32_t o0 = (uint32_t)(PS.ring_dw[m] + (r0 % PS.ring_rows[m]) * PS.ring_pitch[m] / 4);
+            const uint32_t o1 = (uint32_t)(PS.ring_dw[m] + (r1 % PS.ring_rows[m]) * PS.ring_pitch[m] / 4);
+            const uint32_t dst = l < L - 1 ? (uint32_t)(PS.ring_dw[l] + (dy % PS.ring_rows[l]) * PS.ring_pitch[l] / 4)
+                                           : 0xffffffffu;
+            uint32_t* r = &img[PS.yt_dw[l] + 4 * dy];
+            r[0] = o0 | (o1 << 16);
+            r[1] = (uint32_t)e.y;
+            r[2] = dst;
+            r[3] = (uint32_t)(d.off + (long long)dy * d.pitch);
+        }
+    }
+    PS.tab_u4 = tab_dw / 4;
+    PS.lds_bytes = 4 * rdw;
+    PS.ok = true;
+    P.ps = PS;
+}
+
 // Builds the size-dependent plan into P; returns ORB_OK or an error.  The
 // caller (build_plan) releases P on any error, so a failed size never leaves a
 // plan that a later call with the same size would take for a built one.
@@ -233,7 +473,8 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         // levels narrower than 46 px are refused here (the 35-px cell check
         // below refuses the rest of that range).
         if (d.w < 2 * kEdge + 8 || d.h < 2 * kEdge + 8) return ORB_ERR_UNSUPPORTED;
-        d.pitch = round_up(d.w, 64);
+        // 12 bytes of slack: k_pyr_level reads 3 dwords from a tap's dword
+        d.pitch = round_up(d.w + 12, 64);
         d.off = l == 0 ? 0 : poff;
         if (l > 0) poff += (long long)d.pitch * d.h;
         d.scale = hd->scale[l];
@@ -326,6 +567,10 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     std::vector<uint32_t> pxw;
     std::vector<int2> pyt;
     build_pyramid(P, tab, pband, pxs, pxw, pyt);
+    std::vector<uint32_t> psimg, plcol;
+    std::vector<int4> pssteps;
+    build_pyr_stream(P, tab, psimg, pssteps);
+    build_pyr_level(P, tab, pyt, plcol);
     for (const PyrGroup& g : P.pgroups)
         if (pyr_group_lds(g) > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
     P.pyr_bytes = poff;
@@ -365,6 +610,14 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         ORB_CHECK(hipMemcpy(P.d_pxs, pxs.data(), pxs.size() * sizeof(int), hipMemcpyHostToDevice));
         ORB_CHECK(hipMemcpy(P.d_pxw, pxw.data(), pxw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         ORB_CHECK(hipMemcpy(P.d_pyt, pyt.data(), pyt.size() * sizeof(int2), hipMemcpyHostToDevice));
+    }
+    if (P.pl.ok) {
+        ORB_CHECK(hipMalloc(&P.d_pcol, plcol.size() * sizeof(uint32_t)));
+        ORB_CHECK(hipMemcpy(P.d_pcol, plcol.data(), plcol.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    if (P.ps.ok) {
+        ORB_CHECK(hipMalloc(&P.d_ps_tab, psimg.size() * sizeof(uint32_t)));
+        ORB_CHECK(hipMemcpy(P.d_ps_tab, psimg.data(), psimg.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     ORB_CHECK(hipMemcpy(P.d_lv, P.lv.data(), L * sizeof(LevelDev), hipMemcpyHostToDevice));
     ORB_CHECK(hipMemcpy(P.d_cells, P.cells.data(), P.cells.size() * sizeof(CellDev), hipMemcpyHostToDevice));
@@ -582,6 +835,318 @@ __global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
             if (row >= db.z && row < db.w) *(uint32_t*)(G + (__umul24(row, pitch) + 4 * g)) = out;
         }
         __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_stream: ComputePyramid (ORBextractor.cc:1170-1195) of one frame per
+// 1024-thread workgroup, cv::resize INTER_LINEAR 8UC1, as a
+// software pipeline that slides down the frame once.
+//
+// Step s: chunk s of level 0 (K0 rows, prefetched into registers with 16-byte
+// loads during step s-1) lands in level 0's LDS ring, and every level l >= 1
+// computes the rows whose two source rows of level l-1 were in its ring by
+// the end of step s-1, writing each row to HBM and (levels < L-1) into its own
+// ring.  All levels of a step are independent, so a step is one flat list of
+// wave-items (64 column groups of 4 outputs; levels padded to whole waves)
+// followed by ONE barrier.  Nothing is recomputed and level 0 is read from HBM
+// exactly once; ring sizes come from the host's run of the same schedule.
+//
+// Per item: 3 dwords of each source row (the 4 outputs' taps lie within 12
+// bytes of the first tap's dword), the (S[sx], S[sx+1]) pair of output c by
+// one v_perm with a host-made selector (window D0:D1 or D1:D2 by a flag bit),
+// h = a0*S[sx] + a1*S[sx+1] by v_dot2_u32_u16 with weights pre-scaled by 16 so
+// that (16h) & ~0xff = (h >> 4) << 8, and OpenCV's (b * (h >> 4)) >> 16 as
+// v_mul_hi_u32_u24(b << 8, (h >> 4) << 8).
+// ---------------------------------------------------------------------------
+
+struct PyrStreamArgs {
+    const uint8_t* src;         // level 0 of frame 0
+    long long src_fstride;
+    int src_pitch, load_mode;   // 16 / 4 / 1
+    uint8_t* pyr;               // levels >= 1 of frame 0
+    long long pyr_fstride;
+    const uint4* tab;           // LDS table image
+    int tab_u4, lev_u4, steps_u4;   // table image size; level and step tables inside it (uint4 units)
+    int L, nsteps, nchunks, K0, h0, w0, nframes;
+    int ring0_dw, ring0_rows, ring0_pitch;
+    int cnt_dw;                 // per-step wave-item counters (nsteps dwords)
+};
+
+// Workgroup barrier that orders LDS only: __syncthreads()' workgroup fence
+// also waits for every outstanding global load and store (vmcnt(0)), which
+// would drain the next chunk's prefetch and the step's HBM writes each step.
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
+    return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
+}
+
+__global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
+    extern __shared__ uint4 ps_lds[];
+    uint32_t* lds = (uint32_t*)ps_lds;
+    const int f = blockIdx.x;
+    if (f >= a.nframes) return;
+    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    for (int i = tid; i < a.tab_u4; i += 1024) ps_lds[i] = a.tab[i];
+    lds_barrier();
+    // lane l: level l's {column records, row records} dword offsets
+    const uint4 lvt = ps_lds[a.lev_u4 + min(lane, a.L - 1)];
+    const uint8_t* src = a.src + f * a.src_fstride;
+    uint8_t* pyr = a.pyr + f * a.pyr_fstride;
+    const int nq = (a.w0 + 15) >> 4;
+    const float inv_nq = 1.0f / (float)nq;
+    uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0;
+    // chunk c of level 0 -> registers (two 16-byte pieces per thread at most)
+#define PS_FETCH(c)                                                                            \
+    do {                                                                                       \
+        const int r0_ = (c) * a.K0, n_ = min(a.K0, a.h0 - r0_) * nq;                           \
+        if (tid < n_) {                                                                        \
+            const int r_ = (int)(((float)tid + 0.5f) * inv_nq), q_ = tid - r_ * nq;            \
+            pre0 = *(const uint4*)(src + (long long)(r0_ + r_) * a.src_pitch + 16 * q_);       \
+        }                                                                                      \
+        if (tid + 1024 < n_) {                                                                 \
+            const int i_ = tid + 1024;                                                         \
+            const int r_ = (int)(((float)i_ + 0.5f) * inv_nq), q_ = i_ - r_ * nq;              \
+            pre1 = *(const uint4*)(src + (long long)(r0_ + r_) * a.src_pitch + 16 * q_);       \
+        }                                                                                      \
+    } while (0)
+    // chunk c -> level 0's ring
+    auto land = [&](int c, uint4 v0, uint4 v1) {
+        const int r0 = c * a.K0, rows = min(a.K0, a.h0 - r0);
+        const int base = r0 % a.ring0_rows;
+        if (a.load_mode == 16) {
+            const int n = rows * nq;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int i = tid + k * 1024;
+                if (i < n) {
+                    const int r = (int)(((float)i + 0.5f) * inv_nq), q = i - r * nq;
+                    int slot = base + r;
+                    if (slot >= a.ring0_rows) slot -= a.ring0_rows;
+                    ps_lds[(a.ring0_dw + slot * (a.ring0_pitch >> 2)) / 4 + q] = k ? v1 : v0;
+                }
+            }
+        } else if (a.load_mode == 4) {
+            const int nd = (a.w0 + 3) >> 2, n = rows * nd;
+            const float inv = 1.0f / (float)nd;
+            for (int i = tid; i < n; i += 1024) {
+                const int r = (int)(((float)i + 0.5f) * inv), q = i - r * nd;
+                int slot = base + r;
+                if (slot >= a.ring0_rows) slot -= a.ring0_rows;
+                lds[a.ring0_dw + slot * (a.ring0_pitch >> 2) + q] =
+                    *(const uint32_t*)(src + (long long)(r0 + r) * a.src_pitch + 4 * q);
+            }
+        } else {
+            const int n = rows * a.w0;
+            const float inv = 1.0f / (float)a.w0;
+            uint8_t* l8 = (uint8_t*)lds;
+            for (int i = tid; i < n; i += 1024) {
+                const int r = (int)(((float)i + 0.5f) * inv), q = i - r * a.w0;
+                int slot = base + r;
+                if (slot >= a.ring0_rows) slot -= a.ring0_rows;
+                l8[4 * a.ring0_dw + slot * a.ring0_pitch + q] = src[(long long)(r0 + r) * a.src_pitch + q];
+            }
+        }
+    };
+    if (a.load_mode == 16) PS_FETCH(0);
+    for (int s = 0; s < a.nsteps; ++s) {
+        if (s < a.nchunks) {
+            land(s, pre0, pre1);
+            if (a.load_mode == 16 && s + 1 < a.nchunks) PS_FETCH(s + 1);
+        }
+        // lane l >= 1 holds level l's entry of this step {first row, rows, first
+        // wave-item, ng | runs << 16}; lane 0 {wave-items of the step}
+        const uint4 se = ps_lds[a.steps_u4 + s * a.L + min(lane, a.L - 1)];
+        const int W = __builtin_amdgcn_readfirstlane((int)se.x);
+        for (int it = 0; it <= W; ++it) {      // bounded: a wave never takes more than W items
+            // wave-items are taken from a per-step LDS counter: waves that drew
+            // cheap items take more, so the step ends when the work does
+            // (the counters sit in the first 64 KiB of LDS: an LDS atomic at
+            // a higher address was measured to return garbage on gfx950)
+            int jj = 0;
+            if (lane == 0) jj = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
+            const int j = __builtin_amdgcn_readfirstlane(jj);
+            if (j >= W) break;
+            const int l = __builtin_popcountll(__ballot(lane >= 1 && lane < a.L && (int)se.z <= j));
+            const int lo = __builtin_amdgcn_readlane((int)se.x, l), nrows = __builtin_amdgcn_readlane((int)se.y, l);
+            const int wst = __builtin_amdgcn_readlane((int)se.z, l), ngr = __builtin_amdgcn_readlane((int)se.w, l);
+            const int rec = __builtin_amdgcn_readlane((int)lvt.x, l), ytd = __builtin_amdgcn_readlane((int)lvt.y, l);
+            const int runs = ngr >> 16, ng = ngr & 0xffff;
+            const int local = (j - wst) * kWave + lane;
+            const int run = (int)(((float)local + 0.5f) * __builtin_amdgcn_rcpf((float)ng));
+            const int g = local - (int)__umul24(run, ng);
+            if (run < runs) {
+                // rows [y0, y1) of the step's nrows, split into `runs` nearly equal runs
+                const float inv_runs = __builtin_amdgcn_rcpf((float)runs);
+                const int y0 = lo + (int)(((float)__umul24(run, nrows) + 0.5f) * inv_runs);
+                const int y1 = lo + (int)(((float)__umul24(run + 1, nrows) + 0.5f) * inv_runs);
+                const int nr = y1 - y0;
+                const uint4 wt = ps_lds[(rec >> 2) + g];
+                const uint4 sl = ps_lds[(rec >> 2) + ng + g];
+                const uint32_t bf = lds[rec + 8 * ng + g];
+                const uint32_t bd = bf & 0xffff;
+                const bool hi3 = (bf >> 19) & 1;        // output 3's taps in D1:D2 (outputs 0-2: D0:D1)
+                // horizontal pass of one source row: the perm puts each tap pixel
+                // in the high byte of its u16, so with weights 16a the dot product
+                // is 4096 h and its upper half-word is OpenCV's h >> 4
+                auto hrow = [&](const uint32_t (&d)[3], uint32_t (&hv)[4]) {
+                    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+                    hv[0] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.x)), as_u16x2(wt.x), 0u, false);
+                    hv[1] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.y)), as_u16x2(wt.y), 0u, false);
+                    hv[2] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.z)), as_u16x2(wt.z), 0u, false);
+                    hv[3] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(hi3 ? d2 : d1, hi3 ? d1 : d0, sl.w)),
+                                                   as_u16x2(wt.w), 0u, false);
+                };
+                // every LDS read of the run first (row records, then both source
+                // rows of every output row), so the run waits on LDS latency twice
+                uint4 yr[kPsRun];
+#pragma unroll
+                for (int q = 0; q < kPsRun; ++q) yr[q] = ps_lds[(ytd >> 2) + y0 + min(q, nr - 1)];
+                uint32_t D[kPsRun][2][3];
+#pragma unroll
+                for (int q = 0; q < kPsRun; ++q)
+#pragma unroll
+                    for (int t = 0; t < 2; ++t) {
+                        const uint32_t* Rp = lds + (t ? yr[q].x >> 16 : yr[q].x & 0xffff) + bd;
+                        D[q][t][0] = Rp[0]; D[q][t][1] = Rp[1]; D[q][t][2] = Rp[2];
+                    }
+                uint32_t hA[4], hB[4];
+#pragma unroll
+                for (int q = 0; q < kPsRun; ++q) {
+                    if (q < nr) {
+                        const uint32_t o0 = yr[q].x & 0xffff, o1 = yr[q].x >> 16;
+                        // the top source row is usually the previous row's bottom one
+                        if (q > 0 && o0 == (yr[q - 1].x >> 16)) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) hA[c] = hB[c];
+                        } else {
+                            hrow(D[q][0], hA);
+                        }
+                        if (o1 == o0) {
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) hB[c] = hA[c];
+                        } else {
+                            hrow(D[q][1], hB);
+                        }
+                        // OpenCV's ((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2
+                        const uint32_t b0 = yr[q].y & 0xffff, b1 = yr[q].y >> 16;
+                        uint32_t out = 0;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            const uint32_t x0 = __umul24(b0, hA[c] >> 16), x1 = __umul24(b1, hB[c] >> 16);
+                            out |= (((x0 >> 16) + (x1 >> 16) + 2) >> 2) << (8 * c);
+                        }
+                        if (yr[q].z != 0xffffffffu) lds[yr[q].z + g] = out;
+                        *(uint32_t*)(pyr + yr[q].w + 4 * g) = out;
+                    }
+                }
+            }
+        }
+        lds_barrier();
+    }
+#undef PS_FETCH
+}
+
+// ---------------------------------------------------------------------------
+// k_pyr_level: level l of ComputePyramid (ORBextractor.cc:1170-1195) from
+// level l-1 in HBM for every frame, cv::resize INTER_LINEAR 8UC1 (SURVEY.md
+// A.1); one launch per level, no LDS and no barrier.
+//
+// A wave owns 64 column groups (4 outputs each) of a run of R output rows of
+// one frame.  The run's row taps are wave-uniform (scalar loads); its source
+// rows are consecutive, so every one of them is requested at once (3 dwords
+// per lane and row, <= kPlNS rows in flight), then each source row is resized
+// horizontally ONCE -- the perm/dot2 form of k_pyr_stream gives 4096 h per
+// output -- and every output row whose bottom tap is that row is finished
+// from it and the row before: at scale 1.2 a source row serves ~1.2 output
+// rows instead of being recomputed for each.
+// ---------------------------------------------------------------------------
+struct PyrLevelArgs {
+    const uint8_t* src;
+    long long src_fstride;
+    int src_pitch, src_h, src_dwords;   // dwords of a source row holding pixels
+    uint8_t* dst;
+    long long dst_fstride;
+    int dst_pitch;
+    const uint32_t* col;                // W[4 ng] | S[4 ng] | BF[ng]
+    const int2* rows;                   // per output row: r0 | r1 << 16 (clamped), b0 | b1 << 16
+    int ng, nchunk, runs, R, h, nframes;
+    int guard_last;                     // clamp the loads of the buffer's last source row
+};
+
+__global__ __launch_bounds__(256) void k_pyr_level(PyrLevelArgs a) {
+    const int gw = blockIdx.x * 4 + wave_id();
+    const int per_frame = a.runs * a.nchunk;
+    const int f = gw / per_frame;
+    if (f >= a.nframes) return;
+    const int rem = gw - f * per_frame, run = rem / a.nchunk, ch = rem - run * a.nchunk;
+    const int lane = lane_id();
+    const int gi = ch * kWave + lane;
+    const bool active = gi < a.ng;
+    const int g = min(gi, a.ng - 1);
+    // row taps as 64-bit words {r0 | r1 << 16, b0 | b1 << 16}, read by scalar loads
+    typedef __attribute__((address_space(4))) const unsigned long long* ConstRows;
+    const ConstRows rows = (ConstRows)a.rows;
+    const int y0 = run * a.R, y1 = min(a.h, y0 + a.R);
+    const int rbase = (int)(rows[y0] & 0xffff), nsrc = (int)((rows[y1 - 1] >> 16) & 0xffff) - rbase + 1;
+    const uint4 wt = ((const uint4*)a.col)[g];
+    const uint4 sl = ((const uint4*)a.col)[a.ng + g];
+    const uint32_t bf = a.col[8 * a.ng + g];
+    const int bd = bf & 0xffff;
+    const bool hi3 = (bf >> 19) & 1;
+    const uint8_t* S = a.src + f * a.src_fstride + (long long)rbase * a.src_pitch;
+    uint32_t D[kPlNS][3];
+    const bool guard = a.guard_last && f == a.nframes - 1;
+#pragma unroll
+    for (int k = 0; k < kPlNS; ++k) {
+        if (k < nsrc) {
+            const uint8_t* p = S + (long long)k * a.src_pitch;
+            if (guard && rbase + k == a.src_h - 1) {
+                // the buffer's last row: no dword past its last pixel dword
+                const uint32_t* q = (const uint32_t*)p;
+                const int last = a.src_dwords - 1;
+                D[k][0] = q[min(bd, last)]; D[k][1] = q[min(bd + 1, last)]; D[k][2] = q[min(bd + 2, last)];
+            } else {
+                const uint32_t* q = (const uint32_t*)p + bd;
+                D[k][0] = q[0]; D[k][1] = q[1]; D[k][2] = q[2];
+            }
+        }
+    }
+    uint8_t* O = a.dst + f * a.dst_fstride + 4 * g;
+    uint32_t hP[4] = {0, 0, 0, 0}, hC[4] = {0, 0, 0, 0};
+    int y = y0;
+#pragma unroll
+    for (int k = 0; k < kPlNS; ++k) {
+        if (k < nsrc) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) hP[c] = hC[c];
+            const uint32_t d0 = D[k][0], d1 = D[k][1], d2 = D[k][2];
+            hC[0] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.x)), as_u16x2(wt.x), 0u, false);
+            hC[1] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.y)), as_u16x2(wt.y), 0u, false);
+            hC[2] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.z)), as_u16x2(wt.z), 0u, false);
+            hC[3] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(hi3 ? d2 : d1, hi3 ? d1 : d0, sl.w)),
+                                           as_u16x2(wt.w), 0u, false);
+            // every output row whose bottom tap is this source row
+            while (y < y1) {
+                const unsigned long long e = rows[y];
+                const int r0 = (int)(e & 0xffff), r1 = (int)((e >> 16) & 0xffff);
+                if (r1 != rbase + k) break;
+                const uint32_t b0 = (uint32_t)(e >> 32) & 0xffff, b1 = (uint32_t)(e >> 48);
+                uint32_t out = 0;
+#pragma unroll
+                for (int c = 0; c < 4; ++c) {
+                    const uint32_t x0 = __umul24(b0, (r0 == r1 ? hC[c] : hP[c]) >> 16), x1 = __umul24(b1, hC[c] >> 16);
+                    out |= (((x0 >> 16) + (x1 >> 16) + 2) >> 2) << (8 * c);
+                }
+                if (active) *(uint32_t*)(O + (long long)y * a.dst_pitch) = out;
+                ++y;
+            }
+        }
     }
 }
 
@@ -1981,8 +2546,46 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     };
     mark();
     // pyramid
-    static const bool legacy_pyr = [] { const char* e = std::getenv("ORB_PYR_LEGACY"); return e && e[0] == '1'; }();
-    if (!legacy_pyr) {
+    const int pm = hd->pyr_mode;
+    const bool legacy_pyr = pm == 3;
+    const bool use_stream = P0.ps.ok && (pm == 2 || (pm == 0 && B >= kPyrStreamMinFrames));
+    const bool al4 = (((uintptr_t)d_frames | (uintptr_t)pitch0 | (uintptr_t)(B > 1 ? fstride : 0)) & 3) == 0;
+    const bool use_level = P0.pl.ok && al4 && pm == 4;
+    hd->pyr_last = legacy_pyr ? 3 : (use_level ? 4 : (use_stream ? 2 : 1));
+    if (!legacy_pyr && use_level) {
+        for (int l = 1; l < L; ++l) {
+            const LevelDev& d = P.lv[l];
+            const LevelDev& sv = P.lv[l - 1];
+            PyrLevelArgs la;
+            la.src = l == 1 ? d_frames : P.d_pyr + sv.off;
+            la.src_fstride = l == 1 ? fstride : P.pyr_bytes;
+            la.src_pitch = l == 1 ? pitch0 : sv.pitch;
+            la.src_h = sv.h;
+            la.src_dwords = (sv.w + 3) / 4;
+            la.dst = P.d_pyr + d.off; la.dst_fstride = P.pyr_bytes; la.dst_pitch = d.pitch;
+            la.col = P0.d_pcol + P0.pl.col_off[l];
+            la.rows = P0.d_pyt + d.ytab;
+            la.ng = (d.w + 3) / 4;
+            la.nchunk = (la.ng + kWave - 1) / kWave;
+            la.runs = P0.pl.runs[l]; la.R = P0.pl.R[l]; la.h = d.h; la.nframes = B;
+            la.guard_last = l == 1;
+            const long long nw = (long long)B * la.runs * la.nchunk;
+            hipLaunchKernelGGL(k_pyr_level, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st, la);
+        }
+    } else if (!legacy_pyr && use_stream) {
+        const PyrStream& S = P0.ps;
+        PyrStreamArgs pa;
+        pa.src = d_frames; pa.src_fstride = fstride; pa.src_pitch = pitch0;
+        const uintptr_t al = (uintptr_t)d_frames | (uintptr_t)pitch0 | (uintptr_t)(B > 1 ? fstride : 0);
+        pa.load_mode = (al & 15) == 0 ? 16 : ((al & 3) == 0 ? 4 : 1);
+        pa.pyr = P.d_pyr; pa.pyr_fstride = P.pyr_bytes;
+        pa.tab = P0.d_ps_tab;
+        pa.tab_u4 = S.tab_u4; pa.lev_u4 = S.lev_u4; pa.steps_u4 = S.steps_u4; pa.L = L; pa.nsteps = S.nsteps; pa.nchunks = S.nchunks; pa.K0 = S.K0;
+        pa.h0 = P.lv[0].h; pa.w0 = P.lv[0].w; pa.nframes = B;
+        pa.ring0_dw = S.ring_dw[0]; pa.ring0_rows = S.ring_rows[0]; pa.ring0_pitch = S.ring_pitch[0];
+        pa.cnt_dw = S.cnt_dw;
+        hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(1024), S.lds_bytes, st, pa);
+    } else if (!legacy_pyr) {
         for (const PyrGroup& g : P.pgroups) {
             PyrArgs pa;
             if (g.la == 0) {
@@ -2127,6 +2730,7 @@ orbx_handle* orbx_create(const orbx_params* p, int device) {
     orbx_handle* h = new orbx_handle();
     h->prm = *p;
     h->device = device;
+    if (const char* e = std::getenv("ORB_PYR_MODE")) h->pyr_mode = std::min(4, std::max(0, std::atoi(e)));   // A/B runs
     init_tables(h);
     return h;
 }
@@ -2385,6 +2989,15 @@ int orbx_set_profiling(orbx_handle* h, int enable) {
     h->ev_next = 0;
     return ORB_OK;
 }
+
+int orbx_set_pyramid_mode(orbx_handle* h, int mode) {
+    if (!h || mode < 0 || mode > 4) return ORB_ERR_PARAM;
+    h->pyr_mode = mode;
+    h->x_key[4] = -1;                       // the captured single-image graph holds the old choice
+    return ORB_OK;
+}
+
+int orbx_pyramid_kernel(orbx_handle* h) { return h ? h->pyr_last : 0; }
 
 int orbx_set_streams(orbx_handle* h, int nsub) {
     if (!h || nsub < 1 || nsub > 16) return ORB_ERR_PARAM;

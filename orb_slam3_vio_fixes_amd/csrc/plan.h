@@ -38,6 +38,34 @@ struct PyrGroup {
     int lds_a, lds_b, lds_x, lds_y;   // LDS: two level buffers, column taps, row taps
 };
 
+// k_pyr_stream: one workgroup per frame slides down the frame once, keeping
+// a ring of the most recent rows of every level but the last in LDS (no halo
+// recompute, level 0 read once).  Host-side layout of its LDS image.
+constexpr int kPsMaxLevels = 16;
+struct PyrStream {
+    bool ok = false;
+    int K0 = 0, nchunks = 0, nsteps = 0;   // level-0 rows per chunk; chunks; pipeline steps
+    int tab_u4 = 0;                        // table image (uint4 units) = the first bytes of LDS
+    int lev_u4 = 0, steps_u4 = 0;          // level table {rec_dw, yt_dw} [L]; step table [nsteps][L]
+    int lds_bytes = 0;
+    int ring_rows[kPsMaxLevels] = {}, ring_pitch[kPsMaxLevels] = {};   // levels 0..L-2
+    int ring_dw[kPsMaxLevels] = {};        // LDS dword offset of each ring
+    int rec_dw[kPsMaxLevels] = {};         // level l >= 1: column records W[ng] uint4, S[ng] uint4, BF[ng] u32
+    int yt_dw[kPsMaxLevels] = {};          // level l >= 1: row records uint4 per row
+    int ng[kPsMaxLevels] = {};             // column groups of 4 per level
+    int cnt_dw = 0;                        // per-step wave-item counters (LDS dword offset)
+};
+
+// k_pyr_level: one launch per level, a wave per (frame, run of R rows, 64
+// column groups); column records shared with k_pyr_stream's format.
+constexpr int kPlNS = 12;                  // source rows a run may span
+constexpr int kPlRmax = 16;                // output rows per run at most
+struct PyrLevelPlan {
+    bool ok = false;
+    int col_off[kMaxLevels] = {};          // dword offset of level l's column records in d_pcol
+    int R[kMaxLevels] = {}, runs[kMaxLevels] = {};
+};
+
 struct CellDev {
     int level;
     int x0, y0, cols, rows;   // ROI in level coordinates (ORBextractor.cc:807-826)
@@ -54,6 +82,8 @@ struct Plan {
     std::vector<int> xmax;           // per level
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     std::vector<PyrGroup> pgroups;   // k_pyramid launches
+    PyrStream ps;                    // k_pyr_stream layout (ps.ok: usable for this size)
+    PyrLevelPlan pl;                 // k_pyr_level layout
     // device
     uint8_t *d_pyr = nullptr, *d_in = nullptr;
     int2* d_tab = nullptr;
@@ -72,6 +102,8 @@ struct Plan {
     int* d_pxs = nullptr;            // k_pyramid column taps: source column
     uint32_t* d_pxw = nullptr;       //   and weights a0 | a1 << 16
     int2* d_pyt = nullptr;           // k_pyramid row taps: sy0 | sy1 << 16 (clamped), b0 | b1 << 16
+    uint4* d_ps_tab = nullptr;       // k_pyr_stream LDS table image
+    uint32_t* d_pcol = nullptr;      // k_pyr_level column records
     // single-image host path outputs
     orb_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
@@ -82,7 +114,7 @@ struct Plan {
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt};
+                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_pcol};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();
@@ -106,6 +138,8 @@ struct orbx_handle {
     size_t ev_next = 0;
     // sub-batch streams (orbx_set_streams)
     int nsub = 1;
+    // pyramid kernel choice (orbx_set_pyramid_mode) and the last one run
+    int pyr_mode = 0, pyr_last = 0;
     std::vector<hipStream_t> sub_streams;
     std::vector<hipEvent_t> sub_done;
     hipEvent_t fork_ev = nullptr;

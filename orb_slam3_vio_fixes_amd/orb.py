@@ -49,6 +49,15 @@ class ORBextractor:
     def FeaturesPerLevel(self): return self._tab[4].copy()
     def UMax(self): return self._tab[5].copy()
 
+    def set_pyramid_mode(self, mode: int) -> None:
+        """0 auto, 1 row bands (k_pyramid), 2 sliding frame (k_pyr_stream), 3 per-level k_resize,
+        4 per-level runs (k_pyr_level)."""
+        capi.check(capi.lib().orbx_set_pyramid_mode(self._h, mode), "orbx_set_pyramid_mode")
+
+    def pyramid_kernel(self) -> int:
+        """Pyramid kernel of the last extraction: 1 k_pyramid, 2 k_pyr_stream, 3 k_resize, 4 k_pyr_level."""
+        return int(capi.lib().orbx_pyramid_kernel(self._h))
+
     def max_keypoints(self, w: int, h: int) -> int:
         return capi.check(capi.lib().orbx_max_keypoints(self._h, w, h), "orbx_max_keypoints")
 

@@ -178,16 +178,27 @@ def test_extract_batch_threaded_gather_row_steps(gpu_lib):
         same_frame(*out[i], *ref(seq[i], (0, 1000)))
 
 
-@pytest.mark.parametrize("w,h", [(753, 481), (756, 480), (1920, 1080), (320, 240)])
-def test_pyramid_row_load_widths(gpu_lib, w, h):
-    """k_pyramid stages level 0 with 16-byte, 4-byte or 1-byte row loads by
-    the alignment of the caller's frames (row step = width here): every level
-    of every frame equal to the oracle's ComputePyramid, keypoints too."""
+@pytest.mark.parametrize("mode", [1, 2, 3, 4])
+@pytest.mark.parametrize("w,h", [(752, 480), (753, 481), (756, 480), (1920, 1080), (320, 240)])
+def test_pyramid_row_load_widths(gpu_lib, w, h, mode):
+    """k_pyramid / k_pyr_stream stage level 0 with 16-byte, 4-byte or 1-byte
+    row loads by the alignment of the caller's frames (row step = width here):
+    every level of every frame equal to the oracle's ComputePyramid, keypoints
+    too.  mode: 1 row bands, 2 sliding frame (forced on 3 frames), 3 k_resize,
+    4 per-level runs (forced on 3 frames; 4-byte aligned rows only)."""
     import torch
     seq = synth.sequence(w, h, 3, config=2, start=1200)
     ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.set_pyramid_mode(mode)
     kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
     torch.cuda.synchronize()
+    ran = ex.pyramid_kernel()
+    if mode == 2 and (w, h) != (1920, 1080):
+        assert ran == 2, "k_pyr_stream must take every size up to 756 px wide"
+    elif mode == 4 and w % 4 == 0:
+        assert ran == 4, "k_pyr_level must take every 4-byte aligned size"
+    else:
+        assert ran in (mode, 1), ran
     for f in range(len(seq)):
         ref = O.OracleExtractor(1000, 1.2, 8, 20, 7)
         rk, rd, rm = ref(seq[f], (0, 1000))
