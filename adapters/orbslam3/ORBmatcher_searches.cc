@@ -1,0 +1,204 @@
+/**
+ * Drop-in bodies of the ORB_SLAM3::ORBmatcher searches on the Tracking
+ * thread's per-frame path, over the MI355X C ABI (include/orb_mi355x.h):
+ *
+ *   SearchForInitialization(F1, F2, ...)        src/ORBmatcher.cc:648-763
+ *   SearchByBoW(KeyFrame*, Frame&, ...)         src/ORBmatcher.cc:223-425
+ *   SearchByProjection(Frame&, MapPoints, ...)  src/ORBmatcher.cc:43-221
+ *   SearchByProjection(Frame&, const Frame&, ..) src/ORBmatcher.cc:1676-1887
+ *
+ * Delete those four bodies from the reference's src/ORBmatcher.cc and add this
+ * file to the library sources; the class declaration (include/ORBmatcher.h:36-103)
+ * is unchanged.  The adapter reads the map under the reference's own locks
+ * (MapPoint accessors), does the per-point pose math (Sophus) on the host
+ * exactly as the reference writes it, hands flat snapshots to the device, and
+ * writes MapPoint pointers back from the returned indices.
+ *
+ * Not compiled in this repository's container: Frame.h / KeyFrame.h need
+ * Eigen, Sophus, boost and OpenCV, which the image lacks.  The extractor
+ * adapter next to it is compiled (-fsyntax-only) against the reference header
+ * by tests/test_adapter.py; the ABI calls here are those of
+ * tests/native/cpp_api_test.cpp, which runs on the GPU.
+ */
+#include "ORBmatcher.h"
+#include "KeyFrame.h"
+#include "MapPoint.h"
+#include "orb_mi355x.h"
+
+#include <stdexcept>
+#include <vector>
+
+using namespace std;
+
+namespace ORB_SLAM3
+{
+
+namespace
+{
+// A Frame / KeyFrame as the matchers read it (Frame.h:223-290).
+template <class F> orbm_frame view(const F& f)
+{
+    orbm_frame v;
+    v.n = (int32_t)f.mvKeysUn.size();
+    v.kps = reinterpret_cast<const orb_keypoint*>(f.mvKeysUn.data());
+    v.desc = f.mDescriptors.data;
+    v.min_x = f.mnMinX; v.max_x = f.mnMaxX; v.min_y = f.mnMinY; v.max_y = f.mnMaxY;
+    v.grid_inv_w = f.mfGridElementWidthInv;
+    v.grid_inv_h = f.mfGridElementHeightInv;
+    v.u_right = f.mvuRight.empty() ? nullptr : f.mvuRight.data();
+    v.scale_factors = f.mvScaleFactors.data();
+    v.nlevels = (int32_t)f.mvScaleFactors.size();
+    return v;
+}
+
+// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>) as CSR
+struct FeatVecCSR {
+    vector<uint32_t> nodes, idx;
+    vector<int32_t> off;
+    orbm_featvec c;
+    explicit FeatVecCSR(const DBoW2::FeatureVector& fv)
+    {
+        off.push_back(0);
+        for (const auto& kv : fv) {
+            nodes.push_back(kv.first);
+            idx.insert(idx.end(), kv.second.begin(), kv.second.end());
+            off.push_back((int32_t)idx.size());
+        }
+        c.nnodes = (int32_t)nodes.size();
+        c.node_ids = nodes.data();
+        c.offsets = off.data();
+        c.idx = idx.data();
+    }
+};
+
+void check(int rc, const char* what)
+{
+    if (rc < 0) throw std::runtime_error(std::string("ORBmatcher: ") + what + " failed");
+}
+}  // namespace
+
+int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
+                                        vector<int>& vnMatches12, int windowSize)
+{
+    vnMatches12 = vector<int>(F1.mvKeysUn.size(), -1);
+    orbm_frame f1 = view(F1), f2 = view(F2);
+    static_assert(sizeof(cv::Point2f) == 2 * sizeof(float), "Point2f is two floats");
+    const int n = orbm_search_for_initialization(&f1, &f2, reinterpret_cast<float*>(vbPrevMatched.data()),
+                                                 windowSize, mfNNratio, mbCheckOrientation ? 1 : 0,
+                                                 vnMatches12.data());
+    check(n, "SearchForInitialization");
+    return n;   // vbPrevMatched updated in place as :753-756 does
+}
+
+int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPointMatches)
+{
+    const vector<MapPoint*> vpMapPointsKF = pKF->GetMapPointMatches();
+    vpMapPointMatches = vector<MapPoint*>(F.N, static_cast<MapPoint*>(NULL));
+    vector<uint8_t> valid(vpMapPointsKF.size());
+    for (size_t i = 0; i < vpMapPointsKF.size(); ++i)
+        valid[i] = vpMapPointsKF[i] && !vpMapPointsKF[i]->isBad();   // :262-268
+    FeatVecCSR kfv(pKF->mFeatVec), fv(F.mFeatVec);
+    orbm_frame kf = view(*pKF), f = view(F);
+    vector<int32_t> match(F.N, -1);
+    const int n = F.Nleft == -1
+                      ? orbm_search_by_bow(&kf, &kfv.c, valid.data(), &f, &fv.c, mfNNratio,
+                                           mbCheckOrientation ? 1 : 0, match.data())
+                      : orbm_search_by_bow_fisheye(&kf, &kfv.c, valid.data(), &f, &fv.c, F.Nleft, mfNNratio,
+                                                   mbCheckOrientation ? 1 : 0, match.data());
+    check(n, "SearchByBoW");
+    for (int i = 0; i < F.N; ++i)
+        if (match[i] >= 0) vpMapPointMatches[i] = vpMapPointsKF[match[i]];
+    return n;
+}
+
+int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, const float th,
+                                   const bool bFarPoints, const float thFarPoints)
+{
+    if (F.Nleft != -1)
+        throw std::runtime_error("ORBmatcher adapter: use orbm_search_by_projection_mps_fisheye for Nleft != -1");
+    const int n = (int)vpMapPoints.size();
+    // MapPoint snapshot (the fields :50-75 read, under the MapPoint's locks)
+    vector<float> px(n), py(n), pxr(n), vcos(n), depth(n);
+    vector<int32_t> level(n);
+    vector<uint8_t> in_view(n), has_obs(n), desc((size_t)n * 32);
+    for (int i = 0; i < n; ++i) {
+        MapPoint* pMP = vpMapPoints[i];
+        in_view[i] = pMP->mbTrackInView && !pMP->isBad();
+        px[i] = pMP->mTrackProjX; py[i] = pMP->mTrackProjY; pxr[i] = pMP->mTrackProjXR;
+        level[i] = pMP->mnTrackScaleLevel; vcos[i] = pMP->mTrackViewCos; depth[i] = pMP->mTrackDepth;
+        has_obs[i] = pMP->Observations() > 0;
+        if (in_view[i]) {
+            const cv::Mat d = pMP->GetDescriptor();
+            std::copy(d.data, d.data + 32, desc.begin() + (size_t)i * 32);
+        }
+    }
+    orbm_mappoints mps{n, px.data(), py.data(), pxr.data(), level.data(), vcos.data(), depth.data(),
+                       in_view.data(), has_obs.data(), desc.data()};
+    // slots that already hold a MapPoint: opaque owner, blocked when observed (:86-88)
+    vector<int32_t> owner(F.N, -1);
+    vector<uint8_t> blocked(F.N, 0);
+    for (int i = 0; i < F.N; ++i)
+        if (F.mvpMapPoints[i]) { owner[i] = -2; blocked[i] = F.mvpMapPoints[i]->Observations() > 0; }
+    orbm_frame f = view(F);
+    const int nm = orbm_search_by_projection_mps(&f, &mps, th, bFarPoints ? 1 : 0, thFarPoints, mfNNratio,
+                                                 owner.data(), blocked.data());
+    check(nm, "SearchByProjection(F, MapPoints)");
+    for (int i = 0; i < F.N; ++i)
+        if (owner[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[owner[i]];
+    return nm;
+}
+
+int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono)
+{
+    if (CurrentFrame.Nleft != -1)
+        throw std::runtime_error("ORBmatcher adapter: use orbm_search_by_projection_last_fisheye for Nleft != -1");
+    // the pose math of :1686-1720, per last-frame point, unchanged
+    const Sophus::SE3f Tcw = CurrentFrame.GetPose();
+    const Eigen::Vector3f twc = Tcw.inverse().translation();
+    const Sophus::SE3f Tlw = LastFrame.GetPose();
+    const Eigen::Vector3f tlc = Tlw * twc;
+    const bool bForward = tlc(2) > CurrentFrame.mb && !bMono;
+    const bool bBackward = -tlc(2) > CurrentFrame.mb && !bMono;
+
+    const int n = LastFrame.N;
+    vector<uint8_t> valid(n, 0), has_obs(n, 0), desc((size_t)n * 32, 0);
+    vector<float> u(n, 0.f), v(n, 0.f), ur(n, 0.f), angle(n, 0.f);
+    vector<int32_t> octave(n, 0);
+    for (int i = 0; i < n; ++i) {
+        MapPoint* pMP = LastFrame.mvpMapPoints[i];
+        if (!pMP || LastFrame.mvbOutlier[i]) continue;
+        const Eigen::Vector3f x3Dc = Tcw * pMP->GetWorldPos();
+        const float invzc = 1.0 / x3Dc(2);
+        if (invzc < 0) continue;
+        const Eigen::Vector2f uv = CurrentFrame.mpCamera->project(x3Dc);
+        if (uv(0) < CurrentFrame.mnMinX || uv(0) > CurrentFrame.mnMaxX) continue;
+        if (uv(1) < CurrentFrame.mnMinY || uv(1) > CurrentFrame.mnMaxY) continue;
+        valid[i] = 1;
+        u[i] = uv(0); v[i] = uv(1);
+        ur[i] = uv(0) - CurrentFrame.mbf * invzc;   // :1763
+        octave[i] = LastFrame.mvKeys[i].octave;
+        angle[i] = LastFrame.mvKeysUn[i].angle;
+        // a slot this point claims blocks later points iff it is observed (:1747-1749)
+        has_obs[i] = pMP->Observations() > 0;
+        const cv::Mat d = pMP->GetDescriptor();
+        std::copy(d.data, d.data + 32, desc.begin() + (size_t)i * 32);
+    }
+    vector<int32_t> owner(CurrentFrame.N, -1);
+    vector<uint8_t> blocked(CurrentFrame.N, 0);
+    for (int i = 0; i < CurrentFrame.N; ++i)
+        if (CurrentFrame.mvpMapPoints[i]) {
+            owner[i] = -2;
+            blocked[i] = CurrentFrame.mvpMapPoints[i]->Observations() > 0;
+        }
+    orbm_frame cur = view(CurrentFrame);
+    const int mode = bForward ? 1 : (bBackward ? 2 : 0);
+    const int nm = orbm_search_by_projection_last(&cur, n, valid.data(), u.data(), v.data(), ur.data(), octave.data(),
+                                                  angle.data(), has_obs.data(), desc.data(), th, mode,
+                                                  mbCheckOrientation ? 1 : 0, owner.data(), blocked.data());
+    check(nm, "SearchByProjection(F, LastFrame)");
+    for (int i = 0; i < CurrentFrame.N; ++i)
+        if (owner[i] >= 0) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[owner[i]];
+    return nm;
+}
+
+}  // namespace ORB_SLAM3

@@ -1,0 +1,84 @@
+// Declaration-only subset of the OpenCV 4.x API that the reference's
+// include/ORBextractor.h and adapters/orbslam3/ORBextractor.cc use, with
+// OpenCV's own signatures (core/types.hpp, core/mat.hpp, core/hal/interface.h).
+// Test infrastructure for `g++ -fsyntax-only` of the adapter against the
+// reference header only (tests/test_adapter.py): nothing here is defined,
+// linked or run, and it stands in for no part of the reference itself.
+#pragma once
+#include <cstddef>
+#include <vector>
+
+#define CV_8U 0
+#define CV_8UC1 0
+
+namespace cv {
+typedef unsigned char uchar;
+template <typename T> class Point_ {
+public:
+    Point_();
+    Point_(T x, T y);
+    Point_& operator*=(T s);
+    T x, y;
+};
+typedef Point_<int> Point2i;
+typedef Point_<float> Point2f;
+typedef Point2i Point;
+template <typename T> class Size_ {
+public:
+    Size_(T w, T h);
+    T width, height;
+};
+typedef Size_<int> Size;
+
+class KeyPoint {
+public:
+    Point2f pt;
+    float size;
+    float angle;
+    float response;
+    int octave;
+    int class_id;
+};
+
+struct MatStep {
+    size_t operator[](int i) const;
+};
+
+class _OutputArray;
+class Mat {
+public:
+    Mat();
+    Mat(int rows, int cols, int type);
+    Mat(const Mat& m);
+    Mat& operator=(const Mat& m);
+    ~Mat();
+    void create(int rows, int cols, int type);
+    Mat rowRange(int startrow, int endrow) const;
+    Mat row(int y) const;
+    Mat clone() const;
+    void copyTo(const _OutputArray& m) const;
+    void release();
+    bool empty() const;
+    int type() const;
+    int flags, dims, rows, cols;
+    uchar* data;
+    MatStep step;
+};
+
+class _InputArray {
+public:
+    _InputArray(const Mat& m);
+    Mat getMat(int idx = -1) const;
+    bool empty() const;
+};
+class _OutputArray : public _InputArray {
+public:
+    _OutputArray(Mat& m);
+    _OutputArray(const Mat& m);
+    void create(int rows, int cols, int type, int i = -1, bool allowTransposed = false, int fixedDepthMask = 0) const;
+    void release() const;
+    Mat& getMatRef(int i = -1) const;
+};
+typedef const _InputArray& InputArray;
+typedef const _OutputArray& OutputArray;
+}  // namespace cv
