@@ -61,6 +61,14 @@ int device_ordinal()
 }
 }  // namespace
 
+// The device handle of an extractor object: Frame::ComputeStereoMatches
+// passes the left and right extractors' handles to orbs_compute_stereo_matches
+// (INTEGRATION.md §4).
+orbx_handle* ORBextractorDeviceHandle(const ORBextractor* e)
+{
+    return handle_of(e);
+}
+
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
     : nfeatures(_nfeatures), scaleFactor(_scaleFactor), nlevels(_nlevels), iniThFAST(_iniThFAST),
       minThFAST(_minThFAST)
