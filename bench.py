@@ -3,7 +3,7 @@
 
 Metric (BASELINE.json): frames/s ORB extract+match (752x480, 1000 feat),
 keypoints/descriptors bit-exact.  One step = one batch of B distinct
-synthetic 752x480 frames of a panning camera (synth.sequence), resident in
+synthetic 752x480 frames of a panning camera (synth.global_sequence), resident in
 HBM before the timed region:
 ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
 on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
@@ -69,6 +69,7 @@ def parse():
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run SearchForInitialization on the extraction stream (no step overlap)")
     ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
+    ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
     return ap.parse_args()
 
 
@@ -227,8 +228,13 @@ def main():
     dev = torch.device("cuda", local)
     B = args.batch
 
-    # distinct frames per rank (weak scaling), generated once, uploaded before timing
-    frames_np = synth.sequence(W, H, B, config=2, start=rank * B)
+    # distinct frames per rank (weak scaling), generated once, uploaded before
+    # timing.  Seam halo: every rank but the last also
+    # extracts the next rank's first frame, so SearchForInitialization covers
+    # the pair across each shard seam and the job matches all N*B-1 pairs
+    # with no data-path collective; the halo frame is not counted in `value`.
+    Bx = B + (1 if rank < world - 1 else 0)
+    frames_np = synth.global_sequence(W, H, rank * B, Bx, config=2)
     frames = torch.from_numpy(frames_np).to(dev)
     ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local)
     L = capi.lib()
@@ -242,8 +248,8 @@ def main():
     outs_dev = outs
     mstream = torch.cuda.Stream(dev) if args.pipeline else stream
     done = [None, None]                  # match of set i finished (recorded on mstream)
-    matches = torch.empty((B - 1, cap), dtype=torch.int32, device=dev)
-    nmatch = torch.empty(B - 1, dtype=torch.int32, device=dev)
+    matches = torch.empty((Bx - 1, cap), dtype=torch.int32, device=dev)
+    nmatch = torch.empty(Bx - 1, dtype=torch.int32, device=dev)
     inv_w = float(np.float32(64) / np.float32(W))
     inv_h = float(np.float32(48) / np.float32(H))
 
@@ -264,7 +270,7 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(mstream)
         rc = L.orbm_search_for_initialization_batch_device(
-            B, k_.data_ptr(), d_.data_ptr(), n_.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
+            Bx, k_.data_ptr(), d_.data_ptr(), n_.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
             100, 0.9, 1, matches.data_ptr(), nmatch.data_ptr(), mstream.cuda_stream)
         capi.check(rc, "SearchForInitialization batch")
         if timed:
@@ -295,14 +301,21 @@ def main():
         calls = L.orbx_get_profile(ex._h, stage_ms.ctypes.data, len(STAGES))
         L.orbx_set_profiling(ex._h, 0)
         stage_ms /= max(1, calls)
-        frames_per_launch = B * args.steps / max(1, calls)   # each sub-batch range is one launch per stage
+        frames_per_launch = Bx * args.steps / max(1, calls)  # each sub-batch range is one launch per stage
     else:
-        frames_per_launch = B
+        frames_per_launch = Bx
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    if args.dump:
+        # the last step's outputs of this rank, with global frame / pair indices
+        last = outs_dev[(counter[0] - 1) % 2]
+        Path(args.dump).mkdir(parents=True, exist_ok=True)
+        np.savez(Path(args.dump) / f"rank{rank}.npz", first=rank * B, frames=Bx, world=world,
+                 kps=last[0].cpu().numpy(), desc=last[1].cpu().numpy(), n=last[2].cpu().numpy(),
+                 mono=last[3].cpu().numpy(), nmatch=nmatch.cpu().numpy(), matches=matches.cpu().numpy())
     if rank == 0:
         total_frames = B * args.steps * world
         value = total_frames / elapsed

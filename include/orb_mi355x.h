@@ -424,6 +424,13 @@ typedef struct orbv_vocab {
 int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levelsup,
                    int32_t* word_id, double* weight, int32_t* node_id, int device);
 
+/* orbv_transform with the vocabulary and the descriptors resident in HBM:
+ * every array of voc and d_desc / d_word_id / d_weight / d_node_id are
+ * DEVICE pointers (e.g. the vocabulary a multi-GPU job broadcast once over
+ * RCCL, orb_slam3_vio_fixes_amd/sharding.py).  Asynchronous on `stream`. */
+int orbv_transform_device(const orbv_vocab* voc, int n, const uint8_t* d_desc, int levelsup,
+                          int32_t* d_word_id, double* d_weight, int32_t* d_node_id, void* stream);
+
 /* ---------------- mapping matchers ---------------- */
 
 /* ORBmatcher::Fuse(pKF, vpMapPoints, th, bRight = false) (src/ORBmatcher.cc:1148-1331)

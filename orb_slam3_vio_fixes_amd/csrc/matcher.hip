@@ -2609,6 +2609,20 @@ int orbv_transform(const orbv_vocab* voc, int n, const uint8_t* desc, int levels
     return ORB_OK;
 }
 
+int orbv_transform_device(const orbv_vocab* voc, int n, const uint8_t* d_desc, int levelsup, int32_t* d_word_id,
+                          double* d_weight, int32_t* d_node_id, void* stream) {
+    if (!voc || n < 0 || (n && (!d_desc || !d_word_id || !d_weight || !d_node_id))) return ORB_ERR_PARAM;
+    if (!voc->first_child || !voc->nchild || !voc->node_desc || !voc->word_id || !voc->weight) return ORB_ERR_PARAM;
+    if (voc->nnodes < 2) return ORB_ERR_EMPTY;
+    if (n == 0) return ORB_OK;
+    const int nid_level = voc->depth_levels - levelsup;
+    hipLaunchKernelGGL(k_transform, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, voc->first_child,
+                       voc->nchild, voc->child_idx, voc->node_desc, voc->word_id, voc->weight, n, d_desc, nid_level,
+                       d_word_id, d_weight, d_node_id);
+    ORB_CHECK(hipGetLastError());
+    return ORB_OK;
+}
+
 int orbm_fuse(const orbm_frame* kf, const float* inv_level_sigma2, int nmp, const uint8_t* valid, const float* u,
               const float* v, const float* ur, const int32_t* level, const uint8_t* desc, float th, int fma,
               int32_t* best_idx, int32_t* best_dist) {

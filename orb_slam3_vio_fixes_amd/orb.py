@@ -577,6 +577,22 @@ def compute_distinctive_descriptors(off, desc, device: int = 0) -> np.ndarray:
     return best
 
 
+def transform_device(voc_dev, desc, levelsup: int = 4, stream=None):
+    """transform on a vocabulary resident in HBM (voc_dev: abi.Keep of an
+    orbv_vocab holding device pointers, e.g. sharding.vocab_device_struct) for
+    a CUDA uint8 tensor of descriptors: (word_id, weight, node_id) tensors."""
+    import torch
+    assert desc.is_cuda and desc.dtype == torch.uint8 and desc.is_contiguous()
+    n = desc.shape[0]
+    wid = torch.empty(n, dtype=torch.int32, device=desc.device)
+    w = torch.empty(n, dtype=torch.float64, device=desc.device)
+    nid = torch.empty(n, dtype=torch.int32, device=desc.device)
+    st = (stream or torch.cuda.current_stream(desc.device)).cuda_stream
+    capi.check(capi.lib().orbv_transform_device(voc_dev.ref(), n, desc.data_ptr(), levelsup, wid.data_ptr(),
+                                                w.data_ptr(), nid.data_ptr(), st), "orbv_transform_device")
+    return wid, w, nid
+
+
 def transform(voc, desc: np.ndarray, levelsup: int = 4, device: int = 0):
     """TemplatedVocabulary::transform per descriptor on the GPU: (word_id, weight, node_id)."""
     desc = np.ascontiguousarray(desc, np.uint8)

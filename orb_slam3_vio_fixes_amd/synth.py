@@ -116,6 +116,28 @@ def sequence(w: int, h: int, nframes: int, config: int = 2, start: int = 0, step
     return out
 
 
+def global_sequence(w: int, h: int, first: int, nframes: int, config: int = 2, step: float = 3.0,
+                    span: int = 776) -> np.ndarray:
+    """Frames [first, first + nframes) of ONE panning sequence whose frame g
+    depends on g alone, so any partition of the frames over ranks (plus the
+    halo frame a rank extracts across its seam) sees the same images: a fixed
+    seeded canvas, a periodic integer trajectory on it, fresh integer sensor
+    noise seeded by g."""
+    seed = frame_seed(config, 0)
+    rng = np.random.default_rng(seed + 12_000_000)
+    canvas = image(w + span, h + span, seed).astype(np.int16)
+    vx, vy = rng.uniform(0.3, 1.0, 2)
+    norm = max(vx, vy)
+    out = np.empty((nframes, h, w), np.uint8)
+    for i in range(nframes):
+        g = first + i
+        ox = int(round(g * step * vx / norm)) % (span - 4)
+        oy = int(round(g * step * vy / norm)) % (span - 4)
+        noise = np.random.default_rng(seed * 7919 + g).integers(-2, 3, size=(h, w), dtype=np.int16)
+        out[i] = np.clip(canvas[oy:oy + h, ox:ox + w] + noise, 0, 255).astype(np.uint8)
+    return out
+
+
 def vocabulary(k: int = 10, levels: int = 6, seed: int = 5):
     """Synthetic complete k-ary vocabulary of depth ``levels`` (the ORBvoc.txt
     shape is k=10, L=6: 1,111,111 nodes) laid out breadth first (orbv_vocab):

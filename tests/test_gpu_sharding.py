@@ -1,0 +1,61 @@
+"""The sharded product path on the GPU: bench.py under torch.distributed.run
+with 2 ranks (fresh processes sharing the one GPU of the box, gloo backend,
+ORB_BENCH_BACKEND=gloo) against 1 rank with the same total frames.  Every
+frame's keypoints/descriptors and every SearchForInitialization pair --
+including the pair across the shard seam, covered by the halo frame each
+rank but the last extracts -- must equal the 1-rank run."""
+import os
+import socket
+import subprocess
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+B = 12   # frames per rank
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _run(args, env):
+    r = subprocess.run(args, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_two_ranks_equal_one_rank_with_seam_pair(tmp_path):
+    env = dict(os.environ, ORB_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    common = ["--steps", "1", "--warmup", "1", "--cpu-sample", "0", "--no-host-api", "--no-profile"]
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+          "--batch", str(B), "--dump", str(tmp_path / "two")] + common, env)
+    env1 = {k: v for k, v in env.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    _run([sys.executable, "bench.py", "--batch", str(2 * B), "--dump", str(tmp_path / "one")] + common, env1)
+    one = np.load(tmp_path / "one" / "rank0.npz")
+    r0 = np.load(tmp_path / "two" / "rank0.npz")
+    r1 = np.load(tmp_path / "two" / "rank1.npz")
+    assert (int(r0["frames"]), int(r1["frames"])) == (B + 1, B)      # rank 0 carries the halo frame
+    pairs = 0
+    for r in (r0, r1):
+        f0 = int(r["first"])
+        for i in range(int(r["frames"])):
+            g = f0 + i
+            n = int(r["n"][i])
+            assert n == int(one["n"][g]) and int(r["mono"][i]) == int(one["mono"][g])
+            assert np.array_equal(r["kps"][i, :n], one["kps"][g, :n]), g
+            assert np.array_equal(r["desc"][i, :n], one["desc"][g, :n]), g
+        for i in range(int(r["frames"]) - 1):
+            t = f0 + i
+            m = int(one["n"][t])                                         # matches12 has F1.N entries
+            assert int(r["nmatch"][i]) == int(one["nmatch"][t]), t
+            assert np.array_equal(r["matches"][i, :m], one["matches"][t, :m]), t
+            pairs += 1
+    assert pairs == 2 * B - 1            # every consecutive pair of the job, seam included

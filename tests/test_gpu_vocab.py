@@ -34,3 +34,25 @@ def test_text_vocab_transform(gpu_lib, tmp_path, trailing):
     np.testing.assert_array_equal(bw, rw)
     np.testing.assert_array_equal(bv.view(np.uint64), rv.view(np.uint64))
     assert list(fn) == list(rfv)
+
+
+def test_transform_device_resident_vocabulary(gpu_lib):
+    """orbv_transform_device on a vocabulary held as CUDA tensors (the form a
+    multi-GPU job keeps after its one RCCL broadcast, sharding.py) equals the
+    host-API descent and the oracle, for a generated tree (implicit children)."""
+    import torch
+    from orb_slam3_vio_fixes_amd import abi, sharding
+    vh = synth.vocabulary(10, 5, seed=91)
+    vt = {k: torch.from_numpy(np.ascontiguousarray(vh[k])).cuda()
+          for k in ("first_child", "nchild", "node_desc", "word_id", "weight")}
+    vt.update(nnodes=int(vh["nnodes"]), depth_levels=int(vh["depth_levels"]), child_idx=None)
+    img = synth.image(1920, 1080, 5001)
+    _, d, _ = orb.ORBextractor(5000, 1.2, 8, 20, 7)(img, None, (0, 1000))
+    got = orb.transform_device(sharding.vocab_device_struct(vt), torch.from_numpy(d).cuda(), 3)
+    torch.cuda.synchronize()
+    got = [x.cpu().numpy() for x in got]
+    host = orb.transform(abi.vocab_struct(vh), d, 3)
+    ref = O.transform(abi.vocab_struct(vh), d, 3)
+    for a, b, c in zip(got, host, ref):
+        np.testing.assert_array_equal(a, b)
+        np.testing.assert_array_equal(a, c)

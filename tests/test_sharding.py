@@ -36,17 +36,21 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         voc = synth.vocabulary(k=4, levels=4, seed=1) if rank == 0 else None
-        v = sharding.broadcast_vocabulary(voc)
+        v = sharding.broadcast_vocabulary(voc)            # tensors on the ranks' device (CPU here)
         ref = synth.vocabulary(k=4, levels=4, seed=1)
-        same = all(np.array_equal(v[k], ref[k]) for k in ("first_child", "nchild", "node_desc", "word_id", "weight"))
+        keys = ("first_child", "nchild", "node_desc", "word_id", "weight")
+        vh = {k: v[k].numpy().view(np.asarray(ref[k]).dtype) for k in keys}
+        same = all(np.array_equal(vh[k], ref[k]) for k in keys) and v["depth_levels"] == ref["depth_levels"]
+        vh.update(nnodes=v["nnodes"], depth_levels=v["depth_levels"], child_idx=None)
         # query frame from rank 0; keyframes = perturbed copies, sharded by id
         rng = np.random.default_rng(5)
         fk = np.zeros(300, abi.KEYPOINT_DTYPE)
         fk["angle"] = rng.uniform(0, 360, 300)
         fd = rng.integers(0, 256, (300, 32), dtype=np.uint8)
-        k, d = sharding.broadcast_frame(fk if rank == 0 else None, fd if rank == 0 else None)
+        kt, dt = sharding.broadcast_frame(fk if rank == 0 else None, fd if rank == 0 else None)
+        k, d = sharding.keypoints_host(kt), dt.numpy()
         same &= np.array_equal(k.view(np.uint8), fk.view(np.uint8)) and np.array_equal(d, fd)
-        vk = abi.vocab_struct(v)
+        vk = abi.vocab_struct(vh)
         _, _, fnode = O.transform(vk, d, 2)
         res = {}
         for kf in sharding.shard(6, rank, world):

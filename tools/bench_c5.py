@@ -71,16 +71,27 @@ def main():
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    voc = abi.vocab_struct(synth.vocabulary(10, 6, seed=55))
+    dev = torch.device("cuda", local)
     if rank == 0:
         img = synth.image(W, H, 5000)
         ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local)
         k, d, _ = ex(img, None, (0, 1000))
+        vh = synth.vocabulary(10, 6, seed=55)
     else:
-        k = d = None
+        k = d = vh = None
     if world > 1:
-        k, d = sharding.broadcast_frame(k, d, 0, torch.device("cuda", local))
-    _, _, nid = orb.transform(voc, d, 4, device=local)
+        # the vocabulary once, the query per query: RCCL broadcasts into HBM
+        vt = sharding.broadcast_vocabulary(vh, 0, dev)
+        kt, dt = sharding.broadcast_frame(k, d, 0, dev)
+        k = sharding.keypoints_host(kt)
+    else:
+        vt = {key: torch.from_numpy(np.ascontiguousarray(vh[key])).to(dev)
+              for key in ("first_child", "nchild", "node_desc", "word_id", "weight")}
+        vt.update(nnodes=int(vh["nnodes"]), depth_levels=int(vh["depth_levels"]), child_idx=None)
+        dt = torch.from_numpy(np.ascontiguousarray(d)).to(dev)
+    d = dt.cpu().numpy()
+    _, _, nid_t = orb.transform_device(sharding.vocab_device_struct(vt), dt, 4)
+    nid = nid_t.cpu().numpy()
     ids = list(sharding.shard(args.nkf, rank, world))
     t0 = time.perf_counter()
     kfs = make_keyframes(k, d, nid, ids, 7)
