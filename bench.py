@@ -70,7 +70,29 @@ def parse():
                     help="run SearchForInitialization on the extraction stream (no step overlap)")
     ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
     ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
+    ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
+                    help="c2: the headline (this file); c3 stereo, c4 fisheye stereo (tools/bench_stereo.py), "
+                         "c5 map-wide SearchByBoW (tools/bench_c5.py): one JSON line each, with its own roofline")
+    ap.add_argument("--nkf", type=int, default=10000, help="c5: keyframes in the map")
     return ap.parse_args()
+
+
+def other_workload(args):
+    """BASELINE.json configs C3-C5 as their own JSON lines (not the headline)."""
+    import types
+    sys.path.insert(0, str(ROOT / "tools"))
+    batch_given = any(a.startswith("--batch") for a in sys.argv)
+    if args.workload in ("c3", "c4"):
+        import bench_stereo
+        a = types.SimpleNamespace(pairs=args.batch if batch_given else (128 if args.workload == "c3" else 64),
+                                  steps=args.steps, warmup=args.warmup,
+                                  cpu_sample=min(args.cpu_sample, 64 if args.workload == "c3" else 8),
+                                  cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))
+        return bench_stereo.run_c3(a) if args.workload == "c3" else bench_stereo.run_c4(a)
+    import bench_c5
+    a = types.SimpleNamespace(nkf=args.nkf, reps=args.steps, warmup=args.warmup, cpu_sample=min(args.cpu_sample, 200),
+                              cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))
+    return bench_c5.run_c5(a)
 
 
 def pmc_row(path, kernel):
@@ -206,6 +228,11 @@ def host_api_rates(frames_np, reps=200):
 
 def main():
     args = parse()
+    if args.workload != "c2":
+        res = other_workload(args)
+        if res is not None:
+            print(json.dumps(res), flush=True)
+        return
     import torch
     import torch.distributed as dist
     from orb_slam3_vio_fixes_amd import capi, orb, synth

@@ -30,6 +30,8 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tools"))
+import benchlib  # noqa: E402
 
 W, H, NFEAT = 1920, 1080, 5000
 
@@ -59,6 +61,19 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=200)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
+    res = run_c5(args)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+
+
+# algorithmic bytes the map-wide search reads per keyframe feature: its
+# descriptor (32 B), its FeatureVector index (4 B) and its MapPoint flag (1 B)
+KF_FEATURE_BYTES = 37
+
+
+def run_c5(args):
+    """Config C5 (see the module docstring); the JSON object on rank 0, None
+    on the other ranks."""
     import torch
     import torch.distributed as dist
     from oracle import oracle as O
@@ -104,8 +119,13 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    evs = []
     for _ in range(args.reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
         match, nm = m.search_by_bow(k, d, nid, 0.75, True)
+        e1.record()
+        evs.append((e0, e1))
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -115,11 +135,20 @@ def main():
     if world > 1:
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
     el = float(tt.item())
+    kf_feat = int(sum(len(x[0]) for x in kfs))
+    search_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    ach = kf_feat * KF_FEATURE_BYTES / (search_ms * 1e-3) / 1e9
+    roof = {"kernel": "k_bow_init + k_bow + k_bow_final (one map-wide search)", "bound": "hbm", "achieved": ach,
+            "peak": benchlib.HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / benchlib.HBM_PEAK_GBS, "traffic": None,
+            "bytes_per_launch": kf_feat * KF_FEATURE_BYTES, "ms_per_launch": search_ms,
+            "bytes_per_unit": f"{KF_FEATURE_BYTES} B per keyframe feature (descriptor, FeatureVector index, "
+                              "MapPoint flag), rank 0's shard"}
     res = {"metric": "C5 map-wide SearchByBoW: keyframe pairs/s (1920x1080, 5000 feat, 10k-KF map)",
            "value": args.nkf * args.reps / el, "unit": "keyframe-pairs/s", "queries_per_s": args.reps / el,
            "ms_per_query": el / args.reps * 1e3, "n_gpus": world, "nkf": args.nkf, "features": int(len(k)),
            "kf_features_total": int(sum(len(x[0]) for x in kfs)) * world, "data": "synthetic",
-           "map_build_s_rank0": build_s, "mean_matches": float(nm.float().mean().item())}
+           "map_build_s_rank0": build_s, "mean_matches": float(nm.float().mean().item()),
+           "scaling": "strong", "higher_is_better": True, "dtype": "u8", "roofline": roof}
     if rank == 0 and args.cpu_sample > 0:
         ns = min(args.cpu_sample, len(kfs))
         f = abi.frame_struct(k, d, W, H)
@@ -140,10 +169,9 @@ def main():
         res["cpu_baseline"] = {"value": ns / dt, "unit": "keyframe-pairs/s", "cores": args.cpu_threads,
                                "kind": "port", "sample": f"first {ns} keyframes of the map, oracle SearchByBoW"}
         res["parity"] = {"keyframes_checked": ns, "keyframes_mismatched": bad}
-    if rank == 0:
-        print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return res if rank == 0 else None
 
 
 if __name__ == "__main__":

@@ -28,6 +28,8 @@ import numpy as np
 
 ROOT = Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "tools"))
+import benchlib  # noqa: E402
 
 W, H, NFEAT, LAP = 752, 480, 1200, (0, 0)
 FX, BASE = 435.2, 0.11            # EuRoC-like rectified rig
@@ -61,8 +63,11 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-threads", type=int, default=16)
     args = ap.parse_args()
-    if args.workload == "c4":
-        return main_c4(args)
+    print(json.dumps(run_c4(args) if args.workload == "c4" else run_c3(args)), flush=True)
+
+
+def run_c3(args):
+    """Config C3 (see the module docstring); returns the JSON object."""
     import torch
     from orb_slam3_vio_fixes_amd import capi, orb, synth
     dev = torch.device("cuda", 0)
@@ -127,11 +132,14 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    exs = [S["ex"] for S in sets]
+    benchlib.profile_on(exs)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    xst, calls = benchlib.profile_read(exs)
     stage = {"extract_2B_images": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
              "compute_stereo_matches_side_stream": float(np.mean([e[2].elapsed_time(e[3]) for e in ev])),
              "search_for_initialization_side_stream": float(np.mean([e[4].elapsed_time(e[5]) for e in ev]))}
@@ -140,7 +148,8 @@ def main():
            "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
            "config": {"workload": "C3: 752x480 rectified stereo, ORBextractor(1200,1.2,8,20,7), lapping {0,0}, "
                                   "mb 0.11 m, fx 435.2", "pairs_per_step": P},
-           "stage_ms": stage}
+           "stage_ms": stage, "extract_stage_ms": xst,
+           "roofline": benchlib.fast_roofline(sets[0]["ex"], W, H, xst, 2 * P * args.steps / max(1, calls))}
     if args.cpu_sample > 0:
         ns = min(args.cpu_sample, P)
         fps, outs = cpu_baseline(left[:ns], right[:ns], args.cpu_threads)
@@ -156,10 +165,11 @@ def main():
                                "sample": f"first {ns} pairs: oracle extraction of L and R + ComputeStereoMatches"}
         out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad,
                          "matched_fraction": float(np.mean([(o[1][0] >= 0).mean() for o in outs]))}
-    print(json.dumps(out), flush=True)
+    return out
 
 
-def main_c4(args):
+def run_c4(args):
+    """Config C4 (see the module docstring); returns the JSON object."""
     import torch
     from oracle import oracle as O
     from orb_slam3_vio_fixes_amd import orb, synth
@@ -208,18 +218,21 @@ def main_c4(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    benchlib.profile_on([ex])
     t0 = time.perf_counter()
     for _ in range(args.steps):
         idx, dist, l2r = step(timed=True)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    xst, calls = benchlib.profile_read([ex])
     stage = {"extract_2B_images": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
              "fisheye_knn2_ratio_side_stream": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
     out = {"metric": "fisheye stereo pairs/s (512x512 L+R ORB extract, knnMatch(2) + ratio over the lapping areas)",
            "value": P * args.steps / dt, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
            "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
            "config": {"workload": "C4: 512x512 fisheye stereo, ORBextractor(1500,1.2,8,20,7), lapping {0,511}",
-                      "pairs_per_step": P}, "stage_ms": stage}
+                      "pairs_per_step": P}, "stage_ms": stage, "extract_stage_ms": xst,
+           "roofline": benchlib.fast_roofline(ex, w, h, xst, 2 * P * args.steps / max(1, calls))}
     if args.cpu_sample > 0:
         ns = min(args.cpu_sample, P)
         O.lib()
@@ -238,7 +251,7 @@ def main_c4(args):
         out["cpu_baseline"] = {"value": fps, "unit": "pairs/s", "cores": 1, "kind": "port",
                                "sample": f"first {ns} pairs: oracle extraction of L and R + knnMatch(2), one thread"}
         out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad}
-    print(json.dumps(out), flush=True)
+    return out
 
 
 if __name__ == "__main__":
