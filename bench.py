@@ -9,9 +9,11 @@ ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
 on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
 F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
 (Tracking.cc:2459-2492).  Steps are pipelined: the matching of step k runs
-on a second HIP stream while step k+1 extracts into a second output set
-(--no-pipeline serialises them); all K steps' work is inside the timed
-region.  Multi-GPU: one process per GPU, frames sharded
+on a second HIP stream while step k+1 extracts into a second output set,
+started once step k+1's extraction has passed its FAST stage
+(orbx_set_stage_event; --sfi-after) so that it shares the GPU with the
+latency-bound quadtree rather than the VALU-bound FAST pass (--no-pipeline
+serialises them); all K steps' work is inside the timed region.  Multi-GPU: one process per GPU, frames sharded
 (weak scaling, no data-path collective); timing = max over ranks.
 
 Extra objects on the JSON line:
@@ -69,6 +71,9 @@ def parse():
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run SearchForInitialization on the extraction stream (no step overlap)")
     ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
+    ap.add_argument("--sfi-after", type=int, default=2,
+                    help="pipeline: step k's SearchForInitialization waits until step k+1's extraction has passed this "
+                         "stage (orbx_set_stage_event: 1 pyramid, 2 FAST (default), 3 quadtree; -1: starts at once)")
     ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: the headline (this file); c3 stereo, c4 fisheye stereo (tools/bench_stereo.py), "
@@ -283,16 +288,21 @@ def main():
     match_events = []
     counter = [0]
 
-    def step(timed=False):
-        i = counter[0] % 2
-        counter[0] += 1
+    # --sfi-after k: the library records a per-set event when the extraction
+    # passes stage k, and step k's matching is enqueued behind step k+1's
+    # event, so it runs beside the latency-bound later stages, not beside FAST
+    stage_ev = [None, None]
+    if args.pipeline and args.sfi_after >= 0:
+        for j in range(2):
+            stage_ev[j] = torch.cuda.Event()
+            stage_ev[j].record(stream)                  # creates the event
+    pending = []                                        # (set, extracted event) whose match is not enqueued yet
+
+    def match(i, extracted, after=None, timed=False):
         k_, d_, n_, m_ = outs[i]
-        if done[i] is not None:
-            stream.wait_event(done[i])   # the match that read this set has finished
-        ex.extract_batch_device(frames, LAP, out=(k_, d_, n_, m_))
-        extracted = torch.cuda.Event()
-        extracted.record(stream)
         mstream.wait_event(extracted)
+        if after is not None:
+            mstream.wait_event(after)
         if timed:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(mstream)
@@ -306,8 +316,33 @@ def main():
         done[i] = torch.cuda.Event()
         done[i].record(mstream)
 
+    def step(timed=False):
+        i = counter[0] % 2
+        counter[0] += 1
+        k_, d_, n_, m_ = outs[i]
+        if done[i] is not None:
+            stream.wait_event(done[i])   # the match that read this set has finished
+        if stage_ev[i] is not None:
+            capi.check(L.orbx_set_stage_event(ex._h, args.sfi_after, stage_ev[i].cuda_event), "stage event")
+        ex.extract_batch_device(frames, LAP, out=(k_, d_, n_, m_))
+        extracted = torch.cuda.Event()
+        extracted.record(stream)
+        if stage_ev[i] is None:
+            match(i, extracted, timed=timed)
+            return
+        while pending:                                  # the previous step's match, behind this step's stage
+            pi, pev = pending.pop()
+            match(pi, pev, after=stage_ev[i], timed=timed)
+        pending.append((i, extracted))
+
+    def flush(timed=False):
+        while pending:
+            pi, pev = pending.pop()
+            match(pi, pev, timed=timed)
+
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -318,6 +353,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=prof)
+    flush(timed=prof)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -366,7 +402,9 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
-                          "frames_per_step_per_gpu": B, "streams": args.streams, "pipeline": args.pipeline, "parallelism": f"frames sharded over {world} GPU(s)"},
+                          "frames_per_step_per_gpu": B, "streams": args.streams, "pipeline": args.pipeline,
+                          "sfi_after_stage": args.sfi_after if args.pipeline else None,
+                          "parallelism": f"frames sharded over {world} GPU(s), halo frame per seam"},
                "stage_ms": {**{k: float(v) for k, v in zip(STAGES, stage_ms)},
                             "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
                                                           if match_events else None)},

@@ -176,6 +176,15 @@ int orbx_set_streams(orbx_handle* h, int nsub);
 int orbx_set_pyramid_mode(orbx_handle* h, int mode);
 int orbx_pyramid_kernel(orbx_handle* h);
 
+/* Pipeline control for work overlapped with extraction: subsequent
+ * extractions on the handle record `event` (a hipEvent_t, NULL = none) on
+ * their stream when stage `stage` ends: 0 start, 1 pyramid, 2 FAST cells,
+ * 3 quadtree, 4 describe, 5 assemble (with sub-batch streams, after each
+ * range).  A caller can thus start other work on another stream once the
+ * extraction's VALU-heavy stages are done.  Not part of the reference
+ * interface. */
+int orbx_set_stage_event(orbx_handle* h, int stage, void* event);
+
 /* ---------------- stereo ---------------- */
 
 /* Frame::ComputeStereoMatches (src/Frame.cc:811-981) for one rectified pair:

@@ -26,6 +26,7 @@ EXPORTS = [
     "orbm_search_by_bow_kf", "orbm_search_by_projection_kf", "orbm_search_by_projection_sim3",
     "orbm_search_by_sim3", "orbm_fuse_sim3", "orbm_search_by_bow_fisheye", "orbm_search_by_projection_mps_fisheye",
     "orbm_search_by_projection_last_fisheye", "orbx_set_pyramid_mode", "orbx_pyramid_kernel", "orbv_transform_device",
+    "orbx_set_stage_event",
 ]
 
 _lib = None
@@ -63,6 +64,7 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_set_pyramid_mode.argtypes = [vp, i32]
     L.orbx_pyramid_kernel.argtypes = [vp]
     L.orbv_transform_device.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
+    L.orbx_set_stage_event.argtypes = [vp, i32, vp]
     L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]
     L.orbm_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
     L.orbm_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]

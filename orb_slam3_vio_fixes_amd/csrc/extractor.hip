@@ -2533,7 +2533,11 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     d_n += F;
     d_mono += F;
     std::vector<hipEvent_t> marks;
+    int stage_no = 0;
     auto mark = [&]() {
+        // caller's pipeline events (orbx_set_stage_event): recorded after stage k
+        hipEvent_t ue = hd->stage_ev[std::min(stage_no++, 5)];
+        if (ue) (void)hipEventRecord(ue, st);
         if (!hd->profiling) return;
         if (hd->ev_next >= hd->ev_pool.size()) {
             hipEvent_t e;
@@ -2998,6 +3002,13 @@ int orbx_set_pyramid_mode(orbx_handle* h, int mode) {
 }
 
 int orbx_pyramid_kernel(orbx_handle* h) { return h ? h->pyr_last : 0; }
+
+int orbx_set_stage_event(orbx_handle* h, int stage, void* event) {
+    if (!h || stage < 0 || stage > 5) return ORB_ERR_PARAM;
+    h->stage_ev[stage] = (hipEvent_t)event;
+    h->x_key[4] = -1;                       // a captured single-image graph holds the old events
+    return ORB_OK;
+}
 
 int orbx_set_streams(orbx_handle* h, int nsub) {
     if (!h || nsub < 1 || nsub > 16) return ORB_ERR_PARAM;

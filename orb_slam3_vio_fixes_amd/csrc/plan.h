@@ -140,6 +140,8 @@ struct orbx_handle {
     int nsub = 1;
     // pyramid kernel choice (orbx_set_pyramid_mode) and the last one run
     int pyr_mode = 0, pyr_last = 0;
+    // caller events recorded after pipeline stages (orbx_set_stage_event)
+    hipEvent_t stage_ev[6] = {};
     std::vector<hipStream_t> sub_streams;
     std::vector<hipEvent_t> sub_done;
     hipEvent_t fork_ev = nullptr;
