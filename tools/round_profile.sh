@@ -12,5 +12,6 @@ tail -2 "$out/gpu_tests.log"
 timeout -k 10 600 python bench.py > "$out/bench.json" 2> "$out/bench.err" || { echo "bench failed"; tail -20 "$out/bench.err"; exit 1; }
 cat "$out/bench.json"
 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o run -- python3 bench.py > "$out/bench_under_rocprof.json" 2> "$out/rocprof.err" || { echo "rocprof failed"; tail -20 "$out/rocprof.err"; exit 1; }
+python tools/kstats.py "$out/trace/run_kernel_trace.csv" --csv "$out/kernel_stats_by_grid.csv" > "$out/kernel_stats_by_grid.txt"
 tools/pmc_profile.sh "$out/pmc" && python tools/pmc_summary.py "$out/pmc" --csv "$out/pmc_summary.csv" > "$out/pmc_summary.txt"
 echo done
