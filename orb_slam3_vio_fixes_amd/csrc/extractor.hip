@@ -1999,12 +1999,19 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 // the IC_Angle disc (radius 15) from it, blurs the 37x37 centre with the same
 // fixed-point separable kernel and evaluates the 256 tests on
 // it: the blurred level never goes to HBM.  Lane l evaluates tests 4l..4l+3.
+// The horizontal pass is stored column-major, so a sample's 7 vertical taps
+// are 7 consecutive u16: two ds_read2_b32 and four v_dot2 per sample instead
+// of 7 scattered u16 reads (54 % bank-conflict cycles in round 1; the kernel
+// time did not change: it is VALU/latency-bound).
 // ---------------------------------------------------------------------------
-constexpr int kRaw = 43, kRawP = 48, kBl = 37, kHbP = 42;
+constexpr int kRaw = 43, kRawP = 48, kBl = 37;
+// column-major horizontal-pass buffer: hbT[col][row], a column's 43 rows plus
+// pad (u16 units; 22 dwords per column)
+constexpr int kHbT = 44;
 #ifndef ORB_DESC_SLOTS
 #define ORB_DESC_SLOTS 16
 #endif
-constexpr int kDescSlots = ORB_DESC_SLOTS;   // keypoint slots per wave   // hb pitch: 21 dwords (odd: conflict-free row stores)
+constexpr int kDescSlots = ORB_DESC_SLOTS;   // keypoint slots per wave
 
 struct DescArgs {
     const uint8_t* in;
@@ -2158,7 +2165,7 @@ extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WAVES))) void k_describe(DescArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
-    __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][kRaw * kHbP];
+    __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][(kBl + 1) * kHbT];
     const int lane = lane_id(), wv = wave_id();
     // lane's 4 tests = 16 consecutive pattern bytes, kept packed in registers
     const uint4 patv = ((const uint4*)c_pattern)[lane];
@@ -2170,6 +2177,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     uint16_t* hb = hb_s[wv];
     // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
     const uint32_t k0 = a.kern[0], k1 = a.kern[1], k2 = a.kern[2], k3 = a.kern[3];
+    // u16 weight pairs of the vertical taps v0..v6 over 4 dwords, for a first
+    // tap at an even index (v0v1 v2v3 v4v5 v6-) or an odd one (-v0 v1v2 v3v4 v5v6)
+    const uint32_t W0e = k0 | (k1 << 16), W1e = k2 | (k3 << 16), W2e = k2 | (k1 << 16), W3e = k0;
+    const uint32_t W0o = k0 << 16, W1o = k1 | (k2 << 16), W2o = k3 | (k2 << 16), W3o = k1 | (k0 << 16);
     // umax in SGPRs: a lane-indexed a.umax[v] compiles to a vector load from
     // the kernarg segment whose vmcnt wait would also drain the patch prefetch
     int um_s[kHalfPatch + 1];
@@ -2289,7 +2300,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             glibc_sincosf(deg_to_rad(ang_deg), &sb, &ca);
             const u16x2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
             const u16x2 K2 = {(unsigned short)k2, (unsigned short)k2}, K3 = {(unsigned short)k3, (unsigned short)k3};
-            uint32_t* orow = (uint32_t*)(hb + rr * kHbP);
             // E(k) = (p[2k], p[2k+1]), O(k) = (p[2k+1], p[2k+2]); two halves of
             // the row keep at most ~26 pairs live
             auto Ep = [&](int k) {
@@ -2310,7 +2320,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                 for (int m = 0; m < mhi - mlo; ++m) {
                     const u16x2 h = K0 * (E[m] + E[m + 3]) + K1 * (O[m] + O[m + 2]) + K2 * (E[m + 1] + E[m + 2]) +
                                     K3 * O[m + 1];
-                    orow[mlo + m] = as_u32(h);
+                    // columns 2(mlo+m) and 2(mlo+m)+1 of this row (the last pair's
+                    // second column, 37, lands in the pad)
+                    hb[(2 * (mlo + m)) * kHbT + rr] = h.x;
+                    hb[(2 * (mlo + m) + 1) * kHbT + rr] = h.y;
                 }
             };
             half(std::integral_constant<int, 0>{}, std::integral_constant<int, 10>{});
@@ -2333,9 +2346,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                 const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
                 int r, c;
                 brief_offset(x, y, sb, ca, a.fma, r, c);
-                const uint16_t* col = hb + (18 + r) * kHbP + 18 + c;
-                const uint32_t acc = k0 * ((uint32_t)col[0] + col[6 * kHbP]) + k1 * ((uint32_t)col[kHbP] + col[5 * kHbP]) +
-                                     k2 * ((uint32_t)col[2 * kHbP] + col[4 * kHbP]) + k3 * (uint32_t)col[3 * kHbP];
+                // the 7 vertical taps are rows 18+r .. 24+r of column 18+c:
+                // contiguous u16, inside the 4 dwords from the even index at or
+                // below the first; the dot2 weight pairs follow its parity
+                const int s0 = (18 + c) * kHbT + 18 + r;
+                const uint32_t* dw = (const uint32_t*)hb + (s0 >> 1);
+                const uint32_t D0 = dw[0], D1 = dw[1], D2 = dw[2], D3 = dw[3];
+                const bool odd = s0 & 1;
+                const uint32_t acc = __builtin_amdgcn_udot2(
+                    as_u16x2(D3), as_u16x2(odd ? W3o : W3e),
+                    __builtin_amdgcn_udot2(
+                        as_u16x2(D2), as_u16x2(odd ? W2o : W2e),
+                        __builtin_amdgcn_udot2(as_u16x2(D1), as_u16x2(odd ? W1o : W1e),
+                                               __builtin_amdgcn_udot2(as_u16x2(D0), as_u16x2(odd ? W0o : W0e), 0u,
+                                                                      false),
+                                               false),
+                        false),
+                    false);
                 val[e] = (int)min(255u, (acc + 32768u) >> 16);   // saturate_cast<uchar>
             }
             nib |= (val[0] < val[1]) << q;
