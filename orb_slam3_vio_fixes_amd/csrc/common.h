@@ -52,6 +52,19 @@ __device__ __forceinline__ T wave_min(T v, T id) {
     return __builtin_bit_cast(T, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), kWave - 1));
 }
 
+// Wave-wide sum by the same DPP steps as wave_min (identity 0 for the lanes a
+// broadcast does not write): six dependent VALU ops instead of six
+// ds_bpermute round trips through the LDS unit.
+__device__ __forceinline__ int wave_sum_dpp(int v) {
+    v += dpp_mov<0xb1, 0xf>(v, 0);    // quad_perm [1,0,3,2]
+    v += dpp_mov<0x4e, 0xf>(v, 0);    // quad_perm [2,3,0,1]
+    v += dpp_mov<0x124, 0xf>(v, 0);   // row_ror:4
+    v += dpp_mov<0x128, 0xf>(v, 0);   // row_ror:8
+    v += dpp_mov<0x142, 0xa>(v, 0);   // row_bcast:15 -> rows 1, 3
+    v += dpp_mov<0x143, 0xc>(v, 0);   // row_bcast:31 -> rows 2, 3
+    return __builtin_amdgcn_readlane(v, kWave - 1);
+}
+
 // Position of this lane among the set bits of `mask` below it.
 __device__ __forceinline__ int mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));

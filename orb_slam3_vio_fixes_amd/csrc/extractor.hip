@@ -1274,7 +1274,11 @@ __device__ __forceinline__ uint64_t item_byte_mask(int s, int e) {
 }
 
 __device__ __forceinline__ uint32_t lo_bytes(uint32_t x) { return x & 0x00ff00ffu; }
-__device__ __forceinline__ uint32_t hi_bytes(uint32_t x) { return (x >> 8) & 0x00ff00ffu; }
+// u16 pair (x.b1, x.b3) in one v_perm (a shift and a mask otherwise)
+__device__ __forceinline__ uint32_t hi_bytes(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); }
+// u16 pair of bytes (hi.bs1 | lo.bs0 selectors 0-3: lo, 4-7: hi) in one v_perm
+template <uint32_t SEL>
+__device__ __forceinline__ uint32_t pair_bytes(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_perm(hi, lo, SEL); }
 constexpr int kCandIdx = 0x3fff, kCandBright = 0x4000, kCandDark = 0x8000;
 
 #ifdef ORB_FAST_TIMING
@@ -1447,13 +1451,18 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     const uint32_t cm = row[-1], c0 = row[0], c1 = row[1], c2 = row[2];
                     const uint32_t u0 = row[-3 * rs4], u1 = row[1 - 3 * rs4];
                     const uint32_t d0 = row[3 * rs4], d1 = row[1 + 3 * rs4];
-                    const uint32_t lf0 = __builtin_amdgcn_alignbyte(c0, cm, 1), rt0 = __builtin_amdgcn_alignbyte(c1, c0, 3);
-                    const uint32_t lf1 = __builtin_amdgcn_alignbyte(c1, c0, 1), rt1 = __builtin_amdgcn_alignbyte(c2, c1, 3);
+                    // u16 pairs of the pixels 3 left / 3 right of pixels (0, 2) and
+                    // (1, 3) of dwords c0, c1: one v_perm each, four shared with C
+                    const uint32_t c0l = lo_bytes(c0), c0h = hi_bytes(c0), c1l = lo_bytes(c1), c1h = hi_bytes(c1);
+                    const uint32_t lf0l = hi_bytes(cm), lf0h = pair_bytes<0x0c040c02u>(c0, cm);
+                    const uint32_t rt0l = pair_bytes<0x0c050c03u>(c1, c0), rt0h = c1l;
+                    const uint32_t lf1l = c0h, lf1h = pair_bytes<0x0c040c02u>(c1, c0);
+                    const uint32_t rt1l = pair_bytes<0x0c050c03u>(c2, c1), rt1h = lo_bytes(c2);
                     uint32_t b0, k0, b1, k1, b2, k2, b3, k3;
-                    compass_signs(lo_bytes(c0), lo_bytes(u0), lo_bytes(d0), lo_bytes(lf0), lo_bytes(rt0), tt, b0, k0);
-                    compass_signs(hi_bytes(c0), hi_bytes(u0), hi_bytes(d0), hi_bytes(lf0), hi_bytes(rt0), tt, b1, k1);
-                    compass_signs(lo_bytes(c1), lo_bytes(u1), lo_bytes(d1), lo_bytes(lf1), lo_bytes(rt1), tt, b2, k2);
-                    compass_signs(hi_bytes(c1), hi_bytes(u1), hi_bytes(d1), hi_bytes(lf1), hi_bytes(rt1), tt, b3, k3);
+                    compass_signs(c0l, lo_bytes(u0), lo_bytes(d0), lf0l, rt0l, tt, b0, k0);
+                    compass_signs(c0h, hi_bytes(u0), hi_bytes(d0), lf0h, rt0h, tt, b1, k1);
+                    compass_signs(c1l, lo_bytes(u1), lo_bytes(d1), lf1l, rt1l, tt, b2, k2);
+                    compass_signs(c1h, hi_bytes(u1), hi_bytes(d1), lf1h, rt1h, tt, b3, k3);
                     const uint64_t vm = k == 0 ? m_first : (k == ndp - 1 ? m_last : 0x8080808080808080ull);
                     const uint32_t vl = (uint32_t)vm, vh = (uint32_t)(vm >> 32);
                     bl = sign_bytes(b0, b1) & vl;
@@ -2294,8 +2303,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                 m10 = (int)sw - kHalfPatch * (int)s1;
                 m01 = (lane - 21) * (int)s1;
             }
-            m10 = wave_sum(m10);
-            m01 = wave_sum(m01);
+            m10 = wave_sum_dpp(m10);
+            m01 = wave_sum_dpp(m01);
             ang_deg = fast_atan2_deg((float)m01, (float)m10);
             glibc_sincosf(deg_to_rad(ang_deg), &sb, &ca);
             const u16x2 K0 = {(unsigned short)k0, (unsigned short)k0}, K1 = {(unsigned short)k1, (unsigned short)k1};
@@ -2661,10 +2670,9 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max + fa.kmask_bytes);
     fa.nframes = B;
     const int nv = (P.roi_dwords + kWave - 1) / kWave;
+    void (*kfast)(FastArgs) = nv <= 12 ? k_fast_cells<12> : (nv <= 24 ? k_fast_cells<24> : k_fast_cells<48>);
     const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
-    if (nv <= 12) hipLaunchKernelGGL(k_fast_cells<12>, fgrid, dim3(256), flds, st, fa);
-    else if (nv <= 24) hipLaunchKernelGGL(k_fast_cells<24>, fgrid, dim3(256), flds, st, fa);
-    else hipLaunchKernelGGL(k_fast_cells<48>, fgrid, dim3(256), flds, st, fa);
+    hipLaunchKernelGGL(kfast, fgrid, dim3(256), flds, st, fa);
     mark();
     // quadtree
     QtArgs qa;
