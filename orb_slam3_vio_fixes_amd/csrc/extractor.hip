@@ -543,6 +543,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
                 P.roi_max = std::max(P.roi_max, c.rows * ((c.cols + 6) & ~3) + 16);
                 P.roi_dwords = std::max(P.roi_dwords, c.rows * (((c.x0 & 3) + c.cols + 3) >> 2));
                 P.win_max = std::max(P.win_max, (std::max(0, c.cols - 6) + 2) * (std::max(0, c.rows - 6) + 2));
+                P.win_pix_max = std::max(P.win_pix_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
                 ++nc;
             }
         }
@@ -1173,6 +1174,7 @@ struct FastArgs {
     int ini_th, min_th;
     int roi_max, win_max;   // LDS per wave
     int kmask_bytes;
+    int cand_bytes;         // u16 candidate list, one entry per window pixel at most
 };
 
 // Arc strength of one direction on the raw ring values: max over the 16 arcs
@@ -1180,16 +1182,30 @@ struct FastArgs {
 // min x) or 0xff (darker ring: 255 - the arc's max x).  With d = v - x,
 // cv::FAST's score is max(A, B) - 1 for B = strength(0) - v and
 // A = strength(0xff) - (255 - v).
+// v_min3 / v_max3 by hand: the shared pairwise minima of the arc windows keep
+// the compiler from forming them (it emitted 45 two-input v_min per score)
+__device__ __forceinline__ int vmin3(int a, int b, int c) {
+    int d;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ int vmax3(int a, int b, int c) {
+    int d;
+    asm("v_max3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 __device__ __forceinline__ int arc_strength(const int (&x)[16], int m) {
-    int w[16], w3[16];
+    int w[16], w3[16], a9[16];
 #pragma unroll
     for (int k = 0; k < 16; ++k) w[k] = x[k] ^ m;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) w3[k] = min(w[k], min(w[(k + 1) & 15], w[(k + 2) & 15]));
-    int a = 0;
+    for (int k = 0; k < 16; ++k) w3[k] = vmin3(w[k], w[(k + 1) & 15], w[(k + 2) & 15]);
 #pragma unroll
-    for (int k = 0; k < 16; ++k) a = max(a, min(w3[k], min(w3[(k + 3) & 15], w3[(k + 6) & 15])));
-    return a;
+    for (int k = 0; k < 16; ++k) a9[k] = vmin3(w3[k], w3[(k + 3) & 15], w3[(k + 6) & 15]);
+    int a = vmax3(a9[0], a9[1], a9[2]);
+#pragma unroll
+    for (int k = 3; k < 15; k += 2) a = vmax3(a, a9[k], a9[k + 1]);
+    return max(a, a9[15]);
 }
 
 __device__ __forceinline__ void fast_ring(const uint8_t* roi, int stride, int r, int c, int& v, int (&x)[16]) {
@@ -1319,6 +1335,12 @@ __device__ __forceinline__ int div_row(int i, float inv_ww) { return (int)(((flo
 #define ORB_FAST_CELLS_PER_WAVE 4
 #endif
 constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
+#ifndef ORB_FAST_PRE2
+#define ORB_FAST_PRE2 0
+#endif
+#ifndef ORB_FAST_ABL
+#define ORB_FAST_ABL 0   // timing ablations (tools only; wrong results): 1 scores, 2 compaction, 3 compass
+#endif
 
 struct RoiFetch {
     const uint8_t* src;
@@ -1348,10 +1370,10 @@ template <int NV>
 __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
-    uint8_t* roi = smem + wv * (a.roi_max + a.win_max * 3 + a.kmask_bytes);   // multiples of 16
+    uint8_t* roi = smem + wv * (a.roi_max + a.win_max + a.cand_bytes + a.kmask_bytes);   // multiples of 16
     uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
-    uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_max entries
-    uint64_t* kmask = (uint64_t*)(sc + 3 * a.win_max);        // NMS ballots, one per 64 candidates
+    uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_pix_max entries
+    uint64_t* kmask = (uint64_t*)(sc + a.win_max + a.cand_bytes);   // NMS ballots, one per 64 candidates
 #ifdef ORB_FAST_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
@@ -1439,10 +1461,10 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             //    loop over the set bits instead of visiting all four bytes)
             const u16x2 tt = {(unsigned short)t, (unsigned short)t};
             ncand = 0;
-            for (int base = 0; base < nitems; base += kWave) {
-                const int it = base + lane;
-                uint32_t bl = 0, bh = 0, dl = 0, dh = 0;     // flag bytes, byte k = item pixel k
-                int idx0 = 0;
+            // one item: flag bytes (byte k = item pixel k) and its window index
+            auto pretest = [&](int it, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh, int& idx0) {
+                bl = bh = dl = dh = 0;
+                idx0 = 0;
                 if (it < nitems) {
                     const int r = div_row(it, inv_ndp);
                     const int k = it - (int)__umul24(r, ndp);
@@ -1459,10 +1481,16 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     const uint32_t lf1l = c0h, lf1h = pair_bytes<0x0c040c02u>(c1, c0);
                     const uint32_t rt1l = pair_bytes<0x0c050c03u>(c2, c1), rt1h = lo_bytes(c2);
                     uint32_t b0, k0, b1, k1, b2, k2, b3, k3;
+#if ORB_FAST_ABL == 3
+                    // ablation: one compass evaluation stands in for all four (timing only)
+                    compass_signs(c0l, lo_bytes(u0), lo_bytes(d0), lf0l, rt0l, tt, b0, k0);
+                    b1 = b2 = b3 = b0; k1 = k2 = k3 = k0;
+#else
                     compass_signs(c0l, lo_bytes(u0), lo_bytes(d0), lf0l, rt0l, tt, b0, k0);
                     compass_signs(c0h, hi_bytes(u0), hi_bytes(d0), lf0h, rt0h, tt, b1, k1);
                     compass_signs(c1l, lo_bytes(u1), lo_bytes(d1), lf1l, rt1l, tt, b2, k2);
                     compass_signs(c1h, hi_bytes(u1), hi_bytes(d1), lf1h, rt1h, tt, b3, k3);
+#endif
                     const uint64_t vm = k == 0 ? m_first : (k == ndp - 1 ? m_last : 0x8080808080808080ull);
                     const uint32_t vl = (uint32_t)vm, vh = (uint32_t)(vm >> 32);
                     bl = sign_bytes(b0, b1) & vl;
@@ -1471,6 +1499,9 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     dh = sign_bytes(k2, k3) & vh;
                     idx0 = (int)__umul24(r, ww) + 4 * j - X0;
                 }
+            };
+            // candidates of one item per lane, appended in row-major order
+            auto emit = [&](uint32_t bl, uint32_t bh, uint32_t dl, uint32_t dh, int idx0) {
                 uint32_t pl = bl | dl, ph = bh | dh;
                 const int pc = __popc(pl) + __popc(ph);
                 // lane-exclusive prefixes of the per-lane counts (<= 8) by bit ballots
@@ -1478,6 +1509,10 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                                q3 = __ballot(pc & 8);
                 const int tot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2) + 8 * __popcll(q3);
                 int pos = ncand + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2) + 8 * mask_rank(q3);
+#if ORB_FAST_ABL == 2
+                pl = ph = 0;   // ablation: no candidate writes (timing only)
+                if (pc) cand[pos] = (uint16_t)idx0;
+#endif
                 while (pl) {
                     const int bb = __builtin_ctz(pl);
                     pl &= pl - 1;
@@ -1491,7 +1526,26 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     cand[pos++] = (uint16_t)((uint32_t)(idx0 + 4 + (bb >> 3)) | fl);
                 }
                 ncand += tot;
+            };
+#if ORB_FAST_PRE2
+            // two items per lane per round: both items' LDS reads and compass
+            // chains in flight together
+            for (int base = 0; base < nitems; base += 2 * kWave) {
+                uint32_t bl, bh, dl, dh, bl2, bh2, dl2, dh2;
+                int i0, i2;
+                pretest(base + lane, bl, bh, dl, dh, i0);
+                pretest(base + kWave + lane, bl2, bh2, dl2, dh2, i2);
+                emit(bl, bh, dl, dh, i0);
+                emit(bl2, bh2, dl2, dh2, i2);
             }
+#else
+            for (int base = 0; base < nitems; base += kWave) {
+                uint32_t bl, bh, dl, dh;
+                int i0;
+                pretest(base + lane, bl, bh, dl, dh, i0);
+                emit(bl, bh, dl, dh, i0);
+            }
+#endif
             fast_wave_sync();
             if (pass == 0) FAST_T(1); else FAST_T(5);
             // 2. FAST score of the candidates (the dark direction too for the rare
@@ -1499,10 +1553,14 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             for (int q = lane; q < ncand; q += kWave) {
                 const int e = cand[q], i = e & kCandIdx;
                 const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+#if ORB_FAST_ABL == 1
+                int sv = (e * 37) & 63;   // ablation: no ring reads / arc scores (timing only)
+#else
                 int v, x[16];
                 fast_ring(R, rstride, r + 3, cc + 3, v, x);
                 int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
                 if ((e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
+#endif
                 sc[(r + 1) * sp + cc + 1] = (uint8_t)max(sv, 0);
             }
             fast_wave_sync();
@@ -2666,8 +2724,9 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
     fa.roi_max = (P.roi_max + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
-    fa.kmask_bytes = ((fa.win_max + kWave - 1) / kWave * 8 + 15) & ~15;
-    const size_t flds = 4 * (size_t)(fa.roi_max + 3 * fa.win_max + fa.kmask_bytes);
+    fa.kmask_bytes = ((P0.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
+    fa.cand_bytes = (2 * P0.win_pix_max + 15) & ~15;
+    const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes);
     fa.nframes = B;
     const int nv = (P.roi_dwords + kWave - 1) / kWave;
     void (*kfast)(FastArgs) = nv <= 12 ? k_fast_cells<12> : (nv <= 24 ? k_fast_cells<24> : k_fast_cells<48>);
