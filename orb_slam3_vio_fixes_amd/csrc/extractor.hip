@@ -1338,6 +1338,9 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #ifndef ORB_FAST_PRE2
 #define ORB_FAST_PRE2 0
 #endif
+#ifndef ORB_QT_LEVEL_MAJOR
+#define ORB_QT_LEVEL_MAJOR 1
+#endif
 #ifndef ORB_FAST_ABL
 #define ORB_FAST_ABL 0   // timing ablations (tools only; wrong results): 1 scores, 2 compaction, 3 compass
 #endif
@@ -1898,7 +1901,12 @@ __device__ void qt_count(QtLds& s, int cur, int size, const int K, const uint32_
 
 __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+#if ORB_QT_LEVEL_MAJOR
+    // grid (frames, levels): every frame's level 0 (the largest trees) dispatches first
+    const int l = blockIdx.y, f = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
+#else
     const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
+#endif
     const LevelDev lv = a.lv[l];
     const int NC = a.ncap;
     QtLds s;
@@ -2740,7 +2748,11 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     qa.ncells_total = P.ncells; qa.slot_total = P.slot_total;
     qa.qt_key = P.d_qt_key; qa.qt_n = P.d_qt_n; qa.out_total = P.out_total; qa.L = L;
     qa.ncap = P.max_out_cap + 8;
+#if ORB_QT_LEVEL_MAJOR
+    hipLaunchKernelGGL(k_quadtree, dim3(B, L), dim3(256), qt_lds_bytes(P), st, qa);
+#else
     hipLaunchKernelGGL(k_quadtree, dim3(L, B), dim3(256), qt_lds_bytes(P), st, qa);
+#endif
     mark();
     // describe
     DescArgs da;
