@@ -2086,6 +2086,9 @@ constexpr int kHbT = 44;
 #ifndef ORB_DESC_SLOTS
 #define ORB_DESC_SLOTS 16
 #endif
+#ifndef ORB_DESC_ABL
+#define ORB_DESC_ABL 0   // timing ablation (tools only; wrong results): 1 = every patch load hits one L2-resident patch
+#endif
 constexpr int kDescSlots = ORB_DESC_SLOTS;   // keypoint slots per wave
 
 struct DescArgs {
@@ -2184,7 +2187,11 @@ __device__ __forceinline__ void patch_issue(const uint8_t* img, int pitch, int x
         const int i = lane + j * kWave;
         if (i < kPN) {
             const int r = i / kPDw, d = i - r * kPDw;
+#if ORB_DESC_ABL == 1
+            v[j] = *(GlobalWords)(g + (long long)r * pitch + 4 * d);   // ablation: one L2-resident patch (timing only)
+#else
             v[j] = *(GlobalWords)(g + (long long)(y0 + r) * pitch + base + 4 * d);
+#endif
         }
     }
 }
