@@ -1390,14 +1390,14 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     const ConstLevels lvc = (ConstLevels)a.lv;
     const ConstCells cells = (ConstCells)a.cells;
     auto cell_at = [&](int it) {
-        const int i = it % a.ncells;
+        const int i = it - (int)blockIdx.y * a.ncells;   // frame = blockIdx.y: no division
         CellDev r;
         r.level = cells[i].level; r.x0 = cells[i].x0; r.y0 = cells[i].y0; r.cols = cells[i].cols;
         r.rows = cells[i].rows; r.slot_off = cells[i].slot_off; r.cap = cells[i].cap;
         return r;
     };
     auto fetch_of = [&](const CellDev& c, int it) {
-        const int f = it / a.ncells;
+        const int f = blockIdx.y;
         RoiFetch rf;
         if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
         else { rf.src = a.pyr + f * a.pyr_fstride + lvc[c.level].off; rf.pitch = lvc[c.level].pitch; }
@@ -1427,7 +1427,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     };
     // one cell from its landed ROI
     auto process = [&](const CellDev& cur, const RoiFetch& rfc, int it) {
-        const int f = it / a.ncells;
+        const int f = blockIdx.y;
         const int shift = cur.x0 - rfc.base, rstride = rfc.nd * 4;
         const uint8_t* R = roi + shift;
         const int ww = max(0, cur.cols - 6), wh = max(0, cur.rows - 6);
