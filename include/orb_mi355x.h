@@ -303,6 +303,11 @@ typedef struct orbm_kf_map_device {
     const uint32_t* fv_idx;
     const int64_t* fv_node_off;  /* nkf + 1 */
     const int64_t* fv_idx_off;   /* nkf */
+    /* host-side totals of the map (0 = unknown: the node-per-wave kernel runs):
+     * fv_node_off[nkf] and the FeatureVector entries of all keyframes.  With
+     * both set the search runs a lane per keyframe feature (k_bowk_*). */
+    int64_t n_nodes_total;
+    int64_t n_fv_total;
 } orbm_kf_map_device;
 
 /* SearchByBoW(KF_i, F) for nkf host keyframes against one frame in one launch:

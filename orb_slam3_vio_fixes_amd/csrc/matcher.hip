@@ -1065,6 +1065,296 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
 }
 
 // ---------------------------------------------------------------------------
+// Map-wide SearchByBoW(KF_i, F) (mono frame, ORBmatcher.cc:223-425) with a
+// lane per KEYFRAME feature.  In k_bow a wave walks one (keyframe, node)'s KF
+// features serially and spends two wave reductions per KF feature; a node of
+// 40 frame features then keeps 24 of 64 lanes idle.  Here:
+//   k_bowk_map     (pair, KF node) g -> frame node fl, KF feature count; a
+//                  slot range in fl's bucket by one atomic
+//   k_bowk_scan    bucket starts (buckets padded to 64 slots)
+//   k_bowk_fill    slot -> global KF feature index (or none: no valid MapPoint)
+//   k_bowk_topk    one wave per 64 slots of one frame node: each lane keeps the
+//                  kBowK smallest keys (distance << 16 | frame feature index)
+//                  of its KF feature over ALL the node's frame features (read
+//                  wave-uniformly through the scalar cache)
+//   k_bowk_resolve one wave per g: the reference's serial walk over the node's
+//                  KF features.  A frame feature is "taken" when an earlier KF
+//                  feature of the same (pair, node) claimed it; best / second
+//                  of a KF feature are the first two untaken keys of its list,
+//                  exact because every frame feature off the list has a larger
+//                  key.  With one untaken key, the last listed distance bounds
+//                  the second from below, which decides the ratio test unless
+//                  best >= ratio * that bound; only then (or with no untaken
+//                  key of an incomplete list while a claim is still possible)
+//                  is the node rescanned exactly, lane-parallel.
+// k_bow_final (rotation filter, counts) follows unchanged.
+// ---------------------------------------------------------------------------
+constexpr int kBowK = 4;
+#ifndef ORB_BOWK_ABL
+#define ORB_BOWK_ABL 0   // timing ablations (tools only)
+#endif
+
+struct BowKArgs {
+    BowArgs b;
+    long long G;           // (pair, KF node) entries
+    int* g_fl;             // [G] frame node of g, -1 if F does not hold it
+    int* g_off;            // [G] offset of g's KF features in the node's bucket
+    int* g_pr;             // [G] pair of g
+    int* bcount;           // [f_nnodes] KF features per frame node (zeroed)
+    int* bstart;           // [f_nnodes + 1] bucket starts, padded to 64 slots
+    uint32_t* slot_src;    // [slots] global KF feature (kp_off[pr] + ikf), ~0: none
+    uint4* lists;          // [slots] kBowK smallest keys, ascending, ~0: none
+};
+
+__global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
+    const BowArgs& a = k.b;
+    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= k.G) return;
+    int lo = 0, hi = a.npairs;                       // last pr with node_off[pr] <= g
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (a.node_off[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    const int pr = lo;
+    const int ia = (int)(g - a.node_off[pr]);
+    const int* ko = a.kf_off + a.node_off[pr] + pr;
+    const int nkf = ko[ia + 1] - ko[ia];
+    const uint32_t na = a.kf_node[g];
+    int fl = 0, fh = a.f_nnodes;                     // lower_bound of na in F's node ids
+    while (fl < fh) {
+        const int mid = (fl + fh) >> 1;
+        if (a.f_node[mid] < na) fl = mid + 1;
+        else fh = mid;
+    }
+    k.g_pr[g] = pr;
+    if (fl < a.f_nnodes && a.f_node[fl] == na && nkf > 0) {
+        k.g_fl[g] = fl;
+        k.g_off[g] = atomicAdd(k.bcount + fl, nkf);
+    } else {
+        k.g_fl[g] = -1;
+    }
+}
+
+__global__ __launch_bounds__(1024) void k_bowk_scan(BowKArgs k) {
+    extern __shared__ int sc_s[];
+    const int n = k.b.f_nnodes;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = (k.bcount[i] + kWave - 1) / kWave * kWave;
+    __syncthreads();
+    __shared__ int tmp[1024 / kWave + 1];
+    const int total = block_excl_scan(sc_s, n, tmp);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) k.bstart[i] = sc_s[i];
+    if (threadIdx.x == 0) k.bstart[n] = total;
+}
+
+// one wave per g: lanes over g's KF features
+__global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
+    const BowArgs& a = k.b;
+    const long long g = (long long)blockIdx.x * 4 + wave_id();
+    if (g >= k.G) return;
+    const int fl = k.g_fl[g];
+    if (fl < 0) return;
+    const int pr = k.g_pr[g];
+    const int ia = (int)(g - a.node_off[pr]);
+    const int* ko = a.kf_off + a.node_off[pr] + pr;
+    const uint32_t* ki = a.kf_idx + a.idx_off[pr];
+    const long long kpo = a.kp_off[pr];
+    uint32_t* dst = k.slot_src + k.bstart[fl] + k.g_off[g];
+    const int p0 = ko[ia], p1 = ko[ia + 1];
+    for (int p = p0 + lane_id(); p < p1; p += kWave) {
+        const long long gk = kpo + (long long)ki[p];
+        dst[p - p0] = a.kf_valid[gk] ? (uint32_t)gk : 0xffffffffu;
+    }
+}
+
+// the kBowK smallest keys seen so far, ascending (keys are unique): with
+// k0 <= k1 <= ..., the new k_t is med3(k_{t-1}, k_t, key) -- independent ops
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ void topk_push(uint32_t (&kk)[kBowK], uint32_t key) {
+    uint32_t n[kBowK];
+    n[0] = min(kk[0], key);
+#pragma unroll
+    for (int t = 1; t < kBowK; ++t) n[t] = umed3(kk[t - 1], kk[t], key);
+#pragma unroll
+    for (int t = 0; t < kBowK; ++t) kk[t] = n[t];
+}
+
+// keys: distance << 16 | frame feature index (a node lists its features in
+// ascending index order, so the index orders ties like the node position)
+__global__ __launch_bounds__(256) void k_bowk_topk(BowKArgs k) {
+    const BowArgs& a = k.b;
+    const long long slot0 = ((long long)blockIdx.x * 4 + wave_id()) * kWave;
+    const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
+    if (slot0 >= total) return;
+    int lo = 0, hi = a.f_nnodes;                     // last fl with bstart[fl] <= slot0
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (k.bstart[mid] <= slot0) lo = mid;
+        else hi = mid;
+    }
+    const int fl = __builtin_amdgcn_readfirstlane(lo);
+    const int fb = __builtin_amdgcn_readfirstlane(a.f_off[fl]);
+    const int nf = __builtin_amdgcn_readfirstlane(a.f_off[fl + 1]) - fb;
+    const uint32_t src = k.slot_src[slot0 + lane_id()];
+    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
+    if (src != 0xffffffffu) {
+        q0 = *(const uint4*)(a.kf_desc + (long long)src * 32);
+        q1 = *(const uint4*)(a.kf_desc + (long long)src * 32 + 16);
+    }
+    uint32_t kk[kBowK];
+#pragma unroll
+    for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
+    // the node's frame features: wave-uniform, through the scalar cache
+    typedef __attribute__((address_space(4))) const uint32_t* ConstU32;
+    const ConstU32 fidx = (ConstU32)(a.f_idx + fb);
+    const ConstU32 fdesc = (ConstU32)a.f_desc;
+    // four frame features per round: their index and descriptor scalar loads
+    // go out together (one wait per round, not two dependent ones per feature);
+    // rounds past the node's end re-read its last feature and push no key
+    constexpr int kR = 4;
+    for (int f0 = 0; f0 < nf; f0 += kR) {
+        uint32_t fi[kR];
+#pragma unroll
+        for (int t = 0; t < kR; ++t) fi[t] = fidx[min(f0 + t, nf - 1)];
+#pragma unroll
+        for (int t = 0; t < kR; ++t) {
+            const ConstU32 d = fdesc + (size_t)fi[t] * 8;
+            const int dist = __popc(q0.x ^ d[0]) + __popc(q0.y ^ d[1]) + __popc(q0.z ^ d[2]) + __popc(q0.w ^ d[3]) +
+                             __popc(q1.x ^ d[4]) + __popc(q1.y ^ d[5]) + __popc(q1.z ^ d[6]) + __popc(q1.w ^ d[7]);
+            topk_push(kk, f0 + t < nf ? (((uint32_t)dist << 16) | fi[t]) : 0xffffffffu);
+        }
+    }
+    k.lists[slot0 + lane_id()] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+}
+
+// One wave per g: the lists of g's KF features are read lane-parallel, then
+// walked in the reference's order (uniform control flow).  The frame features
+// claimed so far in this (pair, node) -- the only ones a KF feature of it can
+// find taken -- are bits of a wave-private LDS bitmap over frame feature
+// indices, cleared again at the end of the walk.
+__global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
+    extern __shared__ uint32_t taken_s[];            // 4 waves x ceil(f_n / 32) words
+    const BowArgs& a = k.b;
+    const int words = (a.f_n + 31) / 32;
+    uint32_t* taken = taken_s + wave_id() * words;
+    const int lane = lane_id();
+    for (int i = lane; i < words; i += kWave) taken[i] = 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const long long g = (long long)blockIdx.x * 4 + wave_id();
+    if (g >= k.G) return;
+    const int fl = k.g_fl[g];
+    if (fl < 0) return;
+    const int pr = k.g_pr[g];
+    const int ia = (int)(g - a.node_off[pr]);
+    const int* ko = a.kf_off + a.node_off[pr] + pr;
+    const long long base = (long long)k.bstart[fl] + k.g_off[g];
+    const int fb = a.f_off[fl], nf = a.f_off[fl + 1] - fb;
+    const bool complete = nf <= kBowK;
+    int32_t* match = a.match + (long long)pr * a.f_n;
+    const long long kpo = a.kp_off[pr];
+    const int nkf = ko[ia + 1] - ko[ia];
+    auto is_taken = [&](uint32_t fi) { return (taken[fi >> 5] >> (fi & 31)) & 1u; };
+    int nm = 0;
+    for (int c0 = 0; c0 < nkf; c0 += kWave) {
+        uint32_t src = 0xffffffffu;
+        uint4 L = make_uint4(~0u, ~0u, ~0u, ~0u);
+        if (c0 + lane < nkf) {
+            src = k.slot_src[base + c0 + lane];
+            L = k.lists[base + c0 + lane];
+        }
+        const int nc = min(kWave, nkf - c0);
+        // the loads land here, once: the walk's claims store to `match`, and a
+        // wait for these registers inside the walk would also wait for every
+        // store issued before it (one vmcnt for loads and stores)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(src), "+v"(L.x), "+v"(L.y), "+v"(L.z), "+v"(L.w));
+#if ORB_BOWK_ABL == 2
+        if (src == 0x12345u && L.x == 7u) nm++;   // timing ablation: loads only (wrong results)
+        continue;
+#endif
+        for (int j = 0; j < nc; ++j) {
+            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)src, j);
+            if (s == 0xffffffffu) continue;                          // no valid MapPoint (:255-260)
+            const uint32_t keys[kBowK] = {(uint32_t)__builtin_amdgcn_readlane((int)L.x, j),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)L.y, j),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)L.z, j),
+                                          (uint32_t)__builtin_amdgcn_readlane((int)L.w, j)};
+            // the four taken bits in parallel (independent LDS reads), then the
+            // first two untaken keys (:275-276)
+            uint32_t tk[kBowK];
+#pragma unroll
+            for (int t = 0; t < kBowK; ++t) tk[t] = is_taken(min(keys[t] & 0xffffu, (uint32_t)a.f_n - 1u));
+#pragma unroll
+            for (int t = 0; t < kBowK; ++t) tk[t] |= keys[t] == 0xffffffffu;
+            uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
+#pragma unroll
+            for (int t = kBowK - 1; t >= 0; --t) {
+                if (tk[t]) continue;
+                e2 = e1;
+                e1 = keys[t];
+            }
+            // best / second of the untaken node features: exact from the list,
+            // or bounded -- every key off the list is larger than the last one
+            int best = 256, best2 = 256;
+            uint32_t bfi = 0;
+            bool exact = true;
+            const int dlast = (int)(keys[kBowK - 1] >> 16);
+            if (e1 != 0xffffffffu) {
+                best = (int)(e1 >> 16); bfi = e1 & 0xffff;
+                if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
+                else if (!complete && best <= kThLow) {
+                    // second >= dlast: decided when even dlast passes the ratio test
+                    if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
+                    else exact = false;
+                }
+            } else if (!complete && dlast <= kThLow) {
+                exact = false;                                        // every listed key taken
+            }
+#if ORB_BOWK_ABL == 1
+            exact = true;   // timing ablation: no rescans (wrong results)
+#endif
+            if (!exact) {
+                // the reference's loop over the whole node (:266-292), lanes over
+                // its features: keys (dist << 16 | index), first two minima
+                const uint8_t* kd = a.kf_desc + (long long)s * 32;
+                const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
+                uint32_t m1 = (uint32_t)INT_MAX, m2 = (uint32_t)INT_MAX;   // wave_min works on ints
+                for (int f = lane; f < nf; f += kWave) {
+                    const uint32_t fi = a.f_idx[fb + f];
+                    if (is_taken(fi)) continue;
+                    const uint32_t key = ((uint32_t)hamming32(q0, q1, a.f_desc + (long long)fi * 32) << 16) | fi;
+                    m2 = min(m2, max(m1, key));
+                    m1 = min(m1, key);
+                }
+                // first and second minima over the lanes (keys < 2^25: positive ints)
+                const int a1 = wave_min((int)m1, INT_MAX);
+                const int own = (m1 == (uint32_t)a1) ? (int)m2 : (int)m1;
+                const int a2 = wave_min(own, INT_MAX);
+                best = a1 == INT_MAX ? 256 : (a1 >> 16);
+                best2 = a2 == INT_MAX ? 256 : (a2 >> 16);
+                bfi = (uint32_t)a1 & 0xffff;
+            }
+            if (best <= kThLow && (float)best < a.ratio * (float)best2) {   // :327-329
+                // no fence: the LDS bit is read back by this wave's own later
+                // LDS reads (in order), and nothing here reads the match store
+                if (lane == 0) {
+                    match[bfi] = (int32_t)((long long)s - kpo);
+                    taken[bfi >> 5] |= 1u << (bfi & 31);
+                }
+                ++nm;
+            }
+        }
+    }
+    if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
+}
+
+// ---------------------------------------------------------------------------
 // k_proj: the projection searches with a serial claim on the target's slots,
 // one wave per target, queries in reference order, the candidates of a query
 // spread over the lanes (cell-start runs, in GetFeaturesInArea order).
@@ -2483,6 +2773,39 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
     return ORB_OK;
 }
 
+// G: (pair, KF node) entries of the map, nfv: its FeatureVector entries (host
+// totals of the resident map: scratch is sized without reading the device).
+static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
+    static thread_local PBuf<int> g_fl, g_off, g_pr, bcount, bstart;
+    static thread_local PBuf<uint32_t> slot_src;
+    static thread_local PBuf<uint4> lists;
+    a.npairs = npairs;
+    const long long slots = nfv + (long long)kWave * a.f_nnodes;
+    int rc;
+    if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bcount.alloc(a.f_nnodes)) ||
+        (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)))
+        return rc;
+    BowKArgs k;
+    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bcount = bcount.p; k.bstart = bstart.p;
+    k.slot_src = slot_src.p; k.lists = lists.p;
+    ORB_CHECK(flush_uploads());
+    ORB_CHECK(hipMemsetAsync(bcount.p, 0, (size_t)a.f_nnodes * sizeof(int), st));
+    ORB_CHECK(hipMemsetAsync(slot_src.p, 0xff, (size_t)slots * sizeof(uint32_t), st));
+    {
+        const long long nmf = (long long)npairs * a.f_n;
+        const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
+        KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
+    }
+    const unsigned gb = (unsigned)((G + 255) / 256), gw = (unsigned)((G + 3) / 4);
+    KLAUNCH(k_bowk_map, dim3(gb), dim3(256), 0, st, k);
+    KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)a.f_nnodes * sizeof(int), st, k);
+    KLAUNCH(k_bowk_fill, dim3(gw), dim3(256), 0, st, k);
+    KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
+    KLAUNCH(k_bowk_resolve, dim3(gw), dim3(256), (size_t)4 * ((a.f_n + 31) / 32) * sizeof(uint32_t), st, k);
+    KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
+    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+}
+
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f, const orbm_featvec* ffv,
                                     float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
     if (!map || !f || !ffv || !d_match || !d_nmatches || map->nkf < 0) return ORB_ERR_PARAM;
@@ -2494,6 +2817,13 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     a.f_kps = f->kps; a.f_desc = f->desc; a.f_n = f->n; a.f_node = ffv->node_ids; a.f_off = ffv->offsets;
     a.f_idx = ffv->idx; a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
     a.match = d_match; a.nmatches = d_nmatches;
+    // the lane-per-KF-feature search is opt-in (ORBM_BOW_KFLANE=1): correct, but
+    // its serial walk runs on the scalar unit and it measured 9.4 ms per
+    // 10k-keyframe query against 7.1 ms for k_bow
+    const char* kfl = std::getenv("ORBM_BOW_KFLANE");
+    if (map->n_nodes_total > 0 && map->n_fv_total > 0 && f->n <= 0xffff && ffv->nnodes > 0 &&
+        ffv->nnodes <= 32 * 1024 && kfl && kfl[0] == '1')
+        return launch_bow_kf(a, map->nkf, map->n_nodes_total, map->n_fv_total, (hipStream_t)stream);
     return launch_bow(a, map->nkf, (hipStream_t)stream);
 }
 

@@ -18,7 +18,8 @@ from . import abi, capi
 class OrbmKfMapDevice(C.Structure):
     _fields_ = [("nkf", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("valid", C.c_void_p),
                 ("kp_off", C.c_void_p), ("fv_node", C.c_void_p), ("fv_off", C.c_void_p), ("fv_idx", C.c_void_p),
-                ("fv_node_off", C.c_void_p), ("fv_idx_off", C.c_void_p)]
+                ("fv_node_off", C.c_void_p), ("fv_idx_off", C.c_void_p),
+                ("n_nodes_total", C.c_int64), ("n_fv_total", C.c_int64)]
 
 
 def featvec_csr(node_of_feature: np.ndarray):
@@ -58,7 +59,8 @@ class DeviceKeyframeMap:
                       fv_idx_off=t([np.array(idx_off, np.int64)], np.int64))
         p = lambda name: self.t[name].data_ptr()
         self.struct = OrbmKfMapDevice(self.nkf, p("kps"), p("desc"), p("valid"), p("kp_off"), p("fv_node"),
-                                      p("fv_off"), p("fv_idx"), p("fv_node_off"), p("fv_idx_off"))
+                                      p("fv_off"), p("fv_idx"), p("fv_node_off"), p("fv_idx_off"),
+                                      node_off[-1], sum(len(x) for x in idxs))
 
     def search_by_bow(self, kps, desc, node_of_feature, nnratio=0.75, check_ori=True, stream=None):
         """SearchByBoW(KF_i, F) for every keyframe: returns (match [nkf, N] int32

@@ -47,7 +47,9 @@ def make_keyframes(k, d, voc, nkf, seed):
     return kfs
 
 
-def test_c5_map_wide_search_by_bow(gpu_lib, c5):
+@pytest.mark.parametrize("kflane", ["0", "1"])
+def test_c5_map_wide_search_by_bow(gpu_lib, c5, kflane, monkeypatch):
+    monkeypatch.setenv("ORBM_BOW_KFLANE", kflane)
     k, d, voc = c5
     kfs = make_keyframes(k, d, voc, 24, 1)
     _, _, fnode = O.transform(voc, d, 4)
@@ -59,3 +61,64 @@ def test_c5_map_wide_search_by_bow(gpu_lib, c5):
                                       abi.frame_struct(k, d, 1920, 1080), abi.featvec_struct(fnode), 0.75, True)
         assert nm[i] == rnm and rnm > 100
         np.testing.assert_array_equal(match[i], rmatch)
+
+
+def _kps(rng, n):
+    k = np.zeros(n, abi.KEYPOINT_DTYPE)
+    k["x"] = rng.uniform(0, 640, n)
+    k["y"] = rng.uniform(0, 480, n)
+    k["angle"] = rng.uniform(0, 360, n)
+    k["size"] = 31
+    return k
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, monkeypatch):
+    """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
+    against the node-per-wave kernel on inputs that exercise its exactness
+    argument: few frame nodes (nodes of 2-400 features, so complete and
+    incomplete top-4 lists), frame descriptors repeated (distance ties,
+    first position wins), keyframe features repeated up to 6 times (the
+    earlier copies take their best candidates, so lists run out of untaken
+    keys and the exact rescan runs), invalid MapPoints, KF nodes the frame
+    does not hold."""
+    rng = np.random.default_rng(seed)
+    nf = 1500
+    fd = rng.integers(0, 256, (nf, 32), dtype=np.uint8)
+    dup = rng.random(nf) < 0.15
+    fd[dup] = fd[rng.integers(0, nf, dup.sum())]
+    fk = _kps(rng, nf)
+    # node sizes from tiny to large: node i holds ~ geometric share
+    fnode = np.minimum(rng.geometric(0.08, nf), 40).astype(np.int64) * 7 + 100
+    fnode[rng.random(nf) < 0.25] = 50                    # a ~375-feature node
+    fnode[rng.random(nf) < 0.003] = 5                    # a 2-5 feature node
+    kfs = []
+    for i in range(12):
+        src = rng.choice(nf, size=int(nf * rng.uniform(0.3, 0.7)), replace=False)
+        reps = np.where(rng.random(len(src)) < 0.2, rng.integers(2, 7, len(src)), 1)
+        src = np.repeat(src, reps)
+        kd = fd[src].copy()
+        flip = rng.integers(0, 256, kd.shape, dtype=np.uint8)
+        for _ in range(int(rng.integers(2, 5))):
+            flip &= rng.integers(0, 256, kd.shape, dtype=np.uint8)
+        kd ^= np.where(rng.random((len(src), 1)) < 0.5, flip, 0).astype(np.uint8)
+        kk = _kps(rng, len(src))
+        kk["angle"] = (fk["angle"][src] + rng.normal(0, 3, len(src))) % 360
+        nid = fnode[src].copy()
+        nid[rng.random(len(src)) < 0.05] = 99999          # a node the frame lacks
+        valid = (rng.random(len(src)) < 0.85).astype(np.uint8)
+        kfs.append((kk, kd, valid, nid))
+    m = kfmap.DeviceKeyframeMap(kfs)
+    assert m.struct.n_nodes_total > 0 and m.struct.n_fv_total > 0
+    monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
+    got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
+    monkeypatch.setenv("ORBM_BOW_KFLANE", "0")
+    old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
+    np.testing.assert_array_equal(got, old)
+    np.testing.assert_array_equal(gnm, onm)
+    for i, (kk, kd, valid, nid) in enumerate(kfs):
+        rnm, rmatch = O.search_by_bow(abi.frame_struct(kk, kd, 640, 480), abi.featvec_struct(nid), valid,
+                                      abi.frame_struct(fk, fd, 640, 480), abi.featvec_struct(fnode), 0.75, True)
+        assert gnm[i] == rnm
+        np.testing.assert_array_equal(got[i], rmatch)
+    assert gnm.min() > 20
