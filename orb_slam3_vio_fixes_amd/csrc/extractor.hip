@@ -540,8 +540,10 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
                 c.cap = cap;
                 slotsum += cap;
                 P.cells.push_back(c);
-                P.roi_max = std::max(P.roi_max, c.rows * ((c.cols + 6) & ~3) + 16);
-                P.roi_dwords = std::max(P.roi_dwords, c.rows * (((c.x0 & 3) + c.cols + 3) >> 2));
+                // + 16: the pre-test reads up to 2 dwords past the last row's window
+                P.roi_max = std::max(P.roi_max, 4 * c.rows * (((c.x0 & 3) + c.cols + 3) >> 2) + 16);
+                P.roi_rows_max = std::max(P.roi_rows_max, c.rows);
+                P.roi_nd_max = std::max(P.roi_nd_max, ((c.x0 & 3) + c.cols + 3) >> 2);
                 P.win_max = std::max(P.win_max, (std::max(0, c.cols - 6) + 2) * (std::max(0, c.rows - 6) + 2));
                 P.win_pix_max = std::max(P.win_pix_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
                 ++nc;
@@ -1345,22 +1347,39 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #define ORB_FAST_ABL 0   // timing ablations (tools only; wrong results): 1 scores, 2 compaction, 3 compass
 #endif
 
+// A cell's ROI lands in LDS row-major at its own pitch of nd dwords (dense:
+// the banks of the pre-test's row reads spread as before).  It is fetched as
+// rows of PDW >= nd dwords, lane i + 64 j holding row (i + 64 j) / PDW, dword
+// (i + 64 j) % PDW: lanes past nd re-read dword nd - 1 and rows past the ROI
+// its last row (identical values to identical places), so the NV loads per
+// lane issue back to back, branch-free, with a clamp and a multiply-add of
+// address math each (the float-reciprocal split of a linear index cost ~14
+// VALU per load).
 struct RoiFetch {
-    const uint8_t* src;
-    int pitch, base, nd, n;
-    float inv_nd;
+    const uint8_t* src;     // ROI row 0, dword 0 (level row y0, column x0 & ~3)
+    int pitch, nd, rows;
 };
 
-template <int NV>
-__device__ __forceinline__ void roi_issue(const RoiFetch& rf, int y0, uint32_t (&v)[NV]) {
+template <int PDW, int NV>
+__device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV]) {
+    static_assert(kWave % PDW == 0, "rows of a load round are whole");
     const int lane = lane_id();
+    const uint8_t* col = rf.src + 4 * min(lane % PDW, rf.nd - 1);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        // branch-free: lanes past the ROI re-read its last dword (rf.n >= 1), so
-        // the loads issue back to back with no per-load vmcnt waits at joins
-        const int i = min(lane + j * kWave, rf.n - 1);
-        const int r = div_row(i, rf.inv_nd), d = i - r * rf.nd;
-        v[j] = *(const uint32_t*)(rf.src + (long long)(y0 + r) * rf.pitch + rf.base + 4 * d);
+        const int r = min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
+        v[j] = *(const uint32_t*)(col + (long long)r * rf.pitch);
+    }
+}
+
+template <int PDW, int NV>
+__device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)[NV], uint32_t* roi) {
+    const int lane = lane_id();
+    const int d = min(lane % PDW, rf.nd - 1);
+#pragma unroll
+    for (int j = 0; j < NV; ++j) {
+        const int r = min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
+        roi[r * rf.nd + d] = v[j];
     }
 }
 
@@ -1369,7 +1388,7 @@ __device__ __forceinline__ void roi_issue(const RoiFetch& rf, int y0, uint32_t (
 #else
 #define FAST_WPE_ATTR
 #endif
-template <int NV>
+template <int PDW, int NV>
 __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
@@ -1401,10 +1420,9 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         RoiFetch rf;
         if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
         else { rf.src = a.pyr + f * a.pyr_fstride + lvc[c.level].off; rf.pitch = lvc[c.level].pitch; }
-        rf.base = c.x0 & ~3;
-        rf.nd = ((c.x0 - rf.base) + c.cols + 3) >> 2;
-        rf.n = max(1, c.rows * rf.nd);   // >= 1: the branch-free issue clamps to rf.n - 1
-        rf.inv_nd = 1.0f / (float)rf.nd;
+        rf.src += (long long)c.y0 * rf.pitch + (c.x0 & ~3);
+        rf.nd = max(1, ((c.x0 & 3) + c.cols + 3) >> 2);
+        rf.rows = max(1, c.rows);
         return rf;
     };
     // cell descriptors (scalar loads) run two cells ahead, ROI loads one cell ahead
@@ -1414,21 +1432,19 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     if (it0 < it_end) {
         c = cell_at(it0);
         rf = fetch_of(c, it0);
-        roi_issue<NV>(rf, c.y0, v);
+        roi_issue<PDW, NV>(rf, v);
     }
     if (it0 + step < it_end) cn = cell_at(it0 + step);
 #ifdef ORB_FAST_TIMING
     unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t5 = 0, t6 = 0, t7 = 0, t9 = 0, t10 = 0;
     unsigned long long tlast = t_start;
 #endif
-    auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) {
-#pragma unroll
-        for (int j = 0; j < NV; ++j) ((uint32_t*)roi)[min(lane + j * kWave, r.n - 1)] = vv[j];
-    };
+    auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) { roi_land<PDW, NV>(r, vv, (uint32_t*)roi); };
     // one cell from its landed ROI
     auto process = [&](const CellDev& cur, const RoiFetch& rfc, int it) {
         const int f = blockIdx.y;
-        const int shift = cur.x0 - rfc.base, rstride = rfc.nd * 4;
+        const int rstride = rfc.nd * 4;
+        const int shift = cur.x0 & 3;
         const uint8_t* R = roi + shift;
         const int ww = max(0, cur.cols - 6), wh = max(0, cur.rows - 6);
         const int sp = ww + 2, npad = sp * (wh + 2);
@@ -1620,7 +1636,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         if (it + step < it_end) {
             c = cn;
             rf = fetch_of(c, it + step);
-            roi_issue<NV>(rf, c.y0, v);
+            roi_issue<PDW, NV>(rf, v);
         }
         if (it + 2 * step < it_end) cn = cell_at(it + 2 * step);
         process(cur, rcur, it);
@@ -2621,8 +2637,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     const int L = P0.L;
     Plan P;                         // shallow view: host tables + offset device pointers (never released)
     P.lv = P0.lv; P.cells = P0.cells; P.pyr_bytes = P0.pyr_bytes; P.ncells = P0.ncells;
-    P.slot_total = P0.slot_total; P.out_total = P0.out_total; P.roi_max = P0.roi_max;
-    P.roi_dwords = P0.roi_dwords; P.win_max = P0.win_max; P.max_level_cells = P0.max_level_cells;
+    P.slot_total = P0.slot_total; P.out_total = P0.out_total; P.roi_rows_max = P0.roi_rows_max; P.roi_max = P0.roi_max;
+    P.roi_nd_max = P0.roi_nd_max; P.win_max = P0.win_max; P.max_level_cells = P0.max_level_cells;
     P.max_out_cap = P0.max_out_cap; P.xmax = P0.xmax; P.tab_off = P0.tab_off; P.L = L; P.pgroups = P0.pgroups;
     P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells; P.d_slot_level = P0.d_slot_level;
     const long long F = f0;
@@ -2737,14 +2753,23 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.cell_count = P.d_cell_count; fa.cell_keys = P.d_cell_keys; fa.slot_total = P.slot_total;
     fa.ini_th = std::min(std::max(hd->prm.ini_th_fast, 0), 255);
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
-    fa.roi_max = (P.roi_max + 15) & ~15;
+    // fetch row width (dwords) and loads per lane: <16, 12> takes ROIs of at
+    // most 16 dwords by 48 rows (W = 35 cells are < 70 px: nd <= 19 and rows <
+    // 76 always fit <32, 40>)
+    void (*kfast)(FastArgs);
+    const int ndm = P.roi_nd_max, rm = P.roi_rows_max;
+    if (ndm <= 16 && rm <= 48) kfast = k_fast_cells<16, 12>;
+    else if (ndm <= 16 && rm <= 64) kfast = k_fast_cells<16, 16>;
+    else if (ndm <= 16 && rm <= 80) kfast = k_fast_cells<16, 20>;
+    else if (ndm <= 32 && rm <= 48) kfast = k_fast_cells<32, 24>;
+    else if (ndm <= 32 && rm <= 80) kfast = k_fast_cells<32, 40>;
+    else return ORB_ERR_UNSUPPORTED;
+    fa.roi_max = (P0.roi_max + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
     fa.kmask_bytes = ((P0.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
     fa.cand_bytes = (2 * P0.win_pix_max + 15) & ~15;
     const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes);
     fa.nframes = B;
-    const int nv = (P.roi_dwords + kWave - 1) / kWave;
-    void (*kfast)(FastArgs) = nv <= 12 ? k_fast_cells<12> : (nv <= 24 ? k_fast_cells<24> : k_fast_cells<48>);
     const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
     hipLaunchKernelGGL(kfast, fgrid, dim3(256), flds, st, fa);
     mark();
