@@ -1104,6 +1104,10 @@ struct BowKArgs {
     int* bstart;           // [f_nnodes + 1] bucket starts, padded to 64 slots
     uint32_t* slot_src;    // [slots] global KF feature (kp_off[pr] + ikf), ~0: none
     uint4* lists;          // [slots] kBowK smallest keys, ascending, ~0: none
+    int* gcount;           // [f_nnodes] g entries per frame node (zeroed)
+    int* gstart;           // [f_nnodes + 1] their starts
+    int* g_rank;           // [G] rank of g among its frame node's entries
+    int* perm;             // [G] g entries ordered by frame node
 };
 
 __global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
@@ -1131,6 +1135,7 @@ __global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
     if (fl < a.f_nnodes && a.f_node[fl] == na && nkf > 0) {
         k.g_fl[g] = fl;
         k.g_off[g] = atomicAdd(k.bcount + fl, nkf);
+        k.g_rank[g] = atomicAdd(k.gcount + fl, 1);
     } else {
         k.g_fl[g] = -1;
     }
@@ -1145,6 +1150,12 @@ __global__ __launch_bounds__(1024) void k_bowk_scan(BowKArgs k) {
     const int total = block_excl_scan(sc_s, n, tmp);
     for (int i = threadIdx.x; i < n; i += blockDim.x) k.bstart[i] = sc_s[i];
     if (threadIdx.x == 0) k.bstart[n] = total;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = k.gcount[i];
+    __syncthreads();
+    const int gtotal = block_excl_scan(sc_s, n, tmp);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) k.gstart[i] = sc_s[i];
+    if (threadIdx.x == 0) k.gstart[n] = gtotal;
 }
 
 // one wave per g: lanes over g's KF features
@@ -1160,6 +1171,7 @@ __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
     const uint32_t* ki = a.kf_idx + a.idx_off[pr];
     const long long kpo = a.kp_off[pr];
     uint32_t* dst = k.slot_src + k.bstart[fl] + k.g_off[g];
+    if (lane_id() == 0) k.perm[k.gstart[fl] + k.g_rank[g]] = (int)g;
     const int p0 = ko[ia], p1 = ko[ia + 1];
     for (int p = p0 + lane_id(); p < p1; p += kWave) {
         const long long gk = kpo + (long long)ki[p];
@@ -1183,8 +1195,8 @@ __device__ __forceinline__ void topk_push(uint32_t (&kk)[kBowK], uint32_t key) {
     for (int t = 0; t < kBowK; ++t) kk[t] = n[t];
 }
 
-// keys: distance << 16 | frame feature index (a node lists its features in
-// ascending index order, so the index orders ties like the node position)
+// keys: distance << 16 | position in the frame node (the reference's order of
+// equal distances)
 __global__ __launch_bounds__(256) void k_bowk_topk(BowKArgs k) {
     const BowArgs& a = k.b;
     const long long slot0 = ((long long)blockIdx.x * 4 + wave_id()) * kWave;
@@ -1225,7 +1237,7 @@ __global__ __launch_bounds__(256) void k_bowk_topk(BowKArgs k) {
             const ConstU32 d = fdesc + (size_t)fi[t] * 8;
             const int dist = __popc(q0.x ^ d[0]) + __popc(q0.y ^ d[1]) + __popc(q0.z ^ d[2]) + __popc(q0.w ^ d[3]) +
                              __popc(q1.x ^ d[4]) + __popc(q1.y ^ d[5]) + __popc(q1.z ^ d[6]) + __popc(q1.w ^ d[7]);
-            topk_push(kk, f0 + t < nf ? (((uint32_t)dist << 16) | fi[t]) : 0xffffffffu);
+            topk_push(kk, f0 + t < nf ? (((uint32_t)dist << 16) | (uint32_t)(f0 + t)) : 0xffffffffu);
         }
     }
     k.lists[slot0 + lane_id()] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
@@ -1239,7 +1251,7 @@ __global__ __launch_bounds__(256) void k_bowk_topk(BowKArgs k) {
 __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
     extern __shared__ uint32_t taken_s[];            // 4 waves x ceil(f_n / 32) words
     const BowArgs& a = k.b;
-    const int words = (a.f_n + 31) / 32;
+    const int words = (a.f_n + 31) / 32;   // positions < nf <= f_n
     uint32_t* taken = taken_s + wave_id() * words;
     const int lane = lane_id();
     for (int i = lane; i < words; i += kWave) taken[i] = 0;
@@ -1289,7 +1301,7 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
             // first two untaken keys (:275-276)
             uint32_t tk[kBowK];
 #pragma unroll
-            for (int t = 0; t < kBowK; ++t) tk[t] = is_taken(min(keys[t] & 0xffffu, (uint32_t)a.f_n - 1u));
+            for (int t = 0; t < kBowK; ++t) tk[t] = is_taken(min(keys[t] & 0xffffu, (uint32_t)nf - 1u));
 #pragma unroll
             for (int t = 0; t < kBowK; ++t) tk[t] |= keys[t] == 0xffffffffu;
             uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
@@ -1326,9 +1338,9 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
                 const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
                 uint32_t m1 = (uint32_t)INT_MAX, m2 = (uint32_t)INT_MAX;   // wave_min works on ints
                 for (int f = lane; f < nf; f += kWave) {
+                    if (is_taken((uint32_t)f)) continue;
                     const uint32_t fi = a.f_idx[fb + f];
-                    if (is_taken(fi)) continue;
-                    const uint32_t key = ((uint32_t)hamming32(q0, q1, a.f_desc + (long long)fi * 32) << 16) | fi;
+                    const uint32_t key = ((uint32_t)hamming32(q0, q1, a.f_desc + (long long)fi * 32) << 16) | (uint32_t)f;
                     m2 = min(m2, max(m1, key));
                     m1 = min(m1, key);
                 }
@@ -1344,7 +1356,7 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
                 // no fence: the LDS bit is read back by this wave's own later
                 // LDS reads (in order), and nothing here reads the match store
                 if (lane == 0) {
-                    match[bfi] = (int32_t)((long long)s - kpo);
+                    match[a.f_idx[fb + bfi]] = (int32_t)((long long)s - kpo);
                     taken[bfi >> 5] |= 1u << (bfi & 31);
                 }
                 ++nm;
@@ -1352,6 +1364,82 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
         }
     }
     if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
+}
+
+// One thread per g, the g entries ordered by frame node (neighbouring lanes
+// walk nodes of one size: little divergence).  The positions of the node
+// claimed so far in this walk are bits of a thread-private LDS bitmap (17
+// words a thread: the odd pitch spreads the threads over the banks); nodes of
+// more than 512 features read "taken" from the match row instead (only this
+// thread writes the node's entries of it).  Otherwise as k_bowk_resolve.
+constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
+__global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
+    __shared__ uint32_t taken_s[256 * kBowLanePitch];
+    const BowArgs& a = k.b;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= k.gstart[a.f_nnodes]) return;
+    const long long g = k.perm[t];
+    const int fl = k.g_fl[g];
+    const int pr = k.g_pr[g];
+    const int ia = (int)(g - a.node_off[pr]);
+    const int* ko = a.kf_off + a.node_off[pr] + pr;
+    const long long base = (long long)k.bstart[fl] + k.g_off[g];
+    const int fb = a.f_off[fl], nf = a.f_off[fl + 1] - fb;
+    const bool complete = nf <= kBowK, lds_bits = nf <= 32 * kBowLaneWords;
+    int32_t* match = a.match + (long long)pr * a.f_n;
+    const uint32_t* fidx = a.f_idx + fb;
+    const long long kpo = a.kp_off[pr];
+    uint32_t* taken = taken_s + threadIdx.x * kBowLanePitch;
+#pragma unroll
+    for (int i = 0; i < kBowLaneWords; ++i) taken[i] = 0;
+    auto is_taken = [&](int f) -> bool {
+        return lds_bits ? ((taken[f >> 5] >> (f & 31)) & 1u) : match[fidx[f]] >= 0;
+    };
+    const int nkf = ko[ia + 1] - ko[ia];
+    int nm = 0;
+    for (int j = 0; j < nkf; ++j) {
+        const uint32_t s = k.slot_src[base + j];
+        if (s == 0xffffffffu) continue;                              // no valid MapPoint (:255-260)
+        const uint4 L = k.lists[base + j];
+        const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
+        uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
+#pragma unroll
+        for (int q = kBowK - 1; q >= 0; --q) {                       // first two untaken keys (:275-276)
+            if (keys[q] == 0xffffffffu || is_taken((int)(keys[q] & 0xffff))) continue;
+            e2 = e1;
+            e1 = keys[q];
+        }
+        int best = 256, best2 = 256, bpos = -1;
+        bool exact = true;
+        const int dlast = (int)(keys[kBowK - 1] >> 16);
+        if (e1 != 0xffffffffu) {
+            best = (int)(e1 >> 16); bpos = (int)(e1 & 0xffff);
+            if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
+            else if (!complete && best <= kThLow) {
+                if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
+                else exact = false;
+            }
+        } else if (!complete && dlast <= kThLow) {
+            exact = false;
+        }
+        if (!exact) {                                                // the reference's node loop (:266-292)
+            const uint8_t* kd = a.kf_desc + (long long)s * 32;
+            const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
+            best = 256; best2 = 256; bpos = -1;
+            for (int f = 0; f < nf; ++f) {
+                if (is_taken(f)) continue;
+                const int d = hamming32(q0, q1, a.f_desc + (long long)fidx[f] * 32);
+                if (d < best) { best2 = best; best = d; bpos = f; }
+                else if (d < best2) best2 = d;
+            }
+        }
+        if (best <= kThLow && (float)best < a.ratio * (float)best2) {   // :327-329
+            match[fidx[bpos]] = (int32_t)((long long)s - kpo);
+            if (lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
+            ++nm;
+        }
+    }
+    if (nm) atomicAdd(&a.nmatches[pr], nm);
 }
 
 // ---------------------------------------------------------------------------
@@ -2776,20 +2864,24 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 // G: (pair, KF node) entries of the map, nfv: its FeatureVector entries (host
 // totals of the resident map: scratch is sized without reading the device).
 static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
-    static thread_local PBuf<int> g_fl, g_off, g_pr, bcount, bstart;
+    static thread_local PBuf<int> g_fl, g_off, g_pr, bcount, bstart, gcount, gstart, g_rank, perm;
     static thread_local PBuf<uint32_t> slot_src;
     static thread_local PBuf<uint4> lists;
     a.npairs = npairs;
     const long long slots = nfv + (long long)kWave * a.f_nnodes;
     int rc;
     if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bcount.alloc(a.f_nnodes)) ||
-        (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)))
+        (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
+        (rc = gcount.alloc(a.f_nnodes)) || (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
+        (rc = perm.alloc(G)))
         return rc;
     BowKArgs k;
     k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bcount = bcount.p; k.bstart = bstart.p;
     k.slot_src = slot_src.p; k.lists = lists.p;
+    k.gcount = gcount.p; k.gstart = gstart.p; k.g_rank = g_rank.p; k.perm = perm.p;
     ORB_CHECK(flush_uploads());
     ORB_CHECK(hipMemsetAsync(bcount.p, 0, (size_t)a.f_nnodes * sizeof(int), st));
+    ORB_CHECK(hipMemsetAsync(gcount.p, 0, (size_t)a.f_nnodes * sizeof(int), st));
     ORB_CHECK(hipMemsetAsync(slot_src.p, 0xff, (size_t)slots * sizeof(uint32_t), st));
     {
         const long long nmf = (long long)npairs * a.f_n;
@@ -2801,7 +2893,11 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)a.f_nnodes * sizeof(int), st, k);
     KLAUNCH(k_bowk_fill, dim3(gw), dim3(256), 0, st, k);
     KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
-    KLAUNCH(k_bowk_resolve, dim3(gw), dim3(256), (size_t)4 * ((a.f_n + 31) / 32) * sizeof(uint32_t), st, k);
+    const char* rw = std::getenv("ORBM_BOW_KFLANE_WAVE_RESOLVE");   // the wave-walk form (A/B)
+    if (rw && rw[0] == '1')
+        KLAUNCH(k_bowk_resolve, dim3(gw), dim3(256), (size_t)4 * ((a.f_n + 31) / 32) * sizeof(uint32_t), st, k);
+    else
+        KLAUNCH(k_bowk_resolve_lane, dim3(gb), dim3(256), 0, st, k);
     KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
@@ -2817,12 +2913,12 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     a.f_kps = f->kps; a.f_desc = f->desc; a.f_n = f->n; a.f_node = ffv->node_ids; a.f_off = ffv->offsets;
     a.f_idx = ffv->idx; a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
     a.match = d_match; a.nmatches = d_nmatches;
-    // the lane-per-KF-feature search is opt-in (ORBM_BOW_KFLANE=1): correct, but
-    // its serial walk runs on the scalar unit and it measured 9.4 ms per
-    // 10k-keyframe query against 7.1 ms for k_bow
+    // the lane-per-KF-feature search (k_bowk_*) when the map carries its totals
+    // (6.7 vs 7.1 ms per 10k-keyframe query); ORBM_BOW_KFLANE=0
+    // selects k_bow (A/B, tests)
     const char* kfl = std::getenv("ORBM_BOW_KFLANE");
     if (map->n_nodes_total > 0 && map->n_fv_total > 0 && f->n <= 0xffff && ffv->nnodes > 0 &&
-        ffv->nnodes <= 32 * 1024 && kfl && kfl[0] == '1')
+        ffv->nnodes <= 32 * 1024 && !(kfl && kfl[0] == '0'))
         return launch_bow_kf(a, map->nkf, map->n_nodes_total, map->n_fv_total, (hipStream_t)stream);
     return launch_bow(a, map->nkf, (hipStream_t)stream);
 }

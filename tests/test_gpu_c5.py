@@ -72,8 +72,8 @@ def _kps(rng, n):
     return k
 
 
-@pytest.mark.parametrize("seed", [3, 4])
-def test_c5_kf_lane_adversarial(gpu_lib, seed, monkeypatch):
+@pytest.mark.parametrize("seed,wave_resolve", [(3, "0"), (4, "0"), (3, "1")])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, monkeypatch):
     """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
     against the node-per-wave kernel on inputs that exercise its exactness
     argument: few frame nodes (nodes of 2-400 features, so complete and
@@ -111,6 +111,7 @@ def test_c5_kf_lane_adversarial(gpu_lib, seed, monkeypatch):
     m = kfmap.DeviceKeyframeMap(kfs)
     assert m.struct.n_nodes_total > 0 and m.struct.n_fv_total > 0
     monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
+    monkeypatch.setenv("ORBM_BOW_KFLANE_WAVE_RESOLVE", wave_resolve)
     got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
     monkeypatch.setenv("ORBM_BOW_KFLANE", "0")
     old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
