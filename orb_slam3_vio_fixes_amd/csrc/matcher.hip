@@ -1373,11 +1373,28 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
 // more than 512 features read "taken" from the match row instead (only this
 // thread writes the node's entries of it).  Otherwise as k_bowk_resolve.
 constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
+// The walk's memory traffic is kept off its critical path: the next keyframe
+// feature's slot and list are loaded one step ahead, the frame-feature
+// indices of the block's first node come from an LDS copy, and every step
+// issues exactly one store (a claim to `match`, otherwise to a scratch
+// word), so the wait for the prefetched loads never covers a store issued
+// after them.
+constexpr int kBowFidxStage = 1024;
 __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
     __shared__ uint32_t taken_s[256 * kBowLanePitch];
+    __shared__ uint16_t s_fidx[kBowFidxStage];
     const BowArgs& a = k.b;
-    const int t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= k.gstart[a.f_nnodes]) return;
+    const int ntot = k.gstart[a.f_nnodes];
+    const int tb = blockIdx.x * blockDim.x;
+    if (tb >= ntot) return;                                        // the whole block
+    const int fl0 = k.g_fl[k.perm[tb]];
+    const int fb0 = a.f_off[fl0], nf0 = a.f_off[fl0 + 1] - fb0;
+    const bool st0 = nf0 <= kBowFidxStage;
+    if (st0)
+        for (int p = threadIdx.x; p < nf0; p += blockDim.x) s_fidx[p] = (uint16_t)a.f_idx[fb0 + p];
+    __syncthreads();
+    const int t = tb + threadIdx.x;
+    if (t >= ntot) return;
     const long long g = k.perm[t];
     const int fl = k.g_fl[g];
     const int pr = k.g_pr[g];
@@ -1385,10 +1402,11 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
     const int* ko = a.kf_off + a.node_off[pr] + pr;
     const long long base = (long long)k.bstart[fl] + k.g_off[g];
     const int fb = a.f_off[fl], nf = a.f_off[fl + 1] - fb;
-    const bool complete = nf <= kBowK, lds_bits = nf <= 32 * kBowLaneWords;
+    const bool complete = nf <= kBowK, lds_bits = nf <= 32 * kBowLaneWords, lds_fidx = st0 && fl == fl0;
     int32_t* match = a.match + (long long)pr * a.f_n;
     const uint32_t* fidx = a.f_idx + fb;
     const long long kpo = a.kp_off[pr];
+    int32_t* sink = k.g_rank + t;                                  // scratch (g_rank is k_bowk_fill's)
     uint32_t* taken = taken_s + threadIdx.x * kBowLanePitch;
 #pragma unroll
     for (int i = 0; i < kBowLaneWords; ++i) taken[i] = 0;
@@ -1397,10 +1415,20 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
     };
     const int nkf = ko[ia + 1] - ko[ia];
     int nm = 0;
+    uint32_t s_n = 0xffffffffu;
+    uint4 L_n = make_uint4(~0u, ~0u, ~0u, ~0u);
+    if (nkf > 0) {
+        s_n = k.slot_src[base];
+        L_n = k.lists[base];
+    }
+    *sink = 0;   // the first step, too, finds one store after its data's loads
     for (int j = 0; j < nkf; ++j) {
-        const uint32_t s = k.slot_src[base + j];
-        if (s == 0xffffffffu) continue;                              // no valid MapPoint (:255-260)
-        const uint4 L = k.lists[base + j];
+        const uint32_t s = s_n;
+        const uint4 L = L_n;
+        const int jn = min(j + 1, nkf - 1);
+        s_n = k.slot_src[base + jn];
+        L_n = k.lists[base + jn];
+        const bool valid = s != 0xffffffffu;                         // a valid MapPoint (:255-260)
         const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
         uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
 #pragma unroll
@@ -1409,7 +1437,7 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
             e2 = e1;
             e1 = keys[q];
         }
-        int best = 256, best2 = 256, bpos = -1;
+        int best = 256, best2 = 256, bpos = 0;
         bool exact = true;
         const int dlast = (int)(keys[kBowK - 1] >> 16);
         if (e1 != 0xffffffffu) {
@@ -1422,10 +1450,10 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
         } else if (!complete && dlast <= kThLow) {
             exact = false;
         }
-        if (!exact) {                                                // the reference's node loop (:266-292)
+        if (valid && !exact) {                                       // the reference's node loop (:266-292)
             const uint8_t* kd = a.kf_desc + (long long)s * 32;
             const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
-            best = 256; best2 = 256; bpos = -1;
+            best = 256; best2 = 256; bpos = 0;
             for (int f = 0; f < nf; ++f) {
                 if (is_taken(f)) continue;
                 const int d = hamming32(q0, q1, a.f_desc + (long long)fidx[f] * 32);
@@ -1433,11 +1461,14 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
                 else if (d < best2) best2 = d;
             }
         }
-        if (best <= kThLow && (float)best < a.ratio * (float)best2) {   // :327-329
-            match[fidx[bpos]] = (int32_t)((long long)s - kpo);
-            if (lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
-            ++nm;
-        }
+        const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
+        uint32_t fi = 0;
+        if (lds_fidx) fi = s_fidx[bpos];
+        else if (claim) fi = fidx[bpos];
+        int32_t* dst = claim ? match + fi : sink;
+        *dst = claim ? (int32_t)((long long)s - kpo) : 0;
+        if (claim && lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
+        nm += claim;
     }
     if (nm) atomicAdd(&a.nmatches[pr], nm);
 }
