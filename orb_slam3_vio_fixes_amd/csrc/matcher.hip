@@ -1243,6 +1243,133 @@ __global__ __launch_bounds__(256) void k_bowk_topk(BowKArgs k) {
     k.lists[slot0 + lane_id()] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
 }
 
+// The same lists with the distances on the matrix cores.  A descriptor's 256
+// bits as +-1 int8 make Hamming distance a dot product, dot = 256 - 2 ham,
+// so a (32 frame features) x (32 keyframe features) tile of a node is eight
+// v_mfma_i32_32x32x32_i8 (K = 32 bits each), exact in i32.  Operand maps
+// (checked by tools/mfma_i8_probe.hip): lane l feeds A row l & 31 and B
+// column l & 31 with the 16-element k-slice 16 (l >> 5) .. +15 of each K = 32
+// block; C holds column l & 31, rows (reg & 3) + 8 (reg >> 2) + 4 (l >> 5).
+// Here A = frame features (rows, expanded once per query by k_bowk_expand),
+// B = the wave's 32 keyframe features (columns); each lane pushes its 16
+// accumulator rows into its column's top-4, and lanes l, l ^ 32 (the other
+// 16 rows of every tile) merge at the end.
+typedef int bowk_v4i __attribute__((ext_vector_type(4)));
+typedef int bowk_v16i __attribute__((ext_vector_type(16)));
+
+// 16 bits (bit e -> byte e) as +-1 int8: four bytes per nibble spread
+__device__ __forceinline__ bowk_v4i bits_pm1(uint32_t x16) {
+    bowk_v4i o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const uint32_t nib = (x16 >> (4 * q)) & 0xfu;
+        const uint32_t t = (nib * 0x00204081u) & 0x01010101u;   // nibble bit i -> byte i, bit 0
+        o[q] = (int)(0xffffffffu ^ (t * 0xfeu));                // 1 -> 0x01, 0 -> 0xff (-1)
+    }
+    return o;
+}
+
+// frame feature fi's descriptor as +-1 int8, [dword s][half h] 16-byte slices
+__global__ __launch_bounds__(256) void k_bowk_expand(const uint8_t* __restrict__ f_desc, int n,
+                                                     bowk_v4i* __restrict__ fexp) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (feature, dword, half)
+    if (i >= n * 16) return;
+    const int fi = i >> 4, s = (i >> 1) & 7, h = i & 1;
+    const uint32_t d = ((const uint32_t*)(f_desc + (long long)fi * 32))[s];
+    fexp[i] = bits_pm1(d >> (16 * h));
+}
+
+// The block's 4 waves (128 keyframe slots) share their frame node's tiles:
+// the block expands each 32-feature tile into LDS once (8 KB, double-
+// buffered), so an A fragment is a ds_read_b128, not a re-read of the 8x
+// larger expanded descriptors from L2 by every wave.  A wave whose slots lie
+// in another node than the block's first reads its tiles from fexp.
+__global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
+    // [buffer][row * 17 + 2 s + h]: the odd row pitch (272 B) keeps a
+    // ds_read_b128 of 32 rows at one (s, h) off a single bank group
+    __shared__ bowk_v4i s_a[2][32 * 17];
+    const BowArgs& a = k.b;
+    const long long slotb = (long long)blockIdx.x * 128;
+    const long long slot0 = slotb + (long long)wave_id() * 32;
+    const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
+    if (slotb >= total) return;                      // the whole block
+    auto node_of = [&](long long slot) {             // last fl with bstart[fl] <= slot
+        int lo = 0, hi = a.f_nnodes;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (k.bstart[mid] <= slot) lo = mid;
+            else hi = mid;
+        }
+        return __builtin_amdgcn_readfirstlane(lo);
+    };
+    const int flb = node_of(slotb);
+    const int fbb = __builtin_amdgcn_readfirstlane(a.f_off[flb]);
+    const int nfb = __builtin_amdgcn_readfirstlane(a.f_off[flb + 1]) - fbb;
+    const bool live = slot0 < total;                 // buckets are padded to 64: 32 slots never straddle
+    const int fl = live ? (slot0 == slotb ? flb : node_of(slot0)) : flb;
+    const bool shared_node = fl == flb;
+    const int fb = __builtin_amdgcn_readfirstlane(a.f_off[fl]);
+    const int nf = __builtin_amdgcn_readfirstlane(a.f_off[fl + 1]) - fb;
+    const int lane = lane_id(), col = lane & 31, h = lane >> 5;
+    const uint32_t src = live ? k.slot_src[slot0 + col] : 0xffffffffu;
+    uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (src != 0xffffffffu) {
+        const uint4 q0 = *(const uint4*)(a.kf_desc + (long long)src * 32);
+        const uint4 q1 = *(const uint4*)(a.kf_desc + (long long)src * 32 + 16);
+        d[0] = q0.x; d[1] = q0.y; d[2] = q0.z; d[3] = q0.w; d[4] = q1.x; d[5] = q1.y; d[6] = q1.z; d[7] = q1.w;
+    }
+    bowk_v4i B[8];
+#pragma unroll
+    for (int s2 = 0; s2 < 8; ++s2) B[s2] = bits_pm1(d[s2] >> (16 * h));
+    uint32_t kk[kBowK];
+#pragma unroll
+    for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
+    // block-uniform loop over the block node's tiles: every thread reaches
+    // every barrier; the staged tile serves the waves of that node
+    const int ntb = (nfb + 31) / 32;
+    auto stage = [&](int tile, int buf) {
+        // thread i: row i >> 3, dword s = i & 7 (both halves)
+        const int i = threadIdx.x, row = i >> 3, s2 = i & 7;
+        const int fr = min(tile * 32 + row, nfb - 1);
+        const uint32_t w = ((const uint32_t*)(a.f_desc + (long long)a.f_idx[fbb + fr] * 32))[s2];
+        s_a[buf][row * 17 + 2 * s2] = bits_pm1(w);
+        s_a[buf][row * 17 + 2 * s2 + 1] = bits_pm1(w >> 16);
+    };
+    auto tile_mfma = [&](const bowk_v4i* ar, int t0, int nfx) {
+        bowk_v4i A[8];
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) A[s2] = ar[2 * s2];
+        bowk_v16i acc = {};
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s2], B[s2], acc, 0, 0, 0);
+#pragma unroll
+        for (int g = 0; g < 16; ++g) {
+            const int f = t0 + (g & 3) + 8 * (g >> 2) + 4 * h;
+            const uint32_t ham = (uint32_t)((256 - acc[g]) >> 1);
+            topk_push(kk, f < nfx ? ((ham << 16) | (uint32_t)f) : 0xffffffffu);
+        }
+    };
+    if (ntb > 0) stage(0, 0);
+    for (int tile = 0; tile < ntb; ++tile) {
+        __syncthreads();                             // tile's buffer written; the other one free
+        if (tile + 1 < ntb) stage(tile + 1, (tile + 1) & 1);
+        if (live && shared_node) tile_mfma(&s_a[tile & 1][col * 17 + h], tile * 32, nf);
+    }
+    if (live && !shared_node) {
+        for (int t0 = 0; t0 < nf; t0 += 32) {
+            const int fr = min(t0 + col, nf - 1);
+            tile_mfma(fexp + (long long)a.f_idx[fb + fr] * 16 + h, t0, nf);
+        }
+    }
+    if (!live) return;
+    uint32_t other[kBowK];
+#pragma unroll
+    for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)kk[t], 32, kWave);
+#pragma unroll
+    for (int t = 0; t < kBowK; ++t) topk_push(kk, other[t]);
+    if (h == 0) k.lists[slot0 + col] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+}
+
 // One wave per g: the lists of g's KF features are read lane-parallel, then
 // walked in the reference's order (uniform control flow).  The frame features
 // claimed so far in this (pair, node) -- the only ones a KF feature of it can
@@ -2898,13 +3025,14 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     static thread_local PBuf<int> g_fl, g_off, g_pr, bcount, bstart, gcount, gstart, g_rank, perm;
     static thread_local PBuf<uint32_t> slot_src;
     static thread_local PBuf<uint4> lists;
+    static thread_local PBuf<bowk_v4i> fexp;
     a.npairs = npairs;
     const long long slots = nfv + (long long)kWave * a.f_nnodes;
     int rc;
     if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bcount.alloc(a.f_nnodes)) ||
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
         (rc = gcount.alloc(a.f_nnodes)) || (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
-        (rc = perm.alloc(G)))
+        (rc = perm.alloc(G)) || (rc = fexp.alloc((size_t)std::max(1, a.f_n) * 16)))
         return rc;
     BowKArgs k;
     k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bcount = bcount.p; k.bstart = bstart.p;
@@ -2923,7 +3051,13 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     KLAUNCH(k_bowk_map, dim3(gb), dim3(256), 0, st, k);
     KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)a.f_nnodes * sizeof(int), st, k);
     KLAUNCH(k_bowk_fill, dim3(gw), dim3(256), 0, st, k);
-    KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
+    const char* mf = std::getenv("ORBM_BOW_KFLANE_MFMA");   // 0: the VALU top-4 pass (A/B)
+    if (!(mf && mf[0] == '0')) {
+        KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_n, fexp.p);
+        KLAUNCH(k_bowk_topk_mfma, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
+    } else {
+        KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
+    }
     const char* rw = std::getenv("ORBM_BOW_KFLANE_WAVE_RESOLVE");   // the wave-walk form (A/B)
     if (rw && rw[0] == '1')
         KLAUNCH(k_bowk_resolve, dim3(gw), dim3(256), (size_t)4 * ((a.f_n + 31) / 32) * sizeof(uint32_t), st, k);

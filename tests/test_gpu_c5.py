@@ -72,8 +72,8 @@ def _kps(rng, n):
     return k
 
 
-@pytest.mark.parametrize("seed,wave_resolve", [(3, "0"), (4, "0"), (3, "1")])
-def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, monkeypatch):
+@pytest.mark.parametrize("seed,wave_resolve,mfma", [(3, "0", "1"), (4, "0", "1"), (3, "1", "1"), (4, "0", "0")])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, monkeypatch):
     """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
     against the node-per-wave kernel on inputs that exercise its exactness
     argument: few frame nodes (nodes of 2-400 features, so complete and
@@ -112,6 +112,7 @@ def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, monkeypatch):
     assert m.struct.n_nodes_total > 0 and m.struct.n_fv_total > 0
     monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
     monkeypatch.setenv("ORBM_BOW_KFLANE_WAVE_RESOLVE", wave_resolve)
+    monkeypatch.setenv("ORBM_BOW_KFLANE_MFMA", mfma)
     got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
     monkeypatch.setenv("ORBM_BOW_KFLANE", "0")
     old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
