@@ -1500,12 +1500,10 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
 // more than 512 features read "taken" from the match row instead (only this
 // thread writes the node's entries of it).  Otherwise as k_bowk_resolve.
 constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
-// The walk's memory traffic is kept off its critical path: the next keyframe
-// feature's slot and list are loaded one step ahead, the frame-feature
-// indices of the block's first node come from an LDS copy, and every step
-// issues exactly one store (a claim to `match`, otherwise to a scratch
-// word), so the wait for the prefetched loads never covers a store issued
-// after them.
+// The walk's memory traffic is kept off its critical path: a thread's slots
+// and lists are read 8 steps at a time, the frame-feature indices of the
+// block's first node come from an LDS copy, and every step issues exactly one
+// store (a claim to `match`, otherwise to a scratch word).
 constexpr int kBowFidxStage = 1024;
 __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
     __shared__ uint32_t taken_s[256 * kBowLanePitch];
@@ -1542,60 +1540,67 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
     };
     const int nkf = ko[ia + 1] - ko[ia];
     int nm = 0;
-    uint32_t s_n = 0xffffffffu;
-    uint4 L_n = make_uint4(~0u, ~0u, ~0u, ~0u);
-    if (nkf > 0) {
-        s_n = k.slot_src[base];
-        L_n = k.lists[base];
-    }
-    *sink = 0;   // the first step, too, finds one store after its data's loads
-    for (int j = 0; j < nkf; ++j) {
-        const uint32_t s = s_n;
-        const uint4 L = L_n;
-        const int jn = min(j + 1, nkf - 1);
-        s_n = k.slot_src[base + jn];
-        L_n = k.lists[base + jn];
-        const bool valid = s != 0xffffffffu;                         // a valid MapPoint (:255-260)
-        const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
-        uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
+    // a thread's slots are contiguous: its walk reads them kChunk at a time
+    // (kChunk lists = one 128-B line), not one 16-B piece of a line per step,
+    // which refetched every line ~8 times from HBM once the 64 streams of a
+    // wave no longer fit the cache between steps
+    constexpr int kChunk = 8;
+    for (int j0 = 0; j0 < nkf; j0 += kChunk) {
+        uint32_t sv[kChunk];
+        uint4 Lv[kChunk];
 #pragma unroll
-        for (int q = kBowK - 1; q >= 0; --q) {                       // first two untaken keys (:275-276)
-            if (keys[q] == 0xffffffffu || is_taken((int)(keys[q] & 0xffff))) continue;
-            e2 = e1;
-            e1 = keys[q];
+        for (int c = 0; c < kChunk; ++c) {
+            const int jc = min(j0 + c, nkf - 1);
+            sv[c] = k.slot_src[base + jc];
+            Lv[c] = k.lists[base + jc];
         }
-        int best = 256, best2 = 256, bpos = 0;
-        bool exact = true;
-        const int dlast = (int)(keys[kBowK - 1] >> 16);
-        if (e1 != 0xffffffffu) {
-            best = (int)(e1 >> 16); bpos = (int)(e1 & 0xffff);
-            if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
-            else if (!complete && best <= kThLow) {
-                if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
-                else exact = false;
+#pragma unroll
+        for (int c = 0; c < kChunk; ++c) {
+            if (j0 + c >= nkf) break;
+            const uint32_t s = sv[c];
+            const uint4 L = Lv[c];
+            const bool valid = s != 0xffffffffu;                         // a valid MapPoint (:255-260)
+            const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
+            uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
+    #pragma unroll
+            for (int q = kBowK - 1; q >= 0; --q) {                       // first two untaken keys (:275-276)
+                if (keys[q] == 0xffffffffu || is_taken((int)(keys[q] & 0xffff))) continue;
+                e2 = e1;
+                e1 = keys[q];
             }
-        } else if (!complete && dlast <= kThLow) {
-            exact = false;
-        }
-        if (valid && !exact) {                                       // the reference's node loop (:266-292)
-            const uint8_t* kd = a.kf_desc + (long long)s * 32;
-            const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
-            best = 256; best2 = 256; bpos = 0;
-            for (int f = 0; f < nf; ++f) {
-                if (is_taken(f)) continue;
-                const int d = hamming32(q0, q1, a.f_desc + (long long)fidx[f] * 32);
-                if (d < best) { best2 = best; best = d; bpos = f; }
-                else if (d < best2) best2 = d;
+            int best = 256, best2 = 256, bpos = 0;
+            bool exact = true;
+            const int dlast = (int)(keys[kBowK - 1] >> 16);
+            if (e1 != 0xffffffffu) {
+                best = (int)(e1 >> 16); bpos = (int)(e1 & 0xffff);
+                if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
+                else if (!complete && best <= kThLow) {
+                    if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
+                    else exact = false;
+                }
+            } else if (!complete && dlast <= kThLow) {
+                exact = false;
             }
+            if (valid && !exact) {                                       // the reference's node loop (:266-292)
+                const uint8_t* kd = a.kf_desc + (long long)s * 32;
+                const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
+                best = 256; best2 = 256; bpos = 0;
+                for (int f = 0; f < nf; ++f) {
+                    if (is_taken(f)) continue;
+                    const int d = hamming32(q0, q1, a.f_desc + (long long)fidx[f] * 32);
+                    if (d < best) { best2 = best; best = d; bpos = f; }
+                    else if (d < best2) best2 = d;
+                }
+            }
+            const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
+            uint32_t fi = 0;
+            if (lds_fidx) fi = s_fidx[bpos];
+            else if (claim) fi = fidx[bpos];
+            int32_t* dst = claim ? match + fi : sink;
+            *dst = claim ? (int32_t)((long long)s - kpo) : 0;
+            if (claim && lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
+            nm += claim;
         }
-        const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
-        uint32_t fi = 0;
-        if (lds_fidx) fi = s_fidx[bpos];
-        else if (claim) fi = fidx[bpos];
-        int32_t* dst = claim ? match + fi : sink;
-        *dst = claim ? (int32_t)((long long)s - kpo) : 0;
-        if (claim && lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
-        nm += claim;
     }
     if (nm) atomicAdd(&a.nmatches[pr], nm);
 }
