@@ -308,7 +308,17 @@ typedef struct orbm_kf_map_device {
      * both set the search runs a lane per keyframe feature (k_bowk_*). */
     int64_t n_nodes_total;
     int64_t n_fv_total;
+    /* optional (NULL = gathered from desc): the descriptors in FeatureVector
+     * order, n_fv_total x 32, row fv_idx_off[i] + p = desc row kp_off[i] +
+     * fv_idx[fv_idx_off[i] + p]; built once per map by orbm_kf_map_fv_desc.  A
+     * (keyframe, node)'s features are then contiguous, so the map-wide search
+     * streams them instead of gathering 32-B rows across the keyframe. */
+    const uint8_t* fv_desc;
 } orbm_kf_map_device;
+
+/* Fills d_fv_desc (n_fv_total x 32 device bytes) for map->fv_desc.
+ * Asynchronous on `stream`.  Returns ORB_OK or an error. */
+int orbm_kf_map_fv_desc(const orbm_kf_map_device* map, uint8_t* d_fv_desc, void* stream);
 
 /* SearchByBoW(KF_i, F) for nkf host keyframes against one frame in one launch:
  * the relocalisation loop over candidates (src/Tracking.cc:3641-3648).

@@ -646,6 +646,7 @@ struct BowArgs {
     const uint32_t* kf_idx;
     const long long* node_off;
     const long long* idx_off;
+    const uint8_t* kf_fvdesc;   // optional: KF descriptors in FeatureVector order (orbm_kf_map_device::fv_desc)
     // frame (shared by all pairs)
     const orb_keypoint* f_kps;  const uint8_t* f_desc;  int f_n;
     const uint32_t* f_node;  const int* f_off;  const uint32_t* f_idx;  int f_nnodes;
@@ -1100,82 +1101,136 @@ struct BowKArgs {
     int* g_fl;             // [G] frame node of g, -1 if F does not hold it
     int* g_off;            // [G] offset of g's KF features in the node's bucket
     int* g_pr;             // [G] pair of g
-    int* bcount;           // [f_nnodes] KF features per frame node (zeroed)
+    unsigned long long* bgcount;   // [f_nnodes] per frame node (zeroed): lo KF features, hi g entries
     int* bstart;           // [f_nnodes + 1] bucket starts, padded to 64 slots
     uint32_t* slot_src;    // [slots] global KF feature (kp_off[pr] + ikf), ~0: none
     uint4* lists;          // [slots] kBowK smallest keys, ascending, ~0: none
-    int* gcount;           // [f_nnodes] g entries per frame node (zeroed)
     int* gstart;           // [f_nnodes + 1] their starts
     int* g_rank;           // [G] rank of g among its frame node's entries
     int* perm;             // [G] g entries ordered by frame node
+    int* chunk_node;       // [slots / 32] frame node of every 32-slot chunk
+    uint32_t* slot_pos;    // [slots] FeatureVector position (row of kf_fvdesc) when kf_fvdesc is set
 };
 
+// One block per pair (its KF nodes g are contiguous: no search for the pair
+// of g), the frame's node ids staged in LDS for the lower_bound of each KF
+// node when they fit (~100 nodes at levelsup 4)
+constexpr int kBowMapStage = 2048;
 __global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
+    __shared__ uint32_t s_fnode[kBowMapStage];
     const BowArgs& a = k.b;
-    const long long g = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= k.G) return;
-    int lo = 0, hi = a.npairs;                       // last pr with node_off[pr] <= g
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (a.node_off[mid] <= g) lo = mid;
-        else hi = mid;
-    }
-    const int pr = lo;
-    const int ia = (int)(g - a.node_off[pr]);
-    const int* ko = a.kf_off + a.node_off[pr] + pr;
-    const int nkf = ko[ia + 1] - ko[ia];
-    const uint32_t na = a.kf_node[g];
-    int fl = 0, fh = a.f_nnodes;                     // lower_bound of na in F's node ids
-    while (fl < fh) {
-        const int mid = (fl + fh) >> 1;
-        if (a.f_node[mid] < na) fl = mid + 1;
-        else fh = mid;
-    }
-    k.g_pr[g] = pr;
-    if (fl < a.f_nnodes && a.f_node[fl] == na && nkf > 0) {
-        k.g_fl[g] = fl;
-        k.g_off[g] = atomicAdd(k.bcount + fl, nkf);
-        k.g_rank[g] = atomicAdd(k.gcount + fl, 1);
-    } else {
-        k.g_fl[g] = -1;
+    const int pr = blockIdx.x;
+    const int nfn = a.f_nnodes;
+    const bool st = nfn <= kBowMapStage;
+    if (st)
+        for (int i = threadIdx.x; i < nfn; i += blockDim.x) s_fnode[i] = a.f_node[i];
+    __syncthreads();
+    const uint32_t* fnode = st ? s_fnode : a.f_node;
+    const long long g0 = a.node_off[pr], g1 = a.node_off[pr + 1];
+    const int* ko = a.kf_off + g0 + pr;
+    for (long long g = g0 + threadIdx.x; g < g1; g += blockDim.x) {
+        const int ia = (int)(g - g0);
+        const int nkf = ko[ia + 1] - ko[ia];
+        const uint32_t na = a.kf_node[g];
+        int fl = 0, fh = nfn;                        // lower_bound of na in F's node ids
+        while (fl < fh) {
+            const int mid = (fl + fh) >> 1;
+            if (fnode[mid] < na) fl = mid + 1;
+            else fh = mid;
+        }
+        k.g_pr[g] = pr;
+        if (fl < nfn && fnode[fl] == na && nkf > 0) {
+            k.g_fl[g] = fl;
+            // one atomic for both counters (a pair holds a frame node at most once, so
+            // nothing aggregates in the block; the ~100 nodes' words are contended)
+            const unsigned long long o = atomicAdd(k.bgcount + fl, (1ull << 32) | (unsigned long long)nkf);
+            k.g_off[g] = (int)(uint32_t)o;
+            k.g_rank[g] = (int)(o >> 32);
+        } else {
+            k.g_fl[g] = -1;
+        }
     }
 }
 
 __global__ __launch_bounds__(1024) void k_bowk_scan(BowKArgs k) {
     extern __shared__ int sc_s[];
     const int n = k.b.f_nnodes;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = (k.bcount[i] + kWave - 1) / kWave * kWave;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = ((int)(uint32_t)k.bgcount[i] + kWave - 1) / kWave * kWave;
     __syncthreads();
     __shared__ int tmp[1024 / kWave + 1];
     const int total = block_excl_scan(sc_s, n, tmp);
     for (int i = threadIdx.x; i < n; i += blockDim.x) k.bstart[i] = sc_s[i];
     if (threadIdx.x == 0) k.bstart[n] = total;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = k.gcount[i];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = (int)(k.bgcount[i] >> 32);
     __syncthreads();
     const int gtotal = block_excl_scan(sc_s, n, tmp);
     for (int i = threadIdx.x; i < n; i += blockDim.x) k.gstart[i] = sc_s[i];
     if (threadIdx.x == 0) k.gstart[n] = gtotal;
 }
 
-// one wave per g: lanes over g's KF features
+// the frame node of every 32-slot chunk of the buckets (a table lookup
+// instead of a binary search over bstart per top-4 wave)
+__global__ __launch_bounds__(256) void k_bowk_chunks(BowKArgs k) {
+    const int fl = blockIdx.x;
+    const int c0 = k.bstart[fl] / 32, c1 = k.bstart[fl + 1] / 32;
+    for (int c = c0 + threadIdx.x; c < c1; c += blockDim.x) k.chunk_node[c] = fl;
+}
+
+// One block per pair: every thread over the pair's KF features in
+// FeatureVector order (contiguous), each feature's node found by a search of
+// the node offsets staged in LDS together with the node's slot base (a wave
+// per node left 60 % of its lanes idle on ~38-feature nodes).  Pairs with
+// more nodes than the stage take them a wave per node.
+constexpr int kBowFillStage = 1024;
 __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
+    __shared__ int s_ko[kBowFillStage + 1];
+    __shared__ int s_base[kBowFillStage];
     const BowArgs& a = k.b;
-    const long long g = (long long)blockIdx.x * 4 + wave_id();
-    if (g >= k.G) return;
-    const int fl = k.g_fl[g];
-    if (fl < 0) return;
-    const int pr = k.g_pr[g];
-    const int ia = (int)(g - a.node_off[pr]);
-    const int* ko = a.kf_off + a.node_off[pr] + pr;
+    const int pr = blockIdx.x;
+    const long long g0 = a.node_off[pr];
+    const int nn = (int)(a.node_off[pr + 1] - g0);
+    const int* ko = a.kf_off + g0 + pr;
     const uint32_t* ki = a.kf_idx + a.idx_off[pr];
     const long long kpo = a.kp_off[pr];
-    uint32_t* dst = k.slot_src + k.bstart[fl] + k.g_off[g];
-    if (lane_id() == 0) k.perm[k.gstart[fl] + k.g_rank[g]] = (int)g;
-    const int p0 = ko[ia], p1 = ko[ia + 1];
-    for (int p = p0 + lane_id(); p < p1; p += kWave) {
+    auto slot_base = [&](int ia) -> int {            // slot of the node's feature p: base + p; -1: no frame node
+        const long long g = g0 + ia;
+        const int fl = k.g_fl[g];
+        if (fl < 0) return -1;
+        k.perm[k.gstart[fl] + k.g_rank[g]] = (int)g;
+        return k.bstart[fl] + k.g_off[g] - ko[ia];
+    };
+    const uint32_t fvo = (uint32_t)a.idx_off[pr];
+    auto put = [&](int base, int p) {
         const long long gk = kpo + (long long)ki[p];
-        dst[p - p0] = a.kf_valid[gk] ? (uint32_t)gk : 0xffffffffu;
+        k.slot_src[base + p] = a.kf_valid[gk] ? (uint32_t)gk : 0xffffffffu;
+        if (a.kf_fvdesc) k.slot_pos[base + p] = fvo + (uint32_t)p;
+    };
+    if (nn > kBowFillStage) {
+        for (int ia = wave_id(); ia < nn; ia += blockDim.x / kWave) {
+            int base = 0;
+            if (lane_id() == 0) base = slot_base(ia);
+            base = __shfl(base, 0, kWave);
+            if (base < 0) continue;
+            for (int p = ko[ia] + lane_id(); p < ko[ia + 1]; p += kWave) put(base, p);
+        }
+        return;
+    }
+    for (int ia = threadIdx.x; ia <= nn; ia += blockDim.x) {
+        s_ko[ia] = ko[ia];
+        if (ia < nn) s_base[ia] = slot_base(ia);
+    }
+    __syncthreads();
+    const int p0 = s_ko[0], p1 = s_ko[nn];
+    for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
+        int lo = 0, hi = nn;                         // last ia with s_ko[ia] <= p (empty nodes skipped)
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (s_ko[mid] <= p) lo = mid;
+            else hi = mid;
+        }
+        const int base = s_base[lo];
+        if (base >= 0) put(base, p);
     }
 }
 
@@ -1269,21 +1324,41 @@ __device__ __forceinline__ bowk_v4i bits_pm1(uint32_t x16) {
     return o;
 }
 
-// frame feature fi's descriptor as +-1 int8, [dword s][half h] 16-byte slices
-__global__ __launch_bounds__(256) void k_bowk_expand(const uint8_t* __restrict__ f_desc, int n,
+// the frame's node positions p (f_idx order: a node's features are
+// contiguous) as +-1 int8, [position][dword s][half h] 16-byte slices, so a
+// node's tile is one contiguous read with no index indirection
+__global__ __launch_bounds__(256) void k_bowk_expand(const uint8_t* __restrict__ f_desc,
+                                                     const uint32_t* __restrict__ f_idx, const int* __restrict__ npos,
                                                      bowk_v4i* __restrict__ fexp) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (feature, dword, half)
-    if (i >= n * 16) return;
-    const int fi = i >> 4, s = (i >> 1) & 7, h = i & 1;
-    const uint32_t d = ((const uint32_t*)(f_desc + (long long)fi * 32))[s];
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;   // (position, dword, half)
+    if (i >= *npos * 16) return;
+    const int p = i >> 4, s = (i >> 1) & 7, h = i & 1;
+    const uint32_t d = ((const uint32_t*)(f_desc + (long long)f_idx[p] * 32))[s];
     fexp[i] = bits_pm1(d >> (16 * h));
 }
 
+// a key without the lane half's row offset: (256 - acc) << 15 == ham << 16
+// (acc = 256 - 2 ham), plus the uniform part of the row, in one v_mad_i32_i24
+__device__ __forceinline__ uint32_t bowk_key(int acc, int neg, int kb) {
+    uint32_t d;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(acc), "v"(neg), "s"(kb));
+    return d;
+}
+
 // The block's 4 waves (128 keyframe slots) share their frame node's tiles:
-// the block expands each 32-feature tile into LDS once (8 KB, double-
-// buffered), so an A fragment is a ds_read_b128, not a re-read of the 8x
-// larger expanded descriptors from L2 by every wave.  A wave whose slots lie
-// in another node than the block's first reads its tiles from fexp.
+// the block copies each 32-feature tile of the node-ordered expansion into
+// LDS once (8 KB, double-buffered), so an A fragment is a ds_read_b128, not a
+// re-read of the 8x larger expanded descriptors from L2 by every wave.  The
+// copy is software-pipelined: tile t+2 is loaded into registers while tile t
+// is on the matrix cores, and lands in LDS after the next barrier (a barrier
+// that orders LDS only, so the load in flight is not drained by it).  A wave
+// whose slots lie in another node than the block's first reads its tiles
+// from fexp.
+__device__ __forceinline__ void bowk_lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
     // [buffer][row * 17 + 2 s + h]: the odd row pitch (272 B) keeps a
     // ds_read_b128 of 32 rows at one (s, h) off a single bank group
@@ -1294,13 +1369,7 @@ __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v
     const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
     if (slotb >= total) return;                      // the whole block
     auto node_of = [&](long long slot) {             // last fl with bstart[fl] <= slot
-        int lo = 0, hi = a.f_nnodes;
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (k.bstart[mid] <= slot) lo = mid;
-            else hi = mid;
-        }
-        return __builtin_amdgcn_readfirstlane(lo);
+        return __builtin_amdgcn_readfirstlane(k.chunk_node[slot >> 5]);
     };
     const int flb = node_of(slotb);
     const int fbb = __builtin_amdgcn_readfirstlane(a.f_off[flb]);
@@ -1314,8 +1383,12 @@ __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v
     const uint32_t src = live ? k.slot_src[slot0 + col] : 0xffffffffu;
     uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (src != 0xffffffffu) {
-        const uint4 q0 = *(const uint4*)(a.kf_desc + (long long)src * 32);
-        const uint4 q1 = *(const uint4*)(a.kf_desc + (long long)src * 32 + 16);
+        // a (keyframe, node)'s slots are consecutive FeatureVector rows: with the
+        // map's fv_desc the wave's 32 descriptors are one contiguous 1 KB read
+        const uint8_t* kd = a.kf_fvdesc ? a.kf_fvdesc + (long long)k.slot_pos[slot0 + col] * 32
+                                        : a.kf_desc + (long long)src * 32;
+        const uint4 q0 = *(const uint4*)kd;
+        const uint4 q1 = *(const uint4*)(kd + 16);
         d[0] = q0.x; d[1] = q0.y; d[2] = q0.z; d[3] = q0.w; d[4] = q1.x; d[5] = q1.y; d[6] = q1.z; d[7] = q1.w;
     }
     bowk_v4i B[8];
@@ -1324,17 +1397,9 @@ __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v
     uint32_t kk[kBowK];
 #pragma unroll
     for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
-    // block-uniform loop over the block node's tiles: every thread reaches
-    // every barrier; the staged tile serves the waves of that node
-    const int ntb = (nfb + 31) / 32;
-    auto stage = [&](int tile, int buf) {
-        // thread i: row i >> 3, dword s = i & 7 (both halves)
-        const int i = threadIdx.x, row = i >> 3, s2 = i & 7;
-        const int fr = min(tile * 32 + row, nfb - 1);
-        const uint32_t w = ((const uint32_t*)(a.f_desc + (long long)a.f_idx[fbb + fr] * 32))[s2];
-        s_a[buf][row * 17 + 2 * s2] = bits_pm1(w);
-        s_a[buf][row * 17 + 2 * s2 + 1] = bits_pm1(w >> 16);
-    };
+    const int neg = -32768;
+    // a 32x32 tile: its 16 accumulator rows of this lane into the column's
+    // top-4 (keys without + 4 h: the order of one lane's keys is the same)
     auto tile_mfma = [&](const bowk_v4i* ar, int t0, int nfx) {
         bowk_v4i A[8];
 #pragma unroll
@@ -1342,26 +1407,52 @@ __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v
         bowk_v16i acc = {};
 #pragma unroll
         for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s2], B[s2], acc, 0, 0, 0);
+        const int kb = (256 << 15) + t0;
+        if (t0 + 32 <= nfx) {
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-            const int f = t0 + (g & 3) + 8 * (g >> 2) + 4 * h;
-            const uint32_t ham = (uint32_t)((256 - acc[g]) >> 1);
-            topk_push(kk, f < nfx ? ((ham << 16) | (uint32_t)f) : 0xffffffffu);
+            for (int g = 0; g < 16; ++g) topk_push(kk, bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2)));
+        } else {
+            const int lim = nfx - t0 - 4 * h;        // rows (g & 3) + 8 (g >> 2) below it exist
+#pragma unroll
+            for (int g = 0; g < 16; ++g) {
+                const uint32_t key = bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2));
+                topk_push(kk, (g & 3) + 8 * (g >> 2) < lim ? key : 0xffffffffu);
+            }
         }
     };
-    if (ntb > 0) stage(0, 0);
+    // block-uniform loop over the block node's tiles: every thread reaches
+    // every barrier; the staged tile serves the waves of that node
+    const int ntb = (nfb + 31) / 32;
+    const int srow = threadIdx.x >> 3, ss = threadIdx.x & 7;   // staging: row, dword (both halves)
+    bowk_v4i p0, p1;
+    auto fetch = [&](int tile) {
+        const bowk_v4i* g = fexp + (long long)(fbb + min(tile * 32 + srow, nfb - 1)) * 16 + 2 * ss;
+        p0 = g[0];
+        p1 = g[1];
+    };
+    auto put = [&](int buf) {
+        s_a[buf][srow * 17 + 2 * ss] = p0;
+        s_a[buf][srow * 17 + 2 * ss + 1] = p1;
+    };
+    if (ntb > 0) { fetch(0); put(0); }
+    if (ntb > 1) fetch(1);
     for (int tile = 0; tile < ntb; ++tile) {
-        __syncthreads();                             // tile's buffer written; the other one free
-        if (tile + 1 < ntb) stage(tile + 1, (tile + 1) & 1);
+        bowk_lds_barrier();                          // tile's buffer written; the other one free
+        if (tile + 1 < ntb) {
+            put((tile + 1) & 1);
+            if (tile + 2 < ntb) fetch(tile + 2);
+        }
         if (live && shared_node) tile_mfma(&s_a[tile & 1][col * 17 + h], tile * 32, nf);
     }
     if (live && !shared_node) {
         for (int t0 = 0; t0 < nf; t0 += 32) {
             const int fr = min(t0 + col, nf - 1);
-            tile_mfma(fexp + (long long)a.f_idx[fb + fr] * 16 + h, t0, nf);
+            tile_mfma(fexp + (long long)(fb + fr) * 16 + h, t0, nf);
         }
     }
     if (!live) return;
+#pragma unroll
+    for (int t = 0; t < kBowK; ++t) kk[t] = kk[t] == 0xffffffffu ? kk[t] : kk[t] + 4u * (uint32_t)h;
     uint32_t other[kBowK];
 #pragma unroll
     for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)kk[t], 32, kWave);
@@ -1505,6 +1596,12 @@ constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
 // block's first node come from an LDS copy, and every step issues exactly one
 // store (a claim to `match`, otherwise to a scratch word).
 constexpr int kBowFidxStage = 1024;
+// Exact rescans (a list that cannot decide) are done by the whole wave: the
+// walk runs in wave-uniform steps (the wave's longest walk), and at each step
+// the lanes needing a rescan are served one after the other with the node's
+// features spread over the 64 lanes (the rescanning lane's claimed positions
+// read from its LDS bitmap, or its match row for large nodes), instead of a
+// serial loop over the whole node by the one lane while the wave waits.
 __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
     __shared__ uint32_t taken_s[256 * kBowLanePitch];
     __shared__ uint16_t s_fidx[kBowFidxStage];
@@ -1519,87 +1616,127 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
         for (int p = threadIdx.x; p < nf0; p += blockDim.x) s_fidx[p] = (uint16_t)a.f_idx[fb0 + p];
     __syncthreads();
     const int t = tb + threadIdx.x;
-    if (t >= ntot) return;
-    const long long g = k.perm[t];
-    const int fl = k.g_fl[g];
-    const int pr = k.g_pr[g];
-    const int ia = (int)(g - a.node_off[pr]);
-    const int* ko = a.kf_off + a.node_off[pr] + pr;
-    const long long base = (long long)k.bstart[fl] + k.g_off[g];
-    const int fb = a.f_off[fl], nf = a.f_off[fl + 1] - fb;
-    const bool complete = nf <= kBowK, lds_bits = nf <= 32 * kBowLaneWords, lds_fidx = st0 && fl == fl0;
+    const int lane = lane_id();
+    if (tb + (int)threadIdx.x - lane >= ntot) return;              // the whole wave
+    const bool have = t < ntot;
+    long long base = 0, kpo = 0;
+    int fb = 0, nf = 0, nkf = 0, pr = 0, fl = -1;
+    if (have) {
+        const long long g = k.perm[t];
+        fl = k.g_fl[g];
+        pr = k.g_pr[g];
+        const int ia = (int)(g - a.node_off[pr]);
+        const int* ko = a.kf_off + a.node_off[pr] + pr;
+        base = (long long)k.bstart[fl] + k.g_off[g];
+        fb = a.f_off[fl];
+        nf = a.f_off[fl + 1] - fb;
+        kpo = a.kp_off[pr];
+        nkf = ko[ia + 1] - ko[ia];
+    }
+    const bool complete = nf <= kBowK, lds_bits = nf <= 32 * kBowLaneWords;
+    const bool lds_fidx = have && st0 && fl == fl0;
     int32_t* match = a.match + (long long)pr * a.f_n;
     const uint32_t* fidx = a.f_idx + fb;
-    const long long kpo = a.kp_off[pr];
     int32_t* sink = k.g_rank + t;                                  // scratch (g_rank is k_bowk_fill's)
     uint32_t* taken = taken_s + threadIdx.x * kBowLanePitch;
 #pragma unroll
     for (int i = 0; i < kBowLaneWords; ++i) taken[i] = 0;
-    auto is_taken = [&](int f) -> bool {
-        return lds_bits ? ((taken[f >> 5] >> (f & 31)) & 1u) : match[fidx[f]] >= 0;
-    };
-    const int nkf = ko[ia + 1] - ko[ia];
+    const int nkf_max = -wave_min(-nkf, 0);
     int nm = 0;
     // a thread's slots are contiguous: its walk reads them kChunk at a time
     // (kChunk lists = one 128-B line), not one 16-B piece of a line per step,
     // which refetched every line ~8 times from HBM once the 64 streams of a
     // wave no longer fit the cache between steps
     constexpr int kChunk = 8;
-    for (int j0 = 0; j0 < nkf; j0 += kChunk) {
+    for (int j0 = 0; j0 < nkf_max; j0 += kChunk) {
         uint32_t sv[kChunk];
         uint4 Lv[kChunk];
 #pragma unroll
         for (int c = 0; c < kChunk; ++c) {
-            const int jc = min(j0 + c, nkf - 1);
-            sv[c] = k.slot_src[base + jc];
-            Lv[c] = k.lists[base + jc];
+            sv[c] = 0xffffffffu;
+            Lv[c] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+        if (j0 < nkf) {
+#pragma unroll
+            for (int c = 0; c < kChunk; ++c) {
+                const int jc = min(j0 + c, nkf - 1);
+                sv[c] = k.slot_src[base + jc];
+                Lv[c] = k.lists[base + jc];
+            }
         }
 #pragma unroll
         for (int c = 0; c < kChunk; ++c) {
-            if (j0 + c >= nkf) break;
-            const uint32_t s = sv[c];
+            const bool act = j0 + c < nkf;
+            const uint32_t s = act ? sv[c] : 0xffffffffu;
             const uint4 L = Lv[c];
             const bool valid = s != 0xffffffffu;                         // a valid MapPoint (:255-260)
             const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
             uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
-    #pragma unroll
-            for (int q = kBowK - 1; q >= 0; --q) {                       // first two untaken keys (:275-276)
-                if (keys[q] == 0xffffffffu || is_taken((int)(keys[q] & 0xffff))) continue;
-                e2 = e1;
-                e1 = keys[q];
-            }
             int best = 256, best2 = 256, bpos = 0;
             bool exact = true;
-            const int dlast = (int)(keys[kBowK - 1] >> 16);
-            if (e1 != 0xffffffffu) {
-                best = (int)(e1 >> 16); bpos = (int)(e1 & 0xffff);
-                if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
-                else if (!complete && best <= kThLow) {
-                    if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
-                    else exact = false;
+            if (valid) {
+#pragma unroll
+                for (int q = kBowK - 1; q >= 0; --q) {                   // first two untaken keys (:275-276)
+                    if (keys[q] == 0xffffffffu) continue;
+                    const int f = (int)(keys[q] & 0xffff);
+                    if (lds_bits ? ((taken[f >> 5] >> (f & 31)) & 1u) : match[fidx[f]] >= 0) continue;
+                    e2 = e1;
+                    e1 = keys[q];
                 }
-            } else if (!complete && dlast <= kThLow) {
-                exact = false;
+                const int dlast = (int)(keys[kBowK - 1] >> 16);
+                if (e1 != 0xffffffffu) {
+                    best = (int)(e1 >> 16); bpos = (int)(e1 & 0xffff);
+                    if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
+                    else if (!complete && best <= kThLow) {
+                        if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
+                        else exact = false;
+                    }
+                } else if (!complete && dlast <= kThLow) {
+                    exact = false;
+                }
             }
-            if (valid && !exact) {                                       // the reference's node loop (:266-292)
-                const uint8_t* kd = a.kf_desc + (long long)s * 32;
+            // the reference's node loop (:266-292) for each lane that needs it,
+            // the node's features over the wave's lanes
+            uint64_t need = __ballot(valid && !exact);
+            while (need) {
+                const int i = __builtin_ctzll(need);
+                need &= need - 1;
+                const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)s, i);
+                const int nfi = __builtin_amdgcn_readlane(nf, i), fbi = __builtin_amdgcn_readlane(fb, i);
+                const int pri = __builtin_amdgcn_readlane(pr, i);
+                const uint32_t* tki = taken_s + (threadIdx.x - lane + i) * kBowLanePitch;
+                const int32_t* mi = a.match + (long long)pri * a.f_n;
+                const bool lbi = nfi <= 32 * kBowLaneWords;
+                const uint8_t* kd = a.kf_desc + (long long)si * 32;
                 const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
-                best = 256; best2 = 256; bpos = 0;
-                for (int f = 0; f < nf; ++f) {
-                    if (is_taken(f)) continue;
-                    const int d = hamming32(q0, q1, a.f_desc + (long long)fidx[f] * 32);
-                    if (d < best) { best2 = best; best = d; bpos = f; }
-                    else if (d < best2) best2 = d;
+                uint32_t m1 = (uint32_t)INT_MAX, m2 = (uint32_t)INT_MAX;   // wave_min works on ints
+                for (int f = lane; f < nfi; f += kWave) {
+                    const uint32_t fi = a.f_idx[fbi + f];
+                    if (lbi ? ((tki[f >> 5] >> (f & 31)) & 1u) : mi[fi] >= 0) continue;
+                    const uint32_t key = ((uint32_t)hamming32(q0, q1, a.f_desc + (long long)fi * 32) << 16) | (uint32_t)f;
+                    m2 = min(m2, max(m1, key));
+                    m1 = min(m1, key);
+                }
+                // first and second minima over the lanes (keys < 2^25: positive ints)
+                const int a1 = wave_min((int)m1, INT_MAX);
+                const int own = (m1 == (uint32_t)a1) ? (int)m2 : (int)m1;
+                const int a2 = wave_min(own, INT_MAX);
+                if (lane == i) {
+                    best = a1 == INT_MAX ? 256 : (a1 >> 16);
+                    best2 = a2 == INT_MAX ? 256 : (a2 >> 16);
+                    bpos = a1 == INT_MAX ? 0 : (a1 & 0xffff);
                 }
             }
-            const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
-            uint32_t fi = 0;
-            if (lds_fidx) fi = s_fidx[bpos];
-            else if (claim) fi = fidx[bpos];
-            int32_t* dst = claim ? match + fi : sink;
-            *dst = claim ? (int32_t)((long long)s - kpo) : 0;
-            if (claim && lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
-            nm += claim;
+            if (act) {
+                const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
+                uint32_t fi = 0;
+                if (lds_fidx) fi = s_fidx[bpos];
+                else if (claim) fi = fidx[bpos];
+                int32_t* dst = claim ? match + fi : sink;
+                *dst = claim ? (int32_t)((long long)s - kpo) : 0;
+                if (claim && lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
+                nm += claim;
+            }
         }
     }
     if (nm) atomicAdd(&a.nmatches[pr], nm);
@@ -2803,6 +2940,21 @@ static int device_ok() {
     return ORB_OK;
 }
 
+// the map's descriptors in FeatureVector order, one block per keyframe
+__global__ __launch_bounds__(256) void k_fv_desc(const uint8_t* __restrict__ desc, const long long* __restrict__ kp_off,
+                                                 const int* __restrict__ fv_off, const uint32_t* __restrict__ fv_idx,
+                                                 const long long* __restrict__ node_off,
+                                                 const long long* __restrict__ idx_off, uint8_t* __restrict__ out) {
+    const int i = blockIdx.x;
+    const long long nn = node_off[i + 1] - node_off[i];
+    const int n = fv_off[node_off[i] + i + nn];        // the keyframe's FeatureVector entries
+    const long long io = idx_off[i], ko = kp_off[i];
+    for (int q = threadIdx.x; q < 2 * n; q += blockDim.x) {   // 16-byte halves
+        const int p = q >> 1, h = q & 1;
+        ((uint4*)out)[(io + p) * 2 + h] = ((const uint4*)desc)[(ko + fv_idx[io + p]) * 2 + h];
+    }
+}
+
 }  // namespace orbmi
 
 using namespace orbmi;
@@ -3027,25 +3179,27 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 // G: (pair, KF node) entries of the map, nfv: its FeatureVector entries (host
 // totals of the resident map: scratch is sized without reading the device).
 static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
-    static thread_local PBuf<int> g_fl, g_off, g_pr, bcount, bstart, gcount, gstart, g_rank, perm;
-    static thread_local PBuf<uint32_t> slot_src;
+    static thread_local PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node;
+    static thread_local PBuf<unsigned long long> bgcount;
+    static thread_local PBuf<uint32_t> slot_src, slot_pos;
     static thread_local PBuf<uint4> lists;
     static thread_local PBuf<bowk_v4i> fexp;
     a.npairs = npairs;
     const long long slots = nfv + (long long)kWave * a.f_nnodes;
     int rc;
-    if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bcount.alloc(a.f_nnodes)) ||
+    if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc(a.f_nnodes)) ||
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
-        (rc = gcount.alloc(a.f_nnodes)) || (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
-        (rc = perm.alloc(G)) || (rc = fexp.alloc((size_t)std::max(1, a.f_n) * 16)))
+        (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
+        (rc = perm.alloc(G)) || (rc = fexp.alloc((size_t)std::max(1, a.f_n) * 16)) ||
+        (rc = chunk_node.alloc(slots / 32 + 1)) || (a.kf_fvdesc && (rc = slot_pos.alloc(slots))))
         return rc;
     BowKArgs k;
-    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bcount = bcount.p; k.bstart = bstart.p;
+    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bgcount = bgcount.p; k.bstart = bstart.p;
     k.slot_src = slot_src.p; k.lists = lists.p;
-    k.gcount = gcount.p; k.gstart = gstart.p; k.g_rank = g_rank.p; k.perm = perm.p;
+    k.gstart = gstart.p; k.g_rank = g_rank.p; k.perm = perm.p; k.chunk_node = chunk_node.p;
+    k.slot_pos = slot_pos.p;
     ORB_CHECK(flush_uploads());
-    ORB_CHECK(hipMemsetAsync(bcount.p, 0, (size_t)a.f_nnodes * sizeof(int), st));
-    ORB_CHECK(hipMemsetAsync(gcount.p, 0, (size_t)a.f_nnodes * sizeof(int), st));
+    ORB_CHECK(hipMemsetAsync(bgcount.p, 0, (size_t)a.f_nnodes * sizeof(unsigned long long), st));
     ORB_CHECK(hipMemsetAsync(slot_src.p, 0xff, (size_t)slots * sizeof(uint32_t), st));
     {
         const long long nmf = (long long)npairs * a.f_n;
@@ -3053,12 +3207,14 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
     }
     const unsigned gb = (unsigned)((G + 255) / 256), gw = (unsigned)((G + 3) / 4);
-    KLAUNCH(k_bowk_map, dim3(gb), dim3(256), 0, st, k);
+    KLAUNCH(k_bowk_map, dim3(npairs), dim3(256), 0, st, k);
     KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)a.f_nnodes * sizeof(int), st, k);
-    KLAUNCH(k_bowk_fill, dim3(gw), dim3(256), 0, st, k);
+    KLAUNCH(k_bowk_fill, dim3(npairs), dim3(256), 0, st, k);
     const char* mf = std::getenv("ORBM_BOW_KFLANE_MFMA");   // 0: the VALU top-4 pass (A/B)
     if (!(mf && mf[0] == '0')) {
-        KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_n, fexp.p);
+        KLAUNCH(k_bowk_chunks, dim3(a.f_nnodes), dim3(256), 0, st, k);
+        KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_idx,
+                a.f_off + a.f_nnodes, fexp.p);
         KLAUNCH(k_bowk_topk_mfma, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
     } else {
         KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
@@ -3072,6 +3228,15 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
+int orbm_kf_map_fv_desc(const orbm_kf_map_device* map, uint8_t* d_fv_desc, void* stream) {
+    if (!map || !d_fv_desc || map->nkf < 0) return ORB_ERR_PARAM;
+    if (map->nkf == 0) return ORB_OK;
+    hipStream_t st = (hipStream_t)stream;
+    KLAUNCH(k_fv_desc, dim3(map->nkf), dim3(256), 0, st, map->desc, (const long long*)map->kp_off, map->fv_off,
+            map->fv_idx, (const long long*)map->fv_node_off, (const long long*)map->fv_idx_off, d_fv_desc);
+    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+}
+
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f, const orbm_featvec* ffv,
                                     float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
     if (!map || !f || !ffv || !d_match || !d_nmatches || map->nkf < 0) return ORB_ERR_PARAM;
@@ -3080,6 +3245,7 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     a.kf_kps = map->kps; a.kf_desc = map->desc; a.kf_valid = map->valid; a.kp_off = (const long long*)map->kp_off;
     a.kf_node = map->fv_node; a.kf_off = map->fv_off; a.kf_idx = map->fv_idx;
     a.node_off = (const long long*)map->fv_node_off; a.idx_off = (const long long*)map->fv_idx_off;
+    a.kf_fvdesc = map->n_fv_total < 0xffffffffll ? map->fv_desc : nullptr;
     a.f_kps = f->kps; a.f_desc = f->desc; a.f_n = f->n; a.f_node = ffv->node_ids; a.f_off = ffv->offsets;
     a.f_idx = ffv->idx; a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
     a.match = d_match; a.nmatches = d_nmatches;

@@ -19,7 +19,7 @@ class OrbmKfMapDevice(C.Structure):
     _fields_ = [("nkf", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("valid", C.c_void_p),
                 ("kp_off", C.c_void_p), ("fv_node", C.c_void_p), ("fv_off", C.c_void_p), ("fv_idx", C.c_void_p),
                 ("fv_node_off", C.c_void_p), ("fv_idx_off", C.c_void_p),
-                ("n_nodes_total", C.c_int64), ("n_fv_total", C.c_int64)]
+                ("n_nodes_total", C.c_int64), ("n_fv_total", C.c_int64), ("fv_desc", C.c_void_p)]
 
 
 def featvec_csr(node_of_feature: np.ndarray):
@@ -34,8 +34,9 @@ def featvec_csr(node_of_feature: np.ndarray):
 
 
 class DeviceKeyframeMap:
-    def __init__(self, keyframes, device="cuda"):
-        """keyframes: iterable of (kps KEYPOINT_DTYPE[n], desc u8[n,32], valid u8[n], node_of_feature i[n])."""
+    def __init__(self, keyframes, device="cuda", fv_desc=True):
+        """keyframes: iterable of (kps KEYPOINT_DTYPE[n], desc u8[n,32], valid u8[n], node_of_feature i[n]).
+        fv_desc: also keep the descriptors in FeatureVector order (map->fv_desc)."""
         import torch
         kps, desc, valid, nodes, offs, idxs = [], [], [], [], [], []
         kp_off, node_off, idx_off = [0], [0], []
@@ -60,7 +61,16 @@ class DeviceKeyframeMap:
         p = lambda name: self.t[name].data_ptr()
         self.struct = OrbmKfMapDevice(self.nkf, p("kps"), p("desc"), p("valid"), p("kp_off"), p("fv_node"),
                                       p("fv_off"), p("fv_idx"), p("fv_node_off"), p("fv_idx_off"),
-                                      node_off[-1], sum(len(x) for x in idxs))
+                                      node_off[-1], sum(len(x) for x in idxs), None)
+        # the descriptors in FeatureVector order (orbm_kf_map_fv_desc), once per map
+        nfv = self.struct.n_fv_total
+        self.t["fv_desc"] = torch.empty(max(1, nfv) * 32, dtype=torch.uint8, device=device)
+        if fv_desc and self.nkf > 0 and torch.device(device).type == "cuda":
+            st = torch.cuda.current_stream(self.t["fv_desc"].device).cuda_stream
+            rc = capi.lib().orbm_kf_map_fv_desc(C.byref(self.struct), C.c_void_p(self.t["fv_desc"].data_ptr()),
+                                                C.c_void_p(st))
+            capi.check(rc, "orbm_kf_map_fv_desc")
+            self.struct.fv_desc = self.t["fv_desc"].data_ptr()
 
     def search_by_bow(self, kps, desc, node_of_feature, nnratio=0.75, check_ori=True, stream=None):
         """SearchByBoW(KF_i, F) for every keyframe: returns (match [nkf, N] int32

@@ -72,8 +72,10 @@ def _kps(rng, n):
     return k
 
 
-@pytest.mark.parametrize("seed,wave_resolve,mfma", [(3, "0", "1"), (4, "0", "1"), (3, "1", "1"), (4, "0", "0")])
-def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, monkeypatch):
+@pytest.mark.parametrize("seed,wave_resolve,mfma,fv_desc", [(3, "0", "1", True), (3, "0", "1", False),
+                                                             (4, "0", "1", True), (3, "1", "1", True),
+                                                             (4, "0", "0", True)])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monkeypatch):
     """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
     against the node-per-wave kernel on inputs that exercise its exactness
     argument: few frame nodes (nodes of 2-400 features, so complete and
@@ -108,8 +110,12 @@ def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, monkeypatch):
         nid[rng.random(len(src)) < 0.05] = 99999          # a node the frame lacks
         valid = (rng.random(len(src)) < 0.85).astype(np.uint8)
         kfs.append((kk, kd, valid, nid))
-    m = kfmap.DeviceKeyframeMap(kfs)
+    m = kfmap.DeviceKeyframeMap(kfs, fv_desc=fv_desc)
     assert m.struct.n_nodes_total > 0 and m.struct.n_fv_total > 0
+    assert bool(m.struct.fv_desc) == fv_desc
+    if fv_desc:   # orbm_kf_map_fv_desc: row fv_idx_off[i] + p = descriptor fv_idx[.] of keyframe i
+        want = np.concatenate([kd[kfmap.featvec_csr(nid)[2]] for kk, kd, valid, nid in kfs])
+        np.testing.assert_array_equal(m.t["fv_desc"].cpu().numpy().reshape(-1, 32)[:len(want)], want)
     monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
     monkeypatch.setenv("ORBM_BOW_KFLANE_WAVE_RESOLVE", wave_resolve)
     monkeypatch.setenv("ORBM_BOW_KFLANE_MFMA", mfma)
