@@ -1313,13 +1313,16 @@ typedef int bowk_v4i __attribute__((ext_vector_type(4)));
 typedef int bowk_v16i __attribute__((ext_vector_type(16)));
 
 // 16 bits (bit e -> byte e) as +-1 int8: four bytes per nibble spread
+// (per nibble: bit i -> byte i as 4 (bfe, v_mul_u32_u24, and), then one v_perm
+// picking byte 0x01 (selector 4) or 0xff (selector 0) -- no quarter-rate
+// v_mul_lo_u32)
 __device__ __forceinline__ bowk_v4i bits_pm1(uint32_t x16) {
     bowk_v4i o;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const uint32_t nib = (x16 >> (4 * q)) & 0xfu;
-        const uint32_t t = (nib * 0x00204081u) & 0x01010101u;   // nibble bit i -> byte i, bit 0
-        o[q] = (int)(0xffffffffu ^ (t * 0xfeu));                // 1 -> 0x01, 0 -> 0xff (-1)
+        const uint32_t sel = (nib * 0x00810204u) & 0x04040404u;   // nibble bit i -> byte i, value 4
+        o[q] = (int)__builtin_amdgcn_perm(0x01010101u, 0xffffffffu, sel);
     }
     return o;
 }
@@ -1602,25 +1605,42 @@ constexpr int kBowFidxStage = 1024;
 // features spread over the 64 lanes (the rescanning lane's claimed positions
 // read from its LDS bitmap, or its match row for large nodes), instead of a
 // serial loop over the whole node by the one lane while the wave waits.
-__global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
-    __shared__ uint32_t taken_s[256 * kBowLanePitch];
-    __shared__ uint16_t s_fidx[kBowFidxStage];
+// BIG = false: 256-thread blocks, nodes of <= 512 features (17 words of LDS
+// bitmap a thread); with big_pitch > 0 the larger nodes are left to the BIG
+// form (one wave a block, a bitmap of big_pitch words a thread covering every
+// frame position), whose few long walks set the kernel's tail: their "taken"
+// checks then cost an LDS read, not two dependent global loads into the
+// match row.  big_pitch = 0: the 256-thread form takes every node (match-row
+// checks above 512 features).
+template <bool BIG, bool ALL_LDS>
+__global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_pitch) {
+    extern __shared__ uint32_t taken_dyn[];                        // BIG: blockDim x big_pitch words
+    __shared__ uint32_t taken_st[BIG ? 1 : 256 * kBowLanePitch];
+    __shared__ uint16_t s_fidx[BIG ? 1 : kBowFidxStage];
     const BowArgs& a = k.b;
     const int ntot = k.gstart[a.f_nnodes];
     const int tb = blockIdx.x * blockDim.x;
     if (tb >= ntot) return;                                        // the whole block
     const int fl0 = k.g_fl[k.perm[tb]];
     const int fb0 = a.f_off[fl0], nf0 = a.f_off[fl0 + 1] - fb0;
-    const bool st0 = nf0 <= kBowFidxStage;
+    const bool st0 = !BIG && nf0 <= kBowFidxStage;
     if (st0)
         for (int p = threadIdx.x; p < nf0; p += blockDim.x) s_fidx[p] = (uint16_t)a.f_idx[fb0 + p];
     __syncthreads();
     const int t = tb + threadIdx.x;
     const int lane = lane_id();
     if (tb + (int)threadIdx.x - lane >= ntot) return;              // the whole wave
-    const bool have = t < ntot;
+    const int kSmall = 32 * kBowLaneWords;
+    const int pitch = BIG ? big_pitch : kBowLanePitch;
+    bool have = t < ntot;
     long long base = 0, kpo = 0;
     int fb = 0, nf = 0, nkf = 0, pr = 0, fl = -1;
+    if (have) {
+        const int flt = k.g_fl[k.perm[t]];
+        const int nft = a.f_off[flt + 1] - a.f_off[flt];
+        have = BIG ? nft > kSmall : (big_pitch == 0 || nft <= kSmall);
+    }
+    if (BIG && !__ballot(have)) return;                            // the whole wave
     if (have) {
         const long long g = k.perm[t];
         fl = k.g_fl[g];
@@ -1633,36 +1653,46 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
         kpo = a.kp_off[pr];
         nkf = ko[ia + 1] - ko[ia];
     }
-    const bool complete = nf <= kBowK, lds_bits = nf <= 32 * kBowLaneWords;
+    const bool complete = nf <= kBowK, lds_bits = BIG || nf <= kSmall;
     const bool lds_fidx = have && st0 && fl == fl0;
     int32_t* match = a.match + (long long)pr * a.f_n;
     const uint32_t* fidx = a.f_idx + fb;
-    int32_t* sink = k.g_rank + t;                                  // scratch (g_rank is k_bowk_fill's)
-    uint32_t* taken = taken_s + threadIdx.x * kBowLanePitch;
+    int32_t* sink;                                                 // scratch (g_rank is k_bowk_fill's)
+    uint32_t* const taken_s = BIG ? taken_dyn : taken_st;
+    uint32_t* taken = taken_s + threadIdx.x * pitch;
+    if (BIG) {
+        if (have)
+            for (int i = 0; i < (nf + 31) / 32; ++i) taken[i] = 0;
+    } else {
 #pragma unroll
-    for (int i = 0; i < kBowLaneWords; ++i) taken[i] = 0;
+        for (int i = 0; i < kBowLaneWords; ++i) taken[i] = 0;
+    }
     const int nkf_max = -wave_min(-nkf, 0);
+    // wave-uniform: every lane's frame indices come from the block's LDS copy
+    const bool wave_lds_fidx = __ballot(have && !lds_fidx) == 0;
+    // the walk is branch-free per lane (selects, not exec-mask round trips
+    // between the vector and the scalar unit, which stalled its issue ~58 % of
+    // the time): the taken checks read the bitmap at clamped positions, the
+    // bitmap update and the claim store run for every lane with a neutral
+    // value, and the only branch per step is the wave's rescan test
+    constexpr bool all_lds = BIG || ALL_LDS;                       // every lane's bitmap in LDS (big_pitch > 0)
+    const int nfc = max(nf, 1) - 1;
+    sink = k.g_rank + min(t, ntot - 1);
     int nm = 0;
     // a thread's slots are contiguous: its walk reads them kChunk at a time
     // (kChunk lists = one 128-B line), not one 16-B piece of a line per step,
     // which refetched every line ~8 times from HBM once the 64 streams of a
     // wave no longer fit the cache between steps
     constexpr int kChunk = 8;
+    const int nkc = max(nkf, 1) - 1;
     for (int j0 = 0; j0 < nkf_max; j0 += kChunk) {
         uint32_t sv[kChunk];
         uint4 Lv[kChunk];
 #pragma unroll
         for (int c = 0; c < kChunk; ++c) {
-            sv[c] = 0xffffffffu;
-            Lv[c] = make_uint4(~0u, ~0u, ~0u, ~0u);
-        }
-        if (j0 < nkf) {
-#pragma unroll
-            for (int c = 0; c < kChunk; ++c) {
-                const int jc = min(j0 + c, nkf - 1);
-                sv[c] = k.slot_src[base + jc];
-                Lv[c] = k.lists[base + jc];
-            }
+            const int jc = min(j0 + c, nkc);
+            sv[c] = k.slot_src[base + jc];
+            Lv[c] = k.lists[base + jc];
         }
 #pragma unroll
         for (int c = 0; c < kChunk; ++c) {
@@ -1672,29 +1702,35 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
             const bool valid = s != 0xffffffffu;                         // a valid MapPoint (:255-260)
             const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
             uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
-            int best = 256, best2 = 256, bpos = 0;
-            bool exact = true;
-            if (valid) {
+            bool tk[kBowK];
+            if constexpr (all_lds) {
 #pragma unroll
-                for (int q = kBowK - 1; q >= 0; --q) {                   // first two untaken keys (:275-276)
-                    if (keys[q] == 0xffffffffu) continue;
-                    const int f = (int)(keys[q] & 0xffff);
-                    if (lds_bits ? ((taken[f >> 5] >> (f & 31)) & 1u) : match[fidx[f]] >= 0) continue;
-                    e2 = e1;
-                    e1 = keys[q];
+                for (int q = 0; q < kBowK; ++q) {
+                    const int f = min((int)(keys[q] & 0xffff), nfc);
+                    tk[q] = (taken[f >> 5] >> (f & 31)) & 1u;
                 }
-                const int dlast = (int)(keys[kBowK - 1] >> 16);
-                if (e1 != 0xffffffffu) {
-                    best = (int)(e1 >> 16); bpos = (int)(e1 & 0xffff);
-                    if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
-                    else if (!complete && best <= kThLow) {
-                        if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
-                        else exact = false;
-                    }
-                } else if (!complete && dlast <= kThLow) {
-                    exact = false;
+            } else {
+#pragma unroll
+                for (int q = 0; q < kBowK; ++q) {
+                    const int f = min((int)(keys[q] & 0xffff), nfc);
+                    tk[q] = lds_bits ? ((taken[f >> 5] >> (f & 31)) & 1u) : (have && match[fidx[f]] >= 0);
                 }
             }
+#pragma unroll
+            for (int q = kBowK - 1; q >= 0; --q) {                       // first two untaken keys (:275-276)
+                const bool u = keys[q] != 0xffffffffu && !tk[q];
+                e2 = u ? e1 : e2;
+                e1 = u ? keys[q] : e1;
+            }
+            const int dlast = (int)(keys[kBowK - 1] >> 16);
+            const bool h1 = e1 != 0xffffffffu, h2 = e2 != 0xffffffffu;
+            int best = h1 ? (int)(e1 >> 16) : 256;
+            int bpos = h1 ? (int)(e1 & 0xffff) : 0;
+            // with one untaken key, dlast bounds the second from below: decided
+            // when even dlast passes the ratio test
+            const bool bound_ok = a.ratio > 0.f && (float)best < a.ratio * (float)dlast;
+            int best2 = h2 ? (int)(e2 >> 16) : ((h1 && !complete && best <= kThLow && bound_ok) ? dlast : 256);
+            const bool exact = complete || (h1 ? (h2 || best > kThLow || bound_ok) : dlast > kThLow);
             // the reference's node loop (:266-292) for each lane that needs it,
             // the node's features over the wave's lanes
             uint64_t need = __ballot(valid && !exact);
@@ -1704,9 +1740,9 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
                 const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)s, i);
                 const int nfi = __builtin_amdgcn_readlane(nf, i), fbi = __builtin_amdgcn_readlane(fb, i);
                 const int pri = __builtin_amdgcn_readlane(pr, i);
-                const uint32_t* tki = taken_s + (threadIdx.x - lane + i) * kBowLanePitch;
+                const uint32_t* tki = taken_s + (threadIdx.x - lane + i) * pitch;
                 const int32_t* mi = a.match + (long long)pri * a.f_n;
-                const bool lbi = nfi <= 32 * kBowLaneWords;
+                const bool lbi = BIG || nfi <= kSmall;
                 const uint8_t* kd = a.kf_desc + (long long)si * 32;
                 const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
                 uint32_t m1 = (uint32_t)INT_MAX, m2 = (uint32_t)INT_MAX;   // wave_min works on ints
@@ -1727,16 +1763,19 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k) {
                     bpos = a1 == INT_MAX ? 0 : (a1 & 0xffff);
                 }
             }
-            if (act) {
-                const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
-                uint32_t fi = 0;
-                if (lds_fidx) fi = s_fidx[bpos];
-                else if (claim) fi = fidx[bpos];
-                int32_t* dst = claim ? match + fi : sink;
-                *dst = claim ? (int32_t)((long long)s - kpo) : 0;
-                if (claim && lds_bits) taken[bpos >> 5] |= 1u << (bpos & 31);
-                nm += claim;
+            const bool claim = valid && best <= kThLow && (float)best < a.ratio * (float)best2;   // :327-329
+            bpos = min(bpos, nfc);
+            uint32_t fi;
+            if (wave_lds_fidx) fi = s_fidx[min(bpos, kBowFidxStage - 1)];
+            else fi = lds_fidx ? s_fidx[min(bpos, kBowFidxStage - 1)] : fidx[claim ? bpos : 0];
+            int32_t* dst = claim ? match + fi : sink;
+            *dst = claim ? (int32_t)((long long)s - kpo) : 0;
+            if constexpr (all_lds) {
+                taken[bpos >> 5] |= (claim ? 1u : 0u) << (bpos & 31);
+            } else if (claim && lds_bits) {
+                taken[bpos >> 5] |= 1u << (bpos & 31);
             }
+            nm += claim;
         }
     }
     if (nm) atomicAdd(&a.nmatches[pr], nm);
@@ -3223,7 +3262,20 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     if (rw && rw[0] == '1')
         KLAUNCH(k_bowk_resolve, dim3(gw), dim3(256), (size_t)4 * ((a.f_n + 31) / 32) * sizeof(uint32_t), st, k);
     else
-        KLAUNCH(k_bowk_resolve_lane, dim3(gb), dim3(256), 0, st, k);
+    {
+        // the BIG form when a bitmap over every frame position fits 64 threads' LDS
+        const int words = (a.f_n + 31) / 32, bp = a.f_n > 32 * kBowLaneWords ? (words | 1) : 0;
+        const size_t big_lds = (size_t)64 * bp * sizeof(uint32_t);
+        const char* bg = std::getenv("ORBM_BOWK_BIG");   // 0: the 256-thread form takes every node (A/B)
+        const int big_pitch = big_lds <= 64 * 1024 && !(bg && bg[0] == '0') ? bp : 0;
+        if (big_pitch) {
+            KLAUNCH((k_bowk_resolve_lane<false, true>), dim3(gb), dim3(256), 0, st, k, big_pitch);
+            KLAUNCH((k_bowk_resolve_lane<true, true>), dim3((unsigned)((G + 63) / 64)), dim3(64), big_lds, st, k,
+                    big_pitch);
+        } else {
+            KLAUNCH((k_bowk_resolve_lane<false, false>), dim3(gb), dim3(256), 0, st, k, 0);
+        }
+    }
     KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
