@@ -1001,12 +1001,27 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
         if (tid < 32) hist[tid] = 0;
         if (tid == 0) drop = 0;
         __syncthreads();
-        for (int i = tid; i < a.f_n; i += nt) {
-            const int m = match[i];
-            if (m < 0) continue;
-            const int b = rot_bin(KK[m].angle, a.f_kps[i].angle);
-            atomicAdd(&hist[b], 1);
-            if (i < kBowFinalBins) sbin[i] = (uint8_t)b;
+        // four rows in flight per thread: their match loads, then their angle
+        // gathers, then the bins (one dependent load chain per four matches)
+        constexpr int kU = 4;
+        for (int i0 = tid; i0 < a.f_n; i0 += kU * nt) {
+            int m[kU];
+            float ka[kU], fa[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) m[u] = i0 + u * nt < a.f_n ? match[i0 + u * nt] : -1;
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                ka[u] = m[u] >= 0 ? KK[m[u]].angle : 0.f;
+                fa[u] = m[u] >= 0 ? a.f_kps[i0 + u * nt].angle : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                if (m[u] < 0) continue;
+                const int i = i0 + u * nt;
+                const int b = rot_bin(ka[u], fa[u]);
+                atomicAdd(&hist[b], 1);
+                if (i < kBowFinalBins) sbin[i] = (uint8_t)b;
+            }
         }
         __syncthreads();
         int i1, i2, i3;
@@ -1362,13 +1377,23 @@ __device__ __forceinline__ void bowk_lds_barrier() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
-__global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
+#ifndef ORB_BOWK_WPE
+#define ORB_BOWK_WPE 5
+#endif
+// NSET keyframe column sets of 32 per wave (a wave's 32 NSET slots lie in one
+// bucket: buckets are padded to 64): with NSET = 2 every A fragment read from
+// LDS feeds two MFMAs and one set's MFMA chain overlaps the other set's
+// top-4 epilogue inside the wave.
+template <int NSET>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NSET == 1 ? ORB_BOWK_WPE : 2)))
+void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
     // [buffer][row * 17 + 2 s + h]: the odd row pitch (272 B) keeps a
     // ds_read_b128 of 32 rows at one (s, h) off a single bank group
     __shared__ bowk_v4i s_a[2][32 * 17];
     const BowArgs& a = k.b;
-    const long long slotb = (long long)blockIdx.x * 128;
-    const long long slot0 = slotb + (long long)wave_id() * 32;
+    constexpr int kWS = 32 * NSET;                   // slots per wave
+    const long long slotb = (long long)blockIdx.x * 4 * kWS;
+    const long long slot0 = slotb + (long long)wave_id() * kWS;
     const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
     if (slotb >= total) return;                      // the whole block
     auto node_of = [&](long long slot) {             // last fl with bstart[fl] <= slot
@@ -1377,50 +1402,62 @@ __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v
     const int flb = node_of(slotb);
     const int fbb = __builtin_amdgcn_readfirstlane(a.f_off[flb]);
     const int nfb = __builtin_amdgcn_readfirstlane(a.f_off[flb + 1]) - fbb;
-    const bool live = slot0 < total;                 // buckets are padded to 64: 32 slots never straddle
+    const bool live = slot0 < total;                 // buckets are padded to 64: a wave's slots never straddle
     const int fl = live ? (slot0 == slotb ? flb : node_of(slot0)) : flb;
     const bool shared_node = fl == flb;
     const int fb = __builtin_amdgcn_readfirstlane(a.f_off[fl]);
     const int nf = __builtin_amdgcn_readfirstlane(a.f_off[fl + 1]) - fb;
     const int lane = lane_id(), col = lane & 31, h = lane >> 5;
-    const uint32_t src = live ? k.slot_src[slot0 + col] : 0xffffffffu;
-    uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    if (src != 0xffffffffu) {
-        // a (keyframe, node)'s slots are consecutive FeatureVector rows: with the
-        // map's fv_desc the wave's 32 descriptors are one contiguous 1 KB read
-        const uint8_t* kd = a.kf_fvdesc ? a.kf_fvdesc + (long long)k.slot_pos[slot0 + col] * 32
-                                        : a.kf_desc + (long long)src * 32;
-        const uint4 q0 = *(const uint4*)kd;
-        const uint4 q1 = *(const uint4*)(kd + 16);
-        d[0] = q0.x; d[1] = q0.y; d[2] = q0.z; d[3] = q0.w; d[4] = q1.x; d[5] = q1.y; d[6] = q1.z; d[7] = q1.w;
+    bowk_v4i B[NSET][8];
+#pragma unroll
+    for (int c = 0; c < NSET; ++c) {
+        const uint32_t src = live ? k.slot_src[slot0 + 32 * c + col] : 0xffffffffu;
+        uint32_t d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (src != 0xffffffffu) {
+            // a (keyframe, node)'s slots are consecutive FeatureVector rows: with the
+            // map's fv_desc the wave's 32 descriptors are one contiguous 1 KB read
+            const uint8_t* kd = a.kf_fvdesc ? a.kf_fvdesc + (long long)k.slot_pos[slot0 + 32 * c + col] * 32
+                                            : a.kf_desc + (long long)src * 32;
+            const uint4 q0 = *(const uint4*)kd;
+            const uint4 q1 = *(const uint4*)(kd + 16);
+            d[0] = q0.x; d[1] = q0.y; d[2] = q0.z; d[3] = q0.w; d[4] = q1.x; d[5] = q1.y; d[6] = q1.z; d[7] = q1.w;
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < 8; ++s2) B[c][s2] = bits_pm1(d[s2] >> (16 * h));
     }
-    bowk_v4i B[8];
+    uint32_t kk[NSET][kBowK];
 #pragma unroll
-    for (int s2 = 0; s2 < 8; ++s2) B[s2] = bits_pm1(d[s2] >> (16 * h));
-    uint32_t kk[kBowK];
+    for (int c = 0; c < NSET; ++c)
 #pragma unroll
-    for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
+        for (int t = 0; t < kBowK; ++t) kk[c][t] = 0xffffffffu;
     const int neg = -32768;
-    // a 32x32 tile: its 16 accumulator rows of this lane into the column's
-    // top-4 (keys without + 4 h: the order of one lane's keys is the same)
+    // a 32x32 tile per set: its 16 accumulator rows of this lane into the
+    // column's top-4 (keys without + 4 h: the order of one lane's keys is the same)
     auto tile_mfma = [&](const bowk_v4i* ar, int t0, int nfx) {
-        bowk_v4i A[8];
+        bowk_v16i acc[NSET];
 #pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) A[s2] = ar[2 * s2];
-        bowk_v16i acc = {};
+        for (int c = 0; c < NSET; ++c) acc[c] = bowk_v16i{};
 #pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(A[s2], B[s2], acc, 0, 0, 0);
+        for (int s2 = 0; s2 < 8; ++s2) {
+            const bowk_v4i A = ar[2 * s2];
+#pragma unroll
+            for (int c = 0; c < NSET; ++c) acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B[c][s2], acc[c], 0, 0, 0);
+        }
         const int kb = (256 << 15) + t0;
         if (t0 + 32 <= nfx) {
 #pragma unroll
-            for (int g = 0; g < 16; ++g) topk_push(kk, bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2)));
+            for (int c = 0; c < NSET; ++c)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) topk_push(kk[c], bowk_key(acc[c][g], neg, kb + (g & 3) + 8 * (g >> 2)));
         } else {
             const int lim = nfx - t0 - 4 * h;        // rows (g & 3) + 8 (g >> 2) below it exist
 #pragma unroll
-            for (int g = 0; g < 16; ++g) {
-                const uint32_t key = bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2));
-                topk_push(kk, (g & 3) + 8 * (g >> 2) < lim ? key : 0xffffffffu);
-            }
+            for (int c = 0; c < NSET; ++c)
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const uint32_t key = bowk_key(acc[c][g], neg, kb + (g & 3) + 8 * (g >> 2));
+                    topk_push(kk[c], (g & 3) + 8 * (g >> 2) < lim ? key : 0xffffffffu);
+                }
         }
     };
     // block-uniform loop over the block node's tiles: every thread reaches
@@ -1455,13 +1492,17 @@ __global__ __launch_bounds__(256) void k_bowk_topk_mfma(BowKArgs k, const bowk_v
     }
     if (!live) return;
 #pragma unroll
-    for (int t = 0; t < kBowK; ++t) kk[t] = kk[t] == 0xffffffffu ? kk[t] : kk[t] + 4u * (uint32_t)h;
-    uint32_t other[kBowK];
+    for (int c = 0; c < NSET; ++c) {
+        uint32_t (&q)[kBowK] = kk[c];
 #pragma unroll
-    for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)kk[t], 32, kWave);
+        for (int t = 0; t < kBowK; ++t) q[t] = q[t] == 0xffffffffu ? q[t] : q[t] + 4u * (uint32_t)h;
+        uint32_t other[kBowK];
 #pragma unroll
-    for (int t = 0; t < kBowK; ++t) topk_push(kk, other[t]);
-    if (h == 0) k.lists[slot0 + col] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+        for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)q[t], 32, kWave);
+#pragma unroll
+        for (int t = 0; t < kBowK; ++t) topk_push(q, other[t]);
+        if (h == 0) k.lists[slot0 + 32 * c + col] = make_uint4(q[0], q[1], q[2], q[3]);
+    }
 }
 
 // One wave per g: the lists of g's KF features are read lane-parallel, then
@@ -3254,7 +3295,13 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         KLAUNCH(k_bowk_chunks, dim3(a.f_nnodes), dim3(256), 0, st, k);
         KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_idx,
                 a.f_off + a.f_nnodes, fexp.p);
-        KLAUNCH(k_bowk_topk_mfma, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
+        // two column sets per wave measured slower (4.27 vs 4.15 ms per query: 136 VGPRs,
+        // 3 waves per SIMD instead of 5); ORBM_BOWK_NSET=2 selects it (A/B)
+        const char* ns = std::getenv("ORBM_BOWK_NSET");
+        if (ns && ns[0] == '2')
+            KLAUNCH(k_bowk_topk_mfma<2>, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k, fexp.p);
+        else
+            KLAUNCH(k_bowk_topk_mfma<1>, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
     } else {
         KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
     }

@@ -138,7 +138,7 @@ def run_c5(args):
     kf_feat = int(sum(len(x[0]) for x in kfs))
     search_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     ach = kf_feat * KF_FEATURE_BYTES / (search_ms * 1e-3) / 1e9
-    roof = {"kernel": "k_bow_init + k_bow + k_bow_final (one map-wide search)", "bound": "hbm", "achieved": ach,
+    roof = {"kernel": "k_bow_init + k_bowk_* (map, fill, top-4 on MFMA, resolve) + k_bow_final (one map-wide search)", "bound": "hbm", "achieved": ach,
             "peak": benchlib.HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / benchlib.HBM_PEAK_GBS, "traffic": None,
             "bytes_per_launch": kf_feat * KF_FEATURE_BYTES, "ms_per_launch": search_ms,
             "bytes_per_unit": f"{KF_FEATURE_BYTES} B per keyframe feature (descriptor, FeatureVector index, "
