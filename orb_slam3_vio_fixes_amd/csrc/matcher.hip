@@ -1443,6 +1443,11 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
 #pragma unroll
             for (int c = 0; c < NSET; ++c) acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B[c][s2], acc[c], 0, 0, 0);
         }
+        // keep the accumulators in AGPRs: when this compiler gave the MFMA a VGPR
+        // destination (read by the epilogue's VALU directly) the C5 parity tests
+        // failed (8 of 2125 matches lost); the AGPR form with v_accvgpr_read passes
+#pragma unroll
+        for (int c = 0; c < NSET; ++c) asm volatile("" : "+a"(acc[c]));
         const int kb = (256 << 15) + t0;
         if (t0 + 32 <= nfx) {
 #pragma unroll
