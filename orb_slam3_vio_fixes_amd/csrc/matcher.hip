@@ -1116,7 +1116,9 @@ struct BowKArgs {
     int* g_fl;             // [G] frame node of g, -1 if F does not hold it
     int* g_off;            // [G] offset of g's KF features in the node's bucket
     int* g_pr;             // [G] pair of g
-    unsigned long long* bgcount;   // [f_nnodes] per frame node (zeroed): lo KF features, hi g entries
+    unsigned long long* bgcount;   // [f_nnodes][nsub] (zeroed): lo KF features, hi g entries; after
+                                   // k_bowk_scan the exclusive prefixes of both within the node
+    int nsub;                      // sub-counters per frame node (pair & (nsub - 1)): spreads the atomics
     int* bstart;           // [f_nnodes + 1] bucket starts, padded to 64 slots
     uint32_t* slot_src;    // [slots] global KF feature (kp_off[pr] + ikf), ~0: none
     uint4* lists;          // [slots] kBowK smallest keys, ascending, ~0: none
@@ -1157,8 +1159,10 @@ __global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
         if (fl < nfn && fnode[fl] == na && nkf > 0) {
             k.g_fl[g] = fl;
             // one atomic for both counters (a pair holds a frame node at most once, so
-            // nothing aggregates in the block; the ~100 nodes' words are contended)
-            const unsigned long long o = atomicAdd(k.bgcount + fl, (1ull << 32) | (unsigned long long)nkf);
+            // nothing aggregates in the block), on one of nsub words of the node: ~10k
+            // same-address atomics per node serialised at L2 (0.22 ms) otherwise
+            const unsigned long long o =
+                atomicAdd(k.bgcount + (long long)fl * k.nsub + (pr & (k.nsub - 1)), (1ull << 32) | (unsigned long long)nkf);
             k.g_off[g] = (int)(uint32_t)o;
             k.g_rank[g] = (int)(o >> 32);
         } else {
@@ -1168,19 +1172,38 @@ __global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
 }
 
 __global__ __launch_bounds__(1024) void k_bowk_scan(BowKArgs k) {
-    extern __shared__ int sc_s[];
+    extern __shared__ int sc_s[];                    // [2 n]: padded KF features, then g entries per node
     const int n = k.b.f_nnodes;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = ((int)(uint32_t)k.bgcount[i] + kWave - 1) / kWave * kWave;
+    // the node's sub-counters -> exclusive prefixes in place, totals to LDS
+    if (k.nsub == kWave) {                           // a wave per node, a lane per sub-counter
+        const int nw = blockDim.x / kWave, lane = lane_id();
+        for (int i = wave_id(); i < n; i += nw) {
+            unsigned long long* c = k.bgcount + (long long)i * kWave;
+            const unsigned long long v = c[lane];
+            const int lo = (int)(uint32_t)v, hi = (int)(v >> 32);
+            const int ilo = wave_incl_scan(lo), ihi = wave_incl_scan(hi);
+            c[lane] = ((unsigned long long)(uint32_t)(ihi - hi) << 32) | (uint32_t)(ilo - lo);
+            if (lane == kWave - 1) {
+                sc_s[i] = (ilo + kWave - 1) / kWave * kWave;
+                sc_s[n + i] = ihi;
+            }
+        }
+    } else {
+        for (int i = threadIdx.x; i < n; i += blockDim.x) {
+            const unsigned long long v = k.bgcount[i];
+            k.bgcount[i] = 0;
+            sc_s[i] = ((int)(uint32_t)v + kWave - 1) / kWave * kWave;
+            sc_s[n + i] = (int)(v >> 32);
+        }
+    }
     __syncthreads();
     __shared__ int tmp[1024 / kWave + 1];
     const int total = block_excl_scan(sc_s, n, tmp);
     for (int i = threadIdx.x; i < n; i += blockDim.x) k.bstart[i] = sc_s[i];
     if (threadIdx.x == 0) k.bstart[n] = total;
     __syncthreads();
-    for (int i = threadIdx.x; i < n; i += blockDim.x) sc_s[i] = (int)(k.bgcount[i] >> 32);
-    __syncthreads();
-    const int gtotal = block_excl_scan(sc_s, n, tmp);
-    for (int i = threadIdx.x; i < n; i += blockDim.x) k.gstart[i] = sc_s[i];
+    const int gtotal = block_excl_scan(sc_s + n, n, tmp);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) k.gstart[i] = sc_s[n + i];
     if (threadIdx.x == 0) k.gstart[n] = gtotal;
 }
 
@@ -1212,8 +1235,13 @@ __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
         const long long g = g0 + ia;
         const int fl = k.g_fl[g];
         if (fl < 0) return -1;
-        k.perm[k.gstart[fl] + k.g_rank[g]] = (int)g;
-        return k.bstart[fl] + k.g_off[g] - ko[ia];
+        // the sub-counter's prefix within the node; the final offset stays in
+        // g_off for the resolve
+        const unsigned long long sb = k.bgcount[(long long)fl * k.nsub + (pr & (k.nsub - 1))];
+        const int off = k.g_off[g] + (int)(uint32_t)sb;
+        k.g_off[g] = off;
+        k.perm[k.gstart[fl] + k.g_rank[g] + (int)(sb >> 32)] = (int)g;
+        return k.bstart[fl] + off - ko[ia];
     };
     const uint32_t fvo = (uint32_t)a.idx_off[pr];
     auto put = [&](int base, int p) {
@@ -3266,25 +3294,26 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
     static thread_local PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node;
     static thread_local PBuf<unsigned long long> bgcount;
+    const int nsub = a.f_nnodes <= 1024 ? 64 : 1;
     static thread_local PBuf<uint32_t> slot_src, slot_pos;
     static thread_local PBuf<uint4> lists;
     static thread_local PBuf<bowk_v4i> fexp;
     a.npairs = npairs;
     const long long slots = nfv + (long long)kWave * a.f_nnodes;
     int rc;
-    if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc(a.f_nnodes)) ||
+    if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc((size_t)a.f_nnodes * nsub)) ||
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
         (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
         (rc = perm.alloc(G)) || (rc = fexp.alloc((size_t)std::max(1, a.f_n) * 16)) ||
         (rc = chunk_node.alloc(slots / 32 + 1)) || (a.kf_fvdesc && (rc = slot_pos.alloc(slots))))
         return rc;
     BowKArgs k;
-    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bgcount = bgcount.p; k.bstart = bstart.p;
+    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bgcount = bgcount.p; k.nsub = nsub; k.bstart = bstart.p;
     k.slot_src = slot_src.p; k.lists = lists.p;
     k.gstart = gstart.p; k.g_rank = g_rank.p; k.perm = perm.p; k.chunk_node = chunk_node.p;
     k.slot_pos = slot_pos.p;
     ORB_CHECK(flush_uploads());
-    ORB_CHECK(hipMemsetAsync(bgcount.p, 0, (size_t)a.f_nnodes * sizeof(unsigned long long), st));
+    ORB_CHECK(hipMemsetAsync(bgcount.p, 0, (size_t)a.f_nnodes * nsub * sizeof(unsigned long long), st));
     ORB_CHECK(hipMemsetAsync(slot_src.p, 0xff, (size_t)slots * sizeof(uint32_t), st));
     {
         const long long nmf = (long long)npairs * a.f_n;
@@ -3293,7 +3322,7 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     }
     const unsigned gb = (unsigned)((G + 255) / 256), gw = (unsigned)((G + 3) / 4);
     KLAUNCH(k_bowk_map, dim3(npairs), dim3(256), 0, st, k);
-    KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)a.f_nnodes * sizeof(int), st, k);
+    KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)2 * a.f_nnodes * sizeof(int), st, k);
     KLAUNCH(k_bowk_fill, dim3(npairs), dim3(256), 0, st, k);
     const char* mf = std::getenv("ORBM_BOW_KFLANE_MFMA");   // 0: the VALU top-4 pass (A/B)
     if (!(mf && mf[0] == '0')) {

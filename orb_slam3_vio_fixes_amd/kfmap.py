@@ -72,9 +72,9 @@ class DeviceKeyframeMap:
             capi.check(rc, "orbm_kf_map_fv_desc")
             self.struct.fv_desc = self.t["fv_desc"].data_ptr()
 
-    def search_by_bow(self, kps, desc, node_of_feature, nnratio=0.75, check_ori=True, stream=None):
-        """SearchByBoW(KF_i, F) for every keyframe: returns (match [nkf, N] int32
-        KF-feature index or -1, nmatches [nkf]) as device tensors."""
+    def prepare_frame(self, kps, desc, node_of_feature):
+        """The query frame resident in HBM (keypoints, descriptors, FeatureVector
+        CSR) plus its output buffers, for search_prepared."""
         import torch
         dev = self.t["kps"].device
         kps = np.ascontiguousarray(kps, abi.KEYPOINT_DTYPE)
@@ -83,15 +83,29 @@ class DeviceKeyframeMap:
         ft = dict(kps=torch.from_numpy(kps.view(np.uint8).copy()).to(dev),
                   desc=torch.from_numpy(np.ascontiguousarray(desc, np.uint8)).to(dev),
                   node=torch.from_numpy(n_ids.astype(np.int64)).to(dev).to(torch.int32),
-                  off=torch.from_numpy(offs).to(dev), idx=torch.from_numpy(idx.astype(np.int64)).to(dev).to(torch.int32))
-        fr = abi.OrbmFrame(n, ft["kps"].data_ptr(), ft["desc"].data_ptr(), 0, 0, 0, 0, 0, 0, None, None, 0)
-        fv = abi.OrbmFeatVec(len(n_ids), ft["node"].data_ptr(), ft["off"].data_ptr(), ft["idx"].data_ptr())
-        match = torch.empty((self.nkf, n), dtype=torch.int32, device=dev)
-        nm = torch.empty(self.nkf, dtype=torch.int32, device=dev)
+                  off=torch.from_numpy(offs).to(dev), idx=torch.from_numpy(idx.astype(np.int64)).to(dev).to(torch.int32),
+                  match=torch.empty((self.nkf, n), dtype=torch.int32, device=dev),
+                  nm=torch.empty(self.nkf, dtype=torch.int32, device=dev))
+        ft["frame"] = abi.OrbmFrame(n, ft["kps"].data_ptr(), ft["desc"].data_ptr(), 0, 0, 0, 0, 0, 0, None, None, 0)
+        ft["featvec"] = abi.OrbmFeatVec(len(n_ids), ft["node"].data_ptr(), ft["off"].data_ptr(), ft["idx"].data_ptr())
+        return ft
+
+    def search_prepared(self, ft, nnratio=0.75, check_ori=True, stream=None):
+        """SearchByBoW(KF_i, F) for every keyframe against a prepared frame:
+        (match [nkf, N] int32 KF-feature index or -1, nmatches [nkf]), the
+        frame's device output tensors (overwritten by the next call)."""
+        import torch
+        dev = self.t["kps"].device
         st = (stream or torch.cuda.current_stream(dev)).cuda_stream
-        rc = capi.lib().orbm_search_by_bow_batch_device(C.byref(self.struct), C.byref(fr), C.byref(fv), nnratio,
-                                                        int(check_ori), match.data_ptr(), nm.data_ptr(),
-                                                        C.c_void_p(st))
+        rc = capi.lib().orbm_search_by_bow_batch_device(C.byref(self.struct), C.byref(ft["frame"]),
+                                                        C.byref(ft["featvec"]), nnratio, int(check_ori),
+                                                        ft["match"].data_ptr(), ft["nm"].data_ptr(), C.c_void_p(st))
         capi.check(rc, "orbm_search_by_bow_batch_device")
+        return ft["match"], ft["nm"]
+
+    def search_by_bow(self, kps, desc, node_of_feature, nnratio=0.75, check_ori=True, stream=None):
+        """SearchByBoW(KF_i, F) for every keyframe: returns (match [nkf, N] int32
+        KF-feature index or -1, nmatches [nkf]) as device tensors."""
+        ft = self.prepare_frame(kps, desc, node_of_feature)
         self._keep = ft
-        return match, nm
+        return self.search_prepared(ft, nnratio, check_ori, stream)
