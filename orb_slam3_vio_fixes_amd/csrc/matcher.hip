@@ -1106,6 +1106,8 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
 // k_bow_final (rotation filter, counts) follows unchanged.
 // ---------------------------------------------------------------------------
 constexpr int kBowK = 4;
+// the lane resolve's LDS bitmap: 16 words (512 positions) a thread, odd pitch
+constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
 #ifndef ORB_BOWK_ABL
 #define ORB_BOWK_ABL 0   // timing ablations (tools only)
 #endif
@@ -1119,6 +1121,8 @@ struct BowKArgs {
     unsigned long long* bgcount;   // [f_nnodes][nsub] (zeroed): lo KF features, hi g entries; after
                                    // k_bowk_scan the exclusive prefixes of both within the node
     int nsub;                      // sub-counters per frame node (pair & (nsub - 1)): spreads the atomics
+    int* node_n;                   // [f_nnodes + 1] KF features per frame node; [f_nnodes]: any node the
+                                   // big-node resolve form takes (written by k_bowk_scan)
     int* bstart;           // [f_nnodes + 1] bucket starts, padded to 64 slots
     uint32_t* slot_src;    // [slots] global KF feature (kp_off[pr] + ikf), ~0: none
     uint4* lists;          // [slots] kBowK smallest keys, ascending, ~0: none
@@ -1186,17 +1190,27 @@ __global__ __launch_bounds__(1024) void k_bowk_scan(BowKArgs k) {
             if (lane == kWave - 1) {
                 sc_s[i] = (ilo + kWave - 1) / kWave * kWave;
                 sc_s[n + i] = ihi;
+                k.node_n[i] = ilo;
             }
         }
     } else {
         for (int i = threadIdx.x; i < n; i += blockDim.x) {
             const unsigned long long v = k.bgcount[i];
             k.bgcount[i] = 0;
+            k.node_n[i] = (int)(uint32_t)v;
             sc_s[i] = ((int)(uint32_t)v + kWave - 1) / kWave * kWave;
             sc_s[n + i] = (int)(v >> 32);
         }
     }
     __syncthreads();
+    // any node with entries that the big-node resolve form takes (> 512 features)
+    __shared__ int s_big;
+    if (threadIdx.x == 0) s_big = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+        if (sc_s[n + i] > 0 && k.b.f_off[i + 1] - k.b.f_off[i] > 32 * kBowLaneWords) s_big = 1;
+    __syncthreads();
+    if (threadIdx.x == 0) k.node_n[n] = s_big;
     __shared__ int tmp[1024 / kWave + 1];
     const int total = block_excl_scan(sc_s, n, tmp);
     for (int i = threadIdx.x; i < n; i += blockDim.x) k.bstart[i] = sc_s[i];
@@ -1213,6 +1227,10 @@ __global__ __launch_bounds__(256) void k_bowk_chunks(BowKArgs k) {
     const int fl = blockIdx.x;
     const int c0 = k.bstart[fl] / 32, c1 = k.bstart[fl + 1] / 32;
     for (int c = c0 + threadIdx.x; c < c1; c += blockDim.x) k.chunk_node[c] = fl;
+    // the bucket's padding slots hold no keyframe feature (instead of a memset
+    // of every slot)
+    const int p0 = k.bstart[fl] + k.node_n[fl], p1 = k.bstart[fl + 1];
+    for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) k.slot_src[p] = 0xffffffffu;
 }
 
 // One block per pair: every thread over the pair's KF features in
@@ -1265,15 +1283,36 @@ __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
     }
     __syncthreads();
     const int p0 = s_ko[0], p1 = s_ko[nn];
-    for (int p = p0 + threadIdx.x; p < p1; p += blockDim.x) {
-        int lo = 0, hi = nn;                         // last ia with s_ko[ia] <= p (empty nodes skipped)
-        while (hi - lo > 1) {
-            const int mid = (lo + hi) >> 1;
-            if (s_ko[mid] <= p) lo = mid;
-            else hi = mid;
+    // four features in flight per thread: their FeatureVector indices, then
+    // their MapPoint flags, then the stores (one dependent load chain per four)
+    constexpr int kU = 4;
+    const int bd = blockDim.x;
+    for (int q = p0 + threadIdx.x; q < p1; q += kU * bd) {
+        int bs[kU];
+        uint32_t kv[kU];
+        uint8_t vv[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int p = q + u * bd;
+            int lo = 0, hi = nn;                     // last ia with s_ko[ia] <= p (empty nodes skipped)
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_ko[mid] <= p) lo = mid;
+                else hi = mid;
+            }
+            bs[u] = p < p1 ? s_base[lo] : -1;
         }
-        const int base = s_base[lo];
-        if (base >= 0) put(base, p);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) kv[u] = bs[u] >= 0 ? ki[q + u * bd] : 0u;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) vv[u] = bs[u] >= 0 ? a.kf_valid[kpo + (long long)kv[u]] : (uint8_t)0;
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            if (bs[u] < 0) continue;
+            const int p = q + u * bd;
+            k.slot_src[bs[u] + p] = vv[u] ? (uint32_t)(kpo + (long long)kv[u]) : 0xffffffffu;
+            if (a.kf_fvdesc) k.slot_pos[bs[u] + p] = fvo + (uint32_t)p;
+        }
     }
 }
 
@@ -1667,7 +1706,6 @@ __global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
 // words a thread: the odd pitch spreads the threads over the banks); nodes of
 // more than 512 features read "taken" from the match row instead (only this
 // thread writes the node's entries of it).  Otherwise as k_bowk_resolve.
-constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
 // The walk's memory traffic is kept off its critical path: a thread's slots
 // and lists are read 8 steps at a time, the frame-feature indices of the
 // block's first node come from an LDS copy, and every step issues exactly one
@@ -1692,6 +1730,7 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
     __shared__ uint32_t taken_st[BIG ? 1 : 256 * kBowLanePitch];
     __shared__ uint16_t s_fidx[BIG ? 1 : kBowFidxStage];
     const BowArgs& a = k.b;
+    if (BIG && k.node_n[a.f_nnodes] == 0) return;                  // no node for this form
     const int ntot = k.gstart[a.f_nnodes];
     const int tb = blockIdx.x * blockDim.x;
     if (tb >= ntot) return;                                        // the whole block
@@ -3292,7 +3331,7 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 // G: (pair, KF node) entries of the map, nfv: its FeatureVector entries (host
 // totals of the resident map: scratch is sized without reading the device).
 static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
-    static thread_local PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node;
+    static thread_local PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node, node_n;
     static thread_local PBuf<unsigned long long> bgcount;
     const int nsub = a.f_nnodes <= 1024 ? 64 : 1;
     static thread_local PBuf<uint32_t> slot_src, slot_pos;
@@ -3305,16 +3344,15 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
         (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
         (rc = perm.alloc(G)) || (rc = fexp.alloc((size_t)std::max(1, a.f_n) * 16)) ||
-        (rc = chunk_node.alloc(slots / 32 + 1)) || (a.kf_fvdesc && (rc = slot_pos.alloc(slots))))
+        (rc = chunk_node.alloc(slots / 32 + 1)) || (rc = node_n.alloc(a.f_nnodes + 1)) || (a.kf_fvdesc && (rc = slot_pos.alloc(slots))))
         return rc;
     BowKArgs k;
-    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bgcount = bgcount.p; k.nsub = nsub; k.bstart = bstart.p;
+    k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bgcount = bgcount.p; k.nsub = nsub; k.node_n = node_n.p; k.bstart = bstart.p;
     k.slot_src = slot_src.p; k.lists = lists.p;
     k.gstart = gstart.p; k.g_rank = g_rank.p; k.perm = perm.p; k.chunk_node = chunk_node.p;
     k.slot_pos = slot_pos.p;
     ORB_CHECK(flush_uploads());
     ORB_CHECK(hipMemsetAsync(bgcount.p, 0, (size_t)a.f_nnodes * nsub * sizeof(unsigned long long), st));
-    ORB_CHECK(hipMemsetAsync(slot_src.p, 0xff, (size_t)slots * sizeof(uint32_t), st));
     {
         const long long nmf = (long long)npairs * a.f_n;
         const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
@@ -3324,9 +3362,9 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     KLAUNCH(k_bowk_map, dim3(npairs), dim3(256), 0, st, k);
     KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)2 * a.f_nnodes * sizeof(int), st, k);
     KLAUNCH(k_bowk_fill, dim3(npairs), dim3(256), 0, st, k);
+    KLAUNCH(k_bowk_chunks, dim3(a.f_nnodes), dim3(256), 0, st, k);
     const char* mf = std::getenv("ORBM_BOW_KFLANE_MFMA");   // 0: the VALU top-4 pass (A/B)
     if (!(mf && mf[0] == '0')) {
-        KLAUNCH(k_bowk_chunks, dim3(a.f_nnodes), dim3(256), 0, st, k);
         KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_idx,
                 a.f_off + a.f_nnodes, fexp.p);
         // two column sets per wave measured slower (4.27 vs 4.15 ms per query: 136 VGPRs,
