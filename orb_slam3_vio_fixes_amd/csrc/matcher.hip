@@ -1445,7 +1445,7 @@ __device__ __forceinline__ void bowk_lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 #ifndef ORB_BOWK_WPE
-#define ORB_BOWK_WPE 5
+#define ORB_BOWK_WPE 4   // 3.96-3.99 vs 4.09 ms per C5 query at 5 (B then stays in VGPRs); 6 and 7 slower
 #endif
 // NSET keyframe column sets of 32 per wave (a wave's 32 NSET slots lie in one
 // bucket: buckets are padded to 64): with NSET = 2 every A fragment read from
