@@ -1027,6 +1027,26 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
         int i1, i2, i3;
         three_maxima(hist, i1, i2, i3);
         int d = 0;
+#ifndef ORB_BOWF_DROP4
+#define ORB_BOWF_DROP4 1   // 3.955 vs 4.02-4.04 ms per C5 query on one box
+#endif
+#if ORB_BOWF_DROP4
+        // four rows' match loads in flight per thread
+        for (int i0 = tid; i0 < a.f_n; i0 += 4 * nt) {
+            int m[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) m[u] = i0 + u * nt < a.f_n ? match[i0 + u * nt] : -1;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (m[u] < 0) continue;
+                const int i = i0 + u * nt;
+                const int b = i < kBowFinalBins ? sbin[i] : rot_bin(KK[m[u]].angle, a.f_kps[i].angle);
+                if (b == i1 || b == i2 || b == i3) continue;
+                match[i] = -1;
+                ++d;
+            }
+        }
+#else
         for (int i = tid; i < a.f_n; i += nt) {
             const int m = match[i];
             if (m < 0) continue;
@@ -1035,6 +1055,7 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
             match[i] = -1;
             ++d;
         }
+#endif
         d = wave_sum(d);
         if (lane_id() == 0 && d) atomicAdd(&drop, d);
         __syncthreads();
@@ -1445,7 +1466,7 @@ __device__ __forceinline__ void bowk_lds_barrier() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 #ifndef ORB_BOWK_WPE
-#define ORB_BOWK_WPE 4   // 3.96-3.99 vs 4.09 ms per C5 query at 5 (B then stays in VGPRs); 6 and 7 slower
+#define ORB_BOWK_WPE 3   // A/B per C5 query: 3.98 at 3, 4.02-4.09 at 4-5 on one box (B stays in VGPRs); 6 and 7 slower
 #endif
 // NSET keyframe column sets of 32 per wave (a wave's 32 NSET slots lie in one
 // bucket: buckets are padded to 64): with NSET = 2 every A fragment read from
