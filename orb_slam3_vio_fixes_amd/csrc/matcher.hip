@@ -1817,7 +1817,10 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
     // (kChunk lists = one 128-B line), not one 16-B piece of a line per step,
     // which refetched every line ~8 times from HBM once the 64 streams of a
     // wave no longer fit the cache between steps
-    constexpr int kChunk = 8;
+#ifndef ORB_BOWK_RES_CHUNK
+#define ORB_BOWK_RES_CHUNK 8
+#endif
+    constexpr int kChunk = ORB_BOWK_RES_CHUNK;
     const int nkc = max(nkf, 1) - 1;
     for (int j0 = 0; j0 < nkf_max; j0 += kChunk) {
         uint32_t sv[kChunk];
