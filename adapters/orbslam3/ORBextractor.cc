@@ -42,10 +42,14 @@ namespace
 // One device handle per extractor object.  The reference header's inline
 // destructor cannot release it; ORB-SLAM3 creates its extractors once per
 // System (src/Tracking.cc:596-603), so the handles live for the process.
+struct Entry {
+    orbx_handle* h = nullptr;
+    bool host_pyramid = true;   // refresh mvImagePyramid after every extraction
+};
 std::mutex g_mutex;
-std::unordered_map<const ORBextractor*, orbx_handle*> g_handles;
+std::unordered_map<const ORBextractor*, Entry> g_handles;
 
-orbx_handle* handle_of(const ORBextractor* e)
+Entry entry_of(const ORBextractor* e)
 {
     std::lock_guard<std::mutex> lock(g_mutex);
     auto it = g_handles.find(e);
@@ -59,6 +63,13 @@ int device_ordinal()
     const char* s = std::getenv("ORB_MI355X_DEVICE");
     return s ? std::atoi(s) : 0;
 }
+
+bool host_pyramid_default()
+{
+    // ORB_MI355X_HOST_PYRAMID=0: no host copies of the levels by default
+    const char* s = std::getenv("ORB_MI355X_HOST_PYRAMID");
+    return !(s && s[0] == '0');
+}
 }  // namespace
 
 // The device handle of an extractor object: Frame::ComputeStereoMatches
@@ -66,7 +77,22 @@ int device_ordinal()
 // (INTEGRATION.md §4).
 orbx_handle* ORBextractorDeviceHandle(const ORBextractor* e)
 {
-    return handle_of(e);
+    return entry_of(e).h;
+}
+
+// mvImagePyramid is read only by the host Frame::ComputeStereoMatches
+// (src/Frame.cc:818-923).  Its eight host copies (blocking device-to-host
+// copies of every level) are made after each extraction while this is on
+// (the default, so an unmodified Frame.cc keeps working); switch it off for
+// the extractors of a monocular / RGB-D system, or when stereo matching runs
+// on the device (orbs_compute_stereo_matches).  Off, the
+// levels are released so a stale pyramid is never read.
+void ORBextractorSetHostPyramid(ORBextractor* e, bool on)
+{
+    std::lock_guard<std::mutex> lock(g_mutex);
+    auto it = g_handles.find(e);
+    if (it == g_handles.end()) throw std::runtime_error("ORBextractor: no MI355X handle");
+    it->second.host_pyramid = on;
 }
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
@@ -101,7 +127,10 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     mvImagePyramid.resize(nlevels);
 
     std::lock_guard<std::mutex> lock(g_mutex);
-    g_handles[this] = h;
+    Entry en;
+    en.h = h;
+    en.host_pyramid = host_pyramid_default();
+    g_handles[this] = en;
 }
 
 int ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoint>& _keypoints,
@@ -113,7 +142,8 @@ int ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoin
     Mat image = _image.getMat();
     if (image.type() != CV_8UC1)
         throw std::runtime_error("ORBextractor: image must be CV_8UC1");   // assert at :1094
-    orbx_handle* h = handle_of(this);
+    const Entry en = entry_of(this);
+    orbx_handle* h = en.h;
 
     const int cap = orbx_max_keypoints(h, image.cols, image.rows);
     if (cap < 0)
@@ -136,6 +166,10 @@ int ORBextractor::operator()(InputArray _image, InputArray _mask, vector<KeyPoin
         desc.rowRange(0, n).copyTo(_descriptors);   // creates the n x 32 CV_8U output
 
     // mvImagePyramid (host copies of the device levels; level 0 is the input)
+    if (!en.host_pyramid) {
+        for (Mat& m : mvImagePyramid) m.release();
+        return mono;
+    }
     for (int level = 0; level < nlevels; ++level) {
         int w = 0, hh = 0;
         if (orbx_get_level(h, level, nullptr, 0, &w, &hh) != ORB_OK)

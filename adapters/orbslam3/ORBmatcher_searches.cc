@@ -14,11 +14,14 @@
  * exactly as the reference writes it, hands flat snapshots to the device, and
  * writes MapPoint pointers back from the returned indices.
  *
- * Not compiled in this repository's container: Frame.h / KeyFrame.h need
- * Eigen, Sophus, boost and OpenCV, which the image lacks.  The extractor
- * adapter next to it is compiled (-fsyntax-only) against the reference header
- * by tests/test_adapter.py; the ABI calls here are those of
- * tests/native/cpp_api_test.cpp, which runs on the GPU.
+ * Not compiled in this repository's container: Frame.h / KeyFrame.h pull in
+ * Eigen, Sophus, g2o, boost serialization and OpenCV, which the image lacks.
+ * Every Frame / KeyFrame / MapPoint / ORBmatcher member read here is checked
+ * against its declaration in the reference's own headers by
+ * tests/test_adapter.py (test_matcher_adapter_members_declared_in_reference_headers);
+ * the extractor adapter next to it is compiled against the reference header
+ * and run on the GPU (tests/test_gpu_adapter.py); the ABI calls here are those
+ * of tests/native/cpp_api_test.cpp, which runs on the GPU.
  */
 #include "ORBmatcher.h"
 #include "KeyFrame.h"

@@ -95,7 +95,9 @@ def other_workload(args):
                                   cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))
         return bench_stereo.run_c3(a) if args.workload == "c3" else bench_stereo.run_c4(a)
     import bench_c5
-    a = types.SimpleNamespace(nkf=args.nkf, reps=args.steps, warmup=args.warmup, cpu_sample=min(args.cpu_sample, 200),
+    # the oracle checks every keyframe of rank 0's shard (a threaded map loop: a few seconds)
+    a = types.SimpleNamespace(nkf=args.nkf, per_kf=5000, reps=args.steps, warmup=args.warmup,
+                              cpu_sample=-1 if args.cpu_sample > 0 else 0,
                               cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))
     return bench_c5.run_c5(a)
 
@@ -225,10 +227,37 @@ def host_api_rates(frames_np, reps=200):
     for i in range(reps // 2):
         ex.extract_batch([imgs[i % 16], imgs[(i + 1) % 16]], [LAP, LAP])
     pair = (time.perf_counter() - t0) / (reps // 2)
-    return {"orbx_extract_ms": single * 1e3, "orbx_extract_frames_per_s": 1.0 / single,
-            "orbx_extract_batch_stereo_pair_ms": pair * 1e3, "orbx_extract_batch_frames_per_s": 2.0 / pair,
-            "calls": reps, "image": f"{W}x{H} u8, host memory, outputs copied back to host",
-            "note": "PCIe-inclusive drop-in rate (one Tracking-thread call at a time); not the metric"}
+    out = {"orbx_extract_ms": single * 1e3, "orbx_extract_frames_per_s": 1.0 / single,
+           "orbx_extract_batch_stereo_pair_ms": pair * 1e3, "orbx_extract_batch_frames_per_s": 2.0 / pair,
+           "calls": reps, "image": f"{W}x{H} u8, host memory, outputs copied back to host",
+           "note": "PCIe-inclusive drop-in rate (one Tracking-thread call at a time); not the metric"}
+    out["adapter"] = adapter_rates(frames_np[0], reps)
+    return out
+
+
+def adapter_rates(img, reps):
+    """The drop-in ORBextractor adapter's true per-call cost (ORBextractor::
+    operator() of adapters/orbslam3/ORBextractor.cc, compiled against the
+    reference header into tests/native/bin/adapter_extractor by build()):
+    with the eight mvImagePyramid host copies it makes by default, and with
+    them off (ORBextractorSetHostPyramid: mono / RGB-D, or stereo matching on
+    the device).  None when the binary was not built."""
+    import subprocess
+    import tempfile
+    exe = ROOT / "tests" / "native" / "bin" / "adapter_extractor"
+    if not exe.exists():
+        return None
+    with tempfile.TemporaryDirectory() as td:
+        src = Path(td) / "img.u8"
+        src.write_bytes(np.ascontiguousarray(img, np.uint8).tobytes())
+        r = subprocess.run([str(exe), str(src), str(W), str(H), str(NFEAT), str(LAP[0]), str(LAP[1]), td, str(reps)],
+                           capture_output=True, text=True, timeout=120)
+        if r.returncode != 0:
+            return {"error": r.stderr[-500:]}
+        with_pyr, without, _ = (Path(td) / "time.txt").read_text().split()
+    return {"ms_per_call_host_pyramid": float(with_pyr), "ms_per_call_no_host_pyramid": float(without),
+            "frames_per_s_host_pyramid": 1e3 / float(with_pyr), "frames_per_s_no_host_pyramid": 1e3 / float(without),
+            "calls": reps}
 
 
 def main():
@@ -426,12 +455,14 @@ def main():
             kh = last[0][:ns].cpu().numpy()
             dh = last[1][:ns].cpu().numpy()
             nh = last[2][:ns].cpu().numpy()
+            monoh = last[3][:ns].cpu().numpy()
             mh = nmatch[:ns - 1].cpu().numpy()
             m12h = matches[:ns - 1].cpu().numpy()
             bad = 0
             for i in range(ns):
-                rk, rd, _ = outs[i]
-                if nh[i] != len(rk) or not np.array_equal(orb.keypoints_from_device(kh[i][:nh[i]]).view(np.uint8),
+                rk, rd, rmono = outs[i]
+                if nh[i] != len(rk) or monoh[i] != rmono or \
+                        not np.array_equal(orb.keypoints_from_device(kh[i][:nh[i]]).view(np.uint8),
                                                           rk.view(np.uint8)) or not np.array_equal(dh[i][:nh[i]], rd):
                     bad += 1
             bad_m = 0
@@ -448,8 +479,8 @@ def main():
                                              f"threads (value); single_thread_fps: the reference's model, one "
                                              f"Tracking thread extracting and matching frame after frame"}
             out["parity"] = {"frames_checked": ns, "frames_mismatched": bad, "pairs_checked": ns - 1,
-                             "pairs_mismatched": bad_m, "compared": "all 28 keypoint bytes, 32 descriptor bytes, "
-                                                                   "monoIndex count, nmatches and the full matches12"}
+                             "pairs_mismatched": bad_m, "compared": "keypoint count, all 28 keypoint bytes, 32 descriptor "
+                                                                   "bytes, monoIndex, nmatches and the full matches12"}
         if world == 1 and args.host_api:
             out["host_api"] = host_api_rates(frames_np)
         print(json.dumps(out), flush=True)

@@ -116,7 +116,8 @@ int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step,
  * extracted in one call.  Level 0 is read from the batch's input frames (for
  * orbx_extract_batch_device: the caller's buffer, which must still be live).
  * ORB_ERR_PARAM when no batch is current (any orbx_extract or plan rebuild
- * ends it).  dst may be NULL to query w/h. */
+ * ends it).  Waits for an orbx_extract_batch_device batch's work on its
+ * stream before copying.  dst may be NULL to query w/h. */
 int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step,
                          int* w, int* h_);
 
@@ -148,6 +149,18 @@ int orbx_debug_stage(orbx_handle* h, int stage, orb_keypoint* kps, int cap,
  * (csrc/orb_math.h: math_mix). */
 int orbx_debug_math(int device, int what, long long begin, long long end, int chunk_log2, int fused,
                     unsigned long long* hashes);
+
+/* Device std::sort check (test infrastructure, not part of the reference
+ * interface): k_quadtree's emulation of DistributeOctTree's
+ * sort(vPrevSizeAndPointerToNode, compareNodes) (src/ORBextractor.cc:538-553,
+ * :700; libstdc++ introsort) run on the device over narrays arrays of
+ * (count, UL.x) pairs, one workgroup per array.  Array i is elements
+ * [off[i], off[i+1]) of cnt / x0, at most 4000 long.  perm[off[i] + j] =
+ * the original index (within array i) of the element the sort puts at j;
+ * fallback[i] = 1 where the depth limit sent the array to the sequential port
+ * (the heap-sort case).  Returns ORB_OK, ORB_ERR_PARAM or ORB_ERR_DEVICE. */
+int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* cnt, const int32_t* x0,
+                    int32_t* perm, int32_t* fallback);
 
 /* Per-stage HIP-event timing of subsequent orbx_extract* calls (on the stream
  * they run on).  orbx_get_profile sums, over the recorded calls, the stage

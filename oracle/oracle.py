@@ -80,6 +80,7 @@ def lib(path: Path | None = None):
         L.orbo_descriptor_distance.argtypes = [vp, vp]
         L.orbo_search_for_initialization.argtypes = [vp, vp, vp, i32, f32, i32, vp]
         L.orbo_search_by_bow.argtypes = [vp, vp, vp, vp, vp, f32, i32, vp]
+        L.orbo_search_by_bow_map.argtypes = [i32] + [vp] * 11 + [f32, i32, i32, vp, vp]
         L.orbo_search_by_projection_mps.argtypes = [vp, vp, f32, i32, f32, f32, vp, vp]
         L.orbo_search_by_projection_last.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp, vp]
         L.orbo_transform.argtypes = [vp, i32, vp, i32, vp, vp, vp]
@@ -209,6 +210,23 @@ def search_by_bow(kf: abi.Keep, kfv: abi.Keep, kf_valid: np.ndarray, f: abi.Keep
     nm = lib().orbo_search_by_bow(kf.ref(), kfv.ref(), abi.ptr(kf_valid), f.ref(), fv.ref(), nnratio,
                                   int(check_ori), abi.ptr(match))
     return nm, match
+
+
+def search_by_bow_map(arrays: dict, f: abi.Keep, fv: abi.Keep, nnratio=0.75, check_ori=True, nthreads=None):
+    """SearchByBoW(KF_i, F) for every keyframe of a packed map (kfmap.pack /
+    synth.keyframe_map layout), keyframes spread over nthreads: (match
+    [nkf, F.N] int32, nmatches [nkf] int32)."""
+    nkf = len(arrays["kp_off"]) - 1
+    nt = nthreads or min(16, os.cpu_count() or 1)
+    a = {key: np.ascontiguousarray(v) for key, v in arrays.items()}
+    match = np.empty((nkf, f.struct.n), np.int32)
+    nm = np.zeros(nkf, np.int32)
+    rc = lib().orbo_search_by_bow_map(nkf, *[abi.ptr(a[key]) for key in ("kps", "desc", "valid", "kp_off", "fv_node",
+                                                                      "fv_off", "fv_idx", "fv_node_off", "fv_idx_off")],
+                                      f.ref(), fv.ref(), nnratio, int(check_ori), nt, abi.ptr(match), abi.ptr(nm))
+    if rc != 0:
+        raise ValueError(f"orbo_search_by_bow_map: {rc}")
+    return match, nm
 
 
 def search_by_projection_mps(f: abi.Keep, mps: abi.Keep, th, far_points, th_far, nnratio, owner, blocked):

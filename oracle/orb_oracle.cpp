@@ -948,6 +948,39 @@ int orbo_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint
 }
 
 
+// The relocalisation loop over candidates (Tracking.cc:3641-3648: one
+// SearchByBoW(KF_i, F) per candidate) over a whole keyframe map laid out like
+// orbm_kf_map_device but in host memory; keyframes are independent, so they are
+// spread over nthreads.  match: nkf x f->n, nm: nkf.
+int orbo_search_by_bow_map(int nkf, const orb_keypoint* kps, const uint8_t* desc, const uint8_t* valid,
+                           const int64_t* kp_off, const uint32_t* fv_node, const int32_t* fv_off,
+                           const uint32_t* fv_idx, const int64_t* fv_node_off, const int64_t* fv_idx_off,
+                           const orbm_frame* f, const orbm_featvec* ffv, float ratio, int check_ori, int nthreads,
+                           int32_t* match, int32_t* nm) {
+    if (nkf < 0 || !f || !ffv) return -3;
+    auto one = [&](int i) {
+        orbm_frame kf{};
+        kf.n = (int32_t)(kp_off[i + 1] - kp_off[i]);
+        kf.kps = kps + kp_off[i];
+        kf.desc = desc + kp_off[i] * 32;
+        orbm_featvec fv{};
+        fv.nnodes = (int32_t)(fv_node_off[i + 1] - fv_node_off[i]);
+        fv.node_ids = fv_node + fv_node_off[i];
+        fv.offsets = fv_off + fv_node_off[i] + i;
+        fv.idx = fv_idx + fv_idx_off[i];
+        nm[i] = orbo_search_by_bow(&kf, &fv, valid + kp_off[i], f, ffv, ratio, check_ori,
+                                   match + (size_t)i * f->n);
+    };
+    const int nt = std::max(1, std::min(nthreads, nkf));
+    std::vector<std::thread> th;
+    for (int t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (int i = t; i < nkf; i += nt) one(i);
+        });
+    for (auto& x : th) x.join();
+    return 0;
+}
+
 // ORBmatcher::SearchByProjection(Frame&, vector<MapPoint*>, th, bFarPoints, thFarPoints)
 // (ORBmatcher.cc:43-213, the F.Nleft == -1 branch) + RadiusByViewingCos (:215-221).
 int orbo_search_by_projection_mps(const orbm_frame* f, const orbm_mappoints* mp, float th, int far_points,

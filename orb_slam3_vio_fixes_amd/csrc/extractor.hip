@@ -421,6 +421,13 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
         rdw += PS.ring_rows[m] * PS.ring_pitch[m] / 4;
     }
     if (rdw >= 65536) return;                              // row records hold 16-bit dword offsets
+    // ORB_PYR_CNT_END=1 (test knob): the per-step counters after the rings, at
+    // the top of the allocation, outside the copied table image (the kernel
+    // zeroes them there); the default keeps them at dword 0 of the image
+    if (const char* e = std::getenv("ORB_PYR_CNT_END"); e && e[0] == '1') {
+        PS.cnt_dw = rdw;
+        rdw += round_up(PS.nsteps, 4);
+    }
     if (4LL * rdw > 160 * 1024) return;
     for (int l = 1; l < L; ++l) {
         const LevelDev& d = P.lv[l];
@@ -896,6 +903,8 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
     if (f >= a.nframes) return;
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     for (int i = tid; i < a.tab_u4; i += 1024) ps_lds[i] = a.tab[i];
+    if (a.cnt_dw >= 4 * a.tab_u4)                    // counters outside the image (ORB_PYR_CNT_END)
+        for (int i = tid; i < a.nsteps; i += 1024) lds[a.cnt_dw + i] = 0;
     lds_barrier();
     // lane l: level l's {column records, row records} dword offsets
     const uint4 lvt = ps_lds[a.lev_u4 + min(lane, a.L - 1)];
@@ -968,9 +977,12 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
         const int W = __builtin_amdgcn_readfirstlane((int)se.x);
         for (int it = 0; it <= W; ++it) {      // bounded: a wave never takes more than W items
             // wave-items are taken from a per-step LDS counter: waves that drew
-            // cheap items take more, so the step ends when the work does
-            // (the counters sit in the first 64 KiB of LDS: an LDS atomic at
-            // a higher address was measured to return garbage on gfx950)
+            // cheap items take more, so the step ends when the work does.  The
+            // counters are zeroes of the copied table image (dword 0 on); with
+            // ORB_PYR_CNT_END=1 they sit at the top of the allocation and are
+            // zeroed above.  (Round 2 blamed a failing end-of-LDS layout on the
+            // hardware; tests/test_gpu_configs.py runs that layout, zeroed,
+            // bit-exact -- see DESIGN.md on the cause.)
             int jj = 0;
             if (lane == 0) jj = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
             const int j = __builtin_amdgcn_readfirstlane(jj);
@@ -1835,6 +1847,42 @@ __device__ void block_std_sort(SortRec* a, int m, SortRec* backup, int* Lp, int*
     const int nleaf = ctl[3];
     for (int i = tid; i < nleaf; i += T) insertion_sort_(a + (leaves[i] >> 16), a + (leaves[i] & 0xffff));
     __syncthreads();
+}
+
+// orbx_debug_sort: block_std_sort -- k_quadtree's device std::sort under
+// compareNodes (ORBextractor.cc:538-553, :700) -- on many arrays, one
+// workgroup each, so the exact permutation can be compared with the host's
+// std::sort on adversarial inputs (tests/test_gpu_sort.py).  LDS: the array
+// and its backup, the partition lists, the range queues and leaves, ctl, the
+// sequential port's stack.
+constexpr int kDbgSortMax = 4000;
+__host__ __device__ inline size_t dbg_sort_lds(int m) {
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    return 2 * al(m * sizeof(SortRec)) + 2 * al(m * sizeof(int)) + 2 * al((m / 17 + 2) * sizeof(SortFrame)) +
+           al((m + 2) * sizeof(int)) + al(4 * sizeof(int)) + al(80 * sizeof(SortFrame));
+}
+__global__ __launch_bounds__(256) void k_debug_sort(const int* __restrict__ off, const int* __restrict__ cnt,
+                                                    const int* __restrict__ x0, int* __restrict__ perm,
+                                                    int* __restrict__ fallback) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int o = off[blockIdx.x], m = off[blockIdx.x + 1] - o;
+    uint8_t* p = smem;
+    auto take = [&](size_t bytes) { uint8_t* q = p; p += (bytes + 15) & ~size_t(15); return q; };
+    SortRec* a = (SortRec*)take(m * sizeof(SortRec));
+    SortRec* backup = (SortRec*)take(m * sizeof(SortRec));
+    int* Lp = (int*)take(m * sizeof(int));
+    int* Rp = (int*)take(m * sizeof(int));
+    SortFrame* qa = (SortFrame*)take((m / 17 + 2) * sizeof(SortFrame));
+    SortFrame* qb = (SortFrame*)take((m / 17 + 2) * sizeof(SortFrame));
+    int* leaves = (int*)take((m + 2) * sizeof(int));
+    int* ctl = (int*)take(4 * sizeof(int));
+    SortFrame* stk = (SortFrame*)take(80 * sizeof(SortFrame));
+    for (int i = threadIdx.x; i < m; i += blockDim.x) a[i] = SortRec{cnt[o + i], x0[o + i], i};
+    if (threadIdx.x == 0) ctl[2] = 0;
+    __syncthreads();
+    block_std_sort(a, m, backup, Lp, Rp, qa, qb, leaves, ctl, stk);
+    for (int i = threadIdx.x; i < m; i += blockDim.x) perm[o + i] = a[i].pos;
+    if (threadIdx.x == 0) fallback[blockIdx.x] = ctl[2];
 }
 
 // Divide s.ord[0..m) (ccnt/kq already computed for them, s.div set for every
@@ -2885,6 +2933,7 @@ void orbx_destroy(orbx_handle* h) {
     for (hipEvent_t e : h->sub_done) (void)hipEventDestroy(e);
     for (hipStream_t s : h->sub_streams) (void)hipStreamDestroy(s);
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+    if (h->batch_done) (void)hipEventDestroy(h->batch_done);
     if (h->st_scratch) (void)hipFree(h->st_scratch);
     if (h->hb_dev) (void)hipFree(h->hb_dev);
     if (h->hb_pin) (void)hipHostFree(h->hb_pin);
@@ -2931,8 +2980,14 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     h->last_pitch0 = (int)row_step;
     h->last_B = nframes;
     h->have_last = false;          // pyramid slot 0 now holds this batch's frame 0
-    return run_batched(h, 0, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
-                       d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
+    rc = run_batched(h, 0, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
+                     d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
+    if (rc) return rc;
+    // orbx_get_batch_level waits for this (the caller's stream may be a
+    // non-blocking one the null-stream copy is not ordered after)
+    if (!h->batch_done) ORB_CHECK(hipEventCreateWithFlags(&h->batch_done, hipEventDisableTiming));
+    ORB_CHECK(hipEventRecord(h->batch_done, (hipStream_t)stream));
+    return ORB_OK;
 }
 
 int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, const size_t* steps, int w, int hh,
@@ -3209,6 +3264,45 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
     return e == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
+int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* cnt, const int32_t* x0,
+                    int32_t* perm, int32_t* fallback) {
+    if (narrays < 0 || (narrays && (!off || !perm || !fallback))) return ORB_ERR_PARAM;
+    if (narrays == 0) return ORB_OK;
+    int maxm = 0;
+    for (int i = 0; i < narrays; ++i) {
+        const int m = off[i + 1] - off[i];
+        if (m < 0 || m > kDbgSortMax || off[i] < 0) return ORB_ERR_PARAM;
+        maxm = std::max(maxm, m);
+    }
+    const long long tot = off[narrays];
+    if (tot && (!cnt || !x0)) return ORB_ERR_PARAM;
+    if (hipSetDevice(device) != hipSuccess) return ORB_ERR_DEVICE;
+    int *d_off = nullptr, *d_buf = nullptr;
+    const size_t nb = (size_t)std::max(1LL, tot);
+    auto done = [&](int rc) {
+        if (d_off) (void)hipFree(d_off);
+        if (d_buf) (void)hipFree(d_buf);
+        return rc;
+    };
+    if (hipMalloc(&d_off, (narrays + 1) * sizeof(int)) != hipSuccess ||
+        hipMalloc(&d_buf, (3 * nb + narrays) * sizeof(int)) != hipSuccess)
+        return done(ORB_ERR_DEVICE);
+    int* d_cnt = d_buf;
+    int* d_x0 = d_buf + nb;
+    int* d_perm = d_buf + 2 * nb;
+    int* d_fb = d_buf + 3 * nb;
+    if (hipMemcpy(d_off, off, (narrays + 1) * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+        (tot && (hipMemcpy(d_cnt, cnt, tot * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
+                 hipMemcpy(d_x0, x0, tot * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)))
+        return done(ORB_ERR_DEVICE);
+    hipLaunchKernelGGL(k_debug_sort, dim3(narrays), dim3(256), dbg_sort_lds(maxm), 0, d_off, d_cnt, d_x0, d_perm, d_fb);
+    if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return done(ORB_ERR_DEVICE);
+    if ((tot && hipMemcpy(perm, d_perm, tot * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
+        hipMemcpy(fallback, d_fb, narrays * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+        return done(ORB_ERR_DEVICE);
+    return done(ORB_OK);
+}
+
 int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int* w, int* hh) {
     if (!h || !h->last_frames || frame < 0 || frame >= h->last_B || level < 0 || level >= h->plan.L)
         return ORB_ERR_PARAM;
@@ -3221,6 +3315,7 @@ int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, siz
     const uint8_t* src = level == 0 ? h->last_frames + (long long)frame * h->last_fstride
                                     : P.d_pyr + (long long)frame * P.pyr_bytes + d.off;
     const size_t sp = level == 0 ? (size_t)h->last_pitch0 : (size_t)d.pitch;
+    if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
     return ORB_OK;
 }

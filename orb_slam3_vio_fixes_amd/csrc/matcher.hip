@@ -25,6 +25,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <vector>
 
 namespace orbmi {
@@ -1444,11 +1445,18 @@ __global__ __launch_bounds__(256) void k_bowk_expand(const uint8_t* __restrict__
 }
 
 // a key without the lane half's row offset: (256 - acc) << 15 == ham << 16
-// (acc = 256 - 2 ham), plus the uniform part of the row, in one v_mad_i32_i24
+// (acc = 256 - 2 ham), plus the uniform part of the row.  Plain 24-bit
+// arithmetic (|acc| <= 256, acc * -32768 and the sum fit 24 x 24 -> 32 bits).
+// It must stay visible to
+// the compiler: acc is an MFMA result, and the hazard recognizer inserts the
+// MFMA -> VALU read wait states only for instructions it can see.  Round 2
+// wrote this as an inline-asm v_mad_i32_i24 reading the accumulator directly;
+// with the accumulators in VGPRs (the compiler's VGPR-destination MFMA form)
+// the asm read them before the MFMA had written them back and lost matches
+// (8 of 2125), which an AGPR pin (a compiler-visible v_accvgpr_read first)
+// had hidden.
 __device__ __forceinline__ uint32_t bowk_key(int acc, int neg, int kb) {
-    uint32_t d;
-    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(acc), "v"(neg), "s"(kb));
-    return d;
+    return (uint32_t)(__mul24(acc, neg) + kb);
 }
 
 // The block's 4 waves (128 keyframe slots) share their frame node's tiles:
@@ -1465,6 +1473,9 @@ __device__ __forceinline__ void bowk_lds_barrier() {
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+#ifndef ORB_BOWK_AGPR_PIN
+#define ORB_BOWK_AGPR_PIN 0
+#endif
 #ifndef ORB_BOWK_WPE
 #define ORB_BOWK_WPE 3   // A/B per C5 query: 3.98 at 3, 4.02-4.09 at 4-5 on one box (B stays in VGPRs); 6 and 7 slower
 #endif
@@ -1518,7 +1529,13 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
     for (int c = 0; c < NSET; ++c)
 #pragma unroll
         for (int t = 0; t < kBowK; ++t) kk[c][t] = 0xffffffffu;
-    const int neg = -32768;
+    // -32768 in a VGPR and the key base in an SGPR, both opaque to the
+    // compiler (empty asm on constants, no MFMA operand involved): a key is
+    // then a v_mul_i32_i24 and an add (as many VALU ops as round 2's
+    // v_accvgpr_read + inline v_mad) instead of a shift, a subtract and an add
+    int neg = -32768, kbase = 256 << 15;
+    asm volatile("" : "+v"(neg));
+    asm volatile("" : "+s"(kbase));
     // a 32x32 tile per set: its 16 accumulator rows of this lane into the
     // column's top-4 (keys without + 4 h: the order of one lane's keys is the same)
     auto tile_mfma = [&](const bowk_v4i* ar, int t0, int nfx) {
@@ -1531,12 +1548,13 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
 #pragma unroll
             for (int c = 0; c < NSET; ++c) acc[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(A, B[c][s2], acc[c], 0, 0, 0);
         }
-        // keep the accumulators in AGPRs: when this compiler gave the MFMA a VGPR
-        // destination (read by the epilogue's VALU directly) the C5 parity tests
-        // failed (8 of 2125 matches lost); the AGPR form with v_accvgpr_read passes
+#if ORB_BOWK_AGPR_PIN
+        // build knob: accumulators forced into AGPRs (round 2's workaround for
+        // the inline-asm key above; see bowk_key)
 #pragma unroll
         for (int c = 0; c < NSET; ++c) asm volatile("" : "+a"(acc[c]));
-        const int kb = (256 << 15) + t0;
+#endif
+        const int kb = kbase + t0;
         if (t0 + 32 <= nfx) {
 #pragma unroll
             for (int c = 0; c < NSET; ++c)
@@ -3067,6 +3085,19 @@ struct PBuf {
 
 static int pow2_at_least(int n) { int p = 64; while (p < n) p <<= 1; return p; }
 
+// Scratch of the asynchronous device entry points, one set per (device,
+// stream) of the calling thread: two searches issued on different streams, or
+// for different GPUs, must not share buffers.  (Calls on one stream are
+// ordered by the stream; buffers only grow, and hipFree of a grown-out buffer
+// waits for the device.)
+template <class S>
+static S& stream_scratch(hipStream_t st) {
+    static thread_local std::map<std::pair<int, hipStream_t>, S>* m = new std::map<std::pair<int, hipStream_t>, S>();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    return (*m)[{dev, st}];
+}
+
 static GridParams grid_params(const orbm_frame* f) {
     return GridParams{f->min_x, f->min_y, f->grid_inv_w, f->grid_inv_h};
 }
@@ -3207,9 +3238,11 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     (void)max_x; (void)max_y;
     if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
     hipStream_t st = (hipStream_t)stream;
-    static thread_local PBuf<uint32_t> sorted, topk, l0s;
-    static thread_local PBuf<int> count, pf, ncand, l0c;
-    static thread_local int pf_frames = 0;
+    struct Scratch { PBuf<uint32_t> sorted, topk, l0s; PBuf<int> count, pf, ncand, l0c; int pf_frames = 0; };
+    Scratch& S = stream_scratch<Scratch>(st);
+    PBuf<uint32_t>&sorted = S.sorted, &topk = S.topk, &l0s = S.l0s;
+    PBuf<int>&count = S.count, &pf = S.pf, &ncand = S.ncand, &l0c = S.l0c;
+    int& pf_frames = S.pf_frames;
     int rc;
     if ((rc = sorted.alloc((size_t)nframes * cap)) || (rc = count.alloc(nframes)) ||
         (rc = topk.alloc((size_t)nframes * cap * kTopK)) || (rc = ncand.alloc((size_t)nframes * cap)) ||
@@ -3355,12 +3388,21 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 // G: (pair, KF node) entries of the map, nfv: its FeatureVector entries (host
 // totals of the resident map: scratch is sized without reading the device).
 static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
-    static thread_local PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node, node_n;
-    static thread_local PBuf<unsigned long long> bgcount;
+    struct Scratch {
+        PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node, node_n;
+        PBuf<unsigned long long> bgcount;
+        PBuf<uint32_t> slot_src, slot_pos;
+        PBuf<uint4> lists;
+        PBuf<bowk_v4i> fexp;
+    };
+    Scratch& S = stream_scratch<Scratch>(st);
+    PBuf<int>&g_fl = S.g_fl, &g_off = S.g_off, &g_pr = S.g_pr, &bstart = S.bstart, &gstart = S.gstart,
+        &g_rank = S.g_rank, &perm = S.perm, &chunk_node = S.chunk_node, &node_n = S.node_n;
+    PBuf<unsigned long long>& bgcount = S.bgcount;
+    PBuf<uint32_t>&slot_src = S.slot_src, &slot_pos = S.slot_pos;
+    PBuf<uint4>& lists = S.lists;
+    PBuf<bowk_v4i>& fexp = S.fexp;
     const int nsub = a.f_nnodes <= 1024 ? 64 : 1;
-    static thread_local PBuf<uint32_t> slot_src, slot_pos;
-    static thread_local PBuf<uint4> lists;
-    static thread_local PBuf<bowk_v4i> fexp;
     a.npairs = npairs;
     const long long slots = nfv + (long long)kWave * a.f_nnodes;
     int rc;
@@ -3448,8 +3490,10 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     // (6.7 vs 7.1 ms per 10k-keyframe query); ORBM_BOW_KFLANE=0
     // selects k_bow (A/B, tests)
     const char* kfl = std::getenv("ORBM_BOW_KFLANE");
+    // (k_bowk_scan holds two ints per frame node in LDS: 20,000 nodes = 160 KB
+    // less its static scratch; beyond that k_bow runs)
     if (map->n_nodes_total > 0 && map->n_fv_total > 0 && f->n <= 0xffff && ffv->nnodes > 0 &&
-        ffv->nnodes <= 32 * 1024 && !(kfl && kfl[0] == '0'))
+        ffv->nnodes <= 20000 && !(kfl && kfl[0] == '0'))
         return launch_bow_kf(a, map->nkf, map->n_nodes_total, map->n_fv_total, (hipStream_t)stream);
     return launch_bow(a, map->nkf, (hipStream_t)stream);
 }

@@ -146,6 +146,7 @@ struct orbx_handle {
     std::vector<hipStream_t> sub_streams;
     std::vector<hipEvent_t> sub_done;
     hipEvent_t fork_ev = nullptr;
+    hipEvent_t batch_done = nullptr;   // recorded after orbx_extract_batch_device's work on its stream
     // frames of the last orbx_extract_batch_device call (level 0 of its
     // pyramid; levels >= 1 stay in plan.d_pyr until the next call)
     const uint8_t* last_frames = nullptr;

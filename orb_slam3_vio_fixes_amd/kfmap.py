@@ -27,50 +27,78 @@ def featvec_csr(node_of_feature: np.ndarray):
     feature order (nodes ascending, feature indices ascending per node)."""
     nid = np.asarray(node_of_feature, dtype=np.int64)
     feats = np.nonzero(nid >= 0)[0]
-    order = np.lexsort((feats, nid[feats]))
-    feats = feats[order]
-    nodes, starts = np.unique(nid[feats], return_index=True)
-    return nodes.astype(np.uint32), np.append(starts, len(feats)).astype(np.int32), feats.astype(np.uint32)
+    feats = feats[np.argsort(nid[feats], kind="stable")]    # by node, feature index ascending within
+    sn = nid[feats]
+    starts = np.flatnonzero(np.r_[True, sn[1:] != sn[:-1]]) if len(sn) else np.zeros(0, np.int64)
+    return sn[starts].astype(np.uint32), np.append(starts, len(feats)).astype(np.int32), feats.astype(np.uint32)
+
+
+def pack(keyframes) -> dict:
+    """The keyframes concatenated in the orbm_kf_map_device layout, as host
+    arrays: kps (u8 view of orb_keypoint rows), desc, valid, kp_off, fv_node,
+    fv_off, fv_idx, fv_node_off, fv_idx_off (include/orb_mi355x.h).
+    keyframes: iterable of (kps KEYPOINT_DTYPE[n], desc u8[n,32], valid u8[n], node_of_feature i[n])."""
+    kps, desc, valid, nodes, offs, idxs = [], [], [], [], [], []
+    kp_off, node_off, idx_off = [0], [0], []
+    nidx = 0
+    for k, d, v, nid in keyframes:
+        n_ids, o, ix = featvec_csr(nid)
+        kps.append(np.ascontiguousarray(k, abi.KEYPOINT_DTYPE).view(np.uint8).reshape(-1))
+        desc.append(np.ascontiguousarray(d, np.uint8).reshape(-1))
+        valid.append(np.ascontiguousarray(v, np.uint8))
+        nodes.append(n_ids)
+        offs.append(o)
+        idx_off.append(nidx)
+        nidx += len(ix)
+        idxs.append(ix)
+        kp_off.append(kp_off[-1] + len(k))
+        node_off.append(node_off[-1] + len(n_ids))
+    cat = lambda a, dt: np.ascontiguousarray(np.concatenate(a) if a else np.zeros(0, dt), dt)
+    return dict(kps=cat(kps, np.uint8), desc=cat(desc, np.uint8), valid=cat(valid, np.uint8),
+                kp_off=np.array(kp_off, np.int64), fv_node=cat(nodes, np.uint32), fv_off=cat(offs, np.int32),
+                fv_idx=cat(idxs, np.uint32), fv_node_off=np.array(node_off, np.int64),
+                fv_idx_off=np.array(idx_off, np.int64))
+
+
+def keyframe_view(arrays: dict, i: int):
+    """Keyframe i of a packed map as (kps, desc, valid, (node_ids, offsets, idx))."""
+    a0, a1 = int(arrays["kp_off"][i]), int(arrays["kp_off"][i + 1])
+    n0, n1 = int(arrays["fv_node_off"][i]), int(arrays["fv_node_off"][i + 1])
+    i0 = int(arrays["fv_idx_off"][i])
+    offs = arrays["fv_off"][n0 + i:n1 + i + 1]
+    kps = arrays["kps"][a0 * 28:a1 * 28].view(abi.KEYPOINT_DTYPE)
+    return (kps, arrays["desc"][a0 * 32:a1 * 32].reshape(-1, 32), arrays["valid"][a0:a1],
+            (arrays["fv_node"][n0:n1], offs, arrays["fv_idx"][i0:i0 + (int(offs[-1]) if len(offs) else 0)]))
 
 
 class DeviceKeyframeMap:
-    def __init__(self, keyframes, device="cuda", fv_desc=True):
-        """keyframes: iterable of (kps KEYPOINT_DTYPE[n], desc u8[n,32], valid u8[n], node_of_feature i[n]).
+    def __init__(self, keyframes=None, device="cuda", fv_desc=True, arrays=None):
+        """keyframes: iterable of (kps KEYPOINT_DTYPE[n], desc u8[n,32], valid u8[n], node_of_feature i[n]),
+        or arrays: the same already packed (pack(), synth.keyframe_map()).
         fv_desc: also keep the descriptors in FeatureVector order (map->fv_desc)."""
         import torch
-        kps, desc, valid, nodes, offs, idxs = [], [], [], [], [], []
-        kp_off, node_off, idx_off = [0], [0], []
-        for k, d, v, nid in keyframes:
-            n_ids, o, ix = featvec_csr(nid)
-            kps.append(np.ascontiguousarray(k, abi.KEYPOINT_DTYPE).view(np.uint8).reshape(-1))
-            desc.append(np.ascontiguousarray(d, np.uint8).reshape(-1))
-            valid.append(np.ascontiguousarray(v, np.uint8))
-            nodes.append(n_ids)
-            offs.append(o)
-            idx_off.append(sum(len(x) for x in idxs))
-            idxs.append(ix)
-            kp_off.append(kp_off[-1] + len(k))
-            node_off.append(node_off[-1] + len(n_ids))
-        self.nkf = len(kp_off) - 1
-        t = lambda a, dt: torch.from_numpy(np.ascontiguousarray(np.concatenate(a) if a else np.zeros(0, dt), dt)).to(device)
-        self.t = dict(kps=t(kps, np.uint8), desc=t(desc, np.uint8), valid=t(valid, np.uint8),
-                      kp_off=t([np.array(kp_off, np.int64)], np.int64), fv_node=t(nodes, np.uint32),
-                      fv_off=t(offs, np.int32), fv_idx=t(idxs, np.uint32),
-                      fv_node_off=t([np.array(node_off, np.int64)], np.int64),
-                      fv_idx_off=t([np.array(idx_off, np.int64)], np.int64))
+        a = arrays if arrays is not None else pack(keyframes)
+        self.nkf = len(a["kp_off"]) - 1
+        self.t = {name: torch.from_numpy(np.ascontiguousarray(a[name])).to(device)
+                  for name in ("kps", "desc", "valid", "kp_off", "fv_node", "fv_off", "fv_idx", "fv_node_off",
+                               "fv_idx_off")}
         p = lambda name: self.t[name].data_ptr()
         self.struct = OrbmKfMapDevice(self.nkf, p("kps"), p("desc"), p("valid"), p("kp_off"), p("fv_node"),
                                       p("fv_off"), p("fv_idx"), p("fv_node_off"), p("fv_idx_off"),
-                                      node_off[-1], sum(len(x) for x in idxs), None)
+                                      int(a["fv_node_off"][-1]), int(len(a["fv_idx"])), None)
+        self.ready = None
         # the descriptors in FeatureVector order (orbm_kf_map_fv_desc), once per map
         nfv = self.struct.n_fv_total
         self.t["fv_desc"] = torch.empty(max(1, nfv) * 32, dtype=torch.uint8, device=device)
         if fv_desc and self.nkf > 0 and torch.device(device).type == "cuda":
-            st = torch.cuda.current_stream(self.t["fv_desc"].device).cuda_stream
+            cur = torch.cuda.current_stream(self.t["fv_desc"].device)
             rc = capi.lib().orbm_kf_map_fv_desc(C.byref(self.struct), C.c_void_p(self.t["fv_desc"].data_ptr()),
-                                                C.c_void_p(st))
+                                                C.c_void_p(cur.cuda_stream))
             capi.check(rc, "orbm_kf_map_fv_desc")
             self.struct.fv_desc = self.t["fv_desc"].data_ptr()
+            # a search on another stream waits for it (search_prepared)
+            self.ready = torch.cuda.Event()
+            self.ready.record(cur)
 
     def prepare_frame(self, kps, desc, node_of_feature):
         """The query frame resident in HBM (keypoints, descriptors, FeatureVector
@@ -96,7 +124,10 @@ class DeviceKeyframeMap:
         frame's device output tensors (overwritten by the next call)."""
         import torch
         dev = self.t["kps"].device
-        st = (stream or torch.cuda.current_stream(dev)).cuda_stream
+        strm = stream or torch.cuda.current_stream(dev)
+        if self.ready is not None:
+            strm.wait_event(self.ready)
+        st = strm.cuda_stream
         rc = capi.lib().orbm_search_by_bow_batch_device(C.byref(self.struct), C.byref(ft["frame"]),
                                                         C.byref(ft["featvec"]), nnratio, int(check_ori),
                                                         ft["match"].data_ptr(), ft["nm"].data_ptr(), C.c_void_p(st))

@@ -171,3 +171,60 @@ def vocabulary(k: int = 10, levels: int = 6, seed: int = 5):
     weight[start:] = rng.uniform(0.1, 5.0, nleaf)
     return dict(nnodes=nnodes, depth_levels=levels, first_child=first_child, nchild=nchild,
                 node_desc=desc, word_id=word_id, weight=weight)
+
+
+def keyframe_map(kps: np.ndarray, desc: np.ndarray, node_of_feature: np.ndarray, ids, seed: int = 7,
+                 per_kf: int | None = None, valid_frac: float = 1.0) -> dict:
+    """A synthetic keyframe map around a query frame (config C5, SURVEY.md
+    §8(d)), packed in the orbm_kf_map_device layout (kfmap.pack).  Keyframe i
+    (ids: the map's keyframe ids, so any shard of the map is the same data)
+    holds per_kf of the query's features (default: all; 5000 of a 5000-feature
+    extractor's ~5008) with their node ids, descriptors with 2^-3, 2^-4 or 2^-5
+    of their bits flipped, angles jittered (+30 degrees for every 7th keyframe,
+    so the rotation filter drops matches), and MapPoints valid with
+    probability valid_frac (1.0: all valid, as SURVEY §8(d) states C5)."""
+    from . import kfmap
+    n = len(kps)
+    m = n if per_kf is None else min(per_kf, n)
+    ids = list(ids)
+    nkf = len(ids)
+    out_k = np.empty((nkf, m), np.dtype(kps.dtype))
+    kb = out_k.view(np.uint8).reshape(nkf, m, -1)            # rows as bytes: fast gathers
+    kps_b = np.ascontiguousarray(kps).view(np.uint8).reshape(n, -1)
+    out_d = np.empty((nkf, m, 32), np.uint8)
+    out_v = np.ones((nkf, m), np.uint8)
+    nodes, offs, idxs = [], [], []
+    node_off, idx_off, nidx = [0], [], 0
+    nid_all = np.asarray(node_of_feature, np.int64)
+    # bit-flip masks at rates 2^-3, 2^-4, 2^-5 (AND of 3..5 random bytes); a
+    # keyframe takes m consecutive rows of one pool from a random start
+    prng = np.random.default_rng(seed)
+    pools = []
+    for ands in (3, 4, 5):
+        p = np.frombuffer(prng.bytes(max(1 << 18, 2 * m) * 32), np.uint8).reshape(-1, 32).copy()
+        for _ in range(ands - 1):
+            p &= np.frombuffer(prng.bytes(p.size), np.uint8).reshape(-1, 32)
+        pools.append(p)
+    for j, i in enumerate(ids):
+        rng = np.random.default_rng(seed * 1_000_003 + int(i))
+        sel = np.sort(rng.permutation(n)[:m])
+        kk = out_k[j]
+        kb[j] = kps_b[sel]
+        kk["angle"] = (kk["angle"] + rng.normal(0, 4, m).astype(np.float32) + (30 if i % 7 == 0 else 0)) % 360
+        r = int(rng.integers(0, 3))
+        s0 = int(rng.integers(0, len(pools[r]) - m + 1))
+        np.bitwise_xor(desc[sel], pools[r][s0:s0 + m], out=out_d[j])
+        if valid_frac < 1.0:
+            out_v[j] = rng.random(m) < valid_frac
+        n_ids, o, ix = kfmap.featvec_csr(nid_all[sel])
+        nodes.append(n_ids)
+        offs.append(o)
+        idx_off.append(nidx)
+        nidx += len(ix)
+        idxs.append(ix)
+        node_off.append(node_off[-1] + len(n_ids))
+    cat = lambda a, dt: np.ascontiguousarray(np.concatenate(a) if a else np.zeros(0, dt), dt)
+    return dict(kps=out_k.reshape(-1).view(np.uint8), desc=out_d.reshape(-1), valid=out_v.reshape(-1),
+                kp_off=np.arange(nkf + 1, dtype=np.int64) * m, fv_node=cat(nodes, np.uint32),
+                fv_off=cat(offs, np.int32), fv_idx=cat(idxs, np.uint32),
+                fv_node_off=np.array(node_off, np.int64), fv_idx_off=np.array(idx_off, np.int64))

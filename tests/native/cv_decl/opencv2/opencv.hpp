@@ -1,9 +1,11 @@
 // Declaration-only subset of the OpenCV 4.x API that the reference's
 // include/ORBextractor.h and adapters/orbslam3/ORBextractor.cc use, with
 // OpenCV's own signatures (core/types.hpp, core/mat.hpp, core/hal/interface.h).
-// Test infrastructure for `g++ -fsyntax-only` of the adapter against the
-// reference header only (tests/test_adapter.py): nothing here is defined,
-// linked or run, and it stands in for no part of the reference itself.
+// Test infrastructure for the adapter against the reference header
+// (tests/test_adapter.py: `g++ -fsyntax-only`; tests/test_gpu_adapter.py: the
+// adapter linked with tests/native/cv_min.cpp, a minimal test-only
+// implementation of this subset, into a program run on the GPU).  It stands in
+// for no part of the reference itself.
 #pragma once
 #include <cstddef>
 #include <vector>
@@ -42,6 +44,7 @@ public:
 
 struct MatStep {
     size_t operator[](int i) const;
+    size_t buf[2];
 };
 
 class _OutputArray;
@@ -63,6 +66,7 @@ public:
     int flags, dims, rows, cols;
     uchar* data;
     MatStep step;
+    void* u;   // the shared buffer (OpenCV: UMatData*)
 };
 
 class _InputArray {
@@ -70,6 +74,9 @@ public:
     _InputArray(const Mat& m);
     Mat getMat(int idx = -1) const;
     bool empty() const;
+protected:
+    int flags;
+    void* obj;
 };
 class _OutputArray : public _InputArray {
 public:

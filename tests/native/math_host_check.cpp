@@ -94,4 +94,62 @@ int sort_mismatches(int trials, int maxn, unsigned seed) {
 }
 
 float port_fast_atan2(float y, float x) { return orbmi::fast_atan2_deg(y, x); }
+
+// The reference's own sort (ORBextractor.cc:700): std::sort of
+// pair<int, ExtractorNode*> under compareNodes (:538-553, non-const
+// references as there), for each array [off[i], off[i+1]) of (cnt, x0);
+// perm receives the original index at every sorted position.
+struct RefNode { int x0; };
+static bool ref_compare_nodes(std::pair<int, RefNode*>& e1, std::pair<int, RefNode*>& e2) {
+    if (e1.first < e2.first) return true;
+    else if (e1.first > e2.first) return false;
+    else return e1.second->x0 < e2.second->x0;
+}
+void std_sort_perm(int narrays, const int* off, const int* cnt, const int* x0, int* perm) {
+    for (int a = 0; a < narrays; ++a) {
+        const int o = off[a], n = off[a + 1] - o;
+        std::vector<RefNode> nodes(n);
+        std::vector<std::pair<int, RefNode*>> v(n);
+        for (int i = 0; i < n; ++i) {
+            nodes[i].x0 = x0[o + i];
+            v[i] = {cnt[o + i], &nodes[i]};
+        }
+        std::sort(v.begin(), v.end(), ref_compare_nodes);
+        for (int i = 0; i < n; ++i) perm[o + i] = (int)(v[i].second - nodes.data());
+    }
+}
+
+// McIlroy's adversary ("A Killer Adversary for Quicksort", 1999) against
+// libstdc++'s std::sort: values are frozen lazily so that every pivot the
+// sort picks is among the smallest; the result (vals, a permutation of
+// 0..n-1) drives introsort to its depth limit (the heap-sort case).
+static int* g_val;
+static int g_gas, g_nsolid, g_cand;
+void antiqsort_vals(int n, int* vals) {
+    std::vector<int> ptr(n);
+    g_val = vals;
+    g_gas = n - 1;
+    g_nsolid = 0;
+    g_cand = 0;
+    for (int i = 0; i < n; ++i) { ptr[i] = i; vals[i] = g_gas; }
+    std::sort(ptr.begin(), ptr.end(), [](int x, int y) {
+        if (g_val[x] == g_gas && g_val[y] == g_gas) {
+            if (x == g_cand) g_val[x] = g_nsolid++;
+            else g_val[y] = g_nsolid++;
+        }
+        if (g_val[x] == g_gas) g_cand = x;
+        else if (g_val[y] == g_gas) g_cand = y;
+        return g_val[x] < g_val[y];
+    });
+}
+
+// std_sort_levels (k_quadtree's data-parallel statement) on one array:
+// 1 if it completes, 0 at the depth limit (where the device falls back).
+int levels_complete(int n, const int* cnt, const int* x0) {
+    std::vector<orbmi::SortRec> a(n);
+    for (int i = 0; i < n; ++i) a[i] = {cnt[i], x0[i], i};
+    std::vector<int> Lp(n + 1), Rp(n + 1);
+    std::vector<orbmi::SortFrame> qa(n + 1), qb(n + 1), lv(n + 1);
+    return orbmi::std_sort_levels(a.data(), n, Lp.data(), Rp.data(), qa.data(), qb.data(), lv.data()) ? 1 : 0;
+}
 }

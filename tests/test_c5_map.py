@@ -1,0 +1,69 @@
+"""Host side of config C5 (map-wide SearchByBoW, src/Tracking.cc:3641-3648 over
+a whole keyframe map): the packed map layout (kfmap.pack,
+synth.keyframe_map), its shard invariance (a keyframe's data depends on its
+id alone), and the oracle's threaded map loop against its
+one-keyframe SearchByBoW (ORBmatcher.cc:223-425).  CPU only."""
+import numpy as np
+
+from oracle import oracle as O
+from orb_slam3_vio_fixes_amd import abi, kfmap, synth
+
+
+def _query(seed=0, n=1200, nodes=40):
+    rng = np.random.default_rng(seed)
+    k = np.zeros(n, abi.KEYPOINT_DTYPE)
+    k["x"] = rng.uniform(0, 1920, n)
+    k["y"] = rng.uniform(0, 1080, n)
+    k["angle"] = rng.uniform(0, 360, n)
+    k["size"] = 31
+    d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    nid = rng.integers(0, nodes, n) * 13 + 5
+    return k, d, nid
+
+
+def test_pack_roundtrip_and_views():
+    k, d, nid = _query(1)
+    a = synth.keyframe_map(k, d, nid, range(6), seed=3, per_kf=1000, valid_frac=0.8)
+    lst = []
+    for i in range(6):
+        kk, kd, kv, (nodes, offs, idx) = kfmap.keyframe_view(a, i)
+        assert len(kk) == 1000 and kd.shape == (1000, 32) and len(kv) == 1000
+        assert np.all(np.diff(nodes.astype(np.int64)) > 0) and offs[0] == 0 and offs[-1] == 1000
+        node_of = np.full(1000, -1, np.int64)
+        for j, node in enumerate(nodes):
+            seg = idx[offs[j]:offs[j + 1]]
+            assert np.all(np.diff(seg.astype(np.int64)) > 0)
+            node_of[seg] = node
+        lst.append((kk, kd, kv, node_of))
+    p = kfmap.pack(lst)
+    for key in p:
+        np.testing.assert_array_equal(p[key], a[key], err_msg=key)
+    assert 0.7 < a["valid"].mean() < 0.9
+
+
+def test_keyframe_map_shard_invariance():
+    k, d, nid = _query(2)
+    whole = synth.keyframe_map(k, d, nid, range(10), seed=7, per_kf=1100)
+    lo = synth.keyframe_map(k, d, nid, range(0, 4), seed=7, per_kf=1100)
+    hi = synth.keyframe_map(k, d, nid, range(4, 10), seed=7, per_kf=1100)
+    for i in range(10):
+        part, j = (lo, i) if i < 4 else (hi, i - 4)
+        for x, y in zip(kfmap.keyframe_view(whole, i)[:3], kfmap.keyframe_view(part, j)[:3]):
+            np.testing.assert_array_equal(x.view(np.uint8), y.view(np.uint8))
+    assert whole["valid"].all()      # C5: every MapPoint valid by default
+
+
+def test_oracle_map_loop_equals_per_keyframe_search():
+    k, d, nid = _query(3)
+    a = synth.keyframe_map(k, d, nid, range(12), seed=5, per_kf=1150, valid_frac=0.9)
+    f, fv = abi.frame_struct(k, d, 1920, 1080), abi.featvec_struct(nid)
+    match, nm = O.search_by_bow_map(a, f, fv, 0.75, True, nthreads=4)
+    for i in range(12):
+        kk, kd, kv, (nodes, offs, idx) = kfmap.keyframe_view(a, i)
+        node_of = np.full(len(kk), -1, np.int64)
+        for j, node in enumerate(nodes):
+            node_of[idx[offs[j]:offs[j + 1]]] = node
+        rnm, rmatch = O.search_by_bow(abi.frame_struct(kk, kd, 1920, 1080), abi.featvec_struct(node_of), kv,
+                                      f, fv, 0.75, True)
+        assert nm[i] == rnm and rnm > 50
+        np.testing.assert_array_equal(match[i], rmatch)

@@ -1,0 +1,85 @@
+"""The drop-in extractor adapter at run time: adapters/orbslam3/ORBextractor.cc
+compiled against the reference's unmodified include/ORBextractor.h (and a
+minimal test-only cv::Mat, tests/native/cv_min.cpp) into
+tests/native/bin/adapter_extractor by __graft_entry__.build(), driven as
+Frame::ExtractORB drives the reference (src/Frame.cc:418-425).  Its
+keypoints, descriptors and monoIndex must equal orbx_extract's and the
+oracle's; the reference's edge behaviour must hold (-1 and untouched outputs
+on an empty image, src/ORBextractor.cc:1090-1091; descriptors released when
+no keypoint is found, :1107-1113); mvImagePyramid must equal the oracle's
+ComputePyramid levels (include/ORBextractor.h:83, read by
+src/Frame.cc:818-923), and be released when the host pyramid is switched off."""
+import subprocess
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from orb_slam3_vio_fixes_amd import abi, orb, synth
+
+pytestmark = pytest.mark.gpu
+ROOT = Path(__file__).resolve().parents[1]
+BIN = ROOT / "tests" / "native" / "bin" / "adapter_extractor"
+
+
+def run_adapter(tmp_path, img, nfeat, lap, reps=0):
+    if not BIN.exists():
+        pytest.fail(f"{BIN} missing: __graft_entry__.build() builds it where the reference tree is present")
+    h, w = img.shape
+    src = tmp_path / "img.u8"
+    src.write_bytes(np.ascontiguousarray(img, np.uint8).tobytes())
+    out = tmp_path / "out"
+    out.mkdir()
+    r = subprocess.run([str(BIN), str(src), str(w), str(h), str(nfeat), str(lap[0]), str(lap[1]), str(out),
+                        str(reps)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    n, mono, drows, dcols, dempty, empty_ret = map(int, (out / "meta.txt").read_text().split())
+    kps = np.frombuffer((out / "kps.bin").read_bytes(), abi.KEYPOINT_DTYPE)
+    desc = np.frombuffer((out / "desc.bin").read_bytes(), np.uint8).reshape(-1, 32)
+    levels = []
+    for lv in range(8):
+        b = (out / f"level{lv}.bin").read_bytes()
+        rows, cols = np.frombuffer(b[:8], np.int32)
+        levels.append(np.frombuffer(b[8:], np.uint8).reshape(rows, cols))
+    timing = (out / "time.txt").read_text().split() if reps else None
+    return dict(n=n, mono=mono, drows=drows, dcols=dcols, dempty=dempty, empty_ret=empty_ret, kps=kps, desc=desc,
+                levels=levels, timing=timing)
+
+
+@pytest.mark.parametrize("w,h,nfeat,lap", [(752, 480, 1000, (0, 1000)), (752, 480, 1200, (0, 0)),
+                                           (512, 512, 1500, (0, 511)), (1920, 1080, 5000, (0, 1000))])
+def test_adapter_equals_c_abi_and_oracle(gpu_lib, tmp_path, w, h, nfeat, lap):
+    img = synth.image(w, h, synth.frame_seed(7, w + nfeat))
+    a = run_adapter(tmp_path, img, nfeat, lap)
+    k, d, m = orb.ORBextractor(nfeat, 1.2, 8, 20, 7)(img, None, lap)
+    ref = O.OracleExtractor(nfeat, 1.2, 8, 20, 7)
+    rk, rd, rm = ref(img, lap)
+    assert a["n"] == len(k) == len(rk) and a["mono"] == m == rm
+    assert (a["drows"], a["dcols"], a["dempty"]) == (len(rk), 32, 0)
+    assert np.array_equal(a["kps"].view(np.uint8), rk.view(np.uint8))
+    assert np.array_equal(a["kps"].view(np.uint8), k.view(np.uint8))
+    assert np.array_equal(a["desc"], rd) and np.array_equal(a["desc"], d)
+    assert a["empty_ret"] == -1
+    for lv, lvl in enumerate(a["levels"]):
+        np.testing.assert_array_equal(lvl, ref.level(lv), err_msg=f"mvImagePyramid[{lv}]")
+
+
+def test_adapter_no_keypoints_releases_descriptors(gpu_lib, tmp_path):
+    """A flat image has no FAST corner: zero keypoints and released
+    descriptors (the reference's _descriptors.release(), :1107-1109)."""
+    img = np.full((480, 752), 128, np.uint8)
+    a = run_adapter(tmp_path, img, 1000, (0, 1000))
+    assert a["n"] == 0 and a["dempty"] == 1 and a["drows"] == 0
+    assert len(O.OracleExtractor(1000, 1.2, 8, 20, 7)(img, (0, 1000))[0]) == 0
+
+
+def test_adapter_host_pyramid_cost(gpu_lib, tmp_path):
+    """The adapter's per-call cost with and without the eight host copies of
+    mvImagePyramid (ORBextractorSetHostPyramid); off, the levels are released."""
+    img = synth.image(752, 480, synth.frame_seed(7, 3))
+    a = run_adapter(tmp_path, img, 1000, (0, 1000), reps=100)
+    with_pyr, without, released = float(a["timing"][0]), float(a["timing"][1]), int(a["timing"][2])
+    print(f"adapter ms/call: host pyramid {with_pyr:.3f}, none {without:.3f}")
+    assert released == 1
+    assert 0 < without <= with_pyr * 1.05

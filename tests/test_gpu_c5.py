@@ -72,33 +72,51 @@ def _kps(rng, n):
     return k
 
 
-@pytest.mark.parametrize("seed,wave_resolve,mfma,fv_desc", [(3, "0", "1", True), (3, "0", "1", False),
-                                                             (4, "0", "1", True), (3, "1", "1", True),
-                                                             (4, "0", "0", True)])
-def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monkeypatch):
-    """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
-    against the node-per-wave kernel on inputs that exercise its exactness
-    argument: few frame nodes (nodes of 2-400 features, so complete and
-    incomplete top-4 lists), frame descriptors repeated (distance ties,
-    first position wins), keyframe features repeated up to 6 times (the
-    earlier copies take their best candidates, so lists run out of untaken
-    keys and the exact rescan runs), invalid MapPoints, KF nodes the frame
-    does not hold."""
+def _adversarial(seed, nf=1500, shape="default", nkf=12):
+    """Inputs that exercise the lane-per-keyframe-feature search's exactness
+    argument: frame nodes of 2 to several hundred features (complete and
+    incomplete top-4 lists), frame descriptors repeated (distance ties, first
+    position wins), keyframe features repeated up to 6 times (the earlier
+    copies take their best candidates, so lists run out of untaken keys and
+    the exact rescan runs), invalid MapPoints, KF nodes the frame does not
+    hold.  shape: "default" (largest node ~375 features), "big" (one node of
+    ~45 % of the frame: > 512 features, the big-node resolve form or, without
+    it, the match-row 'taken' test), "many_nodes" (> 1024 frame nodes: one
+    bucket counter per node instead of 64 sub-counters).  The highest frame
+    node (the end of the node-ordered expansion) holds 37 features, not a
+    multiple of the 32-row tile, and the keyframes are padded so the bucketed
+    slots end in a partly live top-4 block."""
     rng = np.random.default_rng(seed)
-    nf = 1500
     fd = rng.integers(0, 256, (nf, 32), dtype=np.uint8)
     dup = rng.random(nf) < 0.15
     fd[dup] = fd[rng.integers(0, nf, dup.sum())]
     fk = _kps(rng, nf)
-    # node sizes from tiny to large: node i holds ~ geometric share
-    fnode = np.minimum(rng.geometric(0.08, nf), 40).astype(np.int64) * 7 + 100
-    fnode[rng.random(nf) < 0.25] = 50                    # a ~375-feature node
-    fnode[rng.random(nf) < 0.003] = 5                    # a 2-5 feature node
+    if shape == "many_nodes":
+        fnode = rng.integers(0, 1500, nf).astype(np.int64) * 3 + 100
+    else:
+        fnode = np.minimum(rng.geometric(0.08, nf), 40).astype(np.int64) * 7 + 100
+        fnode[rng.random(nf) < (0.45 if shape == "big" else 0.25)] = 50   # one large node
+        fnode[rng.random(nf) < 0.003] = 5                                    # a 2-5 feature node
+    top = int(fnode.max()) + 1
+    fnode[rng.choice(nf, 37, replace=False)] = top                            # last node: 37 features
     kfs = []
-    for i in range(12):
+    for i in range(nkf):
         src = rng.choice(nf, size=int(nf * rng.uniform(0.3, 0.7)), replace=False)
         reps = np.where(rng.random(len(src)) < 0.2, rng.integers(2, 7, len(src)), 1)
         src = np.repeat(src, reps)
+        lacks = rng.random(len(src)) < 0.05                # nodes the frame lacks
+        if i == nkf - 1:
+            # bucket sizes are padded to 64 and a top-4 block takes 128 slots:
+            # make the total an odd number of 64s (the last block half live)
+            cnt = {int(nd): 0 for nd in np.unique(fnode)}
+            for nid in [x[3] for x in kfs] + [fnode[src][~lacks]]:
+                for nd in nid[np.isin(nid, fnode)]:
+                    cnt[int(nd)] += 1
+            if sum((c + 63) // 64 for c in cnt.values()) % 2 == 0:
+                # push the top node's bucket over its next multiple of 64
+                extra = 64 - cnt[top] % 64 + 1 if cnt[top] % 64 else 1
+                src = np.concatenate([src, rng.choice(np.nonzero(fnode == top)[0], extra)])
+                lacks = np.concatenate([lacks, np.zeros(extra, bool)])
         kd = fd[src].copy()
         flip = rng.integers(0, 256, kd.shape, dtype=np.uint8)
         for _ in range(int(rng.integers(2, 5))):
@@ -107,9 +125,34 @@ def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monk
         kk = _kps(rng, len(src))
         kk["angle"] = (fk["angle"][src] + rng.normal(0, 3, len(src))) % 360
         nid = fnode[src].copy()
-        nid[rng.random(len(src)) < 0.05] = 99999          # a node the frame lacks
+        nid[lacks] = 99999
         valid = (rng.random(len(src)) < 0.85).astype(np.uint8)
         kfs.append((kk, kd, valid, nid))
+    return fk, fd, fnode, kfs
+
+
+def _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch, min_matches=20):
+    got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
+    monkeypatch.setenv("ORBM_BOW_KFLANE", "0")
+    old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
+    np.testing.assert_array_equal(got, old)
+    np.testing.assert_array_equal(gnm, onm)
+    f, fv = abi.frame_struct(fk, fd, 640, 480), abi.featvec_struct(fnode)
+    for i, (kk, kd, valid, nid) in enumerate(kfs):
+        rnm, rmatch = O.search_by_bow(abi.frame_struct(kk, kd, 640, 480), abi.featvec_struct(nid), valid,
+                                      f, fv, 0.75, True)
+        assert gnm[i] == rnm
+        np.testing.assert_array_equal(got[i], rmatch)
+    assert gnm.min() > min_matches
+
+
+@pytest.mark.parametrize("seed,wave_resolve,mfma,fv_desc", [(3, "0", "1", True), (3, "0", "1", False),
+                                                             (4, "0", "1", True), (3, "1", "1", True),
+                                                             (4, "0", "0", True)])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monkeypatch):
+    """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
+    against the node-per-wave kernel (k_bow) on _adversarial inputs."""
+    fk, fd, fnode, kfs = _adversarial(seed)
     m = kfmap.DeviceKeyframeMap(kfs, fv_desc=fv_desc)
     assert m.struct.n_nodes_total > 0 and m.struct.n_fv_total > 0
     assert bool(m.struct.fv_desc) == fv_desc
@@ -119,14 +162,65 @@ def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monk
     monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
     monkeypatch.setenv("ORBM_BOW_KFLANE_WAVE_RESOLVE", wave_resolve)
     monkeypatch.setenv("ORBM_BOW_KFLANE_MFMA", mfma)
-    got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
-    monkeypatch.setenv("ORBM_BOW_KFLANE", "0")
-    old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
-    np.testing.assert_array_equal(got, old)
-    np.testing.assert_array_equal(gnm, onm)
-    for i, (kk, kd, valid, nid) in enumerate(kfs):
-        rnm, rmatch = O.search_by_bow(abi.frame_struct(kk, kd, 640, 480), abi.featvec_struct(nid), valid,
-                                      abi.frame_struct(fk, fd, 640, 480), abi.featvec_struct(fnode), 0.75, True)
-        assert gnm[i] == rnm
-        np.testing.assert_array_equal(got[i], rmatch)
-    assert gnm.min() > 20
+    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch)
+
+
+@pytest.mark.parametrize("case", ["big", "big_nobig", "huge_frame", "many_nodes", "nset2", "nset2_big"])
+def test_c5_kf_lane_resolve_forms(gpu_lib, case, monkeypatch):
+    """The resolve and top-4 forms the default C5 data never reaches:
+    big      frame nodes of > 512 features: k_bowk_resolve_lane<true, true>
+             (one wave per block, a bitmap over every frame position in LDS);
+    big_nobig ORBM_BOWK_BIG=0: the 256-thread form takes every node, with the
+             'taken' test of large nodes read from the match row;
+    huge_frame a frame of 9000 features (> 8192: no LDS bitmap fits, the
+             match-row form is the only one);
+    many_nodes > 1024 frame nodes: single bucket counters (nsub = 1);
+    nset2    ORBM_BOWK_NSET=2, two 32-column keyframe sets per MFMA wave."""
+    nf = 9000 if case == "huge_frame" else 2500
+    shape = "many_nodes" if case == "many_nodes" else ("big" if "big" in case or case == "huge_frame" else "default")
+    fk, fd, fnode, kfs = _adversarial(11 + len(case), nf=nf, shape=shape, nkf=8)
+    if shape == "big" or case == "huge_frame":
+        assert np.bincount(fnode).max() > 512
+    if case == "many_nodes":
+        assert len(np.unique(fnode)) > 1024
+    m = kfmap.DeviceKeyframeMap(kfs)
+    monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
+    if case == "big_nobig":
+        monkeypatch.setenv("ORBM_BOWK_BIG", "0")
+    if case.startswith("nset2"):
+        monkeypatch.setenv("ORBM_BOWK_NSET", "2")
+    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch, min_matches=5)
+
+
+@pytest.fixture(scope="module")
+def c5_full(c5):
+    """C5 at its stated size: 10,000 keyframes x 5000
+    descriptors (50 M keyframe features, all MapPoints valid) around the
+    query frame, and the oracle's SearchByBoW for every keyframe (16 threads)."""
+    k, d, voc = c5
+    fnode = orb.transform(voc, d, 4)[2]
+    a = synth.keyframe_map(k, d, fnode, range(10000), seed=7, per_kf=5000)
+    assert len(a["kp_off"]) == 10001 and int(a["kp_off"][-1]) == 50_000_000 and a["valid"].all()
+    f, fv = abi.frame_struct(k, d, 1920, 1080), abi.featvec_struct(fnode)
+    rmatch, rnm = O.search_by_bow_map(a, f, fv, 0.75, True, nthreads=16)
+    m = kfmap.DeviceKeyframeMap(arrays=a)
+    return k, d, fnode, m, rmatch, rnm
+
+
+@pytest.mark.parametrize("variant", ["default", "k_bow", "nset2", "no_big", "valu_topk"])
+def test_c5_full_map_every_keyframe(gpu_lib, c5_full, variant, monkeypatch):
+    """Map-wide SearchByBoW (orbm_search_by_bow_batch_device) over the full
+    10k-keyframe map == the oracle for EVERY keyframe (match row and count),
+    in each search form: the default lane-per-keyframe-feature search, the
+    node-per-wave k_bow, two MFMA column sets, no big-node form, the VALU
+    top-4 pass.  Reference: ORBmatcher.cc:223-425, Tracking.cc:3641-3648."""
+    k, d, fnode, m, rmatch, rnm = c5_full
+    env = {"k_bow": ("ORBM_BOW_KFLANE", "0"), "nset2": ("ORBM_BOWK_NSET", "2"),
+           "no_big": ("ORBM_BOWK_BIG", "0"), "valu_topk": ("ORBM_BOW_KFLANE_MFMA", "0")}.get(variant)
+    if env:
+        monkeypatch.setenv(*env)
+    match, nm = m.search_by_bow(k, d, fnode, 0.75, True)
+    nm = nm.cpu().numpy()
+    np.testing.assert_array_equal(nm, rnm)
+    np.testing.assert_array_equal(match.cpu().numpy(), rmatch)
+    assert rnm.min() > 100

@@ -206,3 +206,29 @@ def test_pyramid_row_load_widths(gpu_lib, w, h, mode):
             np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"frame {f} level {lev}")
         ni = int(n[f])
         same_frame(orb.keypoints_from_device(kps[f, :ni]), desc[f, :ni].cpu().numpy(), int(mono[f]), rk, rd, rm)
+
+
+@pytest.mark.parametrize("w,h", [(752, 480), (320, 240), (512, 512)])
+def test_pyr_stream_counters_at_lds_top(gpu_lib, w, h, monkeypatch):
+    """Round 2 moved k_pyr_stream's per-step wave-item counters from the top of
+    its ~139 KiB LDS allocation to dword 0 after wrong pyramids and a hang,
+    and blamed LDS atomics at high addresses.  With ORB_PYR_CNT_END=1 the
+    counters sit after the rings again -- outside the copied table image, so
+    the kernel zeroes them -- and every level of every frame must still equal
+    the oracle's ComputePyramid (ORBextractor.cc:1170-1195): the atomics at the
+    top of LDS are fine once the counters start at zero."""
+    import torch
+    monkeypatch.setenv("ORB_PYR_CNT_END", "1")
+    seq = synth.sequence(w, h, 40, config=2, start=1500)
+    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.set_pyramid_mode(2)
+    kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
+    torch.cuda.synchronize()
+    assert ex.pyramid_kernel() == 2
+    for f in (0, 1, 17, 39):
+        ref = O.OracleExtractor(1000, 1.2, 8, 20, 7)
+        rk, rd, rm = ref(seq[f], (0, 1000))
+        for lev, a in enumerate(ex.batch_pyramid(f)):
+            np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"frame {f} level {lev}")
+        ni = int(n[f])
+        same_frame(orb.keypoints_from_device(kps[f, :ni]), desc[f, :ni].cpu().numpy(), int(mono[f]), rk, rd, rm)

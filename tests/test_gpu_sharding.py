@@ -59,3 +59,31 @@ def test_two_ranks_equal_one_rank_with_seam_pair(tmp_path):
             assert np.array_equal(r["matches"][i, :m], one["matches"][t, :m]), t
             pairs += 1
     assert pairs == 2 * B - 1            # every consecutive pair of the job, seam included
+
+
+def test_c5_two_rank_map_shards_equal_one_rank(tmp_path):
+    """Config C5 sharded as SURVEY §8(e) states it: the keyframe map split by
+    keyframe id over 2 fresh ranks (sharing the box's GPU, gloo), the
+    vocabulary broadcast once and the query frame per query from rank 0, the
+    query's node ids computed on every rank by orbv_transform_device on the
+    broadcast, HBM-resident vocabulary, then the map-wide SearchByBoW on each
+    shard (tools/bench_c5.py).  Reference: KeyFrameDatabase.cc:733-845 (the
+    candidates), Tracking.cc:3641-3648 (one SearchByBoW per candidate).  The
+    merged per-keyframe matches and counts must equal the 1-rank run."""
+    env = dict(os.environ, ORB_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    common = ["--nkf", "601", "--reps", "1", "--warmup", "1", "--cpu-sample", "0"]
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tools/bench_c5.py",
+          "--dump", str(tmp_path / "two")] + common, env)
+    env1 = {k: v for k, v in env.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    _run([sys.executable, "tools/bench_c5.py", "--dump", str(tmp_path / "one")] + common, env1)
+    one = np.load(tmp_path / "one" / "rank0.npz")
+    parts = [np.load(tmp_path / "two" / f"rank{r}.npz") for r in (0, 1)]
+    assert [len(p["ids"]) for p in parts] == [301, 300]
+    ids = np.concatenate([p["ids"] for p in parts])
+    np.testing.assert_array_equal(ids, np.arange(601))
+    for p in parts:
+        np.testing.assert_array_equal(p["nid"], one["nid"])          # device descent on the broadcast vocabulary
+    np.testing.assert_array_equal(np.concatenate([p["match"] for p in parts]), one["match"])
+    np.testing.assert_array_equal(np.concatenate([p["nm"] for p in parts]), one["nm"])
+    assert one["nm"].min() > 100

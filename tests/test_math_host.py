@@ -51,3 +51,19 @@ def test_fast_atan2_port_matches_oracle(lib):
     vals[50:100, 0] = 0
     for y, x in vals:
         assert lib.port_fast_atan2(float(y), float(x)) == O.fast_atan2(float(y), float(x))
+
+
+def test_host_sort_statement_on_adversarial_inputs(lib):
+    """McIlroy's quicksort adversary against libstdc++ std::sort reaches the
+    introsort depth limit; the data-parallel statement reports it (so the
+    device falls back to the sequential port, tests/test_gpu_sort.py)."""
+    lib.antiqsort_vals.argtypes = [C.c_int, C.c_void_p]
+    lib.levels_complete.argtypes = [C.c_int, C.c_void_p, C.c_void_p]
+    for n in [40, 300, 2000]:
+        v = np.zeros(n, np.int32)
+        lib.antiqsort_vals(n, v.ctypes.data)
+        assert sorted(v.tolist()) == list(range(n))
+        z = np.zeros(n, np.int32)
+        assert lib.levels_complete(n, v.ctypes.data, z.ctypes.data) == 0
+        r = np.random.default_rng(n).permutation(n).astype(np.int32)
+        assert lib.levels_complete(n, r.ctypes.data, z.ctypes.data) == 1

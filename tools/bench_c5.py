@@ -7,15 +7,16 @@ orbm_search_by_bow_batch_device).
 
 Query: HIP extraction (ORBextractor(5000, 1.2, 8, 20, 7)), node ids at
 levelsup 4 from a full-size synthetic vocabulary (k=10, L=6, 1,111,111
-nodes) by the GPU descent.  Keyframes: random 60-95 % subsets of the query's
-features with their node ids, descriptors with 3-12 % of bits flipped, angles
-jittered, 90 % valid MapPoints (synthetic data; FeatureVectors are inputs of
-the search, not recomputed).  Timed: K repetitions of the map-wide search on
-one stream, bracketed by synchronisations.  CPU baseline: the oracle's
-SearchByBoW on a sample of keyframes (threads stated), whose results are
-also compared with the GPU's.  Multi-GPU (torch.distributed): the map is
-sharded by keyframe id, the query is broadcast from rank 0 (sharding.py).
-usage: python tools/bench_c5.py [--nkf 10000] [--reps 10] [--cpu-sample 200]"""
+nodes) by the GPU descent.  Map: 10,000 keyframes x 5000
+descriptors, every MapPoint valid (synth.keyframe_map: 5000 of the query's
+features per keyframe with their node ids, 2^-3..2^-5 of the descriptor bits
+flipped, angles jittered; synthetic data, FeatureVectors are inputs of the
+search, not recomputed).  Timed: K repetitions of the map-wide search on
+one stream, bracketed by synchronisations.  CPU baseline and parity: the
+oracle's SearchByBoW for EVERY keyframe of rank 0's shard (threads stated),
+compared with the GPU's.  Multi-GPU (torch.distributed): the map is sharded
+by keyframe id, the query is broadcast from rank 0 (sharding.py).
+usage: python tools/bench_c5.py [--nkf 10000] [--per-kf 5000] [--reps 10] [--cpu-sample N (default: all)]"""
 from __future__ import annotations
 
 import argparse
@@ -23,7 +24,6 @@ import json
 import os
 import sys
 import time
-from concurrent.futures import ThreadPoolExecutor
 from pathlib import Path
 
 import numpy as np
@@ -36,30 +36,15 @@ import benchlib  # noqa: E402
 W, H, NFEAT = 1920, 1080, 5000
 
 
-def make_keyframes(k, d, nid, ids, seed):
-    """Keyframes `ids` (their seeds derive from the id, so shards agree)."""
-    out = []
-    for i in ids:
-        rng = np.random.default_rng(seed * 1_000_003 + i)
-        sel = np.sort(rng.choice(len(k), size=int(len(k) * rng.uniform(0.6, 0.95)), replace=False))
-        kk = k[sel].copy()
-        kk["angle"] = (kk["angle"] + rng.normal(0, 4, len(sel)).astype(np.float32) + (30 if i % 7 == 0 else 0)) % 360
-        flip = rng.integers(0, 256, (len(sel), 32), dtype=np.uint8)
-        for _ in range(int(rng.integers(2, 5))):          # bit-flip rate 2^-3 .. 2^-5
-            flip &= rng.integers(0, 256, (len(sel), 32), dtype=np.uint8)
-        kd = d[sel] ^ flip
-        valid = (rng.random(len(sel)) < 0.9).astype(np.uint8)
-        out.append((kk, kd, valid, nid[sel]))
-    return out
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--nkf", type=int, default=10000)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--cpu-sample", type=int, default=200)
+    ap.add_argument("--per-kf", type=int, default=5000)
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="keyframes the oracle checks (-1: all)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dump", default="", help="directory: each rank saves its shard's matches (tests)")
     args = ap.parse_args()
     res = run_c5(args)
     if res is not None:
@@ -85,7 +70,11 @@ def run_c5(args):
     torch.cuda.set_device(local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        # RCCL; gloo (ORB_BENCH_BACKEND=gloo) when ranks share one GPU (tests)
+        if os.environ.get("ORB_BENCH_BACKEND", "nccl") == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     if rank == 0:
         img = synth.image(W, H, 5000)
@@ -109,9 +98,10 @@ def run_c5(args):
     nid = nid_t.cpu().numpy()
     ids = list(sharding.shard(args.nkf, rank, world))
     t0 = time.perf_counter()
-    kfs = make_keyframes(k, d, nid, ids, 7)
-    m = kfmap.DeviceKeyframeMap(kfs)
+    arrays = synth.keyframe_map(k, d, nid, ids, seed=7, per_kf=args.per_kf)
+    m = kfmap.DeviceKeyframeMap(arrays=arrays)
     build_s = time.perf_counter() - t0
+    nfeat_kf = int(arrays["kp_off"][-1])
     # the query frame resident in HBM before the timed region (keypoints,
     # descriptors, FeatureVector CSR, output rows), as after a device-side
     # extraction and transform; the per-query upload is timed separately below
@@ -148,7 +138,11 @@ def run_c5(args):
     upload_ms = (time.perf_counter() - tu) / args.reps * 1e3
     match, nm = m.search_prepared(fr, 0.75, True)
     torch.cuda.synchronize()
-    kf_feat = int(sum(len(x[0]) for x in kfs))
+    if getattr(args, "dump", ""):
+        os.makedirs(args.dump, exist_ok=True)
+        np.savez(os.path.join(args.dump, f"rank{rank}.npz"), ids=np.asarray(ids, np.int64), nid=nid,
+                 match=match.cpu().numpy(), nm=nm.cpu().numpy())
+    kf_feat = nfeat_kf
     search_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
     ach = kf_feat * KF_FEATURE_BYTES / (search_ms * 1e-3) / 1e9
     roof = {"kernel": "k_bow_init + k_bowk_* (map, fill, top-4 on MFMA, resolve) + k_bow_final (one map-wide search)", "bound": "hbm", "achieved": ach,
@@ -159,31 +153,31 @@ def run_c5(args):
     res = {"metric": "C5 map-wide SearchByBoW: keyframe pairs/s (1920x1080, 5000 feat, 10k-KF map)",
            "value": args.nkf * args.reps / el, "unit": "keyframe-pairs/s", "queries_per_s": args.reps / el,
            "ms_per_query": el / args.reps * 1e3, "n_gpus": world, "nkf": args.nkf, "features": int(len(k)),
-           "kf_features_total": int(sum(len(x[0]) for x in kfs)) * world, "data": "synthetic",
+           "kf_features_total": nfeat_kf * world, "mappoints_valid_frac": float(arrays["valid"].mean()), "data": "synthetic",
            "ms_per_query_with_frame_upload": upload_ms,
            "timed": "map-wide search, query frame resident in HBM (prepare_frame before the timed region)",
            "map_build_s_rank0": build_s, "mean_matches": float(nm.float().mean().item()),
            "scaling": "strong", "higher_is_better": True, "dtype": "u8", "roofline": roof}
-    if rank == 0 and args.cpu_sample > 0:
-        ns = min(args.cpu_sample, len(kfs))
+    if rank == 0 and args.cpu_sample != 0:
+        ns = len(ids) if args.cpu_sample < 0 else min(args.cpu_sample, len(ids))
+        sub = arrays
+        if ns < len(ids):   # the first ns keyframes of the shard
+            e = int(arrays["kp_off"][ns])
+            sub = dict(arrays, kp_off=arrays["kp_off"][:ns + 1], fv_node_off=arrays["fv_node_off"][:ns + 1],
+                       fv_idx_off=arrays["fv_idx_off"][:ns], kps=arrays["kps"][:e * 28], desc=arrays["desc"][:e * 32],
+                       valid=arrays["valid"][:e])
         f = abi.frame_struct(k, d, W, H)
         fv = abi.featvec_struct(nid)
-        sample = [(abi.frame_struct(kk, kd, W, H), abi.featvec_struct(kn), v) for kk, kd, v, kn in kfs[:ns]]
-        outs = [None] * ns
-
-        def work(t):
-            for i in range(t, ns, args.cpu_threads):
-                kf, kfv, v = sample[i]
-                outs[i] = O.search_by_bow(kf, kfv, v, f, fv, 0.75, True)
         t0 = time.perf_counter()
-        with ThreadPoolExecutor(args.cpu_threads) as pool:
-            list(pool.map(work, range(args.cpu_threads)))
+        rmatch, rnm = O.search_by_bow_map(sub, f, fv, 0.75, True, nthreads=args.cpu_threads)
         dt = time.perf_counter() - t0
         mh, nh = match[:ns].cpu().numpy(), nm[:ns].cpu().numpy()
-        bad = sum(int(outs[i][0] != nh[i] or not np.array_equal(outs[i][1], mh[i])) for i in range(ns))
+        bad = int(np.sum((rnm != nh) | np.any(rmatch != mh, axis=1)))
         res["cpu_baseline"] = {"value": ns / dt, "unit": "keyframe-pairs/s", "cores": args.cpu_threads,
-                               "kind": "port", "sample": f"first {ns} keyframes of the map, oracle SearchByBoW"}
-        res["parity"] = {"keyframes_checked": ns, "keyframes_mismatched": bad}
+                               "kind": "port", "sample": f"{'all' if ns == len(ids) else 'first'} {ns} keyframes of "
+                                                         "rank 0's map shard, oracle SearchByBoW (threaded map loop)"}
+        res["parity"] = {"keyframes_checked": ns, "keyframes_mismatched": bad,
+                         "matches_total": int(rnm.sum())}
     if world > 1:
         dist.destroy_process_group()
     return res if rank == 0 else None
