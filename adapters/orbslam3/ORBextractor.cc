@@ -81,9 +81,10 @@ orbx_handle* ORBextractorDeviceHandle(const ORBextractor* e)
 }
 
 // mvImagePyramid is read only by the host Frame::ComputeStereoMatches
-// (src/Frame.cc:818-923).  Its eight host copies (blocking device-to-host
-// copies of every level) are made after each extraction while this is on
-// (the default, so an unmodified Frame.cc keeps working); switch it off for
+// (src/Frame.cc:818-923).  While this is on (the default, so an unmodified
+// Frame.cc keeps working) every extraction also downloads the levels (one
+// copy inside orbx_extract's captured graph, orbx_set_host_pyramid) and
+// refreshes the eight cv::Mats from pinned host memory; switch it off for
 // the extractors of a monocular / RGB-D system, or when stereo matching runs
 // on the device (orbs_compute_stereo_matches).  Off, the
 // levels are released so a stale pyramid is never read.
@@ -93,6 +94,7 @@ void ORBextractorSetHostPyramid(ORBextractor* e, bool on)
     auto it = g_handles.find(e);
     if (it == g_handles.end()) throw std::runtime_error("ORBextractor: no MI355X handle");
     it->second.host_pyramid = on;
+    orbx_set_host_pyramid(it->second.h, on ? 1 : 0);
 }
 
 ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int _iniThFAST, int _minThFAST)
@@ -130,6 +132,9 @@ ORBextractor::ORBextractor(int _nfeatures, float _scaleFactor, int _nlevels, int
     Entry en;
     en.h = h;
     en.host_pyramid = host_pyramid_default();
+    // the levels come back inside orbx_extract's graph (one copy into pinned
+    // memory), so refreshing mvImagePyramid is a host memcpy per row
+    orbx_set_host_pyramid(h, en.host_pyramid ? 1 : 0);
     g_handles[this] = en;
 }
 

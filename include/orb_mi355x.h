@@ -108,6 +108,16 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
 int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step,
                    int* w, int* h_);
 
+/* mvImagePyramid for the host at the cost of one extra copy: with enable != 0
+ * every later orbx_extract on the handle also downloads levels 1.. of its
+ * image (one device-to-host copy inside its captured graph) next to the
+ * pinned copy of its input, and orbx_get_level then reads them from host
+ * memory (a memcpy per row) instead of copying each level from the device.
+ * For an adapter that keeps the public mvImagePyramid of
+ * include/ORBextractor.h:83 filled for the host Frame::ComputeStereoMatches
+ * (src/Frame.cc:818-923).  Not part of the reference interface. */
+int orbx_set_host_pyramid(orbx_handle* h, int enable);
+
 /* mvImagePyramid[level] of frame `frame` of the LAST batch call
  * (orbx_extract_batch or orbx_extract_batch_device) on this handle: the
  * per-image pyramid each of the reference's extractor objects exposes

@@ -650,6 +650,7 @@ static int build_plan(orbx_handle* hd, int w, int h, int maxB) {
     ++hd->plan_epoch;                                        // captured graphs point at the old buffers
     // the pyramids of earlier calls lived in the released buffers
     hd->have_last = false;
+    hd->x_pyr_valid = false;
     hd->last_frames = nullptr;
     hd->last_B = 0;
     const int rc = build_plan_into(hd, P, w, h, maxB);
@@ -2980,6 +2981,7 @@ int orbx_extract_batch_device(orbx_handle* h, int nframes, const uint8_t* d_fram
     h->last_pitch0 = (int)row_step;
     h->last_B = nframes;
     h->have_last = false;          // pyramid slot 0 now holds this batch's frame 0
+    h->x_pyr_valid = false;
     rc = run_batched(h, 0, nframes, d_frames, (long long)frame_stride, (int)row_step, (float)lap0, (float)lap1,
                      d_kps, d_desc, cap, d_n, d_mono, (hipStream_t)stream);
     if (rc) return rc;
@@ -3063,6 +3065,7 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
     }
     h->last_frames = dev;
     h->have_last = false;          // pyramid slot 0 now holds this batch's frame 0
+    h->x_pyr_valid = false;
     h->last_fstride = (long long)fbytes;
     h->last_pitch0 = (int)pitch;
     h->last_B = nframes;
@@ -3094,7 +3097,9 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size
     const size_t in_b = (size_t)P.in_pitch * hh, kp_b = (size_t)P.host_cap * sizeof(orb_keypoint),
                  de_b = (size_t)P.host_cap * 32;
     const size_t o_kp = (in_b + 255) & ~size_t(255), o_de = o_kp + ((kp_b + 255) & ~size_t(255)),
-                 o_nm = o_de + ((de_b + 255) & ~size_t(255)), total = o_nm + 16;
+                 o_nm = o_de + ((de_b + 255) & ~size_t(255)), o_py = o_nm + 256,
+                 total = o_py + (h->host_pyr ? (size_t)P.pyr_bytes : 0);
+    h->x_pyr_valid = false;
     if (h->x_pin_bytes < total) {
         if (h->x_pin) (void)hipHostFree(h->x_pin);
         h->x_pin = nullptr; h->x_pin_bytes = 0;
@@ -3105,8 +3110,8 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size
     if (!h->x_stream && hipStreamCreateWithFlags(&h->x_stream, hipStreamNonBlocking) != hipSuccess)
         return ORB_ERR_DEVICE;
     uint8_t* pin = (uint8_t*)h->x_pin;
-    const long long key[6] = {w, hh, lap0, lap1, h->plan_epoch, h->x_pin_gen};
-    if (!h->x_exec || !std::equal(key, key + 6, h->x_key)) {
+    const long long key[7] = {w, hh, lap0, lap1, h->plan_epoch, h->x_pin_gen, h->host_pyr ? 1 : 0};
+    if (!h->x_exec || !std::equal(key, key + 7, h->x_key)) {
         if (h->x_exec) (void)hipGraphExecDestroy(h->x_exec);
         h->x_exec = nullptr;
         hipStream_t st = h->x_stream;
@@ -3118,18 +3123,24 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size
         ok = ok && hipMemcpyAsync(pin + o_de, P.d_desc, de_b, hipMemcpyDeviceToHost, st) == hipSuccess;
         ok = ok && hipMemcpyAsync(pin + o_nm, P.d_n, 4, hipMemcpyDeviceToHost, st) == hipSuccess;
         ok = ok && hipMemcpyAsync(pin + o_nm + 4, P.d_mono, 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+        // mvImagePyramid for the host (orbx_set_host_pyramid): levels 1.. of
+        // this image in one copy; level 0 is the input already in pin
+        if (h->host_pyr)
+            ok = ok && hipMemcpyAsync(pin + o_py, P.d_pyr, (size_t)P.pyr_bytes, hipMemcpyDeviceToHost, st) == hipSuccess;
         hipGraph_t g = nullptr;
         const bool ended = hipStreamEndCapture(st, &g) == hipSuccess;
         if (ok && ended && g) ok = hipGraphInstantiate(&h->x_exec, g, nullptr, nullptr, 0) == hipSuccess;
         if (g) (void)hipGraphDestroy(g);
         (void)hipGetLastError();
         if (!ok || !ended || !h->x_exec) { h->x_exec = nullptr; return ORB_ERR_UNSUPPORTED; }
-        std::copy(key, key + 6, h->x_key);
+        std::copy(key, key + 7, h->x_key);
     }
     for (int y = 0; y < hh; ++y) std::memcpy(pin + (size_t)y * P.in_pitch, img + (size_t)y * step, w);
     ORB_CHECK(hipGraphLaunch(h->x_exec, h->x_stream));
     ORB_CHECK(hipStreamSynchronize(h->x_stream));
     const int32_t n = *(const int32_t*)(pin + o_nm), mono = *(const int32_t*)(pin + o_nm + 4);
+    h->x_pyr_valid = h->host_pyr;
+    h->x_pyr_off = o_py;
     if (n_out) *n_out = n;
     if (mono_out) *mono_out = mono;
     h->have_last = true;
@@ -3158,6 +3169,7 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
         rc = extract_graph(h, img, w, hh, step, lap0, lap1, kps, desc, cap, n_out, mono_out);
         if (rc != ORB_ERR_UNSUPPORTED) return rc;
     }
+    h->x_pyr_valid = false;
     ORB_CHECK(hipMemcpy2D(P.d_in, P.in_pitch, img, step, w, hh, hipMemcpyHostToDevice));
     rc = run_pipeline(h, 0, 1, P.d_in, (long long)P.in_pitch * hh, (int)P.in_pitch, (float)lap0, (float)lap1, P.d_kps,
                       P.d_desc, P.host_cap, P.d_n, P.d_mono, 0);
@@ -3195,6 +3207,13 @@ int orbx_set_pyramid_mode(orbx_handle* h, int mode) {
 }
 
 int orbx_pyramid_kernel(orbx_handle* h) { return h ? h->pyr_last : 0; }
+
+int orbx_set_host_pyramid(orbx_handle* h, int enable) {
+    if (!h) return ORB_ERR_PARAM;
+    h->host_pyr = enable != 0;
+    h->x_pyr_valid = false;
+    return ORB_OK;
+}
 
 int orbx_set_stage_event(orbx_handle* h, int stage, void* event) {
     if (!h || stage < 0 || stage > 5) return ORB_ERR_PARAM;
@@ -3235,9 +3254,14 @@ int orbx_get_level(orbx_handle* h, int level, uint8_t* dst, size_t dst_step, int
     if (w) *w = d.w;
     if (hh) *hh = d.h;
     if (!dst) return ORB_OK;
+    const size_t sp = level == 0 ? P.in_pitch : (size_t)d.pitch;
+    if (h->x_pyr_valid) {          // the host copy the graph made (orbx_set_host_pyramid)
+        const uint8_t* src = (const uint8_t*)h->x_pin + (level == 0 ? 0 : h->x_pyr_off + d.off);
+        for (int y = 0; y < d.h; ++y) std::memcpy(dst + (size_t)y * dst_step, src + (size_t)y * sp, d.w);
+        return ORB_OK;
+    }
     (void)hipSetDevice(h->device);
     const uint8_t* src = level == 0 ? P.d_in : P.d_pyr + d.off;
-    const size_t sp = level == 0 ? P.in_pitch : (size_t)d.pitch;
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
     return ORB_OK;
 }

@@ -166,8 +166,11 @@ struct orbx_handle {
     int plan_epoch = 0;
     hipStream_t x_stream = nullptr;
     hipGraphExec_t x_exec = nullptr;
-    long long x_key[6] = {0, 0, 0, 0, -1, 0};
+    long long x_key[7] = {0, 0, 0, 0, -1, 0, 0};
     void* x_pin = nullptr;
     size_t x_pin_bytes = 0;
     int x_pin_gen = 0;
+    bool host_pyr = false;           // orbx_set_host_pyramid: the graph also downloads levels 1.. to x_pin
+    bool x_pyr_valid = false;        // x_pin holds the last orbx_extract's pyramid (level 0 = its input)
+    size_t x_pyr_off = 0;            // levels 1.. in x_pin (at the plan's per-frame pyramid layout)
 };

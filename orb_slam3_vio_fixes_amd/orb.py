@@ -54,6 +54,11 @@ class ORBextractor:
         4 per-level runs (k_pyr_level)."""
         capi.check(capi.lib().orbx_set_pyramid_mode(self._h, mode), "orbx_set_pyramid_mode")
 
+    def set_host_pyramid(self, enable: bool) -> None:
+        """orbx_set_host_pyramid: later extractions also download their pyramid
+        (mvImagePyramid then reads host memory)."""
+        capi.check(capi.lib().orbx_set_host_pyramid(self._h, int(enable)), "orbx_set_host_pyramid")
+
     def pyramid_kernel(self) -> int:
         """Pyramid kernel of the last extraction: 1 k_pyramid, 2 k_pyr_stream, 3 k_resize, 4 k_pyr_level."""
         return int(capi.lib().orbx_pyramid_kernel(self._h))

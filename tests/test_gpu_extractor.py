@@ -185,3 +185,27 @@ def test_extract_batch_host_images(gpu_lib):
     (k, d, m), = ex.extract_batch([seq[1]])
     rk, rd, rm = ref(seq[1], (0, 1000))
     assert (len(k), m) == (len(rk), rm) and np.array_equal(d, rd)
+
+
+@pytest.mark.parametrize("host_pyr", [False, True])
+def test_mvimagepyramid_host_and_device_copies(gpu_lib, host_pyr):
+    """mvImagePyramid (include/ORBextractor.h:83) after orbx_extract, read
+    through orbx_get_level either from the device or -- with
+    orbx_set_host_pyramid -- from the copy the extraction graph downloads;
+    both equal the oracle's ComputePyramid levels, frame after frame, and a
+    later batch call or a toggle never serves a stale copy."""
+    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    ex.set_host_pyramid(host_pyr)
+    ref = O.OracleExtractor(1000, 1.2, 8, 20, 7)
+    for f in range(3):
+        img = synth.image(752, 480, synth.frame_seed(9, f))
+        ex(img, None, (0, 1000))
+        ref(img, (0, 1000))
+        for lev, a in enumerate(ex.mvImagePyramid):
+            np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"frame {f} level {lev}")
+    ex.set_host_pyramid(not host_pyr)
+    img = synth.image(752, 480, synth.frame_seed(9, 7))
+    ex(img, None, (0, 1000))
+    ref(img, (0, 1000))
+    for lev, a in enumerate(ex.mvImagePyramid):
+        np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"toggled, level {lev}")

@@ -34,6 +34,7 @@ import benchlib  # noqa: E402
 W, H, NFEAT, LAP = 752, 480, 1200, (0, 0)
 FX, BASE = 435.2, 0.11            # EuRoC-like rectified rig
 MBF = float(np.float32(BASE) * np.float32(FX))
+SFI_AFTER_STAGE = 2    # orbx_set_stage_event: the matching starts once the next extraction's FAST pass is done
 
 
 def cpu_baseline(left, right, threads):
@@ -95,32 +96,36 @@ def run_c3(args):
     s_st, s_sfi = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     ev = []
     it = [0]
+    # as in bench.py (C2): step k's matching is enqueued behind step k+1's
+    # "FAST cells done" stage event (orbx_set_stage_event), so it shares the GPU
+    # with the latency-bound quadtree / describe stages, not with the pyramid
+    # and FAST passes whose times the roofline reports
+    stage_ev = []
+    for S in sets:
+        e_ = torch.cuda.Event()
+        e_.record(stream)                                    # creates the event
+        capi.check(L.orbx_set_stage_event(S["ex"]._h, SFI_AFTER_STAGE, e_.cuda_event), "stage event")
+        stage_ev.append(e_)
+    pending = []
 
-    def step(timed=False):
-        S = sets[it[0] % 2]
-        it[0] += 1
-        ex, (kps, desc, n, mono), cap = S["ex"], S["out"], S["cap"]
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
-        if S["done"] is not None:
-            stream.wait_event(S["done"])                     # step k-2's matching released this set
-        if timed:
-            e[0].record(stream)
-        ex.extract_batch_device(frames, LAP, out=(kps, desc, n, mono))
-        if timed:
-            e[1].record(stream)
-        s_st.wait_stream(stream)
-        s_sfi.wait_stream(stream)
-        if timed:
+    def match(S, extracted, after, e):
+        kps, desc, n, mono = S["out"]
+        cap = S["cap"]
+        for st_ in (s_st, s_sfi):
+            st_.wait_event(extracted)
+            if after is not None:
+                st_.wait_event(after)
+        if e is not None:
             e[2].record(s_st)
             e[4].record(s_sfi)
-        capi.check(L.orbs_compute_stereo_matches_batch_device(ex._h, P, 0, P, kps.data_ptr(), desc.data_ptr(),
+        capi.check(L.orbs_compute_stereo_matches_batch_device(S["ex"]._h, P, 0, P, kps.data_ptr(), desc.data_ptr(),
                                                               n.data_ptr(), cap, BASE, MBF, S["ur"].data_ptr(),
                                                               S["dep"].data_ptr(), S["sad"].data_ptr(),
                                                               s_st.cuda_stream), "stereo")
         capi.check(L.orbm_search_for_initialization_batch_device(
             P, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
             100, 0.9, 1, S["matches"].data_ptr(), S["nmatch"].data_ptr(), s_sfi.cuda_stream), "sfi")
-        if timed:
+        if e is not None:
             e[3].record(s_st)
             e[5].record(s_sfi)
             ev.append(e)
@@ -129,14 +134,41 @@ def run_c3(args):
         done.record(s_sfi)
         S["done"] = done
 
+    def step(timed=False):
+        i = it[0] % 2
+        S = sets[i]
+        it[0] += 1
+        ex, (kps, desc, n, mono) = S["ex"], S["out"]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(6)] if timed else None
+        if S["done"] is not None:
+            stream.wait_event(S["done"])                     # step k-2's matching released this set
+        if timed:
+            e[0].record(stream)
+        ex.extract_batch_device(frames, LAP, out=(kps, desc, n, mono))
+        if timed:
+            e[1].record(stream)
+        extracted = torch.cuda.Event()
+        extracted.record(stream)
+        while pending:                                       # the previous step's matching, behind this stage
+            pS, pev, pe = pending.pop()
+            match(pS, pev, stage_ev[i], pe)
+        pending.append((S, extracted, e))
+
+    def flush():
+        while pending:
+            pS, pev, pe = pending.pop()
+            match(pS, pev, None, pe)
+
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     exs = [S["ex"] for S in sets]
     benchlib.profile_on(exs)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=True)
+    flush()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     xst, calls = benchlib.profile_read(exs)
@@ -172,7 +204,7 @@ def run_c4(args):
     """Config C4 (see the module docstring); returns the JSON object."""
     import torch
     from oracle import oracle as O
-    from orb_slam3_vio_fixes_amd import orb, synth
+    from orb_slam3_vio_fixes_amd import capi, orb, synth
     w = h = 512
     nf, lap = 1500, (0, 511)
     dev = torch.device("cuda", 0)
@@ -189,40 +221,69 @@ def run_c4(args):
     side = torch.cuda.Stream(dev)
     ev = []
     it = [0]
+    L = capi.lib()
+    # step k's knnMatch behind step k+1's "FAST cells done" stage event (C2's placement)
+    stage_ev = []
+    for _ in range(2):
+        e_ = torch.cuda.Event()
+        e_.record(stream)
+        stage_ev.append(e_)
+    pending = []
+    res = [None]
 
-    def step(timed=False):
-        S = sets[it[0] % 2]
-        it[0] += 1
+    def match(S, extracted, after, e):
         kps, desc, n, mono = S[:4]
-        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
-        if S[5] is not None:
-            stream.wait_event(S[5])
-        if timed:
-            e[0].record(stream)
-        ex.extract_batch_device(frames, lap, out=(kps, desc, n, mono))
-        if timed:
-            e[1].record(stream)
-        side.wait_stream(stream)
+        side.wait_event(extracted)
+        if after is not None:
+            side.wait_event(after)
         with torch.cuda.stream(side):
-            if timed:
+            if e is not None:
                 e[2].record(side)
-            res = orb.fisheye_stereo_candidates_batch_device(P, 0, P, desc, n, mono, cap)
-            if timed:
+            res[0] = orb.fisheye_stereo_candidates_batch_device(P, 0, P, desc, n, mono, cap)
+            if e is not None:
                 e[3].record(side)
                 ev.append(e)
             done = torch.cuda.Event()
             done.record(side)
         S[5] = done
-        return res
+
+    def step(timed=False):
+        i = it[0] % 2
+        S = sets[i]
+        it[0] += 1
+        kps, desc, n, mono = S[:4]
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timed else None
+        if S[5] is not None:
+            stream.wait_event(S[5])
+        capi.check(L.orbx_set_stage_event(ex._h, SFI_AFTER_STAGE, stage_ev[i].cuda_event), "stage event")
+        if timed:
+            e[0].record(stream)
+        ex.extract_batch_device(frames, lap, out=(kps, desc, n, mono))
+        if timed:
+            e[1].record(stream)
+        extracted = torch.cuda.Event()
+        extracted.record(stream)
+        while pending:
+            pS, pev, pe = pending.pop()
+            match(pS, pev, stage_ev[i], pe)
+        pending.append((S, extracted, e))
+
+    def flush():
+        while pending:
+            pS, pev, pe = pending.pop()
+            match(pS, pev, None, pe)
 
     for _ in range(args.warmup):
         step()
+    flush()
     torch.cuda.synchronize()
     benchlib.profile_on([ex])
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        idx, dist, l2r = step(timed=True)
+        step(timed=True)
+    flush()
     torch.cuda.synchronize()
+    idx, dist, l2r = res[0]
     dt = time.perf_counter() - t0
     xst, calls = benchlib.profile_read([ex])
     stage = {"extract_2B_images": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
