@@ -553,11 +553,17 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
                 P.roi_nd_max = std::max(P.roi_nd_max, ((c.x0 & 3) + c.cols + 3) >> 2);
                 P.win_max = std::max(P.win_max, (std::max(0, c.cols - 6) + 2) * (std::max(0, c.rows - 6) + 2));
                 P.win_pix_max = std::max(P.win_pix_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
+                {   // k_fast_cells' pre-test items of this cell: window rows x aligned dword pairs
+                    const int ww = std::max(0, c.cols - 6), X0 = (c.x0 & 3) + 3, j0 = X0 >> 2;
+                    const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
+                    P.item_max = std::max(P.item_max, std::max(0, c.rows - 6) * ((ndw + 1) >> 1));
+                }
                 ++nc;
             }
         }
         d.ncells = nc;
         cellsum += nc;
+        if (P.item_max >= 65536) return ORB_ERR_UNSUPPORTED;   // 16-bit item indices in k_fast_cells' list
         d.slot_total = slotsum - d.slot_base;
         P.max_level_cells = std::max(P.max_level_cells, nc);
         // DistributeOctTree sizing (ORBextractor.cc:559-561)
@@ -1190,6 +1196,7 @@ struct FastArgs {
     int roi_max, win_max;   // LDS per wave
     int kmask_bytes;
     int cand_bytes;         // u16 candidate list, one entry per window pixel at most
+    int ilist_bytes;        // u32 list of the pre-test items holding a candidate (ORB_FAST_EMIT 1)
 };
 
 // Arc strength of one direction on the raw ring values: max over the 16 arcs
@@ -1353,6 +1360,9 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #ifndef ORB_FAST_PRE2
 #define ORB_FAST_PRE2 0
 #endif
+#ifndef ORB_FAST_EMIT
+#define ORB_FAST_EMIT 1   // 1: items list + one expansion pass; 0: per-round bit loops (round 2)
+#endif
 #ifndef ORB_QT_LEVEL_MAJOR
 #define ORB_QT_LEVEL_MAJOR 1
 #endif
@@ -1405,10 +1415,11 @@ template <int PDW, int NV>
 __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
-    uint8_t* roi = smem + wv * (a.roi_max + a.win_max + a.cand_bytes + a.kmask_bytes);   // multiples of 16
+    uint8_t* roi = smem + wv * (a.roi_max + a.win_max + a.cand_bytes + a.kmask_bytes + a.ilist_bytes);   // multiples of 16
     uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
     uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_pix_max entries
     uint64_t* kmask = (uint64_t*)(sc + a.win_max + a.cand_bytes);   // NMS ballots, one per 64 candidates
+    uint32_t* ilist = (uint32_t*)(sc + a.win_max + a.cand_bytes + a.kmask_bytes);   // items holding candidates
 #ifdef ORB_FAST_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
@@ -1559,7 +1570,51 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 }
                 ncand += tot;
             };
-#if ORB_FAST_PRE2
+#if ORB_FAST_EMIT == 1
+            // 1a. items holding a candidate go to the wave's item list, one
+            //     ballot per round (at iniTh ~20 % of the items, ~3 pixels
+            //     each): item index | bright mask << 16 | dark mask << 24, bit
+            //     k = item pixel k (byte flags folded by one v_dot4 per half)
+            int nlist = 0;
+            for (int base = 0; base < nitems; base += kWave) {
+                uint32_t bl, bh, dl, dh;
+                int i0;
+                pretest(base + lane, bl, bh, dl, dh, i0);
+                const uint32_t mb = __builtin_amdgcn_udot4(bh >> 7, 0x80402010u,
+                                                           __builtin_amdgcn_udot4(bl >> 7, 0x08040201u, 0u, false), false);
+                const uint32_t md = __builtin_amdgcn_udot4(dh >> 7, 0x80402010u,
+                                                           __builtin_amdgcn_udot4(dl >> 7, 0x08040201u, 0u, false), false);
+                const bool has = (mb | md) != 0u;
+                const uint64_t bal = __ballot(has);
+                if (has) ilist[nlist + mask_rank(bal)] = (uint32_t)(base + lane) | (mb << 16) | (md << 24);
+                nlist += __popcll(bal);
+            }
+            fast_wave_sync();
+            // 1b. the listed items' pixels -> the candidate list, row-major
+            //     (items in order, pixels in order within an item)
+            for (int b0 = 0; b0 < nlist; b0 += kWave) {
+                const uint32_t e = b0 + lane < nlist ? ilist[b0 + lane] : 0u;
+                const uint32_t mb = (e >> 16) & 0xffu, md = e >> 24;
+                uint32_t m = mb | md;
+                const int pc = __popc(m);
+                const uint64_t q0 = __ballot(pc & 1), q1 = __ballot(pc & 2), q2 = __ballot(pc & 4),
+                               q3 = __ballot(pc & 8);
+                const int tot = __popcll(q0) + 2 * __popcll(q1) + 4 * __popcll(q2) + 8 * __popcll(q3);
+                int pos = ncand + mask_rank(q0) + 2 * mask_rank(q1) + 4 * mask_rank(q2) + 8 * mask_rank(q3);
+                if (m) {
+                    const int itm = (int)(e & 0xffffu);
+                    const int r = div_row(itm, inv_ndp);
+                    const int k = itm - (int)__umul24(r, ndp);
+                    const int idx0 = (int)__umul24(r, ww) + 4 * (j0 + 2 * k) - X0;
+                    while (m) {
+                        const int bb = __builtin_ctz(m);
+                        m &= m - 1;
+                        cand[pos++] = (uint16_t)((uint32_t)(idx0 + bb) | (((mb >> bb) & 1u) << 14) | (((md >> bb) & 1u) << 15));
+                    }
+                }
+                ncand += tot;
+            }
+#elif ORB_FAST_PRE2
             // two items per lane per round: both items' LDS reads and compass
             // chains in flight together
             for (int base = 0; base < nitems; base += 2 * kWave) {
@@ -2307,6 +2362,9 @@ extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
 #ifndef ORB_DESC_WAVES
 #define ORB_DESC_WAVES 4
 #endif
+#ifndef ORB_DESC_HDOT4
+#define ORB_DESC_HDOT4 1   // horizontal pass by v_dot4_u32_u8 (0: packed-u16 pairs, round 2)
+#endif
 #ifndef ORB_Q_UNROLL
 #define ORB_Q_UNROLL 1
 #endif
@@ -2328,6 +2386,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     // tap at an even index (v0v1 v2v3 v4v5 v6-) or an odd one (-v0 v1v2 v3v4 v5v6)
     const uint32_t W0e = k0 | (k1 << 16), W1e = k2 | (k3 << 16), W2e = k2 | (k1 << 16), W3e = k0;
     const uint32_t W0o = k0 << 16, W1o = k1 | (k2 << 16), W2o = k3 | (k2 << 16), W3o = k1 | (k0 << 16);
+#if ORB_DESC_HDOT4
+    // horizontal taps w = (k0 k1 k2 k3 k2 k1 k0) as bytes for v_dot4 on the
+    // words al[j], al[j+1], al[j+2] of an output at byte offset b = 0..3:
+    // b 0: (w0..w3)(w4 w5 w6 -); 1: (- w0 w1 w2)(w3..w6); 2: (- - w0 w1)(w2..w5)(w6 - - -);
+    // 3: (- - - w0)(w1..w4)(w5 w6 - -)
+    const uint32_t hw[10] = {k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), k2 | (k1 << 8) | (k0 << 16),
+                             (k0 << 8) | (k1 << 16) | (k2 << 24), k3 | (k2 << 8) | (k1 << 16) | (k0 << 24),
+                             (k0 << 16) | (k1 << 24), k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), k0,
+                             k0 << 24, k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), k1 | (k0 << 8)};
+#endif
     // umax in SGPRs: a lane-indexed a.umax[v] compiles to a vector load from
     // the kernarg segment whose vmcnt wait would also drain the patch prefetch
     int um_s[kHalfPatch + 1];
@@ -2473,9 +2541,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                     hb[(2 * (mlo + m) + 1) * kHbT + rr] = h.y;
                 }
             };
+#if ORB_DESC_HDOT4
+            // output x = 4 j + b takes raw columns x .. x + 6: bytes b.. of
+            // al[j], al[j + 1] and (b >= 2) al[j + 2], one v_dot4_u32_u8 per
+            // word with the 7 weights placed at the matching bytes (every sum
+            // <= 257 * 255 < 2^16, the u16 of ufixedpoint16); no pair
+            // unpacking, 2.5 dot4 per output
+            (void)half;
+#pragma unroll
+            for (int x = 0; x < kBl; ++x) {
+                const int j = x >> 2, b = x & 3;
+                uint32_t h;
+                if (b == 0) h = __builtin_amdgcn_udot4(al[j + 1], hw[1], __builtin_amdgcn_udot4(al[j], hw[0], 0u, false), false);
+                else if (b == 1) h = __builtin_amdgcn_udot4(al[j + 1], hw[3], __builtin_amdgcn_udot4(al[j], hw[2], 0u, false), false);
+                else if (b == 2)
+                    h = __builtin_amdgcn_udot4(al[j + 2], hw[6], __builtin_amdgcn_udot4(al[j + 1], hw[5],
+                                               __builtin_amdgcn_udot4(al[j], hw[4], 0u, false), false), false);
+                else
+                    h = __builtin_amdgcn_udot4(al[j + 2], hw[9], __builtin_amdgcn_udot4(al[j + 1], hw[8],
+                                               __builtin_amdgcn_udot4(al[j], hw[7], 0u, false), false), false);
+                hb[x * kHbT + rr] = (uint16_t)h;
+            }
+#else
             half(std::integral_constant<int, 0>{}, std::integral_constant<int, 10>{});
             __builtin_amdgcn_sched_barrier(0);
             half(std::integral_constant<int, 10>{}, std::integral_constant<int, (kBl + 1) / 2>{});
+#endif
         }
         DESC_T(d2);
         wave_sync();
@@ -2817,7 +2908,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.win_max = (P.win_max + 15) & ~15;
     fa.kmask_bytes = ((P0.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
     fa.cand_bytes = (2 * P0.win_pix_max + 15) & ~15;
-    const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes);
+    fa.ilist_bytes = ORB_FAST_EMIT == 1 ? (4 * P0.item_max + 15) & ~15 : 0;
+    const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes + fa.ilist_bytes);
     fa.nframes = B;
     const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
     hipLaunchKernelGGL(kfast, fgrid, dim3(256), flds, st, fa);

@@ -80,6 +80,7 @@ struct Plan {
     int ncells = 0, slot_total = 0, out_total = 0;
     int roi_max = 0, roi_rows_max = 0, roi_nd_max = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     int win_pix_max = 0;             // largest FAST window (cols-6)*(rows-6): candidate list entries
+    int item_max = 0;                // most FAST pre-test items of a cell (k_fast_cells item list; < 65536)
     std::vector<int> xmax;           // per level
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     std::vector<PyrGroup> pgroups;   // k_pyramid launches
