@@ -2362,12 +2362,19 @@ extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
 #ifndef ORB_DESC_WAVES
 #define ORB_DESC_WAVES 4
 #endif
+#ifndef ORB_DESC_PF2
+#define ORB_DESC_PF2 0   // 1: two patches in flight per wave (measured slower: describe 0.352-0.362 -> 0.369-0.372 ms)
+#endif
+#ifndef ORB_DESC_ICM_REG
+#define ORB_DESC_ICM_REG 1   // IC_Angle disc masks held in 9 VGPRs (0: made per use from umax)
+#endif
 #ifndef ORB_DESC_HDOT4
 #define ORB_DESC_HDOT4 1   // horizontal pass by v_dot4_u32_u8 (0: packed-u16 pairs, round 2)
 #endif
 #ifndef ORB_Q_UNROLL
 #define ORB_Q_UNROLL 1
 #endif
+template <bool FMA>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WAVES))) void k_describe(DescArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
     __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][(kBl + 1) * kHbT];
@@ -2382,10 +2389,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     uint16_t* hb = hb_s[wv];
     // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
     const uint32_t k0 = a.kern[0], k1 = a.kern[1], k2 = a.kern[2], k3 = a.kern[3];
-    // u16 weight pairs of the vertical taps v0..v6 over 4 dwords, for a first
-    // tap at an even index (v0v1 v2v3 v4v5 v6-) or an odd one (-v0 v1v2 v3v4 v5v6)
+    // u16 weight pairs of the vertical taps v0..v6 over 4 dwords whose first
+    // tap is at the low half of the first (v0v1 v2v3 v4v5 v6-)
     const uint32_t W0e = k0 | (k1 << 16), W1e = k2 | (k3 << 16), W2e = k2 | (k1 << 16), W3e = k0;
-    const uint32_t W0o = k0 << 16, W1o = k1 | (k2 << 16), W2o = k3 | (k2 << 16), W3o = k1 | (k0 << 16);
 #if ORB_DESC_HDOT4
     // horizontal taps w = (k0 k1 k2 k3 k2 k1 k0) as bytes for v_dot4 on the
     // words al[j], al[j+1], al[j+2] of an output at byte offset b = 0..3:
@@ -2403,6 +2409,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     for (int v = 0; v <= kHalfPatch; ++v) um_s[v] = __builtin_amdgcn_readfirstlane(a.umax[v]);
     // IC_Angle disc masks for the h-pass lanes: lane r holds patch row r
     // (v = r - 21); byte b of its aligned word j is column 4j + b (u = 4j + b - 21)
+#if ORB_DESC_ICM_REG
     uint32_t icm[9];
     {
         const int av = lane >= 21 ? lane - 21 : 21 - lane;
@@ -2422,6 +2429,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             icm[j - 1] = m;
         }
     }
+#else
+    // the lane's disc half-width (-1: no disc row) for masks made per use
+    int um_l = -1;
+    {
+        const int av = lane >= 21 ? lane - 21 : 21 - lane;
+#pragma unroll
+        for (int k = 0; k <= kHalfPatch; ++k)
+            if (av == k) um_l = um_s[k];
+        if (lane >= kRaw) um_l = -1;
+    }
+    // bytes of 128 + umax (0x7f: no disc row), so (um_rep - |u|) has bit 7
+    // set per byte exactly where |u| <= umax, with no borrow across bytes
+    const uint32_t um_rep = (uint32_t)((um_l + 128) & 0xff) * 0x01010101u;
+#endif
     // this wave's run of kDescSlots slots; the next valid slot's patch is
     // always in flight while the current one is described
     const long long s_begin = ((long long)blockIdx.x * 4 + wv) * kDescSlots;
@@ -2429,42 +2450,54 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     DescLane mine{};
     const bool valid = lane < nrun && desc_lane(a, s_begin + lane, mine);
     uint64_t todo = __ballot(valid);
+    // two patches in flight (ORB_DESC_PF2): the current keypoint's, landed at
+    // the top of its iteration, and the next one's; the register set freed by
+    // the landing takes the keypoint after that, so the sets alternate and the
+    // loop body is instantiated once per set
     uint32_t pv[kPV];
-    DescKp cur{};
-    int jc = -1;
+#if ORB_DESC_PF2
+    uint32_t pv2[kPV];
+#endif
+    DescKp cur{}, nxt{};
+    int jc = -1, jn = -1;
 #ifdef ORB_DESC_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long tlast = t_start, d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0, dk = 0;
 #endif
-    if (todo) {
-        jc = __builtin_ctzll(todo);
+    auto take = [&](int& j, DescKp& k, uint32_t (&v)[kPV]) {       // the next valid slot, its patch issued
+        j = -1;
+        if (!todo) return;
+        j = __builtin_ctzll(todo);
         todo &= todo - 1;
-        cur = desc_pick(mine, jc);
-        const int x0 = (int)(cur.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((cur.key >> 12) & 0xfff) + (kEdge - 3) - 21;
-        if (patch_interior(cur.w, cur.h, x0, y0)) patch_issue(cur.img, cur.pitch, x0, y0, pv);
-    }
-    while (jc >= 0) {
+        k = desc_pick(mine, j);
+        const int x0 = (int)(k.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((k.key >> 12) & 0xfff) + (kEdge - 3) - 21;
+        if (patch_interior(k.w, k.h, x0, y0)) patch_issue(k.img, k.pitch, x0, y0, v);
+    };
+    take(jc, cur, pv);
+#if ORB_DESC_PF2
+    take(jn, nxt, pv2);
+#endif
+    auto body = [&](uint32_t (&pvl)[kPV]) {
         const long long s = s_begin + jc;
         const uint32_t key = cur.key;
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
         // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
         int sh = 0;
         if (patch_interior(cur.w, cur.h, cx - 21, cy - 21)) {
-            patch_land(pv, raw);
+            patch_land(pvl, raw);
             sh = (cx - 21) & 3;
         } else {
             patch_border(cur.img, cur.pitch, cur.w, cur.h, cx - 21, cy - 21, raw);
         }
-        // prefetch the next keypoint's patch (in flight during this keypoint)
-        int jn = -1;
-        DescKp nxt{};
-        if (todo) {
-            jn = __builtin_ctzll(todo);
-            todo &= todo - 1;
-            nxt = desc_pick(mine, jn);
-            const int x0 = (int)(nxt.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((nxt.key >> 12) & 0xfff) + (kEdge - 3) - 21;
-            if (patch_interior(nxt.w, nxt.h, x0, y0)) patch_issue(nxt.img, nxt.pitch, x0, y0, pv);
-        }
+        // refill the landed set: the keypoint after the next one (PF2), or
+        // the next one (one patch in flight during this keypoint)
+        int jnn = -1;
+        DescKp nn{};
+#if ORB_DESC_PF2
+        take(jnn, nn, pvl);
+#else
+        take(jn, nxt, pvl);
+#endif
         wave_sync();
         DESC_T(d0);
 #ifdef ORB_DESC_TIMING
@@ -2502,7 +2535,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                         const int u = 4 * j + b - 21;
                         if (u >= -kHalfPatch && u <= kHalfPatch) wgt |= (uint32_t)(u + kHalfPatch) << (8 * b);
                     }
+#if ORB_DESC_ICM_REG
                     const uint32_t px = al[j] & icm[j - 1];
+#else
+                    // bytes with |u| <= umax(v): SWAR (um | 0x80) - |u| keeps bit 7 exactly there
+                    uint32_t au = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) {
+                        const int u = 4 * j + b - 21;
+                        au |= (uint32_t)(u < 0 ? -u : u) << (8 * b);
+                    }
+                    const uint32_t ge = ((um_rep - au) & 0x80808080u) >> 7;
+                    const uint32_t px = al[j] & ((ge << 8) - ge);
+#endif
                     s1 = __builtin_amdgcn_udot4(px, 0x01010101u, s1, false);
                     sw = __builtin_amdgcn_udot4(px, wgt, sw, false);
                 }
@@ -2583,21 +2628,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                 const float x = (float)(int)(int8_t)(patw[q] >> (16 * e));
                 const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
                 int r, c;
-                brief_offset(x, y, sb, ca, a.fma, r, c);
+                brief_offset(x, y, sb, ca, FMA, r, c);
                 // the 7 vertical taps are rows 18+r .. 24+r of column 18+c:
-                // contiguous u16, inside the 4 dwords from the even index at or
-                // below the first; the dot2 weight pairs follow its parity
-                const int s0 = (18 + c) * kHbT + 18 + r;
+                // contiguous u16 from index s0, inside the 4 dwords from the
+                // even index at or below s0; for an odd s0 the dwords are
+                // realigned by 16 bits (v_alignbit), so one set of dot2 weights
+                // serves both parities
+                const int s0 = (int)__umul24(18 + c, kHbT) + 18 + r;
                 const uint32_t* dw = (const uint32_t*)hb + (s0 >> 1);
                 const uint32_t D0 = dw[0], D1 = dw[1], D2 = dw[2], D3 = dw[3];
-                const bool odd = s0 & 1;
+                const uint32_t sh = (uint32_t)(s0 & 1) << 4;
+                const uint32_t E0 = __builtin_amdgcn_alignbit(D1, D0, sh), E1 = __builtin_amdgcn_alignbit(D2, D1, sh);
+                const uint32_t E2 = __builtin_amdgcn_alignbit(D3, D2, sh), E3 = __builtin_amdgcn_alignbit(0u, D3, sh);
                 const uint32_t acc = __builtin_amdgcn_udot2(
-                    as_u16x2(D3), as_u16x2(odd ? W3o : W3e),
+                    as_u16x2(E3), as_u16x2(W3e),
                     __builtin_amdgcn_udot2(
-                        as_u16x2(D2), as_u16x2(odd ? W2o : W2e),
-                        __builtin_amdgcn_udot2(as_u16x2(D1), as_u16x2(odd ? W1o : W1e),
-                                               __builtin_amdgcn_udot2(as_u16x2(D0), as_u16x2(odd ? W0o : W0e), 0u,
-                                                                      false),
+                        as_u16x2(E2), as_u16x2(W2e),
+                        __builtin_amdgcn_udot2(as_u16x2(E1), as_u16x2(W1e),
+                                               __builtin_amdgcn_udot2(as_u16x2(E0), as_u16x2(W0e), 0u, false),
                                                false),
                         false),
                     false);
@@ -2612,8 +2660,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         if (lane == 0) a.angle[s] = ang_deg;
         jc = jn;
         cur = nxt;
+#if ORB_DESC_PF2
+        jn = jnn;
+        nxt = nn;
+#else
+        (void)jnn; (void)nn;
+#endif
         wave_sync();
         DESC_T(d5);
+    };
+    while (jc >= 0) {
+        body(pv);
+#if ORB_DESC_PF2
+        if (jc < 0) break;
+        body(pv2);
+#endif
     }
 #ifdef ORB_DESC_TIMING
     if (lane == 0) {
@@ -2941,7 +3002,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
     da.slot_level = P.d_slot_level;
     da.nslots = (long long)B * P.out_total;
-    hipLaunchKernelGGL(k_describe, dim3((unsigned)((da.nslots + 4 * kDescSlots - 1) / (4 * kDescSlots))), dim3(256), 0,
+    hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>,
+                       dim3((unsigned)((da.nslots + 4 * kDescSlots - 1) / (4 * kDescSlots))), dim3(256), 0,
                        st, da);
     mark();
     // assemble
