@@ -1350,6 +1350,25 @@ __device__ __forceinline__ void fast_wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// XCD-aware block order (ORB_XCD_REMAP): the hardware deals the blocks of a
+// launch round-robin over the 8 XCDs (linear id L to XCD L % 8).  Over a grid
+// of `per` units x B frames, XCD x is given frames x, x + 8, x + 16, ...
+// (the XCD whose L2 k_pyr_stream wrote them through: one block per frame),
+// each frame's units in order, so a frame's neighbouring cells or patches --
+// which share ROI rows and cache lines -- meet in one L2.  Identity when B is
+// not a multiple of 8.
+#ifndef ORB_XCD_REMAP
+#define ORB_XCD_REMAP 1
+#endif
+__device__ __forceinline__ void xcd_remap(int per, int B, int& unit, int& frame) {
+    const int L = (int)blockIdx.x + per * (int)blockIdx.y;
+    if (!ORB_XCD_REMAP || (B & 7)) { unit = blockIdx.x; frame = blockIdx.y; return; }
+    const int x = L & 7, k = L >> 3;
+    const int fl = k / per;
+    unit = k - fl * per;
+    frame = 8 * fl + x;
+}
+
 // row/column of linear window index i (ww <= 4096): exact via a float reciprocal
 __device__ __forceinline__ int div_row(int i, float inv_ww) { return (int)(((float)i + 0.5f) * inv_ww); }
 
@@ -1424,23 +1443,27 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
     // work items it = frame * ncells + cell
-    const int c_begin = (blockIdx.x * 4 + wv) * kCellsPerWave;
-    const int it0 = blockIdx.y * a.ncells + c_begin, step = 1;
-    const int it_end = blockIdx.y * a.ncells + min(c_begin + kCellsPerWave, a.ncells);
+    int bunit, bframe;
+    xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
+    bunit = __builtin_amdgcn_readfirstlane(bunit);
+    bframe = __builtin_amdgcn_readfirstlane(bframe);
+    const int c_begin = (bunit * 4 + wv) * kCellsPerWave;
+    const int it0 = bframe * a.ncells + c_begin, step = 1;
+    const int it_end = bframe * a.ncells + min(c_begin + kCellsPerWave, a.ncells);
     // the plan tables are read-only here: constant address space -> scalar loads
     typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
     typedef __attribute__((address_space(4))) const CellDev* ConstCells;
     const ConstLevels lvc = (ConstLevels)a.lv;
     const ConstCells cells = (ConstCells)a.cells;
     auto cell_at = [&](int it) {
-        const int i = it - (int)blockIdx.y * a.ncells;   // frame = blockIdx.y: no division
+        const int i = it - bframe * a.ncells;   // frame = bframe: no division
         CellDev r;
         r.level = cells[i].level; r.x0 = cells[i].x0; r.y0 = cells[i].y0; r.cols = cells[i].cols;
         r.rows = cells[i].rows; r.slot_off = cells[i].slot_off; r.cap = cells[i].cap;
         return r;
     };
     auto fetch_of = [&](const CellDev& c, int it) {
-        const int f = blockIdx.y;
+        const int f = bframe;
         RoiFetch rf;
         if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
         else { rf.src = a.pyr + f * a.pyr_fstride + lvc[c.level].off; rf.pitch = lvc[c.level].pitch; }
@@ -1466,7 +1489,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) { roi_land<PDW, NV>(r, vv, (uint32_t*)roi); };
     // one cell from its landed ROI
     auto process = [&](const CellDev& cur, const RoiFetch& rfc, int it) {
-        const int f = blockIdx.y;
+        const int f = bframe;
         const int rstride = rfc.nd * 4;
         const int shift = cur.x0 & 3;
         const uint8_t* R = roi + shift;
@@ -1715,7 +1738,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                                            1ull, t9, t10};
 #pragma unroll
         for (int k = 0; k < 11; ++k)
-            atomicAdd(&g_fast_t[(blockIdx.x * 4 + wv + blockIdx.y * 61) & 1023][k], tv[k]);
+            atomicAdd(&g_fast_t[(bunit * 4 + wv + bframe * 61) & 1023][k], tv[k]);
     }
 #endif
 }
@@ -2445,8 +2468,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
 #endif
     // this wave's run of kDescSlots slots; the next valid slot's patch is
     // always in flight while the current one is described
-    const long long s_begin = ((long long)blockIdx.x * 4 + wv) * kDescSlots;
-    const int nrun = (int)min((long long)kDescSlots, a.nslots - s_begin);
+    // grid (runs of 4 * kDescSlots slots of a frame, frames), XCD-aware order
+    int bunit, bframe;
+    xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
+    const int lb = (bunit * 4 + wv) * kDescSlots;                  // frame-local slot
+    const long long s_begin = (long long)bframe * a.out_total + lb;
+    const int nrun = max(0, min(kDescSlots, a.out_total - lb));
     DescLane mine{};
     const bool valid = lane < nrun && desc_lane(a, s_begin + lane, mine);
     uint64_t todo = __ballot(valid);
@@ -2680,7 +2707,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     if (lane == 0) {
         const unsigned long long tv[8] = {d0, d1, d2, d3, d4, d5, dk, __builtin_amdgcn_s_memtime() - t_start};
 #pragma unroll
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_desc_t[(blockIdx.x * 4 + wv) & 1023][k], tv[k]);
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_desc_t[(bunit * 4 + wv + bframe * 61) & 1023][k], tv[k]);
     }
 #endif
 }
@@ -3003,7 +3030,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     da.slot_level = P.d_slot_level;
     da.nslots = (long long)B * P.out_total;
     hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>,
-                       dim3((unsigned)((da.nslots + 4 * kDescSlots - 1) / (4 * kDescSlots))), dim3(256), 0,
+                       dim3((unsigned)((P.out_total + 4 * kDescSlots - 1) / (4 * kDescSlots)), (unsigned)B), dim3(256), 0,
                        st, da);
     mark();
     // assemble
