@@ -52,7 +52,7 @@ W, H, NFEAT, LAP = 752, 480, 1000, (0, 1000)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_SUMMARY = ROOT / "profiles" / "pmc_summary_latest.csv"
 METRIC = "frames/s ORB extract+match (752×480, 1000 feat) @1/2/4/8 GPU; bit-exact kp/desc"
-STAGES = ["pyramid", "fast_cells", "quadtree", "describe", "assemble"]
+STAGES = ["pyramid", "fast_cells", "quadtree", "blur", "describe", "assemble"]
 
 
 def parse():
@@ -129,10 +129,12 @@ def stage_roofline(ex, stage_ms, frames_per_launch, kps_per_frame):
     """Achieved GB/s of each stage on its algorithmic bytes:
     pyramid reads levels 0..L-2 and writes 1..L-1; FAST reads every level once;
     the north-star pass (pyramid + FAST) reads R = 2*sum(P) - P_{L-1} per frame;
-    describe reads the 43x43 raw patch (1,849 B) and writes 36 B per keypoint."""
+    blur reads and writes every level once (2 sum(P)); describe reads the raw
+    IC_Angle disc rows (31 x 36 B) and the blurred 37 x 37 square (37 x 40 B)
+    and writes 36 B per keypoint."""
     P = level_sizes(ex)
-    per_frame = {"pyramid": sum(P[:-1]) + sum(P[1:]), "fast_cells": sum(P),
-                 "describe": (1849 + 36) * kps_per_frame}
+    per_frame = {"pyramid": sum(P[:-1]) + sum(P[1:]), "fast_cells": sum(P), "blur": 2 * sum(P),
+                 "describe": (31 * 36 + 37 * 40 + 36) * kps_per_frame}
     out = {}
     for k, b in per_frame.items():
         ms = float(stage_ms.get(k) or 0)

@@ -169,14 +169,25 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
  * the original index (within array i) of the element the sort puts at j;
  * fallback[i] = 1 where the depth limit sent the array to the sequential port
  * (the heap-sort case).  Returns ORB_OK, ORB_ERR_PARAM or ORB_ERR_DEVICE. */
+/* The blurred level (GaussianBlur 7x7, sigma 2, REFLECT_101 of the level,
+ * ORBextractor.cc:1132-1133, as k_blur_levels wrote it for k_describe_pb) of
+ * frame `frame` of the last extraction on the handle (orbx_extract: frame 0),
+ * w x h bytes at dst with row step dst_step (dst may be NULL to query w/h).
+ * ORB_ERR_UNSUPPORTED unless the
+ * handle was created with ORB_DESC_PREBLUR=1 in the environment (the
+ * alternative describe path: the level blurred once, then sampled; off by
+ * default).  Test hook, not part of the reference interface. */
+int orbx_debug_blur_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int* w,
+                          int* h_);
+
 int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* cnt, const int32_t* x0,
                     int32_t* perm, int32_t* fallback);
 
 /* Per-stage HIP-event timing of subsequent orbx_extract* calls (on the stream
  * they run on).  orbx_get_profile sums, over the recorded calls, the stage
- * times in ms: [0] pyramid (k_resize x L-1), [1] FAST cells, [2] quadtree,
- * [3] describe (orientation + blur + rBRIEF), [4] assemble; returns the number of calls and
- * clears the record.  Not part of the reference interface. */
+ * times in ms: [0] pyramid, [1] FAST cells, [2] quadtree, [3] level blur
+ * (k_blur_levels), [4] describe (orientation + rBRIEF), [5] assemble; returns
+ * the number of calls and clears the record.  Not part of the reference interface. */
 int orbx_set_profiling(orbx_handle* h, int enable);
 int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);
 

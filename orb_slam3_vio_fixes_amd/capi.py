@@ -14,7 +14,7 @@ LIB_PATH = Path(__file__).resolve().parent / "liborb_mi355x.so"
 
 EXPORTS = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_max_keypoints", "orbx_extract", "orbx_extract_batch",
-    "orbx_get_level", "orbx_get_batch_level", "orbx_debug_math", "orbx_debug_sort", "orbx_set_host_pyramid",
+    "orbx_get_level", "orbx_get_batch_level", "orbx_debug_math", "orbx_debug_sort", "orbx_set_host_pyramid", "orbx_debug_blur_level",
     "orbx_extract_batch_device", "orbx_debug_stage", "orbm_descriptor_distance", "orbm_search_for_initialization",
     "orbm_search_for_initialization_batch_device", "orbm_search_by_bow", "orbm_search_by_projection_mps",
     "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device", "orbm_search_by_bow_many", "orbm_kf_map_fv_desc",
@@ -48,6 +48,7 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_debug_math.argtypes = [i32, i32, C.c_longlong, C.c_longlong, i32, i32, vp]
     L.orbx_debug_sort.argtypes = [i32, i32, vp, vp, vp, vp, vp]
     L.orbx_set_host_pyramid.argtypes = [vp, i32]
+    L.orbx_debug_blur_level.argtypes = [vp, i32, i32, vp, C.c_size_t, vp, vp]
     L.orbx_extract_batch_device.argtypes = [vp, i32, vp, sz, sz, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp]
     L.orbx_debug_stage.argtypes = [vp, i32, vp, i32, vp]
     L.orbm_descriptor_distance.argtypes = [vp, vp]

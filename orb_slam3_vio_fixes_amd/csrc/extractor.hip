@@ -590,6 +590,25 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     for (const PyrGroup& g : P.pgroups)
         if (pyr_group_lds(g) > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
     P.pyr_bytes = poff;
+    // blurred levels 0..L-1 of a frame (k_blur_levels), 64-byte rows with >= 12
+    // bytes of slack past the level (k_describe's 10-dword patch rows)
+    std::vector<int4> bitems;
+    {
+        long long boff = 0;
+        for (int l = 0; l < L; ++l) {
+            LevelDev& d = P.lv[l];
+            d.bpitch = round_up(d.w + 12, 64);
+            d.boff = boff;
+            boff += (long long)d.bpitch * d.h;
+            const int nd = (d.w + 3) / 4;
+            for (int g0 = 0; g0 < nd; g0 += kBlurDw)
+                for (int y0 = 0; y0 < d.h; y0 += kBlurRows)
+                    bitems.push_back(make_int4(l, g0, y0, std::min(kBlurRows, d.h - y0)));
+        }
+        P.blur_bytes = round_up((int)std::min<long long>(boff, 1ll << 30), 256);
+        if (boff >= (1ll << 30)) return ORB_ERR_UNSUPPORTED;
+        P.nblur_items = (int)bitems.size();
+    }
     P.ncells = cellsum;
     P.slot_total = slotsum;
     P.out_total = outsum;
@@ -597,6 +616,9 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
 
     const size_t B = (size_t)maxB;
     ORB_CHECK(hipMalloc(&P.d_pyr, std::max<size_t>(1, B * P.pyr_bytes)));
+    if (hd->preblur) ORB_CHECK(hipMalloc(&P.d_blur, B * P.blur_bytes + 256));
+    ORB_CHECK(hipMalloc(&P.d_blur_items, bitems.size() * sizeof(int4)));
+    ORB_CHECK(hipMemcpy(P.d_blur_items, bitems.data(), bitems.size() * sizeof(int4), hipMemcpyHostToDevice));
     ORB_CHECK(hipMalloc(&P.d_in, P.in_pitch * h));
     ORB_CHECK(hipMalloc(&P.d_tab, std::max<size_t>(1, tab.size()) * sizeof(int2)));
     ORB_CHECK(hipMalloc(&P.d_lv, L * sizeof(LevelDev)));
@@ -1230,8 +1252,17 @@ __device__ __forceinline__ int arc_strength(const int (&x)[16], int m) {
     return max(a, a9[15]);
 }
 
+// a * b + c for a, b < 2^24 in one full-rate v_mad_u32_u24: with __umul24
+// the compiler, unable to bound a min() result, fuses the product and the add
+// into a quarter-rate v_mad_u64_u32
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+
 __device__ __forceinline__ void fast_ring(const uint8_t* roi, int stride, int r, int c, int& v, int (&x)[16]) {
-    const uint8_t* p = roi + r * stride + c;
+    const uint8_t* p = roi + mad24((uint32_t)r, (uint32_t)stride, (uint32_t)c);
     v = p[0];
     x[0] = p[3 * stride];
     x[1] = p[3 * stride + 1];
@@ -1265,7 +1296,7 @@ __device__ __forceinline__ int fast_dir_score(const int (&x)[16], int v, int dar
 // s(p) >= max(t, 1) and s(p) > s_t(q) for its 8 neighbours, s_t(q) = s(q) if
 // s(q) >= t else 0; the zero border stands for pixels outside the window.
 __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c, int t) {
-    const uint8_t* p = sc + (r + 1) * sp + (c + 1);
+    const uint8_t* p = sc + mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(c + 1));
     const int s = p[0];
     if (s < max(t, 1)) return false;
     const int q[8] = {p[-sp - 1], p[-sp], p[-sp + 1], p[-1], p[1], p[sp - 1], p[sp], p[sp + 1]};
@@ -1397,31 +1428,42 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 // lane issue back to back, branch-free, with a clamp and a multiply-add of
 // address math each (the float-reciprocal split of a linear index cost ~14
 // VALU per load).
+// Global-address-space views: image pointers that reach a loop through
+// readlanes lose their address space, and flat loads also count in lgkmcnt
+// (the next LDS wait would drain a prefetch); a uniform base plus a 32-bit
+// offset also gives the saddr form of global_load.
+typedef __attribute__((address_space(1))) const uint8_t* GlobalBytes;
+typedef __attribute__((address_space(1))) const uint32_t* GlobalWords;
+
 struct RoiFetch {
     const uint8_t* src;     // ROI row 0, dword 0 (level row y0, column x0 & ~3)
     int pitch, nd, rows;
 };
 
+// Addresses as 32-bit offsets from the cell's uniform row-0 pointer (one
+// v_mad_u32_u24 per load: a 64-bit product per load was two quarter-rate
+// v_mad_u64_u32, and the landing's r * nd a quarter-rate v_mul_lo_u32).
 template <int PDW, int NV>
 __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV]) {
     static_assert(kWave % PDW == 0, "rows of a load round are whole");
     const int lane = lane_id();
-    const uint8_t* col = rf.src + 4 * min(lane % PDW, rf.nd - 1);
+    const uint32_t col = 4u * (uint32_t)min(lane % PDW, rf.nd - 1);
+    const GlobalBytes base = (GlobalBytes)rf.src;
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const int r = min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
-        v[j] = *(const uint32_t*)(col + (long long)r * rf.pitch);
+        const uint32_t r = (uint32_t)min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
+        v[j] = *(GlobalWords)(base + mad24(r, (uint32_t)rf.pitch, col));
     }
 }
 
 template <int PDW, int NV>
 __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)[NV], uint32_t* roi) {
     const int lane = lane_id();
-    const int d = min(lane % PDW, rf.nd - 1);
+    const uint32_t d = (uint32_t)min(lane % PDW, rf.nd - 1);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
-        const int r = min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
-        roi[r * rf.nd + d] = v[j];
+        const uint32_t r = (uint32_t)min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
+        roi[mad24(r, (uint32_t)rf.nd, d)] = v[j];
     }
 }
 
@@ -1627,8 +1669,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 if (m) {
                     const int itm = (int)(e & 0xffffu);
                     const int r = div_row(itm, inv_ndp);
-                    const int k = itm - (int)__umul24(r, ndp);
-                    const int idx0 = (int)__umul24(r, ww) + 4 * (j0 + 2 * k) - X0;
+                    const int k = itm - (int)mad24((uint32_t)r, (uint32_t)ndp, 0u);
+                    const int idx0 = (int)mad24((uint32_t)r, (uint32_t)ww, (uint32_t)(4 * (j0 + 2 * k) - X0));
                     while (m) {
                         const int bb = __builtin_ctz(m);
                         m &= m - 1;
@@ -1671,7 +1713,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
                 if ((e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
 #endif
-                sc[(r + 1) * sp + cc + 1] = (uint8_t)max(sv, 0);
+                sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(cc + 1))] = (uint8_t)max(sv, 0);
             }
             fast_wave_sync();
             if (pass == 0) FAST_T(2); else FAST_T(6);
@@ -2042,6 +2084,28 @@ __device__ void qt_count(QtLds& s, int cur, int size, const int K, const uint32_
     __syncthreads();
 }
 
+#ifdef ORB_QT_TIMING
+// phase profile of k_quadtree (tools/fast_phases.py --quadtree): per level,
+// shader cycles per phase summed over blocks, the longest block, pass counts
+__device__ unsigned long long g_qt_t[16][12];
+#define QT_T(k)                                                              \
+    do {                                                                     \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
+        if (tid == 0) atomicAdd(&g_qt_t[l][k], t_ - qt_last);                \
+        qt_last = t_;                                                        \
+    } while (0)
+extern "C" int orbx_debug_qt_timing(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_t), sizeof(g_qt_t)) != hipSuccess) return -4;
+    if (reset) {
+        static unsigned long long z[16][12];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_qt_t), z, sizeof(z)) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#else
+#define QT_T(k) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #if ORB_QT_LEVEL_MAJOR
@@ -2052,6 +2116,11 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 #endif
     const LevelDev lv = a.lv[l];
     const int NC = a.ncap;
+#ifdef ORB_QT_TIMING
+    const unsigned long long qt_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long qt_last = qt_t0;
+    int qt_outer = 0, qt_lastr = 0;
+#endif
     QtLds s;
     {
         uint8_t* p = smem;
@@ -2096,6 +2165,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         for (int j = lane_id(); j < n; j += kWave) keys[base + j] = cslots[c * cap + j];
     }
     __syncthreads();
+    QT_T(0);
     if (K == 0) {
         if (tid == 0) a.qt_n[f * a.L + l] = 0;
         return;
@@ -2132,6 +2202,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     int cur = 0;
     const int N = lv.N;
     __syncthreads();
+    QT_T(1);
 
     // 3. outer passes (:610-689)
     int nexp = 0;
@@ -2146,11 +2217,18 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         for (int i = tid; i < size; i += T)
             if (s.div[i]) s.ord[s.nd[i]] = i;
         __syncthreads();
+#ifdef ORB_QT_TIMING
+        ++qt_outer;
+        QT_T(5);
+#endif
         qt_count(s, cur, size, K, keys, knode, kq);
+        QT_T(6);
         size = qt_divide(s, cur, size, m, K, knode, kq, &nexp);
+        QT_T(7);
         if (size >= N || size == prev) break;
         if (size + nexp * 3 > N) { last = true; break; }
     }
+    QT_T(2);
     // 4. last rounds (:692-753)
     while (last) {
         const int prev = size;
@@ -2192,8 +2270,12 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         }
         __syncthreads();
         size = qt_divide(s, cur, size, mp, K, knode, kq, &nexp);
+#ifdef ORB_QT_TIMING
+        ++qt_lastr;
+#endif
         if (size >= N || size == prev) break;
     }
+    QT_T(3);
     // 5. retain the best key per node (:757-776)
     int* best = s.ccnt;
     for (int i = tid; i < size; i += T) best[i] = 0;
@@ -2204,6 +2286,15 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     const int nout = min(size, lv.out_cap);
     for (int i = tid; i < nout; i += T) out[i] = keys[0x7FFFFF - (best[i] & 0x7FFFFF)];
     if (tid == 0) a.qt_n[f * a.L + l] = nout;
+#ifdef ORB_QT_TIMING
+    QT_T(4);
+    if (tid == 0) {
+        atomicMax(&g_qt_t[l][8], __builtin_amdgcn_s_memtime() - qt_t0);
+        atomicAdd(&g_qt_t[l][9], (unsigned long long)qt_outer);
+        atomicAdd(&g_qt_t[l][10], (unsigned long long)qt_lastr);
+        atomicAdd(&g_qt_t[l][11], 1ull);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -2251,6 +2342,8 @@ struct DescArgs {
     int fma;
     int kern[7];
     int umax[16];
+    const uint8_t* blur;            // blurred levels (k_describe_pb)
+    long long blur_fstride;
 };
 
 // One keypoint slot of the flat (frame, quadtree output) space: qt_key, angle
@@ -2315,12 +2408,6 @@ constexpr int kPDw = kRawP / 4, kPN = kRaw * kPDw, kPV = (kPN + kWave - 1) / kWa
 __device__ __forceinline__ bool patch_interior(int w, int h, int x0, int y0) {
     return y0 >= 0 && y0 + kRaw <= h && x0 >= 0 && (x0 & ~3) + kRawP <= w;
 }
-
-// the image pointers reach the describe loop through readlanes, which loses
-// their address space: without the global cast these become flat loads, which
-// also count in lgkmcnt, so the next LDS wait would drain the prefetch
-typedef __attribute__((address_space(1))) const uint8_t* GlobalBytes;
-typedef __attribute__((address_space(1))) const uint32_t* GlobalWords;
 
 __device__ __forceinline__ void patch_issue(const uint8_t* img, int pitch, int x0, int y0, uint32_t (&v)[kPV]) {
     const int lane = lane_id(), base = x0 & ~3;
@@ -2713,6 +2800,339 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
 }
 
 // ---------------------------------------------------------------------------
+// k_blur_levels: the level blur of ORBextractor::operator() --
+// GaussianBlur(workingMat, workingMat, Size(7,7), 2, 2, BORDER_REFLECT_101)
+// on a clone() of every level (ORBextractor.cc:1132-1133) -- for every frame,
+// into the blurred slab d_blur, with the fixed-point separable kernel of
+// SURVEY.md A.5 (k_describe's arithmetic: ufixedpoint16 horizontal sums,
+// ufixedpoint32 vertical sums, +2^15 >> 16, saturate).
+//
+// One wave per item = kBlurDw dword columns x kBlurRows rows of a level.
+// Lane i holds dword column g = g0 - 1 + i: per source row it loads 8 bytes
+// with one dwordx2 and picks its 4 columns -- REFLECT_101 applied -- by one
+// v_perm whose selector was made once (the identity inside the level; at the
+// borders the reflected columns, which always lie in two adjacent dwords);
+// its neighbours' dwords arrive by DPP wave_shr:1 / wave_shl:1, so lanes
+// 1..62 output 4 columns each and no lane branches on the border.  The
+// kBlurRows + 6 source rows (REFLECT_101 row index) are all requested before
+// any is used; each gives 4 horizontal sums by 10 v_dot4_u32_u8 with
+// byte-placed taps, a row is paired with the next as u16 pairs, and each
+// output is three v_dot2_u32_u16 and one v_mad_u32_u24.
+// HBM: every level pixel read once (the 6-row halo between items and the
+// 2-dword overlap between column strips hit L2), every blurred pixel written
+// once: 2 ΣP per frame.
+// ---------------------------------------------------------------------------
+struct BlurArgs {
+    const uint8_t* in;
+    long long in_fstride;
+    int in_pitch;
+    const uint8_t* pyr;
+    long long pyr_fstride;
+    uint8_t* blur;
+    long long blur_fstride;
+    const LevelDev* lv;
+    const int4* items;
+    int nitems;
+    uint32_t hw[10];    // horizontal taps as bytes (k_describe's hw layout)
+    uint32_t vw[3];     // vertical taps as u16 pairs (k0 k1) (k2 k3) (k2 k1); k0 alone for the 7th
+    uint32_t k0;
+};
+
+typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u32x2v* GlobalPairs;
+
+__global__ __launch_bounds__(256) void k_blur_levels(BlurArgs a) {
+    int bunit, bframe;
+    xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
+    const int item = __builtin_amdgcn_readfirstlane(bunit * 4 + wave_id());
+    bframe = __builtin_amdgcn_readfirstlane(bframe);
+    if (item >= a.nitems) return;
+    typedef __attribute__((address_space(4))) const int* ConstInts;
+    typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
+    const ConstInts itp = (ConstInts)a.items + 4 * item;
+    const int l = itp[0], g0 = itp[1], y0 = itp[2], nr = itp[3];
+    const ConstLevels lvc = (ConstLevels)a.lv;
+    const int w = lvc[l].w, h = lvc[l].h;
+    const GlobalBytes src = (GlobalBytes)(l == 0 ? a.in + bframe * a.in_fstride
+                                                 : a.pyr + bframe * a.pyr_fstride + lvc[l].off);
+    const int pitch = l == 0 ? a.in_pitch : lvc[l].pitch;
+    uint8_t* dst = a.blur + bframe * a.blur_fstride + lvc[l].boff;
+    const int bp = lvc[l].bpitch;
+    const int lane = lane_id(), nd = (w + 3) >> 2;
+    const int g = g0 - 1 + lane;
+    // this lane's columns 4g .. 4g+3 (g clamped to [-1, nd]: lanes past it are
+    // never read), REFLECT_101, as bytes of the dword pair at dword column ca
+    int ca;
+    uint32_t sel;
+    {
+        const int gc = min(max(g, -1), nd);
+        int sk[4], smin = 1 << 30;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            int c = 4 * gc + k;
+            c = c < 0 ? -c : (c >= w ? 2 * w - 2 - c : c);
+            c = min(max(c, 0), w - 1);
+            sk[k] = c;
+            smin = min(smin, c);
+        }
+        ca = min(smin >> 2, nd - 2);
+        sel = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) sel |= (uint32_t)(sk[k] - 4 * ca) << (8 * k);
+    }
+    const bool out_lane = lane >= 1 && lane <= kBlurDw && g < nd;
+    // every source row first
+    u32x2v raw[kBlurRows + 6];
+#pragma unroll
+    for (int i = 0; i < kBlurRows + 6; ++i) {
+        int y = y0 - 3 + i;
+        y = y < 0 ? -y : (y >= h ? 2 * h - 2 - y : y);
+        y = min(max(y, 0), h - 1);
+        raw[i] = *(GlobalPairs)(src + (long long)y * pitch + 4 * ca);
+    }
+    uint32_t hv[kBlurRows + 6][4];
+#pragma unroll
+    for (int i = 0; i < kBlurRows + 6; ++i) {
+        const uint32_t e = __builtin_amdgcn_perm(raw[i].y, raw[i].x, sel);
+        const uint32_t em = __builtin_amdgcn_update_dpp(0u, e, 0x138, 0xf, 0xf, false);   // wave_shr:1
+        const uint32_t ep = __builtin_amdgcn_update_dpp(0u, e, 0x130, 0xf, 0xf, false);   // wave_shl:1
+        // columns 4g-3 .. 4g+6 as three words
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(e, em, 1u), w1 = __builtin_amdgcn_alignbyte(ep, e, 1u);
+        const uint32_t w2 = ep >> 8;
+        hv[i][0] = __builtin_amdgcn_udot4(w1, a.hw[1], __builtin_amdgcn_udot4(w0, a.hw[0], 0u, false), false);
+        hv[i][1] = __builtin_amdgcn_udot4(w1, a.hw[3], __builtin_amdgcn_udot4(w0, a.hw[2], 0u, false), false);
+        hv[i][2] = __builtin_amdgcn_udot4(
+            w2, a.hw[6], __builtin_amdgcn_udot4(w1, a.hw[5], __builtin_amdgcn_udot4(w0, a.hw[4], 0u, false), false),
+            false);
+        hv[i][3] = __builtin_amdgcn_udot4(
+            w2, a.hw[9], __builtin_amdgcn_udot4(w1, a.hw[8], __builtin_amdgcn_udot4(w0, a.hw[7], 0u, false), false),
+            false);
+    }
+    if (!out_lane) return;
+    // rows i, i+1 as u16 pairs (every horizontal sum < 2^16)
+    uint32_t pr[kBlurRows + 5][4];
+#pragma unroll
+    for (int i = 0; i < kBlurRows + 5; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) pr[i][b] = hv[i][b] | (hv[i + 1][b] << 16);
+#pragma unroll
+    for (int o = 0; o < kBlurRows; ++o) {
+        uint32_t out = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            uint32_t acc = __builtin_amdgcn_udot2(as_u16x2(pr[o][b]), as_u16x2(a.vw[0]), 32768u, false);
+            acc = __builtin_amdgcn_udot2(as_u16x2(pr[o + 2][b]), as_u16x2(a.vw[1]), acc, false);
+            acc = __builtin_amdgcn_udot2(as_u16x2(pr[o + 4][b]), as_u16x2(a.vw[2]), acc, false);
+            acc += __umul24(hv[o + 6][b], a.k0);
+            out |= min(acc >> 16, 255u) << (8 * b);
+        }
+        if (o < nr) *(uint32_t*)(dst + (long long)(y0 + o) * bp + 4 * g) = out;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_describe_pb: computeOrientation/IC_Angle (ORBextractor.cc:76-103,471-478)
+// and computeOrbDescriptor (:107-146) on the blurred levels k_blur_levels
+// wrote.  Off by default (orbx_handle::preblur, env ORB_DESC_PREBLUR=1):
+// measured slower end to end, DESIGN.md §8.
+//
+// One wave per keypoint, the next valid keypoint's inputs always in flight in
+// registers: the raw IC_Angle disc (31 rows; lane r loads row r as two
+// dwordx4 and a dword from the aligned column at or left of x - 15) and the
+// 37 x 37 blurred square around it (rows y - 18 .. y + 18, 10 aligned dwords
+// each; 6 dwords per lane), which lands in the wave's 1.5 KB of LDS.  Every
+// keypoint is >= 19 px inside its level (the FAST window), so neither ever
+// leaves the level: no border path.  IC_Angle by byte dot products of the
+// disc rows (integer, order-free sums), then the 512 samples are single LDS
+// byte reads at the rotated pattern points; lane l evaluates tests 4l..4l+3.
+// Per keypoint 1,116 B of raw disc rows and 1,480 B of blurred rows.
+// ---------------------------------------------------------------------------
+constexpr int kIcRows = 2 * kHalfPatch + 1, kBlSq = 37, kBlDw = 10, kBlN = kBlSq * kBlDw;
+constexpr int kBlV = (kBlN + kWave - 1) / kWave;   // 6
+
+struct DescLanePb {
+    uint64_t img, bimg;
+    int pitch, bpitch;
+    uint32_t key;
+};
+
+struct DescKpPb {
+    const uint8_t* img;
+    const uint8_t* bimg;
+    int pitch, bpitch;
+    uint32_t key;
+};
+
+__device__ __forceinline__ bool desc_lane_pb(const DescArgs& a, long long s, DescLanePb& k) {
+    const int f = (int)(s / a.out_total);
+    const int o = (int)(s - (long long)f * a.out_total);
+    const int l = a.slot_level[o];
+    const LevelDev& lv = a.lv[l];
+    if (o - lv.out_base >= a.qt_n[f * a.L + l]) return false;
+    k.img = (uint64_t)(l == 0 ? a.in + f * a.in_fstride : a.pyr + f * a.pyr_fstride + lv.off);
+    k.pitch = l == 0 ? a.in_pitch : lv.pitch;
+    k.bimg = (uint64_t)(a.blur + f * a.blur_fstride + lv.boff);
+    k.bpitch = lv.bpitch;
+    k.key = a.qt_key[s];
+    return true;
+}
+
+__device__ __forceinline__ DescKpPb desc_pick_pb(const DescLanePb& k, int j) {
+    auto rl64 = [&](uint64_t v) {
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
+        return ((uint64_t)hi << 32) | lo;
+    };
+    DescKpPb d;
+    d.img = (const uint8_t*)rl64(k.img);
+    d.bimg = (const uint8_t*)rl64(k.bimg);
+    d.pitch = __builtin_amdgcn_readlane(k.pitch, j);
+    d.bpitch = __builtin_amdgcn_readlane(k.bpitch, j);
+    d.key = (uint32_t)__builtin_amdgcn_readlane((int)k.key, j);
+    return d;
+}
+
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u32x4v* GlobalQuads;
+
+__device__ __forceinline__ void pb_issue(const DescKpPb& k, uint32_t (&rv)[9], uint32_t (&bv)[kBlV]) {
+    const int lane = lane_id();
+    const int cx = (int)(k.key & 0xfff) + (kEdge - 3), cy = (int)((k.key >> 12) & 0xfff) + (kEdge - 3);
+    if (lane < kIcRows) {
+        const GlobalBytes rp = (GlobalBytes)k.img + (long long)(cy - kHalfPatch + lane) * k.pitch + ((cx - kHalfPatch) & ~3);
+        const u32x4v q0 = *(GlobalQuads)rp, q1 = *(GlobalQuads)(rp + 16);
+        rv[0] = q0.x; rv[1] = q0.y; rv[2] = q0.z; rv[3] = q0.w;
+        rv[4] = q1.x; rv[5] = q1.y; rv[6] = q1.z; rv[7] = q1.w;
+        rv[8] = *(GlobalWords)(rp + 32);
+    }
+    const GlobalBytes bp0 = (GlobalBytes)k.bimg + (long long)(cy - 18) * k.bpitch + ((cx - 18) & ~3);
+#pragma unroll
+    for (int j = 0; j < kBlV; ++j) {
+        const int i = lane + j * kWave;
+        if (i < kBlN) {
+            const int r = (i * 6554) >> 16, d = i - r * kBlDw;   // i / 10 for i < 16384
+            bv[j] = *(GlobalWords)(bp0 + (int)__umul24(r, k.bpitch) + 4 * d);
+        }
+    }
+}
+
+template <bool FMA>
+__global__ __launch_bounds__(256) void k_describe_pb(DescArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t bl_s[4][kBlN + 2];
+    const int lane = lane_id(), wv = wave_id();
+    const uint4 patv = ((const uint4*)c_pattern)[lane];
+    asm volatile("" ::"v"(patv.x), "v"(patv.y), "v"(patv.z), "v"(patv.w));
+    const uint32_t patw[4] = {patv.x, patv.y, patv.z, patv.w};
+    uint32_t* bl = bl_s[wv];
+    int um_s[kHalfPatch + 1];
+#pragma unroll
+    for (int v = 0; v <= kHalfPatch; ++v) um_s[v] = __builtin_amdgcn_readfirstlane(a.umax[v]);
+    // lane r < 31 holds disc row v = r - 15: byte b of its aligned word j is
+    // u = 4j + b - 15; masks of |u| <= umax[|v|], weights u + 15
+    uint32_t icm[8];
+    {
+        const int av = lane >= kHalfPatch ? lane - kHalfPatch : kHalfPatch - lane;
+        int um = -1;
+#pragma unroll
+        for (int k = 0; k <= kHalfPatch; ++k)
+            if (av == k) um = um_s[k];
+        if (lane >= kIcRows) um = -1;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * j + b - kHalfPatch;
+                if (u >= -um && u <= um) m |= 0xffu << (8 * b);
+            }
+            icm[j] = m;
+        }
+    }
+    int bunit, bframe;
+    xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
+    const int lb = (bunit * 4 + wv) * kDescSlots;
+    const long long s_begin = (long long)bframe * a.out_total + lb;
+    const int nrun = max(0, min(kDescSlots, a.out_total - lb));
+    DescLanePb mine{};
+    const bool valid = lane < nrun && desc_lane_pb(a, s_begin + lane, mine);
+    uint64_t todo = __ballot(valid);
+    uint32_t rv[9], bv[kBlV];
+    DescKpPb cur{}, nxt{};
+    int jc = -1, jn = -1;
+    auto take = [&](int& j, DescKpPb& k) {
+        j = -1;
+        if (!todo) return;
+        j = __builtin_ctzll(todo);
+        todo &= todo - 1;
+        k = desc_pick_pb(mine, j);
+        pb_issue(k, rv, bv);
+    };
+    take(jc, cur);
+    while (jc >= 0) {
+        const long long s = s_begin + jc;
+        const int cx = (int)(cur.key & 0xfff) + (kEdge - 3);
+        // the current keypoint's registers -> LDS (blurred square) and locals (disc rows)
+#pragma unroll
+        for (int j = 0; j < kBlV; ++j) {
+            const int i = lane + j * kWave;
+            if (i < kBlN) bl[i] = bv[j];
+        }
+        uint32_t al[8];
+        {
+            const uint32_t sh = (uint32_t)((cx - kHalfPatch) & 3);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) al[j] = __builtin_amdgcn_alignbyte(rv[j + 1], rv[j], sh);
+        }
+        take(jn, nxt);
+        // IC_Angle (ORBextractor.cc:76-103): per disc row sum I and sum (u + 15) I
+        uint32_t s1 = 0, sw = 0;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            uint32_t wgt = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                const int u = 4 * j + b - kHalfPatch;
+                if (u <= kHalfPatch) wgt |= (uint32_t)(u + kHalfPatch) << (8 * b);
+            }
+            const uint32_t px = al[j] & icm[j];
+            s1 = __builtin_amdgcn_udot4(px, 0x01010101u, s1, false);
+            sw = __builtin_amdgcn_udot4(px, wgt, sw, false);
+        }
+        int m10 = (int)sw - kHalfPatch * (int)s1;
+        int m01 = (lane - kHalfPatch) * (int)s1;
+        m10 = wave_sum_dpp(m10);
+        m01 = wave_sum_dpp(m01);
+        const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
+        float sb, ca;
+        glibc_sincosf(deg_to_rad(ang_deg), &sb, &ca);
+        wave_sync();
+        // rBRIEF: each sample one byte of the blurred square, centre (18, 18)
+        const uint8_t* C = (const uint8_t*)bl + ((cx - 18) & 3) + 18 * (4 * kBlDw) + 18;
+        int nib = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            int val[2];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+                const float x = (float)(int)(int8_t)(patw[q] >> (16 * e));
+                const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
+                int r, c;
+                brief_offset(x, y, sb, ca, FMA, r, c);
+                val[e] = C[r * (4 * kBlDw) + c];
+            }
+            nib |= (val[0] < val[1]) << q;
+        }
+        const int hi = __shfl_down(nib, 1, kWave);
+        uint8_t* d = a.sdesc + s * 32;
+        if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
+        if (lane == 0) a.angle[s] = ang_deg;
+        jc = jn;
+        cur = nxt;
+        wave_sync();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // k_debug_math: the device compile of k_describe's scalar math over whole
 // input domains, as chunk hashes (orbx_debug_math; host side: the oracle with
 // the system libm, tests/test_gpu_math.py).  One workgroup per chunk.
@@ -2871,6 +3291,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells; P.d_slot_level = P0.d_slot_level;
     const long long F = f0;
     P.d_pyr = P0.d_pyr + F * P0.pyr_bytes;
+    P.d_blur = P0.d_blur + F * P0.blur_bytes;
     P.d_cell_count = P0.d_cell_count + F * P0.ncells;
     P.d_cell_keys = P0.d_cell_keys + F * P0.slot_total;
     P.d_key_scr = P0.d_key_scr + F * P0.slot_total;
@@ -2887,11 +3308,19 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     d_mono += F;
     std::vector<hipEvent_t> marks;
     int stage_no = 0;
-    auto mark = [&]() {
+    auto mark = [&](bool pub = true) {
         // caller's pipeline events (orbx_set_stage_event): recorded after stage k
-        hipEvent_t ue = hd->stage_ev[std::min(stage_no++, 5)];
-        if (ue) (void)hipEventRecord(ue, st);
+        // (the blur stage's own boundary is a profiling mark only; without the
+        // level blur it is a null mark: a zero-length stage, nothing recorded)
+        if (pub) {
+            hipEvent_t ue = hd->stage_ev[std::min(stage_no++, 5)];
+            if (ue) (void)hipEventRecord(ue, st);
+        }
         if (!hd->profiling) return;
+        if (!pub && !hd->preblur) {
+            marks.push_back(nullptr);
+            return;
+        }
         if (hd->ev_next >= hd->ev_pool.size()) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return;
@@ -2973,6 +3402,50 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
                            P.d_pyr + d.off, P.pyr_bytes, d.pitch, d.w, d.h, scx, xt + d.w, P.xmax[l]);
     }
     mark();
+    // level blur (GaussianBlur of every level, k_blur_levels): needs only the
+    // pyramid, so it runs on a side stream beside FAST and the quadtree
+    int kern[7];
+    {
+        static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
+        for (int t = 0; t < 7; ++t) kern[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
+    }
+    const orbx_handle::BlurSide* bside = nullptr;
+    if (hd->preblur) {
+    hipStream_t bst = st;
+    if (hd->blur_fork) {
+        orbx_handle::BlurSide* sd = nullptr;
+        for (auto& b : hd->blur_side)
+            if (b.caller == st) sd = &b;
+        if (!sd) {
+            orbx_handle::BlurSide b{st, nullptr, nullptr, nullptr};
+            ORB_CHECK(hipStreamCreateWithFlags(&b.st, hipStreamNonBlocking));
+            ORB_CHECK(hipEventCreateWithFlags(&b.fork, hipEventDisableTiming));
+            ORB_CHECK(hipEventCreateWithFlags(&b.join, hipEventDisableTiming));
+            hd->blur_side.push_back(b);
+            sd = &hd->blur_side.back();
+        }
+        ORB_CHECK(hipEventRecord(sd->fork, st));
+        ORB_CHECK(hipStreamWaitEvent(sd->st, sd->fork, 0));
+        bst = sd->st;
+        bside = sd;
+    }
+    {
+        BlurArgs ba;
+        ba.in = d_frames; ba.in_fstride = fstride; ba.in_pitch = pitch0;
+        ba.pyr = P.d_pyr; ba.pyr_fstride = P.pyr_bytes;
+        ba.blur = P.d_blur; ba.blur_fstride = P0.blur_bytes;
+        ba.lv = P.d_lv; ba.items = P0.d_blur_items; ba.nitems = P0.nblur_items;
+        const uint32_t k0 = kern[0], k1 = kern[1], k2 = kern[2], k3 = kern[3];
+        const uint32_t hw[10] = {k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), k2 | (k1 << 8) | (k0 << 16),
+                                 (k0 << 8) | (k1 << 16) | (k2 << 24), k3 | (k2 << 8) | (k1 << 16) | (k0 << 24),
+                                 (k0 << 16) | (k1 << 24), k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), k0,
+                                 k0 << 24, k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), k1 | (k0 << 8)};
+        for (int t = 0; t < 10; ++t) ba.hw[t] = hw[t];
+        ba.vw[0] = k0 | (k1 << 16); ba.vw[1] = k2 | (k3 << 16); ba.vw[2] = k2 | (k1 << 16); ba.k0 = k0;
+        hipLaunchKernelGGL(k_blur_levels, dim3((unsigned)((P0.nblur_items + 3) / 4), (unsigned)B), dim3(256), 0, bst, ba);
+    }
+    if (bside) ORB_CHECK(hipEventRecord(bside->join, bst));
+    }
     // FAST cells
     FastArgs fa;
     fa.in = d_frames; fa.in_fstride = fstride; fa.in_pitch = pitch0;
@@ -3015,23 +3488,27 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     hipLaunchKernelGGL(k_quadtree, dim3(L, B), dim3(256), qt_lds_bytes(P), st, qa);
 #endif
     mark();
+    // the blurred levels are complete (profiling stage "blur": the join's wait,
+    // or k_blur_levels itself when it runs in line)
+    if (bside) ORB_CHECK(hipStreamWaitEvent(st, bside->join, 0));
+    mark(false);
     // describe
     DescArgs da;
     da.in = d_frames; da.in_fstride = fstride; da.in_pitch = pitch0;
     da.pyr = P.d_pyr; da.pyr_fstride = P.pyr_bytes;
-    {
-        static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
-        for (int t = 0; t < 7; ++t) da.kern[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
-    }
+    da.blur = P.d_blur; da.blur_fstride = P0.blur_bytes;
+    for (int t = 0; t < 7; ++t) da.kern[t] = kern[t];
     da.lv = P.d_lv; da.qt_key = P.d_qt_key; da.qt_n = P.d_qt_n;
     da.angle = P.d_angle; da.sdesc = P.d_sdesc; da.out_total = P.out_total; da.L = L;
     da.fma = hd->prm.fma_sampling != 0;
     for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
     da.slot_level = P.d_slot_level;
     da.nslots = (long long)B * P.out_total;
-    hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>,
-                       dim3((unsigned)((P.out_total + 4 * kDescSlots - 1) / (4 * kDescSlots)), (unsigned)B), dim3(256), 0,
-                       st, da);
+    const dim3 dgrid((unsigned)((P.out_total + 4 * kDescSlots - 1) / (4 * kDescSlots)), (unsigned)B);
+    if (hd->preblur)
+        hipLaunchKernelGGL(da.fma ? k_describe_pb<true> : k_describe_pb<false>, dgrid, dim3(256), 0, st, da);
+    else
+        hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(256), 0, st, da);
     mark();
     // assemble
     AsmArgs aa;
@@ -3103,6 +3580,8 @@ orbx_handle* orbx_create(const orbx_params* p, int device) {
     h->prm = *p;
     h->device = device;
     if (const char* e = std::getenv("ORB_PYR_MODE")) h->pyr_mode = std::min(4, std::max(0, std::atoi(e)));   // A/B runs
+    if (const char* e = std::getenv("ORB_BLUR_FORK")) h->blur_fork = e[0] != '0';                        // A/B runs
+    if (const char* e = std::getenv("ORB_DESC_PREBLUR")) h->preblur = e[0] == '1';
     init_tables(h);
     return h;
 }
@@ -3115,6 +3594,11 @@ void orbx_destroy(orbx_handle* h) {
     for (hipEvent_t e : h->sub_done) (void)hipEventDestroy(e);
     for (hipStream_t s : h->sub_streams) (void)hipStreamDestroy(s);
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
+    for (auto& b : h->blur_side) {
+        (void)hipEventDestroy(b.fork);
+        (void)hipEventDestroy(b.join);
+        (void)hipStreamDestroy(b.st);
+    }
     if (h->batch_done) (void)hipEventDestroy(h->batch_done);
     if (h->st_scratch) (void)hipFree(h->st_scratch);
     if (h->hb_dev) (void)hipFree(h->hb_dev);
@@ -3417,8 +3901,10 @@ int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages) {
         if (m.size() < 2) continue;
         ORB_CHECK(hipEventSynchronize(m.back()));
         for (size_t i = 0; i + 1 < m.size() && (int)i < nstages; ++i) {
+            if (!m[i + 1]) continue;                          // a null mark closes an empty stage
+            const hipEvent_t a = m[i] ? m[i] : m[i - 1];      // the stage after it starts at the mark before
             float ms = 0.f;
-            ORB_CHECK(hipEventElapsedTime(&ms, m[i], m[i + 1]));
+            ORB_CHECK(hipEventElapsedTime(&ms, a, m[i + 1]));
             stage_ms[i] += ms;
         }
         ++calls;
@@ -3522,6 +4008,24 @@ int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, siz
     const size_t sp = level == 0 ? (size_t)h->last_pitch0 : (size_t)d.pitch;
     if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_debug_blur_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int* w, int* hh) {
+    if (!h || level < 0 || level >= h->plan.L || frame < 0) return ORB_ERR_PARAM;
+    const int nb = h->last_frames ? h->last_B : (h->have_last ? 1 : 0);
+    if (frame >= nb) return ORB_ERR_PARAM;
+    if (!h->preblur) return ORB_ERR_UNSUPPORTED;
+    const Plan& P = h->plan;
+    const LevelDev& d = P.lv[level];
+    if (w) *w = d.w;
+    if (hh) *hh = d.h;
+    if (!dst) return ORB_OK;
+    (void)hipSetDevice(h->device);
+    if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
+    ORB_CHECK(hipDeviceSynchronize());
+    ORB_CHECK(hipMemcpy2D(dst, dst_step, P.d_blur + (long long)frame * P.blur_bytes + d.boff, (size_t)d.bpitch, d.w,
+                          d.h, hipMemcpyDeviceToHost));
     return ORB_OK;
 }
 

@@ -146,6 +146,18 @@ class ORBextractor:
         assert off == n
         return out
 
+    def debug_blur_level(self, level: int, frame: int = 0) -> np.ndarray:
+        """The blurred level k_describe_pb sampled (GaussianBlur 7x7 of the
+        level, ORBextractor.cc:1132-1133) for frame `frame` of the last call."""
+        w, hh = C.c_int(0), C.c_int(0)
+        lib = capi.lib()
+        capi.check(lib.orbx_debug_blur_level(self._h, frame, level, None, 0, C.byref(w), C.byref(hh)),
+                   "orbx_debug_blur_level")
+        out = np.zeros((hh.value, w.value), np.uint8)
+        capi.check(lib.orbx_debug_blur_level(self._h, frame, level, abi.ptr(out), w.value, None, None),
+                   "orbx_debug_blur_level")
+        return out
+
     def extract_batch_device(self, frames, lapping=(0, 1000), out=None, stream=None):
         """HBM-resident batch path: ``frames`` is a (B, H, W) uint8 CUDA tensor.
         Returns (kps (B, cap) as a raw int32 tensor view, desc (B, cap, 32),

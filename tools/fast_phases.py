@@ -18,6 +18,8 @@ def main():
     frames = torch.from_numpy(synth.sequence(752, 480, 256, config=2)).cuda()
     ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
     L = capi.lib()
+    if hasattr(L, "orbx_debug_qt_timing"):
+        return quadtree_phases(L, ex, frames)
     if hasattr(L, "orbx_debug_desc_timing"):
         return describe_phases(L, ex, frames)
     timing = hasattr(L, "orbx_debug_fast_timing")
@@ -47,6 +49,26 @@ def main():
     ev1.record()
     torch.cuda.synchronize()
     print(f"extract batch {ev0.elapsed_time(ev1) / 10:.3f} ms")
+
+
+def quadtree_phases(L, ex, frames):
+    """k_quadtree phases per level from a -DORB_QT_TIMING library."""
+    import torch
+    L.orbx_debug_qt_timing.argtypes = [C.c_void_p, C.c_int]
+    out = np.zeros((16, 12), np.uint64)
+    for _ in range(3):
+        ex.extract_batch_device(frames, (0, 1000))
+    torch.cuda.synchronize()
+    L.orbx_debug_qt_timing(out.ctypes.data, 1)
+    ex.extract_batch_device(frames, (0, 1000))
+    torch.cuda.synchronize()
+    L.orbx_debug_qt_timing(out.ctypes.data, 1)
+    names = ["gather", "init", "outer", "last", "retain", "o:setup", "o:count", "o:divide"]
+    print("level " + " ".join(f"{n:>9s}" for n in names) + "   max_block  outer/blk last/blk (kcyc per block)")
+    for l in range(8):
+        nb = max(1, int(out[l, 11]))
+        print(f"{l:5d} " + " ".join(f"{int(out[l, k]) / nb / 1e3:9.1f}" for k in range(8))
+              + f"   {int(out[l, 8]) / 1e3:9.1f}  {int(out[l, 9]) / nb:8.2f} {int(out[l, 10]) / nb:8.2f}")
 
 
 def describe_phases(L, ex, frames):
