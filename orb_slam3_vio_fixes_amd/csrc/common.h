@@ -104,4 +104,38 @@ __device__ int block_excl_scan(int* a, int n, int* tmp) {
     return total;
 }
 
+// Three exclusive scans in place (a[0..na), b[0..nb), c[0..nc)) with one set
+// of barriers; tot receives the three totals.  tmp: >= 3 * (waves + 1) ints.
+__device__ inline void block_excl_scan3(int* a, int na, int* b, int nb, int* c, int nc, int* tmp, int (&tot)[3]) {
+    const int T = blockDim.x, t = threadIdx.x, W = T / kWave;
+    int* arr[3] = {a, b, c};
+    const int n[3] = {na, nb, nc};
+    int sum[3], incl[3], lo[3], hi[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        const int per = (n[j] + T - 1) / T;
+        lo[j] = min(n[j], t * per);
+        hi[j] = min(n[j], lo[j] + per);
+        int s = 0;
+        for (int i = lo[j]; i < hi[j]; ++i) s += arr[j][i];
+        sum[j] = s;
+        incl[j] = wave_incl_scan(s);
+        if (lane_id() == kWave - 1) tmp[j * (W + 1) + wave_id()] = incl[j];
+    }
+    __syncthreads();
+    if (t < 3) {
+        int acc = 0;
+        for (int w = 0; w < W; ++w) { const int x = tmp[t * (W + 1) + w]; tmp[t * (W + 1) + w] = acc; acc += x; }
+        tmp[t * (W + 1) + W] = acc;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+        int run = tmp[j * (W + 1) + wave_id()] + incl[j] - sum[j];
+        for (int i = lo[j]; i < hi[j]; ++i) { const int x = arr[j][i]; arr[j][i] = run; run += x; }
+        tot[j] = tmp[j * (W + 1) + W];
+    }
+    __syncthreads();
+}
+
 }  // namespace orbmi

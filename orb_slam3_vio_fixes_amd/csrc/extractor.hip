@@ -1965,8 +1965,31 @@ __device__ void block_std_sort(SortRec* a, int m, SortRec* backup, int* Lp, int*
         __syncthreads();
         return;
     }
+    // leaves (<= 16 records, never crossed by the final insertion pass):
+    // insertion sort under a strict weak order is the stable sort, so record
+    // j of a leaf goes to #{less} + #{equivalent before j} -- 16 lanes per
+    // leaf, four leaves per wave, instead of a serial insertion sort by one
+    // thread per leaf (~20 % of the sort)
     const int nleaf = ctl[3];
-    for (int i = tid; i < nleaf; i += T) insertion_sort_(a + (leaves[i] >> 16), a + (leaves[i] & 0xffff));
+    for (int L0 = wv * 4; L0 < nleaf; L0 += nw * 4) {
+        const int leaf = L0 + (lane >> 4), sub = lane & 15;
+        int f = 0, len = 0, rank = 0;
+        SortRec x{};
+        if (leaf < nleaf) {
+            f = leaves[leaf] >> 16;
+            len = (leaves[leaf] & 0xffff) - f;
+        }
+        if (sub < len) {
+            x = a[f + sub];
+            for (int j = 0; j < len; ++j) {
+                const SortRec y = a[f + j];
+                rank += node_less(y, x) || (j < sub && !node_less(x, y));
+            }
+        }
+        fast_wave_sync();
+        if (sub < len) a[f + rank] = x;
+        fast_wave_sync();
+    }
     __syncthreads();
 }
 
@@ -2006,6 +2029,8 @@ __global__ __launch_bounds__(256) void k_debug_sort(const int* __restrict__ off,
     if (threadIdx.x == 0) fallback[blockIdx.x] = ctl[2];
 }
 
+constexpr int kQtB = 4;   // keys per thread per round of the quadtree's key passes
+
 // Divide s.ord[0..m) (ccnt/kq already computed for them, s.div set for every
 // node); rebuild the list into buffer cur^1; remap the keys.  Returns the new
 // size; *nexp receives the queue length.
@@ -2021,9 +2046,9 @@ __device__ int qt_divide(QtLds& s, int& cur, int size, int m, const int K, int* 
     }
     for (int i = tid; i < size; i += T) s.nd[i] = s.div[i] ? 0 : 1;
     __syncthreads();
-    const int totNE = block_excl_scan(s.rne, m, s.tmp);
-    const int totGT = block_excl_scan(s.rgt, m, s.tmp);
-    block_excl_scan(s.nd, size, s.tmp);
+    int tot3[3];
+    block_excl_scan3(s.rne, m, s.rgt, m, s.nd, size, s.tmp, tot3);
+    const int totNE = tot3[0], totGT = tot3[1];
     const int nx = cur ^ 1;
     const short4* R = qsel(s.rect, cur);
     const int* C = qsel(s.cnt, cur);
@@ -2056,9 +2081,23 @@ __device__ int qt_divide(QtLds& s, int& cur, int size, int m, const int K, int* 
         qsel(s.nomore, nx)[np] = qsel(s.nomore, cur)[i];
     }
     __syncthreads();
-    for (int k = tid; k < K; k += T) {
-        const int n = knode[k];
-        knode[k] = s.div[n] ? s.newpos[4 * n + kq[k]] : s.keep[n];
+    {
+        int* __restrict__ kn = knode;
+        const uint8_t* __restrict__ kqi = kq;
+        for (int k0 = tid; k0 < K; k0 += kQtB * T) {
+            int n[kQtB], q[kQtB];
+#pragma unroll
+            for (int b = 0; b < kQtB; ++b) {
+                const int k = k0 + b * T;
+                n[b] = k < K ? kn[k] : 0;
+                q[b] = k < K ? kqi[k] : 0;
+            }
+#pragma unroll
+            for (int b = 0; b < kQtB; ++b) {
+                const int k = k0 + b * T;
+                if (k < K) kn[k] = s.div[n[b]] ? s.newpos[4 * n[b] + q[b]] : s.keep[n[b]];
+            }
+        }
     }
     __syncthreads();
     cur = nx;
@@ -2073,12 +2112,27 @@ __device__ void qt_count(QtLds& s, int cur, int size, const int K, const uint32_
     for (int i = tid; i < 4 * size; i += T) s.ccnt[i] = 0;
     __syncthreads();
     const short4* R = qsel(s.rect, cur);
-    for (int k = tid; k < K; k += T) {
-        const int n = knode[k];
-        if (s.div[n]) {
-            const int q = quadrant(keys[k], R[n]);
-            kq[k] = (uint8_t)q;
-            atomicAdd(&s.ccnt[4 * n + q], 1);
+    // kQtB keys per thread per round, every load of the round in flight at once
+    const int* __restrict__ kn = knode;
+    const uint32_t* __restrict__ ks = keys;
+    uint8_t* __restrict__ kqo = kq;
+    for (int k0 = tid; k0 < K; k0 += kQtB * T) {
+        int n[kQtB];
+        uint32_t key[kQtB];
+#pragma unroll
+        for (int b = 0; b < kQtB; ++b) {
+            const int k = k0 + b * T;
+            n[b] = k < K ? kn[k] : 0;
+            key[b] = k < K ? ks[k] : 0u;
+        }
+#pragma unroll
+        for (int b = 0; b < kQtB; ++b) {
+            const int k = k0 + b * T;
+            if (k < K && s.div[n[b]]) {
+                const int q = quadrant(key[b], R[n[b]]);
+                kqo[k] = (uint8_t)q;
+                atomicAdd(&s.ccnt[4 * n[b] + q], 1);
+            }
         }
     }
     __syncthreads();
@@ -2087,7 +2141,7 @@ __device__ void qt_count(QtLds& s, int cur, int size, const int K, const uint32_
 #ifdef ORB_QT_TIMING
 // phase profile of k_quadtree (tools/fast_phases.py --quadtree): per level,
 // shader cycles per phase summed over blocks, the longest block, pass counts
-__device__ unsigned long long g_qt_t[16][12];
+__device__ unsigned long long g_qt_t[16][16];
 #define QT_T(k)                                                              \
     do {                                                                     \
         const unsigned long long t_ = __builtin_amdgcn_s_memtime();          \
@@ -2097,7 +2151,7 @@ __device__ unsigned long long g_qt_t[16][12];
 extern "C" int orbx_debug_qt_timing(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_qt_t), sizeof(g_qt_t)) != hipSuccess) return -4;
     if (reset) {
-        static unsigned long long z[16][12];
+        static unsigned long long z[16][16];
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_qt_t), z, sizeof(z)) != hipSuccess) return -4;
     }
     return 0;
@@ -2159,29 +2213,57 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     __syncthreads();
     const int K = block_excl_scan(s.off, lv.ncells, s.tmp);
     const int cap = lv.ncells ? lv.slot_total / lv.ncells : 0;
-    for (int c = wave_id(); c < lv.ncells; c += T / kWave) {
-        const int base = s.off[c];
-        const int n = (c + 1 < lv.ncells ? s.off[c + 1] : K) - base;
-        for (int j = lane_id(); j < n; j += kWave) keys[base + j] = cslots[c * cap + j];
-    }
-    __syncthreads();
-    QT_T(0);
     if (K == 0) {
+        QT_T(0);
         if (tid == 0) a.qt_n[f * a.L + l] = 0;
         return;
     }
-    // 2. initial nodes (:559-601)
+    // 1+2. keys in vToDistributeKeys order, each with its initial node's bin
+    // (:559-601, vpIniNodes[kp.pt.x / hX]) -- one flat pass: key k's cell by a
+    // binary search of the cell offsets in LDS, kQtB keys per thread in flight
     const int nIni = lv.nIni;
     int* bcnt = s.rne;
     int* bpos = s.rgt;
     for (int i = tid; i < nIni; i += T) bcnt[i] = 0;
     __syncthreads();
-    for (int k = tid; k < K; k += T) {
-        const int b = (int)((float)(keys[k] & 0xfff) / lv.hX);
-        knode[k] = b;
-        atomicAdd(&bcnt[b], 1);
+    {
+        const uint32_t* __restrict__ src = cslots;
+        uint32_t* __restrict__ dst = keys;
+        int* __restrict__ kn = knode;
+        const int nc = lv.ncells;
+        for (int k0 = tid; k0 < K; k0 += kQtB * T) {
+            int c[kQtB];
+#pragma unroll
+            for (int q = 0; q < kQtB; ++q) {
+                const int k = min(k0 + q * T, K - 1);
+                int lo = 0, hi = nc;                   // off[lo] <= k < off[hi] (off[nc] = K)
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s.off[mid] <= k) lo = mid;
+                    else hi = mid;
+                }
+                c[q] = lo;
+            }
+            uint32_t v[kQtB];
+#pragma unroll
+            for (int q = 0; q < kQtB; ++q) {
+                const int k = min(k0 + q * T, K - 1);
+                v[q] = src[c[q] * cap + (k - s.off[c[q]])];
+            }
+#pragma unroll
+            for (int q = 0; q < kQtB; ++q) {
+                const int k = k0 + q * T;
+                if (k < K) {
+                    dst[k] = v[q];
+                    const int bn = (int)((float)(v[q] & 0xfff) / lv.hX);
+                    kn[k] = bn;
+                    atomicAdd(&bcnt[bn], 1);
+                }
+            }
+        }
     }
     __syncthreads();
+    QT_T(0);
     if (tid == 0) {
         int n = 0;
         for (int i = 0; i < nIni; ++i) {
@@ -2197,7 +2279,9 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         s.misc[0] = n;
     }
     __syncthreads();
-    for (int k = tid; k < K; k += T) knode[k] = bpos[knode[k]];
+    // bins to list positions: the identity unless a bin is empty
+    if (s.misc[0] != nIni)
+        for (int k = tid; k < K; k += T) knode[k] = bpos[knode[k]];
     int size = s.misc[0];
     int cur = 0;
     const int N = lv.N;
@@ -2209,9 +2293,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     bool last = false;
     while (true) {
         const int prev = size;
-        for (int i = tid; i < size; i += T) s.nd[i] = qsel(s.nomore, cur)[i] ? 0 : 1;
-        __syncthreads();
-        for (int i = tid; i < size; i += T) s.div[i] = s.nd[i];
+        for (int i = tid; i < size; i += T) s.div[i] = s.nd[i] = qsel(s.nomore, cur)[i] ? 0 : 1;
         __syncthreads();
         const int m = block_excl_scan(s.nd, size, s.tmp);
         for (int i = tid; i < size; i += T)
@@ -2239,12 +2321,15 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
         }
         for (int i = tid; i < size; i += T) s.div[i] = 0;
         __syncthreads();
+        QT_T(15);
         // ccnt / newpos / ord are free until qt_count below
         block_std_sort(s.srt, m, (SortRec*)s.ccnt, s.newpos, s.newpos + NC, (SortFrame*)(s.newpos + 2 * NC),
                        (SortFrame*)(s.newpos + 3 * NC), s.ord, s.misc + 4, s.stk);
         for (int j = tid; j < m; j += T) s.div[s.srt[j].pos] = 1;
         __syncthreads();
+        QT_T(12);
         qt_count(s, cur, size, K, keys, knode, kq);
+        QT_T(13);
         // processing rank r = m-1-j; stop after the first rank at which the list reaches N
         for (int r = tid; r < m; r += T) {
             const int i = s.srt[m - 1 - r].pos;
@@ -2269,7 +2354,9 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
             else s.div[i] = 0;
         }
         __syncthreads();
+        QT_T(15);
         size = qt_divide(s, cur, size, mp, K, knode, kq, &nexp);
+        QT_T(14);
 #ifdef ORB_QT_TIMING
         ++qt_lastr;
 #endif
@@ -2280,8 +2367,21 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     int* best = s.ccnt;
     for (int i = tid; i < size; i += T) best[i] = 0;
     __syncthreads();
-    for (int k = tid; k < K; k += T)
-        atomicMax(&best[knode[k]], (int)(((keys[k] >> 24) << 23) | (0x7FFFFF - k)));
+    for (int k0 = tid; k0 < K; k0 += kQtB * T) {
+        int n[kQtB];
+        uint32_t key[kQtB];
+#pragma unroll
+        for (int b = 0; b < kQtB; ++b) {
+            const int k = k0 + b * T;
+            n[b] = k < K ? knode[k] : 0;
+            key[b] = k < K ? keys[k] : 0u;
+        }
+#pragma unroll
+        for (int b = 0; b < kQtB; ++b) {
+            const int k = k0 + b * T;
+            if (k < K) atomicMax(&best[n[b]], (int)(((key[b] >> 24) << 23) | (0x7FFFFF - k)));
+        }
+    }
     __syncthreads();
     const int nout = min(size, lv.out_cap);
     for (int i = tid; i < nout; i += T) out[i] = keys[0x7FFFFF - (best[i] & 0x7FFFFF)];

@@ -55,7 +55,7 @@ def quadtree_phases(L, ex, frames):
     """k_quadtree phases per level from a -DORB_QT_TIMING library."""
     import torch
     L.orbx_debug_qt_timing.argtypes = [C.c_void_p, C.c_int]
-    out = np.zeros((16, 12), np.uint64)
+    out = np.zeros((16, 16), np.uint64)
     for _ in range(3):
         ex.extract_batch_device(frames, (0, 1000))
     torch.cuda.synchronize()
@@ -64,10 +64,12 @@ def quadtree_phases(L, ex, frames):
     torch.cuda.synchronize()
     L.orbx_debug_qt_timing(out.ctypes.data, 1)
     names = ["gather", "init", "outer", "last", "retain", "o:setup", "o:count", "o:divide"]
+    cols = list(range(8)) + [12, 13, 14, 15]
+    names += ["l:sort", "l:count", "l:divide", "l:other"]
     print("level " + " ".join(f"{n:>9s}" for n in names) + "   max_block  outer/blk last/blk (kcyc per block)")
     for l in range(8):
         nb = max(1, int(out[l, 11]))
-        print(f"{l:5d} " + " ".join(f"{int(out[l, k]) / nb / 1e3:9.1f}" for k in range(8))
+        print(f"{l:5d} " + " ".join(f"{int(out[l, k]) / nb / 1e3:9.1f}" for k in cols)
               + f"   {int(out[l, 8]) / 1e3:9.1f}  {int(out[l, 9]) / nb:8.2f} {int(out[l, 10]) / nb:8.2f}")
 
 
