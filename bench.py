@@ -71,6 +71,9 @@ def parse():
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run SearchForInitialization on the extraction stream (no step overlap)")
     ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
+    ap.add_argument("--overlap", type=int, default=1, choices=[1, 2],
+                    help="batches in flight: 2 = consecutive steps alternate between two extractor handles "
+                         "(own plan and scratch each) on two streams, so step k+1 extracts beside step k")
     ap.add_argument("--sfi-after", type=int, default=2,
                     help="pipeline: step k's SearchForInitialization waits until step k+1's extraction has passed this "
                          "stage (orbx_set_stage_event: 1 pyramid, 2 FAST (default), 3 quadtree; -1: starts at once)")
@@ -299,10 +302,14 @@ def main():
     Bx = B + (1 if rank < world - 1 else 0)
     frames_np = synth.global_sequence(W, H, rank * B, Bx, config=2)
     frames = torch.from_numpy(frames_np).to(dev)
-    ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local)
+    exs = [orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local) for _ in range(args.overlap)]
+    ex = exs[0]
     L = capi.lib()
-    capi.check(L.orbx_set_streams(ex._h, args.streams), "orbx_set_streams")
+    for e in exs:
+        capi.check(L.orbx_set_streams(e._h, args.streams), "orbx_set_streams")
     stream = torch.cuda.current_stream(dev)
+    # extraction stream of each handle (--overlap 2: the second on its own stream)
+    xstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.overlap - 1)]
     kps, desc, n, mono, cap = ex.extract_batch_device(frames, LAP)
     # two output sets: SearchForInitialization of step k runs on its own
     # stream while step k+1 extracts into the other set (--no-pipeline: both
@@ -351,13 +358,14 @@ def main():
         i = counter[0] % 2
         counter[0] += 1
         k_, d_, n_, m_ = outs[i]
+        xe, xs = exs[i % args.overlap], xstreams[i % args.overlap]
         if done[i] is not None:
-            stream.wait_event(done[i])   # the match that read this set has finished
+            xs.wait_event(done[i])       # the match that read this set has finished
         if stage_ev[i] is not None:
-            capi.check(L.orbx_set_stage_event(ex._h, args.sfi_after, stage_ev[i].cuda_event), "stage event")
-        ex.extract_batch_device(frames, LAP, out=(k_, d_, n_, m_))
+            capi.check(L.orbx_set_stage_event(xe._h, args.sfi_after, stage_ev[i].cuda_event), "stage event")
+        xe.extract_batch_device(frames, LAP, out=(k_, d_, n_, m_), stream=xs)
         extracted = torch.cuda.Event()
-        extracted.record(stream)
+        extracted.record(xs)
         if stage_ev[i] is None:
             match(i, extracted, timed=timed)
             return
@@ -380,7 +388,8 @@ def main():
     torch.cuda.synchronize()
     prof = not args.no_profile
     if prof:
-        L.orbx_set_profiling(ex._h, 1)
+        for e in exs:
+            L.orbx_set_profiling(e._h, 1)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=prof)
@@ -392,8 +401,12 @@ def main():
     elapsed = time.perf_counter() - t0
     stage_ms = np.zeros(len(STAGES), np.float32)
     if prof:
-        calls = L.orbx_get_profile(ex._h, stage_ms.ctypes.data, len(STAGES))
-        L.orbx_set_profiling(ex._h, 0)
+        calls = 0
+        for e in exs:
+            sm = np.zeros(len(STAGES), np.float32)
+            calls += L.orbx_get_profile(e._h, sm.ctypes.data, len(STAGES))
+            L.orbx_set_profiling(e._h, 0)
+            stage_ms += sm
         stage_ms /= max(1, calls)
         frames_per_launch = Bx * args.steps / max(1, calls)  # each sub-batch range is one launch per stage
     else:
@@ -433,7 +446,7 @@ def main():
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
-                          "frames_per_step_per_gpu": B, "streams": args.streams, "pipeline": args.pipeline,
+                          "frames_per_step_per_gpu": B, "streams": args.streams, "overlap": args.overlap, "pipeline": args.pipeline,
                           "sfi_after_stage": args.sfi_after if args.pipeline else None,
                           "parallelism": f"frames sharded over {world} GPU(s), halo frame per seam"},
                "stage_ms": {**{k: float(v) for k, v in zip(STAGES, stage_ms)},

@@ -1413,6 +1413,9 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #ifndef ORB_FAST_EMIT
 #define ORB_FAST_EMIT 1   // 1: items list + one expansion pass; 0: per-round bit loops (round 2)
 #endif
+#ifndef ORB_FAST_PIPE
+#define ORB_FAST_PIPE 1   // pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
+#endif
 #ifndef ORB_QT_LEVEL_MAJOR
 #define ORB_QT_LEVEL_MAJOR 1
 #endif
@@ -1608,6 +1611,43 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     idx0 = (int)__umul24(r, ww) + 4 * j - X0;
                 }
             };
+#if ORB_FAST_PIPE
+            // the same pre-test split at its LDS reads, so the reads of round
+            // r + 1 are in flight while round r is evaluated (the ilist store
+            // between them would otherwise keep the compiler from hoisting)
+            struct PreIn {
+                uint32_t cm, c0, c1, c2, u0, u1, d0, d1;
+                int k;
+            };
+            auto pre_load = [&](int it, PreIn& q) {
+                const int itc = min(it, nitems - 1);
+                const int r = div_row(itc, inv_ndp);
+                q.k = itc - (int)__umul24(r, ndp);
+                const uint32_t* row = roi32 + __umul24(r + 3, rs4) + (j0 + 2 * q.k);
+                q.cm = row[-1]; q.c0 = row[0]; q.c1 = row[1]; q.c2 = row[2];
+                q.u0 = row[-3 * rs4]; q.u1 = row[1 - 3 * rs4];
+                q.d0 = row[3 * rs4]; q.d1 = row[1 + 3 * rs4];
+            };
+            auto pre_eval = [&](const PreIn& q, bool ok, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh) {
+                const uint32_t c0l = lo_bytes(q.c0), c0h = hi_bytes(q.c0), c1l = lo_bytes(q.c1), c1h = hi_bytes(q.c1);
+                const uint32_t lf0l = hi_bytes(q.cm), lf0h = pair_bytes<0x0c040c02u>(q.c0, q.cm);
+                const uint32_t rt0l = pair_bytes<0x0c050c03u>(q.c1, q.c0), rt0h = c1l;
+                const uint32_t lf1l = c0h, lf1h = pair_bytes<0x0c040c02u>(q.c1, q.c0);
+                const uint32_t rt1l = pair_bytes<0x0c050c03u>(q.c2, q.c1), rt1h = lo_bytes(q.c2);
+                uint32_t b0, k0, b1, k1, b2, k2, b3, k3;
+                compass_signs(c0l, lo_bytes(q.u0), lo_bytes(q.d0), lf0l, rt0l, tt, b0, k0);
+                compass_signs(c0h, hi_bytes(q.u0), hi_bytes(q.d0), lf0h, rt0h, tt, b1, k1);
+                compass_signs(c1l, lo_bytes(q.u1), lo_bytes(q.d1), lf1l, rt1l, tt, b2, k2);
+                compass_signs(c1h, hi_bytes(q.u1), hi_bytes(q.d1), lf1h, rt1h, tt, b3, k3);
+                uint64_t vm = q.k == 0 ? m_first : (q.k == ndp - 1 ? m_last : 0x8080808080808080ull);
+                if (!ok) vm = 0;
+                const uint32_t vl = (uint32_t)vm, vh = (uint32_t)(vm >> 32);
+                bl = sign_bytes(b0, b1) & vl;
+                bh = sign_bytes(b2, b3) & vh;
+                dl = sign_bytes(k0, k1) & vl;
+                dh = sign_bytes(k2, k3) & vh;
+            };
+#endif
             // candidates of one item per lane, appended in row-major order
             auto emit = [&](uint32_t bl, uint32_t bh, uint32_t dl, uint32_t dh, int idx0) {
                 uint32_t pl = bl | dl, ph = bh | dh;
@@ -1641,10 +1681,20 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             //     each): item index | bright mask << 16 | dark mask << 24, bit
             //     k = item pixel k (byte flags folded by one v_dot4 per half)
             int nlist = 0;
+#if ORB_FAST_PIPE
+            PreIn pq{};
+            if (nitems > 0) pre_load(lane, pq);
+#endif
             for (int base = 0; base < nitems; base += kWave) {
                 uint32_t bl, bh, dl, dh;
+#if ORB_FAST_PIPE
+                const PreIn cq = pq;
+                if (base + kWave < nitems) pre_load(base + kWave + lane, pq);
+                pre_eval(cq, base + lane < nitems, bl, bh, dl, dh);
+#else
                 int i0;
                 pretest(base + lane, bl, bh, dl, dh, i0);
+#endif
                 const uint32_t mb = __builtin_amdgcn_udot4(bh >> 7, 0x80402010u,
                                                            __builtin_amdgcn_udot4(bl >> 7, 0x08040201u, 0u, false), false);
                 const uint32_t md = __builtin_amdgcn_udot4(dh >> 7, 0x80402010u,
