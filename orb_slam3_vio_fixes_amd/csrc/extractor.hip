@@ -1414,7 +1414,7 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #define ORB_FAST_EMIT 1   // 1: items list + one expansion pass; 0: per-round bit loops (round 2)
 #endif
 #ifndef ORB_FAST_PIPE
-#define ORB_FAST_PIPE 1   // pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
+#define ORB_FAST_PIPE 0   // 1: pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
 #endif
 #ifndef ORB_QT_LEVEL_MAJOR
 #define ORB_QT_LEVEL_MAJOR 1
