@@ -925,6 +925,9 @@ __device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
     return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
 }
 
+#ifndef ORB_PYR_PREF
+#define ORB_PYR_PREF 0   // 1: draw the next wave-item ticket while the current item runs
+#endif
 __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
     extern __shared__ uint4 ps_lds[];
     uint32_t* lds = (uint32_t*)ps_lds;
@@ -1004,6 +1007,11 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
         // wave-item, ng | runs << 16}; lane 0 {wave-items of the step}
         const uint4 se = ps_lds[a.steps_u4 + s * a.L + min(lane, a.L - 1)];
         const int W = __builtin_amdgcn_readfirstlane((int)se.x);
+#if ORB_PYR_PREF
+        // the next item's ticket is drawn while the current item runs
+        int jn = 0;
+        if (lane == 0) jn = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
+#endif
         for (int it = 0; it <= W; ++it) {      // bounded: a wave never takes more than W items
             // wave-items are taken from a per-step LDS counter: waves that drew
             // cheap items take more, so the step ends when the work does.  The
@@ -1012,10 +1020,16 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
             // zeroed above.  (Round 2 blamed a failing end-of-LDS layout on the
             // hardware; tests/test_gpu_configs.py runs that layout, zeroed,
             // bit-exact -- see DESIGN.md on the cause.)
+#if ORB_PYR_PREF
+            const int j = __builtin_amdgcn_readfirstlane(jn);
+            if (j >= W) break;
+            if (lane == 0) jn = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
+#else
             int jj = 0;
             if (lane == 0) jj = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
             const int j = __builtin_amdgcn_readfirstlane(jj);
             if (j >= W) break;
+#endif
             const int l = __builtin_popcountll(__ballot(lane >= 1 && lane < a.L && (int)se.z <= j));
             const int lo = __builtin_amdgcn_readlane((int)se.x, l), nrows = __builtin_amdgcn_readlane((int)se.y, l);
             const int wst = __builtin_amdgcn_readlane((int)se.z, l), ngr = __builtin_amdgcn_readlane((int)se.w, l);
@@ -1295,9 +1309,9 @@ __device__ __forceinline__ int fast_dir_score(const int (&x)[16], int v, int dar
 // NMS on the zero-padded score map (pitch ww+2): p survives at threshold t iff
 // s(p) >= max(t, 1) and s(p) > s_t(q) for its 8 neighbours, s_t(q) = s(q) if
 // s(q) >= t else 0; the zero border stands for pixels outside the window.
-__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c, int t) {
+__device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c, int t, int& s) {
     const uint8_t* p = sc + mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(c + 1));
-    const int s = p[0];
+    s = p[0];
     if (s < max(t, 1)) return false;
     const int q[8] = {p[-sp - 1], p[-sp], p[-sp + 1], p[-1], p[1], p[sp - 1], p[sp], p[sp + 1]};
     bool keep = true;
@@ -1412,6 +1426,12 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #endif
 #ifndef ORB_FAST_EMIT
 #define ORB_FAST_EMIT 1   // 1: items list + one expansion pass; 0: per-round bit loops (round 2)
+#endif
+#ifndef ORB_FAST_FUSED_OUT
+#define ORB_FAST_FUSED_OUT 1   // survivors written inside the NMS loop (0: a separate output pass)
+#endif
+#ifndef ORB_FAST_RESET
+#define ORB_FAST_RESET 0   // 1: score map zeroed once per wave, each cell resets its own entries (measured slower: 0.418-0.420 vs 0.408-0.413 ms)
 #endif
 #ifndef ORB_FAST_PIPE
 #define ORB_FAST_PIPE 0   // 1: pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
@@ -1540,8 +1560,12 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         const uint8_t* R = roi + shift;
         const int ww = max(0, cur.cols - 6), wh = max(0, cur.rows - 6);
         const int sp = ww + 2, npad = sp * (wh + 2);
+#if ORB_FAST_RESET
+        (void)npad;   // the map is all zero here: zeroed once, and each cell resets the entries it wrote
+#else
         for (int i = lane; i < (npad + 3) / 4; i += kWave) ((uint32_t*)sc)[i] = 0u;
         fast_wave_sync();
+#endif
         if (it == it0) FAST_T(10); else FAST_T(0);
         const float inv_ww = ww ? 1.0f / (float)ww : 0.f;
         const int X0 = shift + 3, j0 = X0 >> 2;
@@ -1767,24 +1791,52 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             }
             fast_wave_sync();
             if (pass == 0) FAST_T(2); else FAST_T(6);
-            // 3. NMS at this pass's threshold; keep its ballots
+            // 3. NMS at this pass's threshold.  ORB_FAST_FUSED_OUT: the
+            //    survivors go out in the same loop (the candidate list is
+            //    row-major, so ballot order is the reference's order; a pass
+            //    with no survivor writes nothing, so writing speculatively in
+            //    the iniTh pass is exact); otherwise keep the ballots for step 4
             cnt = 0;
             const int nchunk = (ncand + kWave - 1) / kWave;
+#if ORB_FAST_FUSED_OUT
+            uint32_t* outp = a.cell_keys + (long long)f * a.slot_total + cur.slot_off;
+#endif
             for (int k = 0; k < nchunk; ++k) {
                 const int q = k * kWave + lane;
                 bool keep = false;
+#if ORB_FAST_FUSED_OUT
+                uint32_t key = 0;
+                if (q < ncand) {
+                    const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                    int sv;
+                    keep = nms_keep(sc, sp, r, cc, t, sv);
+                    // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
+                    key = (uint32_t)(cur.x0 + cc + 3 - (kEdge - 3)) | ((uint32_t)(cur.y0 + r + 3 - (kEdge - 3)) << 12) |
+                          ((uint32_t)sv << 24);
+                }
+                const uint64_t m = __ballot(keep);
+                if (keep) {
+                    const int pos = cnt + mask_rank(m);
+                    if (pos < cur.cap) outp[pos] = key;
+                }
+#else
                 if (q < ncand) {
                     const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
-                    keep = nms_keep(sc, sp, r, i - (int)__umul24(r, ww), t);
+                    int sv;
+                    keep = nms_keep(sc, sp, r, i - (int)__umul24(r, ww), t, sv);
                 }
                 const uint64_t m = __ballot(keep);
                 if (lane == 0) kmask[k] = m;
+#endif
                 cnt += __popcll(m);
             }
             fast_wave_sync();
             if (pass == 0) FAST_T(3); else FAST_T(7);
             if (cnt > 0) break;
         }
+#if ORB_FAST_FUSED_OUT
+        const int written = cnt;
+#else
         // 4. survivors of the deciding pass, row-major
         uint32_t* out = a.cell_keys + (long long)f * a.slot_total + cur.slot_off;
         int written = 0;
@@ -1807,10 +1859,23 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 written += __popcll(m);
             }
         }
+#endif
         if (lane == 0) a.cell_count[it] = min(written, cur.cap);
+#if ORB_FAST_RESET
+        // back to an all-zero map: the deciding pass's candidates cover every
+        // entry either pass wrote (a pixel passing the pre-test at iniTh
+        // passes it at minThFAST < iniThFAST)
+        for (int q = lane; q < ncand; q += kWave) {
+            const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
+            sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(i - (int)__umul24(r, ww) + 1))] = 0;
+        }
+#endif
         fast_wave_sync();
         FAST_T(9);
     };
+#if ORB_FAST_RESET
+    for (int i = lane; i < a.win_max / 4; i += kWave) ((uint32_t*)sc)[i] = 0u;
+#endif
     for (int it = it0; it < it_end; it += step) {
         // land the prefetched ROI in LDS, then prefetch the next cell's ROI
         land(v, rf);
@@ -2628,6 +2693,9 @@ extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
 #ifndef ORB_DESC_ICM_REG
 #define ORB_DESC_ICM_REG 1   // IC_Angle disc masks held in 9 VGPRs (0: made per use from umax)
 #endif
+#ifndef ORB_DESC_PATF
+#define ORB_DESC_PATF 0   // 1: pattern points converted to float once per wave
+#endif
 #ifndef ORB_DESC_HDOT4
 #define ORB_DESC_HDOT4 1   // horizontal pass by v_dot4_u32_u8 (0: packed-u16 pairs, round 2)
 #endif
@@ -2645,6 +2713,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     // conservative vmcnt(0) that also drains the patch prefetch
     asm volatile("" ::"v"(patv.x), "v"(patv.y), "v"(patv.z), "v"(patv.w));
     const uint32_t patw[4] = {patv.x, patv.y, patv.z, patv.w};
+#if ORB_DESC_PATF
+    // the lane's 8 pattern points as floats, made once (4 VALU per sample in the loop otherwise)
+    float pfx[8], pfy[8];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+            pfx[2 * q + e] = (float)(int)(int8_t)(patw[q] >> (16 * e));
+            pfy[2 * q + e] = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
+        }
+#endif
     uint8_t* raw = raw_s[wv];
     uint16_t* hb = hb_s[wv];
     // symmetric 7-tap kernel: k0 = k6, k1 = k5, k2 = k4
@@ -2889,8 +2968,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
             int val[2];
 #pragma unroll
             for (int e = 0; e < 2; ++e) {
+#if ORB_DESC_PATF
+                const float x = pfx[2 * q + e], y = pfy[2 * q + e];
+#else
                 const float x = (float)(int)(int8_t)(patw[q] >> (16 * e));
                 const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
+#endif
                 int r, c;
                 brief_offset(x, y, sb, ca, FMA, r, c);
                 // the 7 vertical taps are rows 18+r .. 24+r of column 18+c:

@@ -87,3 +87,24 @@ def test_c5_two_rank_map_shards_equal_one_rank(tmp_path):
     np.testing.assert_array_equal(np.concatenate([p["match"] for p in parts]), one["match"])
     np.testing.assert_array_equal(np.concatenate([p["nm"] for p in parts]), one["nm"])
     assert one["nm"].min() > 100
+
+
+def test_bench_overlap_two_handles_equals_one(tmp_path):
+    """bench.py --overlap 2 (consecutive steps alternate between two extractor
+    handles on two streams, each with its own plan and scratch) gives the
+    last step's keypoints, descriptors and SearchForInitialization matches of
+    the one-handle run."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    common = ["--batch", str(B), "--steps", "3", "--warmup", "1", "--cpu-sample", "0", "--no-host-api"]
+    _run([sys.executable, "bench.py", "--overlap", "2", "--dump", str(tmp_path / "two")] + common, env)
+    _run([sys.executable, "bench.py", "--overlap", "1", "--dump", str(tmp_path / "one")] + common, env)
+    a = np.load(tmp_path / "two" / "rank0.npz")
+    b = np.load(tmp_path / "one" / "rank0.npz")
+    for k in ("n", "mono", "nmatch"):
+        np.testing.assert_array_equal(a[k], b[k])
+    for i in range(B):
+        n = int(b["n"][i])
+        assert np.array_equal(a["kps"][i, :n], b["kps"][i, :n]) and np.array_equal(a["desc"][i, :n], b["desc"][i, :n])
+    for i in range(B - 1):
+        m = int(b["n"][i])
+        assert np.array_equal(a["matches"][i, :m], b["matches"][i, :m])
