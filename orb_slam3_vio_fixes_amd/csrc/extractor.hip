@@ -553,6 +553,8 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
                 P.roi_nd_max = std::max(P.roi_nd_max, ((c.x0 & 3) + c.cols + 3) >> 2);
                 P.win_max = std::max(P.win_max, (std::max(0, c.cols - 6) + 2) * (std::max(0, c.rows - 6) + 2));
                 P.win_pix_max = std::max(P.win_pix_max, std::max(0, c.cols - 6) * std::max(0, c.rows - 6));
+                // k_fast_cells' candidates hold (row, column) in 7 bits each (< 70 px: wCell < 2 * 35)
+                if (c.cols - 6 >= 128 || c.rows - 6 >= 128) return ORB_ERR_UNSUPPORTED;
                 {   // k_fast_cells' pre-test items of this cell: window rows x aligned dword pairs
                     const int ww = std::max(0, c.cols - 6), X0 = (c.x0 & 3) + 3, j0 = X0 >> 2;
                     const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
@@ -1321,9 +1323,10 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c
 }
 
 // Compass pre-test, 4 pixels per lane: a 9-pixel arc of the 16-ring always
-// covers >= 2 of the 4 compass pixels, so a brighter corner at threshold t has
-// the second largest compass pixel > v + t and a darker one the second smallest
-// < v - t.  Pixels failing both at min(iniTh, minTh) are corners at no
+// covers two ring-adjacent compass pixels -- one of {U, D} and one of {L, R} --
+// so a brighter corner at threshold t has min(max(U,D), max(L,R)) > v + t and
+// a darker one max(min(U,D), min(L,R)) < v - t (ORB_FAST_COMPASS_AND; round 2
+// tested the looser 2nd largest / 2nd smallest of the four).  Pixels failing both at min(iniTh, minTh) are corners at no
 // threshold used; their score stays 0, which the NMS treats exactly like a
 // non-corner (s_t(q) = 0).  Bytes are split into u16 pairs (pixels 0/2 and
 // 1/3) and tested with packed u16 min/max; the flags are the signs of packed
@@ -1331,6 +1334,9 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c
 // even and odd columns de-interleaved at landing, no splitting here -- was
 // measured slower: 0.575 vs 0.510 ms, twice the LDS reads per item.)
 
+#ifndef ORB_FAST_COMPASS_AND
+#define ORB_FAST_COMPASS_AND 1   // pre-test: one vertical AND one horizontal compass pixel past the threshold
+#endif
 // Flags as signs: (C + t) - L2 and (S2 + t) - C as packed u16 differences;
 // every value is < 2^10, so the i16 sign bit is exactly the bright / dark test.
 __device__ __forceinline__ void compass_signs(uint32_t c, uint32_t u, uint32_t d, uint32_t l, uint32_t r,
@@ -1339,9 +1345,19 @@ __device__ __forceinline__ void compass_signs(uint32_t c, uint32_t u, uint32_t d
     const u16x2 m1 = __builtin_elementwise_min(U, D), M1 = __builtin_elementwise_max(U, D);
     const u16x2 m2 = __builtin_elementwise_min(L, R), M2 = __builtin_elementwise_max(L, R);
     const u16x2 X = __builtin_elementwise_min(M1, M2), Y = __builtin_elementwise_max(m1, m2);
+#if ORB_FAST_COMPASS_AND
+    // every 9-arc holds two ring-adjacent compass pixels, one of {U, D} and
+    // one of {L, R}: a bright corner has min(max(U,D), max(L,R)) > v + t, a
+    // dark one max(min(U,D), min(L,R)) < v - t -- tighter than the 2nd
+    // largest / 2nd smallest of the four (which also passes U, D alone) and
+    // two packed ops cheaper; a failing direction still has strength - 1 < t
+    bneg = as_u32((C + tt) - X);
+    dneg = as_u32((Y + tt) - C);
+#else
     const u16x2 L2 = __builtin_elementwise_max(X, Y), S2 = __builtin_elementwise_min(X, Y);
     bneg = as_u32((C + tt) - L2);
     dneg = as_u32((S2 + tt) - C);
+#endif
 }
 
 // pairs (pixels 0, 2) and (1, 3) of a dword -> one flag byte per pixel (bit 7), pixel order
@@ -1416,6 +1432,26 @@ __device__ __forceinline__ void xcd_remap(int per, int B, int& unit, int& frame)
 
 // row/column of linear window index i (ww <= 4096): exact via a float reciprocal
 __device__ __forceinline__ int div_row(int i, float inv_ww) { return (int)(((float)i + 0.5f) * inv_ww); }
+
+#ifndef ORB_FAST_RC
+#define ORB_FAST_RC 1   // candidate entries hold (row, column) as 7-bit fields (0: the window's linear index)
+#endif
+// A candidate's 14-bit window position: row | column << 7 (windows are < 70
+// px a side: wCell = ceil(width / floor(width / 35)) < 70; the plan checks
+// < 128), so it decodes in two ops instead of a float-reciprocal division
+constexpr int kCandColStep = ORB_FAST_RC ? 128 : 1;
+__device__ __forceinline__ int cand_enc(int r, int c, int ww) {
+    return ORB_FAST_RC ? (r | (c << 7)) : (int)__umul24((uint32_t)r, (uint32_t)ww) + c;
+}
+__device__ __forceinline__ void cand_dec(int i, float inv_ww, int ww, int& r, int& c) {
+    if (ORB_FAST_RC) {
+        r = i & 127;
+        c = i >> 7;
+    } else {
+        r = div_row(i, inv_ww);
+        c = i - (int)__umul24((uint32_t)r, (uint32_t)ww);
+    }
+}
 
 #ifndef ORB_FAST_CELLS_PER_WAVE
 #define ORB_FAST_CELLS_PER_WAVE 4
@@ -1632,7 +1668,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     bh = sign_bytes(b2, b3) & vh;
                     dl = sign_bytes(k0, k1) & vl;
                     dh = sign_bytes(k2, k3) & vh;
-                    idx0 = (int)__umul24(r, ww) + 4 * j - X0;
+                    idx0 = cand_enc(r, 4 * j - X0, ww);
                 }
             };
 #if ORB_FAST_PIPE
@@ -1689,13 +1725,13 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     const int bb = __builtin_ctz(pl);
                     pl &= pl - 1;
                     const uint32_t fl = (((bl >> bb) & 1u) << 14) | (((dl >> bb) & 1u) << 15);
-                    cand[pos++] = (uint16_t)((uint32_t)(idx0 + (bb >> 3)) | fl);
+                    cand[pos++] = (uint16_t)((uint32_t)(idx0 + kCandColStep * (bb >> 3)) | fl);
                 }
                 while (ph) {
                     const int bb = __builtin_ctz(ph);
                     ph &= ph - 1;
                     const uint32_t fl = (((bh >> bb) & 1u) << 14) | (((dh >> bb) & 1u) << 15);
-                    cand[pos++] = (uint16_t)((uint32_t)(idx0 + 4 + (bb >> 3)) | fl);
+                    cand[pos++] = (uint16_t)((uint32_t)(idx0 + kCandColStep * (4 + (bb >> 3))) | fl);
                 }
                 ncand += tot;
             };
@@ -1744,11 +1780,12 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     const int itm = (int)(e & 0xffffu);
                     const int r = div_row(itm, inv_ndp);
                     const int k = itm - (int)mad24((uint32_t)r, (uint32_t)ndp, 0u);
-                    const int idx0 = (int)mad24((uint32_t)r, (uint32_t)ww, (uint32_t)(4 * (j0 + 2 * k) - X0));
+                    const int idx0 = cand_enc(r, 4 * (j0 + 2 * k) - X0, ww);
                     while (m) {
                         const int bb = __builtin_ctz(m);
                         m &= m - 1;
-                        cand[pos++] = (uint16_t)((uint32_t)(idx0 + bb) | (((mb >> bb) & 1u) << 14) | (((md >> bb) & 1u) << 15));
+                        cand[pos++] = (uint16_t)((uint32_t)(idx0 + kCandColStep * bb) | (((mb >> bb) & 1u) << 14) |
+                                                 (((md >> bb) & 1u) << 15));
                     }
                 }
                 ncand += tot;
@@ -1778,7 +1815,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             //    pixels passing both pre-tests)
             for (int q = lane; q < ncand; q += kWave) {
                 const int e = cand[q], i = e & kCandIdx;
-                const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                int r, cc;
+                cand_dec(i, inv_ww, ww, r, cc);
 #if ORB_FAST_ABL == 1
                 int sv = (e * 37) & 63;   // ablation: no ring reads / arc scores (timing only)
 #else
@@ -1807,7 +1845,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #if ORB_FAST_FUSED_OUT
                 uint32_t key = 0;
                 if (q < ncand) {
-                    const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                    int r, cc;
+                    cand_dec(cand[q] & kCandIdx, inv_ww, ww, r, cc);
                     int sv;
                     keep = nms_keep(sc, sp, r, cc, t, sv);
                     // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
@@ -1821,9 +1860,9 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 }
 #else
                 if (q < ncand) {
-                    const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
-                    int sv;
-                    keep = nms_keep(sc, sp, r, i - (int)__umul24(r, ww), t, sv);
+                    int r, cc, sv;
+                    cand_dec(cand[q] & kCandIdx, inv_ww, ww, r, cc);
+                    keep = nms_keep(sc, sp, r, cc, t, sv);
                 }
                 const uint64_t m = __ballot(keep);
                 if (lane == 0) kmask[k] = m;
@@ -1848,8 +1887,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 if (keep) {
                     const int pos = written + mask_rank(m);
                     if (pos < cur.cap) {
-                        const int i = cand[k * kWave + lane] & kCandIdx;
-                        const int r = div_row(i, inv_ww), cc = i - (int)__umul24(r, ww);
+                        int r, cc;
+                        cand_dec(cand[k * kWave + lane] & kCandIdx, inv_ww, ww, r, cc);
                         // key coordinates relative to minBorder (ORBextractor.cc:865-866 add j*wCell, i*hCell)
                         const uint32_t x = (uint32_t)(cur.x0 + cc + 3 - (kEdge - 3));
                         const uint32_t y = (uint32_t)(cur.y0 + r + 3 - (kEdge - 3));
@@ -1866,8 +1905,9 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         // entry either pass wrote (a pixel passing the pre-test at iniTh
         // passes it at minThFAST < iniThFAST)
         for (int q = lane; q < ncand; q += kWave) {
-            const int i = cand[q] & kCandIdx, r = div_row(i, inv_ww);
-            sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(i - (int)__umul24(r, ww) + 1))] = 0;
+            int r, cc;
+            cand_dec(cand[q] & kCandIdx, inv_ww, ww, r, cc);
+            sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(cc + 1))] = 0;
         }
 #endif
         fast_wave_sync();
