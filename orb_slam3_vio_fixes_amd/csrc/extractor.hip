@@ -1463,6 +1463,15 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #ifndef ORB_FAST_EMIT
 #define ORB_FAST_EMIT 1   // 1: items list + one expansion pass; 0: per-round bit loops (round 2)
 #endif
+#ifndef ORB_FAST_KEEPLIST
+#define ORB_FAST_KEEPLIST 1   // the NMS list keeps only candidates scoring >= max(t, 1)
+#endif
+#if ORB_FAST_RESET && ORB_FAST_KEEPLIST
+#error "ORB_FAST_RESET needs every scored candidate in the list (ORB_FAST_KEEPLIST=0)"
+#endif
+#ifndef ORB_FAST_DIAG
+#define ORB_FAST_DIAG 1   // diagonal-pair filter on the candidate list before scoring
+#endif
 #ifndef ORB_FAST_FUSED_OUT
 #define ORB_FAST_FUSED_OUT 1   // survivors written inside the NMS loop (0: a separate output pass)
 #endif
@@ -1811,8 +1820,74 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #endif
             fast_wave_sync();
             if (pass == 0) FAST_T(1); else FAST_T(5);
+#if ORB_FAST_DIAG
+            // 1c. a second necessary condition, on the candidates only: a 9-arc
+            //     also holds two ring-adjacent diagonal pixels (ring positions
+            //     2, 6, 10, 14: one of each opposite pair), so a direction
+            //     survives only if min(max(x2,x10), max(x6,x14)) > v + t
+            //     (bright) / max(min(x2,x10), min(x6,x14)) < v - t (dark).  A
+            //     dropped direction has strength - 1 < t: its score acts as 0
+            //     at t, like a pixel the compass test dropped.  The list is
+            //     compacted in place, in order (~40 % of the candidates go)
+            {
+                int n2 = 0;
+                for (int q0 = 0; q0 < ncand; q0 += kWave) {
+                    const int q = q0 + lane;
+                    uint32_t e2 = 0;
+                    bool keep = false;
+                    if (q < ncand) {
+                        const int e = cand[q];
+                        int r, cc;
+                        cand_dec(e & kCandIdx, inv_ww, ww, r, cc);
+                        const uint8_t* p = R + mad24((uint32_t)(r + 3), (uint32_t)rstride, (uint32_t)(cc + 3));
+                        const int v = p[0];
+                        const int x2 = p[2 * rstride + 2], x6 = p[-2 * rstride + 2];
+                        const int x10 = p[-2 * rstride - 2], x14 = p[2 * rstride - 2];
+                        const bool bo = (e & kCandBright) && min(max(x2, x10), max(x6, x14)) > v + t;
+                        const bool dk = (e & kCandDark) && max(min(x2, x10), min(x6, x14)) < v - t;
+                        keep = bo || dk;
+                        e2 = (uint32_t)(e & kCandIdx) | (bo ? (uint32_t)kCandBright : 0u) | (dk ? (uint32_t)kCandDark : 0u);
+                    }
+                    const uint64_t m = __ballot(keep);
+                    if (keep) cand[n2 + mask_rank(m)] = (uint16_t)e2;
+                    n2 += __popcll(m);
+                }
+                ncand = n2;
+                fast_wave_sync();
+            }
+#endif
             // 2. FAST score of the candidates (the dark direction too for the rare
-            //    pixels passing both pre-tests)
+            //    pixels passing both pre-tests).  ORB_FAST_KEEPLIST: the list
+            //    keeps only scores >= max(t, 1) -- the NMS at t keeps nothing
+            //    else, and the map holds every score for the neighbour reads --
+            //    compacted in place, in order (~1/3 of the candidates remain)
+#if ORB_FAST_KEEPLIST
+            {
+                const int tk = max(t, 1);
+                int n3 = 0;
+                for (int q0 = 0; q0 < ncand; q0 += kWave) {
+                    const int q = q0 + lane;
+                    bool keep = false;
+                    int e = 0;
+                    if (q < ncand) {
+                        e = cand[q];
+                        int r, cc;
+                        cand_dec(e & kCandIdx, inv_ww, ww, r, cc);
+                        int v, x[16];
+                        fast_ring(R, rstride, r + 3, cc + 3, v, x);
+                        int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
+                        if ((e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
+                        sv = max(sv, 0);
+                        sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(cc + 1))] = (uint8_t)sv;
+                        keep = sv >= tk;
+                    }
+                    const uint64_t m = __ballot(keep);
+                    if (keep) cand[n3 + mask_rank(m)] = (uint16_t)e;
+                    n3 += __popcll(m);
+                }
+                ncand = n3;
+            }
+#else
             for (int q = lane; q < ncand; q += kWave) {
                 const int e = cand[q], i = e & kCandIdx;
                 int r, cc;
@@ -1827,6 +1902,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #endif
                 sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(cc + 1))] = (uint8_t)max(sv, 0);
             }
+#endif
             fast_wave_sync();
             if (pass == 0) FAST_T(2); else FAST_T(6);
             // 3. NMS at this pass's threshold.  ORB_FAST_FUSED_OUT: the
