@@ -1277,8 +1277,12 @@ __device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
     return d;
 }
 
+// RP > 0: the ROI pitch is the compile-time RP dwords (every ring read an
+// immediate offset from one base); 0: the runtime stride
+template <int RP>
 __device__ __forceinline__ void fast_ring(const uint8_t* roi, int stride, int r, int c, int& v, int (&x)[16]) {
-    const uint8_t* p = roi + mad24((uint32_t)r, (uint32_t)stride, (uint32_t)c);
+    if (RP) stride = 4 * RP;
+    const uint8_t* p = roi + (RP ? r * (4 * RP) + c : (int)mad24((uint32_t)r, (uint32_t)stride, (uint32_t)c));
     v = p[0];
     x[0] = p[3 * stride];
     x[1] = p[3 * stride + 1];
@@ -1463,6 +1467,9 @@ constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
 #ifndef ORB_FAST_EMIT
 #define ORB_FAST_EMIT 1   // 1: items list + one expansion pass; 0: per-round bit loops (round 2)
 #endif
+#ifndef ORB_FAST_FIXED_PITCH
+#define ORB_FAST_FIXED_PITCH 1   // ROIs of <= 13 dwords land at a compile-time LDS pitch (11 or 13)
+#endif
 #ifndef ORB_FAST_KEEPLIST
 #define ORB_FAST_KEEPLIST 1   // the NMS list keeps only candidates scoring >= max(t, 1)
 #endif
@@ -1524,14 +1531,15 @@ __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV])
     }
 }
 
-template <int PDW, int NV>
+template <int PDW, int NV, int RP>
 __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)[NV], uint32_t* roi) {
     const int lane = lane_id();
     const uint32_t d = (uint32_t)min(lane % PDW, rf.nd - 1);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const uint32_t r = (uint32_t)min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
-        roi[mad24(r, (uint32_t)rf.nd, d)] = v[j];
+        if (RP) roi[r * RP + d] = v[j];
+        else roi[mad24(r, (uint32_t)rf.nd, d)] = v[j];
     }
 }
 
@@ -1540,7 +1548,10 @@ __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)
 #else
 #define FAST_WPE_ATTR
 #endif
-template <int PDW, int NV>
+// RP: the LDS pitch of a landed ROI in dwords, fixed at compile time (every
+// row offset of the pre-test, the ring and the diagonal reads an immediate),
+// or 0 for each cell's own nd
+template <int PDW, int NV, int RP>
 __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
@@ -1596,11 +1607,11 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t5 = 0, t6 = 0, t7 = 0, t9 = 0, t10 = 0;
     unsigned long long tlast = t_start;
 #endif
-    auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) { roi_land<PDW, NV>(r, vv, (uint32_t*)roi); };
+    auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) { roi_land<PDW, NV, RP>(r, vv, (uint32_t*)roi); };
     // one cell from its landed ROI
     auto process = [&](const CellDev& cur, const RoiFetch& rfc, int it) {
         const int f = bframe;
-        const int rstride = rfc.nd * 4;
+        const int rstride = (RP ? RP : rfc.nd) * 4;
         const int shift = cur.x0 & 3;
         const uint8_t* R = roi + shift;
         const int ww = max(0, cur.cols - 6), wh = max(0, cur.rows - 6);
@@ -1839,7 +1850,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                         const int e = cand[q];
                         int r, cc;
                         cand_dec(e & kCandIdx, inv_ww, ww, r, cc);
-                        const uint8_t* p = R + mad24((uint32_t)(r + 3), (uint32_t)rstride, (uint32_t)(cc + 3));
+                        const uint8_t* p = R + (RP ? (r + 3) * rstride + cc + 3
+                                                   : (int)mad24((uint32_t)(r + 3), (uint32_t)rstride, (uint32_t)(cc + 3)));
                         const int v = p[0];
                         const int x2 = p[2 * rstride + 2], x6 = p[-2 * rstride + 2];
                         const int x10 = p[-2 * rstride - 2], x14 = p[2 * rstride - 2];
@@ -1874,7 +1886,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                         int r, cc;
                         cand_dec(e & kCandIdx, inv_ww, ww, r, cc);
                         int v, x[16];
-                        fast_ring(R, rstride, r + 3, cc + 3, v, x);
+                        fast_ring<RP>(R, rstride, r + 3, cc + 3, v, x);
                         int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
                         if ((e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
                         sv = max(sv, 0);
@@ -1896,7 +1908,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 int sv = (e * 37) & 63;   // ablation: no ring reads / arc scores (timing only)
 #else
                 int v, x[16];
-                fast_ring(R, rstride, r + 3, cc + 3, v, x);
+                fast_ring<RP>(R, rstride, r + 3, cc + 3, v, x);
                 int sv = fast_dir_score(x, v, (e & kCandBright) ? 0 : 1);
                 if ((e & kCandBright) && (e & kCandDark)) sv = max(sv, fast_dir_score(x, v, 1));
 #endif
@@ -3808,13 +3820,19 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     // 76 always fit <32, 40>)
     void (*kfast)(FastArgs);
     const int ndm = P.roi_nd_max, rm = P.roi_rows_max;
-    if (ndm <= 16 && rm <= 48) kfast = k_fast_cells<16, 12>;
-    else if (ndm <= 16 && rm <= 64) kfast = k_fast_cells<16, 16>;
-    else if (ndm <= 16 && rm <= 80) kfast = k_fast_cells<16, 20>;
-    else if (ndm <= 32 && rm <= 48) kfast = k_fast_cells<32, 24>;
-    else if (ndm <= 32 && rm <= 80) kfast = k_fast_cells<32, 40>;
+    int rp = 0;    // fixed LDS pitch of the ROIs (dwords), 0: per cell
+#if ORB_FAST_FIXED_PITCH
+    if (ndm <= 11 && rm <= 64) { kfast = rm <= 48 ? k_fast_cells<16, 12, 11> : k_fast_cells<16, 16, 11>; rp = 11; }
+    else if (ndm <= 13 && rm <= 64) { kfast = rm <= 48 ? k_fast_cells<16, 12, 13> : k_fast_cells<16, 16, 13>; rp = 13; }
+    else
+#endif
+    if (ndm <= 16 && rm <= 48) kfast = k_fast_cells<16, 12, 0>;
+    else if (ndm <= 16 && rm <= 64) kfast = k_fast_cells<16, 16, 0>;
+    else if (ndm <= 16 && rm <= 80) kfast = k_fast_cells<16, 20, 0>;
+    else if (ndm <= 32 && rm <= 48) kfast = k_fast_cells<32, 24, 0>;
+    else if (ndm <= 32 && rm <= 80) kfast = k_fast_cells<32, 40, 0>;
     else return ORB_ERR_UNSUPPORTED;
-    fa.roi_max = (P0.roi_max + 15) & ~15;
+    fa.roi_max = (std::max(P0.roi_max, 4 * rm * rp + 16) + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
     fa.kmask_bytes = ((P0.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
     fa.cand_bytes = (2 * P0.win_pix_max + 15) & ~15;
