@@ -1619,7 +1619,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #if ORB_FAST_RESET
         (void)npad;   // the map is all zero here: zeroed once, and each cell resets the entries it wrote
 #else
-        for (int i = lane; i < (npad + 3) / 4; i += kWave) ((uint32_t*)sc)[i] = 0u;
+        // 16 bytes per lane per store (sc is 16-byte aligned, win_max a multiple of 16)
+        for (int i = lane; i < (npad + 15) / 16; i += kWave) ((uint4*)sc)[i] = make_uint4(0u, 0u, 0u, 0u);
         fast_wave_sync();
 #endif
         if (it == it0) FAST_T(10); else FAST_T(0);
@@ -1653,12 +1654,12 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             const u16x2 tt = {(unsigned short)t, (unsigned short)t};
             ncand = 0;
             // one item: flag bytes (byte k = item pixel k) and its window index
-            auto pretest = [&](int it, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh, int& idx0) {
+            // item (row r, dword pair k) -> flag bytes; ok: the item exists
+            auto pretest_rk = [&](bool ok, int r, int k, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh,
+                                  int& idx0) {
                 bl = bh = dl = dh = 0;
                 idx0 = 0;
-                if (it < nitems) {
-                    const int r = div_row(it, inv_ndp);
-                    const int k = it - (int)__umul24(r, ndp);
+                if (ok) {
                     const int j = j0 + 2 * k;
                     const uint32_t* row = roi32 + __umul24(r + 3, rs4) + j;
                     const uint32_t cm = row[-1], c0 = row[0], c1 = row[1], c2 = row[2];
@@ -1690,6 +1691,10 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     dh = sign_bytes(k2, k3) & vh;
                     idx0 = cand_enc(r, 4 * j - X0, ww);
                 }
+            };
+            auto pretest = [&](int it, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh, int& idx0) {
+                const int r = div_row(it, inv_ndp);
+                pretest_rk(it < nitems, r, it - (int)__umul24(r, ndp), bl, bh, dl, dh, idx0);
             };
 #if ORB_FAST_PIPE
             // the same pre-test split at its LDS reads, so the reads of round
