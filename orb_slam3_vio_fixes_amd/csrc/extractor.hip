@@ -2835,11 +2835,56 @@ extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
 #ifndef ORB_Q_UNROLL
 #define ORB_Q_UNROLL 1
 #endif
+#ifndef ORB_DESC_HMFMA
+#define ORB_DESC_HMFMA 1   // horizontal pass on the matrix cores (v_mfma_i32_16x16x64_i8); 0: v_dot4 per row
+#endif
+// The horizontal pass as a product on the matrix cores: H[r][x] = sum_t w_t
+// raw[r][x + t] is (the raw patch, its rows realigned by the column shift sh)
+// x (a 64 x 37 banded matrix, w_t at row x + t of column x).
+// v_mfma_i32_16x16x64_i8 takes i8 operands, so the pixels go in as p ^ 0x80 =
+// p - 128 and every output starts from 128 * sum(w) (all 7 taps of an output
+// lie inside the row); the taps are < 128 (checked on the host).  Integer and
+// exact: H is the ufixedpoint16 sum of the dot4 form.  M = 43 rows as the
+// 16-row blocks at rows 0, 16, 28 (the last overlaps: rows 28..31 are written
+// twice with equal values, row 43 lands in the column pad), N = 37 outputs as
+// the 16-column blocks at 0, 16, 22 (likewise), K = 64 (bytes 43.. meet zero
+// weights), so every lane's store is in bounds and unpredicated.  Operand maps
+// (as the 32x32x32 form, tools/mfma_i8_probe.hip): lane l feeds A row (l & 15)
+// and B column (l & 15) with the 16-byte k-slice 16 (l >> 4); result rows
+// 4 (l >> 4) + i, column l & 15.  The band is 12 VGPRs made once per wave.
+constexpr int kHmNb = 3;
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ int hm_row0(int mb) { return mb == 0 ? 0 : (mb == 1 ? 16 : 28); }
+__device__ __forceinline__ int hm_col0(int nb) { return nb == 0 ? 0 : (nb == 1 ? 16 : 22); }
 template <bool FMA>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WAVES))) void k_describe(DescArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
     __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][(kBl + 1) * kHbT];
     const int lane = lane_id(), wv = wave_id();
+#if ORB_DESC_HMFMA
+    // lane's 16 band bytes: byte e = w[16 (l >> 4) + e - n], i.e. the 7 taps as
+    // a 56-bit little-endian word T shifted by d = 16 (l >> 4) - n bytes
+    v4i_t Bm[kHmNb];
+    {
+        uint64_t T = 0;
+#pragma unroll
+        for (int q = 0; q < 7; ++q) T |= (uint64_t)((uint32_t)a.kern[q] & 0xffu) << (8 * q);
+#pragma unroll
+        for (int nb = 0; nb < kHmNb; ++nb) {
+            const int d = 16 * (lane >> 4) - (hm_col0(nb) + (lane & 15));
+            uint64_t lo = 0, hi = 0;
+            if (d >= 0) {
+                if (d < 7) lo = T >> (8 * d);
+            } else {
+                const int s = -8 * d;
+                if (s < 64) { lo = T << s; hi = T >> (64 - s); }
+                else if (s < 128) hi = T << (s - 64);
+            }
+            Bm[nb] = v4i_t{(int)(uint32_t)lo, (int)(uint32_t)(lo >> 32), (int)(uint32_t)hi, (int)(uint32_t)(hi >> 32)};
+        }
+    }
+    const int hbias = 128 * (a.kern[0] + a.kern[1] + a.kern[2] + a.kern[3] + a.kern[4] + a.kern[5] + a.kern[6]);
+#endif
     // lane's 4 tests = 16 consecutive pattern bytes, kept packed in registers
     const uint4 patv = ((const uint4*)c_pattern)[lane];
     // wait for the pattern here: a use inside the keypoint loop would get a
@@ -3062,7 +3107,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                     hb[(2 * (mlo + m) + 1) * kHbT + rr] = h.y;
                 }
             };
-#if ORB_DESC_HDOT4
+#if ORB_DESC_HMFMA
+            (void)half;
+            {
+                const v4i_t bias = {hbias, hbias, hbias, hbias};
+                // slice 3 (k >= 48) meets zero weights: it takes slice 2's bytes
+                const int ks = 16 * min(lane >> 4, 2);
+                const uint32_t shb = (uint32_t)sh;
+#pragma unroll
+                for (int mb = 0; mb < 3; ++mb) {
+                    // the slice's 16 bytes from byte ks + sh of the row: one
+                    // 16-byte read, the next dword (slice 2: bytes 48.. meet zero
+                    // weights, so its own last dword) and 4 v_alignbyte
+                    const int row = min(hm_row0(mb) + (lane & 15), kRaw - 1);
+                    const uint8_t* rp = raw + row * kRawP + ks;
+                    const uint4 q = *(const uint4*)rp;
+                    const uint32_t q4 = *(const uint32_t*)(rp + (ks < 32 ? 16 : 12));
+                    const v4i_t A = {(int)(__builtin_amdgcn_alignbyte(q.y, q.x, shb) ^ 0x80808080u),
+                                     (int)(__builtin_amdgcn_alignbyte(q.z, q.y, shb) ^ 0x80808080u),
+                                     (int)(__builtin_amdgcn_alignbyte(q.w, q.z, shb) ^ 0x80808080u),
+                                     (int)(__builtin_amdgcn_alignbyte(q4, q.w, shb) ^ 0x80808080u)};
+                    const int r0 = hm_row0(mb) + 4 * (lane >> 4);
+#pragma unroll
+                    for (int nb = 0; nb < kHmNb; ++nb) {
+                        const v4i_t acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bm[nb], bias, 0, 0, 0);
+                        // rows r0..r0+3 of column x as u16
+                        const int x = hm_col0(nb) + (lane & 15);
+                        *(uint2*)(hb + x * kHbT + r0) =
+                            make_uint2(__builtin_amdgcn_perm((uint32_t)acc[1], (uint32_t)acc[0], 0x05040100u),
+                                       __builtin_amdgcn_perm((uint32_t)acc[3], (uint32_t)acc[2], 0x05040100u));
+                    }
+                }
+            }
+#elif ORB_DESC_HDOT4
             // output x = 4 j + b takes raw columns x .. x + 6: bytes b.. of
             // al[j], al[j + 1] and (b >= 2) al[j + 2], one v_dot4_u32_u8 per
             // word with the 7 weights placed at the matching bytes (every sum
@@ -3772,6 +3849,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     // pyramid, so it runs on a side stream beside FAST and the quadtree
     int kern[7];
     {
+        // every tap < 128: k_describe's matrix-core horizontal pass takes them as i8
         static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
         for (int t = 0; t < 7; ++t) kern[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
     }

@@ -464,15 +464,21 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
     }
 }
 
-// one wave per pair: the serial pass.  STAGED: the queries' top-K lists are
-// copied into LDS first (32 B per F1 keypoint); otherwise (frames of more
-// than ~2,900 keypoints, e.g. the 5 x nFeatures initialization extractor of
-// Tracking.cc:601) each query reads its list from global memory, one query
-// ahead of its use (the lists do not depend on the serial state).
+// One block per pair: the serial pass runs on wave 0; the four waves stage
+// everything it reads into LDS first (the pair's level-0 list, both frames'
+// angles, the query list and counts, the queries' top-K lists) and finish the
+// orientation filter and the outputs after it, so no loop waits on one global
+// load per iteration.  The matches live in LDS until the end.  STAGED: the
+// queries' top-K lists are copied into LDS (32 B per F1 keypoint); otherwise
+// (frames of more than ~2,700 keypoints, e.g. the 5 x nFeatures
+// initialization extractor of Tracking.cc:601) each query reads its list from
+// global memory, one query ahead of its use (the lists do not depend on the
+// serial state).
+constexpr int kSfiThreads = 256;
 template <bool STAGED>
-__global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
+__global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
-    const int pr = blockIdx.x, lane = lane_id();
+    const int pr = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
     const int n1 = min(a.n[f1], a.cap), n2 = min(a.n[f2], a.cap);
     const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
@@ -482,119 +488,164 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
     int* list = lds;                          // cap
     int* mdist = list + a.cap;                // cap
     int* m21 = mdist + a.cap;                 // cap
-    int* hist = m21 + a.cap;                  // 32
+    int* hist = m21 + a.cap;                  // 32 (hist[31]: the filter's drop count)
     int* qlist = hist + 32;                   // cap: query indices i1 (level 0, >= 1 candidate)
-    int* qcnt = qlist + a.cap;                // cap: candidate counts
-    uint32_t* qtop = (uint32_t*)(qcnt + a.cap);   // STAGED: cap * kTopK
-    int8_t* bin1 = (int8_t*)(qtop + (STAGED ? (size_t)a.cap * kTopK : 0));   // cap
-    int32_t* m12 = a.matches + (long long)pr * a.cap;
-    const int nl = level0_list(a, f2, list, lane, kWave);
-    for (int i = lane; i < n2; i += kWave) { mdist[i] = INT_MAX; m21[i] = -1; }
-    for (int i = lane; i < 32; i += kWave) hist[i] = 0;
-    for (int i = lane; i < n1; i += kWave) { m12[i] = -1; bin1[i] = -1; }
+    int* qcnt = qlist + a.cap;                // cap: candidate counts (first: every F1 keypoint's)
+    int* m12 = qcnt + a.cap;                  // cap
+    uint32_t* qtop = (uint32_t*)(m12 + a.cap);   // STAGED: cap * kTopK
+    float* ang1 = (float*)(qtop + (STAGED ? (size_t)a.cap * kTopK : 0));   // cap
+    float* ang2 = ang1 + a.cap;                                             // cap
+    int8_t* bin1 = (int8_t*)(ang2 + a.cap);                                 // cap
+    int32_t* m12g = a.matches + (long long)pr * a.cap;
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
     const int* ncand = a.ncand + (long long)pr * a.cap;
-    // compact the queries in F1 order and stage their top-K lists in LDS
-    int nq = 0;
-    for (int base = 0; base < n1; base += kWave) {
-        const int i = base + lane;
-        const int c = i < n1 ? ncand[i] : -1;
-        const uint64_t m = __ballot(c > 0);
-        if (c > 0) { qlist[nq + mask_rank(m)] = i; qcnt[nq + mask_rank(m)] = c; }
-        nq += __popcll(m);
+    const int nl = level0_list(a, f2, list, tid, kSfiThreads);
+    for (int i = tid; i < n1; i += kSfiThreads) {
+        qcnt[i] = ncand[i];
+        m12[i] = -1;
+        bin1[i] = -1;
+        if (a.check_ori) ang1[i] = K1[i].angle;
+    }
+    for (int i = tid; i < n2; i += kSfiThreads) {
+        mdist[i] = INT_MAX;
+        m21[i] = -1;
+        if (a.check_ori) ang2[i] = K2[i].angle;
+    }
+    if (tid < 32) hist[tid] = 0;
+    __syncthreads();
+    // compact the queries in F1 order (wave 0, in place: a round reads its 64
+    // counts before it writes, and writes only below its own reads)
+    __shared__ int s_nq;
+    if (tid < kWave) {
+        int nq = 0;
+        for (int base = 0; base < n1; base += kWave) {
+            const int i = base + lane;
+            const int c = i < n1 ? qcnt[i] : -1;
+            const uint64_t m = __ballot(c > 0);
+            if (c > 0) { qlist[nq + mask_rank(m)] = i; qcnt[nq + mask_rank(m)] = c; }
+            nq += __popcll(m);
+        }
+        if (lane == 0) s_nq = nq;
     }
     __syncthreads();
+    const int nq = s_nq;
     if (STAGED)
-        for (int e = lane; e < nq * kTopK; e += kWave) qtop[e] = topk[(long long)qlist[e / kTopK] * kTopK + e % kTopK];
+        for (int q = tid; q < nq; q += kSfiThreads) {
+            const uint4* src = (const uint4*)(topk + (long long)qlist[q] * kTopK);
+            uint32_t* dst = qtop + (long long)q * kTopK;   // 4-byte aligned only
+            const uint4 t0 = src[0], t1 = src[1];
+            dst[0] = t0.x; dst[1] = t0.y; dst[2] = t0.z; dst[3] = t0.w;
+            dst[4] = t1.x; dst[5] = t1.y; dst[6] = t1.z; dst[7] = t1.w;
+        }
     __syncthreads();
-    int nm = 0;
-    const float r = a.window;
-    uint32_t next_key = kNoKey;
-    if (!STAGED && nq > 0 && lane < kTopK) next_key = topk[(long long)qlist[0] * kTopK + lane];
-    for (int j = 0; j < nq; ++j) {
-        const int i1 = qlist[j];
-        const int cur_cnt = qcnt[j];
-        uint32_t cur_key;
-        if (STAGED) {
-            cur_key = lane < kTopK ? qtop[j * kTopK + lane] : kNoKey;
-        } else {
-            cur_key = next_key;
-            if (j + 1 < nq && lane < kTopK) next_key = topk[(long long)qlist[j + 1] * kTopK + lane];
-        }
-        int best = INT_MAX, best2 = INT_MAX, bi = -1;
-        bool ok = false;
-        {
-            const bool have = lane < kTopK && cur_key != kNoKey;
-            const int d = (int)(cur_key >> 16);
-            const int fi = have ? (list[cur_key & 0xffff] & 0xffff) : 0;
-            const bool live = have && !(mdist[fi] <= d);
-            uint64_t m = __ballot(live);
-            const int nlive = __popcll(m);
-            if (nlive >= 2 || cur_cnt <= kTopK) {
-                ok = true;
-                if (nlive >= 1) {
-                    const int l0 = __ffsll((long long)m) - 1;
-                    best = __shfl(d, l0, kWave);
-                    bi = __shfl(fi, l0, kWave);
-                    m &= m - 1;
-                    if (m) best2 = __shfl(d, __ffsll((long long)m) - 1, kWave);
+    if (tid < kWave) {
+        int nm = 0, hreg = 0;   // lane b: the rotation histogram's bin b
+        const float r = a.window;
+        // everything of query j + 1 that does not depend on the serial state
+        // (its index, count, top-K keys and their F2 features) is read during
+        // query j, so a step waits on one LDS round trip (mdist) instead of four
+        uint32_t next_key = kNoKey;
+        int next_i1 = 0, next_cnt = 0, next_fi = 0;
+        auto peek = [&](int j) {
+            next_i1 = qlist[j];
+            next_cnt = qcnt[j];
+            if (STAGED) next_key = lane < kTopK ? qtop[j * kTopK + lane] : kNoKey;
+            else next_key = lane < kTopK ? topk[(long long)next_i1 * kTopK + lane] : kNoKey;
+            // (the direct form's keys are global loads: their features are read at use)
+            if (STAGED) next_fi = next_key != kNoKey ? (list[next_key & 0xffff] & 0xffff) : 0;
+        };
+        if (nq > 0) peek(0);
+        for (int j = 0; j < nq; ++j) {
+            const int i1 = next_i1;
+            const int cur_cnt = next_cnt;
+            const uint32_t cur_key = next_key;
+            const int cur_fi = next_fi;
+            if (j + 1 < nq) peek(j + 1);
+            int best = INT_MAX, best2 = INT_MAX, bi = -1;
+            bool ok = false;
+            {
+                const bool have = lane < kTopK && cur_key != kNoKey;
+                const int d = (int)(cur_key >> 16);
+                const int fi = STAGED ? cur_fi : (have ? (list[cur_key & 0xffff] & 0xffff) : 0);
+                const bool live = have && !(mdist[fi] <= d);
+                uint64_t m = __ballot(live);
+                const int nlive = __popcll(m);
+                if (nlive >= 2 || cur_cnt <= kTopK) {
+                    ok = true;
+                    if (nlive >= 1) {
+                        // the ballot is uniform: readlane, not an LDS-routed shuffle
+                        const int l0 = __ffsll((long long)m) - 1;
+                        best = __builtin_amdgcn_readlane(d, l0);
+                        bi = __builtin_amdgcn_readlane(fi, l0);
+                        m &= m - 1;
+                        if (m) best2 = __builtin_amdgcn_readlane(d, __ffsll((long long)m) - 1);
+                    }
                 }
             }
-        }
-        if (!ok) {   // exact fallback: full candidate scan under the current state
-            const orb_keypoint k1 = K1[i1];
-            float px, py;
-            query_pos(a, pr, i1, k1, px, py);
-            CellRange cr;
-            cell_range(px, py, r, a.g, cr);
-            const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32);
-            const uint4 q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
-            Best2 st{INT_MAX, INT_MAX, -1, 0, 0};
-            for (int base = 0; base < nl; base += kWave) {
-                const int jj = base + lane;
-                int d = INT_MAX, fi = -1;
-                if (jj < nl) {
-                    d = cand_dist(list, jj, cr, px, py, r, K2, D2, q0, q1);
-                    fi = list[jj] & 0xffff;
-                    if (d != INT_MAX && mdist[fi] <= d) d = INT_MAX;
+            if (!ok) {   // exact fallback: full candidate scan under the current state
+                const orb_keypoint k1 = K1[i1];
+                float px, py;
+                query_pos(a, pr, i1, k1, px, py);
+                CellRange cr;
+                cell_range(px, py, r, a.g, cr);
+                const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32);
+                const uint4 q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+                Best2 st{INT_MAX, INT_MAX, -1, 0, 0};
+                for (int base = 0; base < nl; base += kWave) {
+                    const int jj = base + lane;
+                    int d = INT_MAX, fi = -1;
+                    if (jj < nl) {
+                        d = cand_dist(list, jj, cr, px, py, r, K2, D2, q0, q1);
+                        fi = list[jj] & 0xffff;
+                        if (d != INT_MAX && mdist[fi] <= d) d = INT_MAX;
+                    }
+                    merge_chunk(st, d, fi, 0);
                 }
-                merge_chunk(st, d, fi, 0);
+                best = st.best; best2 = st.best2; bi = st.idx;
             }
-            best = st.best; best2 = st.best2; bi = st.idx;
+            if (best <= kThLow && (float)best < (float)best2 * a.ratio) {
+                const int prev = m21[bi];
+                const int bn = a.check_ori ? rot_bin(ang1[i1], ang2[bi]) : 0;
+                if (prev >= 0) --nm;
+                if (lane == 0) {
+                    if (prev >= 0) m12[prev] = -1;
+                    m12[i1] = bi;
+                    m21[bi] = i1;
+                    mdist[bi] = best;
+                    if (a.check_ori) bin1[i1] = (int8_t)bn;
+                }
+                if (a.check_ori && lane == bn) ++hreg;
+                ++nm;
+                // Only this wave touches the state and one wave's LDS
+                // operations complete in order, so the next step's reads see
+                // these writes without a wait; the compiler keeps the order
+                // (the indices may alias) and the asm keeps it from moving
+                // the next step's loads above the stores.
+                asm volatile("" ::: "memory");
+            }
         }
-        if (best <= kThLow && (float)best < (float)best2 * a.ratio) {
-            if (m21[bi] >= 0) {
-                if (lane == 0) m12[m21[bi]] = -1;
-                --nm;
-            }
-            if (lane == 0) {
-                m12[i1] = bi;
-                m21[bi] = i1;
-                mdist[bi] = best;
-            }
-            ++nm;
-            if (a.check_ori) {
-                const int bn = rot_bin(K1[i1].angle, K2[bi].angle);
-                if (lane == 0) { hist[bn]++; bin1[i1] = (int8_t)bn; }
-            }
-            wave_sync_m();
-        }
+        if (lane < 32) hist[lane] = hreg;   // bins 0..29; hist[31] = 0 counts the drops below
+        if (lane == 0) qcnt[0] = nm;        // the query list is spent: hand nm to the block
     }
     __syncthreads();
+    int nm = qcnt[0];
     if (a.check_ori) {
         int i1x, i2x, i3x;
-        three_maxima(hist, i1x, i2x, i3x);
+        three_maxima(hist, i1x, i2x, i3x);   // bins 0..29; hist[31] (zero) counts the drops
         int drop = 0;
-        for (int i = lane; i < n1; i += kWave) {
+        for (int i = tid; i < n1; i += kSfiThreads) {
             const int b = bin1[i];
             if (b < 0 || b == i1x || b == i2x || b == i3x) continue;
             if (m12[i] >= 0) { m12[i] = -1; ++drop; }
         }
-        nm -= wave_sum(drop);
+        drop = wave_sum(drop);
+        if (lane == 0 && drop) atomicAdd(&hist[31], drop);
+        __syncthreads();
+        nm -= hist[31];
     }
-    __syncthreads();
+    for (int i = tid; i < n1; i += kSfiThreads) m12g[i] = m12[i];
     if (a.prev_out) {
-        for (int i = lane; i < n1; i += kWave) {
+        for (int i = tid; i < n1; i += kSfiThreads) {
             float px, py;
             query_pos(a, pr, i, K1[i], px, py);
             const int m = m12[i];
@@ -603,7 +654,7 @@ __global__ __launch_bounds__(64) void k_sfi_resolve(SfiArgs a) {
             a.prev_out[((long long)pr * a.cap + i) * 2 + 1] = py;
         }
     }
-    if (lane == 0) a.nmatches[pr] = nm;
+    if (tid == 0) a.nmatches[pr] = nm;
 }
 
 constexpr size_t kLdsMax = 160 * 1024;
@@ -612,12 +663,12 @@ constexpr size_t kLdsMax = 160 * 1024;
 // ORB_ERR_UNSUPPORTED before any launch.
 static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
-    const size_t lds_staged = (size_t)a.cap * (20 + 4 * kTopK + 1) + 128 + 16;
-    const size_t lds_direct = (size_t)a.cap * (20 + 1) + 128 + 16;
+    const size_t lds_staged = (size_t)a.cap * (24 + 4 * kTopK + 8 + 1) + 128 + 16;
+    const size_t lds_direct = (size_t)a.cap * (24 + 8 + 1) + 128 + 16;
     if (lds_topk > kLdsMax || lds_direct > kLdsMax) return ORB_ERR_UNSUPPORTED;
     KLAUNCH(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
-    if (lds_staged <= kLdsMax) KLAUNCH(k_sfi_resolve<true>, dim3(npairs), dim3(64), lds_staged, st, a);
-    else KLAUNCH(k_sfi_resolve<false>, dim3(npairs), dim3(64), lds_direct, st, a);
+    if (lds_staged <= kLdsMax) KLAUNCH(k_sfi_resolve<true>, dim3(npairs), dim3(kSfiThreads), lds_staged, st, a);
+    else KLAUNCH(k_sfi_resolve<false>, dim3(npairs), dim3(kSfiThreads), lds_direct, st, a);
     return ORB_OK;
 }
 

@@ -5,6 +5,6 @@ set -o pipefail
 tag=$1; vars=$2
 out=gpurun_out/$tag
 mkdir -p "$out"
-timeout -k 10 420 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_extractor.py tests/test_gpu_configs.py tests/test_gpu_sort.py tests/test_gpu_sharding.py tests/test_gpu_adapter.py > "$out/tests.log" 2>&1 || { echo "tests failed"; tail -30 "$out/tests.log"; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests -m gpu > "$out/tests.log" 2>&1 || { echo "tests failed"; tail -30 "$out/tests.log"; exit 1; }
 tail -1 "$out/tests.log"
 bash tools/ab_variants.sh "$out/ab" "$vars $vars" "1"
