@@ -77,6 +77,8 @@ def parse():
     ap.add_argument("--sfi-after", type=int, default=2,
                     help="pipeline: step k's SearchForInitialization waits until step k+1's extraction has passed this "
                          "stage (orbx_set_stage_event: 1 pyramid, 2 FAST (default), 3 quadtree; -1: starts at once)")
+    ap.add_argument("--match-prio", type=int, default=0,
+                    help="priority of the SearchForInitialization stream (torch.cuda.Stream priority: -1 = high)")
     ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
     ap.add_argument("--workload", choices=["c2", "c3", "c4", "c5"], default="c2",
                     help="c2: the headline (this file); c3 stereo, c4 fisheye stereo (tools/bench_stereo.py), "
@@ -316,7 +318,10 @@ def main():
     # on the extraction stream)
     outs = [(kps, desc, n, mono), tuple(torch.empty_like(x) for x in (kps, desc, n, mono))]
     outs_dev = outs
-    mstream = torch.cuda.Stream(dev) if args.pipeline else stream
+    # the matching stream at a higher priority (--match-prio -1): its kernels
+    # are dispatched ahead of the extraction's as CUs free up, instead of
+    # waiting for LDS behind a stream of small extraction blocks
+    mstream = torch.cuda.Stream(dev, priority=args.match_prio) if args.pipeline else stream
     done = [None, None]                  # match of set i finished (recorded on mstream)
     matches = torch.empty((Bx - 1, cap), dtype=torch.int32, device=dev)
     nmatch = torch.empty(Bx - 1, dtype=torch.int32, device=dev)

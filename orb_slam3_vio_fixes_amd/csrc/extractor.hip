@@ -1461,6 +1461,13 @@ __device__ __forceinline__ void cand_dec(int i, float inv_ww, int ww, int& r, in
 #define ORB_FAST_CELLS_PER_WAVE 4
 #endif
 constexpr int kCellsPerWave = ORB_FAST_CELLS_PER_WAVE;
+#ifndef ORB_FAST_WPB
+// waves per k_fast_cells block: each wave owns its cells and its LDS region,
+// so one-wave blocks free their LDS the moment their wave ends instead of
+// waiting for the slowest of four (FAST 0.345 -> 0.327 ms, same-box A/B)
+#define ORB_FAST_WPB 1
+#endif
+constexpr int kFastWpb = ORB_FAST_WPB;
 #ifndef ORB_FAST_PRE2
 #define ORB_FAST_PRE2 0
 #endif
@@ -1568,7 +1575,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
     bunit = __builtin_amdgcn_readfirstlane(bunit);
     bframe = __builtin_amdgcn_readfirstlane(bframe);
-    const int c_begin = (bunit * 4 + wv) * kCellsPerWave;
+    const int c_begin = (bunit * kFastWpb + wv) * kCellsPerWave;
     const int it0 = bframe * a.ncells + c_begin, step = 1;
     const int it_end = bframe * a.ncells + min(c_begin + kCellsPerWave, a.ncells);
     // the plan tables are read-only here: constant address space -> scalar loads
@@ -2672,6 +2679,10 @@ constexpr int kHbT = 44;
 #define ORB_DESC_ABL 0   // timing ablation (tools only; wrong results): 1 = every patch load hits one L2-resident patch
 #endif
 constexpr int kDescSlots = ORB_DESC_SLOTS;   // keypoint slots per wave
+#ifndef ORB_DESC_WPB
+#define ORB_DESC_WPB 4   // waves per k_describe block (each wave owns its slots and its LDS buffers)
+#endif
+constexpr int kDescWpb = ORB_DESC_WPB;
 
 struct DescArgs {
     const uint8_t* in;
@@ -2858,8 +2869,8 @@ __device__ __forceinline__ int hm_row0(int mb) { return mb == 0 ? 0 : (mb == 1 ?
 __device__ __forceinline__ int hm_col0(int nb) { return nb == 0 ? 0 : (nb == 1 ? 16 : 22); }
 template <bool FMA>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WAVES))) void k_describe(DescArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t raw_s[4][kRaw * kRawP];
-    __shared__ __attribute__((aligned(16))) uint16_t hb_s[4][(kBl + 1) * kHbT];
+    __shared__ __attribute__((aligned(16))) uint8_t raw_s[kDescWpb][kRaw * kRawP];
+    __shared__ __attribute__((aligned(16))) uint16_t hb_s[kDescWpb][(kBl + 1) * kHbT];
     const int lane = lane_id(), wv = wave_id();
 #if ORB_DESC_HMFMA
     // lane's 16 band bytes: byte e = w[16 (l >> 4) + e - n], i.e. the 7 taps as
@@ -2965,7 +2976,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     // grid (runs of 4 * kDescSlots slots of a frame, frames), XCD-aware order
     int bunit, bframe;
     xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
-    const int lb = (bunit * 4 + wv) * kDescSlots;                  // frame-local slot
+    const int lb = (bunit * kDescWpb + wv) * kDescSlots;           // frame-local slot
     const long long s_begin = (long long)bframe * a.out_total + lb;
     const int nrun = max(0, min(kDescSlots, a.out_total - lb));
     DescLane mine{};
@@ -3920,10 +3931,10 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.kmask_bytes = ((P0.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
     fa.cand_bytes = (2 * P0.win_pix_max + 15) & ~15;
     fa.ilist_bytes = ORB_FAST_EMIT == 1 ? (4 * P0.item_max + 15) & ~15 : 0;
-    const size_t flds = 4 * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes + fa.ilist_bytes);
+    const size_t flds = kFastWpb * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes + fa.ilist_bytes);
     fa.nframes = B;
-    const dim3 fgrid((P.ncells + 4 * kCellsPerWave - 1) / (4 * kCellsPerWave), B);
-    hipLaunchKernelGGL(kfast, fgrid, dim3(256), flds, st, fa);
+    const dim3 fgrid((P.ncells + kFastWpb * kCellsPerWave - 1) / (kFastWpb * kCellsPerWave), B);
+    hipLaunchKernelGGL(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
     mark();
     // quadtree
     QtArgs qa;
@@ -3954,11 +3965,13 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
     da.slot_level = P.d_slot_level;
     da.nslots = (long long)B * P.out_total;
-    const dim3 dgrid((unsigned)((P.out_total + 4 * kDescSlots - 1) / (4 * kDescSlots)), (unsigned)B);
-    if (hd->preblur)
-        hipLaunchKernelGGL(da.fma ? k_describe_pb<true> : k_describe_pb<false>, dgrid, dim3(256), 0, st, da);
-    else
-        hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(256), 0, st, da);
+    if (hd->preblur) {
+        const dim3 pgrid((unsigned)((P.out_total + 4 * kDescSlots - 1) / (4 * kDescSlots)), (unsigned)B);
+        hipLaunchKernelGGL(da.fma ? k_describe_pb<true> : k_describe_pb<false>, pgrid, dim3(256), 0, st, da);
+    } else {
+        const dim3 dgrid((unsigned)((P.out_total + kDescWpb * kDescSlots - 1) / (kDescWpb * kDescSlots)), (unsigned)B);
+        hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(kWave * kDescWpb), 0, st, da);
+    }
     mark();
     // assemble
     AsmArgs aa;

@@ -358,7 +358,7 @@ struct SfiArgs {
     GridParams g;
     float window, ratio;
     int check_ori;
-    uint32_t* topk;          // [pair][cap][kTopK]  (dist << 16 | order in the level-0 list)
+    uint32_t* topk;          // [pair][cap][kTopK]  (rotation bin << 25 | dist << 16 | F2 feature), in (dist, grid order)
     int* ncand;              // [pair][cap]  (-1: not a query)
     int32_t* matches;        // [pair][cap]
     int32_t* nmatches;       // [pair]
@@ -394,29 +394,15 @@ __device__ __forceinline__ int cand_dist(const int* list, int j, const CellRange
     return hamming32(q0, q1, D2 + (long long)fi * 32);
 }
 
-// grid (npairs, ceil(cap / 16)), 256 threads: 4 waves x 4 queries each
-__global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];
+// The queries [qbeg + wave * qpw, + qpw) of pair pr: every candidate key into
+// the wave's LDS pool, then kTopK rounds of wave minimum over it.  LDS: the
+// level-0 list (cap) and four pools (cap each).
+__device__ void sfi_topk_pool(const SfiArgs& a, int pr, int qbeg, int qpw, int* lds) {
     int* list = lds;                              // cap entries (block-shared)
     uint32_t* pool = (uint32_t*)(lds + a.cap);    // per wave: cap keys
-    const int pr = blockIdx.x, lane = lane_id(), wv = wave_id();
+    const int lane = lane_id(), wv = wave_id();
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
     const int n1 = min(a.n[f1], a.cap);
-    __shared__ int s_any;
-    if (threadIdx.x == 0) s_any = 0;
-    __syncthreads();
-    {   // does this block hold any level-0 query?
-        const int i1 = blockIdx.y * 16 + (int)threadIdx.x;
-        if (threadIdx.x < 16 && i1 < n1 && a.kps[(long long)f1 * a.cap + i1].octave == 0) s_any = 1;
-    }
-    __syncthreads();
-    if (!s_any) {
-        for (int t = threadIdx.x; t < 16; t += blockDim.x) {
-            const int i1 = blockIdx.y * 16 + t;
-            if (i1 < n1) a.ncand[(long long)pr * a.cap + i1] = -1;
-        }
-        return;
-    }
     const int nl = level0_list(a, f2, list, threadIdx.x, blockDim.x);
     __syncthreads();
     uint32_t* mypool = pool + wv * a.cap;
@@ -425,8 +411,8 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
     const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
     const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
     const float r = a.window;
-    for (int t = 0; t < 4; ++t) {
-        const int i1 = blockIdx.y * 16 + wv * 4 + t;
+    for (int t = 0; t < qpw; ++t) {
+        const int i1 = qbeg + wv * qpw + t;
         if (i1 >= n1) break;
         uint32_t* tk = a.topk + ((long long)pr * a.cap + i1) * kTopK;
         int* nc = a.ncand + (long long)pr * a.cap + i1;
@@ -453,7 +439,15 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
             uint32_t mn = kNoKey;
             for (int q = lane; q < cnt; q += kWave) mn = min(mn, mypool[q]);
             mn = wave_min(mn, 0xffffffffu);
-            if (lane == 0) tk[k] = mn;
+            // out: rotation bin, distance and F2 feature index (the list
+            // position only ordered the ties)
+            if (lane == 0 && mn != kNoKey) {
+                const uint32_t fi = (uint32_t)list[mn & 0xffff] & 0xffffu;
+                const uint32_t bn = a.check_ori ? (uint32_t)rot_bin(k1.angle, K2[fi].angle) : 0u;
+                tk[k] = (bn << 25) | (mn & 0xffff0000u) | fi;
+            } else if (lane == 0) {
+                tk[k] = kNoKey;
+            }
             if (mn == kNoKey) { for (int kk = k + 1 + lane; kk < kTopK; kk += kWave) tk[kk] = kNoKey; break; }
             for (int q = lane; q < cnt; q += kWave)
                 if (mypool[q] == mn) mypool[q] = kNoKey;
@@ -464,18 +458,159 @@ __global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
     }
 }
 
+// grid (npairs, ceil(cap / 16)), 256 threads: 4 waves x 4 queries each
+__global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    const int pr = blockIdx.x;
+    const int f1 = a.pair_f1[pr];
+    const int n1 = min(a.n[f1], a.cap);
+    __shared__ int s_any;
+    if (threadIdx.x == 0) s_any = 0;
+    __syncthreads();
+    {   // does this block hold any level-0 query?
+        const int i1 = blockIdx.y * 16 + (int)threadIdx.x;
+        if (threadIdx.x < 16 && i1 < n1 && a.kps[(long long)f1 * a.cap + i1].octave == 0) s_any = 1;
+    }
+    __syncthreads();
+    if (!s_any) {
+        for (int t = threadIdx.x; t < 16; t += blockDim.x) {
+            const int i1 = blockIdx.y * 16 + t;
+            if (i1 < n1) a.ncand[(long long)pr * a.cap + i1] = -1;
+        }
+        return;
+    }
+    sfi_topk_pool(a, pr, blockIdx.y * 16, 4, lds);
+}
+
+// k_sfi_topk_st: the same top-K lists with F2's level-0 features staged in
+// LDS once per block of 64 queries (cell, position and descriptor in grid
+// order: 44 bytes each), so a query's candidate scan reads only LDS, and the
+// K smallest keys are drawn from registers (a lane holds the keys of its list
+// positions lane, lane + 64, ...; kStIt positions at most, longer lists take
+// k_sfi_topk).  Rounds stop after min(count, K) draws.
+constexpr int kStIt = 4;                  // level-0 lists of <= 256 features
+constexpr int kStQ = 64;                  // queries per block
+__global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
+    extern __shared__ __attribute__((aligned(16))) int lds[];
+    uint4* d2s = (uint4*)lds;                                   // 2 * kStIt * 64 (descriptor halves)
+    float2* xy2 = (float2*)(d2s + 2 * kStIt * kWave);           // kStIt * 64
+    int* list = (int*)(xy2 + kStIt * kWave);                    // kStIt * 64
+    float* an2 = (float*)(list + kStIt * kWave);                // kStIt * 64
+    const int pr = blockIdx.x, lane = lane_id(), wv = wave_id(), tid = threadIdx.x;
+    const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
+    const int n1 = min(a.n[f1], a.cap);
+    const int q0 = blockIdx.y * kStQ;
+    const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
+    __shared__ int s_any;
+    if (tid == 0) s_any = 0;
+    __syncthreads();
+    if (tid < kStQ && q0 + tid < n1 && K1[q0 + tid].octave == 0) s_any = 1;
+    __syncthreads();
+    if (!s_any) {
+        if (tid < kStQ && q0 + tid < n1) a.ncand[(long long)pr * a.cap + q0 + tid] = -1;
+        return;
+    }
+    const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
+    const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
+    const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
+    const int nl = a.gcount[f2];
+    if (nl > kStIt * kWave) {             // a long level-0 list: the pool form (LDS sized for it)
+        sfi_topk_pool(a, pr, q0, kStQ / 4, lds);
+        return;
+    }
+    {
+        const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
+        for (int j = tid; j < nl; j += 256) {
+            const int v = (int)gs[j], fi = v & 0xffff;
+            list[j] = v;
+            xy2[j] = make_float2(K2[fi].x, K2[fi].y);
+            an2[j] = K2[fi].angle;
+            d2s[2 * j] = *(const uint4*)(D2 + (long long)fi * 32);
+            d2s[2 * j + 1] = *(const uint4*)(D2 + (long long)fi * 32 + 16);
+        }
+    }
+    __syncthreads();
+    const float r = a.window;
+    for (int t = 0; t < kStQ / 4; ++t) {
+        const int i1 = q0 + wv * (kStQ / 4) + t;
+        if (i1 >= n1) break;
+        uint32_t* tk = a.topk + ((long long)pr * a.cap + i1) * kTopK;
+        int* nc = a.ncand + (long long)pr * a.cap + i1;
+        const orb_keypoint k1 = K1[i1];
+        float px, py;
+        query_pos(a, pr, i1, k1, px, py);
+        CellRange cr;
+        if (k1.octave > 0 || !cell_range(px, py, r, a.g, cr)) {
+            if (lane == 0) *nc = -1;
+            continue;
+        }
+        const uint4 qa = *(const uint4*)(D1 + (long long)i1 * 32), qb = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+        uint32_t kv[kStIt];
+        int cnt = 0;
+#pragma unroll
+        for (int it = 0; it < kStIt; ++it) {
+            const int j = it * kWave + lane;
+            kv[it] = kNoKey;
+            if (j < nl) {
+                const int v = list[j];
+                const int cell = v >> 16, gx = cell / kGridRows, gy = cell - gx * kGridRows;
+                const float2 p2 = xy2[j];
+                if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1 && fabsf(p2.x - px) < r &&
+                    fabsf(p2.y - py) < r) {
+                    const uint4 b0 = d2s[2 * j], b1 = d2s[2 * j + 1];
+                    const int d = __popc(qa.x ^ b0.x) + __popc(qa.y ^ b0.y) + __popc(qa.z ^ b0.z) +
+                                  __popc(qa.w ^ b0.w) + __popc(qb.x ^ b1.x) + __popc(qb.y ^ b1.y) +
+                                  __popc(qb.z ^ b1.z) + __popc(qb.w ^ b1.w);
+                    kv[it] = ((uint32_t)d << 16) | (uint32_t)j;
+                }
+            }
+            cnt += __popcll(__ballot(kv[it] != kNoKey));
+        }
+        const int rounds = min(cnt, kTopK);
+        uint32_t mine = kNoKey;   // lane k < kTopK: the k-th draw
+        for (int k = 0; k < rounds; ++k) {
+            uint32_t mn = kv[0];
+#pragma unroll
+            for (int it = 1; it < kStIt; ++it) mn = min(mn, kv[it]);
+            mn = wave_min(mn, 0xffffffffu);
+#pragma unroll
+            for (int it = 0; it < kStIt; ++it)
+                if (kv[it] == mn) kv[it] = kNoKey;
+            if (lane == k) mine = mn;
+        }
+        // out: rotation bin, distance and F2 feature index (the list position
+        // only ordered the ties), one store per draw
+        if (lane < kTopK) {
+            uint32_t o = kNoKey;
+            if (mine != kNoKey) {
+                const int j = (int)(mine & 0xffffu);
+                const uint32_t bn = a.check_ori ? (uint32_t)rot_bin(k1.angle, an2[j]) : 0u;
+                o = (bn << 25) | (mine & 0xffff0000u) | ((uint32_t)list[j] & 0xffffu);
+            }
+            tk[lane] = o;
+        }
+        if (lane == 0) *nc = cnt;
+    }
+}
+
 // One block per pair: the serial pass runs on wave 0; the four waves stage
-// everything it reads into LDS first (the pair's level-0 list, both frames'
-// angles, the query list and counts, the queries' top-K lists) and finish the
-// orientation filter and the outputs after it, so no loop waits on one global
-// load per iteration.  The matches live in LDS until the end.  STAGED: the
-// queries' top-K lists are copied into LDS (32 B per F1 keypoint); otherwise
-// (frames of more than ~2,700 keypoints, e.g. the 5 x nFeatures
-// initialization extractor of Tracking.cc:601) each query reads its list from
-// global memory, one query ahead of its use (the lists do not depend on the
-// serial state).
+// what it reads into LDS first (the pair's level-0 list, both frames' angles,
+// the query list) and finish the orientation filter and the outputs after it.
+// The top-K lists stay in global memory: lanes 8t..8t+7 of the wave hold the
+// keys of query j0 + t of a run of 8 queries (one gather per run), the next
+// run is in flight while this one is walked, and query t's step ballots only
+// its own lanes -- its keys are already in (distance, grid order).  The
+// serial state (matched distance and F2 -> F1 match, packed) and the matches
+// live in LDS: ~25 bytes per keypoint, so the block does not hold off the
+// extraction's blocks it runs beside.
 constexpr int kSfiThreads = 256;
-template <bool STAGED>
+#ifndef ORB_SFI_TOPK_ST
+#define ORB_SFI_TOPK_ST 1
+#endif
+#ifndef ORB_SFI_PRIO
+#define ORB_SFI_PRIO 1
+#endif
+constexpr uint32_t kMdNone = 0xffff0000u;    // md21: no match yet (distance field 0xffff)
 __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
@@ -485,98 +620,82 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
     const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
     const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
-    int* list = lds;                          // cap
-    int* mdist = list + a.cap;                // cap
-    int* m21 = mdist + a.cap;                 // cap
-    int* hist = m21 + a.cap;                  // 32 (hist[31]: the filter's drop count)
-    int* qlist = hist + 32;                   // cap: query indices i1 (level 0, >= 1 candidate)
-    int* qcnt = qlist + a.cap;                // cap: candidate counts (first: every F1 keypoint's)
-    int* m12 = qcnt + a.cap;                  // cap
-    uint32_t* qtop = (uint32_t*)(m12 + a.cap);   // STAGED: cap * kTopK
-    float* ang1 = (float*)(qtop + (STAGED ? (size_t)a.cap * kTopK : 0));   // cap
-    float* ang2 = ang1 + a.cap;                                             // cap
-    int8_t* bin1 = (int8_t*)(ang2 + a.cap);                                 // cap
+    int* list = lds;                              // cap
+    uint32_t* md21 = (uint32_t*)(list + a.cap);   // cap: matched distance << 16 | (F1 match + 1)
+    int* hist = (int*)(md21 + a.cap);             // 32 (hist[31]: the filter's drop count)
+    int* qlist = hist + 32;                       // cap: query i1 | (more than kTopK candidates) << 31
+    int* m12 = qlist + a.cap;                     // cap
+    int8_t* bin1 = (int8_t*)(m12 + a.cap);        // cap
     int32_t* m12g = a.matches + (long long)pr * a.cap;
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
     const int* ncand = a.ncand + (long long)pr * a.cap;
     const int nl = level0_list(a, f2, list, tid, kSfiThreads);
     for (int i = tid; i < n1; i += kSfiThreads) {
-        qcnt[i] = ncand[i];
+        qlist[i] = ncand[i];
         m12[i] = -1;
         bin1[i] = -1;
-        if (a.check_ori) ang1[i] = K1[i].angle;
     }
-    for (int i = tid; i < n2; i += kSfiThreads) {
-        mdist[i] = INT_MAX;
-        m21[i] = -1;
-        if (a.check_ori) ang2[i] = K2[i].angle;
-    }
+    for (int i = tid; i < n2; i += kSfiThreads) md21[i] = kMdNone;
     if (tid < 32) hist[tid] = 0;
     __syncthreads();
-    // compact the queries in F1 order (wave 0, in place: a round reads its 64
-    // counts before it writes, and writes only below its own reads)
-    __shared__ int s_nq;
     if (tid < kWave) {
+#if ORB_SFI_PRIO
+        // the serial walk is one latency-bound wave beside the extraction's
+        // waves on its SIMD: it issues first
+        __builtin_amdgcn_s_setprio(3);
+#endif
+        // compact the queries in F1 order (in place: a round reads its 64
+        // counts before it writes, and writes only below its own reads)
         int nq = 0;
         for (int base = 0; base < n1; base += kWave) {
             const int i = base + lane;
-            const int c = i < n1 ? qcnt[i] : -1;
+            const int c = i < n1 ? qlist[i] : -1;
             const uint64_t m = __ballot(c > 0);
-            if (c > 0) { qlist[nq + mask_rank(m)] = i; qcnt[nq + mask_rank(m)] = c; }
+            if (c > 0) qlist[nq + mask_rank(m)] = i | (c > kTopK ? (int)0x80000000 : 0);
             nq += __popcll(m);
         }
-        if (lane == 0) s_nq = nq;
-    }
-    __syncthreads();
-    const int nq = s_nq;
-    if (STAGED)
-        for (int q = tid; q < nq; q += kSfiThreads) {
-            const uint4* src = (const uint4*)(topk + (long long)qlist[q] * kTopK);
-            uint32_t* dst = qtop + (long long)q * kTopK;   // 4-byte aligned only
-            const uint4 t0 = src[0], t1 = src[1];
-            dst[0] = t0.x; dst[1] = t0.y; dst[2] = t0.z; dst[3] = t0.w;
-            dst[4] = t1.x; dst[5] = t1.y; dst[6] = t1.z; dst[7] = t1.w;
-        }
-    __syncthreads();
-    if (tid < kWave) {
         int nm = 0, hreg = 0;   // lane b: the rotation histogram's bin b
         const float r = a.window;
-        // everything of query j + 1 that does not depend on the serial state
-        // (its index, count, top-K keys and their F2 features) is read during
-        // query j, so a step waits on one LDS round trip (mdist) instead of four
-        uint32_t next_key = kNoKey;
-        int next_i1 = 0, next_cnt = 0, next_fi = 0;
-        auto peek = [&](int j) {
-            next_i1 = qlist[j];
-            next_cnt = qcnt[j];
-            if (STAGED) next_key = lane < kTopK ? qtop[j * kTopK + lane] : kNoKey;
-            else next_key = lane < kTopK ? topk[(long long)next_i1 * kTopK + lane] : kNoKey;
-            // (the direct form's keys are global loads: their features are read at use)
-            if (STAGED) next_fi = next_key != kNoKey ? (list[next_key & 0xffff] & 0xffff) : 0;
+        const int grp = lane >> 3;
+        // run of 8 queries from j0: lane 8t + k holds key k of query j0 + t
+        auto run_keys = [&](int j0) -> uint32_t {
+            const int j = j0 + grp;
+            return j < nq ? topk[(long long)(qlist[j] & 0x7fffffff) * kTopK + (lane & 7)] : kNoKey;
         };
-        if (nq > 0) peek(0);
+        uint32_t kcur = nq > 0 ? run_keys(0) : kNoKey;
+        uint32_t knxt = nq > 8 ? run_keys(8) : kNoKey;
+        int qn = nq > 0 ? qlist[0] : 0;
         for (int j = 0; j < nq; ++j) {
-            const int i1 = next_i1;
-            const int cur_cnt = next_cnt;
-            const uint32_t cur_key = next_key;
-            const int cur_fi = next_fi;
-            if (j + 1 < nq) peek(j + 1);
-            int best = INT_MAX, best2 = INT_MAX, bi = -1;
+            const int t = j & 7;
+            if (t == 0 && j > 0) {
+                kcur = knxt;
+                knxt = j + 8 < nq ? run_keys(j + 8) : kNoKey;
+            }
+            const int qe = qn;
+            if (j + 1 < nq) qn = qlist[j + 1];
+            const int i1 = qe & 0x7fffffff;
+            const bool many = qe < 0;
+            int best = INT_MAX, best2 = INT_MAX, bi = -1, prev = -1, bn = 0;
             bool ok = false;
             {
-                const bool have = lane < kTopK && cur_key != kNoKey;
-                const int d = (int)(cur_key >> 16);
-                const int fi = STAGED ? cur_fi : (have ? (list[cur_key & 0xffff] & 0xffff) : 0);
-                const bool live = have && !(mdist[fi] <= d);
+                // one LDS read per step: the state of the lane's candidate,
+                // which for the winner is also its previous match
+                const bool have = grp == t && kcur != kNoKey;
+                const int d = (int)((kcur >> 16) & 0x1ffu);
+                const int fi = (int)(kcur & 0xffffu);
+                const uint32_t st = md21[have ? fi : 0];
+                const bool live = have && !((int)(st >> 16) <= d);
                 uint64_t m = __ballot(live);
                 const int nlive = __popcll(m);
-                if (nlive >= 2 || cur_cnt <= kTopK) {
+                if (nlive >= 2 || !many) {
                     ok = true;
                     if (nlive >= 1) {
                         // the ballot is uniform: readlane, not an LDS-routed shuffle
                         const int l0 = __ffsll((long long)m) - 1;
                         best = __builtin_amdgcn_readlane(d, l0);
                         bi = __builtin_amdgcn_readlane(fi, l0);
+                        prev = (int)((uint32_t)__builtin_amdgcn_readlane((int)st, l0) & 0xffffu) - 1;
+                        bn = (int)((uint32_t)__builtin_amdgcn_readlane((int)kcur, l0) >> 25);
                         m &= m - 1;
                         if (m) best2 = __builtin_amdgcn_readlane(d, __ffsll((long long)m) - 1);
                     }
@@ -597,21 +716,22 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                     if (jj < nl) {
                         d = cand_dist(list, jj, cr, px, py, r, K2, D2, q0, q1);
                         fi = list[jj] & 0xffff;
-                        if (d != INT_MAX && mdist[fi] <= d) d = INT_MAX;
+                        if (d != INT_MAX && (int)(md21[fi] >> 16) <= d) d = INT_MAX;
                     }
                     merge_chunk(st, d, fi, 0);
                 }
                 best = st.best; best2 = st.best2; bi = st.idx;
+                if (bi >= 0) {
+                    prev = (int)(md21[bi] & 0xffffu) - 1;
+                    bn = a.check_ori ? rot_bin(k1.angle, K2[bi].angle) : 0;
+                }
             }
             if (best <= kThLow && (float)best < (float)best2 * a.ratio) {
-                const int prev = m21[bi];
-                const int bn = a.check_ori ? rot_bin(ang1[i1], ang2[bi]) : 0;
                 if (prev >= 0) --nm;
                 if (lane == 0) {
                     if (prev >= 0) m12[prev] = -1;
                     m12[i1] = bi;
-                    m21[bi] = i1;
-                    mdist[bi] = best;
+                    md21[bi] = ((uint32_t)best << 16) | (uint32_t)(i1 + 1);
                     if (a.check_ori) bin1[i1] = (int8_t)bn;
                 }
                 if (a.check_ori && lane == bn) ++hreg;
@@ -625,13 +745,13 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             }
         }
         if (lane < 32) hist[lane] = hreg;   // bins 0..29; hist[31] = 0 counts the drops below
-        if (lane == 0) qcnt[0] = nm;        // the query list is spent: hand nm to the block
+        if (lane == 0) qlist[0] = nm;       // the query list is spent: hand nm to the block
     }
     __syncthreads();
-    int nm = qcnt[0];
+    int nm = qlist[0];
     if (a.check_ori) {
         int i1x, i2x, i3x;
-        three_maxima(hist, i1x, i2x, i3x);   // bins 0..29; hist[31] (zero) counts the drops
+        three_maxima(hist, i1x, i2x, i3x);   // bins 0..29
         int drop = 0;
         for (int i = tid; i < n1; i += kSfiThreads) {
             const int b = bin1[i];
@@ -663,12 +783,18 @@ constexpr size_t kLdsMax = 160 * 1024;
 // ORB_ERR_UNSUPPORTED before any launch.
 static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
-    const size_t lds_staged = (size_t)a.cap * (24 + 4 * kTopK + 8 + 1) + 128 + 16;
-    const size_t lds_direct = (size_t)a.cap * (24 + 8 + 1) + 128 + 16;
-    if (lds_topk > kLdsMax || lds_direct > kLdsMax) return ORB_ERR_UNSUPPORTED;
+    const size_t lds_res = (size_t)a.cap * (4 * 4 + 1) + 128 + 16;
+    if (lds_topk > kLdsMax || lds_res > kLdsMax) return ORB_ERR_UNSUPPORTED;
+    if (a.cap > 65535) return ORB_ERR_UNSUPPORTED;   // 16-bit feature fields of the keys and the state
+#if ORB_SFI_TOPK_ST
+    // staged form; a block whose F2 level-0 list is longer than its
+    // registers take runs the pool form in the same LDS
+    KLAUNCH(k_sfi_topk_st, dim3(npairs, (a.cap + kStQ - 1) / kStQ), dim3(256),
+            std::max(lds_topk, (size_t)kStIt * kWave * (32 + 8 + 4 + 4)), st, a);
+#else
     KLAUNCH(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
-    if (lds_staged <= kLdsMax) KLAUNCH(k_sfi_resolve<true>, dim3(npairs), dim3(kSfiThreads), lds_staged, st, a);
-    else KLAUNCH(k_sfi_resolve<false>, dim3(npairs), dim3(kSfiThreads), lds_direct, st, a);
+#endif
+    KLAUNCH(k_sfi_resolve, dim3(npairs), dim3(kSfiThreads), lds_res, st, a);
     return ORB_OK;
 }
 
