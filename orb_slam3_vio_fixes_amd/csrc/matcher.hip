@@ -665,12 +665,17 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         uint32_t kcur = nq > 0 ? run_keys(0) : kNoKey;
         uint32_t knxt = nq > 8 ? run_keys(8) : kNoKey;
         int qn = nq > 0 ? qlist[0] : 0;
-        for (int j = 0; j < nq; ++j) {
-            const int t = j & 7;
-            if (t == 0 && j > 0) {
-                kcur = knxt;
-                knxt = j + 8 < nq ? run_keys(j + 8) : kNoKey;
-            }
+        // runs as a loop nest: inside a run no step reads the run in flight,
+        // so the compiler's wait counts never stall a step on that load (a
+        // flat loop with the swap inside made every step wait for it)
+        for (int j0 = 0; j0 < nq; j0 += 8) {
+          if (j0 > 0) {
+            kcur = knxt;
+            knxt = j0 + 8 < nq ? run_keys(j0 + 8) : kNoKey;
+          }
+          const int jend = min(j0 + 8, nq);
+          for (int j = j0; j < jend; ++j) {
+            const int t = j - j0;
             const int qe = qn;
             if (j + 1 < nq) qn = qlist[j + 1];
             const int i1 = qe & 0x7fffffff;
@@ -743,6 +748,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 // the next step's loads above the stores.
                 asm volatile("" ::: "memory");
             }
+          }
         }
         if (lane < 32) hist[lane] = hreg;   // bins 0..29; hist[31] = 0 counts the drops below
         if (lane == 0) qlist[0] = nm;       // the query list is spent: hand nm to the block
