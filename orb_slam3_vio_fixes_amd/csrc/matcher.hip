@@ -664,7 +664,6 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         };
         uint32_t kcur = nq > 0 ? run_keys(0) : kNoKey;
         uint32_t knxt = nq > 8 ? run_keys(8) : kNoKey;
-        int qn = nq > 0 ? qlist[0] : 0;
         // runs as a loop nest: inside a run no step reads the run in flight,
         // so the compiler's wait counts never stall a step on that load (a
         // flat loop with the swap inside made every step wait for it)
@@ -673,36 +672,39 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             kcur = knxt;
             knxt = j0 + 8 < nq ? run_keys(j0 + 8) : kNoKey;
           }
+          // per run, everything but the state: lane 8t + k's key fields and
+          // state address, lane t's query entry (read per step by readlane)
+          const bool kval = kcur != kNoKey;
+          const int kd = (int)((kcur >> 16) & 0x1ffu);
+          const int kfi = kval ? (int)(kcur & 0xffffu) : 0;
+          const int qv = lane < 8 && j0 + lane < nq ? qlist[j0 + lane] : 0;
           const int jend = min(j0 + 8, nq);
           for (int j = j0; j < jend; ++j) {
             const int t = j - j0;
-            const int qe = qn;
-            if (j + 1 < nq) qn = qlist[j + 1];
+            const int qe = __builtin_amdgcn_readlane(qv, t);
             const int i1 = qe & 0x7fffffff;
             const bool many = qe < 0;
             int best = INT_MAX, best2 = INT_MAX, bi = -1, prev = -1, bn = 0;
             bool ok = false;
             {
-                // one LDS read per step: the state of the lane's candidate,
-                // which for the winner is also its previous match
-                const bool have = grp == t && kcur != kNoKey;
-                const int d = (int)((kcur >> 16) & 0x1ffu);
-                const int fi = (int)(kcur & 0xffffu);
-                const uint32_t st = md21[have ? fi : 0];
-                const bool live = have && !((int)(st >> 16) <= d);
-                uint64_t m = __ballot(live);
+                // one LDS read per step: the state of each lane's candidate
+                // (query t's lanes count), which for the winner is also its
+                // previous match
+                const uint32_t st = md21[kfi];
+                const bool live = kval && !((int)(st >> 16) <= kd);
+                uint64_t m = __ballot(live) & (0xffull << (8 * t));
                 const int nlive = __popcll(m);
                 if (nlive >= 2 || !many) {
                     ok = true;
                     if (nlive >= 1) {
                         // the ballot is uniform: readlane, not an LDS-routed shuffle
                         const int l0 = __ffsll((long long)m) - 1;
-                        best = __builtin_amdgcn_readlane(d, l0);
-                        bi = __builtin_amdgcn_readlane(fi, l0);
+                        best = __builtin_amdgcn_readlane(kd, l0);
+                        bi = __builtin_amdgcn_readlane(kfi, l0);
                         prev = (int)((uint32_t)__builtin_amdgcn_readlane((int)st, l0) & 0xffffu) - 1;
                         bn = (int)((uint32_t)__builtin_amdgcn_readlane((int)kcur, l0) >> 25);
                         m &= m - 1;
-                        if (m) best2 = __builtin_amdgcn_readlane(d, __ffsll((long long)m) - 1);
+                        if (m) best2 = __builtin_amdgcn_readlane(kd, __ffsll((long long)m) - 1);
                     }
                 }
             }
