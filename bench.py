@@ -10,10 +10,10 @@ on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
 F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
 (Tracking.cc:2459-2492).  Steps are pipelined: the matching of step k runs
 on a second HIP stream while step k+1 extracts into a second output set,
-started once step k+1's extraction has passed its FAST stage
-(orbx_set_stage_event; --sfi-after) so that it shares the GPU with the
-latency-bound quadtree rather than the VALU-bound FAST pass (--no-pipeline
-serialises them); all K steps' work is inside the timed region.  Multi-GPU: one process per GPU, frames sharded
+started once step k+1's extraction has passed its pyramid stage
+(orbx_set_stage_event; --sfi-after): its parallel top-K pass then runs beside
+FAST and its latency-bound serial walk beside the quadtree and describe
+(--no-pipeline serialises them); all K steps' work is inside the timed region.  Multi-GPU: one process per GPU, frames sharded
 (weak scaling, no data-path collective); timing = max over ranks.
 
 Extra objects on the JSON line:
@@ -74,9 +74,9 @@ def parse():
     ap.add_argument("--overlap", type=int, default=1, choices=[1, 2],
                     help="batches in flight: 2 = consecutive steps alternate between two extractor handles "
                          "(own plan and scratch each) on two streams, so step k+1 extracts beside step k")
-    ap.add_argument("--sfi-after", type=int, default=2,
+    ap.add_argument("--sfi-after", type=int, default=1,
                     help="pipeline: step k's SearchForInitialization waits until step k+1's extraction has passed this "
-                         "stage (orbx_set_stage_event: 1 pyramid, 2 FAST (default), 3 quadtree; -1: starts at once)")
+                         "stage (orbx_set_stage_event: 1 pyramid (default), 2 FAST, 3 quadtree; -1: starts at once)")
     ap.add_argument("--match-prio", type=int, default=0,
                     help="priority of the SearchForInitialization stream (torch.cuda.Stream priority: -1 = high)")
     ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")

@@ -2682,7 +2682,10 @@ constexpr int kHbT = 44;
 #endif
 constexpr int kDescSlots = ORB_DESC_SLOTS;   // keypoint slots per wave
 #ifndef ORB_DESC_WPB
-#define ORB_DESC_WPB 4   // waves per k_describe block (each wave owns its slots and its LDS buffers)
+// waves per k_describe block (each wave owns its slots and its LDS buffers):
+// one-wave blocks free their LDS when their wave ends (describe 0.325 -> 0.30
+// ms); with the matching placed after the pyramid stage (bench --sfi-after 1)
+#define ORB_DESC_WPB 1
 #endif
 constexpr int kDescWpb = ORB_DESC_WPB;
 
