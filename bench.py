@@ -77,6 +77,9 @@ def parse():
     ap.add_argument("--sfi-after", type=int, default=1,
                     help="pipeline: step k's SearchForInitialization waits until step k+1's extraction has passed this "
                          "stage (orbx_set_stage_event: 1 pyramid (default), 2 FAST, 3 quadtree; -1: starts at once)")
+    ap.add_argument("--sets", type=int, default=2,
+                    help="pipeline: output sets in rotation (2: step k+2 waits for step k's matching; "
+                         "--overlap 2 wants 4)")
     ap.add_argument("--match-prio", type=int, default=0,
                     help="priority of the SearchForInitialization stream (torch.cuda.Stream priority: -1 = high)")
     ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
@@ -313,16 +316,20 @@ def main():
     # extraction stream of each handle (--overlap 2: the second on its own stream)
     xstreams = [stream] + [torch.cuda.Stream(dev) for _ in range(args.overlap - 1)]
     kps, desc, n, mono, cap = ex.extract_batch_device(frames, LAP)
-    # two output sets: SearchForInitialization of step k runs on its own
-    # stream while step k+1 extracts into the other set (--no-pipeline: both
-    # on the extraction stream)
-    outs = [(kps, desc, n, mono), tuple(torch.empty_like(x) for x in (kps, desc, n, mono))]
+    # --sets output sets (default 2): SearchForInitialization of step k runs on
+    # its own stream while step k+1 extracts into another set; with more sets
+    # step k+2 does not wait for step k's matching either (measured: no gain
+    # at --overlap 1; --overlap 2 wants 4) (--no-pipeline: both on the
+    # extraction stream)
+    nsets = max(2, args.sets)
+    outs = [(kps, desc, n, mono)] + [tuple(torch.empty_like(x) for x in (kps, desc, n, mono))
+                                     for _ in range(nsets - 1)]
     outs_dev = outs
     # the matching stream at a higher priority (--match-prio -1): its kernels
     # are dispatched ahead of the extraction's as CUs free up, instead of
     # waiting for LDS behind a stream of small extraction blocks
     mstream = torch.cuda.Stream(dev, priority=args.match_prio) if args.pipeline else stream
-    done = [None, None]                  # match of set i finished (recorded on mstream)
+    done = [None] * nsets                # match of set i finished (recorded on mstream)
     matches = torch.empty((Bx - 1, cap), dtype=torch.int32, device=dev)
     nmatch = torch.empty(Bx - 1, dtype=torch.int32, device=dev)
     inv_w = float(np.float32(64) / np.float32(W))
@@ -334,9 +341,9 @@ def main():
     # --sfi-after k: the library records a per-set event when the extraction
     # passes stage k, and step k's matching is enqueued behind step k+1's
     # event, so it runs beside the latency-bound later stages, not beside FAST
-    stage_ev = [None, None]
+    stage_ev = [None] * nsets
     if args.pipeline and args.sfi_after >= 0:
-        for j in range(2):
+        for j in range(nsets):
             stage_ev[j] = torch.cuda.Event()
             stage_ev[j].record(stream)                  # creates the event
     pending = []                                        # (set, extracted event) whose match is not enqueued yet
@@ -360,10 +367,11 @@ def main():
         done[i].record(mstream)
 
     def step(timed=False):
-        i = counter[0] % 2
+        i = counter[0] % nsets
+        h = counter[0] % args.overlap                   # --overlap 2: consecutive steps alternate handles
         counter[0] += 1
         k_, d_, n_, m_ = outs[i]
-        xe, xs = exs[i % args.overlap], xstreams[i % args.overlap]
+        xe, xs = exs[h], xstreams[h]
         if done[i] is not None:
             xs.wait_event(done[i])       # the match that read this set has finished
         if stage_ev[i] is not None:
@@ -423,7 +431,7 @@ def main():
 
     if args.dump:
         # the last step's outputs of this rank, with global frame / pair indices
-        last = outs_dev[(counter[0] - 1) % 2]
+        last = outs_dev[(counter[0] - 1) % nsets]
         Path(args.dump).mkdir(parents=True, exist_ok=True)
         np.savez(Path(args.dump) / f"rank{rank}.npz", first=rank * B, frames=Bx, world=world,
                  kps=last[0].cpu().numpy(), desc=last[1].cpu().numpy(), n=last[2].cpu().numpy(),
@@ -453,6 +461,7 @@ def main():
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
                           "frames_per_step_per_gpu": B, "streams": args.streams, "overlap": args.overlap, "pipeline": args.pipeline,
                           "sfi_after_stage": args.sfi_after if args.pipeline else None,
+                          "output_sets": nsets if args.pipeline else 1,
                           "parallelism": f"frames sharded over {world} GPU(s), halo frame per seam"},
                "stage_ms": {**{k: float(v) for k, v in zip(STAGES, stage_ms)},
                             "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
@@ -471,7 +480,7 @@ def main():
             # parity of the sampled frames (the CPU leg doubles as a checker):
             # every keypoint byte, descriptor, and the whole matches12 array
             # of every sampled pair (the output set of the last step)
-            last = outs_dev[(counter[0] - 1) % 2]
+            last = outs_dev[(counter[0] - 1) % nsets]
             kh = last[0][:ns].cpu().numpy()
             dh = last[1][:ns].cpu().numpy()
             nh = last[2][:ns].cpu().numpy()
