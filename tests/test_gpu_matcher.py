@@ -222,3 +222,52 @@ def test_search_by_bow_many(gpu_lib, frames):
     e = (np.zeros(0, abi.KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8))
     c0, m0 = m.SearchByBoWMany(kfs, fvs, valids, fr(e), abi.featvec_struct(np.zeros(0, np.int64)))
     assert (c0 == 0).all() and m0.shape == (len(kfs), 0)
+
+
+def _graded_copies(k0, d0, base, copies, jitter, seed, flip):
+    """Level-0 keypoints: `copies` copies of each base keypoint a few pixels
+    apart; copy c's descriptor has c bits flipped when `flip` (distances
+    0, 1, 2, ... to an unflipped copy), else the base descriptor."""
+    rng = np.random.default_rng(seed)
+    ks, ds = [], []
+    for b in base:
+        for c in range(copies):
+            k = k0[b].copy()
+            k["x"] = k["x"] + rng.uniform(-jitter, jitter)
+            k["y"] = k["y"] + rng.uniform(-jitter, jitter)
+            k["angle"] = (k["angle"] + rng.uniform(0, 20)) % 360
+            k["octave"] = 0
+            d = d0[b].copy()
+            if flip:
+                bits = np.unpackbits(d)
+                bits[rng.permutation(256)[:c]] ^= 1
+                d = np.packbits(bits)
+            ks.append(k)
+            ds.append(d)
+    return np.array(ks, dtype=k0.dtype), np.array(ds, dtype=np.uint8)
+
+
+@pytest.mark.parametrize("copies,ratio,ori", [(12, 0.9, True), (20, 1.0, False), (9, 0.95, True)])
+def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, ratio, ori):
+    """F1 holds `copies` identical copies of each of 24 keypoints, F2 `copies`
+    copies whose descriptors sit 0, 1, 2, ... bits away.  The copies of one
+    F1 keypoint steal F2's copies one after the other (ORBmatcher.cc:680-700:
+    a candidate whose matched distance is <= the query's is skipped), so
+    after the eighth claim a query's top-8 list holds at most one live entry
+    and the device resolve must fall back to its exact full rescan; the
+    ratio test stops the chain part way."""
+    k0, d0 = frames[0][0], frames[0][1]
+    l0 = np.where(k0["octave"] == 0)[0]
+    xs = k0["x"][l0]
+    base = l0[np.argsort(xs)][:: max(1, len(l0) // 24)][:24]
+    k1, d1 = _graded_copies(k0, d0, base, copies, 2.0, 1, False)
+    k2, d2 = _graded_copies(k0, d0, base, copies, 2.0, 2, True)
+    prev = np.stack([k1["x"], k1["y"]], 1)
+    f1 = abi.frame_struct(k1, d1, 752, 480)
+    f2 = abi.frame_struct(k2, d2, 752, 480)
+    nm, m12, p2 = orb.ORBmatcher(ratio, ori).SearchForInitialization(f1, f2, prev, 100)
+    rnm, rm12, rp2 = O.search_for_initialization(f1, f2, prev, 100, ratio, ori)
+    assert rnm > len(base)          # chains of steals happened
+    assert nm == rnm
+    np.testing.assert_array_equal(m12, rm12)
+    np.testing.assert_array_equal(p2, rp2)
