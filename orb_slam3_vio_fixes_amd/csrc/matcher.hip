@@ -336,8 +336,9 @@ __host__ __device__ __forceinline__ void three_maxima(const int* h, int& i1, int
 // the first two elements, in (distance, candidate order), of its candidates
 // that survive that rule under the state left by i1-1.  k_sfi_topk computes,
 // for every level-0 F1 feature in parallel, its candidate count and its
-// kTopK smallest (distance, order) pairs.  k_sfi_resolve then walks F1 in
-// order with one wave per frame pair; each step filters <= kTopK entries
+// kTopK smallest (distance, order) pairs (k_sfi_topk_st / k_sfi_topk).
+// k_sfi_resolve then walks F1 in order with one wave per frame pair; each
+// step filters <= kTopK entries
 // against vMatchedDistance.  When fewer than two entries survive and the list
 // was truncated, the wave re-scans the full candidate list (exact fallback).
 // ---------------------------------------------------------------------------
@@ -594,15 +595,16 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
 }
 
 // One block per pair: the serial pass runs on wave 0; the four waves stage
-// what it reads into LDS first (the pair's level-0 list, both frames' angles,
-// the query list) and finish the orientation filter and the outputs after it.
-// The top-K lists stay in global memory: lanes 8t..8t+7 of the wave hold the
-// keys of query j0 + t of a run of 8 queries (one gather per run), the next
-// run is in flight while this one is walked, and query t's step ballots only
-// its own lanes -- its keys are already in (distance, grid order).  The
-// serial state (matched distance and F2 -> F1 match, packed) and the matches
-// live in LDS: ~25 bytes per keypoint, so the block does not hold off the
-// extraction's blocks it runs beside.
+// what it reads into LDS first (the pair's level-0 list, the query list) and
+// finish the orientation filter and the outputs after it.  The top-K lists
+// stay in global memory: lanes 8t..8t+7 of the wave hold the keys of query
+// j0 + t of a run of 8 queries (one gather per run), the next run is in
+// flight while this one is walked, and query t's step ballots only its own
+// lanes -- its keys are already in (distance, grid order) and carry the F2
+// feature and the rotation bin.  The serial state (matched distance and
+// F2 -> F1 match, packed) and the matches live in LDS: ~17 bytes per
+// keypoint, so the block does not hold off the extraction's blocks it runs
+// beside.
 constexpr int kSfiThreads = 256;
 #ifndef ORB_SFI_TOPK_ST
 #define ORB_SFI_TOPK_ST 1
