@@ -4,7 +4,9 @@
 Metric (BASELINE.json): frames/s ORB extract+match (752x480, 1000 feat),
 keypoints/descriptors bit-exact.  One step = one batch of B distinct
 synthetic 752x480 frames of a panning camera (synth.global_sequence), resident in
-HBM before the timed region:
+HBM before the timed region; consecutive steps rotate through a ring of
+--ring batches (default 4 x 256 frames = 370 MB, more than the 256 MB
+Infinity Cache), so no step reads the frames the step before it read:
 ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
 on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
 F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
@@ -24,11 +26,18 @@ Extra objects on the JSON line:
                traffic = HBM bytes per launch of the same kernel from the committed
                rocprofv3 PMC summary (FETCH_SIZE x2 per the gfx950 note +
                WRITE_SIZE; tools/pmc_profile.sh, same command/config), and
-               valu_issue_frac = its VALU wave-instructions / (2 per CU per
-               cycle) from the same summary: the FAST pass is VALU-bound.
-  stage_roofline  achieved GB/s of each stage on its algorithmic bytes, and the
-               north-star pass (pyramid + FAST read bytes, R = 2*sum(P) - P_7
-               per frame) against the HBM peak.
+               valu_roofline_frac = its VALU wave-instructions per launch (PMC)
+               / (2 per CU per cycle x 256 CUs x the PMC clock x this run's
+               launch time): the FAST pass is VALU-bound.
+  stage_roofline  per stage (one kernel each): algorithmic bytes and their
+               fraction of the HBM peak, the PMC bytes (FETCH_SIZE x2 +
+               WRITE_SIZE of that kernel) over this run's launch time, and the
+               VALU roofline fraction; the pyramid's algorithmic bytes are
+               level 0 read once + levels 1..7 written once (sum(P)), with
+               SURVEY §8(d)'s per-level figure (read P_0..P_6 + write
+               P_1..P_7) beside it; describe's are the 43 x 43 raw patch read
+               + 36 B written per keypoint; and the north-star pass (pyramid +
+               FAST read bytes, R = 2*sum(P) - P_7 per frame).
   cpu_baseline the CPU oracle (oracle/, "port") on the host, rank 0, N=1,
                on a bounded sample of the same frames, threads stated; its
                outputs double as a parity check of the sampled frames.
@@ -52,7 +61,12 @@ W, H, NFEAT, LAP = 752, 480, 1000, (0, 1000)
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
 PMC_SUMMARY = ROOT / "profiles" / "pmc_summary_latest.csv"
 METRIC = "frames/s ORB extract+match (752×480, 1000 feat) @1/2/4/8 GPU; bit-exact kp/desc"
-STAGES = ["pyramid", "fast_cells", "quadtree", "blur", "describe", "assemble"]
+STAGES = ["pyramid", "fast_cells", "quadtree", "describe", "assemble"]
+STAGE_KERNEL = {"pyramid": "k_pyr_stream", "fast_cells": "k_fast_cells", "quadtree": "k_quadtree",
+                "describe": "k_describe", "assemble": "k_assemble"}
+PMC_FRAMES_PER_LAUNCH = 256     # tools/pmc_profile.sh runs the default config
+CUS = 256
+DESC_BYTES_PER_KP = 43 * 43 + 4 + 32   # k_describe: raw 43x43 patch read; angle + descriptor written
 
 
 def parse():
@@ -61,6 +75,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
+    ap.add_argument("--ring", type=int, default=4,
+                    help="distinct input batches the steps rotate through (4 x 256 frames exceed the 256 MB "
+                         "Infinity Cache, so every step reads cold frames)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the CPU-baseline pool (0 = the cores this process may run on, at most 16)")
@@ -133,23 +150,48 @@ def level_pixels(ex):
     return sum(level_sizes(ex))
 
 
-def stage_roofline(ex, stage_ms, frames_per_launch, kps_per_frame):
-    """Achieved GB/s of each stage on its algorithmic bytes:
-    pyramid reads levels 0..L-2 and writes 1..L-1; FAST reads every level once;
-    the north-star pass (pyramid + FAST) reads R = 2*sum(P) - P_{L-1} per frame;
-    blur reads and writes every level once (2 sum(P)); describe reads the raw
-    IC_Angle disc rows (31 x 36 B) and the blurred 37 x 37 square (37 x 40 B)
-    and writes 36 B per keypoint."""
+def pmc_figures(row, ms, frames_per_launch):
+    """PMC bytes and VALU roofline fraction of one kernel from its PMC summary
+    row (per dispatch at PMC_FRAMES_PER_LAUNCH frames, scaled to this run's
+    launch) over this run's launch time `ms`."""
+    if not row or ms <= 0:
+        return {}
+    scale = frames_per_launch / PMC_FRAMES_PER_LAUNCH
+    out = {}
+    if row.get("fetch_MB_x2") and row.get("write_MB"):
+        b = (float(row["fetch_MB_x2"]) + float(row["write_MB"])) * 1024 * 1024 * scale
+        out["pmc_bytes_per_launch"] = b
+        out["pmc_frac"] = b / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    if row.get("valu_per_wave") and row.get("waves") and row.get("clock_GHz"):
+        wi = float(row["valu_per_wave"]) * float(row["waves"]) * scale        # VALU wave-instructions per launch
+        out["valu_roofline_frac"] = wi / (2 * CUS * float(row["clock_GHz"]) * 1e9 * ms * 1e-3)
+    return out
+
+
+def stage_roofline(ex, stage_ms, frames_per_launch, kps_per_frame, pmc_path):
+    """Per stage: algorithmic bytes and their HBM fraction,
+    PMC bytes and VALU fraction (pmc_figures).  Algorithmic bytes per frame:
+    pyramid sum(P) (level 0 read once, levels 1..L-1 written once; SURVEY's
+    per-level figure sum(P[:-1]) + sum(P[1:]) as survey_*), FAST sum(P) (every
+    level pixel read once), describe (43 x 43 + 36) B per keypoint.  The
+    north-star pass (pyramid + FAST) reads R = 2*sum(P) - P_{L-1} per frame."""
     P = level_sizes(ex)
-    per_frame = {"pyramid": sum(P[:-1]) + sum(P[1:]), "fast_cells": sum(P), "blur": 2 * sum(P),
-                 "describe": (31 * 36 + 37 * 40 + 36) * kps_per_frame}
+    per_frame = {"pyramid": sum(P), "fast_cells": sum(P), "quadtree": None,
+                 "describe": DESC_BYTES_PER_KP * kps_per_frame, "assemble": None}
     out = {}
     for k, b in per_frame.items():
         ms = float(stage_ms.get(k) or 0)
-        if ms > 0:
+        if ms <= 0:
+            continue
+        e = {"kernel": STAGE_KERNEL[k], "ms": ms}
+        if b is not None:
             gbs = b * frames_per_launch / (ms * 1e-3) / 1e9
-            out[k] = {"bytes_per_launch": b * frames_per_launch, "ms": ms, "achieved_GBs": gbs,
-                      "frac": gbs / HBM_PEAK_GBS}
+            e.update({"bytes_per_launch": b * frames_per_launch, "achieved_GBs": gbs, "frac": gbs / HBM_PEAK_GBS})
+        e.update(pmc_figures(pmc_row(pmc_path, STAGE_KERNEL[k]), ms, frames_per_launch))
+        if k == "pyramid":
+            sb = (sum(P[:-1]) + sum(P[1:])) * frames_per_launch
+            e.update({"survey_bytes_per_launch": sb, "survey_frac": sb / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS})
+        out[k] = e
     ms = float(stage_ms.get("pyramid") or 0) + float(stage_ms.get("fast_cells") or 0)
     if ms > 0:
         r = (2 * sum(P) - P[-1]) * frames_per_launch
@@ -305,8 +347,14 @@ def main():
     # the pair across each shard seam and the job matches all N*B-1 pairs
     # with no data-path collective; the halo frame is not counted in `value`.
     Bx = B + (1 if rank < world - 1 else 0)
-    frames_np = synth.global_sequence(W, H, rank * B, Bx, config=2)
-    frames = torch.from_numpy(frames_np).to(dev)
+    # ring batch j of rank r holds global frames (j*world + r)*B ...: every
+    # frame of the job is distinct, and the seam halo of batch j is frame 0
+    # of rank r+1's batch j
+    R = max(1, args.ring)
+    ring_first = [(j * world + rank) * B for j in range(R)]
+    ring_np = [synth.global_sequence(W, H, f0, Bx, config=2) for f0 in ring_first]
+    ring = [torch.from_numpy(a).to(dev) for a in ring_np]
+    frames_np, frames = ring_np[0], ring[0]
     exs = [orb.ORBextractor(NFEAT, 1.2, 8, 20, 7, device=local) for _ in range(args.overlap)]
     ex = exs[0]
     L = capi.lib()
@@ -369,6 +417,7 @@ def main():
     def step(timed=False):
         i = counter[0] % nsets
         h = counter[0] % args.overlap                   # --overlap 2: consecutive steps alternate handles
+        frames = ring[counter[0] % R]                   # a different input batch than the step before
         counter[0] += 1
         k_, d_, n_, m_ = outs[i]
         xe, xs = exs[h], xstreams[h]
@@ -429,11 +478,12 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
 
+    last_slot = (counter[0] - 1) % R                    # the ring batch of the last step
     if args.dump:
         # the last step's outputs of this rank, with global frame / pair indices
         last = outs_dev[(counter[0] - 1) % nsets]
         Path(args.dump).mkdir(parents=True, exist_ok=True)
-        np.savez(Path(args.dump) / f"rank{rank}.npz", first=rank * B, frames=Bx, world=world,
+        np.savez(Path(args.dump) / f"rank{rank}.npz", first=ring_first[last_slot], frames=Bx, world=world,
                  kps=last[0].cpu().numpy(), desc=last[1].cpu().numpy(), n=last[2].cpu().numpy(),
                  mono=last[3].cpu().numpy(), nmatch=nmatch.cpu().numpy(), matches=matches.cpu().numpy())
     if rank == 0:
@@ -442,24 +492,21 @@ def main():
         px = level_pixels(ex)                          # algorithmic bytes per frame of the FAST pass
         fast_ms = float(stage_ms[1])
         achieved = (px * frames_per_launch / (fast_ms * 1e-3)) / 1e9 if fast_ms > 0 else None
-        pmc = pmc_row(args.pmc_summary, "k_fast_cells")
-        traffic = valu = None
-        if pmc and pmc.get("fetch_MB_x2") and pmc.get("write_MB"):
-            traffic = (float(pmc["fetch_MB_x2"]) + float(pmc["write_MB"])) * 1024 * 1024
-        if pmc and pmc.get("valu_issue_frac"):
-            valu = float(pmc["valu_issue_frac"])
+        pf = pmc_figures(pmc_row(args.pmc_summary, "k_fast_cells"), fast_ms, frames_per_launch)
+        traffic = pf.get("pmc_bytes_per_launch")
         roof = {"kernel": "k_fast_cells", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
                 "bytes_per_launch": px * frames_per_launch, "ms_per_launch": fast_ms,
                 "frames_per_launch": frames_per_launch,
                 "traffic_source": (os.path.relpath(args.pmc_summary, ROOT) if traffic else None),
-                "valu_issue_frac": valu}
+                "valu_roofline_frac": pf.get("valu_roofline_frac")}
         out = {"metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
-                          "frames_per_step_per_gpu": B, "streams": args.streams, "overlap": args.overlap, "pipeline": args.pipeline,
+                          "frames_per_step_per_gpu": B, "input_ring_batches": R,
+                          "input_ring_MB": round(R * Bx * W * H / 2**20, 1), "streams": args.streams, "overlap": args.overlap, "pipeline": args.pipeline,
                           "sfi_after_stage": args.sfi_after if args.pipeline else None,
                           "output_sets": nsets if args.pipeline else 1,
                           "parallelism": f"frames sharded over {world} GPU(s), halo frame per seam"},
@@ -468,13 +515,14 @@ def main():
                                                           if match_events else None)},
                "roofline": roof,
                "stage_roofline": stage_roofline(ex, dict(zip(STAGES, map(float, stage_ms))), frames_per_launch,
-                                                float(n.float().mean().item()))}
+                                                float(n.float().mean().item()), args.pmc_summary)}
         if world == 1 and args.cpu_sample > 0:
             from oracle import oracle as O
             ns = min(args.cpu_sample, B)
             avail = len(os.sched_getaffinity(0))
             threads = args.cpu_threads or min(16, avail)
             lib_path, flags = O.fast_variant()
+            frames_np = ring_np[last_slot]             # the frames of the output set compared below
             fps, outs, nms = cpu_baseline(frames_np[:ns], threads, lib_path)
             fps1, n1 = cpu_single_thread(frames_np[:ns], lib_path)
             # parity of the sampled frames (the CPU leg doubles as a checker):

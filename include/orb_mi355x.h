@@ -169,25 +169,14 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
  * the original index (within array i) of the element the sort puts at j;
  * fallback[i] = 1 where the depth limit sent the array to the sequential port
  * (the heap-sort case).  Returns ORB_OK, ORB_ERR_PARAM or ORB_ERR_DEVICE. */
-/* The blurred level (GaussianBlur 7x7, sigma 2, REFLECT_101 of the level,
- * ORBextractor.cc:1132-1133, as k_blur_levels wrote it for k_describe_pb) of
- * frame `frame` of the last extraction on the handle (orbx_extract: frame 0),
- * w x h bytes at dst with row step dst_step (dst may be NULL to query w/h).
- * ORB_ERR_UNSUPPORTED unless the
- * handle was created with ORB_DESC_PREBLUR=1 in the environment (the
- * alternative describe path: the level blurred once, then sampled; off by
- * default).  Test hook, not part of the reference interface. */
-int orbx_debug_blur_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int* w,
-                          int* h_);
-
 int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* cnt, const int32_t* x0,
                     int32_t* perm, int32_t* fallback);
 
 /* Per-stage HIP-event timing of subsequent orbx_extract* calls (on the stream
  * they run on).  orbx_get_profile sums, over the recorded calls, the stage
- * times in ms: [0] pyramid, [1] FAST cells, [2] quadtree, [3] level blur
- * (k_blur_levels), [4] describe (orientation + rBRIEF), [5] assemble; returns
- * the number of calls and clears the record.  Not part of the reference interface. */
+ * times in ms: [0] pyramid, [1] FAST cells, [2] quadtree, [3] describe
+ * (orientation + rBRIEF), [4] assemble; returns the number of calls and clears
+ * the record.  Not part of the reference interface. */
 int orbx_set_profiling(orbx_handle* h, int enable);
 int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages);
 
@@ -201,14 +190,36 @@ int orbx_set_streams(orbx_handle* h, int nsub);
 /* Pyramid kernel of subsequent extractions (results identical for every
  * choice): 0 auto (k_pyr_stream for batches of >= 32 frames, k_pyramid row
  * bands below that), 1 k_pyramid, 2 k_pyr_stream (one workgroup sliding down
- * each frame) whenever the image size allows it, 3 per-level k_resize, 4
- * k_pyr_level (one launch per level, a wave per run of rows) whenever the
- * size and the frames' 4-byte alignment allow it.  orbx_pyramid_kernel returns
- * the kernel (1-4) the last extraction on the handle ran, 0 before any.  The
- * environment variable ORB_PYR_MODE sets a new handle's mode.  Not part of
- * the reference interface. */
+ * each frame) whenever the image size allows it.  orbx_pyramid_kernel returns
+ * the kernel (1 or 2) the last extraction on the handle ran, 0 before any.
+ * Not part of the reference interface. */
 int orbx_set_pyramid_mode(orbx_handle* h, int mode);
 int orbx_pyramid_kernel(orbx_handle* h);
+
+/* Alternative kernel forms for parity tests and A/B runs (test hooks, not part
+ * of the reference interface; process-wide, read when a call is issued).
+ * Every form gives identical results; the defaults (0) are the measured
+ * fastest, and the alternatives are also the forms a size falls back to when
+ * the default's LDS tables do not fit.
+ *   ORB_OPT_PROJ_FORM    projection searches: 0 top-K + speculative resolve,
+ *                        1 top-K + serial resolve, 2 single-wave search
+ *   ORB_OPT_BOW_FORM     map-wide SearchByBoW: 0 lane per keyframe feature
+ *                        (k_bowk_*) when the map carries its totals, 1 k_bow
+ *   ORB_OPT_BOWK_BIG     0 auto, 1 no big-node resolve form (every frame node
+ *                        in the 256-thread form)
+ *   ORB_OPT_PYR_CNT_END  k_pyr_stream's step counters at the top of its LDS
+ *                        allocation instead of inside the table image
+ * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
+ * (-1 for an unknown option). */
+enum {
+    ORB_OPT_PROJ_FORM = 0,
+    ORB_OPT_BOW_FORM = 1,
+    ORB_OPT_BOWK_BIG = 2,
+    ORB_OPT_PYR_CNT_END = 3,
+    ORB_OPT_COUNT = 4
+};
+int orb_debug_set_option(int option, int value);
+int orb_debug_get_option(int option);
 
 /* Pipeline control for work overlapped with extraction: subsequent
  * extractions on the handle record `event` (a hipEvent_t, NULL = none) on
@@ -369,6 +380,16 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f,
                                     const orbm_featvec* ffv, float nnratio, int check_ori,
                                     int32_t* d_match, int32_t* d_nmatches, void* stream);
+
+/* The batched device searches (orbm_search_by_bow_batch_device,
+ * orbm_search_for_initialization_batch_device) keep their scratch between
+ * calls, one set per (device, stream) of the calling thread; at most a few
+ * sets stay allocated (the least recently used is freed after a device
+ * synchronisation).  This frees the calling thread's sets for `stream` on the
+ * current device (all = 1: every set of the thread) after a device
+ * synchronisation.  Call it before destroying a stream these calls used.
+ * Returns ORB_OK or ORB_ERR_DEVICE. */
+int orbm_release_scratch(void* stream, int all);
 
 /* Map points projected into F (the fields ORBmatcher reads from MapPoint,
  * MapPoint.h mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos, mbTrackInView,

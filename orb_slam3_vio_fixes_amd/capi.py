@@ -5,6 +5,7 @@ every entry point raises.  The shared object is built in-tree by build.py.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from pathlib import Path
 
@@ -14,7 +15,7 @@ LIB_PATH = Path(__file__).resolve().parent / "liborb_mi355x.so"
 
 EXPORTS = [
     "orbx_create", "orbx_destroy", "orbx_get_tables", "orbx_max_keypoints", "orbx_extract", "orbx_extract_batch",
-    "orbx_get_level", "orbx_get_batch_level", "orbx_debug_math", "orbx_debug_sort", "orbx_set_host_pyramid", "orbx_debug_blur_level",
+    "orbx_get_level", "orbx_get_batch_level", "orbx_debug_math", "orbx_debug_sort", "orbx_set_host_pyramid",
     "orbx_extract_batch_device", "orbx_debug_stage", "orbm_descriptor_distance", "orbm_search_for_initialization",
     "orbm_search_for_initialization_batch_device", "orbm_search_by_bow", "orbm_search_by_projection_mps",
     "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device", "orbm_search_by_bow_many", "orbm_kf_map_fv_desc",
@@ -26,8 +27,12 @@ EXPORTS = [
     "orbm_search_by_bow_kf", "orbm_search_by_projection_kf", "orbm_search_by_projection_sim3",
     "orbm_search_by_sim3", "orbm_fuse_sim3", "orbm_search_by_bow_fisheye", "orbm_search_by_projection_mps_fisheye",
     "orbm_search_by_projection_last_fisheye", "orbx_set_pyramid_mode", "orbx_pyramid_kernel", "orbv_transform_device",
-    "orbx_set_stage_event",
+    "orbx_set_stage_event", "orb_debug_set_option", "orb_debug_get_option",
+    "orbm_release_scratch",
 ]
+
+# orb_debug_set_option keys (include/orb_mi355x.h): alternative kernel forms
+ORB_OPT_PROJ_FORM, ORB_OPT_BOW_FORM, ORB_OPT_BOWK_BIG, ORB_OPT_PYR_CNT_END = 0, 1, 2, 3
 
 _lib = None
 
@@ -48,7 +53,6 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_debug_math.argtypes = [i32, i32, C.c_longlong, C.c_longlong, i32, i32, vp]
     L.orbx_debug_sort.argtypes = [i32, i32, vp, vp, vp, vp, vp]
     L.orbx_set_host_pyramid.argtypes = [vp, i32]
-    L.orbx_debug_blur_level.argtypes = [vp, i32, i32, vp, C.c_size_t, vp, vp]
     L.orbx_extract_batch_device.argtypes = [vp, i32, vp, sz, sz, i32, i32, i32, i32, vp, vp, i32, vp, vp, vp]
     L.orbx_debug_stage.argtypes = [vp, i32, vp, i32, vp]
     L.orbm_descriptor_distance.argtypes = [vp, vp]
@@ -69,6 +73,9 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_pyramid_kernel.argtypes = [vp]
     L.orbv_transform_device.argtypes = [vp, i32, vp, i32, vp, vp, vp, vp]
     L.orbx_set_stage_event.argtypes = [vp, i32, vp]
+    L.orb_debug_set_option.argtypes = [i32, i32]
+    L.orb_debug_get_option.argtypes = [i32]
+    L.orbm_release_scratch.argtypes = [vp, i32]
     L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]
     L.orbm_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
     L.orbm_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]
@@ -119,3 +126,16 @@ def check(rc: int, what: str) -> int:
                  abi.ORB_ERR_DEVICE: "HIP device error", abi.ORB_ERR_UNSUPPORTED: "unsupported configuration"}
         raise RuntimeError(f"{what} failed: {names.get(rc, rc)}")
     return rc
+
+
+@contextlib.contextmanager
+def debug_option(option: int, value: int):
+    """Selects an alternative kernel form (orb_debug_set_option, a test hook)
+    for the duration of the block, then restores the previous value."""
+    L = lib()
+    old = L.orb_debug_get_option(option)
+    check(L.orb_debug_set_option(option, value), "orb_debug_set_option")
+    try:
+        yield
+    finally:
+        L.orb_debug_set_option(option, old)

@@ -13,6 +13,10 @@ namespace orbmi {
 
 constexpr int kWave = 64;
 
+// orb_debug_set_option's process-wide table (matcher.hip): alternative kernel
+// forms for parity tests; every product default is 0
+int debug_opt(int option);
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 // wave index within the block, made wave-uniform (SGPR) so per-wave indexing
 // of global tables compiles to scalar loads

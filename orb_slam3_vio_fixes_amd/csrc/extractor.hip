@@ -3,18 +3,21 @@
 // Replaces ORB_SLAM3::ORBextractor (reference include/ORBextractor.h:43-109,
 // src/ORBextractor.cc:409-1195) behind the C ABI of include/orb_mi355x.h.
 //
-// Per batch of same-size frames the path is seven kinds of launches, all
-// batched over frames (one grid dimension indexes the frame):
-//   k_resize       level l from level l-1, OpenCV INTER_LINEAR 8U fixed point
-//   k_fast_cells   one wave per FAST cell: LDS-staged ROI, FAST-9 score map,
-//                  cell-local 3x3 NMS at iniThFAST / minThFAST, ballot compaction
+// Per batch of same-size frames the path is five launches, all batched over
+// frames (one grid dimension indexes the frame):
+//   k_pyr_stream   ComputePyramid: one workgroup per frame slides down it once
+//                  with LDS row rings (k_pyramid row bands for small batches)
+//   k_fast_cells   one wave per 2 FAST cells: LDS-staged ROI, compass
+//                  pre-test, FAST-9 scores, cell-local 3x3 NMS at iniThFAST /
+//                  minThFAST, ballot compaction
 //   k_quadtree     one workgroup per (frame, level): DistributeOctTree as
 //                  data-parallel passes over the node list + exact std::sort
-//   k_describe     one wave per keypoint: LDS raw patch, IC_Angle moments,
-//                  7x7 fixed-point blur of the 37x37 patch only, glibc-exact
-//                  sincosf, 256 rBRIEF tests
+//   k_describe     one wave per run of keypoint slots: raw patch in registers,
+//                  IC_Angle moments, the 7x7 fixed-point blur of the 37x37
+//                  patch only (horizontal pass on v_mfma_i32_16x16x64_i8),
+//                  glibc-exact sincosf, 256 rBRIEF tests
 //   k_assemble     per frame: scaling, lapping partition (monoIndex), output
-// Everything is integer/bitwise; no MFMA.
+// Everything is integer/bitwise and bit-exact against the reference.
 #include "../../include/orb_mi355x.h"
 #include "common.h"
 #include "orb_math.h"
@@ -147,7 +150,7 @@ static int pyr_group_lds(const PyrGroup& g) { return g.lds_a + g.lds_b + g.lds_x
 
 // Tap tables and launch groups of k_pyramid.  Groups: greedily the longest
 // run of levels (at most 4) whose bands of >= 8 top-level rows fit the LDS
-// budget; ORB_PYR_GROUPS="la-lb:R,..." overrides (A/B experiments).
+// budget.
 static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int4>& bands, std::vector<int>& xs,
                           std::vector<uint32_t>& xw, std::vector<int2>& yt) {
     const int L = P.L;
@@ -168,27 +171,11 @@ static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int
         }
     }
     P.pgroups.clear();
-    std::vector<std::array<int, 3>> req;
-    if (const char* env = std::getenv("ORB_PYR_GROUPS")) {
-        int la, lb, R, n = 0;
-        const char* q = env;
-        while (std::sscanf(q, "%d-%d:%d%n", &la, &lb, &R, &n) == 3) {
-            req.push_back({la, lb, R});
-            q += n;
-            if (*q == ',') ++q;
-        }
-    }
     std::vector<int4> bt;
     int la = 0;
-    size_t ri = 0;
     while (la < L - 1) {
         PyrGroup g{};
         bool ok = false;
-        if (ri < req.size() && req[ri][0] == la && req[ri][1] > la && req[ri][1] < L && req[ri][2] > 0) {
-            g.la = la; g.lb = req[ri][1]; g.R = req[ri][2];
-            ok = pyr_bands(P, yt, g.la, g.lb, g.R, bt, g.lds_a, g.lds_b, g.lds_x, g.lds_y) <= 160 * 1024;
-            ++ri;
-        }
         for (int span = 4; span >= 1 && !ok; --span) {
             const int lb = std::min(L - 1, la + span);
             for (int R : {32, 24, 16, 12, 8, 6, 4, 2, 1}) {
@@ -212,6 +199,9 @@ static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int
 
 constexpr int kPyrStreamMinFrames = 32;   // below this a frame per CU leaves the chip idle: row bands
 constexpr int kPsRun = 4;                 // k_pyr_stream: output rows per run (one lane, one column group)
+#ifndef ORB_PYR_K0
+#define ORB_PYR_K0 0
+#endif
 
 // k_pyr_stream layout for level-0 chunks of K0 rows: runs the step schedule
 // (level l computes at step s every row whose two source rows of level l-1
@@ -275,7 +265,7 @@ static long long pyr_stream_schedule(const Plan& P, const std::vector<int2>& row
     return bytes;
 }
 
-// Column records of level l (>= 1) for k_pyr_stream / k_pyr_level: per group
+// Column records of level l (>= 1) for k_pyr_stream: per group
 // of 4 output columns the weights (16 a0 | 16 a1 << 16) of each output, the
 // v_perm selectors that place (S[sx] << 8, S[sx+1] << 8) in a u16 pair from
 // the 3 dwords at the group's first tap dword bd, and bd | window flags << 16
@@ -304,43 +294,6 @@ static bool pyr_col_records(const Plan& P, const std::vector<int2>& tab, int l, 
         rec[8 * ng + g] = (uint32_t)bd | (flags << 16);
     }
     return true;
-}
-
-// k_pyr_level plan: column records of every level, and per level the run
-// length R (output rows per wave) such that a run's source rows fit kPlNS.
-static void build_pyr_level(Plan& P, const std::vector<int2>& tab, const std::vector<int2>& yt,
-                            std::vector<uint32_t>& col) {
-    PyrLevelPlan& Q = P.pl;
-    Q = PyrLevelPlan();
-    col.clear();
-    const int L = P.L;
-    for (int l = 1; l < L; ++l) {
-        const LevelDev& d = P.lv[l];
-        std::vector<uint32_t> rec;
-        if (!pyr_col_records(P, tab, l, rec)) return;
-        const int ng = (d.w + 3) / 4;
-        // dword loads of 3 dwords at bd stay inside the source row's pitch
-        // (level 0: the kernel clamps them in the buffer's last row)
-        if (l >= 2)
-            for (int g = 0; g < ng; ++g)
-                if (4 * (int)(rec[8 * ng + g] & 0xffff) + 12 > P.lv[l - 1].pitch) return;
-        Q.col_off[l] = (int)col.size();
-        col.insert(col.end(), rec.begin(), rec.end());
-        col.resize(round_up((int)col.size(), 4), 0u);
-        int R = 0;
-        for (int r = kPlRmax; r >= 1 && !R; --r) {
-            bool fits = true;
-            for (int y0 = 0; y0 < d.h && fits; y0 += r) {
-                const int y1 = std::min(d.h, y0 + r);
-                fits = (yt[d.ytab + y1 - 1].x >> 16) - (yt[d.ytab + y0].x & 0xffff) + 1 <= kPlNS;
-            }
-            if (fits) R = r;
-        }
-        if (!R) return;
-        Q.R[l] = R;
-        Q.runs[l] = (d.h + R - 1) / R;
-    }
-    Q.ok = true;
 }
 
 // The k_pyr_stream plan: table image (column records, row records) and
@@ -376,9 +329,8 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
         const int ng = (P.lv[l].w + 3) / 4;
         rec_dw += round_up(9 * ng, 4) + 4 * P.lv[l].h;
     }
-    int k0_env = 0, run_rows = kPsRun;
-    if (const char* e = std::getenv("ORB_PYR_K0")) k0_env = std::atoi(e);
-    if (const char* e = std::getenv("ORB_PYR_RUN")) run_rows = std::max(1, std::min(kPsRun, std::atoi(e)));
+    // ORB_PYR_K0 (build flag, A/B): force the level-0 chunk rows (0: the largest that fits)
+    const int k0_env = ORB_PYR_K0, run_rows = kPsRun;
     const int nq16 = (P.lv[0].w + 15) / 16;
     int tab_dw = 0;
     for (int k : {32, 24, 16, 12, 8, 6, 4}) {
@@ -421,10 +373,11 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
         rdw += PS.ring_rows[m] * PS.ring_pitch[m] / 4;
     }
     if (rdw >= 65536) return;                              // row records hold 16-bit dword offsets
-    // ORB_PYR_CNT_END=1 (test knob): the per-step counters after the rings, at
-    // the top of the allocation, outside the copied table image (the kernel
-    // zeroes them there); the default keeps them at dword 0 of the image
-    if (const char* e = std::getenv("ORB_PYR_CNT_END"); e && e[0] == '1') {
+    // ORB_OPT_PYR_CNT_END (test hook, orb_debug_set_option): the per-step
+    // counters after the rings, at the top of the allocation, outside the copied
+    // table image (the kernel zeroes them there); the default keeps them at dword
+    // 0 of the image
+    if (debug_opt(ORB_OPT_PYR_CNT_END)) {
         PS.cnt_dw = rdw;
         rdw += round_up(PS.nsteps, 4);
     }
@@ -480,7 +433,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         // levels narrower than 46 px are refused here (the 35-px cell check
         // below refuses the rest of that range).
         if (d.w < 2 * kEdge + 8 || d.h < 2 * kEdge + 8) return ORB_ERR_UNSUPPORTED;
-        // 12 bytes of slack: k_pyr_level reads 3 dwords from a tap's dword
+        // 12 bytes of slack past the level's last pixel
         d.pitch = round_up(d.w + 12, 64);
         d.off = l == 0 ? 0 : poff;
         if (l > 0) poff += (long long)d.pitch * d.h;
@@ -585,32 +538,12 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     std::vector<uint32_t> pxw;
     std::vector<int2> pyt;
     build_pyramid(P, tab, pband, pxs, pxw, pyt);
-    std::vector<uint32_t> psimg, plcol;
+    std::vector<uint32_t> psimg;
     std::vector<int4> pssteps;
     build_pyr_stream(P, tab, psimg, pssteps);
-    build_pyr_level(P, tab, pyt, plcol);
     for (const PyrGroup& g : P.pgroups)
         if (pyr_group_lds(g) > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
     P.pyr_bytes = poff;
-    // blurred levels 0..L-1 of a frame (k_blur_levels), 64-byte rows with >= 12
-    // bytes of slack past the level (k_describe's 10-dword patch rows)
-    std::vector<int4> bitems;
-    {
-        long long boff = 0;
-        for (int l = 0; l < L; ++l) {
-            LevelDev& d = P.lv[l];
-            d.bpitch = round_up(d.w + 12, 64);
-            d.boff = boff;
-            boff += (long long)d.bpitch * d.h;
-            const int nd = (d.w + 3) / 4;
-            for (int g0 = 0; g0 < nd; g0 += kBlurDw)
-                for (int y0 = 0; y0 < d.h; y0 += kBlurRows)
-                    bitems.push_back(make_int4(l, g0, y0, std::min(kBlurRows, d.h - y0)));
-        }
-        P.blur_bytes = round_up((int)std::min<long long>(boff, 1ll << 30), 256);
-        if (boff >= (1ll << 30)) return ORB_ERR_UNSUPPORTED;
-        P.nblur_items = (int)bitems.size();
-    }
     P.ncells = cellsum;
     P.slot_total = slotsum;
     P.out_total = outsum;
@@ -618,9 +551,6 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
 
     const size_t B = (size_t)maxB;
     ORB_CHECK(hipMalloc(&P.d_pyr, std::max<size_t>(1, B * P.pyr_bytes)));
-    if (hd->preblur) ORB_CHECK(hipMalloc(&P.d_blur, B * P.blur_bytes + 256));
-    ORB_CHECK(hipMalloc(&P.d_blur_items, bitems.size() * sizeof(int4)));
-    ORB_CHECK(hipMemcpy(P.d_blur_items, bitems.data(), bitems.size() * sizeof(int4), hipMemcpyHostToDevice));
     ORB_CHECK(hipMalloc(&P.d_in, P.in_pitch * h));
     ORB_CHECK(hipMalloc(&P.d_tab, std::max<size_t>(1, tab.size()) * sizeof(int2)));
     ORB_CHECK(hipMalloc(&P.d_lv, L * sizeof(LevelDev)));
@@ -650,10 +580,6 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         ORB_CHECK(hipMemcpy(P.d_pxs, pxs.data(), pxs.size() * sizeof(int), hipMemcpyHostToDevice));
         ORB_CHECK(hipMemcpy(P.d_pxw, pxw.data(), pxw.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         ORB_CHECK(hipMemcpy(P.d_pyt, pyt.data(), pyt.size() * sizeof(int2), hipMemcpyHostToDevice));
-    }
-    if (P.pl.ok) {
-        ORB_CHECK(hipMalloc(&P.d_pcol, plcol.size() * sizeof(uint32_t)));
-        ORB_CHECK(hipMemcpy(P.d_pcol, plcol.data(), plcol.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     if (P.ps.ok) {
         ORB_CHECK(hipMalloc(&P.d_ps_tab, psimg.size() * sizeof(uint32_t)));
@@ -692,46 +618,6 @@ typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t x) { return __builtin_bit_cast(u16x2, x); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 x) { return __builtin_bit_cast(uint32_t, x); }
 __device__ __forceinline__ int round_up_d(int x, int m) { return (x + m - 1) / m * m; }
-
-// ---------------------------------------------------------------------------
-// k_resize: cv::resize INTER_LINEAR 8UC1.  One output row per
-// wave, lanes over consecutive columns (coalesced byte taps and stores); four
-// rows per block.  The column taps and weights are recomputed in registers
-// with the host table's exact double/float steps (build_plan): a table load per
-// pixel cost a third of the kernel's time.  Row taps come from the table.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_resize(const uint8_t* __restrict__ src, long long s_fstride, int s_pitch,
-                                                int sw, int sh, uint8_t* __restrict__ dst, long long d_fstride,
-                                                int d_pitch, int dw, int dh, double scx,
-                                                const int2* __restrict__ yt, int xmax) {
-    const int dy = blockIdx.x * 4 + wave_id();
-    if (dy >= dh) return;
-    const long long f = blockIdx.y;
-    const uint8_t* S = src + f * s_fstride;
-    uint8_t* D = dst + f * d_fstride + (long long)dy * d_pitch;
-    const int2 ty = yt[dy];
-    const int r0 = min(max(ty.x, 0), sh - 1), r1 = min(max(ty.x + 1, 0), sh - 1);
-    const int b0 = (short)(ty.y & 0xffff), b1 = ty.y >> 16;
-    const uint8_t* S0 = S + (long long)r0 * s_pitch;
-    const uint8_t* S1 = S + (long long)r1 * s_pitch;
-    for (int dx = lane_id(); dx < dw; dx += kWave) {
-        float fx = (float)((dx + 0.5) * scx - 0.5);
-        int sx = (int)floorf(fx);
-        fx -= (float)sx;
-        if (sx < 0) { fx = 0.f; sx = 0; }
-        if (sx >= sw - 1) { fx = 0.f; sx = sw - 1; }
-        const int a0 = (int)rintf((1.f - fx) * 2048.f), a1 = (int)rintf(fx * 2048.f);
-        int h0, h1;
-        if (dx < xmax) {
-            h0 = S0[sx] * a0 + S0[sx + 1] * a1;
-            h1 = S1[sx] * a0 + S1[sx + 1] * a1;
-        } else {
-            h0 = S0[sx] * 2048;
-            h1 = S1[sx] * 2048;
-        }
-        D[dx] = (uint8_t)((((b0 * (h0 >> 4)) >> 16) + ((b1 * (h1 >> 4)) >> 16) + 2) >> 2);
-    }
-}
 
 // ---------------------------------------------------------------------------
 // k_pyramid: ComputePyramid (ORBextractor.cc:1170-1195) for levels la+1..lb
@@ -937,7 +823,7 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
     if (f >= a.nframes) return;
     const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     for (int i = tid; i < a.tab_u4; i += 1024) ps_lds[i] = a.tab[i];
-    if (a.cnt_dw >= 4 * a.tab_u4)                    // counters outside the image (ORB_PYR_CNT_END)
+    if (a.cnt_dw >= 4 * a.tab_u4)                    // counters outside the image (ORB_OPT_PYR_CNT_END)
         for (int i = tid; i < a.nsteps; i += 1024) lds[a.cnt_dw + i] = 0;
     lds_barrier();
     // lane l: level l's {column records, row records} dword offsets
@@ -1018,7 +904,7 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
             // wave-items are taken from a per-step LDS counter: waves that drew
             // cheap items take more, so the step ends when the work does.  The
             // counters are zeroes of the copied table image (dword 0 on); with
-            // ORB_PYR_CNT_END=1 they sit at the top of the allocation and are
+            // ORB_OPT_PYR_CNT_END they sit at the top of the allocation and are
             // zeroed above.  (Round 2 blamed a failing end-of-LDS layout on the
             // hardware; tests/test_gpu_configs.py runs that layout, zeroed,
             // bit-exact -- see DESIGN.md on the cause.)
@@ -1110,104 +996,6 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
         lds_barrier();
     }
 #undef PS_FETCH
-}
-
-// ---------------------------------------------------------------------------
-// k_pyr_level: level l of ComputePyramid (ORBextractor.cc:1170-1195) from
-// level l-1 in HBM for every frame, cv::resize INTER_LINEAR 8UC1 (SURVEY.md
-// A.1); one launch per level, no LDS and no barrier.
-//
-// A wave owns 64 column groups (4 outputs each) of a run of R output rows of
-// one frame.  The run's row taps are wave-uniform (scalar loads); its source
-// rows are consecutive, so every one of them is requested at once (3 dwords
-// per lane and row, <= kPlNS rows in flight), then each source row is resized
-// horizontally ONCE -- the perm/dot2 form of k_pyr_stream gives 4096 h per
-// output -- and every output row whose bottom tap is that row is finished
-// from it and the row before: at scale 1.2 a source row serves ~1.2 output
-// rows instead of being recomputed for each.
-// ---------------------------------------------------------------------------
-struct PyrLevelArgs {
-    const uint8_t* src;
-    long long src_fstride;
-    int src_pitch, src_h, src_dwords;   // dwords of a source row holding pixels
-    uint8_t* dst;
-    long long dst_fstride;
-    int dst_pitch;
-    const uint32_t* col;                // W[4 ng] | S[4 ng] | BF[ng]
-    const int2* rows;                   // per output row: r0 | r1 << 16 (clamped), b0 | b1 << 16
-    int ng, nchunk, runs, R, h, nframes;
-    int guard_last;                     // clamp the loads of the buffer's last source row
-};
-
-__global__ __launch_bounds__(256) void k_pyr_level(PyrLevelArgs a) {
-    const int gw = blockIdx.x * 4 + wave_id();
-    const int per_frame = a.runs * a.nchunk;
-    const int f = gw / per_frame;
-    if (f >= a.nframes) return;
-    const int rem = gw - f * per_frame, run = rem / a.nchunk, ch = rem - run * a.nchunk;
-    const int lane = lane_id();
-    const int gi = ch * kWave + lane;
-    const bool active = gi < a.ng;
-    const int g = min(gi, a.ng - 1);
-    // row taps as 64-bit words {r0 | r1 << 16, b0 | b1 << 16}, read by scalar loads
-    typedef __attribute__((address_space(4))) const unsigned long long* ConstRows;
-    const ConstRows rows = (ConstRows)a.rows;
-    const int y0 = run * a.R, y1 = min(a.h, y0 + a.R);
-    const int rbase = (int)(rows[y0] & 0xffff), nsrc = (int)((rows[y1 - 1] >> 16) & 0xffff) - rbase + 1;
-    const uint4 wt = ((const uint4*)a.col)[g];
-    const uint4 sl = ((const uint4*)a.col)[a.ng + g];
-    const uint32_t bf = a.col[8 * a.ng + g];
-    const int bd = bf & 0xffff;
-    const bool hi3 = (bf >> 19) & 1;
-    const uint8_t* S = a.src + f * a.src_fstride + (long long)rbase * a.src_pitch;
-    uint32_t D[kPlNS][3];
-    const bool guard = a.guard_last && f == a.nframes - 1;
-#pragma unroll
-    for (int k = 0; k < kPlNS; ++k) {
-        if (k < nsrc) {
-            const uint8_t* p = S + (long long)k * a.src_pitch;
-            if (guard && rbase + k == a.src_h - 1) {
-                // the buffer's last row: no dword past its last pixel dword
-                const uint32_t* q = (const uint32_t*)p;
-                const int last = a.src_dwords - 1;
-                D[k][0] = q[min(bd, last)]; D[k][1] = q[min(bd + 1, last)]; D[k][2] = q[min(bd + 2, last)];
-            } else {
-                const uint32_t* q = (const uint32_t*)p + bd;
-                D[k][0] = q[0]; D[k][1] = q[1]; D[k][2] = q[2];
-            }
-        }
-    }
-    uint8_t* O = a.dst + f * a.dst_fstride + 4 * g;
-    uint32_t hP[4] = {0, 0, 0, 0}, hC[4] = {0, 0, 0, 0};
-    int y = y0;
-#pragma unroll
-    for (int k = 0; k < kPlNS; ++k) {
-        if (k < nsrc) {
-#pragma unroll
-            for (int c = 0; c < 4; ++c) hP[c] = hC[c];
-            const uint32_t d0 = D[k][0], d1 = D[k][1], d2 = D[k][2];
-            hC[0] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.x)), as_u16x2(wt.x), 0u, false);
-            hC[1] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.y)), as_u16x2(wt.y), 0u, false);
-            hC[2] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(d1, d0, sl.z)), as_u16x2(wt.z), 0u, false);
-            hC[3] = __builtin_amdgcn_udot2(as_u16x2(__builtin_amdgcn_perm(hi3 ? d2 : d1, hi3 ? d1 : d0, sl.w)),
-                                           as_u16x2(wt.w), 0u, false);
-            // every output row whose bottom tap is this source row
-            while (y < y1) {
-                const unsigned long long e = rows[y];
-                const int r0 = (int)(e & 0xffff), r1 = (int)((e >> 16) & 0xffff);
-                if (r1 != rbase + k) break;
-                const uint32_t b0 = (uint32_t)(e >> 32) & 0xffff, b1 = (uint32_t)(e >> 48);
-                uint32_t out = 0;
-#pragma unroll
-                for (int c = 0; c < 4; ++c) {
-                    const uint32_t x0 = __umul24(b0, (r0 == r1 ? hC[c] : hP[c]) >> 16), x1 = __umul24(b1, hC[c] >> 16);
-                    out |= (((x0 >> 16) + (x1 >> 16) + 2) >> 2) << (8 * c);
-                }
-                if (active) *(uint32_t*)(O + (long long)y * a.dst_pitch) = out;
-                ++y;
-            }
-        }
-    }
 }
 
 // ---------------------------------------------------------------------------
@@ -2177,9 +1965,11 @@ __device__ int wave_partition(SortRec* a, int f, int l, int* Lp, int* Rp) {
 }
 
 // std::sort(a, a + m) under compareNodes by the whole workgroup: levels of
-// disjoint ranges partitioned by one wave each, then a stable insertion sort
-// per leaf by one thread each (std_sort_levels, orb_math.h, checked against
-// std::sort on the host).  Where the reference would heap-sort (depth limit),
+// disjoint ranges partitioned by one wave each, then every leaf (<= 16
+// records) put in stable order by 16 lanes, each placing one record at its
+// rank -- the permutation the final insertion sort gives (std_sort_levels,
+// orb_math.h, states it sequentially and is checked against std::sort on the
+// host).  Where the reference would heap-sort (depth limit),
 // the original array is restored and sorted by the sequential port.
 __device__ void block_std_sort(SortRec* a, int m, SortRec* backup, int* Lp, int* Rp, SortFrame* qa, SortFrame* qb,
                                int* leaves, int* ctl, SortFrame* stk) {
@@ -2706,8 +2496,6 @@ struct DescArgs {
     int fma;
     int kern[7];
     int umax[16];
-    const uint8_t* blur;            // blurred levels (k_describe_pb)
-    long long blur_fstride;
 };
 
 // One keypoint slot of the flat (frame, quadtree output) space: qt_key, angle
@@ -3259,339 +3047,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
 }
 
 // ---------------------------------------------------------------------------
-// k_blur_levels: the level blur of ORBextractor::operator() --
-// GaussianBlur(workingMat, workingMat, Size(7,7), 2, 2, BORDER_REFLECT_101)
-// on a clone() of every level (ORBextractor.cc:1132-1133) -- for every frame,
-// into the blurred slab d_blur, with the fixed-point separable kernel of
-// SURVEY.md A.5 (k_describe's arithmetic: ufixedpoint16 horizontal sums,
-// ufixedpoint32 vertical sums, +2^15 >> 16, saturate).
-//
-// One wave per item = kBlurDw dword columns x kBlurRows rows of a level.
-// Lane i holds dword column g = g0 - 1 + i: per source row it loads 8 bytes
-// with one dwordx2 and picks its 4 columns -- REFLECT_101 applied -- by one
-// v_perm whose selector was made once (the identity inside the level; at the
-// borders the reflected columns, which always lie in two adjacent dwords);
-// its neighbours' dwords arrive by DPP wave_shr:1 / wave_shl:1, so lanes
-// 1..62 output 4 columns each and no lane branches on the border.  The
-// kBlurRows + 6 source rows (REFLECT_101 row index) are all requested before
-// any is used; each gives 4 horizontal sums by 10 v_dot4_u32_u8 with
-// byte-placed taps, a row is paired with the next as u16 pairs, and each
-// output is three v_dot2_u32_u16 and one v_mad_u32_u24.
-// HBM: every level pixel read once (the 6-row halo between items and the
-// 2-dword overlap between column strips hit L2), every blurred pixel written
-// once: 2 ΣP per frame.
-// ---------------------------------------------------------------------------
-struct BlurArgs {
-    const uint8_t* in;
-    long long in_fstride;
-    int in_pitch;
-    const uint8_t* pyr;
-    long long pyr_fstride;
-    uint8_t* blur;
-    long long blur_fstride;
-    const LevelDev* lv;
-    const int4* items;
-    int nitems;
-    uint32_t hw[10];    // horizontal taps as bytes (k_describe's hw layout)
-    uint32_t vw[3];     // vertical taps as u16 pairs (k0 k1) (k2 k3) (k2 k1); k0 alone for the 7th
-    uint32_t k0;
-};
-
-typedef unsigned int u32x2v __attribute__((ext_vector_type(2)));
-typedef __attribute__((address_space(1))) const u32x2v* GlobalPairs;
-
-__global__ __launch_bounds__(256) void k_blur_levels(BlurArgs a) {
-    int bunit, bframe;
-    xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
-    const int item = __builtin_amdgcn_readfirstlane(bunit * 4 + wave_id());
-    bframe = __builtin_amdgcn_readfirstlane(bframe);
-    if (item >= a.nitems) return;
-    typedef __attribute__((address_space(4))) const int* ConstInts;
-    typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
-    const ConstInts itp = (ConstInts)a.items + 4 * item;
-    const int l = itp[0], g0 = itp[1], y0 = itp[2], nr = itp[3];
-    const ConstLevels lvc = (ConstLevels)a.lv;
-    const int w = lvc[l].w, h = lvc[l].h;
-    const GlobalBytes src = (GlobalBytes)(l == 0 ? a.in + bframe * a.in_fstride
-                                                 : a.pyr + bframe * a.pyr_fstride + lvc[l].off);
-    const int pitch = l == 0 ? a.in_pitch : lvc[l].pitch;
-    uint8_t* dst = a.blur + bframe * a.blur_fstride + lvc[l].boff;
-    const int bp = lvc[l].bpitch;
-    const int lane = lane_id(), nd = (w + 3) >> 2;
-    const int g = g0 - 1 + lane;
-    // this lane's columns 4g .. 4g+3 (g clamped to [-1, nd]: lanes past it are
-    // never read), REFLECT_101, as bytes of the dword pair at dword column ca
-    int ca;
-    uint32_t sel;
-    {
-        const int gc = min(max(g, -1), nd);
-        int sk[4], smin = 1 << 30;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            int c = 4 * gc + k;
-            c = c < 0 ? -c : (c >= w ? 2 * w - 2 - c : c);
-            c = min(max(c, 0), w - 1);
-            sk[k] = c;
-            smin = min(smin, c);
-        }
-        ca = min(smin >> 2, nd - 2);
-        sel = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) sel |= (uint32_t)(sk[k] - 4 * ca) << (8 * k);
-    }
-    const bool out_lane = lane >= 1 && lane <= kBlurDw && g < nd;
-    // every source row first
-    u32x2v raw[kBlurRows + 6];
-#pragma unroll
-    for (int i = 0; i < kBlurRows + 6; ++i) {
-        int y = y0 - 3 + i;
-        y = y < 0 ? -y : (y >= h ? 2 * h - 2 - y : y);
-        y = min(max(y, 0), h - 1);
-        raw[i] = *(GlobalPairs)(src + (long long)y * pitch + 4 * ca);
-    }
-    uint32_t hv[kBlurRows + 6][4];
-#pragma unroll
-    for (int i = 0; i < kBlurRows + 6; ++i) {
-        const uint32_t e = __builtin_amdgcn_perm(raw[i].y, raw[i].x, sel);
-        const uint32_t em = __builtin_amdgcn_update_dpp(0u, e, 0x138, 0xf, 0xf, false);   // wave_shr:1
-        const uint32_t ep = __builtin_amdgcn_update_dpp(0u, e, 0x130, 0xf, 0xf, false);   // wave_shl:1
-        // columns 4g-3 .. 4g+6 as three words
-        const uint32_t w0 = __builtin_amdgcn_alignbyte(e, em, 1u), w1 = __builtin_amdgcn_alignbyte(ep, e, 1u);
-        const uint32_t w2 = ep >> 8;
-        hv[i][0] = __builtin_amdgcn_udot4(w1, a.hw[1], __builtin_amdgcn_udot4(w0, a.hw[0], 0u, false), false);
-        hv[i][1] = __builtin_amdgcn_udot4(w1, a.hw[3], __builtin_amdgcn_udot4(w0, a.hw[2], 0u, false), false);
-        hv[i][2] = __builtin_amdgcn_udot4(
-            w2, a.hw[6], __builtin_amdgcn_udot4(w1, a.hw[5], __builtin_amdgcn_udot4(w0, a.hw[4], 0u, false), false),
-            false);
-        hv[i][3] = __builtin_amdgcn_udot4(
-            w2, a.hw[9], __builtin_amdgcn_udot4(w1, a.hw[8], __builtin_amdgcn_udot4(w0, a.hw[7], 0u, false), false),
-            false);
-    }
-    if (!out_lane) return;
-    // rows i, i+1 as u16 pairs (every horizontal sum < 2^16)
-    uint32_t pr[kBlurRows + 5][4];
-#pragma unroll
-    for (int i = 0; i < kBlurRows + 5; ++i)
-#pragma unroll
-        for (int b = 0; b < 4; ++b) pr[i][b] = hv[i][b] | (hv[i + 1][b] << 16);
-#pragma unroll
-    for (int o = 0; o < kBlurRows; ++o) {
-        uint32_t out = 0;
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            uint32_t acc = __builtin_amdgcn_udot2(as_u16x2(pr[o][b]), as_u16x2(a.vw[0]), 32768u, false);
-            acc = __builtin_amdgcn_udot2(as_u16x2(pr[o + 2][b]), as_u16x2(a.vw[1]), acc, false);
-            acc = __builtin_amdgcn_udot2(as_u16x2(pr[o + 4][b]), as_u16x2(a.vw[2]), acc, false);
-            acc += __umul24(hv[o + 6][b], a.k0);
-            out |= min(acc >> 16, 255u) << (8 * b);
-        }
-        if (o < nr) *(uint32_t*)(dst + (long long)(y0 + o) * bp + 4 * g) = out;
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_describe_pb: computeOrientation/IC_Angle (ORBextractor.cc:76-103,471-478)
-// and computeOrbDescriptor (:107-146) on the blurred levels k_blur_levels
-// wrote.  Off by default (orbx_handle::preblur, env ORB_DESC_PREBLUR=1):
-// measured slower end to end, DESIGN.md §8.
-//
-// One wave per keypoint, the next valid keypoint's inputs always in flight in
-// registers: the raw IC_Angle disc (31 rows; lane r loads row r as two
-// dwordx4 and a dword from the aligned column at or left of x - 15) and the
-// 37 x 37 blurred square around it (rows y - 18 .. y + 18, 10 aligned dwords
-// each; 6 dwords per lane), which lands in the wave's 1.5 KB of LDS.  Every
-// keypoint is >= 19 px inside its level (the FAST window), so neither ever
-// leaves the level: no border path.  IC_Angle by byte dot products of the
-// disc rows (integer, order-free sums), then the 512 samples are single LDS
-// byte reads at the rotated pattern points; lane l evaluates tests 4l..4l+3.
-// Per keypoint 1,116 B of raw disc rows and 1,480 B of blurred rows.
-// ---------------------------------------------------------------------------
-constexpr int kIcRows = 2 * kHalfPatch + 1, kBlSq = 37, kBlDw = 10, kBlN = kBlSq * kBlDw;
-constexpr int kBlV = (kBlN + kWave - 1) / kWave;   // 6
-
-struct DescLanePb {
-    uint64_t img, bimg;
-    int pitch, bpitch;
-    uint32_t key;
-};
-
-struct DescKpPb {
-    const uint8_t* img;
-    const uint8_t* bimg;
-    int pitch, bpitch;
-    uint32_t key;
-};
-
-__device__ __forceinline__ bool desc_lane_pb(const DescArgs& a, long long s, DescLanePb& k) {
-    const int f = (int)(s / a.out_total);
-    const int o = (int)(s - (long long)f * a.out_total);
-    const int l = a.slot_level[o];
-    const LevelDev& lv = a.lv[l];
-    if (o - lv.out_base >= a.qt_n[f * a.L + l]) return false;
-    k.img = (uint64_t)(l == 0 ? a.in + f * a.in_fstride : a.pyr + f * a.pyr_fstride + lv.off);
-    k.pitch = l == 0 ? a.in_pitch : lv.pitch;
-    k.bimg = (uint64_t)(a.blur + f * a.blur_fstride + lv.boff);
-    k.bpitch = lv.bpitch;
-    k.key = a.qt_key[s];
-    return true;
-}
-
-__device__ __forceinline__ DescKpPb desc_pick_pb(const DescLanePb& k, int j) {
-    auto rl64 = [&](uint64_t v) {
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), j);
-        return ((uint64_t)hi << 32) | lo;
-    };
-    DescKpPb d;
-    d.img = (const uint8_t*)rl64(k.img);
-    d.bimg = (const uint8_t*)rl64(k.bimg);
-    d.pitch = __builtin_amdgcn_readlane(k.pitch, j);
-    d.bpitch = __builtin_amdgcn_readlane(k.bpitch, j);
-    d.key = (uint32_t)__builtin_amdgcn_readlane((int)k.key, j);
-    return d;
-}
-
-typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(1))) const u32x4v* GlobalQuads;
-
-__device__ __forceinline__ void pb_issue(const DescKpPb& k, uint32_t (&rv)[9], uint32_t (&bv)[kBlV]) {
-    const int lane = lane_id();
-    const int cx = (int)(k.key & 0xfff) + (kEdge - 3), cy = (int)((k.key >> 12) & 0xfff) + (kEdge - 3);
-    if (lane < kIcRows) {
-        const GlobalBytes rp = (GlobalBytes)k.img + (long long)(cy - kHalfPatch + lane) * k.pitch + ((cx - kHalfPatch) & ~3);
-        const u32x4v q0 = *(GlobalQuads)rp, q1 = *(GlobalQuads)(rp + 16);
-        rv[0] = q0.x; rv[1] = q0.y; rv[2] = q0.z; rv[3] = q0.w;
-        rv[4] = q1.x; rv[5] = q1.y; rv[6] = q1.z; rv[7] = q1.w;
-        rv[8] = *(GlobalWords)(rp + 32);
-    }
-    const GlobalBytes bp0 = (GlobalBytes)k.bimg + (long long)(cy - 18) * k.bpitch + ((cx - 18) & ~3);
-#pragma unroll
-    for (int j = 0; j < kBlV; ++j) {
-        const int i = lane + j * kWave;
-        if (i < kBlN) {
-            const int r = (i * 6554) >> 16, d = i - r * kBlDw;   // i / 10 for i < 16384
-            bv[j] = *(GlobalWords)(bp0 + (int)__umul24(r, k.bpitch) + 4 * d);
-        }
-    }
-}
-
-template <bool FMA>
-__global__ __launch_bounds__(256) void k_describe_pb(DescArgs a) {
-    __shared__ __attribute__((aligned(16))) uint32_t bl_s[4][kBlN + 2];
-    const int lane = lane_id(), wv = wave_id();
-    const uint4 patv = ((const uint4*)c_pattern)[lane];
-    asm volatile("" ::"v"(patv.x), "v"(patv.y), "v"(patv.z), "v"(patv.w));
-    const uint32_t patw[4] = {patv.x, patv.y, patv.z, patv.w};
-    uint32_t* bl = bl_s[wv];
-    int um_s[kHalfPatch + 1];
-#pragma unroll
-    for (int v = 0; v <= kHalfPatch; ++v) um_s[v] = __builtin_amdgcn_readfirstlane(a.umax[v]);
-    // lane r < 31 holds disc row v = r - 15: byte b of its aligned word j is
-    // u = 4j + b - 15; masks of |u| <= umax[|v|], weights u + 15
-    uint32_t icm[8];
-    {
-        const int av = lane >= kHalfPatch ? lane - kHalfPatch : kHalfPatch - lane;
-        int um = -1;
-#pragma unroll
-        for (int k = 0; k <= kHalfPatch; ++k)
-            if (av == k) um = um_s[k];
-        if (lane >= kIcRows) um = -1;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            uint32_t m = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int u = 4 * j + b - kHalfPatch;
-                if (u >= -um && u <= um) m |= 0xffu << (8 * b);
-            }
-            icm[j] = m;
-        }
-    }
-    int bunit, bframe;
-    xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
-    const int lb = (bunit * 4 + wv) * kDescSlots;
-    const long long s_begin = (long long)bframe * a.out_total + lb;
-    const int nrun = max(0, min(kDescSlots, a.out_total - lb));
-    DescLanePb mine{};
-    const bool valid = lane < nrun && desc_lane_pb(a, s_begin + lane, mine);
-    uint64_t todo = __ballot(valid);
-    uint32_t rv[9], bv[kBlV];
-    DescKpPb cur{}, nxt{};
-    int jc = -1, jn = -1;
-    auto take = [&](int& j, DescKpPb& k) {
-        j = -1;
-        if (!todo) return;
-        j = __builtin_ctzll(todo);
-        todo &= todo - 1;
-        k = desc_pick_pb(mine, j);
-        pb_issue(k, rv, bv);
-    };
-    take(jc, cur);
-    while (jc >= 0) {
-        const long long s = s_begin + jc;
-        const int cx = (int)(cur.key & 0xfff) + (kEdge - 3);
-        // the current keypoint's registers -> LDS (blurred square) and locals (disc rows)
-#pragma unroll
-        for (int j = 0; j < kBlV; ++j) {
-            const int i = lane + j * kWave;
-            if (i < kBlN) bl[i] = bv[j];
-        }
-        uint32_t al[8];
-        {
-            const uint32_t sh = (uint32_t)((cx - kHalfPatch) & 3);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) al[j] = __builtin_amdgcn_alignbyte(rv[j + 1], rv[j], sh);
-        }
-        take(jn, nxt);
-        // IC_Angle (ORBextractor.cc:76-103): per disc row sum I and sum (u + 15) I
-        uint32_t s1 = 0, sw = 0;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            uint32_t wgt = 0;
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int u = 4 * j + b - kHalfPatch;
-                if (u <= kHalfPatch) wgt |= (uint32_t)(u + kHalfPatch) << (8 * b);
-            }
-            const uint32_t px = al[j] & icm[j];
-            s1 = __builtin_amdgcn_udot4(px, 0x01010101u, s1, false);
-            sw = __builtin_amdgcn_udot4(px, wgt, sw, false);
-        }
-        int m10 = (int)sw - kHalfPatch * (int)s1;
-        int m01 = (lane - kHalfPatch) * (int)s1;
-        m10 = wave_sum_dpp(m10);
-        m01 = wave_sum_dpp(m01);
-        const float ang_deg = fast_atan2_deg((float)m01, (float)m10);
-        float sb, ca;
-        glibc_sincosf(deg_to_rad(ang_deg), &sb, &ca);
-        wave_sync();
-        // rBRIEF: each sample one byte of the blurred square, centre (18, 18)
-        const uint8_t* C = (const uint8_t*)bl + ((cx - 18) & 3) + 18 * (4 * kBlDw) + 18;
-        int nib = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            int val[2];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-                const float x = (float)(int)(int8_t)(patw[q] >> (16 * e));
-                const float y = (float)(int)(int8_t)(patw[q] >> (16 * e + 8));
-                int r, c;
-                brief_offset(x, y, sb, ca, FMA, r, c);
-                val[e] = C[r * (4 * kBlDw) + c];
-            }
-            nib |= (val[0] < val[1]) << q;
-        }
-        const int hi = __shfl_down(nib, 1, kWave);
-        uint8_t* d = a.sdesc + s * 32;
-        if ((lane & 1) == 0) d[lane >> 1] = (uint8_t)(nib | (hi << 4));
-        if (lane == 0) a.angle[s] = ang_deg;
-        jc = jn;
-        cur = nxt;
-        wave_sync();
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_debug_math: the device compile of k_describe's scalar math over whole
 // input domains, as chunk hashes (orbx_debug_math; host side: the oracle with
 // the system libm, tests/test_gpu_math.py).  One workgroup per chunk.
@@ -3750,7 +3205,6 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells; P.d_slot_level = P0.d_slot_level;
     const long long F = f0;
     P.d_pyr = P0.d_pyr + F * P0.pyr_bytes;
-    P.d_blur = P0.d_blur + F * P0.blur_bytes;
     P.d_cell_count = P0.d_cell_count + F * P0.ncells;
     P.d_cell_keys = P0.d_cell_keys + F * P0.slot_total;
     P.d_key_scr = P0.d_key_scr + F * P0.slot_total;
@@ -3767,19 +3221,11 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     d_mono += F;
     std::vector<hipEvent_t> marks;
     int stage_no = 0;
-    auto mark = [&](bool pub = true) {
+    auto mark = [&]() {
         // caller's pipeline events (orbx_set_stage_event): recorded after stage k
-        // (the blur stage's own boundary is a profiling mark only; without the
-        // level blur it is a null mark: a zero-length stage, nothing recorded)
-        if (pub) {
-            hipEvent_t ue = hd->stage_ev[std::min(stage_no++, 5)];
-            if (ue) (void)hipEventRecord(ue, st);
-        }
+        hipEvent_t ue = hd->stage_ev[std::min(stage_no++, 5)];
+        if (ue) (void)hipEventRecord(ue, st);
         if (!hd->profiling) return;
-        if (!pub && !hd->preblur) {
-            marks.push_back(nullptr);
-            return;
-        }
         if (hd->ev_next >= hd->ev_pool.size()) {
             hipEvent_t e;
             if (hipEventCreate(&e) != hipSuccess) return;
@@ -3792,32 +3238,9 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     mark();
     // pyramid
     const int pm = hd->pyr_mode;
-    const bool legacy_pyr = pm == 3;
     const bool use_stream = P0.ps.ok && (pm == 2 || (pm == 0 && B >= kPyrStreamMinFrames));
-    const bool al4 = (((uintptr_t)d_frames | (uintptr_t)pitch0 | (uintptr_t)(B > 1 ? fstride : 0)) & 3) == 0;
-    const bool use_level = P0.pl.ok && al4 && pm == 4;
-    hd->pyr_last = legacy_pyr ? 3 : (use_level ? 4 : (use_stream ? 2 : 1));
-    if (!legacy_pyr && use_level) {
-        for (int l = 1; l < L; ++l) {
-            const LevelDev& d = P.lv[l];
-            const LevelDev& sv = P.lv[l - 1];
-            PyrLevelArgs la;
-            la.src = l == 1 ? d_frames : P.d_pyr + sv.off;
-            la.src_fstride = l == 1 ? fstride : P.pyr_bytes;
-            la.src_pitch = l == 1 ? pitch0 : sv.pitch;
-            la.src_h = sv.h;
-            la.src_dwords = (sv.w + 3) / 4;
-            la.dst = P.d_pyr + d.off; la.dst_fstride = P.pyr_bytes; la.dst_pitch = d.pitch;
-            la.col = P0.d_pcol + P0.pl.col_off[l];
-            la.rows = P0.d_pyt + d.ytab;
-            la.ng = (d.w + 3) / 4;
-            la.nchunk = (la.ng + kWave - 1) / kWave;
-            la.runs = P0.pl.runs[l]; la.R = P0.pl.R[l]; la.h = d.h; la.nframes = B;
-            la.guard_last = l == 1;
-            const long long nw = (long long)B * la.runs * la.nchunk;
-            hipLaunchKernelGGL(k_pyr_level, dim3((unsigned)((nw + 3) / 4)), dim3(256), 0, st, la);
-        }
-    } else if (!legacy_pyr && use_stream) {
+    hd->pyr_last = use_stream ? 2 : 1;
+    if (use_stream) {
         const PyrStream& S = P0.ps;
         PyrStreamArgs pa;
         pa.src = d_frames; pa.src_fstride = fstride; pa.src_pitch = pitch0;
@@ -3830,7 +3253,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
         pa.ring0_dw = S.ring_dw[0]; pa.ring0_rows = S.ring_rows[0]; pa.ring0_pitch = S.ring_pitch[0];
         pa.cnt_dw = S.cnt_dw;
         hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(1024), S.lds_bytes, st, pa);
-    } else if (!legacy_pyr) {
+    } else {
         for (const PyrGroup& g : P.pgroups) {
             PyrArgs pa;
             if (g.la == 0) {
@@ -3848,63 +3271,13 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
             const unsigned nwg = (unsigned)((B + 7) / 8 * 8 * g.nb);
             hipLaunchKernelGGL(k_pyramid, dim3(nwg), dim3(256), pyr_group_lds(g), st, pa);
         }
-    } else
-    for (int l = 1; l < L; ++l) {
-        const LevelDev& d = P.lv[l];
-        const LevelDev& s = P.lv[l - 1];
-        const uint8_t* src = l == 1 ? d_frames : P.d_pyr + s.off;
-        const long long sfs = l == 1 ? fstride : P.pyr_bytes;
-        const int sp = l == 1 ? pitch0 : s.pitch;
-        const int2* xt = P.d_tab + P.tab_off[l];
-        const double scx = 1. / ((double)d.w / s.w);          // as build_plan / cv::resize
-        hipLaunchKernelGGL(k_resize, dim3((d.h + 3) / 4, B), dim3(256), 0, st, src, sfs, sp, s.w, s.h,
-                           P.d_pyr + d.off, P.pyr_bytes, d.pitch, d.w, d.h, scx, xt + d.w, P.xmax[l]);
     }
     mark();
-    // level blur (GaussianBlur of every level, k_blur_levels): needs only the
-    // pyramid, so it runs on a side stream beside FAST and the quadtree
     int kern[7];
     {
         // every tap < 128: k_describe's matrix-core horizontal pass takes them as i8
         static const int ked[7] = {18, 34, 48, 56, 48, 34, 18}, kleg[7] = {18, 34, 49, 55, 49, 34, 18};
         for (int t = 0; t < 7; ++t) kern[t] = hd->prm.blur_variant == 1 ? kleg[t] : ked[t];
-    }
-    const orbx_handle::BlurSide* bside = nullptr;
-    if (hd->preblur) {
-    hipStream_t bst = st;
-    if (hd->blur_fork) {
-        orbx_handle::BlurSide* sd = nullptr;
-        for (auto& b : hd->blur_side)
-            if (b.caller == st) sd = &b;
-        if (!sd) {
-            orbx_handle::BlurSide b{st, nullptr, nullptr, nullptr};
-            ORB_CHECK(hipStreamCreateWithFlags(&b.st, hipStreamNonBlocking));
-            ORB_CHECK(hipEventCreateWithFlags(&b.fork, hipEventDisableTiming));
-            ORB_CHECK(hipEventCreateWithFlags(&b.join, hipEventDisableTiming));
-            hd->blur_side.push_back(b);
-            sd = &hd->blur_side.back();
-        }
-        ORB_CHECK(hipEventRecord(sd->fork, st));
-        ORB_CHECK(hipStreamWaitEvent(sd->st, sd->fork, 0));
-        bst = sd->st;
-        bside = sd;
-    }
-    {
-        BlurArgs ba;
-        ba.in = d_frames; ba.in_fstride = fstride; ba.in_pitch = pitch0;
-        ba.pyr = P.d_pyr; ba.pyr_fstride = P.pyr_bytes;
-        ba.blur = P.d_blur; ba.blur_fstride = P0.blur_bytes;
-        ba.lv = P.d_lv; ba.items = P0.d_blur_items; ba.nitems = P0.nblur_items;
-        const uint32_t k0 = kern[0], k1 = kern[1], k2 = kern[2], k3 = kern[3];
-        const uint32_t hw[10] = {k0 | (k1 << 8) | (k2 << 16) | (k3 << 24), k2 | (k1 << 8) | (k0 << 16),
-                                 (k0 << 8) | (k1 << 16) | (k2 << 24), k3 | (k2 << 8) | (k1 << 16) | (k0 << 24),
-                                 (k0 << 16) | (k1 << 24), k2 | (k3 << 8) | (k2 << 16) | (k1 << 24), k0,
-                                 k0 << 24, k1 | (k2 << 8) | (k3 << 16) | (k2 << 24), k1 | (k0 << 8)};
-        for (int t = 0; t < 10; ++t) ba.hw[t] = hw[t];
-        ba.vw[0] = k0 | (k1 << 16); ba.vw[1] = k2 | (k3 << 16); ba.vw[2] = k2 | (k1 << 16); ba.k0 = k0;
-        hipLaunchKernelGGL(k_blur_levels, dim3((unsigned)((P0.nblur_items + 3) / 4), (unsigned)B), dim3(256), 0, bst, ba);
-    }
-    if (bside) ORB_CHECK(hipEventRecord(bside->join, bst));
     }
     // FAST cells
     FastArgs fa;
@@ -3954,15 +3327,10 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     hipLaunchKernelGGL(k_quadtree, dim3(L, B), dim3(256), qt_lds_bytes(P), st, qa);
 #endif
     mark();
-    // the blurred levels are complete (profiling stage "blur": the join's wait,
-    // or k_blur_levels itself when it runs in line)
-    if (bside) ORB_CHECK(hipStreamWaitEvent(st, bside->join, 0));
-    mark(false);
     // describe
     DescArgs da;
     da.in = d_frames; da.in_fstride = fstride; da.in_pitch = pitch0;
     da.pyr = P.d_pyr; da.pyr_fstride = P.pyr_bytes;
-    da.blur = P.d_blur; da.blur_fstride = P0.blur_bytes;
     for (int t = 0; t < 7; ++t) da.kern[t] = kern[t];
     da.lv = P.d_lv; da.qt_key = P.d_qt_key; da.qt_n = P.d_qt_n;
     da.angle = P.d_angle; da.sdesc = P.d_sdesc; da.out_total = P.out_total; da.L = L;
@@ -3970,13 +3338,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     for (int v = 0; v < 16; ++v) da.umax[v] = hd->umax[v];
     da.slot_level = P.d_slot_level;
     da.nslots = (long long)B * P.out_total;
-    if (hd->preblur) {
-        const dim3 pgrid((unsigned)((P.out_total + 4 * kDescSlots - 1) / (4 * kDescSlots)), (unsigned)B);
-        hipLaunchKernelGGL(da.fma ? k_describe_pb<true> : k_describe_pb<false>, pgrid, dim3(256), 0, st, da);
-    } else {
-        const dim3 dgrid((unsigned)((P.out_total + kDescWpb * kDescSlots - 1) / (kDescWpb * kDescSlots)), (unsigned)B);
-        hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(kWave * kDescWpb), 0, st, da);
-    }
+    const dim3 dgrid((unsigned)((P.out_total + kDescWpb * kDescSlots - 1) / (kDescWpb * kDescSlots)), (unsigned)B);
+    hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(kWave * kDescWpb), 0, st, da);
     mark();
     // assemble
     AsmArgs aa;
@@ -4047,9 +3410,6 @@ orbx_handle* orbx_create(const orbx_params* p, int device) {
     orbx_handle* h = new orbx_handle();
     h->prm = *p;
     h->device = device;
-    if (const char* e = std::getenv("ORB_PYR_MODE")) h->pyr_mode = std::min(4, std::max(0, std::atoi(e)));   // A/B runs
-    if (const char* e = std::getenv("ORB_BLUR_FORK")) h->blur_fork = e[0] != '0';                        // A/B runs
-    if (const char* e = std::getenv("ORB_DESC_PREBLUR")) h->preblur = e[0] == '1';
     init_tables(h);
     return h;
 }
@@ -4062,11 +3422,6 @@ void orbx_destroy(orbx_handle* h) {
     for (hipEvent_t e : h->sub_done) (void)hipEventDestroy(e);
     for (hipStream_t s : h->sub_streams) (void)hipStreamDestroy(s);
     if (h->fork_ev) (void)hipEventDestroy(h->fork_ev);
-    for (auto& b : h->blur_side) {
-        (void)hipEventDestroy(b.fork);
-        (void)hipEventDestroy(b.join);
-        (void)hipStreamDestroy(b.st);
-    }
     if (h->batch_done) (void)hipEventDestroy(h->batch_done);
     if (h->st_scratch) (void)hipFree(h->st_scratch);
     if (h->hb_dev) (void)hipFree(h->hb_dev);
@@ -4333,7 +3688,7 @@ int orbx_set_profiling(orbx_handle* h, int enable) {
 }
 
 int orbx_set_pyramid_mode(orbx_handle* h, int mode) {
-    if (!h || mode < 0 || mode > 4) return ORB_ERR_PARAM;
+    if (!h || mode < 0 || mode > 2) return ORB_ERR_PARAM;
     h->pyr_mode = mode;
     h->x_key[4] = -1;                       // the captured single-image graph holds the old choice
     return ORB_OK;
@@ -4369,10 +3724,8 @@ int orbx_get_profile(orbx_handle* h, float* stage_ms, int nstages) {
         if (m.size() < 2) continue;
         ORB_CHECK(hipEventSynchronize(m.back()));
         for (size_t i = 0; i + 1 < m.size() && (int)i < nstages; ++i) {
-            if (!m[i + 1]) continue;                          // a null mark closes an empty stage
-            const hipEvent_t a = m[i] ? m[i] : m[i - 1];      // the stage after it starts at the mark before
             float ms = 0.f;
-            ORB_CHECK(hipEventElapsedTime(&ms, a, m[i + 1]));
+            ORB_CHECK(hipEventElapsedTime(&ms, m[i], m[i + 1]));
             stage_ms[i] += ms;
         }
         ++calls;
@@ -4476,24 +3829,6 @@ int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, siz
     const size_t sp = level == 0 ? (size_t)h->last_pitch0 : (size_t)d.pitch;
     if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
-    return ORB_OK;
-}
-
-int orbx_debug_blur_level(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int* w, int* hh) {
-    if (!h || level < 0 || level >= h->plan.L || frame < 0) return ORB_ERR_PARAM;
-    const int nb = h->last_frames ? h->last_B : (h->have_last ? 1 : 0);
-    if (frame >= nb) return ORB_ERR_PARAM;
-    if (!h->preblur) return ORB_ERR_UNSUPPORTED;
-    const Plan& P = h->plan;
-    const LevelDev& d = P.lv[level];
-    if (w) *w = d.w;
-    if (hh) *hh = d.h;
-    if (!dst) return ORB_OK;
-    (void)hipSetDevice(h->device);
-    if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
-    ORB_CHECK(hipDeviceSynchronize());
-    ORB_CHECK(hipMemcpy2D(dst, dst_step, P.d_blur + (long long)frame * P.blur_bytes + d.boff, (size_t)d.bpitch, d.w,
-                          d.h, hipMemcpyDeviceToHost));
     return ORB_OK;
 }
 

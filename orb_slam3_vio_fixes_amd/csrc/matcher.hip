@@ -21,11 +21,14 @@
 #include "orb_math.h"
 
 #include <algorithm>
+#include <atomic>
 #include <climits>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <list>
 #include <map>
+#include <memory>
 #include <vector>
 
 namespace orbmi {
@@ -1298,12 +1301,14 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
 //                  slot range in fl's bucket by one atomic
 //   k_bowk_scan    bucket starts (buckets padded to 64 slots)
 //   k_bowk_fill    slot -> global KF feature index (or none: no valid MapPoint)
-//   k_bowk_topk    one wave per 64 slots of one frame node: each lane keeps the
-//                  kBowK smallest keys (distance << 16 | frame feature index)
-//                  of its KF feature over ALL the node's frame features (read
-//                  wave-uniformly through the scalar cache)
-//   k_bowk_resolve one wave per g: the reference's serial walk over the node's
-//                  KF features.  A frame feature is "taken" when an earlier KF
+//   k_bowk_expand  the frame's descriptors as +-1 int8 rows in node order
+//   k_bowk_topk_mfma  one wave per 32 slots of one frame node: each slot's KF
+//                  feature keeps the kBowK smallest keys (distance << 16 |
+//                  position in the frame node) over ALL the node's frame
+//                  features, the distances as int8 dot products on
+//                  v_mfma_i32_32x32x32_i8
+//   k_bowk_resolve_lane  one thread per g: the reference's serial walk over the
+//                  node's KF features.  A frame feature is "taken" when an earlier KF
 //                  feature of the same (pair, node) claimed it; best / second
 //                  of a KF feature are the first two untaken keys of its list,
 //                  exact because every frame feature off the list has a larger
@@ -1541,54 +1546,6 @@ __device__ __forceinline__ void topk_push(uint32_t (&kk)[kBowK], uint32_t key) {
     for (int t = 0; t < kBowK; ++t) kk[t] = n[t];
 }
 
-// keys: distance << 16 | position in the frame node (the reference's order of
-// equal distances)
-__global__ __launch_bounds__(256) void k_bowk_topk(BowKArgs k) {
-    const BowArgs& a = k.b;
-    const long long slot0 = ((long long)blockIdx.x * 4 + wave_id()) * kWave;
-    const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
-    if (slot0 >= total) return;
-    int lo = 0, hi = a.f_nnodes;                     // last fl with bstart[fl] <= slot0
-    while (hi - lo > 1) {
-        const int mid = (lo + hi) >> 1;
-        if (k.bstart[mid] <= slot0) lo = mid;
-        else hi = mid;
-    }
-    const int fl = __builtin_amdgcn_readfirstlane(lo);
-    const int fb = __builtin_amdgcn_readfirstlane(a.f_off[fl]);
-    const int nf = __builtin_amdgcn_readfirstlane(a.f_off[fl + 1]) - fb;
-    const uint32_t src = k.slot_src[slot0 + lane_id()];
-    uint4 q0 = make_uint4(0, 0, 0, 0), q1 = q0;
-    if (src != 0xffffffffu) {
-        q0 = *(const uint4*)(a.kf_desc + (long long)src * 32);
-        q1 = *(const uint4*)(a.kf_desc + (long long)src * 32 + 16);
-    }
-    uint32_t kk[kBowK];
-#pragma unroll
-    for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
-    // the node's frame features: wave-uniform, through the scalar cache
-    typedef __attribute__((address_space(4))) const uint32_t* ConstU32;
-    const ConstU32 fidx = (ConstU32)(a.f_idx + fb);
-    const ConstU32 fdesc = (ConstU32)a.f_desc;
-    // four frame features per round: their index and descriptor scalar loads
-    // go out together (one wait per round, not two dependent ones per feature);
-    // rounds past the node's end re-read its last feature and push no key
-    constexpr int kR = 4;
-    for (int f0 = 0; f0 < nf; f0 += kR) {
-        uint32_t fi[kR];
-#pragma unroll
-        for (int t = 0; t < kR; ++t) fi[t] = fidx[min(f0 + t, nf - 1)];
-#pragma unroll
-        for (int t = 0; t < kR; ++t) {
-            const ConstU32 d = fdesc + (size_t)fi[t] * 8;
-            const int dist = __popc(q0.x ^ d[0]) + __popc(q0.y ^ d[1]) + __popc(q0.z ^ d[2]) + __popc(q0.w ^ d[3]) +
-                             __popc(q1.x ^ d[4]) + __popc(q1.y ^ d[5]) + __popc(q1.z ^ d[6]) + __popc(q1.w ^ d[7]);
-            topk_push(kk, f0 + t < nf ? (((uint32_t)dist << 16) | (uint32_t)(f0 + t)) : 0xffffffffu);
-        }
-    }
-    k.lists[slot0 + lane_id()] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
-}
-
 // The same lists with the distances on the matrix cores.  A descriptor's 256
 // bits as +-1 int8 make Hamming distance a dot product, dot = 256 - 2 ham,
 // so a (32 frame features) x (32 keyframe features) tile of a node is eight
@@ -1803,135 +1760,12 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
     }
 }
 
-// One wave per g: the lists of g's KF features are read lane-parallel, then
-// walked in the reference's order (uniform control flow).  The frame features
-// claimed so far in this (pair, node) -- the only ones a KF feature of it can
-// find taken -- are bits of a wave-private LDS bitmap over frame feature
-// indices, cleared again at the end of the walk.
-__global__ __launch_bounds__(256) void k_bowk_resolve(BowKArgs k) {
-    extern __shared__ uint32_t taken_s[];            // 4 waves x ceil(f_n / 32) words
-    const BowArgs& a = k.b;
-    const int words = (a.f_n + 31) / 32;   // positions < nf <= f_n
-    uint32_t* taken = taken_s + wave_id() * words;
-    const int lane = lane_id();
-    for (int i = lane; i < words; i += kWave) taken[i] = 0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const long long g = (long long)blockIdx.x * 4 + wave_id();
-    if (g >= k.G) return;
-    const int fl = k.g_fl[g];
-    if (fl < 0) return;
-    const int pr = k.g_pr[g];
-    const int ia = (int)(g - a.node_off[pr]);
-    const int* ko = a.kf_off + a.node_off[pr] + pr;
-    const long long base = (long long)k.bstart[fl] + k.g_off[g];
-    const int fb = a.f_off[fl], nf = a.f_off[fl + 1] - fb;
-    const bool complete = nf <= kBowK;
-    int32_t* match = a.match + (long long)pr * a.f_n;
-    const long long kpo = a.kp_off[pr];
-    const int nkf = ko[ia + 1] - ko[ia];
-    auto is_taken = [&](uint32_t fi) { return (taken[fi >> 5] >> (fi & 31)) & 1u; };
-    int nm = 0;
-    for (int c0 = 0; c0 < nkf; c0 += kWave) {
-        uint32_t src = 0xffffffffu;
-        uint4 L = make_uint4(~0u, ~0u, ~0u, ~0u);
-        if (c0 + lane < nkf) {
-            src = k.slot_src[base + c0 + lane];
-            L = k.lists[base + c0 + lane];
-        }
-        const int nc = min(kWave, nkf - c0);
-        // the loads land here, once: the walk's claims store to `match`, and a
-        // wait for these registers inside the walk would also wait for every
-        // store issued before it (one vmcnt for loads and stores)
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("" : "+v"(src), "+v"(L.x), "+v"(L.y), "+v"(L.z), "+v"(L.w));
-#if ORB_BOWK_ABL == 2
-        if (src == 0x12345u && L.x == 7u) nm++;   // timing ablation: loads only (wrong results)
-        continue;
-#endif
-        for (int j = 0; j < nc; ++j) {
-            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)src, j);
-            if (s == 0xffffffffu) continue;                          // no valid MapPoint (:255-260)
-            const uint32_t keys[kBowK] = {(uint32_t)__builtin_amdgcn_readlane((int)L.x, j),
-                                          (uint32_t)__builtin_amdgcn_readlane((int)L.y, j),
-                                          (uint32_t)__builtin_amdgcn_readlane((int)L.z, j),
-                                          (uint32_t)__builtin_amdgcn_readlane((int)L.w, j)};
-            // the four taken bits in parallel (independent LDS reads), then the
-            // first two untaken keys (:275-276)
-            uint32_t tk[kBowK];
-#pragma unroll
-            for (int t = 0; t < kBowK; ++t) tk[t] = is_taken(min(keys[t] & 0xffffu, (uint32_t)nf - 1u));
-#pragma unroll
-            for (int t = 0; t < kBowK; ++t) tk[t] |= keys[t] == 0xffffffffu;
-            uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
-#pragma unroll
-            for (int t = kBowK - 1; t >= 0; --t) {
-                if (tk[t]) continue;
-                e2 = e1;
-                e1 = keys[t];
-            }
-            // best / second of the untaken node features: exact from the list,
-            // or bounded -- every key off the list is larger than the last one
-            int best = 256, best2 = 256;
-            uint32_t bfi = 0;
-            bool exact = true;
-            const int dlast = (int)(keys[kBowK - 1] >> 16);
-            if (e1 != 0xffffffffu) {
-                best = (int)(e1 >> 16); bfi = e1 & 0xffff;
-                if (e2 != 0xffffffffu) best2 = (int)(e2 >> 16);
-                else if (!complete && best <= kThLow) {
-                    // second >= dlast: decided when even dlast passes the ratio test
-                    if (a.ratio > 0.f && (float)best < a.ratio * (float)dlast) best2 = dlast;
-                    else exact = false;
-                }
-            } else if (!complete && dlast <= kThLow) {
-                exact = false;                                        // every listed key taken
-            }
-#if ORB_BOWK_ABL == 1
-            exact = true;   // timing ablation: no rescans (wrong results)
-#endif
-            if (!exact) {
-                // the reference's loop over the whole node (:266-292), lanes over
-                // its features: keys (dist << 16 | index), first two minima
-                const uint8_t* kd = a.kf_desc + (long long)s * 32;
-                const uint4 q0 = *(const uint4*)kd, q1 = *(const uint4*)(kd + 16);
-                uint32_t m1 = (uint32_t)INT_MAX, m2 = (uint32_t)INT_MAX;   // wave_min works on ints
-                for (int f = lane; f < nf; f += kWave) {
-                    if (is_taken((uint32_t)f)) continue;
-                    const uint32_t fi = a.f_idx[fb + f];
-                    const uint32_t key = ((uint32_t)hamming32(q0, q1, a.f_desc + (long long)fi * 32) << 16) | (uint32_t)f;
-                    m2 = min(m2, max(m1, key));
-                    m1 = min(m1, key);
-                }
-                // first and second minima over the lanes (keys < 2^25: positive ints)
-                const int a1 = wave_min((int)m1, INT_MAX);
-                const int own = (m1 == (uint32_t)a1) ? (int)m2 : (int)m1;
-                const int a2 = wave_min(own, INT_MAX);
-                best = a1 == INT_MAX ? 256 : (a1 >> 16);
-                best2 = a2 == INT_MAX ? 256 : (a2 >> 16);
-                bfi = (uint32_t)a1 & 0xffff;
-            }
-            if (best <= kThLow && (float)best < a.ratio * (float)best2) {   // :327-329
-                // no fence: the LDS bit is read back by this wave's own later
-                // LDS reads (in order), and nothing here reads the match store
-                if (lane == 0) {
-                    match[a.f_idx[fb + bfi]] = (int32_t)((long long)s - kpo);
-                    taken[bfi >> 5] |= 1u << (bfi & 31);
-                }
-                ++nm;
-            }
-        }
-    }
-    if (lane == 0 && nm) atomicAdd(&a.nmatches[pr], nm);
-}
-
 // One thread per g, the g entries ordered by frame node (neighbouring lanes
 // walk nodes of one size: little divergence).  The positions of the node
 // claimed so far in this walk are bits of a thread-private LDS bitmap (17
 // words a thread: the odd pitch spreads the threads over the banks); nodes of
 // more than 512 features read "taken" from the match row instead (only this
-// thread writes the node's entries of it).  Otherwise as k_bowk_resolve.
+// thread writes the node's entries of it).
 // The walk's memory traffic is kept off its critical path: a thread's slots
 // and lists are read 8 steps at a time, the frame-feature indices of the
 // block's first node come from an LDS copy, and every step issues exactly one
@@ -3252,6 +3086,12 @@ template <typename T>
 struct PBuf {
     T* p = nullptr;
     size_t n = 0;
+    PBuf() = default;
+    PBuf(const PBuf&) = delete;
+    PBuf& operator=(const PBuf&) = delete;
+    ~PBuf() {
+        if (p) (void)hipFree(p);
+    }
     int alloc(size_t cnt) {
         if (cnt <= n) return ORB_OK;
         if (p) (void)hipFree(p);
@@ -3277,12 +3117,45 @@ static int pow2_at_least(int n) { int p = 64; while (p < n) p <<= 1; return p; }
 // for different GPUs, must not share buffers.  (Calls on one stream are
 // ordered by the stream; buffers only grow, and hipFree of a grown-out buffer
 // waits for the device.)
+// Device scratch that batched launches keep between calls (grown on demand),
+// one set per (device, stream, kind) of the calling thread, most recently used
+// first.  At most kScratchSets stay allocated: a call on a further stream
+// frees the least recently used set after a device synchronisation (work still
+// queued on its stream may read it).  orbm_release_scratch frees a stream's
+// sets at once; a caller must do so before destroying a stream it used here,
+// or a new stream at the same address would inherit the buffers unordered
+// against the old stream's work.
+struct ScratchBase {
+    virtual ~ScratchBase() = default;
+};
+constexpr size_t kScratchSets = 6;
+struct ScratchEntry {
+    int dev;
+    hipStream_t st;
+    const void* kind;
+    std::unique_ptr<ScratchBase> s;
+};
+static std::list<ScratchEntry>& scratch_sets() {
+    static thread_local std::list<ScratchEntry>* l = new std::list<ScratchEntry>();   // never destroyed at exit
+    return *l;
+}
 template <class S>
 static S& stream_scratch(hipStream_t st) {
-    static thread_local std::map<std::pair<int, hipStream_t>, S>* m = new std::map<std::pair<int, hipStream_t>, S>();
+    static const char kind = 0;                      // one address per scratch type
+    auto& L = scratch_sets();
     int dev = 0;
     (void)hipGetDevice(&dev);
-    return (*m)[{dev, st}];
+    for (auto it = L.begin(); it != L.end(); ++it)
+        if (it->dev == dev && it->st == st && it->kind == &kind) {
+            L.splice(L.begin(), L, it);
+            return *static_cast<S*>(L.front().s.get());
+        }
+    if (L.size() >= kScratchSets) {
+        (void)hipDeviceSynchronize();
+        L.pop_back();
+    }
+    L.push_front(ScratchEntry{dev, st, &kind, std::make_unique<S>()});
+    return *static_cast<S*>(L.front().s.get());
 }
 
 static GridParams grid_params(const orbm_frame* f) {
@@ -3353,7 +3226,37 @@ __global__ __launch_bounds__(256) void k_fv_desc(const uint8_t* __restrict__ des
 
 using namespace orbmi;
 
+static std::atomic<int> g_debug_opt[ORB_OPT_COUNT];
+
+int orbmi::debug_opt(int option) {
+    return option >= 0 && option < ORB_OPT_COUNT ? g_debug_opt[option].load(std::memory_order_relaxed) : 0;
+}
+
 extern "C" {
+
+int orb_debug_set_option(int option, int value) {
+    if (option < 0 || option >= ORB_OPT_COUNT) return ORB_ERR_PARAM;
+    g_debug_opt[option].store(value, std::memory_order_relaxed);
+    return ORB_OK;
+}
+
+int orbm_release_scratch(void* stream, int all) {
+    if (device_ok() != ORB_OK) return ORB_ERR_DEVICE;
+    auto& L = scratch_sets();
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    bool any = false;
+    for (const auto& e : L) any |= all || (e.dev == dev && e.st == (hipStream_t)stream);
+    if (!any) return ORB_OK;
+    ORB_CHECK(hipDeviceSynchronize());
+    L.remove_if([&](const ScratchEntry& e) { return all || (e.dev == dev && e.st == (hipStream_t)stream); });
+    return ORB_OK;
+}
+
+int orb_debug_get_option(int option) {
+    return option >= 0 && option < ORB_OPT_COUNT ? g_debug_opt[option].load(std::memory_order_relaxed) : -1;
+}
+
 
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     // host inline utility (Frame.cc:886, MapPoint.cc:377 call it on single pairs)
@@ -3425,7 +3328,7 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     (void)max_x; (void)max_y;
     if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
     hipStream_t st = (hipStream_t)stream;
-    struct Scratch { PBuf<uint32_t> sorted, topk, l0s; PBuf<int> count, pf, ncand, l0c; int pf_frames = 0; };
+    struct Scratch : ScratchBase { PBuf<uint32_t> sorted, topk, l0s; PBuf<int> count, pf, ncand, l0c; int pf_frames = 0; };
     Scratch& S = stream_scratch<Scratch>(st);
     PBuf<uint32_t>&sorted = S.sorted, &topk = S.topk, &l0s = S.l0s;
     PBuf<int>&count = S.count, &pf = S.pf, &ncand = S.ncand, &l0c = S.l0c;
@@ -3575,7 +3478,7 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 // G: (pair, KF node) entries of the map, nfv: its FeatureVector entries (host
 // totals of the resident map: scratch is sized without reading the device).
 static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hipStream_t st) {
-    struct Scratch {
+    struct Scratch : ScratchBase {
         PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node, node_n;
         PBuf<unsigned long long> bgcount;
         PBuf<uint32_t> slot_src, slot_pos;
@@ -3611,35 +3514,21 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
         KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
     }
-    const unsigned gb = (unsigned)((G + 255) / 256), gw = (unsigned)((G + 3) / 4);
+    const unsigned gb = (unsigned)((G + 255) / 256);
     KLAUNCH(k_bowk_map, dim3(npairs), dim3(256), 0, st, k);
     KLAUNCH(k_bowk_scan, dim3(1), dim3(1024), (size_t)2 * a.f_nnodes * sizeof(int), st, k);
     KLAUNCH(k_bowk_fill, dim3(npairs), dim3(256), 0, st, k);
     KLAUNCH(k_bowk_chunks, dim3(a.f_nnodes), dim3(256), 0, st, k);
-    const char* mf = std::getenv("ORBM_BOW_KFLANE_MFMA");   // 0: the VALU top-4 pass (A/B)
-    if (!(mf && mf[0] == '0')) {
-        KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_idx,
-                a.f_off + a.f_nnodes, fexp.p);
-        // two column sets per wave measured slower (4.27 vs 4.15 ms per query: 136 VGPRs,
-        // 3 waves per SIMD instead of 5); ORBM_BOWK_NSET=2 selects it (A/B)
-        const char* ns = std::getenv("ORBM_BOWK_NSET");
-        if (ns && ns[0] == '2')
-            KLAUNCH(k_bowk_topk_mfma<2>, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k, fexp.p);
-        else
-            KLAUNCH(k_bowk_topk_mfma<1>, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
-    } else {
-        KLAUNCH(k_bowk_topk, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, k);
-    }
-    const char* rw = std::getenv("ORBM_BOW_KFLANE_WAVE_RESOLVE");   // the wave-walk form (A/B)
-    if (rw && rw[0] == '1')
-        KLAUNCH(k_bowk_resolve, dim3(gw), dim3(256), (size_t)4 * ((a.f_n + 31) / 32) * sizeof(uint32_t), st, k);
-    else
+    KLAUNCH(k_bowk_expand, dim3((unsigned)((16 * a.f_n + 255) / 256)), dim3(256), 0, st, a.f_desc, a.f_idx,
+            a.f_off + a.f_nnodes, fexp.p);
+    // (measured and dropped, DESIGN.md §5: the VALU top-4 pass, two 32-column
+    // keyframe sets per MFMA wave, a wave-walk resolve)
+    KLAUNCH(k_bowk_topk_mfma<1>, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
     {
         // the BIG form when a bitmap over every frame position fits 64 threads' LDS
         const int words = (a.f_n + 31) / 32, bp = a.f_n > 32 * kBowLaneWords ? (words | 1) : 0;
         const size_t big_lds = (size_t)64 * bp * sizeof(uint32_t);
-        const char* bg = std::getenv("ORBM_BOWK_BIG");   // 0: the 256-thread form takes every node (A/B)
-        const int big_pitch = big_lds <= 64 * 1024 && !(bg && bg[0] == '0') ? bp : 0;
+        const int big_pitch = big_lds <= 64 * 1024 && !debug_opt(ORB_OPT_BOWK_BIG) ? bp : 0;
         if (big_pitch) {
             KLAUNCH((k_bowk_resolve_lane<false, true>), dim3(gb), dim3(256), 0, st, k, big_pitch);
             KLAUNCH((k_bowk_resolve_lane<true, true>), dim3((unsigned)((G + 63) / 64)), dim3(64), big_lds, st, k,
@@ -3674,13 +3563,12 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     a.f_idx = ffv->idx; a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
     a.match = d_match; a.nmatches = d_nmatches;
     // the lane-per-KF-feature search (k_bowk_*) when the map carries its totals
-    // (6.7 vs 7.1 ms per 10k-keyframe query); ORBM_BOW_KFLANE=0
-    // selects k_bow (A/B, tests)
-    const char* kfl = std::getenv("ORBM_BOW_KFLANE");
+    // (6.7 vs 7.1 ms per 10k-keyframe query); ORB_OPT_BOW_FORM
+    // 1 selects k_bow (A/B, tests)
     // (k_bowk_scan holds two ints per frame node in LDS: 20,000 nodes = 160 KB
     // less its static scratch; beyond that k_bow runs)
     if (map->n_nodes_total > 0 && map->n_fv_total > 0 && f->n <= 0xffff && ffv->nnodes > 0 &&
-        ffv->nnodes <= 20000 && !(kfl && kfl[0] == '0'))
+        ffv->nnodes <= 20000 && debug_opt(ORB_OPT_BOW_FORM) != 1)
         return launch_bow_kf(a, map->nkf, map->n_nodes_total, map->n_fv_total, (hipStream_t)stream);
     return launch_bow(a, map->nkf, (hipStream_t)stream);
 }
@@ -3694,17 +3582,15 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p;
     a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
     // two-phase form unless its LDS slot table does not fit; phase 2 speculative
-    // unless its table does not fit.  For testing, ORBM_PROJ_SINGLE_WAVE=1
-    // forces the single-wave form and ORBM_PROJ_SERIAL_RESOLVE=1 the serial
-    // phase 2.
-    const char* force = std::getenv("ORBM_PROJ_SINGLE_WAVE");
-    const char* serial = std::getenv("ORBM_PROJ_SERIAL_RESOLVE");
+    // unless its table does not fit.  For testing, ORB_OPT_PROJ_FORM 2 forces
+    // the single-wave form and 1 the serial phase 2.
+    const int form = debug_opt(ORB_OPT_PROJ_FORM);
     const size_t lds2 = proj_resolve_lds(a.n, a.nq), lds3 = proj_spec_lds(a.n, a.nq);
-    if (lds2 <= 160 * 1024 && !(force && force[0] == '1')) {
+    if (lds2 <= 160 * 1024 && form != 2) {
         DBuf<uint2> topk; DBuf<int> cnt;
         if ((rc = topk.alloc((size_t)std::max(1, a.nq) * kProjK)) || (rc = cnt.alloc(std::max(1, a.nq)))) return rc;
         if (a.nq) KLAUNCH(k_proj_topk, dim3((a.nq + 3) / 4), dim3(256), 0, 0, a, proj_bound(a), topk.p, cnt.p);
-        if (lds3 <= 160 * 1024 && !(serial && serial[0] == '1'))
+        if (lds3 <= 160 * 1024 && form != 1)
             KLAUNCH(k_proj_resolve_spec, dim3(1), dim3(64), lds3, 0, a, topk.p, cnt.p);
         else
             KLAUNCH(k_proj_resolve, dim3(1), dim3(64), lds2, 0, a, topk.p, cnt.p);

@@ -274,7 +274,8 @@ ORB_HD void std_sort(SortRec* first, int n, SortFrame* stk) {
 // the left scanner runs into the value the last swap left at R[k*-1]), and the
 // swaps are the pairs (L[k], R[k]), k < k*, all disjoint.  Every leaf range
 // (<= 16 elements) ends up holding exactly its own elements, so the final
-// insertion pass is a stable insertion sort per leaf.
+// insertion pass is a stable insertion sort per leaf (k_quadtree places each
+// leaf's records at their stable ranks, 16 lanes a leaf: the same permutation).
 // partition_ranks is the sequential statement (host check); the kernel
 // computes L, R and k* with ballots.
 // ---------------------------------------------------------------------------

@@ -26,10 +26,6 @@ struct LevelDev {
     // k_pyramid tables (l >= 1): column taps at xtab (padded to a multiple of
     // 4 columns), row taps at ytab
     int xtab, ytab;
-    // the blurred level (k_blur_levels -> k_describe): byte offset inside one
-    // frame's blurred slab, row pitch
-    long long boff;
-    int bpitch;
 };
 
 // One launch of k_pyramid: levels la+1..lb from level la, in nb bands of
@@ -60,20 +56,6 @@ struct PyrStream {
     int cnt_dw = 0;                        // per-step wave-item counters (LDS dword offset)
 };
 
-// k_pyr_level: one launch per level, a wave per (frame, run of R rows, 64
-// column groups); column records shared with k_pyr_stream's format.
-constexpr int kPlNS = 12;                  // source rows a run may span
-constexpr int kPlRmax = 16;                // output rows per run at most
-struct PyrLevelPlan {
-    bool ok = false;
-    int col_off[kMaxLevels] = {};          // dword offset of level l's column records in d_pcol
-    int R[kMaxLevels] = {}, runs[kMaxLevels] = {};
-};
-
-// k_blur_levels: one wave per item = kBlurDw dword columns x kBlurRows rows of
-// a level (lanes 1..62 of a wave output; lanes 0 and 63 hold the halo)
-constexpr int kBlurRows = 16, kBlurDw = 62;
-
 struct CellDev {
     int level;
     int x0, y0, cols, rows;   // ROI in level coordinates (ORBextractor.cc:807-826)
@@ -85,8 +67,6 @@ struct Plan {
     std::vector<LevelDev> lv;
     std::vector<CellDev> cells;
     long long pyr_bytes = 0;
-    long long blur_bytes = 0;        // one frame's blurred levels 0..L-1
-    int nblur_items = 0;             // k_blur_levels wave-items per frame
     int ncells = 0, slot_total = 0, out_total = 0;
     int roi_max = 0, roi_rows_max = 0, roi_nd_max = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     int win_pix_max = 0;             // largest FAST window (cols-6)*(rows-6): candidate list entries
@@ -95,7 +75,6 @@ struct Plan {
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     std::vector<PyrGroup> pgroups;   // k_pyramid launches
     PyrStream ps;                    // k_pyr_stream layout (ps.ok: usable for this size)
-    PyrLevelPlan pl;                 // k_pyr_level layout
     // device
     uint8_t *d_pyr = nullptr, *d_in = nullptr;
     int2* d_tab = nullptr;
@@ -115,9 +94,6 @@ struct Plan {
     uint32_t* d_pxw = nullptr;       //   and weights a0 | a1 << 16
     int2* d_pyt = nullptr;           // k_pyramid row taps: sy0 | sy1 << 16 (clamped), b0 | b1 << 16
     uint4* d_ps_tab = nullptr;       // k_pyr_stream LDS table image
-    uint32_t* d_pcol = nullptr;      // k_pyr_level column records
-    uint8_t* d_blur = nullptr;       // [maxB][blur_bytes] blurred levels (GaussianBlur of each level)
-    int4* d_blur_items = nullptr;    // k_blur_levels items {level, first dword column, first row, rows}
     // single-image host path outputs
     orb_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
@@ -128,7 +104,7 @@ struct Plan {
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_pcol, d_blur, d_blur_items};
+                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();
@@ -159,17 +135,6 @@ struct orbx_handle {
     std::vector<hipStream_t> sub_streams;
     std::vector<hipEvent_t> sub_done;
     hipEvent_t fork_ev = nullptr;
-    // k_blur_levels on a side stream forked after the pyramid and joined
-    // before k_describe_pb, per calling stream (ORB_BLUR_FORK, default on)
-    struct BlurSide {
-        hipStream_t caller, st;
-        hipEvent_t fork, join;
-    };
-    bool blur_fork = true;
-    // level blur once per level + k_describe_pb (env ORB_DESC_PREBLUR=1; off:
-    // k_describe blurs around each keypoint, measured faster end to end)
-    bool preblur = false;
-    std::vector<BlurSide> blur_side;
     hipEvent_t batch_done = nullptr;   // recorded after orbx_extract_batch_device's work on its stream
     // frames of the last orbx_extract_batch_device call (level 0 of its
     // pyramid; levels >= 1 stay in plan.d_pyr until the next call)

@@ -50,8 +50,7 @@ class ORBextractor:
     def UMax(self): return self._tab[5].copy()
 
     def set_pyramid_mode(self, mode: int) -> None:
-        """0 auto, 1 row bands (k_pyramid), 2 sliding frame (k_pyr_stream), 3 per-level k_resize,
-        4 per-level runs (k_pyr_level)."""
+        """0 auto, 1 row bands (k_pyramid), 2 sliding frame (k_pyr_stream)."""
         capi.check(capi.lib().orbx_set_pyramid_mode(self._h, mode), "orbx_set_pyramid_mode")
 
     def set_host_pyramid(self, enable: bool) -> None:
@@ -144,18 +143,6 @@ class ORBextractor:
             out.append(kps[off:off + c].copy())
             off += c
         assert off == n
-        return out
-
-    def debug_blur_level(self, level: int, frame: int = 0) -> np.ndarray:
-        """The blurred level k_describe_pb sampled (GaussianBlur 7x7 of the
-        level, ORBextractor.cc:1132-1133) for frame `frame` of the last call."""
-        w, hh = C.c_int(0), C.c_int(0)
-        lib = capi.lib()
-        capi.check(lib.orbx_debug_blur_level(self._h, frame, level, None, 0, C.byref(w), C.byref(hh)),
-                   "orbx_debug_blur_level")
-        out = np.zeros((hh.value, w.value), np.uint8)
-        capi.check(lib.orbx_debug_blur_level(self._h, frame, level, abi.ptr(out), w.value, None, None),
-                   "orbx_debug_blur_level")
         return out
 
     def extract_batch_device(self, frames, lapping=(0, 1000), out=None, stream=None):

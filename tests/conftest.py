@@ -29,3 +29,30 @@ def gpu_lib():
         pytest.fail("gpu test selected but no GPU is visible")
     from orb_slam3_vio_fixes_amd import capi
     return capi.lib()
+
+
+@pytest.fixture
+def debug_option():
+    """Sets orb_debug_set_option values (alternative kernel forms, a test hook of
+    include/orb_mi355x.h) for one test and restores them afterwards."""
+    from orb_slam3_vio_fixes_amd import capi
+    L = capi.lib()
+    saved = {}
+
+    def set_(option, value):
+        saved.setdefault(option, L.orb_debug_get_option(option))
+        capi.check(L.orb_debug_set_option(option, value), "orb_debug_set_option")
+    yield set_
+    for option, value in saved.items():
+        L.orb_debug_set_option(option, value)
+
+
+@pytest.fixture
+def proj_form(debug_option):
+    """Projection-search form by name: spec (top-K + speculative resolve, the
+    default), serial (top-K + serial resolve), single (single-wave search)."""
+    from orb_slam3_vio_fixes_amd import capi
+
+    def set_(name):
+        debug_option(capi.ORB_OPT_PROJ_FORM, {"spec": 0, "serial": 1, "single": 2}[name])
+    return set_

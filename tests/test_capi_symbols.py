@@ -11,7 +11,7 @@ HEADER = ROOT / "include" / "orb_mi355x.h"
 
 def declared():
     txt = re.sub(r"/\*.*?\*/", " ", HEADER.read_text(), flags=re.S)
-    return sorted(set(re.findall(r"\b(orb[xmvsk]_[a-z0-9_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(orb(?:[xmvsk]|_debug)_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_declares_entry_points():
@@ -29,6 +29,21 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if not hasattr(L, n)]
     assert not missing, missing
     assert set(capi.EXPORTS) == set(declared())
+
+
+def test_release_library_reads_no_environment():
+    """Kernel choice is not switchable from a process's environment: the
+    release library imports no getenv (alternative forms are reachable only
+    through the explicit orb_debug_set_option test hook)."""
+    import subprocess
+    from orb_slam3_vio_fixes_amd import build, capi
+    build.build()
+    out = subprocess.run(["nm", "-D", "--undefined-only", str(capi.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    assert "getenv" not in out
+    L = capi.load()
+    assert L.orb_debug_get_option(capi.ORB_OPT_PROJ_FORM) == 0
+    assert L.orb_debug_set_option(99, 1) == -3 and L.orb_debug_get_option(99) == -1
 
 
 def test_no_device_fails_loudly():

@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from orb_slam3_vio_fixes_amd import abi, kfmap, orb, synth
+from orb_slam3_vio_fixes_amd import abi, capi, kfmap, orb, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -47,9 +47,9 @@ def make_keyframes(k, d, voc, nkf, seed):
     return kfs
 
 
-@pytest.mark.parametrize("kflane", ["0", "1"])
-def test_c5_map_wide_search_by_bow(gpu_lib, c5, kflane, monkeypatch):
-    monkeypatch.setenv("ORBM_BOW_KFLANE", kflane)
+@pytest.mark.parametrize("bow_form", [0, 1])
+def test_c5_map_wide_search_by_bow(gpu_lib, c5, bow_form, debug_option):
+    debug_option(capi.ORB_OPT_BOW_FORM, bow_form)
     k, d, voc = c5
     kfs = make_keyframes(k, d, voc, 24, 1)
     _, _, fnode = O.transform(voc, d, 4)
@@ -131,9 +131,9 @@ def _adversarial(seed, nf=1500, shape="default", nkf=12):
     return fk, fd, fnode, kfs
 
 
-def _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch, min_matches=20):
+def _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option, min_matches=20):
     got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
-    monkeypatch.setenv("ORBM_BOW_KFLANE", "0")
+    debug_option(capi.ORB_OPT_BOW_FORM, 1)
     old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
     np.testing.assert_array_equal(got, old)
     np.testing.assert_array_equal(gnm, onm)
@@ -146,10 +146,8 @@ def _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch, min_matches=2
     assert gnm.min() > min_matches
 
 
-@pytest.mark.parametrize("seed,wave_resolve,mfma,fv_desc", [(3, "0", "1", True), (3, "0", "1", False),
-                                                             (4, "0", "1", True), (3, "1", "1", True),
-                                                             (4, "0", "0", True)])
-def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monkeypatch):
+@pytest.mark.parametrize("seed,fv_desc", [(3, True), (3, False), (4, True), (5, True)])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, fv_desc, debug_option):
     """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
     against the node-per-wave kernel (k_bow) on _adversarial inputs."""
     fk, fd, fnode, kfs = _adversarial(seed)
@@ -159,23 +157,19 @@ def test_c5_kf_lane_adversarial(gpu_lib, seed, wave_resolve, mfma, fv_desc, monk
     if fv_desc:   # orbm_kf_map_fv_desc: row fv_idx_off[i] + p = descriptor fv_idx[.] of keyframe i
         want = np.concatenate([kd[kfmap.featvec_csr(nid)[2]] for kk, kd, valid, nid in kfs])
         np.testing.assert_array_equal(m.t["fv_desc"].cpu().numpy().reshape(-1, 32)[:len(want)], want)
-    monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
-    monkeypatch.setenv("ORBM_BOW_KFLANE_WAVE_RESOLVE", wave_resolve)
-    monkeypatch.setenv("ORBM_BOW_KFLANE_MFMA", mfma)
-    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch)
+    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option)
 
 
-@pytest.mark.parametrize("case", ["big", "big_nobig", "huge_frame", "many_nodes", "nset2", "nset2_big"])
-def test_c5_kf_lane_resolve_forms(gpu_lib, case, monkeypatch):
+@pytest.mark.parametrize("case", ["big", "big_nobig", "huge_frame", "many_nodes"])
+def test_c5_kf_lane_resolve_forms(gpu_lib, case, debug_option):
     """The resolve and top-4 forms the default C5 data never reaches:
     big      frame nodes of > 512 features: k_bowk_resolve_lane<true, true>
              (one wave per block, a bitmap over every frame position in LDS);
-    big_nobig ORBM_BOWK_BIG=0: the 256-thread form takes every node, with the
+    big_nobig ORB_OPT_BOWK_BIG 1: the 256-thread form takes every node, with the
              'taken' test of large nodes read from the match row;
     huge_frame a frame of 9000 features (> 8192: no LDS bitmap fits, the
              match-row form is the only one);
-    many_nodes > 1024 frame nodes: single bucket counters (nsub = 1);
-    nset2    ORBM_BOWK_NSET=2, two 32-column keyframe sets per MFMA wave."""
+    many_nodes > 1024 frame nodes: single bucket counters (nsub = 1)."""
     nf = 9000 if case == "huge_frame" else 2500
     shape = "many_nodes" if case == "many_nodes" else ("big" if "big" in case or case == "huge_frame" else "default")
     fk, fd, fnode, kfs = _adversarial(11 + len(case), nf=nf, shape=shape, nkf=8)
@@ -184,12 +178,9 @@ def test_c5_kf_lane_resolve_forms(gpu_lib, case, monkeypatch):
     if case == "many_nodes":
         assert len(np.unique(fnode)) > 1024
     m = kfmap.DeviceKeyframeMap(kfs)
-    monkeypatch.setenv("ORBM_BOW_KFLANE", "1")
     if case == "big_nobig":
-        monkeypatch.setenv("ORBM_BOWK_BIG", "0")
-    if case.startswith("nset2"):
-        monkeypatch.setenv("ORBM_BOWK_NSET", "2")
-    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, monkeypatch, min_matches=5)
+        debug_option(capi.ORB_OPT_BOWK_BIG, 1)
+    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option, min_matches=5)
 
 
 @pytest.fixture(scope="module")
@@ -207,18 +198,17 @@ def c5_full(c5):
     return k, d, fnode, m, rmatch, rnm
 
 
-@pytest.mark.parametrize("variant", ["default", "k_bow", "nset2", "no_big", "valu_topk"])
-def test_c5_full_map_every_keyframe(gpu_lib, c5_full, variant, monkeypatch):
+@pytest.mark.parametrize("variant", ["default", "k_bow", "no_big"])
+def test_c5_full_map_every_keyframe(gpu_lib, c5_full, variant, debug_option):
     """Map-wide SearchByBoW (orbm_search_by_bow_batch_device) over the full
     10k-keyframe map == the oracle for EVERY keyframe (match row and count),
     in each search form: the default lane-per-keyframe-feature search, the
-    node-per-wave k_bow, two MFMA column sets, no big-node form, the VALU
-    top-4 pass.  Reference: ORBmatcher.cc:223-425, Tracking.cc:3641-3648."""
+    node-per-wave k_bow, no big-node form.  Reference: ORBmatcher.cc:223-425,
+    Tracking.cc:3641-3648."""
     k, d, fnode, m, rmatch, rnm = c5_full
-    env = {"k_bow": ("ORBM_BOW_KFLANE", "0"), "nset2": ("ORBM_BOWK_NSET", "2"),
-           "no_big": ("ORBM_BOWK_BIG", "0"), "valu_topk": ("ORBM_BOW_KFLANE_MFMA", "0")}.get(variant)
-    if env:
-        monkeypatch.setenv(*env)
+    opt = {"k_bow": (capi.ORB_OPT_BOW_FORM, 1), "no_big": (capi.ORB_OPT_BOWK_BIG, 1)}.get(variant)
+    if opt:
+        debug_option(*opt)
     match, nm = m.search_by_bow(k, d, fnode, 0.75, True)
     nm = nm.cpu().numpy()
     np.testing.assert_array_equal(nm, rnm)

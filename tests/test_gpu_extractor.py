@@ -104,35 +104,6 @@ def test_pyramid_and_stages(gpu_lib):
                                           np.stack([b["x"], b["y"], b["response"]]))
 
 
-@pytest.mark.parametrize("blur", [0, 1])
-def test_preblur_path_matches_oracle(gpu_lib, blur, monkeypatch):
-    """The alternative describe path (ORB_DESC_PREBLUR=1): k_blur_levels'
-    GaussianBlur(7x7, 2, 2, REFLECT_101) of every level (ORBextractor.cc:
-    1132-1133) equals the oracle's blur7 of the oracle's level, every pixel
-    including the reflected borders, for a single image and for frames of a
-    batch; and k_describe_pb's keypoints and descriptors equal the oracle's."""
-    monkeypatch.setenv("ORB_DESC_PREBLUR", "1")
-    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7, blur_variant=blur)
-    ref = O.OracleExtractor(1000, 1.2, 8, 20, 7, blur, 1)
-    img = synth.image(752, 480, 31)
-    k, d, m = ex(img, None, (0, 1000))
-    rk, rd, rm = ref(img, (0, 1000))
-    assert (len(k), m) == (len(rk), rm) and np.array_equal(k.view(np.uint8), rk.view(np.uint8))
-    assert np.array_equal(d, rd)
-    for l in range(8):
-        np.testing.assert_array_equal(ex.debug_blur_level(l), O.blur(ref.level(l), blur))
-    seq = synth.sequence(752, 480, 3, config=2, start=40)
-    out = ex.extract_batch(list(seq), [(0, 1000)] * 3)
-    for f in (0, 2):
-        rk, rd, rm = ref(seq[f], (0, 1000))
-        assert np.array_equal(out[f][1], rd)
-        for l in (0, 3, 7):
-            np.testing.assert_array_equal(ex.debug_blur_level(l, f), O.blur(ref.level(l), blur))
-    # the default path has no blurred levels to read
-    with pytest.raises(Exception):
-        pair(blur=blur)[0].debug_blur_level(0)
-
-
 def test_tables_match_oracle(gpu_lib):
     ex, ref = pair()
     t = ref.tables()

@@ -92,9 +92,8 @@ def projection_queries(frames, seed, n=600):
 
 @pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
-def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, monkeypatch):
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
-    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
+def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, proj_form):
+    proj_form(single)
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
@@ -117,9 +116,8 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, 
 
 @pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
-def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, monkeypatch):
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
-    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
+def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, proj_form):
+    proj_form(single)
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     valid = (rng.random(n) < 0.9).astype(np.uint8)
@@ -138,14 +136,13 @@ def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, singl
 
 @pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("seed,reps", [(21, 2), (22, 3), (23, 4)])
-def test_search_by_projection_overlapping_lists(gpu_lib, frames, seed, reps, single, monkeypatch):
+def test_search_by_projection_overlapping_lists(gpu_lib, frames, seed, reps, single, proj_form):
     """Queries repeated `reps` times (consecutive and far apart in the query
     order, positions jittered, a few descriptor bits flipped) so that candidate
     lists overlap and later queries find their best slot claimed; slots start
     free, pre-existing (-2) or owned by a query of this call (earlier or later
     in the order) with or without observations."""
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
-    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
+    proj_form(single)
     rng = np.random.default_rng(seed)
     src, cur = frames[0], frames[1]
     k0 = src[0][:300]

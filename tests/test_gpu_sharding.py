@@ -44,8 +44,9 @@ def test_two_ranks_equal_one_rank_with_seam_pair(tmp_path):
     r1 = np.load(tmp_path / "two" / "rank1.npz")
     assert (int(r0["frames"]), int(r1["frames"])) == (B + 1, B)      # rank 0 carries the halo frame
     pairs = 0
+    base = int(one["first"])          # the last step's ring batch: global frames [base, base + 2B)
     for r in (r0, r1):
-        f0 = int(r["first"])
+        f0 = int(r["first"]) - base
         for i in range(int(r["frames"])):
             g = f0 + i
             n = int(r["n"][i])

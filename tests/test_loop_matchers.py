@@ -177,9 +177,8 @@ def test_gpu_bow_kf(gpu_lib, kfs, ratio, ori, seed):
 @pytest.mark.gpu
 @pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("th,orb_dist,ori,seed", [(10, 100, True, 4), (3, 64, True, 5), (10, 100, False, 6)])
-def test_gpu_projection_kf(gpu_lib, kfs, th, orb_dist, ori, seed, single, monkeypatch):
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
-    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
+def test_gpu_projection_kf(gpu_lib, kfs, th, orb_dist, ori, seed, single, proj_form):
+    proj_form(single)
     from orb_slam3_vio_fixes_amd import orb
     k, d, valid, u, v, level, desc, angle, owner = proj_kf_inputs(kfs, seed)
     f = abi.frame_struct(k, d, W, H, scale_factors=kfs[1]["scale"])
@@ -192,9 +191,8 @@ def test_gpu_projection_kf(gpu_lib, kfs, th, orb_dist, ori, seed, single, monkey
 @pytest.mark.gpu
 @pytest.mark.parametrize("single", ["spec", "serial", "single"])
 @pytest.mark.parametrize("th,ratio,seed", [(10, 1.0, 7), (8, 0.5, 8), (40, 2.0, 13)])
-def test_gpu_projection_sim3(gpu_lib, kfs, th, ratio, seed, single, monkeypatch):
-    monkeypatch.setenv("ORBM_PROJ_SINGLE_WAVE", "1" if single == "single" else "0")
-    monkeypatch.setenv("ORBM_PROJ_SERIAL_RESOLVE", "1" if single == "serial" else "0")
+def test_gpu_projection_sim3(gpu_lib, kfs, th, ratio, seed, single, proj_form):
+    proj_form(single)
     from orb_slam3_vio_fixes_amd import orb
     k, d, valid, u, v, level, desc, _, matched = proj_kf_inputs(kfs, seed)
     kf = abi.frame_struct(k, d, W, H, scale_factors=kfs[1]["scale"])

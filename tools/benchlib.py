@@ -6,7 +6,7 @@ from __future__ import annotations
 import numpy as np
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
-STAGES = ["pyramid", "fast_cells", "quadtree", "blur", "describe", "assemble"]
+STAGES = ["pyramid", "fast_cells", "quadtree", "describe", "assemble"]
 
 
 def level_sizes(ex, w: int, h: int) -> list[int]:
