@@ -14,14 +14,19 @@
  * exactly as the reference writes it, hands flat snapshots to the device, and
  * writes MapPoint pointers back from the returned indices.
  *
- * Not compiled in this repository's container: Frame.h / KeyFrame.h pull in
- * Eigen, Sophus, g2o, boost serialization and OpenCV, which the image lacks.
- * Every Frame / KeyFrame / MapPoint / ORBmatcher member read here is checked
- * against its declaration in the reference's own headers by
- * tests/test_adapter.py (test_matcher_adapter_members_declared_in_reference_headers);
- * the extractor adapter next to it is compiled against the reference header
- * and run on the GPU (tests/test_gpu_adapter.py); the ABI calls here are those
- * of tests/native/cpp_api_test.cpp, which runs on the GPU.
+ * Both camera set-ups of the reference are handled: a pinhole / rectified
+ * frame (Nleft == -1: mvKeysUn, the stereo gate on mvuRight) and a fisheye
+ * stereo frame (Nleft != -1: keypoints indexed as [mvKeys; mvKeysRight],
+ * Frame.cc:1069-1071, with the right camera's grid, stereo partners and
+ * projections, ORBmatcher.cc:131-209, :1794-1860).
+ *
+ * tests/test_adapter.py compiles this file (g++ -fsyntax-only) against the
+ * reference's unmodified ORBmatcher.h / Frame.h / KeyFrame.h / MapPoint.h and
+ * their includes, with declaration-only stand-ins for the third-party headers
+ * the image lacks (OpenCV, Eigen, Sophus, g2o, boost serialization, Pangolin;
+ * tests/native/decl/); the extractor adapter next to it is compiled against
+ * the reference header and run on the GPU (tests/test_gpu_adapter.py); the ABI
+ * calls here are those of tests/native/cpp_api_test.cpp, which runs on the GPU.
  */
 #include "ORBmatcher.h"
 #include "KeyFrame.h"
@@ -38,17 +43,35 @@ namespace ORB_SLAM3
 
 namespace
 {
+static_assert(sizeof(cv::KeyPoint) == sizeof(orb_keypoint), "cv::KeyPoint is the 28-byte orb_keypoint");
+
+// The keypoints a frame's matchers index: mvKeysUn, or for a fisheye stereo
+// frame (nleft != -1) mvKeys followed by mvKeysRight (Frame.cc:1069-1071,
+// AssignFeaturesToGrid :401-415); `store` keeps the combined copy alive.
+template <class F> const cv::KeyPoint* keys_of(const F& f, int nleft, vector<cv::KeyPoint>& store, int& n)
+{
+    if (nleft == -1) {
+        n = (int)f.mvKeysUn.size();
+        return f.mvKeysUn.data();
+    }
+    store.assign(f.mvKeys.begin(), f.mvKeys.end());
+    store.insert(store.end(), f.mvKeysRight.begin(), f.mvKeysRight.end());
+    n = (int)store.size();
+    return store.data();
+}
+
 // A Frame / KeyFrame as the matchers read it (Frame.h:223-290).
-template <class F> orbm_frame view(const F& f)
+template <class F> orbm_frame view(const F& f, int nleft, vector<cv::KeyPoint>& store)
 {
     orbm_frame v;
-    v.n = (int32_t)f.mvKeysUn.size();
-    v.kps = reinterpret_cast<const orb_keypoint*>(f.mvKeysUn.data());
+    int n = 0;
+    v.kps = reinterpret_cast<const orb_keypoint*>(keys_of(f, nleft, store, n));
+    v.n = (int32_t)n;
     v.desc = f.mDescriptors.data;
     v.min_x = f.mnMinX; v.max_x = f.mnMaxX; v.min_y = f.mnMinY; v.max_y = f.mnMaxY;
     v.grid_inv_w = f.mfGridElementWidthInv;
     v.grid_inv_h = f.mfGridElementHeightInv;
-    v.u_right = f.mvuRight.empty() ? nullptr : f.mvuRight.data();
+    v.u_right = nleft != -1 || f.mvuRight.empty() ? nullptr : f.mvuRight.data();
     v.scale_factors = f.mvScaleFactors.data();
     v.nlevels = (int32_t)f.mvScaleFactors.size();
     return v;
@@ -84,7 +107,8 @@ int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f
                                         vector<int>& vnMatches12, int windowSize)
 {
     vnMatches12 = vector<int>(F1.mvKeysUn.size(), -1);
-    orbm_frame f1 = view(F1), f2 = view(F2);
+    vector<cv::KeyPoint> s1, s2;
+    orbm_frame f1 = view(F1, -1, s1), f2 = view(F2, -1, s2);     // monocular initialization: mvKeysUn
     static_assert(sizeof(cv::Point2f) == 2 * sizeof(float), "Point2f is two floats");
     const int n = orbm_search_for_initialization(&f1, &f2, reinterpret_cast<float*>(vbPrevMatched.data()),
                                                  windowSize, mfNNratio, mbCheckOrientation ? 1 : 0,
@@ -101,7 +125,11 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPoi
     for (size_t i = 0; i < vpMapPointsKF.size(); ++i)
         valid[i] = vpMapPointsKF[i] && !vpMapPointsKF[i]->isBad();   // :262-268
     FeatVecCSR kfv(pKF->mFeatVec), fv(F.mFeatVec);
-    orbm_frame kf = view(*pKF), f = view(F);
+    // keypoints for the rotation check (:290-292, :349-351): the keyframe's
+    // mvKeysUn, or its [mvKeys; mvKeysRight] when it has a second camera; the
+    // frame's combined array when it is a fisheye stereo frame
+    vector<cv::KeyPoint> skf, sf;
+    orbm_frame kf = view(*pKF, pKF->mpCamera2 ? pKF->NLeft : -1, skf), f = view(F, F.Nleft, sf);
     vector<int32_t> match(F.N, -1);
     const int n = F.Nleft == -1
                       ? orbm_search_by_bow(&kf, &kfv.c, valid.data(), &f, &fv.c, mfNNratio,
@@ -117,34 +145,57 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF, Frame& F, vector<MapPoint*>& vpMapPoi
 int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoints, const float th,
                                    const bool bFarPoints, const float thFarPoints)
 {
-    if (F.Nleft != -1)
-        throw std::runtime_error("ORBmatcher adapter: use orbm_search_by_projection_mps_fisheye for Nleft != -1");
     const int n = (int)vpMapPoints.size();
-    // MapPoint snapshot (the fields :50-75 read, under the MapPoint's locks)
+    const bool fisheye = F.Nleft != -1;
+    // MapPoint snapshot (the fields :50-75 and, for a fisheye frame, the right
+    // camera's :131-140 read, under the MapPoint's locks)
     vector<float> px(n), py(n), pxr(n), vcos(n), depth(n);
     vector<int32_t> level(n);
     vector<uint8_t> in_view(n), has_obs(n), desc((size_t)n * 32);
+    vector<float> rx, ry, rcos;
+    vector<int32_t> rlevel;
+    vector<uint8_t> rin_view;
+    if (fisheye) {
+        rx.resize(n); ry.resize(n); rcos.resize(n); rlevel.resize(n); rin_view.resize(n);
+    }
     for (int i = 0; i < n; ++i) {
         MapPoint* pMP = vpMapPoints[i];
-        in_view[i] = pMP->mbTrackInView && !pMP->isBad();
+        const bool bad = pMP->isBad();
+        in_view[i] = pMP->mbTrackInView && !bad;
         px[i] = pMP->mTrackProjX; py[i] = pMP->mTrackProjY; pxr[i] = pMP->mTrackProjXR;
         level[i] = pMP->mnTrackScaleLevel; vcos[i] = pMP->mTrackViewCos; depth[i] = pMP->mTrackDepth;
         has_obs[i] = pMP->Observations() > 0;
-        if (in_view[i]) {
+        if (fisheye) {
+            rin_view[i] = pMP->mbTrackInViewR && !bad;
+            rx[i] = pMP->mTrackProjXR; ry[i] = pMP->mTrackProjYR;
+            rlevel[i] = pMP->mnTrackScaleLevelR; rcos[i] = pMP->mTrackViewCosR;
+        }
+        if (in_view[i] || (fisheye && rin_view[i])) {
             const cv::Mat d = pMP->GetDescriptor();
             std::copy(d.data, d.data + 32, desc.begin() + (size_t)i * 32);
         }
     }
     orbm_mappoints mps{n, px.data(), py.data(), pxr.data(), level.data(), vcos.data(), depth.data(),
                        in_view.data(), has_obs.data(), desc.data()};
-    // slots that already hold a MapPoint: opaque owner, blocked when observed (:86-88)
+    // slots that already hold a MapPoint: opaque owner, blocked when observed (:86-88, :155-157)
     vector<int32_t> owner(F.N, -1);
     vector<uint8_t> blocked(F.N, 0);
     for (int i = 0; i < F.N; ++i)
         if (F.mvpMapPoints[i]) { owner[i] = -2; blocked[i] = F.mvpMapPoints[i]->Observations() > 0; }
-    orbm_frame f = view(F);
-    const int nm = orbm_search_by_projection_mps(&f, &mps, th, bFarPoints ? 1 : 0, thFarPoints, mfNNratio,
-                                                 owner.data(), blocked.data());
+    vector<cv::KeyPoint> store;
+    orbm_frame f = view(F, F.Nleft, store);
+    int nm;
+    if (!fisheye) {
+        nm = orbm_search_by_projection_mps(&f, &mps, th, bFarPoints ? 1 : 0, thFarPoints, mfNNratio, owner.data(),
+                                           blocked.data());
+    } else {
+        // left camera, then the right camera's grid by local index; a match
+        // also claims its stereo partner (mvLeftToRightMatch / mvRightToLeftMatch)
+        orbm_mappoints_right mpr{rin_view.data(), rx.data(), ry.data(), rlevel.data(), rcos.data()};
+        nm = orbm_search_by_projection_mps_fisheye(&f, F.Nleft, F.mvLeftToRightMatch.data(),
+                                                   F.mvRightToLeftMatch.data(), &mps, &mpr, th, bFarPoints ? 1 : 0,
+                                                   thFarPoints, mfNNratio, owner.data(), blocked.data());
+    }
     check(nm, "SearchByProjection(F, MapPoints)");
     for (int i = 0; i < F.N; ++i)
         if (owner[i] >= 0) F.mvpMapPoints[i] = vpMapPoints[owner[i]];
@@ -153,19 +204,21 @@ int ORBmatcher::SearchByProjection(Frame& F, const vector<MapPoint*>& vpMapPoint
 
 int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, const float th, const bool bMono)
 {
-    if (CurrentFrame.Nleft != -1)
-        throw std::runtime_error("ORBmatcher adapter: use orbm_search_by_projection_last_fisheye for Nleft != -1");
-    // the pose math of :1686-1720, per last-frame point, unchanged
+    const bool fisheye = CurrentFrame.Nleft != -1;
+    // the pose math of :1686-1720 (and :1794-1796 for the right camera), per
+    // last-frame point, unchanged
     const Sophus::SE3f Tcw = CurrentFrame.GetPose();
     const Eigen::Vector3f twc = Tcw.inverse().translation();
     const Sophus::SE3f Tlw = LastFrame.GetPose();
     const Eigen::Vector3f tlc = Tlw * twc;
     const bool bForward = tlc(2) > CurrentFrame.mb && !bMono;
     const bool bBackward = -tlc(2) > CurrentFrame.mb && !bMono;
+    Sophus::SE3f Trl;
+    if (fisheye) Trl = CurrentFrame.GetRelativePoseTrl();
 
     const int n = LastFrame.N;
     vector<uint8_t> valid(n, 0), has_obs(n, 0), desc((size_t)n * 32, 0);
-    vector<float> u(n, 0.f), v(n, 0.f), ur(n, 0.f), angle(n, 0.f);
+    vector<float> u(n, 0.f), v(n, 0.f), ur(n, 0.f), vr(n, 0.f), angle(n, 0.f);
     vector<int32_t> octave(n, 0);
     for (int i = 0; i < n; ++i) {
         MapPoint* pMP = LastFrame.mvpMapPoints[i];
@@ -178,9 +231,21 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
         if (uv(1) < CurrentFrame.mnMinY || uv(1) > CurrentFrame.mnMaxY) continue;
         valid[i] = 1;
         u[i] = uv(0); v[i] = uv(1);
-        ur[i] = uv(0) - CurrentFrame.mbf * invzc;   // :1763
-        octave[i] = LastFrame.mvKeys[i].octave;
-        angle[i] = LastFrame.mvKeysUn[i].angle;
+        // the last frame's keypoint of point i (:1721-1722, :1775-1777)
+        const bool right_kp = LastFrame.Nleft != -1 && i >= LastFrame.Nleft;
+        const cv::KeyPoint& kpo = right_kp ? LastFrame.mvKeysRight[i - LastFrame.Nleft] : LastFrame.mvKeys[i];
+        const cv::KeyPoint& kpa = LastFrame.Nleft == -1 ? LastFrame.mvKeysUn[i] : kpo;
+        octave[i] = kpo.octave;
+        angle[i] = kpa.angle;
+        if (fisheye) {
+            // the right camera's projection (:1795-1796: the reference projects
+            // with mpCamera)
+            const Eigen::Vector3f x3Dr = Trl * x3Dc;
+            const Eigen::Vector2f uvr = CurrentFrame.mpCamera->project(x3Dr);
+            ur[i] = uvr(0); vr[i] = uvr(1);
+        } else {
+            ur[i] = uv(0) - CurrentFrame.mbf * invzc;   // :1763
+        }
         // a slot this point claims blocks later points iff it is observed (:1747-1749)
         has_obs[i] = pMP->Observations() > 0;
         const cv::Mat d = pMP->GetDescriptor();
@@ -193,11 +258,18 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, const Frame& LastFrame, 
             owner[i] = -2;
             blocked[i] = CurrentFrame.mvpMapPoints[i]->Observations() > 0;
         }
-    orbm_frame cur = view(CurrentFrame);
+    vector<cv::KeyPoint> store;
+    orbm_frame cur = view(CurrentFrame, CurrentFrame.Nleft, store);
     const int mode = bForward ? 1 : (bBackward ? 2 : 0);
-    const int nm = orbm_search_by_projection_last(&cur, n, valid.data(), u.data(), v.data(), ur.data(), octave.data(),
-                                                  angle.data(), has_obs.data(), desc.data(), th, mode,
-                                                  mbCheckOrientation ? 1 : 0, owner.data(), blocked.data());
+    const int nm = !fisheye
+                       ? orbm_search_by_projection_last(&cur, n, valid.data(), u.data(), v.data(), ur.data(),
+                                                        octave.data(), angle.data(), has_obs.data(), desc.data(), th,
+                                                        mode, mbCheckOrientation ? 1 : 0, owner.data(), blocked.data())
+                       : orbm_search_by_projection_last_fisheye(&cur, CurrentFrame.Nleft, n, valid.data(), u.data(),
+                                                                v.data(), ur.data(), vr.data(), octave.data(),
+                                                                angle.data(), has_obs.data(), desc.data(), th, mode,
+                                                                mbCheckOrientation ? 1 : 0, owner.data(),
+                                                                blocked.data());
     check(nm, "SearchByProjection(F, LastFrame)");
     for (int i = 0; i < CurrentFrame.N; ++i)
         if (owner[i] >= 0) CurrentFrame.mvpMapPoints[i] = LastFrame.mvpMapPoints[owner[i]];

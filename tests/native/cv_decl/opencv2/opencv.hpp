@@ -12,6 +12,9 @@
 
 #define CV_8U 0
 #define CV_8UC1 0
+#define CV_32F 5
+#define CV_32FC1 5
+#define CV_64F 6
 
 namespace cv {
 typedef unsigned char uchar;
@@ -24,7 +27,16 @@ public:
 };
 typedef Point_<int> Point2i;
 typedef Point_<float> Point2f;
+typedef Point_<double> Point2d;
 typedef Point2i Point;
+template <typename T> class Point3_ {
+public:
+    Point3_();
+    Point3_(T x, T y, T z);
+    T x, y, z;
+};
+typedef Point3_<float> Point3f;
+typedef Point3_<double> Point3d;
 template <typename T> class Size_ {
 public:
     Size_(T w, T h);
@@ -52,6 +64,7 @@ class Mat {
 public:
     Mat();
     Mat(int rows, int cols, int type);
+    Mat(int rows, int cols, int type, void* data, size_t step = 0);
     Mat(const Mat& m);
     Mat& operator=(const Mat& m);
     ~Mat();
@@ -63,6 +76,17 @@ public:
     void release();
     bool empty() const;
     int type() const;
+    bool isContinuous() const;
+    size_t elemSize() const;
+    size_t total() const;
+    uchar* ptr(int i0 = 0);
+    const uchar* ptr(int i0 = 0) const;
+    template <typename T> T* ptr(int i0 = 0);
+    template <typename T> const T* ptr(int i0 = 0) const;
+    template <typename T> T& at(int i0, int i1);
+    template <typename T> const T& at(int i0, int i1) const;
+    template <typename T> T& at(int i0);
+    template <typename T> const T& at(int i0) const;
     int flags, dims, rows, cols;
     uchar* data;
     MatStep step;

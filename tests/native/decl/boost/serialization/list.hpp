@@ -1,0 +1,3 @@
+// Declaration-only stand-in (see serialization.hpp).
+#pragma once
+#include "serialization.hpp"

@@ -1,9 +1,12 @@
 """The drop-in adapters.  The ORBextractor adapter (adapters/orbslam3/ORBextractor.cc)
 compiles against the reference's own, unmodified include/ORBextractor.h
-(include/ORBextractor.h:43-109) and this repository's C ABI.  OpenCV is absent
-from the image, so tests/native/cv_decl/ declares the subset of its API that
-the header and the adapter use (syntax check only: nothing is linked or run).
-Skipped where the reference tree is not present (the GPU box)."""
+(include/ORBextractor.h:43-109) and this repository's C ABI; the ORBmatcher
+adapter against ORBmatcher.h, Frame.h, KeyFrame.h, MapPoint.h and their
+includes.  OpenCV, Eigen, Sophus, g2o, Boost.Serialization and Pangolin are
+absent from the image, so tests/native/cv_decl/ and tests/native/decl/ declare
+the subset of their APIs those headers and the adapters use (syntax check
+only: nothing is linked or run).  Skipped where the reference tree is not
+present (the GPU box)."""
 import shutil
 import subprocess
 from pathlib import Path
@@ -34,54 +37,32 @@ def test_adapter_uses_only_declared_abi():
         assert used <= declared, (src.name, used - declared)
 
 
-# Every Frame / KeyFrame / MapPoint / ORBmatcher member the matcher adapter
-# (adapters/orbslam3/ORBmatcher_searches.cc) reads, with the declaration the
-# adapter's use assumes, found in the reference's own headers.  The adapter
-# itself cannot be compiled here: those headers pull in Eigen, Sophus, g2o
-# and boost serialization (Frame.h:25-40, KeyFrame.h:23-39, Converter.h:23-30),
-# none of which the image has.
-MATCHER_MEMBERS = {
-    "Frame.h": [r"float mbf;", r"float mb;", r"int N;", r"std::vector<cv::KeyPoint> mvKeys\b",
-                r"std::vector<cv::KeyPoint> mvKeysUn;", r"std::vector<MapPoint\*> mvpMapPoints;",
-                r"std::vector<float> mvuRight;", r"DBoW2::FeatureVector mFeatVec;", r"cv::Mat mDescriptors\b",
-                r"std::vector<bool> mvbOutlier;", r"static float mfGridElementWidthInv;",
-                r"static float mfGridElementHeightInv;", r"vector<float> mvScaleFactors;", r"static float mnMinX;",
-                r"static float mnMaxX;", r"static float mnMinY;", r"static float mnMaxY;",
-                r"GeometricCamera\* mpCamera\b", r"int Nleft\b", r"inline Sophus::SE3<float> GetPose\(\) const"],
-    "KeyFrame.h": [r"const float mfGridElementWidthInv;", r"const float mfGridElementHeightInv;",
-                   r"const std::vector<cv::KeyPoint> mvKeysUn;", r"const std::vector<float> mvuRight;",
-                   r"const cv::Mat mDescriptors;", r"DBoW2::FeatureVector mFeatVec;",
-                   r"const std::vector<float> mvScaleFactors;", r"const int mnMinX;", r"const int mnMinY;",
-                   r"const int mnMaxX;", r"const int mnMaxY;", r"std::vector<MapPoint\*> GetMapPointMatches\(\);"],
-    "MapPoint.h": [r"float mTrackProjX;", r"float mTrackProjY;", r"float mTrackDepth;", r"float mTrackProjXR;",
-                   r"bool mbTrackInView\b", r"int mnTrackScaleLevel\b", r"float mTrackViewCos\b",
-                   r"Eigen::Vector3f GetWorldPos\(\);", r"int Observations\(\);", r"bool isBad\(\);",
-                   r"cv::Mat GetDescriptor\(\);"],
-    "ORBmatcher.h": [r"float mfNNratio;", r"bool mbCheckOrientation;",
-                     r"int SearchByProjection\(Frame &F, const std::vector<MapPoint\*> &vpMapPoints, const float th=3, "
-                     r"const bool bFarPoints = false, const float thFarPoints = 50.0f\);",
-                     r"int SearchByProjection\(Frame &CurrentFrame, const Frame &LastFrame, const float th, "
-                     r"const bool bMono\);",
-                     r"int SearchByBoW\(KeyFrame \*pKF, Frame &F, std::vector<MapPoint\*> &vpMapPointMatches\);",
-                     r"int SearchForInitialization\(Frame &F1, Frame &F2, std::vector<cv::Point2f> &vbPrevMatched, "
-                     r"std::vector<int> &vnMatches12, int windowSize=10\);"],
-    "CameraModels/GeometricCamera.h": [r"virtual Eigen::Vector2f project\(const Eigen::Vector3f & v3D\) = 0;"],
-}
-
-
 @pytest.mark.skipif(not (REF_INC / "Frame.h").exists(), reason="reference tree not present")
-def test_matcher_adapter_members_declared_in_reference_headers():
-    import re
-    for hdr, pats in MATCHER_MEMBERS.items():
-        text = (REF_INC / hdr).read_text()
-        for pat in pats:
-            assert re.search(pat, text), f"{hdr}: no declaration matching {pat!r}"
-    # and the adapter reads no member outside that list
-    src = (ROOT / "adapters" / "orbslam3" / "ORBmatcher_searches.cc").read_text()
-    src = re.sub(r"//[^\n]*", "", re.sub(r"/\*.*?\*/", "", src, flags=re.S))
-    used = set(re.findall(r"(?:\.|->)\s*(m[a-z]{0,2}[A-Z]\w*|mbf?|N|Nleft|GetPose|GetMapPointMatches|GetWorldPos|Observations|"
-                          r"isBad|GetDescriptor|project)\b", src))
-    missing = {u for u in used if not any(re.search(r"\b%s\b" % re.escape(u), p) for ps in MATCHER_MEMBERS.values()
-                                          for p in ps)}
-    assert not missing, f"adapter members not checked against the reference headers: {missing}"
-    assert {"mTrackProjX", "mnTrackScaleLevel", "mvbOutlier", "mFeatVec"} <= used
+@pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
+def test_matcher_adapter_compiles_against_reference_headers():
+    """adapters/orbslam3/ORBmatcher_searches.cc -- the four per-frame search
+    bodies, pinhole and fisheye stereo (Nleft != -1) branches -- compiles
+    against the reference's unmodified ORBmatcher.h / Frame.h / KeyFrame.h /
+    MapPoint.h and every reference header they include (Map.h, Converter.h,
+    GeometricCamera.h, ImuTypes.h, Settings.h, SerializationUtils.h, the
+    vendored DBoW2), with declaration-only stand-ins only for the third-party
+    libraries the image lacks (tests/native/decl: OpenCV, Eigen, Sophus, g2o,
+    Boost.Serialization, Pangolin).  Syntax check: nothing is linked or run.
+    The adapter itself must compile warning-free under -Wall -Wextra (the
+    reference's own headers warn)."""
+    ref = REF_INC.parent
+    native = ROOT / "tests" / "native"
+    src = ROOT / "adapters" / "orbslam3" / "ORBmatcher_searches.cc"
+    cmd = ["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra",
+           "-I", str(native / "decl"), "-I", str(REF_INC), "-I", str(REF_INC / "CameraModels"), "-I", str(ref),
+           "-I", str(ROOT / "include"), str(src)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-4000:]
+    own = [ln for ln in r.stderr.splitlines() if ln.startswith(str(src) + ":") and "warning" in ln]
+    assert not own, own
+    # no branch the reference handles is refused: the only throw is the C ABI's error status
+    text = src.read_text()
+    assert text.count("throw ") == 1 and "Nleft != -1" not in text.split("throw ")[1].split(";")[0]
+    for fn in ("orbm_search_by_projection_mps_fisheye", "orbm_search_by_projection_last_fisheye",
+               "orbm_search_by_bow_fisheye"):
+        assert fn + "(" in text
