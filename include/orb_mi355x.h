@@ -169,6 +169,16 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
  * the original index (within array i) of the element the sort puts at j;
  * fallback[i] = 1 where the depth limit sent the array to the sequential port
  * (the heap-sort case).  Returns ORB_OK, ORB_ERR_PARAM or ORB_ERR_DEVICE. */
+/* The fused FAST pre-test of k_pyr_stream (test hook, not part of the
+ * reference interface): for frame `frame` of the last orbx_extract_batch_device
+ * call and level `level`, the bitmap of the pixels passing the compass test of
+ * ORBextractor's FAST(iniThFAST) candidates (bit x & 7 of byte x >> 3 of row
+ * y; defined inside the union of the level's FAST windows, rows win[0]..win[1],
+ * columns win[2]..win[3]); win[4] / win[5] receive the bytes per row and the
+ * rows dst must hold (dst may be NULL to query win).  ORB_ERR_UNSUPPORTED when
+ * that call's FAST pass did not take its candidates from the pre-test. */
+int orbx_debug_pretest(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int32_t* win);
+
 int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* cnt, const int32_t* x0,
                     int32_t* perm, int32_t* fallback);
 

@@ -206,16 +206,22 @@ constexpr int kPsRun = 4;                 // k_pyr_stream: output rows per run (
 // k_pyr_stream layout for level-0 chunks of K0 rows: runs the step schedule
 // (level l computes at step s every row whose two source rows of level l-1
 // were visible at the start of step s, i.e. written at a step < s; chunk c of
-// level 0 is written at step c) and sizes each level's ring to the rows that
-// must coexist: those written at a step and every row still to be read at
-// that step or later.  Fills PS (except the table offsets) and `steps`;
+// level 0 is written at step c; with the fused FAST pre-test, level m's
+// pre-test at step s takes every window row y whose row y + 3 was visible)
+// and sizes each level's ring to the rows that must coexist: those written at
+// a step and every row still to be read at that step or later.  Fills PS
+// (except the table offsets) and `steps` (PS.E entries per step: [0] the
+// step's wave-items, [l] level l's resize, [L + m] level m's pre-test);
 // returns the LDS bytes of the rings.
-static long long pyr_stream_schedule(const Plan& P, const std::vector<int2>& rows_tab, int K0, int R, PyrStream& PS,
-                                     std::vector<int4>& steps) {
+static long long pyr_stream_schedule(const Plan& P, const std::vector<int2>& rows_tab, int K0, int R, bool pretest,
+                                     PyrStream& PS, std::vector<int4>& steps) {
     const int L = P.L, h0 = P.lv[0].h;
     PS.K0 = K0;
     PS.nchunks = (h0 + K0 - 1) / K0;
-    std::vector<int> next(L, 0), vis(L, 0);
+    PS.pretest = pretest;
+    PS.E = pretest ? 2 * L : L;
+    std::vector<int> next(L, 0), vis(L, 0), ptn(L, 0);
+    for (int m = 0; m < L; ++m) ptn[m] = PS.pt_y0[m];
     struct Span { int rd_lo, wr_lo, wr_hi; };
     std::vector<std::vector<Span>> hist(L);
     steps.clear();
@@ -223,10 +229,12 @@ static long long pyr_stream_schedule(const Plan& P, const std::vector<int2>& row
     for (;; ++s) {
         bool done = true;
         for (int l = 1; l < L; ++l) done &= next[l] >= P.lv[l].h;
+        if (pretest)
+            for (int m = 0; m < L; ++m) done &= ptn[m] >= PS.pt_y1[m];
         if (done) break;
         if (s > 4 * h0 + 64) return -1;                  // no progress (cannot happen for valid tables)
         vis[0] = std::min(s * K0, h0);
-        std::vector<int4> row(L, make_int4(0, 0, 0, 0));
+        std::vector<int4> row(PS.E, make_int4(0, 0, 0, 0));
         int wtotal = 0;
         std::vector<Span> sp(L, Span{INT32_MAX, 0, 0});
         // level 0: chunk s written at this step
@@ -236,22 +244,34 @@ static long long pyr_stream_schedule(const Plan& P, const std::vector<int2>& row
             const int lo = next[l];
             int hi = lo;
             while (hi < hl && (rows_tab[P.lv[l].ytab + hi].x >> 16) < vis[l - 1]) ++hi;
-            if (hi > lo) sp[l - 1].rd_lo = rows_tab[P.lv[l].ytab + lo].x & 0xffff;
-            if (l < L - 1) sp[l].wr_lo = lo, sp[l].wr_hi = hi;
+            if (hi > lo) sp[l - 1].rd_lo = std::min(sp[l - 1].rd_lo, rows_tab[P.lv[l].ytab + lo].x & 0xffff);
+            sp[l].wr_lo = lo, sp[l].wr_hi = hi;
             const int runs = (hi - lo + R - 1) / R;           // runs of <= R rows per column group
             const int wi = (runs * ng + kWave - 1) / kWave;
             row[l] = make_int4(lo, hi - lo, wtotal, ng | (runs << 16));
             wtotal += wi;
             next[l] = hi;
         }
+        if (pretest)
+            for (int m = 0; m < L; ++m) {
+                const int lo = ptn[m];
+                int hi = lo;
+                while (hi < PS.pt_y1[m] && hi + 3 < vis[m]) ++hi;
+                if (hi > lo) sp[m].rd_lo = std::min(sp[m].rd_lo, lo - 3);
+                const int wi = ((hi - lo) * PS.pt_ngx[m] + kWave - 1) / kWave;
+                row[L + m] = make_int4(lo, hi - lo, wtotal, PS.pt_ngx[m]);
+                wtotal += wi;
+                ptn[m] = hi;
+            }
         row[0] = make_int4(wtotal, 0, 0, 0);
         steps.insert(steps.end(), row.begin(), row.end());
         for (int l = 1; l < L; ++l) vis[l] = next[l];
-        for (int m = 0; m < L - 1; ++m) hist[m].push_back(sp[m]);
+        for (int m = 0; m < L; ++m) hist[m].push_back(sp[m]);
     }
     PS.nsteps = s;
     long long bytes = 0;
-    for (int m = 0; m < L - 1; ++m) {
+    const int nring = pretest ? L : L - 1;               // the last level's rows only feed the pre-test
+    for (int m = 0; m < nring; ++m) {
         int need = 1, fut = INT32_MAX;
         for (int t = s - 1; t >= 0; --t) {                // minimum row read at step >= t
             fut = std::min(fut, hist[m][t].rd_lo);
@@ -298,9 +318,19 @@ static bool pyr_col_records(const Plan& P, const std::vector<int2>& tab, int l, 
 
 // The k_pyr_stream plan: table image (column records, row records) and
 // rings in one LDS image of at most 160 KiB, with the largest level-0 chunk
-// (<= 32 rows) that fits; PS.ok stays false when the size is not supported
-// (more than kPsMaxLevels levels, weights or tap spans outside what the
-// kernel's byte selection handles, or no chunk size fits).
+// (<= 32 rows) that fits -- with the fused FAST pre-test if any chunk size
+// leaves room for its rings (7 rows of every level), else without; PS.ok stays
+// false when the size is not supported (more than kPsMaxLevels levels,
+// weights or tap spans outside what the kernel's byte selection handles, or no
+// chunk size fits).  Table image (dwords, 16-byte aligned sections):
+//   [nsteps]            per-step wave-item counters (zeros)
+//   [L] uint4 level A   {column records dw, row records dw, HBM offset, pitch}
+//   [L] uint4 level B   {ring dw | ring pitch dw << 16, ring rows | pre-test
+//                        16-px group origin << 8 | bitmap pitch << 16,
+//                        bitmap offset, 0}
+//   [nsteps][E] uint4   step entries (pyr_stream_schedule)
+//   per level l >= 1: column records W[4 ng] S[4 ng] BF[ng], row records
+//                        uint2 {source ring dw r0 | r1 << 16, b0 | b1 << 16}
 static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<uint32_t>& img,
                              std::vector<int4>& steps) {
     PyrStream PS;
@@ -321,58 +351,72 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
             rows_tab.push_back(make_int2(r0 | (r1 << 16), e.y));
         }
     }
+    // the fused pre-test covers the union of the level's FAST windows, in
+    // groups of 16 pixels (columns 16 g - 4 .. 16 g + 19 of a ring row must
+    // exist: the windows lie >= 19 px inside the level); the bitmap path of
+    // k_fast_cells reads windows of <= 64 columns
+    bool pt_ok = P.bm_ok;
+    for (int m = 0; m < L && pt_ok; ++m) {
+        PS.pt_y0[m] = P.win_y0[m]; PS.pt_y1[m] = P.win_y1[m];
+        PS.pt_gx0[m] = P.win_x0[m] >> 4;
+        PS.pt_ngx[m] = ((P.win_x1[m] + 15) >> 4) - PS.pt_gx0[m];
+        pt_ok = PS.pt_gx0[m] >= 1 && PS.pt_gx0[m] < 256 && 16 * (PS.pt_gx0[m] + PS.pt_ngx[m]) + 4 <= P.lv[m].w + 12 &&
+                PS.pt_y0[m] >= 3 && PS.pt_y1[m] + 3 <= P.lv[m].h && PS.pt_y1[m] > PS.pt_y0[m];
+    }
     Plan Q = P;                       // the schedule reads lv[l].ytab of the row table above
     Q.lv = lv;
     int K0 = 0;
     int rec_dw = 0;                   // column and row records
     for (int l = 1; l < L; ++l) {
         const int ng = (P.lv[l].w + 3) / 4;
-        rec_dw += round_up(9 * ng, 4) + 4 * P.lv[l].h;
+        rec_dw += round_up(9 * ng, 4) + round_up(2 * P.lv[l].h, 4);
     }
     // ORB_PYR_K0 (build flag, A/B): force the level-0 chunk rows (0: the largest that fits)
     const int k0_env = ORB_PYR_K0, run_rows = kPsRun;
     const int nq16 = (P.lv[0].w + 15) / 16;
     int tab_dw = 0;
-    for (int k : {32, 24, 16, 12, 8, 6, 4}) {
-        if (k0_env > 0 && k != k0_env) continue;
-        if (k * nq16 > 2 * 1024) continue;                 // two 16-byte chunk loads per thread at most
-        std::vector<int4> st;
-        PyrStream T;
-        const long long rb = pyr_stream_schedule(Q, rows_tab, k, run_rows, T, st);
-        const int td = round_up(T.nsteps, 4) + 4 * L + 4 * T.nsteps * L + rec_dw;
-        if (rb < 0 || 4LL * td + rb > 160 * 1024) continue;
-        K0 = k;
-        tab_dw = td;
-        PS = T;
-        steps = st;
-        break;
+    for (int pass = pt_ok ? 0 : 1; pass < 2 && !K0; ++pass) {
+        const bool pretest = pass == 0;
+        for (int k : {32, 24, 16, 12, 8, 6, 4}) {
+            if (k0_env > 0 && k != k0_env) continue;
+            if (k * nq16 > 2 * 1024) continue;                 // two 16-byte chunk loads per thread at most
+            std::vector<int4> st;
+            PyrStream T = PS;
+            const long long rb = pyr_stream_schedule(Q, rows_tab, k, run_rows, pretest, T, st);
+            const int td = round_up(T.nsteps, 4) + 8 * L + 4 * T.nsteps * T.E + rec_dw;
+            if (rb < 0 || 4LL * td + rb > 160 * 1024) continue;
+            K0 = k;
+            tab_dw = td;
+            PS = T;
+            steps = st;
+            break;
+        }
     }
     if (K0 == 0) return;
-    // LDS image: level table, step table, records, then the rings (16-byte aligned)
+    // LDS image: counters, level tables, step table, records, then the rings
     img.assign(tab_dw, 0u);
-    // per-step wave-item counters first (zeros in the image), then the level
-    // and step tables
     PS.cnt_dw = 0;
     PS.lev_u4 = round_up(PS.nsteps, 4) / 4;
-    PS.steps_u4 = PS.lev_u4 + L;
+    PS.steps_u4 = PS.lev_u4 + 2 * L;
     std::memcpy(&img[4 * PS.steps_u4], steps.data(), steps.size() * sizeof(int4));
-    int dw = 4 * (PS.steps_u4 + PS.nsteps * L);
+    int dw = 4 * (PS.steps_u4 + PS.nsteps * PS.E);
     for (int l = 1; l < L; ++l) {
         const int ng = (P.lv[l].w + 3) / 4;
         PS.ng[l] = ng;
         PS.rec_dw[l] = dw;
         dw += round_up(9 * ng, 4);
         PS.yt_dw[l] = dw;
-        dw += 4 * P.lv[l].h;
-        img[4 * (PS.lev_u4 + l)] = (uint32_t)PS.rec_dw[l];
-        img[4 * (PS.lev_u4 + l) + 1] = (uint32_t)PS.yt_dw[l];
+        dw += round_up(2 * P.lv[l].h, 4);
     }
     int rdw = tab_dw;
-    for (int m = 0; m < L - 1; ++m) {
+    const int nring = PS.pretest ? L : L - 1;
+    for (int m = 0; m < nring; ++m) {
         PS.ring_dw[m] = rdw;
         rdw += PS.ring_rows[m] * PS.ring_pitch[m] / 4;
     }
     if (rdw >= 65536) return;                              // row records hold 16-bit dword offsets
+    for (int m = 0; m < nring; ++m)
+        if (PS.ring_rows[m] >= 256 || PS.ring_pitch[m] / 4 >= 65536) return;   // 8-bit ring rows in level table B
     // ORB_OPT_PYR_CNT_END (test hook, orb_debug_set_option): the per-step
     // counters after the rings, at the top of the allocation, outside the copied
     // table image (the kernel zeroes them there); the default keeps them at dword
@@ -382,6 +426,22 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
         rdw += round_up(PS.nsteps, 4);
     }
     if (4LL * rdw > 160 * 1024) return;
+    for (int l = 0; l < L; ++l) {
+        const LevelDev& d = P.lv[l];
+        uint32_t* A = &img[4 * (PS.lev_u4 + l)];
+        uint32_t* Bv = &img[4 * (PS.lev_u4 + L + l)];
+        if (l >= 1) {
+            A[0] = (uint32_t)PS.rec_dw[l];
+            A[1] = (uint32_t)PS.yt_dw[l];
+            A[2] = (uint32_t)d.off;
+            A[3] = (uint32_t)d.pitch;
+        }
+        if (l < nring) {
+            Bv[0] = (uint32_t)PS.ring_dw[l] | ((uint32_t)(PS.ring_pitch[l] / 4) << 16);
+            Bv[1] = (uint32_t)PS.ring_rows[l] | ((uint32_t)PS.pt_gx0[l] << 8) | ((uint32_t)d.bm_pitch << 16);
+            Bv[2] = (uint32_t)d.bm_off;
+        }
+    }
     for (int l = 1; l < L; ++l) {
         const LevelDev& d = P.lv[l];
         const int ng = PS.ng[l];
@@ -395,13 +455,9 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
             const int r0 = e.x & 0xffff, r1 = e.x >> 16, m = l - 1;
             const uint32_t o0 = (uint32_t)(PS.ring_dw[m] + (r0 % PS.ring_rows[m]) * PS.ring_pitch[m] / 4);
             const uint32_t o1 = (uint32_t)(PS.ring_dw[m] + (r1 % PS.ring_rows[m]) * PS.ring_pitch[m] / 4);
-            const uint32_t dst = l < L - 1 ? (uint32_t)(PS.ring_dw[l] + (dy % PS.ring_rows[l]) * PS.ring_pitch[l] / 4)
-                                           : 0xffffffffu;
-            uint32_t* r = &img[PS.yt_dw[l] + 4 * dy];
+            uint32_t* r = &img[PS.yt_dw[l] + 2 * dy];
             r[0] = o0 | (o1 << 16);
             r[1] = (uint32_t)e.y;
-            r[2] = dst;
-            r[3] = (uint32_t)(d.off + (long long)dy * d.pitch);
         }
     }
     PS.tab_u4 = tab_dw / 4;
@@ -423,6 +479,9 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     P.tab_off.assign(L, 0);
     long long poff = 0;
     int cellsum = 0, slotsum = 0, outsum = 0;
+    P.win_y0.assign(L, INT32_MAX); P.win_y1.assign(L, 0); P.win_x0.assign(L, INT32_MAX); P.win_x1.assign(L, 0);
+    P.bm_ok = true;
+    long long bmoff = 0;
     for (int l = 0; l < L; ++l) {
         LevelDev& d = P.lv[l];
         // ComputePyramid sizes (ORBextractor.cc:1174-1175)
@@ -498,6 +557,12 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
                 c.cols = (int)maxX - c.x0; c.rows = (int)maxY - c.y0;
                 c.slot_off = slotsum;
                 c.cap = cap;
+                // the FAST window (the ROI less its 3-px border): union per level
+                P.win_y0[l] = std::min(P.win_y0[l], c.y0 + 3);
+                P.win_y1[l] = std::max(P.win_y1[l], c.y0 + c.rows - 3);
+                P.win_x0[l] = std::min(P.win_x0[l], c.x0 + 3);
+                P.win_x1[l] = std::max(P.win_x1[l], c.x0 + c.cols - 3);
+                P.bm_ok &= c.cols - 6 <= 64 && c.rows - 6 <= 64;
                 slotsum += cap;
                 P.cells.push_back(c);
                 // + 16: the pre-test reads up to 2 dwords past the last row's window
@@ -518,6 +583,11 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         }
         d.ncells = nc;
         cellsum += nc;
+        // pre-test bitmap rows: one bit per pixel, 16 bytes of slack (k_fast_cells
+        // reads 4 dwords from the dword holding a window row's first bit)
+        d.bm_pitch = round_up((d.w + 7) / 8 + 16, 16);
+        d.bm_off = bmoff;
+        bmoff += (long long)d.bm_pitch * d.h;
         if (P.item_max >= 65536) return ORB_ERR_UNSUPPORTED;   // 16-bit item indices in k_fast_cells' list
         d.slot_total = slotsum - d.slot_base;
         P.max_level_cells = std::max(P.max_level_cells, nc);
@@ -544,6 +614,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     for (const PyrGroup& g : P.pgroups)
         if (pyr_group_lds(g) > 160 * 1024) return ORB_ERR_UNSUPPORTED;   // a level row beyond ~80 KB
     P.pyr_bytes = poff;
+    P.bm_bytes = round_up((int)std::min<long long>(bmoff, 1ll << 30), 256);
     P.ncells = cellsum;
     P.slot_total = slotsum;
     P.out_total = outsum;
@@ -551,6 +622,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
 
     const size_t B = (size_t)maxB;
     ORB_CHECK(hipMalloc(&P.d_pyr, std::max<size_t>(1, B * P.pyr_bytes)));
+    if (P.ps.ok && P.ps.pretest) ORB_CHECK(hipMalloc(&P.d_bm, B * P.bm_bytes));
     ORB_CHECK(hipMalloc(&P.d_in, P.in_pitch * h));
     ORB_CHECK(hipMalloc(&P.d_tab, std::max<size_t>(1, tab.size()) * sizeof(int2)));
     ORB_CHECK(hipMalloc(&P.d_lv, L * sizeof(LevelDev)));
@@ -765,6 +837,62 @@ __global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
     }
 }
 
+// Compass pre-test, 4 pixels per lane: a 9-pixel arc of the 16-ring always
+// covers two ring-adjacent compass pixels -- one of {U, D} and one of {L, R} --
+// so a brighter corner at threshold t has min(max(U,D), max(L,R)) > v + t and
+// a darker one max(min(U,D), min(L,R)) < v - t (ORB_FAST_COMPASS_AND; round 2
+// tested the looser 2nd largest / 2nd smallest of the four).  Pixels failing both at min(iniTh, minTh) are corners at no
+// threshold used; their score stays 0, which the NMS treats exactly like a
+// non-corner (s_t(q) = 0).  Bytes are split into u16 pairs (pixels 0/2 and
+// 1/3) and tested with packed u16 min/max; the flags are the signs of packed
+// differences, gathered into one flag byte per pixel.  (A planar u16 ROI --
+// even and odd columns de-interleaved at landing, no splitting here -- was
+// measured slower: 0.575 vs 0.510 ms, twice the LDS reads per item.)
+
+#ifndef ORB_FAST_COMPASS_AND
+#define ORB_FAST_COMPASS_AND 1   // pre-test: one vertical AND one horizontal compass pixel past the threshold
+#endif
+// Flags as signs: (C + t) - L2 and (S2 + t) - C as packed u16 differences;
+// every value is < 2^10, so the i16 sign bit is exactly the bright / dark test.
+__device__ __forceinline__ void compass_signs(uint32_t c, uint32_t u, uint32_t d, uint32_t l, uint32_t r,
+                                              u16x2 tt, uint32_t& bneg, uint32_t& dneg) {
+    const u16x2 C = as_u16x2(c), U = as_u16x2(u), D = as_u16x2(d), L = as_u16x2(l), R = as_u16x2(r);
+    const u16x2 m1 = __builtin_elementwise_min(U, D), M1 = __builtin_elementwise_max(U, D);
+    const u16x2 m2 = __builtin_elementwise_min(L, R), M2 = __builtin_elementwise_max(L, R);
+    const u16x2 X = __builtin_elementwise_min(M1, M2), Y = __builtin_elementwise_max(m1, m2);
+#if ORB_FAST_COMPASS_AND
+    // every 9-arc holds two ring-adjacent compass pixels, one of {U, D} and
+    // one of {L, R}: a bright corner has min(max(U,D), max(L,R)) > v + t, a
+    // dark one max(min(U,D), min(L,R)) < v - t -- tighter than the 2nd
+    // largest / 2nd smallest of the four (which also passes U, D alone) and
+    // two packed ops cheaper; a failing direction still has strength - 1 < t
+    bneg = as_u32((C + tt) - X);
+    dneg = as_u32((Y + tt) - C);
+#else
+    const u16x2 L2 = __builtin_elementwise_max(X, Y), S2 = __builtin_elementwise_min(X, Y);
+    bneg = as_u32((C + tt) - L2);
+    dneg = as_u32((S2 + tt) - C);
+#endif
+}
+
+// pairs (pixels 0, 2) and (1, 3) of a dword -> one flag byte per pixel (bit 7), pixel order
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t p02, uint32_t p13) {
+    return __builtin_amdgcn_perm(p13, p02, 0x07030501u) & 0x80808080u;
+}
+
+// byte-flag mask of item pixels [s, e) (0 <= s, e <= 8): byte k of the (lo, hi) pair = pixel k
+__device__ __forceinline__ uint64_t item_byte_mask(int s, int e) {
+    const uint64_t hi = e >= 8 ? ~0ull : ((1ull << (8 * e)) - 1ull);
+    const uint64_t lo = s >= 8 ? ~0ull : ((1ull << (8 * s)) - 1ull);
+    return hi & ~lo & 0x8080808080808080ull;
+}
+
+__device__ __forceinline__ uint32_t lo_bytes(uint32_t x) { return x & 0x00ff00ffu; }
+// u16 pair (x.b1, x.b3) in one v_perm (a shift and a mask otherwise)
+__device__ __forceinline__ uint32_t hi_bytes(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); }
+// u16 pair of bytes (hi.bs1 | lo.bs0 selectors 0-3: lo, 4-7: hi) in one v_perm
+template <uint32_t SEL>
+__device__ __forceinline__ uint32_t pair_bytes(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_perm(hi, lo, SEL); }
 // ---------------------------------------------------------------------------
 // k_pyr_stream: ComputePyramid (ORBextractor.cc:1170-1195) of one frame per
 // 1024-thread workgroup, cv::resize INTER_LINEAR 8UC1, as a
@@ -795,9 +923,13 @@ struct PyrStreamArgs {
     long long pyr_fstride;
     const uint4* tab;           // LDS table image
     int tab_u4, lev_u4, steps_u4;   // table image size; level and step tables inside it (uint4 units)
-    int L, nsteps, nchunks, K0, h0, w0, nframes;
+    int L, E, nsteps, nchunks, K0, h0, w0, nframes;
     int ring0_dw, ring0_rows, ring0_pitch;
     int cnt_dw;                 // per-step wave-item counters (nsteps dwords)
+    int pretest;                // the fused FAST pre-test at ini_th (E = 2L)
+    int ini_th;
+    uint8_t* bm;                // pre-test bitmaps of frame 0 (LevelDev::bm_off / bm_pitch layout)
+    long long bm_fstride;
 };
 
 // Workgroup barrier that orders LDS only: __syncthreads()' workgroup fence
@@ -813,25 +945,57 @@ __device__ __forceinline__ uint32_t mulhi_u24(uint32_t a, uint32_t b) {
     return (uint32_t)(((uint64_t)(a & 0xffffffu) * (uint64_t)(b & 0xffffffu)) >> 32);
 }
 
-#ifndef ORB_PYR_PREF
-#define ORB_PYR_PREF 0   // 1: draw the next wave-item ticket while the current item runs
-#endif
+// y % n for 0 <= y < 2^16, 1 <= n < 256 by a float reciprocal: (y + 0.5) / n
+// lies >= 1 / (2n) from every integer, far beyond the reciprocal's error
+__device__ __forceinline__ int small_mod(int y, int n, float inv_n) {
+    return y - (int)__umul24((uint32_t)(((float)y + 0.5f) * inv_n), (uint32_t)n);
+}
+
+// The compass pre-test (above) of 16 consecutive pixels of a ring row at
+// threshold t: c[0..3] the pixels' dwords, cm / c4 the dwords left / right of
+// them, u / d the dwords 3 rows up / down.  Bit k of the result: pixel k passes
+// in some direction (bright or dark) -- a FAST candidate at t.
+__device__ __forceinline__ uint32_t pretest16(uint32_t cm, const uint4& c, uint32_t c4, const uint4& u,
+                                              const uint4& d, u16x2 tt) {
+    const uint32_t cw[6] = {cm, c.x, c.y, c.z, c.w, c4};
+    const uint32_t uw[4] = {u.x, u.y, u.z, u.w}, dw[4] = {d.x, d.y, d.z, d.w};
+    uint32_t bits = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t left = cw[k], cur = cw[k + 1], right = cw[k + 2];
+        uint32_t b0, k0, b1, k1;
+        // pixels (0, 2): left (-3, -1), right (3, 5); pixels (1, 3): left (-2, 0), right (4, 6)
+        compass_signs(lo_bytes(cur), lo_bytes(uw[k]), lo_bytes(dw[k]), hi_bytes(left),
+                      pair_bytes<0x0c050c03u>(right, cur), tt, b0, k0);
+        compass_signs(hi_bytes(cur), hi_bytes(uw[k]), hi_bytes(dw[k]), pair_bytes<0x0c040c02u>(cur, left),
+                      lo_bytes(right), tt, b1, k1);
+        const uint32_t f = sign_bytes(b0 | k0, b1 | k1);           // byte j: pixel j passes (bit 7)
+        bits |= __builtin_amdgcn_udot4(f >> 7, 0x08040201u, 0u, false) << (4 * k);
+    }
+    return bits;
+}
+
 __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
     extern __shared__ uint4 ps_lds[];
     uint32_t* lds = (uint32_t*)ps_lds;
     const int f = blockIdx.x;
     if (f >= a.nframes) return;
-    const int tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const int tid = threadIdx.x, lane = lane_id();
     for (int i = tid; i < a.tab_u4; i += 1024) ps_lds[i] = a.tab[i];
     if (a.cnt_dw >= 4 * a.tab_u4)                    // counters outside the image (ORB_OPT_PYR_CNT_END)
         for (int i = tid; i < a.nsteps; i += 1024) lds[a.cnt_dw + i] = 0;
     lds_barrier();
-    // lane l: level l's {column records, row records} dword offsets
-    const uint4 lvt = ps_lds[a.lev_u4 + min(lane, a.L - 1)];
+    // lane l: level l's tables A {column records dw, row records dw, HBM
+    // offset, pitch} and B {ring dw | ring pitch dw << 16, ring rows | pre-test
+    // group origin << 8 | bitmap pitch << 16, bitmap offset, -}
+    const uint4 lva = ps_lds[a.lev_u4 + min(lane, a.L - 1)];
+    const uint4 lvb = ps_lds[a.lev_u4 + a.L + min(lane, a.L - 1)];
     const uint8_t* src = a.src + f * a.src_fstride;
     uint8_t* pyr = a.pyr + f * a.pyr_fstride;
+    uint8_t* bm = a.bm + f * a.bm_fstride;
     const int nq = (a.w0 + 15) >> 4;
     const float inv_nq = 1.0f / (float)nq;
+    const u16x2 tt = {(unsigned short)a.ini_th, (unsigned short)a.ini_th};
     uint4 pre0 = make_uint4(0, 0, 0, 0), pre1 = pre0;
     // chunk c of level 0 -> registers (two 16-byte pieces per thread at most)
 #define PS_FETCH(c)                                                                            \
@@ -891,15 +1055,12 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
             land(s, pre0, pre1);
             if (a.load_mode == 16 && s + 1 < a.nchunks) PS_FETCH(s + 1);
         }
-        // lane l >= 1 holds level l's entry of this step {first row, rows, first
-        // wave-item, ng | runs << 16}; lane 0 {wave-items of the step}
-        const uint4 se = ps_lds[a.steps_u4 + s * a.L + min(lane, a.L - 1)];
+        // lane e >= 1 holds entry e of this step {first row, rows, first
+        // wave-item, ng | runs << 16 (resize) / groups (pre-test)}: e < L the
+        // resize of level e, e >= L the pre-test of level e - L; lane 0 {the
+        // step's wave-items}
+        const uint4 se = ps_lds[a.steps_u4 + s * a.E + min(lane, a.E - 1)];
         const int W = __builtin_amdgcn_readfirstlane((int)se.x);
-#if ORB_PYR_PREF
-        // the next item's ticket is drawn while the current item runs
-        int jn = 0;
-        if (lane == 0) jn = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
-#endif
         for (int it = 0; it <= W; ++it) {      // bounded: a wave never takes more than W items
             // wave-items are taken from a per-step LDS counter: waves that drew
             // cheap items take more, so the step ends when the work does.  The
@@ -908,22 +1069,45 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
             // zeroed above.  (Round 2 blamed a failing end-of-LDS layout on the
             // hardware; tests/test_gpu_configs.py runs that layout, zeroed,
             // bit-exact -- see DESIGN.md on the cause.)
-#if ORB_PYR_PREF
-            const int j = __builtin_amdgcn_readfirstlane(jn);
-            if (j >= W) break;
-            if (lane == 0) jn = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
-#else
             int jj = 0;
             if (lane == 0) jj = atomicAdd((int*)&lds[a.cnt_dw + s], 1);
             const int j = __builtin_amdgcn_readfirstlane(jj);
             if (j >= W) break;
-#endif
-            const int l = __builtin_popcountll(__ballot(lane >= 1 && lane < a.L && (int)se.z <= j));
-            const int lo = __builtin_amdgcn_readlane((int)se.x, l), nrows = __builtin_amdgcn_readlane((int)se.y, l);
-            const int wst = __builtin_amdgcn_readlane((int)se.z, l), ngr = __builtin_amdgcn_readlane((int)se.w, l);
-            const int rec = __builtin_amdgcn_readlane((int)lvt.x, l), ytd = __builtin_amdgcn_readlane((int)lvt.y, l);
-            const int runs = ngr >> 16, ng = ngr & 0xffff;
+            const int e = __builtin_popcountll(__ballot(lane >= 1 && lane < a.E && (int)se.z <= j));
+            const int lo = __builtin_amdgcn_readlane((int)se.x, e), nrows = __builtin_amdgcn_readlane((int)se.y, e);
+            const int wst = __builtin_amdgcn_readlane((int)se.z, e), ngr = __builtin_amdgcn_readlane((int)se.w, e);
             const int local = (j - wst) * kWave + lane;
+            if (e >= a.L) {
+                // pre-test of level m: lane = (row, 16-pixel group) of the step's rows
+                const int m = e - a.L;
+                const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)lvb.x, m);
+                const uint32_t b1 = (uint32_t)__builtin_amdgcn_readlane((int)lvb.y, m);
+                const uint32_t boff = (uint32_t)__builtin_amdgcn_readlane((int)lvb.z, m);
+                const int rdw = b0 & 0xffff, pdw = b0 >> 16, rr = b1 & 0xff, gx0 = (b1 >> 8) & 0xff, bp = b1 >> 16;
+                const int row = (int)(((float)local + 0.5f) * __builtin_amdgcn_rcpf((float)ngr));
+                const int g = local - (int)__umul24((uint32_t)row, (uint32_t)ngr);
+                if (row < nrows) {
+                    const int y = lo + row, gg = gx0 + g;
+                    const int sc = small_mod(y, rr, __builtin_amdgcn_rcpf((float)rr));
+                    const int su = sc >= 3 ? sc - 3 : sc - 3 + rr, sd = sc + 3 < rr ? sc + 3 : sc + 3 - rr;
+                    const int bc = rdw + (int)__umul24((uint32_t)sc, (uint32_t)pdw) + 4 * gg;
+                    const uint4 c = ps_lds[bc >> 2];
+                    const uint32_t cm = lds[bc - 1], c4 = lds[bc + 4];
+                    const uint4 u = ps_lds[(rdw + (int)__umul24((uint32_t)su, (uint32_t)pdw)) / 4 + gg];
+                    const uint4 d = ps_lds[(rdw + (int)__umul24((uint32_t)sd, (uint32_t)pdw)) / 4 + gg];
+                    const uint32_t bits = pretest16(cm, c, c4, u, d, tt);
+                    *(uint16_t*)(bm + boff + (uint32_t)y * (uint32_t)bp + 2 * gg) = (uint16_t)bits;
+                }
+                continue;
+            }
+            const int l = e;
+            const int rec = __builtin_amdgcn_readlane((int)lva.x, l), ytd = __builtin_amdgcn_readlane((int)lva.y, l);
+            const uint32_t loff = (uint32_t)__builtin_amdgcn_readlane((int)lva.z, l);
+            const uint32_t lpitch = (uint32_t)__builtin_amdgcn_readlane((int)lva.w, l);
+            const uint32_t rb0 = (uint32_t)__builtin_amdgcn_readlane((int)lvb.x, l);
+            const int rr = __builtin_amdgcn_readlane((int)lvb.y, l) & 0xff;
+            const bool ring_out = l < a.L - 1 || a.pretest;     // the last level's rows feed only the pre-test
+            const int runs = ngr >> 16, ng = ngr & 0xffff;
             const int run = (int)(((float)local + 0.5f) * __builtin_amdgcn_rcpf((float)ng));
             const int g = local - (int)__umul24(run, ng);
             if (run < runs) {
@@ -950,9 +1134,9 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
                 };
                 // every LDS read of the run first (row records, then both source
                 // rows of every output row), so the run waits on LDS latency twice
-                uint4 yr[kPsRun];
+                uint2 yr[kPsRun];
 #pragma unroll
-                for (int q = 0; q < kPsRun; ++q) yr[q] = ps_lds[(ytd >> 2) + y0 + min(q, nr - 1)];
+                for (int q = 0; q < kPsRun; ++q) yr[q] = ((const uint2*)lds)[(ytd >> 1) + y0 + min(q, nr - 1)];
                 uint32_t D[kPsRun][2][3];
 #pragma unroll
                 for (int q = 0; q < kPsRun; ++q)
@@ -961,6 +1145,8 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
                         const uint32_t* Rp = lds + (t ? yr[q].x >> 16 : yr[q].x & 0xffff) + bd;
                         D[q][t][0] = Rp[0]; D[q][t][1] = Rp[1]; D[q][t][2] = Rp[2];
                     }
+                // the run's ring slots: y0 % rr once, then consecutive with wrap
+                int slot = ring_out ? small_mod(y0, rr, __builtin_amdgcn_rcpf((float)rr)) : 0;
                 uint32_t hA[4], hB[4];
 #pragma unroll
                 for (int q = 0; q < kPsRun; ++q) {
@@ -987,8 +1173,9 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
                             const uint32_t x0 = __umul24(b0, hA[c] >> 16), x1 = __umul24(b1, hB[c] >> 16);
                             out |= (((x0 >> 16) + (x1 >> 16) + 2) >> 2) << (8 * c);
                         }
-                        if (yr[q].z != 0xffffffffu) lds[yr[q].z + g] = out;
-                        *(uint32_t*)(pyr + yr[q].w + 4 * g) = out;
+                        if (ring_out) lds[(rb0 & 0xffff) + __umul24((uint32_t)slot, rb0 >> 16) + g] = out;
+                        *(uint32_t*)(pyr + loff + (uint32_t)(y0 + q) * lpitch + 4 * g) = out;
+                        if (++slot == rr) slot = 0;
                     }
                 }
             }
@@ -1023,6 +1210,8 @@ struct FastArgs {
     int kmask_bytes;
     int cand_bytes;         // u16 candidate list, one entry per window pixel at most
     int ilist_bytes;        // u32 list of the pre-test items holding a candidate (ORB_FAST_EMIT 1)
+    const uint8_t* bm;      // k_pyr_stream's iniThFAST pre-test bitmaps of frame 0 (k_fast_cells<..., true>)
+    long long bm_fstride;
 };
 
 // Arc strength of one direction on the raw ring values: max over the 16 arcs
@@ -1114,62 +1303,6 @@ __device__ __forceinline__ bool nms_keep(const uint8_t* sc, int sp, int r, int c
     return keep;
 }
 
-// Compass pre-test, 4 pixels per lane: a 9-pixel arc of the 16-ring always
-// covers two ring-adjacent compass pixels -- one of {U, D} and one of {L, R} --
-// so a brighter corner at threshold t has min(max(U,D), max(L,R)) > v + t and
-// a darker one max(min(U,D), min(L,R)) < v - t (ORB_FAST_COMPASS_AND; round 2
-// tested the looser 2nd largest / 2nd smallest of the four).  Pixels failing both at min(iniTh, minTh) are corners at no
-// threshold used; their score stays 0, which the NMS treats exactly like a
-// non-corner (s_t(q) = 0).  Bytes are split into u16 pairs (pixels 0/2 and
-// 1/3) and tested with packed u16 min/max; the flags are the signs of packed
-// differences, gathered into one flag byte per pixel.  (A planar u16 ROI --
-// even and odd columns de-interleaved at landing, no splitting here -- was
-// measured slower: 0.575 vs 0.510 ms, twice the LDS reads per item.)
-
-#ifndef ORB_FAST_COMPASS_AND
-#define ORB_FAST_COMPASS_AND 1   // pre-test: one vertical AND one horizontal compass pixel past the threshold
-#endif
-// Flags as signs: (C + t) - L2 and (S2 + t) - C as packed u16 differences;
-// every value is < 2^10, so the i16 sign bit is exactly the bright / dark test.
-__device__ __forceinline__ void compass_signs(uint32_t c, uint32_t u, uint32_t d, uint32_t l, uint32_t r,
-                                              u16x2 tt, uint32_t& bneg, uint32_t& dneg) {
-    const u16x2 C = as_u16x2(c), U = as_u16x2(u), D = as_u16x2(d), L = as_u16x2(l), R = as_u16x2(r);
-    const u16x2 m1 = __builtin_elementwise_min(U, D), M1 = __builtin_elementwise_max(U, D);
-    const u16x2 m2 = __builtin_elementwise_min(L, R), M2 = __builtin_elementwise_max(L, R);
-    const u16x2 X = __builtin_elementwise_min(M1, M2), Y = __builtin_elementwise_max(m1, m2);
-#if ORB_FAST_COMPASS_AND
-    // every 9-arc holds two ring-adjacent compass pixels, one of {U, D} and
-    // one of {L, R}: a bright corner has min(max(U,D), max(L,R)) > v + t, a
-    // dark one max(min(U,D), min(L,R)) < v - t -- tighter than the 2nd
-    // largest / 2nd smallest of the four (which also passes U, D alone) and
-    // two packed ops cheaper; a failing direction still has strength - 1 < t
-    bneg = as_u32((C + tt) - X);
-    dneg = as_u32((Y + tt) - C);
-#else
-    const u16x2 L2 = __builtin_elementwise_max(X, Y), S2 = __builtin_elementwise_min(X, Y);
-    bneg = as_u32((C + tt) - L2);
-    dneg = as_u32((S2 + tt) - C);
-#endif
-}
-
-// pairs (pixels 0, 2) and (1, 3) of a dword -> one flag byte per pixel (bit 7), pixel order
-__device__ __forceinline__ uint32_t sign_bytes(uint32_t p02, uint32_t p13) {
-    return __builtin_amdgcn_perm(p13, p02, 0x07030501u) & 0x80808080u;
-}
-
-// byte-flag mask of item pixels [s, e) (0 <= s, e <= 8): byte k of the (lo, hi) pair = pixel k
-__device__ __forceinline__ uint64_t item_byte_mask(int s, int e) {
-    const uint64_t hi = e >= 8 ? ~0ull : ((1ull << (8 * e)) - 1ull);
-    const uint64_t lo = s >= 8 ? ~0ull : ((1ull << (8 * s)) - 1ull);
-    return hi & ~lo & 0x8080808080808080ull;
-}
-
-__device__ __forceinline__ uint32_t lo_bytes(uint32_t x) { return x & 0x00ff00ffu; }
-// u16 pair (x.b1, x.b3) in one v_perm (a shift and a mask otherwise)
-__device__ __forceinline__ uint32_t hi_bytes(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); }
-// u16 pair of bytes (hi.bs1 | lo.bs0 selectors 0-3: lo, 4-7: hi) in one v_perm
-template <uint32_t SEL>
-__device__ __forceinline__ uint32_t pair_bytes(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_perm(hi, lo, SEL); }
 constexpr int kCandIdx = 0x3fff, kCandBright = 0x4000, kCandDark = 0x8000;
 
 #ifdef ORB_FAST_TIMING
@@ -1348,8 +1481,35 @@ __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)
 // RP: the LDS pitch of a landed ROI in dwords, fixed at compile time (every
 // row offset of the pre-test, the ring and the diagonal reads an immediate),
 // or 0 for each cell's own nd
-template <int PDW, int NV, int RP>
+// Inclusive prefix sum over the wave by DPP (row_shr within rows of 16, then
+// the row broadcasts), no LDS traffic.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += dpp_mov<0x111, 0xf>(v, 0);   // row_shr:1
+    v += dpp_mov<0x112, 0xf>(v, 0);   // row_shr:2
+    v += dpp_mov<0x114, 0xf>(v, 0);   // row_shr:4
+    v += dpp_mov<0x118, 0xf>(v, 0);   // row_shr:8
+    v += dpp_mov<0x142, 0xa>(v, 0);   // row_bcast:15 -> rows 1, 3
+    v += dpp_mov<0x143, 0xc>(v, 0);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
+// The iniThFAST candidates of a cell's window from k_pyr_stream's bitmap
+// (k_fast_cells<..., BM = true>): lane r holds window row r's bitmap dwords
+// (the 3 dwords from the one holding the window's first column: a window is
+// <= 64 columns, so its bits lie within 96), issued one cell ahead like the ROI.
+struct BmFetch {
+    const uint8_t* row0;    // the bitmap row of window row 0, dword-aligned at the window's first column
+    int pitch, sh, ww, wh;
+};
+__device__ __forceinline__ void bm_issue(const BmFetch& bf, uint32_t (&w)[3]) {
+    const int r = min(lane_id(), max(bf.wh - 1, 0));
+    const GlobalWords p = (GlobalWords)(bf.row0 + (uint32_t)r * (uint32_t)bf.pitch);
+    w[0] = p[0]; w[1] = p[1]; w[2] = p[2];
+}
+
+template <int PDW, int NV, int RP, bool BM>
 __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
+    static_assert(!BM || ORB_FAST_DIAG, "bitmap candidates get their compass directions in the diagonal filter");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = lane_id(), wv = wave_id();
     uint8_t* roi = smem + wv * (a.roi_max + a.win_max + a.cand_bytes + a.kmask_bytes + a.ilist_bytes);   // multiples of 16
@@ -1390,14 +1550,30 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         rf.rows = max(1, c.rows);
         return rf;
     };
-    // cell descriptors (scalar loads) run two cells ahead, ROI loads one cell ahead
+    auto bm_of = [&](const CellDev& c) {
+        BmFetch bf;
+        const int xs = c.x0 + 3;
+        bf.pitch = lvc[c.level].bm_pitch;
+        bf.row0 = a.bm + bframe * a.bm_fstride + lvc[c.level].bm_off + (long long)(c.y0 + 3) * bf.pitch + 4 * (xs >> 5);
+        bf.sh = xs & 31;
+        bf.ww = max(0, c.cols - 6);
+        bf.wh = max(0, c.rows - 6);
+        return bf;
+    };
+    // cell descriptors (scalar loads) run two cells ahead, ROI (and bitmap) loads one cell ahead
     uint32_t v[NV];
+    uint32_t bmw[3] = {0u, 0u, 0u};
     CellDev c{}, cn{};
     RoiFetch rf{};
+    BmFetch bfc{};
     if (it0 < it_end) {
         c = cell_at(it0);
         rf = fetch_of(c, it0);
         roi_issue<PDW, NV>(rf, v);
+        if (BM) {
+            bfc = bm_of(c);
+            bm_issue(bfc, bmw);
+        }
     }
     if (it0 + step < it_end) cn = cell_at(it0 + step);
 #ifdef ORB_FAST_TIMING
@@ -1406,7 +1582,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #endif
     auto land = [&](const uint32_t (&vv)[NV], const RoiFetch& r) { roi_land<PDW, NV, RP>(r, vv, (uint32_t*)roi); };
     // one cell from its landed ROI
-    auto process = [&](const CellDev& cur, const RoiFetch& rfc, int it) {
+    auto process = [&](const CellDev& cur, const RoiFetch& rfc, const BmFetch& bfw, const uint32_t (&bw)[3], int it) {
         const int f = bframe;
         const int rstride = (RP ? RP : rfc.nd) * 4;
         const int shift = cur.x0 & 3;
@@ -1557,6 +1733,28 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 }
                 ncand += tot;
             };
+            if (BM && pass == 0) {
+                // 1'. the iniThFAST candidates from k_pyr_stream's pre-test bitmap:
+                //     lane r = window row r, its bits placed by a funnel shift,
+                //     row-major order by a wave prefix sum of the rows' counts.
+                //     Their passing directions are decided below (1c, from the
+                //     ring), so every candidate is tagged with both.
+                const int r = lane;
+                const uint64_t lo64 = ((uint64_t)bw[1] << 32) | bw[0];
+                uint64_t m64 = bfw.sh ? (lo64 >> bfw.sh) | ((uint64_t)bw[2] << (64 - bfw.sh)) : lo64;
+                if (ww < 64) m64 &= (1ull << ww) - 1ull;
+                if (r >= wh) m64 = 0;
+                const int pc = __popcll(m64);
+                const int incl = wave_incl_scan_dpp(pc);
+                int pos = incl - pc;
+                const int base = cand_enc(r, 0, ww) | kCandBright | kCandDark;
+                while (m64) {
+                    const int cb = __builtin_ctzll(m64);
+                    m64 &= m64 - 1;
+                    cand[pos++] = (uint16_t)(base + kCandColStep * cb);
+                }
+                ncand = __builtin_amdgcn_readlane(incl, kWave - 1);
+            } else {
 #if ORB_FAST_EMIT == 1
             // 1a. items holding a candidate go to the wave's item list, one
             //     ballot per round (at iniTh ~20 % of the items, ~3 pixels
@@ -1631,6 +1829,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 emit(bl, bh, dl, dh, i0);
             }
 #endif
+            }
             fast_wave_sync();
             if (pass == 0) FAST_T(1); else FAST_T(5);
 #if ORB_FAST_DIAG
@@ -1657,8 +1856,15 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                         const int v = p[0];
                         const int x2 = p[2 * rstride + 2], x6 = p[-2 * rstride + 2];
                         const int x10 = p[-2 * rstride - 2], x14 = p[2 * rstride - 2];
-                        const bool bo = (e & kCandBright) && min(max(x2, x10), max(x6, x14)) > v + t;
-                        const bool dk = (e & kCandDark) && max(min(x2, x10), min(x6, x14)) < v - t;
+                        bool bo = (e & kCandBright) && min(max(x2, x10), max(x6, x14)) > v + t;
+                        bool dk = (e & kCandDark) && max(min(x2, x10), min(x6, x14)) < v - t;
+                        if (BM && pass == 0) {
+                            // bitmap candidates: the compass directions (ring positions 0,
+                            // 4, 8, 12) here, as the pre-test would have tagged them
+                            const int xu = p[-3 * rstride], xd = p[3 * rstride], xl = p[-3], xr = p[3];
+                            bo = bo && min(max(xu, xd), max(xl, xr)) > v + t;
+                            dk = dk && max(min(xu, xd), min(xl, xr)) < v - t;
+                        }
                         keep = bo || dk;
                         e2 = (uint32_t)(e & kCandIdx) | (bo ? (uint32_t)kCandBright : 0u) | (dk ? (uint32_t)kCandDark : 0u);
                     }
@@ -1811,13 +2017,19 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         land(v, rf);
         const CellDev cur = c;
         const RoiFetch rcur = rf;
+        const BmFetch bcur = bfc;
+        uint32_t bw[3] = {bmw[0], bmw[1], bmw[2]};
         if (it + step < it_end) {
             c = cn;
             rf = fetch_of(c, it + step);
             roi_issue<PDW, NV>(rf, v);
+            if (BM) {
+                bfc = bm_of(c);
+                bm_issue(bfc, bmw);
+            }
         }
         if (it + 2 * step < it_end) cn = cell_at(it + 2 * step);
-        process(cur, rcur, it);
+        process(cur, rcur, bcur, bw, it);
     }
 #ifdef ORB_FAST_TIMING
     if (lane == 0) {
@@ -3205,6 +3417,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     P.d_tab = P0.d_tab; P.d_lv = P0.d_lv; P.d_cells = P0.d_cells; P.d_slot_level = P0.d_slot_level;
     const long long F = f0;
     P.d_pyr = P0.d_pyr + F * P0.pyr_bytes;
+    P.d_bm = P0.d_bm ? P0.d_bm + F * P0.bm_bytes : nullptr;
     P.d_cell_count = P0.d_cell_count + F * P0.ncells;
     P.d_cell_keys = P0.d_cell_keys + F * P0.slot_total;
     P.d_key_scr = P0.d_key_scr + F * P0.slot_total;
@@ -3248,10 +3461,14 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
         pa.load_mode = (al & 15) == 0 ? 16 : ((al & 3) == 0 ? 4 : 1);
         pa.pyr = P.d_pyr; pa.pyr_fstride = P.pyr_bytes;
         pa.tab = P0.d_ps_tab;
-        pa.tab_u4 = S.tab_u4; pa.lev_u4 = S.lev_u4; pa.steps_u4 = S.steps_u4; pa.L = L; pa.nsteps = S.nsteps; pa.nchunks = S.nchunks; pa.K0 = S.K0;
+        pa.tab_u4 = S.tab_u4; pa.lev_u4 = S.lev_u4; pa.steps_u4 = S.steps_u4; pa.L = L; pa.E = S.E;
+        pa.nsteps = S.nsteps; pa.nchunks = S.nchunks; pa.K0 = S.K0;
         pa.h0 = P.lv[0].h; pa.w0 = P.lv[0].w; pa.nframes = B;
         pa.ring0_dw = S.ring_dw[0]; pa.ring0_rows = S.ring_rows[0]; pa.ring0_pitch = S.ring_pitch[0];
         pa.cnt_dw = S.cnt_dw;
+        pa.pretest = S.pretest;
+        pa.ini_th = std::min(std::max(hd->prm.ini_th_fast, 0), 255);
+        pa.bm = P.d_bm; pa.bm_fstride = P0.bm_bytes;
         hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(1024), S.lds_bytes, st, pa);
     } else {
         for (const PyrGroup& g : P.pgroups) {
@@ -3290,19 +3507,31 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     // fetch row width (dwords) and loads per lane: <16, 12> takes ROIs of at
     // most 16 dwords by 48 rows (W = 35 cells are < 70 px: nd <= 19 and rows <
     // 76 always fit <32, 40>)
-    void (*kfast)(FastArgs);
+    void (*kfast)(FastArgs) = nullptr;
     const int ndm = P.roi_nd_max, rm = P.roi_rows_max;
     int rp = 0;    // fixed LDS pitch of the ROIs (dwords), 0: per cell
+    // the iniThFAST candidates come from k_pyr_stream's fused pre-test when it
+    // ran (BM forms); otherwise k_fast_cells pre-tests the landed ROI itself
+    const bool bm = use_stream && P0.ps.pretest && P.d_bm;
+    hd->bm_last = bm;
+    fa.bm = bm ? P.d_bm : nullptr;
+    fa.bm_fstride = P0.bm_bytes;
 #if ORB_FAST_FIXED_PITCH
-    if (ndm <= 11 && rm <= 64) { kfast = rm <= 48 ? k_fast_cells<16, 12, 11> : k_fast_cells<16, 16, 11>; rp = 11; }
-    else if (ndm <= 13 && rm <= 64) { kfast = rm <= 48 ? k_fast_cells<16, 12, 13> : k_fast_cells<16, 16, 13>; rp = 13; }
-    else
+    if (ndm <= 11 && rm <= 64) {
+        kfast = rm <= 48 ? (bm ? k_fast_cells<16, 12, 11, true> : k_fast_cells<16, 12, 11, false>)
+                         : (bm ? k_fast_cells<16, 16, 11, true> : k_fast_cells<16, 16, 11, false>);
+        rp = 11;
+    } else if (ndm <= 13 && rm <= 64) {
+        kfast = rm <= 48 ? (bm ? k_fast_cells<16, 12, 13, true> : k_fast_cells<16, 12, 13, false>)
+                         : (bm ? k_fast_cells<16, 16, 13, true> : k_fast_cells<16, 16, 13, false>);
+        rp = 13;
+    } else
 #endif
-    if (ndm <= 16 && rm <= 48) kfast = k_fast_cells<16, 12, 0>;
-    else if (ndm <= 16 && rm <= 64) kfast = k_fast_cells<16, 16, 0>;
-    else if (ndm <= 16 && rm <= 80) kfast = k_fast_cells<16, 20, 0>;
-    else if (ndm <= 32 && rm <= 48) kfast = k_fast_cells<32, 24, 0>;
-    else if (ndm <= 32 && rm <= 80) kfast = k_fast_cells<32, 40, 0>;
+    if (ndm <= 16 && rm <= 48) kfast = bm ? k_fast_cells<16, 12, 0, true> : k_fast_cells<16, 12, 0, false>;
+    else if (ndm <= 16 && rm <= 64) kfast = bm ? k_fast_cells<16, 16, 0, true> : k_fast_cells<16, 16, 0, false>;
+    else if (ndm <= 16 && rm <= 80) kfast = k_fast_cells<16, 20, 0, false>;
+    else if (ndm <= 32 && rm <= 48) kfast = k_fast_cells<32, 24, 0, false>;
+    else if (ndm <= 32 && rm <= 80) kfast = k_fast_cells<32, 40, 0, false>;
     else return ORB_ERR_UNSUPPORTED;
     fa.roi_max = (std::max(P0.roi_max, 4 * rm * rp + 16) + 15) & ~15;
     fa.win_max = (P.win_max + 15) & ~15;
@@ -3829,6 +4058,24 @@ int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, siz
     const size_t sp = level == 0 ? (size_t)h->last_pitch0 : (size_t)d.pitch;
     if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_debug_pretest(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int32_t* win) {
+    if (!h || !h->last_frames || frame < 0 || frame >= h->last_B || level < 0 || level >= h->plan.L)
+        return ORB_ERR_PARAM;
+    const Plan& P = h->plan;
+    if (!h->bm_last || !P.d_bm) return ORB_ERR_UNSUPPORTED;
+    const LevelDev& d = P.lv[level];
+    if (win) {
+        win[0] = P.win_y0[level]; win[1] = P.win_y1[level]; win[2] = P.win_x0[level]; win[3] = P.win_x1[level];
+        win[4] = (d.w + 7) / 8; win[5] = d.h;
+    }
+    if (!dst) return ORB_OK;
+    (void)hipSetDevice(h->device);
+    if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
+    ORB_CHECK(hipMemcpy2D(dst, dst_step, P.d_bm + (long long)frame * P.bm_bytes + d.bm_off, (size_t)d.bm_pitch,
+                          (size_t)(d.w + 7) / 8, d.h, hipMemcpyDeviceToHost));
     return ORB_OK;
 }
 

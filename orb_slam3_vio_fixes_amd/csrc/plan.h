@@ -26,6 +26,11 @@ struct LevelDev {
     // k_pyramid tables (l >= 1): column taps at xtab (padded to a multiple of
     // 4 columns), row taps at ytab
     int xtab, ytab;
+    // the fused pre-test's candidate bitmap (k_pyr_stream -> k_fast_cells): one
+    // bit per pixel (bit x & 7 of byte x >> 3 of a row), rows of bm_pitch bytes
+    // at bm_off of the frame's bitmap slab
+    long long bm_off;
+    int bm_pitch;
 };
 
 // One launch of k_pyramid: levels la+1..lb from level la, in nb bands of
@@ -54,6 +59,12 @@ struct PyrStream {
     int yt_dw[kPsMaxLevels] = {};          // level l >= 1: row records uint4 per row
     int ng[kPsMaxLevels] = {};             // column groups of 4 per level
     int cnt_dw = 0;                        // per-step wave-item counters (LDS dword offset)
+    // fused FAST pre-test at iniThFAST (k_fast_cells then reads the bitmap):
+    // per level the window rows [pt_y0, pt_y1) and 16-pixel groups
+    // [pt_gx0, pt_gx0 + pt_ngx); E step entries per step (2L with it, L without)
+    bool pretest = false;
+    int E = 0;
+    int pt_y0[kPsMaxLevels] = {}, pt_y1[kPsMaxLevels] = {}, pt_gx0[kPsMaxLevels] = {}, pt_ngx[kPsMaxLevels] = {};
 };
 
 struct CellDev {
@@ -71,6 +82,9 @@ struct Plan {
     int roi_max = 0, roi_rows_max = 0, roi_nd_max = 0, win_max = 0, max_level_cells = 0, max_out_cap = 0;
     int win_pix_max = 0;             // largest FAST window (cols-6)*(rows-6): candidate list entries
     int item_max = 0;                // most FAST pre-test items of a cell (k_fast_cells item list; < 65536)
+    std::vector<int> win_y0, win_y1, win_x0, win_x1;   // per level: union of the FAST windows
+    bool bm_ok = false;              // every window <= 64 x 64 px (k_fast_cells' bitmap path)
+    long long bm_bytes = 0;          // one frame's pre-test bitmap (k_pyr_stream with ps.pretest)
     std::vector<int> xmax;           // per level
     std::vector<long long> tab_off;  // per level: offset (int2 units) of the x table, y table follows
     std::vector<PyrGroup> pgroups;   // k_pyramid launches
@@ -94,6 +108,7 @@ struct Plan {
     uint32_t* d_pxw = nullptr;       //   and weights a0 | a1 << 16
     int2* d_pyt = nullptr;           // k_pyramid row taps: sy0 | sy1 << 16 (clamped), b0 | b1 << 16
     uint4* d_ps_tab = nullptr;       // k_pyr_stream LDS table image
+    uint8_t* d_bm = nullptr;         // [maxB][bm_bytes] pre-test bitmaps (ps.pretest)
     // single-image host path outputs
     orb_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
@@ -104,7 +119,7 @@ struct Plan {
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab};
+                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_bm};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();
@@ -130,6 +145,7 @@ struct orbx_handle {
     int nsub = 1;
     // pyramid kernel choice (orbx_set_pyramid_mode) and the last one run
     int pyr_mode = 0, pyr_last = 0;
+    bool bm_last = false;            // the last extraction's FAST candidates came from the fused pre-test
     // caller events recorded after pipeline stages (orbx_set_stage_event)
     hipEvent_t stage_ev[6] = {};
     std::vector<hipStream_t> sub_streams;

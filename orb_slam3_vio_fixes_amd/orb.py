@@ -133,6 +133,18 @@ class ORBextractor:
             out.append(a)
         return out
 
+    def debug_pretest(self, frame: int, level: int):
+        """k_pyr_stream's fused FAST pre-test bitmap of (frame, level) of the
+        last batch call (orbx_debug_pretest) as a bool array (h, w), and the
+        window union (y0, y1, x0, x1) inside which it is defined."""
+        win = np.zeros(6, np.int32)
+        capi.check(capi.lib().orbx_debug_pretest(self._h, frame, level, None, 0, abi.ptr(win)), "orbx_debug_pretest")
+        nb, h = int(win[4]), int(win[5])
+        raw = np.zeros((h, nb), np.uint8)
+        capi.check(capi.lib().orbx_debug_pretest(self._h, frame, level, abi.ptr(raw), nb, None), "orbx_debug_pretest")
+        bits = np.unpackbits(raw, axis=1, bitorder="little")
+        return bits.astype(bool), tuple(int(x) for x in win[:4])
+
     def debug_stage(self, stage: int, cap: int = 400000):
         kps = np.zeros(cap, abi.KEYPOINT_DTYPE)
         counts = np.zeros(self.nlevels, np.int32)

@@ -229,3 +229,46 @@ def test_pyr_stream_counters_at_lds_top(gpu_lib, w, h):
             np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"frame {f} level {lev}")
         ni = int(n[f])
         same_frame(orb.keypoints_from_device(kps[f, :ni]), desc[f, :ni].cpu().numpy(), int(mono[f]), rk, rd, rm)
+
+
+def _compass_candidates(img, t):
+    """The compass pre-test of k_fast_cells / k_pyr_stream restated in numpy:
+    every 9-arc of FAST's 16-ring holds one of {U, D} and one of {L, R}
+    (the pixels 3 px away), so a corner at t has min(max(U,D), max(L,R)) > v + t
+    (brighter ring) or max(min(U,D), min(L,R)) < v - t (darker ring)."""
+    a = img.astype(np.int32)
+    v = a[3:-3, 3:-3]
+    U, D, Lf, R = a[:-6, 3:-3], a[6:, 3:-3], a[3:-3, :-6], a[3:-3, 6:]
+    bright = np.minimum(np.maximum(U, D), np.maximum(Lf, R)) > v + t
+    dark = np.maximum(np.minimum(U, D), np.minimum(Lf, R)) < v - t
+    out = np.zeros(a.shape, bool)
+    out[3:-3, 3:-3] = bright | dark
+    return out
+
+
+@pytest.mark.parametrize("w,h,ini,mn", [(752, 480, 20, 7), (512, 512, 20, 7), (640, 480, 12, 5), (320, 240, 20, 7),
+                                        (753, 481, 30, 10)])
+def test_fused_pretest_bitmap(gpu_lib, w, h, ini, mn):
+    """k_pyr_stream's fused FAST pre-test (ORBextractor.cc:826 FAST(iniThFAST)
+    candidates, computed while each level's rows sit in the LDS rings) equals
+    the numpy compass test on the oracle's pyramid for every pixel of every
+    level's window union, and the FAST pass that takes its candidates from it
+    gives the oracle's keypoints and descriptors (ORBextractor.cc:781-896)."""
+    import torch
+    seq = synth.sequence(w, h, 3, config=2, start=900)
+    ex = orb.ORBextractor(1000, 1.2, 8, ini, mn)
+    ex.set_pyramid_mode(2)
+    kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
+    torch.cuda.synchronize()
+    assert ex.pyramid_kernel() == 2
+    for f in range(len(seq)):
+        ref = O.OracleExtractor(1000, 1.2, 8, ini, mn)
+        rk, rd, rm = ref(seq[f], (0, 1000))
+        for lev in range(8):
+            bm, (y0, y1, x0, x1) = ex.debug_pretest(f, lev)
+            lv = ref.level(lev)
+            want = _compass_candidates(lv, ini)
+            got = bm[:lv.shape[0], :lv.shape[1]]
+            np.testing.assert_array_equal(got[y0:y1, x0:x1], want[y0:y1, x0:x1], err_msg=f"frame {f} level {lev}")
+        ni = int(n[f])
+        same_frame(orb.keypoints_from_device(kps[f, :ni]), desc[f, :ni].cpu().numpy(), int(mono[f]), rk, rd, rm)
