@@ -117,7 +117,8 @@ def other_workload(args):
         a = types.SimpleNamespace(pairs=args.batch if batch_given else (128 if args.workload == "c3" else 64),
                                   steps=args.steps, warmup=args.warmup,
                                   cpu_sample=min(args.cpu_sample, 64 if args.workload == "c3" else 8),
-                                  cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))
+                                  cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))),
+                                  dump=args.dump)
         return bench_stereo.run_c3(a) if args.workload == "c3" else bench_stereo.run_c4(a)
     import bench_c5
     # the oracle checks every keyframe of rank 0's shard (a threaded map loop: a few seconds)

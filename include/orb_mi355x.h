@@ -179,6 +179,12 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
  * that call's FAST pass did not take its candidates from the pre-test. */
 int orbx_debug_pretest(orbx_handle* h, int frame, int level, uint8_t* dst, size_t dst_step, int32_t* win);
 
+/* The extraction plan of a w x h image on this handle (built if needed; test
+ * hook, not part of the reference interface): info[0..7] = k_pyr_stream usable,
+ * fused pre-test on, level-0 chunk rows, steps, LDS bytes, step entries, FAST
+ * cells per frame, every window <= 64 x 64 px.  Returns ORB_OK or an error. */
+int orbx_debug_plan_info(orbx_handle* h, int w, int h_, int32_t* info, int n);
+
 int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* cnt, const int32_t* x0,
                     int32_t* perm, int32_t* fallback);
 

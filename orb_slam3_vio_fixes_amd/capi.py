@@ -28,7 +28,7 @@ EXPORTS = [
     "orbm_search_by_sim3", "orbm_fuse_sim3", "orbm_search_by_bow_fisheye", "orbm_search_by_projection_mps_fisheye",
     "orbm_search_by_projection_last_fisheye", "orbx_set_pyramid_mode", "orbx_pyramid_kernel", "orbv_transform_device",
     "orbx_set_stage_event", "orb_debug_set_option", "orb_debug_get_option",
-    "orbm_release_scratch", "orbx_debug_pretest",
+    "orbm_release_scratch", "orbx_debug_pretest", "orbx_debug_plan_info",
 ]
 
 # orb_debug_set_option keys (include/orb_mi355x.h): alternative kernel forms
@@ -77,6 +77,7 @@ def load(path: Path | str = LIB_PATH):
     L.orb_debug_get_option.argtypes = [i32]
     L.orbm_release_scratch.argtypes = [vp, i32]
     L.orbx_debug_pretest.argtypes = [vp, i32, i32, vp, sz, vp]
+    L.orbx_debug_plan_info.argtypes = [vp, i32, i32, vp, i32]
     L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]
     L.orbm_fuse.argtypes = [vp, vp, i32, vp, vp, vp, vp, vp, vp, f32, i32, vp, vp]
     L.orbm_search_for_triangulation.argtypes = [vp, vp, vp, vp, vp, vp, vp, f32, f32, vp, i32, i32, i32, i32, vp]

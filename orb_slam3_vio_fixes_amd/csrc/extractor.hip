@@ -199,6 +199,9 @@ static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int
 
 constexpr int kPyrStreamMinFrames = 32;   // below this a frame per CU leaves the chip idle: row bands
 constexpr int kPsRun = 4;                 // k_pyr_stream: output rows per run (one lane, one column group)
+#ifndef ORB_PYR_PRETEST
+#define ORB_PYR_PRETEST 1   // the FAST pre-test at iniThFAST fused into k_pyr_stream (0: k_fast_cells pre-tests)
+#endif
 #ifndef ORB_PYR_K0
 #define ORB_PYR_K0 0
 #endif
@@ -355,7 +358,7 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
     // groups of 16 pixels (columns 16 g - 4 .. 16 g + 19 of a ring row must
     // exist: the windows lie >= 19 px inside the level); the bitmap path of
     // k_fast_cells reads windows of <= 64 columns
-    bool pt_ok = P.bm_ok;
+    bool pt_ok = P.bm_ok && ORB_PYR_PRETEST;
     for (int m = 0; m < L && pt_ok; ++m) {
         PS.pt_y0[m] = P.win_y0[m]; PS.pt_y1[m] = P.win_y1[m];
         PS.pt_gx0[m] = P.win_x0[m] >> 4;
@@ -2674,8 +2677,12 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
 // ---------------------------------------------------------------------------
 constexpr int kRaw = 43, kRawP = 48, kBl = 37;
 // column-major horizontal-pass buffer: hbT[col][row], a column's 43 rows plus
-// pad (u16 units; 22 dwords per column)
-constexpr int kHbT = 44;
+// pad (u16 units; ORB_DESC_HBT / 2 dwords per column)
+#ifndef ORB_DESC_HBT
+#define ORB_DESC_HBT 44
+#endif
+constexpr int kHbT = ORB_DESC_HBT;
+static_assert(kHbT >= 44 && kHbT % 2 == 0, "a column holds 43 rows plus the 7-tap read's pad, in whole dwords");
 #ifndef ORB_DESC_SLOTS
 #define ORB_DESC_SLOTS 16
 #endif
@@ -3149,9 +3156,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
                         const v4i_t acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(A, Bm[nb], bias, 0, 0, 0);
                         // rows r0..r0+3 of column x as u16
                         const int x = hm_col0(nb) + (lane & 15);
-                        *(uint2*)(hb + x * kHbT + r0) =
-                            make_uint2(__builtin_amdgcn_perm((uint32_t)acc[1], (uint32_t)acc[0], 0x05040100u),
-                                       __builtin_amdgcn_perm((uint32_t)acc[3], (uint32_t)acc[2], 0x05040100u));
+                        const uint32_t lo = __builtin_amdgcn_perm((uint32_t)acc[1], (uint32_t)acc[0], 0x05040100u);
+                        const uint32_t hi = __builtin_amdgcn_perm((uint32_t)acc[3], (uint32_t)acc[2], 0x05040100u);
+                        if ((kHbT / 2) % 2 == 0) {
+                            *(uint2*)(hb + x * kHbT + r0) = make_uint2(lo, hi);
+                        } else {
+                            // odd dword pitch: the pair is 4-byte aligned only (ds_write2_b32)
+                            uint32_t* d32 = (uint32_t*)(hb + x * kHbT + r0);
+                            d32[0] = lo;
+                            d32[1] = hi;
+                        }
                     }
                 }
             }
@@ -4058,6 +4072,17 @@ int orbx_get_batch_level(orbx_handle* h, int frame, int level, uint8_t* dst, siz
     const size_t sp = level == 0 ? (size_t)h->last_pitch0 : (size_t)d.pitch;
     if (h->batch_done) ORB_CHECK(hipEventSynchronize(h->batch_done));
     ORB_CHECK(hipMemcpy2D(dst, dst_step, src, sp, d.w, d.h, hipMemcpyDeviceToHost));
+    return ORB_OK;
+}
+
+int orbx_debug_plan_info(orbx_handle* h, int w, int hh, int32_t* info, int n) {
+    if (!h || !info || n < 1) return ORB_ERR_PARAM;
+    (void)hipSetDevice(h->device);
+    const int rc = build_plan(h, w, hh, std::max(1, h->plan.maxB));
+    if (rc != ORB_OK) return rc;
+    const PyrStream& S = h->plan.ps;
+    const int32_t v[8] = {S.ok, S.pretest, S.K0, S.nsteps, S.lds_bytes, S.E, h->plan.ncells, h->plan.bm_ok};
+    for (int i = 0; i < n && i < 8; ++i) info[i] = v[i];
     return ORB_OK;
 }
 

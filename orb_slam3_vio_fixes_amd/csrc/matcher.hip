@@ -615,6 +615,9 @@ constexpr int kSfiThreads = 256;
 #ifndef ORB_SFI_PRIO
 #define ORB_SFI_PRIO 1
 #endif
+#ifndef ORB_SFI_SPEC
+#define ORB_SFI_SPEC 1   // speculative 8-query runs (0: the serial step-per-query walk)
+#endif
 constexpr uint32_t kMdNone = 0xffff0000u;    // md21: no match yet (distance field 0xffff)
 __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
@@ -659,6 +662,133 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             if (c > 0) qlist[nq + mask_rank(m)] = i | (c > kTopK ? (int)0x80000000 : 0);
             nq += __popcll(m);
         }
+#if ORB_SFI_SPEC
+        // Speculative runs of 8 queries (the approach of k_proj_resolve_spec):
+        // lane 8t + k holds key k of query j0 + t; every query of the run
+        // decides against the state at the run's start, and the longest
+        // prefix of queries whose decision no earlier claim of the run can
+        // change is committed at once.  A query's decision reads its list up
+        // to its second live entry (all of it when fewer than two are live), and
+        // the state only ever blocks more entries (a claim lowers
+        // vMatchedDistance), so an earlier claim of an F2 feature outside that
+        // part leaves the decision exactly as the serial walk takes it.
+        // Committed claims are on distinct F2 features whose previous F1
+        // matches are distinct, so they are written in parallel.  A query whose
+        // truncated list cannot decide is rescanned exactly by the wave after
+        // the prefix is committed; a conflicting one is re-decided next round.
+        int nm = 0;
+        const float r = a.window;
+        const int grp = lane >> 3, kk = lane & 7;
+        auto run_keys = [&](int j0) -> uint32_t {
+            const int j = j0 + grp;
+            return j < nq ? topk[(long long)(qlist[j] & 0x7fffffff) * kTopK + kk] : kNoKey;
+        };
+        uint32_t kcur = nq > 0 ? run_keys(0) : kNoKey;
+        int j0 = 0;
+        while (j0 < nq) {
+            const int nrun = min(8, nq - j0);
+            const uint32_t knxt = j0 + 8 < nq ? run_keys(j0 + 8) : kNoKey;
+            const int qe = grp < nrun ? qlist[j0 + grp] : 0;
+            const bool many = qe < 0;
+            const bool kval = kcur != kNoKey;
+            const int kd = (int)((kcur >> 16) & 0x1ffu);
+            const int kfi = kval ? (int)(kcur & 0xffffu) : 0;
+            const uint32_t st = md21[kfi];
+            const bool live = kval && !((int)(st >> 16) <= kd);
+            const uint64_t m = __ballot(live);
+            const uint32_t gm = (uint32_t)(m >> (8 * grp)) & 0xffu;
+            const uint32_t gm2 = gm & (gm - 1);
+            const int p1 = gm ? __ffs(gm) - 1 : 8, p2 = gm2 ? __ffs(gm2) - 1 : 8;
+            const bool ok = __popc(gm) >= 2 || !many;
+            const int sl1 = 8 * grp + min(p1, 7), sl2 = 8 * grp + min(p2, 7);
+            const int best = p1 < 8 ? __shfl(kd, sl1, kWave) : INT_MAX;
+            const int bi = __shfl(kfi, sl1, kWave);
+            const uint32_t stb = (uint32_t)__shfl((int)st, sl1, kWave);
+            const uint32_t kb = (uint32_t)__shfl((int)kcur, sl1, kWave);
+            const int best2 = p2 < 8 ? __shfl(kd, sl2, kWave) : INT_MAX;
+            const bool acc = ok && grp < nrun && best <= kThLow && (float)best < (float)best2 * a.ratio;
+            // an earlier claim on an entry this query's decision reads stops it
+            const bool reads = kval && kk <= p2;
+            uint64_t confl = 0;
+            for (uint64_t am = __ballot(acc && kk == 0); am; am &= am - 1) {
+                const int l = __ffsll((long long)am) - 1;           // lane 8t' of a claiming query
+                const int cb = __builtin_amdgcn_readlane(bi, l);
+                confl |= __ballot(reads && kfi == cb && lane >= l + 8);
+            }
+            const bool stop = ((confl >> (8 * grp)) & 0xffull) != 0 || !ok || grp >= nrun;
+            const uint64_t sm = __ballot(stop && kk == 0);
+            const int P = sm ? (__ffsll((long long)sm) - 1) >> 3 : 8;
+            const bool commit = acc && grp < P && kk == 0;
+            const int i1 = qe & 0x7fffffff;
+            const int prev = (int)(stb & 0xffffu) - 1;
+            if (commit) {
+                if (prev >= 0) m12[prev] = -1;
+                m12[i1] = bi;
+                md21[bi] = ((uint32_t)best << 16) | (uint32_t)(i1 + 1);
+                if (a.check_ori) {
+                    bin1[i1] = (int8_t)(kb >> 25);
+                    atomicAdd(&hist[kb >> 25], 1);
+                }
+            }
+            nm += __popcll(__ballot(commit)) - __popcll(__ballot(commit && prev >= 0));
+            // the next round reads the state these writes left (one wave: its
+            // LDS operations complete in order; the asm keeps the compiler from
+            // hoisting the next reads above the stores)
+            asm volatile("" ::: "memory");
+            int adv = P;
+            if (P < nrun && __builtin_amdgcn_readlane((int)ok, 8 * P) == 0) {
+                // query j0 + P cannot decide from its truncated list: exact
+                // full candidate scan under the state after the prefix
+                const int qx = __builtin_amdgcn_readlane(qe, 8 * P);
+                const int q1 = qx & 0x7fffffff;
+                const orb_keypoint k1 = K1[q1];
+                float px, py;
+                query_pos(a, pr, q1, k1, px, py);
+                CellRange cr;
+                cell_range(px, py, r, a.g, cr);
+                const uint4 d0 = *(const uint4*)(D1 + (long long)q1 * 32);
+                const uint4 d1 = *(const uint4*)(D1 + (long long)q1 * 32 + 16);
+                Best2 bs{INT_MAX, INT_MAX, -1, 0, 0};
+                for (int base = 0; base < nl; base += kWave) {
+                    const int jj = base + lane;
+                    int d = INT_MAX, fi = -1;
+                    if (jj < nl) {
+                        d = cand_dist(list, jj, cr, px, py, r, K2, D2, d0, d1);
+                        fi = list[jj] & 0xffff;
+                        if (d != INT_MAX && (int)(md21[fi] >> 16) <= d) d = INT_MAX;
+                    }
+                    merge_chunk(bs, d, fi, 0);
+                }
+                if (bs.idx >= 0 && bs.best <= kThLow && (float)bs.best < (float)bs.best2 * a.ratio) {
+                    const int pv = (int)(md21[bs.idx] & 0xffffu) - 1;
+                    if (pv >= 0) --nm;
+                    ++nm;
+                    if (lane == 0) {
+                        if (pv >= 0) m12[pv] = -1;
+                        m12[q1] = bs.idx;
+                        md21[bs.idx] = ((uint32_t)bs.best << 16) | (uint32_t)(q1 + 1);
+                        if (a.check_ori) {
+                            const int bn = rot_bin(k1.angle, K2[bs.idx].angle);
+                            bin1[q1] = (int8_t)bn;
+                            atomicAdd(&hist[bn], 1);
+                        }
+                    }
+                    asm volatile("" ::: "memory");
+                }
+                adv = P + 1;
+            }
+            j0 += adv;
+            // the next run's keys: the uncommitted part of this run, then the prefetch
+            if (adv == 8) {
+                kcur = knxt;
+            } else {
+                const int src = lane + 8 * adv;
+                const uint32_t v1 = (uint32_t)__shfl((int)kcur, src & 63, kWave);
+                const uint32_t v2 = (uint32_t)__shfl((int)knxt, src & 63, kWave);
+                kcur = src < 64 ? v1 : v2;
+            }
+        }
+#else
         int nm = 0, hreg = 0;   // lane b: the rotation histogram's bin b
         const float r = a.window;
         const int grp = lane >> 3;
@@ -757,7 +887,10 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             }
           }
         }
+#if !ORB_SFI_SPEC
         if (lane < 32) hist[lane] = hreg;   // bins 0..29; hist[31] = 0 counts the drops below
+#endif
+#endif
         if (lane == 0) qlist[0] = nm;       // the query list is spent: hand nm to the block
     }
     __syncthreads();

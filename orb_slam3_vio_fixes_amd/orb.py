@@ -133,6 +133,13 @@ class ORBextractor:
             out.append(a)
         return out
 
+    def plan_info(self, w: int, h: int) -> dict:
+        """orbx_debug_plan_info: the k_pyr_stream / FAST plan for a w x h image."""
+        info = np.zeros(8, np.int32)
+        capi.check(capi.lib().orbx_debug_plan_info(self._h, w, h, abi.ptr(info), 8), "orbx_debug_plan_info")
+        keys = ["stream", "pretest", "K0", "nsteps", "lds_bytes", "entries", "ncells", "bm_ok"]
+        return dict(zip(keys, (int(x) for x in info)))
+
     def debug_pretest(self, frame: int, level: int):
         """k_pyr_stream's fused FAST pre-test bitmap of (frame, level) of the
         last batch call (orbx_debug_pretest) as a bool array (h, w), and the

@@ -244,21 +244,28 @@ def _graded_copies(k0, d0, base, copies, jitter, seed, flip):
     return np.array(ks, dtype=k0.dtype), np.array(ds, dtype=np.uint8)
 
 
-@pytest.mark.parametrize("copies,ratio,ori", [(12, 0.9, True), (20, 1.0, False), (9, 0.95, True)])
-def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, ratio, ori):
+@pytest.mark.parametrize("copies,ratio,ori,shuffle", [(12, 0.9, True, False), (20, 1.0, False, False),
+                                                      (9, 0.95, True, False), (12, 0.9, True, True),
+                                                      (20, 1.0, False, True)])
+def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, ratio, ori, shuffle):
     """F1 holds `copies` identical copies of each of 24 keypoints, F2 `copies`
     copies whose descriptors sit 0, 1, 2, ... bits away.  The copies of one
     F1 keypoint steal F2's copies one after the other (ORBmatcher.cc:680-700:
     a candidate whose matched distance is <= the query's is skipped), so
     after the eighth claim a query's top-8 list holds at most one live entry
     and the device resolve must fall back to its exact full rescan; the
-    ratio test stops the chain part way."""
+    ratio test stops the chain part way.  Consecutive copies make every
+    speculative 8-query run of k_sfi_resolve conflict; shuffled F1 spreads
+    the copies over runs (partial prefixes, rescans mid-run)."""
     k0, d0 = frames[0][0], frames[0][1]
     l0 = np.where(k0["octave"] == 0)[0]
     xs = k0["x"][l0]
     base = l0[np.argsort(xs)][:: max(1, len(l0) // 24)][:24]
     k1, d1 = _graded_copies(k0, d0, base, copies, 2.0, 1, False)
     k2, d2 = _graded_copies(k0, d0, base, copies, 2.0, 2, True)
+    if shuffle:
+        perm = np.random.default_rng(copies).permutation(len(k1))
+        k1, d1 = k1[perm], d1[perm]
     prev = np.stack([k1["x"], k1["y"]], 1)
     f1 = abi.frame_struct(k1, d1, 752, 480)
     f2 = abi.frame_struct(k2, d2, 752, 480)

@@ -109,3 +109,65 @@ def test_bench_overlap_two_handles_equals_one(tmp_path):
     for i in range(B - 1):
         m = int(b["n"][i])
         assert np.array_equal(a["matches"][i, :m], b["matches"][i, :m])
+
+
+def _stereo_runs(tmp_path, workload, P):
+    env = dict(os.environ, ORB_BENCH_BACKEND="gloo", MASTER_ADDR="127.0.0.1")
+    common = ["--workload", workload, "--steps", "1", "--warmup", "1", "--cpu-sample", "0"]
+    _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+          "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tools/bench_stereo.py",
+          "--pairs", str(P), "--dump", str(tmp_path / "two")] + common, env)
+    env1 = {k: v for k, v in env.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    _run([sys.executable, "tools/bench_stereo.py", "--pairs", str(2 * P), "--dump", str(tmp_path / "one")] + common,
+         env1)
+    return (np.load(tmp_path / "one" / "rank0.npz"), np.load(tmp_path / "two" / "rank0.npz"),
+            np.load(tmp_path / "two" / "rank1.npz"))
+
+
+def test_c3_two_ranks_equal_one_rank_with_seam_pair(tmp_path):
+    """Config C3 sharded: 2 ranks x 6 stereo pairs against 1
+    rank x 12 of the same global sequence.  Every pair's left keypoints and
+    descriptors, ComputeStereoMatches' mvuRight / mvDepth (Frame.cc:811-981,
+    bit-exact floats) and every consecutive-left-frame SearchForInitialization
+    (Tracking.cc:2459-2492) -- the seam pair through rank 0's halo frame --
+    equal the 1-rank run."""
+    P = 6
+    one, r0, r1 = _stereo_runs(tmp_path, "c3", P)
+    assert (int(r0["frames"]), int(r1["frames"])) == (P + 1, P)          # rank 0 carries the halo left frame
+    pairs = 0
+    for r in (r0, r1):
+        f0 = int(r["first"])
+        for i in range(P):
+            g = f0 + i
+            n = int(r["n"][i])
+            assert n == int(one["n"][g])
+            assert np.array_equal(r["kps"][i, :n], one["kps"][g, :n]) and np.array_equal(r["desc"][i, :n], one["desc"][g, :n])
+            assert np.array_equal(r["ur"][i, :n].view(np.uint32), one["ur"][g, :n].view(np.uint32)), g
+            assert np.array_equal(r["dep"][i, :n].view(np.uint32), one["dep"][g, :n].view(np.uint32)), g
+        for i in range(int(r["frames"]) - 1):
+            t = f0 + i
+            m = int(one["n"][t])
+            assert int(r["nmatch"][i]) == int(one["nmatch"][t]), t
+            assert np.array_equal(r["matches"][i, :m], one["matches"][t, :m]), t
+            pairs += 1
+    assert pairs == 2 * P - 1
+
+
+def test_c4_two_ranks_equal_one_rank(tmp_path):
+    """Config C4 sharded: 2 ranks x 4 fisheye pairs against 1 rank x 8; every
+    pair's keypoints, monoIndex and knnMatch(2) + ratio candidates over the
+    lapping areas (Frame.cc:1126-1156) equal the 1-rank run."""
+    P = 4
+    one, r0, r1 = _stereo_runs(tmp_path, "c4", P)
+    for r in (r0, r1):
+        f0 = int(r["first"])
+        for i in range(P):
+            g = f0 + i
+            for side in (i, P + i):                                      # left, right image of the pair
+                gs = g if side < P else 2 * P + g
+                n = int(r["n"][side])
+                assert n == int(one["n"][gs]) and int(r["mono"][side]) == int(one["mono"][gs])
+                assert np.array_equal(r["kps"][side, :n], one["kps"][gs, :n])
+            n = int(r["n"][i])
+            assert np.array_equal(r["l2r"][i, :n], one["l2r"][g, :n]), g
+            assert np.array_equal(r["idx"][i, :n], one["idx"][g, :n]), g

@@ -13,7 +13,15 @@ ORBextractor(1500) with lapping {0, 511}, the ComputeStereoFishEyeMatches
 candidates (knnMatch k=2 + Lowe 0.7 over the lapping areas, Frame.cc:1126-1156);
 the Kannala-Brandt triangulation of the candidates stays on the host.
 
-usage: python tools/bench_stereo.py [--workload c3|c4] [--pairs 128] [--steps 10] [--warmup 2]
+Multi-GPU (SURVEY.md §8(e)): one process per GPU under torch.distributed.run;
+pairs are sharded by contiguous range of ONE global sequence (pair g depends
+on g alone), --pairs per rank (weak scaling), no data-path collective; a
+barrier brackets the timed region and its time is the max over ranks.  C3's
+SearchForInitialization runs on consecutive LEFT frames, so every rank but the
+last also extracts the next rank's first left frame (the seam halo, not
+counted) and matches the pair across the seam; C4's pairs are independent.
+
+usage: python tools/bench_stereo.py [--workload c3|c4] [--pairs 128] [--steps 10] [--warmup 2] [--dump DIR]
 """
 from __future__ import annotations
 
@@ -55,6 +63,52 @@ def cpu_baseline(left, right, threads):
     return n / (time.perf_counter() - t0), outs
 
 
+def dist_init():
+    """(world, rank, device index) of this process; initialises the process
+    group for world > 1 (RCCL, or gloo with ORB_BENCH_BACKEND=gloo when ranks
+    share one GPU in tests), as bench.py does."""
+    import os
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = os.environ.get("ORB_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    return world, rank, local
+
+
+def dist_time(t0_fn, world, dev):
+    """Barrier + synchronize on both sides of the timed region; returns the
+    max over ranks of the elapsed time (t0_fn runs the timed steps)."""
+    import os
+    import torch
+    import torch.distributed as dist
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    t0_fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        nccl = os.environ.get("ORB_BENCH_BACKEND", "nccl") == "nccl"
+        t = torch.tensor([dt], dtype=torch.float64, device=dev if nccl else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workload", choices=["c3", "c4"], default="c3")
@@ -63,17 +117,26 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
     args = ap.parse_args()
-    print(json.dumps(run_c4(args) if args.workload == "c4" else run_c3(args)), flush=True)
+    out = run_c4(args) if args.workload == "c4" else run_c3(args)
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
 
 def run_c3(args):
     """Config C3 (see the module docstring); returns the JSON object."""
     import torch
     from orb_slam3_vio_fixes_amd import capi, orb, synth
-    dev = torch.device("cuda", 0)
+    world, rank, local = dist_init()
+    dev = torch.device("cuda", local)
     P = args.pairs
-    left, right = synth.stereo_sequence(W, H, P, config=3)
+    # pairs [rank P, (rank + 1) P) of one global sequence; the seam halo (the
+    # next rank's first left frame) is extracted but not counted
+    first = rank * P
+    Px = P + (1 if rank < world - 1 else 0)
+    left = synth.global_sequence(W, H, first, Px, config=3)
+    right = np.stack([synth.right_view(left[i], synth.frame_seed(3, first + i)) for i in range(P)])
     frames = torch.from_numpy(np.concatenate([left, right])).to(dev)
     L = capi.lib()
     stream = torch.cuda.current_stream(dev)
@@ -91,8 +154,8 @@ def run_c3(args):
         ur = torch.empty((P, cap), dtype=torch.float32, device=dev)
         sets.append({"ex": ex, "out": (kps, desc, n, mono), "cap": cap, "ur": ur, "dep": torch.empty_like(ur),
                      "sad": torch.empty((P, cap), dtype=torch.int32, device=dev),
-                     "matches": torch.empty((P - 1, cap), dtype=torch.int32, device=dev),
-                     "nmatch": torch.empty(P - 1, dtype=torch.int32, device=dev), "done": None})
+                     "matches": torch.empty((Px - 1, cap), dtype=torch.int32, device=dev),
+                     "nmatch": torch.empty(Px - 1, dtype=torch.int32, device=dev), "done": None})
     s_st, s_sfi = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     ev = []
     it = [0]
@@ -118,12 +181,12 @@ def run_c3(args):
         if e is not None:
             e[2].record(s_st)
             e[4].record(s_sfi)
-        capi.check(L.orbs_compute_stereo_matches_batch_device(S["ex"]._h, P, 0, P, kps.data_ptr(), desc.data_ptr(),
+        capi.check(L.orbs_compute_stereo_matches_batch_device(S["ex"]._h, P, 0, Px, kps.data_ptr(), desc.data_ptr(),
                                                               n.data_ptr(), cap, BASE, MBF, S["ur"].data_ptr(),
                                                               S["dep"].data_ptr(), S["sad"].data_ptr(),
                                                               s_st.cuda_stream), "stereo")
         capi.check(L.orbm_search_for_initialization_batch_device(
-            P, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
+            Px, kps.data_ptr(), desc.data_ptr(), n.data_ptr(), cap, 0.0, float(W), 0.0, float(H), inv_w, inv_h,
             100, 0.9, 1, S["matches"].data_ptr(), S["nmatch"].data_ptr(), s_sfi.cuda_stream), "sfi")
         if e is not None:
             e[3].record(s_st)
@@ -165,24 +228,38 @@ def run_c3(args):
     torch.cuda.synchronize()
     exs = [S["ex"] for S in sets]
     benchlib.profile_on(exs)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed=True)
-    flush()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+
+    def timed():
+        for _ in range(args.steps):
+            step(timed=True)
+        flush()
+    dt = dist_time(timed, world, dev)
     xst, calls = benchlib.profile_read(exs)
+    if args.dump:
+        S = sets[(it[0] - 1) % 2]                            # the last step's outputs, global pair indices
+        Path(args.dump).mkdir(parents=True, exist_ok=True)
+        np.savez(Path(args.dump) / f"rank{rank}.npz", first=first, pairs=P, frames=Px, world=world,
+                 kps=S["out"][0].cpu().numpy(), desc=S["out"][1].cpu().numpy(), n=S["out"][2].cpu().numpy(),
+                 ur=S["ur"].cpu().numpy(), dep=S["dep"].cpu().numpy(), matches=S["matches"].cpu().numpy(),
+                 nmatch=S["nmatch"].cpu().numpy())
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return None
     stage = {"extract_2B_images": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
              "compute_stereo_matches_side_stream": float(np.mean([e[2].elapsed_time(e[3]) for e in ev])),
              "search_for_initialization_side_stream": float(np.mean([e[4].elapsed_time(e[5]) for e in ev]))}
     out = {"metric": "stereo pairs/s (752x480 L+R ORB extract, ComputeStereoMatches, SearchForInitialization)",
-           "value": P * args.steps / dt, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+           "value": P * args.steps * world / dt, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "dtype": "u8", "data": "synthetic",
            "config": {"workload": "C3: 752x480 rectified stereo, ORBextractor(1200,1.2,8,20,7), lapping {0,0}, "
-                                  "mb 0.11 m, fx 435.2", "pairs_per_step": P},
+                                  "mb 0.11 m, fx 435.2", "pairs_per_step_per_gpu": P,
+                      "parallelism": f"pairs sharded over {world} GPU(s), halo left frame per seam"},
            "stage_ms": stage, "extract_stage_ms": xst,
            "roofline": benchlib.fast_roofline(sets[0]["ex"], W, H, xst, 2 * P * args.steps / max(1, calls))}
-    if args.cpu_sample > 0:
+    if args.cpu_sample > 0 and world == 1:
         ns = min(args.cpu_sample, P)
         fps, outs = cpu_baseline(left[:ns], right[:ns], args.cpu_threads)
         S = sets[(it[0] - 1) % 2]                            # the last step's outputs
@@ -197,6 +274,9 @@ def run_c3(args):
                                "sample": f"first {ns} pairs: oracle extraction of L and R + ComputeStereoMatches"}
         out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad,
                          "matched_fraction": float(np.mean([(o[1][0] >= 0).mean() for o in outs]))}
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return out
 
 
@@ -207,10 +287,13 @@ def run_c4(args):
     from orb_slam3_vio_fixes_amd import capi, orb, synth
     w = h = 512
     nf, lap = 1500, (0, 511)
-    dev = torch.device("cuda", 0)
+    world, rank, local = dist_init()
+    dev = torch.device("cuda", local)
     P = args.pairs
-    left = synth.sequence(w, h, P, config=4)
-    right = np.stack([synth.right_view(left[i], synth.frame_seed(4, i)) for i in range(P)])
+    # pairs [rank P, (rank + 1) P) of one global sequence (independent pairs: no halo)
+    first = rank * P
+    left = synth.global_sequence(w, h, first, P, config=4)
+    right = np.stack([synth.right_view(left[i], synth.frame_seed(4, first + i)) for i in range(P)])
     frames = torch.from_numpy(np.concatenate([left, right])).to(dev)
     ex = orb.ORBextractor(nf, 1.2, 8, 20, 7)
     stream = torch.cuda.current_stream(dev)
@@ -278,23 +361,36 @@ def run_c4(args):
     flush()
     torch.cuda.synchronize()
     benchlib.profile_on([ex])
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(timed=True)
-    flush()
-    torch.cuda.synchronize()
-    idx, dist, l2r = res[0]
-    dt = time.perf_counter() - t0
+
+    def timed():
+        for _ in range(args.steps):
+            step(timed=True)
+        flush()
+    dt = dist_time(timed, world, dev)
+    idx, _, l2r = res[0]
     xst, calls = benchlib.profile_read([ex])
+    if args.dump:
+        S = sets[(it[0] - 1) % 2]
+        Path(args.dump).mkdir(parents=True, exist_ok=True)
+        np.savez(Path(args.dump) / f"rank{rank}.npz", first=first, pairs=P, world=world,
+                 kps=S[0].cpu().numpy(), desc=S[1].cpu().numpy(), n=S[2].cpu().numpy(), mono=S[3].cpu().numpy(),
+                 idx=idx.cpu().numpy(), l2r=l2r.cpu().numpy())
+    if rank != 0:
+        if world > 1:
+            import torch.distributed as dist
+            dist.destroy_process_group()
+        return None
     stage = {"extract_2B_images": float(np.mean([e[0].elapsed_time(e[1]) for e in ev])),
              "fisheye_knn2_ratio_side_stream": float(np.mean([e[2].elapsed_time(e[3]) for e in ev]))}
     out = {"metric": "fisheye stereo pairs/s (512x512 L+R ORB extract, knnMatch(2) + ratio over the lapping areas)",
-           "value": P * args.steps / dt, "unit": "pairs/s", "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
-           "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "dtype": "u8", "data": "synthetic",
+           "value": P * args.steps * world / dt, "unit": "pairs/s", "n_gpus": world, "steps": args.steps,
+           "warmup": args.warmup, "ms_per_step": dt / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
+           "dtype": "u8", "data": "synthetic",
            "config": {"workload": "C4: 512x512 fisheye stereo, ORBextractor(1500,1.2,8,20,7), lapping {0,511}",
-                      "pairs_per_step": P}, "stage_ms": stage, "extract_stage_ms": xst,
+                      "pairs_per_step_per_gpu": P, "parallelism": f"pairs sharded over {world} GPU(s)"},
+           "stage_ms": stage, "extract_stage_ms": xst,
            "roofline": benchlib.fast_roofline(ex, w, h, xst, 2 * P * args.steps / max(1, calls))}
-    if args.cpu_sample > 0:
+    if args.cpu_sample > 0 and world == 1:
         ns = min(args.cpu_sample, P)
         O.lib()
         S = sets[(it[0] - 1) % 2]                            # the last step's outputs
@@ -312,6 +408,9 @@ def run_c4(args):
         out["cpu_baseline"] = {"value": fps, "unit": "pairs/s", "cores": 1, "kind": "port",
                                "sample": f"first {ns} pairs: oracle extraction of L and R + knnMatch(2), one thread"}
         out["parity"] = {"pairs_checked": ns, "pairs_mismatched": bad}
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
     return out
 
 
