@@ -225,6 +225,11 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        in the 256-thread form)
  *   ORB_OPT_PYR_CNT_END  k_pyr_stream's step counters at the top of its LDS
  *                        allocation instead of inside the table image
+ *   ORB_OPT_PYR_PRETEST  1: FAST's iniThFAST compass pre-test fused into
+ *                        k_pyr_stream (a candidate bitmap k_fast_cells reads;
+ *                        measured slower)
+ * The two k_pyr_stream options are read when a handle builds its plan (the
+ * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
  * (-1 for an unknown option). */
 enum {
@@ -232,7 +237,8 @@ enum {
     ORB_OPT_BOW_FORM = 1,
     ORB_OPT_BOWK_BIG = 2,
     ORB_OPT_PYR_CNT_END = 3,
-    ORB_OPT_COUNT = 4
+    ORB_OPT_PYR_PRETEST = 4,
+    ORB_OPT_COUNT = 5
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);

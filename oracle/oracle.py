@@ -141,6 +141,16 @@ class OracleExtractor:
             raise RuntimeError(f"oracle extract failed: {rc}")
         return kps[:n.value].copy(), desc[:n.value].copy(), mono.value
 
+    def run_rc(self, img: np.ndarray, lapping=(0, 1000), cap: int = 20000) -> int:
+        """orbo_extract's status only (negative: a size the oracle refuses)."""
+        img = np.ascontiguousarray(img, np.uint8)
+        h, w = img.shape
+        kps = np.zeros(cap, abi.KEYPOINT_DTYPE)
+        desc = np.zeros((cap, 32), np.uint8)
+        n, mono = C.c_int(0), C.c_int(0)
+        return int(self.L.orbo_extract(self.h, abi.ptr(img), w, h, w, int(lapping[0]), int(lapping[1]),
+                                       abi.ptr(kps), abi.ptr(desc), cap, C.byref(n), C.byref(mono)))
+
     def level(self, l: int) -> np.ndarray:
         w, h = C.c_int(0), C.c_int(0)
         lib().orbo_get_level(self.h, l, None, 0, C.byref(w), C.byref(h))

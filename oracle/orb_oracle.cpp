@@ -77,10 +77,14 @@ int resize_linear(const Img& s, Img& d) {
     if (d.w == s.w && d.h == s.h) { d.px = s.px; return 0; }
     const double inv_sx = (double)d.w / s.w, inv_sy = (double)d.h / s.h;
     const double scale_x = 1. / inv_sx, scale_y = 1. / inv_sy;
-    const int isx = (int)std::nearbyint(scale_x), isy = (int)std::nearbyint(scale_y);
-    if (std::fabs(scale_x - isx) < 2.220446049250313e-16 &&
-        std::fabs(scale_y - isy) < 2.220446049250313e-16 && isx == 2 && isy == 2)
-        return ORB_ERR_UNSUPPORTED;   // OpenCV switches to INTER_AREA here
+    // At an exact 2x reduction in both directions OpenCV switches to INTER_AREA
+    // (resize.cpp: is_area_fast && iscale_x == 2 && iscale_y == 2), whose fast
+    // path for 8UC1 is (a + b + c + d + 2) >> 2 per 2x2 block
+    // (ResizeAreaFastVec::operator()).  The linear fixed point below reproduces
+    // it exactly there: every weight is 1024 (fx = fy = 0.5, sx = 2 dx,
+    // sy = 2 dy, no clamping), so a row gives (1024 * ((1024 (a + b)) >> 4)) >> 16
+    // = a + b and the output ((a + b) + (c + d) + 2) >> 2.  No separate area
+    // path is needed (tests/test_oracle_tables.py checks the block average).
     std::vector<int> xo(d.w), xa(2 * d.w), yo(d.h), yb(2 * d.h);
     int xmax = d.w;
     for (int dx = 0; dx < d.w; ++dx) {
@@ -458,12 +462,18 @@ struct Extractor {
         }
     }
 
+    int err = 0;   // keypoints(): a size the reference does not survive
+
     // ComputePyramid (ORBextractor.cc:1170-1195)
     int pyramid(const uint8_t* img, int w, int h, size_t step) {
         pyr.assign(prm.nlevels, Img());
         for (int l = 0; l < prm.nlevels; ++l) {
             const float s = inv_scale[l];
             const int lw = cv_round((float)w * s), lh = cv_round((float)h * s);
+            // a level of <= 32 px on a side: DistributeOctTree divides by
+            // maxY - minY <= 0 and sizes a vector from it (ORBextractor.cc:
+            // 559-565), which the reference does not survive
+            if (lw - 2 * (kEdge - 3) < 1 || lh - 2 * (kEdge - 3) < 1) return ORB_ERR_UNSUPPORTED;
             pyr[l].alloc(lw, lh);
             if (l == 0) {
                 for (int y = 0; y < h; ++y) std::memcpy(pyr[0].row(y), img + (size_t)y * step, w);
@@ -487,7 +497,11 @@ struct Extractor {
             std::vector<KP>& cand = stage_cand[l];
             const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
             const int nCols = (int)(width / kCellW), nRows = (int)(height / kCellW);
-            const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+            // nCols or nRows = 0 (a level of 33..66 px): the cell loops below
+            // do not run; the reference's cell sizes are then a division by
+            // zero nothing reads (kept out of the integer conversion here)
+            const int wCell = nCols ? (int)std::ceil(width / nCols) : 0;
+            const int hCell = nRows ? (int)std::ceil(height / nRows) : 0;
             for (int i = 0; i < nRows; ++i) {
                 const float iniY = (float)(minBY + i * hCell);
                 float maxY = iniY + hCell + 6;
@@ -512,6 +526,9 @@ struct Extractor {
                 }
             }
             std::vector<KP>& kp = all[l];
+            // nIni = 0 with keys indexes an empty vpIniNodes (:583-584): refused
+            const int nIni = (int)std::round((float)(maxBX - minBX) / (maxBY - minBY));
+            if (nIni < 0 || (nIni == 0 && !cand.empty())) { err = ORB_ERR_UNSUPPORTED; return; }
             kp = distribute(cand, minBX, maxBX, minBY, maxBY, nfeat[l]);
             const int patch = (int)(kPatchSize * scale[l]);
             for (KP& k : kp) {
@@ -533,7 +550,9 @@ struct Extractor {
         int rc = pyramid(img, w, h, step);
         if (rc) return rc;
         std::vector<std::vector<KP>> all;
+        err = 0;
         keypoints(all);
+        if (err) return err;
         int n = 0;
         for (auto& v : all) n += (int)v.size();
         out.assign(n, KP{});

@@ -199,9 +199,13 @@ static void build_pyramid(Plan& P, const std::vector<int2>& tab, std::vector<int
 
 constexpr int kPyrStreamMinFrames = 32;   // below this a frame per CU leaves the chip idle: row bands
 constexpr int kPsRun = 4;                 // k_pyr_stream: output rows per run (one lane, one column group)
-#ifndef ORB_PYR_PRETEST
-#define ORB_PYR_PRETEST 1   // the FAST pre-test at iniThFAST fused into k_pyr_stream (0: k_fast_cells pre-tests)
-#endif
+// The FAST pre-test at iniThFAST fused into k_pyr_stream (candidate bitmap ->
+// k_fast_cells<..., BM = true>) is exact but off by default: same-box A/B
+//  put pyramid + FAST at 0.507 ms with it against 0.475 ms
+// without -- the pre-test's VALU work moves ~1:1 into the pyramid, which
+// issues it at lower efficiency (one 1024-thread workgroup per CU) than
+// k_fast_cells does.  orb_debug_set_option(ORB_OPT_PYR_PRETEST, 1) selects it
+// when a plan is built (tests, A/B).
 #ifndef ORB_PYR_K0
 #define ORB_PYR_K0 0
 #endif
@@ -358,7 +362,7 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
     // groups of 16 pixels (columns 16 g - 4 .. 16 g + 19 of a ring row must
     // exist: the windows lie >= 19 px inside the level); the bitmap path of
     // k_fast_cells reads windows of <= 64 columns
-    bool pt_ok = P.bm_ok && ORB_PYR_PRETEST;
+    bool pt_ok = P.bm_ok && debug_opt(ORB_OPT_PYR_PRETEST) == 1;
     for (int m = 0; m < L && pt_ok; ++m) {
         PS.pt_y0[m] = P.win_y0[m]; PS.pt_y1[m] = P.win_y1[m];
         PS.pt_gx0[m] = P.win_x0[m] >> 4;
@@ -490,11 +494,12 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         // ComputePyramid sizes (ORBextractor.cc:1174-1175)
         d.w = cv_round((float)w * hd->inv_scale[l]);
         d.h = cv_round((float)h * hd->inv_scale[l]);
-        // The reference needs a level of at least 2*19+35 px per side (nCols,
-        // nRows >= 1), else it divides by zero at ORBextractor.cc:800-802;
-        // levels narrower than 46 px are refused here (the 35-px cell check
-        // below refuses the rest of that range).
-        if (d.w < 2 * kEdge + 8 || d.h < 2 * kEdge + 8) return ORB_ERR_UNSUPPORTED;
+        // A level of 33..66 px on a side has no FAST cells in the reference
+        // (nCols or nRows = 0 at ORBextractor.cc:798-799: the cell loops do not
+        // run) and gives no keypoints; one of <= 32 px makes DistributeOctTree
+        // divide by maxY - minY <= 0 and size a vector from the result
+        // (:559-565), which the reference does not survive: refused here.
+        if (d.w - 2 * (kEdge - 3) < 1 || d.h - 2 * (kEdge - 3) < 1) return ORB_ERR_UNSUPPORTED;
         // 12 bytes of slack past the level's last pixel
         d.pitch = round_up(d.w + 12, 64);
         d.off = l == 0 ? 0 : poff;
@@ -506,10 +511,15 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
             const LevelDev& s = P.lv[l - 1];
             const double sx_inv = (double)d.w / s.w, sy_inv = (double)d.h / s.h;
             const double scx = 1. / sx_inv, scy = 1. / sy_inv;
-            const int isx = (int)std::nearbyint(scx), isy = (int)std::nearbyint(scy);
-            if (std::fabs(scx - isx) < 2.220446049250313e-16 && std::fabs(scy - isy) < 2.220446049250313e-16 &&
-                isx == 2 && isy == 2)
-                return ORB_ERR_UNSUPPORTED;   // OpenCV would take its INTER_AREA path
+            // At an exact 2x reduction in both directions cv::resize switches
+            // INTER_LINEAR to INTER_AREA (resize.cpp: is_area_fast, iscale 2),
+            // whose fast path is (a + b + c + d + 2) >> 2 over each 2x2 block
+            // (ResizeAreaFastVec).  The fixed-point linear taps below are then
+            // all 1024 (fx = fy = 0.5, sx = 2 dx, sy = 2 dy, never clamped) and
+            // give (1024 * ((1024 (a + b)) >> 4)) >> 16 = a + b per source row:
+            // ((a + b) + (c + d) + 2) >> 2, the same value, so the linear
+            // kernels serve that case unchanged (tests/test_gpu_configs.py
+            // checks every level against the 2x2 block average).
             P.tab_off[l] = (long long)tab.size();
             int xmax = d.w;
             for (int dx = 0; dx < d.w; ++dx) {
@@ -538,8 +548,9 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         const int maxBX = d.w - kEdge + 3, maxBY = d.h - kEdge + 3;
         const float width = (float)(maxBX - minBX), height = (float)(maxBY - minBY);
         const int nCols = (int)(width / 35.f), nRows = (int)(height / 35.f);
-        if (nCols < 1 || nRows < 1) return ORB_ERR_UNSUPPORTED;
-        const int wCell = (int)std::ceil(width / nCols), hCell = (int)std::ceil(height / nRows);
+        // (nCols or nRows = 0: no cells; the reference's cell sizes are then
+        // a division by zero that nothing reads)
+        const int wCell = nCols ? (int)std::ceil(width / nCols) : 0, hCell = nRows ? (int)std::ceil(height / nRows) : 0;
         const int cap = ((wCell + 1) / 2) * ((hCell + 1) / 2);
         d.cell_base = cellsum;
         d.slot_base = slotsum;
@@ -599,8 +610,10 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         d.qH = maxBY - minBY;
         d.N = hd->nfeat[l];
         d.nIni = (int)std::round((float)(maxBX - minBX) / (maxBY - minBY));
-        if (d.nIni < 1) return ORB_ERR_UNSUPPORTED;
-        d.hX = (float)(maxBX - minBX) / d.nIni;
+        // nIni = 0 is harmless only without keys (the reference indexes
+        // vpIniNodes[x / inf] = [0] of an empty vector otherwise, :583-584)
+        if (d.nIni < 0 || (d.nIni == 0 && nc > 0)) return ORB_ERR_UNSUPPORTED;
+        d.hX = d.nIni ? (float)(maxBX - minBX) / d.nIni : 0.f;
         d.out_base = outsum;
         d.out_cap = std::max(d.N + 3, 4 * d.nIni);
         outsum += d.out_cap;
@@ -3555,7 +3568,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     const size_t flds = kFastWpb * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes + fa.ilist_bytes);
     fa.nframes = B;
     const dim3 fgrid((P.ncells + kFastWpb * kCellsPerWave - 1) / (kFastWpb * kCellsPerWave), B);
-    hipLaunchKernelGGL(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
+    if (P.ncells > 0)                        // (every level under 67 px: no FAST cells at all)
+        hipLaunchKernelGGL(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
     mark();
     // quadtree
     QtArgs qa;

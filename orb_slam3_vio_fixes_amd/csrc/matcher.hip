@@ -368,13 +368,21 @@ struct SfiArgs {
     int32_t* nmatches;       // [pair]
 };
 
-// F2's level-0 features in grid order (GetFeaturesInArea(.., level1, level1)
-// with level1 = 0 keeps octave 0 only, :668), prepared by k_grid -> LDS.
-__device__ int level0_list(const SfiArgs& a, int f2, int* list, int tid, int nthreads) {
-    const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
-    const int nl = a.gcount[f2];
-    for (int i = tid; i < nl; i += nthreads) list[i] = (int)gs[i];
-    return nl;
+// the K smallest keys seen so far, ascending (keys are unique): with
+// k0 <= k1 <= ..., the new k_t is med3(k_{t-1}, k_t, key) -- independent ops
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+template <int K>
+__device__ __forceinline__ void topk_push(uint32_t (&kk)[K], uint32_t key) {
+    uint32_t n[K];
+    n[0] = min(kk[0], key);
+#pragma unroll
+    for (int t = 1; t < K; ++t) n[t] = umed3(kk[t - 1], kk[t], key);
+#pragma unroll
+    for (int t = 0; t < K; ++t) kk[t] = n[t];
 }
 
 __device__ __forceinline__ void query_pos(const SfiArgs& a, int pr, int i1, const orb_keypoint& k1, float& px,
@@ -386,7 +394,9 @@ __device__ __forceinline__ void query_pos(const SfiArgs& a, int pr, int i1, cons
     }
 }
 
-// distance of list entry j to query i1 if it is a candidate, else INT_MAX
+// distance of level-0 list entry j (F2's level-0 features in grid order:
+// GetFeaturesInArea(.., level1, level1) with level1 = 0 keeps octave 0 only,
+// :668) to query i1 if it is a candidate, else INT_MAX
 __device__ __forceinline__ int cand_dist(const int* list, int j, const CellRange& cr, float px, float py, float r,
                                          const orb_keypoint* K2, const uint8_t* D2, uint4 q0, uint4 q1) {
     const int v = list[j];
@@ -398,18 +408,19 @@ __device__ __forceinline__ int cand_dist(const int* list, int j, const CellRange
     return hamming32(q0, q1, D2 + (long long)fi * 32);
 }
 
-// The queries [qbeg + wave * qpw, + qpw) of pair pr: every candidate key into
-// the wave's LDS pool, then kTopK rounds of wave minimum over it.  LDS: the
-// level-0 list (cap) and four pools (cap each).
-__device__ void sfi_topk_pool(const SfiArgs& a, int pr, int qbeg, int qpw, int* lds) {
-    int* list = lds;                              // cap entries (block-shared)
-    uint32_t* pool = (uint32_t*)(lds + a.cap);    // per wave: cap keys
+// The queries [qbeg + wave * qpw, + qpw) of pair pr against an F2 level-0 list
+// of any length (read from global memory): each lane keeps the kTopK smallest
+// keys (distance << 16 | list position) of the candidates at positions lane,
+// lane + 64, ... in registers (one min and kTopK - 1 med3 per candidate), then
+// kTopK rounds of wave minimum over the lanes' heads draw the query's kTopK
+// smallest -- every key of the query's top-K is in its own lane's top-K.  No
+// LDS, so frames of any keypoint count (16-bit list positions) take it.
+__device__ void sfi_topk_lanes(const SfiArgs& a, int pr, int qbeg, int qpw) {
     const int lane = lane_id(), wv = wave_id();
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
     const int n1 = min(a.n[f1], a.cap);
-    const int nl = level0_list(a, f2, list, threadIdx.x, blockDim.x);
-    __syncthreads();
-    uint32_t* mypool = pool + wv * a.cap;
+    const int* list = (const int*)(a.gsorted + (long long)f2 * a.cap);
+    const int nl = a.gcount[f2];
     const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
     const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
     const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
@@ -429,69 +440,48 @@ __device__ void sfi_topk_pool(const SfiArgs& a, int pr, int qbeg, int qpw, int* 
             continue;
         }
         const uint4 q0 = *(const uint4*)(D1 + (long long)i1 * 32), q1 = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+        uint32_t kk[kTopK];
+#pragma unroll
+        for (int k = 0; k < kTopK; ++k) kk[k] = kNoKey;
         int cnt = 0;
         for (int base = 0; base < nl; base += kWave) {
             const int j = base + lane;
             const int d = j < nl ? cand_dist(list, j, cr, px, py, r, K2, D2, q0, q1) : INT_MAX;
-            const uint64_t m = __ballot(d != INT_MAX);
-            if (d != INT_MAX) mypool[cnt + mask_rank(m)] = ((uint32_t)d << 16) | (uint32_t)j;
-            cnt += __popcll(m);
+            cnt += __popcll(__ballot(d != INT_MAX));
+            if (d != INT_MAX) topk_push(kk, ((uint32_t)d << 16) | (uint32_t)j);
         }
-        wave_sync_m();
-        // kTopK rounds of wave minimum over the pool
-        for (int k = 0; k < kTopK; ++k) {
-            uint32_t mn = kNoKey;
-            for (int q = lane; q < cnt; q += kWave) mn = min(mn, mypool[q]);
-            mn = wave_min(mn, 0xffffffffu);
-            // out: rotation bin, distance and F2 feature index (the list
-            // position only ordered the ties)
-            if (lane == 0 && mn != kNoKey) {
-                const uint32_t fi = (uint32_t)list[mn & 0xffff] & 0xffffu;
-                const uint32_t bn = a.check_ori ? (uint32_t)rot_bin(k1.angle, K2[fi].angle) : 0u;
-                tk[k] = (bn << 25) | (mn & 0xffff0000u) | fi;
-            } else if (lane == 0) {
-                tk[k] = kNoKey;
+        const int rounds = min(cnt, kTopK);
+        uint32_t mine = kNoKey;   // lane k < kTopK: the k-th draw
+        for (int k = 0; k < rounds; ++k) {
+            const uint32_t mn = wave_min(kk[0], 0xffffffffu);
+            if (kk[0] == mn) {
+#pragma unroll
+                for (int q = 0; q + 1 < kTopK; ++q) kk[q] = kk[q + 1];
+                kk[kTopK - 1] = kNoKey;
             }
-            if (mn == kNoKey) { for (int kk = k + 1 + lane; kk < kTopK; kk += kWave) tk[kk] = kNoKey; break; }
-            for (int q = lane; q < cnt; q += kWave)
-                if (mypool[q] == mn) mypool[q] = kNoKey;
-            wave_sync_m();
+            if (lane == k) mine = mn;
+        }
+        // out: rotation bin, distance and F2 feature index (the list position
+        // only ordered the ties), one store per draw
+        if (lane < kTopK) {
+            uint32_t o = kNoKey;
+            if (mine != kNoKey) {
+                const uint32_t fi = (uint32_t)list[mine & 0xffffu] & 0xffffu;
+                const uint32_t bn = a.check_ori ? (uint32_t)rot_bin(k1.angle, K2[fi].angle) : 0u;
+                o = (bn << 25) | (mine & 0xffff0000u) | fi;
+            }
+            tk[lane] = o;
         }
         if (lane == 0) *nc = cnt;
-        wave_sync_m();
     }
 }
 
-// grid (npairs, ceil(cap / 16)), 256 threads: 4 waves x 4 queries each
-__global__ __launch_bounds__(256) void k_sfi_topk(SfiArgs a) {
-    extern __shared__ __attribute__((aligned(16))) int lds[];
-    const int pr = blockIdx.x;
-    const int f1 = a.pair_f1[pr];
-    const int n1 = min(a.n[f1], a.cap);
-    __shared__ int s_any;
-    if (threadIdx.x == 0) s_any = 0;
-    __syncthreads();
-    {   // does this block hold any level-0 query?
-        const int i1 = blockIdx.y * 16 + (int)threadIdx.x;
-        if (threadIdx.x < 16 && i1 < n1 && a.kps[(long long)f1 * a.cap + i1].octave == 0) s_any = 1;
-    }
-    __syncthreads();
-    if (!s_any) {
-        for (int t = threadIdx.x; t < 16; t += blockDim.x) {
-            const int i1 = blockIdx.y * 16 + t;
-            if (i1 < n1) a.ncand[(long long)pr * a.cap + i1] = -1;
-        }
-        return;
-    }
-    sfi_topk_pool(a, pr, blockIdx.y * 16, 4, lds);
-}
-
-// k_sfi_topk_st: the same top-K lists with F2's level-0 features staged in
+// k_sfi_topk_st: the top-K lists with F2's level-0 features staged in
 // LDS once per block of 64 queries (cell, position and descriptor in grid
 // order: 44 bytes each), so a query's candidate scan reads only LDS, and the
 // K smallest keys are drawn from registers (a lane holds the keys of its list
 // positions lane, lane + 64, ...; kStIt positions at most, longer lists take
-// k_sfi_topk).  Rounds stop after min(count, K) draws.
+// sfi_topk_lanes).  Rounds stop after min(count, K) draws.
 constexpr int kStIt = 4;                  // level-0 lists of <= 256 features
 constexpr int kStQ = 64;                  // queries per block
 __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
@@ -518,8 +508,8 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
     const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
     const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
     const int nl = a.gcount[f2];
-    if (nl > kStIt * kWave) {             // a long level-0 list: the pool form (LDS sized for it)
-        sfi_topk_pool(a, pr, q0, kStQ / 4, lds);
+    if (nl > kStIt * kWave) {             // a long level-0 list: per-lane top-K from global memory
+        sfi_topk_lanes(a, pr, q0, kStQ / 4);
         return;
     }
     {
@@ -609,9 +599,6 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
 // keypoint, so the block does not hold off the extraction's blocks it runs
 // beside.
 constexpr int kSfiThreads = 256;
-#ifndef ORB_SFI_TOPK_ST
-#define ORB_SFI_TOPK_ST 1
-#endif
 #ifndef ORB_SFI_PRIO
 #define ORB_SFI_PRIO 1
 #endif
@@ -628,16 +615,19 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     const orb_keypoint* K2 = a.kps + (long long)f2 * a.cap;
     const uint8_t* D1 = a.desc + (long long)f1 * a.cap * 32;
     const uint8_t* D2 = a.desc + (long long)f2 * a.cap * 32;
-    int* list = lds;                              // cap
-    uint32_t* md21 = (uint32_t*)(list + a.cap);   // cap: matched distance << 16 | (F1 match + 1)
+    // LDS: the serial state, the query list and the rotation bins (9 bytes a
+    // keypoint); F2's level-0 list (read only by exact rescans) and the
+    // matches (written by the walk, read after the block's barrier) stay in
+    // global memory
+    uint32_t* md21 = (uint32_t*)lds;              // cap: matched distance << 16 | (F1 match + 1)
     int* hist = (int*)(md21 + a.cap);             // 32 (hist[31]: the filter's drop count)
     int* qlist = hist + 32;                       // cap: query i1 | (more than kTopK candidates) << 31
-    int* m12 = qlist + a.cap;                     // cap
-    int8_t* bin1 = (int8_t*)(m12 + a.cap);        // cap
-    int32_t* m12g = a.matches + (long long)pr * a.cap;
+    int8_t* bin1 = (int8_t*)(qlist + a.cap);      // cap
+    int32_t* m12 = a.matches + (long long)pr * a.cap;
+    const int* list = (const int*)(a.gsorted + (long long)f2 * a.cap);
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
     const int* ncand = a.ncand + (long long)pr * a.cap;
-    const int nl = level0_list(a, f2, list, tid, kSfiThreads);
+    const int nl = a.gcount[f2];
     for (int i = tid; i < n1; i += kSfiThreads) {
         qlist[i] = ncand[i];
         m12[i] = -1;
@@ -683,11 +673,14 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             const int j = j0 + grp;
             return j < nq ? topk[(long long)(qlist[j] & 0x7fffffff) * kTopK + kk] : kNoKey;
         };
+        // the next two runs' keys are in flight while a round runs (a round is
+        // shorter than a global load's latency)
         uint32_t kcur = nq > 0 ? run_keys(0) : kNoKey;
+        uint32_t kn1 = nq > 8 ? run_keys(8) : kNoKey;
+        uint32_t kn2 = nq > 16 ? run_keys(16) : kNoKey;
         int j0 = 0;
         while (j0 < nq) {
             const int nrun = min(8, nq - j0);
-            const uint32_t knxt = j0 + 8 < nq ? run_keys(j0 + 8) : kNoKey;
             const int qe = grp < nrun ? qlist[j0 + grp] : 0;
             const bool many = qe < 0;
             const bool kval = kcur != kNoKey;
@@ -778,15 +771,20 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 adv = P + 1;
             }
             j0 += adv;
-            // the next run's keys: the uncommitted part of this run, then the prefetch
+            // the next runs' keys: shifted by the queries done (a whole run in
+            // the usual case), the run after them loaded
             if (adv == 8) {
-                kcur = knxt;
+                kcur = kn1;
+                kn1 = kn2;
             } else {
                 const int src = lane + 8 * adv;
-                const uint32_t v1 = (uint32_t)__shfl((int)kcur, src & 63, kWave);
-                const uint32_t v2 = (uint32_t)__shfl((int)knxt, src & 63, kWave);
-                kcur = src < 64 ? v1 : v2;
+                const uint32_t a0 = (uint32_t)__shfl((int)kcur, src & 63, kWave);
+                const uint32_t a1 = (uint32_t)__shfl((int)kn1, src & 63, kWave);
+                const uint32_t a2 = (uint32_t)__shfl((int)kn2, src & 63, kWave);
+                kcur = src < 64 ? a0 : a1;
+                kn1 = src < 64 ? a1 : a2;
             }
+            kn2 = j0 + 16 < nq ? run_keys(j0 + 16) : kNoKey;
         }
 #else
         int nm = 0, hreg = 0;   // lane b: the rotation histogram's bin b
@@ -909,7 +907,6 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         __syncthreads();
         nm -= hist[31];
     }
-    for (int i = tid; i < n1; i += kSfiThreads) m12g[i] = m12[i];
     if (a.prev_out) {
         for (int i = tid; i < n1; i += kSfiThreads) {
             float px, py;
@@ -925,21 +922,16 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
 
 constexpr size_t kLdsMax = 160 * 1024;
 
-// Frames up to ~7,800 keypoints (LDS of the candidate pools); beyond that
-// ORB_ERR_UNSUPPORTED before any launch.
+// Frames up to ~18,000 keypoints (the resolve's 9 bytes of LDS a keypoint);
+// beyond that ORB_ERR_UNSUPPORTED before any launch.
 static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
-    const size_t lds_topk = (size_t)a.cap * 4 * 5 + 64;
-    const size_t lds_res = (size_t)a.cap * (4 * 4 + 1) + 128 + 16;
-    if (lds_topk > kLdsMax || lds_res > kLdsMax) return ORB_ERR_UNSUPPORTED;
+    const size_t lds_res = (size_t)a.cap * (4 + 4 + 1) + 128 + 16;
+    if (lds_res > kLdsMax) return ORB_ERR_UNSUPPORTED;
     if (a.cap > 65535) return ORB_ERR_UNSUPPORTED;   // 16-bit feature fields of the keys and the state
-#if ORB_SFI_TOPK_ST
     // staged form; a block whose F2 level-0 list is longer than its
-    // registers take runs the pool form in the same LDS
+    // registers take runs the per-lane form from global memory
     KLAUNCH(k_sfi_topk_st, dim3(npairs, (a.cap + kStQ - 1) / kStQ), dim3(256),
-            std::max(lds_topk, (size_t)kStIt * kWave * (32 + 8 + 4 + 4)), st, a);
-#else
-    KLAUNCH(k_sfi_topk, dim3(npairs, (a.cap + 15) / 16), dim3(256), lds_topk, st, a);
-#endif
+            (size_t)kStIt * kWave * (32 + 8 + 4 + 4), st, a);
     KLAUNCH(k_sfi_resolve, dim3(npairs), dim3(kSfiThreads), lds_res, st, a);
     return ORB_OK;
 }
@@ -1663,21 +1655,7 @@ __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
     }
 }
 
-// the kBowK smallest keys seen so far, ascending (keys are unique): with
-// k0 <= k1 <= ..., the new k_t is med3(k_{t-1}, k_t, key) -- independent ops
-__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-    uint32_t d;
-    asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
-    return d;
-}
-__device__ __forceinline__ void topk_push(uint32_t (&kk)[kBowK], uint32_t key) {
-    uint32_t n[kBowK];
-    n[0] = min(kk[0], key);
-#pragma unroll
-    for (int t = 1; t < kBowK; ++t) n[t] = umed3(kk[t - 1], kk[t], key);
-#pragma unroll
-    for (int t = 0; t < kBowK; ++t) kk[t] = n[t];
-}
+// (topk_push, the sorted insertion of the kBowK smallest keys: above, with SearchForInitialization)
 
 // The same lists with the distances on the matrix cores.  A descriptor's 256
 // bits as +-1 int8 make Hamming distance a dot product, dot = 256 - 2 ham,

@@ -59,7 +59,7 @@ class ORBextractor:
         capi.check(capi.lib().orbx_set_host_pyramid(self._h, int(enable)), "orbx_set_host_pyramid")
 
     def pyramid_kernel(self) -> int:
-        """Pyramid kernel of the last extraction: 1 k_pyramid, 2 k_pyr_stream, 3 k_resize, 4 k_pyr_level."""
+        """Pyramid kernel of the last extraction: 1 k_pyramid, 2 k_pyr_stream."""
         return int(capi.lib().orbx_pyramid_kernel(self._h))
 
     def max_keypoints(self, w: int, h: int) -> int:

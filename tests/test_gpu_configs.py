@@ -102,6 +102,28 @@ def test_monocular_init_extractor_5000(gpu_lib):
     np.testing.assert_array_equal(prev_out, rprev)
 
 
+def test_monocular_init_over_8k_keypoints(gpu_lib):
+    """The initialization search of Tracking's init extractor at nFeatures =
+    2000 (ORBextractor(5 * 2000), Tracking.cc:601) on 1280x960 frames:
+    > 8,192 keypoints a frame, beyond the LDS-resident pools of round 3 (the
+    per-lane top-K from global memory and the 9-byte resolve state take it);
+    matches and the updated vbPrevMatched equal the oracle's
+    (ORBmatcher.cc:648-763)."""
+    seq = synth.sequence(1280, 960, 2, config=2, start=700)
+    ex = orb.ORBextractor(10000, 1.2, 8, 20, 7)
+    outs = [ex(seq[i], None, (0, 1000))[:2] for i in range(2)]
+    assert len(outs[0][0]) > 8192 and len(outs[1][0]) > 8192
+    k1, d1 = outs[0]
+    prev = np.stack([k1["x"], k1["y"]], 1)
+    f1 = abi.frame_struct(k1, d1, 1280, 960)
+    f2 = abi.frame_struct(*outs[1], 1280, 960)
+    nm, m12, prev_out = orb.ORBmatcher(0.9, True).SearchForInitialization(f1, f2, prev, 100)
+    rnm, rm12, rprev = O.search_for_initialization(f1, f2, prev, 100, 0.9, True)
+    assert nm == rnm and nm > 1000
+    np.testing.assert_array_equal(m12, rm12)
+    np.testing.assert_array_equal(prev_out, rprev)
+
+
 def test_monocular_init_extractor_5000_batch(gpu_lib):
     import torch
     seq = synth.sequence(752, 480, 6, config=2, start=700)
@@ -115,22 +137,60 @@ def test_monocular_init_extractor_5000_batch(gpu_lib):
                    *ref(seq[i], (0, 1000)))
 
 
-@pytest.mark.parametrize("w,h,sf,nl", [(160, 120, 1.2, 8), (752, 480, 2.0, 3), (40, 30, 1.2, 1)])
+@pytest.mark.parametrize("w,h,sf,nl", [(40, 30, 1.2, 1), (160, 120, 1.2, 9), (100, 300, 1.2, 1)])
 def test_unsupported_size_fails_every_time(gpu_lib, w, h, sf, nl):
-    """A refused plan (level narrower than 46 px; an exact 2x level, where
-    cv::resize takes INTER_AREA) must not leave a plan behind that a second
-    call with the same size takes for a built one."""
+    """Sizes the reference does not survive are refused, every time: a level
+    of <= 32 px on a side (DistributeOctTree divides by maxY - minY <= 0 and
+    sizes a vector from it, ORBextractor.cc:559-565), and nIni = 0 with FAST
+    cells (vpIniNodes[0] of an empty vector, :583-584).  A refused plan must
+    not leave a plan behind that a second call with the same size takes for a
+    built one, and the handle still works for a supported size afterwards."""
     ex = orb.ORBextractor(1000, sf, nl, 20, 7)
     img = synth.image(w, h, 5)
+    assert O.OracleExtractor(1000, sf, nl, 20, 7).run_rc(img, (0, 1000)) < 0     # the oracle refuses too
     for _ in range(3):
         with pytest.raises(RuntimeError):
             ex(img, None, (0, 1000))
         assert capi.lib().orbx_max_keypoints(ex._h, w, h) < 0
-    if sf == 2.0:
-        return
-    # the handle still works for a supported size afterwards
     good = synth.image(752, 480, 6)
     same_frame(*ex(good, None, (0, 1000)), *O.OracleExtractor(1000, sf, nl, 20, 7)(good, (0, 1000)))
+
+
+@pytest.mark.parametrize("w,h,sf,nl", [(160, 120, 1.2, 8), (752, 480, 2.0, 3), (640, 480, 2.0, 4),
+                                        (120, 90, 1.2, 3)])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_small_levels_and_exact_2x(gpu_lib, w, h, sf, nl, mode):
+    """Sizes the reference accepts at the edges of the plan: levels of 33..66
+    px (no FAST cells, ORBextractor.cc:798-799: no keypoints there) and exact
+    2x reductions, where cv::resize takes INTER_AREA (resize.cpp:
+    is_area_fast), whose 2x2 fast path (a + b + c + d + 2) >> 2 the linear
+    fixed point reproduces.  Single image and a batch (mode 0 single-image
+    path; 1 row bands, 2 sliding frame on 3 frames): keypoints, descriptors
+    and every level equal the oracle's, and every exact-2x level equals the
+    2x2 block average of the level above it."""
+    import torch
+    ex = orb.ORBextractor(1000, sf, nl, 20, 7)
+    seq = synth.sequence(w, h, 3, config=2, start=400)
+    if mode == 0:
+        outs = [ex(seq[0], None, (0, 1000))]
+        pyr = [ex.mvImagePyramid]
+    else:
+        ex.set_pyramid_mode(mode)
+        kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
+        torch.cuda.synchronize()
+        outs = [(orb.keypoints_from_device(kps[f, :int(n[f])]), desc[f, :int(n[f])].cpu().numpy(), int(mono[f]))
+                for f in range(3)]
+        pyr = [ex.batch_pyramid(f) for f in range(3)]
+    for f, (k, d, m) in enumerate(outs):
+        ref = O.OracleExtractor(1000, sf, nl, 20, 7)
+        same_frame(k, d, m, *ref(seq[f], (0, 1000)))
+        for lev in range(nl):
+            np.testing.assert_array_equal(pyr[f][lev], ref.level(lev), err_msg=f"frame {f} level {lev}")
+        for lev in range(1, nl):
+            a, b = pyr[f][lev - 1].astype(np.int32), pyr[f][lev]
+            if a.shape[0] == 2 * b.shape[0] and a.shape[1] == 2 * b.shape[1]:
+                avg = (a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2] + 2) >> 2
+                np.testing.assert_array_equal(b, avg.astype(np.uint8), err_msg=f"INTER_AREA level {lev}")
 
 
 def test_mixed_lapping_batch_keeps_every_pyramid(gpu_lib):
@@ -256,11 +316,12 @@ def test_fused_pretest_bitmap(gpu_lib, w, h, ini, mn):
     gives the oracle's keypoints and descriptors (ORBextractor.cc:781-896)."""
     import torch
     seq = synth.sequence(w, h, 3, config=2, start=900)
-    ex = orb.ORBextractor(1000, 1.2, 8, ini, mn)
-    ex.set_pyramid_mode(2)
-    kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
-    torch.cuda.synchronize()
-    assert ex.pyramid_kernel() == 2
+    with capi.debug_option(capi.ORB_OPT_PYR_PRETEST, 1):      # read when the handle builds its plan
+        ex = orb.ORBextractor(1000, 1.2, 8, ini, mn)
+        ex.set_pyramid_mode(2)
+        kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
+        torch.cuda.synchronize()
+    assert ex.pyramid_kernel() == 2 and ex.plan_info(w, h)["pretest"] == 1
     for f in range(len(seq)):
         ref = O.OracleExtractor(1000, 1.2, 8, ini, mn)
         rk, rd, rm = ref(seq[f], (0, 1000))

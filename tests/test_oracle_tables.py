@@ -46,3 +46,25 @@ def test_pyramid_sizes(size):
     got = [ex.level(l).shape[::-1] for l in range(8)]
     assert got == LEVELS[size]
     assert sum(a * b for a, b in got) == SUMP[size]
+
+
+@pytest.mark.parametrize("w,h,nl", [(752, 480, 4), (640, 480, 4), (512, 512, 4)])
+def test_exact_2x_levels_are_the_area_average(w, h, nl):
+    """ORBextractor(scaleFactor 2.0): every level that halves both sides is
+    cv::resize's INTER_AREA 2x2 fast path (resize.cpp: is_area_fast, iscale
+    2; ResizeAreaFastVec: (a + b + c + d + 2) >> 2), which the oracle's
+    INTER_LINEAR fixed point (all weights 1024 there) must reproduce exactly;
+    levels that do not halve both sides exactly stay INTER_LINEAR."""
+    import numpy as np
+    from oracle import oracle as O
+    from orb_slam3_vio_fixes_amd import synth
+    ref = O.OracleExtractor(500, 2.0, nl, 20, 7)
+    ref(synth.image(w, h, 9), (0, 1000))
+    halved = 0
+    for lev in range(1, nl):
+        a, b = ref.level(lev - 1).astype(np.int32), ref.level(lev)
+        if a.shape[0] == 2 * b.shape[0] and a.shape[1] == 2 * b.shape[1]:
+            avg = (a[0::2, 0::2] + a[0::2, 1::2] + a[1::2, 0::2] + a[1::2, 1::2] + 2) >> 2
+            np.testing.assert_array_equal(b, avg.astype(np.uint8), err_msg=f"level {lev}")
+            halved += 1
+    assert halved >= 2

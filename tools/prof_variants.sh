@@ -10,6 +10,7 @@ cp orb_slam3_vio_fixes_amd/liborb_mi355x.so "$out/.default.so"
 ARGS="--no-pipeline --steps 10 --warmup 2 --cpu-sample 0 --no-host-api"
 for v in $vars; do
   cp "variants/lib_$v.so" orb_slam3_vio_fixes_amd/liborb_mi355x.so
+  mkdir -p "$out/$v"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/$v/trace" -o run -- python3 bench.py $ARGS > "$out/$v/bench.json" 2> "$out/$v/rocprof.err" || { echo "$v trace failed"; tail -5 "$out/$v/rocprof.err"; cp "$out/.default.so" orb_slam3_vio_fixes_amd/liborb_mi355x.so; exit 1; }
   python tools/kstats.py "$out/$v/trace/run_kernel_trace.csv" --csv "$out/$v/kernel_stats_by_grid.csv" > "$out/$v/kstats.txt"
   i=0
