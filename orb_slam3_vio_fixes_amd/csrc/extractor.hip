@@ -97,6 +97,7 @@ static int round_up(int x, int m) { return (x + m - 1) / m * m; }
 // k_pyramid plan: column/row tap tables in the form the kernel reads, and the
 // launch groups with their band tables.
 // ---------------------------------------------------------------------------
+constexpr int kLdsMax = 160 * 1024;          // LDS of one CU: a workgroup's ceiling
 constexpr int kPyrLdsBudget = 64 * 1024;   // per workgroup: 2 workgroups of 256 threads per CU
 
 static int pyr_lds_pitch(int w) { return round_up(w + 4, 16); }
@@ -476,6 +477,8 @@ static void build_pyr_stream(Plan& P, const std::vector<int2>& tab, std::vector<
 // Builds the size-dependent plan into P; returns ORB_OK or an error.  The
 // caller (build_plan) releases P on any error, so a failed size never leaves a
 // plan that a later call with the same size would take for a built one.
+static void qt_lds_split(const Plan& P, size_t& lds, size_t& gstride);
+
 static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     if (w > 4096 + 16 || h > 4096 + 16) return ORB_ERR_UNSUPPORTED;   // 12-bit key coordinates
     const int L = hd->prm.nlevels;
@@ -634,6 +637,9 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     P.ncells = cellsum;
     P.slot_total = slotsum;
     P.out_total = outsum;
+    // k_assemble holds a flag per output slot of a frame in LDS: up to ~40,000
+    // features a frame (Tracking's largest extractor is 5 x nFeatures)
+    if ((size_t)outsum * 4 + 64 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
     P.in_pitch = (size_t)round_up(w, 64);
 
     const size_t B = (size_t)maxB;
@@ -649,6 +655,11 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     ORB_CHECK(hipMalloc(&P.d_knode, B * P.slot_total * sizeof(int)));
     ORB_CHECK(hipMalloc(&P.d_kq, B * P.slot_total));
     ORB_CHECK(hipMalloc(&P.d_qt_key, B * P.out_total * sizeof(uint32_t)));
+    {
+        size_t qlds, qgs;
+        qt_lds_split(P, qlds, qgs);
+        if (qgs) ORB_CHECK(hipMalloc(&P.d_qt_gscr, B * L * qgs));
+    }
     ORB_CHECK(hipMalloc(&P.d_qt_n, B * L * sizeof(int)));
     ORB_CHECK(hipMalloc(&P.d_angle, B * P.out_total * sizeof(float)));
     ORB_CHECK(hipMalloc(&P.d_sdesc, B * P.out_total * 32));
@@ -2101,8 +2112,23 @@ struct QtArgs {
     int ncells_total, slot_total;
     uint32_t* qt_key;   // [B][out_total]
     int* qt_n;          // [B][L]
-    int out_total, L, ncap;
+    int out_total, L;
+    int lds_bytes;          // dynamic LDS of the launch
+    uint8_t* gscr;          // k_quadtree<true>: [B][L] node arrays of levels beyond the LDS
+    long long gscr_stride;
 };
+
+// Bytes of a level's node arrays (NC = out_cap + 8 nodes: the list never
+// grows past N + 3 or 4 nIni, see qt_divide) and cell offsets; the layout
+// k_quadtree carves.
+__host__ __device__ inline size_t qt_scratch_bytes(int NC, int ncells) {
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    const size_t n = (size_t)NC;
+    size_t b = al((size_t)(ncells + 1) * 4);
+    b += 2 * al(n * 8) + 2 * al(n * 4) + 2 * al(n) + 2 * al(n * 16);
+    b += 7 * al(n * 4) + al(n * sizeof(SortRec)) + al(80 * sizeof(SortFrame)) + 2 * al(64);
+    return b;
+}
 
 // double-buffered arrays are picked by a select, never by a dynamic index:
 // an indexed pointer array would live in scratch and every access through it
@@ -2435,6 +2461,11 @@ extern "C" int orbx_debug_qt_timing(unsigned long long* out, int reset) {
 #define QT_T(k) do { } while (0)
 #endif
 
+// GS: a level whose node arrays exceed the launch's LDS (N beyond ~1,600 a
+// level: Tracking's 5 x nFeatures initialization extractor) keeps them in a
+// global scratch slice instead; the instantiation is only launched when a
+// plan has such a level, so the LDS form keeps its ds_* instructions.
+template <bool GS>
 __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #if ORB_QT_LEVEL_MAJOR
@@ -2444,7 +2475,7 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
 #endif
     const LevelDev lv = a.lv[l];
-    const int NC = a.ncap;
+    const int NC = lv.out_cap + 8;
 #ifdef ORB_QT_TIMING
     const unsigned long long qt_t0 = __builtin_amdgcn_s_memtime();
     unsigned long long qt_last = qt_t0;
@@ -2453,6 +2484,8 @@ __global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
     QtLds s;
     {
         uint8_t* p = smem;
+        if (GS && qt_scratch_bytes(NC, lv.ncells) > (size_t)a.lds_bytes)
+            p = a.gscr + ((long long)f * a.L + l) * a.gscr_stride;
         auto take = [&](size_t bytes) { uint8_t* q = p; p += (bytes + 15) & ~size_t(15); return q; };
         s.off = (int*)take((lv.ncells + 1) * sizeof(int));
         s.rect[0] = (short4*)take(NC * sizeof(short4));
@@ -3419,13 +3452,16 @@ __global__ __launch_bounds__(256) void k_assemble(AsmArgs a) {
 // ---------------------------------------------------------------------------
 // Host orchestration
 // ---------------------------------------------------------------------------
-static size_t qt_lds_bytes(const Plan& P) {
-    const size_t NC = (size_t)P.max_out_cap + 8;
-    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
-    size_t b = al((P.max_level_cells + 1) * 4);
-    b += 2 * al(NC * 8) + 2 * al(NC * 4) + 2 * al(NC) + 2 * al(NC * 16);
-    b += 7 * al(NC * 4) + al(NC * sizeof(SortRec)) + al(80 * sizeof(SortFrame)) + 2 * al(64);
-    return b;
+// k_quadtree's launch LDS (the largest level that fits kLdsMax) and the
+// global slice size of the levels that do not (0: none)
+static void qt_lds_split(const Plan& P, size_t& lds, size_t& gstride) {
+    lds = 0;
+    gstride = 0;
+    for (const LevelDev& d : P.lv) {
+        const size_t b = qt_scratch_bytes(d.out_cap + 8, d.ncells);
+        if (b <= (size_t)kLdsMax) lds = std::max(lds, b);
+        else gstride = std::max(gstride, (b + 255) & ~size_t(255));
+    }
 }
 
 // Frames [f0, f0+B) of the batch: every per-frame work buffer is addressed
@@ -3577,12 +3613,20 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     qa.key_scr = P.d_key_scr; qa.knode = P.d_knode; qa.kq = P.d_kq;
     qa.ncells_total = P.ncells; qa.slot_total = P.slot_total;
     qa.qt_key = P.d_qt_key; qa.qt_n = P.d_qt_n; qa.out_total = P.out_total; qa.L = L;
-    qa.ncap = P.max_out_cap + 8;
+    {
+        size_t qlds, qgs;
+        qt_lds_split(P0, qlds, qgs);
+        qa.lds_bytes = (int)qlds;
+        qa.gscr = P0.d_qt_gscr ? P0.d_qt_gscr + F * L * (long long)qgs : nullptr;
+        qa.gscr_stride = (long long)qgs;
+        if (qgs && !qa.gscr) return ORB_ERR_DEVICE;
 #if ORB_QT_LEVEL_MAJOR
-    hipLaunchKernelGGL(k_quadtree, dim3(B, L), dim3(256), qt_lds_bytes(P), st, qa);
+        const dim3 qg(B, L);
 #else
-    hipLaunchKernelGGL(k_quadtree, dim3(L, B), dim3(256), qt_lds_bytes(P), st, qa);
+        const dim3 qg(L, B);
 #endif
+        hipLaunchKernelGGL(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(256), qlds, st, qa);
+    }
     mark();
     // describe
     DescArgs da;

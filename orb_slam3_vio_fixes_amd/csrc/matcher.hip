@@ -1871,6 +1871,141 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
     }
 }
 
+// Persistent form of k_bowk_topk_mfma<1> (ORB_BOWK_PERSIST): a block loops
+// over items of 128 slots (4 waves x 32; item += gridDim.x) instead of being
+// one item.  A block of a ~40-feature frame node has two tiles of matrix
+// work behind a chain of dependent loads (slot -> keyframe feature ->
+// descriptor), so the one-item form spent most of its life waiting; here the
+// chain runs ahead -- slot sources two items ahead, keyframe descriptors one
+// item ahead -- while the current item's tiles are on the matrix cores.
+#ifndef ORB_BOWK_PERSIST
+#define ORB_BOWK_PERSIST 1
+#endif
+constexpr int kBowkItemsPerCU = 3;   // persistent blocks per CU (waves_per_eu ORB_BOWK_WPE: 3 blocks of 4 waves)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_BOWK_WPE)))
+void k_bowk_topk_mfma_p(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
+    __shared__ bowk_v4i s_a[2][32 * 17];
+    const BowArgs& a = k.b;
+    const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
+    const int nitems = (total + 127) / 128;
+    const int G = (int)gridDim.x;
+    const int lane = lane_id(), col = lane & 31, h = lane >> 5, wv = wave_id();
+    auto node_of = [&](long long slot) {             // last fl with bstart[fl] <= slot
+        return __builtin_amdgcn_readfirstlane(k.chunk_node[slot >> 5]);
+    };
+    // stage A: this lane's slot of item `it` -> (keyframe feature, FeatureVector row)
+    auto stage_a = [&](int it, uint32_t& src, uint32_t& pos) {
+        const long long sl = (long long)it * 128 + wv * 32 + col;
+        src = 0xffffffffu;
+        pos = 0;
+        if (it < nitems && sl < total) {
+            src = k.slot_src[sl];
+            if (a.kf_fvdesc) pos = k.slot_pos[sl];
+        }
+    };
+    // stage B: the keyframe descriptor of that slot (a (keyframe, node)'s
+    // slots are consecutive FeatureVector rows: with fv_desc one 1 KB read a wave)
+    auto stage_b = [&](uint32_t src, uint32_t pos, uint4& q0, uint4& q1) {
+        q0 = q1 = make_uint4(0u, 0u, 0u, 0u);
+        if (src != 0xffffffffu) {
+            const uint8_t* kd = a.kf_fvdesc ? a.kf_fvdesc + (long long)pos * 32 : a.kf_desc + (long long)src * 32;
+            q0 = *(const uint4*)kd;
+            q1 = *(const uint4*)(kd + 16);
+        }
+    };
+    int neg = -32768, kbase = 256 << 15;
+    asm volatile("" : "+v"(neg));
+    asm volatile("" : "+s"(kbase));
+    const int srow = threadIdx.x >> 3, ss = threadIdx.x & 7;   // staging: row, dword (both halves)
+    int it = blockIdx.x;
+    uint32_t src0, pos0, src1, pos1;
+    uint4 d0, d1;
+    stage_a(it, src0, pos0);
+    stage_b(src0, pos0, d0, d1);
+    stage_a(it + G, src1, pos1);
+    for (; it < nitems; it += G) {
+        const uint4 c0 = d0, c1 = d1;
+        const bool has = src0 != 0xffffffffu;
+        // the chain of the next items, in flight during this one
+        stage_b(src1, pos1, d0, d1);
+        src0 = src1;
+        stage_a(it + 2 * G, src1, pos1);
+        const long long slotb = (long long)it * 128;
+        const long long slot0 = slotb + (long long)wv * 32;
+        const int flb = node_of(slotb);
+        const int fbb = __builtin_amdgcn_readfirstlane(a.f_off[flb]);
+        const int nfb = __builtin_amdgcn_readfirstlane(a.f_off[flb + 1]) - fbb;
+        const bool live = slot0 < total;             // buckets are padded to 64: a wave's slots never straddle
+        const int fl = live ? (slot0 == slotb ? flb : node_of(slot0)) : flb;
+        const bool shared_node = fl == flb;
+        const int fb = __builtin_amdgcn_readfirstlane(a.f_off[fl]);
+        const int nf = __builtin_amdgcn_readfirstlane(a.f_off[fl + 1]) - fb;
+        bowk_v4i B[8];
+        {
+            const uint32_t dd[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) B[s2] = bits_pm1((has ? dd[s2] : 0u) >> (16 * h));
+        }
+        uint32_t kk[kBowK];
+#pragma unroll
+        for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
+        auto tile_mfma = [&](const bowk_v4i* ar, int t0, int nfx) {
+            bowk_v16i acc = bowk_v16i{};
+#pragma unroll
+            for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ar[2 * s2], B[s2], acc, 0, 0, 0);
+            const int kb = kbase + t0;
+            if (t0 + 32 <= nfx) {
+#pragma unroll
+                for (int g = 0; g < 16; ++g) topk_push(kk, bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2)));
+            } else {
+                const int lim = nfx - t0 - 4 * h;    // rows (g & 3) + 8 (g >> 2) below it exist
+#pragma unroll
+                for (int g = 0; g < 16; ++g) {
+                    const uint32_t key = bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2));
+                    topk_push(kk, (g & 3) + 8 * (g >> 2) < lim ? key : 0xffffffffu);
+                }
+            }
+        };
+        const int ntb = (nfb + 31) / 32;
+        bowk_v4i p0, p1;
+        auto fetch = [&](int tile) {
+            const bowk_v4i* g = fexp + (long long)(fbb + min(tile * 32 + srow, nfb - 1)) * 16 + 2 * ss;
+            p0 = g[0];
+            p1 = g[1];
+        };
+        auto put = [&](int buf) {
+            s_a[buf][srow * 17 + 2 * ss] = p0;
+            s_a[buf][srow * 17 + 2 * ss + 1] = p1;
+        };
+        bowk_lds_barrier();                          // every wave is done with the previous item's tiles
+        if (ntb > 0) { fetch(0); put(0); }
+        if (ntb > 1) fetch(1);
+        for (int tile = 0; tile < ntb; ++tile) {
+            bowk_lds_barrier();                      // tile's buffer written; the other one free
+            if (tile + 1 < ntb) {
+                put((tile + 1) & 1);
+                if (tile + 2 < ntb) fetch(tile + 2);
+            }
+            if (live && shared_node) tile_mfma(&s_a[tile & 1][col * 17 + h], tile * 32, nf);
+        }
+        if (live && !shared_node) {
+            for (int t0 = 0; t0 < nf; t0 += 32) {
+                const int fr = min(t0 + col, nf - 1);
+                tile_mfma(fexp + (long long)(fb + fr) * 16 + h, t0, nf);
+            }
+        }
+        if (!live) continue;
+#pragma unroll
+        for (int t = 0; t < kBowK; ++t) kk[t] = kk[t] == 0xffffffffu ? kk[t] : kk[t] + 4u * (uint32_t)h;
+        uint32_t other[kBowK];
+#pragma unroll
+        for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)kk[t], 32, kWave);
+#pragma unroll
+        for (int t = 0; t < kBowK; ++t) topk_push(kk, other[t]);
+        if (h == 0) k.lists[slot0 + col] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
+    }
+}
+
 // One thread per g, the g entries ordered by frame node (neighbouring lanes
 // walk nodes of one size: little divergence).  The positions of the node
 // claimed so far in this walk are bits of a thread-private LDS bitmap (17
@@ -3634,7 +3769,18 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
             a.f_off + a.f_nnodes, fexp.p);
     // (measured and dropped, DESIGN.md §5: the VALU top-4 pass, two 32-column
     // keyframe sets per MFMA wave, a wave-walk resolve)
+#if ORB_BOWK_PERSIST
+    {
+        int ncu = 0, dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+        const long long items = (slots + 127) / 128;
+        KLAUNCH(k_bowk_topk_mfma_p, dim3((unsigned)std::min<long long>(items, (long long)ncu * kBowkItemsPerCU)),
+                dim3(256), 0, st, k, fexp.p);
+    }
+#else
     KLAUNCH(k_bowk_topk_mfma<1>, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
+#endif
     {
         // the BIG form when a bitmap over every frame position fits 64 threads' LDS
         const int words = (a.f_n + 31) / 32, bp = a.f_n > 32 * kBowLaneWords ? (words | 1) : 0;

@@ -109,6 +109,7 @@ struct Plan {
     int2* d_pyt = nullptr;           // k_pyramid row taps: sy0 | sy1 << 16 (clamped), b0 | b1 << 16
     uint4* d_ps_tab = nullptr;       // k_pyr_stream LDS table image
     uint8_t* d_bm = nullptr;         // [maxB][bm_bytes] pre-test bitmaps (ps.pretest)
+    uint8_t* d_qt_gscr = nullptr;    // [maxB][L][stride] k_quadtree node arrays of levels beyond the LDS
     // single-image host path outputs
     orb_keypoint* d_kps = nullptr;
     uint8_t* d_desc = nullptr;
@@ -119,7 +120,7 @@ struct Plan {
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_bm};
+                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_bm, d_qt_gscr};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();
