@@ -104,6 +104,9 @@ def parse():
                     help="c2: the headline (this file); c3 stereo, c4 fisheye stereo (tools/bench_stereo.py), "
                          "c5 map-wide SearchByBoW (tools/bench_c5.py): one JSON line each, with its own roofline")
     ap.add_argument("--nkf", type=int, default=10000, help="c5: keyframes in the map")
+    ap.add_argument("--per-kf", type=int, default=5000, help="c5: features per keyframe (of the query's ~5008)")
+    ap.add_argument("--valid-frac", type=float, default=1.0,
+                    help="c5: share of keyframe features with a valid MapPoint (the stated map: 1.0)")
     return ap.parse_args()
 
 
@@ -122,7 +125,8 @@ def other_workload(args):
         return bench_stereo.run_c3(a) if args.workload == "c3" else bench_stereo.run_c4(a)
     import bench_c5
     # the oracle checks every keyframe of rank 0's shard (a threaded map loop: a few seconds)
-    a = types.SimpleNamespace(nkf=args.nkf, per_kf=5000, reps=args.steps, warmup=args.warmup,
+    a = types.SimpleNamespace(nkf=args.nkf, per_kf=args.per_kf, valid_frac=args.valid_frac,
+                              reps=args.steps, warmup=args.warmup,
                               cpu_sample=-1 if args.cpu_sample > 0 else 0,
                               cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))
     return bench_c5.run_c5(a)

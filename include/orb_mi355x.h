@@ -381,11 +381,20 @@ typedef struct orbm_kf_map_device {
      * (keyframe, node)'s features are then contiguous, so the map-wide search
      * streams them instead of gathering 32-B rows across the keyframe. */
     const uint8_t* fv_desc;
+    /* optional (NULL = gathered from kps): the keypoint angles in FeatureVector
+     * order, n_fv_total floats, row as fv_desc; built once per map by
+     * orbm_kf_map_fv_angle.  The rotation filter of the map-wide search then
+     * reads 4 contiguous bytes per match instead of a 28-B keypoint row. */
+    const float* fv_angle;
 } orbm_kf_map_device;
 
 /* Fills d_fv_desc (n_fv_total x 32 device bytes) for map->fv_desc.
  * Asynchronous on `stream`.  Returns ORB_OK or an error. */
 int orbm_kf_map_fv_desc(const orbm_kf_map_device* map, uint8_t* d_fv_desc, void* stream);
+
+/* Fills d_fv_angle (n_fv_total device floats) for map->fv_angle.
+ * Asynchronous on `stream`.  Returns ORB_OK or an error. */
+int orbm_kf_map_fv_angle(const orbm_kf_map_device* map, float* d_fv_angle, void* stream);
 
 /* SearchByBoW(KF_i, F) for nkf host keyframes against one frame in one launch:
  * the relocalisation loop over candidates (src/Tracking.cc:3641-3648).

@@ -18,7 +18,7 @@ EXPORTS = [
     "orbx_get_level", "orbx_get_batch_level", "orbx_debug_math", "orbx_debug_sort", "orbx_set_host_pyramid",
     "orbx_extract_batch_device", "orbx_debug_stage", "orbm_descriptor_distance", "orbm_search_for_initialization",
     "orbm_search_for_initialization_batch_device", "orbm_search_by_bow", "orbm_search_by_projection_mps",
-    "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device", "orbm_search_by_bow_many", "orbm_kf_map_fv_desc",
+    "orbm_search_by_projection_last", "orbv_transform", "orbx_set_profiling", "orbx_get_profile", "orbm_search_by_bow_batch_device", "orbm_search_by_bow_many", "orbm_kf_map_fv_desc", "orbm_kf_map_fv_angle",
     "orbx_set_streams", "orbs_compute_stereo_matches", "orbs_compute_stereo_matches_batch_device",
     "orbs_knn_match2", "orbs_fisheye_stereo_candidates_batch_device",
     "orbv_load_text", "orbv_text_vocab_view", "orbv_free_text", "orbv_bow_assemble", "orbv_score",
@@ -67,6 +67,7 @@ def load(path: Path | str = LIB_PATH):
     L.orbx_get_profile.argtypes = [vp, vp, i32]
     L.orbm_search_by_bow_batch_device.argtypes = [vp, vp, vp, f32, i32, vp, vp, vp]
     L.orbm_kf_map_fv_desc.argtypes = [vp, vp, vp]
+    L.orbm_kf_map_fv_angle.argtypes = [vp, vp, vp]
     L.orbm_search_by_bow_many.argtypes = [i32, vp, vp, vp, vp, vp, f32, i32, vp, vp]
     L.orbx_set_streams.argtypes = [vp, i32]
     L.orbx_set_pyramid_mode.argtypes = [vp, i32]

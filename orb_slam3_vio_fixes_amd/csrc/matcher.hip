@@ -963,6 +963,7 @@ struct BowArgs {
     const long long* node_off;
     const long long* idx_off;
     const uint8_t* kf_fvdesc;   // optional: KF descriptors in FeatureVector order (orbm_kf_map_device::fv_desc)
+    const float* kf_fvangle;    // optional: KF keypoint angles in FeatureVector order (::fv_angle)
     // frame (shared by all pairs)
     const orb_keypoint* f_kps;  const uint8_t* f_desc;  int f_n;
     const uint32_t* f_node;  const int* f_off;  const uint32_t* f_idx;  int f_nnodes;
@@ -1447,9 +1448,6 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
 constexpr int kBowK = 4;
 // the lane resolve's LDS bitmap: 16 words (512 positions) a thread, odd pitch
 constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
-#ifndef ORB_BOWK_ABL
-#define ORB_BOWK_ABL 0   // timing ablations (tools only)
-#endif
 
 struct BowKArgs {
     BowArgs b;
@@ -1470,6 +1468,8 @@ struct BowKArgs {
     int* perm;             // [G] g entries ordered by frame node
     int* chunk_node;       // [slots / 32] frame node of every 32-slot chunk
     uint32_t* slot_pos;    // [slots] FeatureVector position (row of kf_fvdesc) when kf_fvdesc is set
+    int32_t* claim;        // [slots] the resolve's claim (frame feature index, -1: none) for k_bowk_final,
+                           // or NULL: claims go straight to the match rows (then k_bow_final)
 };
 
 // One block per pair (its KF nodes g are contiguous: no search for the pair
@@ -1814,14 +1814,23 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
 #pragma unroll
             for (int c = 0; c < NSET; ++c)
 #pragma unroll
-                for (int g = 0; g < 16; ++g) topk_push(kk[c], bowk_key(acc[c][g], neg, kb + (g & 3) + 8 * (g >> 2)));
+                for (int g = 0; g < 16; ++g) {
+                    // the row's key base opaque in an SGPR: one v_mad_i32_i24 per key
+                    // (the compiler otherwise folds the row constant into a
+                    // v_mul_i32_i24 + v_add3_u32 pair)
+                    int cg = kb + (g & 3) + 8 * (g >> 2);
+                    asm volatile("" : "+s"(cg));
+                    topk_push(kk[c], bowk_key(acc[c][g], neg, cg));
+                }
         } else {
             const int lim = nfx - t0 - 4 * h;        // rows (g & 3) + 8 (g >> 2) below it exist
 #pragma unroll
             for (int c = 0; c < NSET; ++c)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
-                    const uint32_t key = bowk_key(acc[c][g], neg, kb + (g & 3) + 8 * (g >> 2));
+                    int cg = kb + (g & 3) + 8 * (g >> 2);
+                    asm volatile("" : "+s"(cg));
+                    const uint32_t key = bowk_key(acc[c][g], neg, cg);
                     topk_push(kk[c], (g & 3) + 8 * (g >> 2) < lim ? key : 0xffffffffu);
                 }
         }
@@ -1868,141 +1877,6 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
 #pragma unroll
         for (int t = 0; t < kBowK; ++t) topk_push(q, other[t]);
         if (h == 0) k.lists[slot0 + 32 * c + col] = make_uint4(q[0], q[1], q[2], q[3]);
-    }
-}
-
-// Persistent form of k_bowk_topk_mfma<1> (ORB_BOWK_PERSIST): a block loops
-// over items of 128 slots (4 waves x 32; item += gridDim.x) instead of being
-// one item.  A block of a ~40-feature frame node has two tiles of matrix
-// work behind a chain of dependent loads (slot -> keyframe feature ->
-// descriptor), so the one-item form spent most of its life waiting; here the
-// chain runs ahead -- slot sources two items ahead, keyframe descriptors one
-// item ahead -- while the current item's tiles are on the matrix cores.
-#ifndef ORB_BOWK_PERSIST
-#define ORB_BOWK_PERSIST 1
-#endif
-constexpr int kBowkItemsPerCU = 3;   // persistent blocks per CU (waves_per_eu ORB_BOWK_WPE: 3 blocks of 4 waves)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_BOWK_WPE)))
-void k_bowk_topk_mfma_p(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
-    __shared__ bowk_v4i s_a[2][32 * 17];
-    const BowArgs& a = k.b;
-    const int total = __builtin_amdgcn_readfirstlane(k.bstart[a.f_nnodes]);
-    const int nitems = (total + 127) / 128;
-    const int G = (int)gridDim.x;
-    const int lane = lane_id(), col = lane & 31, h = lane >> 5, wv = wave_id();
-    auto node_of = [&](long long slot) {             // last fl with bstart[fl] <= slot
-        return __builtin_amdgcn_readfirstlane(k.chunk_node[slot >> 5]);
-    };
-    // stage A: this lane's slot of item `it` -> (keyframe feature, FeatureVector row)
-    auto stage_a = [&](int it, uint32_t& src, uint32_t& pos) {
-        const long long sl = (long long)it * 128 + wv * 32 + col;
-        src = 0xffffffffu;
-        pos = 0;
-        if (it < nitems && sl < total) {
-            src = k.slot_src[sl];
-            if (a.kf_fvdesc) pos = k.slot_pos[sl];
-        }
-    };
-    // stage B: the keyframe descriptor of that slot (a (keyframe, node)'s
-    // slots are consecutive FeatureVector rows: with fv_desc one 1 KB read a wave)
-    auto stage_b = [&](uint32_t src, uint32_t pos, uint4& q0, uint4& q1) {
-        q0 = q1 = make_uint4(0u, 0u, 0u, 0u);
-        if (src != 0xffffffffu) {
-            const uint8_t* kd = a.kf_fvdesc ? a.kf_fvdesc + (long long)pos * 32 : a.kf_desc + (long long)src * 32;
-            q0 = *(const uint4*)kd;
-            q1 = *(const uint4*)(kd + 16);
-        }
-    };
-    int neg = -32768, kbase = 256 << 15;
-    asm volatile("" : "+v"(neg));
-    asm volatile("" : "+s"(kbase));
-    const int srow = threadIdx.x >> 3, ss = threadIdx.x & 7;   // staging: row, dword (both halves)
-    int it = blockIdx.x;
-    uint32_t src0, pos0, src1, pos1;
-    uint4 d0, d1;
-    stage_a(it, src0, pos0);
-    stage_b(src0, pos0, d0, d1);
-    stage_a(it + G, src1, pos1);
-    for (; it < nitems; it += G) {
-        const uint4 c0 = d0, c1 = d1;
-        const bool has = src0 != 0xffffffffu;
-        // the chain of the next items, in flight during this one
-        stage_b(src1, pos1, d0, d1);
-        src0 = src1;
-        stage_a(it + 2 * G, src1, pos1);
-        const long long slotb = (long long)it * 128;
-        const long long slot0 = slotb + (long long)wv * 32;
-        const int flb = node_of(slotb);
-        const int fbb = __builtin_amdgcn_readfirstlane(a.f_off[flb]);
-        const int nfb = __builtin_amdgcn_readfirstlane(a.f_off[flb + 1]) - fbb;
-        const bool live = slot0 < total;             // buckets are padded to 64: a wave's slots never straddle
-        const int fl = live ? (slot0 == slotb ? flb : node_of(slot0)) : flb;
-        const bool shared_node = fl == flb;
-        const int fb = __builtin_amdgcn_readfirstlane(a.f_off[fl]);
-        const int nf = __builtin_amdgcn_readfirstlane(a.f_off[fl + 1]) - fb;
-        bowk_v4i B[8];
-        {
-            const uint32_t dd[8] = {c0.x, c0.y, c0.z, c0.w, c1.x, c1.y, c1.z, c1.w};
-#pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) B[s2] = bits_pm1((has ? dd[s2] : 0u) >> (16 * h));
-        }
-        uint32_t kk[kBowK];
-#pragma unroll
-        for (int t = 0; t < kBowK; ++t) kk[t] = 0xffffffffu;
-        auto tile_mfma = [&](const bowk_v4i* ar, int t0, int nfx) {
-            bowk_v16i acc = bowk_v16i{};
-#pragma unroll
-            for (int s2 = 0; s2 < 8; ++s2) acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(ar[2 * s2], B[s2], acc, 0, 0, 0);
-            const int kb = kbase + t0;
-            if (t0 + 32 <= nfx) {
-#pragma unroll
-                for (int g = 0; g < 16; ++g) topk_push(kk, bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2)));
-            } else {
-                const int lim = nfx - t0 - 4 * h;    // rows (g & 3) + 8 (g >> 2) below it exist
-#pragma unroll
-                for (int g = 0; g < 16; ++g) {
-                    const uint32_t key = bowk_key(acc[g], neg, kb + (g & 3) + 8 * (g >> 2));
-                    topk_push(kk, (g & 3) + 8 * (g >> 2) < lim ? key : 0xffffffffu);
-                }
-            }
-        };
-        const int ntb = (nfb + 31) / 32;
-        bowk_v4i p0, p1;
-        auto fetch = [&](int tile) {
-            const bowk_v4i* g = fexp + (long long)(fbb + min(tile * 32 + srow, nfb - 1)) * 16 + 2 * ss;
-            p0 = g[0];
-            p1 = g[1];
-        };
-        auto put = [&](int buf) {
-            s_a[buf][srow * 17 + 2 * ss] = p0;
-            s_a[buf][srow * 17 + 2 * ss + 1] = p1;
-        };
-        bowk_lds_barrier();                          // every wave is done with the previous item's tiles
-        if (ntb > 0) { fetch(0); put(0); }
-        if (ntb > 1) fetch(1);
-        for (int tile = 0; tile < ntb; ++tile) {
-            bowk_lds_barrier();                      // tile's buffer written; the other one free
-            if (tile + 1 < ntb) {
-                put((tile + 1) & 1);
-                if (tile + 2 < ntb) fetch(tile + 2);
-            }
-            if (live && shared_node) tile_mfma(&s_a[tile & 1][col * 17 + h], tile * 32, nf);
-        }
-        if (live && !shared_node) {
-            for (int t0 = 0; t0 < nf; t0 += 32) {
-                const int fr = min(t0 + col, nf - 1);
-                tile_mfma(fexp + (long long)(fb + fr) * 16 + h, t0, nf);
-            }
-        }
-        if (!live) continue;
-#pragma unroll
-        for (int t = 0; t < kBowK; ++t) kk[t] = kk[t] == 0xffffffffu ? kk[t] : kk[t] + 4u * (uint32_t)h;
-        uint32_t other[kBowK];
-#pragma unroll
-        for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)kk[t], 32, kWave);
-#pragma unroll
-        for (int t = 0; t < kBowK; ++t) topk_push(kk, other[t]);
-        if (h == 0) k.lists[slot0 + col] = make_uint4(kk[0], kk[1], kk[2], kk[3]);
     }
 }
 
@@ -2190,8 +2064,16 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
             uint32_t fi;
             if (wave_lds_fidx) fi = s_fidx[min(bpos, kBowFidxStage - 1)];
             else fi = lds_fidx ? s_fidx[min(bpos, kBowFidxStage - 1)] : fidx[claim ? bpos : 0];
-            int32_t* dst = claim ? match + fi : sink;
-            *dst = claim ? (int32_t)((long long)s - kpo) : 0;
+            if (k.claim) {
+                // the claim beside the slot (this lane's slots are consecutive, so
+                // a line fills over 32 steps of one lane); k_bowk_final builds the
+                // match rows.  Storing straight into the rows (4 B scattered over
+                // a 20 KB row per step) cost the walk ~0.9 ms of its ~1.6
+                if (act) k.claim[base + j0 + c] = claim ? (int32_t)fi : -1;
+            } else {
+                int32_t* dst = claim ? match + fi : sink;
+                *dst = claim ? (int32_t)((long long)s - kpo) : 0;
+            }
             if constexpr (all_lds) {
                 taken[bpos >> 5] |= (claim ? 1u : 0u) << (bpos & 31);
             } else if (claim && lds_bits) {
@@ -2200,7 +2082,68 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
             nm += claim;
         }
     }
-    if (nm) atomicAdd(&a.nmatches[pr], nm);
+    if (nm && !k.claim) atomicAdd(&a.nmatches[pr], nm);
+}
+
+// The match rows from the resolve's claims, with the rotation filter
+// (:404-422) and the counts: one block per pair, its row and the match bins
+// in LDS, the claims read per (pair, node) as contiguous slot runs, the
+// keyframe angles from the map's FeatureVector-order copy (contiguous too)
+// when it has one, and the row written once, coalesced.
+constexpr int kBowkRow = 8192;   // frame features of the LDS row (the all-LDS resolve's bound)
+__global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
+    __shared__ int s_row[kBowkRow];
+    __shared__ uint8_t s_bin[kBowkRow];
+    __shared__ int hist[32];
+    __shared__ int s_cnt;
+    const BowArgs& a = k.b;
+    const int pr = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, lane = lane_id();
+    for (int i = tid; i < a.f_n; i += nt) s_row[i] = -1;
+    if (tid < 32) hist[tid] = 0;
+    if (tid == 0) s_cnt = 0;
+    __syncthreads();
+    const long long g0 = a.node_off[pr];
+    const int nn = (int)(a.node_off[pr + 1] - g0);
+    const int* ko = a.kf_off + g0 + pr;
+    const long long io = a.idx_off[pr], kpo = a.kp_off[pr];
+    const uint32_t* ki = a.kf_idx + io;
+    // a wave per KF node, a lane per feature
+    for (int ia = wave_id(); ia < nn; ia += nt / kWave) {
+        const int fl = k.g_fl[g0 + ia];
+        if (fl < 0) continue;
+        const int base = k.bstart[fl] + k.g_off[g0 + ia];
+        const int p0 = ko[ia], n = ko[ia + 1] - p0;
+        for (int j = lane; j < n; j += kWave) {
+            const int c = k.claim[base + j];
+            if (c < 0) continue;
+            const int ikf = (int)ki[p0 + j];
+            s_row[c] = ikf;
+            if (a.check_ori) {
+                const float ka = a.kf_fvangle ? a.kf_fvangle[io + p0 + j] : a.kf_kps[kpo + ikf].angle;
+                const int b = rot_bin(ka, a.f_kps[c].angle);
+                s_bin[c] = (uint8_t)b;
+                atomicAdd(&hist[b], 1);
+            }
+        }
+    }
+    __syncthreads();
+    int i1 = -1, i2 = -1, i3 = -1;
+    if (a.check_ori) three_maxima(hist, i1, i2, i3);
+    int32_t* match = a.match + (long long)pr * a.f_n;
+    int cnt = 0;
+    for (int i = tid; i < a.f_n; i += nt) {
+        int m = s_row[i];
+        if (m >= 0 && a.check_ori) {
+            const int b = s_bin[i];
+            if (b != i1 && b != i2 && b != i3) m = -1;
+        }
+        cnt += m >= 0;
+        match[i] = m;
+    }
+    cnt = wave_sum(cnt);
+    if (lane == 0 && cnt) atomicAdd(&s_cnt, cnt);
+    __syncthreads();
+    if (tid == 0) a.nmatches[pr] = s_cnt;
 }
 
 // ---------------------------------------------------------------------------
@@ -3468,6 +3411,18 @@ __global__ __launch_bounds__(256) void k_fv_desc(const uint8_t* __restrict__ des
     }
 }
 
+// the map's keypoint angles in FeatureVector order, one block per keyframe
+__global__ __launch_bounds__(256) void k_fv_angle(const orb_keypoint* __restrict__ kps, const long long* __restrict__ kp_off,
+                                                  const int* __restrict__ fv_off, const uint32_t* __restrict__ fv_idx,
+                                                  const long long* __restrict__ node_off,
+                                                  const long long* __restrict__ idx_off, float* __restrict__ out) {
+    const int i = blockIdx.x;
+    const long long nn = node_off[i + 1] - node_off[i];
+    const int n = fv_off[node_off[i] + i + nn];
+    const long long io = idx_off[i], ko = kp_off[i];
+    for (int p = threadIdx.x; p < n; p += blockDim.x) out[io + p] = kps[ko + fv_idx[io + p]].angle;
+}
+
 }  // namespace orbmi
 
 using namespace orbmi;
@@ -3728,6 +3683,7 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node, node_n;
         PBuf<unsigned long long> bgcount;
         PBuf<uint32_t> slot_src, slot_pos;
+        PBuf<int32_t> claim;
         PBuf<uint4> lists;
         PBuf<bowk_v4i> fexp;
     };
@@ -3736,26 +3692,38 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         &g_rank = S.g_rank, &perm = S.perm, &chunk_node = S.chunk_node, &node_n = S.node_n;
     PBuf<unsigned long long>& bgcount = S.bgcount;
     PBuf<uint32_t>&slot_src = S.slot_src, &slot_pos = S.slot_pos;
+    PBuf<int32_t>& claim = S.claim;
     PBuf<uint4>& lists = S.lists;
     PBuf<bowk_v4i>& fexp = S.fexp;
     const int nsub = a.f_nnodes <= 1024 ? 64 : 1;
     a.npairs = npairs;
     const long long slots = nfv + (long long)kWave * a.f_nnodes;
+    // the resolve form: every thread's claimed positions in an LDS bitmap when a
+    // bitmap over every frame position fits 64 threads' LDS (nodes of > 512
+    // features then take the BIG form); its claims then go beside the slots and
+    // k_bowk_final builds the rows
+    const int words = (a.f_n + 31) / 32, bp = a.f_n > 32 * kBowLaneWords ? (words | 1) : 0;
+    const size_t big_lds = (size_t)64 * bp * sizeof(uint32_t);
+    const bool all_lds = big_lds <= 64 * 1024 && !debug_opt(ORB_OPT_BOWK_BIG);
+    const int big_pitch = all_lds ? bp : 0;
+    const bool claims = all_lds && a.f_n <= kBowkRow && !a.out12 && !a.f_valid;
     int rc;
     if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc((size_t)a.f_nnodes * nsub)) ||
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
         (rc = gstart.alloc(a.f_nnodes + 1)) || (rc = g_rank.alloc(G)) ||
         (rc = perm.alloc(G)) || (rc = fexp.alloc((size_t)std::max(1, a.f_n) * 16)) ||
-        (rc = chunk_node.alloc(slots / 32 + 1)) || (rc = node_n.alloc(a.f_nnodes + 1)) || (a.kf_fvdesc && (rc = slot_pos.alloc(slots))))
+        (rc = chunk_node.alloc(slots / 32 + 1)) || (rc = node_n.alloc(a.f_nnodes + 1)) || (a.kf_fvdesc && (rc = slot_pos.alloc(slots))) ||
+        (claims && (rc = claim.alloc(slots))))
         return rc;
     BowKArgs k;
     k.b = a; k.G = G; k.g_fl = g_fl.p; k.g_off = g_off.p; k.g_pr = g_pr.p; k.bgcount = bgcount.p; k.nsub = nsub; k.node_n = node_n.p; k.bstart = bstart.p;
     k.slot_src = slot_src.p; k.lists = lists.p;
     k.gstart = gstart.p; k.g_rank = g_rank.p; k.perm = perm.p; k.chunk_node = chunk_node.p;
     k.slot_pos = slot_pos.p;
+    k.claim = claims ? claim.p : nullptr;
     ORB_CHECK(flush_uploads());
     ORB_CHECK(hipMemsetAsync(bgcount.p, 0, (size_t)a.f_nnodes * nsub * sizeof(unsigned long long), st));
-    {
+    if (!claims) {                                   // (k_bowk_final writes every row and count)
         const long long nmf = (long long)npairs * a.f_n;
         const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
         KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
@@ -3769,32 +3737,17 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
             a.f_off + a.f_nnodes, fexp.p);
     // (measured and dropped, DESIGN.md §5: the VALU top-4 pass, two 32-column
     // keyframe sets per MFMA wave, a wave-walk resolve)
-#if ORB_BOWK_PERSIST
-    {
-        int ncu = 0, dev = 0;
-        (void)hipGetDevice(&dev);
-        if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
-        const long long items = (slots + 127) / 128;
-        KLAUNCH(k_bowk_topk_mfma_p, dim3((unsigned)std::min<long long>(items, (long long)ncu * kBowkItemsPerCU)),
-                dim3(256), 0, st, k, fexp.p);
-    }
-#else
     KLAUNCH(k_bowk_topk_mfma<1>, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
-#endif
-    {
-        // the BIG form when a bitmap over every frame position fits 64 threads' LDS
-        const int words = (a.f_n + 31) / 32, bp = a.f_n > 32 * kBowLaneWords ? (words | 1) : 0;
-        const size_t big_lds = (size_t)64 * bp * sizeof(uint32_t);
-        const int big_pitch = big_lds <= 64 * 1024 && !debug_opt(ORB_OPT_BOWK_BIG) ? bp : 0;
-        if (big_pitch) {
-            KLAUNCH((k_bowk_resolve_lane<false, true>), dim3(gb), dim3(256), 0, st, k, big_pitch);
+    if (all_lds) {
+        KLAUNCH((k_bowk_resolve_lane<false, true>), dim3(gb), dim3(256), 0, st, k, big_pitch);
+        if (big_pitch)
             KLAUNCH((k_bowk_resolve_lane<true, true>), dim3((unsigned)((G + 63) / 64)), dim3(64), big_lds, st, k,
                     big_pitch);
-        } else {
-            KLAUNCH((k_bowk_resolve_lane<false, false>), dim3(gb), dim3(256), 0, st, k, 0);
-        }
+    } else {
+        KLAUNCH((k_bowk_resolve_lane<false, false>), dim3(gb), dim3(256), 0, st, k, 0);
     }
-    KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
+    if (claims) KLAUNCH(k_bowk_final, dim3(npairs), dim3(256), 0, st, k);
+    else KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
@@ -3807,6 +3760,15 @@ int orbm_kf_map_fv_desc(const orbm_kf_map_device* map, uint8_t* d_fv_desc, void*
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
+int orbm_kf_map_fv_angle(const orbm_kf_map_device* map, float* d_fv_angle, void* stream) {
+    if (!map || !d_fv_angle || map->nkf < 0) return ORB_ERR_PARAM;
+    if (map->nkf == 0) return ORB_OK;
+    hipStream_t st = (hipStream_t)stream;
+    KLAUNCH(k_fv_angle, dim3(map->nkf), dim3(256), 0, st, map->kps, (const long long*)map->kp_off, map->fv_off,
+            map->fv_idx, (const long long*)map->fv_node_off, (const long long*)map->fv_idx_off, d_fv_angle);
+    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+}
+
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f, const orbm_featvec* ffv,
                                     float nnratio, int check_ori, int32_t* d_match, int32_t* d_nmatches, void* stream) {
     if (!map || !f || !ffv || !d_match || !d_nmatches || map->nkf < 0) return ORB_ERR_PARAM;
@@ -3816,6 +3778,7 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     a.kf_node = map->fv_node; a.kf_off = map->fv_off; a.kf_idx = map->fv_idx;
     a.node_off = (const long long*)map->fv_node_off; a.idx_off = (const long long*)map->fv_idx_off;
     a.kf_fvdesc = map->n_fv_total < 0xffffffffll ? map->fv_desc : nullptr;
+    a.kf_fvangle = map->fv_angle;
     a.f_kps = f->kps; a.f_desc = f->desc; a.f_n = f->n; a.f_node = ffv->node_ids; a.f_off = ffv->offsets;
     a.f_idx = ffv->idx; a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori;
     a.match = d_match; a.nmatches = d_nmatches;

@@ -19,7 +19,8 @@ class OrbmKfMapDevice(C.Structure):
     _fields_ = [("nkf", C.c_int32), ("kps", C.c_void_p), ("desc", C.c_void_p), ("valid", C.c_void_p),
                 ("kp_off", C.c_void_p), ("fv_node", C.c_void_p), ("fv_off", C.c_void_p), ("fv_idx", C.c_void_p),
                 ("fv_node_off", C.c_void_p), ("fv_idx_off", C.c_void_p),
-                ("n_nodes_total", C.c_int64), ("n_fv_total", C.c_int64), ("fv_desc", C.c_void_p)]
+                ("n_nodes_total", C.c_int64), ("n_fv_total", C.c_int64), ("fv_desc", C.c_void_p),
+                ("fv_angle", C.c_void_p)]
 
 
 def featvec_csr(node_of_feature: np.ndarray):
@@ -72,10 +73,11 @@ def keyframe_view(arrays: dict, i: int):
 
 
 class DeviceKeyframeMap:
-    def __init__(self, keyframes=None, device="cuda", fv_desc=True, arrays=None):
+    def __init__(self, keyframes=None, device="cuda", fv_desc=True, arrays=None, fv_angle=True):
         """keyframes: iterable of (kps KEYPOINT_DTYPE[n], desc u8[n,32], valid u8[n], node_of_feature i[n]),
         or arrays: the same already packed (pack(), synth.keyframe_map()).
-        fv_desc: also keep the descriptors in FeatureVector order (map->fv_desc)."""
+        fv_desc / fv_angle: also keep the descriptors / keypoint angles in
+        FeatureVector order (map->fv_desc, map->fv_angle)."""
         import torch
         a = arrays if arrays is not None else pack(keyframes)
         self.nkf = len(a["kp_off"]) - 1
@@ -85,18 +87,25 @@ class DeviceKeyframeMap:
         p = lambda name: self.t[name].data_ptr()
         self.struct = OrbmKfMapDevice(self.nkf, p("kps"), p("desc"), p("valid"), p("kp_off"), p("fv_node"),
                                       p("fv_off"), p("fv_idx"), p("fv_node_off"), p("fv_idx_off"),
-                                      int(a["fv_node_off"][-1]), int(len(a["fv_idx"])), None)
+                                      int(a["fv_node_off"][-1]), int(len(a["fv_idx"])), None, None)
         self.ready = None
         # the descriptors in FeatureVector order (orbm_kf_map_fv_desc), once per map
         nfv = self.struct.n_fv_total
         self.t["fv_desc"] = torch.empty(max(1, nfv) * 32, dtype=torch.uint8, device=device)
-        if fv_desc and self.nkf > 0 and torch.device(device).type == "cuda":
+        self.t["fv_angle"] = torch.empty(max(1, nfv), dtype=torch.float32, device=device)
+        if (fv_desc or fv_angle) and self.nkf > 0 and torch.device(device).type == "cuda":
             cur = torch.cuda.current_stream(self.t["fv_desc"].device)
-            rc = capi.lib().orbm_kf_map_fv_desc(C.byref(self.struct), C.c_void_p(self.t["fv_desc"].data_ptr()),
-                                                C.c_void_p(cur.cuda_stream))
-            capi.check(rc, "orbm_kf_map_fv_desc")
-            self.struct.fv_desc = self.t["fv_desc"].data_ptr()
-            # a search on another stream waits for it (search_prepared)
+            if fv_desc:
+                rc = capi.lib().orbm_kf_map_fv_desc(C.byref(self.struct), C.c_void_p(self.t["fv_desc"].data_ptr()),
+                                                    C.c_void_p(cur.cuda_stream))
+                capi.check(rc, "orbm_kf_map_fv_desc")
+                self.struct.fv_desc = self.t["fv_desc"].data_ptr()
+            if fv_angle:
+                rc = capi.lib().orbm_kf_map_fv_angle(C.byref(self.struct), C.c_void_p(self.t["fv_angle"].data_ptr()),
+                                                     C.c_void_p(cur.cuda_stream))
+                capi.check(rc, "orbm_kf_map_fv_angle")
+                self.struct.fv_angle = self.t["fv_angle"].data_ptr()
+            # a search on another stream waits for them (search_prepared)
             self.ready = torch.cuda.Event()
             self.ready.record(cur)
 

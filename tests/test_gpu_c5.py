@@ -131,36 +131,44 @@ def _adversarial(seed, nf=1500, shape="default", nkf=12):
     return fk, fd, fnode, kfs
 
 
-def _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option, min_matches=20):
-    got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
+def _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option, min_matches=20, check_ori=True):
+    got, gnm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, check_ori))
     debug_option(capi.ORB_OPT_BOW_FORM, 1)
-    old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, True))
+    old, onm = (t.cpu().numpy() for t in m.search_by_bow(fk, fd, fnode, 0.75, check_ori))
     np.testing.assert_array_equal(got, old)
     np.testing.assert_array_equal(gnm, onm)
     f, fv = abi.frame_struct(fk, fd, 640, 480), abi.featvec_struct(fnode)
     for i, (kk, kd, valid, nid) in enumerate(kfs):
         rnm, rmatch = O.search_by_bow(abi.frame_struct(kk, kd, 640, 480), abi.featvec_struct(nid), valid,
-                                      f, fv, 0.75, True)
+                                      f, fv, 0.75, check_ori)
         assert gnm[i] == rnm
         np.testing.assert_array_equal(got[i], rmatch)
     assert gnm.min() > min_matches
 
 
-@pytest.mark.parametrize("seed,fv_desc", [(3, True), (3, False), (4, True), (5, True)])
-def test_c5_kf_lane_adversarial(gpu_lib, seed, fv_desc, debug_option):
+@pytest.mark.parametrize("seed,fv_desc,fv_angle,check_ori", [(3, True, True, True), (3, False, False, True),
+                                                             (4, True, True, True), (5, True, False, True),
+                                                             (6, True, True, False)])
+def test_c5_kf_lane_adversarial(gpu_lib, seed, fv_desc, fv_angle, check_ori, debug_option):
     """The lane-per-keyframe-feature search (k_bowk_*) against the oracle and
-    against the node-per-wave kernel (k_bow) on _adversarial inputs."""
+    against the node-per-wave kernel (k_bow) on _adversarial inputs; the
+    rotation filter of k_bowk_final with the map's FeatureVector-order angles
+    and with the keypoint gather, and without the filter."""
     fk, fd, fnode, kfs = _adversarial(seed)
-    m = kfmap.DeviceKeyframeMap(kfs, fv_desc=fv_desc)
+    m = kfmap.DeviceKeyframeMap(kfs, fv_desc=fv_desc, fv_angle=fv_angle)
     assert m.struct.n_nodes_total > 0 and m.struct.n_fv_total > 0
-    assert bool(m.struct.fv_desc) == fv_desc
+    assert bool(m.struct.fv_desc) == fv_desc and bool(m.struct.fv_angle) == fv_angle
+    order = [kfmap.featvec_csr(nid)[2] for kk, kd, valid, nid in kfs]
     if fv_desc:   # orbm_kf_map_fv_desc: row fv_idx_off[i] + p = descriptor fv_idx[.] of keyframe i
-        want = np.concatenate([kd[kfmap.featvec_csr(nid)[2]] for kk, kd, valid, nid in kfs])
+        want = np.concatenate([kd[o] for (kk, kd, valid, nid), o in zip(kfs, order)])
         np.testing.assert_array_equal(m.t["fv_desc"].cpu().numpy().reshape(-1, 32)[:len(want)], want)
-    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option)
+    if fv_angle:  # orbm_kf_map_fv_angle: the same rows, keypoint angles
+        want = np.concatenate([kk["angle"][o] for (kk, kd, valid, nid), o in zip(kfs, order)])
+        np.testing.assert_array_equal(m.t["fv_angle"].cpu().numpy()[:len(want)], want)
+    _check_vs_oracle_and_k_bow(m, fk, fd, fnode, kfs, debug_option, check_ori=check_ori)
 
 
-@pytest.mark.parametrize("case", ["big", "big_nobig", "huge_frame", "many_nodes"])
+@pytest.mark.parametrize("case", ["big", "big_nobig", "huge_frame", "many_nodes", "small_frame"])
 def test_c5_kf_lane_resolve_forms(gpu_lib, case, debug_option):
     """The resolve and top-4 forms the default C5 data never reaches:
     big      frame nodes of > 512 features: k_bowk_resolve_lane<true, true>
@@ -169,8 +177,10 @@ def test_c5_kf_lane_resolve_forms(gpu_lib, case, debug_option):
              'taken' test of large nodes read from the match row;
     huge_frame a frame of 9000 features (> 8192: no LDS bitmap fits, the
              match-row form is the only one);
-    many_nodes > 1024 frame nodes: single bucket counters (nsub = 1)."""
-    nf = 9000 if case == "huge_frame" else 2500
+    many_nodes > 1024 frame nodes: single bucket counters (nsub = 1);
+    small_frame a frame of <= 512 features: every thread's bitmap covers the
+             frame, no big-node launch."""
+    nf = {"huge_frame": 9000, "small_frame": 480}.get(case, 2500)
     shape = "many_nodes" if case == "many_nodes" else ("big" if "big" in case or case == "huge_frame" else "default")
     fk, fd, fnode, kfs = _adversarial(11 + len(case), nf=nf, shape=shape, nkf=8)
     if shape == "big" or case == "huge_frame":

@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--per-kf", type=int, default=5000)
+    ap.add_argument("--valid-frac", type=float, default=1.0,
+                    help="share of keyframe features with a valid MapPoint (1.0: the stated C5 map)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="keyframes the oracle checks (-1: all)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--dump", default="", help="directory: each rank saves its shard's matches (tests)")
@@ -98,7 +100,8 @@ def run_c5(args):
     nid = nid_t.cpu().numpy()
     ids = list(sharding.shard(args.nkf, rank, world))
     t0 = time.perf_counter()
-    arrays = synth.keyframe_map(k, d, nid, ids, seed=7, per_kf=args.per_kf)
+    arrays = synth.keyframe_map(k, d, nid, ids, seed=7, per_kf=args.per_kf,
+                                valid_frac=getattr(args, "valid_frac", 1.0))
     m = kfmap.DeviceKeyframeMap(arrays=arrays)
     build_s = time.perf_counter() - t0
     nfeat_kf = int(arrays["kp_off"][-1])
