@@ -876,6 +876,9 @@ __global__ __launch_bounds__(256) void k_pyramid(PyrArgs a) {
 // even and odd columns de-interleaved at landing, no splitting here -- was
 // measured slower: 0.575 vs 0.510 ms, twice the LDS reads per item.)
 
+#ifndef ORB_FAST_LERP
+#define ORB_FAST_LERP 1   // k_fast_cells' pre-test in bytes by v_lerp_u8 (0: packed u16 pairs)
+#endif
 #ifndef ORB_FAST_COMPASS_AND
 #define ORB_FAST_COMPASS_AND 1   // pre-test: one vertical AND one horizontal compass pixel past the threshold
 #endif
@@ -917,6 +920,33 @@ __device__ __forceinline__ uint64_t item_byte_mask(int s, int e) {
 __device__ __forceinline__ uint32_t lo_bytes(uint32_t x) { return x & 0x00ff00ffu; }
 // u16 pair (x.b1, x.b3) in one v_perm (a shift and a mask otherwise)
 __device__ __forceinline__ uint32_t hi_bytes(uint32_t x) { return __builtin_amdgcn_perm(0u, x, 0x0c030c01u); }
+
+// The compass pre-test on four pixels at once, in bytes (ORB_FAST_LERP).
+// v_lerp_u8 averages bytes with a 9-bit sum, so with the complement of the
+// centre, h = lerp(X, ~C, 1) = 128 + floor((X - C) / 2) per byte, and a second
+// lerp against a complemented constant puts "h >= T" in bit 7 of each byte.
+// X > C + t  =>  h >= 128 + floor((t + 1) / 2)  (= tb), and
+// X < C - t  =>  h <= 128 + floor((-t - 1) / 2) (= td1 - 1): necessary
+// conditions (the halving admits X - C = t for odd t + 1 and -t for odd t), so
+// a cleared flag still proves the direction's strength - 1 < t, as the u16
+// form's.  ntb = ~tb, ntd = ~td1 per byte.  Flags: bit 7 of byte k = pixel k.
+struct LerpTh { uint32_t ntb, ntd; };
+__device__ __forceinline__ LerpTh lerp_thresholds(int t) {
+    const uint32_t tb = min(128 + ((t + 1) >> 1), 255), td1 = 129 - ((t + 2) >> 1);
+    return LerpTh{~(tb * 0x01010101u), ~(td1 * 0x01010101u)};
+}
+__device__ __forceinline__ void compass_lerp(uint32_t c, uint32_t u, uint32_t d, uint32_t l, uint32_t r,
+                                             LerpTh th, uint32_t& bright, uint32_t& darkx) {
+    const uint32_t nc = ~c, one = 0x01010101u;
+    const uint32_t hu = __builtin_amdgcn_lerp(u, nc, one), hd = __builtin_amdgcn_lerp(d, nc, one);
+    const uint32_t hl = __builtin_amdgcn_lerp(l, nc, one), hr = __builtin_amdgcn_lerp(r, nc, one);
+    const uint32_t bu = __builtin_amdgcn_lerp(hu, th.ntb, one), bd = __builtin_amdgcn_lerp(hd, th.ntb, one);
+    const uint32_t bl = __builtin_amdgcn_lerp(hl, th.ntb, one), br = __builtin_amdgcn_lerp(hr, th.ntb, one);
+    const uint32_t gu = __builtin_amdgcn_lerp(hu, th.ntd, one), gd = __builtin_amdgcn_lerp(hd, th.ntd, one);
+    const uint32_t gl = __builtin_amdgcn_lerp(hl, th.ntd, one), gr = __builtin_amdgcn_lerp(hr, th.ntd, one);
+    bright = (bu | bd) & (bl | br);              // bit 7: one of U, D and one of L, R brighter
+    darkx = (gu & gd) | (gl & gr);               // bit 7 CLEAR: one of U, D and one of L, R darker
+}
 // u16 pair of bytes (hi.bs1 | lo.bs0 selectors 0-3: lo, 4-7: hi) in one v_perm
 template <uint32_t SEL>
 __device__ __forceinline__ uint32_t pair_bytes(uint32_t hi, uint32_t lo) { return __builtin_amdgcn_perm(hi, lo, SEL); }
@@ -1652,19 +1682,43 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             //    pixels pass, ~8% of items hold one, so the compaction writes
             //    loop over the set bits instead of visiting all four bytes)
             const u16x2 tt = {(unsigned short)t, (unsigned short)t};
+#if ORB_FAST_LERP
+            const LerpTh lth = lerp_thresholds(t);
+#endif
             ncand = 0;
             // one item: flag bytes (byte k = item pixel k) and its window index
             // item (row r, dword pair k) -> flag bytes; ok: the item exists
             auto pretest_rk = [&](bool ok, int r, int k, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh,
                                   int& idx0) {
+#if ORB_FAST_LERP
+                {   // branch-free: the caller clamps a missing item onto the last one, ok = 0 clears its flags
+#else
                 bl = bh = dl = dh = 0;
                 idx0 = 0;
                 if (ok) {
+#endif
                     const int j = j0 + 2 * k;
                     const uint32_t* row = roi32 + __umul24(r + 3, rs4) + j;
                     const uint32_t cm = row[-1], c0 = row[0], c1 = row[1], c2 = row[2];
                     const uint32_t u0 = row[-3 * rs4], u1 = row[1 - 3 * rs4];
                     const uint32_t d0 = row[3 * rs4], d1 = row[1 + 3 * rs4];
+#if ORB_FAST_LERP
+                    uint64_t vm = k == 0 ? m_first : (k == ndp - 1 ? m_last : 0x8080808080808080ull);
+                    if (!ok) vm = 0;
+                    const uint32_t vl = (uint32_t)vm, vh = (uint32_t)(vm >> 32);
+                    uint32_t br0, dx0, br1, dx1;
+                    // the pixels 3 left / 3 right of each dword's 4: one v_alignbyte each
+                    compass_lerp(c0, u0, d0, __builtin_amdgcn_alignbyte(c0, cm, 1), __builtin_amdgcn_alignbyte(c1, c0, 3),
+                                 lth, br0, dx0);
+                    compass_lerp(c1, u1, d1, __builtin_amdgcn_alignbyte(c1, c0, 1), __builtin_amdgcn_alignbyte(c2, c1, 3),
+                                 lth, br1, dx1);
+                    bl = br0 & vl;
+                    bh = br1 & vh;
+                    dl = ~dx0 & vl;
+                    dh = ~dx1 & vh;
+                    idx0 = cand_enc(r, 4 * j - X0, ww);
+                    (void)tt;
+#else
                     // u16 pairs of the pixels 3 left / 3 right of pixels (0, 2) and
                     // (1, 3) of dwords c0, c1: one v_perm each, four shared with C
                     const uint32_t c0l = lo_bytes(c0), c0h = hi_bytes(c0), c1l = lo_bytes(c1), c1h = hi_bytes(c1);
@@ -1690,11 +1744,17 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                     dl = sign_bytes(k0, k1) & vl;
                     dh = sign_bytes(k2, k3) & vh;
                     idx0 = cand_enc(r, 4 * j - X0, ww);
+#endif
                 }
             };
             auto pretest = [&](int it, uint32_t& bl, uint32_t& bh, uint32_t& dl, uint32_t& dh, int& idx0) {
-                const int r = div_row(it, inv_ndp);
-                pretest_rk(it < nitems, r, it - (int)__umul24(r, ndp), bl, bh, dl, dh, idx0);
+#if ORB_FAST_LERP
+                const int itc = min(it, nitems - 1);
+#else
+                const int itc = it;
+#endif
+                const int r = div_row(itc, inv_ndp);
+                pretest_rk(it < nitems, r, itc - (int)__umul24(r, ndp), bl, bh, dl, dh, idx0);
             };
 #if ORB_FAST_PIPE
             // the same pre-test split at its LDS reads, so the reads of round
@@ -1802,13 +1862,15 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 int i0;
                 pretest(base + lane, bl, bh, dl, dh, i0);
 #endif
-                const uint32_t mb = __builtin_amdgcn_udot4(bh >> 7, 0x80402010u,
-                                                           __builtin_amdgcn_udot4(bl >> 7, 0x08040201u, 0u, false), false);
-                const uint32_t md = __builtin_amdgcn_udot4(dh >> 7, 0x80402010u,
-                                                           __builtin_amdgcn_udot4(dl >> 7, 0x08040201u, 0u, false), false);
+                // flag bytes (bit 7 only) -> 8-bit masks, still scaled by 128
+                // (the shift folds into the list entry's)
+                const uint32_t mb = __builtin_amdgcn_udot4(bh, 0x80402010u, __builtin_amdgcn_udot4(bl, 0x08040201u, 0u, false),
+                                                           false);
+                const uint32_t md = __builtin_amdgcn_udot4(dh, 0x80402010u, __builtin_amdgcn_udot4(dl, 0x08040201u, 0u, false),
+                                                           false);
                 const bool has = (mb | md) != 0u;
                 const uint64_t bal = __ballot(has);
-                if (has) ilist[nlist + mask_rank(bal)] = (uint32_t)(base + lane) | (mb << 16) | (md << 24);
+                if (has) ilist[nlist + mask_rank(bal)] = (uint32_t)(base + lane) | (mb << 9) | (md << 17);
                 nlist += __popcll(bal);
             }
             fast_wave_sync();
