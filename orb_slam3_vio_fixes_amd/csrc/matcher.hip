@@ -317,6 +317,19 @@ __host__ __device__ __forceinline__ int rot_bin(float a1, float a2) {
     return bin;
 }
 
+// hist[b] += 1 for every active lane's bin b (b < 0: none), one LDS atomic
+// per distinct bin of the wave: the matches of a keyframe share one or two
+// rotation bins, and 64 same-address LDS atomics serialise
+__device__ __forceinline__ void hist_add_wave(int* hist, int b) {
+    for (uint64_t act = __ballot(b >= 0); act;) {
+        const int l = __ffsll((long long)act) - 1;
+        const int b0 = __builtin_amdgcn_readlane(b, l);
+        const uint64_t m = __ballot(b == b0) & act;
+        if (lane_id() == l) atomicAdd(&hist[b0], __popcll(m));
+        act &= ~m;
+    }
+}
+
 // ComputeThreeMaxima (ORBmatcher.cc:2012-2053)
 __host__ __device__ __forceinline__ void three_maxima(const int* h, int& i1, int& i2, int& i3) {
     int m1 = 0, m2 = 0, m3 = 0;
@@ -1333,11 +1346,10 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
             }
 #pragma unroll
             for (int u = 0; u < kU; ++u) {
-                if (m[u] < 0) continue;
                 const int i = i0 + u * nt;
-                const int b = rot_bin(ka[u], fa[u]);
-                atomicAdd(&hist[b], 1);
-                if (i < kBowFinalBins) sbin[i] = (uint8_t)b;
+                const int b = m[u] >= 0 ? rot_bin(ka[u], fa[u]) : -1;
+                hist_add_wave(hist, b);
+                if (b >= 0 && i < kBowFinalBins) sbin[i] = (uint8_t)b;
             }
         }
         __syncthreads();
@@ -1445,7 +1457,12 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
 //                  is the node rescanned exactly, lane-parallel.
 // k_bow_final (rotation filter, counts) follows unchanged.
 // ---------------------------------------------------------------------------
-constexpr int kBowK = 4;
+#ifndef ORB_BOWK_K
+#define ORB_BOWK_K 4
+#endif
+constexpr int kBowK = ORB_BOWK_K;
+static_assert(kBowK == 2 || kBowK == 4, "a slot's list is one 8- or 16-byte load");
+typedef uint32_t bowk_list __attribute__((ext_vector_type(kBowK)));
 // the lane resolve's LDS bitmap: 16 words (512 positions) a thread, odd pitch
 constexpr int kBowLaneWords = 16, kBowLanePitch = 17;
 
@@ -1462,15 +1479,21 @@ struct BowKArgs {
                                    // big-node resolve form takes (written by k_bowk_scan)
     int* bstart;           // [f_nnodes + 1] bucket starts, padded to 64 slots
     uint32_t* slot_src;    // [slots] global KF feature (kp_off[pr] + ikf), ~0: none
-    uint4* lists;          // [slots] kBowK smallest keys, ascending, ~0: none
+    bowk_list* lists;      // [slots] kBowK smallest keys, ascending, ~0: none
     int* gstart;           // [f_nnodes + 1] their starts
     int* g_rank;           // [G] rank of g among its frame node's entries
     int* perm;             // [G] g entries ordered by frame node
     int* chunk_node;       // [slots / 32] frame node of every 32-slot chunk
     uint32_t* slot_pos;    // [slots] FeatureVector position (row of kf_fvdesc) when kf_fvdesc is set
-    int32_t* claim;        // [slots] the resolve's claim (frame feature index, -1: none) for k_bowk_final,
-                           // or NULL: claims go straight to the match rows (then k_bow_final)
+    uint16_t* claim;       // [slots] the resolve's claim (frame feature index, 0xffff: none) for
+                           // k_bowk_final, or NULL: claims go straight to the match rows (then k_bow_final)
 };
+
+// A g's slots run from an 8-aligned offset of its bucket (buckets start at
+// multiples of 64) over its KF features rounded up to 8, the tail slots
+// holding no feature: the resolve reads and writes a g's slots 8 at a time
+// with aligned vector accesses.
+__device__ __forceinline__ int kf_run(int nkf) { return (nkf + 7) & ~7; }
 
 // One block per pair (its KF nodes g are contiguous: no search for the pair
 // of g), the frame's node ids staged in LDS for the lower_bound of each KF
@@ -1505,7 +1528,8 @@ __global__ __launch_bounds__(256) void k_bowk_map(BowKArgs k) {
             // nothing aggregates in the block), on one of nsub words of the node: ~10k
             // same-address atomics per node serialised at L2 (0.22 ms) otherwise
             const unsigned long long o =
-                atomicAdd(k.bgcount + (long long)fl * k.nsub + (pr & (k.nsub - 1)), (1ull << 32) | (unsigned long long)nkf);
+                atomicAdd(k.bgcount + (long long)fl * k.nsub + (pr & (k.nsub - 1)),
+                          (1ull << 32) | (unsigned long long)kf_run(nkf));
             k.g_off[g] = (int)(uint32_t)o;
             k.g_rank[g] = (int)(o >> 32);
         } else {
@@ -1613,12 +1637,21 @@ __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
             base = __shfl(base, 0, kWave);
             if (base < 0) continue;
             for (int p = ko[ia] + lane_id(); p < ko[ia + 1]; p += kWave) put(base, p);
+            const int pe = ko[ia] + kf_run(ko[ia + 1] - ko[ia]);       // the run's tail: no feature
+            if (ko[ia + 1] + lane_id() < pe) k.slot_src[base + ko[ia + 1] + lane_id()] = 0xffffffffu;
         }
         return;
     }
     for (int ia = threadIdx.x; ia <= nn; ia += blockDim.x) {
         s_ko[ia] = ko[ia];
-        if (ia < nn) s_base[ia] = slot_base(ia);
+        if (ia < nn) {
+            const int b = slot_base(ia);
+            s_base[ia] = b;
+            if (b >= 0) {                                              // the run's tail: no feature
+                const int p0 = ko[ia], p1 = ko[ia + 1];
+                for (int p = p1; p < p0 + kf_run(p1 - p0); ++p) k.slot_src[b + p] = 0xffffffffu;
+            }
+        }
     }
     __syncthreads();
     const int p0 = s_ko[0], p1 = s_ko[nn];
@@ -1744,6 +1777,17 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
     // [buffer][row * 17 + 2 s + h]: the odd row pitch (272 B) keeps a
     // ds_read_b128 of 32 rows at one (s, h) off a single bank group
     __shared__ bowk_v4i s_a[2][32 * 17];
+    // byte -> its 8 bits as +-1 int8 (bit e -> byte e): a keyframe descriptor's
+    // B operand is 2 table reads per 16 bits (4 VALU ops) instead of 4 nibble
+    // spreads (16 VALU ops)
+    __shared__ uint2 s_pm1[256];
+    {
+        const uint32_t t = threadIdx.x;   // blockDim = 256: one entry each
+        const uint32_t sel = ((t & 0xfu) * 0x00810204u) & 0x04040404u, seh = ((t >> 4) * 0x00810204u) & 0x04040404u;
+        s_pm1[t] = make_uint2(__builtin_amdgcn_perm(0x01010101u, 0xffffffffu, sel),
+                              __builtin_amdgcn_perm(0x01010101u, 0xffffffffu, seh));
+    }
+    __syncthreads();
     const BowArgs& a = k.b;
     constexpr int kWS = 32 * NSET;                   // slots per wave
     const long long slotb = (long long)blockIdx.x * 4 * kWS;
@@ -1777,7 +1821,11 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
             d[0] = q0.x; d[1] = q0.y; d[2] = q0.z; d[3] = q0.w; d[4] = q1.x; d[5] = q1.y; d[6] = q1.z; d[7] = q1.w;
         }
 #pragma unroll
-        for (int s2 = 0; s2 < 8; ++s2) B[c][s2] = bits_pm1(d[s2] >> (16 * h));
+        for (int s2 = 0; s2 < 8; ++s2) {
+            const uint2 lo = s_pm1[__builtin_amdgcn_ubfe(d[s2], 16 * h, 8)];
+            const uint2 hi = s_pm1[__builtin_amdgcn_ubfe(d[s2], 16 * h + 8, 8)];
+            B[c][s2] = bowk_v4i{(int)lo.x, (int)lo.y, (int)hi.x, (int)hi.y};
+        }
     }
     uint32_t kk[NSET][kBowK];
 #pragma unroll
@@ -1876,7 +1924,12 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
         for (int t = 0; t < kBowK; ++t) other[t] = (uint32_t)__shfl_xor((int)q[t], 32, kWave);
 #pragma unroll
         for (int t = 0; t < kBowK; ++t) topk_push(q, other[t]);
-        if (h == 0) k.lists[slot0 + 32 * c + col] = make_uint4(q[0], q[1], q[2], q[3]);
+        if (h == 0) {
+            bowk_list o;
+#pragma unroll
+            for (int t = 0; t < kBowK; ++t) o[t] = q[t];
+            k.lists[slot0 + 32 * c + col] = o;
+        }
     }
 }
 
@@ -1981,22 +2034,28 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
 #endif
     constexpr int kChunk = ORB_BOWK_RES_CHUNK;
     const int nkc = max(nkf, 1) - 1;
+    static_assert(kChunk == 8, "a chunk is one aligned 8-slot run");
     for (int j0 = 0; j0 < nkf_max; j0 += kChunk) {
         uint32_t sv[kChunk];
-        uint4 Lv[kChunk];
+        bowk_list Lv[kChunk];
+        uint32_t cw[kChunk / 2] = {0u, 0u, 0u, 0u};   // the chunk's claims, u16 each
+        {
+            // inside the lane's own run (past its end: its last chunk again, unused)
+            const int jb = min(j0, nkc & ~7);
+            const uint4 s0 = *(const uint4*)(k.slot_src + base + jb), s1 = *(const uint4*)(k.slot_src + base + jb + 4);
+            sv[0] = s0.x; sv[1] = s0.y; sv[2] = s0.z; sv[3] = s0.w; sv[4] = s1.x; sv[5] = s1.y; sv[6] = s1.z; sv[7] = s1.w;
 #pragma unroll
-        for (int c = 0; c < kChunk; ++c) {
-            const int jc = min(j0 + c, nkc);
-            sv[c] = k.slot_src[base + jc];
-            Lv[c] = k.lists[base + jc];
+            for (int c = 0; c < kChunk; ++c) Lv[c] = k.lists[base + jb + c];
         }
 #pragma unroll
         for (int c = 0; c < kChunk; ++c) {
             const bool act = j0 + c < nkf;
             const uint32_t s = act ? sv[c] : 0xffffffffu;
-            const uint4 L = Lv[c];
+            const bowk_list L = Lv[c];
             const bool valid = s != 0xffffffffu;                         // a valid MapPoint (:255-260)
-            const uint32_t keys[kBowK] = {L.x, L.y, L.z, L.w};
+            uint32_t keys[kBowK];
+#pragma unroll
+            for (int q = 0; q < kBowK; ++q) keys[q] = L[q];
             uint32_t e1 = 0xffffffffu, e2 = 0xffffffffu;
             bool tk[kBowK];
             if constexpr (all_lds) {
@@ -2065,11 +2124,8 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
             if (wave_lds_fidx) fi = s_fidx[min(bpos, kBowFidxStage - 1)];
             else fi = lds_fidx ? s_fidx[min(bpos, kBowFidxStage - 1)] : fidx[claim ? bpos : 0];
             if (k.claim) {
-                // the claim beside the slot (this lane's slots are consecutive, so
-                // a line fills over 32 steps of one lane); k_bowk_final builds the
-                // match rows.  Storing straight into the rows (4 B scattered over
-                // a 20 KB row per step) cost the walk ~0.9 ms of its ~1.6
-                if (act) k.claim[base + j0 + c] = claim ? (int32_t)fi : -1;
+                // the claim beside the slot, stored 8 at a time below
+                cw[c >> 1] |= (claim ? fi : 0xffffu) << (16 * (c & 1));
             } else {
                 int32_t* dst = claim ? match + fi : sink;
                 *dst = claim ? (int32_t)((long long)s - kpo) : 0;
@@ -2081,49 +2137,118 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
             }
             nm += claim;
         }
+        // one aligned 16-B store per lane per chunk: a store of 64 lanes' claims
+        // touches 64 lines, and one per step (or a scattered 4-B store into the
+        // match rows) cost the walk ~0.9 ms of its ~1.6 on the C5 map
+        if (k.claim && j0 < nkf) *(uint4*)(k.claim + base + j0) = make_uint4(cw[0], cw[1], cw[2], cw[3]);
     }
     if (nm && !k.claim) atomicAdd(&a.nmatches[pr], nm);
 }
 
 // The match rows from the resolve's claims, with the rotation filter
 // (:404-422) and the counts: one block per pair, its row and the match bins
-// in LDS, the claims read per (pair, node) as contiguous slot runs, the
-// keyframe angles from the map's FeatureVector-order copy (contiguous too)
-// when it has one, and the row written once, coalesced.
-constexpr int kBowkRow = 8192;   // frame features of the LDS row (the all-LDS resolve's bound)
+// in LDS.  Like k_bowk_fill, every thread takes the pair's KF features in
+// FeatureVector order (contiguous), each one's run base found by a search of
+// the node offsets staged in LDS, four features' loads in flight per thread;
+// the keyframe angles come from the map's FeatureVector-order copy
+// (contiguous too) when it has one; the row is written once, coalesced.
+constexpr int kBowkRow = 8192;          // frame features of the LDS row (the all-LDS resolve's bound)
+constexpr int kBowkFinalStage = 256;    // KF nodes whose run bases are staged in LDS
 __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
-    __shared__ int s_row[kBowkRow];
-    __shared__ uint8_t s_bin[kBowkRow];
+    extern __shared__ int s_row[];                       // [f_n] KF feature or -1, then [f_n] u8 bins
+    __shared__ int s_ko[kBowkFinalStage + 1];
+    __shared__ int s_base[kBowkFinalStage];
     __shared__ int hist[32];
     __shared__ int s_cnt;
     const BowArgs& a = k.b;
+    uint8_t* s_bin = (uint8_t*)(s_row + a.f_n);
     const int pr = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, lane = lane_id();
     for (int i = tid; i < a.f_n; i += nt) s_row[i] = -1;
     if (tid < 32) hist[tid] = 0;
     if (tid == 0) s_cnt = 0;
-    __syncthreads();
     const long long g0 = a.node_off[pr];
     const int nn = (int)(a.node_off[pr + 1] - g0);
     const int* ko = a.kf_off + g0 + pr;
     const long long io = a.idx_off[pr], kpo = a.kp_off[pr];
     const uint32_t* ki = a.kf_idx + io;
-    // a wave per KF node, a lane per feature
-    for (int ia = wave_id(); ia < nn; ia += nt / kWave) {
+    auto run_base = [&](int ia) -> int {              // slot of the node's feature p: base + p; -1: no frame node
         const int fl = k.g_fl[g0 + ia];
-        if (fl < 0) continue;
-        const int base = k.bstart[fl] + k.g_off[g0 + ia];
-        const int p0 = ko[ia], n = ko[ia + 1] - p0;
-        for (int j = lane; j < n; j += kWave) {
-            const int c = k.claim[base + j];
-            if (c < 0) continue;
-            const int ikf = (int)ki[p0 + j];
+        return fl < 0 ? -1 : k.bstart[fl] + k.g_off[g0 + ia] - ko[ia];
+    };
+    // claim c (0xffff: none) of KF feature row p; the bins counted per wave by
+    // bin value (a keyframe's matches share one or two bins: one LDS atomic per
+    // distinct bin, not 64 serialised same-address atomics)
+    auto take = [&](int c, int p) {
+        int b = -1;
+        if (c != 0xffff) {
+            const int ikf = (int)ki[p];
             s_row[c] = ikf;
             if (a.check_ori) {
-                const float ka = a.kf_fvangle ? a.kf_fvangle[io + p0 + j] : a.kf_kps[kpo + ikf].angle;
-                const int b = rot_bin(ka, a.f_kps[c].angle);
+                const float ka = a.kf_fvangle ? a.kf_fvangle[io + p] : a.kf_kps[kpo + ikf].angle;
+                b = rot_bin(ka, a.f_kps[c].angle);
                 s_bin[c] = (uint8_t)b;
-                atomicAdd(&hist[b], 1);
             }
+        }
+        hist_add_wave(hist, b);
+    };
+    const bool staged = nn <= kBowkFinalStage;
+    if (staged)
+        for (int ia = tid; ia <= nn; ia += nt) {
+            s_ko[ia] = ko[ia];
+            if (ia < nn) s_base[ia] = run_base(ia);
+        }
+    __syncthreads();
+    if (staged) {
+        // every thread over the pair's KF features in FeatureVector order (as
+        // k_bowk_fill), four claims in flight per thread
+        const int p0 = s_ko[0], p1 = s_ko[nn];
+        constexpr int kU = 4;
+        for (int q = p0 + tid; q < p1; q += kU * nt) {
+            // every load of the four rows that does not need a claim first, then
+            // the frame angles of the claimed ones: two dependent rounds
+            int cs[kU], ik[kU];
+            float ka[kU], fa[kU];
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int p = q + u * nt;
+                int lo = 0, hi = nn;                     // last ia with s_ko[ia] <= p
+                while (hi - lo > 1) {
+                    const int mid = (lo + hi) >> 1;
+                    if (s_ko[mid] <= p) lo = mid;
+                    else hi = mid;
+                }
+                const int b = p < p1 ? s_base[lo] : -1;
+                const int pc = min(p, p1 - 1);
+                cs[u] = b >= 0 ? (int)k.claim[b + p] : 0xffff;
+                ik[u] = (int)ki[pc];
+                ka[u] = a.kf_fvangle ? a.kf_fvangle[io + pc] : 0.f;
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                fa[u] = 0.f;
+                if (a.check_ori && cs[u] != 0xffff) {
+                    fa[u] = a.f_kps[cs[u]].angle;
+                    if (!a.kf_fvangle) ka[u] = a.kf_kps[kpo + ik[u]].angle;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                int b = -1;
+                if (cs[u] != 0xffff) {
+                    s_row[cs[u]] = ik[u];
+                    if (a.check_ori) {
+                        b = rot_bin(ka[u], fa[u]);
+                        s_bin[cs[u]] = (uint8_t)b;
+                    }
+                }
+                hist_add_wave(hist, b);
+            }
+        }
+    } else {
+        for (int ia = wave_id(); ia < nn; ia += nt / kWave) {   // a wave per KF node
+            const int b = run_base(ia);
+            if (b < 0) continue;
+            for (int p = ko[ia] + lane; p < ko[ia + 1]; p += kWave) take(k.claim[b + p], p);
         }
     }
     __syncthreads();
@@ -3683,8 +3808,8 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         PBuf<int> g_fl, g_off, g_pr, bstart, gstart, g_rank, perm, chunk_node, node_n;
         PBuf<unsigned long long> bgcount;
         PBuf<uint32_t> slot_src, slot_pos;
-        PBuf<int32_t> claim;
-        PBuf<uint4> lists;
+        PBuf<uint16_t> claim;
+        PBuf<bowk_list> lists;
         PBuf<bowk_v4i> fexp;
     };
     Scratch& S = stream_scratch<Scratch>(st);
@@ -3692,12 +3817,13 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         &g_rank = S.g_rank, &perm = S.perm, &chunk_node = S.chunk_node, &node_n = S.node_n;
     PBuf<unsigned long long>& bgcount = S.bgcount;
     PBuf<uint32_t>&slot_src = S.slot_src, &slot_pos = S.slot_pos;
-    PBuf<int32_t>& claim = S.claim;
-    PBuf<uint4>& lists = S.lists;
+    PBuf<uint16_t>& claim = S.claim;
+    PBuf<bowk_list>& lists = S.lists;
     PBuf<bowk_v4i>& fexp = S.fexp;
     const int nsub = a.f_nnodes <= 1024 ? 64 : 1;
     a.npairs = npairs;
-    const long long slots = nfv + (long long)kWave * a.f_nnodes;
+    // every g's run rounded up to 8 slots, every bucket to 64
+    const long long slots = nfv + 7 * G + (long long)kWave * a.f_nnodes;
     // the resolve form: every thread's claimed positions in an LDS bitmap when a
     // bitmap over every frame position fits 64 threads' LDS (nodes of > 512
     // features then take the BIG form); its claims then go beside the slots and
@@ -3737,6 +3863,9 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
             a.f_off + a.f_nnodes, fexp.p);
     // (measured and dropped, DESIGN.md §5: the VALU top-4 pass, two 32-column
     // keyframe sets per MFMA wave, a wave-walk resolve)
+    // (measured and dropped in round 4: persistent blocks over the whole grid,
+    // 3.1-3.2 ms; blocks of 2 / 4 consecutive items with the next item's
+    // descriptors prefetched, 2.88 / 2.78 vs 2.51 ms)
     KLAUNCH(k_bowk_topk_mfma<1>, dim3((unsigned)((slots + 127) / 128)), dim3(256), 0, st, k, fexp.p);
     if (all_lds) {
         KLAUNCH((k_bowk_resolve_lane<false, true>), dim3(gb), dim3(256), 0, st, k, big_pitch);
@@ -3746,7 +3875,7 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     } else {
         KLAUNCH((k_bowk_resolve_lane<false, false>), dim3(gb), dim3(256), 0, st, k, 0);
     }
-    if (claims) KLAUNCH(k_bowk_final, dim3(npairs), dim3(256), 0, st, k);
+    if (claims) KLAUNCH(k_bowk_final, dim3(npairs), dim3(256), (size_t)a.f_n * 5 + 16, st, k);
     else KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
