@@ -407,7 +407,8 @@ int orbm_search_by_bow_many(int nkf, const orbm_frame* const* kfs, const orbm_fe
 
 /* SearchByBoW(KF_i, F) for every keyframe of the map against one frame; f and
  * ffv hold DEVICE pointers.  d_match: nkf x f->n (KF feature index or -1),
- * d_nmatches: nkf.  Asynchronous on `stream`. */
+ * d_nmatches: nkf.  A keyframe holds fewer than 2^26 features.  Asynchronous
+ * on `stream`. */
 int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_frame* f,
                                     const orbm_featvec* ffv, float nnratio, int check_ori,
                                     int32_t* d_match, int32_t* d_nmatches, void* stream);

@@ -2155,13 +2155,12 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
 constexpr int kBowkRow = 8192;          // frame features of the LDS row (the all-LDS resolve's bound)
 constexpr int kBowkFinalStage = 256;    // KF nodes whose run bases are staged in LDS
 __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
-    extern __shared__ int s_row[];                       // [f_n] KF feature or -1, then [f_n] u8 bins
+    extern __shared__ int s_row[];                       // [f_n] KF feature | rotation bin << 26, or -1
     __shared__ int s_ko[kBowkFinalStage + 1];
     __shared__ int s_base[kBowkFinalStage];
     __shared__ int hist[32];
     __shared__ int s_cnt;
     const BowArgs& a = k.b;
-    uint8_t* s_bin = (uint8_t*)(s_row + a.f_n);
     const int pr = blockIdx.x, tid = threadIdx.x, nt = blockDim.x, lane = lane_id();
     for (int i = tid; i < a.f_n; i += nt) s_row[i] = -1;
     if (tid < 32) hist[tid] = 0;
@@ -2182,12 +2181,11 @@ __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
         int b = -1;
         if (c != 0xffff) {
             const int ikf = (int)ki[p];
-            s_row[c] = ikf;
             if (a.check_ori) {
                 const float ka = a.kf_fvangle ? a.kf_fvangle[io + p] : a.kf_kps[kpo + ikf].angle;
                 b = rot_bin(ka, a.f_kps[c].angle);
-                s_bin[c] = (uint8_t)b;
             }
+            s_row[c] = ikf | (max(b, 0) << 26);
         }
         hist_add_wave(hist, b);
     };
@@ -2235,11 +2233,8 @@ __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
             for (int u = 0; u < kU; ++u) {
                 int b = -1;
                 if (cs[u] != 0xffff) {
-                    s_row[cs[u]] = ik[u];
-                    if (a.check_ori) {
-                        b = rot_bin(ka[u], fa[u]);
-                        s_bin[cs[u]] = (uint8_t)b;
-                    }
+                    if (a.check_ori) b = rot_bin(ka[u], fa[u]);
+                    s_row[cs[u]] = ik[u] | (max(b, 0) << 26);
                 }
                 hist_add_wave(hist, b);
             }
@@ -2257,9 +2252,10 @@ __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
     int32_t* match = a.match + (long long)pr * a.f_n;
     int cnt = 0;
     for (int i = tid; i < a.f_n; i += nt) {
-        int m = s_row[i];
+        const int e = s_row[i];
+        int m = e < 0 ? -1 : (e & 0x3ffffff);
         if (m >= 0 && a.check_ori) {
-            const int b = s_bin[i];
+            const int b = e >> 26;
             if (b != i1 && b != i2 && b != i3) m = -1;
         }
         cnt += m >= 0;
@@ -3832,6 +3828,7 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     const size_t big_lds = (size_t)64 * bp * sizeof(uint32_t);
     const bool all_lds = big_lds <= 64 * 1024 && !debug_opt(ORB_OPT_BOWK_BIG);
     const int big_pitch = all_lds ? bp : 0;
+    // (k_bowk_final packs a KF feature index, < 2^26 by the C ABI's contract, with its bin)
     const bool claims = all_lds && a.f_n <= kBowkRow && !a.out12 && !a.f_valid;
     int rc;
     if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc((size_t)a.f_nnodes * nsub)) ||
@@ -3875,7 +3872,7 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     } else {
         KLAUNCH((k_bowk_resolve_lane<false, false>), dim3(gb), dim3(256), 0, st, k, 0);
     }
-    if (claims) KLAUNCH(k_bowk_final, dim3(npairs), dim3(256), (size_t)a.f_n * 5 + 16, st, k);
+    if (claims) KLAUNCH(k_bowk_final, dim3(npairs), dim3(256), (size_t)a.f_n * 4, st, k);
     else KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }

@@ -81,6 +81,8 @@ class DeviceKeyframeMap:
         import torch
         a = arrays if arrays is not None else pack(keyframes)
         self.nkf = len(a["kp_off"]) - 1
+        if self.nkf > 0 and int(np.diff(np.asarray(a["kp_off"], np.int64)).max()) >= 1 << 26:
+            raise ValueError("a keyframe holds fewer than 2^26 features (orbm_search_by_bow_batch_device)")
         self.t = {name: torch.from_numpy(np.ascontiguousarray(a[name])).to(device)
                   for name in ("kps", "desc", "valid", "kp_off", "fv_node", "fv_off", "fv_idx", "fv_node_off",
                                "fv_idx_off")}

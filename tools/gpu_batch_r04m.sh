@@ -1,7 +1,7 @@
 #!/bin/bash
 # round 4: C5 tests, trace and PMC passes on the default build
 set -o pipefail
-out=gpurun_out/r04m
+out=gpurun_out/r04q
 mkdir -p "$out"
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_c5.py -m gpu > "$out/c5_tests.log" 2>&1 \
   || { echo "c5 tests failed"; grep -E "FAIL|Error|assert" "$out/c5_tests.log" | head -20; exit 1; }

@@ -13,6 +13,7 @@ for v in $vars; do
   mkdir -p "$out/$v"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/$v/trace" -o run -- python3 bench.py $ARGS > "$out/$v/bench.json" 2> "$out/$v/rocprof.err" || { echo "$v trace failed"; tail -5 "$out/$v/rocprof.err"; cp "$out/.default.so" orb_slam3_vio_fixes_amd/liborb_mi355x.so; exit 1; }
   python tools/kstats.py "$out/$v/trace/run_kernel_trace.csv" --csv "$out/$v/kernel_stats_by_grid.csv" > "$out/$v/kstats.txt"
+  if [ -n "$NOPMC" ]; then echo "== $v"; head -4 "$out/$v/kstats.txt"; continue; fi
   i=0
   for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES" \
              "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM GRBM_GUI_ACTIVE"; do
