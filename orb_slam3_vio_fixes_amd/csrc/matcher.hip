@@ -618,6 +618,15 @@ constexpr int kSfiThreads = 256;
 #ifndef ORB_SFI_SPEC
 #define ORB_SFI_SPEC 1   // speculative 8-query runs (0: the serial step-per-query walk)
 #endif
+#ifndef ORB_SFI_DEPTH
+#define ORB_SFI_DEPTH 3  // runs of keys in registers: the current one and the next ones in flight
+#endif
+constexpr int kSfiDepth = ORB_SFI_DEPTH;
+#ifndef ORB_SFI_STAGE
+#define ORB_SFI_STAGE 256   // queries whose top-K keys are staged in LDS before the walk (32 B each)
+#endif
+constexpr int kSfiStage = ORB_SFI_STAGE;
+static_assert(kSfiDepth >= 2, "the current run and at least one in flight");
 constexpr uint32_t kMdNone = 0xffff0000u;    // md21: no match yet (distance field 0xffff)
 __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
@@ -636,6 +645,9 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     int* hist = (int*)(md21 + a.cap);             // 32 (hist[31]: the filter's drop count)
     int* qlist = hist + 32;                       // cap: query i1 | (more than kTopK candidates) << 31
     int8_t* bin1 = (int8_t*)(qlist + a.cap);      // cap
+    // the first kSfiStage queries' keys (staged by all four waves before the
+    // walk: the walk then does no global load for them)
+    uint32_t* skeys = (uint32_t*)(lds + ((a.cap * 9 + 128 + 15) >> 2 & ~3));
     int32_t* m12 = a.matches + (long long)pr * a.cap;
     const int* list = (const int*)(a.gsorted + (long long)f2 * a.cap);
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
@@ -650,11 +662,6 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     if (tid < 32) hist[tid] = 0;
     __syncthreads();
     if (tid < kWave) {
-#if ORB_SFI_PRIO
-        // the serial walk is one latency-bound wave beside the extraction's
-        // waves on its SIMD: it issues first
-        __builtin_amdgcn_s_setprio(3);
-#endif
         // compact the queries in F1 order (in place: a round reads its 64
         // counts before it writes, and writes only below its own reads)
         int nq = 0;
@@ -665,6 +672,21 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             if (c > 0) qlist[nq + mask_rank(m)] = i | (c > kTopK ? (int)0x80000000 : 0);
             nq += __popcll(m);
         }
+        if (lane == 0) hist[31] = nq;                // (hist[31] is zeroed again below)
+    }
+    __syncthreads();
+    const int nq = hist[31];
+    const int nst = min(nq, kSfiStage);
+    for (int e = tid; e < nst * kTopK; e += kSfiThreads)
+        skeys[e] = topk[(long long)(qlist[e / kTopK] & 0x7fffffff) * kTopK + e % kTopK];
+    __syncthreads();
+    if (tid == 0) hist[31] = 0;
+    if (tid < kWave) {
+#if ORB_SFI_PRIO
+        // the serial walk is one latency-bound wave beside the extraction's
+        // waves on its SIMD: it issues first
+        __builtin_amdgcn_s_setprio(3);
+#endif
 #if ORB_SFI_SPEC
         // Speculative runs of 8 queries (the approach of k_proj_resolve_spec):
         // lane 8t + k holds key k of query j0 + t; every query of the run
@@ -684,15 +706,20 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         const int grp = lane >> 3, kk = lane & 7;
         auto run_keys = [&](int j0) -> uint32_t {
             const int j = j0 + grp;
-            return j < nq ? topk[(long long)(qlist[j] & 0x7fffffff) * kTopK + kk] : kNoKey;
+            return j < nst ? skeys[j * kTopK + kk]
+                           : (j < nq ? topk[(long long)(qlist[j] & 0x7fffffff) * kTopK + kk] : kNoKey);
         };
-        // the next two runs' keys are in flight while a round runs (a round is
-        // shorter than a global load's latency)
-        uint32_t kcur = nq > 0 ? run_keys(0) : kNoKey;
-        uint32_t kn1 = nq > 8 ? run_keys(8) : kNoKey;
-        uint32_t kn2 = nq > 16 ? run_keys(16) : kNoKey;
+        // keys of the staged queries come from LDS (walk 84.8 -> 78.7 us
+        // alone); past them the next kSfiDepth - 1 runs' keys are in flight
+        // while a round runs (the register rotation waits for the newest load
+        // every round, so deeper prefetch does not help: 82 / 82 / 85 / 90 us
+        // at 3 / 4 / 6 / 8 runs)
+        uint32_t kr[kSfiDepth];
+#pragma unroll
+        for (int i = 0; i < kSfiDepth; ++i) kr[i] = nq > 8 * i ? run_keys(8 * i) : kNoKey;
         int j0 = 0;
         while (j0 < nq) {
+            const uint32_t kcur = kr[0];
             const int nrun = min(8, nq - j0);
             const int qe = grp < nrun ? qlist[j0 + grp] : 0;
             const bool many = qe < 0;
@@ -787,17 +814,17 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             // the next runs' keys: shifted by the queries done (a whole run in
             // the usual case), the run after them loaded
             if (adv == 8) {
-                kcur = kn1;
-                kn1 = kn2;
+#pragma unroll
+                for (int i = 0; i + 1 < kSfiDepth; ++i) kr[i] = kr[i + 1];
             } else {
                 const int src = lane + 8 * adv;
-                const uint32_t a0 = (uint32_t)__shfl((int)kcur, src & 63, kWave);
-                const uint32_t a1 = (uint32_t)__shfl((int)kn1, src & 63, kWave);
-                const uint32_t a2 = (uint32_t)__shfl((int)kn2, src & 63, kWave);
-                kcur = src < 64 ? a0 : a1;
-                kn1 = src < 64 ? a1 : a2;
+                uint32_t sh[kSfiDepth];
+#pragma unroll
+                for (int i = 0; i < kSfiDepth; ++i) sh[i] = (uint32_t)__shfl((int)kr[i], src & 63, kWave);
+#pragma unroll
+                for (int i = 0; i + 1 < kSfiDepth; ++i) kr[i] = src < 64 ? sh[i] : sh[i + 1];
             }
-            kn2 = j0 + 16 < nq ? run_keys(j0 + 16) : kNoKey;
+            kr[kSfiDepth - 1] = j0 + 8 * (kSfiDepth - 1) < nq ? run_keys(j0 + 8 * (kSfiDepth - 1)) : kNoKey;
         }
 #else
         int nm = 0, hreg = 0;   // lane b: the rotation histogram's bin b
@@ -938,7 +965,7 @@ constexpr size_t kLdsMax = 160 * 1024;
 // Frames up to ~18,000 keypoints (the resolve's 9 bytes of LDS a keypoint);
 // beyond that ORB_ERR_UNSUPPORTED before any launch.
 static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
-    const size_t lds_res = (size_t)a.cap * (4 + 4 + 1) + 128 + 16;
+    const size_t lds_res = ((size_t)a.cap * (4 + 4 + 1) + 128 + 15) / 16 * 16 + (size_t)kSfiStage * kTopK * 4;
     if (lds_res > kLdsMax) return ORB_ERR_UNSUPPORTED;
     if (a.cap > 65535) return ORB_ERR_UNSUPPORTED;   // 16-bit feature fields of the keys and the state
     // staged form; a block whose F2 level-0 list is longer than its
