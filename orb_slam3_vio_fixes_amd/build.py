@@ -18,8 +18,9 @@ DEPS = SOURCES + ["common.h", "orb_math.h", "plan.h", "brief_pattern.inc"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wno-unused-result"]
-# (-mllvm -amdgpu-mfma-vgpr-form, MFMA results in VGPRs, was measured wrong:
-# 5 of 7 C5 parity tests failed with it on this compiler, all pass without)
+# (MFMA accumulators live in VGPRs, the compiler's own choice: round 2's C5
+# failures in that form came from an inline-asm key reading an accumulator
+# the hazard recognizer could not see, fixed in round 3)
 
 
 def stale() -> bool:
