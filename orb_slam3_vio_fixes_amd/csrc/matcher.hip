@@ -626,8 +626,42 @@ constexpr int kSfiDepth = ORB_SFI_DEPTH;
 #define ORB_SFI_STAGE 256   // queries whose top-K keys are staged in LDS before the walk (32 B each)
 #endif
 constexpr int kSfiStage = ORB_SFI_STAGE;
+#ifndef ORB_SFI_STAGE2
+#define ORB_SFI_STAGE2 256  // F2 level-0 list entries staged in LDS for the exact rescans (44 B each)
+#endif
+constexpr int kSfiStage2 = ORB_SFI_STAGE2;
+// LDS of k_sfi_resolve: the state (9 B a keypoint), the staged keys, the
+// staged F2 list (entry, position, descriptor)
+__host__ __device__ inline size_t sfi_lds_base(int cap) { return ((size_t)cap * 9 + 128 + 15) / 16 * 16; }
+__host__ __device__ inline size_t sfi_lds_bytes(int cap) {
+    return sfi_lds_base(cap) + (size_t)kSfiStage * kTopK * 4 + (size_t)kSfiStage2 * (32 + 8 + 4);
+}
 static_assert(kSfiDepth >= 2, "the current run and at least one in flight");
 constexpr uint32_t kMdNone = 0xffff0000u;    // md21: no match yet (distance field 0xffff)
+#ifdef ORB_SFI_COUNT
+// walk statistics (tools/sfi_counts.py): rounds, rounds that committed fewer
+// than 8 queries, exact rescans, queries, committed claims
+__device__ unsigned long long g_sfi_cnt[8];
+extern "C" int orbm_debug_sfi_counts(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sfi_cnt), sizeof(g_sfi_cnt)) != hipSuccess) return -4;
+    if (reset) {
+        static unsigned long long z[8];
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sfi_cnt), z, sizeof(z)) != hipSuccess) return -4;
+    }
+    return 0;
+}
+#define SFI_CNT(k, v) do { if (lane == 0) atomicAdd(&g_sfi_cnt[k], (unsigned long long)(v)); } while (0)
+#else
+#define SFI_CNT(k, v) do { } while (0)
+#endif
+// minimum over each aligned group of 8 lanes, in every lane of the group:
+// quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
+__device__ __forceinline__ uint32_t grp8_min(uint32_t v) {
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xf, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4E, 0xf, 0xf, false));
+    v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
+    return v;
+}
 __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
@@ -647,7 +681,10 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     int8_t* bin1 = (int8_t*)(qlist + a.cap);      // cap
     // the first kSfiStage queries' keys (staged by all four waves before the
     // walk: the walk then does no global load for them)
-    uint32_t* skeys = (uint32_t*)(lds + ((a.cap * 9 + 128 + 15) >> 2 & ~3));
+    uint32_t* skeys = (uint32_t*)((uint8_t*)lds + sfi_lds_base(a.cap));
+    uint4* s2desc = (uint4*)(skeys + kSfiStage * kTopK);          // [kSfiStage2][2]
+    float2* s2xy = (float2*)(s2desc + 2 * kSfiStage2);             // [kSfiStage2]
+    int* s2list = (int*)(s2xy + kSfiStage2);                       // [kSfiStage2]
     int32_t* m12 = a.matches + (long long)pr * a.cap;
     const int* list = (const int*)(a.gsorted + (long long)f2 * a.cap);
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
@@ -675,10 +712,23 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         if (lane == 0) hist[31] = nq;                // (hist[31] is zeroed again below)
     }
     __syncthreads();
-    const int nq = hist[31];
+#ifndef ORB_SFI_ABL
+#define ORB_SFI_ABL 0   // timing ablation (tools only; wrong results): 1 = no walk
+#endif
+    const int nq = ORB_SFI_ABL == 1 ? 0 : hist[31];
     const int nst = min(nq, kSfiStage);
     for (int e = tid; e < nst * kTopK; e += kSfiThreads)
         skeys[e] = topk[(long long)(qlist[e / kTopK] & 0x7fffffff) * kTopK + e % kTopK];
+    // F2's level-0 list for the exact rescans (entry, position, descriptor):
+    // a rescan then reads LDS, not three dependent global loads per candidate
+    const int nl2 = min(nl, kSfiStage2);
+    for (int e = tid; e < nl2; e += kSfiThreads) {
+        const int v = list[e], fi = v & 0xffff;
+        s2list[e] = v;
+        s2xy[e] = make_float2(K2[fi].x, K2[fi].y);
+        s2desc[2 * e] = *(const uint4*)(D2 + (long long)fi * 32);
+        s2desc[2 * e + 1] = *(const uint4*)(D2 + (long long)fi * 32 + 16);
+    }
     __syncthreads();
     if (tid == 0) hist[31] = 0;
     if (tid < kWave) {
@@ -704,6 +754,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         int nm = 0;
         const float r = a.window;
         const int grp = lane >> 3, kk = lane & 7;
+        SFI_CNT(3, nq);
         auto run_keys = [&](int j0) -> uint32_t {
             const int j = j0 + grp;
             return j < nst ? skeys[j * kTopK + kk]
@@ -728,17 +779,20 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             const int kfi = kval ? (int)(kcur & 0xffffu) : 0;
             const uint32_t st = md21[kfi];
             const bool live = kval && !((int)(st >> 16) <= kd);
-            const uint64_t m = __ballot(live);
-            const uint32_t gm = (uint32_t)(m >> (8 * grp)) & 0xffu;
-            const uint32_t gm2 = gm & (gm - 1);
-            const int p1 = gm ? __ffs(gm) - 1 : 8, p2 = gm2 ? __ffs(gm2) - 1 : 8;
-            const bool ok = __popc(gm) >= 2 || !many;
-            const int sl1 = 8 * grp + min(p1, 7), sl2 = 8 * grp + min(p2, 7);
-            const int best = p1 < 8 ? __shfl(kd, sl1, kWave) : INT_MAX;
-            const int bi = __shfl(kfi, sl1, kWave);
-            const uint32_t stb = (uint32_t)__shfl((int)st, sl1, kWave);
-            const uint32_t kb = (uint32_t)__shfl((int)kcur, sl1, kWave);
-            const int best2 = p2 < 8 ? __shfl(kd, sl2, kWave) : INT_MAX;
+            // the query's first two live entries by 8-lane DPP minima of
+            // (entry | distance | F2 feature) words (no LDS-routed shuffle):
+            // the winner's fields and state reach every lane of its group
+            const uint32_t wl = live ? ((uint32_t)kk << 25) | ((uint32_t)kd << 16) | (uint32_t)kfi : 0xffffffffu;
+            const uint32_t w1 = grp8_min(wl);
+            const int p1 = w1 == 0xffffffffu ? 8 : (int)(w1 >> 25);
+            const uint32_t w2 = grp8_min(kk != p1 ? wl : 0xffffffffu);
+            const int p2 = w2 == 0xffffffffu ? 8 : (int)(w2 >> 25);
+            const bool ok = p2 < 8 || !many;
+            const int best = p1 < 8 ? (int)((w1 >> 16) & 0x1ffu) : INT_MAX;
+            const int bi = (int)(w1 & 0xffffu);
+            const uint32_t stb = grp8_min(kk == p1 ? st : 0xffffffffu);
+            const uint32_t kb = grp8_min(kk == p1 ? kcur : 0xffffffffu);
+            const int best2 = p2 < 8 ? (int)((w2 >> 16) & 0x1ffu) : INT_MAX;
             const bool acc = ok && grp < nrun && best <= kThLow && (float)best < (float)best2 * a.ratio;
             // an earlier claim on an entry this query's decision reads stops it
             const bool reads = kval && kk <= p2;
@@ -785,7 +839,19 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 for (int base = 0; base < nl; base += kWave) {
                     const int jj = base + lane;
                     int d = INT_MAX, fi = -1;
-                    if (jj < nl) {
+                    if (jj < nl2) {                            // the staged part of the list
+                        const int v = s2list[jj];
+                        const int cell = v >> 16, gx = cell / kGridRows, gy = cell - gx * kGridRows;
+                        fi = v & 0xffff;
+                        const float2 xy = s2xy[jj];
+                        if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1 && fabsf(xy.x - px) < r &&
+                            fabsf(xy.y - py) < r) {
+                            const uint4 b0 = s2desc[2 * jj], b1 = s2desc[2 * jj + 1];
+                            d = __popc(d0.x ^ b0.x) + __popc(d0.y ^ b0.y) + __popc(d0.z ^ b0.z) + __popc(d0.w ^ b0.w) +
+                                __popc(d1.x ^ b1.x) + __popc(d1.y ^ b1.y) + __popc(d1.z ^ b1.z) + __popc(d1.w ^ b1.w);
+                        }
+                        if (d != INT_MAX && (int)(md21[fi] >> 16) <= d) d = INT_MAX;
+                    } else if (jj < nl) {
                         d = cand_dist(list, jj, cr, px, py, r, K2, D2, d0, d1);
                         fi = list[jj] & 0xffff;
                         if (d != INT_MAX && (int)(md21[fi] >> 16) <= d) d = INT_MAX;
@@ -810,6 +876,10 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 }
                 adv = P + 1;
             }
+            SFI_CNT(0, 1);
+            SFI_CNT(1, adv < min(8, nrun));
+            SFI_CNT(2, P < nrun && __builtin_amdgcn_readlane((int)ok, 8 * P) == 0);
+            SFI_CNT(4, __popcll(__ballot(commit)));
             j0 += adv;
             // the next runs' keys: shifted by the queries done (a whole run in
             // the usual case), the run after them loaded
@@ -962,10 +1032,10 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
 
 constexpr size_t kLdsMax = 160 * 1024;
 
-// Frames up to ~18,000 keypoints (the resolve's 9 bytes of LDS a keypoint);
+// Frames up to ~15,600 keypoints (the resolve's 9 bytes of LDS a keypoint and its ~19 KB of staging);
 // beyond that ORB_ERR_UNSUPPORTED before any launch.
 static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
-    const size_t lds_res = ((size_t)a.cap * (4 + 4 + 1) + 128 + 15) / 16 * 16 + (size_t)kSfiStage * kTopK * 4;
+    const size_t lds_res = sfi_lds_bytes(a.cap);
     if (lds_res > kLdsMax) return ORB_ERR_UNSUPPORTED;
     if (a.cap > 65535) return ORB_ERR_UNSUPPORTED;   // 16-bit feature fields of the keys and the state
     // staged form; a block whose F2 level-0 list is longer than its
