@@ -662,6 +662,11 @@ __device__ __forceinline__ uint32_t grp8_min(uint32_t v) {
     v = min(v, (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x141, 0xf, 0xf, false));
     return v;
 }
+// M12L: the F1 -> F2 matches live in LDS during the walk and go out once,
+// coalesced, at the end (a global store in the walk made the next step wait
+// for it: gfx9 counts stores in vmcnt, and the compiler's waits at the loop
+// head drained them every step)
+template <bool M12L>
 __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
@@ -685,7 +690,8 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     uint4* s2desc = (uint4*)(skeys + kSfiStage * kTopK);          // [kSfiStage2][2]
     float2* s2xy = (float2*)(s2desc + 2 * kSfiStage2);             // [kSfiStage2]
     int* s2list = (int*)(s2xy + kSfiStage2);                       // [kSfiStage2]
-    int32_t* m12 = a.matches + (long long)pr * a.cap;
+    int32_t* const m12g = a.matches + (long long)pr * a.cap;
+    int32_t* m12 = M12L ? (int32_t*)(s2list + kSfiStage2) : m12g;   // [cap] in LDS (M12L)
     const int* list = (const int*)(a.gsorted + (long long)f2 * a.cap);
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
     const int* ncand = a.ncand + (long long)pr * a.cap;
@@ -755,8 +761,13 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         const float r = a.window;
         const int grp = lane >> 3, kk = lane & 7;
         SFI_CNT(3, nq);
+        // the walk in two instantiations: every query's keys staged (no global
+        // load in the loop at all, so no wait at its head drains one), or not
+        auto walk = [&](auto all_staged_c) {
+        constexpr bool kAllStaged = decltype(all_staged_c)::value;
         auto run_keys = [&](int j0) -> uint32_t {
             const int j = j0 + grp;
+            if constexpr (kAllStaged) return j < nq ? skeys[j * kTopK + kk] : kNoKey;
             return j < nst ? skeys[j * kTopK + kk]
                            : (j < nq ? topk[(long long)(qlist[j] & 0x7fffffff) * kTopK + kk] : kNoKey);
         };
@@ -777,53 +788,71 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             const bool kval = kcur != kNoKey;
             const int kd = (int)((kcur >> 16) & 0x1ffu);
             const int kfi = kval ? (int)(kcur & 0xffffu) : 0;
-            const uint32_t st = md21[kfi];
-            const bool live = kval && !((int)(st >> 16) <= kd);
-            // the query's first two live entries by 8-lane DPP minima of
-            // (entry | distance | F2 feature) words (no LDS-routed shuffle):
-            // the winner's fields and state reach every lane of its group
-            const uint32_t wl = live ? ((uint32_t)kk << 25) | ((uint32_t)kd << 16) | (uint32_t)kfi : 0xffffffffu;
-            const uint32_t w1 = grp8_min(wl);
-            const int p1 = w1 == 0xffffffffu ? 8 : (int)(w1 >> 25);
-            const uint32_t w2 = grp8_min(kk != p1 ? wl : 0xffffffffu);
-            const int p2 = w2 == 0xffffffffu ? 8 : (int)(w2 >> 25);
-            const bool ok = p2 < 8 || !many;
-            const int best = p1 < 8 ? (int)((w1 >> 16) & 0x1ffu) : INT_MAX;
-            const int bi = (int)(w1 & 0xffffu);
-            const uint32_t stb = grp8_min(kk == p1 ? st : 0xffffffffu);
-            const uint32_t kb = grp8_min(kk == p1 ? kcur : 0xffffffffu);
-            const int best2 = p2 < 8 ? (int)((w2 >> 16) & 0x1ffu) : INT_MAX;
-            const bool acc = ok && grp < nrun && best <= kThLow && (float)best < (float)best2 * a.ratio;
-            // an earlier claim on an entry this query's decision reads stops it
-            const bool reads = kval && kk <= p2;
-            uint64_t confl = 0;
-            for (uint64_t am = __ballot(acc && kk == 0); am; am &= am - 1) {
-                const int l = __ffsll((long long)am) - 1;           // lane 8t' of a claiming query
-                const int cb = __builtin_amdgcn_readlane(bi, l);
-                confl |= __ballot(reads && kfi == cb && lane >= l + 8);
-            }
-            const bool stop = ((confl >> (8 * grp)) & 0xffull) != 0 || !ok || grp >= nrun;
-            const uint64_t sm = __ballot(stop && kk == 0);
-            const int P = sm ? (__ffsll((long long)sm) - 1) >> 3 : 8;
-            const bool commit = acc && grp < P && kk == 0;
             const int i1 = qe & 0x7fffffff;
-            const int prev = (int)(stb & 0xffffu) - 1;
-            if (commit) {
-                if (prev >= 0) m12[prev] = -1;
-                m12[i1] = bi;
-                md21[bi] = ((uint32_t)best << 16) | (uint32_t)(i1 + 1);
-                if (a.check_ori) {
-                    bin1[i1] = (int8_t)(kb >> 25);
-                    atomicAdd(&hist[kb >> 25], 1);
+            uint32_t st = md21[kfi];
+            // queries t0.. of the run are undecided; after a committed prefix the
+            // lanes' states are brought up to date in registers and the rest of
+            // the run is decided again in place (no new state read, no key shift)
+            int t0 = 0, P = 0;
+            bool ok = true;
+            while (t0 < nrun) {
+                const bool active = grp >= t0 && grp < nrun;
+                const bool live = kval && !((int)(st >> 16) <= kd);
+                // the query's first two live entries by 8-lane DPP minima of
+                // (entry | distance | F2 feature) words (no LDS-routed shuffle):
+                // the winner's fields and state reach every lane of its group
+                const uint32_t wl = live ? ((uint32_t)kk << 25) | ((uint32_t)kd << 16) | (uint32_t)kfi : 0xffffffffu;
+                const uint32_t w1 = grp8_min(wl);
+                const int p1 = w1 == 0xffffffffu ? 8 : (int)(w1 >> 25);
+                const uint32_t w2 = grp8_min(kk != p1 ? wl : 0xffffffffu);
+                const int p2 = w2 == 0xffffffffu ? 8 : (int)(w2 >> 25);
+                ok = p2 < 8 || !many;
+                const int best = p1 < 8 ? (int)((w1 >> 16) & 0x1ffu) : INT_MAX;
+                const int bi = (int)(w1 & 0xffffu);
+                const uint32_t stb = grp8_min(kk == p1 ? st : 0xffffffffu);
+                const uint32_t kb = grp8_min(kk == p1 ? kcur : 0xffffffffu);
+                const int best2 = p2 < 8 ? (int)((w2 >> 16) & 0x1ffu) : INT_MAX;
+                const bool acc = ok && active && best <= kThLow && (float)best < (float)best2 * a.ratio;
+                // an earlier claim on an entry this query's decision reads stops it
+                const bool reads = kval && kk <= p2;
+                uint64_t confl = 0;
+                for (uint64_t am = __ballot(acc && kk == 0); am; am &= am - 1) {
+                    const int l = __ffsll((long long)am) - 1;           // lane 8t' of a claiming query
+                    const int cb = __builtin_amdgcn_readlane(bi, l);
+                    confl |= __ballot(reads && kfi == cb && lane >= l + 8);
                 }
-            }
-            nm += __popcll(__ballot(commit)) - __popcll(__ballot(commit && prev >= 0));
-            // the next round reads the state these writes left (one wave: its
-            // LDS operations complete in order; the asm keeps the compiler from
-            // hoisting the next reads above the stores)
-            asm volatile("" ::: "memory");
-            int adv = P;
-            if (P < nrun && __builtin_amdgcn_readlane((int)ok, 8 * P) == 0) {
+                const bool stop = (active && (((confl >> (8 * grp)) & 0xffull) != 0 || !ok)) || grp >= nrun;
+                const uint64_t sm = __ballot(stop && kk == 0);
+                P = sm ? (__ffsll((long long)sm) - 1) >> 3 : 8;
+                const bool commit = acc && grp < P && kk == 0;
+                const int prev = (int)(stb & 0xffffu) - 1;
+                const uint32_t nst_v = ((uint32_t)best << 16) | (uint32_t)(i1 + 1);
+                if (commit) {
+                    if (prev >= 0) m12[prev] = -1;
+                    m12[i1] = bi;
+                    md21[bi] = nst_v;
+                    if (a.check_ori) {
+                        bin1[i1] = (int8_t)(kb >> 25);
+                        atomicAdd(&hist[kb >> 25], 1);
+                    }
+                }
+                const uint64_t cmask = __ballot(commit);
+                nm += __popcll(cmask) - __popcll(__ballot(commit && prev >= 0));
+                SFI_CNT(4, __popcll(cmask));
+                // the next reads see these writes (one wave: its LDS operations
+                // complete in order; the asm keeps the compiler from hoisting
+                // later reads above the stores)
+                asm volatile("" ::: "memory");
+                if (P >= nrun) break;
+                // the committed claims into the lanes' states (what md21 now holds)
+                for (uint64_t cm = cmask; cm; cm &= cm - 1) {
+                    const int l = __ffsll((long long)cm) - 1;
+                    const int cb = __builtin_amdgcn_readlane(bi, l);
+                    const uint32_t cv = (uint32_t)__builtin_amdgcn_readlane((int)nst_v, l);
+                    st = kfi == cb ? cv : st;
+                }
+                t0 = P;
+                if (__builtin_amdgcn_readlane((int)ok, 8 * P) == 0) {
                 // query j0 + P cannot decide from its truncated list: exact
                 // full candidate scan under the state after the prefix
                 const int qx = __builtin_amdgcn_readlane(qe, 8 * P);
@@ -862,10 +891,11 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                     const int pv = (int)(md21[bs.idx] & 0xffffu) - 1;
                     if (pv >= 0) --nm;
                     ++nm;
+                    const uint32_t nv = ((uint32_t)bs.best << 16) | (uint32_t)(q1 + 1);
                     if (lane == 0) {
                         if (pv >= 0) m12[pv] = -1;
                         m12[q1] = bs.idx;
-                        md21[bs.idx] = ((uint32_t)bs.best << 16) | (uint32_t)(q1 + 1);
+                        md21[bs.idx] = nv;
                         if (a.check_ori) {
                             const int bn = rot_bin(k1.angle, K2[bs.idx].angle);
                             bin1[q1] = (int8_t)bn;
@@ -873,13 +903,20 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                         }
                     }
                     asm volatile("" ::: "memory");
+                    st = kfi == bs.idx ? nv : st;
                 }
-                adv = P + 1;
+                SFI_CNT(2, 1);
+                t0 = P + 1;
+                // drain the rescan's loads here (a rescan is rare): a load left
+                // pending on some path made the compiler wait for memory at the
+                // head of every step
+                __builtin_amdgcn_s_waitcnt(0);
+                }
+                SFI_CNT(1, 1);
             }
+            const int adv = nrun;
             SFI_CNT(0, 1);
-            SFI_CNT(1, adv < min(8, nrun));
-            SFI_CNT(2, P < nrun && __builtin_amdgcn_readlane((int)ok, 8 * P) == 0);
-            SFI_CNT(4, __popcll(__ballot(commit)));
+            (void)P; (void)ok;
             j0 += adv;
             // the next runs' keys: shifted by the queries done (a whole run in
             // the usual case), the run after them loaded
@@ -896,6 +933,9 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             }
             kr[kSfiDepth - 1] = j0 + 8 * (kSfiDepth - 1) < nq ? run_keys(j0 + 8 * (kSfiDepth - 1)) : kNoKey;
         }
+        };
+        if (nq <= kSfiStage) walk(std::true_type{});
+        else walk(std::false_type{});
 #else
         int nm = 0, hreg = 0;   // lane b: the rotation histogram's bin b
         const float r = a.window;
@@ -1027,6 +1067,8 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
             a.prev_out[((long long)pr * a.cap + i) * 2 + 1] = py;
         }
     }
+    if (M12L)
+        for (int i = tid; i < n1; i += kSfiThreads) m12g[i] = m12[i];
     if (tid == 0) a.nmatches[pr] = nm;
 }
 
@@ -1042,7 +1084,11 @@ static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     // registers take runs the per-lane form from global memory
     KLAUNCH(k_sfi_topk_st, dim3(npairs, (a.cap + kStQ - 1) / kStQ), dim3(256),
             (size_t)kStIt * kWave * (32 + 8 + 4 + 4), st, a);
-    KLAUNCH(k_sfi_resolve, dim3(npairs), dim3(kSfiThreads), lds_res, st, a);
+    const size_t lds_m12 = lds_res + (size_t)a.cap * 4;
+    if (lds_m12 <= kLdsMax)
+        KLAUNCH(k_sfi_resolve<true>, dim3(npairs), dim3(kSfiThreads), lds_m12, st, a);
+    else
+        KLAUNCH(k_sfi_resolve<false>, dim3(npairs), dim3(kSfiThreads), lds_res, st, a);
     return ORB_OK;
 }
 

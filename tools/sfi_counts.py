@@ -33,7 +33,7 @@ def main():
     torch.cuda.synchronize()
     L.orbm_debug_sfi_counts(out.ctypes.data, 0)
     pairs = B - 1
-    print(f"pairs {pairs}: queries {out[3] / pairs:.1f}, rounds {out[0] / pairs:.1f}, partial rounds "
+    print(f"pairs {pairs}: queries {out[3] / pairs:.1f}, rounds {out[0] / pairs:.1f}, continuations "
           f"{out[1] / pairs:.1f}, rescans {out[2] / pairs:.2f}, claims {out[4] / pairs:.1f} per pair; "
           f"nmatches mean {nm.float().mean().item():.1f}")
 
