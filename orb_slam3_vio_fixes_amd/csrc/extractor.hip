@@ -1525,7 +1525,9 @@ __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
         const uint32_t r = (uint32_t)min(lane / PDW + j * (kWave / PDW), rf.rows - 1);
-        if (RP) roi[r * RP + d] = v[j];
+        // (r * RP by v_mad_u32_u24: the compiler's r * RP was a quarter-rate
+        // v_mul_lo_u32 per landed dword, r being a min() it cannot bound)
+        if (RP) roi[mad24(r, (uint32_t)RP, d)] = v[j];
         else roi[mad24(r, (uint32_t)rf.nd, d)] = v[j];
     }
 }
@@ -1659,7 +1661,10 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         const int ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
         const int ndp = (ndw + 1) >> 1;                   // items: pairs of aligned dwords
         const int nitems = wh * ndp;
-        const float inv_ndp = ndp ? 1.0f / (float)ndp : 0.f;
+        // (an approximate reciprocal is exact here: (i + 0.5) / ndp < wh lies
+        // >= 1 / (2 ndp) from an integer, while v_rcp's 1 ulp and the product's
+        // rounding err by < wh * 2^-21, smaller whenever nitems < 2^20)
+        const float inv_ndp = ndp ? __builtin_amdgcn_rcpf((float)ndp) : 0.f;
         const uint32_t* roi32 = (const uint32_t*)roi;
         const int rs4 = rstride >> 2;
         // byte-flag masks of the first and the last item of a row (the only
