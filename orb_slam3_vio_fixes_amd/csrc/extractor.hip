@@ -2919,12 +2919,37 @@ __device__ __forceinline__ void patch_land(const uint32_t (&v)[kPV], uint8_t* ra
     }
 }
 
+#ifndef ORB_DESC_BORDER_BATCH
+#define ORB_DESC_BORDER_BATCH 10   // reflected byte loads in flight per lane (0: the round-3 loop, one at a time)
+#endif
 __device__ __forceinline__ void patch_border(const uint8_t* img, int pitch, int w, int h, int x0, int y0,
                                              uint8_t* raw) {
+#if ORB_DESC_BORDER_BATCH
+    // 29 bytes per lane in batches whose loads are all in flight before the
+    // first LDS store (one memory round trip per batch, not per byte)
+    constexpr int kB = ORB_DESC_BORDER_BATCH, kN = (kRaw * kRaw + kWave - 1) / kWave;
+    const int lane = lane_id();
+#pragma unroll 1
+    for (int j0 = 0; j0 < kN; j0 += kB) {   // (rolled: unrolled, the lane-invariant offsets get hoisted out of the keypoint loop and spill)
+        uint32_t v[kB];
+        int o[kB];
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            const int i = min(lane + (j0 + j) * kWave, kRaw * kRaw - 1);   // past the patch: repeats its last byte
+            const int r = i / kRaw, c = i - r * kRaw;
+            o[j] = r * kRawP + c;
+            v[j] = (j0 + j < kN) ? ((GlobalBytes)img)[(long long)refl101(y0 + r, h) * pitch + refl101(x0 + c, w)] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < kB; ++j)
+            if (j0 + j < kN) raw[o[j]] = (uint8_t)v[j];
+    }
+#else
     for (int i = lane_id(); i < kRaw * kRaw; i += kWave) {
         const int r = i / kRaw, c = i - r * kRaw;
         raw[r * kRawP + c] = ((GlobalBytes)img)[(long long)refl101(y0 + r, h) * pitch + refl101(x0 + c, w)];
     }
+#endif
 }
 
 #ifdef ORB_DESC_TIMING
