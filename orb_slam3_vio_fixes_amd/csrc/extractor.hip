@@ -1258,6 +1258,7 @@ struct FastArgs {
     const LevelDev* lv;
     const CellDev* cells;
     int ncells;
+    int cell_begin, cell_end;   // this launch's range of every frame's cells (a level range)
     int nframes;
     int* cell_count;        // [B][ncells]
     uint32_t* cell_keys;    // [B][slot_total]
@@ -1472,6 +1473,15 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #ifndef ORB_FAST_RESET
 #define ORB_FAST_RESET 0   // 1: score map zeroed once per wave, each cell resets its own entries (measured slower: 0.418-0.420 vs 0.408-0.413 ms)
 #endif
+#ifndef ORB_FAST_ILIST_IN_MAP
+// the pre-test's item list lives in the score map's bytes (the list is read
+// out before the map is zeroed and scored; 1 KB less LDS a wave at 752x480,
+// 16 -> 18 waves a CU)
+#define ORB_FAST_ILIST_IN_MAP 1
+#endif
+#if ORB_FAST_ILIST_IN_MAP && ORB_FAST_RESET
+#error "ORB_FAST_RESET keeps the score map zero between cells: the item list cannot live in it"
+#endif
 #ifndef ORB_FAST_PIPE
 #define ORB_FAST_PIPE 0   // 1: pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
 #endif
@@ -1575,7 +1585,8 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     uint8_t* sc = roi + a.roi_max;                            // padded score map, <= win_max bytes
     uint16_t* cand = (uint16_t*)(sc + a.win_max);             // <= win_pix_max entries
     uint64_t* kmask = (uint64_t*)(sc + a.win_max + a.cand_bytes);   // NMS ballots, one per 64 candidates
-    uint32_t* ilist = (uint32_t*)(sc + a.win_max + a.cand_bytes + a.kmask_bytes);   // items holding candidates
+    uint32_t* ilist = ORB_FAST_ILIST_IN_MAP ? (uint32_t*)sc   // items holding candidates
+                                            : (uint32_t*)(sc + a.win_max + a.cand_bytes + a.kmask_bytes);
 #ifdef ORB_FAST_TIMING
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
 #endif
@@ -1584,9 +1595,9 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
     xcd_remap((int)gridDim.x, (int)gridDim.y, bunit, bframe);
     bunit = __builtin_amdgcn_readfirstlane(bunit);
     bframe = __builtin_amdgcn_readfirstlane(bframe);
-    const int c_begin = (bunit * kFastWpb + wv) * kCellsPerWave;
+    const int c_begin = a.cell_begin + (bunit * kFastWpb + wv) * kCellsPerWave;
     const int it0 = bframe * a.ncells + c_begin, step = 1;
-    const int it_end = bframe * a.ncells + min(c_begin + kCellsPerWave, a.ncells);
+    const int it_end = bframe * a.ncells + min(c_begin + kCellsPerWave, a.cell_end);
     // the plan tables are read-only here: constant address space -> scalar loads
     typedef __attribute__((address_space(4))) const LevelDev* ConstLevels;
     typedef __attribute__((address_space(4))) const CellDev* ConstCells;
@@ -1650,7 +1661,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         const int sp = ww + 2, npad = sp * (wh + 2);
 #if ORB_FAST_RESET
         (void)npad;   // the map is all zero here: zeroed once, and each cell resets the entries it wrote
-#else
+#elif !ORB_FAST_ILIST_IN_MAP
         // 16 bytes per lane per store (sc is 16-byte aligned, win_max a multiple of 16)
         for (int i = lane; i < (npad + 15) / 16; i += kWave) ((uint4*)sc)[i] = make_uint4(0u, 0u, 0u, 0u);
         fast_wave_sync();
@@ -1969,6 +1980,13 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 ncand = n2;
                 fast_wave_sync();
             }
+#endif
+#if ORB_FAST_ILIST_IN_MAP
+            // the map zeroed here, over the item list, in each pass: the minThFAST
+            // pass rescores every pixel the first pass scored (its candidates are
+            // a superset), so nothing of the first pass's map is needed
+            for (int i = lane; i < (npad + 15) / 16; i += kWave) ((uint4*)sc)[i] = make_uint4(0u, 0u, 0u, 0u);
+            fast_wave_sync();
 #endif
             // 2. FAST score of the candidates (the dark direction too for the rare
             //    pixels passing both pre-tests).  ORB_FAST_KEEPLIST: the list
@@ -3559,6 +3577,66 @@ static void qt_lds_split(const Plan& P, size_t& lds, size_t& gstride) {
 // Frames [f0, f0+B) of the batch: every per-frame work buffer is addressed
 // through pointers offset by f0, so disjoint frame ranges can run on separate
 // streams without sharing scratch.
+// k_fast_cells launch geometry of a range of every frame's cells
+struct FastGroup {
+    int roi_max = 0, rows_max = 0, nd_max = 0, win_max = 0, win_pix_max = 0, item_max = 0;
+};
+static FastGroup fast_group(const Plan& P, int cb, int ce) {
+    FastGroup G;
+    for (int i = cb; i < ce; ++i) {
+        const CellDev& c = P.cells[i];
+        const int nd = ((c.x0 & 3) + c.cols + 3) >> 2, ww = std::max(0, c.cols - 6), wh = std::max(0, c.rows - 6);
+        // + 16: the pre-test reads up to 2 dwords past the last row's window
+        G.roi_max = std::max(G.roi_max, 4 * c.rows * nd + 16);
+        G.rows_max = std::max(G.rows_max, c.rows);
+        G.nd_max = std::max(G.nd_max, nd);
+        G.win_max = std::max(G.win_max, (ww + 2) * (wh + 2));
+        G.win_pix_max = std::max(G.win_pix_max, ww * wh);
+        const int X0 = (c.x0 & 3) + 3, j0 = X0 >> 2, ndw = ww ? ((X0 + ww - 1) >> 2) - j0 + 1 : 0;
+        G.item_max = std::max(G.item_max, wh * ((ndw + 1) >> 1));
+    }
+    return G;
+}
+// fetch row width (dwords) and loads per lane: <16, 12> takes ROIs of at most
+// 16 dwords by 48 rows (W = 35 cells are < 70 px: nd <= 19 and rows < 76
+// always fit <32, 40>); rp: the fixed LDS pitch of the ROIs (dwords), 0: per cell
+static void (*fast_kernel(const FastGroup& G, bool bm, int& rp))(FastArgs) {
+    const int ndm = G.nd_max, rm = G.rows_max;
+    rp = 0;
+#if ORB_FAST_FIXED_PITCH
+    if (ndm <= 11 && rm <= 64) {
+        rp = 11;
+        return rm <= 48 ? (bm ? k_fast_cells<16, 12, 11, true> : k_fast_cells<16, 12, 11, false>)
+                        : (bm ? k_fast_cells<16, 16, 11, true> : k_fast_cells<16, 16, 11, false>);
+    }
+    if (ndm <= 13 && rm <= 64) {
+        rp = 13;
+        return rm <= 48 ? (bm ? k_fast_cells<16, 12, 13, true> : k_fast_cells<16, 12, 13, false>)
+                        : (bm ? k_fast_cells<16, 16, 13, true> : k_fast_cells<16, 16, 13, false>);
+    }
+#endif
+    if (ndm <= 16 && rm <= 48) return bm ? k_fast_cells<16, 12, 0, true> : k_fast_cells<16, 12, 0, false>;
+    if (ndm <= 16 && rm <= 64) return bm ? k_fast_cells<16, 16, 0, true> : k_fast_cells<16, 16, 0, false>;
+    if (ndm <= 16 && rm <= 80) return k_fast_cells<16, 20, 0, false>;
+    if (ndm <= 32 && rm <= 48) return k_fast_cells<32, 24, 0, false>;
+    if (ndm <= 32 && rm <= 80) return k_fast_cells<32, 40, 0, false>;
+    return nullptr;
+}
+static void fast_lds_layout(const FastGroup& G, int rp, FastArgs& fa) {
+    fa.roi_max = (std::max(G.roi_max, 4 * G.rows_max * rp + 16) + 15) & ~15;
+    const int il = ORB_FAST_EMIT == 1 ? (4 * G.item_max + 15) & ~15 : 0;
+    fa.win_max = (std::max(G.win_max, ORB_FAST_ILIST_IN_MAP ? il : 0) + 15) & ~15;
+    // NMS ballots only for the separate output pass
+    fa.kmask_bytes = ORB_FAST_FUSED_OUT ? 0 : ((G.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
+    fa.cand_bytes = (2 * G.win_pix_max + 15) & ~15;
+    fa.ilist_bytes = ORB_FAST_ILIST_IN_MAP ? 0 : il;
+}
+static size_t fast_wave_lds(const FastArgs& fa) {
+    return (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes + fa.ilist_bytes);
+}
+#ifndef ORB_FAST_LDS_PAD
+#define ORB_FAST_LDS_PAD 0   // occupancy probe (tools only): extra LDS per block
+#endif
 static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames, long long fstride, int pitch0,
                         float lap0, float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n,
                         int32_t* d_mono, hipStream_t st) {
@@ -3659,45 +3737,32 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.cell_count = P.d_cell_count; fa.cell_keys = P.d_cell_keys; fa.slot_total = P.slot_total;
     fa.ini_th = std::min(std::max(hd->prm.ini_th_fast, 0), 255);
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
-    // fetch row width (dwords) and loads per lane: <16, 12> takes ROIs of at
-    // most 16 dwords by 48 rows (W = 35 cells are < 70 px: nd <= 19 and rows <
-    // 76 always fit <32, 40>)
-    void (*kfast)(FastArgs) = nullptr;
-    const int ndm = P.roi_nd_max, rm = P.roi_rows_max;
-    int rp = 0;    // fixed LDS pitch of the ROIs (dwords), 0: per cell
     // the iniThFAST candidates come from k_pyr_stream's fused pre-test when it
     // ran (BM forms); otherwise k_fast_cells pre-tests the landed ROI itself
     const bool bm = use_stream && P0.ps.pretest && P.d_bm;
     hd->bm_last = bm;
     fa.bm = bm ? P.d_bm : nullptr;
     fa.bm_fstride = P0.bm_bytes;
-#if ORB_FAST_FIXED_PITCH
-    if (ndm <= 11 && rm <= 64) {
-        kfast = rm <= 48 ? (bm ? k_fast_cells<16, 12, 11, true> : k_fast_cells<16, 12, 11, false>)
-                         : (bm ? k_fast_cells<16, 16, 11, true> : k_fast_cells<16, 16, 11, false>);
-        rp = 11;
-    } else if (ndm <= 13 && rm <= 64) {
-        kfast = rm <= 48 ? (bm ? k_fast_cells<16, 12, 13, true> : k_fast_cells<16, 12, 13, false>)
-                         : (bm ? k_fast_cells<16, 16, 13, true> : k_fast_cells<16, 16, 13, false>);
-        rp = 13;
-    } else
-#endif
-    if (ndm <= 16 && rm <= 48) kfast = bm ? k_fast_cells<16, 12, 0, true> : k_fast_cells<16, 12, 0, false>;
-    else if (ndm <= 16 && rm <= 64) kfast = bm ? k_fast_cells<16, 16, 0, true> : k_fast_cells<16, 16, 0, false>;
-    else if (ndm <= 16 && rm <= 80) kfast = k_fast_cells<16, 20, 0, false>;
-    else if (ndm <= 32 && rm <= 48) kfast = k_fast_cells<32, 24, 0, false>;
-    else if (ndm <= 32 && rm <= 80) kfast = k_fast_cells<32, 40, 0, false>;
-    else return ORB_ERR_UNSUPPORTED;
-    fa.roi_max = (std::max(P0.roi_max, 4 * rm * rp + 16) + 15) & ~15;
-    fa.win_max = (P.win_max + 15) & ~15;
-    fa.kmask_bytes = ((P0.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
-    fa.cand_bytes = (2 * P0.win_pix_max + 15) & ~15;
-    fa.ilist_bytes = ORB_FAST_EMIT == 1 ? (4 * P0.item_max + 15) & ~15 : 0;
-    const size_t flds = kFastWpb * (size_t)(fa.roi_max + fa.win_max + fa.cand_bytes + fa.kmask_bytes + fa.ilist_bytes);
-    fa.nframes = B;
-    const dim3 fgrid((P.ncells + kFastWpb * kCellsPerWave - 1) / (kFastWpb * kCellsPerWave), B);
-    if (P.ncells > 0)                        // (every level under 67 px: no FAST cells at all)
-        hipLaunchKernelGGL(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
+    // A wave's LDS is sized for the largest cell of the plan and sets
+    // k_fast_cells' occupancy: 18 waves a CU at 752x480 (8.7 KB a wave; one
+    // wave less a SIMD costs 20 %).  Launching the tall-celled levels 5-7
+    // apart (the rest at 20 waves a CU) was measured: alone they are a 55 us
+    // tail, on a side stream their long waves slow the main launch
+    // (profiles/r04/fast_occupancy).
+    {
+        const FastGroup G = fast_group(P0, 0, P0.ncells);
+        int rp = 0;
+        void (*kfast)(FastArgs) = fast_kernel(G, bm, rp);
+        if (!kfast) return ORB_ERR_UNSUPPORTED;
+        fast_lds_layout(G, rp, fa);
+        fa.cell_begin = 0;
+        fa.cell_end = P0.ncells;
+        const size_t flds = fast_wave_lds(fa) * kFastWpb + ORB_FAST_LDS_PAD;
+        fa.nframes = B;
+        const dim3 fgrid((P0.ncells + kFastWpb * kCellsPerWave - 1) / (kFastWpb * kCellsPerWave), B);
+        if (P0.ncells > 0)                        // (every level under 67 px: no FAST cells at all)
+            hipLaunchKernelGGL(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
+    }
     mark();
     // quadtree
     QtArgs qa;
