@@ -1265,9 +1265,10 @@ struct FastArgs {
     int slot_total;
     int ini_th, min_th;
     int roi_max, win_max;   // LDS per wave
-    int kmask_bytes;
+    int kmask_bytes;        // NMS ballots of the separate output pass (0 with ORB_FAST_FUSED_OUT)
     int cand_bytes;         // u16 candidate list, one entry per window pixel at most
-    int ilist_bytes;        // u32 list of the pre-test items holding a candidate (ORB_FAST_EMIT 1)
+    int ilist_bytes;        // u32 list of the pre-test items holding a candidate (ORB_FAST_EMIT 1;
+                            // 0 with ORB_FAST_ILIST_IN_MAP: the list lives in the score map's bytes)
     const uint8_t* bm;      // k_pyr_stream's iniThFAST pre-test bitmaps of frame 0 (k_fast_cells<..., true>)
     long long bm_fstride;
 };
