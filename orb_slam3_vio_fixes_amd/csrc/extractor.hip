@@ -3575,9 +3575,6 @@ static void qt_lds_split(const Plan& P, size_t& lds, size_t& gstride) {
     }
 }
 
-// Frames [f0, f0+B) of the batch: every per-frame work buffer is addressed
-// through pointers offset by f0, so disjoint frame ranges can run on separate
-// streams without sharing scratch.
 // k_fast_cells launch geometry of a range of every frame's cells
 struct FastGroup {
     int roi_max = 0, rows_max = 0, nd_max = 0, win_max = 0, win_pix_max = 0, item_max = 0;
@@ -3638,6 +3635,9 @@ static size_t fast_wave_lds(const FastArgs& fa) {
 #ifndef ORB_FAST_LDS_PAD
 #define ORB_FAST_LDS_PAD 0   // occupancy probe (tools only): extra LDS per block
 #endif
+// Frames [f0, f0+B) of the batch: every per-frame work buffer is addressed
+// through pointers offset by f0, so disjoint frame ranges can run on separate
+// streams without sharing scratch.
 static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames, long long fstride, int pitch0,
                         float lap0, float lap1, orb_keypoint* d_kps, uint8_t* d_desc, int cap, int32_t* d_n,
                         int32_t* d_mono, hipStream_t st) {
@@ -3745,8 +3745,8 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.bm = bm ? P.d_bm : nullptr;
     fa.bm_fstride = P0.bm_bytes;
     // A wave's LDS is sized for the largest cell of the plan and sets
-    // k_fast_cells' occupancy: 18 waves a CU at 752x480 (8.7 KB a wave; one
-    // wave less a SIMD costs 20 %).  Launching the tall-celled levels 5-7
+    // k_fast_cells' occupancy: 17-18 waves a CU at 752x480 (8.7 KB a wave;
+    // 16 -> 14 -> 12 waves a CU cost 6 % and 21 %).  Launching the tall-celled levels 5-7
     // apart (the rest at 20 waves a CU) was measured: alone they are a 55 us
     // tail, on a side stream their long waves slow the main launch
     // (profiles/r04/fast_occupancy).
