@@ -1477,7 +1477,7 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #ifndef ORB_FAST_ILIST_IN_MAP
 // the pre-test's item list lives in the score map's bytes (the list is read
 // out before the map is zeroed and scored; 1 KB less LDS a wave at 752x480,
-// 16 -> 18 waves a CU)
+// 16 -> 17-18 waves a CU)
 #define ORB_FAST_ILIST_IN_MAP 1
 #endif
 #if ORB_FAST_ILIST_IN_MAP && ORB_FAST_RESET
