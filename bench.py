@@ -10,7 +10,10 @@ Infinity Cache), so no step reads the frames the step before it read:
 ORBextractor(1000, 1.2, 8, 20, 7) with vLappingArea {0, 1000} (Frame.cc:311)
 on every frame, then ORBmatcher(0.9, true).SearchForInitialization(F[t],
 F[t+1], prev = F[t] keypoints, window 100) on the B-1 consecutive pairs
-(Tracking.cc:2459-2492).  Steps are pipelined: the matching of step k runs
+(Tracking.cc:2459-2492).  Two steps are in flight (--overlap 2): consecutive steps alternate between two
+extractor handles on two streams, so step k+1's pyramid and FAST run beside
+step k's quadtree and describe, with four output sets in rotation.  Within
+that, the matching of step k runs
 on a second HIP stream while step k+1 extracts into a second output set,
 started once step k+1's extraction has passed its pyramid stage
 (orbx_set_stage_event; --sfi-after): its parallel top-K pass then runs beside
@@ -20,7 +23,11 @@ FAST and its latency-bound serial walk beside the quadtree and describe
 
 Extra objects on the JSON line:
   roofline     dominant kernel (k_fast_cells, the FAST pass) measured with HIP
-               events on the extraction stream over the timed steps;
+               events on the extraction stream over a profiled pass after the
+               timed region (--profile-steps, one step in flight: with two in
+               flight each kernel shares the GPU with the other step's, so its
+               launch time would not be its own; the timed steps carry no
+               events);
                algorithmic bytes = every pyramid pixel read once
                (sum_l w_l*h_l per frame) x frames per launch.
                traffic = HBM bytes per launch of the same kernel from the committed
@@ -71,7 +78,9 @@ DESC_BYTES_PER_KP = 43 * 43 + 4 + 32   # k_describe: raw 43x43 patch read; angle
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without WORLD_SIZE in the environment bench.py starts them itself "
+                         "under torch.distributed.run, with it WORLD_SIZE must equal --gpus")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=256, help="frames per step per GPU")
@@ -83,18 +92,21 @@ def parse():
                     help="threads of the CPU-baseline pool (0 = the cores this process may run on, at most 16)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
                     help="skip the PCIe-inclusive drop-in latency leg")
-    ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--no-profile", action="store_true", help="skip the profiled pass (no stage_ms / roofline)")
+    ap.add_argument("--profile-steps", type=int, default=10,
+                    help="steps of the profiled pass after the timed region: one step in flight, HIP events at "
+                         "every stage boundary (the roofline's per-kernel launch times)")
     ap.add_argument("--pmc-summary", default=str(PMC_SUMMARY), help="rocprofv3 PMC summary (tools/pmc_summary.py)")
     ap.add_argument("--no-pipeline", dest="pipeline", action="store_false",
                     help="run SearchForInitialization on the extraction stream (no step overlap)")
     ap.add_argument("--streams", type=int, default=1, help="sub-batch streams per extractor (orbx_set_streams)")
-    ap.add_argument("--overlap", type=int, default=1, choices=[1, 2],
+    ap.add_argument("--overlap", type=int, default=2, choices=[1, 2],
                     help="batches in flight: 2 = consecutive steps alternate between two extractor handles "
                          "(own plan and scratch each) on two streams, so step k+1 extracts beside step k")
     ap.add_argument("--sfi-after", type=int, default=1,
                     help="pipeline: step k's SearchForInitialization waits until step k+1's extraction has passed this "
                          "stage (orbx_set_stage_event: 1 pyramid (default), 2 FAST, 3 quadtree; -1: starts at once)")
-    ap.add_argument("--sets", type=int, default=2,
+    ap.add_argument("--sets", type=int, default=4,
                     help="pipeline: output sets in rotation (2: step k+2 waits for step k's matching; "
                          "--overlap 2 wants 4)")
     ap.add_argument("--match-prio", type=int, default=0,
@@ -319,6 +331,12 @@ def adapter_rates(img, reps):
 
 def main():
     args = parse()
+    # --gpus N without a launcher: start N ranks as one child process (no
+    # torch import, no GPU call in this process) and exit with its code
+    from orb_slam3_vio_fixes_amd import launch
+    rc = launch.ensure_ranks(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     if args.workload != "c2":
         res = other_workload(args)
         if res is not None:
@@ -419,9 +437,11 @@ def main():
         done[i] = torch.cuda.Event()
         done[i].record(mstream)
 
-    def step(timed=False):
+    def step(timed=False, handle=None):
         i = counter[0] % nsets
-        h = counter[0] % args.overlap                   # --overlap 2: consecutive steps alternate handles
+        # --overlap 2: consecutive steps alternate handles (the profiled pass
+        # pins handle 0: one step in flight)
+        h = counter[0] % args.overlap if handle is None else handle
         frames = ring[counter[0] % R]                   # a different input batch than the step before
         counter[0] += 1
         k_, d_, n_, m_ = outs[i]
@@ -453,21 +473,32 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    prof = not args.no_profile
-    if prof:
-        for e in exs:
-            L.orbx_set_profiling(e._h, 1)
+    # the timed steps carry no instrumentation: per-kernel times come from
+    # the profiled pass below
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(timed=prof)
-    flush(timed=prof)
+        step()
+    flush()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # profiled pass (after the timed region, not in `value`): --profile-steps
+    # more steps of the same pipeline at ONE step in flight (handle 0 only;
+    # step k's matching still beside step k+1's later stages), with HIP events
+    # at every stage boundary on the extraction stream, so each kernel's
+    # launch time is its own and not shared with the other handle's step
     stage_ms = np.zeros(len(STAGES), np.float32)
+    prof = not args.no_profile and args.profile_steps > 0
+    frames_per_launch = Bx
     if prof:
+        for e in exs:
+            L.orbx_set_profiling(e._h, 1)
+        for _ in range(args.profile_steps):
+            step(timed=True, handle=0)
+        flush(timed=True)
+        torch.cuda.synchronize()
         calls = 0
         for e in exs:
             sm = np.zeros(len(STAGES), np.float32)
@@ -475,9 +506,7 @@ def main():
             L.orbx_set_profiling(e._h, 0)
             stage_ms += sm
         stage_ms /= max(1, calls)
-        frames_per_launch = Bx * args.steps / max(1, calls)  # each sub-batch range is one launch per stage
-    else:
-        frames_per_launch = Bx
+        frames_per_launch = Bx * args.profile_steps / max(1, calls)  # each sub-batch range is one launch per stage
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -494,24 +523,35 @@ def main():
     if rank == 0:
         total_frames = B * args.steps * world
         value = total_frames / elapsed
-        px = level_pixels(ex)                          # algorithmic bytes per frame of the FAST pass
-        fast_ms = float(stage_ms[1])
-        achieved = (px * frames_per_launch / (fast_ms * 1e-3)) / 1e9 if fast_ms > 0 else None
-        pf = pmc_figures(pmc_row(args.pmc_summary, "k_fast_cells"), fast_ms, frames_per_launch)
-        traffic = pf.get("pmc_bytes_per_launch")
-        roof = {"kernel": "k_fast_cells", "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": (achieved / HBM_PEAK_GBS) if achieved else None, "traffic": traffic,
-                "bytes_per_launch": px * frames_per_launch, "ms_per_launch": fast_ms,
+        # the roofline names the longest extraction kernel with algorithmic
+        # bytes (the FAST pass or describe; stage_roofline has every stage)
+        sr = stage_roofline(ex, dict(zip(STAGES, map(float, stage_ms))), frames_per_launch,
+                            float(n.float().mean().item()), args.pmc_summary)
+        dom = max(("fast_cells", "describe"), key=lambda k_: sr.get(k_, {}).get("ms", 0.0))
+        d_ = sr.get(dom, {})
+        roof = {"kernel": STAGE_KERNEL[dom], "bound": "hbm", "achieved": d_.get("achieved_GBs"), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": d_.get("frac"), "traffic": d_.get("pmc_bytes_per_launch"),
+                "bytes_per_launch": d_.get("bytes_per_launch"), "ms_per_launch": d_.get("ms"),
                 "frames_per_launch": frames_per_launch,
-                "traffic_source": (os.path.relpath(args.pmc_summary, ROOT) if traffic else None),
-                "valu_roofline_frac": pf.get("valu_roofline_frac")}
+                "bytes_per_unit": ("sum of the pyramid level sizes per frame (every level pixel read once)"
+                                   if dom == "fast_cells" else
+                                   f"{DESC_BYTES_PER_KP} B per keypoint (43x43 raw patch read, angle + descriptor "
+                                   "written)"),
+                "traffic_source": (os.path.relpath(args.pmc_summary, ROOT) if d_.get("pmc_bytes_per_launch") else None),
+                "time_source": (f"HIP events on the extraction stream over a profiled pass of {args.profile_steps} "
+                                "steps after the timed region, one step in flight (the timed steps run "
+                                f"{args.overlap} in flight, uninstrumented)"),
+                "valu_roofline_frac": d_.get("valu_roofline_frac"),
+                "second": {k_: sr.get(k_, {}).get("frac") for k_ in ("fast_cells", "describe") if k_ != dom}}
         out = {"metric": METRIC, "value": value, "unit": "frames/s", "n_gpus": world, "steps": args.steps,
                "warmup": args.warmup, "ms_per_step": elapsed / args.steps * 1e3, "higher_is_better": True,
                "scaling": "weak", "vs_baseline": None, "dtype": "u8", "data": "synthetic",
                "config": {"workload": "C2: 752x480 mono, ORBextractor(1000,1.2,8,20,7), lapping {0,1000}, "
                                       "+ SearchForInitialization(window 100, 0.9, checkOri) on consecutive frames",
                           "frames_per_step_per_gpu": B, "input_ring_batches": R,
-                          "input_ring_MB": round(R * Bx * W * H / 2**20, 1), "streams": args.streams, "overlap": args.overlap, "pipeline": args.pipeline,
+                          "input_ring_MB": round(R * Bx * W * H / 2**20, 1), "streams": args.streams, "overlap": args.overlap,
+                          "steps_in_flight": args.overlap, "pipeline": args.pipeline,
+                          "profiled_pass_steps": args.profile_steps if prof else 0,
                           "sfi_after_stage": args.sfi_after if args.pipeline else None,
                           "output_sets": nsets if args.pipeline else 1,
                           "parallelism": f"frames sharded over {world} GPU(s), halo frame per seam"},
@@ -519,8 +559,7 @@ def main():
                             "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
                                                           if match_events else None)},
                "roofline": roof,
-               "stage_roofline": stage_roofline(ex, dict(zip(STAGES, map(float, stage_ms))), frames_per_launch,
-                                                float(n.float().mean().item()), args.pmc_summary)}
+               "stage_roofline": sr}
         if world == 1 and args.cpu_sample > 0:
             from oracle import oracle as O
             ns = min(args.cpu_sample, B)

@@ -4,6 +4,7 @@ ORB_BENCH_BACKEND=gloo) against 1 rank with the same total frames.  Every
 frame's keypoints/descriptors and every SearchForInitialization pair --
 including the pair across the shard seam, covered by the halo frame each
 rank but the last extracts -- must equal the 1-rank run."""
+import json
 import os
 import socket
 import subprocess
@@ -62,6 +63,37 @@ def test_two_ranks_equal_one_rank_with_seam_pair(tmp_path):
     assert pairs == 2 * B - 1            # every consecutive pair of the job, seam included
 
 
+def test_bench_gpus_2_launches_its_own_ranks(tmp_path):
+    """The driver's scaling form: `python bench.py --gpus 2` with NO launcher
+    around it.  bench.py starts the 2 ranks itself (orb_slam3_vio_fixes_amd/
+    launch.py), the JSON line reports n_gpus 2 and twice the per-rank frames,
+    and the two ranks' outputs equal a 1-rank run of the same frames."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT")}
+    env["ORB_BENCH_BACKEND"] = "gloo"       # two ranks share the box's one GPU
+    common = ["--steps", "1", "--warmup", "1", "--cpu-sample", "0", "--no-host-api", "--no-profile"]
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--batch", str(B), "--dump", str(tmp_path / "two")]
+                       + common, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    assert line["value"] == pytest.approx(2 * B * line["steps"] / (line["ms_per_step"] * line["steps"] * 1e-3))
+    _run([sys.executable, "bench.py", "--batch", str(2 * B), "--dump", str(tmp_path / "one")] + common, env)
+    one = np.load(tmp_path / "one" / "rank0.npz")
+    base = int(one["first"])
+    for rk in (0, 1):
+        r_ = np.load(tmp_path / "two" / f"rank{rk}.npz")
+        f0 = int(r_["first"]) - base
+        for i in range(int(r_["frames"])):
+            n = int(r_["n"][i])
+            assert n == int(one["n"][f0 + i])
+            assert np.array_equal(r_["kps"][i, :n], one["kps"][f0 + i, :n])
+            assert np.array_equal(r_["desc"][i, :n], one["desc"][f0 + i, :n])
+        for i in range(int(r_["frames"]) - 1):
+            m = int(one["n"][f0 + i])
+            assert int(r_["nmatch"][i]) == int(one["nmatch"][f0 + i])
+            assert np.array_equal(r_["matches"][i, :m], one["matches"][f0 + i, :m])
+
+
 def test_c5_two_rank_map_shards_equal_one_rank(tmp_path):
     """Config C5 sharded as SURVEY §8(e) states it: the keyframe map split by
     keyframe id over 2 fresh ranks (sharing the box's GPU, gloo), the
@@ -75,7 +107,7 @@ def test_c5_two_rank_map_shards_equal_one_rank(tmp_path):
     common = ["--nkf", "601", "--reps", "1", "--warmup", "1", "--cpu-sample", "0"]
     _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tools/bench_c5.py",
-          "--dump", str(tmp_path / "two")] + common, env)
+          "--gpus", "2", "--dump", str(tmp_path / "two")] + common, env)
     env1 = {k: v for k, v in env.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     _run([sys.executable, "tools/bench_c5.py", "--dump", str(tmp_path / "one")] + common, env1)
     one = np.load(tmp_path / "one" / "rank0.npz")
@@ -116,7 +148,7 @@ def _stereo_runs(tmp_path, workload, P):
     common = ["--workload", workload, "--steps", "1", "--warmup", "1", "--cpu-sample", "0"]
     _run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "tools/bench_stereo.py",
-          "--pairs", str(P), "--dump", str(tmp_path / "two")] + common, env)
+          "--gpus", "2", "--pairs", str(P), "--dump", str(tmp_path / "two")] + common, env)
     env1 = {k: v for k, v in env.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
     _run([sys.executable, "tools/bench_stereo.py", "--pairs", str(2 * P), "--dump", str(tmp_path / "one")] + common,
          env1)

@@ -50,6 +50,17 @@ def _worker(rank, world, port, q):
         kt, dt = sharding.broadcast_frame(fk if rank == 0 else None, fd if rank == 0 else None)
         k, d = sharding.keypoints_host(kt), dt.numpy()
         same &= np.array_equal(k.view(np.uint8), fk.view(np.uint8)) and np.array_equal(d, fd)
+        # a query loop: one channel (capacity agreed once), frames of varying size
+        chan = sharding.FrameChannel(400 if rank == 0 else 0)
+        for nq in (300, 17, 0, 400):
+            qk, qd = (fk[:nq], fd[:nq]) if nq <= 300 else (np.resize(fk, nq), np.resize(fd, (nq, 32)))
+            ck, cd = chan.broadcast(qk if rank == 0 else None, qd if rank == 0 else None)
+            same &= np.array_equal(sharding.keypoints_host(ck).view(np.uint8), qk.view(np.uint8))
+            same &= np.array_equal(cd.numpy(), qd)
+        # a vocabulary with explicit child lists (the text-file form)
+        cv = dict(ref, child_idx=np.arange(len(ref["nchild"]), dtype=np.int32)[::-1].copy()) if rank == 0 else None
+        v2 = sharding.broadcast_vocabulary(cv)
+        same &= np.array_equal(v2["child_idx"].numpy(), np.arange(len(ref["nchild"]), dtype=np.int32)[::-1])
         vk = abi.vocab_struct(vh)
         _, _, fnode = O.transform(vk, d, 2)
         res = {}

@@ -1,0 +1,12 @@
+#!/usr/bin/env python3
+"""One-line summary of a bench.py JSON line: value, stage times, roofline.
+usage: tools/bench_brief.py bench.json"""
+import json
+import sys
+
+d = json.loads([x for x in open(sys.argv[1]) if x.startswith("{")][-1])
+st = {k: round(v * 1e3, 1) for k, v in (d.get("stage_ms") or {}).items() if v}
+r = d.get("roofline") or {}
+print(round(d["value"]), "n_gpus", d.get("n_gpus"), "ms/step", round(d["ms_per_step"], 4), st,
+      "roof", r.get("kernel"), r.get("frac") and round(r["frac"], 4),
+      "parity", d.get("parity", {}).get("frames_mismatched"), d.get("parity", {}).get("pairs_mismatched"))

@@ -46,8 +46,14 @@ def main():
                     help="share of keyframe features with a valid MapPoint (1.0: the stated C5 map)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="keyframes the oracle checks (-1: all)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); started here under torch.distributed.run when WORLD_SIZE is unset")
     ap.add_argument("--dump", default="", help="directory: each rank saves its shard's matches (tests)")
     args = ap.parse_args()
+    from orb_slam3_vio_fixes_amd import launch
+    rc = launch.ensure_ranks(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     res = run_c5(args)
     if res is not None:
         print(json.dumps(res), flush=True)
@@ -88,7 +94,10 @@ def run_c5(args):
     if world > 1:
         # the vocabulary once, the query per query: RCCL broadcasts into HBM
         vt = sharding.broadcast_vocabulary(vh, 0, dev)
-        kt, dt = sharding.broadcast_frame(k, d, 0, dev)
+        # the query channel is made once (capacity agreed once); each query
+        # is one fixed-size broadcast
+        chan = sharding.FrameChannel(2 * NFEAT, 0, dev)
+        kt, dt = chan.broadcast(k, d)
         k = sharding.keypoints_host(kt)
     else:
         vt = {key: torch.from_numpy(np.ascontiguousarray(vh[key])).to(dev)

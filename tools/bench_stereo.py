@@ -117,8 +117,14 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--cpu-sample", type=int, default=64)
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); started here under torch.distributed.run when WORLD_SIZE is unset")
     ap.add_argument("--dump", default="", help="directory: each rank saves its last step's outputs (tests)")
     args = ap.parse_args()
+    from orb_slam3_vio_fixes_amd import launch
+    rc = launch.ensure_ranks(args.gpus, __file__, sys.argv[1:])
+    if rc is not None:
+        sys.exit(rc)
     out = run_c4(args) if args.workload == "c4" else run_c3(args)
     if out is not None:
         print(json.dumps(out), flush=True)

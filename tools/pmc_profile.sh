@@ -4,7 +4,7 @@
 # usage: tools/pmc_profile.sh <outdir> [bench args...]
 set -o pipefail
 OUT=${1:-gpurun_out/pmc}; shift
-ARGS=${@:---steps 3 --warmup 1 --cpu-sample 0 --no-host-api --no-profile --streams 1}
+ARGS=${@:---steps 3 --warmup 1 --cpu-sample 0 --no-host-api --no-profile --streams 1 --overlap 1 --sets 2}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 rocprofv3 -L > "$OUT/counters.txt" 2>&1 || true
