@@ -87,6 +87,16 @@ def broadcast_vocabulary(voc: dict | None, src: int = 0, device="cpu") -> dict:
     return out
 
 
+def vocab_device_struct(v: dict):
+    """orbv_vocab over the broadcast tensors (device pointers; keeps them alive)."""
+    from . import abi
+    keep = [v[k] for k in ("first_child", "nchild", "node_desc", "word_id", "weight")]
+    ci = v.get("child_idx")
+    s = abi.OrbvVocab(int(v["nnodes"]), int(v["depth_levels"]), *[t.data_ptr() for t in keep],
+                      ci.data_ptr() if ci is not None else None)
+    return abi.Keep(s, keep + ([ci] if ci is not None else []))
+
+
 class FrameChannel:
     """Per-query broadcast of a frame's keypoints (raw 28-B records) and
     descriptors from `src`.  The capacity is agreed once, when the channel is

@@ -61,6 +61,8 @@ def _worker(rank, world, port, q):
         cv = dict(ref, child_idx=np.arange(len(ref["nchild"]), dtype=np.int32)[::-1].copy()) if rank == 0 else None
         v2 = sharding.broadcast_vocabulary(cv)
         same &= np.array_equal(v2["child_idx"].numpy(), np.arange(len(ref["nchild"]), dtype=np.int32)[::-1])
+        vs = sharding.vocab_device_struct(v2)             # the orbv_vocab view the device descent takes
+        same &= vs.struct.child_idx == v2["child_idx"].data_ptr() and vs.struct.nnodes == v2["nnodes"]
         vk = abi.vocab_struct(vh)
         _, _, fnode = O.transform(vk, d, 2)
         res = {}
