@@ -20,6 +20,10 @@
  * Frame.cc:1069-1071, with the right camera's grid, stereo partners and
  * projections, ORBmatcher.cc:131-209, :1794-1860).
  *
+ * The other ten search / Fuse bodies (the mapping and loop-closing threads and
+ * relocalisation's projection) are in ORBmatcher_mapping.cc; the helpers both
+ * files share are in ORBmatcher_adapter.h.
+ *
  * tests/test_adapter.py compiles this file (g++ -fsyntax-only) against the
  * reference's unmodified ORBmatcher.h / Frame.h / KeyFrame.h / MapPoint.h and
  * their includes, with declaration-only stand-ins for the third-party headers
@@ -28,12 +32,8 @@
  * the reference header and run on the GPU (tests/test_gpu_adapter.py); the ABI
  * calls here are those of tests/native/cpp_api_test.cpp, which runs on the GPU.
  */
-#include "ORBmatcher.h"
-#include "KeyFrame.h"
-#include "MapPoint.h"
-#include "orb_mi355x.h"
+#include "ORBmatcher_adapter.h"
 
-#include <stdexcept>
 #include <vector>
 
 using namespace std;
@@ -41,67 +41,7 @@ using namespace std;
 namespace ORB_SLAM3
 {
 
-namespace
-{
-static_assert(sizeof(cv::KeyPoint) == sizeof(orb_keypoint), "cv::KeyPoint is the 28-byte orb_keypoint");
-
-// The keypoints a frame's matchers index: mvKeysUn, or for a fisheye stereo
-// frame (nleft != -1) mvKeys followed by mvKeysRight (Frame.cc:1069-1071,
-// AssignFeaturesToGrid :401-415); `store` keeps the combined copy alive.
-template <class F> const cv::KeyPoint* keys_of(const F& f, int nleft, vector<cv::KeyPoint>& store, int& n)
-{
-    if (nleft == -1) {
-        n = (int)f.mvKeysUn.size();
-        return f.mvKeysUn.data();
-    }
-    store.assign(f.mvKeys.begin(), f.mvKeys.end());
-    store.insert(store.end(), f.mvKeysRight.begin(), f.mvKeysRight.end());
-    n = (int)store.size();
-    return store.data();
-}
-
-// A Frame / KeyFrame as the matchers read it (Frame.h:223-290).
-template <class F> orbm_frame view(const F& f, int nleft, vector<cv::KeyPoint>& store)
-{
-    orbm_frame v;
-    int n = 0;
-    v.kps = reinterpret_cast<const orb_keypoint*>(keys_of(f, nleft, store, n));
-    v.n = (int32_t)n;
-    v.desc = f.mDescriptors.data;
-    v.min_x = f.mnMinX; v.max_x = f.mnMaxX; v.min_y = f.mnMinY; v.max_y = f.mnMaxY;
-    v.grid_inv_w = f.mfGridElementWidthInv;
-    v.grid_inv_h = f.mfGridElementHeightInv;
-    v.u_right = nleft != -1 || f.mvuRight.empty() ? nullptr : f.mvuRight.data();
-    v.scale_factors = f.mvScaleFactors.data();
-    v.nlevels = (int32_t)f.mvScaleFactors.size();
-    return v;
-}
-
-// DBoW2::FeatureVector (std::map<NodeId, std::vector<unsigned int>>) as CSR
-struct FeatVecCSR {
-    vector<uint32_t> nodes, idx;
-    vector<int32_t> off;
-    orbm_featvec c;
-    explicit FeatVecCSR(const DBoW2::FeatureVector& fv)
-    {
-        off.push_back(0);
-        for (const auto& kv : fv) {
-            nodes.push_back(kv.first);
-            idx.insert(idx.end(), kv.second.begin(), kv.second.end());
-            off.push_back((int32_t)idx.size());
-        }
-        c.nnodes = (int32_t)nodes.size();
-        c.node_ids = nodes.data();
-        c.offsets = off.data();
-        c.idx = idx.data();
-    }
-};
-
-void check(int rc, const char* what)
-{
-    if (rc < 0) throw std::runtime_error(std::string("ORBmatcher: ") + what + " failed");
-}
-}  // namespace
+using namespace mi355x_adapter;
 
 int ORBmatcher::SearchForInitialization(Frame& F1, Frame& F2, vector<cv::Point2f>& vbPrevMatched,
                                         vector<int>& vnMatches12, int windowSize)

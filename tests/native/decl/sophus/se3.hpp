@@ -21,6 +21,7 @@ public:
     Eigen::Quaternion<S> unit_quaternion() const;
     Eigen::Matrix<S, 3, 1> log() const;
     static SO3 exp(const Eigen::Matrix<S, 3, 1>& w);
+    static Eigen::Matrix<S, 3, 3> hat(const Eigen::Matrix<S, 3, 1>& w);
     template <class T> SO3<T> cast() const;
     SO3 operator*(const SO3&) const;
     Eigen::Matrix<S, 3, 1> operator*(const Eigen::Matrix<S, 3, 1>&) const;

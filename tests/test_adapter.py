@@ -39,7 +39,8 @@ def test_adapter_uses_only_declared_abi():
 
 @pytest.mark.skipif(not (REF_INC / "Frame.h").exists(), reason="reference tree not present")
 @pytest.mark.skipif(shutil.which("g++") is None, reason="no g++")
-def test_matcher_adapter_compiles_against_reference_headers():
+@pytest.mark.parametrize("name", ["ORBmatcher_searches.cc", "ORBmatcher_mapping.cc"])
+def test_matcher_adapter_compiles_against_reference_headers(name):
     """adapters/orbslam3/ORBmatcher_searches.cc -- the four per-frame search
     bodies, pinhole and fisheye stereo (Nleft != -1) branches -- compiles
     against the reference's unmodified ORBmatcher.h / Frame.h / KeyFrame.h /
@@ -52,17 +53,54 @@ def test_matcher_adapter_compiles_against_reference_headers():
     reference's own headers warn)."""
     ref = REF_INC.parent
     native = ROOT / "tests" / "native"
-    src = ROOT / "adapters" / "orbslam3" / "ORBmatcher_searches.cc"
+    src = ROOT / "adapters" / "orbslam3" / name
+    hdr = ROOT / "adapters" / "orbslam3" / "ORBmatcher_adapter.h"
     cmd = ["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Wextra",
            "-I", str(native / "decl"), "-I", str(REF_INC), "-I", str(REF_INC / "CameraModels"), "-I", str(ref),
            "-I", str(ROOT / "include"), str(src)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
-    own = [ln for ln in r.stderr.splitlines() if ln.startswith(str(src) + ":") and "warning" in ln]
+    own = [ln for ln in r.stderr.splitlines()
+           if (ln.startswith(str(src) + ":") or ln.startswith(str(hdr) + ":")) and "warning" in ln]
     assert not own, own
-    # no branch the reference handles is refused: the only throw is the C ABI's error status
+    # no branch the reference handles is refused: the only throw is the C ABI's
+    # error status, in the shared header's check()
     text = src.read_text()
-    assert text.count("throw ") == 1 and "Nleft != -1" not in text.split("throw ")[1].split(";")[0]
-    for fn in ("orbm_search_by_projection_mps_fisheye", "orbm_search_by_projection_last_fisheye",
-               "orbm_search_by_bow_fisheye"):
-        assert fn + "(" in text
+    assert "throw " not in text
+    htext = hdr.read_text()
+    assert htext.count("throw ") == 1 and "if (rc < 0) throw" in htext
+    if name == "ORBmatcher_searches.cc":
+        for fn in ("orbm_search_by_projection_mps_fisheye", "orbm_search_by_projection_last_fisheye",
+                   "orbm_search_by_bow_fisheye"):
+            assert fn + "(" in text
+
+
+def _bodies(text):
+    """ORBmatcher member definitions in a source file: (name, parameter types)."""
+    import re
+    out = []
+    for m in re.finditer(r"^\s*(?:int|float|void)\s+ORBmatcher::(\w+)\s*\(([^)]*)\)", text, re.M):
+        params = " ".join(m.group(2).split())
+        out.append((m.group(1), re.sub(r"\s*\w+\s*(?=,|$)", "", params)))
+    return out
+
+
+@pytest.mark.skipif(not (REF_INC / "ORBmatcher.h").exists(), reason="reference tree not present")
+def test_adapters_replace_every_search_and_fuse_body():
+    """Every Search* / Fuse overload ORBmatcher.h:46-87 declares (and
+    DescriptorDistance) has exactly one body in adapters/orbslam3/, so the
+    reference's src/ORBmatcher.cc keeps only the constructor,
+    RadiusByViewingCos and ComputeThreeMaxima."""
+    import re
+    decl = (REF_INC / "ORBmatcher.h").read_text()
+    want = re.findall(r"^\s*(?:static\s+)?int\s+(Search\w+|Fuse|DescriptorDistance)\s*\(", decl, re.M)
+    assert len(want) == 13, want      # 5 SearchByProjection, 2 SearchByBoW, 2 Fuse, 4 others
+    have = []
+    for f in ("ORBmatcher_searches.cc", "ORBmatcher_mapping.cc"):
+        have += [n for n, _ in _bodies((ROOT / "adapters" / "orbslam3" / f).read_text())]
+    assert sorted(have) == sorted(want), (sorted(have), sorted(want))
+    ref_src = (REF_INC.parent / "src" / "ORBmatcher.cc").read_text()
+    ref_bodies = re.findall(r"^\s*(?:int|float|void)\s+ORBmatcher::(\w+)\s*\(", ref_src, re.M)
+    left = sorted(set(ref_bodies) - set(have))
+    assert left == ["ComputeThreeMaxima", "ORBmatcher", "RadiusByViewingCos"] or \
+        left == ["ComputeThreeMaxima", "RadiusByViewingCos"], left
