@@ -415,12 +415,13 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
 
 /* The batched device searches (orbm_search_by_bow_batch_device,
  * orbm_search_for_initialization_batch_device) keep their scratch between
- * calls, one set per (device, stream) of the calling thread; at most a few
- * sets stay allocated (the least recently used is freed after a device
+ * calls, one set per (device, stream) of the calling thread; at most 16 sets
+ * stay allocated (the least recently used one is freed once its own stream has
+ * finished its last use of it -- an event wait on that stream, not a device
  * synchronisation).  This frees the calling thread's sets for `stream` on the
- * current device (all = 1: every set of the thread) after a device
- * synchronisation.  Call it before destroying a stream these calls used.
- * Returns ORB_OK or ORB_ERR_DEVICE. */
+ * current device (all = 1: every set of the thread, on any device) the same
+ * way.  Call it before destroying a stream these calls used.  Returns ORB_OK,
+ * or ORB_ERR_DEVICE if a set's stream reported an error (that set is kept). */
 int orbm_release_scratch(void* stream, int all);
 
 /* Map points projected into F (the fields ORBmatcher reads from MapPoint,

@@ -3,15 +3,45 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <unordered_map>
+
 #define ORB_CHECK(call)                                  \
     do {                                                 \
         hipError_t e_ = (call);                          \
         if (e_ != hipSuccess) return ORB_ERR_DEVICE;     \
     } while (0)
 
+// Every product launch: refused with ORB_ERR_UNSUPPORTED when static + dynamic
+// LDS exceed a CU (orbmi::lds_fits), otherwise hipLaunchKernelGGL.
+#define ORB_LAUNCH(K, G, B, S, ST, ...)                                                  \
+    do {                                                                                 \
+        if (!::orbmi::lds_fits(reinterpret_cast<const void*>(K), (size_t)(S)))           \
+            return ORB_ERR_UNSUPPORTED;                                                  \
+        hipLaunchKernelGGL(K, G, B, S, ST, ##__VA_ARGS__);                               \
+    } while (0)
+
 namespace orbmi {
 
 constexpr int kWave = 64;
+constexpr size_t kCuLds = 160 * 1024;       // LDS of one CU: a workgroup's ceiling (MI355X_MICROARCH.md)
+
+// Launch-time LDS guard: a kernel's static LDS (hipFuncGetAttributes, once per
+// kernel and thread) plus the launch's dynamic LDS must fit one CU, or the
+// launch is refused before it reaches the device (an over-subscribed launch
+// faults the GPU instead of failing cleanly).
+inline bool lds_fits(const void* kernel, size_t dyn) {
+    static thread_local std::unordered_map<const void*, size_t>* cache = new std::unordered_map<const void*, size_t>();
+    size_t st = 0;
+    const auto it = cache->find(kernel);
+    if (it != cache->end()) {
+        st = it->second;
+    } else {
+        hipFuncAttributes at{};
+        if (hipFuncGetAttributes(&at, kernel) == hipSuccess) st = at.sharedSizeBytes;
+        cache->emplace(kernel, st);
+    }
+    return dyn + st <= kCuLds;
+}
 
 // orb_debug_set_option's process-wide table (matcher.hip): alternative kernel
 // forms for parity tests; every product default is 0

@@ -637,9 +637,10 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     P.ncells = cellsum;
     P.slot_total = slotsum;
     P.out_total = outsum;
-    // k_assemble holds a flag per output slot of a frame in LDS: up to ~40,000
+    // k_assemble holds a flag per output slot of a frame in LDS (dynamic) next
+    // to its static lvl_start[kMaxLevels + 1] and tmp[16]: up to ~40,000
     // features a frame (Tracking's largest extractor is 5 x nFeatures)
-    if ((size_t)outsum * 4 + 64 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
+    if ((size_t)outsum * 4 + 64 + (size_t)(kMaxLevels + 1 + 16) * 4 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
     P.in_pitch = (size_t)round_up(w, 64);
 
     const size_t B = (size_t)maxB;
@@ -1032,6 +1033,9 @@ __device__ __forceinline__ uint32_t pretest16(uint32_t cm, const uint4& c, uint3
     return bits;
 }
 
+// PRE: the fused iniThFAST pre-test (a test hook, ORB_OPT_PYR_PRETEST; the
+// release path launches k_pyr_stream<false>, which carries none of its code)
+template <bool PRE>
 __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
     extern __shared__ uint4 ps_lds[];
     uint32_t* lds = (uint32_t*)ps_lds;
@@ -1134,7 +1138,7 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
             const int lo = __builtin_amdgcn_readlane((int)se.x, e), nrows = __builtin_amdgcn_readlane((int)se.y, e);
             const int wst = __builtin_amdgcn_readlane((int)se.z, e), ngr = __builtin_amdgcn_readlane((int)se.w, e);
             const int local = (j - wst) * kWave + lane;
-            if (e >= a.L) {
+            if (PRE && e >= a.L) {
                 // pre-test of level m: lane = (row, 16-pixel group) of the step's rows
                 const int m = e - a.L;
                 const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)lvb.x, m);
@@ -1163,7 +1167,7 @@ __global__ __launch_bounds__(1024) void k_pyr_stream(PyrStreamArgs a) {
             const uint32_t lpitch = (uint32_t)__builtin_amdgcn_readlane((int)lva.w, l);
             const uint32_t rb0 = (uint32_t)__builtin_amdgcn_readlane((int)lvb.x, l);
             const int rr = __builtin_amdgcn_readlane((int)lvb.y, l) & 0xff;
-            const bool ring_out = l < a.L - 1 || a.pretest;     // the last level's rows feed only the pre-test
+            const bool ring_out = l < a.L - 1 || (PRE && a.pretest);   // the last level's rows feed only the pre-test
             const int runs = ngr >> 16, ng = ngr & 0xffff;
             const int run = (int)(((float)local + 0.5f) * __builtin_amdgcn_rcpf((float)ng));
             const int g = local - (int)__umul24(run, ng);
@@ -3598,9 +3602,11 @@ static FastGroup fast_group(const Plan& P, int cb, int ce) {
 // fetch row width (dwords) and loads per lane: <16, 12> takes ROIs of at most
 // 16 dwords by 48 rows (W = 35 cells are < 70 px: nd <= 19 and rows < 76
 // always fit <32, 40>); rp: the fixed LDS pitch of the ROIs (dwords), 0: per cell
-static void (*fast_kernel(const FastGroup& G, bool bm, int& rp))(FastArgs) {
+static void (*fast_kernel(const FastGroup& G, bool want_bm, int& rp, bool& bm))(FastArgs) {
     const int ndm = G.nd_max, rm = G.rows_max;
     rp = 0;
+    // bitmap (BM) forms exist for ROIs of <= 64 rows and <= 16 dwords
+    bm = want_bm && rm <= 64 && ndm <= 16;
 #if ORB_FAST_FIXED_PITCH
     if (ndm <= 11 && rm <= 64) {
         rp = 11;
@@ -3703,7 +3709,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
         pa.pretest = S.pretest;
         pa.ini_th = std::min(std::max(hd->prm.ini_th_fast, 0), 255);
         pa.bm = P.d_bm; pa.bm_fstride = P0.bm_bytes;
-        hipLaunchKernelGGL(k_pyr_stream, dim3(B), dim3(1024), S.lds_bytes, st, pa);
+        ORB_LAUNCH(S.pretest ? k_pyr_stream<true> : k_pyr_stream<false>, dim3(B), dim3(1024), S.lds_bytes, st, pa);
     } else {
         for (const PyrGroup& g : P.pgroups) {
             PyrArgs pa;
@@ -3720,7 +3726,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
             pa.la = g.la; pa.lb = g.lb; pa.nb = g.nb; pa.nframes = B; pa.lds_b = g.lds_a;
             pa.lds_x = g.lds_a + g.lds_b; pa.lds_y = pa.lds_x + g.lds_x;
             const unsigned nwg = (unsigned)((B + 7) / 8 * 8 * g.nb);
-            hipLaunchKernelGGL(k_pyramid, dim3(nwg), dim3(256), pyr_group_lds(g), st, pa);
+            ORB_LAUNCH(k_pyramid, dim3(nwg), dim3(256), pyr_group_lds(g), st, pa);
         }
     }
     mark();
@@ -3740,9 +3746,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     fa.min_th = std::min(std::max(hd->prm.min_th_fast, 0), 255);
     // the iniThFAST candidates come from k_pyr_stream's fused pre-test when it
     // ran (BM forms); otherwise k_fast_cells pre-tests the landed ROI itself
-    const bool bm = use_stream && P0.ps.pretest && P.d_bm;
-    hd->bm_last = bm;
-    fa.bm = bm ? P.d_bm : nullptr;
+    bool bm = use_stream && P0.ps.pretest && P.d_bm;
     fa.bm_fstride = P0.bm_bytes;
     // A wave's LDS is sized for the largest cell of the plan and sets
     // k_fast_cells' occupancy: 17-18 waves a CU at 752x480 (8.7 KB a wave;
@@ -3753,8 +3757,12 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     {
         const FastGroup G = fast_group(P0, 0, P0.ncells);
         int rp = 0;
-        void (*kfast)(FastArgs) = fast_kernel(G, bm, rp);
+        void (*kfast)(FastArgs) = fast_kernel(G, bm, rp, bm);
         if (!kfast) return ORB_ERR_UNSUPPORTED;
+        // the bitmap is the candidate source only if a bitmap form was chosen
+        // (fast_kernel falls back to the ROI pre-test beyond 64 rows)
+        hd->bm_last = bm;
+        fa.bm = bm ? P.d_bm : nullptr;
         fast_lds_layout(G, rp, fa);
         fa.cell_begin = 0;
         fa.cell_end = P0.ncells;
@@ -3762,7 +3770,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
         fa.nframes = B;
         const dim3 fgrid((P0.ncells + kFastWpb * kCellsPerWave - 1) / (kFastWpb * kCellsPerWave), B);
         if (P0.ncells > 0)                        // (every level under 67 px: no FAST cells at all)
-            hipLaunchKernelGGL(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
+            ORB_LAUNCH(kfast, fgrid, dim3(kWave * kFastWpb), flds, st, fa);
     }
     mark();
     // quadtree
@@ -3783,7 +3791,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
 #else
         const dim3 qg(L, B);
 #endif
-        hipLaunchKernelGGL(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(256), qlds, st, qa);
+        ORB_LAUNCH(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(256), qlds, st, qa);
     }
     mark();
     // describe
@@ -3798,14 +3806,14 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     da.slot_level = P.d_slot_level;
     da.nslots = (long long)B * P.out_total;
     const dim3 dgrid((unsigned)((P.out_total + kDescWpb * kDescSlots - 1) / (kDescWpb * kDescSlots)), (unsigned)B);
-    hipLaunchKernelGGL(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(kWave * kDescWpb), 0, st, da);
+    ORB_LAUNCH(da.fma ? k_describe<true> : k_describe<false>, dgrid, dim3(kWave * kDescWpb), 0, st, da);
     mark();
     // assemble
     AsmArgs aa;
     aa.lv = P.d_lv; aa.qt_key = P.d_qt_key; aa.qt_n = P.d_qt_n; aa.angle = P.d_angle; aa.sdesc = P.d_sdesc;
     aa.out_total = P.out_total; aa.L = L; aa.lap0 = lap0; aa.lap1 = lap1;
     aa.kps = d_kps; aa.desc = d_desc; aa.cap = cap; aa.n_out = d_n; aa.mono_out = d_mono;
-    hipLaunchKernelGGL(k_assemble, dim3(B), dim3(256), (size_t)P.out_total * 4 + 64, st, aa);
+    ORB_LAUNCH(k_assemble, dim3(B), dim3(256), (size_t)P.out_total * 4 + 64, st, aa);
     mark();
     if (hd->profiling) hd->ev_calls.push_back(marks);
     ORB_CHECK(hipGetLastError());
@@ -4226,9 +4234,9 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
     unsigned long long* d = nullptr;
     ORB_CHECK(hipMalloc(&d, nchunks * sizeof(unsigned long long)));
     const dim3 grid((unsigned)std::min<long long>(nchunks, 8192));
-    if (what == 0) hipLaunchKernelGGL(k_debug_math<0>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
-    else if (what == 1) hipLaunchKernelGGL(k_debug_math<1>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
-    else hipLaunchKernelGGL(k_debug_math<2>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    if (what == 0) ORB_LAUNCH(k_debug_math<0>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    else if (what == 1) ORB_LAUNCH(k_debug_math<1>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    else ORB_LAUNCH(k_debug_math<2>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(hashes, d, nchunks * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     (void)hipFree(d);
@@ -4266,7 +4274,7 @@ int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* 
         (tot && (hipMemcpy(d_cnt, cnt, tot * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
                  hipMemcpy(d_x0, x0, tot * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)))
         return done(ORB_ERR_DEVICE);
-    hipLaunchKernelGGL(k_debug_sort, dim3(narrays), dim3(256), dbg_sort_lds(maxm), 0, d_off, d_cnt, d_x0, d_perm, d_fb);
+    ORB_LAUNCH(k_debug_sort, dim3(narrays), dim3(256), dbg_sort_lds(maxm), 0, d_off, d_cnt, d_x0, d_perm, d_fb);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return done(ORB_ERR_DEVICE);
     if ((tot && hipMemcpy(perm, d_perm, tot * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
         hipMemcpy(fallback, d_fb, narrays * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)

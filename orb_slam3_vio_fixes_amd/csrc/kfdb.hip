@@ -250,13 +250,13 @@ int orbk_detect_relocalization_candidates(orbk_db* db, const int32_t* q_words, c
     ORB_CHECK(hipMemcpyAsync(db->rs, reloc_score, nkf * sizeof(float), hipMemcpyHostToDevice, st));
     ORB_CHECK(hipMemsetAsync(db->ctl, 0, 2 * sizeof(int32_t), st));
     const dim3 g((nkf + 255) / 256);
-    hipLaunchKernelGGL(k_kfdb_reset, g, dim3(256), 0, st, nkf, db->cnt, db->first);
-    hipLaunchKernelGGL(k_kfdb_count, dim3(nq), dim3(256), 0, st, db->qw, db->inv_off, db->inv_kf, db->cnt, db->first,
+    ORB_LAUNCH(k_kfdb_reset, g, dim3(256), 0, st, nkf, db->cnt, db->first);
+    ORB_LAUNCH(k_kfdb_count, dim3(nq), dim3(256), 0, st, db->qw, db->inv_off, db->inv_kf, db->cnt, db->first,
                        db->ctl);
-    hipLaunchKernelGGL(k_kfdb_select, g, dim3(256), 0, st, nkf, db->cnt, db->first, db->ctl, db->sel, db->rec);
-    hipLaunchKernelGGL(k_kfdb_score, g, dim3(256), 0, st, db->ctl, db->sel, nq, db->qw, db->qv, db->bow_off,
+    ORB_LAUNCH(k_kfdb_select, g, dim3(256), 0, st, nkf, db->cnt, db->first, db->ctl, db->sel, db->rec);
+    ORB_LAUNCH(k_kfdb_score, g, dim3(256), 0, st, db->ctl, db->sel, nq, db->qw, db->qv, db->bow_off,
                        db->bow_words, db->bow_vals, db->rs, db->rec);
-    hipLaunchKernelGGL(k_kfdb_neigh, g, dim3(256), 0, st, db->ctl, db->cov_off_d, db->cov_kf_d, db->cnt, db->rs,
+    ORB_LAUNCH(k_kfdb_neigh, g, dim3(256), 0, st, db->ctl, db->cov_off_d, db->cov_kf_d, db->cnt, db->rs,
                        db->rec);
     ORB_CHECK(hipGetLastError());
     int32_t ctl[2];

@@ -36,7 +36,7 @@ namespace orbmi {
 // Host-API uploads are coalesced (h2d below): every other GPU operation of
 // this file flushes the pending copy first.
 static hipError_t flush_uploads();
-#define KLAUNCH(...) do { (void)flush_uploads(); hipLaunchKernelGGL(__VA_ARGS__); } while (0)
+#define KLAUNCH(K, G, B, S, ST, ...) do { (void)flush_uploads(); ORB_LAUNCH(K, G, B, S, ST, ##__VA_ARGS__); } while (0)
 
 constexpr int kGridCols = 64, kGridRows = 48;        // Frame.h:44-45
 constexpr int kThHigh = 100, kThLow = 50, kHisto = 30;   // ORBmatcher.cc:35-37
@@ -3565,35 +3565,51 @@ struct PBuf {
 
 static int pow2_at_least(int n) { int p = 64; while (p < n) p <<= 1; return p; }
 
-// Scratch of the asynchronous device entry points, one set per (device,
-// stream) of the calling thread: two searches issued on different streams, or
-// for different GPUs, must not share buffers.  (Calls on one stream are
-// ordered by the stream; buffers only grow, and hipFree of a grown-out buffer
-// waits for the device.)
 // Device scratch that batched launches keep between calls (grown on demand),
-// one set per (device, stream, kind) of the calling thread, most recently used
-// first.  At most kScratchSets stay allocated: a call on a further stream
-// frees the least recently used set after a device synchronisation (work still
-// queued on its stream may read it).  orbm_release_scratch frees a stream's
-// sets at once; a caller must do so before destroying a stream it used here,
-// or a new stream at the same address would inherit the buffers unordered
-// against the old stream's work.
+// one set per (device, stream, kind) of the calling thread -- two searches
+// issued on different streams, or for different GPUs, must not share buffers
+// -- most recently used first.  Each use ends with an event recorded on the
+// set's stream (scratch_used), so a set is freed only after ITS stream's last
+// use of it has finished (hipEventSynchronize of that event: no device-wide
+// synchronisation, no stall of the other streams).  At most kScratchSets stay
+// allocated (hardware queues x scratch kinds with room to spare); a call on a
+// further stream frees the least recently used set that way.
+// orbm_release_scratch frees a stream's sets at once; a caller must do so
+// before destroying a stream it used here, or a new stream at the same address
+// would inherit the buffers unordered against the old stream's work.
 struct ScratchBase {
     virtual ~ScratchBase() = default;
 };
-constexpr size_t kScratchSets = 6;
+constexpr size_t kScratchSets = 16;
 struct ScratchEntry {
     int dev;
     hipStream_t st;
     const void* kind;
     std::unique_ptr<ScratchBase> s;
+    hipEvent_t ev;              // recorded after the set's last use (nullptr: never used)
 };
 static std::list<ScratchEntry>& scratch_sets() {
     static thread_local std::list<ScratchEntry>* l = new std::list<ScratchEntry>();   // never destroyed at exit
     return *l;
 }
+// Frees a set once its stream's last use of it has completed; false (and the
+// set kept, leaked rather than freed under running work) if that wait fails.
+static bool scratch_free(ScratchEntry& e) {
+    if (e.ev) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        if (cur != e.dev && hipSetDevice(e.dev) != hipSuccess) return false;
+        const hipError_t w = hipEventSynchronize(e.ev);
+        if (w == hipSuccess) (void)hipEventDestroy(e.ev);
+        if (cur != e.dev) (void)hipSetDevice(cur);
+        if (w != hipSuccess) return false;
+        e.ev = nullptr;
+    }
+    e.s.reset();
+    return true;
+}
 template <class S>
-static S& stream_scratch(hipStream_t st) {
+static S* stream_scratch(hipStream_t st) {
     static const char kind = 0;                      // one address per scratch type
     auto& L = scratch_sets();
     int dev = 0;
@@ -3601,14 +3617,24 @@ static S& stream_scratch(hipStream_t st) {
     for (auto it = L.begin(); it != L.end(); ++it)
         if (it->dev == dev && it->st == st && it->kind == &kind) {
             L.splice(L.begin(), L, it);
-            return *static_cast<S*>(L.front().s.get());
+            return static_cast<S*>(L.front().s.get());
         }
     if (L.size() >= kScratchSets) {
-        (void)hipDeviceSynchronize();
+        if (!scratch_free(L.back())) return nullptr;
         L.pop_back();
     }
-    L.push_front(ScratchEntry{dev, st, &kind, std::make_unique<S>()});
-    return *static_cast<S*>(L.front().s.get());
+    L.push_front(ScratchEntry{dev, st, &kind, std::make_unique<S>(), nullptr});
+    return static_cast<S*>(L.front().s.get());
+}
+// After a call's launches on `st`: the front set (the one stream_scratch just
+// returned) records its stream's progress.
+static int scratch_used(hipStream_t st) {
+    ScratchEntry& e = scratch_sets().front();
+    if (!e.ev && hipEventCreateWithFlags(&e.ev, hipEventDisableTiming) != hipSuccess) {
+        e.ev = nullptr;
+        return ORB_ERR_DEVICE;
+    }
+    return hipEventRecord(e.ev, st) == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
 static GridParams grid_params(const orbm_frame* f) {
@@ -3710,12 +3736,20 @@ int orbm_release_scratch(void* stream, int all) {
     auto& L = scratch_sets();
     int dev = 0;
     (void)hipGetDevice(&dev);
-    bool any = false;
-    for (const auto& e : L) any |= all || (e.dev == dev && e.st == (hipStream_t)stream);
-    if (!any) return ORB_OK;
-    ORB_CHECK(hipDeviceSynchronize());
-    L.remove_if([&](const ScratchEntry& e) { return all || (e.dev == dev && e.st == (hipStream_t)stream); });
-    return ORB_OK;
+    int rc = ORB_OK;
+    for (auto it = L.begin(); it != L.end();) {
+        if (all || (it->dev == dev && it->st == (hipStream_t)stream)) {
+            if (!scratch_free(*it)) {               // its stream's work did not finish cleanly: keep it
+                rc = ORB_ERR_DEVICE;
+                ++it;
+                continue;
+            }
+            it = L.erase(it);
+        } else {
+            ++it;
+        }
+    }
+    return rc;
 }
 
 int orb_debug_get_option(int option) {
@@ -3794,7 +3828,9 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     if (nframes < 2 || cap <= 0 || cap > 0xffff) return ORB_ERR_PARAM;
     hipStream_t st = (hipStream_t)stream;
     struct Scratch : ScratchBase { PBuf<uint32_t> sorted, topk, l0s; PBuf<int> count, pf, ncand, l0c; int pf_frames = 0; };
-    Scratch& S = stream_scratch<Scratch>(st);
+    Scratch* Sp = stream_scratch<Scratch>(st);
+    if (!Sp) return ORB_ERR_DEVICE;
+    Scratch& S = *Sp;
     PBuf<uint32_t>&sorted = S.sorted, &topk = S.topk, &l0s = S.l0s;
     PBuf<int>&count = S.count, &pf = S.pf, &ncand = S.ncand, &l0c = S.l0c;
     int& pf_frames = S.pf_frames;
@@ -3806,9 +3842,8 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     if (pf_frames < nframes) {
         std::vector<int> idx(nframes);
         for (int i = 0; i < nframes; ++i) idx[i] = i;
-        if ((rc = pf.put(idx.data(), nframes))) return rc;
-        ORB_CHECK(flush_uploads());
-        ORB_CHECK(hipDeviceSynchronize());
+        if ((rc = pf.put(idx.data(), nframes, st))) return rc;
+        ORB_CHECK(hipStreamSynchronize(st));           // (idx is pageable and leaves scope)
         pf_frames = nframes;
     }
     const GridParams g{min_x, min_y, grid_inv_w, grid_inv_h};
@@ -3826,7 +3861,7 @@ int orbm_search_for_initialization_batch_device(int nframes, const orb_keypoint*
     a.matches = d_matches; a.nmatches = d_nmatches; a.topk = topk.p; a.ncand = ncand.p;
     if ((rc = launch_sfi(a, nframes - 1, st))) return rc;
     ORB_CHECK(hipGetLastError());
-    return ORB_OK;
+    return scratch_used(st);
 }
 
 // Frame nodes the large-node blocks take (host FeatureVector).
@@ -3951,7 +3986,9 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
         PBuf<bowk_list> lists;
         PBuf<bowk_v4i> fexp;
     };
-    Scratch& S = stream_scratch<Scratch>(st);
+    Scratch* Sp = stream_scratch<Scratch>(st);
+    if (!Sp) return ORB_ERR_DEVICE;
+    Scratch& S = *Sp;
     PBuf<int>&g_fl = S.g_fl, &g_off = S.g_off, &g_pr = S.g_pr, &bstart = S.bstart, &gstart = S.gstart,
         &g_rank = S.g_rank, &perm = S.perm, &chunk_node = S.chunk_node, &node_n = S.node_n;
     PBuf<unsigned long long>& bgcount = S.bgcount;
@@ -3971,8 +4008,10 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     const size_t big_lds = (size_t)64 * bp * sizeof(uint32_t);
     const bool all_lds = big_lds <= 64 * 1024 && !debug_opt(ORB_OPT_BOWK_BIG);
     const int big_pitch = all_lds ? bp : 0;
-    // (k_bowk_final packs a KF feature index, < 2^26 by the C ABI's contract, with its bin)
-    const bool claims = all_lds && a.f_n <= kBowkRow && !a.out12 && !a.f_valid;
+    // (k_bowk_final packs a KF feature index, < 2^26 by the C ABI's contract,
+    // with its bin; the map's FeatureVector total bounds it where the host
+    // knows it: a larger map takes k_bow_final)
+    const bool claims = all_lds && a.f_n <= kBowkRow && !a.out12 && !a.f_valid && nfv < (1LL << 26);
     int rc;
     if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc((size_t)a.f_nnodes * nsub)) ||
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
@@ -4017,7 +4056,8 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     }
     if (claims) KLAUNCH(k_bowk_final, dim3(npairs), dim3(256), (size_t)a.f_n * 4, st, k);
     else KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
-    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+    if (hipGetLastError() != hipSuccess) return ORB_ERR_DEVICE;
+    return scratch_used(st);
 }
 
 int orbm_kf_map_fv_desc(const orbm_kf_map_device* map, uint8_t* d_fv_desc, void* stream) {

@@ -377,12 +377,12 @@ static int launch_stereo(StereoArgs& a, const orbx_handle* h, int npairs, int ma
         a.scale[l] = h->scale[l];
         a.inv_scale[l] = h->inv_scale[l];
     }
-    hipLaunchKernelGGL(k_stereo_rows, dim3(npairs), dim3(256), (a.rows + 1) * sizeof(int), st, a);
+    ORB_LAUNCH(k_stereo_rows, dim3(npairs), dim3(256), (a.rows + 1) * sizeof(int), st, a);
     if (max_nl > 0)
-        hipLaunchKernelGGL(k_stereo_match, dim3((max_nl + 3) / 4, npairs), dim3(256), 0, st, a);
+        ORB_LAUNCH(k_stereo_match, dim3((max_nl + 3) / 4, npairs), dim3(256), 0, st, a);
     int np2 = 1;
     while (np2 < std::max(1, max_nl)) np2 <<= 1;
-    hipLaunchKernelGGL(k_stereo_prune, dim3(npairs), dim3(256), np2 * sizeof(uint32_t), st, a, np2);
+    ORB_LAUNCH(k_stereo_prune, dim3(npairs), dim3(256), np2 * sizeof(uint32_t), st, a, np2);
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }
@@ -514,7 +514,7 @@ int orbs_knn_match2(const uint8_t* query, int nq, const uint8_t* train, int nt, 
     if (nt) ORB_CHECK(hipMemcpy(bt.p, train, (size_t)nt * 32, hipMemcpyHostToDevice));
     ORB_CHECK(hipMemcpy(bn.p, ns, sizeof(ns), hipMemcpyHostToDevice));
     KnnArgs a{bq.p, bt.p, bn.p, bn.p + 1, bn.p + 2, bn.p + 3, stride, 0.7, bi.p, bd.p, bl.p};
-    hipLaunchKernelGGL(k_knn2, dim3((nq + 255) / 256, 1), dim3(256), 0, 0, a);
+    ORB_LAUNCH(k_knn2, dim3((nq + 255) / 256, 1), dim3(256), 0, 0, a);
     ORB_CHECK(hipGetLastError());
     ORB_CHECK(hipMemcpy(idx, bi.p, (size_t)nq * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
     ORB_CHECK(hipMemcpy(dist, bd.p, (size_t)nq * 2 * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -540,7 +540,7 @@ int orbs_fisheye_stereo_candidates_batch_device(int npairs, int left0, int right
     a.idx = d_idx;
     a.dist = d_dist;
     a.l2r = d_l2r;
-    hipLaunchKernelGGL(k_knn2, dim3((cap + 255) / 256, npairs), dim3(256), 0, (hipStream_t)stream, a);
+    ORB_LAUNCH(k_knn2, dim3((cap + 255) / 256, npairs), dim3(256), 0, (hipStream_t)stream, a);
     ORB_CHECK(hipGetLastError());
     return ORB_OK;
 }
