@@ -329,6 +329,109 @@ def adapter_rates(img, reps):
             "calls": reps}
 
 
+MATCHER_SEARCHES = ["search_for_initialization", "search_by_projection_last", "search_by_projection_mps",
+                    "search_by_bow"]
+MATCHER_OUT = {"search_for_initialization": "sfi", "search_by_projection_last": "last",
+               "search_by_projection_mps": "mps", "search_by_bow": "bow"}
+LATENCY_EXE = ROOT / "tests" / "native" / "bin" / "matcher_latency"
+
+
+def matcher_inputs(frames_np, d):
+    """The Tracking thread's per-frame matcher calls at their stated sizes,
+    written as raw arrays into directory d for tests/native/matcher_latency:
+    two consecutive 752x480 frames of the batch extracted by the GPU extractor
+    (1000 features); SearchForInitialization(F1, F2); SearchByProjection(F2,
+    LastFrame) with the last frame's ~1000 points projected onto F2's keypoints
+    (1 px noise, 2 % descriptor bits flipped); SearchByProjection(F2, 3000
+    local map points) (map points drawn from F2's keypoints, 2 px noise);
+    SearchByBoW(KF = F1, F2) with level-2 vocabulary nodes (synthetic k = 10
+    vocabulary) and 90 % of the keyframe's MapPoints valid."""
+    from orb_slam3_vio_fixes_amd import abi, orb, synth
+    d = Path(d)
+    ex = orb.ORBextractor(NFEAT, 1.2, 8, 20, 7)
+    k1, d1, _ = ex(np.ascontiguousarray(frames_np[0]), None, LAP)
+    k2, d2, _ = ex(np.ascontiguousarray(frames_np[1]), None, LAP)
+    rng = np.random.default_rng(11)
+    meta = {"W": W, "H": H, "n1": len(k1), "n2": len(k2), "nlevels": 8}
+    w = lambda name, a: np.ascontiguousarray(a).tofile(d / name)
+    w("f1_kps.bin", k1.view(np.uint8)); w("f2_kps.bin", k2.view(np.uint8))
+    w("f1_desc.bin", d1); w("f2_desc.bin", d2)
+    w("scale.bin", np.asarray(ex.GetScaleFactors(), np.float32))
+    # the last frame's points, projected near the current frame's keypoints
+    nl = len(k2)
+    flip = lambda a, p: np.where(rng.random(a.shape) < p, a ^ np.uint8(1 << int(rng.integers(0, 8))), a)
+    w("last_valid.bin", (rng.random(nl) < 0.9).astype(np.uint8))
+    w("last_u.bin", (k2["x"] + rng.normal(0, 1, nl)).astype(np.float32))
+    w("last_v.bin", (k2["y"] + rng.normal(0, 1, nl)).astype(np.float32))
+    w("last_ur.bin", np.full(nl, -1, np.float32))
+    w("last_oct.bin", k2["octave"].astype(np.int32))
+    w("last_ang.bin", ((k2["angle"] + rng.normal(0, 3, nl)) % 360).astype(np.float32))
+    w("last_hobs.bin", np.ones(nl, np.uint8))
+    w("last_desc.bin", flip(d2, 0.02))
+    meta["nlast"] = nl
+    # local map points
+    nq = 3000
+    src = rng.integers(0, len(k2), nq)
+    qx = (k2["x"][src] + rng.normal(0, 2, nq)).astype(np.float32)
+    w("mps_x.bin", qx); w("mps_y.bin", (k2["y"][src] + rng.normal(0, 2, nq)).astype(np.float32))
+    w("mps_xr.bin", (qx - 20).astype(np.float32))
+    w("mps_lvl.bin", k2["octave"][src].astype(np.int32))
+    w("mps_vcos.bin", rng.uniform(0.99, 1.0, nq).astype(np.float32))
+    w("mps_depth.bin", rng.uniform(0, 100, nq).astype(np.float32))
+    w("mps_inview.bin", (rng.random(nq) < 0.9).astype(np.uint8))
+    w("mps_hobs.bin", np.ones(nq, np.uint8))
+    w("mps_desc.bin", flip(d2[src], 0.02))
+    meta["nmps"] = nq
+    # BoW: FeatureVectors at level 2 of a synthetic k = 10 vocabulary
+    voc = abi.vocab_struct(synth.vocabulary(10, 3, seed=31))
+    for tag, dd in (("fv1", d1), ("fv2", d2)):
+        fv = abi.featvec_struct(orb.transform(voc, dd, 1)[2])
+        node_ids, offsets, idx = fv.arrays
+        w(f"{tag}_nodes.bin", node_ids); w(f"{tag}_off.bin", offsets); w(f"{tag}_idx.bin", idx)
+        meta[f"{tag}_nodes"] = len(node_ids)
+    w("kf_valid.bin", (rng.random(len(k1)) < 0.9).astype(np.uint8))
+    (d / "meta.txt").write_text("".join(f"{k} {v}\n" for k, v in meta.items()))
+    return {"frame_features": [len(k1), len(k2)], "last_frame_points": nl, "local_map_points": nq}
+
+
+def run_latency(lib, prefix, d, reps):
+    import subprocess
+    r = subprocess.run([str(LATENCY_EXE), str(lib), prefix, str(d), str(reps)], capture_output=True, text=True,
+                       timeout=300)
+    if r.returncode != 0:
+        raise RuntimeError(f"matcher_latency {prefix}: {r.stderr[-500:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def host_api_matchers(frames_np, d, reps=200):
+    """Per-call latency of the Tracking thread's matcher calls through the C
+    ABI, from C++ (tests/native/matcher_latency: host inputs in, host outputs
+    out, PCIe and every synchronisation included; no Python in the timed
+    loop).  Not the metric: the drop-in latency."""
+    from orb_slam3_vio_fixes_amd import capi
+    if not LATENCY_EXE.exists():
+        return None
+    sizes = matcher_inputs(frames_np, d)
+    gpu = run_latency(capi.LIB_PATH, "orbm", d, reps)
+    return {"sizes": sizes, "calls": reps, "gpu": gpu,
+            "note": "median per call from C++ through the C ABI, host arrays in and out (PCIe included)"}
+
+
+def cpu_baseline_matchers(d, blk, reps=200):
+    """CPU leg of host_api.matchers: the oracle's same entry points, one
+    thread (the reference's per-call model), same inputs and harness; the
+    outputs of every search compared with the GPU's (parity)."""
+    from oracle import oracle as O
+    lib_path, flags = O.fast_variant()
+    cpu = run_latency(lib_path, "orbo", d, reps)
+    blk["cpu_1thread"] = cpu
+    blk["speedup_vs_1thread"] = {k: cpu[k]["median_us"] / blk["gpu"][k]["median_us"] for k in MATCHER_SEARCHES}
+    blk["parity"] = {k: bool(np.array_equal(np.fromfile(Path(d) / f"orbm_{MATCHER_OUT[k]}.bin", np.int32),
+                                            np.fromfile(Path(d) / f"orbo_{MATCHER_OUT[k]}.bin", np.int32)))
+                     for k in MATCHER_SEARCHES}
+    blk["cpu_flags"] = flags
+
+
 def main():
     args = parse()
     # --gpus N without a launcher: start N ranks as one child process (no
@@ -604,6 +707,12 @@ def main():
                                                                    "bytes, monoIndex, nmatches and the full matches12"}
         if world == 1 and args.host_api:
             out["host_api"] = host_api_rates(frames_np)
+            import tempfile
+            with tempfile.TemporaryDirectory() as td:
+                mb = host_api_matchers(ring_np[0][:2], td)
+                if mb is not None and args.cpu_sample > 0:
+                    cpu_baseline_matchers(td, mb)
+                out["host_api"]["matchers"] = mb
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -217,8 +217,11 @@ int orbx_pyramid_kernel(orbx_handle* h);
  * Every form gives identical results; the defaults (0) are the measured
  * fastest, and the alternatives are also the forms a size falls back to when
  * the default's LDS tables do not fit.
- *   ORB_OPT_PROJ_FORM    projection searches: 0 top-K + speculative resolve,
- *                        1 top-K + serial resolve, 2 single-wave search
+ *   ORB_OPT_PROJ_FORM    projection searches: 0 fused single launch
+ *                        (brute-force top-K + last-block fixpoint resolve,
+ *                        frames <= 4096 keypoints, <= 8192 queries; else 3),
+ *                        1 top-K + serial resolve, 2 single-wave search,
+ *                        3 top-K + speculative resolve
  *   ORB_OPT_BOW_FORM     map-wide SearchByBoW: 0 lane per keyframe feature
  *                        (k_bowk_*) when the map carries its totals, 1 k_bow
  *   ORB_OPT_BOWK_BIG     0 auto, 1 no big-node resolve form (every frame node

@@ -3065,6 +3065,288 @@ __global__ __launch_bounds__(64) void k_proj_resolve_spec(ProjArgs a, const uint
     if (lane == 0) a.nmatches[0] = nm;
 }
 
+// ---- fused single-launch form (the host APIs' default) --------------------
+// k_proj_fused: a whole projection search in ONE launch, no grid build.
+//
+// Phase 1, one wave per query, every query in parallel: its kProjK smallest
+// candidates by (distance, GetFeaturesInArea order) from a brute-force pass
+// over the frame's keypoints.  A keypoint is in the query's GetFeaturesInArea
+// list iff its PosInGrid cell lies in the cell range the window visits and it
+// passes the window / level / stereo tests (Frame.cc:661-708 visit the cells
+// ix outer, iy inner, and a cell's keypoints in index order), so its list
+// position is (cell = gx * 48 + gy, index) -- a 32-bit key d << 24 | cell << 12
+// | index for frames of <= 4096 keypoints.  Only candidates that can still
+// decide the query are kept (d <= bound, as k_proj_topk); cnt = how many.
+//
+// Phase 2, in the LAST block to finish phase 1 (a ticket counter): the serial
+// claim loop over all queries at once, as a fixpoint.  T[s] = the first query
+// that claims slot s blocking (-1: blocked before the search, INT_MAX: never);
+// query j's decision reads only whether T[s] < j for its listed slots -- the
+// claims of EARLIER queries -- so recomputing every decision from the previous
+// round's T leaves the earliest wrong decision right after each round (a
+// Jacobi iteration of a recursion well-founded in query order), and two equal
+// consecutive rounds are the serial loop's outcome.  A decision its truncated
+// list cannot make (fewer unblocked entries than it needs) is made by a wave's
+// exact brute-force scan under the round's T.  Then: nmatches = accepted
+// decisions, owner[s] = the last query accepted on s (a later claim of a slot
+// its earlier claimer left unblocked overwrites it, as the serial loop does),
+// and the rotation filter clears the slot of every claim in a rejected bin.
+constexpr int kFusedThreads = 1024;
+constexpr int kFusedQpt = 8;                        // queries per thread in phase 2 (nq <= 8192)
+constexpr int kFusedMaxN = 4096;                    // 12-bit keypoint index in the order key
+constexpr int kFusedMaxQ = kFusedThreads * kFusedQpt;
+constexpr uint32_t kFusedNone = 0xffffffffu;
+
+// LDS: T[n] | D[nq] (decision per query) | dry[nq] | hist[32] | misc[8] | pre[n] bytes
+static size_t proj_fused_lds(int n, int nq) {
+    return (size_t)(n + 2 * nq + 32 + 8) * 4 + ((size_t)n + 15) / 16 * 16;
+}
+
+// The kProjK (or 2 for a rescan) smallest 32-bit keys of query i's candidates
+// with d <= bound, skipping (T != nullptr) slots blocked before query j; lane
+// r < K holds the r-th key and its packed entry d << 24 | (lvl | bin << 3) << 16
+// | slot.  Returns the number of such candidates.
+template <int K>
+__device__ int fused_select(const ProjArgs& a, int i, const ProjQuery& q, int bound, const int* T, int j,
+                            uint32_t& run, uint32_t& run_e) {
+    const int lane = lane_id();
+    const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
+    const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
+    const float qang = (a.mode == 1 && a.check_ori) ? a.qangle[i] : 0.0f;
+    run = kFusedNone;
+    run_e = kFusedNone;
+    int total = 0;
+    for (int base = 0; base < a.n; base += kWave) {
+        const int fi = base + lane;
+        uint32_t key = kFusedNone, ent = kFusedNone;
+        if (fi < a.n) {
+            const orb_keypoint k = a.kps[fi];
+            const int c = grid_cell(k, a.g);
+            const int gx = c / kGridRows, gy = c - gx * kGridRows;
+            int lv;
+            if (c >= 0 && gx >= q.cr.x0 && gx <= q.cr.x1 && gy >= q.cr.y0 && gy <= q.cr.y1 &&
+                proj_static(a, i, q, fi, lv) && (!T || T[fi] >= j)) {
+                const int d = hamming32(q0, q1, a.desc + (long long)fi * 32);
+                if (d <= bound) {
+                    key = ((uint32_t)d << 24) | ((uint32_t)c << 12) | (uint32_t)fi;
+                    ent = ((uint32_t)d << 24) | ((uint32_t)(lv & 7) << 16) | (uint32_t)fi;
+                }
+            }
+        }
+        const uint64_t has = __ballot(key != kFusedNone);
+        if (!has) continue;
+        total += __popcll(has);
+        // K smallest of (running list) U (this chunk); keys are distinct
+        uint32_t prev = 0, nrun = kFusedNone, nrun_e = kFusedNone;
+        bool first = true;
+        for (int r = 0; r < K; ++r) {
+            const uint32_t xa = (first || key > prev) ? key : kFusedNone;
+            const uint32_t xb = (lane < K && (first || run > prev)) ? run : kFusedNone;
+            const uint32_t x = min(xa, xb);
+            const uint32_t xe = xa <= xb ? ent : run_e;
+            const uint32_t m = wave_min(x, kFusedNone);
+            if (m == kFusedNone) break;
+            const int src = __ffsll((long long)__ballot(x == m)) - 1;
+            const uint32_t me = (uint32_t)__builtin_amdgcn_readlane((int)xe, src);
+            if (lane == r) { nrun = m; nrun_e = me; }
+            prev = m;
+            first = false;
+        }
+        run = nrun;
+        run_e = nrun_e;
+    }
+    if (lane < K && run_e != kFusedNone && a.mode == 1 && a.check_ori) {
+        const uint32_t bin = (uint32_t)rot_bin(qang, a.kps[run_e & 0xfff].angle);
+        run_e |= bin << 19;                           // (lvl | bin << 3) << 16
+    }
+    return total;
+}
+
+// A decision: -1 none, else slot | blocking << 12 | bin << 13.
+__device__ __forceinline__ int fused_accept(const ProjArgs& a, int best, int lvl, int best2, int lvl2) {
+    if (a.mode == 0) return best <= kThHigh && !(lvl == lvl2 && (float)best > a.ratio * (float)best2);
+    return (float)best <= a.accept;
+}
+
+__global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bound, uint32_t* __restrict__ lists,
+                                                               int* __restrict__ cnt, unsigned* __restrict__ ticket,
+                                                               const int32_t* __restrict__ owner_in,
+                                                               int32_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) int fl[];
+    const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    int* T = fl;
+    int* D = T + n;
+    int* dry = D + nq;
+    int* hist = dry + nq;
+    int* misc = hist + 32;                          // 0 last-block flag, 1 changed, 2 ndry, 3 nm, 4 dropped
+    uint8_t* pre = (uint8_t*)(misc + 8);
+    // ---- phase 1: one wave per query
+    {
+        const int i = blockIdx.x * (kFusedThreads / kWave) + wv;
+        if (i < nq) {
+            ProjQuery q;
+            if (!proj_query(a, i, q)) {
+                if (lane == 0) cnt[i] = -1;
+            } else {
+                uint32_t run, run_e;
+                const int total = fused_select<kProjK>(a, i, q, bound, nullptr, 0, run, run_e);
+                if (lane < kProjK) lists[(long long)i * kProjK + lane] = run_e;
+                if (lane == 0) cnt[i] = total;
+            }
+        }
+    }
+    // ---- the last block to finish phase 1 runs phase 2
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) misc[0] = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!misc[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const int mode = a.mode, skip_any = a.skip_any, ori = a.mode == 1 && a.check_ori;
+    for (int s = tid; s < n; s += kFusedThreads) {
+        const int o = owner_in[s];
+        const bool b = o != -1 && (skip_any || (o <= -2 ? a.blocked[s] != 0 : a.qhas_obs[o] != 0));
+        pre[s] = b;
+        T[s] = b ? -1 : INT_MAX;
+    }
+    for (int j = tid; j < nq; j += kFusedThreads) D[j] = -2;           // "no decision yet"
+    if (tid < 32) hist[tid] = 0;
+    if (tid < 8) misc[tid] = 0;
+    __syncthreads();
+    for (int round = 0; round <= nq; ++round) {
+        // decisions under this round's T.  The thread's lists are read again
+        // each round (L2 hits, every load in flight at once) so they are live
+        // in registers only here, not across the rescans below
+        // (groups of 4 queries: 8 lists in registers at once spill)
+#pragma unroll 1
+        for (int u0 = 0; u0 < kFusedQpt; u0 += 4) {
+        uint4 LA[4], LB[4];
+        int C[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int jj = tid + (u0 + u) * kFusedThreads;
+            const int j = min(jj, max(nq - 1, 0));
+            C[u] = jj < nq ? cnt[j] : -1;
+            LA[u] = ((const uint4*)lists)[(long long)j * 2];
+            LB[u] = ((const uint4*)lists)[(long long)j * 2 + 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int j = tid + (u0 + u) * kFusedThreads;
+            if (j >= nq) continue;
+            const uint32_t L[kProjK] = {LA[u].x, LA[u].y, LA[u].z, LA[u].w, LB[u].x, LB[u].y, LB[u].z, LB[u].w};
+            int dec = -1;
+            if (C[u] > 0) {
+                int best = 256, lvl = -1, slot = -1, bin = 0, best2 = 256, lvl2 = -1, nav = 0;
+#pragma unroll
+                for (int k = 0; k < kProjK; ++k) {
+                    const uint32_t e = L[k];
+                    if (k >= C[u] || e == kFusedNone) continue;
+                    const int s = (int)(e & 0xfff);
+                    if (T[s] < j) continue;
+                    if (nav == 0) {
+                        best = (int)(e >> 24); lvl = (int)((e >> 16) & 7); bin = (int)((e >> 19) & 31); slot = s;
+                    } else if (nav == 1) {
+                        best2 = (int)(e >> 24); lvl2 = (int)((e >> 16) & 7);
+                    }
+                    ++nav;
+                }
+                const bool exact = C[u] <= kProjK || nav >= 2 || (mode == 1 && nav >= 1);
+                if (!exact) {
+                    dec = -3;                                            // made by an exact rescan below
+                    dry[atomicAdd(&misc[2], 1)] = j;
+                } else if (slot >= 0 && fused_accept(a, best, lvl, best2, lvl2)) {
+                    const int hob = skip_any ? 1 : a.qhas_obs[j] != 0;
+                    dec = slot | (hob << 12) | (bin << 13);
+                }
+            }
+            if (dec != -3) {
+                if (dec != D[j]) misc[1] = 1;
+                D[j] = dec;
+            }
+        }
+        }
+        __syncthreads();
+        // exact rescans of the decisions a truncated list could not make: one wave each
+        const int ndry = misc[2];
+        for (int t = wv; t < ndry; t += kFusedThreads / kWave) {
+            const int j = dry[t];
+            ProjQuery q;
+            proj_query(a, j, q);
+            uint32_t run, run_e;
+            fused_select<2>(a, j, q, bound, T, j, run, run_e);
+            const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 0);
+            const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 1);
+            int dec = -1;
+            if (e1 != kFusedNone) {
+                const int best = (int)(e1 >> 24), lvl = (int)((e1 >> 16) & 7);
+                const int best2 = e2 != kFusedNone ? (int)(e2 >> 24) : 256, lvl2 = e2 != kFusedNone ? (int)((e2 >> 16) & 7) : -1;
+                if (fused_accept(a, best, lvl, best2, lvl2)) {
+                    const int hob = skip_any ? 1 : a.qhas_obs[j] != 0;
+                    dec = (int)(e1 & 0xfff) | (hob << 12) | (int)(((e1 >> 19) & 31) << 13);
+                }
+            }
+            if (lane == 0) {
+                if (dec != D[j]) misc[1] = 1;
+                D[j] = dec;
+            }
+        }
+        __syncthreads();
+        const bool changed = misc[1] != 0;
+        __syncthreads();
+        if (!changed) break;
+        // T from this round's decisions: the first blocking claim of each slot
+        for (int s = tid; s < n; s += kFusedThreads) T[s] = pre[s] ? -1 : INT_MAX;
+        if (tid == 0) { misc[1] = 0; misc[2] = 0; }
+        __syncthreads();
+        for (int j = tid; j < nq; j += kFusedThreads) {
+            const int dec = D[j];
+            if (dec >= 0 && (dec >> 12 & 1)) atomicMin(&T[dec & 0xfff], j);
+        }
+        __syncthreads();
+    }
+    // ---- outputs: the last claimer of each slot, nmatches, rotation filter
+    for (int s = tid; s < n; s += kFusedThreads) T[s] = -1;
+    __syncthreads();
+    int nacc = 0;
+    for (int j = tid; j < nq; j += kFusedThreads) {
+        const int dec = D[j];
+        if (dec < 0) continue;
+        ++nacc;
+        atomicMax(&T[dec & 0xfff], j);
+        if (ori) atomicAdd(&hist[(dec >> 13) & 31], 1);
+    }
+    nacc = wave_sum(nacc);
+    if (lane == 0) atomicAdd(&misc[3], nacc);
+    __syncthreads();
+    if (ori) {
+        __shared__ int tm[3];
+        if (tid == 0) three_maxima(hist, tm[0], tm[1], tm[2]);
+        for (int s = tid; s < n; s += kFusedThreads) pre[s] = 0;          // reused: slot cleared
+        __syncthreads();
+        int drop = 0;
+        for (int j = tid; j < nq; j += kFusedThreads) {
+            const int dec = D[j];
+            if (dec < 0) continue;
+            const int b = (dec >> 13) & 31;
+            if (b == tm[0] || b == tm[1] || b == tm[2]) continue;
+            pre[dec & 0xfff] = 1;
+            ++drop;
+        }
+        drop = wave_sum(drop);
+        if (lane == 0) atomicAdd(&misc[4], drop);
+        __syncthreads();
+    }
+    for (int s = tid; s < n; s += kFusedThreads) {
+        const int last = T[s];
+        out[1 + s] = (ori && pre[s]) ? -1 : (last >= 0 ? last : owner_in[s]);
+    }
+    if (tid == 0) {
+        out[0] = misc[3] - misc[4];
+        *ticket = 0u;                                                   // reusable
+    }
+}
+
 // Largest distance that can still decide a query (see k_proj_topk).
 static int proj_bound(const ProjArgs& a) {
     if (a.mode == 1) return a.accept < 0 ? -1 : (int)std::min(255.0f, std::floor(a.accept));
@@ -3661,17 +3943,21 @@ struct DevFrame {
         }
         if (f->u_right && (rc = ur.put(f->u_right, f->n, st))) return rc;
         if (f->scale_factors && (rc = scale.put(f->scale_factors, f->nlevels, st))) return rc;
-        if (grid) {
-            if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1)) || (rc = cs.alloc(kCells + 1))) return rc;
-            if (grid_cs_lds(nn) <= 160 * 1024) {
-                KLAUNCH(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), st, kps.p, n.p, nn,
-                                   grid_params(f), sorted.p, count.p, cs.p, (uint32_t*)nullptr, (int*)nullptr);
-            } else {
-                const int sc = pow2_at_least(nn);
-                KLAUNCH(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
-                                   grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
-                KLAUNCH(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
-            }
+        return grid ? build_grid(f, st) : ORB_OK;
+    }
+    // the frame's grid order and cell-start table (AssignFeaturesToGrid)
+    int build_grid(const orbm_frame* f, hipStream_t st) {
+        int rc;
+        const int nn = std::max(1, f->n);
+        if ((rc = sorted.alloc(nn)) || (rc = count.alloc(1)) || (rc = cs.alloc(kCells + 1))) return rc;
+        if (grid_cs_lds(nn) <= 160 * 1024) {
+            KLAUNCH(k_grid_cs, dim3(1), dim3(256), grid_cs_lds(nn), st, kps.p, n.p, nn,
+                               grid_params(f), sorted.p, count.p, cs.p, (uint32_t*)nullptr, (int*)nullptr);
+        } else {
+            const int sc = pow2_at_least(nn);
+            KLAUNCH(k_grid, dim3(1), dim3(256), sc * sizeof(uint32_t), st, kps.p, n.p, nn,
+                               grid_params(f), sorted.p, count.p, sc, (uint32_t*)nullptr, (int*)nullptr);
+            KLAUNCH(k_cell_start, dim3(1), dim3(256), 0, st, sorted.p, count.p, nn, cs.p);
         }
         return ORB_OK;
     }
@@ -4102,18 +4388,41 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
     return launch_bow(a, map->nkf, (hipStream_t)stream);
 }
 
+// The projection searches' device part.  df holds the uploaded frame (no grid
+// yet).  Default: the fused single-launch form (k_proj_fused) when the frame
+// has <= 4096 keypoints of <= 8 levels and <= 8192 queries -- one coalesced
+// upload, one launch, one download of [nmatches, owner[n]].  Otherwise (or
+// ORB_OPT_PROJ_FORM 1 / 2 / 3: serial phase 2 / single wave / two-phase
+// speculative) the grid is built and the multi-kernel forms run.
 static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* owner, const uint8_t* blocked) {
     int rc;
     DBuf<int32_t> own, nm; DBuf<uint8_t> blk;
-    if ((rc = own.put(owner, std::max(1, f->n))) || (rc = blk.put(blocked, std::max(1, f->n))) || (rc = nm.alloc(1)))
-        return rc;
+    if ((rc = own.put(owner, std::max(1, f->n))) || (rc = blk.put(blocked, std::max(1, f->n)))) return rc;
     a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
-    a.scale = df.scale.p; a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p;
-    a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p; a.nmatches = nm.p;
+    a.scale = df.scale.p; a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p;
+    const int form = debug_opt(ORB_OPT_PROJ_FORM);
+    if (form == 0 && f->n <= kFusedMaxN && a.nq <= kFusedMaxQ && f->nlevels <= 8 &&
+        proj_fused_lds(f->n, a.nq) <= kCuLds) {
+        DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; DBuf<int32_t> out;
+        const unsigned zero = 0;
+        if ((rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, a.nq) * kProjK)) ||
+            (rc = cnt.alloc(std::max(1, a.nq))) || (rc = out.alloc((size_t)f->n + 1)))
+            return rc;
+        a.nmatches = nullptr;
+        const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
+        KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), proj_fused_lds(f->n, a.nq), 0, a, proj_bound(a),
+                lists.p, cnt.p, ticket.p, own.p, out.p);
+        ORB_CHECK(hipGetLastError());
+        std::vector<int32_t> res((size_t)f->n + 1);
+        ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
+        if (f->n) std::memcpy(owner, res.data() + 1, (size_t)f->n * sizeof(int32_t));
+        return res[0];
+    }
+    if ((rc = df.build_grid(f, 0)) || (rc = nm.alloc(1))) return rc;
+    a.gsorted = df.sorted.p; a.gcount = df.count.p; a.cellstart = df.cs.p; a.nmatches = nm.p;
     // two-phase form unless its LDS slot table does not fit; phase 2 speculative
     // unless its table does not fit.  For testing, ORB_OPT_PROJ_FORM 2 forces
     // the single-wave form and 1 the serial phase 2.
-    const int form = debug_opt(ORB_OPT_PROJ_FORM);
     const size_t lds2 = proj_resolve_lds(a.n, a.nq), lds3 = proj_spec_lds(a.n, a.nq);
     if (lds2 <= 160 * 1024 && form != 2) {
         DBuf<uint2> topk; DBuf<int> cnt;
@@ -4141,7 +4450,7 @@ int orbm_search_by_projection_mps(const orbm_frame* f, const orbm_mappoints* mps
     if (device_ok()) return ORB_ERR_DEVICE;
     if (f->n > 0xffff) return ORB_ERR_UNSUPPORTED;
     DevFrame df;
-    int rc = df.upload(f, true, 0);
+    int rc = df.upload(f, false, 0);
     if (rc) return rc;
     const int nq = mps->n;
     DBuf<float> qx, qy, qxr, vc, dp; DBuf<int32_t> lv; DBuf<uint8_t> iv, ho, qd;
@@ -4166,7 +4475,7 @@ int orbm_search_by_projection_last(const orbm_frame* cur, int nlast, const uint8
     if (device_ok()) return ORB_ERR_DEVICE;
     if (cur->n > 0xffff) return ORB_ERR_UNSUPPORTED;
     DevFrame df;
-    int rc = df.upload(cur, true, 0);
+    int rc = df.upload(cur, false, 0);
     if (rc) return rc;
     DBuf<float> qx, qy, qxr, qa; DBuf<int32_t> lv; DBuf<uint8_t> iv, ho, qd;
     if ((rc = qx.put(u, nlast)) || (rc = qy.put(v, nlast)) || (rc = qxr.put(ur, nlast)) ||
@@ -4463,7 +4772,7 @@ static int proj_best_only(const orbm_frame* f, int nq, const uint8_t* valid, con
     orbm_frame fn = *f;
     fn.u_right = nullptr;                       // no stereo gate in these searches
     DevFrame df;
-    if ((rc = df.upload(&fn, true, 0))) return rc;
+    if ((rc = df.upload(&fn, false, 0))) return rc;
     DBuf<float> qx, qy, qa; DBuf<int32_t> lv; DBuf<uint8_t> iv, qd;
     if ((rc = qx.put(u, nq)) || (rc = qy.put(v, nq)) || (rc = lv.put(level, nq)) || (rc = iv.put(valid, nq)) ||
         (rc = qd.put(desc, (size_t)nq * 32)))

@@ -49,10 +49,11 @@ def debug_option():
 
 @pytest.fixture
 def proj_form(debug_option):
-    """Projection-search form by name: spec (top-K + speculative resolve, the
-    default), serial (top-K + serial resolve), single (single-wave search)."""
+    """Projection-search form by name: fused (one launch: brute-force top-K +
+    last-block fixpoint resolve, the default), serial (top-K + serial resolve),
+    single (single-wave search), spec (top-K + speculative resolve)."""
     from orb_slam3_vio_fixes_amd import capi
 
     def set_(name):
-        debug_option(capi.ORB_OPT_PROJ_FORM, {"spec": 0, "serial": 1, "single": 2}[name])
+        debug_option(capi.ORB_OPT_PROJ_FORM, {"fused": 0, "serial": 1, "single": 2, "spec": 3}[name])
     return set_

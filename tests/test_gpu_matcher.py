@@ -90,7 +90,7 @@ def projection_queries(frames, seed, n=600):
     return rng, src, cur, k, qx.astype(np.float32), qy.astype(np.float32)
 
 
-@pytest.mark.parametrize("single", ["spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
 def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, proj_form):
     proj_form(single)
@@ -114,7 +114,7 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, 
     np.testing.assert_array_equal(own, rown)
 
 
-@pytest.mark.parametrize("single", ["spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
 def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, proj_form):
     proj_form(single)
@@ -134,8 +134,8 @@ def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, singl
     np.testing.assert_array_equal(own, rown)
 
 
-@pytest.mark.parametrize("single", ["spec", "serial", "single"])
-@pytest.mark.parametrize("seed,reps", [(21, 2), (22, 3), (23, 4)])
+@pytest.mark.parametrize("single", ["fused", "spec", "serial", "single"])
+@pytest.mark.parametrize("seed,reps", [(21, 2), (22, 3), (23, 4), (24, 12)])
 def test_search_by_projection_overlapping_lists(gpu_lib, frames, seed, reps, single, proj_form):
     """Queries repeated `reps` times (consecutive and far apart in the query
     order, positions jittered, a few descriptor bits flipped) so that candidate
