@@ -119,6 +119,8 @@ def parse():
     ap.add_argument("--per-kf", type=int, default=5000, help="c5: features per keyframe (of the query's ~5008)")
     ap.add_argument("--valid-frac", type=float, default=1.0,
                     help="c5: share of keyframe features with a valid MapPoint (the stated map: 1.0)")
+    ap.add_argument("--near-frac", type=float, default=1.0,
+                    help="c5: share of keyframes near the query (1.0: the stated map; 0.1: mostly far keyframes)")
     return ap.parse_args()
 
 
@@ -137,7 +139,7 @@ def other_workload(args):
         return bench_stereo.run_c3(a) if args.workload == "c3" else bench_stereo.run_c4(a)
     import bench_c5
     # the oracle checks every keyframe of rank 0's shard (a threaded map loop: a few seconds)
-    a = types.SimpleNamespace(nkf=args.nkf, per_kf=args.per_kf, valid_frac=args.valid_frac,
+    a = types.SimpleNamespace(nkf=args.nkf, per_kf=args.per_kf, valid_frac=args.valid_frac, near_frac=args.near_frac,
                               reps=args.steps, warmup=args.warmup,
                               cpu_sample=-1 if args.cpu_sample > 0 else 0,
                               cpu_threads=args.cpu_threads or min(16, len(os.sched_getaffinity(0))))

@@ -174,7 +174,8 @@ def vocabulary(k: int = 10, levels: int = 6, seed: int = 5):
 
 
 def keyframe_map(kps: np.ndarray, desc: np.ndarray, node_of_feature: np.ndarray, ids, seed: int = 7,
-                 per_kf: int | None = None, valid_frac: float = 1.0) -> dict:
+                 per_kf: int | None = None, valid_frac: float = 1.0, near_frac: float = 1.0,
+                 far_nodes: int = 30) -> dict:
     """A synthetic keyframe map around a query frame (config C5, SURVEY.md
     §8(d)), packed in the orbm_kf_map_device layout (kfmap.pack).  Keyframe i
     (ids: the map's keyframe ids, so any shard of the map is the same data)
@@ -182,7 +183,15 @@ def keyframe_map(kps: np.ndarray, desc: np.ndarray, node_of_feature: np.ndarray,
     extractor's ~5008) with their node ids, descriptors with 2^-3, 2^-4 or 2^-5
     of their bits flipped, angles jittered (+30 degrees for every 7th keyframe,
     so the rotation filter drops matches), and MapPoints valid with
-    probability valid_frac (1.0: all valid, as SURVEY §8(d) states C5)."""
+    probability valid_frac (1.0: all valid, as SURVEY §8(d) states C5).
+
+    near_frac < 1 makes the relocalisation case (Tracking.cc:3609-3662) of a
+    map mostly from elsewhere: a keyframe is "near" (as above) with
+    probability near_frac, otherwise "far": per_kf features with unrelated
+    random descriptors whose node ids come from a keyframe-specific set of
+    far_nodes of the query's level-(L - levelsup) nodes and nodes the query
+    does not hold (ids just past its largest), so it shares a minority of its
+    nodes with the query and almost no match passes TH_LOW."""
     from . import kfmap
     n = len(kps)
     m = n if per_kf is None else min(per_kf, n)
@@ -205,18 +214,30 @@ def keyframe_map(kps: np.ndarray, desc: np.ndarray, node_of_feature: np.ndarray,
         for _ in range(ands - 1):
             p &= np.frombuffer(prng.bytes(p.size), np.uint8).reshape(-1, 32)
         pools.append(p)
+    qnodes = np.unique(nid_all[nid_all >= 0])
+    hi = int(qnodes.max()) + 1 if len(qnodes) else 1
+    other = np.arange(hi, hi + max(len(qnodes), far_nodes), dtype=np.int64)   # nodes the query lacks
     for j, i in enumerate(ids):
         rng = np.random.default_rng(seed * 1_000_003 + int(i))
         sel = np.sort(rng.permutation(n)[:m])
         kk = out_k[j]
         kb[j] = kps_b[sel]
-        kk["angle"] = (kk["angle"] + rng.normal(0, 4, m).astype(np.float32) + (30 if i % 7 == 0 else 0)) % 360
-        r = int(rng.integers(0, 3))
-        s0 = int(rng.integers(0, len(pools[r]) - m + 1))
-        np.bitwise_xor(desc[sel], pools[r][s0:s0 + m], out=out_d[j])
+        far = near_frac < 1.0 and rng.random() >= near_frac
+        if far:
+            kk["angle"] = rng.uniform(0, 360, m).astype(np.float32)
+            out_d[j] = np.frombuffer(rng.bytes(m * 32), np.uint8).reshape(m, 32)
+            shared = rng.choice(qnodes, size=min(len(qnodes), far_nodes // 3), replace=False)
+            pool = np.concatenate([shared, rng.choice(other, size=far_nodes - len(shared), replace=False)])
+            nid_kf = pool[rng.integers(0, len(pool), m)]
+        else:
+            kk["angle"] = (kk["angle"] + rng.normal(0, 4, m).astype(np.float32) + (30 if i % 7 == 0 else 0)) % 360
+            r = int(rng.integers(0, 3))
+            s0 = int(rng.integers(0, len(pools[r]) - m + 1))
+            np.bitwise_xor(desc[sel], pools[r][s0:s0 + m], out=out_d[j])
+            nid_kf = nid_all[sel]
         if valid_frac < 1.0:
             out_v[j] = rng.random(m) < valid_frac
-        n_ids, o, ix = kfmap.featvec_csr(nid_all[sel])
+        n_ids, o, ix = kfmap.featvec_csr(nid_kf)
         nodes.append(n_ids)
         offs.append(o)
         idx_off.append(nidx)

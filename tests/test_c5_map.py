@@ -67,3 +67,31 @@ def test_oracle_map_loop_equals_per_keyframe_search():
                                       f, fv, 0.75, True)
         assert nm[i] == rnm and rnm > 50
         np.testing.assert_array_equal(match[i], rmatch)
+
+
+def test_low_overlap_map_shards_and_near_fraction():
+    """synth.keyframe_map(near_frac < 1): a keyframe's data depends on its id
+    alone (so map shards are the same data), ~near_frac of the keyframes are
+    near the query (hundreds of matches), the far ones match almost nothing
+    and share only part of their nodes with the query (oracle as checker)."""
+    import numpy as np
+    from oracle import oracle as O
+    from orb_slam3_vio_fixes_amd import abi, synth
+    rng = np.random.default_rng(1)
+    n = 600
+    k = np.zeros(n, abi.KEYPOINT_DTYPE)
+    k["x"], k["y"], k["angle"] = rng.uniform(0, 640, n), rng.uniform(0, 480, n), rng.uniform(0, 360, n)
+    d = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    nid = rng.integers(11, 111, n)
+    full = synth.keyframe_map(k, d, nid, range(60), seed=9, near_frac=0.25)
+    part = synth.keyframe_map(k, d, nid, range(30, 60), seed=9, near_frac=0.25)
+    off = int(full["kp_off"][30])
+    assert np.array_equal(full["desc"][off * 32:], part["desc"]) and np.array_equal(full["fv_idx"][-len(part["fv_idx"]):], part["fv_idx"])
+    _, rn = O.search_by_bow_map(full, abi.frame_struct(k, d, 640, 480), abi.featvec_struct(nid), 0.75, True, nthreads=4)
+    near = rn > 100
+    assert 5 <= near.sum() <= 30 and rn[~near].max() < 10
+    qn = set(np.unique(nid).tolist())
+    for i in np.nonzero(~near)[0][:5]:
+        nodes = full["fv_node"][full["fv_node_off"][i]:full["fv_node_off"][i + 1]]
+        shared = sum(int(x) in qn for x in nodes)
+        assert 0 < shared < len(nodes)

@@ -224,3 +224,26 @@ def test_c5_full_map_every_keyframe(gpu_lib, c5_full, variant, debug_option):
     np.testing.assert_array_equal(nm, rnm)
     np.testing.assert_array_equal(match.cpu().numpy(), rmatch)
     assert rnm.min() > 100
+
+
+def test_c5_low_overlap_map_every_keyframe(gpu_lib, c5):
+    """The relocalisation case of Tracking.cc:3609-3662 on a map mostly from
+    elsewhere: 10,000 keyframes x 5000 features of which only ~10 % are near
+    the query (synth.keyframe_map near_frac 0.1); the far ones hold unrelated
+    descriptors in node sets that share a minority of nodes with the query.
+    The map-wide search == the oracle for EVERY keyframe (row and count),
+    default form and k_bow."""
+    k, d, voc = c5
+    fnode = orb.transform(voc, d, 4)[2]
+    a = synth.keyframe_map(k, d, fnode, range(10000), seed=9, per_kf=5000, near_frac=0.1)
+    f, fv = abi.frame_struct(k, d, 1920, 1080), abi.featvec_struct(fnode)
+    rmatch, rnm = O.search_by_bow_map(a, f, fv, 0.75, True, nthreads=16)
+    near = rnm > 100
+    assert 800 < near.sum() < 1200 and np.median(rnm[~near]) < 5
+    m = kfmap.DeviceKeyframeMap(arrays=a)
+    import contextlib
+    for form in (0, 1):
+        with capi.debug_option(capi.ORB_OPT_BOW_FORM, form) if form else contextlib.nullcontext():
+            match, nm = m.search_by_bow(k, d, fnode, 0.75, True)
+            np.testing.assert_array_equal(nm.cpu().numpy(), rnm)
+            np.testing.assert_array_equal(match.cpu().numpy(), rmatch)

@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--per-kf", type=int, default=5000)
     ap.add_argument("--valid-frac", type=float, default=1.0,
                     help="share of keyframe features with a valid MapPoint (1.0: the stated C5 map)")
+    ap.add_argument("--near-frac", type=float, default=1.0,
+                    help="share of keyframes near the query (1.0: the stated map; e.g. 0.1: a relocalisation map "
+                         "mostly from elsewhere, synth.keyframe_map)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="keyframes the oracle checks (-1: all)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--gpus", type=int, default=1,
@@ -110,7 +113,8 @@ def run_c5(args):
     ids = list(sharding.shard(args.nkf, rank, world))
     t0 = time.perf_counter()
     arrays = synth.keyframe_map(k, d, nid, ids, seed=7, per_kf=args.per_kf,
-                                valid_frac=getattr(args, "valid_frac", 1.0))
+                                valid_frac=getattr(args, "valid_frac", 1.0),
+                                near_frac=getattr(args, "near_frac", 1.0))
     m = kfmap.DeviceKeyframeMap(arrays=arrays)
     build_s = time.perf_counter() - t0
     nfeat_kf = int(arrays["kp_off"][-1])
@@ -165,7 +169,8 @@ def run_c5(args):
     res = {"metric": "C5 map-wide SearchByBoW: keyframe pairs/s (1920x1080, 5000 feat, 10k-KF map)",
            "value": args.nkf * args.reps / el, "unit": "keyframe-pairs/s", "queries_per_s": args.reps / el,
            "ms_per_query": el / args.reps * 1e3, "n_gpus": world, "nkf": args.nkf, "features": int(len(k)),
-           "kf_features_total": nfeat_kf * world, "mappoints_valid_frac": float(arrays["valid"].mean()), "data": "synthetic",
+           "kf_features_total": nfeat_kf * world, "mappoints_valid_frac": float(arrays["valid"].mean()),
+           "near_frac": getattr(args, "near_frac", 1.0), "data": "synthetic",
            "ms_per_query_with_frame_upload": upload_ms,
            "timed": "map-wide search, query frame resident in HBM (prepare_frame before the timed region)",
            "map_build_s_rank0": build_s, "mean_matches": float(nm.float().mean().item()),
