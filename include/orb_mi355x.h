@@ -427,6 +427,11 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
  * or ORB_ERR_DEVICE if a set's stream reported an error (that set is kept). */
 int orbm_release_scratch(void* stream, int all);
 
+/* Test hook: statistics of the calling thread's last projection search that
+ * took the fused form (ORB_OPT_PROJ_FORM 0): fixpoint rounds, exact rescans,
+ * and the last block's phase-1 and phase-2 shader clocks (s_memtime ticks). */
+int orbm_debug_proj_stats(int32_t* out4);
+
 /* Map points projected into F (the fields ORBmatcher reads from MapPoint,
  * MapPoint.h mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos, mbTrackInView,
  * isBad(), GetDescriptor(), Observations()). */

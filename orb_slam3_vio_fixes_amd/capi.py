@@ -28,7 +28,7 @@ EXPORTS = [
     "orbm_search_by_sim3", "orbm_fuse_sim3", "orbm_search_by_bow_fisheye", "orbm_search_by_projection_mps_fisheye",
     "orbm_search_by_projection_last_fisheye", "orbx_set_pyramid_mode", "orbx_pyramid_kernel", "orbv_transform_device",
     "orbx_set_stage_event", "orb_debug_set_option", "orb_debug_get_option",
-    "orbm_release_scratch", "orbx_debug_pretest", "orbx_debug_plan_info",
+    "orbm_release_scratch", "orbm_debug_proj_stats", "orbx_debug_pretest", "orbx_debug_plan_info",
 ]
 
 # orb_debug_set_option keys (include/orb_mi355x.h): alternative kernel forms
@@ -77,6 +77,7 @@ def load(path: Path | str = LIB_PATH):
     L.orb_debug_set_option.argtypes = [i32, i32]
     L.orb_debug_get_option.argtypes = [i32]
     L.orbm_release_scratch.argtypes = [vp, i32]
+    L.orbm_debug_proj_stats.argtypes = [vp]
     L.orbx_debug_pretest.argtypes = [vp, i32, i32, vp, sz, vp]
     L.orbx_debug_plan_info.argtypes = [vp, i32, i32, vp, i32]
     L.orbm_compute_distinctive_descriptors.argtypes = [i32, vp, vp, vp, i32]

@@ -3174,6 +3174,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                                                                int32_t* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
     int* T = fl;
     int* D = T + n;
     int* dry = D + nq;
@@ -3202,7 +3203,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     __syncthreads();
     if (!misc[0]) return;
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const int mode = a.mode, skip_any = a.skip_any, ori = a.mode == 1 && a.check_ori;
+    int rounds = 0, ndry_total = 0;
     for (int s = tid; s < n; s += kFusedThreads) {
         const int o = owner_in[s];
         const bool b = o != -1 && (skip_any || (o <= -2 ? a.blocked[s] != 0 : a.qhas_obs[o] != 0));
@@ -3269,6 +3272,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         __syncthreads();
         // exact rescans of the decisions a truncated list could not make: one wave each
         const int ndry = misc[2];
+        ++rounds;
+        ndry_total += ndry;
         for (int t = wv; t < ndry; t += kFusedThreads / kWave) {
             const int j = dry[t];
             ProjQuery q;
@@ -3344,6 +3349,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     if (tid == 0) {
         out[0] = misc[3] - misc[4];
         *ticket = 0u;                                                   // reusable
+        // statistics after the owner row (orbm_debug_proj_stats): rounds, exact
+        // rescans, phase-1 and phase-2 shader clocks of the last block
+        out[n + 1] = rounds;
+        out[n + 2] = ndry_total;
+        out[n + 3] = (int)min(t1 - t0, 0x7fffffffull);
+        out[n + 4] = (int)min(__builtin_amdgcn_s_memtime() - t1, 0x7fffffffull);
     }
 }
 
@@ -3963,6 +3974,9 @@ struct DevFrame {
     }
 };
 
+// the last fused projection search's statistics (orbm_debug_proj_stats)
+static int32_t* proj_stats() { static thread_local int32_t st[4] = {0, 0, 0, 0}; return st; }
+
 // Start of a synchronous host-API call: a device must be present; the call's
 // arenas start empty.
 static int device_ok() {
@@ -4042,6 +4056,12 @@ int orb_debug_get_option(int option) {
     return option >= 0 && option < ORB_OPT_COUNT ? g_debug_opt[option].load(std::memory_order_relaxed) : -1;
 }
 
+
+int orbm_debug_proj_stats(int32_t* out4) {
+    if (!out4) return ORB_ERR_PARAM;
+    std::memcpy(out4, proj_stats(), 4 * sizeof(int32_t));
+    return ORB_OK;
+}
 
 int orbm_descriptor_distance(const uint8_t* a, const uint8_t* b) {
     // host inline utility (Frame.cc:886, MapPoint.cc:377 call it on single pairs)
@@ -4406,16 +4426,17 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
         DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; DBuf<int32_t> out;
         const unsigned zero = 0;
         if ((rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, a.nq) * kProjK)) ||
-            (rc = cnt.alloc(std::max(1, a.nq))) || (rc = out.alloc((size_t)f->n + 1)))
+            (rc = cnt.alloc(std::max(1, a.nq))) || (rc = out.alloc((size_t)f->n + 5)))
             return rc;
         a.nmatches = nullptr;
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), proj_fused_lds(f->n, a.nq), 0, a, proj_bound(a),
                 lists.p, cnt.p, ticket.p, own.p, out.p);
         ORB_CHECK(hipGetLastError());
-        std::vector<int32_t> res((size_t)f->n + 1);
+        std::vector<int32_t> res((size_t)f->n + 5);
         ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
         if (f->n) std::memcpy(owner, res.data() + 1, (size_t)f->n * sizeof(int32_t));
+        std::memcpy(proj_stats(), res.data() + f->n + 1, 4 * sizeof(int32_t));
         return res[0];
     }
     if ((rc = df.build_grid(f, 0)) || (rc = nm.alloc(1))) return rc;

@@ -122,6 +122,18 @@ int main(int argc, char** argv)
     };
     const orbm_frame F1 = frame(k1, d1, n1), F2 = frame(k2, d2, n2);
     std::string json = "{";
+    // the product's last fused projection search: rounds, rescans, phase clocks
+    typedef int (*StatFn)(int32_t*);
+    StatFn statfn = (StatFn)dlsym(lib, "orbm_debug_proj_stats");
+    std::string extra;
+    auto stats = [&](const char* name) {
+        int32_t st[4];
+        if (!statfn || statfn(st) != 0) return;
+        char b[200];
+        std::snprintf(b, sizeof b, ", \"%s_stats\": {\"rounds\": %d, \"rescans\": %d, \"phase1_clk\": %d, "
+                      "\"phase2_clk\": %d}", name, st[0], st[1], st[2], st[3]);
+        extra += b;
+    };
     auto put = [&](const char* name, const Stat& s) {
         char b[160];
         std::snprintf(b, sizeof b, "%s\"%s\": {\"median_us\": %.2f, \"mean_us\": %.2f}", json.size() > 1 ? ", " : "",
@@ -168,6 +180,7 @@ int main(int argc, char** argv)
             check(nm, "SearchByProjection(F, LastFrame)");
         });
         put("search_by_projection_last", s);
+        stats("search_by_projection_last");
         owner.resize(n2);
         owner.push_back(nm);
         save(pre + "_last.bin", owner.data(), owner.size());
@@ -193,6 +206,7 @@ int main(int argc, char** argv)
             check(nm, "SearchByProjection(F, MapPoints)");
         });
         put("search_by_projection_mps", s);
+        stats("search_by_projection_mps");
         owner.resize(n2);
         owner.push_back(nm);
         save(pre + "_mps.bin", owner.data(), owner.size());
@@ -220,7 +234,7 @@ int main(int argc, char** argv)
         match.push_back(nm);
         save(pre + "_bow.bin", match.data(), match.size());
     }
-    json += "}";
+    json += extra + "}";
     std::printf("%s\n", json.c_str());
     return 0;
 }
