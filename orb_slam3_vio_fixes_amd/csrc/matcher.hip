@@ -3097,9 +3097,12 @@ constexpr int kFusedMaxN = 4096;                    // 12-bit keypoint index in 
 constexpr int kFusedMaxQ = kFusedThreads * kFusedQpt;
 constexpr uint32_t kFusedNone = 0xffffffffu;
 
-// LDS: T[n] | D[nq] (decision per query) | dry[nq] | hist[32] | misc[8] | pre[n] bytes
-static size_t proj_fused_lds(int n, int nq) {
-    return (size_t)(n + 2 * nq + 32 + 8) * 4 + ((size_t)n + 15) / 16 * 16;
+// LDS: T[n] | D[nq] (decision per query) | dry[nq] | hist[32] | misc[8] |
+// pre[n] bytes | (lds_lists) C[nq] and the lists, kProjK words per query
+static size_t proj_fused_lds(int n, int nq, bool lds_lists) {
+    size_t b = (size_t)(n + 2 * nq + 32 + 8) * 4 + ((size_t)n + 15) / 16 * 16;
+    if (lds_lists) b += (size_t)nq * 4 + (size_t)nq * kProjK * 4;
+    return b;
 }
 
 // The kProjK (or 2 for a rescan) smallest 32-bit keys of query i's candidates
@@ -3116,20 +3119,42 @@ __device__ int fused_select(const ProjArgs& a, int i, const ProjQuery& q, int bo
     run = kFusedNone;
     run_e = kFusedNone;
     int total = 0;
+    // x, y, octave of the next chunk's keypoints are in flight while this
+    // chunk is tested (the scan is a chain of L2 round trips otherwise)
+    const float* kf = (const float*)a.kps;
+    const int kw = (int)(sizeof(orb_keypoint) / 4);
+    auto kload = [&](int base, float& x, float& y, int& o) {
+        const int fi = min(base + lane, max(a.n - 1, 0));
+        x = kf[(long long)fi * kw + 0];
+        y = kf[(long long)fi * kw + 1];
+        o = ((const int*)kf)[(long long)fi * kw + 5];
+    };
+    float nx = 0.f, ny = 0.f;
+    int no = 0;
+    if (a.n > 0) kload(0, nx, ny, no);
     for (int base = 0; base < a.n; base += kWave) {
+        const float kx = nx, ky = ny;
+        const int ko = no;
+        if (base + kWave < a.n) kload(base + kWave, nx, ny, no);
         const int fi = base + lane;
         uint32_t key = kFusedNone, ent = kFusedNone;
         if (fi < a.n) {
-            const orb_keypoint k = a.kps[fi];
-            const int c = grid_cell(k, a.g);
-            const int gx = c / kGridRows, gy = c - gx * kGridRows;
-            int lv;
-            if (c >= 0 && gx >= q.cr.x0 && gx <= q.cr.x1 && gy >= q.cr.y0 && gy <= q.cr.y1 &&
-                proj_static(a, i, q, fi, lv) && (!T || T[fi] >= j)) {
+            // PosInGrid (Frame.cc:725-735) and the cell range the window visits
+            const int gx = (int)roundf((kx - a.g.min_x) * a.g.inv_w);
+            const int gy = (int)roundf((ky - a.g.min_y) * a.g.inv_h);
+            const bool in_cells = gx >= q.cr.x0 && gx <= q.cr.x1 && gy >= q.cr.y0 && gy <= q.cr.y1 &&
+                                  gx < kGridCols && gy < kGridRows && gx >= 0 && gy >= 0;
+            // proj_static: level range, window, stereo gate
+            bool ok = in_cells;
+            if ((q.minL > 0) || (q.maxL >= 0)) ok = ok && ko >= q.minL && !(q.maxL >= 0 && ko > q.maxL);
+            ok = ok && fabsf(kx - q.x) < q.r && fabsf(ky - q.y) < q.r;
+            if (ok && a.u_right && a.u_right[fi] > 0 && fabsf(a.qxr[i] - a.u_right[fi]) > q.r) ok = false;
+            if (ok && (!T || T[fi] >= j)) {
                 const int d = hamming32(q0, q1, a.desc + (long long)fi * 32);
                 if (d <= bound) {
+                    const int c = gx * kGridRows + gy;
                     key = ((uint32_t)d << 24) | ((uint32_t)c << 12) | (uint32_t)fi;
-                    ent = ((uint32_t)d << 24) | ((uint32_t)(lv & 7) << 16) | (uint32_t)fi;
+                    ent = ((uint32_t)d << 24) | ((uint32_t)(ko & 7) << 16) | (uint32_t)fi;
                 }
             }
         }
@@ -3171,7 +3196,7 @@ __device__ __forceinline__ int fused_accept(const ProjArgs& a, int best, int lvl
 __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bound, uint32_t* __restrict__ lists,
                                                                int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                                const int32_t* __restrict__ owner_in,
-                                                               int32_t* __restrict__ out) {
+                                                               int32_t* __restrict__ out, int lds_lists) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
@@ -3179,8 +3204,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     int* D = T + n;
     int* dry = D + nq;
     int* hist = dry + nq;
-    int* misc = hist + 32;                          // 0 last-block flag, 1 changed, 2 ndry, 3 nm, 4 dropped
+    int* misc = hist + 32;          // 0 last-block flag, 1 first changed query, 2 ndry, 3 nm, 4 dropped, 5 settled prefix
     uint8_t* pre = (uint8_t*)(misc + 8);
+    int* Cs = (int*)(pre + ((n + 15) / 16 * 16));
+    uint32_t* Ls = (uint32_t*)(Cs + nq);
     // ---- phase 1: one wave per query
     {
         const int i = blockIdx.x * (kFusedThreads / kWave) + wv;
@@ -3213,30 +3240,38 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         T[s] = b ? -1 : INT_MAX;
     }
     for (int j = tid; j < nq; j += kFusedThreads) D[j] = -2;           // "no decision yet"
+    if (lds_lists) {
+        for (int j = tid; j < nq; j += kFusedThreads) Cs[j] = cnt[j];
+        for (int e = tid; e < nq * (kProjK / 4); e += kFusedThreads) ((uint4*)Ls)[e] = ((const uint4*)lists)[e];
+    }
     if (tid < 32) hist[tid] = 0;
     if (tid < 8) misc[tid] = 0;
+    if (tid == 0) misc[1] = nq;
     __syncthreads();
+    const uint4* Lsrc = lds_lists ? (const uint4*)Ls : (const uint4*)lists;
+    const int* Csrc = lds_lists ? Cs : cnt;
+    int settled = 0;          // queries below it decided the same in the last two rounds: final
     for (int round = 0; round <= nq; ++round) {
-        // decisions under this round's T.  The thread's lists are read again
-        // each round (L2 hits, every load in flight at once) so they are live
-        // in registers only here, not across the rescans below
-        // (groups of 4 queries: 8 lists in registers at once spill)
+        // decisions under this round's T, queries >= settled only (an earlier
+        // query's decision reads only claims of queries before it, all final).
+        // Groups of 4 queries per thread: 8 lists in registers at once spill
 #pragma unroll 1
         for (int u0 = 0; u0 < kFusedQpt; u0 += 4) {
+        if (tid + u0 * kFusedThreads >= nq) break;
         uint4 LA[4], LB[4];
         int C[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int jj = tid + (u0 + u) * kFusedThreads;
             const int j = min(jj, max(nq - 1, 0));
-            C[u] = jj < nq ? cnt[j] : -1;
-            LA[u] = ((const uint4*)lists)[(long long)j * 2];
-            LB[u] = ((const uint4*)lists)[(long long)j * 2 + 1];
+            C[u] = (jj < nq && jj >= settled) ? Csrc[j] : -1;
+            LA[u] = Lsrc[(long long)j * 2];
+            LB[u] = Lsrc[(long long)j * 2 + 1];
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int j = tid + (u0 + u) * kFusedThreads;
-            if (j >= nq) continue;
+            if (j >= nq || j < settled) continue;
             const uint32_t L[kProjK] = {LA[u].x, LA[u].y, LA[u].z, LA[u].w, LB[u].x, LB[u].y, LB[u].z, LB[u].w};
             int dec = -1;
             if (C[u] > 0) {
@@ -3264,7 +3299,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                 }
             }
             if (dec != -3) {
-                if (dec != D[j]) misc[1] = 1;
+                if (dec != D[j]) atomicMin(&misc[1], j);
                 D[j] = dec;
             }
         }
@@ -3292,17 +3327,18 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                 }
             }
             if (lane == 0) {
-                if (dec != D[j]) misc[1] = 1;
+                if (dec != D[j]) atomicMin(&misc[1], j);
                 D[j] = dec;
             }
         }
         __syncthreads();
-        const bool changed = misc[1] != 0;
+        const int first_changed = misc[1];
         __syncthreads();
-        if (!changed) break;
+        if (first_changed >= nq) break;
+        settled = first_changed;
         // T from this round's decisions: the first blocking claim of each slot
         for (int s = tid; s < n; s += kFusedThreads) T[s] = pre[s] ? -1 : INT_MAX;
-        if (tid == 0) { misc[1] = 0; misc[2] = 0; }
+        if (tid == 0) { misc[1] = nq; misc[2] = 0; }
         __syncthreads();
         for (int j = tid; j < nq; j += kFusedThreads) {
             const int dec = D[j];
@@ -4422,7 +4458,9 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     a.scale = df.scale.p; a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p;
     const int form = debug_opt(ORB_OPT_PROJ_FORM);
     if (form == 0 && f->n <= kFusedMaxN && a.nq <= kFusedMaxQ && f->nlevels <= 8 &&
-        proj_fused_lds(f->n, a.nq) <= kCuLds) {
+        proj_fused_lds(f->n, a.nq, false) <= kCuLds) {
+        // the lists in LDS for phase 2 when they fit (else read from L2 each round)
+        const int lds_lists = proj_fused_lds(f->n, a.nq, true) <= kCuLds;
         DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; DBuf<int32_t> out;
         const unsigned zero = 0;
         if ((rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, a.nq) * kProjK)) ||
@@ -4430,8 +4468,8 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
             return rc;
         a.nmatches = nullptr;
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
-        KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), proj_fused_lds(f->n, a.nq), 0, a, proj_bound(a),
-                lists.p, cnt.p, ticket.p, own.p, out.p);
+        KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), proj_fused_lds(f->n, a.nq, lds_lists != 0), 0, a,
+                proj_bound(a), lists.p, cnt.p, ticket.p, own.p, out.p, lds_lists);
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)f->n + 5);
         ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
