@@ -696,8 +696,15 @@ def main():
                 rnm, rm12 = nms[i]
                 if mh[i] != rnm or not np.array_equal(m12h[i][:len(rm12)], rm12):
                     bad_m += 1
+            nproc = os.cpu_count() or avail
             out["cpu_baseline"] = {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
-                                   "cores_available": avail, "flags": flags,
+                                   "cores_available": avail, "host_cpus_nproc": nproc,
+                                   "cores_note": ("all host cores this job may use: the pool's per-GPU CPU share "
+                                                  f"({threads} threads; nproc reports {nproc} on the shared host). "
+                                                  "all_cores_linear_estimate scales the measured per-thread rate to "
+                                                  "nproc -- an upper bound, not a measurement"),
+                                   "per_thread_fps": fps / threads,
+                                   "all_cores_linear_estimate": fps / threads * nproc, "flags": flags,
                                    "library": os.path.relpath(lib_path, ROOT),
                                    "single_thread_fps": fps1, "single_thread_frames": n1,
                                    "sample": f"first {ns} frames of the step batch: extraction + SearchForInitialization "

@@ -1490,6 +1490,9 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #ifndef ORB_FAST_PIPE
 #define ORB_FAST_PIPE 0   // 1: pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
 #endif
+#ifndef ORB_FAST_INC
+#define ORB_FAST_INC 1    // pre-test item (row, pair) advanced by a carry per round (0: divided per round)
+#endif
 #ifndef ORB_QT_LEVEL_MAJOR
 #define ORB_QT_LEVEL_MAJOR 1
 #endif
@@ -1873,12 +1876,36 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             PreIn pq{};
             if (nitems > 0) pre_load(lane, pq);
 #endif
+#if ORB_FAST_INC
+            // the lane's item (row rr, pair kk) advanced by 64 items a round
+            // (a carry instead of a float-reciprocal division per round); lanes
+            // past the end take the last item (branch-free, flags cleared)
+            int rr = 0, kk = 0, rl = 0, kl = 0, sr = 0, sk = 0;
+            if (nitems > 0) {
+                rr = div_row(lane, inv_ndp);
+                kk = lane - (int)__umul24(rr, ndp);
+                rl = div_row(nitems - 1, inv_ndp);
+                kl = nitems - 1 - (int)__umul24(rl, ndp);
+                sr = div_row(kWave, inv_ndp);
+                sk = kWave - (int)__umul24(sr, ndp);
+            }
+#endif
             for (int base = 0; base < nitems; base += kWave) {
                 uint32_t bl, bh, dl, dh;
 #if ORB_FAST_PIPE
                 const PreIn cq = pq;
                 if (base + kWave < nitems) pre_load(base + kWave + lane, pq);
                 pre_eval(cq, base + lane < nitems, bl, bh, dl, dh);
+#elif ORB_FAST_INC
+                {
+                    const bool ok = base + lane < nitems;
+                    int i0;
+                    pretest_rk(ok, ok ? rr : rl, ok ? kk : kl, bl, bh, dl, dh, i0);
+                    (void)i0;
+                    kk += sk;
+                    rr += sr;
+                    if (kk >= ndp) { kk -= ndp; ++rr; }
+                }
 #else
                 int i0;
                 pretest(base + lane, bl, bh, dl, dh, i0);
