@@ -574,6 +574,8 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
                 c.cols = (int)maxX - c.x0; c.rows = (int)maxY - c.y0;
                 c.slot_off = slotsum;
                 c.cap = cap;
+                c.pitch = l == 0 ? 0 : P.lv[l].pitch;
+                c.roi_off = l == 0 ? 0 : (int)(P.lv[l].off + (long long)c.y0 * P.lv[l].pitch + (c.x0 & ~3));
                 // the FAST window (the ROI less its 3-px border): union per level
                 P.win_y0[l] = std::min(P.win_y0[l], c.y0 + 3);
                 P.win_y1[l] = std::max(P.win_y1[l], c.y0 + c.rows - 3);
@@ -1493,6 +1495,9 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #ifndef ORB_FAST_INC
 #define ORB_FAST_INC 1    // pre-test item (row, pair) advanced by a carry per round (0: divided per round)
 #endif
+#ifndef ORB_FAST_CELLOFF
+#define ORB_FAST_CELLOFF 1   // ROI address from the cell record alone (0: through the level table)
+#endif
 #ifndef ORB_QT_LEVEL_MAJOR
 #define ORB_QT_LEVEL_MAJOR 1
 #endif
@@ -1616,14 +1621,25 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
         CellDev r;
         r.level = cells[i].level; r.x0 = cells[i].x0; r.y0 = cells[i].y0; r.cols = cells[i].cols;
         r.rows = cells[i].rows; r.slot_off = cells[i].slot_off; r.cap = cells[i].cap;
+        r.roi_off = cells[i].roi_off; r.pitch = cells[i].pitch;
         return r;
     };
     auto fetch_of = [&](const CellDev& c, int it) {
         const int f = bframe;
         RoiFetch rf;
+#if ORB_FAST_CELLOFF
+        if (c.level == 0) {
+            rf.pitch = a.in_pitch;
+            rf.src = a.in + f * a.in_fstride + (long long)c.y0 * rf.pitch + (c.x0 & ~3);
+        } else {
+            rf.pitch = c.pitch;
+            rf.src = a.pyr + f * a.pyr_fstride + c.roi_off;
+        }
+#else
         if (c.level == 0) { rf.src = a.in + f * a.in_fstride; rf.pitch = a.in_pitch; }
         else { rf.src = a.pyr + f * a.pyr_fstride + lvc[c.level].off; rf.pitch = lvc[c.level].pitch; }
         rf.src += (long long)c.y0 * rf.pitch + (c.x0 & ~3);
+#endif
         rf.nd = max(1, ((c.x0 & 3) + c.cols + 3) >> 2);
         rf.rows = max(1, c.rows);
         return rf;

@@ -71,6 +71,11 @@ struct CellDev {
     int level;
     int x0, y0, cols, rows;   // ROI in level coordinates (ORBextractor.cc:807-826)
     int slot_off, cap;        // key slots (u32) relative to the frame's slot slab
+    // levels >= 1: the ROI's first dword (row y0, column x0 & ~3) as a byte
+    // offset in the frame's pyramid slab, and the level pitch, so k_fast_cells
+    // addresses it from the cell record alone (no dependent level-table load
+    // before its first ROI load); level 0 (the caller's image) uses its pitch
+    int roi_off, pitch;
 };
 
 struct Plan {
