@@ -231,6 +231,9 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *   ORB_OPT_PYR_PRETEST  1: FAST's iniThFAST compass pre-test fused into
  *                        k_pyr_stream (a candidate bitmap k_fast_cells reads;
  *                        measured slower)
+ *   ORB_OPT_SFI_FORM     host SearchForInitialization: 0 fused single launch
+ *                        (frames <= 4096 keypoints, nnratio >= 0.2; else 1),
+ *                        1 grid + top-K + serial resolve
  * The two k_pyr_stream options are read when a handle builds its plan (the
  * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
@@ -241,7 +244,8 @@ enum {
     ORB_OPT_BOWK_BIG = 2,
     ORB_OPT_PYR_CNT_END = 3,
     ORB_OPT_PYR_PRETEST = 4,
-    ORB_OPT_COUNT = 5
+    ORB_OPT_SFI_FORM = 5,
+    ORB_OPT_COUNT = 6
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);

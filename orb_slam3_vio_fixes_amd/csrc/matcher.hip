@@ -4049,6 +4049,323 @@ __global__ __launch_bounds__(256) void k_fv_angle(const orb_keypoint* __restrict
     for (int p = threadIdx.x; p < n; p += blockDim.x) out[io + p] = kps[ko + fv_idx[io + p]].angle;
 }
 
+// ---------------------------------------------------------------------------
+// k_sfi_fused: SearchForInitialization(F1, F2, ...) (ORBmatcher.cc:648-763)
+// in ONE launch for the host API, no grid build (the k_proj_fused pattern).
+//
+// Phase 1, one wave per F1 keypoint of octave 0: its kTopK smallest F2
+// candidates by (distance, GetFeaturesInArea order) from a brute-force pass
+// over F2 (octave 0, in a visited cell, |dx| < window, |dy| < window), only
+// distances that can still decide (d <= bound: a best above TH_LOW is
+// rejected anyway, and a second above TH_LOW / ratio cannot fail the ratio
+// test).  Phase 2, last block: the serial loop's only order dependence is the
+// skip rule `vMatchedDistance[i2] <= dist` (:687-688), where vMatchedDistance
+// of slot s seen by query j is the distance of the LATEST claim on s by a
+// query before j (a steal needs a strictly smaller distance, so that is also
+// the smallest).  Recomputing every decision from the previous round's claims
+// (per-slot claim lists sorted by query) leaves the earliest wrong decision
+// right after each round; two equal rounds are the serial outcome.  Then the
+// last claimer of each slot keeps it (earlier ones were stolen: vnMatches12 =
+// -1), nmatches = claimed slots, the rotation histogram counts every accepted
+// claim (stolen ones too, as rotHist does) and unmatches the kept matches of
+// rejected bins, and vbPrevMatched takes the matched F2 positions.
+// ---------------------------------------------------------------------------
+struct SfiFusedArgs {
+    const orb_keypoint* k1; const uint8_t* d1; int n1;
+    const orb_keypoint* k2; const uint8_t* d2; int n2;
+    const float* prev;                          // [n1][2]
+    GridParams g;
+    float window, ratio;
+    int check_ori, bound;
+};
+
+// LDS: D[n1] | dry[n1] | ccnt[n2 + 1] | cstart[n2 + 1] | claims[n1] | hist[32] | misc[8]
+static size_t sfi_fused_lds(int n1, int n2) { return (size_t)(3 * n1 + 2 * (n2 + 1) + 40) * 4; }
+
+// K smallest candidate keys of F1 keypoint i (d << 24 | cell << 12 | F2 index),
+// skipping (cl != nullptr) candidates a claim before query j blocks; lane r < K
+// holds the r-th key and its entry d << 24 | bin << 16 | slot.  Returns the
+// number of candidates within the bound.
+template <int K>
+__device__ int sfi_select(const SfiFusedArgs& a, int i, const CellRange& cr, float px, float py, const int* ccnt,
+                          const int* cstart, const int* claims, int j, uint32_t& run, uint32_t& run_e) {
+    const int lane = lane_id();
+    const uint4 q0 = *(const uint4*)(a.d1 + (long long)i * 32);
+    const uint4 q1 = *(const uint4*)(a.d1 + (long long)i * 32 + 16);
+    const float r = a.window;
+    const float* kf = (const float*)a.k2;
+    const int kw = (int)(sizeof(orb_keypoint) / 4);
+    auto kload = [&](int base, float& x, float& y, int& o) {
+        const int fi = min(base + lane, max(a.n2 - 1, 0));
+        x = kf[(long long)fi * kw + 0];
+        y = kf[(long long)fi * kw + 1];
+        o = ((const int*)kf)[(long long)fi * kw + 5];
+    };
+    run = kFusedNone;
+    run_e = kFusedNone;
+    int total = 0;
+    float nx = 0.f, ny = 0.f;
+    int no = 0;
+    if (a.n2 > 0) kload(0, nx, ny, no);
+    for (int base = 0; base < a.n2; base += kWave) {
+        const float kx = nx, ky = ny;
+        const int ko = no;
+        if (base + kWave < a.n2) kload(base + kWave, nx, ny, no);
+        const int fi = base + lane;
+        uint32_t key = kFusedNone, ent = kFusedNone;
+        if (fi < a.n2 && ko == 0) {
+            const int gx = (int)roundf((kx - a.g.min_x) * a.g.inv_w);
+            const int gy = (int)roundf((ky - a.g.min_y) * a.g.inv_h);
+            if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1 && gx >= 0 && gx < kGridCols && gy >= 0 &&
+                gy < kGridRows && fabsf(kx - px) < r && fabsf(ky - py) < r) {
+                const int d = hamming32(q0, q1, a.d2 + (long long)fi * 32);
+                bool usable = d <= a.bound;
+                if (usable && claims) {
+                    // vMatchedDistance[fi] before query j: the latest claim before j
+                    int md = INT_MAX;
+                    for (int c = cstart[fi], ce = c + ccnt[fi]; c < ce; ++c) {
+                        const int cl = claims[c];
+                        if ((cl >> 8) >= j) break;
+                        md = cl & 0xff;
+                    }
+                    usable = md > d;
+                }
+                if (usable) {
+                    key = ((uint32_t)d << 24) | ((uint32_t)(gx * kGridRows + gy) << 12) | (uint32_t)fi;
+                    ent = ((uint32_t)d << 24) | (uint32_t)fi;
+                }
+            }
+        }
+        const uint64_t has = __ballot(key != kFusedNone);
+        if (!has) continue;
+        total += __popcll(has);
+        uint32_t prev = 0, nrun = kFusedNone, nrun_e = kFusedNone;
+        bool first = true;
+        for (int rr = 0; rr < K; ++rr) {
+            const uint32_t xa = (first || key > prev) ? key : kFusedNone;
+            const uint32_t xb = (lane < K && (first || run > prev)) ? run : kFusedNone;
+            const uint32_t x = min(xa, xb);
+            const uint32_t xe = xa <= xb ? ent : run_e;
+            const uint32_t m = wave_min(x, kFusedNone);
+            if (m == kFusedNone) break;
+            const int src = __ffsll((long long)__ballot(x == m)) - 1;
+            const uint32_t me = (uint32_t)__builtin_amdgcn_readlane((int)xe, src);
+            if (lane == rr) { nrun = m; nrun_e = me; }
+            prev = m;
+            first = false;
+        }
+        run = nrun;
+        run_e = nrun_e;
+    }
+    if (lane < K && run_e != kFusedNone && a.check_ori)
+        run_e |= (uint32_t)rot_bin(a.k1[i].angle, a.k2[run_e & 0xfff].angle) << 16;
+    return total;
+}
+
+// accept (:701-703): bestDist <= TH_LOW and bestDist < bestDist2 * nnratio
+__device__ __forceinline__ bool sfi_accept(int best, int best2, float ratio) {
+    return best <= kThLow && (float)best < (float)best2 * ratio;
+}
+
+__global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uint32_t* __restrict__ lists,
+                                                              int* __restrict__ cnt, unsigned* __restrict__ ticket,
+                                                              int32_t* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) int sl[];
+    const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    int* D = sl;                                // decision: -1 none, else slot | d << 12 | bin << 20
+    int* dry = D + n1;
+    int* ccnt = dry + n1;                       // claims per slot
+    int* cstart = ccnt + n2 + 1;                // their segment starts
+    int* claims = cstart + n2 + 1;              // j << 8 | d, by slot, ascending j
+    int* hist = claims + n1;
+    int* misc = hist + 32;                      // 0 last block, 1 first changed, 2 ndry, 3 fill, 4 nm, 5 dropped
+    // ---- phase 1
+    {
+        const int i = blockIdx.x * (kFusedThreads / kWave) + wv;
+        if (i < n1) {
+            const float px = a.prev[2 * i], py = a.prev[2 * i + 1];
+            CellRange cr;
+            if (a.k1[i].octave != 0 || !cell_range(px, py, a.window, a.g, cr)) {
+                if (lane == 0) cnt[i] = -1;
+            } else {
+                uint32_t run, run_e;
+                const int total = sfi_select<kTopK>(a, i, cr, px, py, nullptr, nullptr, nullptr, 0, run, run_e);
+                if (lane < kTopK) lists[(long long)i * kTopK + lane] = run_e;
+                if (lane == 0) cnt[i] = total;
+            }
+        }
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) misc[0] = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!misc[0]) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    // ---- phase 2: fixpoint over all queries
+    for (int j = tid; j < n1; j += kFusedThreads) D[j] = -2;
+    for (int s = tid; s <= n2; s += kFusedThreads) { ccnt[s] = 0; cstart[s] = 0; }
+    if (tid < 32) hist[tid] = 0;
+    if (tid < 8) misc[tid] = 0;
+    if (tid == 0) misc[1] = n1;
+    __syncthreads();
+    const float ratio = a.ratio;
+    const int* cl = nullptr;                    // no claims in round 0
+    int settled = 0;
+    for (int round = 0; round <= n1; ++round) {
+        for (int j = tid; j < n1; j += kFusedThreads) {
+            if (j < settled) continue;
+            const int c = cnt[j];
+            int dec = -1;
+            if (c > 0) {
+                const uint4 LA = ((const uint4*)lists)[(long long)j * 2], LB = ((const uint4*)lists)[(long long)j * 2 + 1];
+                const uint32_t L[kTopK] = {LA.x, LA.y, LA.z, LA.w, LB.x, LB.y, LB.z, LB.w};
+                int best = INT_MAX, slot = -1, bin = 0, best2 = INT_MAX, nav = 0, dlast = 0;
+#pragma unroll
+                for (int k = 0; k < kTopK; ++k) {
+                    const uint32_t e = L[k];
+                    if (k >= c || e == kFusedNone) continue;
+                    const int s = (int)(e & 0xfff), d = (int)(e >> 24);
+                    dlast = d;
+                    if (cl) {
+                        int md = INT_MAX;
+                        for (int q = cstart[s], qe = q + ccnt[s]; q < qe; ++q) {
+                            const int x = cl[q];
+                            if ((x >> 8) >= j) break;
+                            md = x & 0xff;
+                        }
+                        if (md <= d) continue;                          // :687-688
+                    }
+                    if (nav == 0) { best = d; slot = s; bin = (int)((e >> 16) & 31); }
+                    else if (nav == 1) best2 = d;
+                    ++nav;
+                }
+                // a truncated list decides when two usable entries are listed, or
+                // one that fails TH_LOW, or one the unlisted rest (every distance
+                // >= the last listed one) cannot reject by the ratio
+                const bool exact = c <= kTopK || nav >= 2 ||
+                                   (nav == 1 && (best > kThLow || (float)best < (float)dlast * ratio));
+                if (!exact) {
+                    dec = -3;
+                    dry[atomicAdd(&misc[2], 1)] = j;
+                } else if (slot >= 0 && sfi_accept(best, best2, ratio)) {
+                    dec = slot | (best << 12) | (bin << 20);
+                }
+            }
+            if (dec != -3) {
+                if (dec != D[j]) atomicMin(&misc[1], j);
+                D[j] = dec;
+            }
+        }
+        __syncthreads();
+        const int ndry = misc[2];
+        for (int t = wv; t < ndry; t += kFusedThreads / kWave) {
+            const int j = dry[t];
+            const float px = a.prev[2 * j], py = a.prev[2 * j + 1];
+            CellRange cr;
+            cell_range(px, py, a.window, a.g, cr);
+            uint32_t run, run_e;
+            sfi_select<2>(a, j, cr, px, py, ccnt, cstart, cl, j, run, run_e);
+            const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 0);
+            const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 1);
+            int dec = -1;
+            if (e1 != kFusedNone) {
+                const int best = (int)(e1 >> 24), best2 = e2 != kFusedNone ? (int)(e2 >> 24) : INT_MAX;
+                if (sfi_accept(best, best2, ratio)) dec = (int)(e1 & 0xfff) | (best << 12) | (int)(((e1 >> 16) & 31) << 20);
+            }
+            if (lane == 0) {
+                if (dec != D[j]) atomicMin(&misc[1], j);
+                D[j] = dec;
+            }
+        }
+        __syncthreads();
+        const int first_changed = misc[1];
+        __syncthreads();
+        if (first_changed >= n1 && round > 0) break;
+        settled = first_changed;
+        // the claim lists of this round's decisions, by slot and ascending query
+        for (int s = tid; s <= n2; s += kFusedThreads) ccnt[s] = 0;
+        if (tid == 0) { misc[1] = n1; misc[2] = 0; misc[3] = 0; }
+        __syncthreads();
+        for (int j = tid; j < n1; j += kFusedThreads)
+            if (D[j] >= 0) atomicAdd(&ccnt[D[j] & 0xfff], 1);
+        __syncthreads();
+        if (wv == 0) {                                   // exclusive scan of the counts (one wave)
+            int run = 0;
+            for (int b = 0; b < n2; b += kWave) {
+                const int v = b + lane < n2 ? ccnt[b + lane] : 0;
+                const int inc = wave_incl_scan(v);
+                if (b + lane < n2) cstart[b + lane] = run + inc - v;
+                run += __shfl(inc, kWave - 1, kWave);
+            }
+        }
+        __syncthreads();
+        for (int s = tid; s < n2; s += kFusedThreads) ccnt[s] = 0;      // reused as fill positions
+        __syncthreads();
+        for (int j = tid; j < n1; j += kFusedThreads) {
+            const int dec = D[j];
+            if (dec < 0) continue;
+            const int s = dec & 0xfff;
+            claims[cstart[s] + atomicAdd(&ccnt[s], 1)] = (j << 8) | ((dec >> 12) & 0xff);
+        }
+        __syncthreads();
+        for (int s = tid; s < n2; s += kFusedThreads) {     // insertion sort of each slot's few claims by query
+            const int b = cstart[s], m = ccnt[s];
+            for (int x = b + 1; x < b + m; ++x) {
+                const int v = claims[x];
+                int y = x - 1;
+                while (y >= b && claims[y] > v) { claims[y + 1] = claims[y]; --y; }
+                claims[y + 1] = v;
+            }
+        }
+        cl = claims;
+        __syncthreads();
+    }
+    // ---- outputs (with the final claim lists: the rounds ended on a fixpoint)
+    // every accepted claim enters the histogram; the last claimer of a slot keeps it
+    int nacc = 0;
+    for (int j = tid; j < n1; j += kFusedThreads) {
+        const int dec = D[j];
+        if (dec < 0) continue;
+        if (a.check_ori) atomicAdd(&hist[(dec >> 20) & 31], 1);
+    }
+    for (int s = tid; s < n2; s += kFusedThreads) nacc += ccnt[s] > 0;
+    nacc = wave_sum(nacc);
+    if (lane == 0) atomicAdd(&misc[4], nacc);
+    __syncthreads();
+    __shared__ int tm[3];
+    if (tid == 0) {
+        tm[0] = tm[1] = tm[2] = -1;
+        if (a.check_ori) three_maxima(hist, tm[0], tm[1], tm[2]);
+    }
+    __syncthreads();
+    int drop = 0;
+    int32_t* m12 = out + 1;
+    float* pout = (float*)(out + 1 + n1);
+    for (int j = tid; j < n1; j += kFusedThreads) {
+        const int dec = D[j];
+        int m = -1;
+        if (dec >= 0) {
+            const int s = dec & 0xfff;
+            const bool last = (claims[cstart[s] + ccnt[s] - 1] >> 8) == j;
+            if (last) {
+                const int b = (dec >> 20) & 31;
+                if (a.check_ori && b != tm[0] && b != tm[1] && b != tm[2]) ++drop;
+                else m = s;
+            }
+        }
+        m12[j] = m;
+        pout[2 * j] = m >= 0 ? a.k2[m].x : a.prev[2 * j];
+        pout[2 * j + 1] = m >= 0 ? a.k2[m].y : a.prev[2 * j + 1];
+    }
+    drop = wave_sum(drop);
+    if (lane == 0) atomicAdd(&misc[5], drop);
+    __syncthreads();
+    if (tid == 0) {
+        out[0] = misc[4] - misc[5];
+        *ticket = 0u;
+    }
+}
+
 }  // namespace orbmi
 
 using namespace orbmi;
@@ -4111,6 +4428,40 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     if (!f1 || !f2 || !prev_xy || !matches12) return ORB_ERR_PARAM;
     if (device_ok()) return ORB_ERR_DEVICE;
     if (f1->n > 0xffff || f2->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    // fused single launch: one coalesced upload, one launch, one download of
+    // [nmatches, matches12[n1], prev_xy[n1][2]]
+    if (debug_opt(ORB_OPT_SFI_FORM) == 0 && f1->n <= kFusedMaxN && f2->n <= kFusedMaxN && nnratio >= 0.2f &&
+        sfi_fused_lds(f1->n, f2->n) <= kCuLds) {
+        SfiFusedArgs a{};
+        DBuf<orb_keypoint> k1, k2; DBuf<uint8_t> d1, d2; DBuf<float> pv;
+        DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; DBuf<int32_t> out;
+        const unsigned zero = 0;
+        const int n1 = f1->n, n2 = f2->n;
+        int rc;
+        if ((rc = k1.put(f1->kps, n1)) || (rc = d1.put(f1->desc, (size_t)n1 * 32)) || (rc = k2.put(f2->kps, n2)) ||
+            (rc = d2.put(f2->desc, (size_t)n2 * 32)) || (rc = pv.put(prev_xy, (size_t)2 * n1)) ||
+            (rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, n1) * kTopK)) ||
+            (rc = cnt.alloc(std::max(1, n1))) || (rc = out.alloc((size_t)1 + 3 * n1)))
+            return rc;
+        a.k1 = k1.p; a.d1 = d1.p; a.n1 = n1; a.k2 = k2.p; a.d2 = d2.p; a.n2 = n2; a.prev = pv.p;
+        a.g = grid_params(f2); a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
+        // a best above TH_LOW is rejected; a second d with (float)d * ratio > TH_LOW
+        // cannot fail the ratio test of an accepted best
+        int bound = kThLow;
+        while (bound < 255 && (float)(bound + 1) * nnratio <= (float)kThLow) ++bound;
+        a.bound = bound;
+        const int nblk = std::max(1, (n1 + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
+        KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), sfi_fused_lds(n1, n2), 0, a, lists.p, cnt.p, ticket.p,
+                out.p);
+        ORB_CHECK(hipGetLastError());
+        std::vector<int32_t> res((size_t)1 + 3 * n1);
+        ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
+        if (n1) {
+            std::memcpy(matches12, res.data() + 1, (size_t)n1 * sizeof(int32_t));
+            std::memcpy(prev_xy, res.data() + 1 + n1, (size_t)n1 * 2 * sizeof(float));
+        }
+        return res[0];
+    }
     // both frames share one [2][cap] layout
     const int cap = std::max(1, std::max(f1->n, f2->n));
     DBuf<orb_keypoint> kps; DBuf<uint8_t> desc; DBuf<int> n; DBuf<uint32_t> sorted; DBuf<int> count;

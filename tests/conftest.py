@@ -57,3 +57,13 @@ def proj_form(debug_option):
     def set_(name):
         debug_option(capi.ORB_OPT_PROJ_FORM, {"fused": 0, "serial": 1, "single": 2, "spec": 3}[name])
     return set_
+
+
+@pytest.fixture
+def sfi_form(debug_option):
+    """Host SearchForInitialization form by name: fused (one launch: brute-force
+    top-K + last-block fixpoint resolve, the default) or grid (grid order +
+    top-K + serial resolve)."""
+    def set_(name):
+        debug_option(capi.ORB_OPT_SFI_FORM, {"fused": 0, "grid": 1}[name])
+    return set_

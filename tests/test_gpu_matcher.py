@@ -30,8 +30,10 @@ def test_descriptor_distance(gpu_lib):
 
 @pytest.mark.parametrize("i1,i2,window,ratio,ori", [(0, 1, 100, 0.9, True), (1, 2, 100, 0.9, True),
                                                     (0, 2, 60, 0.8, False), (4, 5, 100, 0.9, True),
-                                                    (2, 3, 400, 1.0, True)])
-def test_search_for_initialization(gpu_lib, frames, i1, i2, window, ratio, ori):
+                                                    (2, 3, 400, 1.0, True), (0, 1, 30, 0.15, True)])
+@pytest.mark.parametrize("form", ["fused", "grid"])
+def test_search_for_initialization(gpu_lib, frames, i1, i2, window, ratio, ori, form, sfi_form):
+    sfi_form(form)
     f1, f2 = frames[i1], frames[i2]
     prev = np.stack([f1[0]["x"], f1[0]["y"]], 1)
     nm, m12, p2 = orb.ORBmatcher(ratio, ori).SearchForInitialization(fr(f1), fr(f2), prev, window)
@@ -247,9 +249,11 @@ def _graded_copies(k0, d0, base, copies, jitter, seed, flip):
 @pytest.mark.parametrize("copies,ratio,ori,shuffle", [(12, 0.9, True, False), (20, 1.0, False, False),
                                                       (9, 0.95, True, False), (12, 0.9, True, True),
                                                       (20, 1.0, False, True)])
-def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, ratio, ori, shuffle):
+@pytest.mark.parametrize("form", ["fused", "grid"])
+def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, ratio, ori, shuffle, form, sfi_form):
     """F1 holds `copies` identical copies of each of 24 keypoints, F2 `copies`
-    copies whose descriptors sit 0, 1, 2, ... bits away.  The copies of one
+    copies whose descriptors sit 0, 1, 2, ... bits away (both forms: the fused
+    fixpoint's claim lists see the same chains).  The copies of one
     F1 keypoint steal F2's copies one after the other (ORBmatcher.cc:680-700:
     a candidate whose matched distance is <= the query's is skipped), so
     after the eighth claim a query's top-8 list holds at most one live entry
@@ -266,12 +270,30 @@ def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, rati
     if shuffle:
         perm = np.random.default_rng(copies).permutation(len(k1))
         k1, d1 = k1[perm], d1[perm]
+    sfi_form(form)
     prev = np.stack([k1["x"], k1["y"]], 1)
     f1 = abi.frame_struct(k1, d1, 752, 480)
     f2 = abi.frame_struct(k2, d2, 752, 480)
     nm, m12, p2 = orb.ORBmatcher(ratio, ori).SearchForInitialization(f1, f2, prev, 100)
     rnm, rm12, rp2 = O.search_for_initialization(f1, f2, prev, 100, ratio, ori)
     assert rnm > len(base)          # chains of steals happened
+    assert nm == rnm
+    np.testing.assert_array_equal(m12, rm12)
+    np.testing.assert_array_equal(p2, rp2)
+
+
+@pytest.mark.parametrize("seed,jitter,window", [(31, 40.0, 100), (32, 150.0, 60), (33, 5.0, 200)])
+@pytest.mark.parametrize("form", ["fused", "grid"])
+def test_search_for_initialization_moved_prev(gpu_lib, frames, seed, jitter, window, form, sfi_form):
+    """vbPrevMatched moved away from F1's own positions, some outside the image
+    (windows clipped at the grid border or missing it: no candidates)."""
+    sfi_form(form)
+    f1, f2 = frames[seed % 3], frames[seed % 3 + 1]
+    rng = np.random.default_rng(seed)
+    prev = np.stack([f1[0]["x"], f1[0]["y"]], 1) + rng.uniform(-jitter, jitter, (len(f1[0]), 2))
+    prev = prev.astype(np.float32)
+    nm, m12, p2 = orb.ORBmatcher(0.9, True).SearchForInitialization(fr(f1), fr(f2), prev, window)
+    rnm, rm12, rp2 = O.search_for_initialization(fr(f1), fr(f2), prev, window, 0.9, True)
     assert nm == rnm
     np.testing.assert_array_equal(m12, rm12)
     np.testing.assert_array_equal(p2, rp2)
