@@ -1131,6 +1131,7 @@ struct BowArgs {
     const uint8_t* f_valid;   // KF-KF form: pKF2 MapPoint != NULL && !isBad(), else NULL
     int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
     int f_nleft = -1;         // the frame's Nleft (-1: mono / rectified)
+    unsigned* fin_ticket = nullptr;   // single pair: k_bow's last block runs the final (k_bow_final's body)
 };
 
 // One wave per (pair, vocabulary node) the two FeatureVectors share: the
@@ -1449,12 +1450,26 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
 // bound serial chains), the rest the small ones (VALU-bound), so the two
 // co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private KF
 // descriptor areas (2 * 64 uint4 each).
+__device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins);
 static_assert(2 * kBowBigCap >= 4 * 2 * kWave, "s_fd holds the small-node waves' descriptor areas");
+static_assert(kBowBigCap >= 33, "s_fi holds the fused final's histogram and drop count");
 __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_slots) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
     if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, big_slots, s_fd, s_fi);
     else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 2 * kWave);
+    if (a.fin_ticket) {
+        // a single pair: the last block to finish runs the rotation filter on
+        // every block's matches (the match rows, nmatches and the LDS are free)
+        __shared__ int last;
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(a.fin_ticket, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!last) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd));
+    }
 }
 
 // Rotation-consistency filter (:404-422 / :884-902) and the KF-KF output, one
@@ -1463,12 +1478,12 @@ __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_
 // here, lane-parallel over the frame features, instead of in the serial loop.
 constexpr int kBowFinalBins = 16384;    // frame features whose bin k_bow_final keeps in LDS
 
-__global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
-    const int pr = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
+// hist: 32 ints, drop: 1 int, sbin: nbins bytes of LDS (the bin of each match,
+// one gather of the KF angle)
+__device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins) {
+    const int tid = threadIdx.x, nt = blockDim.x;
     int32_t* match = a.match + (long long)pr * a.f_n;
-    __shared__ int hist[32];
-    __shared__ int drop;
-    __shared__ uint8_t sbin[kBowFinalBins];             // bin of each match (one gather of the KF angle)
+    int& drop = *drop_p;
     if (a.check_ori) {
         const orb_keypoint* KK = a.kf_kps + a.kp_off[pr];
         if (tid < 32) hist[tid] = 0;
@@ -1492,7 +1507,7 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
                 const int i = i0 + u * nt;
                 const int b = m[u] >= 0 ? rot_bin(ka[u], fa[u]) : -1;
                 hist_add_wave(hist, b);
-                if (b >= 0 && i < kBowFinalBins) sbin[i] = (uint8_t)b;
+                if (b >= 0 && i < nbins) sbin[i] = (uint8_t)b;
             }
         }
         __syncthreads();
@@ -1512,7 +1527,7 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
             for (int u = 0; u < 4; ++u) {
                 if (m[u] < 0) continue;
                 const int i = i0 + u * nt;
-                const int b = i < kBowFinalBins ? sbin[i] : rot_bin(KK[m[u]].angle, a.f_kps[i].angle);
+                const int b = i < nbins ? sbin[i] : rot_bin(KK[m[u]].angle, a.f_kps[i].angle);
                 if (b == i1 || b == i2 || b == i3) continue;
                 match[i] = -1;
                 ++d;
@@ -1522,7 +1537,7 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
         for (int i = tid; i < a.f_n; i += nt) {
             const int m = match[i];
             if (m < 0) continue;
-            const int b = i < kBowFinalBins ? sbin[i] : rot_bin(KK[m].angle, a.f_kps[i].angle);
+            const int b = i < nbins ? sbin[i] : rot_bin(KK[m].angle, a.f_kps[i].angle);
             if (b == i1 || b == i2 || b == i3) continue;
             match[i] = -1;
             ++d;
@@ -1545,6 +1560,13 @@ __global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
     }
 }
 
+__global__ __launch_bounds__(256) void k_bow_final(BowArgs a) {
+    __shared__ int hist[32];
+    __shared__ int drop;
+    __shared__ uint8_t sbin[kBowFinalBins];
+    bow_final_body(a, blockIdx.x, hist, &drop, sbin, kBowFinalBins);
+}
+
 // The per-call state of k_bow in one launch (instead of memsets).
 __global__ __launch_bounds__(256) void k_bow_init(BowArgs a) {
     const long long nmf = (long long)a.npairs * a.f_n, stride = (long long)gridDim.x * blockDim.x;
@@ -1557,9 +1579,12 @@ __global__ __launch_bounds__(256) void k_bow_init(BowArgs a) {
 // when the host holds the frame's FeatureVector, else 1); kf_nodes: the KF
 // FeatureVector nodes in all when the host knows them (a single pair: one
 // wave per node, for latency), else -1.
+// With a.fin_ticket (one pair, match / nmatches initialised by the caller)
+// the call is the one k_bow launch.
 static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1, long long kf_nodes = -1) {
     a.npairs = npairs;
-    {
+    if (a.fin_ticket && npairs != 1) return ORB_ERR_PARAM;
+    if (!a.fin_ticket) {
         const long long nmf = (long long)npairs * a.f_n;
         const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
         KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
@@ -1569,7 +1594,7 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
     big_slots = std::max(1, big_slots);
     const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs * big_slots;
     KLAUNCH(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes), st, a, big_blocks, big_slots);
-    KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
+    if (!a.fin_ticket) KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
@@ -4570,27 +4595,32 @@ static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t
     if (device_ok()) return ORB_ERR_DEVICE;
     int rc;
     DBuf<orb_keypoint> kk, fk; DBuf<uint8_t> kd, fd, kvv; DBuf<uint32_t> kn, ki, fn, fi; DBuf<int> ko, fo;
-    DBuf<long long> kpo, nodo, idxo; DBuf<int32_t> m, nm;
+    DBuf<long long> kpo, nodo, idxo; DBuf<int32_t> m;
     const long long kp_off[2] = {0, kf->n}, node_off[2] = {0, kfv->nnodes}, idx_off[1] = {0};
     if ((rc = kk.put(kf->kps, kf->n)) || (rc = kd.put(kf->desc, (size_t)kf->n * 32)) || (rc = kvv.put(kf_valid, kf->n)) ||
         (rc = kn.put(kfv->node_ids, kfv->nnodes)) || (rc = ko.put(kfv->offsets, kfv->nnodes + 1)) ||
         (rc = ki.put(kfv->idx, kfv->offsets[kfv->nnodes])) || (rc = fk.put(f->kps, f->n)) ||
         (rc = fd.put(f->desc, (size_t)f->n * 32)) || (rc = fn.put(ffv->node_ids, ffv->nnodes)) ||
         (rc = fo.put(ffv->offsets, ffv->nnodes + 1)) || (rc = fi.put(ffv->idx, ffv->offsets[ffv->nnodes])) ||
-        (rc = kpo.put(kp_off, 2)) || (rc = nodo.put(node_off, 2)) || (rc = idxo.put(idx_off, 1)) ||
-        (rc = m.alloc(std::max(1, f->n))) || (rc = nm.alloc(1)))
+        (rc = kpo.put(kp_off, 2)) || (rc = nodo.put(node_off, 2)) || (rc = idxo.put(idx_off, 1)))
         return rc;
+    // match[n] = -1 and nmatches = 0 go up with the inputs, and come back as one
+    // download; the last k_bow block runs the rotation filter (one launch)
+    std::vector<int32_t> init((size_t)f->n + 1, -1);
+    init[f->n] = 0;
+    const unsigned zero = 0;
+    DBuf<unsigned> ticket;
+    if ((rc = m.put(init.data(), init.size())) || (rc = ticket.put(&zero, 1))) return rc;
     BowArgs a{};
     a.kf_kps = kk.p; a.kf_desc = kd.p; a.kf_valid = kvv.p; a.kp_off = kpo.p;
     a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
-    a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = nm.p;
-    a.f_nleft = f_nleft;
+    a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = m.p + f->n;
+    a.f_nleft = f_nleft; a.fin_ticket = ticket.p;
     if ((rc = launch_bow(a, 1, 0, bow_big_nodes(ffv), kfv->nnodes))) return rc;
-    int32_t res = 0;
-    ORB_CHECK(d2h(&res, nm.p, 4));
-    if (f->n) ORB_CHECK(d2h(match_f, m.p, f->n * 4));
-    return res;
+    ORB_CHECK(d2h(init.data(), m.p, init.size() * 4));
+    if (f->n) std::memcpy(match_f, init.data(), (size_t)f->n * 4);
+    return init[f->n];
 }
 
 int orbm_search_by_bow(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t* kf_valid, const orbm_frame* f,
