@@ -234,6 +234,10 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *   ORB_OPT_SFI_FORM     host SearchForInitialization: 0 fused single launch
  *                        (frames <= 4096 keypoints, nnratio >= 0.2; else 1),
  *                        1 grid + top-K + serial resolve
+ *   ORB_OPT_HOST_OUT     single-launch host calls (fused projection and
+ *                        initialization searches): 0 result block copied back
+ *                        by one device-to-host copy, 1 written by the kernel
+ *                        straight into pinned host memory (zero-copy)
  * The two k_pyr_stream options are read when a handle builds its plan (the
  * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
@@ -245,7 +249,8 @@ enum {
     ORB_OPT_PYR_CNT_END = 3,
     ORB_OPT_PYR_PRETEST = 4,
     ORB_OPT_SFI_FORM = 5,
-    ORB_OPT_COUNT = 6
+    ORB_OPT_HOST_OUT = 6,
+    ORB_OPT_COUNT = 7
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);

@@ -3869,6 +3869,34 @@ static hipError_t d2h(void* dst, const void* src, size_t bytes) {
     return e;
 }
 
+// The result block of a single-launch host call: with ORB_OPT_HOST_OUT 1 the
+// kernel writes it straight into pinned host memory (the staging arena, mapped
+// into the device's address space) and the call only synchronises; else it is
+// device memory brought back by one d2h.
+struct OutBlock {
+    int32_t* d = nullptr;      // what the kernel writes
+    int32_t* h = nullptr;      // host view (zero-copy) or nullptr
+    size_t n = 0;
+    int alloc(size_t cnt) {
+        n = std::max<size_t>(1, cnt);
+        if (debug_opt(ORB_OPT_HOST_OUT) == 1) {
+            h = (int32_t*)host_stage().get(n * sizeof(int32_t));
+            if (!h || hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) return ORB_ERR_DEVICE;
+            return ORB_OK;
+        }
+        h = nullptr;
+        d = (int32_t*)dev_arena().get(n * sizeof(int32_t));
+        return d ? ORB_OK : ORB_ERR_DEVICE;
+    }
+    // after the launch: the block's words [0, cnt) into dst
+    hipError_t fetch(int32_t* dst, size_t cnt) const {
+        if (!h) return d2h(dst, d, cnt * sizeof(int32_t));
+        if (const hipError_t e = hipStreamSynchronize(0); e != hipSuccess) return e;
+        std::memcpy(dst, h, cnt * sizeof(int32_t));
+        return hipSuccess;
+    }
+};
+
 // A device buffer of the current host-API call (arena-backed).
 template <typename T>
 struct DBuf {
@@ -4459,7 +4487,7 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         sfi_fused_lds(f1->n, f2->n) <= kCuLds) {
         SfiFusedArgs a{};
         DBuf<orb_keypoint> k1, k2; DBuf<uint8_t> d1, d2; DBuf<float> pv;
-        DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; DBuf<int32_t> out;
+        DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; OutBlock out;
         const unsigned zero = 0;
         const int n1 = f1->n, n2 = f2->n;
         int rc;
@@ -4477,10 +4505,10 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         a.bound = bound;
         const int nblk = std::max(1, (n1 + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), sfi_fused_lds(n1, n2), 0, a, lists.p, cnt.p, ticket.p,
-                out.p);
+                out.d);
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)1 + 3 * n1);
-        ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
+        ORB_CHECK(out.fetch(res.data(), res.size()));
         if (n1) {
             std::memcpy(matches12, res.data() + 1, (size_t)n1 * sizeof(int32_t));
             std::memcpy(prev_xy, res.data() + 1 + n1, (size_t)n1 * 2 * sizeof(float));
@@ -4606,11 +4634,24 @@ static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t
         return rc;
     // match[n] = -1 and nmatches = 0 go up with the inputs, and come back as one
     // download; the last k_bow block runs the rotation filter (one launch)
+    // (zero-copy, ORB_OPT_HOST_OUT 1: the block is initialised in pinned host
+    // memory and the kernel works on it there)
     std::vector<int32_t> init((size_t)f->n + 1, -1);
     init[f->n] = 0;
     const unsigned zero = 0;
     DBuf<unsigned> ticket;
-    if ((rc = m.put(init.data(), init.size())) || (rc = ticket.put(&zero, 1))) return rc;
+    OutBlock out;
+    if ((rc = ticket.put(&zero, 1))) return rc;
+    if (debug_opt(ORB_OPT_HOST_OUT) == 1) {
+        if ((rc = out.alloc(init.size()))) return rc;
+        std::memcpy(out.h, init.data(), init.size() * sizeof(int32_t));
+        m.p = out.d;
+        m.n = init.size();
+    } else {
+        if ((rc = m.put(init.data(), init.size()))) return rc;
+        out.d = m.p;
+        out.n = init.size();
+    }
     BowArgs a{};
     a.kf_kps = kk.p; a.kf_desc = kd.p; a.kf_valid = kvv.p; a.kp_off = kpo.p;
     a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
@@ -4618,7 +4659,7 @@ static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = m.p + f->n;
     a.f_nleft = f_nleft; a.fin_ticket = ticket.p;
     if ((rc = launch_bow(a, 1, 0, bow_big_nodes(ffv), kfv->nnodes))) return rc;
-    ORB_CHECK(d2h(init.data(), m.p, init.size() * 4));
+    ORB_CHECK(out.fetch(init.data(), init.size()));
     if (f->n) std::memcpy(match_f, init.data(), (size_t)f->n * 4);
     return init[f->n];
 }
@@ -4842,7 +4883,7 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
         proj_fused_lds(f->n, a.nq, false) <= kCuLds) {
         // the lists in LDS for phase 2 when they fit (else read from L2 each round)
         const int lds_lists = proj_fused_lds(f->n, a.nq, true) <= kCuLds;
-        DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; DBuf<int32_t> out;
+        DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; OutBlock out;
         const unsigned zero = 0;
         if ((rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, a.nq) * kProjK)) ||
             (rc = cnt.alloc(std::max(1, a.nq))) || (rc = out.alloc((size_t)f->n + 5)))
@@ -4850,10 +4891,10 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
         a.nmatches = nullptr;
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), proj_fused_lds(f->n, a.nq, lds_lists != 0), 0, a,
-                proj_bound(a), lists.p, cnt.p, ticket.p, own.p, out.p, lds_lists);
+                proj_bound(a), lists.p, cnt.p, ticket.p, own.p, out.d, lds_lists);
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)f->n + 5);
-        ORB_CHECK(d2h(res.data(), out.p, res.size() * sizeof(int32_t)));
+        ORB_CHECK(out.fetch(res.data(), res.size()));
         if (f->n) std::memcpy(owner, res.data() + 1, (size_t)f->n * sizeof(int32_t));
         std::memcpy(proj_stats(), res.data() + f->n + 1, 4 * sizeof(int32_t));
         return res[0];

@@ -1,8 +1,10 @@
 // Per-call latency of the Tracking thread's matcher calls through a C ABI, as
 // a C++ caller (the drop-in adapters) sees it: no Python in the timed loop.
 //
-//   matcher_latency <library.so> <prefix> <input dir> <reps>
+//   matcher_latency <library.so> <prefix> <input dir> <reps> [opt=value,...]
 //
+// The optional last argument sets orb_debug_set_option values first (the
+// product's A/B forms, e.g. 6=1 for zero-copy result blocks).
 // <prefix> "orbm" times the MI355X library (include/orb_mi355x.h); "orbo" the
 // same entry points of the CPU oracle (oracle/liborb_oracle.so, one thread:
 // the reference's own per-call model) -- test infrastructure, run by
@@ -96,13 +98,27 @@ void check(int rc, const char* what)
 
 int main(int argc, char** argv)
 {
-    if (argc != 5) {
-        std::fprintf(stderr, "usage: %s <library.so> <orbm|orbo> <input dir> <reps>\n", argv[0]);
+    if (argc != 5 && argc != 6) {
+        std::fprintf(stderr, "usage: %s <library.so> <orbm|orbo> <input dir> <reps> [opt=value,...]\n", argv[0]);
         return 2;
     }
     void* lib = dlopen(argv[1], RTLD_NOW | RTLD_LOCAL);
     if (!lib) { std::fprintf(stderr, "dlopen: %s\n", dlerror()); return 2; }
     const std::string pre = argv[2];
+    if (argc == 6) {
+        typedef int (*SetFn)(int, int);
+        SetFn set = (SetFn)dlsym(lib, "orb_debug_set_option");
+        if (!set) { std::fprintf(stderr, "no orb_debug_set_option\n"); return 2; }
+        for (const char* p = argv[5]; *p;) {
+            int o = 0, v = 0, used = 0;
+            if (std::sscanf(p, "%d=%d%n", &o, &v, &used) != 2 || set(o, v) != 0) {
+                std::fprintf(stderr, "bad option list %s\n", argv[5]);
+                return 2;
+            }
+            p += used;
+            if (*p == ',') ++p;
+        }
+    }
     g_dir = argv[3];
     const int reps = std::max(1, std::atoi(argv[4]));
     auto meta = read_meta();

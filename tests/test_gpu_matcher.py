@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 
 from oracle import oracle as O
-from orb_slam3_vio_fixes_amd import abi, orb, synth
+from orb_slam3_vio_fixes_amd import abi, capi, orb, synth
 
 pytestmark = pytest.mark.gpu
 
@@ -92,10 +92,12 @@ def projection_queries(frames, seed, n=600):
     return rng, src, cur, k, qx.astype(np.float32), qy.astype(np.float32)
 
 
+@pytest.mark.parametrize("zc", [0, 1])
 @pytest.mark.parametrize("single", ["fused", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
-def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, proj_form):
+def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, proj_form, zc, debug_option):
     proj_form(single)
+    debug_option(capi.ORB_OPT_HOST_OUT, zc)   # 1: result block written into pinned host memory
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
@@ -118,8 +120,10 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, 
 
 @pytest.mark.parametrize("single", ["fused", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
-def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, proj_form):
+@pytest.mark.parametrize("zc", [0, 1])
+def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, proj_form, zc, debug_option):
     proj_form(single)
+    debug_option(capi.ORB_OPT_HOST_OUT, zc)
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     valid = (rng.random(n) < 0.9).astype(np.uint8)
