@@ -64,6 +64,8 @@ def sfi_form(debug_option):
     """Host SearchForInitialization form by name: fused (one launch: brute-force
     top-K + last-block fixpoint resolve, the default) or grid (grid order +
     top-K + serial resolve)."""
+    from orb_slam3_vio_fixes_amd import capi
+
     def set_(name):
         debug_option(capi.ORB_OPT_SFI_FORM, {"fused": 0, "grid": 1}[name])
     return set_
