@@ -221,7 +221,9 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        (brute-force top-K + last-block fixpoint resolve,
  *                        frames <= 4096 keypoints, <= 8192 queries; else 3),
  *                        1 top-K + serial resolve, 2 single-wave search,
- *                        3 top-K + speculative resolve
+ *                        3 top-K + speculative resolve, 4 the fused form
+ *                        without its in-block LDS grid (every window scans
+ *                        the whole frame)
  *   ORB_OPT_BOW_FORM     map-wide SearchByBoW: 0 lane per keyframe feature
  *                        (k_bowk_*) when the map carries its totals, 1 k_bow
  *   ORB_OPT_BOWK_BIG     0 auto, 1 no big-node resolve form (every frame node
@@ -233,7 +235,8 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        measured slower)
  *   ORB_OPT_SFI_FORM     host SearchForInitialization: 0 fused single launch
  *                        (frames <= 4096 keypoints, nnratio >= 0.2; else 1),
- *                        1 grid + top-K + serial resolve
+ *                        1 grid + top-K + serial resolve, 2 fused without
+ *                        its in-block LDS grid
  *   ORB_OPT_HOST_OUT     single-launch host calls (fused projection and
  *                        initialization searches): 0 result block copied back
  *                        by one device-to-host copy, 1 written by the kernel

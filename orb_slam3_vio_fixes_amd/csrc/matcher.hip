@@ -3124,10 +3124,71 @@ constexpr uint32_t kFusedNone = 0xffffffffu;
 
 // LDS: T[n] | D[nq] (decision per query) | dry[nq] | hist[32] | misc[8] |
 // pre[n] bytes | (lds_lists) C[nq] and the lists, kProjK words per query
-static size_t proj_fused_lds(int n, int nq, bool lds_lists) {
+__host__ __device__ inline size_t proj_fused_lds(int n, int nq, bool lds_lists) {
     size_t b = (size_t)(n + 2 * nq + 32 + 8) * 4 + ((size_t)n + 15) / 16 * 16;
     if (lds_lists) b += (size_t)nq * 4 + (size_t)nq * kProjK * 4;
     return b;
+}
+
+// The frame's grid in each block's LDS (no grid-build launch): gcs[c] = start
+// of cell c in gent (c in [0, kCells]), gent = cell << 12 | keypoint index, by
+// cell (the order inside a cell is free: a candidate's key carries its list
+// position).  oct >= 0 keeps the keypoints of that octave only.  Every thread
+// of the block calls it; tmp holds blockDim / 64 + 1 ints.  A query's window
+// then enumerates only the keypoints of its cell range instead of the frame.
+constexpr int kGridInts = kCells + 1;
+__host__ __device__ inline size_t lds_grid_bytes(int n) { return (size_t)(kGridInts + (n > 1 ? n : 1) + 32) * 4; }
+
+__device__ void lds_grid_build(const orb_keypoint* kps, int n, const GridParams& g, int oct, int* gcs,
+                               uint32_t* gent, int* tmp) {
+    const int tid = threadIdx.x, nt = blockDim.x;
+    for (int c = tid; c < kGridInts; c += nt) gcs[c] = 0;
+    __syncthreads();
+    constexpr int kPer = kFusedMaxN / kFusedThreads;
+    int cell[kPer], rank[kPer];
+#pragma unroll
+    for (int u = 0; u < kPer; ++u) {
+        const int i = tid + u * nt;
+        cell[u] = -1;
+        if (i < n && (oct < 0 || kps[i].octave == oct)) cell[u] = grid_cell(kps[i], g);
+        rank[u] = cell[u] >= 0 ? atomicAdd(&gcs[cell[u]], 1) : 0;
+    }
+    __syncthreads();
+    block_excl_scan(gcs, kGridInts, tmp);
+#pragma unroll
+    for (int u = 0; u < kPer; ++u)
+        if (cell[u] >= 0) gent[gcs[cell[u]] + rank[u]] = ((uint32_t)cell[u] << 12) | (uint32_t)(tid + u * nt);
+    __syncthreads();
+}
+
+// A window's cell columns on the lanes: lane c < ncol holds column cr.x0 + c's
+// run [start, start + cnt) of gent and its exclusive offset in the window's
+// list; total = the list length (wave-uniform).
+struct WinCols { int ncol, total, start, excl; };
+__device__ __forceinline__ WinCols win_cols(const int* gcs, const CellRange& cr) {
+    WinCols w;
+    const int lane = lane_id();
+    w.ncol = cr.x1 - cr.x0 + 1;
+    int cnt = 0;
+    w.start = 0;
+    if (lane < w.ncol) {
+        const int c0 = (cr.x0 + lane) * kGridRows;
+        w.start = gcs[c0 + cr.y0];
+        cnt = gcs[c0 + cr.y1 + 1] - w.start;
+    }
+    const int incl = wave_incl_scan(cnt);
+    w.excl = incl - cnt;
+    w.total = __builtin_amdgcn_readlane(incl, kWave - 1);
+    return w;
+}
+// the entry at window list position p (< total)
+__device__ __forceinline__ uint32_t win_entry(const WinCols& w, const uint32_t* gent, int p) {
+    int st = 0, ex = 0;
+    for (int c = 0; c < w.ncol; ++c) {
+        const int e = __builtin_amdgcn_readlane(w.excl, c);
+        if (p >= e) { ex = e; st = __builtin_amdgcn_readlane(w.start, c); }
+    }
+    return gent[st + p - ex];
 }
 
 // The kProjK (or 2 for a rescan) smallest 32-bit keys of query i's candidates
@@ -3136,7 +3197,7 @@ static size_t proj_fused_lds(int n, int nq, bool lds_lists) {
 // | slot.  Returns the number of such candidates.
 template <int K>
 __device__ int fused_select(const ProjArgs& a, int i, const ProjQuery& q, int bound, const int* T, int j,
-                            uint32_t& run, uint32_t& run_e) {
+                            const int* gcs, const uint32_t* gent, uint32_t& run, uint32_t& run_e) {
     const int lane = lane_id();
     const uint4 q0 = *(const uint4*)(a.qdesc + (long long)i * 32);
     const uint4 q1 = *(const uint4*)(a.qdesc + (long long)i * 32 + 16);
@@ -3148,22 +3209,29 @@ __device__ int fused_select(const ProjArgs& a, int i, const ProjQuery& q, int bo
     // chunk is tested (the scan is a chain of L2 round trips otherwise)
     const float* kf = (const float*)a.kps;
     const int kw = (int)(sizeof(orb_keypoint) / 4);
-    auto kload = [&](int base, float& x, float& y, int& o) {
-        const int fi = min(base + lane, max(a.n - 1, 0));
-        x = kf[(long long)fi * kw + 0];
-        y = kf[(long long)fi * kw + 1];
-        o = ((const int*)kf)[(long long)fi * kw + 5];
+    // the list to scan: the window's cells of the LDS grid, or the whole frame
+    WinCols w{};
+    int len = a.n;
+    if (gcs) {
+        w = win_cols(gcs, q.cr);
+        len = w.total;
+    }
+    auto kload = [&](int base, int& f, float& x, float& y, int& o) {
+        const int p = min(base + lane, max(len - 1, 0));
+        f = gcs ? (int)(win_entry(w, gent, p) & 0xfff) : p;
+        x = kf[(long long)f * kw + 0];
+        y = kf[(long long)f * kw + 1];
+        o = ((const int*)kf)[(long long)f * kw + 5];
     };
     float nx = 0.f, ny = 0.f;
-    int no = 0;
-    if (a.n > 0) kload(0, nx, ny, no);
-    for (int base = 0; base < a.n; base += kWave) {
+    int no = 0, nf = 0;
+    if (len > 0) kload(0, nf, nx, ny, no);
+    for (int base = 0; base < len; base += kWave) {
         const float kx = nx, ky = ny;
-        const int ko = no;
-        if (base + kWave < a.n) kload(base + kWave, nx, ny, no);
-        const int fi = base + lane;
+        const int ko = no, fi = nf;
+        if (base + kWave < len) kload(base + kWave, nf, nx, ny, no);
         uint32_t key = kFusedNone, ent = kFusedNone;
-        if (fi < a.n) {
+        if (base + lane < len) {
             // PosInGrid (Frame.cc:725-735) and the cell range the window visits
             const int gx = (int)roundf((kx - a.g.min_x) * a.g.inv_w);
             const int gy = (int)roundf((ky - a.g.min_y) * a.g.inv_h);
@@ -3221,10 +3289,19 @@ __device__ __forceinline__ int fused_accept(const ProjArgs& a, int best, int lvl
 __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bound, uint32_t* __restrict__ lists,
                                                                int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                                const int32_t* __restrict__ owner_in,
-                                                               int32_t* __restrict__ out, int lds_lists) {
+                                                               int32_t* __restrict__ out, int lds_lists,
+                                                               int use_grid) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    // the frame's grid after the phase-2 tables (used by phase 1 and the rescans)
+    int* gcs = nullptr;
+    uint32_t* gent = nullptr;
+    if (use_grid) {
+        gcs = fl + proj_fused_lds(n, nq, lds_lists != 0) / 4;
+        gent = (uint32_t*)(gcs + kGridInts);
+        lds_grid_build(a.kps, n, a.g, -1, gcs, gent, (int*)(gent + max(1, n)));
+    }
     int* T = fl;
     int* D = T + n;
     int* dry = D + nq;
@@ -3242,7 +3319,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                 if (lane == 0) cnt[i] = -1;
             } else {
                 uint32_t run, run_e;
-                const int total = fused_select<kProjK>(a, i, q, bound, nullptr, 0, run, run_e);
+                const int total = fused_select<kProjK>(a, i, q, bound, nullptr, 0, gcs, gent, run, run_e);
                 if (lane < kProjK) lists[(long long)i * kProjK + lane] = run_e;
                 if (lane == 0) cnt[i] = total;
             }
@@ -3339,7 +3416,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
             ProjQuery q;
             proj_query(a, j, q);
             uint32_t run, run_e;
-            fused_select<2>(a, j, q, bound, T, j, run, run_e);
+            fused_select<2>(a, j, q, bound, T, j, gcs, gent, run, run_e);
             const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 0);
             const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 1);
             int dec = -1;
@@ -4133,7 +4210,7 @@ struct SfiFusedArgs {
 };
 
 // LDS: D[n1] | dry[n1] | ccnt[n2 + 1] | cstart[n2 + 1] | claims[n1] | hist[32] | misc[8]
-static size_t sfi_fused_lds(int n1, int n2) { return (size_t)(3 * n1 + 2 * (n2 + 1) + 40) * 4; }
+__host__ __device__ inline size_t sfi_fused_lds(int n1, int n2) { return (size_t)(3 * n1 + 2 * (n2 + 1) + 40) * 4; }
 
 // K smallest candidate keys of F1 keypoint i (d << 24 | cell << 12 | F2 index),
 // skipping (cl != nullptr) candidates a claim before query j blocks; lane r < K
@@ -4141,32 +4218,39 @@ static size_t sfi_fused_lds(int n1, int n2) { return (size_t)(3 * n1 + 2 * (n2 +
 // number of candidates within the bound.
 template <int K>
 __device__ int sfi_select(const SfiFusedArgs& a, int i, const CellRange& cr, float px, float py, const int* ccnt,
-                          const int* cstart, const int* claims, int j, uint32_t& run, uint32_t& run_e) {
+                          const int* cstart, const int* claims, int j, const int* gcs, const uint32_t* gent,
+                          uint32_t& run, uint32_t& run_e) {
     const int lane = lane_id();
     const uint4 q0 = *(const uint4*)(a.d1 + (long long)i * 32);
     const uint4 q1 = *(const uint4*)(a.d1 + (long long)i * 32 + 16);
     const float r = a.window;
     const float* kf = (const float*)a.k2;
     const int kw = (int)(sizeof(orb_keypoint) / 4);
-    auto kload = [&](int base, float& x, float& y, int& o) {
-        const int fi = min(base + lane, max(a.n2 - 1, 0));
-        x = kf[(long long)fi * kw + 0];
-        y = kf[(long long)fi * kw + 1];
-        o = ((const int*)kf)[(long long)fi * kw + 5];
+    WinCols w{};
+    int len = a.n2;
+    if (gcs) {
+        w = win_cols(gcs, cr);
+        len = w.total;
+    }
+    auto kload = [&](int base, int& f, float& x, float& y, int& o) {
+        const int p = min(base + lane, max(len - 1, 0));
+        f = gcs ? (int)(win_entry(w, gent, p) & 0xfff) : p;
+        x = kf[(long long)f * kw + 0];
+        y = kf[(long long)f * kw + 1];
+        o = ((const int*)kf)[(long long)f * kw + 5];
     };
     run = kFusedNone;
     run_e = kFusedNone;
     int total = 0;
     float nx = 0.f, ny = 0.f;
-    int no = 0;
-    if (a.n2 > 0) kload(0, nx, ny, no);
-    for (int base = 0; base < a.n2; base += kWave) {
+    int no = 0, nf = 0;
+    if (len > 0) kload(0, nf, nx, ny, no);
+    for (int base = 0; base < len; base += kWave) {
         const float kx = nx, ky = ny;
-        const int ko = no;
-        if (base + kWave < a.n2) kload(base + kWave, nx, ny, no);
-        const int fi = base + lane;
+        const int ko = no, fi = nf;
+        if (base + kWave < len) kload(base + kWave, nf, nx, ny, no);
         uint32_t key = kFusedNone, ent = kFusedNone;
-        if (fi < a.n2 && ko == 0) {
+        if (base + lane < len && ko == 0) {
             const int gx = (int)roundf((kx - a.g.min_x) * a.g.inv_w);
             const int gy = (int)roundf((ky - a.g.min_y) * a.g.inv_h);
             if (gx >= cr.x0 && gx <= cr.x1 && gy >= cr.y0 && gy <= cr.y1 && gx >= 0 && gx < kGridCols && gy >= 0 &&
@@ -4222,9 +4306,17 @@ __device__ __forceinline__ bool sfi_accept(int best, int best2, float ratio) {
 
 __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uint32_t* __restrict__ lists,
                                                               int* __restrict__ cnt, unsigned* __restrict__ ticket,
-                                                              int32_t* __restrict__ out) {
+                                                              int32_t* __restrict__ out, int use_grid) {
     extern __shared__ __attribute__((aligned(16))) int sl[];
     const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    // F2's level-0 grid after the phase-2 tables (phase 1 and the rescans)
+    int* gcs = nullptr;
+    uint32_t* gent = nullptr;
+    if (use_grid) {
+        gcs = sl + sfi_fused_lds(n1, n2) / 4;
+        gent = (uint32_t*)(gcs + kGridInts);
+        lds_grid_build(a.k2, n2, a.g, 0, gcs, gent, (int*)(gent + max(1, n2)));
+    }
     int* D = sl;                                // decision: -1 none, else slot | d << 12 | bin << 20
     int* dry = D + n1;
     int* ccnt = dry + n1;                       // claims per slot
@@ -4242,7 +4334,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
                 if (lane == 0) cnt[i] = -1;
             } else {
                 uint32_t run, run_e;
-                const int total = sfi_select<kTopK>(a, i, cr, px, py, nullptr, nullptr, nullptr, 0, run, run_e);
+                const int total = sfi_select<kTopK>(a, i, cr, px, py, nullptr, nullptr, nullptr, 0, gcs, gent, run, run_e);
                 if (lane < kTopK) lists[(long long)i * kTopK + lane] = run_e;
                 if (lane == 0) cnt[i] = total;
             }
@@ -4317,7 +4409,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
             CellRange cr;
             cell_range(px, py, a.window, a.g, cr);
             uint32_t run, run_e;
-            sfi_select<2>(a, j, cr, px, py, ccnt, cstart, cl, j, run, run_e);
+            sfi_select<2>(a, j, cr, px, py, ccnt, cstart, cl, j, gcs, gent, run, run_e);
             const uint32_t e1 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 0);
             const uint32_t e2 = (uint32_t)__builtin_amdgcn_readlane((int)run_e, 1);
             int dec = -1;
@@ -4483,7 +4575,8 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     if (f1->n > 0xffff || f2->n > 0xffff) return ORB_ERR_UNSUPPORTED;
     // fused single launch: one coalesced upload, one launch, one download of
     // [nmatches, matches12[n1], prev_xy[n1][2]]
-    if (debug_opt(ORB_OPT_SFI_FORM) == 0 && f1->n <= kFusedMaxN && f2->n <= kFusedMaxN && nnratio >= 0.2f &&
+    const int sform = debug_opt(ORB_OPT_SFI_FORM);
+    if ((sform == 0 || sform == 2) && f1->n <= kFusedMaxN && f2->n <= kFusedMaxN && nnratio >= 0.2f &&
         sfi_fused_lds(f1->n, f2->n) <= kCuLds) {
         SfiFusedArgs a{};
         DBuf<orb_keypoint> k1, k2; DBuf<uint8_t> d1, d2; DBuf<float> pv;
@@ -4504,8 +4597,11 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         while (bound < 255 && (float)(bound + 1) * nnratio <= (float)kThLow) ++bound;
         a.bound = bound;
         const int nblk = std::max(1, (n1 + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
-        KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), sfi_fused_lds(n1, n2), 0, a, lists.p, cnt.p, ticket.p,
-                out.d);
+        // F2's level-0 grid in LDS (form 2: none, every window scans F2)
+        const size_t gb = lds_grid_bytes(n2);
+        const int use_grid = sform == 0 && sfi_fused_lds(n1, n2) + gb <= kCuLds;
+        KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), sfi_fused_lds(n1, n2) + (use_grid ? gb : 0), 0, a,
+                lists.p, cnt.p, ticket.p, out.d, use_grid);
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)1 + 3 * n1);
         ORB_CHECK(out.fetch(res.data(), res.size()));
@@ -4879,10 +4975,14 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
     a.scale = df.scale.p; a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p;
     const int form = debug_opt(ORB_OPT_PROJ_FORM);
-    if (form == 0 && f->n <= kFusedMaxN && a.nq <= kFusedMaxQ && f->nlevels <= 8 &&
+    if ((form == 0 || form == 4) && f->n <= kFusedMaxN && a.nq <= kFusedMaxQ && f->nlevels <= 8 &&
         proj_fused_lds(f->n, a.nq, false) <= kCuLds) {
-        // the lists in LDS for phase 2 when they fit (else read from L2 each round)
-        const int lds_lists = proj_fused_lds(f->n, a.nq, true) <= kCuLds;
+        // the frame's grid in LDS (form 4: none, every window scans the frame),
+        // then the lists in LDS for phase 2 when they fit (else read from L2 each round)
+        const size_t gb = lds_grid_bytes(f->n);
+        const int use_grid = form == 0 && proj_fused_lds(f->n, a.nq, false) + gb <= kCuLds;
+        const int lds_lists = proj_fused_lds(f->n, a.nq, true) + (use_grid ? gb : 0) <= kCuLds;
+        const size_t lds = proj_fused_lds(f->n, a.nq, lds_lists != 0) + (use_grid ? gb : 0);
         DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; OutBlock out;
         const unsigned zero = 0;
         if ((rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, a.nq) * kProjK)) ||
@@ -4890,8 +4990,8 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
             return rc;
         a.nmatches = nullptr;
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
-        KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), proj_fused_lds(f->n, a.nq, lds_lists != 0), 0, a,
-                proj_bound(a), lists.p, cnt.p, ticket.p, own.p, out.d, lds_lists);
+        KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p, ticket.p,
+                own.p, out.d, lds_lists, use_grid);
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)f->n + 5);
         ORB_CHECK(out.fetch(res.data(), res.size()));

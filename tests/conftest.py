@@ -51,11 +51,12 @@ def debug_option():
 def proj_form(debug_option):
     """Projection-search form by name: fused (one launch: brute-force top-K +
     last-block fixpoint resolve, the default), serial (top-K + serial resolve),
-    single (single-wave search), spec (top-K + speculative resolve)."""
+    single (single-wave search), spec (top-K + speculative resolve),
+    fused_nogrid (the fused form scanning the whole frame per window)."""
     from orb_slam3_vio_fixes_amd import capi
 
     def set_(name):
-        debug_option(capi.ORB_OPT_PROJ_FORM, {"fused": 0, "serial": 1, "single": 2, "spec": 3}[name])
+        debug_option(capi.ORB_OPT_PROJ_FORM, {"fused": 0, "serial": 1, "single": 2, "spec": 3, "fused_nogrid": 4}[name])
     return set_
 
 
@@ -63,9 +64,9 @@ def proj_form(debug_option):
 def sfi_form(debug_option):
     """Host SearchForInitialization form by name: fused (one launch: brute-force
     top-K + last-block fixpoint resolve, the default) or grid (grid order +
-    top-K + serial resolve)."""
+    top-K + serial resolve) or fused_nogrid (fused, scanning all of F2)."""
     from orb_slam3_vio_fixes_amd import capi
 
     def set_(name):
-        debug_option(capi.ORB_OPT_SFI_FORM, {"fused": 0, "grid": 1}[name])
+        debug_option(capi.ORB_OPT_SFI_FORM, {"fused": 0, "grid": 1, "fused_nogrid": 2}[name])
     return set_
