@@ -223,7 +223,8 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        1 top-K + serial resolve, 2 single-wave search,
  *                        3 top-K + speculative resolve, 4 the fused form
  *                        without its in-block LDS grid (every window scans
- *                        the whole frame)
+ *                        the whole frame), 5 the fused form as two
+ *                        launches (phase 1; phase 2 in one block)
  *   ORB_OPT_BOW_FORM     map-wide SearchByBoW: 0 lane per keyframe feature
  *                        (k_bowk_*) when the map carries its totals, 1 k_bow
  *   ORB_OPT_BOWK_BIG     0 auto, 1 no big-node resolve form (every frame node
@@ -236,7 +237,7 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *   ORB_OPT_SFI_FORM     host SearchForInitialization: 0 fused single launch
  *                        (frames <= 4096 keypoints, nnratio >= 0.2; else 1),
  *                        1 grid + top-K + serial resolve, 2 fused without
- *                        its in-block LDS grid
+ *                        its in-block LDS grid, 3 fused as two launches
  *   ORB_OPT_HOST_OUT     single-launch host calls (fused projection and
  *                        initialization searches): 0 result block copied back
  *                        by one device-to-host copy, 1 written by the kernel
@@ -440,9 +441,12 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
 int orbm_release_scratch(void* stream, int all);
 
 /* Test hook: statistics of the calling thread's last projection search that
- * took the fused form (ORB_OPT_PROJ_FORM 0): fixpoint rounds, exact rescans,
- * and the last block's phase-1 and phase-2 shader clocks (s_memtime ticks). */
-int orbm_debug_proj_stats(int32_t* out4);
+ * took the fused form (ORB_OPT_PROJ_FORM 0), 12 ints: fixpoint rounds, exact
+ * rescans, the last block's phase-1 and phase-2 shader clocks (s_memtime
+ * ticks), its wave 0's grid-build and top-K selection clocks, the block's
+ * lifetime in 100 MHz ticks (s_memrealtime), phase 2's table setup clocks,
+ * and phase 2's decision passes, rescans, claim-table rebuilds and outputs. */
+int orbm_debug_proj_stats(int32_t* out12);
 
 /* Map points projected into F (the fields ORBmatcher reads from MapPoint,
  * MapPoint.h mTrackProjX/Y/XR, mnTrackScaleLevel, mTrackViewCos, mbTrackInView,

@@ -1451,8 +1451,31 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
 // co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private KF
 // descriptor areas (2 * 64 uint4 each).
 __device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins);
+// The last-arriver hand-off of the single-launch kernels (the split-K recipe
+// of cdna_hip_programming.md): every wave drains its stores, ONE lane releases
+// at agent scope (a buffer_wbl2 per block, not one per thread as
+// __threadfence() in every thread costs) and draws a relaxed agent-scope
+// ticket; the block drawing the last one acquires and reads everyone's
+// results.  flag: one int of the block's LDS.  Every thread calls it.
+__device__ __forceinline__ bool last_arriver(unsigned* ticket, int* flag) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // keep: the fence's own wait can be dropped
+        const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int last = t == gridDim.x - 1;
+        if (last) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        *flag = last;
+    }
+    __syncthreads();
+    return *flag != 0;
+}
 static_assert(2 * kBowBigCap >= 4 * 2 * kWave, "s_fd holds the small-node waves' descriptor areas");
-static_assert(kBowBigCap >= 33, "s_fi holds the fused final's histogram and drop count");
+static_assert(kBowBigCap >= 41, "s_fi holds the fused final's histogram, drop count and last-arriver flag");
 __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_slots) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
@@ -1461,13 +1484,7 @@ __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_
     if (a.fin_ticket) {
         // a single pair: the last block to finish runs the rotation filter on
         // every block's matches (the match rows, nmatches and the LDS are free)
-        __shared__ int last;
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(a.fin_ticket, 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (!last) return;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        if (!last_arriver(a.fin_ticket, s_fi + 40)) return;
         bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd));
     }
 }
@@ -3290,10 +3307,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                                                                int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                                const int32_t* __restrict__ owner_in,
                                                                int32_t* __restrict__ out, int lds_lists,
-                                                               int use_grid) {
+                                                               int use_grid, int part) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
-    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     // the frame's grid after the phase-2 tables (used by phase 1 and the rescans)
     int* gcs = nullptr;
     uint32_t* gent = nullptr;
@@ -3302,6 +3319,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         gent = (uint32_t*)(gcs + kGridInts);
         lds_grid_build(a.kps, n, a.g, -1, gcs, gent, (int*)(gent + max(1, n)));
     }
+    const unsigned long long tg = __builtin_amdgcn_s_memtime();
+    unsigned long long tsel = 0;
     int* T = fl;
     int* D = T + n;
     int* dry = D + nq;
@@ -3310,8 +3329,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     uint8_t* pre = (uint8_t*)(misc + 8);
     int* Cs = (int*)(pre + ((n + 15) / 16 * 16));
     uint32_t* Ls = (uint32_t*)(Cs + nq);
-    // ---- phase 1: one wave per query
-    {
+    // ---- phase 1: one wave per query (part 0: all of it in this launch with
+    // a ticket; part 1: phase 1 only; part 2: one block, phase 2 only)
+    if (part != 2) {
         const int i = blockIdx.x * (kFusedThreads / kWave) + wv;
         if (i < nq) {
             ProjQuery q;
@@ -3319,19 +3339,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                 if (lane == 0) cnt[i] = -1;
             } else {
                 uint32_t run, run_e;
+                const unsigned long long ts = __builtin_amdgcn_s_memtime();
                 const int total = fused_select<kProjK>(a, i, q, bound, nullptr, 0, gcs, gent, run, run_e);
+                tsel = __builtin_amdgcn_s_memtime() - ts;
                 if (lane < kProjK) lists[(long long)i * kProjK + lane] = run_e;
                 if (lane == 0) cnt[i] = total;
             }
         }
     }
+    if (part == 1) return;
     // ---- the last block to finish phase 1 runs phase 2
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) misc[0] = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!misc[0]) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (part == 0 && !last_arriver(ticket, &misc[0])) return;
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const int mode = a.mode, skip_any = a.skip_any, ori = a.mode == 1 && a.check_ori;
     int rounds = 0, ndry_total = 0;
@@ -3350,9 +3368,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     if (tid < 8) misc[tid] = 0;
     if (tid == 0) misc[1] = nq;
     __syncthreads();
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
     const uint4* Lsrc = lds_lists ? (const uint4*)Ls : (const uint4*)lists;
     const int* Csrc = lds_lists ? Cs : cnt;
     int settled = 0;          // queries below it decided the same in the last two rounds: final
+    unsigned long long c_dec = 0, c_res = 0, c_reb = 0, tc = __builtin_amdgcn_s_memtime();
     for (int round = 0; round <= nq; ++round) {
         // decisions under this round's T, queries >= settled only (an earlier
         // query's decision reads only claims of queries before it, all final).
@@ -3407,6 +3427,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         }
         }
         __syncthreads();
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_dec += t_ - tc; tc = t_; }
         // exact rescans of the decisions a truncated list could not make: one wave each
         const int ndry = misc[2];
         ++rounds;
@@ -3434,6 +3455,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
             }
         }
         __syncthreads();
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_res += t_ - tc; tc = t_; }
         const int first_changed = misc[1];
         __syncthreads();
         if (first_changed >= nq) break;
@@ -3447,6 +3469,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
             if (dec >= 0 && (dec >> 12 & 1)) atomicMin(&T[dec & 0xfff], j);
         }
         __syncthreads();
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_reb += t_ - tc; tc = t_; }
     }
     // ---- outputs: the last claimer of each slot, nmatches, rotation filter
     for (int s = tid; s < n; s += kFusedThreads) T[s] = -1;
@@ -3493,6 +3516,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         out[n + 2] = ndry_total;
         out[n + 3] = (int)min(t1 - t0, 0x7fffffffull);
         out[n + 4] = (int)min(__builtin_amdgcn_s_memtime() - t1, 0x7fffffffull);
+        // wave 0's grid build and selection, the whole block in 100 MHz ticks
+        // (calibrates the shader clock), phase 2's table setup
+        out[n + 5] = (int)min(tg - t0, 0x7fffffffull);
+        out[n + 6] = (int)min(tsel, 0x7fffffffull);
+        out[n + 7] = (int)min(__builtin_amdgcn_s_memrealtime() - rt0, 0x7fffffffull);
+        out[n + 8] = (int)min(t2 - t1, 0x7fffffffull);
+        // phase 2 by step: decision passes, rescans, T rebuilds, the outputs
+        out[n + 9] = (int)min(c_dec, 0x7fffffffull);
+        out[n + 10] = (int)min(c_res, 0x7fffffffull);
+        out[n + 11] = (int)min(c_reb, 0x7fffffffull);
+        out[n + 12] = (int)min(__builtin_amdgcn_s_memtime() - tc, 0x7fffffffull);
     }
 }
 
@@ -4141,7 +4175,7 @@ struct DevFrame {
 };
 
 // the last fused projection search's statistics (orbm_debug_proj_stats)
-static int32_t* proj_stats() { static thread_local int32_t st[4] = {0, 0, 0, 0}; return st; }
+static int32_t* proj_stats() { static thread_local int32_t st[12] = {}; return st; }
 
 // Start of a synchronous host-API call: a device must be present; the call's
 // arenas start empty.
@@ -4306,7 +4340,7 @@ __device__ __forceinline__ bool sfi_accept(int best, int best2, float ratio) {
 
 __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uint32_t* __restrict__ lists,
                                                               int* __restrict__ cnt, unsigned* __restrict__ ticket,
-                                                              int32_t* __restrict__ out, int use_grid) {
+                                                              int32_t* __restrict__ out, int use_grid, int part) {
     extern __shared__ __attribute__((aligned(16))) int sl[];
     const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     // F2's level-0 grid after the phase-2 tables (phase 1 and the rescans)
@@ -4324,8 +4358,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     int* claims = cstart + n2 + 1;              // j << 8 | d, by slot, ascending j
     int* hist = claims + n1;
     int* misc = hist + 32;                      // 0 last block, 1 first changed, 2 ndry, 3 fill, 4 nm, 5 dropped
-    // ---- phase 1
-    {
+    // ---- phase 1 (part 0: both phases in this launch with a ticket; part 1:
+    // phase 1 only; part 2: one block, phase 2 only)
+    if (part != 2) {
         const int i = blockIdx.x * (kFusedThreads / kWave) + wv;
         if (i < n1) {
             const float px = a.prev[2 * i], py = a.prev[2 * i + 1];
@@ -4340,12 +4375,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
             }
         }
     }
-    __threadfence();
-    __syncthreads();
-    if (tid == 0) misc[0] = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!misc[0]) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (part == 1) return;
+    if (part == 0 && !last_arriver(ticket, &misc[0])) return;
     // ---- phase 2: fixpoint over all queries
     for (int j = tid; j < n1; j += kFusedThreads) D[j] = -2;
     for (int s = tid; s <= n2; s += kFusedThreads) { ccnt[s] = 0; cstart[s] = 0; }
@@ -4555,9 +4586,9 @@ int orb_debug_get_option(int option) {
 }
 
 
-int orbm_debug_proj_stats(int32_t* out4) {
-    if (!out4) return ORB_ERR_PARAM;
-    std::memcpy(out4, proj_stats(), 4 * sizeof(int32_t));
+int orbm_debug_proj_stats(int32_t* out12) {
+    if (!out12) return ORB_ERR_PARAM;
+    std::memcpy(out12, proj_stats(), 12 * sizeof(int32_t));
     return ORB_OK;
 }
 
@@ -4576,7 +4607,7 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
     // fused single launch: one coalesced upload, one launch, one download of
     // [nmatches, matches12[n1], prev_xy[n1][2]]
     const int sform = debug_opt(ORB_OPT_SFI_FORM);
-    if ((sform == 0 || sform == 2) && f1->n <= kFusedMaxN && f2->n <= kFusedMaxN && nnratio >= 0.2f &&
+    if ((sform == 0 || sform == 2 || sform == 3) && f1->n <= kFusedMaxN && f2->n <= kFusedMaxN && nnratio >= 0.2f &&
         sfi_fused_lds(f1->n, f2->n) <= kCuLds) {
         SfiFusedArgs a{};
         DBuf<orb_keypoint> k1, k2; DBuf<uint8_t> d1, d2; DBuf<float> pv;
@@ -4599,9 +4630,16 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         const int nblk = std::max(1, (n1 + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         // F2's level-0 grid in LDS (form 2: none, every window scans F2)
         const size_t gb = lds_grid_bytes(n2);
-        const int use_grid = sform == 0 && sfi_fused_lds(n1, n2) + gb <= kCuLds;
-        KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), sfi_fused_lds(n1, n2) + (use_grid ? gb : 0), 0, a,
-                lists.p, cnt.p, ticket.p, out.d, use_grid);
+        const int use_grid = sform != 2 && sfi_fused_lds(n1, n2) + gb <= kCuLds;
+        const size_t lds = sfi_fused_lds(n1, n2) + (use_grid ? gb : 0);
+        if (sform == 3) {      // phase 1, then phase 2 as a one-block launch (no ticket)
+            KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
+                    use_grid, 1);
+            KLAUNCH(k_sfi_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d, use_grid, 2);
+        } else {
+            KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
+                    use_grid, 0);
+        }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)1 + 3 * n1);
         ORB_CHECK(out.fetch(res.data(), res.size()));
@@ -4975,28 +5013,35 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
     a.kps = df.kps.p; a.desc = df.desc.p; a.n = f->n; a.u_right = f->u_right ? df.ur.p : nullptr;
     a.scale = df.scale.p; a.g = grid_params(f); a.owner = own.p; a.blocked = blk.p;
     const int form = debug_opt(ORB_OPT_PROJ_FORM);
-    if ((form == 0 || form == 4) && f->n <= kFusedMaxN && a.nq <= kFusedMaxQ && f->nlevels <= 8 &&
+    if ((form == 0 || form == 4 || form == 5) && f->n <= kFusedMaxN && a.nq <= kFusedMaxQ && f->nlevels <= 8 &&
         proj_fused_lds(f->n, a.nq, false) <= kCuLds) {
         // the frame's grid in LDS (form 4: none, every window scans the frame),
         // then the lists in LDS for phase 2 when they fit (else read from L2 each round)
         const size_t gb = lds_grid_bytes(f->n);
-        const int use_grid = form == 0 && proj_fused_lds(f->n, a.nq, false) + gb <= kCuLds;
+        const int use_grid = form != 4 && proj_fused_lds(f->n, a.nq, false) + gb <= kCuLds;
         const int lds_lists = proj_fused_lds(f->n, a.nq, true) + (use_grid ? gb : 0) <= kCuLds;
         const size_t lds = proj_fused_lds(f->n, a.nq, lds_lists != 0) + (use_grid ? gb : 0);
         DBuf<uint32_t> lists; DBuf<int> cnt; DBuf<unsigned> ticket; OutBlock out;
         const unsigned zero = 0;
         if ((rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, a.nq) * kProjK)) ||
-            (rc = cnt.alloc(std::max(1, a.nq))) || (rc = out.alloc((size_t)f->n + 5)))
+            (rc = cnt.alloc(std::max(1, a.nq))) || (rc = out.alloc((size_t)f->n + 13)))
             return rc;
         a.nmatches = nullptr;
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
-        KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p, ticket.p,
-                own.p, out.d, lds_lists, use_grid);
+        if (form == 5) {       // phase 1, then phase 2 as a one-block launch (no ticket)
+            KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 1);
+            KLAUNCH(k_proj_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p, ticket.p,
+                    own.p, out.d, lds_lists, use_grid, 2);
+        } else {
+            KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 0);
+        }
         ORB_CHECK(hipGetLastError());
-        std::vector<int32_t> res((size_t)f->n + 5);
+        std::vector<int32_t> res((size_t)f->n + 13);
         ORB_CHECK(out.fetch(res.data(), res.size()));
         if (f->n) std::memcpy(owner, res.data() + 1, (size_t)f->n * sizeof(int32_t));
-        std::memcpy(proj_stats(), res.data() + f->n + 1, 4 * sizeof(int32_t));
+        std::memcpy(proj_stats(), res.data() + f->n + 1, 12 * sizeof(int32_t));
         return res[0];
     }
     if ((rc = df.build_grid(f, 0)) || (rc = nm.alloc(1))) return rc;

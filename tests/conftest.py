@@ -56,7 +56,7 @@ def proj_form(debug_option):
     from orb_slam3_vio_fixes_amd import capi
 
     def set_(name):
-        debug_option(capi.ORB_OPT_PROJ_FORM, {"fused": 0, "serial": 1, "single": 2, "spec": 3, "fused_nogrid": 4}[name])
+        debug_option(capi.ORB_OPT_PROJ_FORM, {"fused": 0, "serial": 1, "single": 2, "spec": 3, "fused_nogrid": 4, "fused_split": 5}[name])
     return set_
 
 
@@ -68,5 +68,5 @@ def sfi_form(debug_option):
     from orb_slam3_vio_fixes_amd import capi
 
     def set_(name):
-        debug_option(capi.ORB_OPT_SFI_FORM, {"fused": 0, "grid": 1, "fused_nogrid": 2}[name])
+        debug_option(capi.ORB_OPT_SFI_FORM, {"fused": 0, "grid": 1, "fused_nogrid": 2, "fused_split": 3}[name])
     return set_

@@ -143,11 +143,14 @@ int main(int argc, char** argv)
     StatFn statfn = (StatFn)dlsym(lib, "orbm_debug_proj_stats");
     std::string extra;
     auto stats = [&](const char* name) {
-        int32_t st[4];
+        int32_t st[12];
         if (!statfn || statfn(st) != 0) return;
-        char b[200];
+        char b[600];
         std::snprintf(b, sizeof b, ", \"%s_stats\": {\"rounds\": %d, \"rescans\": %d, \"phase1_clk\": %d, "
-                      "\"phase2_clk\": %d}", name, st[0], st[1], st[2], st[3]);
+                      "\"phase2_clk\": %d, \"grid_clk\": %d, \"select_clk\": %d, \"block_10ns\": %d, "
+                      "\"p2_setup_clk\": %d, \"p2_decide_clk\": %d, \"p2_rescan_clk\": %d, \"p2_rebuild_clk\": %d, "
+                      "\"p2_out_clk\": %d}", name, st[0], st[1], st[2], st[3], st[4], st[5], st[6], st[7], st[8], st[9],
+                      st[10], st[11]);
         extra += b;
     };
     auto put = [&](const char* name, const Stat& s) {

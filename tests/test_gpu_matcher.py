@@ -31,7 +31,7 @@ def test_descriptor_distance(gpu_lib):
 @pytest.mark.parametrize("i1,i2,window,ratio,ori", [(0, 1, 100, 0.9, True), (1, 2, 100, 0.9, True),
                                                     (0, 2, 60, 0.8, False), (4, 5, 100, 0.9, True),
                                                     (2, 3, 400, 1.0, True), (0, 1, 30, 0.15, True)])
-@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "grid"])
+@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "fused_split", "grid"])
 def test_search_for_initialization(gpu_lib, frames, i1, i2, window, ratio, ori, form, sfi_form):
     sfi_form(form)
     f1, f2 = frames[i1], frames[i2]
@@ -93,7 +93,7 @@ def projection_queries(frames, seed, n=600):
 
 
 @pytest.mark.parametrize("zc", [0, 1])
-@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
 def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, proj_form, zc, debug_option):
     proj_form(single)
@@ -118,7 +118,7 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, 
     np.testing.assert_array_equal(own, rown)
 
 
-@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
 @pytest.mark.parametrize("zc", [0, 1])
 def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, proj_form, zc, debug_option):
@@ -140,7 +140,7 @@ def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, singl
     np.testing.assert_array_equal(own, rown)
 
 
-@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,reps", [(21, 2), (22, 3), (23, 4), (24, 12)])
 def test_search_by_projection_overlapping_lists(gpu_lib, frames, seed, reps, single, proj_form):
     """Queries repeated `reps` times (consecutive and far apart in the query
@@ -253,7 +253,7 @@ def _graded_copies(k0, d0, base, copies, jitter, seed, flip):
 @pytest.mark.parametrize("copies,ratio,ori,shuffle", [(12, 0.9, True, False), (20, 1.0, False, False),
                                                       (9, 0.95, True, False), (12, 0.9, True, True),
                                                       (20, 1.0, False, True)])
-@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "grid"])
+@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "fused_split", "grid"])
 def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, ratio, ori, shuffle, form, sfi_form):
     """F1 holds `copies` identical copies of each of 24 keypoints, F2 `copies`
     copies whose descriptors sit 0, 1, 2, ... bits away (both forms: the fused
@@ -287,7 +287,7 @@ def test_search_for_initialization_exhausted_lists(gpu_lib, frames, copies, rati
 
 
 @pytest.mark.parametrize("seed,jitter,window", [(31, 40.0, 100), (32, 150.0, 60), (33, 5.0, 200)])
-@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "grid"])
+@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "fused_split", "grid"])
 def test_search_for_initialization_moved_prev(gpu_lib, frames, seed, jitter, window, form, sfi_form):
     """vbPrevMatched moved away from F1's own positions, some outside the image
     (windows clipped at the grid border or missing it: no candidates)."""

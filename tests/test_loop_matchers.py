@@ -175,7 +175,7 @@ def test_gpu_bow_kf(gpu_lib, kfs, ratio, ori, seed):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("th,orb_dist,ori,seed", [(10, 100, True, 4), (3, 64, True, 5), (10, 100, False, 6)])
 def test_gpu_projection_kf(gpu_lib, kfs, th, orb_dist, ori, seed, single, proj_form):
     proj_form(single)
@@ -189,7 +189,7 @@ def test_gpu_projection_kf(gpu_lib, kfs, th, orb_dist, ori, seed, single, proj_f
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "spec", "serial", "single"])
+@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("th,ratio,seed", [(10, 1.0, 7), (8, 0.5, 8), (40, 2.0, 13)])
 def test_gpu_projection_sim3(gpu_lib, kfs, th, ratio, seed, single, proj_form):
     proj_form(single)
