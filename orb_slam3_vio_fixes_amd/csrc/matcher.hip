@@ -3343,7 +3343,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                 const int total = fused_select<kProjK>(a, i, q, bound, nullptr, 0, gcs, gent, run, run_e);
                 tsel = __builtin_amdgcn_s_memtime() - ts;
                 if (lane < kProjK) lists[(long long)i * kProjK + lane] = run_e;
-                if (lane == 0) cnt[i] = total;
+                // the count with the query's "blocking claim" flag (bit 30): phase 2
+                // reads no per-query global array
+                const int hob = a.skip_any ? 1 : a.qhas_obs[i] != 0;
+                if (lane == 0) cnt[i] = min(total, (1 << 30) - 1) | (hob << 30);
             }
         }
     }
@@ -3377,16 +3380,19 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         // decisions under this round's T, queries >= settled only (an earlier
         // query's decision reads only claims of queries before it, all final).
         // Groups of 4 queries per thread: 8 lists in registers at once spill
+        int chg = INT_MAX;        // the thread's first changed query (one LDS atomic per wave below)
 #pragma unroll 1
         for (int u0 = 0; u0 < kFusedQpt; u0 += 4) {
         if (tid + u0 * kFusedThreads >= nq) break;
         uint4 LA[4], LB[4];
-        int C[4];
+        int C[4], H[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int jj = tid + (u0 + u) * kFusedThreads;
             const int j = min(jj, max(nq - 1, 0));
-            C[u] = (jj < nq && jj >= settled) ? Csrc[j] : -1;
+            const int cr = (jj < nq && jj >= settled) ? Csrc[j] : -1;
+            C[u] = cr < 0 ? -1 : (cr & ((1 << 30) - 1));
+            H[u] = cr < 0 ? 0 : (cr >> 30) & 1;
             LA[u] = Lsrc[(long long)j * 2];
             LB[u] = Lsrc[(long long)j * 2 + 1];
         }
@@ -3416,16 +3422,17 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                     dec = -3;                                            // made by an exact rescan below
                     dry[atomicAdd(&misc[2], 1)] = j;
                 } else if (slot >= 0 && fused_accept(a, best, lvl, best2, lvl2)) {
-                    const int hob = skip_any ? 1 : a.qhas_obs[j] != 0;
-                    dec = slot | (hob << 12) | (bin << 13);
+                    dec = slot | (H[u] << 12) | (bin << 13);
                 }
             }
             if (dec != -3) {
-                if (dec != D[j]) atomicMin(&misc[1], j);
+                if (dec != D[j]) chg = min(chg, j);
                 D[j] = dec;
             }
         }
         }
+        chg = wave_min(chg, INT_MAX);
+        if (lane == 0 && chg < INT_MAX) atomicMin(&misc[1], chg);
         __syncthreads();
         { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_dec += t_ - tc; tc = t_; }
         // exact rescans of the decisions a truncated list could not make: one wave each
@@ -3480,7 +3487,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         if (dec < 0) continue;
         ++nacc;
         atomicMax(&T[dec & 0xfff], j);
-        if (ori) atomicAdd(&hist[(dec >> 13) & 31], 1);
+        if (ori) hist_add_wave(hist, (dec >> 13) & 31);
     }
     nacc = wave_sum(nacc);
     if (lane == 0) atomicAdd(&misc[3], nacc);
@@ -4388,6 +4395,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     const int* cl = nullptr;                    // no claims in round 0
     int settled = 0;
     for (int round = 0; round <= n1; ++round) {
+        int chg = INT_MAX;                       // the thread's first changed query
         for (int j = tid; j < n1; j += kFusedThreads) {
             if (j < settled) continue;
             const int c = cnt[j];
@@ -4428,10 +4436,12 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
                 }
             }
             if (dec != -3) {
-                if (dec != D[j]) atomicMin(&misc[1], j);
+                if (dec != D[j]) chg = min(chg, j);
                 D[j] = dec;
             }
         }
+        chg = wave_min(chg, INT_MAX);            // one LDS atomic per wave
+        if (lane == 0 && chg < INT_MAX) atomicMin(&misc[1], chg);
         __syncthreads();
         const int ndry = misc[2];
         for (int t = wv; t < ndry; t += kFusedThreads / kWave) {
@@ -4502,7 +4512,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     for (int j = tid; j < n1; j += kFusedThreads) {
         const int dec = D[j];
         if (dec < 0) continue;
-        if (a.check_ori) atomicAdd(&hist[(dec >> 20) & 31], 1);
+        if (a.check_ori) hist_add_wave(hist, (dec >> 20) & 31);
     }
     for (int s = tid; s < n2; s += kFusedThreads) nacc += ccnt[s] > 0;
     nacc = wave_sum(nacc);

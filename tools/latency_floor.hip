@@ -80,6 +80,33 @@ int main() {
     CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     std::printf("graph(H2D + kernel + D2H) + sync:    %.1f us\n",
                 med_us([&] { chk(hipGraphLaunch(ge, st)); chk(hipStreamSynchronize(st)); }));
+    // the same graph with its three nodes' parameters set again before every
+    // launch (what a per-call graph of a host API with varying sizes pays)
+    {
+        size_t nn = 0;
+        CK(hipGraphGetNodes(g, nullptr, &nn));
+        std::vector<hipGraphNode_t> nodes(nn);
+        CK(hipGraphGetNodes(g, nodes.data(), &nn));
+        hipGraphNode_t kn = nullptr, h2d = nullptr, d2h = nullptr;
+        for (auto nd : nodes) {
+            hipGraphNodeType t;
+            CK(hipGraphNodeGetType(nd, &t));
+            if (t == hipGraphNodeTypeKernel) kn = nd;
+            else if (t == hipGraphNodeTypeMemcpy) (h2d ? d2h : h2d) = nd;
+        }
+        hipKernelNodeParams kp{};
+        CK(hipGraphKernelNodeGetParams(kn, &kp));
+        int nin = NIN, nout = NOUT;
+        void* args[4] = {&din, &nin, &dout, &nout};
+        kp.kernelParams = args;
+        std::printf("graph + per-launch node updates:     %.1f us\n", med_us([&] {
+            chk(hipGraphExecMemcpyNodeSetParams1D(ge, h2d, din, hin, NIN * 4, hipMemcpyHostToDevice));
+            chk(hipGraphExecKernelNodeSetParams(ge, kn, &kp));
+            chk(hipGraphExecMemcpyNodeSetParams1D(ge, d2h, hout, dout, NOUT * 4, hipMemcpyDeviceToHost));
+            chk(hipGraphLaunch(ge, st));
+            chk(hipStreamSynchronize(st));
+        }));
+    }
     // zero-copy: the kernel reads the pinned host inputs and writes the pinned host outputs
     int *hin_d, *hout_d;
     CK(hipHostGetDevicePointer((void**)&hin_d, hin, 0));
