@@ -440,8 +440,9 @@ int orbm_search_by_bow_batch_device(const orbm_kf_map_device* map, const orbm_fr
  * or ORB_ERR_DEVICE if a set's stream reported an error (that set is kept). */
 int orbm_release_scratch(void* stream, int all);
 
-/* Test hook: statistics of the calling thread's last projection search that
- * took the fused form (ORB_OPT_PROJ_FORM 0), 12 ints: fixpoint rounds, exact
+/* Test hook: statistics of the calling thread's last projection or
+ * initialization search that took the fused form (ORB_OPT_PROJ_FORM 0,
+ * ORB_OPT_SFI_FORM 0), 12 ints: fixpoint rounds, exact
  * rescans, the last block's phase-1 and phase-2 shader clocks (s_memtime
  * ticks), its wave 0's grid-build and top-K selection clocks, the block's
  * lifetime in 100 MHz ticks (s_memrealtime), phase 2's table setup clocks,

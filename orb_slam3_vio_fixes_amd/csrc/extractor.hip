@@ -1493,7 +1493,7 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #define ORB_FAST_PIPE 0   // 1: pre-test LDS reads one round ahead (ORB_FAST_EMIT 1)
 #endif
 #ifndef ORB_FAST_INC
-#define ORB_FAST_INC 1    // pre-test item (row, pair) advanced by a carry per round (0: divided per round)
+#define ORB_FAST_INC 0    // 1: pre-test item (row, pair) advanced by a carry per round (measured: time neutral, VALU per wave 1,686 -> 1,749); 0: divided per round
 #endif
 #ifndef ORB_FAST_CELLOFF
 #define ORB_FAST_CELLOFF 1   // ROI address from the cell record alone (0: through the level table)

@@ -344,6 +344,29 @@ __host__ __device__ __forceinline__ void three_maxima(const int* h, int& i1, int
     else if (m3 < 0.1f * (float)m1) { i3 = -1; }
 }
 
+// The same from a whole wave (every lane active; every lane gets the result):
+// the serial scan's strict comparisons in ascending bin order rank the nonzero
+// bins by (count descending, bin ascending), so the three are three wave maxima
+// of count << 8 | (255 - bin) -- three DPP reductions instead of a 30-step
+// chain of dependent LDS reads on one lane.
+__device__ __forceinline__ void three_maxima_wave(const int* h, int& i1, int& i2, int& i3) {
+    const int l = lane_id();
+    const int c = l < kHisto ? h[l] : 0;
+    uint32_t key = c > 0 ? ((uint32_t)c << 8) | (uint32_t)(255 - l) : 0u;
+    uint32_t k[3];
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+        k[t] = ~wave_min(~key, 0xffffffffu);
+        if (key == k[t]) key = 0u;
+    }
+    const int m1 = (int)(k[0] >> 8), m2 = (int)(k[1] >> 8), m3 = (int)(k[2] >> 8);
+    i1 = k[0] ? 255 - (int)(k[0] & 0xff) : -1;
+    i2 = k[1] ? 255 - (int)(k[1] & 0xff) : -1;
+    i3 = k[2] ? 255 - (int)(k[2] & 0xff) : -1;
+    if (m2 < 0.1f * (float)m1) { i2 = -1; i3 = -1; }
+    else if (m3 < 0.1f * (float)m1) { i3 = -1; }
+}
+
 // ---------------------------------------------------------------------------
 // SearchForInitialization (ORBmatcher.cc:648-763) in two kernels.
 //
@@ -1529,7 +1552,7 @@ __device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p,
         }
         __syncthreads();
         int i1, i2, i3;
-        three_maxima(hist, i1, i2, i3);
+        three_maxima_wave(hist, i1, i2, i3);
         int d = 0;
 #ifndef ORB_BOWF_DROP4
 #define ORB_BOWF_DROP4 1   // 3.955 vs 4.02-4.04 ms per C5 query on one box
@@ -3494,7 +3517,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     __syncthreads();
     if (ori) {
         __shared__ int tm[3];
-        if (tid == 0) three_maxima(hist, tm[0], tm[1], tm[2]);
+        if (wv == 0) {
+            int x1, x2, x3;
+            three_maxima_wave(hist, x1, x2, x3);
+            if (lane == 0) { tm[0] = x1; tm[1] = x2; tm[2] = x3; }
+        }
         for (int s = tid; s < n; s += kFusedThreads) pre[s] = 0;          // reused: slot cleared
         __syncthreads();
         int drop = 0;
@@ -4250,8 +4277,8 @@ struct SfiFusedArgs {
     int check_ori, bound;
 };
 
-// LDS: D[n1] | dry[n1] | ccnt[n2 + 1] | cstart[n2 + 1] | claims[n1] | hist[32] | misc[8]
-__host__ __device__ inline size_t sfi_fused_lds(int n1, int n2) { return (size_t)(3 * n1 + 2 * (n2 + 1) + 40) * 4; }
+// LDS: D[n1] | dry[n1] | ccnt[n2 + 1] | cstart[n2 + 1] | claims[n1] | hist[32] | misc[8] | scan tmp[32]
+__host__ __device__ inline size_t sfi_fused_lds(int n1, int n2) { return (size_t)(3 * n1 + 2 * (n2 + 1) + 72) * 4; }
 
 // K smallest candidate keys of F1 keypoint i (d << 24 | cell << 12 | F2 index),
 // skipping (cl != nullptr) candidates a claim before query j blocks; lane r < K
@@ -4350,6 +4377,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
                                                               int32_t* __restrict__ out, int use_grid, int part) {
     extern __shared__ __attribute__((aligned(16))) int sl[];
     const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
     // F2's level-0 grid after the phase-2 tables (phase 1 and the rescans)
     int* gcs = nullptr;
     uint32_t* gent = nullptr;
@@ -4358,6 +4386,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
         gent = (uint32_t*)(gcs + kGridInts);
         lds_grid_build(a.k2, n2, a.g, 0, gcs, gent, (int*)(gent + max(1, n2)));
     }
+    const unsigned long long tg = __builtin_amdgcn_s_memtime();
+    unsigned long long tsel = 0;
     int* D = sl;                                // decision: -1 none, else slot | d << 12 | bin << 20
     int* dry = D + n1;
     int* ccnt = dry + n1;                       // claims per slot
@@ -4376,7 +4406,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
                 if (lane == 0) cnt[i] = -1;
             } else {
                 uint32_t run, run_e;
+                const unsigned long long ts = __builtin_amdgcn_s_memtime();
                 const int total = sfi_select<kTopK>(a, i, cr, px, py, nullptr, nullptr, nullptr, 0, gcs, gent, run, run_e);
+                tsel = __builtin_amdgcn_s_memtime() - ts;
                 if (lane < kTopK) lists[(long long)i * kTopK + lane] = run_e;
                 if (lane == 0) cnt[i] = total;
             }
@@ -4384,6 +4416,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     }
     if (part == 1) return;
     if (part == 0 && !last_arriver(ticket, &misc[0])) return;
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     // ---- phase 2: fixpoint over all queries
     for (int j = tid; j < n1; j += kFusedThreads) D[j] = -2;
     for (int s = tid; s <= n2; s += kFusedThreads) { ccnt[s] = 0; cstart[s] = 0; }
@@ -4393,7 +4426,9 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     __syncthreads();
     const float ratio = a.ratio;
     const int* cl = nullptr;                    // no claims in round 0
-    int settled = 0;
+    int settled = 0, rounds = 0, ndry_total = 0;
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    unsigned long long c_dec = 0, c_res = 0, c_reb = 0, tc = t2;
     for (int round = 0; round <= n1; ++round) {
         int chg = INT_MAX;                       // the thread's first changed query
         for (int j = tid; j < n1; j += kFusedThreads) {
@@ -4443,7 +4478,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
         chg = wave_min(chg, INT_MAX);            // one LDS atomic per wave
         if (lane == 0 && chg < INT_MAX) atomicMin(&misc[1], chg);
         __syncthreads();
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_dec += t_ - tc; tc = t_; }
         const int ndry = misc[2];
+        ++rounds;
+        ndry_total += ndry;
         for (int t = wv; t < ndry; t += kFusedThreads / kWave) {
             const int j = dry[t];
             const float px = a.prev[2 * j], py = a.prev[2 * j + 1];
@@ -4464,30 +4502,20 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
             }
         }
         __syncthreads();
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_res += t_ - tc; tc = t_; }
         const int first_changed = misc[1];
         __syncthreads();
         if (first_changed >= n1 && round > 0) break;
         settled = first_changed;
         // the claim lists of this round's decisions, by slot and ascending query
-        for (int s = tid; s <= n2; s += kFusedThreads) ccnt[s] = 0;
+        for (int s = tid; s <= n2; s += kFusedThreads) { ccnt[s] = 0; cstart[s] = 0; }
         if (tid == 0) { misc[1] = n1; misc[2] = 0; misc[3] = 0; }
         __syncthreads();
-        for (int j = tid; j < n1; j += kFusedThreads)
-            if (D[j] >= 0) atomicAdd(&ccnt[D[j] & 0xfff], 1);
+        for (int j = tid; j < n1; j += kFusedThreads)      // counts, then the segment starts in place
+            if (D[j] >= 0) atomicAdd(&cstart[D[j] & 0xfff], 1);
         __syncthreads();
-        if (wv == 0) {                                   // exclusive scan of the counts (one wave)
-            int run = 0;
-            for (int b = 0; b < n2; b += kWave) {
-                const int v = b + lane < n2 ? ccnt[b + lane] : 0;
-                const int inc = wave_incl_scan(v);
-                if (b + lane < n2) cstart[b + lane] = run + inc - v;
-                run += __shfl(inc, kWave - 1, kWave);
-            }
-        }
-        __syncthreads();
-        for (int s = tid; s < n2; s += kFusedThreads) ccnt[s] = 0;      // reused as fill positions
-        __syncthreads();
-        for (int j = tid; j < n1; j += kFusedThreads) {
+        block_excl_scan(cstart, n2, misc + 8);              // (ends in a barrier)
+        for (int j = tid; j < n1; j += kFusedThreads) {     // fill; ccnt ends as the counts
             const int dec = D[j];
             if (dec < 0) continue;
             const int s = dec & 0xfff;
@@ -4505,6 +4533,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
         }
         cl = claims;
         __syncthreads();
+        { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_reb += t_ - tc; tc = t_; }
     }
     // ---- outputs (with the final claim lists: the rounds ended on a fixpoint)
     // every accepted claim enters the histogram; the last claimer of a slot keeps it
@@ -4519,9 +4548,10 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     if (lane == 0) atomicAdd(&misc[4], nacc);
     __syncthreads();
     __shared__ int tm[3];
-    if (tid == 0) {
-        tm[0] = tm[1] = tm[2] = -1;
-        if (a.check_ori) three_maxima(hist, tm[0], tm[1], tm[2]);
+    if (wv == 0) {
+        int x1 = -1, x2 = -1, x3 = -1;
+        if (a.check_ori) three_maxima_wave(hist, x1, x2, x3);
+        if (lane == 0) { tm[0] = x1; tm[1] = x2; tm[2] = x3; }
     }
     __syncthreads();
     int drop = 0;
@@ -4549,6 +4579,20 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     if (tid == 0) {
         out[0] = misc[4] - misc[5];
         *ticket = 0u;
+        // statistics after the outputs, as k_proj_fused's (orbm_debug_proj_stats)
+        int32_t* st = out + 1 + 3 * n1;
+        st[0] = rounds;
+        st[1] = ndry_total;
+        st[2] = (int)min(t1 - t0, 0x7fffffffull);
+        st[3] = (int)min(__builtin_amdgcn_s_memtime() - t1, 0x7fffffffull);
+        st[4] = (int)min(tg - t0, 0x7fffffffull);
+        st[5] = (int)min(tsel, 0x7fffffffull);
+        st[6] = (int)min(__builtin_amdgcn_s_memrealtime() - rt0, 0x7fffffffull);
+        st[7] = (int)min(t2 - t1, 0x7fffffffull);
+        st[8] = (int)min(c_dec, 0x7fffffffull);
+        st[9] = (int)min(c_res, 0x7fffffffull);
+        st[10] = (int)min(c_reb, 0x7fffffffull);
+        st[11] = (int)min(__builtin_amdgcn_s_memtime() - tc, 0x7fffffffull);
     }
 }
 
@@ -4628,7 +4672,7 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         if ((rc = k1.put(f1->kps, n1)) || (rc = d1.put(f1->desc, (size_t)n1 * 32)) || (rc = k2.put(f2->kps, n2)) ||
             (rc = d2.put(f2->desc, (size_t)n2 * 32)) || (rc = pv.put(prev_xy, (size_t)2 * n1)) ||
             (rc = ticket.put(&zero, 1)) || (rc = lists.alloc((size_t)std::max(1, n1) * kTopK)) ||
-            (rc = cnt.alloc(std::max(1, n1))) || (rc = out.alloc((size_t)1 + 3 * n1)))
+            (rc = cnt.alloc(std::max(1, n1))) || (rc = out.alloc((size_t)13 + 3 * n1)))
             return rc;
         a.k1 = k1.p; a.d1 = d1.p; a.n1 = n1; a.k2 = k2.p; a.d2 = d2.p; a.n2 = n2; a.prev = pv.p;
         a.g = grid_params(f2); a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
@@ -4651,8 +4695,9 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
                     use_grid, 0);
         }
         ORB_CHECK(hipGetLastError());
-        std::vector<int32_t> res((size_t)1 + 3 * n1);
+        std::vector<int32_t> res((size_t)13 + 3 * n1);
         ORB_CHECK(out.fetch(res.data(), res.size()));
+        std::memcpy(proj_stats(), res.data() + 1 + 3 * n1, 12 * sizeof(int32_t));
         if (n1) {
             std::memcpy(matches12, res.data() + 1, (size_t)n1 * sizeof(int32_t));
             std::memcpy(prev_xy, res.data() + 1 + n1, (size_t)n1 * 2 * sizeof(float));

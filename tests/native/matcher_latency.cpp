@@ -174,6 +174,7 @@ int main(int argc, char** argv)
             check(nm, "SearchForInitialization");
         });
         put("search_for_initialization", s);
+        stats("search_for_initialization");
         m12.push_back(nm);
         save(pre + "_sfi.bin", m12.data(), m12.size());
     }
