@@ -2080,10 +2080,14 @@ void k_bowk_topk_mfma(BowKArgs k, const bowk_v4i* __restrict__ fexp) {
                 }
         } else {
             const int lim = nfx - t0 - 4 * h;        // rows (g & 3) + 8 (g >> 2) below it exist
+            const int lim0 = nfx - t0;               // the h = 0 half's bound, wave-uniform
 #pragma unroll
             for (int c = 0; c < NSET; ++c)
 #pragma unroll
                 for (int g = 0; g < 16; ++g) {
+                    // a row no lane holds is skipped by a scalar branch (a node's
+                    // last tile is on average half empty)
+                    if ((g & 3) + 8 * (g >> 2) >= lim0) continue;
                     int cg = kb + (g & 3) + 8 * (g >> 2);
                     asm volatile("" : "+s"(cg));
                     const uint32_t key = bowk_key(acc[c][g], neg, cg);
