@@ -239,9 +239,14 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        1 grid + top-K + serial resolve, 2 fused without
  *                        its in-block LDS grid, 3 fused as two launches
  *   ORB_OPT_HOST_OUT     single-launch host calls (fused projection and
- *                        initialization searches): 0 result block copied back
- *                        by one device-to-host copy, 1 written by the kernel
- *                        straight into pinned host memory (zero-copy)
+ *                        initialization searches, SearchByBoW): 0 result
+ *                        block written by the kernel into pinned host memory,
+ *                        then a completion word the call spins on (no stream
+ *                        synchronisation); 1 the same block, the call
+ *                        synchronises the stream; 2 a device block copied
+ *                        back by one device-to-host copy
+ *   ORB_OPT_UPLOAD       host calls' inputs: 0 one kernel reading the pinned
+ *                        staging buffer (k_pull), 1 hipMemcpyAsync
  * The two k_pyr_stream options are read when a handle builds its plan (the
  * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
@@ -254,7 +259,8 @@ enum {
     ORB_OPT_PYR_PRETEST = 4,
     ORB_OPT_SFI_FORM = 5,
     ORB_OPT_HOST_OUT = 6,
-    ORB_OPT_COUNT = 7
+    ORB_OPT_UPLOAD = 7,
+    ORB_OPT_COUNT = 8
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);

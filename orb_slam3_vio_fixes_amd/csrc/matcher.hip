@@ -1155,6 +1155,9 @@ struct BowArgs {
     int32_t* out12;           // KF-KF form: [KF1 features] KF2 feature or -1, else NULL
     int f_nleft = -1;         // the frame's Nleft (-1: mono / rectified)
     unsigned* fin_ticket = nullptr;   // single pair: k_bow's last block runs the final (k_bow_final's body)
+    int32_t* host_out = nullptr;      // ... and then copies match[f_n] + nmatches there (pinned host memory)
+    int* done = nullptr;              // ... and writes seq into this word (signal_done)
+    int seq = 0;
 };
 
 // One wave per (pair, vocabulary node) the two FeatureVectors share: the
@@ -1474,6 +1477,20 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
 // co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private KF
 // descriptor areas (2 * 64 uint4 each).
 __device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins);
+// The end of a host call's kernel (the last block, every thread): each wave's
+// result stores complete, then one lane releases them at system scope and
+// writes the call's sequence number into the word the host polls.
+__device__ __forceinline__ void signal_done(int* flag, int seq) {
+    if (!flag) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // The last-arriver hand-off of the single-launch kernels (the split-K recipe
 // of cdna_hip_programming.md): every wave drains its stores, ONE lane releases
 // at agent scope (a buffer_wbl2 per block, not one per thread as
@@ -1509,6 +1526,12 @@ __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_
         // every block's matches (the match rows, nmatches and the LDS are free)
         if (!last_arriver(a.fin_ticket, s_fi + 40)) return;
         bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd));
+        if (a.host_out) {
+            __syncthreads();
+            for (int i = threadIdx.x; i < a.f_n; i += blockDim.x) a.host_out[i] = a.match[i];
+            if (threadIdx.x == 0) a.host_out[a.f_n] = a.nmatches[0];
+            signal_done(a.done, a.seq);
+        }
     }
 }
 
@@ -3334,7 +3357,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                                                                int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                                const int32_t* __restrict__ owner_in,
                                                                int32_t* __restrict__ out, int lds_lists,
-                                                               int use_grid, int part) {
+                                                               int use_grid, int part, int* done, int seq) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -3566,6 +3589,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         out[n + 11] = (int)min(c_reb, 0x7fffffffull);
         out[n + 12] = (int)min(__builtin_amdgcn_s_memtime() - tc, 0x7fffffffull);
     }
+    signal_done(done, seq);
 }
 
 // Largest distance that can still decide a query (see k_proj_topk).
@@ -3981,12 +4005,32 @@ static Arena& host_stage() {
 struct PendingUpload { char* dst = nullptr; char* src = nullptr; size_t len = 0; };
 static PendingUpload& pending_upload() { static thread_local PendingUpload p; return p; }
 static size_t round256(size_t b) { return (b + 255) & ~size_t(255); }
+// The run goes up by k_pull, a kernel reading the pinned staging through its
+// device mapping, not by hipMemcpyAsync: a copy-engine transfer followed by a
+// dependent kernel costs ~30 us of hand-off on this box, a kernel followed by a
+// kernel ~5 us (tools/latency_floor.hip: upload + kernel + completion 41 vs
+// 22 us).  ORB_OPT_UPLOAD 1 selects hipMemcpyAsync.
+__global__ __launch_bounds__(256) void k_pull(const uint4* __restrict__ src, uint4* __restrict__ dst, long long n16,
+                                              int tail) {
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) dst[i] = src[i];
+    if (blockIdx.x == 0 && (int)threadIdx.x < tail)
+        ((uint8_t*)(dst + n16))[threadIdx.x] = ((const uint8_t*)(src + n16))[threadIdx.x];
+}
 static hipError_t flush_uploads() {
     PendingUpload& p = pending_upload();
     if (!p.len) return hipSuccess;
-    const hipError_t e = hipMemcpyAsync(p.dst, p.src, p.len, hipMemcpyHostToDevice, 0);
+    const PendingUpload q = p;
     p = PendingUpload{};
-    return e;
+    void* src_d = nullptr;
+    if (debug_opt(ORB_OPT_UPLOAD) == 1 || hipHostGetDevicePointer(&src_d, q.src, 0) != hipSuccess || !src_d ||
+        ((uintptr_t)q.dst | (uintptr_t)src_d) % 16)
+        return hipMemcpyAsync(q.dst, q.src, q.len, hipMemcpyHostToDevice, 0);
+    const long long n16 = (long long)(q.len / 16);
+    const int blocks = (int)std::min<long long>(1024, std::max<long long>(1, (n16 + 255) / 256));
+    hipLaunchKernelGGL(k_pull, dim3(blocks), dim3(256), 0, 0, (const uint4*)src_d, (uint4*)q.dst, n16,
+                       (int)(q.len % 16));
+    return hipGetLastError();
 }
 // A run still pending at the next call's reset was never used by a GPU
 // operation: it is dropped (issuing it now would race the reused staging).
@@ -4018,19 +4062,52 @@ static hipError_t d2h(void* dst, const void* src, size_t bytes) {
     return e;
 }
 
-// The result block of a single-launch host call: with ORB_OPT_HOST_OUT 1 the
-// kernel writes it straight into pinned host memory (the staging arena, mapped
-// into the device's address space) and the call only synchronises; else it is
-// device memory brought back by one d2h.
+// The word a host call's kernel writes last (system scope) and the host polls
+// instead of synchronising the stream: a sequence number per call, pinned and
+// mapped, one per host thread.
+struct DoneWord {
+    int* h = nullptr;
+    int* d = nullptr;
+    int seq = 0;
+};
+static DoneWord& done_word() {
+    static thread_local DoneWord w = [] {
+        DoneWord x;
+        if (hipHostMalloc((void**)&x.h, 64, hipHostMallocPortable) != hipSuccess ||
+            hipHostGetDevicePointer((void**)&x.d, x.h, 0) != hipSuccess) {
+            x.h = x.d = nullptr;
+        } else {
+            *(volatile int*)x.h = 0;
+        }
+        return x;
+    }();
+    return w;
+}
+
+// The result block of a single-launch host call.  ORB_OPT_HOST_OUT 0 (default):
+// the kernel writes it straight into pinned host memory (the staging arena,
+// mapped into the device's address space) and then a completion word the host
+// spins on; 1: the same block, but the call synchronises the stream; 2: device
+// memory brought back by one d2h.
 struct OutBlock {
     int32_t* d = nullptr;      // what the kernel writes
     int32_t* h = nullptr;      // host view (zero-copy) or nullptr
     size_t n = 0;
+    int* flag = nullptr;       // ORB_OPT_HOST_OUT 0: the completion word the kernel writes last (device view)
+    int seq = 0;
     int alloc(size_t cnt) {
         n = std::max<size_t>(1, cnt);
-        if (debug_opt(ORB_OPT_HOST_OUT) == 1) {
+        const int mode = debug_opt(ORB_OPT_HOST_OUT);
+        flag = nullptr;
+        if (mode != 2) {
             h = (int32_t*)host_stage().get(n * sizeof(int32_t));
             if (!h || hipHostGetDevicePointer((void**)&d, h, 0) != hipSuccess) return ORB_ERR_DEVICE;
+            if (mode != 1) {
+                DoneWord& w = done_word();
+                if (!w.h) return ORB_ERR_DEVICE;
+                flag = w.d;
+                seq = ++w.seq;
+            }
             return ORB_OK;
         }
         h = nullptr;
@@ -4040,7 +4117,22 @@ struct OutBlock {
     // after the launch: the block's words [0, cnt) into dst
     hipError_t fetch(int32_t* dst, size_t cnt) const {
         if (!h) return d2h(dst, d, cnt * sizeof(int32_t));
-        if (const hipError_t e = hipStreamSynchronize(0); e != hipSuccess) return e;
+        if (flag) {
+            // spin on the word; every 256 reads ask the stream whether it ended
+            // without writing it (a fault) -- then its error is the result
+            const volatile int* w = done_word().h;
+            for (unsigned spin = 1; *w != seq; ++spin) {
+                if ((spin & 255) == 0) {
+                    const hipError_t q = hipStreamQuery(0);
+                    if (q != hipErrorNotReady) {
+                        if (*w == seq) break;
+                        return q == hipSuccess ? hipErrorUnknown : q;
+                    }
+                }
+            }
+        } else if (const hipError_t e = hipStreamSynchronize(0); e != hipSuccess) {
+            return e;
+        }
         std::memcpy(dst, h, cnt * sizeof(int32_t));
         return hipSuccess;
     }
@@ -4378,7 +4470,8 @@ __device__ __forceinline__ bool sfi_accept(int best, int best2, float ratio) {
 
 __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uint32_t* __restrict__ lists,
                                                               int* __restrict__ cnt, unsigned* __restrict__ ticket,
-                                                              int32_t* __restrict__ out, int use_grid, int part) {
+                                                              int32_t* __restrict__ out, int use_grid, int part,
+                                                              int* done, int seq) {
     extern __shared__ __attribute__((aligned(16))) int sl[];
     const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -4598,6 +4691,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
         st[10] = (int)min(c_reb, 0x7fffffffull);
         st[11] = (int)min(__builtin_amdgcn_s_memtime() - tc, 0x7fffffffull);
     }
+    signal_done(done, seq);
 }
 
 }  // namespace orbmi
@@ -4692,11 +4786,12 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         const size_t lds = sfi_fused_lds(n1, n2) + (use_grid ? gb : 0);
         if (sform == 3) {      // phase 1, then phase 2 as a one-block launch (no ticket)
             KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
-                    use_grid, 1);
-            KLAUNCH(k_sfi_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d, use_grid, 2);
+                    use_grid, 1, (int*)nullptr, 0);
+            KLAUNCH(k_sfi_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d, use_grid, 2,
+                    out.flag, out.seq);
         } else {
             KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
-                    use_grid, 0);
+                    use_grid, 0, out.flag, out.seq);
         }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)13 + 3 * n1);
@@ -4827,30 +4922,23 @@ static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t
         return rc;
     // match[n] = -1 and nmatches = 0 go up with the inputs, and come back as one
     // download; the last k_bow block runs the rotation filter (one launch)
-    // (zero-copy, ORB_OPT_HOST_OUT 1: the block is initialised in pinned host
-    // memory and the kernel works on it there)
+    // (the zero-copy modes: the last block copies the finished row and count
+    // into the pinned result block)
     std::vector<int32_t> init((size_t)f->n + 1, -1);
     init[f->n] = 0;
     const unsigned zero = 0;
     DBuf<unsigned> ticket;
     OutBlock out;
-    if ((rc = ticket.put(&zero, 1))) return rc;
-    if (debug_opt(ORB_OPT_HOST_OUT) == 1) {
-        if ((rc = out.alloc(init.size()))) return rc;
-        std::memcpy(out.h, init.data(), init.size() * sizeof(int32_t));
-        m.p = out.d;
-        m.n = init.size();
-    } else {
-        if ((rc = m.put(init.data(), init.size()))) return rc;
-        out.d = m.p;
-        out.n = init.size();
-    }
+    if ((rc = ticket.put(&zero, 1)) || (rc = m.put(init.data(), init.size())) || (rc = out.alloc(init.size())))
+        return rc;
+    if (!out.h) out.d = m.p;          // ORB_OPT_HOST_OUT 2: the row itself comes back by d2h
     BowArgs a{};
     a.kf_kps = kk.p; a.kf_desc = kd.p; a.kf_valid = kvv.p; a.kp_off = kpo.p;
     a.kf_node = kn.p; a.kf_off = ko.p; a.kf_idx = ki.p; a.node_off = nodo.p; a.idx_off = idxo.p;
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = m.p + f->n;
     a.f_nleft = f_nleft; a.fin_ticket = ticket.p;
+    if (out.h) { a.host_out = out.d; a.done = out.flag; a.seq = out.seq; }
     if ((rc = launch_bow(a, 1, 0, bow_big_nodes(ffv), kfv->nnodes))) return rc;
     ORB_CHECK(out.fetch(init.data(), init.size()));
     if (f->n) std::memcpy(match_f, init.data(), (size_t)f->n * 4);
@@ -5089,12 +5177,12 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         if (form == 5) {       // phase 1, then phase 2 as a one-block launch (no ticket)
             KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
-                    ticket.p, own.p, out.d, lds_lists, use_grid, 1);
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 1, (int*)nullptr, 0);
             KLAUNCH(k_proj_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p, ticket.p,
-                    own.p, out.d, lds_lists, use_grid, 2);
+                    own.p, out.d, lds_lists, use_grid, 2, out.flag, out.seq);
         } else {
             KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
-                    ticket.p, own.p, out.d, lds_lists, use_grid, 0);
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 0, out.flag, out.seq);
         }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)f->n + 13);

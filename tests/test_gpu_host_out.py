@@ -1,6 +1,7 @@
-"""The single-launch host calls with their result block written straight into
-pinned host memory (ORB_OPT_HOST_OUT 1, zero-copy) equal the oracle, as the
-default copy-back form does (tests/test_gpu_matcher.py)."""
+"""The single-launch host calls in their other result modes (ORB_OPT_HOST_OUT
+1: zero-copy block + stream sync; 2: device block copied back) equal the
+oracle, as the default (zero-copy block + completion word) does
+(tests/test_gpu_matcher.py)."""
 import numpy as np
 import pytest
 
@@ -21,9 +22,10 @@ def fr(f):
     return abi.frame_struct(f[0], f[1], 752, 480, scale_factors=np.float32(1.2) ** np.arange(8, dtype=np.float32))
 
 
+@pytest.mark.parametrize("mode", [1, 2])
 @pytest.mark.parametrize("sfi", ["fused", "grid"])
-def test_initialization_zero_copy(gpu_lib, frames, debug_option, sfi_form, sfi):
-    debug_option(capi.ORB_OPT_HOST_OUT, 1)
+def test_initialization_result_modes(gpu_lib, frames, debug_option, sfi_form, sfi, mode):
+    debug_option(capi.ORB_OPT_HOST_OUT, mode)
     sfi_form(sfi)
     for i1, i2 in [(0, 1), (1, 2)]:
         f1, f2 = frames[i1], frames[i2]
@@ -35,8 +37,9 @@ def test_initialization_zero_copy(gpu_lib, frames, debug_option, sfi_form, sfi):
         np.testing.assert_array_equal(p2, rp2)
 
 
-def test_bow_zero_copy(gpu_lib, frames, debug_option):
-    debug_option(capi.ORB_OPT_HOST_OUT, 1)
+@pytest.mark.parametrize("mode", [1, 2])
+def test_bow_result_modes(gpu_lib, frames, debug_option, mode):
+    debug_option(capi.ORB_OPT_HOST_OUT, mode)
     rng = np.random.default_rng(5)
     f1, f2 = frames[0], frames[1]
     n1, n2 = len(f1[0]), len(f2[0])

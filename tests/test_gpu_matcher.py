@@ -92,12 +92,12 @@ def projection_queries(frames, seed, n=600):
     return rng, src, cur, k, qx.astype(np.float32), qy.astype(np.float32)
 
 
-@pytest.mark.parametrize("zc", [0, 1])
+@pytest.mark.parametrize("zc", [0, 1, 2])
 @pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
 def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, proj_form, zc, debug_option):
     proj_form(single)
-    debug_option(capi.ORB_OPT_HOST_OUT, zc)   # 1: result block written into pinned host memory
+    debug_option(capi.ORB_OPT_HOST_OUT, zc)   # 0 spin on a completion word, 1 stream sync, 2 copy back
     rng, src, cur, k, qx, qy = projection_queries(frames, seed)
     n = len(k)
     mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
@@ -120,7 +120,7 @@ def test_search_by_projection_mappoints(gpu_lib, frames, seed, th, far, single, 
 
 @pytest.mark.parametrize("single", ["fused", "fused_nogrid", "fused_split", "spec", "serial", "single"])
 @pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
-@pytest.mark.parametrize("zc", [0, 1])
+@pytest.mark.parametrize("zc", [0, 1, 2])
 def test_search_by_projection_last_frame(gpu_lib, frames, seed, mode, ori, single, proj_form, zc, debug_option):
     proj_form(single)
     debug_option(capi.ORB_OPT_HOST_OUT, zc)

@@ -22,6 +22,27 @@ __global__ void k_touch(const int* __restrict__ in, int n, int* __restrict__ out
     for (int i = threadIdx.x; i < m; i += blockDim.x) out[i] = red[i % blockDim.x] + i;
 }
 
+// reads n words of device data, writes m words and then a flag (seq) into
+// pinned host memory with system-scope release: the host polls the flag
+__global__ void k_touch_flag(const int* __restrict__ in, int n, int* __restrict__ out, int m, int* flag, int seq) {
+    int s = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += in[i];
+    __shared__ int red[1024];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += blockDim.x) out[i] = red[i % blockDim.x] + i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// host -> device by a kernel reading the pinned host buffer (16 B a thread)
+__global__ void k_pull(const uint4* __restrict__ src, uint4* __restrict__ dst, int n16) {
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += gridDim.x * blockDim.x) dst[i] = src[i];
+}
+
 template <class F> double med_us(F&& f, int reps = 300) {
     for (int i = 0; i < 20; ++i) f();
     std::vector<double> t(reps);
@@ -113,6 +134,56 @@ int main() {
     CK(hipHostGetDevicePointer((void**)&hout_d, hout, 0));
     std::printf("zero-copy kernel (1 block) + sync:   %.1f us\n",
                 med_us([&] { hipLaunchKernelGGL(k_touch, dim3(1), dim3(1024), 0, st, hin_d, NIN, hout_d, NOUT); chk(hipStreamSynchronize(st)); }));
+    {
+        int* hflag;
+        CK(hipHostMalloc((void**)&hflag, 64, hipHostMallocDefault));
+        int *hflag_d, *hout_d2;
+        CK(hipHostGetDevicePointer((void**)&hflag_d, hflag, 0));
+        CK(hipHostGetDevicePointer((void**)&hout_d2, hout, 0));
+        volatile int* vf = hflag;
+        int seq = 0;
+        *vf = 0;
+        std::printf("kernel + host poll (no sync):        %.1f us\n", med_us([&] {
+            ++seq;
+            hipLaunchKernelGGL(k_touch_flag, dim3(1), dim3(1024), 0, st, din, NIN, hout_d2, NOUT, hflag_d, seq);
+            while (*vf != seq) {}
+        }));
+        std::printf("H2D + kernel + host poll:            %.1f us\n", med_us([&] {
+            ++seq;
+            chk(hipMemcpyAsync(din, hin, NIN * 4, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_touch_flag, dim3(1), dim3(1024), 0, st, din, NIN, hout_d2, NOUT, hflag_d, seq);
+            while (*vf != seq) {}
+        }));
+        std::printf("H2D + kernel + host poll + sync:     %.1f us\n", med_us([&] {
+            ++seq;
+            chk(hipMemcpyAsync(din, hin, NIN * 4, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_touch_flag, dim3(1), dim3(1024), 0, st, din, NIN, hout_d2, NOUT, hflag_d, seq);
+            while (*vf != seq) {}
+            chk(hipStreamSynchronize(st));
+        }));
+        int* hin_d2;
+        CK(hipHostGetDevicePointer((void**)&hin_d2, hin, 0));
+        for (int nb : {16, 64, 160}) {
+            std::printf("pull kernel(%3d blk) + kernel + poll: %.1f us\n", nb, med_us([&] {
+                ++seq;
+                hipLaunchKernelGGL(k_pull, dim3(nb), dim3(256), 0, st, (const uint4*)hin_d2, (uint4*)din, NIN / 4);
+                hipLaunchKernelGGL(k_touch_flag, dim3(1), dim3(1024), 0, st, din, NIN, hout_d2, NOUT, hflag_d, seq);
+                while (*vf != seq) {}
+            }));
+        }
+        std::printf("pull + kernel + poll + D2H-free sync: %.1f us\n", med_us([&] {
+            ++seq;
+            hipLaunchKernelGGL(k_pull, dim3(64), dim3(256), 0, st, (const uint4*)hin_d2, (uint4*)din, NIN / 4);
+            hipLaunchKernelGGL(k_touch_flag, dim3(1), dim3(1024), 0, st, din, NIN, hout_d2, NOUT, hflag_d, seq);
+            chk(hipStreamSynchronize(st));
+        }));
+        std::printf("H2D + kernel + sync (zero-copy out): %.1f us\n", med_us([&] {
+            ++seq;
+            chk(hipMemcpyAsync(din, hin, NIN * 4, hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_touch_flag, dim3(1), dim3(1024), 0, st, din, NIN, hout_d2, NOUT, hflag_d, seq);
+            chk(hipStreamSynchronize(st));
+        }));
+    }
     std::printf("kernel alone on device data + sync:  %.1f us\n",
                 med_us([&] { hipLaunchKernelGGL(k_touch, dim3(1), dim3(1024), 0, st, din, NIN, dout, NOUT); chk(hipStreamSynchronize(st)); }));
     std::printf("status: %s\n", hipGetErrorString(err));
