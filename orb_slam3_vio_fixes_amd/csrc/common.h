@@ -47,6 +47,11 @@ inline bool lds_fits(const void* kernel, size_t dyn) {
 // forms for parity tests; every product default is 0
 int debug_opt(int option);
 
+// Host -> device copy of a pinned host buffer by a kernel reading it through
+// its device mapping (matcher.hip; hipMemcpyAsync when the buffer is not
+// mapped, misaligned, or ORB_OPT_UPLOAD is 1).  Stream-ordered, capturable.
+hipError_t pull_to_device(void* dst, const void* src_pinned, size_t len, hipStream_t st);
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & (kWave - 1); }
 // wave index within the block, made wave-uniform (SGPR) so per-wave indexing
 // of global tables compiles to scalar loads

@@ -4017,20 +4017,23 @@ __global__ __launch_bounds__(256) void k_pull(const uint4* __restrict__ src, uin
     if (blockIdx.x == 0 && (int)threadIdx.x < tail)
         ((uint8_t*)(dst + n16))[threadIdx.x] = ((const uint8_t*)(src + n16))[threadIdx.x];
 }
+hipError_t pull_to_device(void* dst, const void* src, size_t len, hipStream_t st) {
+    if (!len) return hipSuccess;
+    void* src_d = nullptr;
+    if (debug_opt(ORB_OPT_UPLOAD) == 1 || hipHostGetDevicePointer(&src_d, const_cast<void*>(src), 0) != hipSuccess ||
+        !src_d || ((uintptr_t)dst | (uintptr_t)src_d) % 16)
+        return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, st);
+    const long long n16 = (long long)(len / 16);
+    const int blocks = (int)std::min<long long>(1024, std::max<long long>(1, (n16 + 255) / 256));
+    hipLaunchKernelGGL(k_pull, dim3(blocks), dim3(256), 0, st, (const uint4*)src_d, (uint4*)dst, n16, (int)(len % 16));
+    return hipGetLastError();
+}
 static hipError_t flush_uploads() {
     PendingUpload& p = pending_upload();
     if (!p.len) return hipSuccess;
     const PendingUpload q = p;
     p = PendingUpload{};
-    void* src_d = nullptr;
-    if (debug_opt(ORB_OPT_UPLOAD) == 1 || hipHostGetDevicePointer(&src_d, q.src, 0) != hipSuccess || !src_d ||
-        ((uintptr_t)q.dst | (uintptr_t)src_d) % 16)
-        return hipMemcpyAsync(q.dst, q.src, q.len, hipMemcpyHostToDevice, 0);
-    const long long n16 = (long long)(q.len / 16);
-    const int blocks = (int)std::min<long long>(1024, std::max<long long>(1, (n16 + 255) / 256));
-    hipLaunchKernelGGL(k_pull, dim3(blocks), dim3(256), 0, 0, (const uint4*)src_d, (uint4*)q.dst, n16,
-                       (int)(q.len % 16));
-    return hipGetLastError();
+    return pull_to_device(q.dst, q.src, q.len, 0);
 }
 // A run still pending at the next call's reset was never used by a GPU
 // operation: it is dropped (issuing it now would race the reused staging).
