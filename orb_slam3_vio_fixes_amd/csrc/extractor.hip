@@ -2985,6 +2985,40 @@ __device__ __forceinline__ void patch_land(const uint32_t (&v)[kPV], uint8_t* ra
     }
 }
 
+#ifndef ORB_DESC_ROWLOAD
+#define ORB_DESC_ROWLOAD 0   // 1: lane r loads patch row r as three 16-byte loads (one address per lane, no div/mod)
+#endif
+// The row form: lane r < 43 holds row r's 12 dwords (3 x 16 B from a 4-byte
+// aligned address), lands them as 3 x ds_write_b128 at raw + 48 r.
+constexpr int kPR = 12;
+__device__ __forceinline__ void patch_issue_rows(const uint8_t* img, int pitch, int x0, int y0, uint32_t (&v)[kPR]) {
+    const int lane = lane_id();
+    if (lane < kRaw) {
+        // 12 consecutive dwords (the load vectorizer makes them dwordx4 loads)
+        const GlobalWords p = (GlobalWords)(img + (long long)(y0 + lane) * pitch + (x0 & ~3));
+#pragma unroll
+        for (int k = 0; k < kPR; ++k) v[k] = p[k];
+    }
+}
+__device__ __forceinline__ void patch_land_rows(const uint32_t (&v)[kPR], uint8_t* raw) {
+    const int lane = lane_id();
+    if (lane < kRaw) {
+        uint4* q = (uint4*)(raw + lane * kRawP);
+        q[0] = make_uint4(v[0], v[1], v[2], v[3]);
+        q[1] = make_uint4(v[4], v[5], v[6], v[7]);
+        q[2] = make_uint4(v[8], v[9], v[10], v[11]);
+    }
+}
+#if ORB_DESC_ROWLOAD
+constexpr int kPVN = kPR;
+#define DESC_PATCH_ISSUE patch_issue_rows
+#define DESC_PATCH_LAND patch_land_rows
+#else
+constexpr int kPVN = kPV;
+#define DESC_PATCH_ISSUE patch_issue
+#define DESC_PATCH_LAND patch_land
+#endif
+
 #ifndef ORB_DESC_BORDER_BATCH
 #define ORB_DESC_BORDER_BATCH 10   // reflected byte loads in flight per lane (0: the round-3 loop, one at a time)
 #endif
@@ -3202,9 +3236,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     // the top of its iteration, and the next one's; the register set freed by
     // the landing takes the keypoint after that, so the sets alternate and the
     // loop body is instantiated once per set
-    uint32_t pv[kPV];
+    uint32_t pv[kPVN];
 #if ORB_DESC_PF2
-    uint32_t pv2[kPV];
+    uint32_t pv2[kPVN];
 #endif
     DescKp cur{}, nxt{};
     int jc = -1, jn = -1;
@@ -3212,27 +3246,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
     const unsigned long long t_start = __builtin_amdgcn_s_memtime();
     unsigned long long tlast = t_start, d0 = 0, d1 = 0, d2 = 0, d3 = 0, d4 = 0, d5 = 0, dk = 0;
 #endif
-    auto take = [&](int& j, DescKp& k, uint32_t (&v)[kPV]) {       // the next valid slot, its patch issued
+    auto take = [&](int& j, DescKp& k, uint32_t (&v)[kPVN]) {      // the next valid slot, its patch issued
         j = -1;
         if (!todo) return;
         j = __builtin_ctzll(todo);
         todo &= todo - 1;
         k = desc_pick(mine, j);
         const int x0 = (int)(k.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((k.key >> 12) & 0xfff) + (kEdge - 3) - 21;
-        if (patch_interior(k.w, k.h, x0, y0)) patch_issue(k.img, k.pitch, x0, y0, v);
+        if (patch_interior(k.w, k.h, x0, y0)) DESC_PATCH_ISSUE(k.img, k.pitch, x0, y0, v);
     };
     take(jc, cur, pv);
 #if ORB_DESC_PF2
     take(jn, nxt, pv2);
 #endif
-    auto body = [&](uint32_t (&pvl)[kPV]) {
+    auto body = [&](uint32_t (&pvl)[kPVN]) {
         const long long s = s_begin + jc;
         const uint32_t key = cur.key;
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
         // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
         int sh = 0;
         if (patch_interior(cur.w, cur.h, cx - 21, cy - 21)) {
-            patch_land(pvl, raw);
+            DESC_PATCH_LAND(pvl, raw);
             sh = (cx - 21) & 3;
         } else {
             patch_border(cur.img, cur.pitch, cur.w, cur.h, cx - 21, cy - 21, raw);
