@@ -2986,7 +2986,7 @@ __device__ __forceinline__ void patch_land(const uint32_t (&v)[kPV], uint8_t* ra
 }
 
 #ifndef ORB_DESC_ROWLOAD
-#define ORB_DESC_ROWLOAD 0   // 1: lane r loads patch row r as three 16-byte loads (one address per lane, no div/mod)
+#define ORB_DESC_ROWLOAD 1   // lane r loads patch row r as three 16-byte loads (one address per lane, no div/mod): describe 281-285 -> 261-267 us (profiles/r05/desc_rowload_*); 0: the 516-dword spread
 #endif
 // The row form: lane r < 43 holds row r's 12 dwords (3 x 16 B from a 4-byte
 // aligned address), lands them as 3 x ds_write_b128 at raw + 48 r.
