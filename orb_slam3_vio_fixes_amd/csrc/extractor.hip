@@ -1528,10 +1528,23 @@ struct RoiFetch {
 // Addresses as 32-bit offsets from the cell's uniform row-0 pointer (one
 // v_mad_u32_u24 per load: a 64-bit product per load was two quarter-rate
 // v_mad_u64_u32, and the landing's r * nd a quarter-rate v_mul_lo_u32).
+#ifndef ORB_FAST_ROWLOAD
+X
+#endif
 template <int PDW, int NV>
 __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV]) {
     static_assert(kWave % PDW == 0, "rows of a load round are whole");
     const int lane = lane_id();
+#if ORB_FAST_ROWLOAD
+    if constexpr (PDW == 16 && NV == 16) {
+        // rows <= 64 in this form (NV * 64 / PDW); the dword offsets are immediates
+        const GlobalWords p = (GlobalWords)((GlobalBytes)rf.src + (uint32_t)min(lane, rf.rows - 1) * (uint32_t)rf.pitch);
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+            if (k < rf.nd) v[k] = p[k];
+        return;
+    }
+#endif
     const uint32_t col = 4u * (uint32_t)min(lane % PDW, rf.nd - 1);
     const GlobalBytes base = (GlobalBytes)rf.src;
 #pragma unroll
@@ -1544,6 +1557,17 @@ __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV])
 template <int PDW, int NV, int RP>
 __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)[NV], uint32_t* roi) {
     const int lane = lane_id();
+#if ORB_FAST_ROWLOAD
+    if constexpr (PDW == 16 && NV == 16) {
+        if (lane < rf.rows) {
+            uint32_t* q = roi + mad24((uint32_t)lane, (uint32_t)(RP ? RP : rf.nd), 0u);
+#pragma unroll
+            for (int k = 0; k < NV; ++k)
+                if (k < rf.nd) q[k] = v[k];
+        }
+        return;
+    }
+#endif
     const uint32_t d = (uint32_t)min(lane % PDW, rf.nd - 1);
 #pragma unroll
     for (int j = 0; j < NV; ++j) {
