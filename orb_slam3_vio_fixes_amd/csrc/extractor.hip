@@ -1529,7 +1529,7 @@ struct RoiFetch {
 // v_mad_u32_u24 per load: a 64-bit product per load was two quarter-rate
 // v_mad_u64_u32, and the landing's r * nd a quarter-rate v_mul_lo_u32).
 #ifndef ORB_FAST_ROWLOAD
-X
+#define ORB_FAST_ROWLOAD 1   // lane r fetches ROI row r's nd dwords (16-dword, 16-load forms; one address per lane): FAST 268.7-268.8 -> 265.1-266.1 us, VGPRs 95 -> 78 (profiles/r05/fast_rowload_*); 0: the spread
 #endif
 template <int PDW, int NV>
 __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV]) {
