@@ -1529,7 +1529,7 @@ struct RoiFetch {
 // v_mad_u32_u24 per load: a 64-bit product per load was two quarter-rate
 // v_mad_u64_u32, and the landing's r * nd a quarter-rate v_mul_lo_u32).
 #ifndef ORB_FAST_ROWLOAD
-#define ORB_FAST_ROWLOAD 1   // lane r fetches ROI row r's nd dwords (16-dword, 16-load forms; one address per lane): FAST 268.7-268.8 -> 265.1-266.1 us, VGPRs 95 -> 78 (profiles/r05/fast_rowload_*); 0: the spread
+#define ORB_FAST_ROWLOAD 2   // lane r fetches ROI row r (16-dword, 16-load forms; one address per lane): 2 in 16-byte groups (FAST 264.5-265.3 -> 260.4-261.7 us), 1 dword by dword (268.7-268.8 -> 265.1-266.1 us, VGPRs 95 -> 78; profiles/r05/fast_rowload_*); 0: the spread
 #endif
 template <int PDW, int NV>
 __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV]) {
@@ -1539,9 +1539,25 @@ __device__ __forceinline__ void roi_issue(const RoiFetch& rf, uint32_t (&v)[NV])
     if constexpr (PDW == 16 && NV == 16) {
         // rows <= 64 in this form (NV * 64 / PDW); the dword offsets are immediates
         const GlobalWords p = (GlobalWords)((GlobalBytes)rf.src + (uint32_t)min(lane, rf.rows - 1) * (uint32_t)rf.pitch);
+#if ORB_FAST_ROWLOAD == 2
+        // whole groups of 4 dwords as one 16-byte load each (4 line requests
+        // a lane instead of nd); the group holding the ROI's end dword by dword
+#pragma unroll
+        for (int g = 0; g < NV / 4; ++g) {
+            if (4 * g + 3 < rf.nd) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k) v[4 * g + k] = p[4 * g + k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (4 * g + k < rf.nd) v[4 * g + k] = p[4 * g + k];
+            }
+        }
+#else
 #pragma unroll
         for (int k = 0; k < NV; ++k)
             if (k < rf.nd) v[k] = p[k];
+#endif
         return;
     }
 #endif
