@@ -4109,7 +4109,9 @@ struct OutBlock {
                 DoneWord& w = done_word();
                 if (!w.h) return ORB_ERR_DEVICE;
                 flag = w.d;
-                seq = ++w.seq;
+                w.seq = (w.seq + 1) & 0x7fffffff;    // never 0 (the word's initial value)
+                if (!w.seq) w.seq = 1;
+                seq = w.seq;
             }
             return ORB_OK;
         }
@@ -4133,6 +4135,7 @@ struct OutBlock {
                     }
                 }
             }
+            std::atomic_thread_fence(std::memory_order_acquire);   // the block was released before the word
         } else if (const hipError_t e = hipStreamSynchronize(0); e != hipSuccess) {
             return e;
         }
