@@ -301,3 +301,42 @@ def test_search_for_initialization_moved_prev(gpu_lib, frames, seed, jitter, win
     assert nm == rnm
     np.testing.assert_array_equal(m12, rm12)
     np.testing.assert_array_equal(p2, rp2)
+
+
+@pytest.mark.parametrize("form", ["fused", "fused_nogrid", "grid"])
+def test_search_for_initialization_empty_frames(gpu_lib, frames, form, sfi_form):
+    """An empty F1 or F2 (no features): no matches, vbPrevMatched unchanged."""
+    sfi_form(form)
+    e = (np.zeros(0, abi.KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8))
+    f1 = frames[0]
+    prev = np.stack([f1[0]["x"], f1[0]["y"]], 1).astype(np.float32)
+    for a, b, p in [(f1, e, prev), (e, f1, np.zeros((0, 2), np.float32)), (e, e, np.zeros((0, 2), np.float32))]:
+        nm, m12, p2 = orb.ORBmatcher(0.9, True).SearchForInitialization(fr(a), fr(b), p, 100)
+        rnm, rm12, rp2 = O.search_for_initialization(fr(a), fr(b), p, 100, 0.9, True)
+        assert nm == rnm == 0
+        np.testing.assert_array_equal(m12, rm12)
+        np.testing.assert_array_equal(p2, rp2)
+
+
+@pytest.mark.parametrize("single", ["fused", "fused_nogrid", "spec"])
+def test_search_by_projection_empty_inputs(gpu_lib, frames, single, proj_form):
+    """No map points, or a frame without features: nothing matched, owner unchanged."""
+    proj_form(single)
+    rng, src, cur, k, qx, qy = projection_queries(frames, 8, n=0)
+    N = len(cur[0])
+    mps = abi.mappoints_struct(qx, qy, qx, k["octave"], np.zeros(0, np.float32), np.zeros(0, np.float32),
+                               np.zeros(0, np.uint8), np.zeros(0, np.uint8), src[1][:0])
+    F = abi.frame_struct(cur[0], cur[1], 752, 480, scale_factors=np.float32(1.2) ** np.arange(8, dtype=np.float32))
+    owner = np.full(N, -1, np.int32)
+    nm, own = orb.ORBmatcher(0.8, True).SearchByProjection(F, mps, 3.0, False, 50.0, owner, np.zeros(N, np.uint8))
+    assert nm == 0
+    np.testing.assert_array_equal(own, owner)
+    e = abi.frame_struct(np.zeros(0, abi.KEYPOINT_DTYPE), np.zeros((0, 32), np.uint8), 752, 480,
+                         scale_factors=np.float32(1.2) ** np.arange(8, dtype=np.float32))
+    rng, src, cur, k, qx, qy = projection_queries(frames, 9)
+    n = len(k)
+    mps = abi.mappoints_struct(qx, qy, qx, k["octave"], np.ones(n, np.float32), np.full(n, 10, np.float32),
+                               np.ones(n, np.uint8), np.ones(n, np.uint8), src[1][:n])
+    nm, own = orb.ORBmatcher(0.8, True).SearchByProjection(e, mps, 3.0, False, 50.0, np.zeros(0, np.int32),
+                                                           np.zeros(0, np.uint8))
+    assert nm == 0 and len(own) == 0
