@@ -3035,7 +3035,11 @@ __device__ __forceinline__ void patch_issue_rows(const uint8_t* img, int pitch, 
     const int lane = lane_id();
     if (lane < kRaw) {
         // 12 consecutive dwords (the load vectorizer makes them dwordx4 loads)
+#if ORB_DESC_ABL == 1
+        const GlobalWords p = (GlobalWords)(img + (long long)lane * pitch);   // ablation: one L2-resident patch (timing only)
+#else
         const GlobalWords p = (GlobalWords)(img + (long long)(y0 + lane) * pitch + (x0 & ~3));
+#endif
 #pragma unroll
         for (int k = 0; k < kPR; ++k) v[k] = p[k];
     }
