@@ -3189,12 +3189,26 @@ constexpr int kFusedMaxN = 4096;                    // 12-bit keypoint index in 
 constexpr int kFusedMaxQ = kFusedThreads * kFusedQpt;
 constexpr uint32_t kFusedNone = 0xffffffffu;
 
-// LDS: T[n] | D[nq] (decision per query) | dry[nq] | hist[32] | misc[8] |
-// pre[n] bytes | (lds_lists) C[nq] and the lists, kProjK words per query
+// byte offsets of k_proj_fused's phase-2 tables, every table 16-byte aligned
+// (the lists are read as 16-byte words)
+struct ProjLds { size_t T, D, dry, hist, misc, pre, Cs, Ls, total; };
+__host__ __device__ inline ProjLds proj_lds_layout(int n, int nq, bool lds_lists) {
+    auto al = [](size_t b) { return (b + 15) & ~size_t(15); };
+    ProjLds o{};
+    size_t at = 0;
+    o.T = at;    at += al((size_t)n * 4);
+    o.D = at;    at += al((size_t)nq * 4);
+    o.dry = at;  at += al((size_t)nq * 4);
+    o.hist = at; at += 32 * 4;
+    o.misc = at; at += 16 * 4;
+    o.pre = at;  at += al((size_t)n);
+    o.Cs = at;   if (lds_lists) at += al((size_t)nq * 4);
+    o.Ls = at;   if (lds_lists) at += (size_t)nq * kProjK * 4;
+    o.total = al(at);
+    return o;
+}
 __host__ __device__ inline size_t proj_fused_lds(int n, int nq, bool lds_lists) {
-    size_t b = (size_t)(n + 2 * nq + 32 + 8) * 4 + ((size_t)n + 15) / 16 * 16;
-    if (lds_lists) b += (size_t)nq * 4 + (size_t)nq * kProjK * 4;
-    return b;
+    return proj_lds_layout(n, nq, lds_lists).total;
 }
 
 // The frame's grid in each block's LDS (no grid-build launch): gcs[c] = start
@@ -3371,14 +3385,16 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     }
     const unsigned long long tg = __builtin_amdgcn_s_memtime();
     unsigned long long tsel = 0;
-    int* T = fl;
-    int* D = T + n;
-    int* dry = D + nq;
-    int* hist = dry + nq;
-    int* misc = hist + 32;          // 0 last-block flag, 1 first changed query, 2 ndry, 3 nm, 4 dropped, 5 settled prefix
-    uint8_t* pre = (uint8_t*)(misc + 8);
-    int* Cs = (int*)(pre + ((n + 15) / 16 * 16));
-    uint32_t* Ls = (uint32_t*)(Cs + nq);
+    const ProjLds lo = proj_lds_layout(n, nq, lds_lists != 0);
+    uint8_t* const fb = (uint8_t*)fl;
+    int* T = (int*)(fb + lo.T);
+    int* D = (int*)(fb + lo.D);
+    int* dry = (int*)(fb + lo.dry);
+    int* hist = (int*)(fb + lo.hist);
+    int* misc = (int*)(fb + lo.misc);   // 0 last-block flag, 1 first changed query, 2 ndry, 3 nm, 4 dropped
+    uint8_t* pre = fb + lo.pre;
+    int* Cs = (int*)(fb + lo.Cs);
+    uint32_t* Ls = (uint32_t*)(fb + lo.Ls);
     // ---- phase 1: one wave per query (part 0: all of it in this launch with
     // a ticket; part 1: phase 1 only; part 2: one block, phase 2 only)
     if (part != 2) {
