@@ -51,3 +51,28 @@ def test_bow_result_modes(gpu_lib, frames, debug_option, mode):
     rnm, rmatch = O.search_by_bow(fr(f1), kfv, valid, fr(f2), fv, 0.7, True)
     assert nm == rnm
     np.testing.assert_array_equal(match, rmatch)
+
+
+@pytest.mark.parametrize("upload", [0, 1])
+def test_projection_upload_forms(gpu_lib, frames, debug_option, upload):
+    """Inputs uploaded by the pull kernel (ORB_OPT_UPLOAD 0, default) or by
+    hipMemcpyAsync (1): the same owners as the oracle."""
+    debug_option(capi.ORB_OPT_UPLOAD, upload)
+    rng = np.random.default_rng(11 + upload)
+    src, cur = frames[0], frames[1]
+    k = src[0][:500]
+    qx = (k["x"] + rng.normal(0, 3, len(k)) + 3).astype(np.float32)
+    qy = (k["y"] + rng.normal(0, 3, len(k)) + 3).astype(np.float32)
+    n = len(k)
+    mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
+                               rng.uniform(0.99, 1.0, n).astype(np.float32), rng.uniform(0, 100, n).astype(np.float32),
+                               (rng.random(n) < 0.9).astype(np.uint8), (rng.random(n) < 0.7).astype(np.uint8),
+                               src[1][:n])
+    N = len(cur[0])
+    F = fr(cur)
+    owner = np.full(N, -1, np.int32)
+    blocked = np.zeros(N, np.uint8)
+    nm, own = orb.ORBmatcher(0.8, True).SearchByProjection(F, mps, 3.0, False, 50.0, owner, blocked)
+    rnm, rown = O.search_by_projection_mps(F, mps, 3.0, False, 50.0, 0.8, owner, blocked)
+    assert nm == rnm and nm > 0
+    np.testing.assert_array_equal(own, rown)
