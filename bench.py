@@ -715,12 +715,20 @@ def main():
                              "pairs_mismatched": bad_m, "compared": "keypoint count, all 28 keypoint bytes, 32 descriptor "
                                                                    "bytes, monoIndex, nmatches and the full matches12"}
         if world == 1 and args.host_api:
-            out["host_api"] = host_api_rates(frames_np)
+            # side measurements (not the metric): a failure here is reported in
+            # the line instead of losing it
+            try:
+                out["host_api"] = host_api_rates(frames_np)
+            except Exception as e:          # noqa: BLE001
+                out["host_api"] = {"error": f"{type(e).__name__}: {e}"[:300]}
             import tempfile
             with tempfile.TemporaryDirectory() as td:
-                mb = host_api_matchers(ring_np[0][:2], td)
-                if mb is not None and args.cpu_sample > 0:
-                    cpu_baseline_matchers(td, mb)
+                try:
+                    mb = host_api_matchers(ring_np[0][:2], td)
+                    if mb is not None and args.cpu_sample > 0:
+                        cpu_baseline_matchers(td, mb)
+                except Exception as e:      # noqa: BLE001
+                    mb = {"error": f"{type(e).__name__}: {e}"[:300]}
                 out["host_api"]["matchers"] = mb
         print(json.dumps(out), flush=True)
     if world > 1:
