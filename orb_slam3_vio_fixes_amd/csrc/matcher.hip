@@ -1068,7 +1068,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     int nm = qlist[0];
     if (a.check_ori) {
         int i1x, i2x, i3x;
-        three_maxima(hist, i1x, i2x, i3x);   // bins 0..29
+        three_maxima_wave(hist, i1x, i2x, i3x);   // bins 0..29
         int drop = 0;
         for (int i = tid; i < n1; i += kSfiThreads) {
             const int b = bin1[i];
@@ -2483,7 +2483,7 @@ __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
     }
     __syncthreads();
     int i1 = -1, i2 = -1, i3 = -1;
-    if (a.check_ori) three_maxima(hist, i1, i2, i3);
+    if (a.check_ori) three_maxima_wave(hist, i1, i2, i3);
     int32_t* match = a.match + (long long)pr * a.f_n;
     int cnt = 0;
     for (int i = tid; i < a.f_n; i += nt) {
@@ -2625,7 +2625,7 @@ __device__ __forceinline__ void proj_claim(const ProjArgs& a, const Best2& st, i
 __device__ __forceinline__ void proj_rot_filter(const ProjArgs& a, const int* hist, const int* hent, int nh,
                                                 int* owner, int& nm) {
     int i1, i2, i3;
-    three_maxima(hist, i1, i2, i3);
+    three_maxima_wave(hist, i1, i2, i3);
     __syncthreads();
     int drop = 0;
     for (int e = lane_id(); e < nh; e += kWave) {
@@ -3884,10 +3884,10 @@ __global__ __launch_bounds__(256) void k_tri_final(TriArgs a, int n1, int32_t* m
         for (int t = tid; t < a.nitems; t += 256)
             if (a.item_match[t] >= 0) atomicAdd(&hist[a.item_bin[t]], 1);
     __syncthreads();
-    if (tid == 0) {
+    if (tid < kWave) {
         int i1 = -1, i2 = -1, i3 = -1;
-        if (a.check_ori) three_maxima(hist, i1, i2, i3);
-        keep[0] = i1; keep[1] = i2; keep[2] = i3;
+        if (a.check_ori) three_maxima_wave(hist, i1, i2, i3);
+        if (tid == 0) { keep[0] = i1; keep[1] = i2; keep[2] = i3; }
     }
     __syncthreads();
     for (int t = tid; t < a.nitems; t += 256) {
