@@ -2389,6 +2389,9 @@ __global__ __launch_bounds__(256) void k_bowk_resolve_lane(BowKArgs k, int big_p
 // (contiguous too) when it has one; the row is written once, coalesced.
 constexpr int kBowkRow = 8192;          // frame features of the LDS row (the all-LDS resolve's bound)
 constexpr int kBowkFinalStage = 256;    // KF nodes whose run bases are staged in LDS
+#ifndef ORB_BOWKF_U
+#define ORB_BOWKF_U 4
+#endif
 __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
     extern __shared__ int s_row[];                       // [f_n] KF feature | rotation bin << 26, or -1
     __shared__ int s_ko[kBowkFinalStage + 1];
@@ -2433,9 +2436,9 @@ __global__ __launch_bounds__(256) void k_bowk_final(BowKArgs k) {
     __syncthreads();
     if (staged) {
         // every thread over the pair's KF features in FeatureVector order (as
-        // k_bowk_fill), four claims in flight per thread
+        // k_bowk_fill), ORB_BOWKF_U claims in flight per thread
         const int p0 = s_ko[0], p1 = s_ko[nn];
-        constexpr int kU = 4;
+        constexpr int kU = ORB_BOWKF_U;
         for (int q = p0 + tid; q < p1; q += kU * nt) {
             // every load of the four rows that does not need a claim first, then
             // the frame angles of the claimed ones: two dependent rounds
