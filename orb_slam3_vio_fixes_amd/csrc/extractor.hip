@@ -2903,7 +2903,7 @@ constexpr int kRaw = 43, kRawP = 48, kBl = 37;
 constexpr int kHbT = ORB_DESC_HBT;
 static_assert(kHbT >= 44 && kHbT % 2 == 0, "a column holds 43 rows plus the 7-tap read's pad, in whole dwords");
 #ifndef ORB_DESC_SLOTS
-#define ORB_DESC_SLOTS 16
+#define ORB_DESC_SLOTS 8   // 16 -> 8: 257-259 vs 263-267 us (twice as many waves, 4 frames an XCD at a time; profiles/r05/README.md)
 #endif
 #ifndef ORB_DESC_ABL
 #define ORB_DESC_ABL 0   // timing ablation (tools only; wrong results): 1 = every patch load hits one L2-resident patch
