@@ -3138,7 +3138,9 @@ extern "C" int orbx_debug_desc_timing(unsigned long long* out, int reset) {
 #define ORB_DESC_HDOT4 1   // horizontal pass by v_dot4_u32_u8 (0: packed-u16 pairs, round 2)
 #endif
 #ifndef ORB_Q_UNROLL
-#define ORB_Q_UNROLL 1
+// rBRIEF test groups unrolled: all 8 samples of a lane in one block (122 VGPRs,
+// still 4 waves a SIMD): describe 261-264 -> 245 us (profiles/r05/README.md)
+#define ORB_Q_UNROLL 4
 #endif
 #ifndef ORB_DESC_HMFMA
 #define ORB_DESC_HMFMA 1   // horizontal pass on the matrix cores (v_mfma_i32_16x16x64_i8); 0: v_dot4 per row
