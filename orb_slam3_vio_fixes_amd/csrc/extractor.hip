@@ -1502,7 +1502,7 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #define ORB_QT_LEVEL_MAJOR 1
 #endif
 #ifndef ORB_FAST_ABL
-#define ORB_FAST_ABL 0   // timing ablations (tools only; wrong results): 1 scores, 2 compaction, 3 compass
+#define ORB_FAST_ABL 0   // timing ablations (tools only; wrong results): 1 scores, 2 compaction, 3 compass, 4 L2-resident ROIs
 #endif
 
 // A cell's ROI lands in LDS row-major at its own pitch of nd dwords (dense:
@@ -1682,6 +1682,10 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
 #endif
         rf.nd = max(1, ((c.x0 & 3) + c.cols + 3) >> 2);
         rf.rows = max(1, c.rows);
+#if ORB_FAST_ABL == 4
+        rf.src = a.in + (c.x0 & ~3);   // ablation: every ROI from frame 0's first rows, L2-resident (timing only)
+        rf.pitch = a.in_pitch;
+#endif
         return rf;
     };
     auto bm_of = [&](const CellDev& c) {
