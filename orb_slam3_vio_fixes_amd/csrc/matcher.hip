@@ -3186,6 +3186,9 @@ __global__ __launch_bounds__(64) void k_proj_resolve_spec(ProjArgs a, const uint
 // decisions, owner[s] = the last query accepted on s (a later claim of a slot
 // its earlier claimer left unblocked overwrites it, as the serial loop does),
 // and the rotation filter clears the slot of every claim in a rejected bin.
+#ifndef ORB_PROJ_TPRE
+#define ORB_PROJ_TPRE 1   // phase-2 decisions read their list's claim words up front
+#endif
 constexpr int kFusedThreads = 1024;
 constexpr int kFusedQpt = 8;                        // queries per thread in phase 2 (nq <= 8192)
 constexpr int kFusedMaxN = 4096;                    // 12-bit keypoint index in the order key
@@ -3473,12 +3476,24 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
             int dec = -1;
             if (C[u] > 0) {
                 int best = 256, lvl = -1, slot = -1, bin = 0, best2 = 256, lvl2 = -1, nav = 0;
+#if ORB_PROJ_TPRE
+                // the list's 8 claim words read up front, unconditionally (an
+                // index clamped into the table): 8 LDS reads in flight instead of
+                // one behind each data-dependent branch
+                int tv[kProjK];
+#pragma unroll
+                for (int k = 0; k < kProjK; ++k) tv[k] = T[min((int)(L[k] & 0xfff), max(n - 1, 0))];
+#endif
 #pragma unroll
                 for (int k = 0; k < kProjK; ++k) {
                     const uint32_t e = L[k];
                     if (k >= C[u] || e == kFusedNone) continue;
                     const int s = (int)(e & 0xfff);
+#if ORB_PROJ_TPRE
+                    if (tv[k] < j) continue;
+#else
                     if (T[s] < j) continue;
+#endif
                     if (nav == 0) {
                         best = (int)(e >> 24); lvl = (int)((e >> 16) & 7); bin = (int)((e >> 19) & 31); slot = s;
                     } else if (nav == 1) {
