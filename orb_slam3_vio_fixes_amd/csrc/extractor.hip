@@ -210,6 +210,9 @@ constexpr int kPsRun = 4;                 // k_pyr_stream: output rows per run (
 #ifndef ORB_PYR_K0
 #define ORB_PYR_K0 0
 #endif
+#ifndef ORB_ASM_THREADS
+#define ORB_ASM_THREADS 256   // k_assemble: threads per frame's workgroup
+#endif
 
 // k_pyr_stream layout for level-0 chunks of K0 rows: runs the step schedule
 // (level l computes at step s every row whose two source rows of level l-1
@@ -642,7 +645,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     // k_assemble holds a flag per output slot of a frame in LDS (dynamic) next
     // to its static lvl_start[kMaxLevels + 1] and tmp[16]: up to ~40,000
     // features a frame (Tracking's largest extractor is 5 x nFeatures)
-    if ((size_t)outsum * 4 + 64 + (size_t)(kMaxLevels + 1 + 16) * 4 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
+    if ((size_t)outsum * 4 + 64 + (size_t)(kMaxLevels + 1 + ORB_ASM_THREADS / 64 + 1) * 4 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
     P.in_pitch = (size_t)round_up(w, 64);
 
     const size_t B = (size_t)maxB;
@@ -3629,9 +3632,9 @@ struct AsmArgs {
     int32_t* mono_out;
 };
 
-__global__ __launch_bounds__(256) void k_assemble(AsmArgs a) {
+__global__ __launch_bounds__(ORB_ASM_THREADS) void k_assemble(AsmArgs a) {
     __shared__ int lvl_start[kMaxLevels + 1];
-    __shared__ int tmp[16];
+    __shared__ int tmp[ORB_ASM_THREADS / kWave + 1];   // block_excl_scan: a word a wave + the total
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     int* inlap = (int*)smem;                    // per keypoint, scanned
     const int f = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
@@ -3940,7 +3943,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     aa.lv = P.d_lv; aa.qt_key = P.d_qt_key; aa.qt_n = P.d_qt_n; aa.angle = P.d_angle; aa.sdesc = P.d_sdesc;
     aa.out_total = P.out_total; aa.L = L; aa.lap0 = lap0; aa.lap1 = lap1;
     aa.kps = d_kps; aa.desc = d_desc; aa.cap = cap; aa.n_out = d_n; aa.mono_out = d_mono;
-    ORB_LAUNCH(k_assemble, dim3(B), dim3(256), (size_t)P.out_total * 4 + 64, st, aa);
+    ORB_LAUNCH(k_assemble, dim3(B), dim3(ORB_ASM_THREADS), (size_t)P.out_total * 4 + 64, st, aa);
     mark();
     if (hd->profiling) hd->ev_calls.push_back(marks);
     ORB_CHECK(hipGetLastError());
