@@ -3038,14 +3038,17 @@ __device__ __forceinline__ void patch_land(const uint32_t (&v)[kPV], uint8_t* ra
 // The row form: lane r < 43 holds row r's 12 dwords (3 x 16 B from a 4-byte
 // aligned address), lands them as 3 x ds_write_b128 at raw + 48 r.
 constexpr int kPR = 12;
-__device__ __forceinline__ void patch_issue_rows(const uint8_t* img, int pitch, int x0, int y0, uint32_t (&v)[kPR]) {
+// xs: the 4-byte aligned first column; rows outside [0, h) reflected (REFLECT_101)
+__device__ __forceinline__ void patch_issue_rows(const uint8_t* img, int pitch, int h, int xs, int y0,
+                                                 uint32_t (&v)[kPR]) {
     const int lane = lane_id();
     if (lane < kRaw) {
         // 12 consecutive dwords (the load vectorizer makes them dwordx4 loads)
 #if ORB_DESC_ABL == 1
         const GlobalWords p = (GlobalWords)(img + (long long)lane * pitch);   // ablation: one L2-resident patch (timing only)
+        (void)h; (void)xs; (void)y0;
 #else
-        const GlobalWords p = (GlobalWords)(img + (long long)(y0 + lane) * pitch + (x0 & ~3));
+        const GlobalWords p = (GlobalWords)(img + (long long)refl101(y0 + lane, h) * pitch + xs);
 #endif
 #pragma unroll
         for (int k = 0; k < kPR; ++k) v[k] = p[k];
@@ -3059,6 +3062,43 @@ __device__ __forceinline__ void patch_land_rows(const uint32_t (&v)[kPR], uint8_
         q[1] = make_uint4(v[4], v[5], v[6], v[7]);
         q[2] = make_uint4(v[8], v[9], v[10], v[11]);
     }
+}
+// Left-border landing: the row was loaded from column 0 and the patch starts at
+// x0 in [-3, -1]; the row goes in one dword later, and the first dword holds
+// the reflected columns -1, -2, -3 = pixels 1, 2, 3 at bytes 3, 2, 1, so the
+// patch reads from byte 4 + x0 like an interior one from x0 & 3
+__device__ __forceinline__ void patch_land_rows_left(const uint32_t (&v)[kPR], uint8_t* raw) {
+    const int lane = lane_id();
+    if (lane < kRaw) {
+        uint4* q = (uint4*)(raw + lane * kRawP);
+        q[0] = make_uint4(__builtin_amdgcn_perm(v[0], v[0], 0x01020300u), v[0], v[1], v[2]);
+        q[1] = make_uint4(v[3], v[4], v[5], v[6]);
+        q[2] = make_uint4(v[7], v[8], v[9], v[10]);
+    }
+}
+#ifndef ORB_DESC_BORDER_ROWS
+#define ORB_DESC_BORDER_ROWS 1   // border patches by prefetched row loads where the columns allow (0: all by reflected byte loads)
+#endif
+// How the patch whose top-left level pixel is (x0, y0) is fetched: 1 row
+// loads from x0 & ~3, 2 row loads from column 0 (left border, x0 in [-3, -1]),
+// 3 row loads from x0 & ~3 with the one or two columns past the right border
+// (w, w + 1 = pixels w - 2, w - 3) rewritten in LDS after landing, 0
+// reflected byte loads (patch_border).  Rows outside the level are reflected
+// per lane in modes 1-3; a row load may read past the level width but stays
+// inside the row pitch, and no loaded byte of a column >= w is used.
+__device__ __forceinline__ int patch_mode(int w, int h, int pitch, int x0, int y0) {
+#if ORB_DESC_BORDER_ROWS && ORB_DESC_ROWLOAD
+    if (y0 < 1 - h || y0 + kRaw > 2 * h - 1) return 0;
+    if (x0 >= 0) {
+        if ((x0 & ~3) + kRawP > pitch) return 0;
+        if (x0 + kRaw <= w) return 1;
+        return x0 + kRaw <= w + 2 ? 3 : 0;
+    }
+    return x0 >= -3 && x0 + kRaw <= w && kRawP <= pitch ? 2 : 0;
+#else
+    (void)pitch;
+    return patch_interior(w, h, x0, y0) ? 1 : 0;
+#endif
 }
 #if ORB_DESC_ROWLOAD
 constexpr int kPVN = kPR;
@@ -3306,7 +3346,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         todo &= todo - 1;
         k = desc_pick(mine, j);
         const int x0 = (int)(k.key & 0xfff) + (kEdge - 3) - 21, y0 = (int)((k.key >> 12) & 0xfff) + (kEdge - 3) - 21;
+#if ORB_DESC_ROWLOAD
+        const int md = patch_mode(k.w, k.h, k.pitch, x0, y0);
+        if (md) patch_issue_rows(k.img, k.pitch, k.h, md == 2 ? 0 : (x0 & ~3), y0, v);
+#else
         if (patch_interior(k.w, k.h, x0, y0)) DESC_PATCH_ISSUE(k.img, k.pitch, x0, y0, v);
+#endif
     };
     take(jc, cur, pv);
 #if ORB_DESC_PF2
@@ -3318,12 +3363,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ORB_DESC_WA
         const int cx = (int)(key & 0xfff) + (kEdge - 3), cy = (int)((key >> 12) & 0xfff) + (kEdge - 3);
         // 1. raw 43x43 patch centred on (cx, cy), REFLECT_101 at the level border
         int sh = 0;
+#if ORB_DESC_ROWLOAD
+        const int md = patch_mode(cur.w, cur.h, cur.pitch, cx - 21, cy - 21);
+        if (md == 1) {
+            DESC_PATCH_LAND(pvl, raw);
+            sh = (cx - 21) & 3;
+        } else if (md == 2) {
+            patch_land_rows_left(pvl, raw);
+            sh = 4 + (cx - 21);
+        } else if (md == 3) {
+            DESC_PATCH_LAND(pvl, raw);
+            sh = (cx - 21) & 3;
+            // columns w (and w + 1) of the row: bytes P, P + 1 of the loaded
+            // row (P = w - (x0 & ~3) <= 46) take pixels w - 2, w - 3
+            if (lane < kRaw) {
+                uint8_t* rr = raw + lane * kRawP;
+                const int P = cur.w - ((cx - 21) & ~3);
+                const uint8_t a2 = rr[P - 2], a3 = rr[P - 3];
+                rr[P] = a2;
+                if (P + 1 < kRawP) rr[P + 1] = a3;
+            }
+        } else {
+            patch_border(cur.img, cur.pitch, cur.w, cur.h, cx - 21, cy - 21, raw);
+        }
+#else
         if (patch_interior(cur.w, cur.h, cx - 21, cy - 21)) {
             DESC_PATCH_LAND(pvl, raw);
             sh = (cx - 21) & 3;
         } else {
             patch_border(cur.img, cur.pitch, cur.w, cur.h, cx - 21, cy - 21, raw);
         }
+#endif
         // refill the landed set: the keypoint after the next one (PF2), or
         // the next one (one patch in flight during this keypoint)
         int jnn = -1;
