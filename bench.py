@@ -88,6 +88,10 @@ def parse():
                     help="distinct input batches the steps rotate through (4 x 256 frames exceed the 256 MB "
                          "Infinity Cache, so every step reads cold frames)")
     ap.add_argument("--cpu-sample", type=int, default=256, help="frames in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--parity-sample", type=int, default=4,
+                    help="frames of every rank's last timed step checked against the oracle on its host when the "
+                         "CPU baseline does not run (N > 1, or --cpu-sample 0); the mismatch counts are summed over "
+                         "ranks onto rank 0's line")
     ap.add_argument("--cpu-threads", type=int, default=0,
                     help="threads of the CPU-baseline pool (0 = the cores this process may run on, at most 16)")
     ap.add_argument("--no-host-api", dest="host_api", action="store_false",
@@ -251,6 +255,28 @@ def cpu_baseline(frames_np, threads, lib_path):
         nms = dict(x for r in pool.map(match, range(threads)) for x in r)
     dt = time.perf_counter() - t0
     return n / dt, outs, nms
+
+
+def parity_counts(snap, ns, outs, nms):
+    """Mismatches of the first `ns` frames / `ns - 1` pairs of a device output
+    snapshot (kps, desc, n, mono, nmatch, matches12) against the oracle's
+    outputs `outs` / `nms` (cpu_baseline): every keypoint byte, descriptor,
+    monoIndex, nmatches and the whole matches12 row."""
+    from orb_slam3_vio_fixes_amd import orb
+    kh, dh, nh, monoh, mh, m12h = (x.cpu().numpy() for x in snap)
+    bad = 0
+    for i in range(ns):
+        rk, rd, rmono = outs[i]
+        if nh[i] != len(rk) or monoh[i] != rmono or \
+                not np.array_equal(orb.keypoints_from_device(kh[i][:nh[i]]).view(np.uint8), rk.view(np.uint8)) or \
+                not np.array_equal(dh[i][:nh[i]], rd):
+            bad += 1
+    bad_m = 0
+    for i in range(ns - 1):
+        rnm, rm12 = nms[i]
+        if mh[i] != rnm or not np.array_equal(m12h[i][:len(rm12)], rm12):
+            bad_m += 1
+    return bad, bad_m
 
 
 def cpu_single_thread(frames_np, lib_path, seconds=4.0):
@@ -589,6 +615,15 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    # the last TIMED step's outputs (its output set, its ring batch and its
+    # matching, which the final flush ran last), copied before the profiled
+    # pass reuses the sets: the parity legs below check these
+    snap_set, snap_slot = (counter[0] - 1) % nsets, (counter[0] - 1) % R
+    own_cpu = world == 1 and args.cpu_sample > 0
+    ns_snap = max(1, min(Bx, min(args.cpu_sample, B) if own_cpu else args.parity_sample))
+    snap = tuple(x[:ns_snap].clone() for x in outs_dev[snap_set]) + \
+        (nmatch[:ns_snap - 1].clone(), matches[:ns_snap - 1].clone())
+    torch.cuda.synchronize()
     # profiled pass (after the timed region, not in `value`): --profile-steps
     # more steps of the same pipeline at ONE step in flight (handle 0 only;
     # step k's matching still beside step k+1's later stages), with HIP events
@@ -616,6 +651,24 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
+    # every rank's own sample of its last timed step vs the oracle on its host
+    # (N > 1, or no CPU baseline), the counts summed over ranks
+    par = None
+    if not own_cpu and args.parity_sample > 0:
+        from oracle import oracle as O
+        lib_path, _ = O.fast_variant()
+        _, ro, rn = cpu_baseline(ring_np[snap_slot][:ns_snap], min(4, len(os.sched_getaffinity(0))), lib_path)
+        bad, bad_m = parity_counts(snap, ns_snap, ro, rn)
+        pt = torch.tensor([ns_snap, bad, ns_snap - 1, bad_m], dtype=torch.int64,
+                          device=dev if backend == "nccl" else "cpu")
+        if world > 1:
+            dist.all_reduce(pt, op=dist.ReduceOp.SUM)
+        fc, fm, pc, pm = (int(x) for x in pt.tolist())
+        par = {"frames_checked": fc, "frames_mismatched": fm, "pairs_checked": pc, "pairs_mismatched": pm,
+               "ranks": world, "source": f"first {ns_snap} frames / {ns_snap - 1} pairs of every rank's last timed "
+                                         "step, oracle on the rank's host, counts summed over ranks",
+               "compared": "keypoint count, all 28 keypoint bytes, 32 descriptor bytes, monoIndex, nmatches and the "
+                           "full matches12"}
 
     last_slot = (counter[0] - 1) % R                    # the ring batch of the last step
     if args.dump:
@@ -664,38 +717,23 @@ def main():
                             "search_for_initialization": (float(np.mean([a.elapsed_time(b) for a, b in match_events]))
                                                           if match_events else None)},
                "roofline": roof,
-               "stage_roofline": sr}
-        if world == 1 and args.cpu_sample > 0:
+               "stage_roofline": sr,
+               "world_size": dist.get_world_size() if world > 1 else 1,
+               "backend": dist.get_backend() if world > 1 else None}
+        if par is not None:
+            out["parity"] = par
+        if own_cpu:
             from oracle import oracle as O
-            ns = min(args.cpu_sample, B)
+            ns = ns_snap
             avail = len(os.sched_getaffinity(0))
             threads = args.cpu_threads or min(16, avail)
             lib_path, flags = O.fast_variant()
-            frames_np = ring_np[last_slot]             # the frames of the output set compared below
+            frames_np = ring_np[snap_slot]             # the frames of the last timed step
             fps, outs, nms = cpu_baseline(frames_np[:ns], threads, lib_path)
             fps1, n1 = cpu_single_thread(frames_np[:ns], lib_path)
-            # parity of the sampled frames (the CPU leg doubles as a checker):
-            # every keypoint byte, descriptor, and the whole matches12 array
-            # of every sampled pair (the output set of the last step)
-            last = outs_dev[(counter[0] - 1) % nsets]
-            kh = last[0][:ns].cpu().numpy()
-            dh = last[1][:ns].cpu().numpy()
-            nh = last[2][:ns].cpu().numpy()
-            monoh = last[3][:ns].cpu().numpy()
-            mh = nmatch[:ns - 1].cpu().numpy()
-            m12h = matches[:ns - 1].cpu().numpy()
-            bad = 0
-            for i in range(ns):
-                rk, rd, rmono = outs[i]
-                if nh[i] != len(rk) or monoh[i] != rmono or \
-                        not np.array_equal(orb.keypoints_from_device(kh[i][:nh[i]]).view(np.uint8),
-                                                          rk.view(np.uint8)) or not np.array_equal(dh[i][:nh[i]], rd):
-                    bad += 1
-            bad_m = 0
-            for i in range(ns - 1):
-                rnm, rm12 = nms[i]
-                if mh[i] != rnm or not np.array_equal(m12h[i][:len(rm12)], rm12):
-                    bad_m += 1
+            # parity of the sampled frames (the CPU leg doubles as a checker)
+            # against the snapshot of the last timed step (two in flight)
+            bad, bad_m = parity_counts(snap, ns, outs, nms)
             nproc = os.cpu_count() or avail
             out["cpu_baseline"] = {"value": fps, "unit": "frames/s", "cores": threads, "kind": "port",
                                    "cores_available": avail, "host_cpus_nproc": nproc,
@@ -712,8 +750,11 @@ def main():
                                              f"threads (value); single_thread_fps: the reference's model, one "
                                              f"Tracking thread extracting and matching frame after frame"}
             out["parity"] = {"frames_checked": ns, "frames_mismatched": bad, "pairs_checked": ns - 1,
-                             "pairs_mismatched": bad_m, "compared": "keypoint count, all 28 keypoint bytes, 32 descriptor "
-                                                                   "bytes, monoIndex, nmatches and the full matches12"}
+                             "pairs_mismatched": bad_m, "ranks": 1,
+                             "source": f"first {ns} frames / {ns - 1} pairs of the last timed step ({args.overlap} "
+                                       "in flight), the CPU-baseline outputs",
+                             "compared": "keypoint count, all 28 keypoint bytes, 32 descriptor "
+                                         "bytes, monoIndex, nmatches and the full matches12"}
         if world == 1 and args.host_api:
             # side measurements (not the metric): a failure here is reported in
             # the line instead of losing it

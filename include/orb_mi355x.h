@@ -247,6 +247,10 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        back by one device-to-host copy
  *   ORB_OPT_UPLOAD       host calls' inputs: 0 one kernel reading the pinned
  *                        staging buffer (k_pull), 1 hipMemcpyAsync
+ *   ORB_OPT_FAST_CAND_CAP  FAST's per-cell candidate list: 0 the capacity the
+ *                        LDS budget leaves (a cell with more candidates is
+ *                        scored densely), n > 0 at most n - 1 entries (1:
+ *                        every cell through the dense form)
  * The two k_pyr_stream options are read when a handle builds its plan (the
  * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
@@ -260,7 +264,8 @@ enum {
     ORB_OPT_SFI_FORM = 5,
     ORB_OPT_HOST_OUT = 6,
     ORB_OPT_UPLOAD = 7,
-    ORB_OPT_COUNT = 8
+    ORB_OPT_FAST_CAND_CAP = 8,
+    ORB_OPT_COUNT = 9
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);
@@ -494,6 +499,63 @@ int orbm_search_by_projection_last(const orbm_frame* cur, int nlast,
                                    const uint8_t* last_desc, float th, int mode,
                                    int check_ori,
                                    int32_t* owner, const uint8_t* blocked);
+
+/* ---------------- frames resident in HBM (the Tracking thread's searches) ----------------
+ *
+ * The reference runs its per-frame searches on the Frame it just extracted
+ * (Tracking::TrackReferenceKeyFrame: Frame::ComputeBoW, then SearchByBoW(KF, F),
+ * Tracking.cc:2720-2730; TrackWithMotionModel: SearchByProjection(F, LastFrame),
+ * :2886; TrackLocalMap: SearchByProjection(F, local points), :3413), against
+ * keyframes whose keypoints, descriptors and FeatureVector never change once
+ * built (KeyFrame.cc:98-107).  An orbm_dframe holds such a frame or keyframe in
+ * HBM, so a search call moves only its per-call inputs (MapPoint validity,
+ * projected points) and its result across PCIe: the inputs are read by the
+ * search kernel itself from pinned memory, the result comes back the same way,
+ * one launch per call.  The upload forms above stay for callers that hold
+ * host arrays only.  A dframe is immutable between updates; updating or
+ * destroying it while a search on it runs (on another thread) is the caller's
+ * race, as is destroying a keyframe the reference is still reading. */
+typedef struct orbm_dframe orbm_dframe;
+
+/* An empty dframe on HIP device `device`.  NULL on error. */
+orbm_dframe* orbm_dframe_create(int device);
+void orbm_dframe_destroy(orbm_dframe* df);
+
+/* The frame f (host arrays: keypoints, descriptors, u_right / scale factors
+ * when set, bounds and grid factors) and its FeatureVector fv (NULL: none;
+ * the BoW search needs one) copied into HBM.  Synchronous.  Returns ORB_OK,
+ * ORB_ERR_PARAM or ORB_ERR_DEVICE. */
+int orbm_dframe_upload(orbm_dframe* df, const orbm_frame* f, const orbm_featvec* fv);
+
+/* The last image orbx_extract extracted on h (Frame::ExtractORB,
+ * Frame.cc:418-425) as the dframe's keypoints and descriptors, copied device
+ * to device (no PCIe); geom supplies the bounds, grid factors, u_right and
+ * scale factors (its kps / desc / n are ignored); fv as in orbm_dframe_upload
+ * (Frame::ComputeBoW runs after the extraction: orbm_dframe_set_featvec can
+ * add it later).  Asynchronous on the null stream, ordered before every later
+ * search.  ORB_ERR_PARAM when h holds no single-image extraction. */
+int orbm_dframe_from_extractor(orbm_dframe* df, orbx_handle* h, const orbm_frame* geom, const orbm_featvec* fv);
+
+/* Replaces the dframe's FeatureVector (Frame::ComputeBoW / KeyFrame::ComputeBoW). */
+int orbm_dframe_set_featvec(orbm_dframe* df, const orbm_featvec* fv);
+
+/* Keypoint count of the dframe (>= 0), or ORB_ERR_PARAM. */
+int orbm_dframe_count(const orbm_dframe* df);
+
+/* The searches of orbm_search_by_bow, orbm_search_by_projection_last,
+ * orbm_search_by_projection_mps and orbm_search_for_initialization on
+ * dframes: same arguments otherwise, identical results. */
+int orbm_search_by_bow_dframe(const orbm_dframe* kf, const uint8_t* kf_mp_valid, const orbm_dframe* f,
+                              float nnratio, int check_ori, int32_t* match_f);
+int orbm_search_by_projection_last_dframe(const orbm_dframe* cur, int nlast, const uint8_t* valid, const float* u,
+                                          const float* v, const float* ur, const int32_t* last_octave,
+                                          const float* last_angle, const uint8_t* has_obs,
+                                          const uint8_t* last_desc, float th, int mode, int check_ori,
+                                          int32_t* owner, const uint8_t* blocked);
+int orbm_search_by_projection_mps_dframe(const orbm_dframe* f, const orbm_mappoints* mps, float th, int far_points,
+                                         float th_far, float nnratio, int32_t* owner, const uint8_t* blocked);
+int orbm_search_for_initialization_dframe(const orbm_dframe* f1, const orbm_dframe* f2, float* prev_xy, int window,
+                                          float nnratio, int check_ori, int32_t* matches12);
 
 /* ---------------- fisheye stereo frames (Frame::Nleft != -1) ----------------
  * The frame is the combined keypoint array [mvKeys (nleft); mvKeysRight] with

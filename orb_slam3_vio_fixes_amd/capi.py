@@ -29,11 +29,15 @@ EXPORTS = [
     "orbm_search_by_projection_last_fisheye", "orbx_set_pyramid_mode", "orbx_pyramid_kernel", "orbv_transform_device",
     "orbx_set_stage_event", "orb_debug_set_option", "orb_debug_get_option",
     "orbm_release_scratch", "orbm_debug_proj_stats", "orbx_debug_pretest", "orbx_debug_plan_info",
+    "orbm_dframe_create", "orbm_dframe_destroy", "orbm_dframe_upload", "orbm_dframe_from_extractor",
+    "orbm_dframe_set_featvec", "orbm_dframe_count", "orbm_search_by_bow_dframe",
+    "orbm_search_by_projection_last_dframe", "orbm_search_by_projection_mps_dframe",
+    "orbm_search_for_initialization_dframe",
 ]
 
 # orb_debug_set_option keys (include/orb_mi355x.h): alternative kernel forms
 (ORB_OPT_PROJ_FORM, ORB_OPT_BOW_FORM, ORB_OPT_BOWK_BIG, ORB_OPT_PYR_CNT_END, ORB_OPT_PYR_PRETEST, ORB_OPT_SFI_FORM,
- ORB_OPT_HOST_OUT, ORB_OPT_UPLOAD) = 0, 1, 2, 3, 4, 5, 6, 7
+ ORB_OPT_HOST_OUT, ORB_OPT_UPLOAD, ORB_OPT_FAST_CAND_CAP) = 0, 1, 2, 3, 4, 5, 6, 7, 8
 
 _lib = None
 
@@ -94,6 +98,18 @@ def load(path: Path | str = LIB_PATH):
     L.orbm_search_by_projection_mps_fisheye.argtypes = [vp, i32, vp, vp, vp, vp, f32, i32, f32, f32, vp, vp]
     L.orbm_search_by_projection_last_fisheye.argtypes = [vp, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32,
                                                          i32, vp, vp]
+    L.orbm_dframe_create.restype = vp
+    L.orbm_dframe_create.argtypes = [i32]
+    L.orbm_dframe_destroy.argtypes = [vp]
+    L.orbm_dframe_upload.argtypes = [vp, vp, vp]
+    L.orbm_dframe_from_extractor.argtypes = [vp, vp, vp, vp]
+    L.orbm_dframe_set_featvec.argtypes = [vp, vp]
+    L.orbm_dframe_count.argtypes = [vp]
+    L.orbm_search_by_bow_dframe.argtypes = [vp, vp, vp, f32, i32, vp]
+    L.orbm_search_by_projection_last_dframe.argtypes = [vp, i32, vp, vp, vp, vp, vp, vp, vp, vp, f32, i32, i32, vp,
+                                                        vp]
+    L.orbm_search_by_projection_mps_dframe.argtypes = [vp, vp, f32, i32, f32, f32, vp, vp]
+    L.orbm_search_for_initialization_dframe.argtypes = [vp, vp, vp, i32, f32, i32, vp]
     L.orbk_db_create.restype = vp
     L.orbk_db_create.argtypes = [i32]
     L.orbk_db_destroy.argtypes = [vp]

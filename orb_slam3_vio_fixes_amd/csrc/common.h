@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/orb_mi355x.h"
+
 #include <unordered_map>
 
 #define ORB_CHECK(call)                                  \
@@ -28,7 +30,8 @@ constexpr size_t kCuLds = 160 * 1024;       // LDS of one CU: a workgroup's ceil
 // Launch-time LDS guard: a kernel's static LDS (hipFuncGetAttributes, once per
 // kernel and thread) plus the launch's dynamic LDS must fit one CU, or the
 // launch is refused before it reaches the device (an over-subscribed launch
-// faults the GPU instead of failing cleanly).
+// faults the GPU instead of failing cleanly).  A failed attribute query is not
+// cached: the launch is refused and the next one asks again.
 inline bool lds_fits(const void* kernel, size_t dyn) {
     static thread_local std::unordered_map<const void*, size_t>* cache = new std::unordered_map<const void*, size_t>();
     size_t st = 0;
@@ -37,11 +40,19 @@ inline bool lds_fits(const void* kernel, size_t dyn) {
         st = it->second;
     } else {
         hipFuncAttributes at{};
-        if (hipFuncGetAttributes(&at, kernel) == hipSuccess) st = at.sharedSizeBytes;
+        if (hipFuncGetAttributes(&at, kernel) != hipSuccess) {
+            (void)hipGetLastError();
+            return false;
+        }
+        st = at.sharedSizeBytes;
         cache->emplace(kernel, st);
     }
     return dyn + st <= kCuLds;
 }
+
+// The last orbx_extract's keypoints / descriptors in HBM (extractor.hip), for
+// the matcher's device-resident frames (orbm_dframe_from_extractor).
+int extractor_last_outputs(orbx_handle* h, const orb_keypoint** kps, const uint8_t** desc, int* n, int* device);
 
 // orb_debug_set_option's process-wide table (matcher.hip): alternative kernel
 // forms for parity tests; every product default is 0

@@ -1275,8 +1275,9 @@ struct FastArgs {
     int ini_th, min_th;
     int roi_max, win_max;   // LDS per wave
     int kmask_bytes;        // NMS ballots of the separate output pass (0 with ORB_FAST_FUSED_OUT)
-    int cand_bytes;         // u16 candidate list, one entry per window pixel at most
-    int ilist_bytes;        // u32 list of the pre-test items holding a candidate (ORB_FAST_EMIT 1;
+    int cand_bytes;         // u16 candidate list of cand_cap entries
+    int cand_cap;           // a cell whose candidates exceed it takes the dense path (fast_dense_cell)
+    int ilist_bytes;      // u32 list of the pre-test items holding a candidate (ORB_FAST_EMIT 1;
                             // 0 with ORB_FAST_ILIST_IN_MAP: the list lives in the score map's bytes)
     const uint8_t* bm;      // k_pyr_stream's iniThFAST pre-test bitmaps of frame 0 (k_fast_cells<..., true>)
     long long bm_fstride;
@@ -1507,6 +1508,16 @@ constexpr int kFastWpb = ORB_FAST_WPB;
 #ifndef ORB_FAST_ABL
 #define ORB_FAST_ABL 0   // timing ablations (tools only; wrong results): 1 scores, 2 compaction, 3 compass, 4 L2-resident ROIs
 #endif
+// The candidate list is sized for the typical cell, not the worst one: a cell
+// whose pre-test leaves more candidates than FastArgs::cand_cap is scored
+// densely instead (every window pixel, both directions, straight into the
+// score map; the NMS then walks the window in row-major order), which needs no
+// list at all.  The cap comes from an LDS budget of ORB_FAST_WAVES_CU waves a
+// CU (the 8.7 KB worst-case list capped k_fast_cells at 17-18 waves a CU).
+#ifndef ORB_FAST_WAVES_CU
+#define ORB_FAST_WAVES_CU 24
+#endif
+constexpr bool kFastDense = ORB_FAST_FUSED_OUT && ORB_FAST_EMIT == 1 && !ORB_FAST_RESET && ORB_FAST_ILIST_IN_MAP;
 
 // A cell's ROI lands in LDS row-major at its own pitch of nd dwords (dense:
 // the banks of the pre-test's row reads spread as before).  It is fetched as
@@ -1598,6 +1609,9 @@ __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)
     }
 }
 
+#if !defined(ORB_FAST_WPE) && ORB_FAST_WAVES_CU % 4 == 0
+#define ORB_FAST_WPE (ORB_FAST_WAVES_CU / 4)   // registers for the LDS budget's occupancy (79 VGPRs, no spills)
+#endif
 #ifdef ORB_FAST_WPE
 #define FAST_WPE_ATTR __attribute__((amdgpu_waves_per_eu(ORB_FAST_WPE)))
 #else
@@ -1757,6 +1771,57 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             m_first = item_byte_mask(min(max(-cxf, 0), 8), min(max(ww - cxf, 0), 8));
             m_last = item_byte_mask(min(max(-cxl, 0), 8), min(max(ww - cxl, 0), 8));
         }
+        // The dense form of a cell from pass p0 on: the exact score s(p) of
+        // every window pixel (max of both directions, 0 below 1) in the map,
+        // then the NMS of each remaining pass over the window in row-major
+        // order -- the reference's definition itself, for the cells whose
+        // candidates overflow the list.  Returns the survivors of the deciding
+        // pass (written like the list form's).
+        auto dense_cell = [&](int p0) -> int {
+            fast_wave_sync();   // the item list (in the map's bytes) is read out
+            for (int i = lane; i < (npad + 15) / 16; i += kWave) ((uint4*)sc)[i] = make_uint4(0u, 0u, 0u, 0u);
+            fast_wave_sync();
+            const int npix = ww * wh;
+            for (int q0 = 0; q0 < npix; q0 += kWave) {
+                const int q = q0 + lane;
+                if (q < npix) {
+                    const int r = div_row(q, inv_ww), cc = q - (int)__umul24((uint32_t)r, (uint32_t)ww);
+                    int v, x[16];
+                    fast_ring<RP>(R, rstride, r + 3, cc + 3, v, x);
+                    const int sv = max(max(fast_dir_score(x, v, 0), fast_dir_score(x, v, 1)), 0);
+                    sc[mad24((uint32_t)(r + 1), (uint32_t)sp, (uint32_t)(cc + 1))] = (uint8_t)sv;
+                }
+            }
+            fast_wave_sync();
+            uint32_t* outp = a.cell_keys + (long long)f * a.slot_total + cur.slot_off;
+            int n = 0;
+            for (int pass = p0; pass < 2; ++pass) {
+                const int t = pass == 0 ? a.ini_th : a.min_th;
+                n = 0;
+                for (int q0 = 0; q0 < npix; q0 += kWave) {
+                    const int q = q0 + lane;
+                    bool keep = false;
+                    uint32_t key = 0;
+                    if (q < npix) {
+                        const int r = div_row(q, inv_ww), cc = q - (int)__umul24((uint32_t)r, (uint32_t)ww);
+                        int sv;
+                        keep = nms_keep(sc, sp, r, cc, t, sv);
+                        key = (uint32_t)(cur.x0 + cc + 3 - (kEdge - 3)) | ((uint32_t)(cur.y0 + r + 3 - (kEdge - 3)) << 12) |
+                              ((uint32_t)sv << 24);
+                    }
+                    const uint64_t m = __ballot(keep);
+                    if (keep) {
+                        const int pos = n + mask_rank(m);
+                        if (pos < cur.cap) outp[pos] = key;
+                    }
+                    n += __popcll(m);
+                }
+                if (n > 0) break;
+            }
+            fast_wave_sync();
+            return n;
+        };
+        int dense_from = -1;    // pass at which the candidates overflowed the list
         // FAST(ROI, iniThFAST) and, only if that leaves no corner, FAST(ROI,
         // minThFAST) (ORBextractor.cc:826-846).  Each pass pre-tests at its own
         // threshold, so the iniTh pass scores far fewer pixels; scores stored by
@@ -1920,6 +1985,10 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 if (r >= wh) m64 = 0;
                 const int pc = __popcll(m64);
                 const int incl = wave_incl_scan_dpp(pc);
+                if (kFastDense && __builtin_amdgcn_readlane(incl, kWave - 1) > a.cand_cap) {
+                    dense_from = pass;
+                    break;
+                }
                 int pos = incl - pc;
                 const int base = cand_enc(r, 0, ww) | kCandBright | kCandDark;
                 while (m64) {
@@ -1985,6 +2054,19 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
                 nlist += __popcll(bal);
             }
             fast_wave_sync();
+            if (kFastDense && 8 * nlist > a.cand_cap) {
+                // at most 8 pixels an item: count them exactly only when that
+                // bound does not already fit the list
+                int np = 0;
+                for (int b0 = 0; b0 < nlist; b0 += kWave) {
+                    const uint32_t e = b0 + lane < nlist ? ilist[b0 + lane] : 0u;
+                    np += __popc(((e >> 16) & 0xffu) | (e >> 24));
+                }
+                if (wave_sum_dpp(np) > a.cand_cap) {
+                    dense_from = pass;
+                    break;
+                }
+            }
             // 1b. the listed items' pixels -> the candidate list, row-major
             //     (items in order, pixels in order within an item)
             for (int b0 = 0; b0 < nlist; b0 += kWave) {
@@ -2176,6 +2258,7 @@ __global__ __launch_bounds__(256) FAST_WPE_ATTR void k_fast_cells(FastArgs a) {
             if (pass == 0) FAST_T(3); else FAST_T(7);
             if (cnt > 0) break;
         }
+        if (kFastDense && dense_from >= 0) cnt = dense_cell(dense_from);
 #if ORB_FAST_FUSED_OUT
         const int written = cnt;
 #else
@@ -2645,8 +2728,11 @@ extern "C" int orbx_debug_qt_timing(unsigned long long* out, int reset) {
 // level: Tracking's 5 x nFeatures initialization extractor) keeps them in a
 // global scratch slice instead; the instantiation is only launched when a
 // plan has such a level, so the LDS form keeps its ds_* instructions.
+#ifndef ORB_QT_THREADS
+#define ORB_QT_THREADS 256   // threads of a k_quadtree block (one (frame, level) tree)
+#endif
 template <bool GS>
-__global__ __launch_bounds__(256) void k_quadtree(QtArgs a) {
+__global__ __launch_bounds__(ORB_QT_THREADS) void k_quadtree(QtArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
 #if ORB_QT_LEVEL_MAJOR
     // grid (frames, levels): every frame's level 0 (the largest trees) dispatches first
@@ -3832,7 +3918,18 @@ static void fast_lds_layout(const FastGroup& G, int rp, FastArgs& fa) {
     fa.win_max = (std::max(G.win_max, ORB_FAST_ILIST_IN_MAP ? il : 0) + 15) & ~15;
     // NMS ballots only for the separate output pass
     fa.kmask_bytes = ORB_FAST_FUSED_OUT ? 0 : ((G.win_pix_max + kWave - 1) / kWave * 8 + 15) & ~15;
-    fa.cand_bytes = (2 * G.win_pix_max + 15) & ~15;
+    // the list's capacity: what the LDS budget of ORB_FAST_WAVES_CU waves a CU
+    // leaves after the ROI and the map (>= 256 entries), never more than a
+    // window; ORB_OPT_FAST_CAND_CAP n > 0 (test hook) caps it at n - 1
+    int cap = G.win_pix_max;
+    if (kFastDense) {
+        const int budget = (int)(kCuLds / ORB_FAST_WAVES_CU) & ~15;
+        cap = std::min(cap, std::max(256, (budget - fa.roi_max - fa.win_max) / 2));
+        const int opt = debug_opt(ORB_OPT_FAST_CAND_CAP);
+        if (opt > 0) cap = std::min(cap, opt - 1);
+    }
+    fa.cand_cap = cap;
+    fa.cand_bytes = std::max(16, (2 * cap + 15) & ~15);
     fa.ilist_bytes = ORB_FAST_ILIST_IN_MAP ? 0 : il;
 }
 static size_t fast_wave_lds(const FastArgs& fa) {
@@ -3991,7 +4088,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
 #else
         const dim3 qg(L, B);
 #endif
-        ORB_LAUNCH(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(256), qlds, st, qa);
+        ORB_LAUNCH(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(ORB_QT_THREADS), qlds, st, qa);
     }
     mark();
     // describe
@@ -4265,7 +4362,7 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size
     if (!h->x_stream && hipStreamCreateWithFlags(&h->x_stream, hipStreamNonBlocking) != hipSuccess)
         return ORB_ERR_DEVICE;
     uint8_t* pin = (uint8_t*)h->x_pin;
-    const long long key[7] = {w, hh, lap0, lap1, h->plan_epoch, h->x_pin_gen, h->host_pyr ? 1 : 0};
+    const long long key[7] = {w, hh, lap0, lap1, h->plan_epoch, h->x_pin_gen, (h->host_pyr ? 1 : 0) + 2LL * debug_opt(ORB_OPT_FAST_CAND_CAP)};
     if (!h->x_exec || !std::equal(key, key + 7, h->x_key)) {
         if (h->x_exec) (void)hipGraphExecDestroy(h->x_exec);
         h->x_exec = nullptr;
@@ -4299,6 +4396,7 @@ static int extract_graph(orbx_handle* h, const uint8_t* img, int w, int hh, size
     if (n_out) *n_out = n;
     if (mono_out) *mono_out = mono;
     h->have_last = true;
+    h->last_n = n;
     h->last_w = w; h->last_h = hh;
     h->last_frames = nullptr;      // pyramid slot 0 now holds this image
     h->last_B = 0;
@@ -4315,6 +4413,7 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
     if (!h) return ORB_ERR_PARAM;
     if (!img || w <= 0 || hh <= 0) return ORB_ERR_EMPTY;      // ORBextractor.cc:1090-1091
     if (hipSetDevice(h->device) != hipSuccess) return ORB_ERR_DEVICE;
+    h->have_last = false;          // until this extraction's outputs are complete
     int rc = build_plan(h, w, hh, std::max(1, h->plan.maxB));
     if (rc) return rc;
     Plan& P = h->plan;
@@ -4335,6 +4434,7 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
     if (n_out) *n_out = n;
     if (mono_out) *mono_out = mono;
     h->have_last = true;
+    h->last_n = n;
     h->last_w = w; h->last_h = hh;
     h->last_frames = nullptr;      // pyramid slot 0 now holds this image
     h->last_B = 0;
@@ -4343,6 +4443,18 @@ int orbx_extract(orbx_handle* h, const uint8_t* img, int w, int hh, size_t step,
         ORB_CHECK(hipMemcpy(kps, P.d_kps, n * sizeof(orb_keypoint), hipMemcpyDeviceToHost));
         ORB_CHECK(hipMemcpy(desc, P.d_desc, (size_t)n * 32, hipMemcpyDeviceToHost));
     }
+    return ORB_OK;
+}
+
+// The last orbx_extract's outputs in HBM, for orbm_dframe_from_extractor
+// (matcher.hip): valid until the next extraction call on h.
+extern "C++" int orbmi::extractor_last_outputs(orbx_handle* h, const orb_keypoint** kps, const uint8_t** desc,
+                                               int* n, int* device) {
+    if (!h || !h->have_last || h->last_n > h->plan.host_cap) return ORB_ERR_PARAM;
+    *kps = h->plan.d_kps;
+    *desc = h->plan.d_desc;
+    *n = h->last_n;
+    *device = h->device;
     return ORB_OK;
 }
 
@@ -4431,12 +4543,17 @@ int orbx_debug_math(int device, int what, long long begin, long long end, int ch
         ORB_CHECK(hipMemcpyToSymbol(HIP_SYMBOL(c_pattern), h_pattern, sizeof(h_pattern)));
     }
     const long long nchunks = ((end - begin) + (1ll << chunk_log2) - 1) >> chunk_log2;
+    // (the guard before the allocation: nothing to free on a refusal)
+    const void* kd = what == 0 ? reinterpret_cast<const void*>(&k_debug_math<0>)
+                               : what == 1 ? reinterpret_cast<const void*>(&k_debug_math<1>)
+                                           : reinterpret_cast<const void*>(&k_debug_math<2>);
+    if (!lds_fits(kd, 0)) return ORB_ERR_UNSUPPORTED;
     unsigned long long* d = nullptr;
     ORB_CHECK(hipMalloc(&d, nchunks * sizeof(unsigned long long)));
     const dim3 grid((unsigned)std::min<long long>(nchunks, 8192));
-    if (what == 0) ORB_LAUNCH(k_debug_math<0>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
-    else if (what == 1) ORB_LAUNCH(k_debug_math<1>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
-    else ORB_LAUNCH(k_debug_math<2>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    if (what == 0) hipLaunchKernelGGL(k_debug_math<0>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    else if (what == 1) hipLaunchKernelGGL(k_debug_math<1>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
+    else hipLaunchKernelGGL(k_debug_math<2>, grid, dim3(256), 0, 0, begin, end, chunk_log2, fused, d);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipMemcpy(hashes, d, nchunks * sizeof(unsigned long long), hipMemcpyDeviceToHost);
     (void)hipFree(d);
@@ -4474,7 +4591,8 @@ int orbx_debug_sort(int device, int narrays, const int32_t* off, const int32_t* 
         (tot && (hipMemcpy(d_cnt, cnt, tot * sizeof(int), hipMemcpyHostToDevice) != hipSuccess ||
                  hipMemcpy(d_x0, x0, tot * sizeof(int), hipMemcpyHostToDevice) != hipSuccess)))
         return done(ORB_ERR_DEVICE);
-    ORB_LAUNCH(k_debug_sort, dim3(narrays), dim3(256), dbg_sort_lds(maxm), 0, d_off, d_cnt, d_x0, d_perm, d_fb);
+    if (!lds_fits(reinterpret_cast<const void*>(&k_debug_sort), dbg_sort_lds(maxm))) return done(ORB_ERR_UNSUPPORTED);
+    hipLaunchKernelGGL(k_debug_sort, dim3(narrays), dim3(256), dbg_sort_lds(maxm), 0, d_off, d_cnt, d_x0, d_perm, d_fb);
     if (hipGetLastError() != hipSuccess || hipDeviceSynchronize() != hipSuccess) return done(ORB_ERR_DEVICE);
     if ((tot && hipMemcpy(perm, d_perm, tot * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) ||
         hipMemcpy(fallback, d_fb, narrays * sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)

@@ -1158,6 +1158,8 @@ struct BowArgs {
     int32_t* host_out = nullptr;      // ... and then copies match[f_n] + nmatches there (pinned host memory)
     int* done = nullptr;              // ... and writes seq into this word (signal_done)
     int seq = 0;
+    int reset_after = 0;              // ... and leaves match / nmatches / fin_ticket as it found them
+                                      // (-1 / 0 / 0: persistent scratch of the dframe form)
 };
 
 // One wave per (pair, vocabulary node) the two FeatureVectors share: the
@@ -1528,8 +1530,17 @@ __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_
         bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd));
         if (a.host_out) {
             __syncthreads();
-            for (int i = threadIdx.x; i < a.f_n; i += blockDim.x) a.host_out[i] = a.match[i];
-            if (threadIdx.x == 0) a.host_out[a.f_n] = a.nmatches[0];
+            for (int i = threadIdx.x; i < a.f_n; i += blockDim.x) {
+                a.host_out[i] = a.match[i];
+                if (a.reset_after) a.match[i] = -1;
+            }
+            if (threadIdx.x == 0) {
+                a.host_out[a.f_n] = a.nmatches[0];
+                if (a.reset_after) {
+                    a.nmatches[0] = 0;
+                    *a.fin_ticket = 0u;
+                }
+            }
             signal_done(a.done, a.seq);
         }
     }
@@ -3373,11 +3384,32 @@ __device__ __forceinline__ int fused_accept(const ProjArgs& a, int best, int lvl
     return (float)best <= a.accept;
 }
 
+// The per-call inputs of a dframe search (orbm_*_dframe): phase 1 reads its
+// query's rows straight from pinned host memory through the device mapping
+// (one launch, no upload kernel), and every block copies its share of the
+// whole input run into a device mirror before the last-arriver hand-off, so
+// the last block's phase 2 -- which reads every slot and rescans queries --
+// reads HBM.  delta = mirror address - mapped address of the run.
+struct Mirror {
+    const uint4* src = nullptr;
+    uint4* dst = nullptr;
+    long long n16 = 0, delta = 0;
+};
+__device__ __forceinline__ void mirror_share(const Mirror& m) {
+    if (!m.src) return;
+    const long long stride = (long long)gridDim.x * blockDim.x;
+    for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < m.n16; i += stride) m.dst[i] = m.src[i];
+}
+template <class T> __device__ __forceinline__ T* mirrored(T* p, long long delta) {
+    return p ? (T*)((char*)p + delta) : p;
+}
+
 __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bound, uint32_t* __restrict__ lists,
                                                                int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                                const int32_t* __restrict__ owner_in,
                                                                int32_t* __restrict__ out, int lds_lists,
-                                                               int use_grid, int part, int* done, int seq) {
+                                                               int use_grid, int part, int* done, int seq,
+                                                               Mirror mir) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -3421,10 +3453,19 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                 if (lane == 0) cnt[i] = min(total, (1 << 30) - 1) | (hob << 30);
             }
         }
+        mirror_share(mir);
     }
     if (part == 1) return;
     // ---- the last block to finish phase 1 runs phase 2
     if (part == 0 && !last_arriver(ticket, &misc[0])) return;
+    if (mir.src) {             // phase 2 reads the per-call inputs from their HBM mirror
+        const long long d = mir.delta;
+        a.qx = mirrored(a.qx, d); a.qy = mirrored(a.qy, d); a.qxr = mirrored(a.qxr, d);
+        a.qlevel = mirrored(a.qlevel, d); a.qviewcos = mirrored(a.qviewcos, d); a.qdepth = mirrored(a.qdepth, d);
+        a.qvalid = mirrored(a.qvalid, d); a.qhas_obs = mirrored(a.qhas_obs, d); a.qdesc = mirrored(a.qdesc, d);
+        a.qangle = mirrored(a.qangle, d); a.blocked = mirrored(a.blocked, d);
+        owner_in = mirrored(owner_in, d);
+    }
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     const int mode = a.mode, skip_any = a.skip_any, ori = a.mode == 1 && a.check_ori;
     int rounds = 0, ndry_total = 0;
@@ -4059,6 +4100,8 @@ hipError_t pull_to_device(void* dst, const void* src, size_t len, hipStream_t st
         return hipMemcpyAsync(dst, src, len, hipMemcpyHostToDevice, st);
     const long long n16 = (long long)(len / 16);
     const int blocks = (int)std::min<long long>(1024, std::max<long long>(1, (n16 + 255) / 256));
+    // (ORB_LAUNCH's LDS guard; this function speaks hipError_t)
+    if (!lds_fits(reinterpret_cast<const void*>(k_pull), 0)) return hipErrorInvalidConfiguration;
     hipLaunchKernelGGL(k_pull, dim3(blocks), dim3(256), 0, st, (const uint4*)src_d, (uint4*)dst, n16, (int)(len % 16));
     return hipGetLastError();
 }
@@ -4132,9 +4175,12 @@ struct OutBlock {
     size_t n = 0;
     int* flag = nullptr;       // ORB_OPT_HOST_OUT 0: the completion word the kernel writes last (device view)
     int seq = 0;
-    int alloc(size_t cnt) {
+    // host_only: the block is pinned host memory in every mode (mode 2 acts
+    // as 0: the dframe searches' kernels always write their result there)
+    int alloc(size_t cnt, bool host_only = false) {
         n = std::max<size_t>(1, cnt);
-        const int mode = debug_opt(ORB_OPT_HOST_OUT);
+        int mode = debug_opt(ORB_OPT_HOST_OUT);
+        if (host_only && mode == 2) mode = 0;
         flag = nullptr;
         if (mode != 2) {
             h = (int32_t*)host_stage().get(n * sizeof(int32_t));
@@ -4511,7 +4557,7 @@ __device__ __forceinline__ bool sfi_accept(int best, int best2, float ratio) {
 __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uint32_t* __restrict__ lists,
                                                               int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                               int32_t* __restrict__ out, int use_grid, int part,
-                                                              int* done, int seq) {
+                                                              int* done, int seq, Mirror mir) {
     extern __shared__ __attribute__((aligned(16))) int sl[];
     const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -4550,9 +4596,11 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
                 if (lane == 0) cnt[i] = total;
             }
         }
+        mirror_share(mir);
     }
     if (part == 1) return;
     if (part == 0 && !last_arriver(ticket, &misc[0])) return;
+    if (mir.src) a.prev = mirrored(a.prev, mir.delta);   // phase 2: prev from its HBM mirror
     const unsigned long long t1 = __builtin_amdgcn_s_memtime();
     // ---- phase 2: fixpoint over all queries
     for (int j = tid; j < n1; j += kFusedThreads) D[j] = -2;
@@ -4736,6 +4784,221 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
 
 }  // namespace orbmi
 
+
+// ---------------------------------------------------------------------------
+// Frames resident in HBM (orbm_dframe_*, include/orb_mi355x.h).
+// ---------------------------------------------------------------------------
+struct orbm_dframe {
+    int device = 0;
+    int n = 0, cap_k = 0, cap_d = 0;        // keypoints; allocated keypoint rows / descriptor bytes
+    orb_keypoint* kps = nullptr;
+    uint8_t* desc = nullptr;
+    float* ur = nullptr;                    // mvuRight (n) when the frame has one
+    float* scale = nullptr;                 // mvScaleFactors (nlevels)
+    int ur_cap = 0, scale_cap = 0, nlevels = 0;
+    bool has_ur = false, has_scale = false;
+    orbmi::GridParams g{};
+    float max_x = 0.f, max_y = 0.f;
+    // FeatureVector CSR (fv_nnodes < 0: none yet)
+    int fv_nnodes = -1, fv_total = 0, fv_big = 0, fv_cap_node = 0, fv_cap_off = 0, fv_cap_idx = 0;
+    uint32_t* fv_node = nullptr;
+    int32_t* fv_off = nullptr;
+    uint32_t* fv_idx = nullptr;
+    // k_bow's single-pair offsets: kp_off {0, n}, node_off {0, fv_nnodes}, idx_off {0}
+    long long* offs = nullptr;
+    ~orbm_dframe() {
+        void* ps[] = {kps, desc, ur, scale, fv_node, fv_off, fv_idx, offs};
+        for (void* q : ps)
+            if (q) (void)hipFree(q);
+    }
+};
+
+namespace orbmi {
+
+// grows a device array to at least cnt elements (contents not kept)
+template <class T> static int grow_dev(T*& p, int& cap, size_t cnt) {
+    cnt = std::max<size_t>(1, cnt);
+    if ((size_t)cap >= cnt) return ORB_OK;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc((void**)&p, cnt * sizeof(T)) != hipSuccess) return ORB_ERR_DEVICE;
+    cap = (int)cnt;
+    return ORB_OK;
+}
+
+static int df_offsets(orbm_dframe* df) {
+    if (!df->offs && hipMalloc((void**)&df->offs, 8 * sizeof(long long)) != hipSuccess) return ORB_ERR_DEVICE;
+    const long long o[5] = {0, df->n, 0, std::max(0, df->fv_nnodes), 0};
+    return hipMemcpy(df->offs, o, sizeof(o), hipMemcpyHostToDevice) == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
+}
+
+// bounds, grid factors, u_right and scale factors of an orbm_frame
+static int df_geometry(orbm_dframe* df, const orbm_frame* f, int n) {
+    df->g = grid_params(f);
+    df->max_x = f->max_x;
+    df->max_y = f->max_y;
+    df->has_ur = f->u_right != nullptr;
+    df->has_scale = f->scale_factors != nullptr && f->nlevels > 0;
+    df->nlevels = std::max(0, f->nlevels);
+    int rc;
+    if (df->has_ur) {
+        if ((rc = grow_dev(df->ur, df->ur_cap, n))) return rc;
+        if (n && hipMemcpy(df->ur, f->u_right, (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) return ORB_ERR_DEVICE;
+    }
+    if (df->has_scale) {
+        if ((rc = grow_dev(df->scale, df->scale_cap, df->nlevels))) return rc;
+        if (hipMemcpy(df->scale, f->scale_factors, (size_t)df->nlevels * 4, hipMemcpyHostToDevice) != hipSuccess)
+            return ORB_ERR_DEVICE;
+    }
+    return ORB_OK;
+}
+
+static int df_featvec(orbm_dframe* df, const orbm_featvec* fv) {
+    if (!fv) return ORB_OK;
+    if (fv->nnodes < 0 || (fv->nnodes && (!fv->node_ids || !fv->offsets || !fv->idx))) return ORB_ERR_PARAM;
+    const int nn = fv->nnodes, tot = nn ? fv->offsets[nn] : 0;
+    for (int i = 0; i < nn; ++i)
+        if (fv->offsets[i + 1] < fv->offsets[i]) return ORB_ERR_PARAM;
+    for (int i = 0; i < tot; ++i)
+        if (fv->idx[i] >= (uint32_t)df->n) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = grow_dev(df->fv_node, df->fv_cap_node, nn)) || (rc = grow_dev(df->fv_off, df->fv_cap_off, nn + 1)) ||
+        (rc = grow_dev(df->fv_idx, df->fv_cap_idx, tot)))
+        return rc;
+    if ((nn && hipMemcpy(df->fv_node, fv->node_ids, (size_t)nn * 4, hipMemcpyHostToDevice) != hipSuccess) ||
+        hipMemcpy(df->fv_off, fv->offsets, (size_t)(nn + 1) * 4, hipMemcpyHostToDevice) != hipSuccess ||
+        (tot && hipMemcpy(df->fv_idx, fv->idx, (size_t)tot * 4, hipMemcpyHostToDevice) != hipSuccess))
+        return ORB_ERR_DEVICE;
+    df->fv_nnodes = nn;
+    df->fv_total = tot;
+    df->fv_big = 0;                  // k_bow's large frame nodes (bow_big_nodes)
+    for (int i = 0; i < nn; ++i) df->fv_big += fv->offsets[i + 1] - fv->offsets[i] > kBowRegChunks * kWave;
+    return df_offsets(df);
+}
+
+// Per-thread, per-device state of the dframe searches that their kernels
+// leave as they found it: the last-arriver ticket (0) and k_bow's match row
+// (-1) and count (0).  A call that fails marks it dirty; the next one
+// re-initialises it.
+struct DfScratch {
+    int dev = -1;
+    unsigned* ticket = nullptr;
+    int32_t* match = nullptr;              // [match_cap] then nmatches
+    size_t match_cap = 0;
+    bool dirty = true;
+};
+static DfScratch* df_scratch(int dev, size_t nmatch) {
+    static thread_local std::vector<DfScratch>* v = new std::vector<DfScratch>();   // never destroyed at exit
+    DfScratch* S = nullptr;
+    for (auto& x : *v)
+        if (x.dev == dev) S = &x;
+    if (!S) {
+        v->push_back(DfScratch{});
+        S = &v->back();
+        S->dev = dev;
+    }
+    if (!S->ticket && hipMalloc((void**)&S->ticket, 256) != hipSuccess) { S->ticket = nullptr; return nullptr; }
+    if (nmatch > S->match_cap) {
+        if (S->match) (void)hipFree(S->match);
+        S->match = nullptr;
+        S->match_cap = 0;
+        const size_t cap = std::max<size_t>(4096, nmatch);
+        if (hipMalloc((void**)&S->match, (cap + 1) * 4) != hipSuccess) return nullptr;
+        S->match_cap = cap;
+        S->dirty = true;
+    }
+    if (S->dirty) {
+        if (hipMemset(S->ticket, 0, 256) != hipSuccess || hipMemset(S->match, 0xff, S->match_cap * 4) != hipSuccess ||
+            hipMemset(S->match + S->match_cap, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return nullptr;
+        S->dirty = false;
+    }
+    return S;
+}
+
+// The per-call inputs of a dframe search, packed into one run of the pinned
+// staging arena (16-byte aligned pieces): the kernel reads them through the
+// run's device mapping and mirrors the run into HBM for its phase 2 (Mirror).
+struct ZRun {
+    char* h = nullptr;      // pinned staging
+    char* m = nullptr;      // its device mapping
+    char* dev = nullptr;    // the HBM mirror
+    size_t len = 0, cap = 0;
+    int begin(size_t total, bool mirror) {
+        cap = (std::max<size_t>(16, total) + 255) & ~size_t(255);
+        h = (char*)host_stage().get(cap);
+        if (!h || hipHostGetDevicePointer((void**)&m, h, 0) != hipSuccess || !m) return ORB_ERR_DEVICE;
+        if (mirror && !(dev = (char*)dev_arena().get(cap))) return ORB_ERR_DEVICE;
+        len = 0;
+        return ORB_OK;
+    }
+    static size_t piece(size_t bytes) { return (bytes + 15) & ~size_t(15); }
+    template <class T> const T* add(const T* src, size_t cnt) {
+        const size_t b = cnt * sizeof(T);
+        char* q = h + len;
+        if (b) std::memcpy(q, src, b);
+        const T* r = (const T*)(m + len);
+        len += piece(b);
+        return r;
+    }
+    Mirror mirror() const {
+        Mirror x;
+        if (!dev) return x;
+        x.src = (const uint4*)m;
+        x.dst = (uint4*)dev;
+        x.n16 = (long long)(len / 16);
+        x.delta = (long long)((uintptr_t)dev - (uintptr_t)m);
+        return x;
+    }
+};
+
+// The device of a dframe search (every dframe on one device), current on return.
+static int df_device(std::initializer_list<const orbm_dframe*> dfs) {
+    int dev = -1;
+    for (const orbm_dframe* d : dfs) {
+        if (!d) return ORB_ERR_PARAM;
+        if (dev >= 0 && d->device != dev) return ORB_ERR_PARAM;
+        dev = d->device;
+    }
+    if (hipSetDevice(dev) != hipSuccess) return ORB_ERR_DEVICE;
+    arena_reset();
+    return ORB_OK;
+}
+
+// The fused projection search on a dframe (k_proj_fused, part 0, inputs
+// read zero-copy and mirrored): run_proj's fused form with the frame in HBM.
+static int run_proj_dframe(ProjArgs& a, const orbm_dframe* f, ZRun& z, const int32_t* owner_m, int32_t* owner) {
+    const int n = f->n;
+    if (n > kFusedMaxN || a.nq > kFusedMaxQ || f->nlevels > 8 || proj_fused_lds(n, a.nq, false) > kCuLds)
+        return ORB_ERR_UNSUPPORTED;
+    DfScratch* S = df_scratch(f->device, 0);
+    if (!S) return ORB_ERR_DEVICE;
+    a.kps = f->kps; a.desc = f->desc; a.n = n; a.u_right = f->has_ur ? f->ur : nullptr; a.scale = f->scale;
+    a.g = f->g; a.owner = nullptr; a.nmatches = nullptr;
+    const size_t gb = lds_grid_bytes(n);
+    const int use_grid = proj_fused_lds(n, a.nq, false) + gb <= kCuLds;
+    const int lds_lists = proj_fused_lds(n, a.nq, true) + (use_grid ? gb : 0) <= kCuLds;
+    const size_t lds = proj_fused_lds(n, a.nq, lds_lists != 0) + (use_grid ? gb : 0);
+    uint32_t* lists = (uint32_t*)dev_arena().get((size_t)std::max(1, a.nq) * kProjK * 4);
+    int* cnt = (int*)dev_arena().get((size_t)std::max(1, a.nq) * 4);
+    OutBlock out;
+    if (!lists || !cnt || out.alloc((size_t)n + 13, true)) return ORB_ERR_DEVICE;
+    const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
+    S->dirty = true;                   // until the kernel has reset the ticket
+    KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists, cnt, S->ticket, owner_m,
+            out.d, lds_lists, use_grid, 0, out.flag, out.seq, z.mirror());
+    ORB_CHECK(hipGetLastError());
+    std::vector<int32_t> res((size_t)n + 13);
+    ORB_CHECK(out.fetch(res.data(), res.size()));
+    S->dirty = false;
+    if (n) std::memcpy(owner, res.data() + 1, (size_t)n * sizeof(int32_t));
+    std::memcpy(proj_stats(), res.data() + n + 1, 12 * sizeof(int32_t));
+    return res[0];
+}
+
+}  // namespace orbmi
+
 using namespace orbmi;
 
 static std::atomic<int> g_debug_opt[ORB_OPT_COUNT];
@@ -4826,12 +5089,12 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         const size_t lds = sfi_fused_lds(n1, n2) + (use_grid ? gb : 0);
         if (sform == 3) {      // phase 1, then phase 2 as a one-block launch (no ticket)
             KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
-                    use_grid, 1, (int*)nullptr, 0);
+                    use_grid, 1, (int*)nullptr, 0, Mirror{});
             KLAUNCH(k_sfi_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d, use_grid, 2,
-                    out.flag, out.seq);
+                    out.flag, out.seq, Mirror{});
         } else {
             KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
-                    use_grid, 0, out.flag, out.seq);
+                    use_grid, 0, out.flag, out.seq, Mirror{});
         }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)13 + 3 * n1);
@@ -5097,6 +5360,13 @@ static int launch_bow_kf(BowArgs& a, int npairs, long long G, long long nfv, hip
     // with its bin; the map's FeatureVector total bounds it where the host
     // knows it: a larger map takes k_bow_final)
     const bool claims = all_lds && a.f_n <= kBowkRow && !a.out12 && !a.f_valid && nfv < (1LL << 26);
+    // every LDS-sized launch of the sequence checked before the first is
+    // queued: a refusal half-way would leave queued work on scratch that
+    // scratch_used() below would not cover
+    if (!lds_fits(reinterpret_cast<const void*>(&k_bowk_scan), (size_t)2 * a.f_nnodes * sizeof(int)) ||
+        (big_pitch && !lds_fits(reinterpret_cast<const void*>(&k_bowk_resolve_lane<true, true>), big_lds)) ||
+        (claims && !lds_fits(reinterpret_cast<const void*>(&k_bowk_final), (size_t)a.f_n * 4)))
+        return ORB_ERR_UNSUPPORTED;
     int rc;
     if ((rc = g_fl.alloc(G)) || (rc = g_off.alloc(G)) || (rc = g_pr.alloc(G)) || (rc = bgcount.alloc((size_t)a.f_nnodes * nsub)) ||
         (rc = bstart.alloc(a.f_nnodes + 1)) || (rc = slot_src.alloc(slots)) || (rc = lists.alloc(slots)) ||
@@ -5217,12 +5487,12 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         if (form == 5) {       // phase 1, then phase 2 as a one-block launch (no ticket)
             KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
-                    ticket.p, own.p, out.d, lds_lists, use_grid, 1, (int*)nullptr, 0);
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 1, (int*)nullptr, 0, Mirror{});
             KLAUNCH(k_proj_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p, ticket.p,
-                    own.p, out.d, lds_lists, use_grid, 2, out.flag, out.seq);
+                    own.p, out.d, lds_lists, use_grid, 2, out.flag, out.seq, Mirror{});
         } else {
             KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
-                    ticket.p, own.p, out.d, lds_lists, use_grid, 0, out.flag, out.seq);
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 0, out.flag, out.seq, Mirror{});
         }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)f->n + 13);
@@ -5341,7 +5611,7 @@ int orbv_transform_device(const orbv_vocab* voc, int n, const uint8_t* d_desc, i
     if (voc->nnodes < 2) return ORB_ERR_EMPTY;
     if (n == 0) return ORB_OK;
     const int nid_level = voc->depth_levels - levelsup;
-    hipLaunchKernelGGL(k_transform, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, voc->first_child,
+    ORB_LAUNCH(k_transform, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, voc->first_child,
                        voc->nchild, voc->child_idx, voc->node_desc, voc->word_id, voc->weight, n, d_desc, nid_level,
                        d_word_id, d_weight, d_node_id);
     ORB_CHECK(hipGetLastError());
@@ -5809,6 +6079,190 @@ int orbm_search_by_projection_last_fisheye(const orbm_frame* cur, int nleft, int
     FishArgs fa{};
     fa.rqx = rx.p; fa.rqy = ry.p;
     return run_fisheye(a, fa, cur, nleft, owner, blocked);
+}
+
+orbm_dframe* orbm_dframe_create(int device) {
+    int ndev = 0;
+    if (device < 0 || hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return nullptr;
+    orbm_dframe* df = new (std::nothrow) orbm_dframe();
+    if (df) df->device = device;
+    return df;
+}
+
+void orbm_dframe_destroy(orbm_dframe* df) {
+    if (!df) return;
+    if (hipSetDevice(df->device) == hipSuccess) (void)hipDeviceSynchronize();   // no search may still read it
+    delete df;
+}
+
+int orbm_dframe_count(const orbm_dframe* df) { return df ? df->n : ORB_ERR_PARAM; }
+
+int orbm_dframe_upload(orbm_dframe* df, const orbm_frame* f, const orbm_featvec* fv) {
+    if (!df || !f || f->n < 0 || (f->n && (!f->kps || !f->desc))) return ORB_ERR_PARAM;
+    if (hipSetDevice(df->device) != hipSuccess) return ORB_ERR_DEVICE;
+    int rc;
+    if ((rc = grow_dev(df->kps, df->cap_k, f->n)) || (rc = grow_dev(df->desc, df->cap_d, (size_t)f->n * 32))) return rc;
+    df->n = f->n;
+    if (f->n && (hipMemcpy(df->kps, f->kps, (size_t)f->n * sizeof(orb_keypoint), hipMemcpyHostToDevice) != hipSuccess ||
+                 hipMemcpy(df->desc, f->desc, (size_t)f->n * 32, hipMemcpyHostToDevice) != hipSuccess))
+        return ORB_ERR_DEVICE;
+    df->fv_nnodes = -1;
+    if ((rc = df_geometry(df, f, f->n)) || (rc = df_offsets(df))) return rc;
+    return df_featvec(df, fv);
+}
+
+int orbm_dframe_from_extractor(orbm_dframe* df, orbx_handle* h, const orbm_frame* geom, const orbm_featvec* fv) {
+    if (!df || !h || !geom) return ORB_ERR_PARAM;
+    const orb_keypoint* sk = nullptr;
+    const uint8_t* sd = nullptr;
+    int n = 0, dev = 0;
+    if (extractor_last_outputs(h, &sk, &sd, &n, &dev) != ORB_OK || dev != df->device) return ORB_ERR_PARAM;
+    if (hipSetDevice(df->device) != hipSuccess) return ORB_ERR_DEVICE;
+    int rc;
+    if ((rc = grow_dev(df->kps, df->cap_k, n)) || (rc = grow_dev(df->desc, df->cap_d, (size_t)n * 32))) return rc;
+    df->n = n;
+    // device to device by the copy kernel (k_pull) on the null stream: the
+    // extraction has completed (orbx_extract returned after synchronising)
+    if (n && (pull_to_device(df->kps, sk, (size_t)n * sizeof(orb_keypoint), 0) != hipSuccess ||
+              pull_to_device(df->desc, sd, (size_t)n * 32, 0) != hipSuccess))
+        return ORB_ERR_DEVICE;
+    df->fv_nnodes = -1;
+    if ((rc = df_geometry(df, geom, n)) || (rc = df_offsets(df))) return rc;
+    return df_featvec(df, fv);
+}
+
+int orbm_dframe_set_featvec(orbm_dframe* df, const orbm_featvec* fv) {
+    if (!df || !fv) return ORB_ERR_PARAM;
+    if (hipSetDevice(df->device) != hipSuccess) return ORB_ERR_DEVICE;
+    return df_featvec(df, fv);
+}
+
+int orbm_search_by_bow_dframe(const orbm_dframe* kf, const uint8_t* kf_mp_valid, const orbm_dframe* f,
+                              float nnratio, int check_ori, int32_t* match_f) {
+    if (!kf || !f || !match_f || kf->fv_nnodes < 0 || f->fv_nnodes < 0 || (kf->n && !kf_mp_valid))
+        return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = df_device({kf, f}))) return rc;
+    DfScratch* S = df_scratch(f->device, (size_t)std::max(1, f->n));
+    if (!S) return ORB_ERR_DEVICE;
+    ZRun z;
+    OutBlock out;
+    if ((rc = z.begin(kf->n, false)) || (rc = out.alloc((size_t)f->n + 1, true))) return rc;
+    const uint8_t* kv = z.add(kf_mp_valid, kf->n);     // read by k_bow through the mapping
+    BowArgs a{};
+    a.kf_kps = kf->kps; a.kf_desc = kf->desc; a.kf_valid = kv; a.kp_off = kf->offs;
+    a.kf_node = kf->fv_node; a.kf_off = kf->fv_off; a.kf_idx = kf->fv_idx; a.node_off = kf->offs + 2;
+    a.idx_off = kf->offs + 4;
+    a.f_kps = f->kps; a.f_desc = f->desc; a.f_n = f->n; a.f_node = f->fv_node; a.f_off = f->fv_off;
+    a.f_idx = f->fv_idx; a.f_nnodes = f->fv_nnodes; a.ratio = nnratio; a.check_ori = check_ori;
+    a.match = S->match; a.nmatches = S->match + S->match_cap; a.f_nleft = -1; a.fin_ticket = S->ticket;
+    a.host_out = out.d; a.done = out.flag; a.seq = out.seq; a.reset_after = 1;
+    S->dirty = true;                   // until the kernel has reset its scratch
+    if ((rc = launch_bow(a, 1, 0, f->fv_big, kf->fv_nnodes))) return rc;
+    std::vector<int32_t> res((size_t)f->n + 1);
+    ORB_CHECK(out.fetch(res.data(), res.size()));
+    S->dirty = false;
+    if (f->n) std::memcpy(match_f, res.data(), (size_t)f->n * 4);
+    return res[f->n];
+}
+
+int orbm_search_for_initialization_dframe(const orbm_dframe* f1, const orbm_dframe* f2, float* prev_xy, int window,
+                                          float nnratio, int check_ori, int32_t* matches12) {
+    if (!f1 || !f2 || !prev_xy || !matches12) return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = df_device({f1, f2}))) return rc;
+    const int n1 = f1->n, n2 = f2->n;
+    if (n1 > kFusedMaxN || n2 > kFusedMaxN || nnratio < 0.2f || sfi_fused_lds(n1, n2) > kCuLds)
+        return ORB_ERR_UNSUPPORTED;
+    DfScratch* S = df_scratch(f1->device, 0);
+    if (!S) return ORB_ERR_DEVICE;
+    ZRun z;
+    OutBlock out;
+    if ((rc = z.begin((size_t)8 * n1, true)) || (rc = out.alloc((size_t)13 + 3 * n1, true))) return rc;
+    SfiFusedArgs a{};
+    a.k1 = f1->kps; a.d1 = f1->desc; a.n1 = n1; a.k2 = f2->kps; a.d2 = f2->desc; a.n2 = n2;
+    a.prev = z.add(prev_xy, (size_t)2 * n1);
+    a.g = f2->g; a.window = (float)window; a.ratio = nnratio; a.check_ori = check_ori;
+    int bound = kThLow;
+    while (bound < 255 && (float)(bound + 1) * nnratio <= (float)kThLow) ++bound;
+    a.bound = bound;
+    uint32_t* lists = (uint32_t*)dev_arena().get((size_t)std::max(1, n1) * kTopK * 4);
+    int* cnt = (int*)dev_arena().get((size_t)std::max(1, n1) * 4);
+    if (!lists || !cnt) return ORB_ERR_DEVICE;
+    const int nblk = std::max(1, (n1 + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
+    const size_t gb = lds_grid_bytes(n2);
+    const int use_grid = sfi_fused_lds(n1, n2) + gb <= kCuLds;
+    const size_t lds = sfi_fused_lds(n1, n2) + (use_grid ? gb : 0);
+    S->dirty = true;
+    KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists, cnt, S->ticket, out.d, use_grid, 0,
+            out.flag, out.seq, z.mirror());
+    ORB_CHECK(hipGetLastError());
+    std::vector<int32_t> res((size_t)13 + 3 * n1);
+    ORB_CHECK(out.fetch(res.data(), res.size()));
+    S->dirty = false;
+    std::memcpy(proj_stats(), res.data() + 1 + 3 * n1, 12 * sizeof(int32_t));
+    if (n1) {
+        std::memcpy(matches12, res.data() + 1, (size_t)n1 * sizeof(int32_t));
+        std::memcpy(prev_xy, res.data() + 1 + n1, (size_t)n1 * 2 * sizeof(float));
+    }
+    return res[0];
+}
+
+int orbm_search_by_projection_mps_dframe(const orbm_dframe* f, const orbm_mappoints* mps, float th, int far_points,
+                                         float th_far, float nnratio, int32_t* owner, const uint8_t* blocked) {
+    if (!f || !mps || !owner || !blocked || !f->has_scale || mps->n < 0) return ORB_ERR_PARAM;
+    const int nq = mps->n;
+    if (nq && (!mps->proj_x || !mps->proj_y || !mps->proj_xr || !mps->level || !mps->view_cos || !mps->track_depth ||
+               !mps->in_view || !mps->has_obs || !mps->desc))
+        return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = df_device({f}))) return rc;
+    if (f->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    for (int i = 0; i < nq; ++i)
+        if (mps->in_view[i] && (mps->level[i] < 0 || mps->level[i] >= f->nlevels)) return ORB_ERR_PARAM;
+    const size_t nn = (size_t)std::max(1, f->n);
+    ZRun z;
+    if ((rc = z.begin((size_t)nq * (4 * 6 + 2 + 32) + 6 * 16 + nn * 5 + 32, true))) return rc;
+    ProjArgs a{};
+    a.mode = 0; a.nq = nq;
+    a.qdesc = z.add(mps->desc, (size_t)nq * 32);
+    a.qx = z.add(mps->proj_x, nq); a.qy = z.add(mps->proj_y, nq); a.qxr = z.add(mps->proj_xr, nq);
+    a.qlevel = z.add(mps->level, nq); a.qviewcos = z.add(mps->view_cos, nq); a.qdepth = z.add(mps->track_depth, nq);
+    a.qvalid = z.add(mps->in_view, nq); a.qhas_obs = z.add(mps->has_obs, nq); a.qangle = nullptr;
+    const int32_t* own = z.add(owner, (size_t)f->n);
+    a.blocked = z.add(blocked, (size_t)f->n);
+    a.th = th; a.th_far = th_far; a.ratio = nnratio; a.far_points = far_points; a.last_mode = 0; a.check_ori = 0;
+    return run_proj_dframe(a, f, z, own, owner);
+}
+
+int orbm_search_by_projection_last_dframe(const orbm_dframe* cur, int nlast, const uint8_t* valid, const float* u,
+                                          const float* v, const float* ur, const int32_t* last_octave,
+                                          const float* last_angle, const uint8_t* has_obs,
+                                          const uint8_t* last_desc, float th, int mode, int check_ori,
+                                          int32_t* owner, const uint8_t* blocked) {
+    if (!cur || !owner || !blocked || !cur->has_scale || nlast < 0) return ORB_ERR_PARAM;
+    if (nlast && (!valid || !u || !v || !ur || !last_octave || !last_angle || !has_obs || !last_desc))
+        return ORB_ERR_PARAM;
+    int rc;
+    if ((rc = df_device({cur}))) return rc;
+    if (cur->n > 0xffff) return ORB_ERR_UNSUPPORTED;
+    for (int i = 0; i < nlast; ++i)
+        if (valid[i] && (last_octave[i] < 0 || last_octave[i] >= cur->nlevels)) return ORB_ERR_PARAM;
+    const size_t nn = (size_t)std::max(1, cur->n);
+    ZRun z;
+    if ((rc = z.begin((size_t)nlast * (4 * 5 + 2 + 32) + 6 * 16 + nn * 5 + 32, true))) return rc;
+    ProjArgs a{};
+    a.mode = 1; a.nq = nlast;
+    a.qdesc = z.add(last_desc, (size_t)nlast * 32);
+    a.qx = z.add(u, nlast); a.qy = z.add(v, nlast); a.qxr = z.add(ur, nlast);
+    a.qlevel = z.add(last_octave, nlast); a.qangle = z.add(last_angle, nlast);
+    a.qvalid = z.add(valid, nlast); a.qhas_obs = z.add(has_obs, nlast);
+    a.qviewcos = nullptr; a.qdepth = nullptr;
+    const int32_t* own = z.add(owner, (size_t)cur->n);
+    a.blocked = z.add(blocked, (size_t)cur->n);
+    a.th = th; a.th_far = 0; a.ratio = 0; a.far_points = 0; a.last_mode = mode; a.check_ori = check_ori;
+    a.skip_any = 0; a.accept = (float)kThHigh;                                   // :1770
+    return run_proj_dframe(a, cur, z, own, owner);
 }
 
 }  // extern "C"

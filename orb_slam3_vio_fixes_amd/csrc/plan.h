@@ -142,6 +142,7 @@ struct orbx_handle {
     orbmi::Plan plan;
     bool have_last = false;
     int last_w = 0, last_h = 0;
+    int last_n = 0;                  // keypoints of the last orbx_extract (in plan.d_kps / d_desc)
     // optional per-stage HIP-event timing (orbx_set_profiling)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;

@@ -356,6 +356,43 @@ def keypoints_from_device(kps_i32) -> np.ndarray:
     return a.view(abi.KEYPOINT_DTYPE).reshape(a.shape[:-1])
 
 
+class DeviceFrame:
+    """A Frame or KeyFrame resident in HBM (orbm_dframe, include/orb_mi355x.h):
+    the Tracking thread's searches then move only their per-call inputs and
+    results across PCIe (Tracking.cc:2720-2730, 2886, 3413)."""
+
+    def __init__(self, device: int = 0):
+        self._L = capi.lib()
+        self._h = self._L.orbm_dframe_create(device)
+        if not self._h:
+            raise RuntimeError("orbm_dframe_create failed (no device?)")
+        self._keep = None
+
+    def upload(self, F: abi.Keep, fv: abi.Keep | None = None) -> "DeviceFrame":
+        capi.check(self._L.orbm_dframe_upload(self._h, F.ref(), fv.ref() if fv is not None else None),
+                   "orbm_dframe_upload")
+        return self
+
+    def from_extractor(self, ex: "ORBextractor", geom: abi.Keep, fv: abi.Keep | None = None) -> "DeviceFrame":
+        """The last image `ex` extracted (ORBextractor.__call__), copied device to device."""
+        capi.check(self._L.orbm_dframe_from_extractor(self._h, ex._h, geom.ref(), fv.ref() if fv is not None else None),
+                   "orbm_dframe_from_extractor")
+        return self
+
+    def set_featvec(self, fv: abi.Keep) -> "DeviceFrame":
+        capi.check(self._L.orbm_dframe_set_featvec(self._h, fv.ref()), "orbm_dframe_set_featvec")
+        return self
+
+    @property
+    def n(self) -> int:
+        return capi.check(self._L.orbm_dframe_count(self._h), "orbm_dframe_count")
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            self._L.orbm_dframe_destroy(self._h)
+            self._h = None
+
+
 class ORBmatcher:
     TH_HIGH, TH_LOW, HISTO_LENGTH = 100, 50, 30
 
@@ -384,6 +421,50 @@ class ORBmatcher:
                                            self.mfNNratio, int(self.mbCheckOrientation), abi.ptr(match))
         capi.check(nm, "SearchByBoW")
         return nm, match
+
+    # ---- the same searches on HBM-resident frames (orbm_*_dframe) ----
+    def SearchForInitializationDevice(self, F1: DeviceFrame, F2: DeviceFrame, vbPrevMatched: np.ndarray,
+                                      windowSize: int = 10):
+        prev = np.ascontiguousarray(vbPrevMatched, np.float32).copy()
+        m12 = np.zeros(F1.n, np.int32)
+        nm = capi.lib().orbm_search_for_initialization_dframe(F1._h, F2._h, abi.ptr(prev), windowSize,
+                                                              self.mfNNratio, int(self.mbCheckOrientation),
+                                                              abi.ptr(m12))
+        capi.check(nm, "SearchForInitialization(dframe)")
+        return nm, m12, prev
+
+    def SearchByBoWDevice(self, KF: DeviceFrame, kf_valid: np.ndarray, F: DeviceFrame):
+        kf_valid = np.ascontiguousarray(kf_valid, np.uint8)
+        match = np.zeros(F.n, np.int32)
+        nm = capi.lib().orbm_search_by_bow_dframe(KF._h, abi.ptr(kf_valid), F._h, self.mfNNratio,
+                                                  int(self.mbCheckOrientation), abi.ptr(match))
+        capi.check(nm, "SearchByBoW(dframe)")
+        return nm, match
+
+    def SearchByProjectionDevice(self, F: DeviceFrame, mps: abi.Keep, th: float = 3.0, bFarPoints: bool = False,
+                                 thFarPoints: float = 50.0, owner=None, blocked=None):
+        n = F.n
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        blocked = np.zeros(n, np.uint8) if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nm = capi.lib().orbm_search_by_projection_mps_dframe(F._h, mps.ref(), th, int(bFarPoints), thFarPoints,
+                                                             self.mfNNratio, abi.ptr(owner), abi.ptr(blocked))
+        capi.check(nm, "SearchByProjection(dframe, MPs)")
+        return nm, owner
+
+    def SearchByProjectionLastDevice(self, cur: DeviceFrame, valid, u, v, ur, octave, angle, has_obs, desc,
+                                     th: float, mode: int = 0, owner=None, blocked=None):
+        n = cur.n
+        arrs = [np.ascontiguousarray(valid, np.uint8), np.ascontiguousarray(u, np.float32),
+                np.ascontiguousarray(v, np.float32), np.ascontiguousarray(ur, np.float32),
+                np.ascontiguousarray(octave, np.int32), np.ascontiguousarray(angle, np.float32),
+                np.ascontiguousarray(has_obs, np.uint8), np.ascontiguousarray(desc, np.uint8)]
+        owner = np.full(n, -1, np.int32) if owner is None else np.ascontiguousarray(owner, np.int32).copy()
+        blocked = np.zeros(n, np.uint8) if blocked is None else np.ascontiguousarray(blocked, np.uint8)
+        nm = capi.lib().orbm_search_by_projection_last_dframe(cur._h, len(arrs[0]), *[abi.ptr(a) for a in arrs], th,
+                                                              mode, int(self.mbCheckOrientation), abi.ptr(owner),
+                                                              abi.ptr(blocked))
+        capi.check(nm, "SearchByProjection(dframe, LastFrame)")
+        return nm, owner
 
     def SearchByBoWMany(self, KFs, KFfvs, kf_valids, F: abi.Keep, Ffv: abi.Keep):
         """SearchByBoW(KF_i, F) for several candidate keyframes in one launch

@@ -116,7 +116,12 @@ class FrameChannel:
         self._host = np.zeros(16 + self.cap * 60, np.uint8) if self.rank == src else None
 
     def broadcast(self, kps: np.ndarray | None, desc: np.ndarray | None):
-        """([n, 28] uint8, [n, 32] uint8) tensors on the channel's device."""
+        """([n, 28] uint8, [n, 32] uint8) tensors on the channel's device.
+
+        The returned tensors are views into the channel's one persistent
+        buffer: they are valid until the next broadcast, which overwrites them
+        in place (on the current stream).  A caller that keeps a frame past
+        that, or reads it on another stream, must ``.clone()`` it first."""
         import torch
         import torch.distributed as dist
         cap = self.cap

@@ -1,0 +1,214 @@
+"""The Tracking thread's searches on HBM-resident frames (orbm_dframe_*,
+include/orb_mi355x.h): every dframe form gives the upload form's result and
+the oracle's, on the sizes and edge cases the upload forms are tested on.
+Reference: Tracking.cc:2720-2730 (ComputeBoW + SearchByBoW(KF, F)), :2886
+(SearchByProjection(F, LastFrame)), :3413 (SearchLocalPoints), :2459-2492
+(SearchForInitialization); ORBmatcher.cc:43-425, 648-763, 1676-1887."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from orb_slam3_vio_fixes_amd import abi, capi, orb, synth
+
+pytestmark = pytest.mark.gpu
+SCALE = np.float32(1.2) ** np.arange(8, dtype=np.float32)
+
+
+@pytest.fixture(scope="module")
+def frames():
+    seq = synth.sequence(752, 480, 3, config=31)
+    ex = O.OracleExtractor(1000, 1.2, 8, 20, 7)
+    return [ex(seq[i], (0, 1000)) for i in range(3)] + [ex(synth.image(752, 480, 3131), (0, 1000))]
+
+
+def fr(f, **kw):
+    return abi.frame_struct(f[0], f[1], 752, 480, scale_factors=SCALE, **kw)
+
+
+def dev(F, fv=None):
+    return orb.DeviceFrame(0).upload(F, fv)
+
+
+@pytest.mark.parametrize("i1,i2,window,ratio,ori", [(0, 1, 100, 0.9, True), (1, 2, 100, 0.9, True),
+                                                    (0, 2, 60, 0.8, False), (0, 3, 400, 1.0, True)])
+def test_search_for_initialization_dframe(gpu_lib, frames, i1, i2, window, ratio, ori):
+    f1, f2 = frames[i1], frames[i2]
+    prev = np.stack([f1[0]["x"], f1[0]["y"]], 1)
+    m = orb.ORBmatcher(ratio, ori)
+    D1, D2 = dev(fr(f1)), dev(fr(f2))
+    for _ in range(3):      # the kernel leaves its persistent ticket as it found it
+        nm, m12, p2 = m.SearchForInitializationDevice(D1, D2, prev, window)
+        unm, um12, up2 = m.SearchForInitialization(fr(f1), fr(f2), prev, window)
+        rnm, rm12, rp2 = O.search_for_initialization(fr(f1), fr(f2), prev, window, ratio, ori)
+        assert nm == unm == rnm
+        np.testing.assert_array_equal(m12, rm12)
+        np.testing.assert_array_equal(um12, rm12)
+        np.testing.assert_array_equal(p2, rp2)
+
+
+@pytest.mark.parametrize("zc", [0, 1, 2])
+@pytest.mark.parametrize("ori,ratio,nodes", [(True, 0.7, 40), (False, 0.75, 12), (True, 0.9, 200), (True, 0.8, 4)])
+def test_search_by_bow_dframe(gpu_lib, frames, ori, ratio, nodes, zc, debug_option):
+    debug_option(capi.ORB_OPT_HOST_OUT, zc)        # 2 acts as 0 for the dframe form
+    rng = np.random.default_rng(nodes)
+    kf, f = frames[0], frames[1]
+    knode = rng.integers(0, nodes, len(kf[0]))
+    fnode = rng.integers(0, nodes, len(f[0]))
+    knode[rng.random(len(knode)) < 0.05] = -1
+    kfv, ffv = abi.featvec_struct(knode), abi.featvec_struct(fnode)
+    K, F = dev(fr(kf), kfv), dev(fr(f), ffv)
+    m = orb.ORBmatcher(ratio, ori)
+    for rep in range(3):    # new MapPoint validity per call, the same resident keyframe
+        kvalid = (rng.random(len(knode)) < 0.85 - 0.2 * rep).astype(np.uint8)
+        nm, match = m.SearchByBoWDevice(K, kvalid, F)
+        args = (fr(kf), kfv, kvalid, fr(f), ffv)
+        unm, umatch = m.SearchByBoW(*args)
+        rnm, rmatch = O.search_by_bow(*args, ratio, ori)
+        assert nm == unm == rnm and nm > 0
+        np.testing.assert_array_equal(match, rmatch)
+        np.testing.assert_array_equal(umatch, rmatch)
+
+
+def test_search_by_bow_dframe_frames_of_other_sizes(gpu_lib, frames):
+    """The match scratch the kernel resets for the next call: frames of more
+    and fewer keypoints in turn (the scratch grows), every result the oracle's."""
+    rng = np.random.default_rng(5)
+    kf = frames[0]
+    knode = rng.integers(0, 30, len(kf[0]))
+    kfv = abi.featvec_struct(knode)
+    K = dev(fr(kf), kfv)
+    kvalid = (rng.random(len(knode)) < 0.9).astype(np.uint8)
+    m = orb.ORBmatcher(0.75, True)
+    big = orb.DeviceFrame(0)
+    for n in (1000, 300, 5000, 17, 1000):
+        f = frames[1] if n <= len(frames[1][0]) else frames[3]
+        k, d = f[0][:n], f[1][:n]
+        if n > len(k):       # a larger frame: the keypoints tiled (jittered positions)
+            reps = -(-n // len(k))
+            k = np.concatenate([k] * reps)[:n].copy()
+            k["x"] = np.clip(k["x"] + rng.normal(0, 2, n).astype(np.float32), 0, 751)
+            d = np.concatenate([d] * reps)[:n] ^ rng.integers(0, 2, (n, 32), dtype=np.uint8)
+        fnode = rng.integers(0, 30, len(k))
+        ffv = abi.featvec_struct(fnode)
+        F = abi.frame_struct(k, d, 752, 480, scale_factors=SCALE)
+        big.upload(F, ffv)
+        nm, match = m.SearchByBoWDevice(K, kvalid, big)
+        rnm, rmatch = O.search_by_bow(fr(kf), kfv, kvalid, F, ffv, 0.75, True)
+        assert nm == rnm
+        np.testing.assert_array_equal(match, rmatch)
+
+
+def projection_queries(frames, seed, n=600):
+    rng = np.random.default_rng(seed)
+    src, cur = frames[0], frames[1]
+    k = src[0][:n]
+    qx = (k["x"] + rng.normal(0, 3, len(k)).astype(np.float32) + 3).astype(np.float32)
+    qy = (k["y"] + rng.normal(0, 3, len(k)).astype(np.float32) + 3).astype(np.float32)
+    return rng, src, cur, k, qx, qy
+
+
+@pytest.mark.parametrize("seed,th,far", [(1, 3.0, False), (2, 1.0, False), (3, 5.0, True)])
+def test_search_by_projection_mappoints_dframe(gpu_lib, frames, seed, th, far):
+    rng, src, cur, k, qx, qy = projection_queries(frames, seed)
+    n = len(k)
+    mps = abi.mappoints_struct(qx, qy, qx - rng.uniform(0, 40, n).astype(np.float32), k["octave"],
+                               rng.uniform(0.99, 1.0, n).astype(np.float32), rng.uniform(0, 100, n).astype(np.float32),
+                               (rng.random(n) < 0.9).astype(np.uint8), (rng.random(n) < 0.7).astype(np.uint8),
+                               src[1][:n])
+    N = len(cur[0])
+    owner = np.full(N, -1, np.int32)
+    pre = rng.random(N) < 0.05
+    owner[pre] = -2
+    blocked = (pre & (rng.random(N) < 0.5)).astype(np.uint8)
+    ur = np.where(rng.random(N) < 0.3, cur[0]["x"] - rng.uniform(0, 40, N).astype(np.float32), -1).astype(np.float32)
+    F = fr(cur, u_right=ur)
+    D = dev(F)
+    m = orb.ORBmatcher(0.8, True)
+    for _ in range(2):
+        nm, own = m.SearchByProjectionDevice(D, mps, th, far, 50.0, owner, blocked)
+        unm, uown = m.SearchByProjection(F, mps, th, far, 50.0, owner, blocked)
+        rnm, rown = O.search_by_projection_mps(F, mps, th, far, 50.0, 0.8, owner, blocked)
+        assert nm == unm == rnm and nm > 0
+        np.testing.assert_array_equal(own, rown)
+        np.testing.assert_array_equal(uown, rown)
+
+
+@pytest.mark.parametrize("seed,mode,ori", [(4, 0, True), (5, 1, True), (6, 2, False), (7, 0, False)])
+def test_search_by_projection_last_frame_dframe(gpu_lib, frames, seed, mode, ori):
+    rng, src, cur, k, qx, qy = projection_queries(frames, seed)
+    n = len(k)
+    valid = (rng.random(n) < 0.9).astype(np.uint8)
+    has_obs = (rng.random(n) < 0.6).astype(np.uint8)
+    ur = (qx - rng.uniform(0, 40, n)).astype(np.float32)
+    N = len(cur[0])
+    owner = np.full(N, -1, np.int32)
+    owner[rng.random(N) < 0.05] = -2
+    blocked = (rng.random(N) < 0.03).astype(np.uint8)
+    F = fr(cur)
+    D = dev(F)
+    args = (valid, qx, qy, ur, k["octave"], k["angle"], has_obs, src[1][:n], 7.0, mode)
+    m = orb.ORBmatcher(0.9, ori)
+    for _ in range(2):
+        nm, own = m.SearchByProjectionLastDevice(D, *args, owner=owner, blocked=blocked)
+        unm, uown = m.SearchByProjectionLast(F, *args, owner=owner, blocked=blocked)
+        rnm, rown = O.search_by_projection_last(F, *args, ori, owner, blocked)
+        assert nm == unm == rnm and nm > 0
+        np.testing.assert_array_equal(own, rown)
+        np.testing.assert_array_equal(uown, rown)
+
+
+def test_dframe_from_extractor(gpu_lib):
+    """Frame::ExtractORB then the searches on the same Frame with no upload
+    (orbm_dframe_from_extractor copies the extractor's HBM outputs): the
+    results equal the upload form on the host copies the extraction returned."""
+    seq = synth.sequence(752, 480, 2, config=32)
+    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    outs, ds = [], []
+    for i in range(2):
+        k, d, _ = ex(seq[i], None, (0, 1000))
+        geom = abi.frame_struct(k, d, 752, 480, scale_factors=SCALE)
+        rng = np.random.default_rng(i)
+        fv = abi.featvec_struct(rng.integers(0, 25, len(k)))
+        D = orb.DeviceFrame(0).from_extractor(ex, geom, fv)
+        assert D.n == len(k)
+        outs.append((k, d, geom, fv))
+        ds.append(D)
+    (k1, d1, g1, fv1), (k2, d2, g2, fv2) = outs
+    m = orb.ORBmatcher(0.9, True)
+    prev = np.stack([k1["x"], k1["y"]], 1)
+    nm, m12, p = m.SearchForInitializationDevice(ds[0], ds[1], prev, 100)
+    unm, um12, up = m.SearchForInitialization(g1, g2, prev, 100)
+    assert nm == unm and nm > 0
+    np.testing.assert_array_equal(m12, um12)
+    np.testing.assert_array_equal(p, up)
+    kvalid = np.ones(len(k1), np.uint8)
+    nm, match = orb.ORBmatcher(0.7, True).SearchByBoWDevice(ds[0], kvalid, ds[1])
+    unm, umatch = orb.ORBmatcher(0.7, True).SearchByBoW(g1, fv1, kvalid, g2, fv2)
+    assert nm == unm and nm > 0
+    np.testing.assert_array_equal(match, umatch)
+
+
+def test_dframe_empty_and_errors(gpu_lib, frames):
+    L = capi.lib()
+    e = orb.DeviceFrame(0).upload(abi.frame_struct(frames[0][0][:0], frames[0][1][:0], 752, 480,
+                                                   scale_factors=SCALE), abi.featvec_struct(np.zeros(0, np.int64)))
+    F = dev(fr(frames[1]), abi.featvec_struct(np.zeros(len(frames[1][0]), np.int64)))
+    m = orb.ORBmatcher(0.9, True)
+    nm, m12, _ = m.SearchForInitializationDevice(e, F, np.zeros((0, 2), np.float32), 100)
+    assert nm == 0 and len(m12) == 0
+    nm, match = m.SearchByBoWDevice(e, np.zeros(0, np.uint8), F)
+    assert nm == 0 and (match == -1).all()
+    k = frames[0][0][:10]
+    nm, own = m.SearchByProjectionLastDevice(e, np.ones(10, np.uint8), k["x"], k["y"], k["x"], k["octave"], k["angle"],
+                                             np.ones(10, np.uint8), frames[0][1][:10], 7.0)
+    assert nm == 0 and len(own) == 0
+    # no FeatureVector: the BoW search refuses (ORB_ERR_PARAM)
+    G = dev(fr(frames[2]))
+    assert L.orbm_search_by_bow_dframe(G._h, abi.ptr(np.ones(len(frames[2][0]), np.uint8)), F._h, 0.7, 1,
+                                       abi.ptr(np.zeros(len(frames[1][0]), np.int32))) == abi.ORB_ERR_PARAM
+    # an extractor that has not extracted a single image yet
+    ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+    assert L.orbm_dframe_from_extractor(G._h, ex._h, fr(frames[2]).ref(), None) == abi.ORB_ERR_PARAM
+    # a FeatureVector naming a keypoint the frame does not have
+    bad = abi.featvec_struct(np.zeros(len(frames[2][0]) + 5, np.int64))
+    assert L.orbm_dframe_set_featvec(G._h, bad.ref()) == abi.ORB_ERR_PARAM

@@ -209,3 +209,37 @@ def test_mvimagepyramid_host_and_device_copies(gpu_lib, host_pyr):
     ref(img, (0, 1000))
     for lev, a in enumerate(ex.mvImagePyramid):
         np.testing.assert_array_equal(a, ref.level(lev), err_msg=f"toggled, level {lev}")
+
+
+@pytest.mark.parametrize("capopt", [1, 41, 400])
+def test_fast_dense_cells(gpu_lib, capopt):
+    """k_fast_cells' dense form (a cell whose pre-test candidates overflow the
+    LDS list is scored at every window pixel and NMS-walked in row-major order,
+    ORBextractor.cc:826-846 with cv::FAST's own definition): the candidate list
+    capped at capopt - 1 entries through the ORB_OPT_FAST_CAND_CAP hook (1:
+    every cell holding a candidate goes dense; 41 / 400: a mix), on textured,
+    checkerboard and uniform-noise frames, in both the ROI pre-test and the
+    fused-bitmap forms: keypoints and descriptors equal the oracle's."""
+    import torch
+    from orb_slam3_vio_fixes_amd import capi
+    chk = ((np.indices((480, 752)).sum(0) // 5) % 2 * 255).astype(np.uint8)
+    noise = np.random.default_rng(7).integers(0, 256, (480, 752), dtype=np.uint8)
+    imgs = [synth.image(752, 480, 4321), chk, noise]
+    with capi.debug_option(capi.ORB_OPT_FAST_CAND_CAP, capopt):
+        for img in imgs:
+            assert_same(img, (0, 1000))
+        with capi.debug_option(capi.ORB_OPT_PYR_PRETEST, 1):
+            ex = orb.ORBextractor(1000, 1.2, 8, 20, 7)
+            ex.set_pyramid_mode(2)
+            seq = np.stack(imgs)
+            kps, desc, n, mono, cap = ex.extract_batch_device(torch.from_numpy(seq).cuda(), (0, 1000))
+            torch.cuda.synchronize()
+        assert ex.plan_info(752, 480)["pretest"] == 1
+        ref = pair()[1]
+        for f in range(len(seq)):
+            rk, rd, rm = ref(seq[f], (0, 1000))
+            ni = int(n[f])
+            assert (ni, int(mono[f])) == (len(rk), rm)
+            kb = orb.keypoints_from_device(kps[f, :ni])
+            assert np.array_equal(kb.view(np.uint8), rk.view(np.uint8)), f"frame {f}: keypoints differ"
+            assert np.array_equal(desc[f, :ni].cpu().numpy(), rd), f"frame {f}: descriptors differ"

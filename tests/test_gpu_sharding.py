@@ -75,7 +75,12 @@ def test_bench_gpus_2_launches_its_own_ranks(tmp_path):
                        + common, cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2
+    assert line["n_gpus"] == 2 and line["world_size"] == 2 and line["backend"] == "gloo"
+    # every rank checked the first frames / pairs of its last timed step
+    # against the oracle on its host; rank 0's line carries the summed counts
+    par = line["parity"]
+    assert par["ranks"] == 2 and par["frames_checked"] == 2 * min(4, B + 1) and par["pairs_checked"] > 0
+    assert par["frames_mismatched"] == 0 and par["pairs_mismatched"] == 0
     assert line["value"] == pytest.approx(2 * B * line["steps"] / (line["ms_per_step"] * line["steps"] * 1e-3))
     _run([sys.executable, "bench.py", "--batch", str(2 * B), "--dump", str(tmp_path / "one")] + common, env)
     one = np.load(tmp_path / "one" / "rank0.npz")
