@@ -454,9 +454,15 @@ def cpu_baseline_matchers(d, blk, reps=200):
     cpu = run_latency(lib_path, "orbo", d, reps)
     blk["cpu_1thread"] = cpu
     blk["speedup_vs_1thread"] = {k: cpu[k]["median_us"] / blk["gpu"][k]["median_us"] for k in MATCHER_SEARCHES}
-    blk["parity"] = {k: bool(np.array_equal(np.fromfile(Path(d) / f"orbm_{MATCHER_OUT[k]}.bin", np.int32),
-                                            np.fromfile(Path(d) / f"orbo_{MATCHER_OUT[k]}.bin", np.int32)))
-                     for k in MATCHER_SEARCHES}
+    same = lambda a, b: bool(np.array_equal(np.fromfile(Path(d) / a, np.int32), np.fromfile(Path(d) / b, np.int32)))
+    blk["parity"] = {k: same(f"orbm_{MATCHER_OUT[k]}.bin", f"orbo_{MATCHER_OUT[k]}.bin") for k in MATCHER_SEARCHES}
+    # the dframe forms (frames resident in HBM: the Tracking thread's frame as
+    # the extraction leaves it, the keyframe since its creation)
+    if all(f"{k}_dframe" in blk["gpu"] for k in MATCHER_SEARCHES):
+        blk["speedup_vs_1thread_dframe"] = {k: cpu[k]["median_us"] / blk["gpu"][f"{k}_dframe"]["median_us"]
+                                            for k in MATCHER_SEARCHES}
+        blk["parity_dframe"] = {k: same(f"orbm_{MATCHER_OUT[k]}_dframe.bin", f"orbo_{MATCHER_OUT[k]}.bin")
+                                for k in MATCHER_SEARCHES}
     blk["cpu_flags"] = flags
 
 

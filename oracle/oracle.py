@@ -16,11 +16,15 @@ import numpy as np
 from orb_slam3_vio_fixes_amd import abi
 
 HERE = Path(__file__).resolve().parent
-LIB = HERE / "liborb_oracle.so"
+# ORB_ORACLE_LIB: another build of the checker (tools/sanitize_cpu_suite.sh
+# points it at an ASan/UBSan build); the default is built in place
+LIB = Path(os.environ.get("ORB_ORACLE_LIB") or HERE / "liborb_oracle.so")
 
 
 def build(force: bool = False) -> Path:
     src = HERE / "orb_oracle.cpp"
+    if os.environ.get("ORB_ORACLE_LIB"):
+        return LIB
     if force or not LIB.exists() or LIB.stat().st_mtime < src.stat().st_mtime:
         subprocess.run(["make", "-C", str(HERE), "-s"], check=True)
     return LIB

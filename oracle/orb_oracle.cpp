@@ -700,8 +700,10 @@ int orbo_extract(void* h, const uint8_t* img, int w, int hh, size_t step, int la
     if (mono_out) *mono_out = mono;
     if (n > cap) return ORB_ERR_CAPACITY;
     static_assert(sizeof(KP) == sizeof(orb_keypoint), "KeyPoint layout");
-    std::memcpy(kps, out.data(), sizeof(KP) * n);
-    std::memcpy(desc, d.data(), (size_t)n * 32);
+    if (n) {   // (an empty vector's data() may be null: UBSan, tests/test_sanitizers.py)
+        std::memcpy(kps, out.data(), sizeof(KP) * n);
+        std::memcpy(desc, d.data(), (size_t)n * 32);
+    }
     return 0;
 }
 

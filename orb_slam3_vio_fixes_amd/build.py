@@ -14,7 +14,7 @@ PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
 LIB = PKG / "liborb_mi355x.so"
 SOURCES = ["extractor.hip", "matcher.hip", "stereo.hip", "kfdb.hip", "vocab.cpp"]
-DEPS = SOURCES + ["common.h", "orb_math.h", "plan.h", "brief_pattern.inc"]
+DEPS = SOURCES + ["common.h", "orb_math.h", "plan.h", "brief_pattern.inc", "host_gather.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
          "-Wno-unused-result"]

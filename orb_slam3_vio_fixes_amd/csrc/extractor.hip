@@ -21,6 +21,7 @@
 #include "../../include/orb_mi355x.h"
 #include "common.h"
 #include "orb_math.h"
+#include "host_gather.h"
 
 #include <algorithm>
 #include <array>
@@ -4276,31 +4277,7 @@ int orbx_extract_batch(orbx_handle* h, int nframes, const uint8_t* const* imgs, 
     uint8_t* pin = (uint8_t*)h->hb_pin;
     // one upload: the frames gathered into pinned memory at a common pitch (a
     // few host threads for larger batches: the gather is the host-side cost)
-    auto gather = [&](int f0, int f1) {
-        for (int f = f0; f < f1; ++f) {
-            const size_t st = steps ? steps[f] : (size_t)w;
-            for (int y = 0; y < hh; ++y) std::memcpy(pin + f * fbytes + y * pitch, imgs[f] + y * st, w);
-        }
-    };
-    const int nth = std::min(8, nframes / 16);              // >= 16 frames per thread
-    {
-        // frames [done, nframes) are left for this thread: every worker that
-        // could not be started (std::system_error must not cross the C ABI)
-        std::vector<std::thread> th;
-        int done = 0;
-        if (nth > 1) {
-            try {
-                for (int t = 0; t < nth - 1; ++t) {
-                    const int a0 = (int)((long long)nframes * t / nth), a1 = (int)((long long)nframes * (t + 1) / nth);
-                    th.emplace_back(gather, a0, a1);
-                    done = a1;
-                }
-            } catch (...) {
-            }
-        }
-        gather(done, nframes);
-        for (auto& x : th) x.join();
-    }
+    (void)gather_frames(pin, pitch, fbytes, imgs, steps, w, hh, nframes);
     ORB_CHECK(hipMemcpyAsync(dev, pin, in_b, hipMemcpyHostToDevice, 0));
     orb_keypoint* d_kps = (orb_keypoint*)(dev + o_kp);
     uint8_t* d_desc = dev + o_de;

@@ -4899,7 +4899,7 @@ static DfScratch* df_scratch(int dev, size_t nmatch) {
         S->dev = dev;
     }
     if (!S->ticket && hipMalloc((void**)&S->ticket, 256) != hipSuccess) { S->ticket = nullptr; return nullptr; }
-    if (nmatch > S->match_cap) {
+    if (!S->match || nmatch > S->match_cap) {
         if (S->match) (void)hipFree(S->match);
         S->match = nullptr;
         S->match_cap = 0;

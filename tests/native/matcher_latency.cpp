@@ -15,6 +15,10 @@
 //   SearchByProjection(F, LastFrame, th 7, motion model)   Tracking.cc:2886-2894, ORBmatcher.cc:1676-1887
 //   SearchByProjection(F, local map points, th 3)          Tracking.cc:3413, ORBmatcher.cc:43-221
 //   SearchByBoW(KF, F, 0.7, checkOri)                      Tracking.cc:2730, ORBmatcher.cc:223-425
+// With the product (<prefix> orbm) each search is also timed in its dframe form
+// (orbm_*_dframe: the frames resident in HBM -- the current frame as
+// orbx_extract leaves it, the keyframe since its creation -- so a call moves
+// only its per-call inputs and result), as <search>_dframe.
 // Inputs are raw arrays written by bench.py (host_api_matchers) into <input
 // dir>; every call starts from the same in/out arrays.  Prints one JSON line
 // of per-call times (median and mean, microseconds) and writes each search's
@@ -138,6 +142,20 @@ int main(int argc, char** argv)
     };
     const orbm_frame F1 = frame(k1, d1, n1), F2 = frame(k2, d2, n2);
     std::string json = "{";
+    // the dframe forms (product only)
+    const bool dfm = pre == "orbm";
+    typedef orbm_dframe* (*DfCreate)(int);
+    typedef int (*DfUpload)(orbm_dframe*, const orbm_frame*, const orbm_featvec*);
+    DfCreate df_create = dfm ? (DfCreate)sym(lib, pre, "_dframe_create") : nullptr;
+    DfUpload df_upload = dfm ? (DfUpload)sym(lib, pre, "_dframe_upload") : nullptr;
+    orbm_dframe *D1 = nullptr, *D2 = nullptr;
+    if (dfm) {
+        D1 = df_create(0);
+        D2 = df_create(0);
+        if (!D1 || !D2) { std::fprintf(stderr, "orbm_dframe_create failed\n"); return 3; }
+        check(df_upload(D1, &F1, nullptr), "orbm_dframe_upload");
+        check(df_upload(D2, &F2, nullptr), "orbm_dframe_upload");
+    }
     // the product's last fused projection search: rounds, rescans, phase clocks
     typedef int (*StatFn)(int32_t*);
     StatFn statfn = (StatFn)dlsym(lib, "orbm_debug_proj_stats");
@@ -177,6 +195,20 @@ int main(int argc, char** argv)
         stats("search_for_initialization");
         m12.push_back(nm);
         save(pre + "_sfi.bin", m12.data(), m12.size());
+        if (dfm) {
+            typedef int (*DFn)(const orbm_dframe*, const orbm_dframe*, float*, int, float, int, int32_t*);
+            DFn dfn = (DFn)sym(lib, pre, "_search_for_initialization_dframe");
+            std::vector<int32_t> dm12(std::max(1, n1));
+            const Stat sd = timed(reps, [&] {
+                std::memcpy(prev.data(), prev0.data(), prev0.size() * sizeof(float));
+                nm = dfn(D1, D2, prev.data(), 100, 0.9f, 1, dm12.data());
+                check(nm, "SearchForInitialization(dframe)");
+            });
+            put("search_for_initialization_dframe", sd);
+            dm12.resize(n1);
+            dm12.push_back(nm);
+            save(pre + "_sfi_dframe.bin", dm12.data(), dm12.size());
+        }
     }
     // SearchByProjection(F, LastFrame): the last frame's points projected into F2
     {
@@ -204,6 +236,23 @@ int main(int argc, char** argv)
         owner.resize(n2);
         owner.push_back(nm);
         save(pre + "_last.bin", owner.data(), owner.size());
+        if (dfm) {
+            typedef int (*DFn)(const orbm_dframe*, int, const uint8_t*, const float*, const float*, const float*,
+                               const int32_t*, const float*, const uint8_t*, const uint8_t*, float, int, int,
+                               int32_t*, const uint8_t*);
+            DFn dfn = (DFn)sym(lib, pre, "_search_by_projection_last_dframe");
+            std::vector<int32_t> down(std::max(1, n2));
+            const Stat sd = timed(reps, [&] {
+                std::fill(down.begin(), down.end(), -1);
+                nm = dfn(D2, nl, valid.data(), u.data(), v.data(), ur.data(), oct.data(), ang.data(), hobs.data(),
+                         desc.data(), 7.0f, 0, 1, down.data(), blocked.data());
+                check(nm, "SearchByProjection(dframe, LastFrame)");
+            });
+            put("search_by_projection_last_dframe", sd);
+            down.resize(n2);
+            down.push_back(nm);
+            save(pre + "_last_dframe.bin", down.data(), down.size());
+        }
     }
     // SearchByProjection(F, local map points) (TrackLocalMap)
     {
@@ -230,6 +279,21 @@ int main(int argc, char** argv)
         owner.resize(n2);
         owner.push_back(nm);
         save(pre + "_mps.bin", owner.data(), owner.size());
+        if (dfm) {
+            typedef int (*DFn)(const orbm_dframe*, const orbm_mappoints*, float, int, float, float, int32_t*,
+                               const uint8_t*);
+            DFn dfn = (DFn)sym(lib, pre, "_search_by_projection_mps_dframe");
+            std::vector<int32_t> down(std::max(1, n2));
+            const Stat sd = timed(reps, [&] {
+                std::fill(down.begin(), down.end(), -1);
+                nm = dfn(D2, &mp, 3.0f, 0, 50.0f, 0.8f, down.data(), blocked.data());
+                check(nm, "SearchByProjection(dframe, MapPoints)");
+            });
+            put("search_by_projection_mps_dframe", sd);
+            down.resize(n2);
+            down.push_back(nm);
+            save(pre + "_mps_dframe.bin", down.data(), down.size());
+        }
     }
     // SearchByBoW(KF, F): the keyframe = frame 1, the frame = frame 2
     {
@@ -253,6 +317,21 @@ int main(int argc, char** argv)
         match.resize(n2);
         match.push_back(nm);
         save(pre + "_bow.bin", match.data(), match.size());
+        if (dfm) {
+            typedef int (*DFn)(const orbm_dframe*, const uint8_t*, const orbm_dframe*, float, int, int32_t*);
+            DFn dfn = (DFn)sym(lib, pre, "_search_by_bow_dframe");
+            check(df_upload(D1, &F1, &fv1), "orbm_dframe_upload");      // the keyframe with its FeatureVector
+            check(df_upload(D2, &F2, &fv2), "orbm_dframe_upload");      // the frame after Frame::ComputeBoW
+            std::vector<int32_t> dmatch(std::max(1, n2));
+            const Stat sd = timed(reps, [&] {
+                nm = dfn(D1, valid.data(), D2, 0.7f, 1, dmatch.data());
+                check(nm, "SearchByBoW(dframe)");
+            });
+            put("search_by_bow_dframe", sd);
+            dmatch.resize(n2);
+            dmatch.push_back(nm);
+            save(pre + "_bow_dframe.bin", dmatch.data(), dmatch.size());
+        }
     }
     json += extra + "}";
     std::printf("%s\n", json.c_str());
