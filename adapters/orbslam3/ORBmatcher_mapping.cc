@@ -49,6 +49,7 @@
  * against the reference's unmodified headers, like ORBmatcher_searches.cc.
  */
 #include "ORBmatcher_adapter.h"
+#include "ORBmatcher_tails.h"
 
 #include <set>
 #include <tuple>
@@ -62,17 +63,10 @@ namespace ORB_SLAM3
 
 using namespace mi355x_adapter;
 
+using mi355x_tails::PointRows;
+
 namespace
 {
-// The device search's per-point inputs (orbm_fuse / orbm_fuse_sim3 /
-// orbm_search_by_projection_sim3 / orbm_search_by_projection_kf).
-struct PointRows {
-    vector<uint8_t> valid, desc;
-    vector<float> u, v, ur;
-    vector<int32_t> level;
-    explicit PointRows(size_t n) : valid(n, 0), desc(n * 32, 0), u(n, 0.f), v(n, 0.f), ur(n, 0.f), level(n, 0) {}
-};
-
 // ---- SearchByProjection(KeyFrame*, Sim3, ...) :446-486 / :558-604 and
 // Fuse(KeyFrame*, Sim3, ...) :1372-1411: the candidate geometry of one point.
 // project_with_camera: pKF->mpCamera->project (:463, :1385); otherwise the
@@ -138,8 +132,7 @@ int sim3_projection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& 
     }
     // slots: -1 = vpMatched[idx] NULL, -2 = occupied; the device writes the
     // point index into the slots it fills, in the reference's point order
-    vector<int32_t> matched(vpMatched.size());
-    for (size_t k = 0; k < vpMatched.size(); ++k) matched[k] = vpMatched[k] ? -2 : -1;
+    vector<int32_t> matched = mi355x_tails::slot_states(vpMatched);
     vector<cv::KeyPoint> store;
     orbm_frame kf = left_grid_view(*pKF, pKF->NLeft, store);
     check(kf.n == (int32_t)vpMatched.size() ? 0 : ORB_ERR_PARAM, "SearchByProjection(KF, Sim3): vpMatched size");
@@ -147,11 +140,7 @@ int sim3_projection(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& 
                                                   pr.level.data(), pr.desc.data(), (float)th, ratioHamming,
                                                   matched.data());
     check(nm, "SearchByProjection(KF, Sim3)");
-    for (size_t k = 0; k < vpMatched.size(); ++k)
-        if (matched[k] >= 0) {
-            vpMatched[k] = vpPoints[matched[k]];
-            if (vpMatchedKF) (*vpMatchedKF)[k] = (*vpPointsKFs)[matched[k]];
-        }
+    mi355x_tails::slot_writeback(matched, vpPoints, vpPointsKFs, vpMatched, vpMatchedKF);
     return nm;
 }
 
@@ -281,16 +270,14 @@ int ORBmatcher::SearchByProjection(Frame& CurrentFrame, KeyFrame* pKF, const set
                                                : pKF->mvKeysRight[i - (size_t)pKF->NLeft].angle;
     }
     // -1: mvpMapPoints[i2] NULL (a candidate), -2: occupied (:1949-1950)
-    vector<int32_t> owner(CurrentFrame.N);
-    for (int i = 0; i < CurrentFrame.N; ++i) owner[i] = CurrentFrame.mvpMapPoints[i] ? -2 : -1;
+    vector<int32_t> owner = mi355x_tails::slot_states(CurrentFrame.mvpMapPoints);
     vector<cv::KeyPoint> store;
     orbm_frame f = left_grid_view(CurrentFrame, CurrentFrame.Nleft, store);
     const int nm = orbm_search_by_projection_kf(&f, (int)n, pr.valid.data(), pr.u.data(), pr.v.data(), pr.level.data(),
                                                 kf_angle.data(), pr.desc.data(), th, ORBdist,
                                                 mbCheckOrientation ? 1 : 0, owner.data());
     check(nm, "SearchByProjection(F, KF)");
-    for (int i = 0; i < CurrentFrame.N; ++i)
-        if (owner[i] >= 0) CurrentFrame.mvpMapPoints[i] = vpMPs[owner[i]];
+    mi355x_tails::slot_writeback<MapPoint, KeyFrame*>(owner, vpMPs, nullptr, CurrentFrame.mvpMapPoints, nullptr);
     return nm;
 }
 
@@ -315,13 +302,11 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& v
     // a feature takes part iff its MapPoint is set and good (:803-808,
     // :822-827) and, for a two-camera keyframe, its index lies within
     // mvKeysUn (:799-801, :816-818)
-    auto mask = [](KeyFrame* k, const vector<MapPoint*>& mps) {
-        vector<uint8_t> m(mps.size(), 0);
-        for (size_t i = 0; i < mps.size(); ++i)
-            m[i] = mps[i] && !mps[i]->isBad() && (k->NLeft == -1 || i < k->mvKeysUn.size());
-        return m;
+    auto in_range = [](KeyFrame* k, const vector<MapPoint*>& mps) {
+        return k->NLeft == -1 ? mps.size() : k->mvKeysUn.size();
     };
-    const vector<uint8_t> valid1 = mask(pKF1, vpMapPoints1), valid2 = mask(pKF2, vpMapPoints2);
+    const vector<uint8_t> valid1 = mi355x_tails::bow_kf_mask(vpMapPoints1, in_range(pKF1, vpMapPoints1));
+    const vector<uint8_t> valid2 = mi355x_tails::bow_kf_mask(vpMapPoints2, in_range(pKF2, vpMapPoints2));
     FeatVecCSR fv1(pKF1->mFeatVec), fv2(pKF2->mFeatVec);
     vector<cv::KeyPoint> s1, s2;
     orbm_frame k1 = view(*pKF1, pKF1->NLeft, s1), k2 = view(*pKF2, pKF2->NLeft, s2);
@@ -329,8 +314,7 @@ int ORBmatcher::SearchByBoW(KeyFrame* pKF1, KeyFrame* pKF2, vector<MapPoint*>& v
     const int nm = orbm_search_by_bow_kf(&k1, &fv1.c, valid1.data(), &k2, &fv2.c, valid2.data(), mfNNratio,
                                          mbCheckOrientation ? 1 : 0, m12.data());
     check(nm, "SearchByBoW(KF, KF)");
-    for (size_t i = 0; i < m12.size(); ++i)
-        if (m12[i] >= 0) vpMatches12[i] = vpMapPoints2[m12[i]];
+    mi355x_tails::matches_writeback(m12, vpMapPoints2, vpMatches12);
     return nm;
 }
 
@@ -405,12 +389,8 @@ int ORBmatcher::SearchForTriangulation(KeyFrame* pKF1, KeyFrame* pKF2, vector<pa
                                                    m12.data());
     }
     check(nm, "SearchForTriangulation");
-    vMatchedPairs.clear();
     vMatchedPairs.reserve(nm);
-    for (size_t i = 0, iend = m12.size(); i < iend; i++) {
-        if (m12[i] < 0) continue;
-        vMatchedPairs.push_back(make_pair(i, (size_t)m12[i]));
-    }
+    mi355x_tails::triangulation_pairs(m12, vMatchedPairs);
     return nm;
 }
 
@@ -431,16 +411,8 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoin
     const int N1 = vpMapPoints1.size();
     const vector<MapPoint*> vpMapPoints2 = pKF2->GetMapPointMatches();
     const int N2 = vpMapPoints2.size();
-    vector<bool> vbAlreadyMatched1(N1, false);
-    vector<bool> vbAlreadyMatched2(N2, false);
-    for (int i = 0; i < N1; i++) {
-        MapPoint* pMP = vpMatches12[i];
-        if (pMP) {
-            vbAlreadyMatched1[i] = true;
-            int idx2 = get<0>(pMP->GetIndexInKeyFrame(pKF2));
-            if (idx2 >= 0 && idx2 < N2) vbAlreadyMatched2[idx2] = true;
-        }
-    }
+    vector<bool> vbAlreadyMatched1, vbAlreadyMatched2;
+    mi355x_tails::sim3_already_matched(vpMatches12, pKF2, N2, vbAlreadyMatched1, vbAlreadyMatched2);
     // one direction's candidate geometry (:1496-1530 and :1572-1606): both
     // project with pKF1's intrinsics, as the reference does
     auto side = [&](const vector<MapPoint*>& mps, const vector<bool>& already, const Sophus::SE3f& Tw,
@@ -485,8 +457,7 @@ int ORBmatcher::SearchBySim3(KeyFrame* pKF1, KeyFrame* pKF2, std::vector<MapPoin
                                            p2.level.data(), p2.desc.data(), th, m12.data());
     check(nFound, "SearchBySim3");
     // Check agreement (:1653-1671): the device returns the new mutual matches
-    for (int i1 = 0; i1 < N1; i1++)
-        if (m12[i1] >= 0) vpMatches12[i1] = vpMapPoints2[m12[i1]];
+    mi355x_tails::matches_writeback(m12, vpMapPoints2, vpMatches12);
     return nFound;
 }
 
@@ -522,58 +493,21 @@ int ORBmatcher::Fuse(KeyFrame* pKF, const vector<MapPoint*>& vpMapPoints, const 
                     pr.ur.data(), pr.level.data(), pr.desc.data(), th, 1, best.data(), bdist.data()),
           "Fuse");
 
-    // The replace / add decisions (:1311-1328), in index order.  A decision
-    // changes the points it touches (Replace makes one bad and recomputes the
-    // survivor's descriptor, AddObservation puts a point in pKF); a later
-    // occurrence of a touched point is snapshotted again, as the reference
-    // reads it at its turn, and searched again when its row changed.
-    set<MapPoint*> touched;
-    int nFused = 0;
-    for (size_t i = 0; i < n; ++i) {
-        MapPoint* pMP = vpMapPoints[i];
-        int bestIdx = best[i];
-        if (pMP && touched.count(pMP)) {
-            float u = 0.f, v = 0.f, ur = 0.f;
-            int level = 0;
-            const bool ok = fuse_point(pKF, pMP, Tcw, Ow, pCamera, u, v, ur, level);
-            vector<uint8_t> d(32, 0);
-            if (ok) copy_descriptor(pMP, d, 0);
-            const bool same = ok == (pr.valid[i] != 0) &&
-                              (!ok || (u == pr.u[i] && v == pr.v[i] && ur == pr.ur[i] && level == pr.level[i] &&
-                                       std::equal(d.begin(), d.end(), pr.desc.begin() + i * 32)));
-            if (!same) {
-                bestIdx = -1;
-                if (ok) {
-                    const uint8_t one = 1;
-                    int32_t b = -1, bd = 0;
-                    check(orbm_fuse(&kf, pKF->mvInvLevelSigma2.data(), 1, &one, &u, &v, &ur, &level, d.data(), th, 1,
-                                    &b, &bd),
-                          "Fuse");
-                    bestIdx = b;
-                }
-            }
-        }
-        // If there is already a MapPoint replace otherwise add new measurement
-        if (bestIdx < 0) continue;
-        bestIdx += slot0;
-        MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
-        if (pMPinKF) {
-            if (!pMPinKF->isBad()) {
-                if (pMPinKF->Observations() > pMP->Observations())
-                    pMP->Replace(pMPinKF);
-                else
-                    pMPinKF->Replace(pMP);
-                touched.insert(pMP);
-                touched.insert(pMPinKF);
-            }
-        } else {
-            pMP->AddObservation(pKF, bestIdx);
-            pKF->AddMapPoint(pMP, bestIdx);
-            touched.insert(pMP);
-        }
-        nFused++;
-    }
-    return nFused;
+    // The replace / add decisions (:1311-1328), in index order, with the
+    // re-snapshot and single-row re-search of touched points (ORBmatcher_tails.h)
+    auto row = [&](MapPoint* pMP, float& u, float& v, float& ur, int& level, uint8_t* d) {
+        if (!fuse_point(pKF, pMP, Tcw, Ow, pCamera, u, v, ur, level)) return false;
+        const cv::Mat md = pMP->GetDescriptor();
+        std::copy(md.data, md.data + 32, d);
+        return true;
+    };
+    auto search1 = [&](float u, float v, float ur, int level, const uint8_t* d) {
+        const uint8_t one = 1;
+        int32_t b = -1, bd = 0;
+        check(orbm_fuse(&kf, pKF->mvInvLevelSigma2.data(), 1, &one, &u, &v, &ur, &level, d, th, 1, &b, &bd), "Fuse");
+        return (int)b;
+    };
+    return mi355x_tails::fuse_decisions(pKF, vpMapPoints, slot0, pr, best, row, search1);
 }
 
 int ORBmatcher::Fuse(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>& vpPoints, float th,
@@ -602,24 +536,8 @@ int ORBmatcher::Fuse(KeyFrame* pKF, Sophus::Sim3f& Scw, const vector<MapPoint*>&
     check(orbm_fuse_sim3(&kf, (int)n, pr.valid.data(), pr.u.data(), pr.v.data(), pr.level.data(), pr.desc.data(), th,
                          best.data(), bdist.data()),
           "Fuse(KF, Sim3)");
-    // The replace / add decisions (:1439-1449), in index order.  No decision
-    // here changes another point's inputs (no Replace; the already-found set is
-    // fixed), only the keyframe's slots, which are read at each decision.
-    int nFused = 0;
-    for (size_t i = 0; i < n; ++i) {
-        const int bestIdx = best[i];
-        if (bestIdx < 0) continue;
-        MapPoint* pMP = vpPoints[i];
-        MapPoint* pMPinKF = pKF->GetMapPoint(bestIdx);
-        if (pMPinKF) {
-            if (!pMPinKF->isBad()) vpReplacePoint[i] = pMPinKF;
-        } else {
-            pMP->AddObservation(pKF, bestIdx);
-            pKF->AddMapPoint(pMP, bestIdx);
-        }
-        nFused++;
-    }
-    return nFused;
+    // The replace / add decisions (:1439-1449), in index order (ORBmatcher_tails.h)
+    return mi355x_tails::fuse_sim3_decisions(pKF, vpPoints, best, vpReplacePoint);
 }
 
 }  // namespace ORB_SLAM3
