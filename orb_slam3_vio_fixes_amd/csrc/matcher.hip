@@ -1160,6 +1160,11 @@ struct BowArgs {
     int seq = 0;
     int reset_after = 0;              // ... and leaves match / nmatches / fin_ticket as it found them
                                       // (-1 / 0 / 0: persistent scratch of the dframe form)
+    int single_nodes = -1;            // >= 0: one pair whose offsets all start at 0 (kp_off, node_off,
+                                      // idx_off), with this many KF nodes: the kernels skip those loads
+    unsigned* tstart = nullptr;       // dframe form: the first block's start (s_memrealtime, 100 MHz;
+                                      // 0xffffffff before the launch, reset by the last block), and
+                                      // host_out[f_n + 1 ..] = node phase, final phase (10 ns ticks)
 };
 
 // One wave per (pair, vocabulary node) the two FeatureVectors share: the
@@ -1219,11 +1224,12 @@ template <bool kLds, bool kFish>
 __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
                                          const uint4* s_fd, const int* s_fi, uint4* s_q) {
     const int lane = lane_id();
-    const long long kpo = a.kp_off[pr];
+    const bool one = a.single_nodes >= 0;            // one pair at offset 0: no offset loads in the chain
+    const long long kpo = one ? 0 : a.kp_off[pr];
     const uint8_t* KD = a.kf_desc + kpo * 32;
     const uint8_t* KV = a.kf_valid + kpo;
-    const int* ko = a.kf_off + a.node_off[pr] + pr;
-    const uint32_t* ki = a.kf_idx + a.idx_off[pr];
+    const int* ko = a.kf_off + (one ? 0 : a.node_off[pr] + pr);
+    const uint32_t* ki = a.kf_idx + (one ? 0 : a.idx_off[pr]);
     const int nf = fe - fb;
     const int nch = (nf + kWave - 1) / kWave;
     int32_t* match = a.match + (long long)pr * a.f_n;
@@ -1399,15 +1405,17 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         for (int i = threadIdx.x; i <= a.f_nnodes; i += blockDim.x) s_foff[i] = a.f_off[i];
     }
     __syncthreads();
+    if (a.tstart && threadIdx.x == 0) atomicMax(a.tstart + 1, (unsigned)__builtin_amdgcn_s_memrealtime());
     const uint32_t* fnode = lds_f ? s_fnode : a.f_node;
     const int* foff = lds_f ? s_foff : a.f_off;
-    const long long total = a.node_off[a.npairs];
+    const bool one = a.single_nodes >= 0;
+    const long long total = one ? a.single_nodes : a.node_off[a.npairs];
     const long long nw = (long long)nblocks * 4, w = (long long)bid * 4 + wave_id();
     const long long per = (total + nw - 1) / nw;
     const long long g0 = w * per, g1 = min(total, g0 + per);
     if (g0 >= g1) return;
-    int pr;
-    {
+    int pr = 0;
+    if (!one) {
         int lo = 0, hi = a.npairs;                       // last pr with node_off[pr] <= g0
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -1416,9 +1424,10 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         }
         pr = lo;
     }
-    long long pr_end = a.node_off[pr + 1];
+    long long pr_end = one ? total : a.node_off[pr + 1];
     for (long long g = g0; g < g1; ++g) {
         while (g >= pr_end) { ++pr; pr_end = a.node_off[pr + 1]; }
+        const long long pr_base = one ? 0 : a.node_off[pr];
         const uint32_t na = a.kf_node[g];
         int fl = 0, fh = a.f_nnodes;                     // lower_bound of na in F's node ids
         while (fl < fh) {
@@ -1429,9 +1438,10 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         if (fl >= a.f_nnodes || fnode[fl] != na) continue;
         const int fb = foff[fl], fe = foff[fl + 1];
         if (fe - fb > kBowRegChunks * kWave) continue;  // a large-node block's
-        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, s_q);
-        else bow_node<false, false>(a, pr, (int)(g - a.node_off[pr]), fb, fe, nullptr, nullptr, s_q);
+        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q);
+        else bow_node<false, false>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q);
     }
+    if (a.tstart && lane_id() == 0) atomicMax(a.tstart + 2, (unsigned)__builtin_amdgcn_s_memrealtime());
 }
 
 // Large frame nodes: block = kBowBigPairs consecutive keyframes; for each frame
@@ -1444,7 +1454,10 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
     const int slot = bid % slots;
     const int pr = (bid / slots) * kBowBigPairs + wave_id();
     long long k0 = 0, k1 = 0;
-    if (pr < a.npairs) { k0 = a.node_off[pr]; k1 = a.node_off[pr + 1]; }
+    if (pr < a.npairs) {
+        if (a.single_nodes >= 0) { k0 = 0; k1 = a.single_nodes; }
+        else { k0 = a.node_off[pr]; k1 = a.node_off[pr + 1]; }
+    }
     int nbig = 0;
     for (int fl = 0; fl < a.f_nnodes; ++fl) {
         const int fb = a.f_off[fl], fe = a.f_off[fl + 1];
@@ -1521,13 +1534,25 @@ static_assert(kBowBigCap >= 41, "s_fi holds the fused final's histogram, drop co
 __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_slots) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
+    if (a.tstart && threadIdx.x == 0) atomicMin(a.tstart, (unsigned)__builtin_amdgcn_s_memrealtime());
     if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, big_slots, s_fd, s_fi);
     else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 2 * kWave);
     if (a.fin_ticket) {
         // a single pair: the last block to finish runs the rotation filter on
         // every block's matches (the match rows, nmatches and the LDS are free)
         if (!last_arriver(a.fin_ticket, s_fi + 40)) return;
+        const unsigned t_arrive = (unsigned)__builtin_amdgcn_s_memrealtime();
         bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd));
+        if (a.tstart && threadIdx.x == 0) {
+            const unsigned t0 = *a.tstart;
+            a.host_out[a.f_n + 1] = (int)(t_arrive - t0);
+            a.host_out[a.f_n + 2] = (int)((unsigned)__builtin_amdgcn_s_memrealtime() - t_arrive);
+            a.host_out[a.f_n + 3] = (int)(a.tstart[1] - t0);    // the last block past its table load
+            a.host_out[a.f_n + 4] = (int)(a.tstart[2] - t0);    // the last wave past its nodes
+            a.tstart[0] = 0xffffffffu;
+            a.tstart[1] = 0u;
+            a.tstart[2] = 0u;
+        }
         if (a.host_out) {
             __syncthreads();
             for (int i = threadIdx.x; i < a.f_n; i += blockDim.x) {
@@ -1559,7 +1584,7 @@ __device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p,
     int32_t* match = a.match + (long long)pr * a.f_n;
     int& drop = *drop_p;
     if (a.check_ori) {
-        const orb_keypoint* KK = a.kf_kps + a.kp_off[pr];
+        const orb_keypoint* KK = a.kf_kps + (a.single_nodes >= 0 ? 0 : a.kp_off[pr]);
         if (tid < 32) hist[tid] = 0;
         if (tid == 0) drop = 0;
         __syncthreads();
@@ -3259,6 +3284,25 @@ __device__ void lds_grid_build(const orb_keypoint* kps, int n, const GridParams&
     __syncthreads();
 }
 
+// A frame's grid built once (k_grid_prebuild, the dframe searches): the
+// cell starts and entries of lds_grid_build, kGridInts + n ints contiguous,
+// copied into the block's LDS instead of rebuilt.
+__device__ void lds_grid_load(const int* __restrict__ pg, int n, int* gcs) {
+    const int tot = kGridInts + max(1, n);
+    for (int c = threadIdx.x; c < tot; c += blockDim.x) gcs[c] = pg[c];
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kFusedThreads) void k_grid_prebuild(const orb_keypoint* kps, int n, GridParams g,
+                                                                  int oct, int* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) int gl[];
+    int* gcs = gl;
+    uint32_t* gent = (uint32_t*)(gcs + kGridInts);
+    lds_grid_build(kps, n, g, oct, gcs, gent, (int*)(gent + max(1, n)));
+    const int tot = kGridInts + max(1, n);
+    for (int c = threadIdx.x; c < tot; c += blockDim.x) out[c] = gl[c];
+}
+
 // A window's cell columns on the lanes: lane c < ncol holds column cr.x0 + c's
 // run [start, start + cnt) of gent and its exclusive offset in the window's
 // list; total = the list length (wave-uniform).
@@ -3409,7 +3453,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
                                                                const int32_t* __restrict__ owner_in,
                                                                int32_t* __restrict__ out, int lds_lists,
                                                                int use_grid, int part, int* done, int seq,
-                                                               Mirror mir) {
+                                                               Mirror mir, const int* __restrict__ pgrid) {
     extern __shared__ __attribute__((aligned(16))) int fl[];
     const int n = a.n, nq = a.nq, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -3419,7 +3463,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     if (use_grid) {
         gcs = fl + proj_fused_lds(n, nq, lds_lists != 0) / 4;
         gent = (uint32_t*)(gcs + kGridInts);
-        lds_grid_build(a.kps, n, a.g, -1, gcs, gent, (int*)(gent + max(1, n)));
+        if (pgrid) lds_grid_load(pgrid, n, gcs);
+        else lds_grid_build(a.kps, n, a.g, -1, gcs, gent, (int*)(gent + max(1, n)));
     }
     const unsigned long long tg = __builtin_amdgcn_s_memtime();
     unsigned long long tsel = 0;
@@ -4557,7 +4602,8 @@ __device__ __forceinline__ bool sfi_accept(int best, int best2, float ratio) {
 __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uint32_t* __restrict__ lists,
                                                               int* __restrict__ cnt, unsigned* __restrict__ ticket,
                                                               int32_t* __restrict__ out, int use_grid, int part,
-                                                              int* done, int seq, Mirror mir) {
+                                                              int* done, int seq, Mirror mir,
+                                                              const int* __restrict__ pgrid) {
     extern __shared__ __attribute__((aligned(16))) int sl[];
     const int n1 = a.n1, n2 = a.n2, tid = threadIdx.x, lane = lane_id(), wv = wave_id();
     const unsigned long long t0 = __builtin_amdgcn_s_memtime(), rt0 = __builtin_amdgcn_s_memrealtime();
@@ -4567,7 +4613,8 @@ __global__ __launch_bounds__(kFusedThreads) void k_sfi_fused(SfiFusedArgs a, uin
     if (use_grid) {
         gcs = sl + sfi_fused_lds(n1, n2) / 4;
         gent = (uint32_t*)(gcs + kGridInts);
-        lds_grid_build(a.k2, n2, a.g, 0, gcs, gent, (int*)(gent + max(1, n2)));
+        if (pgrid) lds_grid_load(pgrid, n2, gcs);
+        else lds_grid_build(a.k2, n2, a.g, 0, gcs, gent, (int*)(gent + max(1, n2)));
     }
     const unsigned long long tg = __builtin_amdgcn_s_memtime();
     unsigned long long tsel = 0;
@@ -4806,8 +4853,13 @@ struct orbm_dframe {
     uint32_t* fv_idx = nullptr;
     // k_bow's single-pair offsets: kp_off {0, n}, node_off {0, fv_nnodes}, idx_off {0}
     long long* offs = nullptr;
+    // the frame's grid prebuilt for the fused searches (k_grid_prebuild):
+    // [0] every keypoint, [1] octave 0 (SearchForInitialization's F2); null
+    // when the frame exceeds the fused forms' kFusedMaxN keypoints
+    int* grid[2] = {nullptr, nullptr};
+    int grid_cap[2] = {0, 0};
     ~orbm_dframe() {
-        void* ps[] = {kps, desc, ur, scale, fv_node, fv_off, fv_idx, offs};
+        void* ps[] = {kps, desc, ur, scale, fv_node, fv_off, fv_idx, offs, grid[0], grid[1]};
         for (void* q : ps)
             if (q) (void)hipFree(q);
     }
@@ -4818,13 +4870,34 @@ namespace orbmi {
 // grows a device array to at least cnt elements (contents not kept)
 template <class T> static int grow_dev(T*& p, int& cap, size_t cnt) {
     cnt = std::max<size_t>(1, cnt);
-    if ((size_t)cap >= cnt) return ORB_OK;
+    if (p && (size_t)cap >= cnt) return ORB_OK;
     if (p) (void)hipFree(p);
     p = nullptr;
     cap = 0;
     if (hipMalloc((void**)&p, cnt * sizeof(T)) != hipSuccess) return ORB_ERR_DEVICE;
     cap = (int)cnt;
     return ORB_OK;
+}
+
+// the two prebuilt grids of a dframe whose keypoints are in place (stream 0,
+// ordered before every later search)
+static int df_grids(orbm_dframe* df) {
+    if (df->n > kFusedMaxN) {                      // (the fused forms refuse such a frame)
+        for (int k = 0; k < 2; ++k) {
+            if (df->grid[k]) (void)hipFree(df->grid[k]);
+            df->grid[k] = nullptr;
+            df->grid_cap[k] = 0;
+        }
+        return ORB_OK;
+    }
+    for (int k = 0; k < 2; ++k) {
+        int rc;
+        if ((rc = grow_dev(df->grid[k], df->grid_cap[k], (size_t)kGridInts + std::max(1, df->n)))) return rc;
+        if (!df->grid[k]) return ORB_ERR_DEVICE;
+        KLAUNCH(k_grid_prebuild, dim3(1), dim3(kFusedThreads), lds_grid_bytes(df->n), 0, df->kps, df->n, df->g,
+                k ? 0 : -1, df->grid[k]);
+    }
+    return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
 
 static int df_offsets(orbm_dframe* df) {
@@ -4909,7 +4982,9 @@ static DfScratch* df_scratch(int dev, size_t nmatch) {
         S->dirty = true;
     }
     if (S->dirty) {
-        if (hipMemset(S->ticket, 0, 256) != hipSuccess || hipMemset(S->match, 0xff, S->match_cap * 4) != hipSuccess ||
+        if (hipMemset(S->ticket, 0, 256) != hipSuccess || hipMemset(S->ticket + 1, 0xff, 4) != hipSuccess ||
+            hipMemset(S->ticket + 2, 0, 8) != hipSuccess ||
+            hipMemset(S->match, 0xff, S->match_cap * 4) != hipSuccess ||
             hipMemset(S->match + S->match_cap, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
             return nullptr;
         S->dirty = false;
@@ -4987,7 +5062,7 @@ static int run_proj_dframe(ProjArgs& a, const orbm_dframe* f, ZRun& z, const int
     const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
     S->dirty = true;                   // until the kernel has reset the ticket
     KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists, cnt, S->ticket, owner_m,
-            out.d, lds_lists, use_grid, 0, out.flag, out.seq, z.mirror());
+            out.d, lds_lists, use_grid, 0, out.flag, out.seq, z.mirror(), use_grid ? f->grid[0] : nullptr);
     ORB_CHECK(hipGetLastError());
     std::vector<int32_t> res((size_t)n + 13);
     ORB_CHECK(out.fetch(res.data(), res.size()));
@@ -5089,12 +5164,12 @@ int orbm_search_for_initialization(const orbm_frame* f1, const orbm_frame* f2, f
         const size_t lds = sfi_fused_lds(n1, n2) + (use_grid ? gb : 0);
         if (sform == 3) {      // phase 1, then phase 2 as a one-block launch (no ticket)
             KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
-                    use_grid, 1, (int*)nullptr, 0, Mirror{});
+                    use_grid, 1, (int*)nullptr, 0, Mirror{}, (const int*)nullptr);
             KLAUNCH(k_sfi_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d, use_grid, 2,
-                    out.flag, out.seq, Mirror{});
+                    out.flag, out.seq, Mirror{}, (const int*)nullptr);
         } else {
             KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists.p, cnt.p, ticket.p, out.d,
-                    use_grid, 0, out.flag, out.seq, Mirror{});
+                    use_grid, 0, out.flag, out.seq, Mirror{}, (const int*)nullptr);
         }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)13 + 3 * n1);
@@ -5241,6 +5316,7 @@ static int bow_host(const orbm_frame* kf, const orbm_featvec* kfv, const uint8_t
     a.f_kps = fk.p; a.f_desc = fd.p; a.f_n = f->n; a.f_node = fn.p; a.f_off = fo.p; a.f_idx = fi.p;
     a.f_nnodes = ffv->nnodes; a.ratio = nnratio; a.check_ori = check_ori; a.match = m.p; a.nmatches = m.p + f->n;
     a.f_nleft = f_nleft; a.fin_ticket = ticket.p;
+    a.single_nodes = kfv->nnodes;      // (kp_off, node_off, idx_off above all start at 0)
     if (out.h) { a.host_out = out.d; a.done = out.flag; a.seq = out.seq; }
     if ((rc = launch_bow(a, 1, 0, bow_big_nodes(ffv), kfv->nnodes))) return rc;
     ORB_CHECK(out.fetch(init.data(), init.size()));
@@ -5487,12 +5563,12 @@ static int run_proj(ProjArgs& a, const orbm_frame* f, DevFrame& df, int32_t* own
         const int nblk = std::max(1, (a.nq + kFusedThreads / kWave - 1) / (kFusedThreads / kWave));
         if (form == 5) {       // phase 1, then phase 2 as a one-block launch (no ticket)
             KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
-                    ticket.p, own.p, out.d, lds_lists, use_grid, 1, (int*)nullptr, 0, Mirror{});
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 1, (int*)nullptr, 0, Mirror{}, (const int*)nullptr);
             KLAUNCH(k_proj_fused, dim3(1), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p, ticket.p,
-                    own.p, out.d, lds_lists, use_grid, 2, out.flag, out.seq, Mirror{});
+                    own.p, out.d, lds_lists, use_grid, 2, out.flag, out.seq, Mirror{}, (const int*)nullptr);
         } else {
             KLAUNCH(k_proj_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, proj_bound(a), lists.p, cnt.p,
-                    ticket.p, own.p, out.d, lds_lists, use_grid, 0, out.flag, out.seq, Mirror{});
+                    ticket.p, own.p, out.d, lds_lists, use_grid, 0, out.flag, out.seq, Mirror{}, (const int*)nullptr);
         }
         ORB_CHECK(hipGetLastError());
         std::vector<int32_t> res((size_t)f->n + 13);
@@ -6107,7 +6183,7 @@ int orbm_dframe_upload(orbm_dframe* df, const orbm_frame* f, const orbm_featvec*
                  hipMemcpy(df->desc, f->desc, (size_t)f->n * 32, hipMemcpyHostToDevice) != hipSuccess))
         return ORB_ERR_DEVICE;
     df->fv_nnodes = -1;
-    if ((rc = df_geometry(df, f, f->n)) || (rc = df_offsets(df))) return rc;
+    if ((rc = df_geometry(df, f, f->n)) || (rc = df_offsets(df)) || (rc = df_grids(df))) return rc;
     return df_featvec(df, fv);
 }
 
@@ -6127,7 +6203,7 @@ int orbm_dframe_from_extractor(orbm_dframe* df, orbx_handle* h, const orbm_frame
               pull_to_device(df->desc, sd, (size_t)n * 32, 0) != hipSuccess))
         return ORB_ERR_DEVICE;
     df->fv_nnodes = -1;
-    if ((rc = df_geometry(df, geom, n)) || (rc = df_offsets(df))) return rc;
+    if ((rc = df_geometry(df, geom, n)) || (rc = df_offsets(df)) || (rc = df_grids(df))) return rc;
     return df_featvec(df, fv);
 }
 
@@ -6147,7 +6223,7 @@ int orbm_search_by_bow_dframe(const orbm_dframe* kf, const uint8_t* kf_mp_valid,
     if (!S) return ORB_ERR_DEVICE;
     ZRun z;
     OutBlock out;
-    if ((rc = z.begin(kf->n, false)) || (rc = out.alloc((size_t)f->n + 1, true))) return rc;
+    if ((rc = z.begin(kf->n, false)) || (rc = out.alloc((size_t)f->n + 5, true))) return rc;
     const uint8_t* kv = z.add(kf_mp_valid, kf->n);     // read by k_bow through the mapping
     BowArgs a{};
     a.kf_kps = kf->kps; a.kf_desc = kf->desc; a.kf_valid = kv; a.kp_off = kf->offs;
@@ -6157,12 +6233,23 @@ int orbm_search_by_bow_dframe(const orbm_dframe* kf, const uint8_t* kf_mp_valid,
     a.f_idx = f->fv_idx; a.f_nnodes = f->fv_nnodes; a.ratio = nnratio; a.check_ori = check_ori;
     a.match = S->match; a.nmatches = S->match + S->match_cap; a.f_nleft = -1; a.fin_ticket = S->ticket;
     a.host_out = out.d; a.done = out.flag; a.seq = out.seq; a.reset_after = 1;
+    a.tstart = S->ticket + 1;
+    a.single_nodes = kf->fv_nnodes;
     S->dirty = true;                   // until the kernel has reset its scratch
     if ((rc = launch_bow(a, 1, 0, f->fv_big, kf->fv_nnodes))) return rc;
-    std::vector<int32_t> res((size_t)f->n + 1);
+    std::vector<int32_t> res((size_t)f->n + 5);
     ORB_CHECK(out.fetch(res.data(), res.size()));
     S->dirty = false;
     if (f->n) std::memcpy(match_f, res.data(), (size_t)f->n * 4);
+    // orbm_debug_proj_stats (10 ns ticks from the first block's start): [6]
+    // the last arrival, [7] the final phase, [8] the last block past its frame
+    // node table, [9] the last wave past its nodes
+    int32_t* st = proj_stats();
+    std::fill(st, st + 12, 0);
+    st[6] = res[f->n + 1];
+    st[7] = res[f->n + 2];
+    st[8] = res[f->n + 3];
+    st[9] = res[f->n + 4];
     return res[f->n];
 }
 
@@ -6195,7 +6282,7 @@ int orbm_search_for_initialization_dframe(const orbm_dframe* f1, const orbm_dfra
     const size_t lds = sfi_fused_lds(n1, n2) + (use_grid ? gb : 0);
     S->dirty = true;
     KLAUNCH(k_sfi_fused, dim3(nblk), dim3(kFusedThreads), lds, 0, a, lists, cnt, S->ticket, out.d, use_grid, 0,
-            out.flag, out.seq, z.mirror());
+            out.flag, out.seq, z.mirror(), use_grid ? f2->grid[1] : nullptr);
     ORB_CHECK(hipGetLastError());
     std::vector<int32_t> res((size_t)13 + 3 * n1);
     ORB_CHECK(out.fetch(res.data(), res.size()));

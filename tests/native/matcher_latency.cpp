@@ -328,6 +328,7 @@ int main(int argc, char** argv)
                 check(nm, "SearchByBoW(dframe)");
             });
             put("search_by_bow_dframe", sd);
+            stats("search_by_bow_dframe");      // [6] node phase, [7] final phase (10 ns ticks)
             dmatch.resize(n2);
             dmatch.push_back(nm);
             save(pre + "_bow_dframe.bin", dmatch.data(), dmatch.size());
