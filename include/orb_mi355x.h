@@ -251,6 +251,9 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *                        LDS budget leaves (a cell with more candidates is
  *                        scored densely), n > 0 at most n - 1 entries (1:
  *                        every cell through the dense form)
+ *   ORB_OPT_BOW_TRACE    diagnostics: n > 0 makes the n-th
+ *                        orbm_search_by_bow_dframe call after it is set print
+ *                        its small-node waves' checkpoints to stderr
  * The two k_pyr_stream options are read when a handle builds its plan (the
  * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
@@ -265,7 +268,8 @@ enum {
     ORB_OPT_HOST_OUT = 6,
     ORB_OPT_UPLOAD = 7,
     ORB_OPT_FAST_CAND_CAP = 8,
-    ORB_OPT_COUNT = 9
+    ORB_OPT_BOW_TRACE = 9,
+    ORB_OPT_COUNT = 10
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);

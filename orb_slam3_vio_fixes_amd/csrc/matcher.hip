@@ -1165,6 +1165,10 @@ struct BowArgs {
     unsigned* tstart = nullptr;       // dframe form: the first block's start (s_memrealtime, 100 MHz;
                                       // 0xffffffff before the launch, reset by the last block), and
                                       // host_out[f_n + 1 ..] = node phase, final phase (10 ns ticks)
+    int kv_lds = 0;                   // dframe form: kf_valid (host-mapped, 16-B padded) staged in
+                                      // LDS by every block, this many bytes (0: read in place)
+    unsigned* wtrace = nullptr;       // ORB_OPT_BOW_TRACE (diagnostics): per small-node wave, 16 words of
+                                      // s_memrealtime checkpoints (bow_nodes_body)
 };
 
 // One wave per (pair, vocabulary node) the two FeatureVectors share: the
@@ -1180,14 +1184,24 @@ struct BowArgs {
 // features in a few nodes) run in its large-node blocks, which stage the node's F
 // descriptors in LDS once and share them between the block's keyframes.
 constexpr int kBowMaskChunks = 64;
+#ifndef ORB_BOWF_DROP4
+#define ORB_BOWF_DROP4 1   // 3.955 vs 4.02-4.04 ms per C5 query on one box
+#endif
 
 constexpr int kBowRegChunks = 2;        // frame-feature chunks held in registers per node
+#ifndef ORB_BOW_TRANS
+#define ORB_BOW_TRANS 4      // transposed register-chunk nodes: frame features < this x KF features
+#endif
 static_assert(kBowRegChunks == 2, "bow_node's claim selects between two register chunks");
 constexpr int kBowLdsNodes = 4096;      // frame FeatureVector nodes staged in LDS (dynamic size)
 constexpr int kBowBigCap = 512;         // large-node blocks: node positions staged in LDS
 constexpr int kBowBigPairs = 4;         // large-node blocks: keyframes per block (one per wave)
 
-static size_t bow_lds(int f_nnodes) { return f_nnodes <= kBowLdsNodes ? (size_t)(2 * f_nnodes + 1) * 4 : 0; }
+constexpr int kBowKvLds = 16384;        // dframe form: KF validity bytes staged in LDS
+static size_t bow_kv_bytes(int kv) { return ((size_t)kv + 15) & ~size_t(15); }
+static size_t bow_lds(int f_nnodes, int kv = 0) {
+    return bow_kv_bytes(kv) + (f_nnodes <= kBowLdsNodes ? (size_t)(2 * f_nnodes + 1) * 4 : 0);
+}
 
 // Best / second over a BoW node's frame features for one KF feature.  A
 // candidate is the key dist << 22 | position (unique; ordered like the
@@ -1199,6 +1213,15 @@ __device__ __forceinline__ void key_push(int& lo, int& hi, int key) {
     hi = min(hi, max(lo, key));
     lo = min(lo, key);
 }
+// A wave-uniform 64-bit value in SGPRs (the compiler cannot prove a ballot's
+// result uniform once it is merged with other values).
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+           (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32;
+}
+// The median of three (v_med3_i32): with k1 <= k2 <= k3 the sorted three
+// smallest of {k1, k2, k3, key} are (min(k1, key), med3(k1, key, k2), med3(k2, key, k3)).
+__device__ __forceinline__ int med3i(int a, int b, int c) { return max(min(a, b), min(max(a, b), c)); }
 // kSecond: the caller reads best2 (only when best can pass TH_LOW: no claim is
 // possible otherwise, so the second reduction is skipped).
 template <bool kSecond>
@@ -1222,14 +1245,20 @@ __device__ __forceinline__ Best2 key_best2(int lo, int hi) {
 // past either reads global memory.
 template <bool kLds, bool kFish>
 __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
-                                         const uint4* s_fd, const int* s_fi, uint4* s_q) {
+                                         const uint4* s_fd, const int* s_fi, uint4* s_q,
+                                         unsigned* tr = nullptr) {
     const int lane = lane_id();
     const bool one = a.single_nodes >= 0;            // one pair at offset 0: no offset loads in the chain
     const long long kpo = one ? 0 : a.kp_off[pr];
     const uint8_t* KD = a.kf_desc + kpo * 32;
-    const uint8_t* KV = a.kf_valid + kpo;
+    extern __shared__ __attribute__((aligned(16))) int bow_smem[];
+    // the dframe form's validity bytes come from the block's LDS copy: read in
+    // place they are host memory, one PCIe round trip per lane-distinct line
+    const uint8_t* KV = a.kv_lds > 0 ? (const uint8_t*)bow_smem : a.kf_valid + kpo;
     const int* ko = a.kf_off + (one ? 0 : a.node_off[pr] + pr);
     const uint32_t* ki = a.kf_idx + (one ? 0 : a.idx_off[pr]);
+    fb = __builtin_amdgcn_readfirstlane(fb);     // wave-uniform (read from LDS by the caller): keeps
+    fe = __builtin_amdgcn_readfirstlane(fe);     // the node's loops scalar
     const int nf = fe - fb;
     const int nch = (nf + kWave - 1) / kWave;
     int32_t* match = a.match + (long long)pr * a.f_n;
@@ -1268,6 +1297,25 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
     // the node's KF features, 64 at a time, prefetched lane-parallel (index,
     // MapPoint validity, descriptor, angle) and visited in order by readlane
     const int pe = ko[ia + 1];
+    // Register-chunk nodes with many KF features for their frame features run
+    // transposed (a lane per KF feature): per KF feature that costs one pass
+    // over the free positions' descriptors in a lane instead of two wave-wide
+    // reductions (~85 VALU cycles a frame position against ~400 a KF feature).
+    // tk0 / tk1: the taken / invalid flags of chunks 0 / 1 as wave-uniform masks.
+    const bool trans = !kLds && !kFish && nch <= kBowRegChunks && nf < ORB_BOW_TRANS * (pe - ko[ia]);
+    uint64_t tk0 = ~0ull, tk1 = ~0ull;
+    if (!kLds && trans) {
+        tk0 = uniform64(__ballot(taken & 1));
+        tk1 = uniform64(__ballot((taken >> 1) & 1));
+#pragma unroll
+        for (int c = 0; c < kBowRegChunks; ++c) {
+            s_q[c * 2 * kWave + lane] = fr0[c];
+            s_q[c * 2 * kWave + kWave + lane] = fr1[c];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     for (int pbase = ko[ia]; pbase < pe; pbase += kWave) {
       const int pl = pbase + lane;
       int my_ikf = 0, my_ok = 0;
@@ -1277,6 +1325,148 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
           my_ok = KV[my_ikf];
           mq0 = *(const uint4*)(KD + (long long)my_ikf * 32);
           mq1 = *(const uint4*)(KD + (long long)my_ikf * 32 + 16);
+      }
+      if (tr && lane == 0 && pbase == ko[ia]) {
+          tr[3] = (unsigned)__builtin_amdgcn_s_memrealtime();
+          tr[5] = (unsigned)(pe - pbase);
+          tr[6] = (unsigned)nf;
+      }
+      if constexpr (!kLds && !kFish) {
+        if (trans) {
+          // Lane per KF feature: each lane keeps the three smallest keys over
+          // the node's free frame positions (uniform position, descriptor by a
+          // broadcast LDS read: no cross-lane reduction per pair), then the
+          // decisions run in KF order on those lists.  A claim earlier in the
+          // node removes one position: a feature's best / second are the first
+          // two of its list still free, exact while at least two remain (keys
+          // smaller than its third are all in the list; an INT_MAX entry means
+          // the list already holds every candidate).  A list with fewer than
+          // two left is recomputed lanes-over-positions against the flags.
+          int k1 = INT_MAX, k2 = INT_MAX, k3 = INT_MAX;
+          if (tr) {
+              const unsigned ok = (unsigned)__ballot(my_ok != 0) + (unsigned)(mq0.x & 0);   // waits for the loads
+              if (lane == 0 && pbase == ko[ia] && ok != 1u) tr[9] = (unsigned)__builtin_amdgcn_s_memrealtime();
+          }
+#pragma unroll
+          for (int c = 0; c < kBowRegChunks; ++c) {
+              uint64_t av = c < nch ? uniform64(~(c ? tk1 : tk0)) : 0ull;
+              if (!av) continue;
+              const uint4* sf = s_q + c * 2 * kWave;
+              auto step = [&](const uint4& f0, const uint4& f1, int p) {
+                  const int d = __popc(mq0.x ^ f0.x) + __popc(mq0.y ^ f0.y) + __popc(mq0.z ^ f0.z) +
+                                __popc(mq0.w ^ f0.w) + __popc(mq1.x ^ f1.x) + __popc(mq1.y ^ f1.y) +
+                                __popc(mq1.z ^ f1.z) + __popc(mq1.w ^ f1.w);
+                  const int key = (d << 22) | (c * kWave + p);
+                  k3 = med3i(k2, key, k3);
+                  k2 = med3i(k1, key, k2);
+                  k1 = min(k1, key);
+              };
+              // two positions in flight (ping-pong registers, no copies): the
+              // next position's LDS reads go out before this one's math
+              int pa = __ffsll((long long)av) - 1;
+              av &= av - 1;
+              uint4 fa0 = sf[pa], fa1 = sf[kWave + pa];
+              for (;;) {
+                  const bool hb = av != 0;
+                  const int pb = hb ? __ffsll((long long)av) - 1 : pa;
+                  av &= av - 1;
+                  const uint4 fb0 = sf[pb], fb1 = sf[kWave + pb];
+                  __builtin_amdgcn_sched_barrier(0);
+                  step(fa0, fa1, pa);
+                  if (!hb) break;
+                  const bool ha = av != 0;
+                  pa = ha ? __ffsll((long long)av) - 1 : pb;
+                  av &= av - 1;
+                  fa0 = sf[pa]; fa1 = sf[kWave + pa];
+                  __builtin_amdgcn_sched_barrier(0);
+                  step(fb0, fb1, pb);
+                  if (!ha) break;
+              }
+          }
+          constexpr int kPos = (1 << 22) - 1;
+          // the claimed position of a best / second pair, or -1 (:848 / :327, ratio)
+          auto decide = [&](int r0, int r1) -> int {
+              const int best = r0 == INT_MAX ? 256 : r0 >> 22;
+              const int best2 = r1 == INT_MAX ? 256 : r1 >> 22;
+              const bool low = a.f_valid ? best < kThLow : best <= kThLow;
+              return (low && (float)best < a.ratio * (float)best2) ? (r0 & kPos) : -1;
+          };
+          // Lane-parallel, per list: its three positions (0xff: none), which of
+          // them are taken (tb), and whether each pair it can present as (best,
+          // second) -- (1,2) with nothing or only the third taken, (1,3) with
+          // the second taken, (2,3) with the first -- passes the thresholds.
+          // From these every feature's decision at the current flags is a few
+          // VALU ops (cur: claimed position, -1 none, -2 list ran short).  A
+          // feature that does not claim changes nothing, and its decision can
+          // only change after a claim before it: the ordered walk visits only
+          // the claiming (and short) features, re-deciding the rest after each
+          // claim -- steps = claims, not KF features.
+          auto p8 = [&](int k) { return k == INT_MAX ? 0xff : (k & kPos); };
+          const int q1 = p8(k1), q2 = p8(k2), q3 = p8(k3);
+          const int okb = (decide(k1, k2) >= 0 ? 1 : 0) | (decide(k1, k3) >= 0 ? 2 : 0) |
+                          (decide(k2, k3) >= 0 ? 4 : 0);
+          auto tk_has = [&](int q) -> int {                // lane-parallel: position q taken (0xff: never)
+              const uint64_t m = q < kWave ? tk0 : (q < 2 * kWave ? tk1 : 0ull);
+              return (int)((m >> (q & (kWave - 1))) & 1);
+          };
+          int tb = tk_has(q1) | tk_has(q2) << 1 | tk_has(q3) << 2;
+          auto cur_of = [&]() -> int {
+              const int t1 = tb & 1, t2 = (tb >> 1) & 1;
+              if (__popc(tb) >= 2) return -2;
+              const int sel = t1 ? 4 : (t2 ? 2 : 1);
+              return (okb & sel) ? (t1 ? q2 : q1) : -1;
+          };
+          int cur = cur_of();
+          if (tr && lane == 0 && pbase == ko[ia]) tr[7] = (unsigned)__builtin_amdgcn_s_memrealtime();
+          const uint64_t okm = uniform64(__ballot(my_ok != 0));
+          uint64_t todo = okm & uniform64(__ballot(cur != -1));
+          unsigned nsteps = 0, nshort = 0, nclaim = 0;
+          while (todo) {
+              const int u = __ffsll((long long)todo) - 1;
+              int pos = __builtin_amdgcn_readlane(cur, u);
+              if (tr) { ++nsteps; nshort += pos == -2; nclaim += pos >= 0; }
+              if (pos == -2) {                             // list ran short: lanes over positions
+                  uint4 q0, q1;
+                  q0.x = __builtin_amdgcn_readlane(mq0.x, u); q0.y = __builtin_amdgcn_readlane(mq0.y, u);
+                  q0.z = __builtin_amdgcn_readlane(mq0.z, u); q0.w = __builtin_amdgcn_readlane(mq0.w, u);
+                  q1.x = __builtin_amdgcn_readlane(mq1.x, u); q1.y = __builtin_amdgcn_readlane(mq1.y, u);
+                  q1.z = __builtin_amdgcn_readlane(mq1.z, u); q1.w = __builtin_amdgcn_readlane(mq1.w, u);
+                  int lo = INT_MAX, hi = INT_MAX;
+#pragma unroll
+                  for (int c = 0; c < kBowRegChunks; ++c) {
+                      if (c >= nch) break;
+                      const int d = __popc(q0.x ^ fr0[c].x) + __popc(q0.y ^ fr0[c].y) + __popc(q0.z ^ fr0[c].z) +
+                                    __popc(q0.w ^ fr0[c].w) + __popc(q1.x ^ fr1[c].x) + __popc(q1.y ^ fr1[c].y) +
+                                    __popc(q1.z ^ fr1[c].z) + __popc(q1.w ^ fr1[c].w);
+                      const int tbit = (int)(((c ? tk1 : tk0) >> lane) & 1);
+                      key_push(lo, hi, ((d << 22) | (c * kWave + lane)) | (-tbit & INT_MAX));
+                  }
+                  const int r0 = wave_min(lo, INT_MAX);
+                  const int r1 = wave_min(lane == (r0 & (kWave - 1)) ? hi : lo, INT_MAX);
+                  pos = decide(r0, r1);
+              }
+              uint64_t later = todo & (todo - 1);          // the features after u
+              if (pos >= 0) {
+                  const int ikf = __builtin_amdgcn_readlane(my_ikf, u);
+                  if (pos < kWave) {
+                      tk0 |= 1ull << pos;
+                      mcl[0] = lane == pos ? ikf : mcl[0];
+                  } else {
+                      tk1 |= 1ull << (pos - kWave);
+                      mcl[1] = lane == pos - kWave ? ikf : mcl[1];
+                  }
+                  ++nm;
+                  tb |= (q1 == pos ? 1 : 0) | (q2 == pos ? 2 : 0) | (q3 == pos ? 4 : 0);
+                  cur = cur_of();
+                  const uint64_t after = u == kWave - 1 ? 0ull : (~0ull << (u + 1));
+                  later = okm & after & uniform64(__ballot(cur != -1));
+              }
+              todo = later;
+          }
+          if (tr && lane == 0 && pbase == ko[ia]) { tr[12] = nsteps; tr[13] = nshort; tr[14] = nclaim; }
+          if (tr && lane == 0 && pbase == ko[ia]) tr[8] = (unsigned)__builtin_amdgcn_s_memrealtime();
+          continue;
+        }
       }
       if constexpr (!kLds) {
           // wave-private LDS copy: one KF descriptor is then two broadcast LDS
@@ -1397,12 +1587,25 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
 // nodes of consecutive keyframes are adjacent).
 __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nblocks, uint4* s_q) {
     extern __shared__ __attribute__((aligned(16))) int bow_smem[];
-    uint32_t* s_fnode = (uint32_t*)bow_smem;
-    int* s_foff = bow_smem + a.f_nnodes;
+    // dynamic LDS: [staged KF validity][frame node ids][offsets]
+    uint32_t* s_fnode = (uint32_t*)bow_smem + ((a.kv_lds + 15) >> 4) * 4;
+    int* s_foff = (int*)s_fnode + a.f_nnodes;
     const bool lds_f = a.f_nnodes <= kBowLdsNodes;
-    if (lds_f) {
-        for (int i = threadIdx.x; i < a.f_nnodes; i += blockDim.x) s_fnode[i] = a.f_node[i];
-        for (int i = threadIdx.x; i <= a.f_nnodes; i += blockDim.x) s_foff[i] = a.f_off[i];
+    {
+        // the staged validity (host memory) and the frame node table (HBM) in
+        // one pass: each thread's reads of all three go out together
+        const int n16 = (a.kv_lds + 15) >> 4, nn = lds_f ? a.f_nnodes + 1 : 0;
+        for (int i = threadIdx.x; i < max(n16, nn); i += blockDim.x) {
+            uint4 kv = make_uint4(0, 0, 0, 0);
+            uint32_t fnd = 0;
+            int fo = 0;
+            if (i < n16) kv = ((const uint4*)a.kf_valid)[i];
+            if (i < nn - 1) fnd = a.f_node[i];
+            if (i < nn) fo = a.f_off[i];
+            if (i < n16) ((uint4*)bow_smem)[i] = kv;
+            if (i < nn - 1) s_fnode[i] = fnd;
+            if (i < nn) s_foff[i] = fo;
+        }
     }
     __syncthreads();
     if (a.tstart && threadIdx.x == 0) atomicMax(a.tstart + 1, (unsigned)__builtin_amdgcn_s_memrealtime());
@@ -1414,6 +1617,12 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
     const long long per = (total + nw - 1) / nw;
     const long long g0 = w * per, g1 = min(total, g0 + per);
     if (g0 >= g1) return;
+    unsigned* tr = a.wtrace ? a.wtrace + w * 16 : nullptr;
+    if (tr && lane_id() == 0) {
+        tr[0] = a.tstart ? a.tstart[0] : 0u;
+        tr[1] = (unsigned)__builtin_amdgcn_s_memrealtime();
+        tr[10] = (unsigned)__builtin_amdgcn_s_memtime();
+    }
     int pr = 0;
     if (!one) {
         int lo = 0, hi = a.npairs;                       // last pr with node_off[pr] <= g0
@@ -1438,8 +1647,13 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         if (fl >= a.f_nnodes || fnode[fl] != na) continue;
         const int fb = foff[fl], fe = foff[fl + 1];
         if (fe - fb > kBowRegChunks * kWave) continue;  // a large-node block's
-        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q);
-        else bow_node<false, false>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q);
+        if (tr && lane_id() == 0) tr[2] = (unsigned)__builtin_amdgcn_s_memrealtime();
+        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q, tr);
+        else bow_node<false, false>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q, tr);
+    }
+    if (tr && lane_id() == 0) {
+        tr[4] = (unsigned)__builtin_amdgcn_s_memrealtime();
+        tr[11] = (unsigned)__builtin_amdgcn_s_memtime();
     }
     if (a.tstart && lane_id() == 0) atomicMax(a.tstart + 2, (unsigned)__builtin_amdgcn_s_memrealtime());
 }
@@ -1489,9 +1703,11 @@ __device__ __forceinline__ void bow_big_body(const BowArgs& a, int bid, int slot
 
 // One launch for both: blocks [0, big_blocks) take the large nodes (latency-
 // bound serial chains), the rest the small ones (VALU-bound), so the two
-// co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private KF
-// descriptor areas (2 * 64 uint4 each).
-__device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins);
+// co-schedule on the CUs.  Small-node blocks use s_fd as four wave-private
+// descriptor areas (4 * 64 uint4 each: the KF descriptors of 64 features, or a
+// transposed node's frame descriptors).
+__device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins,
+                               int32_t* hcopy = nullptr);
 // The end of a host call's kernel (the last block, every thread): each wave's
 // result stores complete, then one lane releases them at system scope and
 // writes the call's sequence number into the word the host polls.
@@ -1529,20 +1745,27 @@ __device__ __forceinline__ bool last_arriver(unsigned* ticket, int* flag) {
     __syncthreads();
     return *flag != 0;
 }
-static_assert(2 * kBowBigCap >= 4 * 2 * kWave, "s_fd holds the small-node waves' descriptor areas");
+static_assert(2 * kBowBigCap >= 4 * 4 * kWave, "s_fd holds the small-node waves' descriptor areas");
 static_assert(kBowBigCap >= 41, "s_fi holds the fused final's histogram, drop count and last-arriver flag");
 __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_slots) {
     __shared__ uint4 s_fd[2 * kBowBigCap];
     __shared__ int s_fi[kBowBigCap];
     if (a.tstart && threadIdx.x == 0) atomicMin(a.tstart, (unsigned)__builtin_amdgcn_s_memrealtime());
+    if (a.kv_lds > 0 && (int)blockIdx.x < big_blocks) {   // (small-node blocks stage it with their table)
+        extern __shared__ __attribute__((aligned(16))) int bow_smem[];
+        const int n16 = (a.kv_lds + 15) >> 4;
+        for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4*)bow_smem)[i] = ((const uint4*)a.kf_valid)[i];
+        __syncthreads();
+    }
     if ((int)blockIdx.x < big_blocks) bow_big_body(a, blockIdx.x, big_slots, s_fd, s_fi);
-    else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 2 * kWave);
+    else bow_nodes_body(a, blockIdx.x - big_blocks, gridDim.x - big_blocks, s_fd + wave_id() * 4 * kWave);
     if (a.fin_ticket) {
         // a single pair: the last block to finish runs the rotation filter on
         // every block's matches (the match rows, nmatches and the LDS are free)
         if (!last_arriver(a.fin_ticket, s_fi + 40)) return;
         const unsigned t_arrive = (unsigned)__builtin_amdgcn_s_memrealtime();
-        bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd));
+        const bool fused_copy = a.host_out && a.check_ori && ORB_BOWF_DROP4;
+        bow_final_body(a, 0, s_fi, s_fi + 32, (uint8_t*)s_fd, (int)sizeof(s_fd), fused_copy ? a.host_out : nullptr);
         if (a.tstart && threadIdx.x == 0) {
             const unsigned t0 = *a.tstart;
             a.host_out[a.f_n + 1] = (int)(t_arrive - t0);
@@ -1555,10 +1778,11 @@ __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_
         }
         if (a.host_out) {
             __syncthreads();
-            for (int i = threadIdx.x; i < a.f_n; i += blockDim.x) {
-                a.host_out[i] = a.match[i];
-                if (a.reset_after) a.match[i] = -1;
-            }
+            if (!fused_copy)
+                for (int i = threadIdx.x; i < a.f_n; i += blockDim.x) {
+                    a.host_out[i] = a.match[i];
+                    if (a.reset_after) a.match[i] = -1;
+                }
             if (threadIdx.x == 0) {
                 a.host_out[a.f_n] = a.nmatches[0];
                 if (a.reset_after) {
@@ -1578,8 +1802,11 @@ __global__ __launch_bounds__(256) void k_bow(BowArgs a, int big_blocks, int big_
 constexpr int kBowFinalBins = 16384;    // frame features whose bin k_bow_final keeps in LDS
 
 // hist: 32 ints, drop: 1 int, sbin: nbins bytes of LDS (the bin of each match,
-// one gather of the KF angle)
-__device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins) {
+// one gather of the KF angle).  hcopy (the single-pair kernel, with check_ori):
+// the filtered row also goes there in the same pass (and, with reset_after, the
+// row is left at -1), instead of a separate copy pass.
+__device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p, uint8_t* sbin, int nbins,
+                               int32_t* hcopy) {
     const int tid = threadIdx.x, nt = blockDim.x;
     int32_t* match = a.match + (long long)pr * a.f_n;
     int& drop = *drop_p;
@@ -1613,9 +1840,6 @@ __device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p,
         int i1, i2, i3;
         three_maxima_wave(hist, i1, i2, i3);
         int d = 0;
-#ifndef ORB_BOWF_DROP4
-#define ORB_BOWF_DROP4 1   // 3.955 vs 4.02-4.04 ms per C5 query on one box
-#endif
 #if ORB_BOWF_DROP4
         // four rows' match loads in flight per thread
         for (int i0 = tid; i0 < a.f_n; i0 += 4 * nt) {
@@ -1624,8 +1848,19 @@ __device__ void bow_final_body(const BowArgs& a, int pr, int* hist, int* drop_p,
             for (int u = 0; u < 4; ++u) m[u] = i0 + u * nt < a.f_n ? match[i0 + u * nt] : -1;
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                if (m[u] < 0) continue;
                 const int i = i0 + u * nt;
+                if (hcopy && i < a.f_n) {
+                    bool keep = m[u] >= 0;
+                    if (keep) {
+                        const int b = i < nbins ? sbin[i] : rot_bin(KK[m[u]].angle, a.f_kps[i].angle);
+                        keep = b == i1 || b == i2 || b == i3;
+                        d += !keep;
+                    }
+                    hcopy[i] = keep ? m[u] : -1;
+                    if (m[u] >= 0 && (a.reset_after || !keep)) match[i] = -1;
+                    continue;
+                }
+                if (m[u] < 0) continue;
                 const int b = i < nbins ? sbin[i] : rot_bin(KK[m[u]].angle, a.f_kps[i].angle);
                 if (b == i1 || b == i2 || b == i3) continue;
                 match[i] = -1;
@@ -1692,7 +1927,8 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
     const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, want));
     big_slots = std::max(1, big_slots);
     const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs * big_slots;
-    KLAUNCH(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes), st, a, big_blocks, big_slots);
+    KLAUNCH(k_bow, dim3(big_blocks + blocks), dim3(256), bow_lds(a.f_nnodes, a.kv_lds), st, a, big_blocks,
+            big_slots);
     if (!a.fin_ticket) KLAUNCH(k_bow_final, dim3(npairs), dim3(256), 0, st, a);
     return hipGetLastError() == hipSuccess ? ORB_OK : ORB_ERR_DEVICE;
 }
@@ -6235,10 +6471,41 @@ int orbm_search_by_bow_dframe(const orbm_dframe* kf, const uint8_t* kf_mp_valid,
     a.host_out = out.d; a.done = out.flag; a.seq = out.seq; a.reset_after = 1;
     a.tstart = S->ticket + 1;
     a.single_nodes = kf->fv_nnodes;
+    if (kf->n <= kBowKvLds) a.kv_lds = kf->n;
+    // ORB_OPT_BOW_TRACE = n: the n-th call after it is set prints its per-wave
+    // checkpoints to stderr (diagnostics)
+    static int trace_opt = 0, ncall = 0;
+    const int trace_call = orbmi::debug_opt(ORB_OPT_BOW_TRACE);
+    if (trace_call != trace_opt) { trace_opt = trace_call; ncall = 0; }
+    unsigned* wtrace = nullptr;
+    const int nwtr = (int)((kf->fv_nnodes + 3) / 4 * 4);    // (16 words a wave)
+    const bool tracing = trace_call > 0 && ++ncall == trace_call;
+    if (tracing) {
+        if (hipMalloc(&wtrace, (size_t)nwtr * 16 * 4) != hipSuccess ||
+            hipMemset(wtrace, 0, (size_t)nwtr * 16 * 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess)
+            return ORB_ERR_DEVICE;
+        a.wtrace = wtrace;
+    }
     S->dirty = true;                   // until the kernel has reset its scratch
     if ((rc = launch_bow(a, 1, 0, f->fv_big, kf->fv_nnodes))) return rc;
     std::vector<int32_t> res((size_t)f->n + 5);
     ORB_CHECK(out.fetch(res.data(), res.size()));
+    if (tracing) {
+        std::vector<unsigned> t((size_t)nwtr * 16);
+        if (hipMemcpy(t.data(), wtrace, t.size() * 4, hipMemcpyDeviceToHost) != hipSuccess) return ORB_ERR_DEVICE;
+        (void)hipFree(wtrace);
+        fprintf(stderr, "bow trace: wave start search issued end nkf nf loads-done top3-done decided "
+                        "(10 ns from the first block)\n");
+        for (int w = 0; w < nwtr; ++w) {
+            const unsigned* r = t.data() + (size_t)w * 16;
+            if (!r[1]) continue;
+            auto rel = [&](unsigned x) { return x ? (long)(x - r[0]) : -1L; };
+            const double mhz = r[4] > r[1] ? 100.0 * (double)(r[11] - r[10]) / (double)(r[4] - r[1]) : 0.0;
+            fprintf(stderr, "bow trace: %d %ld %ld %ld %ld %u %u %ld %ld %ld clk %.0f MHz steps %u short %u claims %u\n",
+                    w, rel(r[1]), rel(r[2]), rel(r[3]), rel(r[4]), r[5], r[6], rel(r[9]), rel(r[7]), rel(r[8]), mhz,
+                    r[12], r[13], r[14]);
+        }
+    }
     S->dirty = false;
     if (f->n) std::memcpy(match_f, res.data(), (size_t)f->n * 4);
     // orbm_debug_proj_stats (10 ns ticks from the first block's start): [6]
