@@ -1246,7 +1246,7 @@ __device__ __forceinline__ Best2 key_best2(int lo, int hi) {
 template <bool kLds, bool kFish>
 __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int fb, int fe,
                                          const uint4* s_fd, const int* s_fi, uint4* s_q,
-                                         unsigned* tr = nullptr) {
+                                         unsigned* tr = nullptr, int coop_w = -1) {
     const int lane = lane_id();
     const bool one = a.single_nodes >= 0;            // one pair at offset 0: no offset loads in the chain
     const long long kpo = one ? 0 : a.kp_off[pr];
@@ -1303,18 +1303,32 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
     // reductions (~85 VALU cycles a frame position against ~400 a KF feature).
     // tk0 / tk1: the taken / invalid flags of chunks 0 / 1 as wave-uniform masks.
     const bool trans = !kLds && !kFish && nch <= kBowRegChunks && nf < ORB_BOW_TRANS * (pe - ko[ia]);
+    // coop_w >= 0 (single pair: a block per KF node, every wave here with the
+    // same node): a transposed node's positions are split over the block's
+    // four waves for the lists, wave 0 merges them and walks; other nodes are
+    // wave 0's alone.  sq0: wave 0's area (the frame descriptors), the other
+    // waves' areas take their lists, wave 3's also the flags after a walk.
+    const bool coop = coop_w >= 0;
+    if (coop && coop_w > 0 && !trans) return;
+    uint4* const sq0 = coop ? s_q - coop_w * 4 * kWave : s_q;
     uint64_t tk0 = ~0ull, tk1 = ~0ull;
     if (!kLds && trans) {
         tk0 = uniform64(__ballot(taken & 1));
         tk1 = uniform64(__ballot((taken >> 1) & 1));
+        if (coop_w <= 0) {
 #pragma unroll
-        for (int c = 0; c < kBowRegChunks; ++c) {
-            s_q[c * 2 * kWave + lane] = fr0[c];
-            s_q[c * 2 * kWave + kWave + lane] = fr1[c];
+            for (int c = 0; c < kBowRegChunks; ++c) {
+                s_q[c * 2 * kWave + lane] = fr0[c];
+                s_q[c * 2 * kWave + kWave + lane] = fr1[c];
+            }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (coop) {
+            __syncthreads();
+        } else {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
     }
     for (int pbase = ko[ia]; pbase < pe; pbase += kWave) {
       const int pl = pbase + lane;
@@ -1347,40 +1361,61 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
               const unsigned ok = (unsigned)__ballot(my_ok != 0) + (unsigned)(mq0.x & 0);   // waits for the loads
               if (lane == 0 && pbase == ko[ia] && ok != 1u) tr[9] = (unsigned)__builtin_amdgcn_s_memrealtime();
           }
-#pragma unroll
-          for (int c = 0; c < kBowRegChunks; ++c) {
-              uint64_t av = c < nch ? uniform64(~(c ? tk1 : tk0)) : 0ull;
-              if (!av) continue;
-              const uint4* sf = s_q + c * 2 * kWave;
+          {
+              // every position of the node in order, four per iteration (their
+              // LDS reads together, then the math); a taken position's key is
+              // INT_MAX (a wave-uniform test)
               auto step = [&](const uint4& f0, const uint4& f1, int p) {
                   const int d = __popc(mq0.x ^ f0.x) + __popc(mq0.y ^ f0.y) + __popc(mq0.z ^ f0.z) +
                                 __popc(mq0.w ^ f0.w) + __popc(mq1.x ^ f1.x) + __popc(mq1.y ^ f1.y) +
                                 __popc(mq1.z ^ f1.z) + __popc(mq1.w ^ f1.w);
-                  const int key = (d << 22) | (c * kWave + p);
+                  const bool tkp = (((p < kWave ? tk0 : tk1) >> (p & (kWave - 1))) & 1) != 0;
+                  const int key = tkp ? INT_MAX : ((d << 22) | p);
                   k3 = med3i(k2, key, k3);
                   k2 = med3i(k1, key, k2);
                   k1 = min(k1, key);
               };
-              // two positions in flight (ping-pong registers, no copies): the
-              // next position's LDS reads go out before this one's math
-              int pa = __ffsll((long long)av) - 1;
-              av &= av - 1;
-              uint4 fa0 = sf[pa], fa1 = sf[kWave + pa];
-              for (;;) {
-                  const bool hb = av != 0;
-                  const int pb = hb ? __ffsll((long long)av) - 1 : pa;
-                  av &= av - 1;
-                  const uint4 fb0 = sf[pb], fb1 = sf[kWave + pb];
-                  __builtin_amdgcn_sched_barrier(0);
-                  step(fa0, fa1, pa);
-                  if (!hb) break;
-                  const bool ha = av != 0;
-                  pa = ha ? __ffsll((long long)av) - 1 : pb;
-                  av &= av - 1;
-                  fa0 = sf[pa]; fa1 = sf[kWave + pa];
-                  __builtin_amdgcn_sched_barrier(0);
-                  step(fb0, fb1, pb);
-                  if (!ha) break;
+              const int pb0 = coop ? (nf * coop_w) >> 2 : 0, pb1 = coop ? (nf * (coop_w + 1)) >> 2 : nf;
+              for (int p0 = pb0; p0 < pb1; p0 += 4) {
+                  uint4 f0[4], f1[4];
+#pragma unroll
+                  for (int u = 0; u < 4; ++u) {
+                      const int p = min(p0 + u, pb1 - 1);
+                      const uint4* sf = sq0 + (p >> 6) * 2 * kWave + (p & (kWave - 1));
+                      f0[u] = sf[0];
+                      f1[u] = sf[kWave];
+                  }
+#pragma unroll
+                  for (int u = 0; u < 4; ++u)
+                      if (p0 + u < pb1) step(f0[u], f1[u], p0 + u);
+              }
+          }
+          if (coop) {
+              // the other waves' lists into wave 0's (each list sorted; keys distinct)
+              if (coop_w > 0) {
+                  int* L = (int*)s_q;
+                  L[lane] = k1;
+                  L[kWave + lane] = k2;
+                  L[2 * kWave + lane] = k3;
+              }
+              __syncthreads();
+              if (coop_w > 0) {
+                  __syncthreads();                         // wave 0's walk done: its flags
+                  const uint64_t* T = (const uint64_t*)(sq0 + 3 * 4 * kWave + kWave);
+                  tk0 = uniform64(T[0]);
+                  tk1 = uniform64(T[1]);
+                  continue;
+              }
+#pragma unroll
+              for (int w = 1; w < 4; ++w) {
+                  const int* L = (const int*)(sq0 + w * 4 * kWave);
+#pragma unroll
+                  for (int r = 0; r < 3; ++r) {
+                      const int key = L[r * kWave + lane];
+                      k3 = med3i(k2, key, k3);
+                      k2 = med3i(k1, key, k2);
+                      k1 = min(k1, key);
+                  }
               }
           }
           constexpr int kPos = (1 << 22) - 1;
@@ -1395,8 +1430,8 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
           // them are taken (tb), and whether each pair it can present as (best,
           // second) -- (1,2) with nothing or only the third taken, (1,3) with
           // the second taken, (2,3) with the first -- passes the thresholds.
-          // From these every feature's decision at the current flags is a few
-          // VALU ops (cur: claimed position, -1 none, -2 list ran short).  A
+          // From these every feature's decision at the current flags is one
+          // table lookup (cur: claimed position, kNone, kShort: list ran short).  A
           // feature that does not claim changes nothing, and its decision can
           // only change after a claim before it: the ordered walk visits only
           // the claiming (and short) features, re-deciding the rest after each
@@ -1410,22 +1445,29 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
               return (int)((m >> (q & (kWave - 1))) & 1);
           };
           int tb = tk_has(q1) | tk_has(q2) << 1 | tk_has(q3) << 2;
-          auto cur_of = [&]() -> int {
-              const int t1 = tb & 1, t2 = (tb >> 1) & 1;
-              if (__popc(tb) >= 2) return -2;
-              const int sel = t1 ? 4 : (t2 ? 2 : 1);
-              return (okb & sel) ? (t1 ? q2 : q1) : -1;
-          };
+          // the decision for each taken-state tb of the list, a byte each (0xff
+          // none, 0xfe short): tb 0 / 4 -> (1,2), 1 -> (2,3), 2 -> (1,3)
+          constexpr int kNone = 0xff, kShort = 0xfe;
+          uint64_t lut = (uint64_t)kShort << 24 | (uint64_t)kShort << 40 | (uint64_t)kShort << 48 |
+                         (uint64_t)kShort << 56;           // states 3, 5, 6, 7
+          {
+              const uint64_t e12 = (okb & 1) ? (uint64_t)q1 : (uint64_t)kNone;
+              const uint64_t e23 = (okb & 4) ? (uint64_t)q2 : (uint64_t)kNone;
+              const uint64_t e13 = (okb & 2) ? (uint64_t)q1 : (uint64_t)kNone;
+              lut |= e12 | e23 << 8 | e13 << 16 | e12 << 32;
+          }
+          auto cur_of = [&]() -> int { return (int)((lut >> (tb * 8)) & 0xff); };
           int cur = cur_of();
           if (tr && lane == 0 && pbase == ko[ia]) tr[7] = (unsigned)__builtin_amdgcn_s_memrealtime();
           const uint64_t okm = uniform64(__ballot(my_ok != 0));
-          uint64_t todo = okm & uniform64(__ballot(cur != -1));
+          uint64_t todo = okm & uniform64(__ballot(cur != kNone));
           unsigned nsteps = 0, nshort = 0, nclaim = 0;
           while (todo) {
               const int u = __ffsll((long long)todo) - 1;
               int pos = __builtin_amdgcn_readlane(cur, u);
-              if (tr) { ++nsteps; nshort += pos == -2; nclaim += pos >= 0; }
-              if (pos == -2) {                             // list ran short: lanes over positions
+              if (tr) { ++nsteps; nshort += pos == kShort; nclaim += pos < kShort; }
+              if (pos == kNone) pos = -1;
+              if (pos == kShort) {                         // list ran short: lanes over positions
                   uint4 q0, q1;
                   q0.x = __builtin_amdgcn_readlane(mq0.x, u); q0.y = __builtin_amdgcn_readlane(mq0.y, u);
                   q0.z = __builtin_amdgcn_readlane(mq0.z, u); q0.w = __builtin_amdgcn_readlane(mq0.w, u);
@@ -1459,11 +1501,16 @@ __device__ __forceinline__ void bow_node(const BowArgs& a, int pr, int ia, int f
                   tb |= (q1 == pos ? 1 : 0) | (q2 == pos ? 2 : 0) | (q3 == pos ? 4 : 0);
                   cur = cur_of();
                   const uint64_t after = u == kWave - 1 ? 0ull : (~0ull << (u + 1));
-                  later = okm & after & uniform64(__ballot(cur != -1));
+                  later = okm & after & uniform64(__ballot(cur != kNone));
               }
               todo = later;
           }
           if (tr && lane == 0 && pbase == ko[ia]) { tr[12] = nsteps; tr[13] = nshort; tr[14] = nclaim; }
+          if (coop) {
+              uint64_t* T = (uint64_t*)(sq0 + 3 * 4 * kWave + kWave);
+              if (lane == 0) { T[0] = tk0; T[1] = tk1; }
+              __syncthreads();
+          }
           if (tr && lane == 0 && pbase == ko[ia]) tr[8] = (unsigned)__builtin_amdgcn_s_memrealtime();
           continue;
         }
@@ -1613,11 +1660,14 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
     const int* foff = lds_f ? s_foff : a.f_off;
     const bool one = a.single_nodes >= 0;
     const long long total = one ? a.single_nodes : a.node_off[a.npairs];
-    const long long nw = (long long)nblocks * 4, w = (long long)bid * 4 + wave_id();
+    // a single pair: a block per KF node, its four waves on it together (the
+    // transposed nodes' lists split four ways); else a wave per KF node
+    const bool coop = one;
+    const long long nw = coop ? nblocks : (long long)nblocks * 4, w = coop ? bid : (long long)bid * 4 + wave_id();
     const long long per = (total + nw - 1) / nw;
     const long long g0 = w * per, g1 = min(total, g0 + per);
     if (g0 >= g1) return;
-    unsigned* tr = a.wtrace ? a.wtrace + w * 16 : nullptr;
+    unsigned* tr = a.wtrace ? a.wtrace + ((long long)bid * 4 + wave_id()) * 16 : nullptr;
     if (tr && lane_id() == 0) {
         tr[0] = a.tstart ? a.tstart[0] : 0u;
         tr[1] = (unsigned)__builtin_amdgcn_s_memrealtime();
@@ -1648,8 +1698,9 @@ __device__ __forceinline__ void bow_nodes_body(const BowArgs& a, int bid, int nb
         const int fb = foff[fl], fe = foff[fl + 1];
         if (fe - fb > kBowRegChunks * kWave) continue;  // a large-node block's
         if (tr && lane_id() == 0) tr[2] = (unsigned)__builtin_amdgcn_s_memrealtime();
-        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q, tr);
-        else bow_node<false, false>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q, tr);
+        const int cw = coop ? wave_id() : -1;
+        if (a.f_nleft >= 0) bow_node<false, true>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q, tr, cw);
+        else bow_node<false, false>(a, pr, (int)(g - pr_base), fb, fe, nullptr, nullptr, s_q, tr, cw);
     }
     if (tr && lane_id() == 0) {
         tr[4] = (unsigned)__builtin_amdgcn_s_memrealtime();
@@ -1923,7 +1974,8 @@ static int launch_bow(BowArgs& a, int npairs, hipStream_t st, int big_slots = 1,
         const int ib = (int)std::min<long long>(4096, std::max<long long>(1, (nmf + 1023) / 1024));
         KLAUNCH(k_bow_init, dim3(ib), dim3(256), 0, st, a);
     }
-    const long long want = kf_nodes >= 0 ? (kf_nodes + 3) / 4 : (long long)npairs * 8;
+    // (one pair: a block per KF node, bow_nodes_body's cooperative form)
+    const long long want = kf_nodes >= 0 ? (a.single_nodes >= 0 ? kf_nodes : (kf_nodes + 3) / 4) : (long long)npairs * 8;
     const int blocks = (int)std::min<long long>(65535, std::max<long long>(1, want));
     big_slots = std::max(1, big_slots);
     const int big_blocks = (npairs + kBowBigPairs - 1) / kBowBigPairs * big_slots;
@@ -6478,7 +6530,7 @@ int orbm_search_by_bow_dframe(const orbm_dframe* kf, const uint8_t* kf_mp_valid,
     const int trace_call = orbmi::debug_opt(ORB_OPT_BOW_TRACE);
     if (trace_call != trace_opt) { trace_opt = trace_call; ncall = 0; }
     unsigned* wtrace = nullptr;
-    const int nwtr = (int)((kf->fv_nnodes + 3) / 4 * 4);    // (16 words a wave)
+    const int nwtr = (int)(kf->fv_nnodes * 4);               // (16 words a wave, four waves a node)
     const bool tracing = trace_call > 0 && ++ncall == trace_call;
     if (tracing) {
         if (hipMalloc(&wtrace, (size_t)nwtr * 16 * 4) != hipSuccess ||

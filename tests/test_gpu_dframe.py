@@ -69,6 +69,34 @@ def test_search_by_bow_dframe(gpu_lib, frames, ori, ratio, nodes, zc, debug_opti
         np.testing.assert_array_equal(umatch, rmatch)
 
 
+@pytest.mark.parametrize("nodes,ratio,flips", [(10, 0.9, 6), (16, 1.0, 2), (9, 0.75, 12)])
+def test_search_by_bow_dframe_contention(gpu_lib, frames, nodes, ratio, flips):
+    """Keyframe features that are noisy copies of a few frame features, ~100 of
+    each per node: many features of a node want the same positions, so the
+    ordered walk meets claims that take other features' best / second and
+    lists that run short (the exact lanes-over-positions path), over two
+    64-feature blocks per node."""
+    rng = np.random.default_rng(nodes * 100 + flips)
+    kf, f = frames[0], frames[1]
+    fd = f[1]
+    src = rng.integers(0, len(fd), len(kf[0]) // 8)
+    kd = fd[src[rng.integers(0, len(src), len(kf[0]))]].copy()
+    bits = rng.integers(0, 256, (len(kd), flips))
+    for j in range(flips):
+        kd[np.arange(len(kd)), bits[:, j] // 8] ^= (1 << (bits[:, j] % 8)).astype(np.uint8)
+    knode = rng.integers(0, nodes, len(kd))
+    fnode = rng.integers(0, nodes, len(fd))
+    kfv, ffv = abi.featvec_struct(knode), abi.featvec_struct(fnode)
+    KF = abi.frame_struct(kf[0], kd, 752, 480, scale_factors=SCALE)
+    K, F = dev(KF, kfv), dev(fr(f), ffv)
+    m = orb.ORBmatcher(ratio, True)
+    kvalid = (rng.random(len(knode)) < 0.9).astype(np.uint8)
+    nm, match = m.SearchByBoWDevice(K, kvalid, F)
+    rnm, rmatch = O.search_by_bow(KF, kfv, kvalid, fr(f), ffv, ratio, True)
+    assert nm == rnm and nm > 0
+    np.testing.assert_array_equal(match, rmatch)
+
+
 def test_search_by_bow_dframe_frames_of_other_sizes(gpu_lib, frames):
     """The match scratch the kernel resets for the next call: frames of more
     and fewer keypoints in turn (the scratch grows), every result the oracle's."""
