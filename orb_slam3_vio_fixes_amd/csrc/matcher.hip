@@ -3577,7 +3577,20 @@ __device__ void lds_grid_build(const orb_keypoint* kps, int n, const GridParams&
 // copied into the block's LDS instead of rebuilt.
 __device__ void lds_grid_load(const int* __restrict__ pg, int n, int* gcs) {
     const int tot = kGridInts + max(1, n);
-    for (int c = threadIdx.x; c < tot; c += blockDim.x) gcs[c] = pg[c];
+    // in 16-byte pieces when source and LDS share their alignment (one read a
+    // thread for a thousand-point frame: one HBM round trip, not four)
+    const int hs = (int)((16 - ((uintptr_t)pg & 15)) & 15) >> 2, hd = (int)((16 - ((uintptr_t)gcs & 15)) & 15) >> 2;
+    if (hs == hd && ((uintptr_t)pg & 3) == 0) {
+        const int body = (tot - hs) >> 2;
+        const uint4* src = (const uint4*)(pg + hs);
+        uint4* dst = (uint4*)(gcs + hs);
+        for (int c = threadIdx.x; c < body; c += blockDim.x) dst[c] = src[c];
+        const int t0 = hs + body * 4;
+        if ((int)threadIdx.x < hs) gcs[threadIdx.x] = pg[threadIdx.x];
+        if ((int)threadIdx.x < tot - t0) gcs[t0 + threadIdx.x] = pg[t0 + threadIdx.x];
+    } else {
+        for (int c = threadIdx.x; c < tot; c += blockDim.x) gcs[c] = pg[c];
+    }
     __syncthreads();
 }
 

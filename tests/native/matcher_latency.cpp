@@ -205,6 +205,7 @@ int main(int argc, char** argv)
                 check(nm, "SearchForInitialization(dframe)");
             });
             put("search_for_initialization_dframe", sd);
+            stats("search_for_initialization_dframe");
             dm12.resize(n1);
             dm12.push_back(nm);
             save(pre + "_sfi_dframe.bin", dm12.data(), dm12.size());
@@ -249,6 +250,7 @@ int main(int argc, char** argv)
                 check(nm, "SearchByProjection(dframe, LastFrame)");
             });
             put("search_by_projection_last_dframe", sd);
+            stats("search_by_projection_last_dframe");
             down.resize(n2);
             down.push_back(nm);
             save(pre + "_last_dframe.bin", down.data(), down.size());
@@ -290,6 +292,7 @@ int main(int argc, char** argv)
                 check(nm, "SearchByProjection(dframe, MapPoints)");
             });
             put("search_by_projection_mps_dframe", sd);
+            stats("search_by_projection_mps_dframe");
             down.resize(n2);
             down.push_back(nm);
             save(pre + "_mps_dframe.bin", down.data(), down.size());
