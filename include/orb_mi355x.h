@@ -254,6 +254,12 @@ int orbx_pyramid_kernel(orbx_handle* h);
  *   ORB_OPT_BOW_TRACE    diagnostics: n > 0 makes the n-th
  *                        orbm_search_by_bow_dframe call after it is set print
  *                        its small-node waves' checkpoints to stderr
+ *   ORB_OPT_QT_FORM      DistributeOctTree: 0 one 4-wave workgroup per (frame,
+ *                        level), 1 one wave per (frame, level) with the keys
+ *                        in registers (levels of more than 1,536 keys go to
+ *                        the 4-wave form in a fixup launch), n >= 2: the
+ *                        one-wave form with a key capacity of n - 2 (levels
+ *                        beyond it take the fixup path)
  * The two k_pyr_stream options are read when a handle builds its plan (the
  * first extraction of a size).
  * orb_debug_set_option returns ORB_OK or ORB_ERR_PARAM; get returns the value
@@ -269,7 +275,8 @@ enum {
     ORB_OPT_UPLOAD = 7,
     ORB_OPT_FAST_CAND_CAP = 8,
     ORB_OPT_BOW_TRACE = 9,
-    ORB_OPT_COUNT = 10
+    ORB_OPT_QT_FORM = 10,
+    ORB_OPT_COUNT = 11
 };
 int orb_debug_set_option(int option, int value);
 int orb_debug_get_option(int option);

@@ -37,7 +37,7 @@ EXPORTS = [
 
 # orb_debug_set_option keys (include/orb_mi355x.h): alternative kernel forms
 (ORB_OPT_PROJ_FORM, ORB_OPT_BOW_FORM, ORB_OPT_BOWK_BIG, ORB_OPT_PYR_CNT_END, ORB_OPT_PYR_PRETEST, ORB_OPT_SFI_FORM,
- ORB_OPT_HOST_OUT, ORB_OPT_UPLOAD, ORB_OPT_FAST_CAND_CAP, ORB_OPT_BOW_TRACE) = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9
+ ORB_OPT_HOST_OUT, ORB_OPT_UPLOAD, ORB_OPT_FAST_CAND_CAP, ORB_OPT_BOW_TRACE, ORB_OPT_QT_FORM) = 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10
 
 _lib = None
 

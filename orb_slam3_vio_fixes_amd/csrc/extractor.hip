@@ -668,6 +668,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
         if (qgs) ORB_CHECK(hipMalloc(&P.d_qt_gscr, B * L * qgs));
     }
     ORB_CHECK(hipMalloc(&P.d_qt_n, B * L * sizeof(int)));
+    ORB_CHECK(hipMalloc(&P.d_qt_ovf, B * L * sizeof(int)));
     ORB_CHECK(hipMalloc(&P.d_angle, B * P.out_total * sizeof(float)));
     ORB_CHECK(hipMalloc(&P.d_sdesc, B * P.out_total * 32));
     P.host_cap = P.out_total;
@@ -2380,6 +2381,9 @@ struct QtArgs {
     int lds_bytes;          // dynamic LDS of the launch
     uint8_t* gscr;          // k_quadtree<true>: [B][L] node arrays of levels beyond the LDS
     long long gscr_stride;
+    int* qt_ovf;            // [B][L]: k_quadtree_w left the level to k_quadtree (more keys than kcap)
+    int fixup;              // k_quadtree: only the levels whose qt_ovf is set
+    int qw_nc, qw_kcap;     // k_quadtree_w: node capacity of the LDS layout; key capacity (<= 64 KPL)
 };
 
 // Bytes of a level's node arrays (NC = out_cap + 8 nodes: the list never
@@ -2741,6 +2745,7 @@ __global__ __launch_bounds__(ORB_QT_THREADS) void k_quadtree(QtArgs a) {
 #else
     const int l = blockIdx.x, f = blockIdx.y, tid = threadIdx.x, T = blockDim.x;
 #endif
+    if (a.fixup && !a.qt_ovf[f * a.L + l]) return;   // k_quadtree_w distributed this level
     const LevelDev lv = a.lv[l];
     const int NC = lv.out_cap + 8;
 #ifdef ORB_QT_TIMING
@@ -2964,6 +2969,555 @@ __global__ __launch_bounds__(ORB_QT_THREADS) void k_quadtree(QtArgs a) {
 #ifdef ORB_QT_TIMING
     QT_T(4);
     if (tid == 0) {
+        atomicMax(&g_qt_t[l][8], __builtin_amdgcn_s_memtime() - qt_t0);
+        atomicAdd(&g_qt_t[l][9], (unsigned long long)qt_outer);
+        atomicAdd(&g_qt_t[l][10], (unsigned long long)qt_lastr);
+        atomicAdd(&g_qt_t[l][11], 1ull);
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------
+// k_quadtree_w: the same DistributeOctTree steps (ORBextractor.cc:555-779) for
+// one (frame, level) by ONE wave, with the keys in registers.
+//
+// k_quadtree spends 82-103 us per 256 frames at 3 % VALU issue: its keys live
+// in global memory, so every pass over them (gather, quadrant count, remap,
+// retain) is a round trip to L2 per 1,024 keys, and each pass has a dozen
+// block barriers between its four waves.  A level of C2 holds 300-1,500 keys
+// and at most ~230 nodes, which one wave holds comfortably: lane l keeps the
+// run of keys l KPL .. l KPL + KPL - 1 (vToDistributeKeys order: cell by cell,
+// so a lane's keys mostly share a node) and each key's list index (bits 0-15;
+// its quadrant in bits 16+ between the count and the remap).  Per-key passes
+// are branch-free register work plus LDS reads of the key's node, and their
+// LDS atomics are aggregated over a lane's run (a target word that stays the
+// same accumulates in a register; the first passes have 2-8 nodes, so
+// per-key atomics were thousands of same-address conflicts).  Per-node passes
+// walk the list in 64-node chunks with ballots and DPP scans;
+// synchronisation is the wave's own.  Node arrays stay in LDS, indexed by
+// list position, double buffered across a rebuild.  nomore is cnt == 1 (a
+// node never changes its count), so it is not stored.  A level with more than
+// qw_kcap keys sets its overflow flag and is left to k_quadtree, launched
+// after this kernel in fixup mode (only flagged levels run there).
+// ---------------------------------------------------------------------------
+#ifndef ORB_QW_KPL
+#define ORB_QW_KPL 24   // keys per lane: levels of up to 1,536 keys (235 VGPRs; 32 spills 50)
+#endif
+constexpr int kQwKpl = ORB_QW_KPL;
+#ifndef ORB_QW_WAVES
+#define ORB_QW_WAVES 2   // 8 waves a CU (2,048 (frame, level) waves over 256 CUs)
+#endif
+constexpr size_t kQwLdsMax = 64 * 1024;   // larger layouts (Tracking's 5 x nFeatures extractor) keep k_quadtree
+
+struct QwLds {
+    short4* rect[2];
+    int* cnt[2];
+    uint32_t* cc;   // per node: quadrant counts (q0 | q1 << 16, q2 | q3 << 16)
+    int* nb;        // per node: first child (divided) or new index (kept); initial bins: list position
+    uint8_t* dv;    // per node: divides in this step
+    int* ord;       // processing order of the dividing nodes
+    int* queue;     // vSizeAndPointerToNode: children with > 1 key, processing order (list indices)
+    SortRec* srt;
+    uint32_t* mg;   // per node: its split point in the keys' guarded format (qw_guard)
+    uint32_t* dum;  // one word per lane: the no-op target of the run-aggregated atomics
+    uint8_t* u;     // shared by the gather, the divide's scans and the sort
+};
+__host__ __device__ inline size_t qw_al(size_t b) { return (b + 15) & ~size_t(15); }
+// the union region: the gather (cell offsets, key cells), the divide's three
+// scans, block_std_sort's scratch
+__host__ __device__ inline size_t qw_union_bytes(int NC, int ncells, int kcap) {
+    const size_t n = (size_t)NC;
+    const size_t g = qw_al((size_t)(ncells + 1) * 4) + qw_al((size_t)kcap * 2);
+    const size_t d = 3 * qw_al(n * 4);
+    const size_t s = qw_al(n * sizeof(SortRec)) + 2 * qw_al(n * 4) + 2 * qw_al((n / 17 + 2) * sizeof(SortFrame)) +
+                     qw_al((n + 2) * 4) + qw_al(16) + qw_al(80 * sizeof(SortFrame));
+    return g > d ? (g > s ? g : s) : (d > s ? d : s);
+}
+__host__ __device__ inline size_t qw_lds_bytes(int NC, int ncells, int kcap) {
+    const size_t n = (size_t)NC;
+    return 2 * qw_al(n * 8) + 2 * qw_al(n * 4) + qw_al(n * 8) + qw_al(n * 4) + qw_al(n) + 2 * qw_al(n * 4) +
+           qw_al(n * sizeof(SortRec)) + qw_al(n * 4) + qw_al(kWave * 4) + qw_union_bytes(NC, ncells, kcap);
+}
+
+// keys of a per-key pass in groups of kQwGrp: a compiler fence between
+// groups keeps it from hoisting every key's LDS reads at once (spills)
+#ifndef ORB_QW_GRP
+#define ORB_QW_GRP 8
+#endif
+#define QW_GROUP_FENCE(j) do { if (((j) + 1) % ORB_QW_GRP == 0) asm volatile("" ::: "memory"); } while (0)
+
+// Keys in registers in a guarded format: x | 1 << 12 | y << 13 | 1 << 25.
+// With a node's split point (mx, my) as mx | my << 13, one subtraction
+// compares both coordinates: bit 12 of the difference is x >= mx, bit 25 is
+// y >= my (the guard bits absorb the borrows), so ExtractorNode::DivideNode's
+// child (:511-525) is bit 12 | bit 25 >> 24 -- no unpacking a compiler could
+// hoist out of the passes (it kept every key's x and y live: spills).
+__device__ __forceinline__ uint32_t qw_guard(uint32_t key) {
+    return (key & 0xfffu) | ((key & 0xfff000u) << 1) | 0x2001000u;
+}
+__device__ __forceinline__ uint32_t qw_unguard(uint32_t g, uint32_t resp) {
+    return (g & 0xfffu) | ((g >> 1) & 0xfff000u) | (resp << 24);
+}
+__device__ __forceinline__ uint32_t qw_split(short4 r) {
+    const int hx = (int)ceilf((float)(r.z - r.x) / 2), hy = (int)ceilf((float)(r.w - r.y) / 2);
+    return (uint32_t)(r.x + hx) | ((uint32_t)(r.y + hy) << 13);
+}
+__device__ __forceinline__ int qw_quadrant(uint32_t g, uint32_t split) {
+    const uint32_t d = g - split;
+    return (int)(((d >> 12) & 1u) | ((d >> 24) & 2u));
+}
+
+__device__ __forceinline__ int qw_cc(const uint32_t* cc, int i, int q) {
+    return (int)((cc[2 * i + (q >> 1)] >> (16 * (q & 1))) & 0xffffu);
+}
+
+// One step of a lane's run-aggregated LDS add: while the target word w stays
+// the same the increments accumulate in acc; a changed target flushes the run
+// into the previous word, every other step adds 0 to the lane's own dum word
+// (no branch, no same-address conflict).  pw starts at kNoWord; qw_add_end
+// flushes the last run.
+constexpr uint32_t kNoWord = 0xffffffffu;
+__device__ __forceinline__ void qw_add(uint32_t* base, uint32_t* mine, uint32_t w, uint32_t inc, uint32_t& pw,
+                                       uint32_t& acc) {
+    const bool flush = w != pw;
+    atomicAdd(flush && pw != kNoWord ? base + pw : mine, flush ? acc : 0u);
+    acc = flush ? inc : acc + inc;
+    pw = w;
+}
+__device__ __forceinline__ void qw_add_end(uint32_t* base, uint32_t pw, uint32_t acc) {
+    if (pw != kNoWord) atomicAdd(base + pw, acc);
+}
+
+// Divide ord[0..m) (counts in cc, dv set for exactly those nodes), rebuild the
+// list into buffer cur ^ 1 (children blocks n4..n1 in REVERSE processing
+// order, then the kept nodes in their old order: push_front + erase,
+// ORBextractor.cc:633-679, :703-744), queue the children with > 1 key in
+// processing order, remap the keys.  Returns the new size.
+template <int KPL>
+__device__ int qw_divide(QwLds& s, int& cur, int size, int m, uint32_t (&nq)[KPL], int NC, int& nexp) {
+    const int lane = lane_id();
+    int* rne = (int*)s.u;     // per rank: inclusive scan of the non-empty children
+    int* rgt = rne + NC;      // per rank: exclusive scan of the children with > 1 key
+    int* ndx = rgt + NC;      // per node: kept nodes before it
+    int cne = 0, cgt = 0;
+    for (int base = 0; base < m; base += kWave) {
+        const int r = base + lane;
+        int ne = 0, gt = 0;
+        if (r < m) {
+            const int i = s.ord[r];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int c = qw_cc(s.cc, i, q);
+                ne += c > 0;
+                gt += c > 1;
+            }
+        }
+        const int ine = wave_incl_scan_dpp(ne), igt = wave_incl_scan_dpp(gt);
+        if (r < m) {
+            rne[r] = cne + ine;
+            rgt[r] = cgt + igt - gt;
+        }
+        cne += __builtin_amdgcn_readlane(ine, kWave - 1);
+        cgt += __builtin_amdgcn_readlane(igt, kWave - 1);
+    }
+    int cnd = 0;
+    for (int base = 0; base < size; base += kWave) {
+        const int i = base + lane;
+        const bool kept = i < size && !s.dv[i];
+        const uint64_t b = __ballot(kept);
+        if (kept) ndx[i] = cnd + mask_rank(b);
+        cnd += __popcll(b);
+    }
+    const int totNE = cne;
+    const int nx = cur ^ 1;
+    const short4* R = qsel(s.rect, cur);
+    const int* C = qsel(s.cnt, cur);
+    short4* Rn = qsel(s.rect, nx);
+    int* Cn = qsel(s.cnt, nx);
+    for (int r = lane; r < m; r += kWave) {
+        const int i = s.ord[r];
+        const short4 ri = R[i];
+        int c[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) c[q] = qw_cc(s.cc, i, q);
+        const int start = totNE - rne[r];
+        int w = start;
+        int pos[4];
+#pragma unroll
+        for (int q = 3; q >= 0; --q) {
+            pos[q] = w;
+            if (c[q] > 0) {
+                Rn[w] = child_rect(ri, q);
+                Cn[w] = c[q];
+                ++w;
+            }
+        }
+        s.nb[i] = start;
+        int e = rgt[r];
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (c[q] > 1) s.queue[e++] = pos[q];
+    }
+    for (int i = lane; i < size; i += kWave) {
+        if (s.dv[i]) continue;
+        const int np = totNE + ndx[i];
+        s.nb[i] = np;
+        Rn[np] = R[i];
+        Cn[np] = C[i];
+    }
+    fast_wave_sync();
+    // keys: a divided node's child q sits at first child + its non-empty
+    // siblings q' > q (n4 first); a kept node moved to nb
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int n = (int)(nq[j] & 0xffffu), q = (int)(nq[j] >> 16);
+        const int d = s.dv[n], b = s.nb[n];
+        const uint32_t w0 = s.cc[2 * n], w1 = s.cc[2 * n + 1];
+        const int above = (q < 3 && (w1 >> 16) != 0u) + (q < 2 && (w1 & 0xffffu) != 0u) + (q < 1 && (w0 >> 16) != 0u);
+        nq[j] = (uint32_t)(b + (d ? above : 0));
+        QW_GROUP_FENCE(j);
+    }
+    fast_wave_sync();
+    cur = nx;
+    nexp = cgt;
+    return totNE + (size - m);
+}
+
+// Quadrant counts of every node with dv set; every key keeps its quadrant in
+// nq bits 16+ (read by qw_divide only for keys of dividing nodes).
+template <int KPL>
+__device__ void qw_count(QwLds& s, int cur, int size, const uint32_t (&key)[KPL], uint32_t (&nq)[KPL]) {
+    const int lane = lane_id();
+    const short4* R = qsel(s.rect, cur);
+    for (int i = lane; i < size; i += kWave) {
+        s.cc[2 * i] = 0u;
+        s.cc[2 * i + 1] = 0u;
+        s.mg[i] = qw_split(R[i]);
+    }
+    fast_wave_sync();
+    uint32_t pw = kNoWord, acc = 0u;
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int n = (int)nq[j];
+        const int d = s.dv[n];
+        const int q = qw_quadrant(key[j], s.mg[n]);
+        nq[j] = (uint32_t)n | ((uint32_t)q << 16);
+        qw_add(s.cc, s.dum + lane, 2u * (uint32_t)n + (uint32_t)(q >> 1), d ? 1u << (16 * (q & 1)) : 0u, pw, acc);
+        QW_GROUP_FENCE(j);
+    }
+    qw_add_end(s.cc, pw, acc);
+    fast_wave_sync();
+}
+
+template <int KPL>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ORB_QW_WAVES))) void k_quadtree_w(QtArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int f = blockIdx.x, l = blockIdx.y, lane = threadIdx.x;
+    const LevelDev lv = a.lv[l];
+    const int NC = a.qw_nc;
+#ifdef ORB_QT_TIMING
+    const int tid = lane;
+    const unsigned long long qt_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long qt_last = qt_t0;
+    int qt_outer = 0, qt_lastr = 0;
+#endif
+    QwLds s;
+    {
+        uint8_t* p = smem;
+        auto take = [&](size_t bytes) { uint8_t* q = p; p += qw_al(bytes); return q; };
+        s.rect[0] = (short4*)take(NC * 8);
+        s.rect[1] = (short4*)take(NC * 8);
+        s.cnt[0] = (int*)take(NC * 4);
+        s.cnt[1] = (int*)take(NC * 4);
+        s.cc = (uint32_t*)take(NC * 8);
+        s.nb = (int*)take(NC * 4);
+        s.dv = take(NC);
+        s.ord = (int*)take(NC * 4);
+        s.queue = (int*)take(NC * 4);
+        s.srt = (SortRec*)take(NC * sizeof(SortRec));
+        s.mg = (uint32_t*)take(NC * 4);
+        s.dum = (uint32_t*)take(kWave * 4);
+        s.u = p;
+    }
+    const int nc = lv.ncells;
+    const int* ccount = a.cell_count + (long long)f * a.ncells_total + lv.cell_base;
+    const uint32_t* cslots = a.cell_keys + (long long)f * a.slot_total + lv.slot_base;
+    uint32_t* out = a.qt_key + (long long)f * a.out_total + lv.out_base;
+
+    // 1. vToDistributeKeys (:805-872): cell offsets by one scan, lane l over a
+    // contiguous run of cells; then the cell of every key, and the keys
+    int* off = (int*)s.u;
+    uint16_t* kcell = (uint16_t*)(s.u + qw_al((size_t)(nc + 1) * 4));
+    for (int cb = 0; cb < nc; cb += 16 * kWave) {   // 16 loads a lane in flight (a load-store loop waited on each)
+        int v[16];
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int c = cb + t * kWave + lane;
+            v[t] = c < nc ? ccount[c] : 0;
+        }
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int c = cb + t * kWave + lane;
+            if (c < nc) off[c] = v[t];
+        }
+    }
+    fast_wave_sync();
+    const int per = (nc + kWave - 1) / kWave;
+    const int c0 = min(nc, lane * per), c1 = min(nc, c0 + per);
+    int sum = 0;
+    for (int c = c0; c < c1; ++c) sum += off[c];
+    const int incl = wave_incl_scan_dpp(sum);
+    const int K = __builtin_amdgcn_readlane(incl, kWave - 1);
+    if (K > a.qw_kcap) {
+        if (lane == 0) a.qt_ovf[f * a.L + l] = 1;
+        return;
+    }
+    if (lane == 0) a.qt_ovf[f * a.L + l] = 0;
+    if (K == 0) {
+        if (lane == 0) a.qt_n[f * a.L + l] = 0;
+        return;
+    }
+    {
+        int run = incl - sum;
+        for (int c = c0; c < c1; ++c) {
+            const int x = off[c];
+            off[c] = run;
+            run += x;
+        }
+        if (lane == 0) off[nc] = K;
+    }
+    fast_wave_sync();
+    // key k's cell at (k % KPL) * 64 + k / KPL: lane l reads its run's j-th
+    // cell at j * 64 + l (a straight index would put lanes l and l + 4 in one bank)
+    for (int c = c0; c < c1; ++c)
+        for (int j = off[c], e = off[c + 1]; j < e; ++j) kcell[(j % KPL) * kWave + j / KPL] = (uint16_t)c;
+    fast_wave_sync();
+    const int cap = lv.slot_total / nc;
+    const int k0 = lane * KPL;   // this lane's run of keys
+    uint32_t key[KPL], nq[KPL];  // key: guarded x, y (qw_guard)
+    uint32_t rs[(KPL + 3) / 4];  // responses, 4 bytes a register
+    {
+        int src[KPL];
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const int k = k0 + j;
+            const int c = k < K ? (int)kcell[j * kWave + lane] : 0;
+            src[j] = k < K ? c * cap + (k - off[c]) : -1;
+        }
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) key[j] = src[j] >= 0 ? cslots[src[j]] : 0u;
+#pragma unroll
+        for (int j = 0; j < (KPL + 3) / 4; ++j) rs[j] = 0u;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) rs[j / 4] |= (key[j] >> 24) << (8 * (j % 4));
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) key[j] = qw_guard(key[j]);
+    }
+    fast_wave_sync();   // off / kcell (the union region) are dead from here
+    QT_T(0);
+#ifndef ORB_QW_ABL
+#define ORB_QW_ABL 0   // timing ablation (tools only; wrong results): return after phase 1 gather, 2 init, 3 outer, 4 last rounds
+#endif
+#define QW_ABL_RETURN(p)                                           \
+    do {                                                           \
+        if (ORB_QW_ABL == (p)) {                                   \
+            if (lane == 0) a.qt_n[f * a.L + l] = 0;                \
+            if (lane == 0 && key[0] == 12345u) out[0] = nq[0];     \
+            return;                                                \
+        }                                                          \
+    } while (0)
+    if (ORB_QW_ABL == 1)
+        for (int j = 0; j < KPL; ++j) nq[j] = 0;
+    QW_ABL_RETURN(1);
+
+    // 2. the initial nodes (:559-601): key k in bin x / hX (vpIniNodes), empty
+    // bins dropped, the rest in bin order; nomore = one key.  Keys k >= K (the
+    // register slots past the level's keys) sit in the dummy node NC - 1:
+    // never in the list, never dividing, remapped onto itself.
+    const int nIni = lv.nIni;
+    const int dummy = NC - 1;
+    int* bcnt = s.cnt[1];
+    for (int i = lane; i < nIni; i += kWave) bcnt[i] = 0;
+    if (lane == 0) {
+        s.dv[dummy] = 0;
+        s.nb[dummy] = dummy;
+    }
+    fast_wave_sync();
+    {
+        uint32_t pw = kNoWord, acc = 0u;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const bool ok = k0 + j < K;
+            const int bn = ok ? (int)((float)(key[j] & 0xfff) / lv.hX) : 0;
+            nq[j] = ok ? (uint32_t)bn : (uint32_t)dummy;
+            qw_add((uint32_t*)bcnt, s.dum + lane, (uint32_t)bn, ok ? 1u : 0u, pw, acc);
+        }
+        qw_add_end((uint32_t*)bcnt, pw, acc);
+    }
+    fast_wave_sync();
+    int size = 0;
+    for (int base = 0; base < nIni; base += kWave) {
+        const int i = base + lane;
+        const int c = i < nIni ? bcnt[i] : 0;
+        const uint64_t b = __ballot(c > 0);
+        if (c > 0) {
+            const int pos = size + mask_rank(b);
+            s.nb[i] = pos;
+            s.rect[0][pos] = make_short4((short)(int)(lv.hX * (float)i), 0, (short)(int)(lv.hX * (float)(i + 1)),
+                                         (short)lv.qH);
+            s.cnt[0][pos] = c;
+        }
+        size += __popcll(b);
+    }
+    fast_wave_sync();
+    if (size != nIni) {
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            nq[j] = (uint32_t)s.nb[nq[j]];
+            QW_GROUP_FENCE(j);
+        }
+        fast_wave_sync();
+    }
+    int cur = 0;
+    const int N = lv.N;
+    QT_T(1);
+    QW_ABL_RETURN(2);
+
+    // 3. outer passes (:610-689): every node with > 1 key divides, in list order
+    int nexp = 0;
+    bool last = false;
+    while (true) {
+        const int prev = size;
+        int m = 0;
+        const int* C = qsel(s.cnt, cur);
+        for (int base = 0; base < size; base += kWave) {
+            const int i = base + lane;
+            const bool d = i < size && C[i] > 1;
+            const uint64_t b = __ballot(d);
+            if (i < size) s.dv[i] = d;
+            if (d) s.ord[m + mask_rank(b)] = i;
+            m += __popcll(b);
+        }
+        fast_wave_sync();
+#ifdef ORB_QT_TIMING
+        ++qt_outer;
+        QT_T(5);
+#endif
+        qw_count<KPL>(s, cur, size, key, nq);
+        QT_T(6);
+        size = qw_divide<KPL>(s, cur, size, m, nq, NC, nexp);
+        QT_T(7);
+        if (size >= N || size == prev) break;
+        if (size + nexp * 3 > N) {
+            last = true;
+            break;
+        }
+    }
+    QW_ABL_RETURN(3);
+    // 4. last rounds (:692-753): the queue sorted by (count, UL.x) with the
+    // libstdc++ std::sort port, divided from the largest until the list holds N
+    while (last) {
+        const int prev = size;
+        const int m = nexp;
+        {
+            const short4* R = qsel(s.rect, cur);
+            const int* C = qsel(s.cnt, cur);
+            for (int j = lane; j < m; j += kWave) {
+                const int i = s.queue[j];
+                s.srt[j] = SortRec{C[i], (int)R[i].x, i};
+            }
+            for (int i = lane; i < size; i += kWave) s.dv[i] = 0;
+        }
+        fast_wave_sync();
+        QT_T(15);
+        {
+            uint8_t* p = s.u;
+            auto take = [&](size_t bytes) { uint8_t* q = p; p += qw_al(bytes); return q; };
+            SortRec* backup = (SortRec*)take(NC * sizeof(SortRec));
+            int* Lp = (int*)take(NC * 4);
+            int* Rp = (int*)take(NC * 4);
+            SortFrame* qa = (SortFrame*)take((NC / 17 + 2) * sizeof(SortFrame));
+            SortFrame* qb = (SortFrame*)take((NC / 17 + 2) * sizeof(SortFrame));
+            int* leaves = (int*)take((NC + 2) * 4);
+            int* ctl = (int*)take(16);
+            SortFrame* stk = (SortFrame*)take(80 * sizeof(SortFrame));
+            block_std_sort(s.srt, m, backup, Lp, Rp, qa, qb, leaves, ctl, stk);
+        }
+        for (int j = lane; j < m; j += kWave) s.dv[s.srt[j].pos] = 1;
+        fast_wave_sync();
+        QT_T(12);
+        qw_count<KPL>(s, cur, size, key, nq);
+        QT_T(13);
+        // processing rank r = m-1-j; stop after the first rank at which the list reaches N
+        int mp = m, carry = 0;
+        for (int base = 0; base < m; base += kWave) {
+            const int r = base + lane;
+            int d = 0;
+            if (r < m) {
+                const int i = s.srt[m - 1 - r].pos;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) d += qw_cc(s.cc, i, q) > 0;
+                d -= 1;
+            }
+            const int inc = wave_incl_scan_dpp(d);
+            const uint64_t hit = __ballot(r < m && size + carry + inc >= N);
+            if (hit) {
+                mp = base + (int)__builtin_ctzll(hit) + 1;
+                break;
+            }
+            carry += __builtin_amdgcn_readlane(inc, kWave - 1);
+        }
+        for (int r = lane; r < m; r += kWave) {
+            const int i = s.srt[m - 1 - r].pos;
+            if (r < mp) s.ord[r] = i;
+            else s.dv[i] = 0;
+        }
+        fast_wave_sync();
+        QT_T(15);
+        size = qw_divide<KPL>(s, cur, size, mp, nq, NC, nexp);
+        QT_T(14);
+#ifdef ORB_QT_TIMING
+        ++qt_lastr;
+#endif
+        if (size >= N || size == prev) break;
+    }
+    QT_T(3);
+    QW_ABL_RETURN(4);
+    // 5. retain the best key per node (:757-776): max response, the first in
+    // vToDistributeKeys order on ties (key k scores (response << 23) | (2^23 -
+    // 1 - k), distinct per key); the winner writes its node's slot
+    int* best = (int*)s.cc;
+    for (int i = lane; i < size; i += kWave) best[i] = 0;
+    fast_wave_sync();
+    {
+        uint32_t pw = kNoWord;
+        int acc = 0;
+#pragma unroll
+        for (int j = 0; j < KPL; ++j) {
+            const uint32_t resp = (rs[j / 4] >> (8 * (j % 4))) & 0xffu;
+            const int v = (int)((resp << 23) | (uint32_t)(0x7FFFFF - (k0 + j)));
+            const uint32_t w = nq[j];
+            const bool flush = w != pw;
+            atomicMax(flush && pw != kNoWord ? best + pw : (int*)(s.dum + lane), flush ? acc : 0);
+            acc = flush ? v : max(acc, v);
+            pw = w;
+            QW_GROUP_FENCE(j);
+        }
+        atomicMax(best + pw, acc);
+    }
+    fast_wave_sync();
+    const int nout = min(size, lv.out_cap);   // (the dummy node is >= size)
+#pragma unroll
+    for (int j = 0; j < KPL; ++j) {
+        const int n = (int)nq[j];
+        const uint32_t resp = (rs[j / 4] >> (8 * (j % 4))) & 0xffu;
+        if (n < nout && best[n] == (int)((resp << 23) | (uint32_t)(0x7FFFFF - (k0 + j)))) out[n] = qw_unguard(key[j], resp);
+        QW_GROUP_FENCE(j);
+    }
+    if (lane == 0) a.qt_n[f * a.L + l] = nout;
+#ifdef ORB_QT_TIMING
+    QT_T(4);
+    if (lane == 0) {
         atomicMax(&g_qt_t[l][8], __builtin_amdgcn_s_memtime() - qt_t0);
         atomicAdd(&g_qt_t[l][9], (unsigned long long)qt_outer);
         atomicAdd(&g_qt_t[l][10], (unsigned long long)qt_lastr);
@@ -3963,6 +4517,7 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
     P.d_kq = P0.d_kq + F * P0.slot_total;
     P.d_qt_key = P0.d_qt_key + F * P0.out_total;
     P.d_qt_n = P0.d_qt_n + F * L;
+    P.d_qt_ovf = P0.d_qt_ovf + F * L;
     P.d_angle = P0.d_angle + F * P0.out_total;
     P.d_sdesc = P0.d_sdesc + F * P0.out_total * 32;
     d_frames += F * fstride;
@@ -4089,7 +4644,34 @@ static int run_pipeline(orbx_handle* hd, int f0, int B, const uint8_t* d_frames,
 #else
         const dim3 qg(L, B);
 #endif
-        ORB_LAUNCH(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(ORB_QT_THREADS), qlds, st, qa);
+        qa.qt_ovf = P.d_qt_ovf;
+        qa.fixup = 0;
+        // k_quadtree (4 waves per (frame, level)) by default; ORB_OPT_QT_FORM
+        // >= 1 selects k_quadtree_w (one wave per (frame, level)) where the
+        // plan keeps every level's node arrays in LDS and the one-wave layout
+        // fits kQwLdsMax.  Same-box A/B: the one-wave form is
+        // no faster on the 256-frame batch (96-105 vs 92-101 us; its level-0
+        // wave is a 170k-cycle latency chain) and slower on one frame (70 vs
+        // 50 us), and C2 frames reach 1,612 level-0 keys, past its register
+        // capacity (the fixup path)
+        const int form = debug_opt(ORB_OPT_QT_FORM);
+        int ncm = 0, ncells_m = 0;
+        for (const LevelDev& d : P0.lv) {
+            ncm = std::max(ncm, d.out_cap + 8);
+            ncells_m = std::max(ncells_m, d.ncells);
+        }
+        const int kcap = form >= 2 ? std::min(form - 2, 64 * kQwKpl) : 64 * kQwKpl;
+        const size_t qwl = qw_lds_bytes(ncm, ncells_m, 64 * kQwKpl);   // (key cells at swizzled slots of all 64 KPL)
+        if (form >= 1 && !qgs && qwl <= kQwLdsMax && ncells_m < 65536) {
+            qa.qw_nc = ncm;
+            qa.qw_kcap = kcap;
+            ORB_LAUNCH(k_quadtree_w<kQwKpl>, dim3(B, L), dim3(kWave), qwl, st, qa);
+            // the levels with more keys than kcap (flagged), by k_quadtree
+            qa.fixup = 1;
+            ORB_LAUNCH(k_quadtree<false>, qg, dim3(ORB_QT_THREADS), qlds, st, qa);
+        } else {
+            ORB_LAUNCH(qgs ? k_quadtree<true> : k_quadtree<false>, qg, dim3(ORB_QT_THREADS), qlds, st, qa);
+        }
     }
     mark();
     // describe

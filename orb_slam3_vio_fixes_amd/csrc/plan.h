@@ -105,6 +105,7 @@ struct Plan {
     uint8_t* d_kq = nullptr;
     uint32_t* d_qt_key = nullptr;
     int* d_qt_n = nullptr;
+    int* d_qt_ovf = nullptr;         // [maxB][L] k_quadtree_w overflow flags (levels left to k_quadtree)
     float* d_angle = nullptr;
     uint8_t* d_sdesc = nullptr;
     uint8_t* d_slot_level = nullptr;
@@ -125,7 +126,7 @@ struct Plan {
     void release() {
         void* ps[] = {d_pyr, d_in, d_tab, d_lv, d_cells, d_cell_count, d_cell_keys, d_key_scr,
                       d_knode, d_kq, d_qt_key, d_qt_n, d_angle, d_sdesc, d_kps, d_desc, d_n, d_mono,
-                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_bm, d_qt_gscr};
+                      d_slot_level, d_pband, d_pxs, d_pxw, d_pyt, d_ps_tab, d_bm, d_qt_gscr, d_qt_ovf};
         for (void* p : ps)
             if (p) (void)hipFree(p);
         *this = Plan();
