@@ -4410,12 +4410,15 @@ __global__ __launch_bounds__(ORB_ASM_THREADS) void k_assemble(AsmArgs a) {
 // ---------------------------------------------------------------------------
 // k_quadtree's launch LDS (the largest level that fits kLdsMax) and the
 // global slice size of the levels that do not (0: none)
+#ifndef ORB_QT_GLOBAL_NODES
+#define ORB_QT_GLOBAL_NODES 0   // 1: every level's node arrays in global scratch (no LDS: co-residency A/B)
+#endif
 static void qt_lds_split(const Plan& P, size_t& lds, size_t& gstride) {
     lds = 0;
     gstride = 0;
     for (const LevelDev& d : P.lv) {
         const size_t b = qt_scratch_bytes(d.out_cap + 8, d.ncells);
-        if (b <= (size_t)kLdsMax) lds = std::max(lds, b);
+        if (b <= (size_t)kLdsMax && !ORB_QT_GLOBAL_NODES) lds = std::max(lds, b);
         else gstride = std::max(gstride, (b + 255) & ~size_t(255));
     }
 }

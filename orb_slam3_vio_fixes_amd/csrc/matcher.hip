@@ -3517,6 +3517,10 @@ constexpr int kFusedThreads = 1024;
 constexpr int kFusedQpt = 8;                        // queries per thread in phase 2 (nq <= 8192)
 constexpr int kFusedMaxN = 4096;                    // 12-bit keypoint index in the order key
 constexpr int kFusedMaxQ = kFusedThreads * kFusedQpt;
+#ifndef ORB_PROJ_WIN
+#define ORB_PROJ_WIN 0   // phase-2 fixpoint window of queries (0: every query each round; 1024 measured slower: 13 rounds instead of 6 at ~5.5 k cycles each, phase 2 138 k vs 108 k cycles, profiles/r06/README.md)
+#endif
+constexpr int kProjWin = ORB_PROJ_WIN;
 constexpr uint32_t kFusedNone = 0xffffffffu;
 
 // byte offsets of k_proj_fused's phase-2 tables, every table 16-byte aligned
@@ -3834,22 +3838,32 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
     const uint4* Lsrc = lds_lists ? (const uint4*)Ls : (const uint4*)lists;
     const int* Csrc = lds_lists ? Cs : cnt;
     int settled = 0;          // queries below it decided the same in the last two rounds: final
+    // The fixpoint runs over a window of queries [settled, wend) at a time:
+    // the claims of the queries before the window are final, so a window
+    // converges in the rounds of its own dependency chains, and a round
+    // evaluates at most kProjWin queries instead of every unsettled one (6
+    // whole-list rounds at 3,000 queries were ~3 list evaluations a thread
+    // each).  ORB_PROJ_WIN 0: one window of every query (the round-5 form).
+    const int win = kProjWin > 0 ? kProjWin : nq;
+    int wend = min(nq, win);
     unsigned long long c_dec = 0, c_res = 0, c_reb = 0, tc = __builtin_amdgcn_s_memtime();
     for (int round = 0; round <= nq; ++round) {
-        // decisions under this round's T, queries >= settled only (an earlier
-        // query's decision reads only claims of queries before it, all final).
-        // Groups of 4 queries per thread: 8 lists in registers at once spill
+        // decisions under this round's T, queries in [settled, wend) only (an
+        // earlier query's decision reads only claims of queries before it,
+        // all final).  Groups of 4 queries per thread: 8 lists in registers
+        // at once spill
         int chg = INT_MAX;        // the thread's first changed query (one LDS atomic per wave below)
 #pragma unroll 1
         for (int u0 = 0; u0 < kFusedQpt; u0 += 4) {
-        if (tid + u0 * kFusedThreads >= nq) break;
+        if (tid + u0 * kFusedThreads >= wend) break;
+        if (tid + (u0 + 3) * kFusedThreads < settled) continue;
         uint4 LA[4], LB[4];
         int C[4], H[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int jj = tid + (u0 + u) * kFusedThreads;
             const int j = min(jj, max(nq - 1, 0));
-            const int cr = (jj < nq && jj >= settled) ? Csrc[j] : -1;
+            const int cr = (jj < wend && jj >= settled) ? Csrc[j] : -1;
             C[u] = cr < 0 ? -1 : (cr & ((1 << 30) - 1));
             H[u] = cr < 0 ? 0 : (cr >> 30) & 1;
             LA[u] = Lsrc[(long long)j * 2];
@@ -3858,7 +3872,7 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int j = tid + (u0 + u) * kFusedThreads;
-            if (j >= nq || j < settled) continue;
+            if (j >= wend || j < settled) continue;
             const uint32_t L[kProjK] = {LA[u].x, LA[u].y, LA[u].z, LA[u].w, LB[u].x, LB[u].y, LB[u].z, LB[u].w};
             int dec = -1;
             if (C[u] > 0) {
@@ -3936,8 +3950,13 @@ __global__ __launch_bounds__(kFusedThreads) void k_proj_fused(ProjArgs a, int bo
         { const unsigned long long t_ = __builtin_amdgcn_s_memtime(); c_res += t_ - tc; tc = t_; }
         const int first_changed = misc[1];
         __syncthreads();
-        if (first_changed >= nq) break;
-        settled = first_changed;
+        if (first_changed >= wend) {      // the window is final
+            if (wend >= nq) break;
+            settled = wend;
+            wend = min(nq, wend + win);
+        } else {
+            settled = first_changed;
+        }
         // T from this round's decisions: the first blocking claim of each slot
         for (int s = tid; s < n; s += kFusedThreads) T[s] = pre[s] ? -1 : INT_MAX;
         if (tid == 0) { misc[1] = nq; misc[2] = 0; }
