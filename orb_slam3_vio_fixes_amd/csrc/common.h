@@ -115,6 +115,18 @@ __device__ __forceinline__ int wave_sum_dpp(int v) {
     return __builtin_amdgcn_readlane(v, kWave - 1);
 }
 
+// Inclusive prefix sum over the wave by DPP (row_shr within rows of 16, then
+// the row broadcasts), no LDS traffic; every lane of the wave active.
+__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
+    v += dpp_mov<0x111, 0xf>(v, 0);   // row_shr:1
+    v += dpp_mov<0x112, 0xf>(v, 0);   // row_shr:2
+    v += dpp_mov<0x114, 0xf>(v, 0);   // row_shr:4
+    v += dpp_mov<0x118, 0xf>(v, 0);   // row_shr:8
+    v += dpp_mov<0x142, 0xa>(v, 0);   // row_bcast:15 -> rows 1, 3
+    v += dpp_mov<0x143, 0xc>(v, 0);   // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // Position of this lane among the set bits of `mask` below it.
 __device__ __forceinline__ int mask_rank(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
@@ -138,7 +150,7 @@ __device__ int block_excl_scan(int* a, int n, int* tmp) {
     const int b = min(n, t * per), e = min(n, b + per);
     int s = 0;
     for (int i = b; i < e; ++i) s += a[i];
-    const int incl = wave_incl_scan(s);
+    const int incl = wave_incl_scan_dpp(s);   // (DPP: no ds_bpermute round trips)
     if (lane_id() == kWave - 1) tmp[wave_id()] = incl;
     __syncthreads();
     if (t == 0) {
@@ -169,7 +181,7 @@ __device__ inline void block_excl_scan3(int* a, int na, int* b, int nb, int* c, 
         int s = 0;
         for (int i = lo[j]; i < hi[j]; ++i) s += arr[j][i];
         sum[j] = s;
-        incl[j] = wave_incl_scan(s);
+        incl[j] = wave_incl_scan_dpp(s);
         if (lane_id() == kWave - 1) tmp[j * (W + 1) + wave_id()] = incl[j];
     }
     __syncthreads();

@@ -646,7 +646,7 @@ static int build_plan_into(orbx_handle* hd, Plan& P, int w, int h, int maxB) {
     // k_assemble holds a flag per output slot of a frame in LDS (dynamic) next
     // to its static lvl_start[kMaxLevels + 1] and tmp[16]: up to ~40,000
     // features a frame (Tracking's largest extractor is 5 x nFeatures)
-    if ((size_t)outsum * 4 + 64 + (size_t)(kMaxLevels + 1 + ORB_ASM_THREADS / 64 + 1) * 4 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
+    if ((size_t)outsum * 4 + 64 + (size_t)(4 * kMaxLevels + 1 + ORB_ASM_THREADS / 64 + 1) * 4 > (size_t)kLdsMax) return ORB_ERR_UNSUPPORTED;
     P.in_pitch = (size_t)round_up(w, 64);
 
     const size_t B = (size_t)maxB;
@@ -1622,17 +1622,6 @@ __device__ __forceinline__ void roi_land(const RoiFetch& rf, const uint32_t (&v)
 // RP: the LDS pitch of a landed ROI in dwords, fixed at compile time (every
 // row offset of the pre-test, the ring and the diagonal reads an immediate),
 // or 0 for each cell's own nd
-// Inclusive prefix sum over the wave by DPP (row_shr within rows of 16, then
-// the row broadcasts), no LDS traffic.
-__device__ __forceinline__ int wave_incl_scan_dpp(int v) {
-    v += dpp_mov<0x111, 0xf>(v, 0);   // row_shr:1
-    v += dpp_mov<0x112, 0xf>(v, 0);   // row_shr:2
-    v += dpp_mov<0x114, 0xf>(v, 0);   // row_shr:4
-    v += dpp_mov<0x118, 0xf>(v, 0);   // row_shr:8
-    v += dpp_mov<0x142, 0xa>(v, 0);   // row_bcast:15 -> rows 1, 3
-    v += dpp_mov<0x143, 0xc>(v, 0);   // row_bcast:31 -> rows 2, 3
-    return v;
-}
 
 // The iniThFAST candidates of a cell's window from k_pyr_stream's bitmap
 // (k_fast_cells<..., BM = true>): lane r holds window row r's bitmap dwords
@@ -2444,11 +2433,52 @@ __device__ __forceinline__ short4 child_rect(short4 r, int q) {
 
 // One __introsort_loop step on [f, l) by a whole wave: partition_ranks
 // (orb_math.h) with the L / R lists built by ballots.
+#ifndef ORB_QT_OFFLOAD4
+#define ORB_QT_OFFLOAD4 1   // k_quadtree's cell-count loads 4 a thread in flight
+#endif
+#ifndef ORB_SORT_LEAF16
+#define ORB_SORT_LEAF16 0   // 1: a leaf's records read at once (same-box A/B: no gain, profiles/r06/README.md)
+#endif
+#ifndef ORB_SORT_REGMED
+#define ORB_SORT_REGMED 0   // 1: median of three from one round of reads by lanes 0-3 (no gain measured)
+#endif
+__device__ __forceinline__ SortRec rec_lane(const SortRec& r, int l) {
+    return SortRec{__builtin_amdgcn_readlane(r.cnt, l), __builtin_amdgcn_readlane(r.x0, l),
+                   __builtin_amdgcn_readlane(r.pos, l)};
+}
 __device__ int wave_partition(SortRec* a, int f, int l, int* Lp, int* Rp) {
     const int lane = lane_id();
+#if ORB_SORT_REGMED
+    // median_to_first_(a + f, a + f + 1, a + mid, a + l - 1) with the four
+    // records read at once (lanes 0-3) and the choice made in registers:
+    // ranges here hold > 16 records, so f + 1 < mid < l - 1
+    SortRec pv;
+    {
+        const int mid = f + (l - f) / 2;
+        const int src = lane == 1 ? f + 1 : (lane == 2 ? mid : (lane == 3 ? l - 1 : f));
+        const SortRec mine = a[src];
+        const SortRec r0 = rec_lane(mine, 0), A = rec_lane(mine, 1), B = rec_lane(mine, 2), C = rec_lane(mine, 3);
+        int mp;   // the position median_to_first_ swaps with f
+        if (node_less(A, B)) {
+            if (node_less(B, C)) mp = mid;
+            else if (node_less(A, C)) mp = l - 1;
+            else mp = f + 1;
+        } else if (node_less(A, C)) mp = f + 1;
+        else if (node_less(B, C)) mp = l - 1;
+        else mp = mid;
+        pv = mp == mid ? B : (mp == f + 1 ? A : C);
+        fast_wave_sync();   // every lane has read before lane 0 writes
+        if (lane == 0) {
+            a[f] = pv;
+            a[mp] = r0;
+        }
+        fast_wave_sync();
+    }
+#else
     if (lane == 0) median_to_first_(a + f, a + f + 1, a + f + (l - f) / 2, a + l - 1);
     fast_wave_sync();
     const SortRec pv = a[f];
+#endif
     int cl = 0, cr = 0;
     for (int base = f + 1; base < l; base += kWave) {
         const int p = base + lane;
@@ -2550,10 +2580,21 @@ __device__ void block_std_sort(SortRec* a, int m, SortRec* backup, int* Lp, int*
         }
         if (sub < len) {
             x = a[f + sub];
+#if ORB_SORT_LEAF16
+            // the leaf's <= 16 records read at once (16 reads in flight, not a
+            // chain of len dependent round trips)
+            SortRec y[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) y[j] = a[f + min(j, len - 1)];
+#pragma unroll
+            for (int j = 0; j < 16; ++j)
+                rank += j < len && (node_less(y[j], x) || (j < sub && !node_less(x, y[j])));
+#else
             for (int j = 0; j < len; ++j) {
                 const SortRec y = a[f + j];
                 rank += node_less(y, x) || (j < sub && !node_less(x, y));
             }
+#endif
         }
         fast_wave_sync();
         if (sub < len) a[f + rank] = x;
@@ -2789,7 +2830,20 @@ __global__ __launch_bounds__(ORB_QT_THREADS) void k_quadtree(QtArgs a) {
     uint32_t* out = a.qt_key + (long long)f * a.out_total + lv.out_base;
 
     // 1. vToDistributeKeys: cells in (row, col) order, row-major inside a cell (:805-872)
+#if ORB_QT_OFFLOAD4
+    // the cell counts with 4 loads a thread in flight (a load-store loop
+    // waited on each load: three serial round trips to L2 at 700 cells)
+    for (int i0 = tid; i0 < lv.ncells; i0 += 4 * T) {
+        int v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = i0 + u * T < lv.ncells ? ccount[i0 + u * T] : 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (i0 + u * T < lv.ncells) s.off[i0 + u * T] = v[u];
+    }
+#else
     for (int i = tid; i < lv.ncells; i += T) s.off[i] = ccount[i];
+#endif
     __syncthreads();
     const int K = block_excl_scan(s.off, lv.ncells, s.tmp);
     const int cap = lv.ncells ? lv.slot_total / lv.ncells : 0;
@@ -4345,59 +4399,117 @@ struct AsmArgs {
 
 __global__ __launch_bounds__(ORB_ASM_THREADS) void k_assemble(AsmArgs a) {
     __shared__ int lvl_start[kMaxLevels + 1];
+    __shared__ int lvl_base[kMaxLevels];
+    __shared__ float lvl_scale[kMaxLevels];
+    __shared__ float lvl_patch[kMaxLevels];
     __shared__ int tmp[ORB_ASM_THREADS / kWave + 1];   // block_excl_scan: a word a wave + the total
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     int* inlap = (int*)smem;                    // per keypoint, scanned
     const int f = blockIdx.x, tid = threadIdx.x, T = blockDim.x;
-    if (tid == 0) {
-        int acc = 0;
-        for (int l = 0; l < a.L; ++l) { lvl_start[l] = acc; acc += a.qt_n[f * a.L + l]; }
-        lvl_start[a.L] = acc;
+    // the level starts by one DPP scan of the levels' counts (their loads in
+    // flight together: a thread-0 loop waited on each), and the level fields
+    // the keypoints need, in LDS
+    if (tid < kWave) {
+        const int c = tid < a.L ? a.qt_n[f * a.L + tid] : 0;
+        const int incl = wave_incl_scan_dpp(c);
+        if (tid < a.L) {
+            lvl_start[tid] = incl - c;
+            lvl_base[tid] = a.lv[tid].out_base;
+            lvl_scale[tid] = a.lv[tid].scale;
+            lvl_patch[tid] = (float)a.lv[tid].patch;
+        }
+        if (tid == a.L - 1) lvl_start[a.L] = incl;
+        if (a.L == 0 && tid == 0) lvl_start[0] = 0;
     }
     __syncthreads();
     const int total = lvl_start[a.L];
+    // the last level whose start is <= g (empty levels share their start with
+    // the next one): a fixed 5-step search (kMaxLevels = 32), so the keypoint
+    // loops below unroll (a data-dependent while loop kept them rolled and put
+    // their per-keypoint arrays in scratch)
+    static_assert(kMaxLevels == 32, "5 search steps");
+    const int L = a.L;
     auto locate = [&](int g, int& l, int& p) {
         l = 0;
-        while (g >= lvl_start[l + 1]) ++l;
+#pragma unroll
+        for (int step = 16; step >= 1; step >>= 1)
+            if (l + step < L && g >= lvl_start[l + step]) l += step;
         p = g - lvl_start[l];
     };
-    for (int g = tid; g < total; g += T) {
-        int l, p;
-        locate(g, l, p);
-        const uint32_t key = a.qt_key[(long long)f * a.out_total + a.lv[l].out_base + p];
+    const long long fo = (long long)f * a.out_total;
+    constexpr int kU = 4;   // keypoints a thread in flight
+    auto xkey = [&](int g, int& l) {
+        int p;
+        locate(min(g, total - 1), l, p);
+        return a.qt_key[fo + lvl_base[l] + p];
+    };
+    auto flag = [&](int g, int l, uint32_t key) {
         float x = (float)((int)(key & 0xfff) + (kEdge - 3));
-        if (l != 0) x *= a.lv[l].scale;
-        inlap[g] = (x >= a.lap0 && x <= a.lap1) ? 1 : 0;
+        if (l != 0) x *= lvl_scale[l];
+        if (g < total) inlap[g] = (x >= a.lap0 && x <= a.lap1) ? 1 : 0;
+    };
+    for (int g0 = tid; g0 < total; g0 += kU * T) {
+        int l0, l1, l2, l3;
+        const uint32_t q0 = xkey(g0, l0), q1 = xkey(g0 + T, l1), q2 = xkey(g0 + 2 * T, l2), q3 = xkey(g0 + 3 * T, l3);
+        flag(g0, l0, q0);
+        flag(g0 + T, l1, q1);
+        flag(g0 + 2 * T, l2, q2);
+        flag(g0 + 3 * T, l3, q3);
     }
     __syncthreads();
     // keep the flags: recompute them after the scan from the scanned values
     const int nlap = block_excl_scan(inlap, total, tmp);
-    for (int g = tid; g < total; g += T) {
-        int l, p;
-        locate(g, l, p);
-        const LevelDev lv = a.lv[l];
-        const long long src = (long long)f * a.out_total + lv.out_base + p;
-        const uint32_t key = a.qt_key[src];
-        float x = (float)((int)(key & 0xfff) + (kEdge - 3));
-        float y = (float)((int)((key >> 12) & 0xfff) + (kEdge - 3));
-        if (l != 0) { x *= lv.scale; y *= lv.scale; }
+    // four keypoints' loads issued before any of their stores (named values,
+    // not arrays: an array indexed in a rolled loop went to scratch)
+    struct KpIn {
+        uint32_t key;
+        float ang;
+        uint4 d0, d1;
+        int l, g;
+    };
+    auto load = [&](int g) {
+        KpIn k;
+        k.g = g;
+        int p;
+        locate(min(g, total - 1), k.l, p);
+        const long long src = fo + lvl_base[k.l] + p;
+        k.key = a.qt_key[src];
+        k.ang = a.angle[src];
+        const uint4* s4 = (const uint4*)(a.sdesc + src * 32);
+        k.d0 = s4[0];
+        k.d1 = s4[1];
+        return k;
+    };
+    auto store = [&](const KpIn& k) {
+        if (k.g >= total) return;
+        const int l = k.l;
+        float x = (float)((int)(k.key & 0xfff) + (kEdge - 3));
+        float y = (float)((int)((k.key >> 12) & 0xfff) + (kEdge - 3));
+        if (l != 0) { x *= lvl_scale[l]; y *= lvl_scale[l]; }
         const bool in = x >= a.lap0 && x <= a.lap1;
-        const int before_lap = inlap[g];
-        const int dst = in ? total - 1 - before_lap : g - before_lap;
+        const int before_lap = inlap[k.g];
+        const int dst = in ? total - 1 - before_lap : k.g - before_lap;
         orb_keypoint kp;
         kp.x = x; kp.y = y;
-        kp.size = (float)lv.patch;
-        kp.angle = a.angle[src];
-        kp.response = (float)(key >> 24);
+        kp.size = lvl_patch[l];
+        kp.angle = k.ang;
+        kp.response = (float)(k.key >> 24);
         kp.octave = l;
         kp.class_id = -1;
         if (dst < a.cap) {
             a.kps[(long long)f * a.cap + dst] = kp;
-            const uint4* s4 = (const uint4*)(a.sdesc + src * 32);
             uint4* d4 = (uint4*)(a.desc + ((long long)f * a.cap + dst) * 32);
-            d4[0] = s4[0];
-            d4[1] = s4[1];
+            d4[0] = k.d0;
+            d4[1] = k.d1;
         }
+    };
+    static_assert(kU == 4, "four named keypoints");
+    for (int g0 = tid; g0 < total; g0 += kU * T) {
+        const KpIn k0 = load(g0), k1 = load(g0 + T), k2 = load(g0 + 2 * T), k3 = load(g0 + 3 * T);
+        store(k0);
+        store(k1);
+        store(k2);
+        store(k3);
     }
     if (tid == 0) {
         a.n_out[f] = total;

@@ -719,10 +719,20 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     const uint32_t* topk = a.topk + (long long)pr * a.cap * kTopK;
     const int* ncand = a.ncand + (long long)pr * a.cap;
     const int nl = a.gcount[f2];
-    for (int i = tid; i < n1; i += kSfiThreads) {
-        qlist[i] = ncand[i];
-        m12[i] = -1;
-        bin1[i] = -1;
+    // (4 count loads a thread in flight: a load-store loop waited on each)
+    for (int i0 = tid; i0 < n1; i0 += 4 * kSfiThreads) {
+        int c[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) c[u] = i0 + u * kSfiThreads < n1 ? ncand[i0 + u * kSfiThreads] : 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int i = i0 + u * kSfiThreads;
+            if (i < n1) {
+                qlist[i] = c[u];
+                m12[i] = -1;
+                bin1[i] = -1;
+            }
+        }
     }
     for (int i = tid; i < n2; i += kSfiThreads) md21[i] = kMdNone;
     if (tid < 32) hist[tid] = 0;
@@ -746,8 +756,15 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
 #endif
     const int nq = ORB_SFI_ABL == 1 ? 0 : hist[31];
     const int nst = min(nq, kSfiStage);
-    for (int e = tid; e < nst * kTopK; e += kSfiThreads)
-        skeys[e] = topk[(long long)(qlist[e / kTopK] & 0x7fffffff) * kTopK + e % kTopK];
+    // a staged query's whole top-K row (32 B) by one thread, its two 16-byte
+    // loads in flight (an element per thread was 8 dependent round trips each)
+    static_assert(kTopK == 8, "a top-K row is two uint4");
+    for (int q = tid; q < nst; q += kSfiThreads) {
+        const uint4* row = (const uint4*)(topk + (long long)(qlist[q] & 0x7fffffff) * kTopK);
+        const uint4 r0 = row[0], r1 = row[1];
+        ((uint4*)skeys)[2 * q] = r0;
+        ((uint4*)skeys)[2 * q + 1] = r1;
+    }
     // F2's level-0 list for the exact rescans (entry, position, descriptor):
     // a rescan then reads LDS, not three dependent global loads per candidate
     const int nl2 = min(nl, kSfiStage2);
