@@ -2433,6 +2433,9 @@ __device__ __forceinline__ short4 child_rect(short4 r, int q) {
 
 // One __introsort_loop step on [f, l) by a whole wave: partition_ranks
 // (orb_math.h) with the L / R lists built by ballots.
+#ifndef ORB_QT_KCELL
+#define ORB_QT_KCELL 0   // 1: the gather finds a key's cell by a table written per cell instead of a binary search (same-box A/B: quadtree 86-88 vs 83-87 us, no gain)
+#endif
 #ifndef ORB_QT_OFFLOAD4
 #define ORB_QT_OFFLOAD4 1   // k_quadtree's cell-count loads 4 a thread in flight
 #endif
@@ -2639,7 +2642,10 @@ __global__ __launch_bounds__(256) void k_debug_sort(const int* __restrict__ off,
     if (threadIdx.x == 0) fallback[blockIdx.x] = ctl[2];
 }
 
-constexpr int kQtB = 4;   // keys per thread per round of the quadtree's key passes
+#ifndef ORB_QT_B
+#define ORB_QT_B 4
+#endif
+constexpr int kQtB = ORB_QT_B;   // keys per thread per round of the quadtree's key passes
 
 // Divide s.ord[0..m) (ccnt/kq already computed for them, s.div set for every
 // node); rebuild the list into buffer cur^1; remap the keys.  Returns the new
@@ -2865,11 +2871,27 @@ __global__ __launch_bounds__(ORB_QT_THREADS) void k_quadtree(QtArgs a) {
         uint32_t* __restrict__ dst = keys;
         int* __restrict__ kn = knode;
         const int nc = lv.ncells;
+        // key k's cell: written per cell into the (still free) ccnt / newpos
+        // bytes, one LDS read a key instead of a ~10-step binary search of the
+        // offsets (levels whose keys do not fit those bytes keep the search)
+        uint16_t* const kcell = (uint16_t*)s.ccnt;
+        const bool direct = ORB_QT_KCELL && K <= 16 * NC && nc <= 65536;
+        if (direct) {
+            for (int c = tid; c < nc; c += T) {
+                const int e = c + 1 < nc ? s.off[c + 1] : K;
+                for (int j = s.off[c]; j < e; ++j) kcell[j] = (uint16_t)c;
+            }
+            __syncthreads();
+        }
         for (int k0 = tid; k0 < K; k0 += kQtB * T) {
             int c[kQtB];
 #pragma unroll
             for (int q = 0; q < kQtB; ++q) {
                 const int k = min(k0 + q * T, K - 1);
+                if (direct) {
+                    c[q] = kcell[k];
+                    continue;
+                }
                 int lo = 0, hi = nc;                   // off[lo] <= k < off[hi] (off[nc] = K)
                 while (hi - lo > 1) {
                     const int mid = (lo + hi) >> 1;
