@@ -2174,6 +2174,9 @@ __global__ __launch_bounds__(256) void k_bowk_chunks(BowKArgs k) {
 // per node left 60 % of its lanes idle on ~38-feature nodes).  Pairs with
 // more nodes than the stage take them a wave per node.
 constexpr int kBowFillStage = 1024;
+#ifndef ORB_BOWKFILL_U
+#define ORB_BOWKFILL_U 4   // k_bowk_fill: features a thread in flight
+#endif
 __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
     __shared__ int s_ko[kBowFillStage + 1];
     __shared__ int s_base[kBowFillStage];
@@ -2229,7 +2232,7 @@ __global__ __launch_bounds__(256) void k_bowk_fill(BowKArgs k) {
     const int p0 = s_ko[0], p1 = s_ko[nn];
     // four features in flight per thread: their FeatureVector indices, then
     // their MapPoint flags, then the stores (one dependent load chain per four)
-    constexpr int kU = 4;
+    constexpr int kU = ORB_BOWKFILL_U;
     const int bd = blockDim.x;
     for (int q = p0 + threadIdx.x; q < p1; q += kU * bd) {
         int bs[kU];
