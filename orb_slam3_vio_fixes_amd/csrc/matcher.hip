@@ -411,6 +411,11 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     asm("v_med3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
     return d;
 }
+__device__ __forceinline__ uint32_t umin3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_min3_u32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 template <int K>
 __device__ __forceinline__ void topk_push(uint32_t (&kk)[K], uint32_t key) {
     uint32_t n[K];
@@ -641,6 +646,9 @@ constexpr int kSfiThreads = 256;
 #ifndef ORB_SFI_SPEC
 #define ORB_SFI_SPEC 1   // speculative 8-query runs (0: the serial step-per-query walk)
 #endif
+#ifndef ORB_SFI_CONFL
+#define ORB_SFI_CONFL 2  // the run's conflict scan as unrolled readlanes, each query's stop by a DPP group OR (1: by a ballot; 0: a loop over the accepting queries)
+#endif
 #ifndef ORB_SFI_DEPTH
 #define ORB_SFI_DEPTH 3  // runs of keys in registers: the current one and the next ones in flight
 #endif
@@ -664,18 +672,48 @@ constexpr uint32_t kMdNone = 0xffff0000u;    // md21: no match yet (distance fie
 #ifdef ORB_SFI_COUNT
 // walk statistics (tools/sfi_counts.py): rounds, rounds that committed fewer
 // than 8 queries, exact rescans, queries, committed claims
-__device__ unsigned long long g_sfi_cnt[8];
+// and shader cycles per walk phase (g_sfi_cnt[8..15]: decide, conflict
+// scan, commit, in-place state update, rescan, run advance, prologue, the
+// whole block)
+__device__ unsigned long long g_sfi_cnt[16];
 extern "C" int orbm_debug_sfi_counts(unsigned long long* out, int reset) {
     if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sfi_cnt), sizeof(g_sfi_cnt)) != hipSuccess) return -4;
     if (reset) {
-        static unsigned long long z[8];
+        static unsigned long long z[16];
         if (hipMemcpyToSymbol(HIP_SYMBOL(g_sfi_cnt), z, sizeof(z)) != hipSuccess) return -4;
     }
     return 0;
 }
-#define SFI_CNT(k, v) do { if (lane == 0) atomicAdd(&g_sfi_cnt[k], (unsigned long long)(v)); } while (0)
+// (counts in registers, flushed once a block: same-address global atomics per
+// step from every block had been the stamps' largest cost)
+#define SFI_CNT(k, v)                                                  \
+    do {                                                               \
+        switch (k) {                                                   \
+            case 0: sfi_c0 += (v); break;                              \
+            case 1: sfi_c1 += (v); break;                              \
+            case 2: sfi_c2 += (v); break;                              \
+            case 3: sfi_c3 += (v); break;                              \
+            default: sfi_c4 += (v); break;                             \
+        }                                                              \
+    } while (0)
+#define SFI_TS(k)                                                      \
+    do {                                                               \
+        const unsigned long long t_ = __builtin_amdgcn_s_memtime();    \
+        const unsigned long long d_ = t_ - sfi_tl;                     \
+        sfi_tl = t_;                                                   \
+        switch (k) {                                                   \
+            case 0: sfi_a0 += d_; break;                               \
+            case 1: sfi_a1 += d_; break;                               \
+            case 2: sfi_a2 += d_; break;                               \
+            case 3: sfi_a3 += d_; break;                               \
+            case 4: sfi_a4 += d_; break;                               \
+            case 5: sfi_a5 += d_; break;                               \
+            default: sfi_a6 += d_; break;                              \
+        }                                                              \
+    } while (0)
 #else
 #define SFI_CNT(k, v) do { } while (0)
+#define SFI_TS(k) do { } while (0)
 #endif
 // minimum over each aligned group of 8 lanes, in every lane of the group:
 // quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror
@@ -693,6 +731,13 @@ template <bool M12L>
 __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     extern __shared__ __attribute__((aligned(16))) int lds[];
     const int pr = blockIdx.x, lane = lane_id(), tid = threadIdx.x;
+#ifdef ORB_SFI_COUNT
+    // (separate scalars: an array captured by the walk's lambda went to scratch)
+    unsigned long long sfi_c0 = 0, sfi_c1 = 0, sfi_c2 = 0, sfi_c3 = 0, sfi_c4 = 0;
+    unsigned long long sfi_a0 = 0, sfi_a1 = 0, sfi_a2 = 0, sfi_a3 = 0, sfi_a4 = 0, sfi_a5 = 0, sfi_a6 = 0;
+    const unsigned long long sfi_t0 = __builtin_amdgcn_s_memtime();
+    unsigned long long sfi_tl = sfi_t0;
+#endif
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
     const int n1 = min(a.n[f1], a.cap), n2 = min(a.n[f2], a.cap);
     const orb_keypoint* K1 = a.kps + (long long)f1 * a.cap;
@@ -704,7 +749,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     // matches (written by the walk, read after the block's barrier) stay in
     // global memory
     uint32_t* md21 = (uint32_t*)lds;              // cap: matched distance << 16 | (F1 match + 1)
-    int* hist = (int*)(md21 + a.cap);             // 32 (hist[31]: the filter's drop count)
+    int* hist = (int*)(md21 + a.cap);             // 32 (hist[31]: the final match count)
     int* qlist = hist + 32;                       // cap: query i1 | (more than kTopK candidates) << 31
     int8_t* bin1 = (int8_t*)(qlist + a.cap);      // cap
     // the first kSfiStage queries' keys (staged by all four waves before the
@@ -752,7 +797,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     }
     __syncthreads();
 #ifndef ORB_SFI_ABL
-#define ORB_SFI_ABL 0   // timing ablation (tools only; wrong results): 1 = no walk
+#define ORB_SFI_ABL 0   // timing ablation (tools only; wrong results): 1 = no walk, 2 = no rescan work, 3 = no conflict scan
 #endif
     const int nq = ORB_SFI_ABL == 1 ? 0 : hist[31];
     const int nst = min(nq, kSfiStage);
@@ -800,7 +845,13 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         int nm = 0;
         const float r = a.window;
         const int grp = lane >> 3, kk = lane & 7;
+        // per query tp of a run: 0 for the lanes of later queries, else a bit
+        // above any feature index (their entries cannot conflict with tp's claim)
+        uint32_t sfi_pen[7];
+#pragma unroll
+        for (int tp = 0; tp < 7; ++tp) sfi_pen[tp] = grp > tp ? 0u : 0x100000u;
         SFI_CNT(3, nq);
+        SFI_TS(6);
         // the walk in two instantiations: every query's keys staged (no global
         // load in the loop at all, so no wait at its head drains one), or not
         auto walk = [&](auto all_staged_c) {
@@ -855,13 +906,47 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 const bool acc = ok && active && best <= kThLow && (float)best < (float)best2 * a.ratio;
                 // an earlier claim on an entry this query's decision reads stops it
                 const bool reads = kval && kk <= p2;
+                SFI_TS(0);
                 uint64_t confl = 0;
-                for (uint64_t am = __ballot(acc && kk == 0); am; am &= am - 1) {
+                bool gconf = false;
+#if ORB_SFI_CONFL
+                // the claims of queries 0..6 of the run as 7 independent
+                // readlanes, each lane comparing its entry with those of the
+                // earlier queries (a loop over the accepting queries was a
+                // SALU -> readlane -> compare -> SALU chain per claim: 850 of a
+                // step's ~2,100 cycles, profiles/r06/README.md)
+                if (ORB_SFI_ABL != 3) {
+                    const int bia = acc ? bi : 0xffff0;                 // group-uniform: the query's claim
+                    // hit iff some (kfi ^ claim of an earlier query) is 0: one
+                    // v_xor3 a query (the lane's penalty for queries not before
+                    // it) and a v_min3 tree, all VALU -- no SALU mask per claim
+                    uint32_t x[7];
+#pragma unroll
+                    for (int tp = 0; tp < 7; ++tp)
+                        x[tp] = (uint32_t)kfi ^ (uint32_t)__builtin_amdgcn_readlane(bia, 8 * tp) ^ sfi_pen[tp];
+                    const uint32_t m = umin3(umin3(x[0], x[1], x[2]), umin3(x[3], x[4], x[5]), x[6]);
+#if ORB_SFI_CONFL == 2
+                    // the query's conflict as an 8-lane DPP OR (no 64-bit
+                    // per-lane shift of a ballot, no divergent branch)
+                    gconf = grp8_min((reads && m == 0u) ? 0u : 1u) == 0u;
+#else
+                    confl = __ballot(reads && m == 0u);
+#endif
+                }
+#else
+                for (uint64_t am = ORB_SFI_ABL == 3 ? 0 : __ballot(acc && kk == 0); am; am &= am - 1) {
                     const int l = __ffsll((long long)am) - 1;           // lane 8t' of a claiming query
                     const int cb = __builtin_amdgcn_readlane(bi, l);
                     confl |= __ballot(reads && kfi == cb && lane >= l + 8);
                 }
+#endif
+                SFI_TS(1);
+#if ORB_SFI_CONFL == 2
+                (void)confl;
+                const bool stop = (active & (gconf | !ok)) | (grp >= nrun);
+#else
                 const bool stop = (active && (((confl >> (8 * grp)) & 0xffull) != 0 || !ok)) || grp >= nrun;
+#endif
                 const uint64_t sm = __ballot(stop && kk == 0);
                 P = sm ? (__ffsll((long long)sm) - 1) >> 3 : 8;
                 const bool commit = acc && grp < P && kk == 0;
@@ -876,13 +961,15 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                         atomicAdd(&hist[kb >> 25], 1);
                     }
                 }
+                // (the match count is taken from m12 after the walk: no per-step
+                // ballots for it)
                 const uint64_t cmask = __ballot(commit);
-                nm += __popcll(cmask) - __popcll(__ballot(commit && prev >= 0));
                 SFI_CNT(4, __popcll(cmask));
                 // the next reads see these writes (one wave: its LDS operations
                 // complete in order; the asm keeps the compiler from hoisting
                 // later reads above the stores)
                 asm volatile("" ::: "memory");
+                SFI_TS(2);
                 if (P >= nrun) break;
                 // the committed claims into the lanes' states (what md21 now holds)
                 for (uint64_t cm = cmask; cm; cm &= cm - 1) {
@@ -891,8 +978,11 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                     const uint32_t cv = (uint32_t)__builtin_amdgcn_readlane((int)nst_v, l);
                     st = kfi == cb ? cv : st;
                 }
+                SFI_TS(3);
                 t0 = P;
-                if (__builtin_amdgcn_readlane((int)ok, 8 * P) == 0) {
+                if (ORB_SFI_ABL == 2 && __builtin_amdgcn_readlane((int)ok, 8 * P) == 0) {
+                    t0 = P + 1;
+                } else if (__builtin_amdgcn_readlane((int)ok, 8 * P) == 0) {
                 // query j0 + P cannot decide from its truncated list: exact
                 // full candidate scan under the state after the prefix
                 const int qx = __builtin_amdgcn_readlane(qe, 8 * P);
@@ -929,8 +1019,6 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 }
                 if (bs.idx >= 0 && bs.best <= kThLow && (float)bs.best < (float)bs.best2 * a.ratio) {
                     const int pv = (int)(md21[bs.idx] & 0xffffu) - 1;
-                    if (pv >= 0) --nm;
-                    ++nm;
                     const uint32_t nv = ((uint32_t)bs.best << 16) | (uint32_t)(q1 + 1);
                     if (lane == 0) {
                         if (pv >= 0) m12[pv] = -1;
@@ -951,6 +1039,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 // pending on some path made the compiler wait for memory at the
                 // head of every step
                 __builtin_amdgcn_s_waitcnt(0);
+                SFI_TS(4);
                 }
                 SFI_CNT(1, 1);
             }
@@ -972,6 +1061,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 for (int i = 0; i + 1 < kSfiDepth; ++i) kr[i] = src < 64 ? sh[i] : sh[i + 1];
             }
             kr[kSfiDepth - 1] = j0 + 8 * (kSfiDepth - 1) < nq ? run_keys(j0 + 8 * (kSfiDepth - 1)) : kNoKey;
+            SFI_TS(5);
         }
         };
         if (nq <= kSfiStage) walk(std::true_type{});
@@ -1076,27 +1166,27 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
           }
         }
 #if !ORB_SFI_SPEC
-        if (lane < 32) hist[lane] = hreg;   // bins 0..29; hist[31] = 0 counts the drops below
+        if (lane < 32) hist[lane] = hreg;   // bins 0..29; hist[31] = 0 counts the matches below
 #endif
 #endif
-        if (lane == 0) qlist[0] = nm;       // the query list is spent: hand nm to the block
+        (void)nm;
     }
     __syncthreads();
-    int nm = qlist[0];
-    if (a.check_ori) {
-        int i1x, i2x, i3x;
-        three_maxima_wave(hist, i1x, i2x, i3x);   // bins 0..29
-        int drop = 0;
-        for (int i = tid; i < n1; i += kSfiThreads) {
-            const int b = bin1[i];
-            if (b < 0 || b == i1x || b == i2x || b == i3x) continue;
-            if (m12[i] >= 0) { m12[i] = -1; ++drop; }
-        }
-        drop = wave_sum(drop);
-        if (lane == 0 && drop) atomicAdd(&hist[31], drop);
-        __syncthreads();
-        nm -= hist[31];
+    // nmatches = the F1 features left matched (every claim matched one, every
+    // steal unmatched one), after the rotation filter (ORBmatcher.cc:738-758)
+    int i1x = -1, i2x = -1, i3x = -1;
+    if (a.check_ori) three_maxima_wave(hist, i1x, i2x, i3x);   // bins 0..29
+    int nmk = 0;
+    for (int i = tid; i < n1; i += kSfiThreads) {
+        if (m12[i] < 0) continue;
+        const int b = a.check_ori ? (int)bin1[i] : -1;
+        if (b >= 0 && b != i1x && b != i2x && b != i3x) m12[i] = -1;
+        else ++nmk;
     }
+    nmk = wave_sum(nmk);
+    if (lane == 0 && nmk) atomicAdd(&hist[31], nmk);
+    __syncthreads();
+    const int nm = hist[31];
     if (a.prev_out) {
         for (int i = tid; i < n1; i += kSfiThreads) {
             float px, py;
@@ -1110,6 +1200,15 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
     if (M12L)
         for (int i = tid; i < n1; i += kSfiThreads) m12g[i] = m12[i];
     if (tid == 0) a.nmatches[pr] = nm;
+#ifdef ORB_SFI_COUNT
+    const unsigned long long sfi_t[8] = {sfi_a0, sfi_a1, sfi_a2, sfi_a3, sfi_a4, sfi_a5, sfi_a6,
+                                         __builtin_amdgcn_s_memtime() - sfi_t0};
+    const unsigned long long sfi_c[5] = {sfi_c0, sfi_c1, sfi_c2, sfi_c3, sfi_c4};
+    if (tid == 0) {
+        for (int k = 0; k < 5; ++k) atomicAdd(&g_sfi_cnt[k], sfi_c[k]);
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_sfi_cnt[8 + k], sfi_t[k]);
+    }
+#endif
 }
 
 constexpr size_t kLdsMax = 160 * 1024;
