@@ -952,14 +952,14 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 const bool commit = acc && grp < P && kk == 0;
                 const int prev = (int)(stb & 0xffffu) - 1;
                 const uint32_t nst_v = ((uint32_t)best << 16) | (uint32_t)(i1 + 1);
+                // a claim writes only the state and the query's rotation bin:
+                // the matches (md21 holds every F2 feature's final F1 match) and
+                // the rotation histogram (every query claims at most once, and
+                // bin1 keeps a stolen query's bin) are rebuilt after the walk
+                (void)prev;
                 if (commit) {
-                    if (prev >= 0) m12[prev] = -1;
-                    m12[i1] = bi;
                     md21[bi] = nst_v;
-                    if (a.check_ori) {
-                        bin1[i1] = (int8_t)(kb >> 25);
-                        atomicAdd(&hist[kb >> 25], 1);
-                    }
+                    if (a.check_ori) bin1[i1] = (int8_t)(kb >> 25);
                 }
                 // (the match count is taken from m12 after the walk: no per-step
                 // ballots for it)
@@ -1020,15 +1020,10 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 if (bs.idx >= 0 && bs.best <= kThLow && (float)bs.best < (float)bs.best2 * a.ratio) {
                     const int pv = (int)(md21[bs.idx] & 0xffffu) - 1;
                     const uint32_t nv = ((uint32_t)bs.best << 16) | (uint32_t)(q1 + 1);
+                    (void)pv;
                     if (lane == 0) {
-                        if (pv >= 0) m12[pv] = -1;
-                        m12[q1] = bs.idx;
                         md21[bs.idx] = nv;
-                        if (a.check_ori) {
-                            const int bn = rot_bin(k1.angle, K2[bs.idx].angle);
-                            bin1[q1] = (int8_t)bn;
-                            atomicAdd(&hist[bn], 1);
-                        }
+                        if (a.check_ori) bin1[q1] = (int8_t)rot_bin(k1.angle, K2[bs.idx].angle);
                     }
                     asm volatile("" ::: "memory");
                     st = kfi == bs.idx ? nv : st;
@@ -1172,6 +1167,31 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         (void)nm;
     }
     __syncthreads();
+#if ORB_SFI_SPEC
+    // the walk's outcome from its state: F1 feature i matched iff some F2
+    // feature's final claim is i (vnMatches12 / vnMatches21 agree at the end
+    // of ORBmatcher.cc:700-735), and rotHist[b] counts every claim ever made
+    // in bin b (:729-735 push back before any later steal)
+    for (int j = tid; j < n2; j += kSfiThreads) {
+        const int w = (int)(md21[j] & 0xffffu);
+        if (w) m12[w - 1] = j;
+    }
+    if (a.check_ori) {
+        int hb = 0;   // lane b < 30 of each wave: its count of bin b
+        for (int i0 = (tid & ~(kWave - 1)); i0 < n1; i0 += kSfiThreads) {
+            const int b = i0 + lane < n1 ? (int)bin1[i0 + lane] : -1;
+            for (uint64_t bm = __ballot(b >= 0); bm; ) {
+                const int l = __ffsll((long long)bm) - 1;
+                const int bb = __builtin_amdgcn_readlane(b, l);
+                const uint64_t same = __ballot(b == bb);
+                if (lane == bb) hb += __popcll(same & bm);
+                bm &= ~same;
+            }
+        }
+        if (lane < 30 && hb) atomicAdd(&hist[lane], hb);
+    }
+    __syncthreads();
+#endif
     // nmatches = the F1 features left matched (every claim matched one, every
     // steal unmatched one), after the rotation filter (ORBmatcher.cc:738-758)
     int i1x = -1, i2x = -1, i3x = -1;
