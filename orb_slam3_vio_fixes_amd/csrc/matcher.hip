@@ -647,7 +647,7 @@ constexpr int kSfiThreads = 256;
 #define ORB_SFI_SPEC 1   // speculative 8-query runs (0: the serial step-per-query walk)
 #endif
 #ifndef ORB_SFI_CONFL
-#define ORB_SFI_CONFL 2  // the run's conflict scan as unrolled readlanes, each query's stop by a DPP group OR (1: by a ballot; 0: a loop over the accepting queries)
+#define ORB_SFI_CONFL 3  // the run's conflict scan as unrolled readlanes, each query's stop by a DPP group OR, a conflict only where a claim kills a read entry (2: any read of a claimed feature; 1: by a ballot; 0: a loop over the accepting queries)
 #endif
 #ifndef ORB_SFI_DEPTH
 #define ORB_SFI_DEPTH 3  // runs of keys in registers: the current one and the next ones in flight
@@ -837,9 +837,11 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         // to its second live entry (all of it when fewer than two are live), and
         // the state only ever blocks more entries (a claim lowers
         // vMatchedDistance), so an earlier claim of an F2 feature outside that
-        // part leaves the decision exactly as the serial walk takes it.
-        // Committed claims are on distinct F2 features whose previous F1
-        // matches are distinct, so they are written in parallel.  A query whose
+        // part leaves the decision exactly as the serial walk takes it; so
+        // does a claim inside it that leaves the entry live (ORB_SFI_CONFL 3:
+        // its distance above the entry's).  Committed claims are written in
+        // parallel: two of one F2 feature in a prefix are a steal, the later
+        // claim's distance strictly smaller, so an LDS min keeps it.  A query whose
         // truncated list cannot decide is rescanned exactly by the wave after
         // the prefix is committed; a conflicting one is re-decided next round.
         int nm = 0;
@@ -849,7 +851,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
         // above any feature index (their entries cannot conflict with tp's claim)
         uint32_t sfi_pen[7];
 #pragma unroll
-        for (int tp = 0; tp < 7; ++tp) sfi_pen[tp] = grp > tp ? 0u : 0x100000u;
+        for (int tp = 0; tp < 7; ++tp) sfi_pen[tp] = grp > tp ? 0u : (ORB_SFI_CONFL == 3 ? 1u : 0x100000u);
         SFI_CNT(3, nq);
         SFI_TS(6);
         // the walk in two instantiations: every query's keys staged (no global
@@ -916,6 +918,26 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 // SALU -> readlane -> compare -> SALU chain per claim: 850 of a
                 // step's ~2,100 cycles, profiles/r06/README.md)
                 if (ORB_SFI_ABL != 3) {
+#if ORB_SFI_CONFL == 3
+                    // Only a claim that KILLS an entry a later query reads
+                    // changes that query's decision: a claim of distance best
+                    // on the lane's feature kills it iff best <= kd (a claim
+                    // with best > kd leaves it live, as at the run's start: the
+                    // claim lowered the state from above best to best).  So a
+                    // later query may steal an earlier claim of the same run in
+                    // the same prefix (the smaller distance wins: ds_min below).
+                    // With C = bi * 2048 + best and L = kfi * 2048 + kd,
+                    // u = L - C lies in [0, 512) iff kfi == bi and best <= kd
+                    // (|kfi - bi| >= 1 puts u at least 2048 - 511 away);
+                    // v_alignbit(pen, u, 9) is 0 iff that holds and pen is 0.
+                    const uint32_t ca = acc ? ((uint32_t)bi << 11) | (uint32_t)best : 0x7fffffffu;
+                    const uint32_t Lk = ((uint32_t)kfi << 11) | (uint32_t)kd;
+                    uint32_t x[7];
+#pragma unroll
+                    for (int tp = 0; tp < 7; ++tp)
+                        x[tp] = __builtin_amdgcn_alignbit(sfi_pen[tp],
+                                                          Lk - (uint32_t)__builtin_amdgcn_readlane((int)ca, 8 * tp), 9);
+#else
                     const int bia = acc ? bi : 0xffff0;                 // group-uniform: the query's claim
                     // hit iff some (kfi ^ claim of an earlier query) is 0: one
                     // v_xor3 a query (the lane's penalty for queries not before
@@ -924,8 +946,9 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
 #pragma unroll
                     for (int tp = 0; tp < 7; ++tp)
                         x[tp] = (uint32_t)kfi ^ (uint32_t)__builtin_amdgcn_readlane(bia, 8 * tp) ^ sfi_pen[tp];
+#endif
                     const uint32_t m = umin3(umin3(x[0], x[1], x[2]), umin3(x[3], x[4], x[5]), x[6]);
-#if ORB_SFI_CONFL == 2
+#if ORB_SFI_CONFL >= 2
                     // the query's conflict as an 8-lane DPP OR (no 64-bit
                     // per-lane shift of a ballot, no divergent branch)
                     gconf = grp8_min((reads && m == 0u) ? 0u : 1u) == 0u;
@@ -941,7 +964,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 }
 #endif
                 SFI_TS(1);
-#if ORB_SFI_CONFL == 2
+#if ORB_SFI_CONFL >= 2
                 (void)confl;
                 const bool stop = (active & (gconf | !ok)) | (grp >= nrun);
 #else
@@ -958,7 +981,11 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                 // bin1 keeps a stolen query's bin) are rebuilt after the walk
                 (void)prev;
                 if (commit) {
+#if ORB_SFI_CONFL == 3
+                    atomicMin(&md21[bi], nst_v);   // two claims of one feature in a prefix: the later, smaller one
+#else
                     md21[bi] = nst_v;
+#endif
                     if (a.check_ori) bin1[i1] = (int8_t)(kb >> 25);
                 }
                 // (the match count is taken from m12 after the walk: no per-step
@@ -976,7 +1003,7 @@ __global__ __launch_bounds__(kSfiThreads) void k_sfi_resolve(SfiArgs a) {
                     const int l = __ffsll((long long)cm) - 1;
                     const int cb = __builtin_amdgcn_readlane(bi, l);
                     const uint32_t cv = (uint32_t)__builtin_amdgcn_readlane((int)nst_v, l);
-                    st = kfi == cb ? cv : st;
+                    st = kfi == cb ? min(st, cv) : st;
                 }
                 SFI_TS(3);
                 t0 = P;
