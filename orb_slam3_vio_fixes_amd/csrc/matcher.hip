@@ -523,6 +523,9 @@ __device__ void sfi_topk_lanes(const SfiArgs& a, int pr, int qbeg, int qpw) {
 // K smallest keys are drawn from registers (a lane holds the keys of its list
 // positions lane, lane + 64, ...; kStIt positions at most, longer lists take
 // sfi_topk_lanes).  Rounds stop after min(count, K) draws.
+#ifndef ORB_SFI_QSTAGE
+#define ORB_SFI_QSTAGE 1   // k_sfi_topk_st stages its 64 queries in LDS with the F2 list
+#endif
 constexpr int kStIt = 4;                  // level-0 lists of <= 256 features
 constexpr int kStQ = 64;                  // queries per block
 __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
@@ -531,6 +534,11 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
     float2* xy2 = (float2*)(d2s + 2 * kStIt * kWave);           // kStIt * 64
     int* list = (int*)(xy2 + kStIt * kWave);                    // kStIt * 64
     float* an2 = (float*)(list + kStIt * kWave);                // kStIt * 64
+#if ORB_SFI_QSTAGE
+    // the block's 64 queries: descriptor halves, (position, angle, octave)
+    uint4* qd = (uint4*)(an2 + kStIt * kWave);                  // 2 * kStQ
+    float4* qk = (float4*)(qd + 2 * kStQ);                      // kStQ
+#endif
     const int pr = blockIdx.x, lane = lane_id(), wv = wave_id(), tid = threadIdx.x;
     const int f1 = a.pair_f1[pr], f2 = a.pair_f2[pr];
     const int n1 = min(a.n[f1], a.cap);
@@ -554,6 +562,19 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
         return;
     }
     {
+#if ORB_SFI_QSTAGE
+        // (a query's keypoint, position and descriptor were three dependent
+        // global round trips at the head of every query of a wave's 16):
+        // loaded here, in flight with the F2 list's loads, stored after them
+        const bool qs = tid < kStQ && q0 + tid < n1;
+        orb_keypoint qk1{};
+        uint4 qd0{}, qd1{};
+        if (qs) {
+            qk1 = K1[q0 + tid];
+            qd0 = *(const uint4*)(D1 + (long long)(q0 + tid) * 32);
+            qd1 = *(const uint4*)(D1 + (long long)(q0 + tid) * 32 + 16);
+        }
+#endif
         const uint32_t* gs = a.gsorted + (long long)f2 * a.cap;
         for (int j = tid; j < nl; j += 256) {
             const int v = (int)gs[j], fi = v & 0xffff;
@@ -563,6 +584,15 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
             d2s[2 * j] = *(const uint4*)(D2 + (long long)fi * 32);
             d2s[2 * j + 1] = *(const uint4*)(D2 + (long long)fi * 32 + 16);
         }
+#if ORB_SFI_QSTAGE
+        if (qs) {
+            float px, py;
+            query_pos(a, pr, q0 + tid, qk1, px, py);
+            qk[tid] = make_float4(px, py, qk1.angle, __int_as_float(qk1.octave));
+            qd[2 * tid] = qd0;
+            qd[2 * tid + 1] = qd1;
+        }
+#endif
     }
     __syncthreads();
     const float r = a.window;
@@ -571,15 +601,25 @@ __global__ __launch_bounds__(256) void k_sfi_topk_st(SfiArgs a) {
         if (i1 >= n1) break;
         uint32_t* tk = a.topk + ((long long)pr * a.cap + i1) * kTopK;
         int* nc = a.ncand + (long long)pr * a.cap + i1;
+#if ORB_SFI_QSTAGE
+        const float4 kq = qk[i1 - q0];
+        const float px = kq.x, py = kq.y;
+        struct { float angle; int octave; } k1{kq.z, __float_as_int(kq.w)};
+#else
         const orb_keypoint k1 = K1[i1];
         float px, py;
         query_pos(a, pr, i1, k1, px, py);
+#endif
         CellRange cr;
         if (k1.octave > 0 || !cell_range(px, py, r, a.g, cr)) {
             if (lane == 0) *nc = -1;
             continue;
         }
+#if ORB_SFI_QSTAGE
+        const uint4 qa = qd[2 * (i1 - q0)], qb = qd[2 * (i1 - q0) + 1];
+#else
         const uint4 qa = *(const uint4*)(D1 + (long long)i1 * 32), qb = *(const uint4*)(D1 + (long long)i1 * 32 + 16);
+#endif
         uint32_t kv[kStIt];
         int cnt = 0;
 #pragma unroll
@@ -1269,7 +1309,7 @@ static int launch_sfi(SfiArgs& a, int npairs, hipStream_t st) {
     // staged form; a block whose F2 level-0 list is longer than its
     // registers take runs the per-lane form from global memory
     KLAUNCH(k_sfi_topk_st, dim3(npairs, (a.cap + kStQ - 1) / kStQ), dim3(256),
-            (size_t)kStIt * kWave * (32 + 8 + 4 + 4), st, a);
+            (size_t)kStIt * kWave * (32 + 8 + 4 + 4) + (ORB_SFI_QSTAGE ? (size_t)kStQ * (32 + 16) : 0), st, a);
     const size_t lds_m12 = lds_res + (size_t)a.cap * 4;
     if (lds_m12 <= kLdsMax)
         KLAUNCH(k_sfi_resolve<true>, dim3(npairs), dim3(kSfiThreads), lds_m12, st, a);
